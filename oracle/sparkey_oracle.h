@@ -1,0 +1,72 @@
+/*
+ * sparkey_oracle.h -- CPU restatement of spotify/sparkey-java's hash-file build.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This is the parity oracle and the CPU baseline.
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load it.
+ * The product (sparkey-java_amd/, libsparkey_gpu.so) never links or calls it.
+ *
+ * Pinning: MurmurHash3 against the reference's 451 known-answer vectors
+ * (src/test/java/com/spotify/sparkey/MurmurHash3Test.java:27-486), VLQ against
+ * UtilTest.java:43-87, slot byte order against AddressSizeTest.java:16-48,
+ * putSize/deleteSize against BytesWrittenTest.java:55-56, and the table layout
+ * against the reference's own differential invariant IN_MEMORY == SORTING
+ * (TestSparkeyWriter.java:9-36).  The Java reference itself cannot run in this
+ * image (no JDK), so whole-file .spi goldens are restatement-derived.
+ */
+#ifndef SPARKEY_ORACLE_H
+#define SPARKEY_ORACLE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* error codes (mirror include/sparkey_gpu.h) */
+#define ORACLE_OK 0
+#define ORACLE_E_NOT_LOG (-1)
+#define ORACLE_E_VERSION (-2)
+#define ORACLE_E_CORRUPT_LOG (-3)
+#define ORACLE_E_NO_FREE_SLOTS (-4)
+#define ORACLE_E_CORRUPT_DATA (-5)
+#define ORACLE_E_VLQ (-6)
+#define ORACLE_E_HEADER (-7)
+#define ORACLE_E_UNSUPPORTED (-8)
+#define ORACLE_E_ARG (-11)
+#define ORACLE_E_BUFFER (-12)
+
+/* MurmurHash3.java:18-75 */
+uint32_t oracle_murmur3_x86_32(const uint8_t* data, int32_t len, int32_t seed);
+/* MurmurHash3.java:100-201 (x64_128, returns h1) */
+uint64_t oracle_murmur3_x64_64(const uint8_t* data, int32_t len, int32_t seed);
+/* HashType.java:44-46,70-72 */
+uint64_t oracle_hash(int32_t hash_size, const uint8_t* key, int32_t len, int32_t seed);
+
+/* Util.java:86-218 */
+int32_t oracle_vlq_size(int64_t value);
+int32_t oracle_vlq_write(uint64_t value, uint8_t* out);
+int32_t oracle_vlq_read(const uint8_t* buf, int64_t len, int64_t* pos, int32_t* value);
+
+/* LogWriter / UncompressedBlockOutput / LogHeader (append path, produces the input) */
+typedef struct oracle_log oracle_log;
+oracle_log* oracle_log_new(int32_t file_identifier, int32_t compression_block_size);
+int32_t oracle_log_put(oracle_log* log, const uint8_t* key, int32_t klen, const uint8_t* val, int64_t vlen);
+int32_t oracle_log_delete(oracle_log* log, const uint8_t* key, int32_t klen);
+int64_t oracle_log_size(const oracle_log* log);
+int64_t oracle_log_finish(oracle_log* log, uint8_t* out, int64_t cap);
+void oracle_log_free(oracle_log* log);
+
+/* IndexHash.createNew: sizes and build (method 0 AUTO, 1 IN_MEMORY, 2 SORTING) */
+int64_t oracle_index_size(const uint8_t* log, int64_t log_len, int32_t hash_size, double sparsity);
+int64_t oracle_build_index(const uint8_t* log, int64_t log_len, int32_t hash_size, double sparsity,
+                           int32_t seed, int32_t method, int64_t max_memory,
+                           uint8_t* out, int64_t out_cap, char* err, int32_t err_len);
+
+/* IndexHash.get (IndexHash.java:398-452): 1 found, 0 missing, <0 error */
+int32_t oracle_get(const uint8_t* index, int64_t index_len, const uint8_t* log, int64_t log_len,
+                   const uint8_t* key, int32_t klen, int64_t* value_off, int64_t* value_len);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
