@@ -1,0 +1,147 @@
+// build_kernels.hpp -- device data layout and launchers of the .spi build pipeline.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <vector>
+
+#include "device_common.hpp"
+
+namespace sk {
+
+constexpr int kChunkShift = 12;                   // framing chunk: 4 KiB of log bytes
+constexpr int kChunk = 1 << kChunkShift;
+constexpr int kEmitExtra = 1024 + 16;             // bytes staged past a chunk for headers + keys
+constexpr int kBucketShift = 10;                  // placement bucket: 1024 slots
+constexpr int kBucket = 1 << kBucketShift;
+constexpr int kPlaceBlock = 256;
+constexpr int kBinsPerThread = kBucket / kPlaceBlock;
+constexpr uint32_t kGroupMax = 64;                // equal-wanted-slot group sorted by insertion
+constexpr int kScanBlock = 256;
+constexpr int kScanItems = 16;
+constexpr uint64_t kScanTile = (uint64_t)kScanBlock * kScanItems;
+constexpr int kStatBlock = 256;
+constexpr int kStatSlotsPerBlock = 4096;
+
+// One log record as the placement sees it: 16 bytes, AoS so every access is one dwordx4.
+struct alignas(16) Entry {
+  uint64_t hash;  // HashType.hash of the key (32-bit hashes zero-extended)
+  uint64_t addr;  // position << entryBlockBits (| kDelBit for DELETE records)
+};
+
+// Carry function f(x) = max(c, x + a) of a bucket (see k_summary).
+struct MaxPlus {
+  int64_t c;
+  int64_t a;
+};
+
+struct StatPart {
+  unsigned long long sum_disp;
+  unsigned long long collisions;
+  long long max_disp;
+};
+
+// Device-side build status, read back once per build.
+struct Status {
+  unsigned long long err;  // min over (position << 8 | -code); ~0 = none
+  unsigned int spec_fail;  // speculative framing disagreed with the verified chain
+  unsigned int dup;        // two PUTs with the same key (canonical layout does not apply)
+  unsigned int dup_overflow;
+  unsigned int full;       // records >= capacity
+  unsigned int overflow;   // more records than workspace
+  unsigned int pad;
+  unsigned long long n_records;
+  unsigned long long n_deletes;
+  unsigned long long n_pairs;
+  long long num_entries;
+  long long garbage;
+  long long max_disp;
+  long long collisions;
+  long long total_disp;
+};
+
+struct BuildParams {
+  // input log (device) and its header fields (LogHeader.java:55-88)
+  const uint8_t* log;
+  uint64_t log_len;
+  int64_t data_end;
+  int64_t max_key_len;
+  int64_t max_value_len;
+  int64_t max_rec_len;  // longest possible record, bounds the speculative entry window
+  uint64_t nchunks;
+  int32_t emit_extra;
+  // index parameters (IndexHash.createNew, IndexHash.java:131-150)
+  int32_t hash_size;
+  int32_t addr_size;
+  int32_t slot_size;
+  int32_t ebb;
+  int32_t seed;
+  FastMod mod;
+  uint64_t cap;
+  uint64_t nbuckets;
+  uint8_t* out;  // .spi image: 112-byte header + cap slots (device)
+  Status* st;
+  // framing workspace (per chunk)
+  uint8_t* conv;
+  int64_t* exitp;
+  int64_t* qpos;
+  uint32_t* tail;
+  int64_t* G;
+  uint32_t* cnt;
+  uint64_t* off;
+  // entries
+  Entry* ent;   // log order
+  Entry* ent2;  // grouped by bucket
+  Entry* ent3;  // sorted by (wanted, address) within bucket
+  uint64_t max_records;
+  // buckets
+  uint32_t* bcount;
+  uint32_t* bcursor;
+  uint64_t* boff;  // nbuckets + 1
+  MaxPlus* bfun;
+  MaxPlus* bpre;
+  MaxPlus* bfun_total;
+  int64_t* carry;
+  uint64_t* pairs;
+  uint64_t pair_cap;
+  StatPart* parts;
+  uint64_t* scan_scratch_u64;
+  MaxPlus* scan_scratch_mp;
+};
+
+// Per-stage HIP events on the build stream (only when profiling is enabled).
+struct StageTimer {
+  bool enabled = false;
+  std::vector<hipEvent_t> evs;
+  std::vector<const char*> names;
+  size_t used = 0;
+  void begin(hipStream_t s) {
+    used = 0;
+    mark("begin", s);
+  }
+  void mark(const char* name, hipStream_t s) {
+    if (!enabled) return;
+    if (used == evs.size()) {
+      hipEvent_t e;
+      if (hipEventCreate(&e) != hipSuccess) return;
+      evs.push_back(e);
+      names.push_back(name);
+    }
+    names[used] = name;
+    (void)hipEventRecord(evs[used], s);
+    used++;
+  }
+  ~StageTimer() {
+    for (auto e : evs) (void)hipEventDestroy(e);
+  }
+};
+
+void launch_framing(const BuildParams& P, hipStream_t s, StageTimer* tm);
+void launch_framing_serial(const BuildParams& P, hipStream_t s);
+void launch_emit(const BuildParams& P, hipStream_t s, StageTimer* tm);
+void launch_place(const BuildParams& P, hipStream_t s, StageTimer* tm);
+void launch_stats(const BuildParams& P, hipStream_t s, int sequential, StageTimer* tm);
+void launch_sequential(const BuildParams& P, hipStream_t s, int sorted_order);
+
+}  // namespace sk

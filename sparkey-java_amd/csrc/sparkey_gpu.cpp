@@ -1,0 +1,662 @@
+// sparkey_gpu.cpp -- C-ABI (include/sparkey_gpu.h) and host orchestration of the .spi build.
+//
+// Host side of IndexHash.createNew (IndexHash.java:131-167): parse and validate the 84-byte log
+// header (LogHeader.java:55-88, CommonHeader.java:30-44), derive the index parameters
+// (addressSize :140/:247-250, hashType :141-143, capacity :145, entryBlockBits :123-129), build
+// the 112-byte header template (IndexHeader.java:125-155) and drive the device pipeline in
+// build_kernels.hip.  Errors map to the reference's exceptions (include/sparkey_gpu.h).
+#include <errno.h>
+#include <fcntl.h>
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <string.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "../../include/sparkey_gpu.h"
+#include "build_kernels.hpp"
+
+using namespace sk;
+
+namespace {
+
+constexpr uint32_t kLogMagic = 0x49b39c95u;
+constexpr uint32_t kIndexMagic = 0x9a11318fu;
+
+void set_err(char* err, size_t err_len, const std::string& msg) {
+  if (err && err_len > 0) snprintf(err, err_len, "%s", msg.c_str());
+}
+
+uint32_t rd32(const uint8_t* p) {
+  return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+uint64_t rd64(const uint8_t* p) { return (uint64_t)rd32(p) | ((uint64_t)rd32(p + 4) << 32); }
+void wr32(uint8_t* p, uint32_t v) {
+  for (int i = 0; i < 4; i++) p[i] = (uint8_t)(v >> (8 * i));
+}
+void wr64(uint8_t* p, uint64_t v) {
+  for (int i = 0; i < 8; i++) p[i] = (uint8_t)(v >> (8 * i));
+}
+
+struct LogHdr {
+  int32_t major, minor, file_id;
+  int64_t num_puts, num_deletes, data_end, max_key_len, max_value_len, delete_size;
+  int32_t compression_type, compression_block_size;
+  int64_t put_size;
+  int32_t max_entries_per_block;
+};
+
+// LogHeader.read (LogHeader.java:55-88) + CommonHeader bounds (CommonHeader.java:38-43)
+int parse_log_header(const uint8_t* b, uint64_t hdr_len, uint64_t file_len, LogHdr* h, char* err, size_t err_len) {
+  if (hdr_len < 84 || rd32(b) != kLogMagic) {
+    set_err(err, err_len, "File is not a Sparkey log file");
+    return SPARKEY_E_NOT_LOG;
+  }
+  h->major = (int32_t)rd32(b + 4);
+  if (h->major != 1) {
+    set_err(err, err_len, "Incompatible major version. Expected 1, but got " + std::to_string(h->major));
+    return SPARKEY_E_VERSION;
+  }
+  h->minor = (int32_t)rd32(b + 8);
+  if (h->minor > 0) {
+    set_err(err, err_len, "Incompatible minor version. Can handle up to version 0, but got " + std::to_string(h->minor));
+    return SPARKEY_E_VERSION;
+  }
+  h->file_id = (int32_t)rd32(b + 12);
+  h->num_puts = (int64_t)rd64(b + 16);
+  h->num_deletes = (int64_t)rd64(b + 24);
+  h->data_end = (int64_t)rd64(b + 32);
+  h->max_key_len = (int64_t)rd64(b + 40);
+  h->max_value_len = (int64_t)rd64(b + 48);
+  h->delete_size = (int64_t)rd64(b + 56);
+  h->compression_type = (int32_t)rd32(b + 64);
+  h->compression_block_size = (int32_t)rd32(b + 68);
+  h->put_size = (int64_t)rd64(b + 72);
+  h->max_entries_per_block = (int32_t)rd32(b + 80);
+  if (h->data_end > (int64_t)file_len) {
+    set_err(err, err_len, "Corrupt log file: expected at least " + std::to_string(h->data_end) + " size but was " +
+                              std::to_string(file_len));
+    return SPARKEY_E_CORRUPT_LOG;
+  }
+  if (h->max_key_len > 0x7fffffffLL || h->max_key_len < 0) {
+    set_err(err, err_len, "Too large max key len: " + std::to_string(h->max_key_len));
+    return SPARKEY_E_HEADER;
+  }
+  if (h->max_value_len < 0) {
+    set_err(err, err_len, "Too large max value len: " + std::to_string(h->max_value_len));
+    return SPARKEY_E_HEADER;
+  }
+  if (h->compression_type < 0 || h->compression_type > 2) {
+    set_err(err, err_len, "Corrupt log file: unknown compression type " + std::to_string(h->compression_type));
+    return SPARKEY_E_CORRUPT_LOG;
+  }
+  if (h->compression_type != 0) {
+    set_err(err, err_len, "Compressed (SNAPPY/ZSTD) logs are not supported by the GPU builder");
+    return SPARKEY_E_UNSUPPORTED;
+  }
+  return SPARKEY_OK;
+}
+
+int32_t calc_entry_block_bits(int32_t max_entries_per_block) {  // IndexHash.java:123-129
+  int32_t i = 0;
+  while ((1 << i) < max_entries_per_block) i++;
+  return i;
+}
+
+int64_t java_d2l(double d) {  // Java (long) cast: truncation, NaN -> 0, saturating
+  if (d != d) return 0;
+  if (d >= 9.2233720368547758e18) return INT64_MAX;
+  if (d <= -9.2233720368547758e18) return INT64_MIN;
+  return (int64_t)d;
+}
+
+int32_t vlq_size_long(int64_t v) {  // Util.java:102-128
+  int32_t n = 1;
+  while (n < 9 && v >= (1LL << (7 * n))) n++;
+  return n;
+}
+
+struct IndexParams {
+  int32_t hash_size, addr_size, slot_size, ebb;
+  uint64_t cap;
+  int64_t index_size;
+  bool in_memory;
+};
+
+int make_index_params(const LogHdr& lh, const sparkey_build_opts& o, IndexParams* ip, char* err, size_t err_len) {
+  double sparsity = o.sparsity;
+  if (sparsity < 1.3) sparsity = 1.3;                                   // IndexHash.java:135-137
+  ip->ebb = calc_entry_block_bits(lh.max_entries_per_block);
+  ip->addr_size = lh.data_end <= (1LL << (30 - ip->ebb)) ? 4 : 8;      // :140, :247-250
+  int32_t hs = o.hash_size;
+  if (hs == 0) hs = lh.num_puts < (1 << 23) ? 4 : 8;                   // :141-143
+  if (hs != 4 && hs != 8) {
+    set_err(err, err_len, "Can't support hash size " + std::to_string(hs));
+    return SPARKEY_E_ARG;
+  }
+  ip->hash_size = hs;
+  const int64_t cap = 1LL | java_d2l((double)lh.num_puts * sparsity);  // :145 -- the only FP op
+  if (cap <= 0) {
+    set_err(err, err_len, "Invalid hash capacity " + std::to_string(cap));
+    return SPARKEY_E_ARG;
+  }
+  ip->cap = (uint64_t)cap;
+  ip->slot_size = ip->hash_size + ip->addr_size;
+  const int64_t hash_length = (int64_t)ip->slot_size * cap;
+  ip->index_size = kIndexHeaderSize + hash_length;
+  ip->in_memory = o.method == SPARKEY_METHOD_AUTO ? hash_length <= o.max_memory : o.method == SPARKEY_METHOD_IN_MEMORY;
+  return SPARKEY_OK;
+}
+
+// IndexHeader.asBytes (IndexHeader.java:125-155); stats fields are patched on the device.
+void index_header_template(const LogHdr& lh, const IndexParams& ip, int32_t seed, uint8_t* b) {
+  memset(b, 0, kIndexHeaderSize);
+  wr32(b + 0, kIndexMagic);
+  wr32(b + 4, 1);
+  wr32(b + 8, 1);
+  wr32(b + 12, (uint32_t)lh.file_id);
+  wr32(b + 16, (uint32_t)seed);
+  wr64(b + 20, (uint64_t)lh.data_end);
+  wr64(b + 28, (uint64_t)lh.max_key_len);
+  wr64(b + 36, (uint64_t)lh.max_value_len);
+  wr64(b + 44, (uint64_t)lh.num_puts);
+  wr32(b + 68, (uint32_t)ip.addr_size);
+  wr32(b + 72, (uint32_t)ip.hash_size);
+  wr64(b + 76, ip.cap);
+  wr32(b + 92, (uint32_t)ip.ebb);
+}
+
+const char* code_message(int code) {
+  switch (code) {
+    case SPARKEY_OK: return "OK";
+    case SPARKEY_E_NOT_LOG: return "File is not a Sparkey log file";
+    case SPARKEY_E_VERSION: return "Incompatible version";
+    case SPARKEY_E_CORRUPT_LOG: return "Corrupt log file";
+    case SPARKEY_E_NO_FREE_SLOTS: return "No free slots in the hash";
+    case SPARKEY_E_CORRUPT_DATA: return "Corrupt data";
+    case SPARKEY_E_VLQ: return "Too long VLQ value";
+    case SPARKEY_E_HEADER: return "Too large max key len";
+    case SPARKEY_E_UNSUPPORTED: return "Unsupported compression type";
+    case SPARKEY_E_IO: return "I/O error";
+    case SPARKEY_E_GPU: return "GPU error";
+    case SPARKEY_E_ARG: return "Illegal argument";
+    case SPARKEY_E_BUFFER: return "Buffer too small";
+    default: return "Unknown error";
+  }
+}
+
+#define HIP_TRY(expr)                                                                  \
+  do {                                                                                 \
+    hipError_t e_ = (expr);                                                            \
+    if (e_ != hipSuccess) {                                                            \
+      set_err(err, err_len, std::string("HIP error: ") + hipGetErrorString(e_) + " at " #expr); \
+      return SPARKEY_E_GPU;                                                            \
+    }                                                                                  \
+  } while (0)
+
+template <class T>
+hipError_t grow(T** p, uint64_t& have, uint64_t want) {
+  if (want <= have && *p) return hipSuccess;
+  if (*p) (void)hipFree(*p);
+  *p = nullptr;
+  have = 0;
+  const uint64_t n = std::max<uint64_t>(want, 1);
+  hipError_t e = hipMalloc((void**)p, n * sizeof(T));
+  if (e == hipSuccess) have = n;
+  return e;
+}
+
+}  // namespace
+
+struct sparkey_plan {
+  int device = 0;
+  hipStream_t own_stream = nullptr;
+  uint64_t c_conv = 0, c_exitp = 0, c_qpos = 0, c_tail = 0, c_G = 0, c_cnt = 0, c_off = 0;
+  uint64_t c_ent = 0, c_ent2 = 0, c_ent3 = 0;
+  uint64_t c_bcount = 0, c_bcursor = 0, c_boff = 0, c_bfun = 0, c_bpre = 0, c_carry = 0;
+  uint64_t c_pairs = 0, c_parts = 0, c_su = 0, c_smp = 0, c_bft = 0;
+  uint8_t* conv = nullptr;
+  int64_t* exitp = nullptr;
+  int64_t* qpos = nullptr;
+  uint32_t* tail = nullptr;
+  int64_t* G = nullptr;
+  uint32_t* cnt = nullptr;
+  uint64_t* off = nullptr;
+  Entry* ent = nullptr;
+  Entry* ent2 = nullptr;
+  Entry* ent3 = nullptr;
+  uint32_t* bcount = nullptr;
+  uint32_t* bcursor = nullptr;
+  uint64_t* boff = nullptr;
+  MaxPlus* bfun = nullptr;
+  MaxPlus* bpre = nullptr;
+  MaxPlus* bfun_total = nullptr;
+  int64_t* carry = nullptr;
+  uint64_t* pairs = nullptr;
+  StatPart* parts = nullptr;
+  uint64_t* scan_u64 = nullptr;
+  MaxPlus* scan_mp = nullptr;
+  Status* d_status = nullptr;
+  Status* h_status = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  StageTimer timer;
+  std::vector<std::string> stage_names;
+  std::vector<double> stage_ms;
+};
+
+static int plan_reserve(sparkey_plan* pl, uint64_t nchunks, uint64_t nrec, uint64_t nbuckets, uint64_t cap,
+                        char* err, size_t err_len) {
+  HIP_TRY(grow(&pl->conv, pl->c_conv, nchunks));
+  HIP_TRY(grow(&pl->exitp, pl->c_exitp, nchunks));
+  HIP_TRY(grow(&pl->qpos, pl->c_qpos, nchunks));
+  HIP_TRY(grow(&pl->tail, pl->c_tail, nchunks));
+  HIP_TRY(grow(&pl->G, pl->c_G, nchunks + 1));
+  HIP_TRY(grow(&pl->cnt, pl->c_cnt, nchunks));
+  HIP_TRY(grow(&pl->off, pl->c_off, nchunks + 1));
+  HIP_TRY(grow(&pl->ent, pl->c_ent, nrec));
+  HIP_TRY(grow(&pl->ent2, pl->c_ent2, nrec));
+  HIP_TRY(grow(&pl->ent3, pl->c_ent3, nrec));
+  HIP_TRY(grow(&pl->bcount, pl->c_bcount, nbuckets));
+  HIP_TRY(grow(&pl->bcursor, pl->c_bcursor, nbuckets));
+  HIP_TRY(grow(&pl->boff, pl->c_boff, nbuckets + 1));
+  HIP_TRY(grow(&pl->bfun, pl->c_bfun, nbuckets));
+  HIP_TRY(grow(&pl->bpre, pl->c_bpre, nbuckets));
+  HIP_TRY(grow(&pl->bfun_total, pl->c_bft, 1));
+  HIP_TRY(grow(&pl->carry, pl->c_carry, nbuckets));
+  const uint64_t pair_cap = std::max<uint64_t>(1 << 16, std::min<uint64_t>(nrec, 1 << 22));
+  HIP_TRY(grow(&pl->pairs, pl->c_pairs, 2 * pair_cap));
+  HIP_TRY(grow(&pl->parts, pl->c_parts, (cap + kStatSlotsPerBlock - 1) / kStatSlotsPerBlock));
+  const uint64_t scratch = std::max(nchunks, nbuckets) / kScanTile + 64;
+  HIP_TRY(grow(&pl->scan_u64, pl->c_su, scratch + 16));
+  HIP_TRY(grow(&pl->scan_mp, pl->c_smp, scratch + 16));
+  return SPARKEY_OK;
+}
+
+static void fill_stats(sparkey_build_stats* s, const Status& st, const IndexParams& ip, int placement, int framing,
+                       double ms) {
+  if (!s) return;
+  s->num_records = (int64_t)st.n_records;
+  s->num_deletes = (int64_t)st.n_deletes;
+  s->num_puts = (int64_t)st.n_records - (int64_t)st.n_deletes;
+  s->num_entries = st.num_entries;
+  s->capacity = (int64_t)ip.cap;
+  s->garbage_size = st.garbage;
+  s->max_displacement = st.max_disp;
+  s->hash_collisions = st.collisions;
+  s->total_displacement = st.total_disp;
+  s->hash_size = ip.hash_size;
+  s->address_size = ip.addr_size;
+  s->placement_path = placement;
+  s->framing_path = framing;
+  s->device_ms = ms;
+}
+
+static int status_error(const Status& st, char* err, size_t err_len) {
+  if (st.err == ~0ull) return SPARKEY_OK;
+  const int code = -(int)(st.err & 0xff);
+  const unsigned long long pos = st.err >> 8;
+  set_err(err, err_len, std::string(code_message(code)) + " (log offset " + std::to_string(pos) + ")");
+  return code;
+}
+
+static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t* d_log, uint64_t log_len,
+                      uint8_t* d_out, uint64_t index_cap, const sparkey_build_opts* opts, hipStream_t s,
+                      sparkey_build_stats* stats_out, char* err, size_t err_len) {
+  if (!pl || !log_header || !opts) {
+    set_err(err, err_len, "null argument");
+    return SPARKEY_E_ARG;
+  }
+  LogHdr lh;
+  int rc = parse_log_header(log_header, 84, log_len, &lh, err, err_len);
+  if (rc) return rc;
+  IndexParams ip;
+  rc = make_index_params(lh, *opts, &ip, err, err_len);
+  if (rc) return rc;
+  if ((uint64_t)ip.index_size > index_cap) {
+    set_err(err, err_len, "index buffer too small: need " + std::to_string(ip.index_size));
+    return SPARKEY_E_BUFFER;
+  }
+  if (((uintptr_t)d_log & 15) || ((uintptr_t)d_out & 15)) {
+    set_err(err, err_len, "device buffers must be 16-byte aligned");
+    return SPARKEY_E_ARG;
+  }
+  HIP_TRY(hipSetDevice(pl->device));
+  if (!s) s = pl->own_stream;
+
+  BuildParams P;
+  memset(&P, 0, sizeof(P));
+  P.log = d_log;
+  P.log_len = log_len;
+  P.data_end = lh.data_end;
+  P.max_key_len = lh.max_key_len;
+  P.max_value_len = lh.max_value_len;
+  {
+    const int64_t put_len = vlq_size_long(lh.max_key_len + 1) + vlq_size_long(lh.max_value_len) + lh.max_key_len +
+                            lh.max_value_len;
+    const int64_t del_len = 1 + vlq_size_long(lh.max_key_len) + lh.max_key_len;
+    P.max_rec_len = std::max<int64_t>(1, std::max(put_len, del_len));
+  }
+  P.nchunks = lh.data_end > kLogHeaderSize ? (uint64_t)((lh.data_end + kChunk - 1) / kChunk) : 0;
+  P.emit_extra = lh.max_key_len + 16 <= 1024 ? (int32_t)((lh.max_key_len + 16 + 15) & ~15LL) : 16;
+  P.hash_size = ip.hash_size;
+  P.addr_size = ip.addr_size;
+  P.slot_size = ip.slot_size;
+  P.ebb = ip.ebb;
+  P.seed = opts->hash_seed;
+  P.mod = make_fastmod(ip.cap);
+  P.cap = ip.cap;
+  P.nbuckets = (ip.cap + kBucket - 1) / kBucket;
+  P.out = d_out;
+  P.st = pl->d_status;
+
+  uint64_t nrec = (uint64_t)std::max<int64_t>(0, lh.num_puts) + (uint64_t)std::max<int64_t>(0, lh.num_deletes);
+  uint8_t hdr[kIndexHeaderSize];
+  index_header_template(lh, ip, opts->hash_seed, hdr);
+
+  int framing_path = 0, placement_path = 0;
+  float ms = 0.f;
+  Status& st = *pl->h_status;
+  for (int attempt = 0; attempt < 3; attempt++) {
+    rc = plan_reserve(pl, P.nchunks, std::max<uint64_t>(nrec, 1), P.nbuckets, ip.cap, err, err_len);
+    if (rc) return rc;
+    P.conv = pl->conv; P.exitp = pl->exitp; P.qpos = pl->qpos; P.tail = pl->tail; P.G = pl->G;
+    P.cnt = pl->cnt; P.off = pl->off;
+    P.ent = pl->ent; P.ent2 = pl->ent2; P.ent3 = pl->ent3; P.max_records = pl->c_ent;
+    P.bcount = pl->bcount; P.bcursor = pl->bcursor; P.boff = pl->boff; P.bfun = pl->bfun; P.bpre = pl->bpre;
+    P.bfun_total = pl->bfun_total; P.carry = pl->carry; P.pairs = pl->pairs; P.pair_cap = pl->c_pairs / 2;
+    P.parts = pl->parts; P.scan_scratch_u64 = pl->scan_u64; P.scan_scratch_mp = pl->scan_mp;
+
+    Status init;
+    memset(&init, 0, sizeof(init));
+    init.err = ~0ull;
+    HIP_TRY(hipEventRecord(pl->ev0, s));
+    pl->timer.begin(s);
+    HIP_TRY(hipMemcpyAsync(d_out, hdr, kIndexHeaderSize, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(pl->d_status, &init, sizeof(Status), hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemsetAsync(pl->bcount, 0, P.nbuckets * sizeof(uint32_t), s));
+    HIP_TRY(hipMemsetAsync(pl->bcursor, 0, P.nbuckets * sizeof(uint32_t), s));
+    if (framing_path == 0) launch_framing(P, s, &pl->timer);
+    else launch_framing_serial(P, s);
+    launch_emit(P, s, &pl->timer);
+    launch_place(P, s, &pl->timer);
+    launch_stats(P, s, 0, &pl->timer);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(pl->ev1, s));
+    HIP_TRY(hipMemcpyAsync(pl->h_status, pl->d_status, sizeof(Status), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    HIP_TRY(hipEventElapsedTime(&ms, pl->ev0, pl->ev1));
+    if (st.overflow || st.n_records > P.max_records) {  // header under-counts records: grow and redo
+      nrec = std::max<uint64_t>(st.n_records, nrec * 2 + 1);
+      continue;
+    }
+    if (framing_path == 0 && (st.spec_fail || st.err != ~0ull)) {  // only the verified serial walk may report
+      framing_path = 1;
+      continue;
+    }
+    break;
+  }
+  rc = status_error(st, err, err_len);
+  if (rc) return rc;
+  if (st.overflow || st.spec_fail) {
+    set_err(err, err_len, "Corrupt log file: framing did not converge");
+    return SPARKEY_E_CORRUPT_LOG;
+  }
+  // Logs outside the canonical case go through the exact sequential restatement on the device.
+  if (st.n_deletes > 0 || st.dup || st.dup_overflow || st.full || st.n_pairs > P.pair_cap) {
+    placement_path = 1;
+    float ms2 = 0.f;
+    HIP_TRY(hipEventRecord(pl->ev0, s));
+    HIP_TRY(hipMemsetAsync(d_out + kIndexHeaderSize, 0, (size_t)(ip.index_size - kIndexHeaderSize), s));
+    launch_sequential(P, s, ip.in_memory ? 0 : 1);
+    launch_stats(P, s, 1, &pl->timer);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(pl->ev1, s));
+    HIP_TRY(hipMemcpyAsync(pl->h_status, pl->d_status, sizeof(Status), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    HIP_TRY(hipEventElapsedTime(&ms2, pl->ev0, pl->ev1));
+    ms += ms2;
+    rc = status_error(st, err, err_len);
+    if (rc) return rc;
+  }
+  if (pl->timer.enabled) {
+    pl->stage_names.clear();
+    pl->stage_ms.clear();
+    for (size_t i = 1; i < pl->timer.used; i++) {
+      float t = 0.f;
+      (void)hipEventElapsedTime(&t, pl->timer.evs[i - 1], pl->timer.evs[i]);
+      pl->stage_names.push_back(pl->timer.names[i]);
+      pl->stage_ms.push_back(t);
+    }
+  }
+  fill_stats(stats_out, st, ip, placement_path, framing_path, ms);
+  return SPARKEY_OK;
+}
+
+extern "C" {
+
+const char* sparkey_gpu_version(void) { return "sparkey-mi355x 0.1 (gfx950)"; }
+
+const char* sparkey_strerror(int code) { return code_message(code); }
+
+int sparkey_plan_create(sparkey_plan** plan_out, int32_t device, uint64_t max_log_bytes, uint64_t max_records,
+                        char* err, size_t err_len) {
+  (void)max_log_bytes;
+  if (!plan_out) return SPARKEY_E_ARG;
+  *plan_out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= device || device < 0) {
+    set_err(err, err_len, "no HIP device " + std::to_string(device));
+    return SPARKEY_E_GPU;
+  }
+  HIP_TRY(hipSetDevice(device));
+  sparkey_plan* pl = new sparkey_plan();
+  pl->device = device;
+  if (hipStreamCreateWithFlags(&pl->own_stream, hipStreamNonBlocking) != hipSuccess ||
+      hipMalloc((void**)&pl->d_status, sizeof(Status)) != hipSuccess ||
+      hipHostMalloc((void**)&pl->h_status, sizeof(Status), hipHostMallocDefault) != hipSuccess ||
+      hipEventCreate(&pl->ev0) != hipSuccess || hipEventCreate(&pl->ev1) != hipSuccess) {
+    sparkey_plan_destroy(pl);
+    set_err(err, err_len, "HIP allocation failed");
+    return SPARKEY_E_GPU;
+  }
+  if (max_records) {
+    const uint64_t nchunks = max_log_bytes / kChunk + 1;
+    const uint64_t cap = max_records * 2;
+    int rc = plan_reserve(pl, nchunks, max_records, cap / kBucket + 1, cap, err, err_len);
+    if (rc) {
+      sparkey_plan_destroy(pl);
+      return rc;
+    }
+  }
+  *plan_out = pl;
+  return SPARKEY_OK;
+}
+
+int sparkey_plan_build_device(sparkey_plan* plan, const uint8_t* log_header, const uint8_t* d_log, uint64_t log_len,
+                              uint8_t* d_index_out, uint64_t index_cap, const sparkey_build_opts* opts, void* stream,
+                              sparkey_build_stats* stats_out, char* err, size_t err_len) {
+  return plan_build(plan, log_header, d_log, log_len, d_index_out, index_cap, opts, (hipStream_t)stream, stats_out,
+                    err, err_len);
+}
+
+void sparkey_plan_set_profiling(sparkey_plan* plan, int32_t enabled) {
+  if (plan) plan->timer.enabled = enabled != 0;
+  if (plan && !enabled) {
+    plan->stage_names.clear();
+    plan->stage_ms.clear();
+  }
+}
+
+int32_t sparkey_plan_stage_count(const sparkey_plan* plan) { return plan ? (int32_t)plan->stage_names.size() : 0; }
+
+const char* sparkey_plan_stage_name(const sparkey_plan* plan, int32_t i) {
+  if (!plan || i < 0 || i >= (int32_t)plan->stage_names.size()) return "";
+  return plan->stage_names[i].c_str();
+}
+
+double sparkey_plan_stage_ms(const sparkey_plan* plan, int32_t i) {
+  if (!plan || i < 0 || i >= (int32_t)plan->stage_ms.size()) return 0.0;
+  return plan->stage_ms[i];
+}
+
+void sparkey_plan_destroy(sparkey_plan* pl) {
+  if (!pl) return;
+  (void)hipSetDevice(pl->device);
+  void* bufs[] = {pl->conv, pl->exitp, pl->qpos, pl->tail, pl->G, pl->cnt, pl->off, pl->ent, pl->ent2, pl->ent3,
+                  pl->bcount, pl->bcursor, pl->boff, pl->bfun, pl->bpre, pl->bfun_total, pl->carry, pl->pairs,
+                  pl->parts, pl->scan_u64, pl->scan_mp, pl->d_status};
+  for (void* b : bufs)
+    if (b) (void)hipFree(b);
+  if (pl->h_status) (void)hipHostFree(pl->h_status);
+  if (pl->ev0) (void)hipEventDestroy(pl->ev0);
+  if (pl->ev1) (void)hipEventDestroy(pl->ev1);
+  if (pl->own_stream) (void)hipStreamDestroy(pl->own_stream);
+  delete pl;
+}
+
+int64_t sparkey_index_size(const uint8_t* log_header, uint64_t header_len, const sparkey_build_opts* opts) {
+  if (!log_header || !opts) return SPARKEY_E_ARG;
+  LogHdr lh;
+  const uint64_t data_end = header_len >= 40 ? rd64(log_header + 32) : 0;
+  int rc = parse_log_header(log_header, header_len, std::max<uint64_t>(header_len, data_end), &lh, nullptr, 0);
+  if (rc) return rc;
+  IndexParams ip;
+  rc = make_index_params(lh, *opts, &ip, nullptr, 0);
+  if (rc) return rc;
+  return ip.index_size;
+}
+
+int sparkey_build_index_mem(const uint8_t* log, uint64_t log_len, uint8_t* index_out, uint64_t index_cap,
+                            const sparkey_build_opts* opts, sparkey_build_stats* stats_out, char* err,
+                            size_t err_len) {
+  if (!log || !index_out || !opts) {
+    set_err(err, err_len, "null argument");
+    return SPARKEY_E_ARG;
+  }
+  LogHdr lh;
+  int rc = parse_log_header(log, log_len, log_len, &lh, err, err_len);
+  if (rc) return rc;
+  IndexParams ip;
+  rc = make_index_params(lh, *opts, &ip, err, err_len);
+  if (rc) return rc;
+  if ((uint64_t)ip.index_size > index_cap) {
+    set_err(err, err_len, "index buffer too small: need " + std::to_string(ip.index_size));
+    return SPARKEY_E_BUFFER;
+  }
+  sparkey_plan* pl = nullptr;
+  rc = sparkey_plan_create(&pl, opts->device, 0, 0, err, err_len);
+  if (rc) return rc;
+  uint8_t* d_log = nullptr;
+  uint8_t* d_out = nullptr;
+  auto cleanup = [&]() {
+    if (d_log) (void)hipFree(d_log);
+    if (d_out) (void)hipFree(d_out);
+    sparkey_plan_destroy(pl);
+  };
+  if (hipMalloc((void**)&d_log, std::max<uint64_t>(log_len, 16)) != hipSuccess ||
+      hipMalloc((void**)&d_out, (size_t)ip.index_size) != hipSuccess) {
+    cleanup();
+    set_err(err, err_len, "hipMalloc failed");
+    return SPARKEY_E_GPU;
+  }
+  if (hipMemcpyAsync(d_log, log, log_len, hipMemcpyHostToDevice, pl->own_stream) != hipSuccess) {
+    cleanup();
+    set_err(err, err_len, "H2D copy failed");
+    return SPARKEY_E_GPU;
+  }
+  rc = plan_build(pl, log, d_log, log_len, d_out, (uint64_t)ip.index_size, opts, pl->own_stream, stats_out, err,
+                  err_len);
+  if (rc == SPARKEY_OK) {
+    if (hipMemcpyAsync(index_out, d_out, (size_t)ip.index_size, hipMemcpyDeviceToHost, pl->own_stream) != hipSuccess ||
+        hipStreamSynchronize(pl->own_stream) != hipSuccess) {
+      set_err(err, err_len, "D2H copy failed");
+      rc = SPARKEY_E_GPU;
+    }
+  }
+  cleanup();
+  return rc;
+}
+
+int sparkey_build_index_file(const char* log_path, const char* index_out_path, const sparkey_build_opts* opts,
+                             int32_t fsync_out, sparkey_build_stats* stats_out, char* err, size_t err_len) {
+  if (!log_path || !index_out_path || !opts) {
+    set_err(err, err_len, "null argument");
+    return SPARKEY_E_ARG;
+  }
+  int fd = open(log_path, O_RDONLY);
+  if (fd < 0) {
+    set_err(err, err_len, std::string("cannot open log file ") + log_path + ": " + strerror(errno));
+    return SPARKEY_E_IO;
+  }
+  struct stat sb;
+  if (fstat(fd, &sb) != 0) {
+    close(fd);
+    set_err(err, err_len, "fstat failed");
+    return SPARKEY_E_IO;
+  }
+  const uint64_t log_len = (uint64_t)sb.st_size;
+  uint8_t* hlog = nullptr;
+  if (hipHostMalloc((void**)&hlog, std::max<uint64_t>(log_len, 16), hipHostMallocDefault) != hipSuccess) {
+    close(fd);
+    set_err(err, err_len, "pinned allocation failed");
+    return SPARKEY_E_GPU;
+  }
+  uint64_t got = 0;
+  while (got < log_len) {
+    const ssize_t r = read(fd, hlog + got, (size_t)std::min<uint64_t>(log_len - got, 1ull << 30));
+    if (r <= 0) break;
+    got += (uint64_t)r;
+  }
+  close(fd);
+  if (got != log_len) {
+    (void)hipHostFree(hlog);
+    set_err(err, err_len, "short read of log file");
+    return SPARKEY_E_IO;
+  }
+  const int64_t isz = sparkey_index_size(hlog, log_len, opts);
+  if (isz < 0) {
+    LogHdr lh;
+    int rc = parse_log_header(hlog, log_len, log_len, &lh, err, err_len);
+    (void)hipHostFree(hlog);
+    if (!rc) set_err(err, err_len, code_message((int)isz));
+    return rc ? rc : (int)isz;
+  }
+  uint8_t* hidx = nullptr;
+  if (hipHostMalloc((void**)&hidx, (size_t)isz, hipHostMallocDefault) != hipSuccess) {
+    (void)hipHostFree(hlog);
+    set_err(err, err_len, "pinned allocation failed");
+    return SPARKEY_E_GPU;
+  }
+  int rc = sparkey_build_index_mem(hlog, log_len, hidx, (uint64_t)isz, opts, stats_out, err, err_len);
+  (void)hipHostFree(hlog);
+  if (rc == SPARKEY_OK) {  // FileFlushingData.close: header then slots (+fsync), FileFlushingData.java:20-34
+    int ofd = open(index_out_path, O_WRONLY | O_CREAT | O_TRUNC, 0644);
+    if (ofd < 0) {
+      set_err(err, err_len, std::string("cannot create index file ") + index_out_path + ": " + strerror(errno));
+      rc = SPARKEY_E_IO;
+    } else {
+      uint64_t put = 0;
+      while (put < (uint64_t)isz) {
+        const ssize_t w = write(ofd, hidx + put, (size_t)std::min<uint64_t>((uint64_t)isz - put, 1ull << 30));
+        if (w <= 0) break;
+        put += (uint64_t)w;
+      }
+      if (put != (uint64_t)isz) {
+        set_err(err, err_len, "short write of index file");
+        rc = SPARKEY_E_IO;
+      } else if (fsync_out && fsync(ofd) != 0) {
+        set_err(err, err_len, "fsync failed");
+        rc = SPARKEY_E_IO;
+      }
+      close(ofd);
+    }
+  }
+  (void)hipHostFree(hidx);
+  return rc;
+}
+
+}  // extern "C"

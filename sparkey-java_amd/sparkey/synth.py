@@ -1,0 +1,98 @@
+"""Synthetic Sparkey logs for the BASELINE.json configs, written with numpy in the exact byte layout
+LogWriter produces (UncompressedBlockOutput.java:67-72, LogHeader.java:90-115).
+
+  fixed_log(n, 16, 100)      C2: key = LE64(i) || LE64(splitmix64(i ^ seed)) (unique), value = 100 random bytes
+  mixed_log(n, 8, 64, 100)   C3: key length uniform in [8, 64], LE64(i) prefix keeps keys unique
+  key_value_log(n)           C1: put("key_" + i, "value_" + i) as WriteHashBenchmark.java:52-54
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .log_writer import LOG_HEADER_SIZE, LogHeader, vlq_bytes
+
+M64 = np.uint64(0xFFFFFFFFFFFFFFFF)
+
+
+def splitmix64(x: np.ndarray) -> np.ndarray:
+    x = (x + np.uint64(0x9E3779B97F4A7C15)) & M64
+    z = x
+    z = ((z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)) & M64
+    z = ((z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)) & M64
+    return z ^ (z >> np.uint64(31))
+
+
+def _header(n_puts: int, max_key: int, max_val: int, put_size: int, data_end: int, file_id: int,
+            block_size: int) -> bytes:
+    h = LogHeader(0, block_size, file_id)
+    h.num_puts = n_puts
+    h.max_key_len = max_key
+    h.max_value_len = max_val
+    h.put_size = put_size
+    h.data_end = data_end
+    h.max_entries_per_block = 1
+    return h.to_bytes()
+
+
+def fixed_log(n: int, key_len: int = 16, value_len: int = 100, seed: int = 1, file_id: int = 0x5EED5EED,
+              block_size: int = 0) -> np.ndarray:
+    """n PUTs with fixed-size keys (>= 16 B) and values; returns the whole .spl as a uint8 array."""
+    assert key_len >= 16 and key_len + 1 < 128 and value_len < 128
+    rec = 2 + key_len + value_len
+    buf = np.empty(LOG_HEADER_SIZE + n * rec, dtype=np.uint8)
+    body = buf[LOG_HEADER_SIZE:].reshape(n, rec)
+    body[:, 0] = key_len + 1
+    body[:, 1] = value_len
+    i = np.arange(n, dtype=np.uint64)
+    body[:, 2:10] = i.view(np.uint8).reshape(n, 8)
+    body[:, 10:18] = splitmix64(i ^ np.uint64(seed)).view(np.uint8).reshape(n, 8)
+    rng = np.random.default_rng(seed)
+    if key_len > 16:
+        body[:, 18:2 + key_len] = rng.integers(0, 256, size=(n, key_len - 16), dtype=np.uint8)
+    body[:, 2 + key_len:] = rng.integers(0, 256, size=(n, value_len), dtype=np.uint8)
+    buf[:LOG_HEADER_SIZE] = np.frombuffer(
+        _header(n, key_len, value_len, n * rec, LOG_HEADER_SIZE + n * rec, file_id, block_size), dtype=np.uint8)
+    return buf
+
+
+def mixed_log(n: int, min_key: int = 8, max_key: int = 64, value_len: int = 100, seed: int = 3,
+              file_id: int = 0x5EED0003, block_size: int = 0) -> np.ndarray:
+    """n PUTs, key length uniform in [min_key, max_key] (>= 8), fixed value length (< 128)."""
+    assert min_key >= 8 and max_key + 1 < 128 and value_len < 128
+    rng = np.random.default_rng(seed)
+    klen = rng.integers(min_key, max_key + 1, size=n).astype(np.int64)
+    rec = 2 + klen + value_len
+    starts = np.empty(n, dtype=np.int64)
+    starts[0] = 0
+    np.cumsum(rec[:-1], out=starts[1:])
+    total = int(rec.sum())
+    buf = np.empty(LOG_HEADER_SIZE + total, dtype=np.uint8)
+    body = buf[LOG_HEADER_SIZE:]
+    body[:] = rng.integers(0, 256, size=total, dtype=np.uint8)
+    body[starts] = (klen + 1).astype(np.uint8)
+    body[starts + 1] = value_len
+    idx = np.arange(n, dtype=np.uint64).view(np.uint8).reshape(n, 8)
+    for b in range(8):
+        body[starts + 2 + b] = idx[:, b]
+    put_size = total
+    buf[:LOG_HEADER_SIZE] = np.frombuffer(
+        _header(n, int(klen.max()) if n else 0, value_len if n else 0, put_size, LOG_HEADER_SIZE + total, file_id,
+                block_size), dtype=np.uint8)
+    return buf
+
+
+def key_value_log(n: int, file_id: int = 0x0C1C1C1C, block_size: int = 1024) -> bytes:
+    """WriteHashBenchmark's data: put("key_" + i, "value_" + i), NONE, block size 1024."""
+    parts = []
+    max_k = max_v = 0
+    put_size = 0
+    for i in range(n):
+        k = b"key_%d" % i
+        v = b"value_%d" % i
+        rec = vlq_bytes(len(k) + 1) + vlq_bytes(len(v)) + k + v
+        parts.append(rec)
+        max_k = max(max_k, len(k))
+        max_v = max(max_v, len(v))
+        put_size += len(rec)
+    body = b"".join(parts)
+    return _header(n, max_k, max_v, put_size, LOG_HEADER_SIZE + len(body), file_id, block_size) + body

@@ -1,0 +1,169 @@
+"""GPU parity: the HIP build (through the C-ABI) must produce .spi bytes identical to the oracle's
+sequential restatement of IndexHash.createNew (IN_MEMORY and SORTING), on the reference's own test
+scenarios (CorrectnessTest, LargeFilesTest, IndexHashTest, WriteHashBenchmark) and on edge cases.
+Integer/byte work: the bar is bit-exact.
+"""
+import numpy as np
+import pytest
+
+import oracle
+from helpers import diff_report, index_header, key_value_puts, make_log, random_puts
+
+pytestmark = pytest.mark.gpu
+
+IN_MEMORY, SORTING = 1, 2
+
+
+def gpu_build(native, log, seed, hash_size=0, method=IN_MEMORY, sparsity=0.0):
+    opts = native.make_opts(hash_size=hash_size, hash_seed=seed, sparsity=sparsity, method=method)
+    spi, stats = native.build_index_mem(log, opts)
+    return spi, stats
+
+
+def check(native, log, seed, hash_size=0, method=IN_MEMORY, sparsity=0.0, expect_path=None):
+    want = oracle.build_index(log, seed, hash_size=hash_size, sparsity=sparsity, method=method)
+    got, stats = gpu_build(native, log, seed, hash_size, method, sparsity)
+    assert got == want, diff_report(got, want)
+    if expect_path is not None:
+        assert stats.placement_path == expect_path, stats.as_dict()
+    return got, stats
+
+
+# --- WriteHashBenchmark (config C1): 1000 x put("key_"+i, "value_"+i), block size 1024 ---
+@pytest.mark.parametrize("method", [IN_MEMORY, SORTING])
+def test_c1_write_hash_benchmark(native, method):
+    log = make_log(key_value_puts(1000, b"key_%d", b"value_%d"), block_size=1024)
+    spi, stats = check(native, log, 1234, method=method, expect_path=0)
+    assert len(spi) == 10520 and stats.hash_size == 4 and stats.address_size == 4
+
+
+# --- CorrectnessTest.SIZES = {0,1,2,3,4,10,100} x hash types (CorrectnessTest.java:38,190-220) ---
+@pytest.mark.parametrize("n", [0, 1, 2, 3, 4, 10, 100])
+@pytest.mark.parametrize("hash_size", [4, 8])
+@pytest.mark.parametrize("method", [IN_MEMORY, SORTING])
+def test_sizes(native, n, hash_size, method):
+    log = make_log(key_value_puts(n))
+    check(native, log, 1738868818, hash_size=hash_size, method=method)
+
+
+# --- testHelperWithDeletes: delete every 7th key (CorrectnessTest.java:109-162) ---
+@pytest.mark.parametrize("n", [0, 1, 2, 3, 4, 10, 100, 1000])
+@pytest.mark.parametrize("hash_size", [4, 8])
+@pytest.mark.parametrize("method", [IN_MEMORY, SORTING])
+def test_deletes_every_7th(native, n, hash_size, method):
+    log = make_log(key_value_puts(n), deletes=[b"Key%d" % i for i in range(n) if i % 7 == 0])
+    got, stats = check(native, log, -112683590, hash_size=hash_size, method=method)
+    if n:
+        assert stats.placement_path == 1
+    for i in range(n):
+        v = oracle.get(got, log, b"Key%d" % i)
+        assert v == (None if i % 7 == 0 else b"Value%d" % i)
+
+
+# --- testCorrectHashLargeFile: 170,000 keys, seed 1234, 32-bit (CorrectnessTest.java:178-200) ---
+def test_correct_hash_large_file(native):
+    n = 170000
+    log = make_log(key_value_puts(n))
+    got, stats = check(native, log, 1234, hash_size=4, expect_path=0)
+    h = index_header(got)
+    assert h["garbageSize"] == 0 and h["hashCollisions"] > 0
+    assert oracle.build_index(log, 1234, hash_size=4, method=SORTING) == got
+    for i in range(0, n, 997):
+        assert oracle.get(got, log, b"Key%d" % i) == b"Value%d" % i
+
+
+# --- testOverwrite / duplicates: re-put replaces in place (IndexHash.java:606-636) ---
+@pytest.mark.parametrize("method", [IN_MEMORY, SORTING])
+def test_overwrite_duplicates(native, method):
+    puts = key_value_puts(500) + [(b"Key%d" % i, b"New%d" % i) for i in range(0, 500, 3)]
+    log = make_log(puts)
+    got, stats = check(native, log, 99, method=method, expect_path=1)
+    assert index_header(got)["garbageSize"] > 0
+
+
+def test_overwrite_single_key(native):
+    log = make_log([(b"A", b"B")])
+    check(native, log, 5)
+
+
+# --- LargeFilesTest: values larger than a framing chunk (LargeFilesTest.java:28-50) ---
+def test_large_values(native):
+    value = b"value"
+    while len(value) < 5 * 1024:
+        value += value
+    log = make_log([(b"key_%d" % i, value) for i in range(2000)], block_size=1024)
+    got, stats = check(native, log, 77, expect_path=0)
+    assert oracle.get(got, log, b"key_100") == value
+
+
+# --- LargeFilesTest.testLargeIndexFileInner: 64-bit hash, value "i % 13" ---
+@pytest.mark.parametrize("n", [7000, 150000])
+def test_large_index_file(native, n):
+    log = make_log([(b"key_%d" % i, b"%d" % (i % 13)) for i in range(n)], block_size=1024)
+    check(native, log, 4242, hash_size=8, expect_path=0)
+
+
+# --- random logs: key lengths 0..300 (multi-block murmur tails), values 0..5000 ---
+@pytest.mark.parametrize("seed", range(6))
+def test_random_logs(native, seed):
+    rng = np.random.default_rng(seed)
+    n = int(rng.integers(1, 3000))
+    puts = random_puts(n, seed=seed, kmin=0 if seed % 2 else 4, kmax=[16, 40, 130, 300, 8, 64][seed],
+                       vmax=[0, 10, 100, 5000, 300, 1][seed])
+    log = make_log(puts)
+    for hs in (4, 8):
+        check(native, log, int(rng.integers(-2**31, 2**31)), hash_size=hs)
+
+
+# --- sparsity, and a hash seed with the high bit set (unsigned widening, MurmurHash3.java:103) ---
+@pytest.mark.parametrize("sparsity", [1.0, 1.3, 2.0, 7.5])
+def test_sparsity(native, sparsity):
+    log = make_log(key_value_puts(4000))
+    check(native, log, -5, hash_size=8, sparsity=sparsity)
+
+
+# --- nearly full tables: wrap-around clusters (sparsity floor 1.3, small n) ---
+@pytest.mark.parametrize("n", [5, 6, 7, 8, 9, 13, 31, 64])
+@pytest.mark.parametrize("seed", [1, 2, 3, 4])
+def test_small_tables_wrap(native, n, seed):
+    log = make_log(key_value_puts(n))
+    check(native, log, seed, hash_size=4)
+    check(native, log, seed, hash_size=8)
+
+
+# --- mixed puts/deletes/re-puts interleaved ---
+@pytest.mark.parametrize("method", [IN_MEMORY, SORTING])
+def test_interleaved_ops(native, method):
+    rng = np.random.default_rng(11)
+    ops = []
+    for i in range(3000):
+        k = b"k%d" % int(rng.integers(0, 800))
+        if rng.random() < 0.2:
+            ops.append(("del", k, None))
+        else:
+            ops.append(("put", k, b"v%d" % i))
+    log = make_log(ops=ops)
+    check(native, log, 31337, method=method)
+
+
+# --- error behaviour (LogHeader.read, CommonHeader, iterator) ---
+def test_errors(native):
+    log = make_log(key_value_puts(10))
+    opts = native.make_opts(hash_seed=1)
+    with pytest.raises(OSError):
+        native.build_index_mem(b"\0" * 84 + log[84:], opts)       # "File is not a Sparkey log file"
+    bad = bytearray(log)
+    bad[4] = 2
+    with pytest.raises(OSError):
+        native.build_index_mem(bytes(bad), opts)                   # major version
+    trunc = log[:-5]
+    with pytest.raises(OSError):
+        native.build_index_mem(trunc, opts)                        # dataEnd > file length
+    bad = bytearray(log)
+    bad[84] = 0xFF                                                 # corrupt first record header
+    with pytest.raises((OSError, RuntimeError)):
+        native.build_index_mem(bytes(bad), opts)
+    bad = bytearray(log)
+    bad[64] = 1                                                    # SNAPPY: not on this path
+    with pytest.raises(OSError):
+        native.build_index_mem(bytes(bad), opts)
