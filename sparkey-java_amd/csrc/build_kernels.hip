@@ -1,183 +1,28 @@
 // build_kernels.hip -- gfx950 kernels of the Sparkey .spi build (IndexHash.createNew on MI355X).
 //
-// Pipeline (one HIP stream, all device-resident; see DESIGN.md for layouts and rooflines):
-//   framing   k_speculate  per 4 KiB chunk, one wave: every plausible record start in the first
-//                          maxRecLen bytes is walked to the chunk end; if all surviving chains exit
-//                          at one offset the chunk's exit is known without its entry.
-//             k_walk       one thread per run of unresolved chunks walks the true chain serially.
-//             k_count      per resolved chunk: entry = predecessor's exit, head walk to the merge
-//                          point + tail count -> records per chunk.
-//             scan         record offsets per chunk.
-//   hash      k_emit       per chunk, one wave: walk from the verified entry (LDS-staged bytes),
-//                          MurmurHash3 every key, write (hash, address) in log order, count buckets.
-//   place     scan + k_scatter (bucket = wantedSlot >> 10), k_summary (per bucket max-plus carry
-//             function), scan over buckets (+ wrap-around fixed point), k_place: per bucket
-//             counting sort by wantedSlot, ties by address (the canonical Robin-Hood order, see
-//             DESIGN.md "canonical placement"), slot = j + max(carry, prefix-max(w_i - i)), write
-//             every slot of the bucket (entries or zeros).
-//   stats     k_stats + k_stats_final: calculateMaxDisplacement (IndexHash.java:195-245) with its
-//             quirks, patch the 112-byte header.
-//   exact     k_sequential: single-lane restatement of put/delete (IndexHash.java:454-665) for logs
-//             the canonical layout does not cover (DELETEs, duplicate keys, full tables).
+// The fast path lives in fused_kernels.hip (k_frame, radix partition, k_place_lds).  This file
+// holds the exact fallbacks and the shared stages:
+//   k_walk(serial)  one thread walks the whole record chain (SparkeyLogIterator.java:86-138) when
+//                   speculative framing disagreed with the verified chain (inconsistent headers).
+//   k_emit          per chunk, one wave: hash the records of the serially framed chunk.
+//   k_summary/k_carry  per bucket max-plus carry function, scan, wrap-around fixed point
+//                   (DESIGN.md "canonical placement").
+//   k_place         global-memory placement for buckets too big for LDS; (wantedSlot, address)
+//                   order for the SORTING restatement.
+//   k_verify_pairs  equal-hash PUT pairs: same key?  (IndexHash.java:606-636)
+//   k_stats         calculateMaxDisplacement (IndexHash.java:195-245), header patch.
+//   k_sequential    single-lane restatement of put/delete (IndexHash.java:454-665) for logs the
+//                   canonical layout does not cover (DELETEs, duplicate keys, full tables).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "build_kernels.hpp"
 #include "device_common.hpp"
+#include "kernel_utils.hpp"
+#include "scan.hpp"
+#include "place_common.hpp"
 
 namespace sk {
-
-// ------------------------------------------------------------------------------------------------
-// small device utilities
-// ------------------------------------------------------------------------------------------------
-__device__ __forceinline__ void set_error(Status* st, int64_t pos, int code) {
-  atomicMin(&st->err, ((unsigned long long)pos << 8) | (unsigned long long)(-code));
-}
-
-__device__ __forceinline__ int64_t chunk_start(uint64_t k) { return k == 0 ? kLogHeaderSize : (int64_t)(k << kChunkShift); }
-__device__ __forceinline__ int64_t chunk_end(uint64_t k, int64_t data_end) {
-  const int64_t e = (int64_t)((k + 1) << kChunkShift);
-  return e < data_end ? e : data_end;
-}
-
-// Stage log bytes [wb, wb + n) into LDS (bytes past log_len read as 0; they are never decoded
-// because every decode is bounded by log_len).  wb is 16-byte aligned; `log` must be too.
-__device__ __forceinline__ void stage_window(uint8_t* win, const uint8_t* log, int64_t wb, int n, int64_t log_len,
-                                             int lane, int nthreads) {
-  const int nvec = n >> 4;
-  for (int v = lane; v < nvec; v += nthreads) {
-    const int64_t a = wb + ((int64_t)v << 4);
-    uint4 val;
-    if (a + 16 <= log_len) {
-      val = *reinterpret_cast<const uint4*>(log + a);
-    } else {
-      uint8_t tmp[16];
-#pragma unroll
-      for (int i = 0; i < 16; i++) tmp[i] = (a + i < log_len) ? log[a + i] : 0;
-      val = *reinterpret_cast<uint4*>(tmp);
-    }
-    *reinterpret_cast<uint4*>(win + (v << 4)) = val;
-  }
-}
-
-__device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const unsigned long long t = __shfl_xor(v, o, 64);
-    v = t < v ? t : v;
-  }
-  return v;
-}
-__device__ __forceinline__ long long wave_max_i64(long long v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const long long t = __shfl_xor(v, o, 64);
-    v = t > v ? t : v;
-  }
-  return v;
-}
-__device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
-
-// ================================================================================================
-// Framing.  A record's start depends on the previous record (SparkeyLogIterator.java:86-138), so
-// the log is cut into 4 KiB chunks and each chunk's entry (first record start >= chunk start) is
-// recovered speculatively, then verified exactly (k_emit checks entry->exit for every chunk).
-// ================================================================================================
-__global__ __launch_bounds__(64) void k_speculate(BuildParams P) {
-  __shared__ __attribute__((aligned(16))) uint8_t win[kChunk + 32];
-  __shared__ unsigned long long bitmap[kChunk / 64];
-  const uint64_t k = blockIdx.x;
-  const int lane = threadIdx.x;
-  const int64_t wb = (int64_t)(k << kChunkShift);
-  const int64_t s = chunk_start(k);
-  const int64_t e = chunk_end(k, P.data_end);
-  // A record longer than the chunk can start before it and end after it: the chunk may hold no
-  // record start at all, so its exit cannot be known without its entry.
-  if (k > 0 && s + P.max_rec_len - 1 >= e) {
-    if (lane == 0) P.conv[k] = 0;
-    return;
-  }
-  stage_window(win, P.log, wb, kChunk + 32, (int64_t)P.log_len, lane, 64);
-  __syncthreads();
-  const int64_t avail = min((int64_t)P.log_len, wb + kChunk + 32);
-  auto at = [&](int64_t a) -> uint32_t { return win[a - wb]; };
-  const int64_t cand_end = (k == 0) ? s + 1 : min(e, s + P.max_rec_len);
-
-  // Pass A: walk every candidate; record survivors (chains that never hit an implausible header).
-  unsigned long long surv_mask = 0;
-  unsigned long long nsurv = 0, min_exit = ~0ull, min_start = ~0ull;
-  long long max_exit = -1;
-  int ci = 0;
-  for (int64_t c = s + lane; c < cand_end; c += 64, ci++) {
-    int64_t p = c;
-    bool ok = true;
-    while (p < e) {
-      const RecHdr h = decode_header(at, p, avail);
-      if (!header_plausible(h, p, P.max_key_len, P.max_value_len, (int64_t)P.log_len)) { ok = false; break; }
-      p = record_end(h, p);
-    }
-    if (ok) {
-      surv_mask |= 1ull << ci;
-      nsurv++;
-      min_exit = min(min_exit, (unsigned long long)p);
-      max_exit = max(max_exit, (long long)p);
-      min_start = min(min_start, (unsigned long long)c);
-    }
-  }
-  nsurv = wave_sum_u64(nsurv);
-  min_exit = wave_min_u64(min_exit);
-  max_exit = wave_max_i64(max_exit);
-  min_start = wave_min_u64(min_start);
-  const bool converged = nsurv > 0 && (long long)min_exit == max_exit;
-  if (!converged) {
-    if (lane == 0) P.conv[k] = 0;
-    return;
-  }
-  // Pass B: mark the chain of the first survivor; every other survivor walks until it meets that
-  // chain (or exits).  q = last merge point: from q on every survivor -- hence the true chain -- is
-  // the same, so the records in [q, e) are counted here once.
-  bitmap[lane] = 0;
-  __syncthreads();
-  if (lane == 0) {
-    int64_t p = (int64_t)min_start;
-    while (p < e) {
-      const int64_t r = p - wb;
-      bitmap[r >> 6] |= 1ull << (r & 63);
-      p = record_end(decode_header(at, p, avail), p);
-    }
-  }
-  __syncthreads();
-  long long qmax = (long long)min_start;
-  ci = 0;
-  for (int64_t c = s + lane; c < cand_end; c += 64, ci++) {
-    if (!((surv_mask >> ci) & 1)) continue;
-    int64_t p = c;
-    while (p < e) {
-      const int64_t r = p - wb;
-      if ((bitmap[r >> 6] >> (r & 63)) & 1) break;
-      p = record_end(decode_header(at, p, avail), p);
-    }
-    qmax = max(qmax, (long long)p);
-  }
-  qmax = wave_max_i64(qmax);
-  // tail = marked positions >= q (and < e); bitmap word `lane` covers offsets [64*lane, 64*lane+64)
-  unsigned long long word = bitmap[lane];
-  const int64_t qr = qmax - wb;
-  const int64_t lo = (int64_t)lane * 64;
-  if (qr >= lo + 64) word = 0;
-  else if (qr > lo) word &= ~0ull << (qr - lo);
-  const unsigned long long tail = wave_sum_u64((unsigned long long)__popcll(word));
-  if (lane == 0) {
-    P.conv[k] = 1;
-    P.exitp[k] = (int64_t)min_exit;
-    P.qpos[k] = qmax;
-    P.tail[k] = (uint32_t)tail;
-  }
-}
 
 // One thread per run of unresolved chunks (or, with `serial`, one thread for the whole log):
 // walks the true record chain with the reference iterator's own validity rules.
@@ -215,35 +60,6 @@ __global__ void k_walk(BuildParams P, int serial) {
     c++;
     p = record_end(h, p);
   }
-}
-
-// Per resolved chunk: entry from the predecessor (exit if it was resolved, else the walker's G),
-// head walk to the merge point q, count = head + tail.
-__global__ void k_count(BuildParams P) {
-  const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= P.nchunks || !P.conv[k]) return;
-  const int64_t g = (k == 0) ? kLogHeaderSize : (P.conv[k - 1] ? P.exitp[k - 1] : P.G[k]);
-  P.G[k] = g;
-  const int64_t q = P.qpos[k];
-  auto at = [&](int64_t a) -> uint32_t { return P.log[a]; };
-  int64_t p = g;
-  uint32_t h = 0;
-  while (p < q) {
-    const RecHdr r = decode_header(at, p, (int64_t)P.log_len);
-    if (!header_valid(r, p, P.max_key_len, (int64_t)P.log_len)) {
-      set_error(P.st, p, r.rc ? r.rc : kErrCorruptLog);
-      P.cnt[k] = 0;
-      return;
-    }
-    h++;
-    p = record_end(r, p);
-  }
-  if (p != q) {
-    atomicOr(&P.st->spec_fail, 1u);
-    P.cnt[k] = 0;
-    return;
-  }
-  P.cnt[k] = h + P.tail[k];
 }
 
 // ================================================================================================
@@ -310,157 +126,12 @@ __global__ __launch_bounds__(64) void k_emit(BuildParams P) {
     en.hash = hash;
     en.addr = addr;
     P.ent[base + i] = en;
-    const uint64_t w = fast_mod(hash, P.mod);
-    atomicAdd(&P.bcount[w >> kBucketShift], 1u);
   }
-}
-
-// ================================================================================================
-// Scans (3-phase, generic over the combine op; op(a, b) = "a then b").
-// ================================================================================================
-struct OpAdd {
-  __device__ __forceinline__ uint64_t operator()(uint64_t a, uint64_t b) const { return a + b; }
-  __device__ __forceinline__ uint64_t identity() const { return 0; }
-};
-// Carry functions f(x) = max(c, x + a) composed left to right: (f then g)(x) = g(f(x)).
-struct OpMaxPlus {
-  __device__ __forceinline__ MaxPlus operator()(MaxPlus f, MaxPlus g) const {
-    MaxPlus r;
-    r.c = max(g.c, f.c + g.a);
-    r.a = f.a + g.a;
-    return r;
-  }
-  __device__ __forceinline__ MaxPlus identity() const { return MaxPlus{0, 0}; }
-};
-
-template <class T, class Op, int BLOCK>
-__device__ T block_exclusive_scan(T v, T* sh, Op op, T* total) {
-  const int tid = threadIdx.x;
-  sh[tid] = v;
-  __syncthreads();
-  for (int o = 1; o < BLOCK; o <<= 1) {
-    T t = tid >= o ? sh[tid - o] : op.identity();
-    __syncthreads();
-    if (tid >= o) sh[tid] = op(t, sh[tid]);
-    __syncthreads();
-  }
-  if (total) *total = sh[BLOCK - 1];
-  T ex = tid ? sh[tid - 1] : op.identity();
-  __syncthreads();
-  return ex;
-}
-
-template <class In, class T, class Op>
-__global__ __launch_bounds__(kScanBlock) void k_scan_tiles(const In* in, T* out, T* tile_tot, uint64_t n, Op op) {
-  __shared__ T sh[kScanBlock];
-  const uint64_t base = (uint64_t)blockIdx.x * kScanTile + (uint64_t)threadIdx.x * kScanItems;
-  T v[kScanItems];
-  T acc = op.identity();
-#pragma unroll
-  for (int i = 0; i < kScanItems; i++) {
-    const uint64_t idx = base + i;
-    T x = idx < n ? (T)in[idx] : op.identity();
-    v[i] = acc;  // exclusive within the thread
-    acc = op(acc, x);
-  }
-  T tot;
-  const T pre = block_exclusive_scan<T, Op, kScanBlock>(acc, sh, op, &tot);
-#pragma unroll
-  for (int i = 0; i < kScanItems; i++) {
-    const uint64_t idx = base + i;
-    if (idx < n) out[idx] = op(pre, v[i]);
-  }
-  if (threadIdx.x == 0) tile_tot[blockIdx.x] = tot;
-}
-
-template <class T, class Op>
-__global__ void k_scan_add(T* out, const T* tile_pre, uint64_t n, Op op) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint64_t t = i / kScanTile;
-  if (t == 0) return;
-  out[i] = op(tile_pre[t], out[i]);
-}
-
-template <class In, class T, class Op>
-static void scan_exclusive(const In* in, T* out, uint64_t n, T* d_total, Op op, T* scratch, hipStream_t s) {
-  const uint64_t tiles = (n + kScanTile - 1) / kScanTile;
-  if (tiles <= 1) {
-    hipLaunchKernelGGL((k_scan_tiles<In, T, Op>), dim3(1), dim3(kScanBlock), 0, s, in, out, d_total, n, op);
-    return;
-  }
-  T* sums = scratch;
-  hipLaunchKernelGGL((k_scan_tiles<In, T, Op>), dim3((unsigned)tiles), dim3(kScanBlock), 0, s, in, out, sums, n, op);
-  scan_exclusive<T, T, Op>(sums, sums, tiles, d_total, op, scratch + tiles, s);
-  hipLaunchKernelGGL((k_scan_add<T, Op>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, out, sums, n, op);
 }
 
 // ================================================================================================
 // Placement.
 // ================================================================================================
-__global__ void k_scatter(BuildParams P) {
-  const uint64_t N = P.st->n_records;
-  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < N && i < P.max_records; i += stride) {
-    const Entry en = P.ent[i];
-    const uint64_t b = fast_mod(en.hash, P.mod) >> kBucketShift;
-    const uint64_t pos = P.boff[b] + atomicAdd(&P.bcursor[b], 1u);
-    P.ent2[pos] = en;
-  }
-}
-
-// Per bucket: LDS histogram of local wanted slots and its exclusive scan; returns n.
-__device__ __forceinline__ void bucket_histogram(const BuildParams& P, uint64_t b, uint32_t n, uint64_t eoff,
-                                                 uint64_t start, uint32_t* cnt) {
-  for (int t = threadIdx.x; t < kBucket; t += kPlaceBlock) cnt[t] = 0;
-  __syncthreads();
-  for (uint32_t i = threadIdx.x; i < n; i += kPlaceBlock) {
-    const uint64_t w = fast_mod(P.ent2[eoff + i].hash, P.mod) - start;
-    atomicAdd(&cnt[w], 1u);
-  }
-  __syncthreads();
-}
-
-// For the bucket's bins (kBinsPerThread consecutive bins per thread): exclusive base[s] and the
-// inclusive prefix max M(s) of (s - base[s]) over occupied bins.
-__device__ __forceinline__ void bucket_scan(const uint32_t* cnt, uint32_t* base, int32_t* M, uint64_t* sh64,
-                                            int64_t* shm, uint32_t* last_max) {
-  const int tid = threadIdx.x;
-  const int s0 = tid * kBinsPerThread;
-  uint64_t local = 0;
-#pragma unroll
-  for (int i = 0; i < kBinsPerThread; i++) local += cnt[s0 + i];
-  const uint64_t pre = block_exclusive_scan<uint64_t, OpAdd, kPlaceBlock>(local, sh64, OpAdd(), nullptr);
-  int64_t run = -(1ll << 40);
-  uint64_t acc = pre;
-  int64_t vals[kBinsPerThread];
-#pragma unroll
-  for (int i = 0; i < kBinsPerThread; i++) {
-    base[s0 + i] = (uint32_t)acc;
-    vals[i] = cnt[s0 + i] ? (int64_t)(s0 + i) - (int64_t)acc : -(1ll << 40);
-    acc += cnt[s0 + i];
-    run = max(run, vals[i]);
-  }
-  // exclusive max-scan of per-thread maxima
-  shm[tid] = run;
-  __syncthreads();
-  for (int o = 1; o < kPlaceBlock; o <<= 1) {
-    int64_t t = tid >= o ? shm[tid - o] : -(1ll << 40);
-    __syncthreads();
-    if (tid >= o) shm[tid] = max(shm[tid], t);
-    __syncthreads();
-  }
-  int64_t m = tid ? shm[tid - 1] : -(1ll << 40);
-  const int64_t all_max = shm[kPlaceBlock - 1];
-  __syncthreads();
-#pragma unroll
-  for (int i = 0; i < kBinsPerThread; i++) {
-    m = max(m, vals[i]);
-    M[s0 + i] = (int32_t)max(m, (int64_t)INT32_MIN);
-  }
-  if (last_max) *last_max = (uint32_t)(all_max < 0 ? 0 : all_max);
-}
-
 // Carry function of a bucket (DESIGN.md "canonical placement"): entries overflowing past the
 // bucket end as a function of the carry-in x is out(x) = max(c, x + a), c = max(0, n + M_last - B),
 // a = n - B.
@@ -499,127 +170,17 @@ __global__ void k_carry(BuildParams P) {
   P.carry[b] = max(pre.c, tot.c + pre.a);
 }
 
-__device__ __forceinline__ void write_slot(const BuildParams& P, uint64_t slot, uint64_t hash, uint64_t addr) {
-  uint8_t* p = P.out + kIndexHeaderSize + slot * (uint64_t)P.slot_size;
-  if (P.slot_size == 16) {
-    *reinterpret_cast<uint4*>(p) = make_uint4((uint32_t)hash, (uint32_t)(hash >> 32), (uint32_t)addr, (uint32_t)(addr >> 32));
-  } else if (P.slot_size == 8) {
-    *reinterpret_cast<uint2*>(p) = make_uint2((uint32_t)hash, (uint32_t)addr);
-  } else if (P.hash_size == 8) {  // 8 + 4
-    uint32_t* q = reinterpret_cast<uint32_t*>(p);
-    q[0] = (uint32_t)hash; q[1] = (uint32_t)(hash >> 32); q[2] = (uint32_t)addr;
-  } else {  // 4 + 8
-    uint32_t* q = reinterpret_cast<uint32_t*>(p);
-    q[0] = (uint32_t)hash; q[1] = (uint32_t)addr; q[2] = (uint32_t)(addr >> 32);
-  }
-}
-
-__device__ __forceinline__ uint64_t wrap_slot(uint64_t s, uint64_t cap) {
-  while (s >= cap) s -= cap;
-  return s;
-}
-
-__device__ __forceinline__ bool entry_less(const Entry& a, const Entry& b) {
-  return (a.addr & ~kDelBit) < (b.addr & ~kDelBit);
-}
-
-__global__ __launch_bounds__(kPlaceBlock) void k_place(BuildParams P) {
+// Global-memory placement of every bucket (buckets too big for k_place_lds), or, with
+// sort_only, the (wantedSlot, address) order of every bucket into ent3 for the SORTING restatement.
+__global__ __launch_bounds__(kPlaceBlock) void k_place(BuildParams P, int sort_only, int only_big) {
   __shared__ uint32_t cnt[kBucket];
   __shared__ uint32_t base[kBucket];
   __shared__ int32_t M[kBucket];
   __shared__ int32_t slot_of[kBucket];
   __shared__ uint64_t sh64[kPlaceBlock];
   __shared__ int64_t shm[kPlaceBlock];
-  const uint64_t b = blockIdx.x;
-  const uint64_t start = b << kBucketShift;
-  const int64_t bsize = (int64_t)min((uint64_t)kBucket, P.cap - start);
-  const uint32_t n = P.bcount[b];
-  const uint64_t eoff = P.boff[b];
-  const int tid = threadIdx.x;
-  bucket_histogram(P, b, n, eoff, start, cnt);
-  bucket_scan(cnt, base, M, sh64, shm, nullptr);
-  // counting sort of the bucket's entries by wanted slot into ent3 (cnt reused as cursor)
-  for (int t = tid; t < kBucket; t += kPlaceBlock) slot_of[t] = 0;
-  __syncthreads();
-  for (uint32_t i = tid; i < n; i += kPlaceBlock) {
-    const Entry en = P.ent2[eoff + i];
-    const uint64_t w = fast_mod(en.hash, P.mod) - start;
-    const uint32_t r = atomicAdd((uint32_t*)&slot_of[w], 1u);
-    P.ent3[eoff + base[w] + r] = en;
-  }
-  __threadfence_block();
-  __syncthreads();
-  // equal wanted slots: order by address (ENTRY_COMPARATOR, SortHelper.java:42); flag equal-hash
-  // pairs for the duplicate-key check (IndexHash.java:606-636 replaces in place on equal keys).
-  for (int i = 0; i < kBinsPerThread; i++) {
-    const int s = tid * kBinsPerThread + i;
-    const uint32_t g = cnt[s];
-    if (g < 2) continue;
-    Entry* grp = P.ent3 + eoff + base[s];
-    if (g <= kGroupMax) {
-      for (uint32_t x = 1; x < g; x++) {
-        const Entry v = grp[x];
-        uint32_t y = x;
-        while (y > 0 && entry_less(v, grp[y - 1])) { grp[y] = grp[y - 1]; y--; }
-        grp[y] = v;
-      }
-      for (uint32_t x = 0; x < g; x++) {
-        for (uint32_t y = x + 1; y < g; y++) {
-          if (grp[x].hash == grp[y].hash && !(grp[x].addr & kDelBit) && !(grp[y].addr & kDelBit)) {
-            const unsigned long long slotn = atomicAdd(&P.st->n_pairs, 1ull);
-            if (slotn < P.pair_cap) {
-              P.pairs[2 * slotn] = grp[x].addr;
-              P.pairs[2 * slotn + 1] = grp[y].addr;
-            }
-          }
-        }
-      }
-    } else {  // pathological group (massive duplicates): shell sort, defer to the exact path
-      for (uint32_t gap = g / 2; gap > 0; gap /= 2) {
-        for (uint32_t x = gap; x < g; x++) {
-          const Entry v = grp[x];
-          uint32_t y = x;
-          while (y >= gap && entry_less(v, grp[y - gap])) { grp[y] = grp[y - gap]; y -= gap; }
-          grp[y] = v;
-        }
-      }
-      atomicOr(&P.st->dup_overflow, 1u);
-    }
-  }
-  __threadfence_block();
-  __syncthreads();
-  if (P.st->full) return;
-  const int64_t x = P.carry[b];
-  for (int t = tid; t < kBucket; t += kPlaceBlock) slot_of[t] = -1;
-  __syncthreads();
-  // slot of the j-th entry in (wanted, address) order: j + max(carry, M(s))
-  for (int i = 0; i < kBinsPerThread; i++) {
-    const int s = tid * kBinsPerThread + i;
-    const uint32_t g = cnt[s];
-    if (!g) continue;
-    const int64_t shift = max(x, (int64_t)M[s]);
-    for (uint32_t r = 0; r < g; r++) {
-      const int64_t j = (int64_t)base[s] + r;
-      const int64_t p = j + shift;
-      if (p < bsize) {
-        slot_of[p] = (int32_t)j;
-      } else {
-        const Entry en = P.ent3[eoff + j];
-        write_slot(P, wrap_slot(start + (uint64_t)p, P.cap), en.hash, en.addr & ~kDelBit);
-      }
-    }
-  }
-  __syncthreads();
-  // every slot of [x, bsize) is this bucket's: an own entry or empty (zero)
-  for (int64_t t = x + tid; t < bsize; t += kPlaceBlock) {
-    const int32_t j = slot_of[t];
-    if (j >= 0) {
-      const Entry en = P.ent3[eoff + j];
-      write_slot(P, start + (uint64_t)t, en.hash, en.addr & ~kDelBit);
-    } else {
-      write_slot(P, start + (uint64_t)t, 0, 0);
-    }
-  }
+  if (only_big && P.bcount[blockIdx.x] <= kPlaceLdsMax) return;
+  place_bucket_global(P, blockIdx.x, sort_only, cnt, base, M, slot_of, sh64, shm);
 }
 
 // Equal-hash pairs: do they share the key?  (the reference compares key bytes in the log,
@@ -645,23 +206,6 @@ __global__ void k_verify_pairs(BuildParams P) {
 // Stats: calculateMaxDisplacement (IndexHash.java:195-245).  hashCollisions compares a slot's hash
 // with the previous OCCUPIED slot's hash even when the current slot is empty (its hash reads 0).
 // ================================================================================================
-__device__ __forceinline__ void read_slot(const BuildParams& P, uint64_t slot, uint64_t& hash, uint64_t& addr) {
-  const uint8_t* p = P.out + kIndexHeaderSize + slot * (uint64_t)P.slot_size;
-  if (P.slot_size == 16) {
-    const uint4 v = *reinterpret_cast<const uint4*>(p);
-    hash = (uint64_t)v.x | ((uint64_t)v.y << 32);
-    addr = (uint64_t)v.z | ((uint64_t)v.w << 32);
-  } else if (P.slot_size == 8) {
-    const uint2 v = *reinterpret_cast<const uint2*>(p);
-    hash = v.x;
-    addr = v.y;
-  } else {
-    const uint32_t* q = reinterpret_cast<const uint32_t*>(p);
-    if (P.hash_size == 8) { hash = (uint64_t)q[0] | ((uint64_t)q[1] << 32); addr = q[2]; }
-    else { hash = q[0]; addr = (uint64_t)q[1] | ((uint64_t)q[2] << 32); }
-  }
-}
-
 __global__ __launch_bounds__(kStatBlock) void k_stats(BuildParams P) {
   __shared__ uint64_t sh_hash[kStatBlock];
   __shared__ uint32_t sh_occ[kStatBlock];
@@ -955,16 +499,6 @@ __global__ void k_sequential(BuildParams P, int sorted_order) {
 // ================================================================================================
 static inline unsigned grid_for(uint64_t n, unsigned block) { return (unsigned)((n + block - 1) / block); }
 
-void launch_framing(const BuildParams& P, hipStream_t s, StageTimer* tm) {
-  if (P.nchunks == 0) return;
-  hipLaunchKernelGGL(k_speculate, dim3((unsigned)P.nchunks), dim3(64), 0, s, P);
-  tm->mark("speculate", s);
-  hipLaunchKernelGGL(k_walk, dim3(grid_for(P.nchunks, 256)), dim3(256), 0, s, P, 0);
-  tm->mark("walk", s);
-  hipLaunchKernelGGL(k_count, dim3(grid_for(P.nchunks, 256)), dim3(256), 0, s, P);
-  tm->mark("count", s);
-}
-
 void launch_framing_serial(const BuildParams& P, hipStream_t s) {
   if (P.nchunks == 0) return;
   hipLaunchKernelGGL(k_walk, dim3(1), dim3(64), 0, s, P, 1);
@@ -974,25 +508,23 @@ void launch_emit(const BuildParams& P, hipStream_t s, StageTimer* tm) {
   if (P.nchunks == 0) return;
   scan_exclusive<uint32_t, uint64_t, OpAdd>(P.cnt, P.off, P.nchunks, (uint64_t*)&P.st->n_records, OpAdd(),
                                             P.scan_scratch_u64, s);
-  tm->mark("scan_chunks", s);
   hipLaunchKernelGGL(k_emit, dim3((unsigned)P.nchunks), dim3(64), 0, s, P);
   tm->mark("emit", s);
 }
 
-void launch_place(const BuildParams& P, hipStream_t s, StageTimer* tm) {
-  scan_exclusive<uint32_t, uint64_t, OpAdd>(P.bcount, P.boff, P.nbuckets, P.boff + P.nbuckets, OpAdd(),
-                                            P.scan_scratch_u64, s);
-  tm->mark("scan_buckets", s);
-  hipLaunchKernelGGL(k_scatter, dim3(2048), dim3(256), 0, s, P);
-  tm->mark("scatter", s);
+void launch_summary_carry(const BuildParams& P, hipStream_t s, StageTimer* tm) {
   hipLaunchKernelGGL(k_summary, dim3((unsigned)P.nbuckets), dim3(kPlaceBlock), 0, s, P);
-  tm->mark("summary", s);
   scan_exclusive<MaxPlus, MaxPlus, OpMaxPlus>(P.bfun, P.bpre, P.nbuckets, P.bfun_total, OpMaxPlus(),
                                               P.scan_scratch_mp, s);
   hipLaunchKernelGGL(k_carry, dim3(grid_for(P.nbuckets, 256)), dim3(256), 0, s, P);
-  tm->mark("carry", s);
-  hipLaunchKernelGGL(k_place, dim3((unsigned)P.nbuckets), dim3(kPlaceBlock), 0, s, P);
-  tm->mark("place", s);
+  tm->mark("summary", s);
+}
+
+void launch_place_global(const BuildParams& P, hipStream_t s, int sort_only, int only_big) {
+  hipLaunchKernelGGL(k_place, dim3((unsigned)P.nbuckets), dim3(kPlaceBlock), 0, s, P, sort_only, only_big);
+}
+
+void launch_verify(const BuildParams& P, hipStream_t s, StageTimer* tm) {
   hipLaunchKernelGGL(k_verify_pairs, dim3(grid_for(P.pair_cap, 256)), dim3(256), 0, s, P);
   tm->mark("verify", s);
 }

@@ -23,6 +23,11 @@ constexpr int kScanItems = 16;
 constexpr uint64_t kScanTile = (uint64_t)kScanBlock * kScanItems;
 constexpr int kStatBlock = 256;
 constexpr int kStatSlotsPerBlock = 4096;
+constexpr int kPartBlock = 256;                   // radix partition of the entries by bucket
+constexpr int kPartItems = 16;
+constexpr int kPartTile = kPartBlock * kPartItems;
+constexpr int kPart2MaxBits = 14;                 // fine digit of the partition (<= 16384 buckets)
+constexpr uint32_t kPlaceLdsMax = 1536;           // entries of a bucket staged in LDS
 
 // One log record as the placement sees it: 16 bytes, AoS so every access is one dwordx4.
 struct alignas(16) Entry {
@@ -50,7 +55,7 @@ struct Status {
   unsigned int dup_overflow;
   unsigned int full;       // records >= capacity
   unsigned int overflow;   // more records than workspace
-  unsigned int pad;
+  unsigned int big_buckets;  // some bucket exceeded kPlaceLdsMax (placed by the global kernel)
   unsigned long long n_records;
   unsigned long long n_deletes;
   unsigned long long n_pairs;
@@ -108,6 +113,25 @@ struct BuildParams {
   StatPart* parts;
   uint64_t* scan_scratch_u64;
   MaxPlus* scan_scratch_mp;
+  // k_frame granules (zeroed before every launch)
+  unsigned long long* exit_desc;
+  unsigned long long* cnt_desc;
+  // radix partition
+  uint32_t* p1_hist;  // [256][p1_tiles]
+  uint64_t* p1_off;
+  uint64_t* p1_off_total;
+  uint32_t p1_tiles;
+  int32_t p2_bits;
+  unsigned long long* dbg;  // diagnostic phase counters (SPARKEY_FRAME_DEBUG=1), else null
+  // k_frame geometry (chunk C = 2^fr_cshift bytes, fr_w chunks per wave)
+  int32_t fr_cshift;
+  int32_t fr_w;
+  int32_t fr_look;       // speculative walks continue this many bytes past their chunk
+  int32_t fr_rgn_bytes;  // LDS region per wave: W * C + fr_look + 16, rounded up to 256 bytes
+  int32_t fr_mask_words;
+  int32_t fr_fast;  // maxKeyLen + 1 < 128 and maxValueLen < 128: canonical headers are 2 bytes
+  int32_t no_deletes;  // the log header counts no DELETE: speculation treats 0x00 as no record start
+  uint64_t fr_nchunks;
 };
 
 // Per-stage HIP events on the build stream (only when profiling is enabled).
@@ -137,10 +161,16 @@ struct StageTimer {
   }
 };
 
-void launch_framing(const BuildParams& P, hipStream_t s, StageTimer* tm);
+// fast path (fused_kernels.hip)
+void launch_frame_fused(const BuildParams& P, hipStream_t s, StageTimer* tm);
+void launch_partition(const BuildParams& P, hipStream_t s, StageTimer* tm);
+void launch_place_fast(const BuildParams& P, hipStream_t s, StageTimer* tm);
+// fallbacks and shared stages (build_kernels.hip)
 void launch_framing_serial(const BuildParams& P, hipStream_t s);
 void launch_emit(const BuildParams& P, hipStream_t s, StageTimer* tm);
-void launch_place(const BuildParams& P, hipStream_t s, StageTimer* tm);
+void launch_summary_carry(const BuildParams& P, hipStream_t s, StageTimer* tm);
+void launch_place_global(const BuildParams& P, hipStream_t s, int sort_only, int only_big);
+void launch_verify(const BuildParams& P, hipStream_t s, StageTimer* tm);
 void launch_stats(const BuildParams& P, hipStream_t s, int sequential, StageTimer* tm);
 void launch_sequential(const BuildParams& P, hipStream_t s, int sorted_order);
 

@@ -1,0 +1,808 @@
+// fused_kernels.hip -- the fast path of the .spi build on gfx950.
+//
+//   k_frame          ONE pass over the log: a wave owns 64 small chunks (lane = chunk):
+//                    speculative framing -> wave exit published at once -> entry from the previous
+//                    wave's exit -> record count prefix by decoupled look-back -> MurmurHash3 of
+//                    every key out of LDS -> (hash, address) entries in log order.
+//   k_part1_hist/    coarse radix partition of the entries by the top 8 bits of their bucket id
+//   k_part1_scatter  (bucket = wantedSlot >> 10), LDS-staged so every write run is contiguous.
+//   k_part2          one workgroup per coarse partition: fine split into buckets + bucket offsets.
+//   k_place_lds      per bucket, everything in LDS: counting sort by wanted slot, address order
+//                    inside equal slots, canonical positions, every slot of the bucket written once.
+//
+// Inter-workgroup hand-offs in k_frame use 8-byte granules that carry their own state bits
+// (MI355X_MICROARCH.md "Valid forms", R2: the data IS the flag) with relaxed agent-scope atomic
+// loads/stores; every granule is zeroed before the launch and every spin is time-bounded.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "build_kernels.hpp"
+#include "device_common.hpp"
+#include "kernel_utils.hpp"
+#include "scan.hpp"
+#include "place_common.hpp"
+
+namespace sk {
+
+// ------------------------------------------------------------------------------------------------
+// LDS byte access
+// ------------------------------------------------------------------------------------------------
+// 8 bytes starting at any offset of an 8-byte-aligned LDS window (two aligned 8-byte reads).
+__device__ __forceinline__ uint64_t lds_u64_at(const uint8_t* win, int off) {
+  const uint64_t* w = reinterpret_cast<const uint64_t*>(win + (off & ~7));
+  const uint64_t lo = w[0];
+  const uint64_t hi = w[1];
+  const int sh = (off & 7) * 8;
+  return sh ? (lo >> sh) | (hi << (64 - sh)) : lo;
+}
+
+// Record header at absolute position p whose bytes lie in the LDS window starting at wb.
+// Fast path: both VLQs one byte (every key < 127 bytes and value < 128 bytes); otherwise the
+// generic Java-int VLQ decoder on the same bytes.
+__device__ __forceinline__ RecHdr decode_lds(const uint8_t* win, int64_t wb, int64_t p, int64_t avail) {
+  const uint64_t x = lds_u64_at(win, (int)(p - wb));
+  RecHdr h;
+  if ((x & 0x8080ull) == 0) {
+    h.rc = 0;
+    h.hlen = 2;
+    const int32_t first = (int32_t)(x & 0xff);
+    const int32_t second = (int32_t)((x >> 8) & 0xff);
+    if (first == 0) { h.put = 0; h.klen = second; h.vlen = 0; }
+    else { h.put = 1; h.klen = first - 1; h.vlen = second; }
+  } else {
+    auto at = [&](int64_t a) -> uint32_t { return win[a - wb]; };
+    h = decode_header(at, p, p + 12);
+  }
+  if (h.rc == 0 && p + h.hlen > avail) h.rc = kErrCorruptLog;
+  return h;
+}
+
+// Key byte loaders for the hashes: u64(o) = the 8 key bytes starting at key offset o (the bytes
+// past the key are read but masked off).
+struct LdsKey {  // key in an 8-byte aligned LDS window
+  const uint8_t* win;
+  int base;
+  __device__ __forceinline__ uint64_t u64(int o) const { return lds_u64_at(win, base + o); }
+};
+struct GlobalKey {  // key in global memory with at least 16 readable bytes past its end
+  const uint8_t* p;
+  __device__ __forceinline__ uint64_t u64(int o) const {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p + o);
+    const uint64_t* q = reinterpret_cast<const uint64_t*>(a & ~(uintptr_t)7);
+    const uint64_t lo = q[0], hi = q[1];
+    const int sh = (int)(a & 7) * 8;
+    return sh ? (lo >> sh) | (hi << (64 - sh)) : lo;
+  }
+};
+
+// MurmurHash3 x86_32 of `len` key bytes (MurmurHash3.java:18-75).
+template <class Ld>
+__device__ inline uint32_t murmur32_ld(const Ld& ld, int32_t len, uint32_t seed) {
+  const uint32_t c1 = 0xcc9e2d51u, c2 = 0x1b873593u;
+  uint32_t h1 = seed;
+  const int32_t nblocks = len >> 2;
+  auto block = [&](uint32_t k1) {
+    k1 *= c1; k1 = rotl32(k1, 15); k1 *= c2;
+    h1 ^= k1; h1 = rotl32(h1, 13); h1 = h1 * 5 + 0xe6546b64u;
+  };
+  int32_t i = 0;
+  for (; i + 1 < nblocks; i += 2) {
+    const uint64_t x = ld.u64(4 * i);
+    block((uint32_t)x);
+    block((uint32_t)(x >> 32));
+  }
+  if (i < nblocks) block((uint32_t)ld.u64(4 * i));
+  const int32_t rem = len & 3;
+  if (rem) {
+    uint32_t k1 = (uint32_t)ld.u64(4 * nblocks) & ((1u << (8 * rem)) - 1u);
+    k1 *= c1; k1 = rotl32(k1, 15); k1 *= c2; h1 ^= k1;
+  }
+  h1 ^= (uint32_t)len;
+  h1 ^= h1 >> 16; h1 *= 0x85ebca6bu; h1 ^= h1 >> 13; h1 *= 0xc2b2ae35u; h1 ^= h1 >> 16;
+  return h1;
+}
+
+// MurmurHash3 x64_128 -> h1 of `len` key bytes (MurmurHash3.java:100-201).
+template <class Ld>
+__device__ inline uint64_t murmur64_ld(const Ld& ld, int32_t len, uint32_t seed) {
+  const uint64_t c1 = 0x87c37b91114253d5ull, c2 = 0x4cf5ad432745937full;
+  uint64_t h1 = (uint64_t)seed, h2 = h1;
+  const int32_t nblocks = len >> 4;
+  for (int32_t i = 0; i < nblocks; i++) {
+    uint64_t k1 = ld.u64(16 * i);
+    uint64_t k2 = ld.u64(16 * i + 8);
+    k1 *= c1; k1 = rotl64(k1, 31); k1 *= c2; h1 ^= k1;
+    h1 = rotl64(h1, 27); h1 += h2; h1 = h1 * 5 + 0x52dce729ull;
+    k2 *= c2; k2 = rotl64(k2, 33); k2 *= c1; h2 ^= k2;
+    h2 = rotl64(h2, 31); h2 += h1; h2 = h2 * 5 + 0x38495ab5ull;
+  }
+  const int32_t rem = len & 15;
+  const int t = 16 * nblocks;
+  if (rem > 8) {
+    uint64_t k2 = ld.u64(t + 8) & ((1ull << (8 * (rem - 8))) - 1ull);
+    k2 *= c2; k2 = rotl64(k2, 33); k2 *= c1; h2 ^= k2;
+  }
+  if (rem > 0) {
+    uint64_t k1 = ld.u64(t);
+    if (rem < 8) k1 &= (1ull << (8 * rem)) - 1ull;
+    k1 *= c1; k1 = rotl64(k1, 31); k1 *= c2; h1 ^= k1;
+  }
+  h1 ^= (uint64_t)(int64_t)len;
+  h2 ^= (uint64_t)(int64_t)len;
+  h1 += h2; h2 += h1;
+  h1 = fmix64(h1); h2 = fmix64(h2);
+  h1 += h2;
+  return h1;
+}
+
+// ------------------------------------------------------------------------------------------------
+// granules (8-byte {state, value} words) -- relaxed agent-scope atomics, zeroed before the launch
+// ------------------------------------------------------------------------------------------------
+constexpr unsigned long long kReady = 1ull << 63;   // exit granule: bit 63 = published
+constexpr unsigned long long kAgg = 1ull << 62;     // count granule: local aggregate published
+constexpr unsigned long long kIncl = 2ull << 62;    // count granule: inclusive prefix published
+constexpr unsigned long long kStateMask = 3ull << 62;
+constexpr unsigned long long kSpinTicks = 2000000000ull;  // 20 s of the 100 MHz wall clock
+
+__device__ __forceinline__ void granule_store(unsigned long long* g, unsigned long long v) {
+  __hip_atomic_store(g, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long granule_load(unsigned long long* g) {
+  return __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// ================================================================================================
+// k_frame: one wave owns W consecutive chunks of C = 2^fr_cshift bytes (lane j owns chunk k0 + j),
+// staged contiguously in one XOR-swizzled LDS region together with fr_look + 16 bytes past the
+// last chunk.  C >= maxRecLen, so every chunk but a short last one holds a record start, and its
+// first one lies within maxRecLen bytes of the chunk start.
+//   1 screen    every candidate start in [s, s + maxRecLen): 8 at a time from one u64, all lanes
+//   2 walk      screened candidates in lock step, past the chunk end up to fr_look more bytes (the
+//               next chunks' bytes are in the same region): a false start rarely stays plausible
+//               that long.  exit = first record start >= chunk end on the chain.
+//   3 entries   a chunk whose surviving chains share one exit knows it without its entry; the
+//               wave's last exit is published at once, the first entry is the previous wave's
+//               published exit, unresolved chunks are walked in order
+//   4 counts    record counts, wave scan, decoupled look-back across waves for the base offset
+//   5 hash      every lane walks its chunk from the verified entry and hashes each key from LDS
+// ================================================================================================
+__device__ __forceinline__ bool screen_start(uint32_t b0, uint32_t b1, const BuildParams& P) {
+  // Canonical VLQs (what LogWriter writes).  Pruning a true start only costs speed: the chunk is
+  // then unresolved or disagrees with its verified walk, and is re-walked exactly.
+  if (b0 == 0) return P.max_key_len >= 128 || (int64_t)b1 <= P.max_key_len;  // DELETE, VLQ(keyLen)
+  if (b0 >= 0x80) return P.max_key_len + 1 >= 128;                            // multi-byte keyLen+1
+  if ((int64_t)b0 - 1 > P.max_key_len) return false;
+  return P.max_value_len >= 128 || (int64_t)b1 <= P.max_value_len;            // PUT, VLQ(valueLen)
+}
+
+__device__ __forceinline__ uint4 load16_guarded(const uint8_t* log, int64_t a, int64_t log_len) {
+  if (a + 16 <= log_len) return *reinterpret_cast<const uint4*>(log + a);
+  uint8_t tmp[16];
+#pragma unroll
+  for (int i = 0; i < 16; i++) tmp[i] = (a + i < log_len) ? log[a + i] : 0;
+  return *reinterpret_cast<uint4*>(tmp);
+}
+
+// 16-byte-unit XOR swizzle of the region (a bijection on every 256-byte block): lanes reading the
+// same offset of their own chunk fall on different LDS banks.
+__device__ __forceinline__ uint32_t rswz(uint32_t o) {
+  const uint32_t u = o >> 4;
+  return ((u ^ ((u >> 4) & 15u)) << 4) | (o & 15u);
+}
+// 8 bytes at any region offset (two aligned 8-byte reads; the region is allocated in 256 B blocks)
+__device__ __forceinline__ uint64_t rgn_u64(const uint8_t* r, uint32_t o) {
+  const uint32_t a = o & ~7u;
+  const uint64_t lo = *reinterpret_cast<const uint64_t*>(r + rswz(a));
+  const uint64_t hi = *reinterpret_cast<const uint64_t*>(r + rswz(a + 8));
+  const uint32_t sh = (o & 7u) * 8u;
+  return sh ? (lo >> sh) | (hi << (64 - sh)) : lo;
+}
+struct RgnKey {
+  const uint8_t* r;
+  uint32_t base;
+  __device__ __forceinline__ uint64_t u64(int o) const { return rgn_u64(r, base + (uint32_t)o); }
+};
+
+// Record header at absolute position p inside the region (p - R0 + 16 <= region bytes).
+__device__ __forceinline__ RecHdr decode_rgn(const uint8_t* r, int64_t R0, int64_t p, int64_t avail) {
+  const uint64_t x = rgn_u64(r, (uint32_t)(p - R0));
+  RecHdr h;
+  if ((x & 0x8080ull) == 0) {
+    h.rc = 0;
+    h.hlen = 2;
+    const int32_t first = (int32_t)(x & 0xff);
+    const int32_t second = (int32_t)((x >> 8) & 0xff);
+    if (first == 0) { h.put = 0; h.klen = second; h.vlen = 0; }
+    else { h.put = 1; h.klen = first - 1; h.vlen = second; }
+  } else {
+    auto at = [&](int64_t a) -> uint32_t { return r[rswz((uint32_t)(a - R0))]; };
+    h = decode_header(at, p, p + 12);
+  }
+  if (h.rc == 0 && p + h.hlen > avail) h.rc = kErrCorruptLog;
+  return h;
+}
+
+__global__ __launch_bounds__(64) void k_frame(BuildParams P) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int lane = threadIdx.x;
+  const uint64_t wv = blockIdx.x;
+  const int cs = P.fr_cshift;
+  const int64_t C = 1ll << cs;
+  const int W = P.fr_w;
+  const int64_t LOOK = P.fr_look;
+  const int nwords = P.fr_mask_words;
+  const int64_t log_len = (int64_t)P.log_len;
+  const uint64_t k0 = wv * (uint64_t)W;
+  const int nw = (int)min((uint64_t)W, P.fr_nchunks - k0);
+  const int64_t R0 = (int64_t)(k0 << cs);
+  const int64_t RLEN = ((int64_t)nw << cs) + LOOK + 16;  // staged bytes [R0, R0 + RLEN)
+  const int64_t RUSE = R0 + RLEN - 16;                     // headers decodable in LDS below this
+  uint8_t* rgn = lds;
+  unsigned long long* masks = reinterpret_cast<unsigned long long*>(lds + P.fr_rgn_bytes);
+  unsigned long long t_prev = P.dbg ? __builtin_amdgcn_s_memtime() : 0;
+  auto mark = [&](int i) {  // diagnostic only: cycles per phase, per wave (no atomics)
+    if (P.dbg && lane == 0) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      P.dbg[wv * 16 + i] = t - t_prev;
+      t_prev = t;
+    }
+  };
+
+  // ---- stage: [R0, R0 + RLEN) once, coalesced, 16 bytes per lane per step ----
+  for (int v = lane; v < (int)((RLEN + 15) >> 4); v += 64) {
+    const uint4 val = load16_guarded(P.log, R0 + 16ll * v, log_len);
+    *reinterpret_cast<uint4*>(rgn + rswz(16u * v)) = val;
+  }
+  __syncthreads();
+  mark(0);
+
+  const bool act = lane < nw;
+  const uint64_t k = k0 + lane;
+  const int64_t wb = (int64_t)(k << cs);
+  const int64_t s = (k == 0) ? kLogHeaderSize : wb;
+  const int64_t e = act ? min(wb + C, P.data_end) : wb;
+  const int64_t stop = min(min(e + LOOK, P.data_end), RUSE);  // speculative walks end here
+  const bool passthrough = k > 0 && s + P.max_rec_len - 1 >= e;
+  const int64_t cand_end = !act || passthrough ? s : (k == 0 ? s + 1 : min(e, s + P.max_rec_len));
+
+  // ---- 1 screen: 8 candidate starts per step, branch-free (SWAR on one u64) ----
+  {
+    constexpr uint64_t H = 0x8080808080808080ull, L7 = 0x7f7f7f7f7f7f7f7full, ONES = 0x0101010101010101ull;
+    // per byte: b <= T with b < 128 (T >= 127: every byte); thresholds replicated once, outside the loop
+    const int64_t TK = P.max_key_len + 1 >= 128 ? 127 : P.max_key_len + 1;
+    const bool allk = P.max_key_len + 1 >= 128, allv = P.max_value_len >= 127, alld = P.max_key_len >= 127;
+    const uint64_t rk = ONES * (uint64_t)(min(TK, (int64_t)126) + 1);
+    const uint64_t rv = ONES * (uint64_t)(min(P.max_value_len, (int64_t)126) + 1);
+    const uint64_t rd = ONES * (uint64_t)(min(P.max_key_len, (int64_t)126) + 1);
+    auto le_rep = [&](uint64_t x, uint64_t rep, bool all) -> uint64_t { return all ? H : ~(x | ((x | H) - rep)) & H; };
+    const int nq = (int)((min(C, P.max_rec_len) + 7) >> 3);
+    unsigned long long word = 0;
+    for (int q = 0; q < nq; q++) {
+      const int64_t c0 = s + 8ll * q;
+      uint32_t bits = 0;
+      if (c0 < cand_end) {
+        const uint32_t o = (uint32_t)(c0 - R0);
+        const uint64_t x = rgn_u64(rgn, o);
+        const uint64_t y = (x >> 8) | ((uint64_t)rgn[rswz(o + 8)] << 56);
+        const uint64_t z = ~(((x & L7) + L7) | x) & H;  // zero bytes
+        const uint64_t put_first = le_rep(x, rk, allk) & ~z;
+        // a log whose header counts no DELETE has none on its true chain: a 0x00 is no record start
+        const uint64_t r = (put_first & le_rep(y, rv, allv)) | (P.no_deletes ? 0ull : (z & le_rep(y, rd, alld)));
+        uint64_t t = (r >> 7) & ONES;  // gather the 8 flags into the low byte
+        t |= t >> 7;
+        t |= t >> 14;
+        t |= t >> 28;
+        bits = (uint32_t)(t & 0xffu);
+        const int64_t valid = cand_end - c0;
+        if (valid < 8) bits &= (1u << valid) - 1u;
+      }
+      word |= (unsigned long long)bits << (8 * (q & 7));
+      if ((q & 7) == 7 || q == nq - 1) {
+        if (act) masks[lane * nwords + (q >> 3)] = word;
+        word = 0;
+      }
+    }
+  }
+  mark(1);
+
+  // ---- 2 walk the screened candidates in lock step (one header per lane per step) ----
+  unsigned long long nsurv = 0, min_exit = ~0ull, c_min = ~0ull;
+  long long max_exit = -1;
+  int32_t c_min_steps = 0;
+  unsigned long long dbg_iters = 0;
+  {
+    const int nwl = (int)((min(C, P.max_rec_len) + 63) >> 6);
+    int wi = 0;
+    unsigned long long m = (act && cand_end > s) ? masks[lane * nwords] : 0ull;
+    bool done = !act || cand_end <= s;
+    int32_t steps = 0;
+    if (P.fr_fast) {
+      // canonical one-byte VLQs only (keys < 127 bytes, values < 128 bytes): region offsets in
+      // 32 bits, no generic decoder in the loop
+      const int32_t re = (int32_t)(e - R0), rstop = (int32_t)(stop - R0);
+      const int64_t lim64 = log_len - R0;
+      const int32_t lim = lim64 > 0x7fffffff ? 0x7fffffff : (int32_t)lim64;
+      const int32_t mk = (int32_t)P.max_key_len, mv = (int32_t)P.max_value_len;
+      int32_t rp = -1, rst = 0, rex = 0;
+      for (;;) {
+        if (!done && rp < 0) {
+          while (m == 0 && ++wi < nwl) m = masks[lane * nwords + wi];
+          if (m == 0) {
+            done = true;
+          } else {
+            rst = (int32_t)(s - R0) + 64 * wi + __builtin_ctzll(m);
+            m &= m - 1;
+            rp = rst;
+            rex = -1;
+            steps = 0;
+          }
+        }
+        if (__all(done)) break;
+        dbg_iters++;
+        if (!done) {
+          const uint64_t x = rgn_u64(rgn, (uint32_t)rp);
+          const int32_t b0 = (int32_t)(x & 0xff), b1 = (int32_t)((x >> 8) & 0xff);
+          const int32_t klen = b0 ? b0 - 1 : b1;
+          const int32_t vlen = b0 ? b1 : 0;
+          const bool ok = (x & 0x8080ull) == 0 && (b0 || !P.no_deletes) && klen <= mk && vlen <= mv &&
+                          rp + 2 + klen <= lim;
+          if (!ok) {
+            rp = -1;
+          } else {
+            if (rex < 0) steps++;
+            rp += 2 + klen + vlen;
+            if (rex < 0 && rp >= re) rex = rp;
+            if (rp >= rstop) {  // survived the look-ahead: a candidate entry
+              const unsigned long long pe = (unsigned long long)(R0 + rex);
+              nsurv++;
+              min_exit = min(min_exit, pe);
+              max_exit = max(max_exit, (long long)pe);
+              if ((unsigned long long)(R0 + rst) < c_min) { c_min = (unsigned long long)(R0 + rst); c_min_steps = steps; }
+              rp = -1;
+            }
+          }
+        }
+      }
+    } else {
+      int64_t p = -1, cst = 0, pex = -1;
+      for (;;) {
+        if (!done && p < 0) {
+          while (m == 0 && ++wi < nwl) m = masks[lane * nwords + wi];
+          if (m == 0) {
+            done = true;
+          } else {
+            cst = s + 64ll * wi + __builtin_ctzll(m);
+            m &= m - 1;
+            p = cst;
+            pex = -1;
+            steps = 0;
+          }
+        }
+        if (__all(done)) break;
+        if (!done) {
+          const RecHdr h = decode_rgn(rgn, R0, p, log_len);
+          if (!header_plausible(h, p, P.max_key_len, P.max_value_len, log_len) || (!h.put && P.no_deletes)) {
+            p = -1;
+          } else {
+            if (pex < 0) steps++;
+            p = record_end(h, p);
+            if (pex < 0 && p >= e) pex = p;
+            if (p >= stop) {
+              nsurv++;
+              min_exit = min(min_exit, (unsigned long long)pex);
+              max_exit = max(max_exit, (long long)pex);
+              if ((unsigned long long)cst < c_min) { c_min = (unsigned long long)cst; c_min_steps = steps; }
+              p = -1;
+            }
+          }
+        }
+      }
+    }
+  }
+  const bool converged = act && !passthrough && nsurv > 0 && (long long)min_exit == max_exit;
+  mark(2);
+  if (P.dbg) {
+    const unsigned long long sv = wave_sum_u64(nsurv);
+    const unsigned long long nc = wave_sum_u64(converged ? 0ull : (act ? 1ull : 0ull));
+    if (lane == 0) { P.dbg[wv * 16 + 9] = sv; P.dbg[wv * 16 + 10] = nc; P.dbg[wv * 16 + 8] = dbg_iters; }
+  }
+
+  // ---- 3 entries ----
+  int64_t my_exit = converged ? (int64_t)min_exit : -1;
+  if (lane == nw - 1 && converged) granule_store(&P.exit_desc[wv], (unsigned long long)my_exit | kReady);
+  unsigned long long extv = (unsigned long long)kLogHeaderSize;
+  if (k0 > 0 && lane == 0) {
+    const unsigned long long t0 = wall_clock64();
+    for (;;) {
+      const unsigned long long v = granule_load(&P.exit_desc[wv - 1]);
+      if (v & kReady) { extv = v & ~kReady; break; }
+      if (wall_clock64() - t0 > kSpinTicks) {  // should a predecessor never run: serial path
+        atomicOr(&P.st->spec_fail, 2u);
+        extv = (unsigned long long)s;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  const int64_t ext = (int64_t)__shfl(extv, 0, 64);
+  mark(3);
+  // chunks whose exit depends on their entry, in order (a serial walk each, rare)
+  int32_t cnt = 0;
+  bool bad = false;
+  auto at_glb = [&](int64_t a) -> uint32_t { return (uint32_t)P.log[a]; };
+  auto hdr_at = [&](int64_t p) -> RecHdr {
+    return p + 16 <= R0 + RLEN ? decode_rgn(rgn, R0, p, log_len) : decode_header(at_glb, p, log_len);
+  };
+  unsigned long long pending = __ballot(act && !converged);
+  while (pending) {
+    const int j = __builtin_ctzll(pending);
+    pending &= pending - 1;
+    const int64_t prev_exit = __shfl(my_exit, j > 0 ? j - 1 : 0, 64);
+    if (lane == j) {
+      int64_t p = j == 0 ? ext : prev_exit;
+      while (p < e) {
+        const RecHdr h = hdr_at(p);
+        if (!header_valid(h, p, P.max_key_len, log_len)) {
+          set_error(P.st, p, h.rc ? h.rc : kErrCorruptLog);
+          bad = true;
+          break;
+        }
+        cnt++;
+        p = record_end(h, p);
+      }
+      my_exit = max(p, e);
+    }
+  }
+  if (lane == nw - 1 && !converged) granule_store(&P.exit_desc[wv], (unsigned long long)my_exit | kReady);
+  const int64_t up = __shfl_up(my_exit, 1, 64);
+  const int64_t entry = lane == 0 ? ext : up;
+
+  // ---- 4 counts ----
+  const bool need_walk = converged && !(nsurv == 1 && (unsigned long long)entry == c_min);
+  if (converged && !need_walk) cnt = c_min_steps;
+  if (__any(need_walk)) {  // several survivors, or an entry the screen pruned: verified walk
+    int64_t p = need_walk ? entry : e;
+    for (;;) {
+      const bool go = need_walk && !bad && p < e;
+      if (!__any(go)) break;
+      if (go) {
+        const RecHdr h = hdr_at(p);
+        if (!header_valid(h, p, P.max_key_len, log_len)) {
+          set_error(P.st, p, h.rc ? h.rc : kErrCorruptLog);
+          bad = true;
+        } else {
+          cnt++;
+          p = record_end(h, p);
+        }
+      }
+    }
+    if (need_walk && !bad && p != (int64_t)min_exit) atomicOr(&P.st->spec_fail, 1u);
+  }
+  if (!act || bad) cnt = 0;
+  // wave-exclusive scan of the counts
+  unsigned long long incl = (unsigned long long)cnt;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned long long t = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += t;
+  }
+  const unsigned long long total = __shfl(incl, 63, 64);
+  const unsigned long long local_off = incl - (unsigned long long)cnt;
+  mark(4);
+  unsigned long long base = 0;
+  if (wv == 0) {
+    if (lane == 0) granule_store(&P.cnt_desc[0], kIncl | total);
+  } else {
+    if (lane == 0) granule_store(&P.cnt_desc[wv], kAgg | total);
+    int64_t jw = (int64_t)wv - 1;
+    unsigned long long acc = 0;
+    const unsigned long long t0 = wall_clock64();
+    for (;;) {
+      const int64_t idx = jw - lane;
+      const unsigned long long v = idx >= 0 ? granule_load(&P.cnt_desc[idx]) : kIncl;
+      const unsigned long long st = v & kStateMask;
+      const unsigned long long inc = __ballot(st == kIncl);
+      const unsigned long long none = __ballot(st == 0);
+      const int fi = inc ? __builtin_ctzll(inc) : 64;
+      const unsigned long long before = fi == 64 ? ~0ull : ((1ull << fi) - 1ull);
+      if (none & before) {
+        if (wall_clock64() - t0 > kSpinTicks) {
+          if (lane == 0) atomicOr(&P.st->spec_fail, 2u);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+        continue;
+      }
+      acc += wave_sum_u64(lane <= fi ? (v & ~kStateMask) : 0ull);
+      if (fi < 64) break;
+      jw -= 64;
+    }
+    base = acc;
+    if (lane == 0) granule_store(&P.cnt_desc[wv], kIncl | (base + total));
+  }
+  if (wv == gridDim.x - 1 && lane == 0) P.st->n_records = base + total;
+  mark(5);
+  if (base + total > P.max_records) {
+    if (lane == 0) atomicOr(&P.st->overflow, 1u);
+    return;
+  }
+
+  // ---- 5 hash every record of the chunk, entries in log order ----
+  unsigned long long ndel = 0;
+  {
+    int64_t p = (act && cnt > 0) ? entry : e;
+    uint64_t dst = base + local_off;
+    for (;;) {
+      const bool go = p < e;
+      if (!__any(go)) break;
+      if (go) {
+        const RecHdr h = hdr_at(p);
+        const int64_t kp = p + h.hlen;
+        uint64_t hash;
+        if (kp + h.klen + 16 <= R0 + RLEN) {  // key in the region
+          const RgnKey ld{rgn, (uint32_t)(kp - R0)};
+          hash = P.hash_size == 8 ? murmur64_ld(ld, h.klen, (uint32_t)P.seed)
+                                  : (uint64_t)murmur32_ld(ld, h.klen, (uint32_t)P.seed);
+        } else if (kp + h.klen + 16 <= log_len) {  // key runs past the region: unaligned global reads
+          const GlobalKey ld{P.log + kp};
+          hash = P.hash_size == 8 ? murmur64_ld(ld, h.klen, (uint32_t)P.seed)
+                                  : (uint64_t)murmur32_ld(ld, h.klen, (uint32_t)P.seed);
+        } else {
+          hash = key_hash(P.hash_size, P.log + kp, h.klen, (uint32_t)P.seed);
+        }
+        uint64_t addr = (uint64_t)p << P.ebb;
+        if (!h.put) {
+          addr |= kDelBit;
+          ndel++;
+        }
+        Entry en;
+        en.hash = hash;
+        en.addr = addr;
+        P.ent[dst++] = en;
+        p = record_end(h, p);
+      }
+    }
+  }
+  ndel = wave_sum_u64(ndel);
+  if (ndel && lane == 0) atomicAdd(&P.st->n_deletes, ndel);
+  mark(6);
+}
+
+// ================================================================================================
+// Radix partition of the entries by bucket (bucket = wantedSlot >> kBucketShift).
+// Pass 1: digit d1 = bucket >> P.p2_bits (< 256) over tiles of kPartTile entries.
+// ================================================================================================
+__device__ __forceinline__ uint32_t bucket_of(const BuildParams& P, uint64_t hash) {
+  return (uint32_t)(fast_mod(hash, P.mod) >> kBucketShift);
+}
+
+__global__ __launch_bounds__(kPartBlock) void k_part1_hist(BuildParams P) {
+  __shared__ uint32_t hist[256];
+  const uint64_t N = min((uint64_t)P.st->n_records, P.max_records);
+  const uint64_t t0 = (uint64_t)blockIdx.x * kPartTile;
+  hist[threadIdx.x] = 0;
+  __syncthreads();
+  for (int i = 0; i < kPartItems; i++) {
+    const uint64_t idx = t0 + (uint64_t)i * kPartBlock + threadIdx.x;
+    if (idx < N) atomicAdd(&hist[bucket_of(P, P.ent[idx].hash) >> P.p2_bits], 1u);
+  }
+  __syncthreads();
+  P.p1_hist[(uint64_t)threadIdx.x * P.p1_tiles + blockIdx.x] = hist[threadIdx.x];  // digit-major
+}
+
+__global__ __launch_bounds__(kPartBlock) void k_part1_scatter(BuildParams P) {
+  __shared__ Entry stage[kPartTile];
+  __shared__ uint32_t hist[256];
+  __shared__ uint32_t lbase[256];
+  __shared__ uint32_t cursor[256];
+  __shared__ uint64_t sh64[kPartBlock];
+  const uint64_t N = min((uint64_t)P.st->n_records, P.max_records);
+  const uint64_t t0 = (uint64_t)blockIdx.x * kPartTile;
+  const int tid = threadIdx.x;
+  hist[tid] = 0;
+  cursor[tid] = 0;
+  __syncthreads();
+  Entry v[kPartItems];
+  uint32_t d[kPartItems];
+#pragma unroll
+  for (int i = 0; i < kPartItems; i++) {
+    const uint64_t idx = t0 + (uint64_t)i * kPartBlock + tid;
+    d[i] = 0xffffffffu;
+    if (idx < N) {
+      v[i] = P.ent[idx];
+      d[i] = bucket_of(P, v[i].hash) >> P.p2_bits;
+      atomicAdd(&hist[d[i]], 1u);
+    }
+  }
+  __syncthreads();
+  uint64_t total;
+  const uint64_t ex = block_exclusive_scan<uint64_t, OpAdd, kPartBlock>(hist[tid], sh64, OpAdd(), &total);
+  lbase[tid] = (uint32_t)ex;
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < kPartItems; i++) {
+    if (d[i] != 0xffffffffu) stage[lbase[d[i]] + atomicAdd(&cursor[d[i]], 1u)] = v[i];
+  }
+  __syncthreads();
+  // coalesced write-out: LDS position i -> global offset of its digit run
+  for (uint32_t i = tid; i < (uint32_t)total; i += kPartBlock) {
+    const Entry en = stage[i];
+    const uint32_t dd = bucket_of(P, en.hash) >> P.p2_bits;
+    const uint64_t dst = P.p1_off[(uint64_t)dd * P.p1_tiles + blockIdx.x] + (i - lbase[dd]);
+    P.ent3[dst] = en;
+  }
+}
+
+// Pass 2: one workgroup per coarse partition splits it into its 2^p2_bits buckets.
+__global__ __launch_bounds__(kPartBlock) void k_part2(BuildParams P) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t dyn[];  // hist[nbins] ++ cur[nbins]
+  __shared__ uint64_t sh64[kPartBlock];
+  const uint32_t dpart = blockIdx.x;
+  const uint64_t lo = P.p1_off[(uint64_t)dpart * P.p1_tiles];
+  const uint64_t hi = (dpart + 1 < 256) ? P.p1_off[(uint64_t)(dpart + 1) * P.p1_tiles] : P.p1_off_total[0];
+  const uint32_t nbins = 1u << P.p2_bits;
+  uint32_t* hist = dyn;
+  uint32_t* cur = dyn + nbins;
+  const int tid = threadIdx.x;
+  for (uint32_t b = tid; b < nbins; b += kPartBlock) { hist[b] = 0; cur[b] = 0; }
+  __syncthreads();
+  const uint32_t mask = nbins - 1;
+  for (uint64_t i = lo + tid; i < hi; i += kPartBlock) atomicAdd(&hist[bucket_of(P, P.ent3[i].hash) & mask], 1u);
+  __syncthreads();
+  // exclusive scan of the bins (nbins / kPartBlock consecutive bins per thread)
+  const uint32_t per = (nbins + kPartBlock - 1) / kPartBlock;
+  uint64_t local = 0;
+  for (uint32_t q = 0; q < per; q++) {
+    const uint32_t b = tid * per + q;
+    if (b < nbins) local += hist[b];
+  }
+  const uint64_t ex = block_exclusive_scan<uint64_t, OpAdd, kPartBlock>(local, sh64, OpAdd(), nullptr);
+  uint64_t run = ex;
+  for (uint32_t q = 0; q < per; q++) {
+    const uint32_t b = tid * per + q;
+    if (b < nbins) {
+      const uint64_t bucket = ((uint64_t)dpart << P.p2_bits) | b;
+      if (bucket < P.nbuckets) {
+        P.boff[bucket] = lo + run;
+        P.bcount[bucket] = hist[b];
+      }
+      cur[b] = (uint32_t)run;
+      run += hist[b];
+    }
+  }
+  __syncthreads();
+  for (uint64_t i = lo + tid; i < hi; i += kPartBlock) {
+    const Entry en = P.ent3[i];
+    const uint32_t b = bucket_of(P, en.hash) & mask;
+    P.ent2[lo + atomicAdd(&cur[b], 1u)] = en;
+  }
+}
+
+// ================================================================================================
+// k_place_lds: one bucket per workgroup, entries staged in LDS (buckets above kPlaceLdsMax
+// entries are left to the global-memory k_place, flagged in P.st->big_buckets).
+// ================================================================================================
+__global__ __launch_bounds__(kPlaceBlock) void k_place_lds(BuildParams P) {
+  __shared__ uint32_t cnt[kBucket];
+  __shared__ uint32_t base[kBucket];
+  __shared__ int32_t M[kBucket];
+  __shared__ int32_t aux[kBucket];  // cursors, then slot -> sorted index
+  __shared__ Entry raw[kPlaceLdsMax];
+  __shared__ uint16_t order[kPlaceLdsMax];
+  __shared__ uint64_t sh64[kPlaceBlock];
+  __shared__ int64_t shm[kPlaceBlock];
+  const uint64_t b = blockIdx.x;
+  const uint64_t start = b << kBucketShift;
+  const int64_t bsize = (int64_t)min((uint64_t)kBucket, P.cap - start);
+  const uint32_t n = P.bcount[b];
+  const uint64_t eoff = P.boff[b];
+  const int tid = threadIdx.x;
+  if (n > kPlaceLdsMax) {
+    if (tid == 0) atomicOr(&P.st->big_buckets, 1u);
+    return;
+  }
+  for (int t = tid; t < kBucket; t += kPlaceBlock) { cnt[t] = 0; aux[t] = 0; }
+  __syncthreads();
+  for (uint32_t i = tid; i < n; i += kPlaceBlock) {
+    const Entry en = P.ent2[eoff + i];
+    raw[i] = en;
+    atomicAdd(&cnt[fast_mod(en.hash, P.mod) - start], 1u);
+  }
+  __syncthreads();
+  bucket_scan(cnt, base, M, sh64, shm, nullptr);
+  for (uint32_t i = tid; i < n; i += kPlaceBlock) {
+    const uint32_t w = (uint32_t)(fast_mod(raw[i].hash, P.mod) - start);
+    order[base[w] + atomicAdd((uint32_t*)&aux[w], 1u)] = (uint16_t)i;
+  }
+  __syncthreads();
+  // equal wanted slots: address order; equal hashes -> duplicate-key candidates
+  for (int q = 0; q < kBinsPerThread; q++) {
+    const int s = tid * kBinsPerThread + q;
+    const uint32_t g = cnt[s];
+    if (g < 2) continue;
+    uint16_t* grp = order + base[s];
+    if (g > kGroupMax) {
+      atomicOr(&P.st->dup_overflow, 1u);
+      continue;
+    }
+    for (uint32_t x = 1; x < g; x++) {
+      const uint16_t vi = grp[x];
+      const uint64_t va = raw[vi].addr & ~kDelBit;
+      uint32_t y = x;
+      while (y > 0 && va < (raw[grp[y - 1]].addr & ~kDelBit)) { grp[y] = grp[y - 1]; y--; }
+      grp[y] = vi;
+    }
+    for (uint32_t x = 0; x < g; x++)
+      for (uint32_t y = x + 1; y < g; y++) {
+        const Entry ex = raw[grp[x]], ey = raw[grp[y]];
+        if (ex.hash == ey.hash && !(ex.addr & kDelBit) && !(ey.addr & kDelBit)) {
+          const unsigned long long slotn = atomicAdd(&P.st->n_pairs, 1ull);
+          if (slotn < P.pair_cap) {
+            P.pairs[2 * slotn] = ex.addr;
+            P.pairs[2 * slotn + 1] = ey.addr;
+          }
+        }
+      }
+  }
+  __syncthreads();
+  if (P.st->full) return;
+  const int64_t x = P.carry[b];
+  for (int t = tid; t < kBucket; t += kPlaceBlock) aux[t] = -1;
+  __syncthreads();
+  for (int q = 0; q < kBinsPerThread; q++) {
+    const int s = tid * kBinsPerThread + q;
+    const uint32_t g = cnt[s];
+    if (!g) continue;
+    const int64_t shift = max(x, (int64_t)M[s]);
+    for (uint32_t r = 0; r < g; r++) {
+      const int64_t j = (int64_t)base[s] + r;
+      const int64_t p = j + shift;
+      if (p < bsize) {
+        aux[p] = (int32_t)j;
+      } else {
+        const Entry en = raw[order[j]];
+        write_slot(P, wrap_slot(start + (uint64_t)p, P.cap), en.hash, en.addr & ~kDelBit);
+      }
+    }
+  }
+  __syncthreads();
+  for (int64_t t = x + tid; t < bsize; t += kPlaceBlock) {
+    const int32_t j = aux[t];
+    if (j >= 0) {
+      const Entry en = raw[order[j]];
+      write_slot(P, start + (uint64_t)t, en.hash, en.addr & ~kDelBit);
+    } else {
+      write_slot(P, start + (uint64_t)t, 0, 0);
+    }
+  }
+}
+
+// ================================================================================================
+// launchers
+// ================================================================================================
+void launch_frame_fused(const BuildParams& P, hipStream_t s, StageTimer* tm) {
+  if (P.fr_nchunks == 0) return;
+  const uint64_t nwaves = (P.fr_nchunks + P.fr_w - 1) / P.fr_w;
+  const size_t lds = (size_t)P.fr_rgn_bytes + (size_t)P.fr_w * P.fr_mask_words * 8;
+  hipLaunchKernelGGL(k_frame, dim3((unsigned)nwaves), dim3(64), lds, s, P);
+  tm->mark("frame", s);
+}
+
+void launch_partition(const BuildParams& P, hipStream_t s, StageTimer* tm) {
+  hipLaunchKernelGGL(k_part1_hist, dim3((unsigned)P.p1_tiles), dim3(kPartBlock), 0, s, P);
+  scan_exclusive<uint32_t, uint64_t, OpAdd>(P.p1_hist, P.p1_off, (uint64_t)P.p1_tiles * 256, P.p1_off_total,
+                                            OpAdd(), P.scan_scratch_u64, s);
+  hipLaunchKernelGGL(k_part1_scatter, dim3((unsigned)P.p1_tiles), dim3(kPartBlock), 0, s, P);
+  hipLaunchKernelGGL(k_part2, dim3(256), dim3(kPartBlock), (size_t)(2u << P.p2_bits) * sizeof(uint32_t), s, P);
+  tm->mark("partition", s);
+}
+
+void launch_place_fast(const BuildParams& P, hipStream_t s, StageTimer* tm) {
+  launch_summary_carry(P, s, tm);
+  hipLaunchKernelGGL(k_place_lds, dim3((unsigned)P.nbuckets), dim3(kPlaceBlock), 0, s, P);
+  launch_place_global(P, s, 0, 1);  // buckets above kPlaceLdsMax entries (normally none)
+  tm->mark("place", s);
+  launch_verify(P, s, tm);
+}
+
+}  // namespace sk

@@ -1,0 +1,106 @@
+// kernel_utils.hpp -- device helpers shared by the build kernels (chunk geometry, LDS staging,
+// wave reductions, slot encoding).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "build_kernels.hpp"
+#include "device_common.hpp"
+
+namespace sk {
+
+// ------------------------------------------------------------------------------------------------
+// small device utilities
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ void set_error(Status* st, int64_t pos, int code) {
+  atomicMin(&st->err, ((unsigned long long)pos << 8) | (unsigned long long)(-code));
+}
+
+__device__ __forceinline__ int64_t chunk_start(uint64_t k) { return k == 0 ? kLogHeaderSize : (int64_t)(k << kChunkShift); }
+__device__ __forceinline__ int64_t chunk_end(uint64_t k, int64_t data_end) {
+  const int64_t e = (int64_t)((k + 1) << kChunkShift);
+  return e < data_end ? e : data_end;
+}
+
+// Stage log bytes [wb, wb + n) into LDS (bytes past log_len read as 0; they are never decoded
+// because every decode is bounded by log_len).  wb is 16-byte aligned; `log` must be too.
+__device__ __forceinline__ void stage_window(uint8_t* win, const uint8_t* log, int64_t wb, int n, int64_t log_len,
+                                             int lane, int nthreads) {
+  const int nvec = n >> 4;
+  for (int v = lane; v < nvec; v += nthreads) {
+    const int64_t a = wb + ((int64_t)v << 4);
+    uint4 val;
+    if (a + 16 <= log_len) {
+      val = *reinterpret_cast<const uint4*>(log + a);
+    } else {
+      uint8_t tmp[16];
+#pragma unroll
+      for (int i = 0; i < 16; i++) tmp[i] = (a + i < log_len) ? log[a + i] : 0;
+      val = *reinterpret_cast<uint4*>(tmp);
+    }
+    *reinterpret_cast<uint4*>(win + (v << 4)) = val;
+  }
+}
+
+__device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned long long t = __shfl_xor(v, o, 64);
+    v = t < v ? t : v;
+  }
+  return v;
+}
+__device__ __forceinline__ long long wave_max_i64(long long v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const long long t = __shfl_xor(v, o, 64);
+    v = t > v ? t : v;
+  }
+  return v;
+}
+__device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ void write_slot(const BuildParams& P, uint64_t slot, uint64_t hash, uint64_t addr) {
+  uint8_t* p = P.out + kIndexHeaderSize + slot * (uint64_t)P.slot_size;
+  if (P.slot_size == 16) {
+    *reinterpret_cast<uint4*>(p) = make_uint4((uint32_t)hash, (uint32_t)(hash >> 32), (uint32_t)addr, (uint32_t)(addr >> 32));
+  } else if (P.slot_size == 8) {
+    *reinterpret_cast<uint2*>(p) = make_uint2((uint32_t)hash, (uint32_t)addr);
+  } else if (P.hash_size == 8) {  // 8 + 4
+    uint32_t* q = reinterpret_cast<uint32_t*>(p);
+    q[0] = (uint32_t)hash; q[1] = (uint32_t)(hash >> 32); q[2] = (uint32_t)addr;
+  } else {  // 4 + 8
+    uint32_t* q = reinterpret_cast<uint32_t*>(p);
+    q[0] = (uint32_t)hash; q[1] = (uint32_t)addr; q[2] = (uint32_t)(addr >> 32);
+  }
+}
+
+__device__ __forceinline__ uint64_t wrap_slot(uint64_t s, uint64_t cap) {
+  while (s >= cap) s -= cap;
+  return s;
+}
+
+__device__ __forceinline__ void read_slot(const BuildParams& P, uint64_t slot, uint64_t& hash, uint64_t& addr) {
+  const uint8_t* p = P.out + kIndexHeaderSize + slot * (uint64_t)P.slot_size;
+  if (P.slot_size == 16) {
+    const uint4 v = *reinterpret_cast<const uint4*>(p);
+    hash = (uint64_t)v.x | ((uint64_t)v.y << 32);
+    addr = (uint64_t)v.z | ((uint64_t)v.w << 32);
+  } else if (P.slot_size == 8) {
+    const uint2 v = *reinterpret_cast<const uint2*>(p);
+    hash = v.x;
+    addr = v.y;
+  } else {
+    const uint32_t* q = reinterpret_cast<const uint32_t*>(p);
+    if (P.hash_size == 8) { hash = (uint64_t)q[0] | ((uint64_t)q[1] << 32); addr = q[2]; }
+    else { hash = q[0]; addr = (uint64_t)q[1] | ((uint64_t)q[2] << 32); }
+  }
+}
+
+
+}  // namespace sk

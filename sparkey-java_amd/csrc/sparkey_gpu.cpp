@@ -9,6 +9,7 @@
 #include <fcntl.h>
 #include <hip/hip_runtime.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 #include <sys/stat.h>
 #include <unistd.h>
@@ -219,6 +220,7 @@ struct sparkey_plan {
   uint64_t c_ent = 0, c_ent2 = 0, c_ent3 = 0;
   uint64_t c_bcount = 0, c_bcursor = 0, c_boff = 0, c_bfun = 0, c_bpre = 0, c_carry = 0;
   uint64_t c_pairs = 0, c_parts = 0, c_su = 0, c_smp = 0, c_bft = 0;
+  uint64_t c_desc = 0, c_p1h = 0, c_p1o = 0, c_dbg = 0;
   uint8_t* conv = nullptr;
   int64_t* exitp = nullptr;
   int64_t* qpos = nullptr;
@@ -240,8 +242,12 @@ struct sparkey_plan {
   StatPart* parts = nullptr;
   uint64_t* scan_u64 = nullptr;
   MaxPlus* scan_mp = nullptr;
+  unsigned long long* desc = nullptr;  // exit granules ++ count granules ++ ticket (memset per build)
+  uint32_t* p1_hist = nullptr;
+  uint64_t* p1_off = nullptr;
   Status* d_status = nullptr;
   Status* h_status = nullptr;
+  unsigned long long* dbg = nullptr;  // SPARKEY_FRAME_DEBUG=1: k_frame phase counters
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   StageTimer timer;
   std::vector<std::string> stage_names;
@@ -270,7 +276,11 @@ static int plan_reserve(sparkey_plan* pl, uint64_t nchunks, uint64_t nrec, uint6
   const uint64_t pair_cap = std::max<uint64_t>(1 << 16, std::min<uint64_t>(nrec, 1 << 22));
   HIP_TRY(grow(&pl->pairs, pl->c_pairs, 2 * pair_cap));
   HIP_TRY(grow(&pl->parts, pl->c_parts, (cap + kStatSlotsPerBlock - 1) / kStatSlotsPerBlock));
-  const uint64_t scratch = std::max(nchunks, nbuckets) / kScanTile + 64;
+  HIP_TRY(grow(&pl->desc, pl->c_desc, 2 * nchunks + 2));
+  const uint64_t p1_tiles = std::max<uint64_t>(1, (nrec + kPartTile - 1) / kPartTile);
+  HIP_TRY(grow(&pl->p1_hist, pl->c_p1h, 256 * p1_tiles));
+  HIP_TRY(grow(&pl->p1_off, pl->c_p1o, 256 * p1_tiles + 1));
+  const uint64_t scratch = std::max(std::max(nchunks, nbuckets), 256 * p1_tiles) / kScanTile + 64;
   HIP_TRY(grow(&pl->scan_u64, pl->c_su, scratch + 16));
   HIP_TRY(grow(&pl->scan_mp, pl->c_smp, scratch + 16));
   return SPARKEY_OK;
@@ -341,7 +351,24 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
     P.max_rec_len = std::max<int64_t>(1, std::max(put_len, del_len));
   }
   P.nchunks = lh.data_end > kLogHeaderSize ? (uint64_t)((lh.data_end + kChunk - 1) / kChunk) : 0;
-  P.emit_extra = lh.max_key_len + 16 <= 1024 ? (int32_t)((lh.max_key_len + 16 + 15) & ~15LL) : 16;
+  // k_frame geometry: chunk C = max(128, nextpow2(maxRecLen)) so every chunk but a short last one
+  // holds a record start; 8 KiB of chunks per wave, staged contiguously with max(C, 256) bytes of
+  // look-ahead (about 10 KiB of LDS: 16 waves per CU); records longer than 4 KiB -> serial framing.
+  const bool fused_framing = P.max_rec_len <= 4096;
+  {
+    int cs = 7;
+    while ((1ll << cs) < P.max_rec_len) cs++;
+    const int64_t C = 1ll << cs;
+    P.fr_cshift = cs;
+    P.fr_w = (int32_t)std::max<int64_t>(1, std::min<int64_t>(64, 8192 / C));
+    P.fr_look = (int32_t)std::max<int64_t>(C, 256);
+    P.fr_rgn_bytes = (int32_t)(((int64_t)P.fr_w * C + P.fr_look + 16 + 255) & ~255LL);
+    P.fr_mask_words = (int32_t)((std::min<int64_t>(C, P.max_rec_len) + 63) / 64);
+    P.fr_fast = lh.max_key_len + 1 < 128 && lh.max_value_len < 128;
+    P.no_deletes = lh.num_deletes == 0;
+    P.fr_nchunks = lh.data_end > kLogHeaderSize ? (uint64_t)((lh.data_end + C - 1) / C) : 0;
+  }
+  P.emit_extra = lh.max_key_len + 32 <= kEmitExtra ? (int32_t)((lh.max_key_len + 32 + 15) & ~15LL) : 32;
   P.hash_size = ip.hash_size;
   P.addr_size = ip.addr_size;
   P.slot_size = ip.slot_size;
@@ -350,6 +377,15 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
   P.mod = make_fastmod(ip.cap);
   P.cap = ip.cap;
   P.nbuckets = (ip.cap + kBucket - 1) / kBucket;
+  {
+    int nb_bits = 0;
+    while ((1ull << nb_bits) < P.nbuckets) nb_bits++;
+    P.p2_bits = std::max(0, nb_bits - 8);
+    if (P.p2_bits > kPart2MaxBits) {
+      set_err(err, err_len, "hash capacity too large for one device: " + std::to_string(ip.cap));
+      return SPARKEY_E_UNSUPPORTED;
+    }
+  }
   P.out = d_out;
   P.st = pl->d_status;
 
@@ -357,7 +393,7 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
   uint8_t hdr[kIndexHeaderSize];
   index_header_template(lh, ip, opts->hash_seed, hdr);
 
-  int framing_path = 0, placement_path = 0;
+  int framing_path = fused_framing ? 0 : 1, placement_path = 0;
   float ms = 0.f;
   Status& st = *pl->h_status;
   for (int attempt = 0; attempt < 3; attempt++) {
@@ -369,6 +405,15 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
     P.bcount = pl->bcount; P.bcursor = pl->bcursor; P.boff = pl->boff; P.bfun = pl->bfun; P.bpre = pl->bpre;
     P.bfun_total = pl->bfun_total; P.carry = pl->carry; P.pairs = pl->pairs; P.pair_cap = pl->c_pairs / 2;
     P.parts = pl->parts; P.scan_scratch_u64 = pl->scan_u64; P.scan_scratch_mp = pl->scan_mp;
+    const uint64_t nwaves = P.fr_nchunks ? (P.fr_nchunks + P.fr_w - 1) / P.fr_w : 0;
+    P.exit_desc = pl->desc; P.cnt_desc = pl->desc + nwaves;
+    P.p1_tiles = (uint32_t)std::max<uint64_t>(1, (std::max<uint64_t>(nrec, 1) + kPartTile - 1) / kPartTile);
+    P.p1_hist = pl->p1_hist; P.p1_off = pl->p1_off; P.p1_off_total = pl->p1_off + 256ull * P.p1_tiles;
+    if (getenv("SPARKEY_FRAME_DEBUG")) {
+      HIP_TRY(grow(&pl->dbg, pl->c_dbg, 16 * std::max<uint64_t>(P.nchunks, 1)));
+      HIP_TRY(hipMemsetAsync(pl->dbg, 0, 16 * P.nchunks * sizeof(unsigned long long), s));
+      P.dbg = pl->dbg;
+    }
 
     Status init;
     memset(&init, 0, sizeof(init));
@@ -377,18 +422,40 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
     pl->timer.begin(s);
     HIP_TRY(hipMemcpyAsync(d_out, hdr, kIndexHeaderSize, hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemcpyAsync(pl->d_status, &init, sizeof(Status), hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemsetAsync(pl->bcount, 0, P.nbuckets * sizeof(uint32_t), s));
-    HIP_TRY(hipMemsetAsync(pl->bcursor, 0, P.nbuckets * sizeof(uint32_t), s));
-    if (framing_path == 0) launch_framing(P, s, &pl->timer);
-    else launch_framing_serial(P, s);
-    launch_emit(P, s, &pl->timer);
-    launch_place(P, s, &pl->timer);
+    if (framing_path == 0) {
+      HIP_TRY(hipMemsetAsync(pl->desc, 0, (2 * nwaves + 2) * sizeof(unsigned long long), s));
+      launch_frame_fused(P, s, &pl->timer);
+    } else {
+      launch_framing_serial(P, s);
+      launch_emit(P, s, &pl->timer);
+    }
+    launch_partition(P, s, &pl->timer);
+    launch_place_fast(P, s, &pl->timer);
     launch_stats(P, s, 0, &pl->timer);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(pl->ev1, s));
     HIP_TRY(hipMemcpyAsync(pl->h_status, pl->d_status, sizeof(Status), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     HIP_TRY(hipEventElapsedTime(&ms, pl->ev0, pl->ev1));
+    if (P.dbg && P.fr_nchunks) {
+      const uint64_t nwv = (P.fr_nchunks + P.fr_w - 1) / P.fr_w;
+      std::vector<unsigned long long> h(16 * nwv);
+      if (hipMemcpy(h.data(), pl->dbg, h.size() * 8, hipMemcpyDeviceToHost) == hipSuccess) {
+        double sum[16] = {0};
+        unsigned long long mx[16] = {0};
+        for (uint64_t c = 0; c < nwv; c++)
+          for (int i = 0; i < 16; i++) {
+            sum[i] += (double)h[c * 16 + i];
+            mx[i] = std::max(mx[i], h[c * 16 + i]);
+          }
+        const double n = (double)nwv;
+        fprintf(stderr, "[k_frame] waves=%llu C=%d W=%d mean cycles: stage %.0f screen %.0f walk %.0f entry %.0f "
+                "counts %.0f lookback %.0f hash %.0f | max entry %llu max lookback %llu | walk iters %.1f survivors/wave "
+                "%.1f unconverged/wave %.2f\n",
+                (unsigned long long)nwv, 1 << P.fr_cshift, P.fr_w, sum[0] / n, sum[1] / n, sum[2] / n, sum[3] / n,
+                sum[4] / n, sum[5] / n, sum[6] / n, mx[3], mx[5], sum[8] / n, sum[9] / n, sum[10] / n);
+      }
+    }
     if (st.overflow || st.n_records > P.max_records) {  // header under-counts records: grow and redo
       nrec = std::max<uint64_t>(st.n_records, nrec * 2 + 1);
       continue;
@@ -410,6 +477,7 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
     placement_path = 1;
     float ms2 = 0.f;
     HIP_TRY(hipEventRecord(pl->ev0, s));
+    if (!ip.in_memory) launch_place_global(P, s, 1, 0);  // (wantedSlot, address) order into ent3
     HIP_TRY(hipMemsetAsync(d_out + kIndexHeaderSize, 0, (size_t)(ip.index_size - kIndexHeaderSize), s));
     launch_sequential(P, s, ip.in_memory ? 0 : 1);
     launch_stats(P, s, 1, &pl->timer);
@@ -508,7 +576,7 @@ void sparkey_plan_destroy(sparkey_plan* pl) {
   (void)hipSetDevice(pl->device);
   void* bufs[] = {pl->conv, pl->exitp, pl->qpos, pl->tail, pl->G, pl->cnt, pl->off, pl->ent, pl->ent2, pl->ent3,
                   pl->bcount, pl->bcursor, pl->boff, pl->bfun, pl->bpre, pl->bfun_total, pl->carry, pl->pairs,
-                  pl->parts, pl->scan_u64, pl->scan_mp, pl->d_status};
+                  pl->parts, pl->scan_u64, pl->scan_mp, pl->desc, pl->p1_hist, pl->p1_off, pl->d_status, pl->dbg};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (pl->h_status) (void)hipHostFree(pl->h_status);

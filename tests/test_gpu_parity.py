@@ -167,3 +167,45 @@ def test_errors(native):
     bad[64] = 1                                                    # SNAPPY: not on this path
     with pytest.raises(OSError):
         native.build_index_mem(bytes(bad), opts)
+
+
+# --- framing edge cases: the speculative framing must fall back to the exact serial walk ---
+def test_header_understates_max_value_len(native):
+    """The reference never checks valueLen against maxValueLen; speculation prunes with it, so a
+    log whose header understates it must still build identically (chunks whose true chain looks
+    implausible are walked serially with the reference iterator's rules)."""
+    import struct
+    log = bytearray(make_log([(b"k%d" % i, b"v" * (i % 300)) for i in range(5000)]))
+    struct.pack_into("<q", log, 48, 10)  # maxValueLen := 10
+    check(native, bytes(log), 3)
+
+
+def test_trailing_bytes_after_data_end(native):
+    log = make_log(key_value_puts(3000)) + b"\x05garbage" * 1000  # records start < dataEnd only
+    check(native, log, 8)
+
+
+@pytest.mark.parametrize("vlen", [4000, 4096, 9000, 70000])
+def test_records_spanning_chunks(native, vlen):
+    """Records as long as or longer than a framing chunk; past 4 KiB records the build frames the
+    log with the serial walker (few records per byte)."""
+    puts = [(b"key%d" % i, bytes([i % 251]) * (vlen + (i % 7))) for i in range(300)]
+    got, stats = check(native, make_log(puts), 12, hash_size=8)
+    assert stats.framing_path == (0 if vlen + 6 + 16 < 4096 else 1)
+
+
+def test_understated_max_key_len_is_an_error(native):
+    import struct
+    log = bytearray(make_log(key_value_puts(100)))
+    struct.pack_into("<q", log, 40, 3)  # maxKeyLen := 3 < real key lengths: the reference throws
+    with pytest.raises((OSError, RuntimeError)):
+        native.build_index_mem(bytes(log), native.make_opts(hash_seed=1))
+
+
+def test_header_hides_deletes(native):
+    """numDeletes = 0 in a header of a log that holds DELETE records: speculation prunes DELETE
+    starts, the verified chain disagrees, the exact path still gives the reference's bytes."""
+    import struct
+    log = bytearray(make_log(key_value_puts(3000), deletes=[b"Key%d" % i for i in range(0, 3000, 5)]))
+    struct.pack_into("<q", log, 24, 0)
+    check(native, bytes(log), 21)

@@ -7,4 +7,4 @@ export TMPDIR=/tmp
 mkdir -p gpurun_out
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 &&
 timeout -k 10 900 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1 &&
-timeout -k 10 600 python bench.py --steps 10 --warmup 2 > gpurun_out/bench.log 2>&1
+timeout -k 10 600 python bench.py --steps 10 --warmup 2 "$@" > gpurun_out/bench.log 2>&1
