@@ -106,7 +106,7 @@ __global__ __launch_bounds__(64) void k_emit(BuildParams P) {
   const int32_t n = s_n;
   if (n <= 0) return;
   const uint64_t base = P.off[k];
-  if (base + (uint64_t)n > P.max_records) {
+  if (base + (uint64_t)n > P.ent_cap) {
     if (lane == 0) atomicOr(&P.st->overflow, 1u);
     return;
   }
@@ -480,9 +480,16 @@ __global__ void k_sequential(BuildParams P, int sorted_order) {
   c.num_entries = 0;
   c.garbage = 0;
   const uint64_t N = min((uint64_t)P.st->n_records, P.max_records);
-  const Entry* src = sorted_order ? P.ent3 : P.ent;
+  uint64_t w = 0, j = 0;  // IN_MEMORY: log order = slab order
   for (uint64_t i = 0; i < N; i++) {
-    const Entry en = src[i];
+    Entry en;
+    if (sorted_order) {
+      en = P.ent3[i];
+    } else {
+      while (j >= P.wcount[w]) { w++; j = 0; }
+      en = P.ent[w * P.slab_cap + j];
+      j++;
+    }
     const uint64_t addr = en.addr & ~kDelBit;
     const int rc = (en.addr & kDelBit) ? seq_delete(c, en.hash, addr) : seq_put(c, en.hash, addr);
     if (rc) {

@@ -28,6 +28,7 @@ constexpr int kPartItems = 16;
 constexpr int kPartTile = kPartBlock * kPartItems;
 constexpr int kPart2MaxBits = 14;                 // fine digit of the partition (<= 16384 buckets)
 constexpr uint32_t kPlaceLdsMax = 1536;           // entries of a bucket staged in LDS
+constexpr uint32_t kMaxPartGroup = 64;            // slabs per partition tile
 
 // One log record as the placement sees it: 16 bytes, AoS so every access is one dwordx4.
 struct alignas(16) Entry {
@@ -64,6 +65,8 @@ struct Status {
   long long max_disp;
   long long collisions;
   long long total_disp;
+  unsigned int max_wave_count;  // largest per-wave record count when a slab overflowed
+  unsigned int pad2;
 };
 
 struct BuildParams {
@@ -96,10 +99,16 @@ struct BuildParams {
   uint32_t* cnt;
   uint64_t* off;
   // entries
-  Entry* ent;   // log order
-  Entry* ent2;  // grouped by bucket
-  Entry* ent3;  // sorted by (wanted, address) within bucket
-  uint64_t max_records;
+  Entry* ent;   // log order, in slabs: slab w holds wcount[w] entries at ent[w * slab_cap]
+  Entry* ent2;  // grouped by bucket (dense)
+  Entry* ent3;  // partition pass-1 output; sorted by (wanted, address) within bucket for SORTING
+  uint64_t max_records;  // capacity of ent2 / ent3 (dense)
+  uint64_t ent_cap;      // capacity of ent
+  uint32_t* wcount;      // entries per slab
+  uint64_t* woff;        // exclusive prefix of wcount (+ total at [nslabs])
+  uint32_t slab_cap;
+  uint32_t part_group;   // slabs per partition tile
+  uint64_t nslabs;
   // buckets
   uint32_t* bcount;
   uint32_t* bcursor;
@@ -164,6 +173,7 @@ struct StageTimer {
 // fast path (fused_kernels.hip)
 void launch_frame_fused(const BuildParams& P, hipStream_t s, StageTimer* tm);
 void launch_partition(const BuildParams& P, hipStream_t s, StageTimer* tm);
+void launch_dense_slabs(const BuildParams& P, hipStream_t s);
 void launch_place_fast(const BuildParams& P, hipStream_t s, StageTimer* tm);
 // fallbacks and shared stages (build_kernels.hip)
 void launch_framing_serial(const BuildParams& P, hipStream_t s);

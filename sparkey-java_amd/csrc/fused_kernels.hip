@@ -2,15 +2,16 @@
 //
 //   k_frame          ONE pass over the log: a wave owns 64 small chunks (lane = chunk):
 //                    speculative framing -> wave exit published at once -> entry from the previous
-//                    wave's exit -> record count prefix by decoupled look-back -> MurmurHash3 of
-//                    every key out of LDS -> (hash, address) entries in log order.
+//                    wave's exit -> MurmurHash3 of every key out of LDS -> (hash, address) entries
+//                    in log order into the wave's slab.
 //   k_part1_hist/    coarse radix partition of the entries by the top 8 bits of their bucket id
 //   k_part1_scatter  (bucket = wantedSlot >> 10), LDS-staged so every write run is contiguous.
 //   k_part2          one workgroup per coarse partition: fine split into buckets + bucket offsets.
 //   k_place_lds      per bucket, everything in LDS: counting sort by wanted slot, address order
 //                    inside equal slots, canonical positions, every slot of the bucket written once.
 //
-// Inter-workgroup hand-offs in k_frame use 8-byte granules that carry their own state bits
+// The only inter-workgroup hand-off in k_frame (a wave's exit -> the next wave's entry) uses 8-byte
+// granules that carry their own state bits
 // (MI355X_MICROARCH.md "Valid forms", R2: the data IS the flag) with relaxed agent-scope atomic
 // loads/stores; every granule is zeroed before the launch and every spin is time-bounded.
 #include <hip/hip_runtime.h>
@@ -139,9 +140,6 @@ __device__ inline uint64_t murmur64_ld(const Ld& ld, int32_t len, uint32_t seed)
 // granules (8-byte {state, value} words) -- relaxed agent-scope atomics, zeroed before the launch
 // ------------------------------------------------------------------------------------------------
 constexpr unsigned long long kReady = 1ull << 63;   // exit granule: bit 63 = published
-constexpr unsigned long long kAgg = 1ull << 62;     // count granule: local aggregate published
-constexpr unsigned long long kIncl = 2ull << 62;    // count granule: inclusive prefix published
-constexpr unsigned long long kStateMask = 3ull << 62;
 constexpr unsigned long long kSpinTicks = 2000000000ull;  // 20 s of the 100 MHz wall clock
 
 __device__ __forceinline__ void granule_store(unsigned long long* g, unsigned long long v) {
@@ -163,7 +161,7 @@ __device__ __forceinline__ unsigned long long granule_load(unsigned long long* g
 //   3 entries   a chunk whose surviving chains share one exit knows it without its entry; the
 //               wave's last exit is published at once, the first entry is the previous wave's
 //               published exit, unresolved chunks are walked in order
-//   4 counts    record counts, wave scan, decoupled look-back across waves for the base offset
+//   4 counts    record counts and their wave scan: offsets inside the wave's slab of entries
 //   5 hash      every lane walks its chunk from the verified entry and hashes each key from LDS
 // ================================================================================================
 __device__ __forceinline__ bool screen_start(uint32_t b0, uint32_t b1, const BuildParams& P) {
@@ -265,7 +263,10 @@ __global__ __launch_bounds__(64) void k_frame(BuildParams P) {
   const bool passthrough = k > 0 && s + P.max_rec_len - 1 >= e;
   const int64_t cand_end = !act || passthrough ? s : (k == 0 ? s + 1 : min(e, s + P.max_rec_len));
 
-  // ---- 1 screen: 8 candidate starts per step, branch-free (SWAR on one u64) ----
+  // ---- 1 screen: 64 candidate starts per mask word from 9 aligned u64 loads issued together,
+  //      8 per SWAR step (branch-free); masks stay in registers when maxRecLen <= 128 ----
+  const int nwl = (int)((min(C, P.max_rec_len) + 63) >> 6);
+  unsigned long long m0 = 0, m1 = 0;
   {
     constexpr uint64_t H = 0x8080808080808080ull, L7 = 0x7f7f7f7f7f7f7f7full, ONES = 0x0101010101010101ull;
     // per byte: b <= T with b < 128 (T >= 127: every byte); thresholds replicated once, outside the loop
@@ -275,34 +276,43 @@ __global__ __launch_bounds__(64) void k_frame(BuildParams P) {
     const uint64_t rv = ONES * (uint64_t)(min(P.max_value_len, (int64_t)126) + 1);
     const uint64_t rd = ONES * (uint64_t)(min(P.max_key_len, (int64_t)126) + 1);
     auto le_rep = [&](uint64_t x, uint64_t rep, bool all) -> uint64_t { return all ? H : ~(x | ((x | H) - rep)) & H; };
-    const int nq = (int)((min(C, P.max_rec_len) + 7) >> 3);
-    unsigned long long word = 0;
-    for (int q = 0; q < nq; q++) {
-      const int64_t c0 = s + 8ll * q;
-      uint32_t bits = 0;
-      if (c0 < cand_end) {
-        const uint32_t o = (uint32_t)(c0 - R0);
-        const uint64_t x = rgn_u64(rgn, o);
-        const uint64_t y = (x >> 8) | ((uint64_t)rgn[rswz(o + 8)] << 56);
-        const uint64_t z = ~(((x & L7) + L7) | x) & H;  // zero bytes
-        const uint64_t put_first = le_rep(x, rk, allk) & ~z;
-        // a log whose header counts no DELETE has none on its true chain: a 0x00 is no record start
-        const uint64_t r = (put_first & le_rep(y, rv, allv)) | (P.no_deletes ? 0ull : (z & le_rep(y, rd, alld)));
-        uint64_t t = (r >> 7) & ONES;  // gather the 8 flags into the low byte
-        t |= t >> 7;
-        t |= t >> 14;
-        t |= t >> 28;
-        bits = (uint32_t)(t & 0xffu);
-        const int64_t valid = cand_end - c0;
-        if (valid < 8) bits &= (1u << valid) - 1u;
+    for (int mw = 0; mw < nwl; mw++) {
+      unsigned long long word = 0;
+      const int64_t cw = s + 64ll * mw;
+      if (k == 0) {
+        word = (mw == 0 && cand_end > s) ? 1ull : 0ull;  // chunk 0: the only start is byte 84
+      } else if (cw < cand_end) {
+        const uint32_t o0 = (uint32_t)(cw - R0);  // 8-aligned: chunk starts are multiples of C
+        uint64_t w[9];
+#pragma unroll
+        for (int i = 0; i < 9; i++) w[i] = *reinterpret_cast<const uint64_t*>(rgn + rswz(o0 + 8u * i));
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+          const uint64_t x = w[q];
+          const uint64_t y = (x >> 8) | (w[q + 1] << 56);
+          const uint64_t z = ~(((x & L7) + L7) | x) & H;  // zero bytes
+          const uint64_t put_first = le_rep(x, rk, allk) & ~z;
+          // a log whose header counts no DELETE has none on its true chain: 0x00 starts no record
+          const uint64_t r = (put_first & le_rep(y, rv, allv)) | (P.no_deletes ? 0ull : (z & le_rep(y, rd, alld)));
+          uint64_t t = (r >> 7) & ONES;  // gather the 8 flags into one byte
+          t |= t >> 7;
+          t |= t >> 14;
+          t |= t >> 28;
+          word |= (t & 0xffull) << (8 * q);
+        }
+        const int64_t valid = cand_end - cw;
+        if (valid < 64) word &= (1ull << valid) - 1ull;
       }
-      word |= (unsigned long long)bits << (8 * (q & 7));
-      if ((q & 7) == 7 || q == nq - 1) {
-        if (act) masks[lane * nwords + (q >> 3)] = word;
-        word = 0;
+      if (nwl <= 2) {
+        if (mw == 0) m0 = word; else m1 = word;
+      } else if (act) {
+        masks[lane * nwords + mw] = word;
       }
     }
   }
+  auto mask_word = [&](int wi) -> unsigned long long {
+    return nwl <= 2 ? (wi == 0 ? m0 : m1) : masks[lane * nwords + wi];
+  };
   mark(1);
 
   // ---- 2 walk the screened candidates in lock step (one header per lane per step) ----
@@ -311,9 +321,8 @@ __global__ __launch_bounds__(64) void k_frame(BuildParams P) {
   int32_t c_min_steps = 0;
   unsigned long long dbg_iters = 0;
   {
-    const int nwl = (int)((min(C, P.max_rec_len) + 63) >> 6);
     int wi = 0;
-    unsigned long long m = (act && cand_end > s) ? masks[lane * nwords] : 0ull;
+    unsigned long long m = (act && cand_end > s) ? mask_word(0) : 0ull;
     bool done = !act || cand_end <= s;
     int32_t steps = 0;
     if (P.fr_fast) {
@@ -326,7 +335,7 @@ __global__ __launch_bounds__(64) void k_frame(BuildParams P) {
       int32_t rp = -1, rst = 0, rex = 0;
       for (;;) {
         if (!done && rp < 0) {
-          while (m == 0 && ++wi < nwl) m = masks[lane * nwords + wi];
+          while (m == 0 && ++wi < nwl) m = mask_word(wi);
           if (m == 0) {
             done = true;
           } else {
@@ -367,7 +376,7 @@ __global__ __launch_bounds__(64) void k_frame(BuildParams P) {
       int64_t p = -1, cst = 0, pex = -1;
       for (;;) {
         if (!done && p < 0) {
-          while (m == 0 && ++wi < nwl) m = masks[lane * nwords + wi];
+          while (m == 0 && ++wi < nwl) m = mask_word(wi);
           if (m == 0) {
             done = true;
           } else {
@@ -489,43 +498,17 @@ __global__ __launch_bounds__(64) void k_frame(BuildParams P) {
   const unsigned long long total = __shfl(incl, 63, 64);
   const unsigned long long local_off = incl - (unsigned long long)cnt;
   mark(4);
-  unsigned long long base = 0;
-  if (wv == 0) {
-    if (lane == 0) granule_store(&P.cnt_desc[0], kIncl | total);
-  } else {
-    if (lane == 0) granule_store(&P.cnt_desc[wv], kAgg | total);
-    int64_t jw = (int64_t)wv - 1;
-    unsigned long long acc = 0;
-    const unsigned long long t0 = wall_clock64();
-    for (;;) {
-      const int64_t idx = jw - lane;
-      const unsigned long long v = idx >= 0 ? granule_load(&P.cnt_desc[idx]) : kIncl;
-      const unsigned long long st = v & kStateMask;
-      const unsigned long long inc = __ballot(st == kIncl);
-      const unsigned long long none = __ballot(st == 0);
-      const int fi = inc ? __builtin_ctzll(inc) : 64;
-      const unsigned long long before = fi == 64 ? ~0ull : ((1ull << fi) - 1ull);
-      if (none & before) {
-        if (wall_clock64() - t0 > kSpinTicks) {
-          if (lane == 0) atomicOr(&P.st->spec_fail, 2u);
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-        continue;
-      }
-      acc += wave_sum_u64(lane <= fi ? (v & ~kStateMask) : 0ull);
-      if (fi < 64) break;
-      jw -= 64;
+  // the wave's records go to its own slab; the radix partition compacts the slabs
+  if (total > P.slab_cap) {
+    if (lane == 0) {
+      atomicMax(&P.st->max_wave_count, (unsigned int)min(total, 0xffffffffull));
+      atomicOr(&P.st->overflow, 1u);
     }
-    base = acc;
-    if (lane == 0) granule_store(&P.cnt_desc[wv], kIncl | (base + total));
-  }
-  if (wv == gridDim.x - 1 && lane == 0) P.st->n_records = base + total;
-  mark(5);
-  if (base + total > P.max_records) {
-    if (lane == 0) atomicOr(&P.st->overflow, 1u);
     return;
   }
+  if (lane == 0) P.wcount[wv] = (uint32_t)total;
+  const unsigned long long base = wv * (unsigned long long)P.slab_cap;
+  mark(5);
 
   // ---- 5 hash every record of the chunk, entries in log order ----
   unsigned long long ndel = 0;
@@ -576,16 +559,45 @@ __device__ __forceinline__ uint32_t bucket_of(const BuildParams& P, uint64_t has
   return (uint32_t)(fast_mod(hash, P.mod) >> kBucketShift);
 }
 
+// A partition tile is part_group consecutive slabs (<= kPartTile entries together).
+struct SlabTile {
+  uint32_t pre[kMaxPartGroup + 1];  // entry prefix over the tile's slabs
+  uint32_t ng;
+};
+
+__device__ __forceinline__ void load_tile(const BuildParams& P, SlabTile& T, uint64_t g0) {
+  if (threadIdx.x == 0) {
+    const uint64_t ng = min((uint64_t)P.part_group, P.nslabs > g0 ? P.nslabs - g0 : 0);
+    uint32_t acc = 0;
+    T.pre[0] = 0;
+    for (uint64_t g = 0; g < ng; g++) {
+      acc += P.wcount[g0 + g];
+      T.pre[g + 1] = acc;
+    }
+    T.ng = (uint32_t)ng;
+  }
+  __syncthreads();
+}
+
+// Entry i of the tile (i < pre[ng]).
+__device__ __forceinline__ const Entry& tile_entry(const BuildParams& P, const SlabTile& T, uint64_t g0, uint32_t i) {
+  uint32_t lo = 0, hi = T.ng;  // largest g with pre[g] <= i
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (T.pre[mid] <= i) lo = mid; else hi = mid;
+  }
+  return P.ent[(g0 + lo) * (uint64_t)P.slab_cap + (i - T.pre[lo])];
+}
+
 __global__ __launch_bounds__(kPartBlock) void k_part1_hist(BuildParams P) {
   __shared__ uint32_t hist[256];
-  const uint64_t N = min((uint64_t)P.st->n_records, P.max_records);
-  const uint64_t t0 = (uint64_t)blockIdx.x * kPartTile;
+  __shared__ SlabTile T;
+  const uint64_t g0 = (uint64_t)blockIdx.x * P.part_group;
   hist[threadIdx.x] = 0;
-  __syncthreads();
-  for (int i = 0; i < kPartItems; i++) {
-    const uint64_t idx = t0 + (uint64_t)i * kPartBlock + threadIdx.x;
-    if (idx < N) atomicAdd(&hist[bucket_of(P, P.ent[idx].hash) >> P.p2_bits], 1u);
-  }
+  load_tile(P, T, g0);
+  const uint32_t n = T.pre[T.ng];
+  for (uint32_t i = threadIdx.x; i < n; i += kPartBlock)
+    atomicAdd(&hist[bucket_of(P, tile_entry(P, T, g0, i).hash) >> P.p2_bits], 1u);
   __syncthreads();
   P.p1_hist[(uint64_t)threadIdx.x * P.p1_tiles + blockIdx.x] = hist[threadIdx.x];  // digit-major
 }
@@ -596,20 +608,22 @@ __global__ __launch_bounds__(kPartBlock) void k_part1_scatter(BuildParams P) {
   __shared__ uint32_t lbase[256];
   __shared__ uint32_t cursor[256];
   __shared__ uint64_t sh64[kPartBlock];
-  const uint64_t N = min((uint64_t)P.st->n_records, P.max_records);
-  const uint64_t t0 = (uint64_t)blockIdx.x * kPartTile;
+  __shared__ SlabTile T;
+  if (P.st->n_records > P.max_records) return;  // the host grows the workspace and redoes the build
+  const uint64_t g0 = (uint64_t)blockIdx.x * P.part_group;
   const int tid = threadIdx.x;
   hist[tid] = 0;
   cursor[tid] = 0;
-  __syncthreads();
+  load_tile(P, T, g0);
+  const uint32_t n = T.pre[T.ng];
   Entry v[kPartItems];
   uint32_t d[kPartItems];
 #pragma unroll
   for (int i = 0; i < kPartItems; i++) {
-    const uint64_t idx = t0 + (uint64_t)i * kPartBlock + tid;
+    const uint32_t idx = (uint32_t)i * kPartBlock + tid;
     d[i] = 0xffffffffu;
-    if (idx < N) {
-      v[i] = P.ent[idx];
+    if (idx < n) {
+      v[i] = tile_entry(P, T, g0, idx);
       d[i] = bucket_of(P, v[i].hash) >> P.p2_bits;
       atomicAdd(&hist[d[i]], 1u);
     }
@@ -631,6 +645,15 @@ __global__ __launch_bounds__(kPartBlock) void k_part1_scatter(BuildParams P) {
     const uint64_t dst = P.p1_off[(uint64_t)dd * P.p1_tiles + blockIdx.x] + (i - lbase[dd]);
     P.ent3[dst] = en;
   }
+}
+
+// Dense entries (serial framing path) seen as slabs of kPartTile.
+__global__ void k_dense_slabs(BuildParams P) {
+  const uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= P.nslabs) return;
+  const uint64_t N = P.st->n_records;
+  const uint64_t lo = w * P.slab_cap;
+  P.wcount[w] = (uint32_t)(N > lo ? min(N - lo, (uint64_t)P.slab_cap) : 0);
 }
 
 // Pass 2: one workgroup per coarse partition splits it into its 2^p2_bits buckets.
@@ -785,7 +808,13 @@ void launch_frame_fused(const BuildParams& P, hipStream_t s, StageTimer* tm) {
   const uint64_t nwaves = (P.fr_nchunks + P.fr_w - 1) / P.fr_w;
   const size_t lds = (size_t)P.fr_rgn_bytes + (size_t)P.fr_w * P.fr_mask_words * 8;
   hipLaunchKernelGGL(k_frame, dim3((unsigned)nwaves), dim3(64), lds, s, P);
+  scan_exclusive<uint32_t, uint64_t, OpAdd>(P.wcount, P.woff, P.nslabs, (uint64_t*)&P.st->n_records, OpAdd(),
+                                            P.scan_scratch_u64, s);
   tm->mark("frame", s);
+}
+
+void launch_dense_slabs(const BuildParams& P, hipStream_t s) {
+  hipLaunchKernelGGL(k_dense_slabs, dim3((unsigned)((P.nslabs + 255) / 256)), dim3(256), 0, s, P);
 }
 
 void launch_partition(const BuildParams& P, hipStream_t s, StageTimer* tm) {

@@ -220,7 +220,7 @@ struct sparkey_plan {
   uint64_t c_ent = 0, c_ent2 = 0, c_ent3 = 0;
   uint64_t c_bcount = 0, c_bcursor = 0, c_boff = 0, c_bfun = 0, c_bpre = 0, c_carry = 0;
   uint64_t c_pairs = 0, c_parts = 0, c_su = 0, c_smp = 0, c_bft = 0;
-  uint64_t c_desc = 0, c_p1h = 0, c_p1o = 0, c_dbg = 0;
+  uint64_t c_desc = 0, c_p1h = 0, c_p1o = 0, c_dbg = 0, c_wcount = 0, c_woff = 0;
   uint8_t* conv = nullptr;
   int64_t* exitp = nullptr;
   int64_t* qpos = nullptr;
@@ -242,7 +242,9 @@ struct sparkey_plan {
   StatPart* parts = nullptr;
   uint64_t* scan_u64 = nullptr;
   MaxPlus* scan_mp = nullptr;
-  unsigned long long* desc = nullptr;  // exit granules ++ count granules ++ ticket (memset per build)
+  unsigned long long* desc = nullptr;  // k_frame exit granules (memset per build)
+  uint32_t* wcount = nullptr;          // entries per slab
+  uint64_t* woff = nullptr;
   uint32_t* p1_hist = nullptr;
   uint64_t* p1_off = nullptr;
   Status* d_status = nullptr;
@@ -254,8 +256,8 @@ struct sparkey_plan {
   std::vector<double> stage_ms;
 };
 
-static int plan_reserve(sparkey_plan* pl, uint64_t nchunks, uint64_t nrec, uint64_t nbuckets, uint64_t cap,
-                        char* err, size_t err_len) {
+static int plan_reserve(sparkey_plan* pl, uint64_t nchunks, uint64_t nrec, uint64_t ent_cap, uint64_t nslabs,
+                        uint64_t p1_tiles, uint64_t nbuckets, uint64_t cap, char* err, size_t err_len) {
   HIP_TRY(grow(&pl->conv, pl->c_conv, nchunks));
   HIP_TRY(grow(&pl->exitp, pl->c_exitp, nchunks));
   HIP_TRY(grow(&pl->qpos, pl->c_qpos, nchunks));
@@ -263,7 +265,9 @@ static int plan_reserve(sparkey_plan* pl, uint64_t nchunks, uint64_t nrec, uint6
   HIP_TRY(grow(&pl->G, pl->c_G, nchunks + 1));
   HIP_TRY(grow(&pl->cnt, pl->c_cnt, nchunks));
   HIP_TRY(grow(&pl->off, pl->c_off, nchunks + 1));
-  HIP_TRY(grow(&pl->ent, pl->c_ent, nrec));
+  HIP_TRY(grow(&pl->ent, pl->c_ent, ent_cap));
+  HIP_TRY(grow(&pl->wcount, pl->c_wcount, nslabs + 1));
+  HIP_TRY(grow(&pl->woff, pl->c_woff, nslabs + 1));
   HIP_TRY(grow(&pl->ent2, pl->c_ent2, nrec));
   HIP_TRY(grow(&pl->ent3, pl->c_ent3, nrec));
   HIP_TRY(grow(&pl->bcount, pl->c_bcount, nbuckets));
@@ -277,10 +281,9 @@ static int plan_reserve(sparkey_plan* pl, uint64_t nchunks, uint64_t nrec, uint6
   HIP_TRY(grow(&pl->pairs, pl->c_pairs, 2 * pair_cap));
   HIP_TRY(grow(&pl->parts, pl->c_parts, (cap + kStatSlotsPerBlock - 1) / kStatSlotsPerBlock));
   HIP_TRY(grow(&pl->desc, pl->c_desc, 2 * nchunks + 2));
-  const uint64_t p1_tiles = std::max<uint64_t>(1, (nrec + kPartTile - 1) / kPartTile);
   HIP_TRY(grow(&pl->p1_hist, pl->c_p1h, 256 * p1_tiles));
   HIP_TRY(grow(&pl->p1_off, pl->c_p1o, 256 * p1_tiles + 1));
-  const uint64_t scratch = std::max(std::max(nchunks, nbuckets), 256 * p1_tiles) / kScanTile + 64;
+  const uint64_t scratch = std::max(std::max(std::max(nchunks, nbuckets), 256 * p1_tiles), nslabs) / kScanTile + 64;
   HIP_TRY(grow(&pl->scan_u64, pl->c_su, scratch + 16));
   HIP_TRY(grow(&pl->scan_mp, pl->c_smp, scratch + 16));
   return SPARKEY_OK;
@@ -396,18 +399,36 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
   int framing_path = fused_framing ? 0 : 1, placement_path = 0;
   float ms = 0.f;
   Status& st = *pl->h_status;
-  for (int attempt = 0; attempt < 3; attempt++) {
-    rc = plan_reserve(pl, P.nchunks, std::max<uint64_t>(nrec, 1), P.nbuckets, ip.cap, err, err_len);
+  const uint64_t nwaves = P.fr_nchunks ? (P.fr_nchunks + P.fr_w - 1) / P.fr_w : 0;
+  // k_frame writes each wave's entries into a slab sized from the header's record count (twice the
+  // mean per wave + 32); a wave that holds more grows the slabs and the build is redone
+  uint32_t slab_cap = (uint32_t)std::min<uint64_t>(
+      kPartTile, std::max<uint64_t>(64, 2 * ((nrec + std::max<uint64_t>(nwaves, 1) - 1) / std::max<uint64_t>(nwaves, 1)) + 32));
+  for (int attempt = 0; attempt < 4; attempt++) {
+    uint64_t ent_cap;
+    if (framing_path == 0) {
+      P.slab_cap = slab_cap;
+      P.nslabs = nwaves;
+      ent_cap = std::max<uint64_t>(1, nwaves * slab_cap);
+    } else {  // dense entries from the serial framing path, seen as slabs of kPartTile
+      P.slab_cap = kPartTile;
+      ent_cap = std::max<uint64_t>(nrec, 1);
+      P.nslabs = (ent_cap + kPartTile - 1) / kPartTile;
+    }
+    P.part_group = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(kMaxPartGroup, kPartTile / P.slab_cap));
+    P.p1_tiles = (uint32_t)std::max<uint64_t>(1, (P.nslabs + P.part_group - 1) / P.part_group);
+    rc = plan_reserve(pl, P.nchunks, std::max<uint64_t>(nrec, 1), ent_cap, P.nslabs, P.p1_tiles, P.nbuckets, ip.cap,
+                      err, err_len);
     if (rc) return rc;
     P.conv = pl->conv; P.exitp = pl->exitp; P.qpos = pl->qpos; P.tail = pl->tail; P.G = pl->G;
     P.cnt = pl->cnt; P.off = pl->off;
-    P.ent = pl->ent; P.ent2 = pl->ent2; P.ent3 = pl->ent3; P.max_records = pl->c_ent;
+    P.ent = pl->ent; P.ent2 = pl->ent2; P.ent3 = pl->ent3; P.max_records = pl->c_ent2;
+    P.ent_cap = std::min<uint64_t>(pl->c_ent, P.nslabs * P.slab_cap);
+    P.wcount = pl->wcount; P.woff = pl->woff;
     P.bcount = pl->bcount; P.bcursor = pl->bcursor; P.boff = pl->boff; P.bfun = pl->bfun; P.bpre = pl->bpre;
     P.bfun_total = pl->bfun_total; P.carry = pl->carry; P.pairs = pl->pairs; P.pair_cap = pl->c_pairs / 2;
     P.parts = pl->parts; P.scan_scratch_u64 = pl->scan_u64; P.scan_scratch_mp = pl->scan_mp;
-    const uint64_t nwaves = P.fr_nchunks ? (P.fr_nchunks + P.fr_w - 1) / P.fr_w : 0;
     P.exit_desc = pl->desc; P.cnt_desc = pl->desc + nwaves;
-    P.p1_tiles = (uint32_t)std::max<uint64_t>(1, (std::max<uint64_t>(nrec, 1) + kPartTile - 1) / kPartTile);
     P.p1_hist = pl->p1_hist; P.p1_off = pl->p1_off; P.p1_off_total = pl->p1_off + 256ull * P.p1_tiles;
     if (getenv("SPARKEY_FRAME_DEBUG")) {
       HIP_TRY(grow(&pl->dbg, pl->c_dbg, 16 * std::max<uint64_t>(P.nchunks, 1)));
@@ -424,10 +445,12 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
     HIP_TRY(hipMemcpyAsync(pl->d_status, &init, sizeof(Status), hipMemcpyHostToDevice, s));
     if (framing_path == 0) {
       HIP_TRY(hipMemsetAsync(pl->desc, 0, (2 * nwaves + 2) * sizeof(unsigned long long), s));
+      HIP_TRY(hipMemsetAsync(pl->wcount, 0, (P.nslabs + 1) * sizeof(uint32_t), s));
       launch_frame_fused(P, s, &pl->timer);
     } else {
       launch_framing_serial(P, s);
       launch_emit(P, s, &pl->timer);
+      launch_dense_slabs(P, s);
     }
     launch_partition(P, s, &pl->timer);
     launch_place_fast(P, s, &pl->timer);
@@ -451,10 +474,15 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
         const double n = (double)nwv;
         fprintf(stderr, "[k_frame] waves=%llu C=%d W=%d mean cycles: stage %.0f screen %.0f walk %.0f entry %.0f "
                 "counts %.0f lookback %.0f hash %.0f | max entry %llu max lookback %llu | walk iters %.1f survivors/wave "
-                "%.1f unconverged/wave %.2f\n",
+                "%.1f unconverged/wave %.2f | lookback spins %.1f windows %.2f distance %.1f\n",
                 (unsigned long long)nwv, 1 << P.fr_cshift, P.fr_w, sum[0] / n, sum[1] / n, sum[2] / n, sum[3] / n,
-                sum[4] / n, sum[5] / n, sum[6] / n, mx[3], mx[5], sum[8] / n, sum[9] / n, sum[10] / n);
+                sum[4] / n, sum[5] / n, sum[6] / n, mx[3], mx[5], sum[8] / n, sum[9] / n, sum[10] / n, sum[11] / n, sum[12] / n,
+                sum[13] / n);
       }
+    }
+    if (framing_path == 0 && st.max_wave_count > slab_cap) {  // a wave overflowed its slab
+      slab_cap = (uint32_t)std::min<uint64_t>(kPartTile, ((uint64_t)st.max_wave_count + 63) & ~63ull);
+      continue;
     }
     if (st.overflow || st.n_records > P.max_records) {  // header under-counts records: grow and redo
       nrec = std::max<uint64_t>(st.n_records, nrec * 2 + 1);
@@ -534,7 +562,8 @@ int sparkey_plan_create(sparkey_plan** plan_out, int32_t device, uint64_t max_lo
   if (max_records) {
     const uint64_t nchunks = max_log_bytes / kChunk + 1;
     const uint64_t cap = max_records * 2;
-    int rc = plan_reserve(pl, nchunks, max_records, cap / kBucket + 1, cap, err, err_len);
+    const uint64_t nslabs = max_log_bytes / 8192 + 2;
+    int rc = plan_reserve(pl, nchunks, max_records, nslabs * 192, nslabs, nslabs, cap / kBucket + 1, cap, err, err_len);
     if (rc) {
       sparkey_plan_destroy(pl);
       return rc;
@@ -576,7 +605,7 @@ void sparkey_plan_destroy(sparkey_plan* pl) {
   (void)hipSetDevice(pl->device);
   void* bufs[] = {pl->conv, pl->exitp, pl->qpos, pl->tail, pl->G, pl->cnt, pl->off, pl->ent, pl->ent2, pl->ent3,
                   pl->bcount, pl->bcursor, pl->boff, pl->bfun, pl->bpre, pl->bfun_total, pl->carry, pl->pairs,
-                  pl->parts, pl->scan_u64, pl->scan_mp, pl->desc, pl->p1_hist, pl->p1_off, pl->d_status, pl->dbg};
+                  pl->parts, pl->scan_u64, pl->scan_mp, pl->desc, pl->p1_hist, pl->p1_off, pl->d_status, pl->dbg, pl->wcount, pl->woff};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (pl->h_status) (void)hipHostFree(pl->h_status);
