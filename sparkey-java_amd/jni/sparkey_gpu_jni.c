@@ -1,0 +1,82 @@
+/*
+ * sparkey_gpu_jni.c -- JNI shim between com.spotify.sparkey.GpuIndexHash and the
+ * C-ABI in include/sparkey_gpu.h.  It only converts arguments and maps the C-ABI's error codes to
+ * the exception classes and messages the reference throws from IndexHash.createNew
+ * (IndexHash.java:131-167) and the code it calls:
+ *   IOException       LogHeader.read (LogHeader.java:57-83), "No free slots in the hash"
+ *                     (IndexHash.java:574-576,664), CommonHeader (CommonHeader.java:38-43), file I/O
+ *   RuntimeException  "Corrupt data" / "Invalid data - reference to delete entry"
+ *                     (IndexHash.java:484,494,613,624), "Too long VLQ value" (Util.java:181,217)
+ *   IllegalArgumentException  bad hash size / options
+ *
+ * Built by sparkey-java_amd/build.py only when $JAVA_HOME/include/jni.h exists (this image has no
+ * JDK, so the shim is compiled and exercised on machines that do).
+ */
+#include <jni.h>
+#include <string.h>
+
+#include "sparkey_gpu.h"
+
+static void throw_for(JNIEnv* env, int rc, const char* msg) {
+  const char* cls = "java/io/IOException";
+  switch (rc) {
+    case SPARKEY_E_CORRUPT_DATA:
+    case SPARKEY_E_VLQ:
+    case SPARKEY_E_GPU:
+      cls = "java/lang/RuntimeException";
+      break;
+    case SPARKEY_E_ARG:
+    case SPARKEY_E_BUFFER:
+      cls = "java/lang/IllegalArgumentException";
+      break;
+    default:
+      break;
+  }
+  jclass ex = (*env)->FindClass(env, cls);
+  if (ex) (*env)->ThrowNew(env, ex, msg && msg[0] ? msg : sparkey_strerror(rc));
+}
+
+/*
+ * private static native void createNew0(String indexFile, String logFile, int hashSize, double sparsity,
+ *                                       boolean fsync, int hashSeed, long maxMemory, int method,
+ *                                       int device, long[] statsOut);
+ * hashSize: 0 = auto (hashType == null), 4 or 8.  method: ConstructionMethod.ordinal() (AUTO 0,
+ * IN_MEMORY 1, SORTING 2).  statsOut (nullable, length >= 9): numRecords, numPuts, numDeletes,
+ * numEntries, capacity, garbageSize, maxDisplacement, hashCollisions, totalDisplacement.
+ */
+JNIEXPORT void JNICALL Java_com_spotify_sparkey_GpuIndexHash_createNew0(
+    JNIEnv* env, jclass cls, jstring index_file, jstring log_file, jint hash_size, jdouble sparsity,
+    jboolean fsync, jint hash_seed, jlong max_memory, jint method, jint device, jlongArray stats_out) {
+  (void)cls;
+  const char* idx = (*env)->GetStringUTFChars(env, index_file, NULL);
+  const char* log = (*env)->GetStringUTFChars(env, log_file, NULL);
+  if (!idx || !log) {
+    if (idx) (*env)->ReleaseStringUTFChars(env, index_file, idx);
+    if (log) (*env)->ReleaseStringUTFChars(env, log_file, log);
+    return; /* OutOfMemoryError already pending */
+  }
+  sparkey_build_opts opts;
+  memset(&opts, 0, sizeof(opts));
+  opts.hash_size = hash_size;
+  opts.hash_seed = hash_seed;
+  opts.sparsity = sparsity;
+  opts.max_memory = max_memory;
+  opts.method = method;
+  opts.device = device;
+  sparkey_build_stats st;
+  memset(&st, 0, sizeof(st));
+  char err[512];
+  err[0] = 0;
+  const int rc = sparkey_build_index_file(log, idx, &opts, fsync ? 1 : 0, &st, err, sizeof(err));
+  (*env)->ReleaseStringUTFChars(env, index_file, idx);
+  (*env)->ReleaseStringUTFChars(env, log_file, log);
+  if (rc != SPARKEY_OK) {
+    throw_for(env, rc, err);
+    return;
+  }
+  if (stats_out && (*env)->GetArrayLength(env, stats_out) >= 9) {
+    const jlong v[9] = {st.num_records, st.num_puts, st.num_deletes, st.num_entries, st.capacity,
+                        st.garbage_size, st.max_displacement, st.hash_collisions, st.total_displacement};
+    (*env)->SetLongArrayRegion(env, stats_out, 0, 9, v);
+  }
+}
