@@ -35,21 +35,24 @@ __global__ void k_walk(BuildParams P, int serial) {
     if (P.conv[k]) return;
     if (k > 0 && !P.conv[k - 1]) return;
   }
-  int64_t p = (k == 0) ? kLogHeaderSize : P.exitp[k - 1];
+  int64_t p = (k == 0) ? P.fr_entry : P.exitp[k - 1];
   uint64_t m = k;
   P.G[m] = p;
   uint32_t c = 0;
-  int64_t em = chunk_end(m, P.data_end);
+  int64_t em = chunk_end(P.ch_k0 + m, P.data_end);
   auto at = [&](int64_t a) -> uint32_t { return P.log[a]; };
   for (;;) {
     while (p >= em) {
       P.cnt[m] = c;
       c = 0;
       m++;
-      if (m >= nc) return;
+      if (m >= nc) {
+        if (serial) P.st->exit = p;
+        return;
+      }
       P.G[m] = p;
       if (!serial && P.conv[m]) return;
-      em = chunk_end(m, P.data_end);
+      em = chunk_end(P.ch_k0 + m, P.data_end);
     }
     const RecHdr h = decode_header(at, p, (int64_t)P.log_len);
     if (!header_valid(h, p, P.max_key_len, (int64_t)P.log_len)) {
@@ -74,8 +77,8 @@ __global__ __launch_bounds__(64) void k_emit(BuildParams P) {
   __shared__ int32_t s_n;
   const uint64_t k = blockIdx.x;
   const int lane = threadIdx.x;
-  const int64_t wb = (int64_t)(k << kChunkShift);
-  const int64_t e = chunk_end(k, P.data_end);
+  const int64_t wb = (int64_t)((P.ch_k0 + k) << kChunkShift);
+  const int64_t e = chunk_end(P.ch_k0 + k, P.data_end);
   const int wn = kChunk + P.emit_extra;
   stage_window(win, P.log, wb, wn, (int64_t)P.log_len, lane, 64);
   __syncthreads();
@@ -141,7 +144,8 @@ __global__ __launch_bounds__(kPlaceBlock) void k_summary(BuildParams P) {
   __shared__ int32_t M[kBucket];
   __shared__ uint64_t sh64[kPlaceBlock];
   __shared__ int64_t shm[kPlaceBlock];
-  const uint64_t b = blockIdx.x;
+  if (build_aborted(P)) return;
+  const uint64_t b = P.b_lo + blockIdx.x;
   const uint64_t start = b << kBucketShift;
   const int64_t bsize = (int64_t)min((uint64_t)kBucket, P.cap - start);
   const uint32_t n = P.bcount[b];
@@ -158,16 +162,22 @@ __global__ __launch_bounds__(kPlaceBlock) void k_summary(BuildParams P) {
 }
 
 // carry[b] = (F_{b-1} o ... o F_0)(x0), x0 = fixed point of the whole ring = C_total when N < cap.
+// Sharded: the prefix starts at b_lo and x0 is the rank's carry-in (composed on the host).
 __global__ void k_carry(BuildParams P) {
-  const uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (build_aborted(P)) return;
+  const uint64_t b = P.b_lo + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const MaxPlus tot = *P.bfun_total;
-  if (tot.a >= 0) {  // N >= capacity: no empty slot, the canonical layout does not apply
-    if (b == 0) atomicOr(&P.st->full, 1u);
-    return;
+  int64_t x0 = P.carry_in;
+  if (!P.sharded) {
+    if (tot.a >= 0) {  // N >= capacity: no empty slot, the canonical layout does not apply
+      if (b == 0) atomicOr(&P.st->full, 1u);
+      return;
+    }
+    x0 = tot.c;
   }
-  if (b >= P.nbuckets) return;
+  if (b >= P.b_hi) return;
   const MaxPlus pre = P.bpre[b];
-  P.carry[b] = max(pre.c, tot.c + pre.a);
+  P.carry[b] = max(pre.c, x0 + pre.a);
 }
 
 // Global-memory placement of every bucket (buckets too big for k_place_lds), or, with
@@ -179,13 +189,16 @@ __global__ __launch_bounds__(kPlaceBlock) void k_place(BuildParams P, int sort_o
   __shared__ int32_t slot_of[kBucket];
   __shared__ uint64_t sh64[kPlaceBlock];
   __shared__ int64_t shm[kPlaceBlock];
-  if (only_big && P.bcount[blockIdx.x] <= kPlaceLdsMax) return;
-  place_bucket_global(P, blockIdx.x, sort_only, cnt, base, M, slot_of, sh64, shm);
+  if (build_aborted(P)) return;
+  const uint64_t b = P.b_lo + blockIdx.x;
+  if (only_big && P.bcount[b] <= kPlaceLdsMax) return;
+  place_bucket_global(P, b, sort_only, cnt, base, M, slot_of, sh64, shm);
 }
 
 // Equal-hash pairs: do they share the key?  (the reference compares key bytes in the log,
 // IndexHash.java:619-629)
 __global__ void k_verify_pairs(BuildParams P) {
+  if (build_aborted(P)) return;
   const unsigned long long np = min(P.st->n_pairs, (unsigned long long)P.pair_cap);
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= np) return;
@@ -212,11 +225,15 @@ __global__ __launch_bounds__(kStatBlock) void k_stats(BuildParams P) {
   __shared__ unsigned long long red_sum[kStatBlock / 64];
   __shared__ unsigned long long red_col[kStatBlock / 64];
   __shared__ long long red_max[kStatBlock / 64];
+  if (build_aborted(P)) return;
   const int tid = threadIdx.x;
-  const uint64_t blk0 = (uint64_t)blockIdx.x * kStatSlotsPerBlock;
+  const uint64_t blk0 = P.slot_lo + (uint64_t)blockIdx.x * kStatSlotsPerBlock;
   uint64_t prev_hash = 0;
   uint32_t prev_occ = 0;
-  if (blk0 > 0 && blk0 < P.cap) {
+  if (blk0 == P.slot_lo && P.sharded) {  // the slot before the range lives on another rank
+    prev_hash = P.prev_hash;
+    prev_occ = (uint32_t)P.prev_occ;
+  } else if (blk0 > 0 && blk0 < P.slot_hi) {
     uint64_t h, a;
     read_slot(P, blk0 - 1, h, a);
     prev_hash = h;
@@ -227,13 +244,13 @@ __global__ __launch_bounds__(kStatBlock) void k_stats(BuildParams P) {
   for (int it = 0; it < kStatSlotsPerBlock / kStatBlock; it++) {
     const uint64_t slot = blk0 + (uint64_t)it * kStatBlock + tid;
     uint64_t h = 0, a = 0;
-    if (slot < P.cap) read_slot(P, slot, h, a);
+    if (slot < P.slot_hi) read_slot(P, slot, h, a);
     sh_hash[tid] = h;
     sh_occ[tid] = a != 0;
     __syncthreads();
     const uint64_t ph = tid ? sh_hash[tid - 1] : prev_hash;
     const uint32_t po = tid ? sh_occ[tid - 1] : prev_occ;
-    if (slot < P.cap) {
+    if (slot < P.slot_hi) {
       if (po && ph == h) col++;
       if (a != 0) {
         int64_t d = (int64_t)slot - (int64_t)fast_mod(h, P.mod);
@@ -288,12 +305,18 @@ __global__ __launch_bounds__(256) void k_stats_final(BuildParams P, uint32_t npa
   if (tid == 0) {
     sum = s_sum[0]; col = s_col[0]; mx = s_max[0];
     for (int i = 1; i < 256; i++) { sum += s_sum[i]; col += s_col[i]; mx = max(mx, s_max[i]); }
+    Status* st = P.st;
+    if (P.sharded) {  // partial sums of the rank's slots; the host reduces them and adds the quirk
+      st->max_disp = mx;
+      st->collisions = (long long)col;
+      st->total_disp = (long long)sum;
+      return;
+    }
     // wrap quirk (IndexHash.java:239-241): slot 0 and slot cap-1 both occupied with equal hashes
     uint64_t h0, a0, h1, a1;
     read_slot(P, 0, h0, a0);
     read_slot(P, P.cap - 1, h1, a1);
     if (a0 != 0 && a1 != 0 && h0 == h1) col++;
-    Status* st = P.st;
     long long entries, garbage;
     if (sequential) { entries = st->num_entries; garbage = st->garbage; }
     else { entries = (long long)st->n_records; garbage = 0; }
@@ -519,16 +542,23 @@ void launch_emit(const BuildParams& P, hipStream_t s, StageTimer* tm) {
   tm->mark("emit", s);
 }
 
+void launch_carry(const BuildParams& P, hipStream_t s) {
+  if (P.b_hi > P.b_lo) hipLaunchKernelGGL(k_carry, dim3(grid_for(P.b_hi - P.b_lo, 256)), dim3(256), 0, s, P);
+}
+
 void launch_summary_carry(const BuildParams& P, hipStream_t s, StageTimer* tm) {
-  hipLaunchKernelGGL(k_summary, dim3((unsigned)P.nbuckets), dim3(kPlaceBlock), 0, s, P);
-  scan_exclusive<MaxPlus, MaxPlus, OpMaxPlus>(P.bfun, P.bpre, P.nbuckets, P.bfun_total, OpMaxPlus(),
+  const uint64_t nb = P.b_hi - P.b_lo;
+  if (nb == 0) return;
+  hipLaunchKernelGGL(k_summary, dim3((unsigned)nb), dim3(kPlaceBlock), 0, s, P);
+  scan_exclusive<MaxPlus, MaxPlus, OpMaxPlus>(P.bfun + P.b_lo, P.bpre + P.b_lo, nb, P.bfun_total, OpMaxPlus(),
                                               P.scan_scratch_mp, s);
-  hipLaunchKernelGGL(k_carry, dim3(grid_for(P.nbuckets, 256)), dim3(256), 0, s, P);
+  if (!P.sharded) launch_carry(P, s);
   tm->mark("summary", s);
 }
 
 void launch_place_global(const BuildParams& P, hipStream_t s, int sort_only, int only_big) {
-  hipLaunchKernelGGL(k_place, dim3((unsigned)P.nbuckets), dim3(kPlaceBlock), 0, s, P, sort_only, only_big);
+  if (P.b_hi > P.b_lo)
+    hipLaunchKernelGGL(k_place, dim3((unsigned)(P.b_hi - P.b_lo)), dim3(kPlaceBlock), 0, s, P, sort_only, only_big);
 }
 
 void launch_verify(const BuildParams& P, hipStream_t s, StageTimer* tm) {
@@ -537,8 +567,8 @@ void launch_verify(const BuildParams& P, hipStream_t s, StageTimer* tm) {
 }
 
 void launch_stats(const BuildParams& P, hipStream_t s, int sequential, StageTimer* tm) {
-  const uint64_t nparts = (P.cap + kStatSlotsPerBlock - 1) / kStatSlotsPerBlock;
-  hipLaunchKernelGGL(k_stats, dim3((unsigned)nparts), dim3(kStatBlock), 0, s, P);
+  const uint64_t nparts = (P.slot_hi - P.slot_lo + kStatSlotsPerBlock - 1) / kStatSlotsPerBlock;
+  if (nparts) hipLaunchKernelGGL(k_stats, dim3((unsigned)nparts), dim3(kStatBlock), 0, s, P);
   hipLaunchKernelGGL(k_stats_final, dim3(1), dim3(256), 0, s, P, (uint32_t)nparts, sequential);
   tm->mark("stats", s);
 }

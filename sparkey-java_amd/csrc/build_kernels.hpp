@@ -42,6 +42,14 @@ struct MaxPlus {
   int64_t a;
 };
 
+// A slot written outside the rank's slot range in a sharded build: sent to the slot's owner.
+struct alignas(16) SpillEntry {
+  uint64_t slot;
+  uint64_t hash;
+  uint64_t addr;
+  uint64_t pad;
+};
+
 struct StatPart {
   unsigned long long sum_disp;
   unsigned long long collisions;
@@ -67,6 +75,8 @@ struct Status {
   long long total_disp;
   unsigned int max_wave_count;  // largest per-wave record count when a slab overflowed
   unsigned int pad2;
+  long long exit;                // first record start >= the frame end on the framed chain
+  unsigned long long n_spill;    // sharded placement: slots written outside the rank's range
 };
 
 struct BuildParams {
@@ -130,7 +140,8 @@ struct BuildParams {
   uint64_t* p1_off;
   uint64_t* p1_off_total;
   uint32_t p1_tiles;
-  int32_t p2_bits;
+  uint32_t bpp;       // buckets per coarse digit: digit = bucket / bpp (< 256), computed as
+  uint64_t dmagic;    // (bucket * dmagic) >> 40, dmagic = ceil(2^40 / bpp), exact for bpp < 2^18
   unsigned long long* dbg;  // diagnostic phase counters (SPARKEY_FRAME_DEBUG=1), else null
   // k_frame geometry (chunk C = 2^fr_cshift bytes, fr_w chunks per wave)
   int32_t fr_cshift;
@@ -141,6 +152,23 @@ struct BuildParams {
   int32_t fr_fast;  // maxKeyLen + 1 < 128 and maxValueLen < 128: canonical headers are 2 bytes
   int32_t no_deletes;  // the log header counts no DELETE: speculation treats 0x00 as no record start
   uint64_t fr_nchunks;
+  // framing window: records start at fr_entry (84 for a whole log) and are framed while they start
+  // below data_end (the frame end); k_frame chunks are numbered from fr_k0 = fr_entry >> fr_cshift,
+  // serial-path chunks (kChunk) from ch_k0 = fr_entry >> kChunkShift
+  int64_t fr_entry;
+  uint64_t fr_k0;
+  uint64_t ch_k0;
+  // placement range: buckets [b_lo, b_hi), slots [slot_lo, slot_hi) (the whole table unless
+  // sharded); in a sharded build slots outside the range go to the spill list, the carry into
+  // b_lo is carry_in, and the slot before slot_lo is (prev_hash, prev_occ)
+  int32_t sharded;
+  int32_t prev_occ;
+  uint64_t b_lo, b_hi;
+  uint64_t slot_lo, slot_hi;
+  int64_t carry_in;
+  uint64_t prev_hash;
+  SpillEntry* spill;
+  uint64_t spill_cap;
 };
 
 // Per-stage HIP events on the build stream (only when profiling is enabled).
@@ -173,15 +201,25 @@ struct StageTimer {
 // fast path (fused_kernels.hip)
 void launch_frame_fused(const BuildParams& P, hipStream_t s, StageTimer* tm);
 void launch_partition(const BuildParams& P, hipStream_t s, StageTimer* tm);
+void launch_partition1(const BuildParams& P, hipStream_t s);
 void launch_dense_slabs(const BuildParams& P, hipStream_t s);
 void launch_place_fast(const BuildParams& P, hipStream_t s, StageTimer* tm);
+void launch_place_buckets(const BuildParams& P, hipStream_t s);
 // fallbacks and shared stages (build_kernels.hip)
 void launch_framing_serial(const BuildParams& P, hipStream_t s);
 void launch_emit(const BuildParams& P, hipStream_t s, StageTimer* tm);
 void launch_summary_carry(const BuildParams& P, hipStream_t s, StageTimer* tm);
+void launch_carry(const BuildParams& P, hipStream_t s);
 void launch_place_global(const BuildParams& P, hipStream_t s, int sort_only, int only_big);
 void launch_verify(const BuildParams& P, hipStream_t s, StageTimer* tm);
 void launch_stats(const BuildParams& P, hipStream_t s, int sequential, StageTimer* tm);
 void launch_sequential(const BuildParams& P, hipStream_t s, int sorted_order);
+// sharded builds (shard_kernels.hip)
+void launch_dest_counts(const BuildParams& P, hipStream_t s, int world, uint32_t nd, uint64_t* d_out);
+void launch_apply_spill(const BuildParams& P, hipStream_t s, const SpillEntry* in, uint64_t n);
+void launch_fetch_keys(const BuildParams& P, hipStream_t s, const uint64_t* addrs, uint64_t n, uint8_t* rec,
+                       uint32_t rec_size);
+void launch_compare_keys(const BuildParams& P, hipStream_t s, const uint8_t* rec, uint64_t npairs, uint32_t rec_size);
+void launch_find_entry(const BuildParams& P, hipStream_t s, int64_t lo, int64_t cand_end, int64_t target, int64_t* d_out);
 
 }  // namespace sk

@@ -230,8 +230,9 @@ __global__ __launch_bounds__(64) void k_frame(BuildParams P) {
   const int64_t LOOK = P.fr_look;
   const int nwords = P.fr_mask_words;
   const int64_t log_len = (int64_t)P.log_len;
-  const uint64_t k0 = wv * (uint64_t)W;
-  const int nw = (int)min((uint64_t)W, P.fr_nchunks - k0);
+  const uint64_t kf = P.fr_k0;  // chunk of the framing entry
+  const uint64_t k0 = kf + wv * (uint64_t)W;
+  const int nw = (int)min((uint64_t)W, kf + P.fr_nchunks - k0);
   const int64_t R0 = (int64_t)(k0 << cs);
   const int64_t RLEN = ((int64_t)nw << cs) + LOOK + 16;  // staged bytes [R0, R0 + RLEN)
   const int64_t RUSE = R0 + RLEN - 16;                     // headers decodable in LDS below this
@@ -257,11 +258,11 @@ __global__ __launch_bounds__(64) void k_frame(BuildParams P) {
   const bool act = lane < nw;
   const uint64_t k = k0 + lane;
   const int64_t wb = (int64_t)(k << cs);
-  const int64_t s = (k == 0) ? kLogHeaderSize : wb;
+  const int64_t s = (k == kf) ? P.fr_entry : wb;
   const int64_t e = act ? min(wb + C, P.data_end) : wb;
   const int64_t stop = min(min(e + LOOK, P.data_end), RUSE);  // speculative walks end here
-  const bool passthrough = k > 0 && s + P.max_rec_len - 1 >= e;
-  const int64_t cand_end = !act || passthrough ? s : (k == 0 ? s + 1 : min(e, s + P.max_rec_len));
+  const bool passthrough = k > kf && s + P.max_rec_len - 1 >= e;
+  const int64_t cand_end = !act || passthrough ? s : (k == kf ? s + 1 : min(e, s + P.max_rec_len));
 
   // ---- 1 screen: 64 candidate starts per mask word from 9 aligned u64 loads issued together,
   //      8 per SWAR step (branch-free); masks stay in registers when maxRecLen <= 128 ----
@@ -279,8 +280,8 @@ __global__ __launch_bounds__(64) void k_frame(BuildParams P) {
     for (int mw = 0; mw < nwl; mw++) {
       unsigned long long word = 0;
       const int64_t cw = s + 64ll * mw;
-      if (k == 0) {
-        word = (mw == 0 && cand_end > s) ? 1ull : 0ull;  // chunk 0: the only start is byte 84
+      if (k == kf) {
+        word = (mw == 0 && cand_end > s) ? 1ull : 0ull;  // the entry chunk: its only start is the entry
       } else if (cw < cand_end) {
         const uint32_t o0 = (uint32_t)(cw - R0);  // 8-aligned: chunk starts are multiples of C
         uint64_t w[9];
@@ -419,8 +420,8 @@ __global__ __launch_bounds__(64) void k_frame(BuildParams P) {
   // ---- 3 entries ----
   int64_t my_exit = converged ? (int64_t)min_exit : -1;
   if (lane == nw - 1 && converged) granule_store(&P.exit_desc[wv], (unsigned long long)my_exit | kReady);
-  unsigned long long extv = (unsigned long long)kLogHeaderSize;
-  if (k0 > 0 && lane == 0) {
+  unsigned long long extv = (unsigned long long)P.fr_entry;
+  if (wv > 0 && lane == 0) {
     const unsigned long long t0 = wall_clock64();
     for (;;) {
       const unsigned long long v = granule_load(&P.exit_desc[wv - 1]);
@@ -463,6 +464,7 @@ __global__ __launch_bounds__(64) void k_frame(BuildParams P) {
     }
   }
   if (lane == nw - 1 && !converged) granule_store(&P.exit_desc[wv], (unsigned long long)my_exit | kReady);
+  if (lane == nw - 1 && wv + 1 == gridDim.x) P.st->exit = my_exit;  // the framed chain's exit
   const int64_t up = __shfl_up(my_exit, 1, 64);
   const int64_t entry = lane == 0 ? ext : up;
 
@@ -553,10 +555,14 @@ __global__ __launch_bounds__(64) void k_frame(BuildParams P) {
 
 // ================================================================================================
 // Radix partition of the entries by bucket (bucket = wantedSlot >> kBucketShift).
-// Pass 1: digit d1 = bucket >> P.p2_bits (< 256) over tiles of kPartTile entries.
+// Pass 1: coarse digit = bucket / bpp (< 256; every digit holds bpp buckets, so the digits
+// split the table evenly -- a sharded build gives each rank a run of digits) over tiles of slabs.
 // ================================================================================================
 __device__ __forceinline__ uint32_t bucket_of(const BuildParams& P, uint64_t hash) {
   return (uint32_t)(fast_mod(hash, P.mod) >> kBucketShift);
+}
+__device__ __forceinline__ uint32_t digit_of(const BuildParams& P, uint32_t bucket) {
+  return (uint32_t)(((uint64_t)bucket * P.dmagic) >> 40);
 }
 
 // A partition tile is part_group consecutive slabs (<= kPartTile entries together).
@@ -592,12 +598,13 @@ __device__ __forceinline__ const Entry& tile_entry(const BuildParams& P, const S
 __global__ __launch_bounds__(kPartBlock) void k_part1_hist(BuildParams P) {
   __shared__ uint32_t hist[256];
   __shared__ SlabTile T;
+  if (build_aborted(P)) return;
   const uint64_t g0 = (uint64_t)blockIdx.x * P.part_group;
   hist[threadIdx.x] = 0;
   load_tile(P, T, g0);
   const uint32_t n = T.pre[T.ng];
   for (uint32_t i = threadIdx.x; i < n; i += kPartBlock)
-    atomicAdd(&hist[bucket_of(P, tile_entry(P, T, g0, i).hash) >> P.p2_bits], 1u);
+    atomicAdd(&hist[digit_of(P, bucket_of(P, tile_entry(P, T, g0, i).hash))], 1u);
   __syncthreads();
   P.p1_hist[(uint64_t)threadIdx.x * P.p1_tiles + blockIdx.x] = hist[threadIdx.x];  // digit-major
 }
@@ -609,7 +616,7 @@ __global__ __launch_bounds__(kPartBlock) void k_part1_scatter(BuildParams P) {
   __shared__ uint32_t cursor[256];
   __shared__ uint64_t sh64[kPartBlock];
   __shared__ SlabTile T;
-  if (P.st->n_records > P.max_records) return;  // the host grows the workspace and redoes the build
+  if (build_aborted(P)) return;  // the host grows the workspace and redoes the build
   const uint64_t g0 = (uint64_t)blockIdx.x * P.part_group;
   const int tid = threadIdx.x;
   hist[tid] = 0;
@@ -624,7 +631,7 @@ __global__ __launch_bounds__(kPartBlock) void k_part1_scatter(BuildParams P) {
     d[i] = 0xffffffffu;
     if (idx < n) {
       v[i] = tile_entry(P, T, g0, idx);
-      d[i] = bucket_of(P, v[i].hash) >> P.p2_bits;
+      d[i] = digit_of(P, bucket_of(P, v[i].hash));
       atomicAdd(&hist[d[i]], 1u);
     }
   }
@@ -641,7 +648,7 @@ __global__ __launch_bounds__(kPartBlock) void k_part1_scatter(BuildParams P) {
   // coalesced write-out: LDS position i -> global offset of its digit run
   for (uint32_t i = tid; i < (uint32_t)total; i += kPartBlock) {
     const Entry en = stage[i];
-    const uint32_t dd = bucket_of(P, en.hash) >> P.p2_bits;
+    const uint32_t dd = digit_of(P, bucket_of(P, en.hash));
     const uint64_t dst = P.p1_off[(uint64_t)dd * P.p1_tiles + blockIdx.x] + (i - lbase[dd]);
     P.ent3[dst] = en;
   }
@@ -656,21 +663,22 @@ __global__ void k_dense_slabs(BuildParams P) {
   P.wcount[w] = (uint32_t)(N > lo ? min(N - lo, (uint64_t)P.slab_cap) : 0);
 }
 
-// Pass 2: one workgroup per coarse partition splits it into its 2^p2_bits buckets.
+// Pass 2: one workgroup per coarse digit splits it into its bpp buckets.
 __global__ __launch_bounds__(kPartBlock) void k_part2(BuildParams P) {
   extern __shared__ __attribute__((aligned(16))) uint32_t dyn[];  // hist[nbins] ++ cur[nbins]
   __shared__ uint64_t sh64[kPartBlock];
+  if (build_aborted(P)) return;
   const uint32_t dpart = blockIdx.x;
   const uint64_t lo = P.p1_off[(uint64_t)dpart * P.p1_tiles];
   const uint64_t hi = (dpart + 1 < 256) ? P.p1_off[(uint64_t)(dpart + 1) * P.p1_tiles] : P.p1_off_total[0];
-  const uint32_t nbins = 1u << P.p2_bits;
+  const uint32_t nbins = P.bpp;
+  const uint32_t b0 = dpart * nbins;
   uint32_t* hist = dyn;
   uint32_t* cur = dyn + nbins;
   const int tid = threadIdx.x;
   for (uint32_t b = tid; b < nbins; b += kPartBlock) { hist[b] = 0; cur[b] = 0; }
   __syncthreads();
-  const uint32_t mask = nbins - 1;
-  for (uint64_t i = lo + tid; i < hi; i += kPartBlock) atomicAdd(&hist[bucket_of(P, P.ent3[i].hash) & mask], 1u);
+  for (uint64_t i = lo + tid; i < hi; i += kPartBlock) atomicAdd(&hist[bucket_of(P, P.ent3[i].hash) - b0], 1u);
   __syncthreads();
   // exclusive scan of the bins (nbins / kPartBlock consecutive bins per thread)
   const uint32_t per = (nbins + kPartBlock - 1) / kPartBlock;
@@ -684,7 +692,7 @@ __global__ __launch_bounds__(kPartBlock) void k_part2(BuildParams P) {
   for (uint32_t q = 0; q < per; q++) {
     const uint32_t b = tid * per + q;
     if (b < nbins) {
-      const uint64_t bucket = ((uint64_t)dpart << P.p2_bits) | b;
+      const uint64_t bucket = (uint64_t)b0 + b;
       if (bucket < P.nbuckets) {
         P.boff[bucket] = lo + run;
         P.bcount[bucket] = hist[b];
@@ -696,7 +704,7 @@ __global__ __launch_bounds__(kPartBlock) void k_part2(BuildParams P) {
   __syncthreads();
   for (uint64_t i = lo + tid; i < hi; i += kPartBlock) {
     const Entry en = P.ent3[i];
-    const uint32_t b = bucket_of(P, en.hash) & mask;
+    const uint32_t b = bucket_of(P, en.hash) - b0;
     P.ent2[lo + atomicAdd(&cur[b], 1u)] = en;
   }
 }
@@ -714,7 +722,8 @@ __global__ __launch_bounds__(kPlaceBlock) void k_place_lds(BuildParams P) {
   __shared__ uint16_t order[kPlaceLdsMax];
   __shared__ uint64_t sh64[kPlaceBlock];
   __shared__ int64_t shm[kPlaceBlock];
-  const uint64_t b = blockIdx.x;
+  if (build_aborted(P)) return;
+  const uint64_t b = P.b_lo + blockIdx.x;
   const uint64_t start = b << kBucketShift;
   const int64_t bsize = (int64_t)min((uint64_t)kBucket, P.cap - start);
   const uint32_t n = P.bcount[b];
@@ -784,7 +793,7 @@ __global__ __launch_bounds__(kPlaceBlock) void k_place_lds(BuildParams P) {
         aux[p] = (int32_t)j;
       } else {
         const Entry en = raw[order[j]];
-        write_slot(P, wrap_slot(start + (uint64_t)p, P.cap), en.hash, en.addr & ~kDelBit);
+        put_slot(P, wrap_slot(start + (uint64_t)p, P.cap), en.hash, en.addr & ~kDelBit);
       }
     }
   }
@@ -817,19 +826,27 @@ void launch_dense_slabs(const BuildParams& P, hipStream_t s) {
   hipLaunchKernelGGL(k_dense_slabs, dim3((unsigned)((P.nslabs + 255) / 256)), dim3(256), 0, s, P);
 }
 
-void launch_partition(const BuildParams& P, hipStream_t s, StageTimer* tm) {
+void launch_partition1(const BuildParams& P, hipStream_t s) {
   hipLaunchKernelGGL(k_part1_hist, dim3((unsigned)P.p1_tiles), dim3(kPartBlock), 0, s, P);
   scan_exclusive<uint32_t, uint64_t, OpAdd>(P.p1_hist, P.p1_off, (uint64_t)P.p1_tiles * 256, P.p1_off_total,
                                             OpAdd(), P.scan_scratch_u64, s);
   hipLaunchKernelGGL(k_part1_scatter, dim3((unsigned)P.p1_tiles), dim3(kPartBlock), 0, s, P);
-  hipLaunchKernelGGL(k_part2, dim3(256), dim3(kPartBlock), (size_t)(2u << P.p2_bits) * sizeof(uint32_t), s, P);
+}
+
+void launch_partition(const BuildParams& P, hipStream_t s, StageTimer* tm) {
+  launch_partition1(P, s);
+  hipLaunchKernelGGL(k_part2, dim3(256), dim3(kPartBlock), (size_t)(2u * P.bpp) * sizeof(uint32_t), s, P);
   tm->mark("partition", s);
+}
+
+void launch_place_buckets(const BuildParams& P, hipStream_t s) {
+  if (P.b_hi > P.b_lo) hipLaunchKernelGGL(k_place_lds, dim3((unsigned)(P.b_hi - P.b_lo)), dim3(kPlaceBlock), 0, s, P);
+  launch_place_global(P, s, 0, 1);  // buckets above kPlaceLdsMax entries (normally none)
 }
 
 void launch_place_fast(const BuildParams& P, hipStream_t s, StageTimer* tm) {
   launch_summary_carry(P, s, tm);
-  hipLaunchKernelGGL(k_place_lds, dim3((unsigned)P.nbuckets), dim3(kPlaceBlock), 0, s, P);
-  launch_place_global(P, s, 0, 1);  // buckets above kPlaceLdsMax entries (normally none)
+  launch_place_buckets(P, s);
   tm->mark("place", s);
   launch_verify(P, s, tm);
 }

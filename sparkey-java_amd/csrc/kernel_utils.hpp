@@ -13,11 +13,16 @@ namespace sk {
 // ------------------------------------------------------------------------------------------------
 // small device utilities
 // ------------------------------------------------------------------------------------------------
+// The framing wrote more records than the workspace holds: every later stage of this attempt is
+// skipped (its offsets would run past the buffers) and the host redoes the build with more room.
+__device__ __forceinline__ bool build_aborted(const BuildParams& P) {
+  return P.st->overflow != 0 || P.st->n_records > P.max_records;
+}
+
 __device__ __forceinline__ void set_error(Status* st, int64_t pos, int code) {
   atomicMin(&st->err, ((unsigned long long)pos << 8) | (unsigned long long)(-code));
 }
 
-__device__ __forceinline__ int64_t chunk_start(uint64_t k) { return k == 0 ? kLogHeaderSize : (int64_t)(k << kChunkShift); }
 __device__ __forceinline__ int64_t chunk_end(uint64_t k, int64_t data_end) {
   const int64_t e = (int64_t)((k + 1) << kChunkShift);
   return e < data_end ? e : data_end;
@@ -77,6 +82,24 @@ __device__ __forceinline__ void write_slot(const BuildParams& P, uint64_t slot, 
   } else {  // 4 + 8
     uint32_t* q = reinterpret_cast<uint32_t*>(p);
     q[0] = (uint32_t)hash; q[1] = (uint32_t)addr; q[2] = (uint32_t)(addr >> 32);
+  }
+}
+
+// Slot write of the placement kernels: in a sharded build a slot outside [slot_lo, slot_hi) goes
+// to the spill list for its owner.
+__device__ __forceinline__ void put_slot(const BuildParams& P, uint64_t slot, uint64_t hash, uint64_t addr) {
+  if (!P.sharded || (slot >= P.slot_lo && slot < P.slot_hi)) {
+    write_slot(P, slot, hash, addr);
+    return;
+  }
+  const unsigned long long i = atomicAdd(&P.st->n_spill, 1ull);
+  if (i < P.spill_cap) {
+    SpillEntry e;
+    e.slot = slot;
+    e.hash = hash;
+    e.addr = addr;
+    e.pad = 0;
+    P.spill[i] = e;
   }
 }
 

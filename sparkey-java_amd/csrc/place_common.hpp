@@ -151,7 +151,7 @@ __device__ inline void place_bucket_global(const BuildParams& P, uint64_t b, int
         slot_of[p] = (int32_t)j;
       } else {
         const Entry en = P.ent3[eoff + j];
-        write_slot(P, wrap_slot(start + (uint64_t)p, P.cap), en.hash, en.addr & ~kDelBit);
+        put_slot(P, wrap_slot(start + (uint64_t)p, P.cap), en.hash, en.addr & ~kDelBit);
       }
     }
   }

@@ -213,8 +213,25 @@ hipError_t grow(T** p, uint64_t& have, uint64_t want) {
 
 }  // namespace
 
+// Host state of a sharded build between its steps (sparkey_shard_*).
+struct ShardState {
+  bool active = false;
+  LogHdr lh;
+  IndexParams ip;
+  sparkey_build_opts opts;
+  int rank = 0, world = 1;
+  const uint8_t* log = nullptr;  // virtual base of global log position 0
+  uint64_t buf_lo = 0, buf_hi = 0;
+  uint64_t n_local = 0, n_recv = 0;
+  BuildParams P;        // placement over the rank's slot range
+  BuildParams P_frame;  // the rank's framing (entries in slabs)
+};
+
 struct sparkey_plan {
   int device = 0;
+  ShardState shard;
+  uint64_t c_small = 0;
+  uint64_t* small = nullptr;  // a few words of device scratch
   hipStream_t own_stream = nullptr;
   uint64_t c_conv = 0, c_exitp = 0, c_qpos = 0, c_tail = 0, c_G = 0, c_cnt = 0, c_off = 0;
   uint64_t c_ent = 0, c_ent2 = 0, c_ent3 = 0;
@@ -316,6 +333,134 @@ static int status_error(const Status& st, char* err, size_t err_len) {
   return code;
 }
 
+// Geometry of one build over the log bytes a device buffer holds.  `log` is the (virtual) base
+// pointer of global log position 0, `log_len` the end of the bytes it holds; records are framed
+// from `entry` while they start below `frame_end`.
+static int setup_params(const LogHdr& lh, const IndexParams& ip, const sparkey_build_opts& o, const uint8_t* log,
+                        uint64_t log_len, int64_t entry, int64_t frame_end, BuildParams* Pp, char* err,
+                        size_t err_len) {
+  BuildParams& P = *Pp;
+  memset(&P, 0, sizeof(P));
+  P.log = log;
+  P.log_len = log_len;
+  P.data_end = frame_end;
+  P.max_key_len = lh.max_key_len;
+  P.max_value_len = lh.max_value_len;
+  {
+    const int64_t put_len = vlq_size_long(lh.max_key_len + 1) + vlq_size_long(lh.max_value_len) + lh.max_key_len +
+                            lh.max_value_len;
+    const int64_t del_len = 1 + vlq_size_long(lh.max_key_len) + lh.max_key_len;
+    P.max_rec_len = std::max<int64_t>(1, std::max(put_len, del_len));
+  }
+  const bool any = frame_end > entry;
+  P.fr_entry = entry;
+  P.ch_k0 = (uint64_t)entry >> kChunkShift;
+  P.nchunks = any ? (uint64_t)((frame_end + kChunk - 1) / kChunk) - P.ch_k0 : 0;
+  // k_frame geometry: chunk C = max(128, nextpow2(maxRecLen)) so every chunk but a short last one
+  // holds a record start; 8 KiB of chunks per wave, staged contiguously with max(C, 256) bytes of
+  // look-ahead (about 10 KiB of LDS: 16 waves per CU); records longer than 4 KiB -> serial framing.
+  {
+    int cs = 7;
+    while ((1ll << cs) < P.max_rec_len) cs++;
+    const int64_t C = 1ll << cs;
+    P.fr_cshift = cs;
+    P.fr_w = (int32_t)std::max<int64_t>(1, std::min<int64_t>(64, 8192 / C));
+    P.fr_look = (int32_t)std::max<int64_t>(C, 256);
+    P.fr_rgn_bytes = (int32_t)(((int64_t)P.fr_w * C + P.fr_look + 16 + 255) & ~255LL);
+    P.fr_mask_words = (int32_t)((std::min<int64_t>(C, P.max_rec_len) + 63) / 64);
+    P.fr_fast = lh.max_key_len + 1 < 128 && lh.max_value_len < 128;
+    P.no_deletes = lh.num_deletes == 0;
+    P.fr_k0 = (uint64_t)entry >> cs;
+    P.fr_nchunks = any ? (uint64_t)((frame_end + C - 1) / C) - P.fr_k0 : 0;
+  }
+  P.emit_extra = lh.max_key_len + 32 <= kEmitExtra ? (int32_t)((lh.max_key_len + 32 + 15) & ~15LL) : 32;
+  P.hash_size = ip.hash_size;
+  P.addr_size = ip.addr_size;
+  P.slot_size = ip.slot_size;
+  P.ebb = ip.ebb;
+  P.seed = o.hash_seed;
+  P.mod = make_fastmod(ip.cap);
+  P.cap = ip.cap;
+  P.nbuckets = (ip.cap + kBucket - 1) / kBucket;
+  P.bpp = (uint32_t)std::max<uint64_t>(1, (P.nbuckets + 255) / 256);
+  if (P.bpp > (1u << kPart2MaxBits)) {
+    set_err(err, err_len, "hash capacity too large for one device: " + std::to_string(ip.cap));
+    return SPARKEY_E_UNSUPPORTED;
+  }
+  P.dmagic = ((1ull << 40) + P.bpp - 1) / P.bpp;
+  P.b_lo = 0;
+  P.b_hi = P.nbuckets;
+  P.slot_lo = 0;
+  P.slot_hi = ip.cap;
+  return SPARKEY_OK;
+}
+
+// Slab layout of the framing output and the workspace it needs (grown on demand).
+static int reserve_for_framing(sparkey_plan* pl, BuildParams& P, int framing_path, uint64_t nrec, uint32_t slab_cap,
+                               char* err, size_t err_len) {
+  const uint64_t nwaves = P.fr_nchunks ? (P.fr_nchunks + P.fr_w - 1) / P.fr_w : 0;
+  if (framing_path == 0) {
+    P.slab_cap = slab_cap;
+    P.nslabs = nwaves;
+  } else {  // dense entries from the serial framing path, seen as slabs of kPartTile
+    P.slab_cap = kPartTile;
+    P.nslabs = (std::max<uint64_t>(nrec, 1) + kPartTile - 1) / kPartTile;
+  }
+  P.part_group = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(kMaxPartGroup, kPartTile / P.slab_cap));
+  P.p1_tiles = (uint32_t)std::max<uint64_t>(1, (P.nslabs + P.part_group - 1) / P.part_group);
+  const uint64_t ent_cap = std::max<uint64_t>(1, P.nslabs * P.slab_cap);
+  int rc = plan_reserve(pl, std::max<uint64_t>(P.nchunks, nwaves), std::max<uint64_t>(nrec, 1), ent_cap, P.nslabs,
+                        P.p1_tiles, P.nbuckets, P.cap, err, err_len);
+  if (rc) return rc;
+  P.conv = pl->conv; P.exitp = pl->exitp; P.qpos = pl->qpos; P.tail = pl->tail; P.G = pl->G;
+  P.cnt = pl->cnt; P.off = pl->off;
+  P.ent = pl->ent; P.ent2 = pl->ent2; P.ent3 = pl->ent3; P.max_records = pl->c_ent2;
+  P.ent_cap = std::min<uint64_t>(pl->c_ent, P.nslabs * P.slab_cap);
+  P.wcount = pl->wcount; P.woff = pl->woff;
+  P.bcount = pl->bcount; P.bcursor = pl->bcursor; P.boff = pl->boff; P.bfun = pl->bfun; P.bpre = pl->bpre;
+  P.bfun_total = pl->bfun_total; P.carry = pl->carry; P.pairs = pl->pairs; P.pair_cap = pl->c_pairs / 2;
+  P.parts = pl->parts; P.scan_scratch_u64 = pl->scan_u64; P.scan_scratch_mp = pl->scan_mp;
+  P.exit_desc = pl->desc; P.cnt_desc = pl->desc + nwaves;
+  P.p1_hist = pl->p1_hist; P.p1_off = pl->p1_off; P.p1_off_total = pl->p1_off + 256ull * P.p1_tiles;
+  return SPARKEY_OK;
+}
+
+// Framing + hashing launches (entries into the slabs), after the status block was reset.
+static int launch_framing(sparkey_plan* pl, const BuildParams& P, int framing_path, hipStream_t s, char* err,
+                          size_t err_len) {
+  const uint64_t nwaves = P.fr_nchunks ? (P.fr_nchunks + P.fr_w - 1) / P.fr_w : 0;
+  if (framing_path == 0) {
+    HIP_TRY(hipMemsetAsync(pl->desc, 0, (2 * nwaves + 2) * sizeof(unsigned long long), s));
+    HIP_TRY(hipMemsetAsync(pl->wcount, 0, (P.nslabs + 1) * sizeof(uint32_t), s));
+    launch_frame_fused(P, s, &pl->timer);
+  } else {
+    launch_framing_serial(P, s);
+    launch_emit(P, s, &pl->timer);
+    launch_dense_slabs(P, s);
+  }
+  return SPARKEY_OK;
+}
+
+static void print_frame_debug(sparkey_plan* pl, const BuildParams& P) {
+  if (!P.dbg || !P.fr_nchunks) return;
+  const uint64_t nwv = (P.fr_nchunks + P.fr_w - 1) / P.fr_w;
+  std::vector<unsigned long long> h(16 * nwv);
+  if (hipMemcpy(h.data(), pl->dbg, h.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return;
+  double sum[16] = {0};
+  unsigned long long mx[16] = {0};
+  for (uint64_t c = 0; c < nwv; c++)
+    for (int i = 0; i < 16; i++) {
+      sum[i] += (double)h[c * 16 + i];
+      mx[i] = std::max(mx[i], h[c * 16 + i]);
+    }
+  const double n = (double)nwv;
+  fprintf(stderr, "[k_frame] waves=%llu C=%d W=%d mean cycles: stage %.0f screen %.0f walk %.0f entry %.0f "
+          "counts %.0f slab %.0f hash %.0f | max entry %llu | walk iters %.1f survivors/wave %.1f unconverged/wave "
+          "%.2f\n",
+          (unsigned long long)nwv, 1 << P.fr_cshift, P.fr_w, sum[0] / n, sum[1] / n, sum[2] / n, sum[3] / n,
+          sum[4] / n, sum[5] / n, sum[6] / n, mx[3], sum[8] / n, sum[9] / n, sum[10] / n);
+}
+
 static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t* d_log, uint64_t log_len,
                       uint8_t* d_out, uint64_t index_cap, const sparkey_build_opts* opts, hipStream_t s,
                       sparkey_build_stats* stats_out, char* err, size_t err_len) {
@@ -341,56 +486,12 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
   if (!s) s = pl->own_stream;
 
   BuildParams P;
-  memset(&P, 0, sizeof(P));
-  P.log = d_log;
-  P.log_len = log_len;
-  P.data_end = lh.data_end;
-  P.max_key_len = lh.max_key_len;
-  P.max_value_len = lh.max_value_len;
-  {
-    const int64_t put_len = vlq_size_long(lh.max_key_len + 1) + vlq_size_long(lh.max_value_len) + lh.max_key_len +
-                            lh.max_value_len;
-    const int64_t del_len = 1 + vlq_size_long(lh.max_key_len) + lh.max_key_len;
-    P.max_rec_len = std::max<int64_t>(1, std::max(put_len, del_len));
-  }
-  P.nchunks = lh.data_end > kLogHeaderSize ? (uint64_t)((lh.data_end + kChunk - 1) / kChunk) : 0;
-  // k_frame geometry: chunk C = max(128, nextpow2(maxRecLen)) so every chunk but a short last one
-  // holds a record start; 8 KiB of chunks per wave, staged contiguously with max(C, 256) bytes of
-  // look-ahead (about 10 KiB of LDS: 16 waves per CU); records longer than 4 KiB -> serial framing.
-  const bool fused_framing = P.max_rec_len <= 4096;
-  {
-    int cs = 7;
-    while ((1ll << cs) < P.max_rec_len) cs++;
-    const int64_t C = 1ll << cs;
-    P.fr_cshift = cs;
-    P.fr_w = (int32_t)std::max<int64_t>(1, std::min<int64_t>(64, 8192 / C));
-    P.fr_look = (int32_t)std::max<int64_t>(C, 256);
-    P.fr_rgn_bytes = (int32_t)(((int64_t)P.fr_w * C + P.fr_look + 16 + 255) & ~255LL);
-    P.fr_mask_words = (int32_t)((std::min<int64_t>(C, P.max_rec_len) + 63) / 64);
-    P.fr_fast = lh.max_key_len + 1 < 128 && lh.max_value_len < 128;
-    P.no_deletes = lh.num_deletes == 0;
-    P.fr_nchunks = lh.data_end > kLogHeaderSize ? (uint64_t)((lh.data_end + C - 1) / C) : 0;
-  }
-  P.emit_extra = lh.max_key_len + 32 <= kEmitExtra ? (int32_t)((lh.max_key_len + 32 + 15) & ~15LL) : 32;
-  P.hash_size = ip.hash_size;
-  P.addr_size = ip.addr_size;
-  P.slot_size = ip.slot_size;
-  P.ebb = ip.ebb;
-  P.seed = opts->hash_seed;
-  P.mod = make_fastmod(ip.cap);
-  P.cap = ip.cap;
-  P.nbuckets = (ip.cap + kBucket - 1) / kBucket;
-  {
-    int nb_bits = 0;
-    while ((1ull << nb_bits) < P.nbuckets) nb_bits++;
-    P.p2_bits = std::max(0, nb_bits - 8);
-    if (P.p2_bits > kPart2MaxBits) {
-      set_err(err, err_len, "hash capacity too large for one device: " + std::to_string(ip.cap));
-      return SPARKEY_E_UNSUPPORTED;
-    }
-  }
+  rc = setup_params(lh, ip, *opts, d_log, log_len, kLogHeaderSize, std::max<int64_t>(lh.data_end, kLogHeaderSize),
+                    &P, err, err_len);
+  if (rc) return rc;
   P.out = d_out;
   P.st = pl->d_status;
+  const bool fused_framing = P.max_rec_len <= 4096;
 
   uint64_t nrec = (uint64_t)std::max<int64_t>(0, lh.num_puts) + (uint64_t)std::max<int64_t>(0, lh.num_deletes);
   uint8_t hdr[kIndexHeaderSize];
@@ -405,31 +506,8 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
   uint32_t slab_cap = (uint32_t)std::min<uint64_t>(
       kPartTile, std::max<uint64_t>(64, 2 * ((nrec + std::max<uint64_t>(nwaves, 1) - 1) / std::max<uint64_t>(nwaves, 1)) + 32));
   for (int attempt = 0; attempt < 4; attempt++) {
-    uint64_t ent_cap;
-    if (framing_path == 0) {
-      P.slab_cap = slab_cap;
-      P.nslabs = nwaves;
-      ent_cap = std::max<uint64_t>(1, nwaves * slab_cap);
-    } else {  // dense entries from the serial framing path, seen as slabs of kPartTile
-      P.slab_cap = kPartTile;
-      ent_cap = std::max<uint64_t>(nrec, 1);
-      P.nslabs = (ent_cap + kPartTile - 1) / kPartTile;
-    }
-    P.part_group = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(kMaxPartGroup, kPartTile / P.slab_cap));
-    P.p1_tiles = (uint32_t)std::max<uint64_t>(1, (P.nslabs + P.part_group - 1) / P.part_group);
-    rc = plan_reserve(pl, P.nchunks, std::max<uint64_t>(nrec, 1), ent_cap, P.nslabs, P.p1_tiles, P.nbuckets, ip.cap,
-                      err, err_len);
+    rc = reserve_for_framing(pl, P, framing_path, nrec, slab_cap, err, err_len);
     if (rc) return rc;
-    P.conv = pl->conv; P.exitp = pl->exitp; P.qpos = pl->qpos; P.tail = pl->tail; P.G = pl->G;
-    P.cnt = pl->cnt; P.off = pl->off;
-    P.ent = pl->ent; P.ent2 = pl->ent2; P.ent3 = pl->ent3; P.max_records = pl->c_ent2;
-    P.ent_cap = std::min<uint64_t>(pl->c_ent, P.nslabs * P.slab_cap);
-    P.wcount = pl->wcount; P.woff = pl->woff;
-    P.bcount = pl->bcount; P.bcursor = pl->bcursor; P.boff = pl->boff; P.bfun = pl->bfun; P.bpre = pl->bpre;
-    P.bfun_total = pl->bfun_total; P.carry = pl->carry; P.pairs = pl->pairs; P.pair_cap = pl->c_pairs / 2;
-    P.parts = pl->parts; P.scan_scratch_u64 = pl->scan_u64; P.scan_scratch_mp = pl->scan_mp;
-    P.exit_desc = pl->desc; P.cnt_desc = pl->desc + nwaves;
-    P.p1_hist = pl->p1_hist; P.p1_off = pl->p1_off; P.p1_off_total = pl->p1_off + 256ull * P.p1_tiles;
     if (getenv("SPARKEY_FRAME_DEBUG")) {
       HIP_TRY(grow(&pl->dbg, pl->c_dbg, 16 * std::max<uint64_t>(P.nchunks, 1)));
       HIP_TRY(hipMemsetAsync(pl->dbg, 0, 16 * P.nchunks * sizeof(unsigned long long), s));
@@ -443,15 +521,8 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
     pl->timer.begin(s);
     HIP_TRY(hipMemcpyAsync(d_out, hdr, kIndexHeaderSize, hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemcpyAsync(pl->d_status, &init, sizeof(Status), hipMemcpyHostToDevice, s));
-    if (framing_path == 0) {
-      HIP_TRY(hipMemsetAsync(pl->desc, 0, (2 * nwaves + 2) * sizeof(unsigned long long), s));
-      HIP_TRY(hipMemsetAsync(pl->wcount, 0, (P.nslabs + 1) * sizeof(uint32_t), s));
-      launch_frame_fused(P, s, &pl->timer);
-    } else {
-      launch_framing_serial(P, s);
-      launch_emit(P, s, &pl->timer);
-      launch_dense_slabs(P, s);
-    }
+    rc = launch_framing(pl, P, framing_path, s, err, err_len);
+    if (rc) return rc;
     launch_partition(P, s, &pl->timer);
     launch_place_fast(P, s, &pl->timer);
     launch_stats(P, s, 0, &pl->timer);
@@ -460,26 +531,7 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
     HIP_TRY(hipMemcpyAsync(pl->h_status, pl->d_status, sizeof(Status), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     HIP_TRY(hipEventElapsedTime(&ms, pl->ev0, pl->ev1));
-    if (P.dbg && P.fr_nchunks) {
-      const uint64_t nwv = (P.fr_nchunks + P.fr_w - 1) / P.fr_w;
-      std::vector<unsigned long long> h(16 * nwv);
-      if (hipMemcpy(h.data(), pl->dbg, h.size() * 8, hipMemcpyDeviceToHost) == hipSuccess) {
-        double sum[16] = {0};
-        unsigned long long mx[16] = {0};
-        for (uint64_t c = 0; c < nwv; c++)
-          for (int i = 0; i < 16; i++) {
-            sum[i] += (double)h[c * 16 + i];
-            mx[i] = std::max(mx[i], h[c * 16 + i]);
-          }
-        const double n = (double)nwv;
-        fprintf(stderr, "[k_frame] waves=%llu C=%d W=%d mean cycles: stage %.0f screen %.0f walk %.0f entry %.0f "
-                "counts %.0f lookback %.0f hash %.0f | max entry %llu max lookback %llu | walk iters %.1f survivors/wave "
-                "%.1f unconverged/wave %.2f | lookback spins %.1f windows %.2f distance %.1f\n",
-                (unsigned long long)nwv, 1 << P.fr_cshift, P.fr_w, sum[0] / n, sum[1] / n, sum[2] / n, sum[3] / n,
-                sum[4] / n, sum[5] / n, sum[6] / n, mx[3], mx[5], sum[8] / n, sum[9] / n, sum[10] / n, sum[11] / n, sum[12] / n,
-                sum[13] / n);
-      }
-    }
+    print_frame_debug(pl, P);
     if (framing_path == 0 && st.max_wave_count > slab_cap) {  // a wave overflowed its slab
       slab_cap = (uint32_t)std::min<uint64_t>(kPartTile, ((uint64_t)st.max_wave_count + 63) & ~63ull);
       continue;
@@ -544,8 +596,10 @@ int sparkey_plan_create(sparkey_plan** plan_out, int32_t device, uint64_t max_lo
   if (!plan_out) return SPARKEY_E_ARG;
   *plan_out = nullptr;
   int ndev = 0;
-  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= device || device < 0) {
-    set_err(err, err_len, "no HIP device " + std::to_string(device));
+  const hipError_t e = hipGetDeviceCount(&ndev);
+  if (e != hipSuccess || ndev <= device || device < 0) {
+    set_err(err, err_len, "no HIP device " + std::to_string(device) + " (" + hipGetErrorString(e) + ", " +
+                              std::to_string(ndev) + " devices)");
     return SPARKEY_E_GPU;
   }
   HIP_TRY(hipSetDevice(device));
@@ -605,7 +659,7 @@ void sparkey_plan_destroy(sparkey_plan* pl) {
   (void)hipSetDevice(pl->device);
   void* bufs[] = {pl->conv, pl->exitp, pl->qpos, pl->tail, pl->G, pl->cnt, pl->off, pl->ent, pl->ent2, pl->ent3,
                   pl->bcount, pl->bcursor, pl->boff, pl->bfun, pl->bpre, pl->bfun_total, pl->carry, pl->pairs,
-                  pl->parts, pl->scan_u64, pl->scan_mp, pl->desc, pl->p1_hist, pl->p1_off, pl->d_status, pl->dbg, pl->wcount, pl->woff};
+                  pl->parts, pl->scan_u64, pl->scan_mp, pl->desc, pl->p1_hist, pl->p1_off, pl->d_status, pl->dbg, pl->wcount, pl->woff, pl->small};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (pl->h_status) (void)hipHostFree(pl->h_status);
@@ -754,6 +808,421 @@ int sparkey_build_index_file(const char* log_path, const char* index_out_path, c
   }
   (void)hipHostFree(hidx);
   return rc;
+}
+
+}  // extern "C"
+
+// ================================================================================================
+// Sharded build steps.  The host orchestrator (sparkey/sharded.py) calls these in
+// order on every rank and does the collectives between them.
+// ================================================================================================
+static int shard_check(sparkey_plan* pl, char* err, size_t err_len) {
+  if (!pl || !pl->shard.active) {
+    set_err(err, err_len, "sparkey_shard_begin was not called on this plan");
+    return SPARKEY_E_ARG;
+  }
+  return SPARKEY_OK;
+}
+
+static int shard_sync_status(sparkey_plan* pl, hipStream_t s, char* err, size_t err_len) {
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(pl->h_status, pl->d_status, sizeof(Status), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  return SPARKEY_OK;
+}
+
+// the nd = ceil(nbuckets / bpp) coarse digits in use split evenly: rank r owns digits
+// [nd r / world, nd (r + 1) / world) -> buckets -> slots
+static uint64_t used_digits(const BuildParams& P) { return (P.nbuckets + P.bpp - 1) / P.bpp; }
+static void shard_range(const BuildParams& P, int rank, int world, uint64_t* b_lo, uint64_t* b_hi, uint64_t* s_lo,
+                        uint64_t* s_hi) {
+  const uint64_t nd = used_digits(P);
+  const uint64_t d0 = (nd * (uint64_t)rank) / (uint64_t)world;
+  const uint64_t d1 = (nd * (uint64_t)(rank + 1)) / (uint64_t)world;
+  *b_lo = std::min<uint64_t>(P.nbuckets, d0 * P.bpp);
+  *b_hi = std::min<uint64_t>(P.nbuckets, d1 * P.bpp);
+  *s_lo = std::min<uint64_t>(P.cap, *b_lo << kBucketShift);
+  *s_hi = std::min<uint64_t>(P.cap, *b_hi << kBucketShift);
+}
+
+extern "C" {
+
+int sparkey_shard_begin(sparkey_plan* pl, const uint8_t* log_header, uint64_t file_len, const uint8_t* d_buf,
+                        uint64_t buf_lo, uint64_t buf_hi, const sparkey_build_opts* opts, int32_t rank, int32_t world,
+                        char* err, size_t err_len) {
+  if (!pl || !log_header || !opts || world < 1 || rank < 0 || rank >= world || world > 256 || buf_hi < buf_lo ||
+      buf_hi > file_len) {
+    set_err(err, err_len, "bad shard arguments");
+    return SPARKEY_E_ARG;
+  }
+  if (((uintptr_t)d_buf & 15) || (buf_lo & 15)) {
+    set_err(err, err_len, "shard buffer and buf_lo must be 16-byte aligned");
+    return SPARKEY_E_ARG;
+  }
+  ShardState& sh = pl->shard;
+  sh.active = false;
+  int rc = parse_log_header(log_header, 84, file_len, &sh.lh, err, err_len);
+  if (rc) return rc;
+  rc = make_index_params(sh.lh, *opts, &sh.ip, err, err_len);
+  if (rc) return rc;
+  HIP_TRY(hipSetDevice(pl->device));
+  sh.opts = *opts;
+  sh.rank = rank;
+  sh.world = world;
+  sh.log = d_buf - buf_lo;  // virtual base: global log position p is at log[p] for p in [buf_lo, buf_hi)
+  sh.buf_lo = buf_lo;
+  sh.buf_hi = buf_hi;
+  sh.n_local = 0;
+  sh.n_recv = 0;
+  rc = setup_params(sh.lh, sh.ip, *opts, sh.log, buf_hi, kLogHeaderSize, kLogHeaderSize, &sh.P, err, err_len);
+  if (rc) return rc;
+  sh.P.st = pl->d_status;
+  sh.P.sharded = 1;
+  shard_range(sh.P, rank, world, &sh.P.b_lo, &sh.P.b_hi, &sh.P.slot_lo, &sh.P.slot_hi);
+  HIP_TRY(grow(&pl->small, pl->c_small, 512));
+  sh.active = true;
+  return SPARKEY_OK;
+}
+
+int sparkey_shard_slot_range(const sparkey_plan* pl, int32_t rank, uint64_t* slot_lo, uint64_t* slot_hi) {
+  if (!pl || !pl->shard.active || rank < 0 || rank >= pl->shard.world) return SPARKEY_E_ARG;
+  uint64_t b0, b1;
+  shard_range(pl->shard.P, rank, pl->shard.world, &b0, &b1, slot_lo, slot_hi);
+  return SPARKEY_OK;
+}
+
+int64_t sparkey_shard_max_record_len(const sparkey_plan* pl) {
+  return pl && pl->shard.active ? pl->shard.P.max_rec_len : SPARKEY_E_ARG;
+}
+
+int sparkey_shard_find_entry(sparkey_plan* pl, uint64_t lo, uint64_t window, void* stream, int64_t* entry_out,
+                             char* err, size_t err_len) {
+  int rc = shard_check(pl, err, err_len);
+  if (rc) return rc;
+  ShardState& sh = pl->shard;
+  hipStream_t s = stream ? (hipStream_t)stream : pl->own_stream;
+  const int64_t data_end = std::max<int64_t>(sh.lh.data_end, kLogHeaderSize);
+  const int64_t L = sh.P.max_rec_len;
+  const int64_t cand_end = std::min<int64_t>((int64_t)lo + L, data_end);
+  const int64_t target = std::min<int64_t>((int64_t)lo + L + (int64_t)window, data_end);
+  if ((int64_t)lo >= data_end) {
+    *entry_out = data_end;
+    return SPARKEY_OK;
+  }
+  if ((int64_t)lo < (int64_t)sh.buf_lo || (target + 16 > (int64_t)sh.buf_hi && (int64_t)sh.buf_hi < data_end)) {
+    set_err(err, err_len, "entry window outside the shard buffer");
+    return SPARKEY_E_ARG;
+  }
+  BuildParams P = sh.P;
+  P.data_end = data_end;
+  launch_find_entry(P, s, (int64_t)lo, cand_end, target, (int64_t*)pl->small);
+  HIP_TRY(hipGetLastError());
+  int64_t v = -1;
+  HIP_TRY(hipMemcpyAsync(&v, pl->small, sizeof(v), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  *entry_out = v;
+  return SPARKEY_OK;
+}
+
+int sparkey_shard_frame(sparkey_plan* pl, int64_t entry, int64_t frame_end, void* stream,
+                        sparkey_shard_frame_result* res, char* err, size_t err_len) {
+  int rc = shard_check(pl, err, err_len);
+  if (rc) return rc;
+  ShardState& sh = pl->shard;
+  hipStream_t s = stream ? (hipStream_t)stream : pl->own_stream;
+  const int64_t data_end = std::max<int64_t>(sh.lh.data_end, kLogHeaderSize);
+  frame_end = std::min<int64_t>(frame_end, data_end);
+  memset(res, 0, sizeof(*res));
+  res->exit = entry;
+  sh.n_local = 0;
+  if (entry < kLogHeaderSize || entry > data_end) {
+    set_err(err, err_len, "shard entry outside the log data");
+    return SPARKEY_E_ARG;
+  }
+  if (entry >= frame_end) return SPARKEY_OK;  // owns no record
+  if (entry < (int64_t)sh.buf_lo || ((uint64_t)frame_end > sh.buf_hi && sh.buf_hi < (uint64_t)data_end)) {
+    set_err(err, err_len, "shard frame range outside the shard buffer");
+    return SPARKEY_E_ARG;
+  }
+  BuildParams P;
+  rc = setup_params(sh.lh, sh.ip, sh.opts, sh.log, sh.buf_hi, entry, frame_end, &P, err, err_len);
+  if (rc) return rc;
+  P.st = pl->d_status;
+  P.sharded = 1;
+  P.b_lo = sh.P.b_lo; P.b_hi = sh.P.b_hi; P.slot_lo = sh.P.slot_lo; P.slot_hi = sh.P.slot_hi;
+  const bool fused = P.max_rec_len <= 4096;
+  const double frac = (double)(frame_end - entry) / (double)std::max<int64_t>(1, data_end - kLogHeaderSize);
+  uint64_t nrec = (uint64_t)((double)(std::max<int64_t>(0, sh.lh.num_puts) + std::max<int64_t>(0, sh.lh.num_deletes)) *
+                             frac * 1.05) + 4096;
+  int framing_path = fused ? 0 : 1;
+  const uint64_t nwaves = P.fr_nchunks ? (P.fr_nchunks + P.fr_w - 1) / P.fr_w : 0;
+  uint32_t slab_cap = (uint32_t)std::min<uint64_t>(
+      kPartTile, std::max<uint64_t>(64, 2 * ((nrec + std::max<uint64_t>(nwaves, 1) - 1) / std::max<uint64_t>(nwaves, 1)) + 32));
+  Status& st = *pl->h_status;
+  for (int attempt = 0; attempt < 5; attempt++) {
+    rc = reserve_for_framing(pl, P, framing_path, nrec, slab_cap, err, err_len);
+    if (rc) return rc;
+    Status init;
+    memset(&init, 0, sizeof(init));
+    init.err = ~0ull;
+    init.exit = -1;
+    HIP_TRY(hipMemcpyAsync(pl->d_status, &init, sizeof(Status), hipMemcpyHostToDevice, s));
+    rc = launch_framing(pl, P, framing_path, s, err, err_len);
+    if (rc) return rc;
+    rc = shard_sync_status(pl, s, err, err_len);
+    if (rc) return rc;
+    if (framing_path == 0 && st.max_wave_count > slab_cap) {
+      slab_cap = (uint32_t)std::min<uint64_t>(kPartTile, ((uint64_t)st.max_wave_count + 63) & ~63ull);
+      continue;
+    }
+    if (st.overflow || st.n_records > P.max_records) {
+      nrec = std::max<uint64_t>(st.n_records, nrec * 2 + 1);
+      continue;
+    }
+    if (framing_path == 0 && (st.spec_fail || st.err != ~0ull)) {
+      framing_path = 1;
+      continue;
+    }
+    break;
+  }
+  res->framing_path = framing_path;
+  if (st.err != ~0ull) {  // an invalid record on this chain: final only once the entry is verified
+    res->rc = -(int)(st.err & 0xff);
+    res->err_pos = (int64_t)(st.err >> 8);
+    return SPARKEY_OK;
+  }
+  if (st.overflow || st.spec_fail) {
+    set_err(err, err_len, "Corrupt log file: framing did not converge");
+    return SPARKEY_E_CORRUPT_LOG;
+  }
+  res->exit = std::min<int64_t>(st.exit, data_end);
+  res->num_records = (int64_t)st.n_records;
+  res->num_deletes = (int64_t)st.n_deletes;
+  sh.P_frame = P;
+  sh.n_local = st.n_records;
+  return SPARKEY_OK;
+}
+
+int sparkey_shard_bin(sparkey_plan* pl, uint8_t* d_send, uint64_t send_cap, void* stream, uint64_t* counts,
+                      char* err, size_t err_len) {
+  int rc = shard_check(pl, err, err_len);
+  if (rc) return rc;
+  ShardState& sh = pl->shard;
+  hipStream_t s = stream ? (hipStream_t)stream : pl->own_stream;
+  for (int r = 0; r < sh.world; r++) counts[r] = 0;
+  if (sh.n_local == 0) return SPARKEY_OK;
+  if (send_cap < sh.n_local || ((uintptr_t)d_send & 15)) {
+    set_err(err, err_len, "send buffer too small or misaligned: need " + std::to_string(sh.n_local) + " entries");
+    return SPARKEY_E_BUFFER;
+  }
+  BuildParams P = sh.P_frame;
+  P.ent3 = reinterpret_cast<Entry*>(d_send);
+  P.max_records = send_cap;
+  launch_partition1(P, s);
+  launch_dest_counts(P, s, sh.world, (uint32_t)used_digits(P), (uint64_t*)pl->small);
+  HIP_TRY(hipGetLastError());
+  std::vector<uint64_t> off(sh.world + 1);
+  HIP_TRY(hipMemcpyAsync(off.data(), pl->small, (sh.world + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  for (int r = 0; r < sh.world; r++) counts[r] = off[r + 1] - off[r];
+  return SPARKEY_OK;
+}
+
+int sparkey_shard_summarize(sparkey_plan* pl, const uint8_t* d_recv, uint64_t n_recv, void* stream, int64_t* fun_out,
+                            char* err, size_t err_len) {
+  int rc = shard_check(pl, err, err_len);
+  if (rc) return rc;
+  ShardState& sh = pl->shard;
+  hipStream_t s = stream ? (hipStream_t)stream : pl->own_stream;
+  if ((uintptr_t)d_recv & 15) {
+    set_err(err, err_len, "receive buffer must be 16-byte aligned");
+    return SPARKEY_E_ARG;
+  }
+  BuildParams& P = sh.P;
+  P.slab_cap = kPartTile;
+  P.nslabs = (std::max<uint64_t>(n_recv, 1) + kPartTile - 1) / kPartTile;
+  P.part_group = 1;
+  P.p1_tiles = (uint32_t)P.nslabs;
+  rc = plan_reserve(pl, 1, std::max<uint64_t>(n_recv, 1), 1, P.nslabs, P.p1_tiles, P.nbuckets, P.cap, err, err_len);
+  if (rc) return rc;
+  P.ent = const_cast<Entry*>(reinterpret_cast<const Entry*>(d_recv));
+  P.ent_cap = n_recv;
+  P.ent2 = pl->ent2; P.ent3 = pl->ent3; P.max_records = pl->c_ent2;
+  P.wcount = pl->wcount; P.woff = pl->woff;
+  P.bcount = pl->bcount; P.bcursor = pl->bcursor; P.boff = pl->boff; P.bfun = pl->bfun; P.bpre = pl->bpre;
+  P.bfun_total = pl->bfun_total; P.carry = pl->carry; P.pairs = pl->pairs; P.pair_cap = pl->c_pairs / 2;
+  P.parts = pl->parts; P.scan_scratch_u64 = pl->scan_u64; P.scan_scratch_mp = pl->scan_mp;
+  P.p1_hist = pl->p1_hist; P.p1_off = pl->p1_off; P.p1_off_total = pl->p1_off + 256ull * P.p1_tiles;
+  P.st = pl->d_status;
+  sh.n_recv = n_recv;
+  Status init;
+  memset(&init, 0, sizeof(init));
+  init.err = ~0ull;
+  init.n_records = n_recv;
+  HIP_TRY(hipMemcpyAsync(pl->d_status, &init, sizeof(Status), hipMemcpyHostToDevice, s));
+  launch_dense_slabs(P, s);
+  launch_partition(P, s, &pl->timer);
+  fun_out[0] = 0;  // identity carry function f(x) = max(0, x + 0) for an empty range
+  fun_out[1] = 0;
+  if (P.b_hi > P.b_lo) {
+    launch_summary_carry(P, s, &pl->timer);
+    HIP_TRY(hipGetLastError());
+    MaxPlus f;
+    HIP_TRY(hipMemcpyAsync(&f, P.bfun_total, sizeof(f), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    fun_out[0] = f.c;
+    fun_out[1] = f.a;
+  } else {
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(s));
+  }
+  return SPARKEY_OK;
+}
+
+int sparkey_shard_place(sparkey_plan* pl, int64_t carry_in, uint8_t* d_slots, uint8_t* d_spill, uint64_t spill_cap,
+                        void* stream, sparkey_shard_place_result* res, char* err, size_t err_len) {
+  int rc = shard_check(pl, err, err_len);
+  if (rc) return rc;
+  ShardState& sh = pl->shard;
+  hipStream_t s = stream ? (hipStream_t)stream : pl->own_stream;
+  BuildParams& P = sh.P;
+  if (((uintptr_t)d_slots & 3) || ((uintptr_t)d_spill & 15)) {
+    set_err(err, err_len, "slot or spill buffer misaligned");
+    return SPARKEY_E_ARG;
+  }
+  P.out = d_slots - kIndexHeaderSize - P.slot_lo * (uint64_t)P.slot_size;  // virtual .spi base
+  P.carry_in = carry_in;
+  P.spill = reinterpret_cast<SpillEntry*>(d_spill);
+  P.spill_cap = spill_cap;
+  HIP_TRY(hipMemsetAsync(&pl->d_status->n_pairs, 0, sizeof(unsigned long long), s));
+  HIP_TRY(hipMemsetAsync(&pl->d_status->n_spill, 0, sizeof(unsigned long long), s));
+  HIP_TRY(hipMemsetAsync(&pl->d_status->dup_overflow, 0, sizeof(unsigned int), s));
+  launch_carry(P, s);
+  launch_place_buckets(P, s);
+  rc = shard_sync_status(pl, s, err, err_len);
+  if (rc) return rc;
+  const Status& st = *pl->h_status;
+  memset(res, 0, sizeof(*res));
+  res->n_spill = st.n_spill;
+  res->n_pairs = st.n_pairs;
+  res->non_canonical = (st.dup_overflow || st.n_pairs > P.pair_cap) ? 1 : 0;
+  return SPARKEY_OK;
+}
+
+int sparkey_shard_pairs(sparkey_plan* pl, uint64_t* h_addrs, uint64_t n_pairs, char* err, size_t err_len) {
+  int rc = shard_check(pl, err, err_len);
+  if (rc) return rc;
+  if (n_pairs > pl->shard.P.pair_cap) {
+    set_err(err, err_len, "more pairs than recorded");
+    return SPARKEY_E_ARG;
+  }
+  if (n_pairs) HIP_TRY(hipMemcpy(h_addrs, pl->pairs, 2 * n_pairs * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  return SPARKEY_OK;
+}
+
+int32_t sparkey_shard_key_record_size(const sparkey_plan* pl) {
+  if (!pl || !pl->shard.active) return SPARKEY_E_ARG;
+  return (int32_t)(8 + ((pl->shard.lh.max_key_len + 7) & ~7LL));
+}
+
+int sparkey_shard_fetch_keys(sparkey_plan* pl, const uint64_t* d_addrs, uint64_t n, uint8_t* d_records,
+                             uint32_t rec_size, void* stream, char* err, size_t err_len) {
+  int rc = shard_check(pl, err, err_len);
+  if (rc) return rc;
+  hipStream_t s = stream ? (hipStream_t)stream : pl->own_stream;
+  BuildParams P = pl->shard.P;
+  P.fr_entry = (int64_t)pl->shard.buf_lo;
+  launch_fetch_keys(P, s, d_addrs, n, d_records, rec_size);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(s));
+  return SPARKEY_OK;
+}
+
+int sparkey_shard_compare_keys(sparkey_plan* pl, const uint8_t* d_records, uint64_t n_pairs, uint32_t rec_size,
+                               void* stream, int32_t* dup_out, char* err, size_t err_len) {
+  int rc = shard_check(pl, err, err_len);
+  if (rc) return rc;
+  hipStream_t s = stream ? (hipStream_t)stream : pl->own_stream;
+  const BuildParams& P = pl->shard.P;
+  HIP_TRY(hipMemsetAsync(&pl->d_status->dup, 0, sizeof(unsigned int), s));
+  launch_compare_keys(P, s, d_records, n_pairs, rec_size);
+  rc = shard_sync_status(pl, s, err, err_len);
+  if (rc) return rc;
+  *dup_out = (int32_t)pl->h_status->dup;
+  return SPARKEY_OK;
+}
+
+int sparkey_shard_apply_spill(sparkey_plan* pl, const uint8_t* d_spill, uint64_t n, void* stream, char* err,
+                              size_t err_len) {
+  int rc = shard_check(pl, err, err_len);
+  if (rc) return rc;
+  hipStream_t s = stream ? (hipStream_t)stream : pl->own_stream;
+  launch_apply_spill(pl->shard.P, s, reinterpret_cast<const SpillEntry*>(d_spill), n);
+  HIP_TRY(hipGetLastError());
+  return SPARKEY_OK;
+}
+
+// out = {first slot hash, first slot address, last slot hash, last slot address} of the rank's range
+int sparkey_shard_boundary(sparkey_plan* pl, void* stream, uint64_t* out, char* err, size_t err_len) {
+  int rc = shard_check(pl, err, err_len);
+  if (rc) return rc;
+  hipStream_t s = stream ? (hipStream_t)stream : pl->own_stream;
+  const BuildParams& P = pl->shard.P;
+  for (int i = 0; i < 4; i++) out[i] = 0;
+  if (P.slot_hi <= P.slot_lo) return SPARKEY_OK;
+  uint8_t b[32];
+  const uint8_t* base = P.out + kIndexHeaderSize;
+  HIP_TRY(hipMemcpyAsync(b, base + P.slot_lo * P.slot_size, P.slot_size, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(b + 16, base + (P.slot_hi - 1) * P.slot_size, P.slot_size, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  for (int k = 0; k < 2; k++) {
+    const uint8_t* q = b + 16 * k;
+    uint64_t h = 0, a = 0;
+    for (int i = 0; i < P.hash_size; i++) h |= (uint64_t)q[i] << (8 * i);
+    for (int i = 0; i < P.addr_size; i++) a |= (uint64_t)q[P.hash_size + i] << (8 * i);
+    out[2 * k] = h;
+    out[2 * k + 1] = a;
+  }
+  return SPARKEY_OK;
+}
+
+// out = {max displacement, hash collisions, total displacement} over the rank's slots
+int sparkey_shard_stats(sparkey_plan* pl, uint64_t prev_hash, int32_t prev_occ, void* stream, int64_t* out, char* err,
+                        size_t err_len) {
+  int rc = shard_check(pl, err, err_len);
+  if (rc) return rc;
+  hipStream_t s = stream ? (hipStream_t)stream : pl->own_stream;
+  BuildParams& P = pl->shard.P;
+  P.prev_hash = prev_hash;
+  P.prev_occ = prev_occ;
+  out[0] = out[1] = out[2] = 0;
+  if (P.slot_hi <= P.slot_lo) return SPARKEY_OK;
+  launch_stats(P, s, 0, &pl->timer);
+  rc = shard_sync_status(pl, s, err, err_len);
+  if (rc) return rc;
+  out[0] = pl->h_status->max_disp;
+  out[1] = pl->h_status->collisions;
+  out[2] = pl->h_status->total_disp;
+  return SPARKEY_OK;
+}
+
+int sparkey_index_header(const uint8_t* log_header, const sparkey_build_opts* opts, int64_t num_entries,
+                         int64_t garbage_size, int64_t max_displacement, int64_t hash_collisions,
+                         int64_t total_displacement, uint8_t* out, char* err, size_t err_len) {
+  if (!log_header || !opts || !out) return SPARKEY_E_ARG;
+  LogHdr lh;
+  int rc = parse_log_header(log_header, 84, (uint64_t)std::max<int64_t>(rd64(log_header + 32), 84), &lh, err, err_len);
+  if (rc) return rc;
+  IndexParams ip;
+  rc = make_index_params(lh, *opts, &ip, err, err_len);
+  if (rc) return rc;
+  index_header_template(lh, ip, opts->hash_seed, out);
+  wr64(out + 52, (uint64_t)garbage_size);
+  wr64(out + 60, (uint64_t)num_entries);
+  wr64(out + 84, (uint64_t)max_displacement);
+  wr64(out + 96, (uint64_t)hash_collisions);
+  wr64(out + 104, (uint64_t)total_displacement);
+  return SPARKEY_OK;
 }
 
 }  // extern "C"

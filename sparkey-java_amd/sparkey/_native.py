@@ -14,6 +14,24 @@ LIB_PATH = os.environ.get("SPARKEY_GPU_LIB", os.path.join(os.path.dirname(_HERE)
 if not os.path.exists(LIB_PATH):
     raise ImportError(f"libsparkey_gpu.so not built ({LIB_PATH}); run python sparkey-java_amd/build.py")
 
+
+
+def _preload_torch_hip() -> None:
+    """One HIP runtime per process: when PyTorch is installed, load the libamdhip64 it bundles
+    before ours, so libsparkey_gpu.so binds to it (same SONAME) whichever of the two is imported
+    first.  Two runtimes in one process do not see the same devices."""
+    if os.environ.get("SPARKEY_GPU_SYSTEM_HIP"):
+        return
+    import importlib.util
+    spec = importlib.util.find_spec("torch")
+    if spec is None or not spec.origin:
+        return
+    path = os.path.join(os.path.dirname(spec.origin), "lib", "libamdhip64.so")
+    if os.path.exists(path):
+        ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+
+
+_preload_torch_hip()
 _lib = ctypes.CDLL(LIB_PATH)
 
 OK = 0
@@ -83,7 +101,50 @@ _lib.sparkey_gpu_version.restype = ctypes.c_char_p
 _lib.sparkey_strerror.argtypes = [ctypes.c_int]
 _lib.sparkey_strerror.restype = ctypes.c_char_p
 
-EXPORTED = ["sparkey_build_index_file", "sparkey_build_index_mem", "sparkey_index_size", "sparkey_plan_create",
+
+
+class ShardFrameResult(ctypes.Structure):
+    _fields_ = [("exit", ctypes.c_int64), ("num_records", ctypes.c_int64), ("num_deletes", ctypes.c_int64),
+                ("err_pos", ctypes.c_int64), ("rc", ctypes.c_int32), ("framing_path", ctypes.c_int32)]
+
+
+class ShardPlaceResult(ctypes.Structure):
+    _fields_ = [("n_spill", ctypes.c_uint64), ("n_pairs", ctypes.c_uint64), ("non_canonical", ctypes.c_int32),
+                ("pad", ctypes.c_int32)]
+
+
+_u64p = ctypes.POINTER(ctypes.c_uint64)
+_i64p = ctypes.POINTER(ctypes.c_int64)
+_E = [ctypes.c_char_p, ctypes.c_size_t]
+_SIGS = {
+    "sparkey_shard_begin": ([_vp, _vp, ctypes.c_uint64, _vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.POINTER(BuildOpts),
+                             ctypes.c_int32, ctypes.c_int32] + _E, ctypes.c_int),
+    "sparkey_shard_slot_range": ([_vp, ctypes.c_int32, _u64p, _u64p], ctypes.c_int),
+    "sparkey_shard_max_record_len": ([_vp], ctypes.c_int64),
+    "sparkey_shard_find_entry": ([_vp, ctypes.c_uint64, ctypes.c_uint64, _vp, _i64p] + _E, ctypes.c_int),
+    "sparkey_shard_frame": ([_vp, ctypes.c_int64, ctypes.c_int64, _vp, ctypes.POINTER(ShardFrameResult)] + _E,
+                            ctypes.c_int),
+    "sparkey_shard_bin": ([_vp, _vp, ctypes.c_uint64, _vp, _u64p] + _E, ctypes.c_int),
+    "sparkey_shard_summarize": ([_vp, _vp, ctypes.c_uint64, _vp, _i64p] + _E, ctypes.c_int),
+    "sparkey_shard_place": ([_vp, ctypes.c_int64, _vp, _vp, ctypes.c_uint64, _vp, ctypes.POINTER(ShardPlaceResult)]
+                            + _E, ctypes.c_int),
+    "sparkey_shard_pairs": ([_vp, _u64p, ctypes.c_uint64] + _E, ctypes.c_int),
+    "sparkey_shard_key_record_size": ([_vp], ctypes.c_int32),
+    "sparkey_shard_fetch_keys": ([_vp, _vp, ctypes.c_uint64, _vp, ctypes.c_uint32, _vp] + _E, ctypes.c_int),
+    "sparkey_shard_compare_keys": ([_vp, _vp, ctypes.c_uint64, ctypes.c_uint32, _vp, ctypes.POINTER(ctypes.c_int32)]
+                                   + _E, ctypes.c_int),
+    "sparkey_shard_apply_spill": ([_vp, _vp, ctypes.c_uint64, _vp] + _E, ctypes.c_int),
+    "sparkey_shard_boundary": ([_vp, _vp, _u64p] + _E, ctypes.c_int),
+    "sparkey_shard_stats": ([_vp, ctypes.c_uint64, ctypes.c_int32, _vp, _i64p] + _E, ctypes.c_int),
+    "sparkey_index_header": ([_vp, ctypes.POINTER(BuildOpts), ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
+                              ctypes.c_int64, ctypes.c_int64, _vp] + _E, ctypes.c_int),
+}
+for _name, (_args, _res) in _SIGS.items():
+    _f = getattr(_lib, _name)
+    _f.argtypes = _args
+    _f.restype = _res
+
+EXPORTED = list(_SIGS) + ["sparkey_build_index_file", "sparkey_build_index_mem", "sparkey_index_size", "sparkey_plan_create",
             "sparkey_plan_build_device", "sparkey_plan_set_profiling", "sparkey_plan_stage_count",
             "sparkey_plan_stage_name", "sparkey_plan_stage_ms", "sparkey_plan_destroy", "sparkey_gpu_version",
             "sparkey_strerror"]
@@ -155,6 +216,18 @@ def build_index_mem(log: bytes, opts: BuildOpts):
     return out.raw[:n], stats
 
 
+def index_header(log_header: bytes, opts: BuildOpts, num_entries: int, garbage_size: int, max_displacement: int,
+                 hash_collisions: int, total_displacement: int) -> bytes:
+    """The 112-byte .spi header for the given totals (IndexHeader.java:125-155)."""
+    out = ctypes.create_string_buffer(112)
+    err = ctypes.create_string_buffer(512)
+    rc = _lib.sparkey_index_header(log_header, ctypes.byref(opts), num_entries, garbage_size, max_displacement,
+                                   hash_collisions, total_displacement, out, err, 512)
+    if rc != OK:
+        raise_for(rc, err.value.decode(errors="replace"))
+    return out.raw
+
+
 def version() -> str:
     return _lib.sparkey_gpu_version().decode()
 
@@ -183,6 +256,84 @@ class Plan:
 
     def set_profiling(self, enabled: bool) -> None:
         _lib.sparkey_plan_set_profiling(self._h, 1 if enabled else 0)
+
+    # ---- sharded build steps (include/sparkey_gpu.h "sharded build"; orchestrated by sharded.py) ----
+    def _call(self, name, *args):
+        err = ctypes.create_string_buffer(512)
+        rc = getattr(_lib, name)(self._h, *args, err, 512)
+        if rc != OK:
+            raise_for(rc, err.value.decode(errors="replace"))
+
+    def shard_begin(self, log_header: bytes, file_len: int, d_buf: int, buf_lo: int, buf_hi: int, opts: BuildOpts,
+                    rank: int, world: int) -> None:
+        self._call("sparkey_shard_begin", log_header, file_len, ctypes.c_void_p(d_buf), buf_lo, buf_hi,
+                   ctypes.byref(opts), rank, world)
+
+    def shard_slot_range(self, rank: int):
+        lo, hi = ctypes.c_uint64(), ctypes.c_uint64()
+        if _lib.sparkey_shard_slot_range(self._h, rank, ctypes.byref(lo), ctypes.byref(hi)) != OK:
+            raise ValueError("bad rank")
+        return lo.value, hi.value
+
+    def shard_max_record_len(self) -> int:
+        return int(_lib.sparkey_shard_max_record_len(self._h))
+
+    def shard_find_entry(self, lo: int, window: int, stream: int = 0) -> int:
+        v = ctypes.c_int64()
+        self._call("sparkey_shard_find_entry", lo, window, ctypes.c_void_p(stream), ctypes.byref(v))
+        return v.value
+
+    def shard_frame(self, entry: int, frame_end: int, stream: int = 0) -> ShardFrameResult:
+        r = ShardFrameResult()
+        self._call("sparkey_shard_frame", entry, frame_end, ctypes.c_void_p(stream), ctypes.byref(r))
+        return r
+
+    def shard_bin(self, d_send: int, send_cap: int, world: int, stream: int = 0):
+        counts = (ctypes.c_uint64 * world)()
+        self._call("sparkey_shard_bin", ctypes.c_void_p(d_send), send_cap, ctypes.c_void_p(stream), counts)
+        return [int(c) for c in counts]
+
+    def shard_summarize(self, d_recv: int, n_recv: int, stream: int = 0):
+        f = (ctypes.c_int64 * 2)()
+        self._call("sparkey_shard_summarize", ctypes.c_void_p(d_recv), n_recv, ctypes.c_void_p(stream), f)
+        return int(f[0]), int(f[1])
+
+    def shard_place(self, carry_in: int, d_slots: int, d_spill: int, spill_cap: int, stream: int = 0):
+        r = ShardPlaceResult()
+        self._call("sparkey_shard_place", carry_in, ctypes.c_void_p(d_slots), ctypes.c_void_p(d_spill), spill_cap,
+                   ctypes.c_void_p(stream), ctypes.byref(r))
+        return int(r.n_spill), int(r.n_pairs), bool(r.non_canonical)
+
+    def shard_pairs(self, n_pairs: int):
+        out = (ctypes.c_uint64 * max(1, 2 * n_pairs))()
+        self._call("sparkey_shard_pairs", out, n_pairs)
+        return [int(out[i]) for i in range(2 * n_pairs)]
+
+    def shard_key_record_size(self) -> int:
+        return int(_lib.sparkey_shard_key_record_size(self._h))
+
+    def shard_fetch_keys(self, d_addrs: int, n: int, d_records: int, rec_size: int, stream: int = 0) -> None:
+        self._call("sparkey_shard_fetch_keys", ctypes.c_void_p(d_addrs), n, ctypes.c_void_p(d_records), rec_size,
+                   ctypes.c_void_p(stream))
+
+    def shard_compare_keys(self, d_records: int, n_pairs: int, rec_size: int, stream: int = 0) -> int:
+        dup = ctypes.c_int32()
+        self._call("sparkey_shard_compare_keys", ctypes.c_void_p(d_records), n_pairs, rec_size,
+                   ctypes.c_void_p(stream), ctypes.byref(dup))
+        return dup.value
+
+    def shard_apply_spill(self, d_spill: int, n: int, stream: int = 0) -> None:
+        self._call("sparkey_shard_apply_spill", ctypes.c_void_p(d_spill), n, ctypes.c_void_p(stream))
+
+    def shard_boundary(self, stream: int = 0):
+        out = (ctypes.c_uint64 * 4)()
+        self._call("sparkey_shard_boundary", ctypes.c_void_p(stream), out)
+        return [int(x) for x in out]
+
+    def shard_stats(self, prev_hash: int, prev_occ: int, stream: int = 0):
+        out = (ctypes.c_int64 * 3)()
+        self._call("sparkey_shard_stats", prev_hash, prev_occ, ctypes.c_void_p(stream), out)
+        return int(out[0]), int(out[1]), int(out[2])
 
     def stage_times(self):
         n = _lib.sparkey_plan_stage_count(self._h)

@@ -1,0 +1,526 @@
+"""Sharded .spi build: one process per GPU, the log's byte range split across the ranks.
+
+The reference build is single-threaded (Sparkey.java:36, IndexHash.createNew IndexHash.java:131-167);
+this module splits the same computation at the points where ranks must exchange data and runs the
+device steps of include/sparkey_gpu.h ("sharded build") in between:
+
+  1. entries    rank g > 0 finds a record start c_g near the head of its byte range
+                (sparkey_shard_find_entry); the c_g are all-gathered; rank g frames the records
+                starting in [c_g, c_{g+1}) (sparkey_shard_frame) and reports its exact exit x_g.
+                x_g == c_{g+1} proves c_{g+1} is on the true record chain (by induction from
+                c_0 = 84); otherwise rank g+1 re-frames from x_g and the check repeats.
+  2. exchange   every (hash, address) entry goes to the rank that owns its slot range: one
+                all_to_all of 16-byte entries.
+  3. placement  each rank computes the carry function of its slot range; the all-gathered
+                functions give every rank's carry-in (the ring's wrap-around fixed point
+                included); entries placed past a range end are all-gathered to their owner.
+                Equal-hash pairs are checked against the keys, fetched from the ranks holding
+                those records (IndexHash.java:606-636).
+  4. stats      calculateMaxDisplacement (IndexHash.java:195-245) per range with the boundary slots
+                exchanged; the totals are reduced and rank 0 writes the 112-byte header.
+
+Logs the canonical layout does not cover (DELETEs, duplicate keys, a full table) are gathered on
+every rank and built with the exact single-GPU path (correct, not scaled).
+
+Collectives go through torch.distributed: backend "nccl" (RCCL over xGMI) moves device tensors;
+"gloo" (CPU tests, several ranks on one GPU) stages them through host memory.
+"""
+from __future__ import annotations
+
+import contextlib
+import struct
+import time
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+LOG_HEADER_SIZE = 84
+INDEX_HEADER_SIZE = 112
+ENTRY_BYTES = 16
+SPILL_BYTES = 32
+_HDR = struct.Struct("<IIIiqqqqqqiiqi")
+
+
+def _vlq_size(v: int) -> int:  # Util.java:102-128
+    n = 1
+    while n < 9 and v >= (1 << (7 * n)):
+        n += 1
+    return n
+
+
+def max_record_len(max_key_len: int, max_value_len: int) -> int:
+    """Longest record a log with these header maxima can hold (PUT or DELETE)."""
+    put = _vlq_size(max_key_len + 1) + _vlq_size(max_value_len) + max_key_len + max_value_len
+    dele = 1 + _vlq_size(max_key_len) + max_key_len
+    return max(1, put, dele)
+
+
+def entry_window(max_rec: int) -> int:
+    """How far past its candidate window a rank walks the candidates to find its entry."""
+    return max(4096, 8 * max_rec)
+
+
+@dataclass
+class ShardLayout:
+    """Byte ranges of the log per rank and the bytes each rank must hold."""
+    data_end: int
+    file_len: int
+    world: int
+    max_rec: int
+    window: int
+    lo: list
+    hi: list
+    small: bool  # too small to split: rank 0 frames the whole log
+
+    def buffer_range(self, rank: int):
+        """[buf_lo, buf_hi) of global log bytes rank `rank` loads onto its GPU (buf_lo 4 KiB aligned)."""
+        if self.small:
+            return (0, self.file_len) if rank == 0 else (0, 0)
+        lo = 0 if rank == 0 else (self.lo[rank] // 4096) * 4096
+        hi = self.file_len if rank == self.world - 1 else min(self.file_len, self.hi[rank] + self.overlap)
+        return lo, hi
+
+    @property
+    def overlap(self) -> int:
+        return 2 * self.max_rec + self.window + 64
+
+
+def parse_log_header(header: bytes) -> dict:
+    f = _HDR.unpack(header[:LOG_HEADER_SIZE])
+    keys = ("magic", "major", "minor", "file_id", "num_puts", "num_deletes", "data_end", "max_key_len",
+            "max_value_len", "delete_size", "compression_type", "block_size", "put_size", "max_entries_per_block")
+    return dict(zip(keys, f))
+
+
+def shard_layout(header: bytes, file_len: int, world: int) -> ShardLayout:
+    h = parse_log_header(header)
+    data_end = max(int(h["data_end"]), LOG_HEADER_SIZE)
+    mrec = max_record_len(max(0, h["max_key_len"]), max(0, h["max_value_len"]))
+    win = entry_window(mrec)
+    span = data_end - LOG_HEADER_SIZE
+    lo = [LOG_HEADER_SIZE + (g * span) // world for g in range(world)]
+    hi = lo[1:] + [data_end]
+    small = world > 1 and span // world < 2 * (mrec + win) + 64
+    return ShardLayout(data_end, file_len, world, mrec, win, lo, hi, small)
+
+
+# ------------------------------------------------------------------------------------------------
+# collectives
+# ------------------------------------------------------------------------------------------------
+class Comm:
+    """torch.distributed collectives on device tensors (nccl/RCCL) or staged through host (gloo)."""
+
+    def __init__(self, group=None, device=None):
+        import torch.distributed as dist
+        self.dist = dist
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        self.device_native = dist.get_backend(group) == "nccl"
+        self.tdev = device if self.device_native else torch.device("cpu")
+
+    def _to(self, t: torch.Tensor) -> torch.Tensor:
+        return t if t.device == self.tdev else t.to(self.tdev)
+
+    def allgather_i64(self, vals) -> np.ndarray:
+        t = torch.tensor([int(v) for v in vals], dtype=torch.int64, device=self.tdev)
+        out = torch.empty(self.world * t.numel(), dtype=torch.int64, device=self.tdev)
+        self.dist.all_gather_into_tensor(out, t, group=self.group)
+        return out.cpu().numpy().reshape(self.world, -1)
+
+    def all_to_all(self, send: torch.Tensor, in_splits, out_splits, out_device) -> torch.Tensor:
+        """1-D tensors; splits in elements of send's dtype."""
+        recv = torch.empty(int(sum(out_splits)), dtype=send.dtype, device=self.tdev)
+        self.dist.all_to_all_single(recv, self._to(send), [int(x) for x in out_splits], [int(x) for x in in_splits],
+                                    group=self.group)
+        return recv if recv.device == out_device else recv.to(out_device)
+
+    def allgather_var(self, t: torch.Tensor, n: int, out_device):
+        """Every rank's first n[rank] elements of a 1-D tensor -> list of tensors (padded exchange)."""
+        counts = self.allgather_i64([n])[:, 0]
+        m = max(1, int(counts.max()))
+        pad = torch.zeros(m, dtype=t.dtype, device=self.tdev)
+        if n:
+            pad[:n] = self._to(t[:n])
+        out = torch.empty(self.world * m, dtype=t.dtype, device=self.tdev)
+        self.dist.all_gather_into_tensor(out, pad, group=self.group)
+        res = []
+        for r in range(self.world):
+            piece = out[r * m: r * m + int(counts[r])]
+            res.append(piece if piece.device == out_device else piece.to(out_device))
+        return res
+
+    def barrier(self):
+        self.dist.barrier(group=self.group)
+
+
+# ------------------------------------------------------------------------------------------------
+# device steps (the C-ABI); tests substitute a CPU simulation with the same methods
+# ------------------------------------------------------------------------------------------------
+class GpuShardSteps:
+    """The sparkey_shard_* steps of one rank on its GPU (through a sparkey_plan)."""
+
+    def __init__(self, device: torch.device, plan=None):
+        from . import _native
+        self.n = _native
+        self.device = device
+        self.plan = plan if plan is not None else _native.Plan(device.index or 0)
+        # every torch op and every C-ABI step of the build runs in order on this one stream
+        self.tstream = torch.cuda.Stream(device)
+        self.stream = self.tstream.cuda_stream
+        self.header = None
+
+    def stream_ctx(self):
+        return torch.cuda.stream(self.tstream)
+
+    def alloc(self, nbytes: int) -> torch.Tensor:
+        return torch.empty(max(16, (nbytes + 15) // 16 * 16), dtype=torch.uint8, device=self.device)
+
+    def begin(self, header, file_len, buf, buf_lo, buf_hi, opts, rank, world):
+        self.header = header
+        self.plan.shard_begin(header, file_len, buf.data_ptr(), buf_lo, buf_hi, opts, rank, world)
+
+    def slot_range(self, r):
+        return self.plan.shard_slot_range(r)
+
+    def max_record_len(self):
+        return self.plan.shard_max_record_len()
+
+    def find_entry(self, lo, window):
+        return self.plan.shard_find_entry(lo, window, self.stream)
+
+    def frame(self, entry, frame_end):
+        r = self.plan.shard_frame(entry, frame_end, self.stream)
+        return {"exit": r.exit, "n": r.num_records, "ndel": r.num_deletes, "rc": r.rc, "err_pos": r.err_pos,
+                "framing_path": r.framing_path}
+
+    def bin(self, send: torch.Tensor, n: int, world: int):
+        return self.plan.shard_bin(send.data_ptr(), n, world, self.stream)
+
+    def summarize(self, recv: torch.Tensor, n: int):
+        return self.plan.shard_summarize(recv.data_ptr(), n, self.stream)
+
+    def place(self, carry_in, out: torch.Tensor, out_off: int, spill: torch.Tensor, spill_cap: int):
+        return self.plan.shard_place(carry_in, out.data_ptr() + out_off, spill.data_ptr(), spill_cap, self.stream)
+
+    def pairs(self, n):
+        return np.array(self.plan.shard_pairs(n), dtype=np.uint64)
+
+    def key_record_size(self):
+        return self.plan.shard_key_record_size()
+
+    def fetch_keys(self, addrs: torch.Tensor, n: int, rec: torch.Tensor, rec_size: int):
+        self.plan.shard_fetch_keys(addrs.data_ptr(), n, rec.data_ptr(), rec_size, self.stream)
+
+    def compare_keys(self, rec: torch.Tensor, npairs: int, rec_size: int) -> int:
+        return self.plan.shard_compare_keys(rec.data_ptr(), npairs, rec_size, self.stream)
+
+    def apply_spill(self, spill: torch.Tensor, n: int):
+        self.plan.shard_apply_spill(spill.data_ptr(), n, self.stream)
+
+    def boundary(self):
+        return self.plan.shard_boundary(self.stream)
+
+    def stats(self, prev_hash, prev_occ):
+        return self.plan.shard_stats(prev_hash, prev_occ, self.stream)
+
+    def index_header(self, opts, num_entries, garbage, max_disp, collisions, total_disp) -> bytes:
+        return self.n.index_header(self.header, opts, num_entries, garbage, max_disp, collisions, total_disp)
+
+    def full_build(self, log: torch.Tensor, file_len: int, out: torch.Tensor, opts):
+        st = self.plan.build(self.header, log.data_ptr(), file_len, out.data_ptr(), out.numel(), opts, self.stream)
+        return {"num_entries": st.num_entries, "garbage_size": st.garbage_size, "max_displacement": st.max_displacement,
+                "hash_collisions": st.hash_collisions, "total_displacement": st.total_displacement,
+                "placement_path": st.placement_path}
+
+    def to_host_bytes(self, t: torch.Tensor) -> bytes:
+        return t.cpu().numpy().tobytes()
+
+    def from_host(self, b, dtype=torch.uint8) -> torch.Tensor:
+        return torch.frombuffer(bytearray(b), dtype=dtype).to(self.device)
+
+
+# ------------------------------------------------------------------------------------------------
+# the orchestration
+# ------------------------------------------------------------------------------------------------
+@dataclass
+class ShardResult:
+    out: torch.Tensor        # this rank's part of the .spi: [header (rank 0)] + slots [slot_lo, slot_hi)
+    slot_lo: int
+    slot_hi: int
+    out_offset: int          # byte offset of `out` in the .spi file
+    stats: dict = field(default_factory=dict)
+    path: str = "sharded"    # "sharded" or "gathered" (exact single-GPU build of the whole log)
+    rounds: int = 0          # entry-verification rounds
+    n_pairs: int = 0         # equal-hash pairs checked against their keys (all ranks)
+    n_spill: int = 0         # slots placed past a range end (all ranks)
+    phase_ms: dict = field(default_factory=dict)  # host wall time per phase on this rank
+
+
+def _compose(fs):
+    """Compose carry functions f(x) = max(c, x + a) left to right (apply fs[0] first)."""
+    c, a = 0, 0
+    first = True
+    for fc, fa in fs:
+        if first:
+            c, a, first = fc, fa, False
+        else:
+            c, a = max(fc, c + fa), a + fa
+    return c, a
+
+
+def _apply(f, x):
+    return max(f[0], x + f[1])
+
+
+class ShardedBuilder:
+    """One rank's side of a sharded .spi build (call build() on every rank of the group)."""
+
+    def __init__(self, steps, comm: Comm):
+        self.s = steps
+        self.c = comm
+        self._ebb = 0
+
+    def build(self, header: bytes, file_len: int, buf: torch.Tensor, buf_lo: int, buf_hi: int, opts) -> ShardResult:
+        ctx = self.s.stream_ctx() if hasattr(self.s, "stream_ctx") else contextlib.nullcontext()
+        with ctx:
+            return self._build(header, file_len, buf, buf_lo, buf_hi, opts)
+
+    def _build(self, header, file_len, buf, buf_lo, buf_hi, opts) -> ShardResult:
+        s, c = self.s, self.c
+        clock = [time.perf_counter()]
+        phase = {}
+
+        def mark(name):
+            t = time.perf_counter()
+            phase[name] = (t - clock[0]) * 1e3
+            clock[0] = t
+
+        g, G = c.rank, c.world
+        lay = shard_layout(header, file_len, G)
+        data_end = lay.data_end
+        s.begin(header, file_len, buf, buf_lo, buf_hi, opts, g, G)
+        h = parse_log_header(header)
+
+        # ---- 1 entries: speculate, frame, verify by induction from c_0 = 84 ----
+        if g == 0:
+            c_g = LOG_HEADER_SIZE
+        elif lay.small:
+            c_g = data_end
+        else:
+            c_g = s.find_entry(lay.lo[g], lay.window)
+        cs = [int(v) for v in c.allgather_i64([c_g])[:, 0]]
+        entries = []
+        for r, v in enumerate(cs):
+            ok = v >= 0 and (r == 0 or (lay.small and v == data_end) or lay.lo[r] <= v <= data_end)
+            if ok and entries and entries[-1] is not None and v < entries[-1]:
+                ok = False
+            entries.append(v if ok else None)
+
+        def frame_end(r):
+            if r == G - 1:
+                return data_end
+            return entries[r + 1] if entries[r + 1] is not None else lay.hi[r]
+
+        mine = None
+        todo = {r for r in range(G) if entries[r] is not None}
+        rounds = 0
+        while True:
+            rounds += 1
+            if g in todo:
+                fe = frame_end(g)
+                mine = s.frame(entries[g], fe)  # owns nothing when entries[g] >= fe
+                mine["entry"], mine["fe"] = entries[g], fe
+            row = [-1] * 7 if mine is None else [mine["entry"], mine["fe"], mine["exit"], mine["n"], mine["ndel"],
+                                                 mine["rc"], mine["err_pos"]]
+            R = c.allgather_i64(row)
+            todo = set()
+            done = True
+            for r in range(G):
+                ent, fe, ex, n, nd, rc, epos = (int(x) for x in R[r])
+                if rc:
+                    from ._native import raise_for
+                    raise_for(rc, f"{_code_text(rc)} (log offset {epos})")
+                if r == G - 1:
+                    break
+                nxt = min(ex, data_end)
+                if int(R[r + 1][0]) == nxt and entries[r + 1] == nxt:
+                    continue
+                entries[r + 1] = nxt  # rank r + 1 re-frames from the verified exit
+                todo = {r + 1}
+                done = False
+                break
+            if done:
+                break
+        n_local = int(mine["n"]) if mine else 0
+        totals = R[:, 3].astype(np.int64)
+        n_total = int(totals.sum())
+        n_deletes = int(R[:, 4].sum())
+        slot_lo, slot_hi = s.slot_range(g)
+        self._ebb = _entry_block_bits(h)
+        slot_size = _slot_size(h, opts, data_end)
+        out_off = 0 if g == 0 else INDEX_HEADER_SIZE + slot_lo * slot_size
+        out_len = (INDEX_HEADER_SIZE if g == 0 else 0) + (slot_hi - slot_lo) * slot_size
+        res = ShardResult(out=None, slot_lo=slot_lo, slot_hi=slot_hi, out_offset=out_off, rounds=rounds,
+                          phase_ms=phase)
+        mark("entries+frame")
+
+        if n_deletes > 0 or n_total >= _capacity(h, opts):
+            return self._gathered(res, header, file_len, buf, buf_lo, buf_hi, lay, opts, slot_size, out_len)
+
+        # ---- 2 exchange: every entry to the owner of its slot range ----
+        send = s.alloc(max(1, n_local) * ENTRY_BYTES)
+        counts = s.bin(send, n_local, G) if n_local else [0] * G
+        M = c.allgather_i64(counts)                       # M[src][dst]
+        out_splits = [int(M[r][g]) * 2 for r in range(G)]  # int64 elements (2 per entry)
+        in_splits = [int(x) * 2 for x in counts]
+        recv = c.all_to_all(send.view(torch.int64)[: 2 * max(1, n_local)] if n_local else
+                            send.view(torch.int64)[:0], in_splits, out_splits, buf.device)
+        n_recv = sum(out_splits) // 2
+        mark("exchange")
+
+        # ---- 3 placement ----
+        fun = s.summarize(recv, n_recv)
+        F = [tuple(int(v) for v in row) for row in c.allgather_i64(list(fun))]
+        x0 = _compose(F)[0]             # N < capacity: the wrap fixed point is C_total
+        carry = x0
+        for r in range(g):
+            carry = _apply(F[r], carry)
+        out = s.alloc(out_len)
+        spill_cap = 4096
+        while True:
+            spill = s.alloc(spill_cap * SPILL_BYTES)
+            n_spill, n_pairs, non_canon = s.place(carry, out, INDEX_HEADER_SIZE if g == 0 else 0, spill, spill_cap)
+            if n_spill <= spill_cap:
+                break
+            spill_cap = n_spill
+        flags = c.allgather_i64([n_spill, n_pairs, int(non_canon)])
+        res.n_spill, res.n_pairs = int(flags[:, 0].sum()), int(flags[:, 1].sum())
+        if flags[:, 2].any():
+            return self._gathered(res, header, file_len, buf, buf_lo, buf_hi, lay, opts, slot_size, out_len)
+        if flags[:, 1].sum() > 0 and self._pairs_share_a_key(n_pairs, entries, data_end, buf.device):
+            return self._gathered(res, header, file_len, buf, buf_lo, buf_hi, lay, opts, slot_size, out_len)
+        if flags[:, 0].sum() > 0:
+            pieces = c.allgather_var(spill.view(torch.int64), 4 * n_spill, buf.device)
+            allsp = torch.cat([p for p in pieces if p.numel()]) if any(p.numel() for p in pieces) else None
+            if allsp is not None:
+                s.apply_spill(allsp, allsp.numel() // 4)
+
+        mark("place")
+        # ---- 4 stats: boundary slots, per-range sums, reduce, header ----
+        bnd = c.allgather_i64([_signed(v) for v in s.boundary()] + [int(slot_hi > slot_lo)])
+        prev_hash, prev_occ = 0, 0
+        for r in range(g - 1, -1, -1):
+            if bnd[r][4]:
+                prev_hash, prev_occ = int(bnd[r][2]) & 0xFFFFFFFFFFFFFFFF, int(bnd[r][3] != 0)
+                break
+        mx, col, tot = s.stats(prev_hash, prev_occ) if slot_hi > slot_lo else (0, 0, 0)
+        S = c.allgather_i64([mx, col, tot])
+        max_disp, collisions, total_disp = int(S[:, 0].max()), int(S[:, 1].sum()), int(S[:, 2].sum())
+        # wrap quirk (IndexHash.java:239-241): slot 0 and slot cap-1 occupied with equal hashes
+        last = max(r for r in range(G) if bnd[r][4])
+        if bnd[0][1] != 0 and bnd[last][3] != 0 and bnd[0][0] == bnd[last][2]:
+            collisions += 1
+        stats = {"num_entries": n_total, "garbage_size": 0, "max_displacement": max_disp,
+                 "hash_collisions": collisions, "total_displacement": total_disp, "placement_path": 0}
+        if g == 0:
+            hdr = s.index_header(opts, n_total, 0, max_disp, collisions, total_disp)
+            out[:INDEX_HEADER_SIZE].copy_(s.from_host(hdr))
+        res.out = out
+        res.stats = stats
+        mark("stats")
+        return res
+
+    # equal-hash pairs: fetch both keys from the ranks that hold the records, compare on device
+    def _pairs_share_a_key(self, n_pairs, entries, data_end, device) -> bool:
+        s, c = self.s, self.c
+        G = c.world
+        addrs = s.pairs(n_pairs) if n_pairs else np.zeros(0, dtype=np.uint64)
+        starts = np.array([e if e is not None else data_end for e in entries], dtype=np.int64)
+        pos = (addrs & np.uint64(~(1 << 63) & 0xFFFFFFFFFFFFFFFF)).astype(np.int64)
+        owner = np.searchsorted(starts, pos >> self._ebb, side="right") - 1
+        owner = np.clip(owner, 0, G - 1)
+        order = np.argsort(owner, kind="stable")
+        req = addrs[order].astype(np.int64)
+        counts = np.bincount(owner, minlength=G).astype(np.int64)
+        M = c.allgather_i64(counts.tolist())
+        rs = s.key_record_size()
+        send = torch.from_numpy(req.copy()).to(device) if req.size else torch.zeros(1, dtype=torch.int64, device=device)
+        got = c.all_to_all(send[: req.size], counts.tolist(), [int(M[r][c.rank]) for r in range(G)], device)
+        n_req = got.numel()
+        rec = s.alloc(max(1, n_req) * rs)
+        if n_req:
+            s.fetch_keys(got, n_req, rec, rs)
+        back = c.all_to_all(rec[: n_req * rs], [int(M[r][c.rank]) * rs for r in range(G)],
+                            (counts * rs).tolist(), device)
+        # back holds the records in request order; put them back in pair order
+        inv = np.empty_like(order)
+        inv[order] = np.arange(order.size)
+        dup = 0
+        if n_pairs:
+            idx = torch.from_numpy(inv.astype(np.int64)).to(device)
+            recs = back.view(-1, rs)[idx].reshape(-1).contiguous()
+            dup = s.compare_keys(recs, n_pairs, rs)
+        return bool(c.allgather_i64([int(dup != 0)])[:, 0].any())
+
+    # exact path for non-canonical logs: every rank gathers the whole log and builds it
+    def _gathered(self, res, header, file_len, buf, buf_lo, buf_hi, lay, opts, slot_size, out_len):
+        s, c = self.s, self.c
+        g, G = c.rank, c.world
+        if lay.small:
+            own_lo, own_hi = (0, file_len) if g == 0 else (0, 0)
+        else:
+            own_lo = 0 if g == 0 else lay.lo[g]
+            own_hi = file_len if g == G - 1 else lay.lo[g + 1]
+        piece = buf[own_lo - buf_lo: own_hi - buf_lo] if own_hi > own_lo else buf[:0]
+        pieces = c.allgather_var(piece, piece.numel(), buf.device)
+        log = s.alloc(file_len + 16)
+        at = 0
+        for p in pieces:
+            log[at: at + p.numel()].copy_(p)
+            at += p.numel()
+        full = s.alloc(INDEX_HEADER_SIZE + _capacity(parse_log_header(header), opts) * slot_size)
+        stats = s.full_build(log, file_len, full, opts)
+        lo = 0 if g == 0 else INDEX_HEADER_SIZE + res.slot_lo * slot_size
+        out = s.alloc(out_len)
+        out[:out_len].copy_(full[lo: lo + out_len])
+        res.out = out
+        res.stats = stats
+        res.path = "gathered"
+        return res
+
+
+_CODE_TEXT = {-1: "File is not a Sparkey log file", -2: "Incompatible version", -3: "Corrupt log file",
+              -4: "No free slots in the hash", -5: "Corrupt data", -6: "Too long VLQ value",
+              -7: "Too large max key len"}
+
+
+def _code_text(rc: int) -> str:
+    return _CODE_TEXT.get(rc, "error")
+
+
+def _capacity(h: dict, opts) -> int:
+    """IndexHash.java:135-145: capacity = 1 | (long)(numPuts * max(sparsity, 1.3))."""
+    sp = max(float(opts.sparsity), 1.3)
+    v = float(h["num_puts"]) * sp
+    return 1 | (int(v) if v == v else 0)
+
+
+def _signed(v: int) -> int:
+    v = int(v) & 0xFFFFFFFFFFFFFFFF
+    return v - (1 << 64) if v >= (1 << 63) else v
+
+
+def _entry_block_bits(h: dict) -> int:  # IndexHash.java:123-129
+    ebb = 0
+    while (1 << ebb) < h["max_entries_per_block"]:
+        ebb += 1
+    return ebb
+
+
+def _slot_size(h: dict, opts, data_end: int) -> int:
+    ebb = _entry_block_bits(h)
+    addr = 4 if h["data_end"] <= (1 << (30 - ebb)) else 8
+    hs = opts.hash_size or (4 if h["num_puts"] < (1 << 23) else 8)
+    return hs + addr

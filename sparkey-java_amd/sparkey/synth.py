@@ -34,25 +34,48 @@ def _header(n_puts: int, max_key: int, max_val: int, put_size: int, data_end: in
     return h.to_bytes()
 
 
+def fixed_log_range(n: int, lo: int, hi: int, key_len: int = 16, value_len: int = 100, seed: int = 1,
+                    file_id: int = 0x5EED5EED, block_size: int = 0):
+    """Bytes [lo, hi) of the fixed_log(n, ...) file, generated without the rest of the log (every
+    byte is a function of its record index, so each rank of a sharded build makes only its range).
+    Returns (84-byte header, uint8 array of hi - lo bytes)."""
+    assert key_len >= 16 and key_len + 1 < 128 and value_len < 128
+    rec = 2 + key_len + value_len
+    total = LOG_HEADER_SIZE + n * rec
+    hi = min(hi, total)
+    lo = min(lo, hi)
+    header = _header(n, key_len, value_len, n * rec, total, file_id, block_size)
+    i0 = max(0, (lo - LOG_HEADER_SIZE) // rec)
+    i1 = min(n, max(0, (hi - LOG_HEADER_SIZE + rec - 1) // rec))
+    m = max(0, i1 - i0)
+    body = np.empty((m, rec), dtype=np.uint8)
+    i = np.arange(i0, i0 + m, dtype=np.uint64)
+    body[:, 0] = key_len + 1
+    body[:, 1] = value_len
+    body[:, 2:10] = i.view(np.uint8).reshape(m, 8)
+    body[:, 10:18] = splitmix64(i ^ np.uint64(seed)).view(np.uint8).reshape(m, 8)
+    extra = (key_len - 16) + value_len  # remaining key bytes, then the value: splitmix64 words of (i, j)
+    words = (extra + 7) // 8
+    base = i * np.uint64(64) + np.uint64((seed * 0x9E3779B97F4A7C15) & 0xFFFFFFFFFFFFFFFF)
+    fill = splitmix64(base[:, None] + np.arange(words, dtype=np.uint64)[None, :])
+    body[:, 18:] = fill.view(np.uint8).reshape(m, words * 8)[:, :extra]
+    start = LOG_HEADER_SIZE + i0 * rec
+    buf = np.empty(hi - lo, dtype=np.uint8)
+    flat = body.reshape(-1)
+    if lo < LOG_HEADER_SIZE:  # the header bytes
+        k = min(hi, LOG_HEADER_SIZE) - lo
+        buf[:k] = np.frombuffer(header, dtype=np.uint8)[lo: lo + k]
+    a = max(lo, start)
+    if hi > a:
+        buf[a - lo: hi - lo] = flat[a - start: hi - start]
+    return header, buf
+
+
 def fixed_log(n: int, key_len: int = 16, value_len: int = 100, seed: int = 1, file_id: int = 0x5EED5EED,
               block_size: int = 0) -> np.ndarray:
     """n PUTs with fixed-size keys (>= 16 B) and values; returns the whole .spl as a uint8 array."""
-    assert key_len >= 16 and key_len + 1 < 128 and value_len < 128
     rec = 2 + key_len + value_len
-    buf = np.empty(LOG_HEADER_SIZE + n * rec, dtype=np.uint8)
-    body = buf[LOG_HEADER_SIZE:].reshape(n, rec)
-    body[:, 0] = key_len + 1
-    body[:, 1] = value_len
-    i = np.arange(n, dtype=np.uint64)
-    body[:, 2:10] = i.view(np.uint8).reshape(n, 8)
-    body[:, 10:18] = splitmix64(i ^ np.uint64(seed)).view(np.uint8).reshape(n, 8)
-    rng = np.random.default_rng(seed)
-    if key_len > 16:
-        body[:, 18:2 + key_len] = rng.integers(0, 256, size=(n, key_len - 16), dtype=np.uint8)
-    body[:, 2 + key_len:] = rng.integers(0, 256, size=(n, value_len), dtype=np.uint8)
-    buf[:LOG_HEADER_SIZE] = np.frombuffer(
-        _header(n, key_len, value_len, n * rec, LOG_HEADER_SIZE + n * rec, file_id, block_size), dtype=np.uint8)
-    return buf
+    return fixed_log_range(n, 0, LOG_HEADER_SIZE + n * rec, key_len, value_len, seed, file_id, block_size)[1]
 
 
 def mixed_log(n: int, min_key: int = 8, max_key: int = 64, value_len: int = 100, seed: int = 3,

@@ -1,0 +1,188 @@
+"""Multi-process harness for the sharded build (test infrastructure).
+
+run_world() starts `world` processes (torch.multiprocessing, gloo rendezvous on 127.0.0.1), each
+loads ITS byte range of the log (sharded.ShardLayout.buffer_range) and runs ShardedBuilder with
+either the CPU simulation of the device steps (tests/shard_sim.py) or the HIP steps on cuda:0;
+the parent assembles the .spi from the ranks' slices at their file offsets.
+"""
+from __future__ import annotations
+
+import json
+import os
+import socket
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for _p in (os.path.join(ROOT, "sparkey-java_amd"), os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests"), ROOT):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+
+def free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, log_path, opts_kw, out_dir, kind):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch
+    import torch.distributed as dist
+    from sparkey import _native
+    from sparkey.sharded import Comm, ShardedBuilder, shard_layout
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        log = open(log_path, "rb").read()
+        header = log[:84]
+        lay = shard_layout(header, len(log), world)
+        lo, hi = lay.buffer_range(rank)
+        host = torch.frombuffer(bytearray(log[lo:hi] + bytes(16)), dtype=torch.uint8)[: hi - lo]
+        opts = _native.make_opts(**opts_kw)
+        if kind == "cpu":
+            from shard_sim import CpuShardSteps
+            steps = CpuShardSteps()
+            buf = host.clone()
+            comm = Comm()
+        else:
+            from sparkey.sharded import GpuShardSteps
+            dev = torch.device("cuda", 0)
+            torch.cuda.set_device(dev)
+            steps = GpuShardSteps(dev)
+            buf = torch.empty(max(16, hi - lo), dtype=torch.uint8, device=dev)[: hi - lo]
+            buf.copy_(host)
+            comm = Comm(device=dev)
+        res = ShardedBuilder(steps, comm).build(header, len(log), buf, lo, hi, opts)
+        out = res.out.cpu().numpy().tobytes()
+        with open(os.path.join(out_dir, f"rank{rank}.bin"), "wb") as f:
+            f.write(out)
+        meta = {"offset": res.out_offset, "slot_lo": res.slot_lo, "slot_hi": res.slot_hi, "path": res.path,
+                "rounds": res.rounds, "stats": res.stats, "n_pairs": res.n_pairs, "n_spill": res.n_spill}
+        with open(os.path.join(out_dir, f"rank{rank}.json"), "w") as f:
+            json.dump(meta, f)
+    finally:
+        dist.destroy_process_group()
+
+
+def run_world(log: bytes, world: int, opts_kw: dict, tmpdir: str, kind: str = "cpu"):
+    """Runs the sharded build over `world` processes; returns (spi bytes, per-rank metadata)."""
+    import torch.multiprocessing as mp
+    from sparkey.sharded import INDEX_HEADER_SIZE, _capacity, _slot_size, parse_log_header
+    from sparkey import _native
+    log_path = os.path.join(tmpdir, "log.spl")
+    with open(log_path, "wb") as f:
+        f.write(log)
+    mp.spawn(_worker, args=(world, free_port(), log_path, opts_kw, tmpdir, kind), nprocs=world, join=True)
+    h = parse_log_header(log[:84])
+    opts = _native.make_opts(**opts_kw)
+    size = INDEX_HEADER_SIZE + _capacity(h, opts) * _slot_size(h, opts, h["data_end"])
+    spi = bytearray(size)
+    metas = []
+    for r in range(world):
+        meta = json.load(open(os.path.join(tmpdir, f"rank{r}.json")))
+        data = open(os.path.join(tmpdir, f"rank{r}.bin"), "rb").read()
+        want = (INDEX_HEADER_SIZE if r == 0 else 0) + (meta["slot_hi"] - meta["slot_lo"]) * (size - INDEX_HEADER_SIZE) \
+            // max(1, _capacity(h, opts))
+        spi[meta["offset"]: meta["offset"] + want] = data[:want]
+        metas.append(meta)
+    return bytes(spi), metas
+
+
+class ThreadComm:
+    """In-process collectives between threads (one thread per rank): lets several ranks share one
+    GPU inside a single test process."""
+
+    def __init__(self, rank, world, shared):
+        self.rank, self.world, self.sh = rank, world, shared
+
+    def _exchange(self, obj):
+        import torch
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+        self.sh["slots"][self.rank] = obj
+        self.sh["barrier"].wait()
+        res = list(self.sh["slots"])
+        self.sh["barrier"].wait()
+        return res
+
+    def allgather_i64(self, vals):
+        import numpy as np
+        return np.array(self._exchange([int(v) for v in vals]), dtype=np.int64).reshape(self.world, -1)
+
+    def all_to_all(self, send, in_splits, out_splits, out_device):
+        import torch
+        pieces, at = [], 0
+        for n in in_splits:
+            pieces.append(send[at: at + int(n)])
+            at += int(n)
+        res = self._exchange(pieces)
+        got = [res[src][self.rank].to(out_device) for src in range(self.world)]
+        out = torch.cat(got) if got else send[:0]
+        self._exchange(None)  # keep senders' buffers alive until everyone copied
+        return out
+
+    def allgather_var(self, t, n, out_device):
+        res = self._exchange(t[:n])
+        out = [x.to(out_device).clone() for x in res]
+        self._exchange(None)
+        return out
+
+    def barrier(self):
+        self._exchange(None)
+
+
+def run_threads(log: bytes, world: int, opts_kw: dict, device=None):
+    """The sharded build with `world` ranks as threads of this process on one device."""
+    import threading
+    import torch
+    from sparkey import _native
+    from sparkey.sharded import INDEX_HEADER_SIZE, GpuShardSteps, ShardedBuilder, _capacity, _slot_size, \
+        parse_log_header, shard_layout
+    header = log[:84]
+    lay = shard_layout(header, len(log), world)
+    shared = {"barrier": threading.Barrier(world), "slots": [None] * world}
+    results, errors = [None] * world, []
+    dev = device or torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    all_steps = [GpuShardSteps(dev) for _ in range(world)]  # plans created on this thread
+
+    def run(rank):
+        try:
+            torch.cuda.set_device(dev)
+            lo, hi = lay.buffer_range(rank)
+            host = torch.frombuffer(bytearray(log[lo:hi] + bytes(16)), dtype=torch.uint8)[: hi - lo]
+            buf = torch.empty(max(16, hi - lo), dtype=torch.uint8, device=dev)[: hi - lo]
+            buf.copy_(host)
+            torch.cuda.synchronize()
+            steps = all_steps[rank]
+            res = ShardedBuilder(steps, ThreadComm(rank, world, shared)).build(
+                header, len(log), buf, lo, hi, _native.make_opts(**opts_kw))
+            torch.cuda.synchronize()
+            results[rank] = (res, res.out.cpu().numpy().tobytes())
+            steps.plan.close()
+        except BaseException as e:  # noqa: BLE001 -- reported by the caller
+            errors.append((rank, e))
+            shared["barrier"].abort()
+
+    threads = [threading.Thread(target=run, args=(r,)) for r in range(world)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    if errors:
+        raise errors[0][1]
+    h = parse_log_header(header)
+    opts = _native.make_opts(**opts_kw)
+    cap = _capacity(h, opts)
+    S = _slot_size(h, opts, h["data_end"])
+    spi = bytearray(INDEX_HEADER_SIZE + cap * S)
+    metas = []
+    for r in range(world):
+        res, data = results[r]
+        want = (INDEX_HEADER_SIZE if r == 0 else 0) + (res.slot_hi - res.slot_lo) * S
+        spi[res.out_offset: res.out_offset + want] = data[:want]
+        metas.append({"path": res.path, "rounds": res.rounds, "n_pairs": res.n_pairs, "n_spill": res.n_spill,
+                      "stats": res.stats})
+    return bytes(spi), metas

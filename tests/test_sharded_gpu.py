@@ -1,0 +1,89 @@
+"""Sharded build on the GPU: the sparkey_shard_* HIP steps driven by sparkey/sharded.py, 2-4 ranks
+sharing cuda:0 as threads of this process (in-process collectives; the RCCL transport is the
+bench's N > 1 path).  The assembled .spi must equal the oracle's single-process build byte for
+byte, and the single-GPU build of the same log."""
+import struct
+
+import numpy as np
+import pytest
+
+import oracle
+from helpers import diff_report, key_value_puts, make_log, random_puts
+from sharded_harness import run_threads
+
+pytestmark = pytest.mark.gpu
+
+IN_MEMORY, SORTING = 1, 2
+
+
+def check(native, log, world, seed=7, hash_size=0, method=IN_MEMORY, sparsity=0.0):
+    kw = dict(hash_size=hash_size, hash_seed=seed, sparsity=sparsity, method=method)
+    got, metas = run_threads(log, world, kw)
+    want = oracle.build_index(log, seed, hash_size=hash_size, sparsity=sparsity, method=method)
+    assert got == want, diff_report(got, want)
+    return metas
+
+
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_sharded_gpu_key_value(native, world):
+    metas = check(native, make_log(key_value_puts(20000)), world)
+    assert metas[0]["path"] == "sharded"
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_sharded_gpu_c2_shape(native, world):
+    """C2's record shape (16 B keys, 100 B values, fused framing) at 300K records."""
+    from sparkey import synth
+    log = synth.fixed_log(300000, 16, 100, seed=5).tobytes()
+    metas = check(native, log, world, seed=0x2545F491)
+    assert metas[0]["path"] == "sharded"
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_sharded_gpu_random_keys(native, seed):
+    log = make_log(random_puts(8000, seed=seed, kmin=0, kmax=130, vmax=500))
+    check(native, log, 3, seed=seed * 77, hash_size=8)
+
+
+def test_sharded_gpu_large_values(native):
+    """Records longer than 4 KiB: every rank frames with the serial walker."""
+    value = b"v" * 6000
+    log = make_log([(b"key_%d" % i, value) for i in range(600)])
+    check(native, log, 2, seed=17)
+
+
+def test_sharded_gpu_collision_pairs(native):
+    metas = check(native, make_log(key_value_puts(300000)), 2, seed=11, hash_size=4)
+    assert metas[0]["n_pairs"] > 0 and metas[0]["path"] == "sharded"
+
+
+def test_sharded_gpu_small_log(native):
+    check(native, make_log(key_value_puts(30)), 3)
+
+
+@pytest.mark.parametrize("method", [IN_MEMORY, SORTING])
+def test_sharded_gpu_deletes_gather(native, method):
+    log = make_log(key_value_puts(5000), deletes=[b"Key%d" % i for i in range(0, 5000, 7)])
+    metas = check(native, log, 2, seed=-5, method=method)
+    assert metas[0]["path"] == "gathered"
+
+
+def test_sharded_gpu_duplicates_gather(native):
+    puts = key_value_puts(5000) + [(b"Key%d" % i, b"again") for i in range(0, 5000, 13)]
+    metas = check(native, make_log(puts), 2, seed=5)
+    assert metas[0]["path"] == "gathered"
+
+
+def test_sharded_gpu_understated_header(native):
+    log = bytearray(make_log([(b"k%d" % i, b"v" * (i % 300)) for i in range(6000)]))
+    struct.pack_into("<q", log, 48, 10)
+    check(native, bytes(log), 3, seed=9)
+
+
+def test_sharded_gpu_matches_single(native):
+    from sparkey import synth
+    log = synth.mixed_log(100000, 8, 64, 100, seed=4).tobytes()
+    opts = native.make_opts(hash_seed=99)
+    single, _ = native.build_index_mem(log, opts)
+    got, metas = run_threads(log, 4, dict(hash_seed=99))
+    assert got == single, diff_report(got, single)
