@@ -182,7 +182,7 @@ def sharded(args, dev, world, rank):
     torch.cuda.synchronize(dev)
     dist.barrier()
     elapsed = time.perf_counter() - t_start
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.backend == "nccl" else "cpu")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
     assert res.path == "sharded" and res.stats["num_entries"] == n_total, (res.path, res.stats)
@@ -217,16 +217,23 @@ def main():
     ap.add_argument("--entries", type=int, default=10_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--backend", default="nccl", help="nccl (RCCL); gloo only to rehearse N > 1 ranks on one GPU")
+    ap.add_argument("--sharded", action="store_true", help="the sharded build even at N = 1 (rehearsal)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.backend == "gloo":
+        local_rank = 0  # rehearsal: every rank on the one GPU
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
-    if world > 1:
+    if world > 1 or args.sharded:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.backend)
         r = sharded(args, dev, world, rank)
         dist.destroy_process_group()
     else:
