@@ -137,8 +137,16 @@ class OracleError(RuntimeError):
         self.code = code
 
 
-def index_size(log: bytes, hash_size: int = 0, sparsity: float = 0.0) -> int:
-    return lib().oracle_index_size(log, len(log), hash_size, sparsity)
+def _log_arg(log):
+    """bytes, or a contiguous uint8 numpy array (large logs without a copy)."""
+    if hasattr(log, "ctypes") and hasattr(log, "nbytes"):
+        return ctypes.c_void_p(log.ctypes.data), int(log.nbytes)
+    return log, len(log)
+
+
+def index_size(log, hash_size: int = 0, sparsity: float = 0.0) -> int:
+    p, n = _log_arg(log)
+    return lib().oracle_index_size(p, n, hash_size, sparsity)
 
 
 def build_index(log: bytes, hash_seed: int, hash_size: int = 0, sparsity: float = 0.0,
@@ -149,7 +157,8 @@ def build_index(log: bytes, hash_seed: int, hash_size: int = 0, sparsity: float 
         raise OracleError(n, "index_size failed")
     out = ctypes.create_string_buffer(n)
     err = ctypes.create_string_buffer(256)
-    rc = lib().oracle_build_index(log, len(log), hash_size, sparsity, ctypes.c_int32(hash_seed).value,
+    lp, ln = _log_arg(log)
+    rc = lib().oracle_build_index(lp, ln, hash_size, sparsity, ctypes.c_int32(hash_seed).value,
                                   method, max_memory, out, n, err, 256)
     if rc < 0:
         raise OracleError(rc, err.value.decode())

@@ -1,0 +1,74 @@
+"""Full-size BASELINE.json configurations on the GPU, bit-exact against the oracle:
+C2 (10M x 16 B keys / 100 B values), C3 (100M, keys 8-64 B), C5 (C3 with SORTING), and the sharded
+build of C2 (4 ranks) against the single-GPU build."""
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from helpers import diff_report, index_header
+
+pytestmark = pytest.mark.gpu
+IN_MEMORY, SORTING = 1, 2
+
+
+def device_build(native, log_np, seed, method=IN_MEMORY):
+    """Log resident in HBM -> .spi resident in HBM -> host bytes."""
+    dev = torch.device("cuda", 0)
+    header = log_np[:84].tobytes()
+    opts = native.make_opts(hash_seed=seed, method=method)
+    n_out = native.index_size(header, opts)
+    d_log = torch.from_numpy(log_np).to(dev)
+    d_out = torch.empty(n_out, dtype=torch.uint8, device=dev)
+    plan = native.Plan(0)
+    torch.cuda.synchronize()
+    stats = plan.build(header, d_log.data_ptr(), log_np.size, d_out.data_ptr(), n_out, opts)
+    out = d_out.cpu().numpy().tobytes()
+    plan.close()
+    del d_log, d_out
+    torch.cuda.empty_cache()
+    return out, stats
+
+
+def test_c2_full_size(native):
+    from sparkey import synth
+    log = synth.fixed_log(10_000_000, 16, 100, seed=1)
+    got, stats = device_build(native, log, 0x2545F491)
+    want = oracle.build_index(log, 0x2545F491)
+    assert got == want, diff_report(got, want)
+    assert stats.placement_path == 0 and stats.framing_path == 0
+
+
+@pytest.fixture(scope="module")
+def c3_log():
+    from sparkey import synth
+    return synth.mixed_log(100_000_000, 8, 64, 100, seed=3)
+
+
+@pytest.fixture(scope="module")
+def c3_want(c3_log):
+    return oracle.build_index(c3_log, 77)
+
+
+def test_c3_100m_mixed_keys(native, c3_log, c3_want):
+    got, stats = device_build(native, c3_log, 77)
+    assert got == c3_want, diff_report(got, c3_want)
+    h = index_header(got)
+    assert h["numEntries"] == 100_000_000 and h["hashSize"] == 8 and h["addressSize"] == 8
+    assert stats.framing_path == 0 and stats.placement_path == 0
+
+
+def test_c5_100m_sorting(native, c3_log, c3_want):
+    """SORTING on the C3 log: identical to IN_MEMORY for unique keys (TestSparkeyWriter.java:9-36)."""
+    got, stats = device_build(native, c3_log, 77, method=SORTING)
+    assert got == c3_want, diff_report(got, c3_want)
+
+
+def test_sharded_c2_4_ranks_matches_single(native):
+    from sparkey import synth
+    from sharded_harness import run_threads
+    log = synth.fixed_log(10_000_000, 16, 100, seed=8)
+    single, _ = device_build(native, log, 4242)
+    got, metas = run_threads(log.tobytes(), 4, dict(hash_seed=4242))
+    assert all(m["path"] == "sharded" for m in metas)
+    assert got == single, diff_report(got, single)
