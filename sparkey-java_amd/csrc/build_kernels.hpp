@@ -26,6 +26,7 @@ constexpr int kStatSlotsPerBlock = 4096;
 constexpr int kPartBlock = 256;                   // radix partition of the entries by bucket
 constexpr int kPartItems = 16;
 constexpr int kPartTile = kPartBlock * kPartItems;
+constexpr int kPart2Block = 1024;                 // k_part2: one workgroup per coarse digit
 constexpr int kPart2MaxBits = 14;                 // fine digit of the partition (<= 16384 buckets)
 constexpr uint32_t kPlaceLdsMax = 1536;           // entries of a bucket staged in LDS
 constexpr uint32_t kMaxPartGroup = 64;            // slabs per partition tile

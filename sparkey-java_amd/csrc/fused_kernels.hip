@@ -565,34 +565,41 @@ __device__ __forceinline__ uint32_t digit_of(const BuildParams& P, uint32_t buck
   return (uint32_t)(((uint64_t)bucket * P.dmagic) >> 40);
 }
 
-// A partition tile is part_group consecutive slabs (<= kPartTile entries together).
+// A partition tile is part_group (<= 64) consecutive slabs, <= kPartTile entries together.
+// Wave 0 scans the slab counts with shuffles; slab_of maps a tile index to its slab, so every
+// thread then loads its entries with independent reads.
 struct SlabTile {
   uint32_t pre[kMaxPartGroup + 1];  // entry prefix over the tile's slabs
-  uint32_t ng;
+  uint8_t slab_of[kPartTile];
 };
 
-__device__ __forceinline__ void load_tile(const BuildParams& P, SlabTile& T, uint64_t g0) {
-  if (threadIdx.x == 0) {
-    const uint64_t ng = min((uint64_t)P.part_group, P.nslabs > g0 ? P.nslabs - g0 : 0);
-    uint32_t acc = 0;
-    T.pre[0] = 0;
-    for (uint64_t g = 0; g < ng; g++) {
-      acc += P.wcount[g0 + g];
-      T.pre[g + 1] = acc;
+__device__ __forceinline__ uint32_t load_tile(const BuildParams& P, SlabTile& T, uint64_t g0) {
+  const uint32_t ng = (uint32_t)min((uint64_t)P.part_group, P.nslabs > g0 ? P.nslabs - g0 : 0);
+  const int tid = threadIdx.x;
+  if (tid < 64) {
+    const uint32_t c = (uint32_t)tid < ng ? P.wcount[g0 + tid] : 0u;
+    uint32_t incl = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t t = __shfl_up(incl, o, 64);
+      if (tid >= o) incl += t;
     }
-    T.ng = (uint32_t)ng;
+    T.pre[tid] = incl - c;
+    if (tid == 63) T.pre[64] = incl;
   }
   __syncthreads();
+  const int lane = tid & 63;
+  for (uint32_t g = tid >> 6; g < ng; g += kPartBlock / 64) {
+    const uint32_t lo = T.pre[g], n = T.pre[g + 1] - lo;
+    for (uint32_t j = lane; j < n; j += 64) T.slab_of[lo + j] = (uint8_t)g;
+  }
+  __syncthreads();
+  return T.pre[64];
 }
 
-// Entry i of the tile (i < pre[ng]).
 __device__ __forceinline__ const Entry& tile_entry(const BuildParams& P, const SlabTile& T, uint64_t g0, uint32_t i) {
-  uint32_t lo = 0, hi = T.ng;  // largest g with pre[g] <= i
-  while (hi - lo > 1) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if (T.pre[mid] <= i) lo = mid; else hi = mid;
-  }
-  return P.ent[(g0 + lo) * (uint64_t)P.slab_cap + (i - T.pre[lo])];
+  const uint32_t g = T.slab_of[i];
+  return P.ent[(g0 + g) * (uint64_t)P.slab_cap + (i - T.pre[g])];
 }
 
 __global__ __launch_bounds__(kPartBlock) void k_part1_hist(BuildParams P) {
@@ -601,8 +608,7 @@ __global__ __launch_bounds__(kPartBlock) void k_part1_hist(BuildParams P) {
   if (build_aborted(P)) return;
   const uint64_t g0 = (uint64_t)blockIdx.x * P.part_group;
   hist[threadIdx.x] = 0;
-  load_tile(P, T, g0);
-  const uint32_t n = T.pre[T.ng];
+  const uint32_t n = load_tile(P, T, g0);
   for (uint32_t i = threadIdx.x; i < n; i += kPartBlock)
     atomicAdd(&hist[digit_of(P, bucket_of(P, tile_entry(P, T, g0, i).hash))], 1u);
   __syncthreads();
@@ -611,42 +617,36 @@ __global__ __launch_bounds__(kPartBlock) void k_part1_hist(BuildParams P) {
 
 __global__ __launch_bounds__(kPartBlock) void k_part1_scatter(BuildParams P) {
   __shared__ Entry stage[kPartTile];
-  __shared__ uint32_t hist[256];
   __shared__ uint32_t lbase[256];
   __shared__ uint32_t cursor[256];
-  __shared__ uint64_t sh64[kPartBlock];
+  __shared__ uint64_t sh64[kPartBlock / 64 + 1];
   __shared__ SlabTile T;
   if (build_aborted(P)) return;  // the host grows the workspace and redoes the build
   const uint64_t g0 = (uint64_t)blockIdx.x * P.part_group;
   const int tid = threadIdx.x;
-  hist[tid] = 0;
+  const uint32_t h = P.p1_hist[(uint64_t)tid * P.p1_tiles + blockIdx.x];
+  lbase[tid] = (uint32_t)block_excl_sum<kPartBlock>(h, sh64, nullptr);
   cursor[tid] = 0;
-  load_tile(P, T, g0);
-  const uint32_t n = T.pre[T.ng];
+  const uint32_t n = load_tile(P, T, g0);
   Entry v[kPartItems];
   uint32_t d[kPartItems];
 #pragma unroll
   for (int i = 0; i < kPartItems; i++) {
     const uint32_t idx = (uint32_t)i * kPartBlock + tid;
+    if (idx < n) v[i] = tile_entry(P, T, g0, idx);
+  }
+#pragma unroll
+  for (int i = 0; i < kPartItems; i++) {
+    const uint32_t idx = (uint32_t)i * kPartBlock + tid;
     d[i] = 0xffffffffu;
     if (idx < n) {
-      v[i] = tile_entry(P, T, g0, idx);
       d[i] = digit_of(P, bucket_of(P, v[i].hash));
-      atomicAdd(&hist[d[i]], 1u);
+      stage[lbase[d[i]] + atomicAdd(&cursor[d[i]], 1u)] = v[i];
     }
   }
   __syncthreads();
-  uint64_t total;
-  const uint64_t ex = block_exclusive_scan<uint64_t, OpAdd, kPartBlock>(hist[tid], sh64, OpAdd(), &total);
-  lbase[tid] = (uint32_t)ex;
-  __syncthreads();
-#pragma unroll
-  for (int i = 0; i < kPartItems; i++) {
-    if (d[i] != 0xffffffffu) stage[lbase[d[i]] + atomicAdd(&cursor[d[i]], 1u)] = v[i];
-  }
-  __syncthreads();
   // coalesced write-out: LDS position i -> global offset of its digit run
-  for (uint32_t i = tid; i < (uint32_t)total; i += kPartBlock) {
+  for (uint32_t i = tid; i < n; i += kPartBlock) {
     const Entry en = stage[i];
     const uint32_t dd = digit_of(P, bucket_of(P, en.hash));
     const uint64_t dst = P.p1_off[(uint64_t)dd * P.p1_tiles + blockIdx.x] + (i - lbase[dd]);
@@ -664,9 +664,9 @@ __global__ void k_dense_slabs(BuildParams P) {
 }
 
 // Pass 2: one workgroup per coarse digit splits it into its bpp buckets.
-__global__ __launch_bounds__(kPartBlock) void k_part2(BuildParams P) {
+__global__ __launch_bounds__(kPart2Block) void k_part2(BuildParams P) {
   extern __shared__ __attribute__((aligned(16))) uint32_t dyn[];  // hist[nbins] ++ cur[nbins]
-  __shared__ uint64_t sh64[kPartBlock];
+  __shared__ uint64_t sh64[kPart2Block / 64 + 1];
   if (build_aborted(P)) return;
   const uint32_t dpart = blockIdx.x;
   const uint64_t lo = P.p1_off[(uint64_t)dpart * P.p1_tiles];
@@ -676,19 +676,18 @@ __global__ __launch_bounds__(kPartBlock) void k_part2(BuildParams P) {
   uint32_t* hist = dyn;
   uint32_t* cur = dyn + nbins;
   const int tid = threadIdx.x;
-  for (uint32_t b = tid; b < nbins; b += kPartBlock) { hist[b] = 0; cur[b] = 0; }
+  for (uint32_t b = tid; b < nbins; b += kPart2Block) hist[b] = 0;
   __syncthreads();
-  for (uint64_t i = lo + tid; i < hi; i += kPartBlock) atomicAdd(&hist[bucket_of(P, P.ent3[i].hash) - b0], 1u);
+  for (uint64_t i = lo + tid; i < hi; i += kPart2Block) atomicAdd(&hist[bucket_of(P, P.ent3[i].hash) - b0], 1u);
   __syncthreads();
-  // exclusive scan of the bins (nbins / kPartBlock consecutive bins per thread)
-  const uint32_t per = (nbins + kPartBlock - 1) / kPartBlock;
+  // exclusive scan of the bins (per consecutive bins per thread)
+  const uint32_t per = (nbins + kPart2Block - 1) / kPart2Block;
   uint64_t local = 0;
   for (uint32_t q = 0; q < per; q++) {
     const uint32_t b = tid * per + q;
     if (b < nbins) local += hist[b];
   }
-  const uint64_t ex = block_exclusive_scan<uint64_t, OpAdd, kPartBlock>(local, sh64, OpAdd(), nullptr);
-  uint64_t run = ex;
+  uint64_t run = block_excl_sum<kPart2Block>(local, sh64, nullptr);
   for (uint32_t q = 0; q < per; q++) {
     const uint32_t b = tid * per + q;
     if (b < nbins) {
@@ -702,7 +701,7 @@ __global__ __launch_bounds__(kPartBlock) void k_part2(BuildParams P) {
     }
   }
   __syncthreads();
-  for (uint64_t i = lo + tid; i < hi; i += kPartBlock) {
+  for (uint64_t i = lo + tid; i < hi; i += kPart2Block) {
     const Entry en = P.ent3[i];
     const uint32_t b = bucket_of(P, en.hash) - b0;
     P.ent2[lo + atomicAdd(&cur[b], 1u)] = en;
@@ -835,7 +834,7 @@ void launch_partition1(const BuildParams& P, hipStream_t s) {
 
 void launch_partition(const BuildParams& P, hipStream_t s, StageTimer* tm) {
   launch_partition1(P, s);
-  hipLaunchKernelGGL(k_part2, dim3(256), dim3(kPartBlock), (size_t)(2u * P.bpp) * sizeof(uint32_t), s, P);
+  hipLaunchKernelGGL(k_part2, dim3(256), dim3(kPart2Block), (size_t)(2u * P.bpp) * sizeof(uint32_t), s, P);
   tm->mark("partition", s);
 }
 

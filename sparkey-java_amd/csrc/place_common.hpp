@@ -44,17 +44,8 @@ __device__ __forceinline__ void bucket_scan(const uint32_t* cnt, uint32_t* base,
     run = max(run, vals[i]);
   }
   // exclusive max-scan of per-thread maxima
-  shm[tid] = run;
-  __syncthreads();
-  for (int o = 1; o < kPlaceBlock; o <<= 1) {
-    int64_t t = tid >= o ? shm[tid - o] : -(1ll << 40);
-    __syncthreads();
-    if (tid >= o) shm[tid] = max(shm[tid], t);
-    __syncthreads();
-  }
-  int64_t m = tid ? shm[tid - 1] : -(1ll << 40);
-  const int64_t all_max = shm[kPlaceBlock - 1];
-  __syncthreads();
+  int64_t all_max;
+  int64_t m = block_exclusive_scan<int64_t, OpMaxI64, kPlaceBlock>(run, shm, OpMaxI64(), &all_max);
 #pragma unroll
   for (int i = 0; i < kBinsPerThread; i++) {
     m = max(m, vals[i]);

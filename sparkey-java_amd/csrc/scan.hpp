@@ -26,19 +26,79 @@ struct OpMaxPlus {
   __device__ __forceinline__ MaxPlus identity() const { return MaxPlus{0, 0}; }
 };
 
+struct OpMaxI64 {
+  __device__ __forceinline__ int64_t operator()(int64_t a, int64_t b) const { return a > b ? a : b; }
+  __device__ __forceinline__ int64_t identity() const { return -(1ll << 40); }
+};
+
+__device__ __forceinline__ uint64_t shfl_up_any(uint64_t v, int o) { return __shfl_up(v, o, 64); }
+__device__ __forceinline__ int64_t shfl_up_any(int64_t v, int o) { return __shfl_up(v, o, 64); }
+__device__ __forceinline__ uint32_t shfl_up_any(uint32_t v, int o) { return __shfl_up(v, o, 64); }
+__device__ __forceinline__ MaxPlus shfl_up_any(MaxPlus v, int o) {
+  MaxPlus r;
+  r.c = __shfl_up(v.c, o, 64);
+  r.a = __shfl_up(v.a, o, 64);
+  return r;
+}
+
+// Block-wide exclusive scan (op(a, b) = "a then b"): shuffles inside each wave, one LDS round for
+// the wave totals.  sh needs at least BLOCK / 64 + 1 slots.
 template <class T, class Op, int BLOCK>
 __device__ T block_exclusive_scan(T v, T* sh, Op op, T* total) {
-  const int tid = threadIdx.x;
-  sh[tid] = v;
-  __syncthreads();
-  for (int o = 1; o < BLOCK; o <<= 1) {
-    T t = tid >= o ? sh[tid - o] : op.identity();
-    __syncthreads();
-    if (tid >= o) sh[tid] = op(t, sh[tid]);
-    __syncthreads();
+  constexpr int NW = BLOCK / 64;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  T incl = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const T t = shfl_up_any(incl, o);
+    if (lane >= o) incl = op(t, incl);
   }
-  if (total) *total = sh[BLOCK - 1];
-  T ex = tid ? sh[tid - 1] : op.identity();
+  if (lane == 63) sh[w] = incl;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    T run = op.identity();
+    for (int i = 0; i < NW; i++) {
+      const T t = sh[i];
+      sh[i] = run;
+      run = op(run, t);
+    }
+    sh[NW] = run;
+  }
+  __syncthreads();
+  T exw = shfl_up_any(incl, 1);
+  if (lane == 0) exw = op.identity();
+  const T ex = op(sh[w], exw);
+  if (total) *total = sh[NW];
+  __syncthreads();
+  return ex;
+}
+
+// Exclusive sum over a block of BLOCK threads (wave shuffles, one LDS round for the wave totals).
+// sh needs BLOCK / 64 + 1 slots.
+template <int BLOCK>
+__device__ __forceinline__ uint64_t block_excl_sum(uint64_t v, uint64_t* sh, uint64_t* total) {
+  constexpr int NW = BLOCK / 64;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint64_t incl = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint64_t t = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += t;
+  }
+  if (lane == 63) sh[w] = incl;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t run = 0;
+    for (int i = 0; i < NW; i++) {
+      const uint64_t t = sh[i];
+      sh[i] = run;
+      run += t;
+    }
+    sh[NW] = run;
+  }
+  __syncthreads();
+  const uint64_t ex = sh[w] + incl - v;
+  if (total) *total = sh[NW];
   __syncthreads();
   return ex;
 }
