@@ -142,8 +142,8 @@ __global__ __launch_bounds__(kPlaceBlock) void k_summary(BuildParams P) {
   __shared__ uint32_t cnt[kBucket];
   __shared__ uint32_t base[kBucket];
   __shared__ int32_t M[kBucket];
-  __shared__ uint64_t sh64[kPlaceBlock];
-  __shared__ int64_t shm[kPlaceBlock];
+  __shared__ uint64_t sh64[kPlaceBlock / 64 + 1];
+  __shared__ int64_t shm[kPlaceBlock / 64 + 1];
   if (build_aborted(P)) return;
   const uint64_t b = P.b_lo + blockIdx.x;
   const uint64_t start = b << kBucketShift;
@@ -187,8 +187,8 @@ __global__ __launch_bounds__(kPlaceBlock) void k_place(BuildParams P, int sort_o
   __shared__ uint32_t base[kBucket];
   __shared__ int32_t M[kBucket];
   __shared__ int32_t slot_of[kBucket];
-  __shared__ uint64_t sh64[kPlaceBlock];
-  __shared__ int64_t shm[kPlaceBlock];
+  __shared__ uint64_t sh64[kPlaceBlock / 64 + 1];
+  __shared__ int64_t shm[kPlaceBlock / 64 + 1];
   if (build_aborted(P)) return;
   const uint64_t b = P.b_lo + blockIdx.x;
   if (only_big && P.bcount[b] <= kPlaceLdsMax) return;

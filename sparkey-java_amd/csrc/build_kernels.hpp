@@ -16,6 +16,8 @@ constexpr int kEmitExtra = 1024 + 16;             // bytes staged past a chunk f
 constexpr int kBucketShift = 10;                  // placement bucket: 1024 slots
 constexpr int kBucket = 1 << kBucketShift;
 constexpr int kPlaceBlock = 256;
+constexpr int kPlaceLdsBlock = 512;              // k_place_lds: one bucket per workgroup
+constexpr int kLdsBins = kBucket / kPlaceLdsBlock;
 constexpr int kBinsPerThread = kBucket / kPlaceBlock;
 constexpr uint32_t kGroupMax = 64;                // equal-wanted-slot group sorted by insertion
 constexpr int kScanBlock = 256;

@@ -712,15 +712,15 @@ __global__ __launch_bounds__(kPart2Block) void k_part2(BuildParams P) {
 // k_place_lds: one bucket per workgroup, entries staged in LDS (buckets above kPlaceLdsMax
 // entries are left to the global-memory k_place, flagged in P.st->big_buckets).
 // ================================================================================================
-__global__ __launch_bounds__(kPlaceBlock) void k_place_lds(BuildParams P) {
+__global__ __launch_bounds__(kPlaceLdsBlock) void k_place_lds(BuildParams P) {
   __shared__ uint32_t cnt[kBucket];
   __shared__ uint32_t base[kBucket];
   __shared__ int32_t M[kBucket];
   __shared__ int32_t aux[kBucket];  // cursors, then slot -> sorted index
   __shared__ Entry raw[kPlaceLdsMax];
   __shared__ uint16_t order[kPlaceLdsMax];
-  __shared__ uint64_t sh64[kPlaceBlock];
-  __shared__ int64_t shm[kPlaceBlock];
+  __shared__ uint64_t sh64[kPlaceLdsBlock / 64 + 1];
+  __shared__ int64_t shm[kPlaceLdsBlock / 64 + 1];
   if (build_aborted(P)) return;
   const uint64_t b = P.b_lo + blockIdx.x;
   const uint64_t start = b << kBucketShift;
@@ -732,23 +732,23 @@ __global__ __launch_bounds__(kPlaceBlock) void k_place_lds(BuildParams P) {
     if (tid == 0) atomicOr(&P.st->big_buckets, 1u);
     return;
   }
-  for (int t = tid; t < kBucket; t += kPlaceBlock) { cnt[t] = 0; aux[t] = 0; }
+  for (int t = tid; t < kBucket; t += kPlaceLdsBlock) { cnt[t] = 0; aux[t] = 0; }
   __syncthreads();
-  for (uint32_t i = tid; i < n; i += kPlaceBlock) {
+  for (uint32_t i = tid; i < n; i += kPlaceLdsBlock) {
     const Entry en = P.ent2[eoff + i];
     raw[i] = en;
     atomicAdd(&cnt[fast_mod(en.hash, P.mod) - start], 1u);
   }
   __syncthreads();
-  bucket_scan(cnt, base, M, sh64, shm, nullptr);
-  for (uint32_t i = tid; i < n; i += kPlaceBlock) {
+  bucket_scan<kPlaceLdsBlock>(cnt, base, M, sh64, shm, nullptr);
+  for (uint32_t i = tid; i < n; i += kPlaceLdsBlock) {
     const uint32_t w = (uint32_t)(fast_mod(raw[i].hash, P.mod) - start);
     order[base[w] + atomicAdd((uint32_t*)&aux[w], 1u)] = (uint16_t)i;
   }
   __syncthreads();
   // equal wanted slots: address order; equal hashes -> duplicate-key candidates
-  for (int q = 0; q < kBinsPerThread; q++) {
-    const int s = tid * kBinsPerThread + q;
+  for (int q = 0; q < kLdsBins; q++) {
+    const int s = tid * kLdsBins + q;
     const uint32_t g = cnt[s];
     if (g < 2) continue;
     uint16_t* grp = order + base[s];
@@ -778,10 +778,10 @@ __global__ __launch_bounds__(kPlaceBlock) void k_place_lds(BuildParams P) {
   __syncthreads();
   if (P.st->full) return;
   const int64_t x = P.carry[b];
-  for (int t = tid; t < kBucket; t += kPlaceBlock) aux[t] = -1;
+  for (int t = tid; t < kBucket; t += kPlaceLdsBlock) aux[t] = -1;
   __syncthreads();
-  for (int q = 0; q < kBinsPerThread; q++) {
-    const int s = tid * kBinsPerThread + q;
+  for (int q = 0; q < kLdsBins; q++) {
+    const int s = tid * kLdsBins + q;
     const uint32_t g = cnt[s];
     if (!g) continue;
     const int64_t shift = max(x, (int64_t)M[s]);
@@ -797,7 +797,7 @@ __global__ __launch_bounds__(kPlaceBlock) void k_place_lds(BuildParams P) {
     }
   }
   __syncthreads();
-  for (int64_t t = x + tid; t < bsize; t += kPlaceBlock) {
+  for (int64_t t = x + tid; t < bsize; t += kPlaceLdsBlock) {
     const int32_t j = aux[t];
     if (j >= 0) {
       const Entry en = raw[order[j]];
@@ -839,7 +839,7 @@ void launch_partition(const BuildParams& P, hipStream_t s, StageTimer* tm) {
 }
 
 void launch_place_buckets(const BuildParams& P, hipStream_t s) {
-  if (P.b_hi > P.b_lo) hipLaunchKernelGGL(k_place_lds, dim3((unsigned)(P.b_hi - P.b_lo)), dim3(kPlaceBlock), 0, s, P);
+  if (P.b_hi > P.b_lo) hipLaunchKernelGGL(k_place_lds, dim3((unsigned)(P.b_hi - P.b_lo)), dim3(kPlaceLdsBlock), 0, s, P);
   launch_place_global(P, s, 0, 1);  // buckets above kPlaceLdsMax entries (normally none)
 }
 

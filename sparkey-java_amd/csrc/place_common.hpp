@@ -23,21 +23,23 @@ __device__ __forceinline__ void bucket_histogram(const BuildParams& P, uint64_t 
   __syncthreads();
 }
 
-// For the bucket's bins (kBinsPerThread consecutive bins per thread): exclusive base[s] and the
+// For the bucket's bins (BINS consecutive bins per thread): exclusive base[s] and the
 // inclusive prefix max M(s) of (s - base[s]) over occupied bins.
+template <int BLOCK = kPlaceBlock>
 __device__ __forceinline__ void bucket_scan(const uint32_t* cnt, uint32_t* base, int32_t* M, uint64_t* sh64,
                                             int64_t* shm, uint32_t* last_max) {
+  constexpr int BINS = kBucket / BLOCK;
   const int tid = threadIdx.x;
-  const int s0 = tid * kBinsPerThread;
+  const int s0 = tid * BINS;
   uint64_t local = 0;
 #pragma unroll
-  for (int i = 0; i < kBinsPerThread; i++) local += cnt[s0 + i];
-  const uint64_t pre = block_exclusive_scan<uint64_t, OpAdd, kPlaceBlock>(local, sh64, OpAdd(), nullptr);
+  for (int i = 0; i < BINS; i++) local += cnt[s0 + i];
+  const uint64_t pre = block_exclusive_scan<uint64_t, OpAdd, BLOCK>(local, sh64, OpAdd(), nullptr);
   int64_t run = -(1ll << 40);
   uint64_t acc = pre;
-  int64_t vals[kBinsPerThread];
+  int64_t vals[BINS];
 #pragma unroll
-  for (int i = 0; i < kBinsPerThread; i++) {
+  for (int i = 0; i < BINS; i++) {
     base[s0 + i] = (uint32_t)acc;
     vals[i] = cnt[s0 + i] ? (int64_t)(s0 + i) - (int64_t)acc : -(1ll << 40);
     acc += cnt[s0 + i];
@@ -45,9 +47,9 @@ __device__ __forceinline__ void bucket_scan(const uint32_t* cnt, uint32_t* base,
   }
   // exclusive max-scan of per-thread maxima
   int64_t all_max;
-  int64_t m = block_exclusive_scan<int64_t, OpMaxI64, kPlaceBlock>(run, shm, OpMaxI64(), &all_max);
+  int64_t m = block_exclusive_scan<int64_t, OpMaxI64, BLOCK>(run, shm, OpMaxI64(), &all_max);
 #pragma unroll
-  for (int i = 0; i < kBinsPerThread; i++) {
+  for (int i = 0; i < BINS; i++) {
     m = max(m, vals[i]);
     M[s0 + i] = (int32_t)max(m, (int64_t)INT32_MIN);
   }
