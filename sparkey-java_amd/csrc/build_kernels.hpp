@@ -31,7 +31,8 @@ constexpr int kPartTile = kPartBlock * kPartItems;
 constexpr int kPart2Block = 1024;                 // k_part2: one workgroup per coarse digit
 constexpr int kPart2MaxBits = 14;                 // fine digit of the partition (<= 16384 buckets)
 constexpr uint32_t kPlaceLdsMax = 1536;           // entries of a bucket staged in LDS
-constexpr uint32_t kMaxPartGroup = 64;            // slabs per partition tile
+constexpr uint32_t kMaxPartGroup = 64;
+constexpr int kCandCap = 448;                     // k_frame balanced walk: candidates per wave            // slabs per partition tile
 
 // One log record as the placement sees it: 16 bytes, AoS so every access is one dwordx4.
 struct alignas(16) Entry {

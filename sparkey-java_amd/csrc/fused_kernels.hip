@@ -321,7 +321,100 @@ __global__ __launch_bounds__(64) void k_frame(BuildParams P) {
   long long max_exit = -1;
   int32_t c_min_steps = 0;
   unsigned long long dbg_iters = 0;
-  {
+  // Balanced walk (C = 128, masks in registers, canonical one-byte VLQs): the wave's candidates go
+  // to one LDS list and lane L walks candidates L, L + 64, ..., so the walk takes about the mean
+  // work per lane instead of the largest; each lane then folds its own chunk's results.
+  // cand[i] = start | (exit - start) << 14 | steps << 22 | survived << 31 (region offsets).
+  bool balanced = false;
+  if (P.fr_fast && nwl <= 2) {
+    uint32_t* cand = reinterpret_cast<uint32_t*>(lds + P.fr_rgn_bytes);
+    const bool has = act && cand_end > s;
+    const uint32_t cnt_c = has ? (uint32_t)(__builtin_popcountll(m0) + __builtin_popcountll(m1)) : 0u;
+    uint32_t incl = cnt_c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t t = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += t;
+    }
+    const uint32_t T = __shfl(incl, 63, 64);
+    const uint32_t cpre = incl - cnt_c;
+    if (T <= (uint32_t)kCandCap) {
+      balanced = true;
+      {  // enumerate: lane's candidates in ascending order at cand[cpre ..)
+        unsigned long long a0 = has ? m0 : 0ull, a1 = has ? m1 : 0ull;
+        uint32_t o = cpre;
+        const uint32_t base = (uint32_t)(s - R0);
+        while (__any((a0 | a1) != 0ull)) {
+          if (a0) {
+            cand[o++] = base + (uint32_t)__builtin_ctzll(a0);
+            a0 &= a0 - 1;
+          } else if (a1) {
+            cand[o++] = base + 64u + (uint32_t)__builtin_ctzll(a1);
+            a1 &= a1 - 1;
+          }
+        }
+      }
+      __syncthreads();
+      const int64_t lim64 = log_len - R0;
+      const int32_t lim = lim64 > 0x7fffffff ? 0x7fffffff : (int32_t)lim64;
+      const int32_t de = (int32_t)min((int64_t)0x7fffffff, P.data_end - R0);
+      const int32_t ruse = (int32_t)(RUSE - R0);
+      const int32_t mk = (int32_t)P.max_key_len, mv = (int32_t)P.max_value_len;
+      const int32_t look = (int32_t)LOOK;
+      uint32_t gi = (uint32_t)lane, cur = 0;
+      int32_t rp = -1, rst = 0, rex = -1, st = 0, re = 0, rstop = 0;
+      for (;;) {
+        if (rp < 0 && gi < T) {
+          cur = gi;
+          gi += 64;
+          rst = (int32_t)cand[cur];
+          rp = rst;
+          rex = -1;
+          st = 0;
+          re = min((((rst >> cs) + 1) << cs), de);
+          rstop = min(min(re + look, de), ruse);
+        }
+        if (!__any(rp >= 0)) break;
+        dbg_iters++;
+        if (rp >= 0) {
+          const uint64_t x = rgn_u64(rgn, (uint32_t)rp);
+          const int32_t b0 = (int32_t)(x & 0xff), b1 = (int32_t)((x >> 8) & 0xff);
+          const int32_t klen = b0 ? b0 - 1 : b1;
+          const int32_t vlen = b0 ? b1 : 0;
+          const bool ok = (x & 0x8080ull) == 0 && (b0 || !P.no_deletes) && klen <= mk && vlen <= mv &&
+                          rp + 2 + klen <= lim;
+          if (!ok) {
+            rp = -1;  // dead: cand[cur] keeps its bare start
+          } else {
+            if (rex < 0) st++;
+            rp += 2 + klen + vlen;
+            if (rex < 0 && rp >= re) rex = rp;
+            if (rp >= rstop) {
+              cand[cur] = (uint32_t)rst | ((uint32_t)(rex - rst) << 14) | ((uint32_t)st << 22) | 0x80000000u;
+              rp = -1;
+            }
+          }
+        }
+      }
+      __syncthreads();
+      // fold the lane's own chunk
+      for (uint32_t i = 0; i < cnt_c; i++) {
+        const uint32_t v = cand[cpre + i];
+        if (v & 0x80000000u) {
+          const uint32_t st0 = v & 0x3fffu;
+          const unsigned long long pe = (unsigned long long)(R0 + st0 + ((v >> 14) & 0xffu));
+          if (nsurv == 0) {
+            c_min = (unsigned long long)(R0 + st0);
+            c_min_steps = (int32_t)((v >> 22) & 0x1ffu);
+          }
+          nsurv++;
+          min_exit = min(min_exit, pe);
+          max_exit = max(max_exit, (long long)pe);
+        }
+      }
+    }
+  }
+  if (!balanced) {
     int wi = 0;
     unsigned long long m = (act && cand_end > s) ? mask_word(0) : 0ull;
     bool done = !act || cand_end <= s;
@@ -814,7 +907,8 @@ __global__ __launch_bounds__(kPlaceLdsBlock) void k_place_lds(BuildParams P) {
 void launch_frame_fused(const BuildParams& P, hipStream_t s, StageTimer* tm) {
   if (P.fr_nchunks == 0) return;
   const uint64_t nwaves = (P.fr_nchunks + P.fr_w - 1) / P.fr_w;
-  const size_t lds = (size_t)P.fr_rgn_bytes + (size_t)P.fr_w * P.fr_mask_words * 8;
+  // masks (when they do not fit in registers) or the balanced walk's candidate list
+  const size_t lds = (size_t)P.fr_rgn_bytes + std::max<size_t>((size_t)P.fr_w * P.fr_mask_words * 8, kCandCap * 4);
   hipLaunchKernelGGL(k_frame, dim3((unsigned)nwaves), dim3(64), lds, s, P);
   scan_exclusive<uint32_t, uint64_t, OpAdd>(P.wcount, P.woff, P.nslabs, (uint64_t*)&P.st->n_records, OpAdd(),
                                             P.scan_scratch_u64, s);
