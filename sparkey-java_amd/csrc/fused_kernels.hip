@@ -248,9 +248,25 @@ __global__ __launch_bounds__(64) void k_frame(BuildParams P) {
   };
 
   // ---- stage: [R0, R0 + RLEN) once, coalesced, 16 bytes per lane per step ----
-  for (int v = lane; v < (int)((RLEN + 15) >> 4); v += 64) {
-    const uint4 val = load16_guarded(P.log, R0 + 16ll * v, log_len);
-    *reinterpret_cast<uint4*>(rgn + rswz(16u * v)) = val;
+  {
+    const int nvec = (int)((RLEN + 15) >> 4);
+    if (R0 + 16ll * nvec <= log_len) {  // 4 loads in flight per lane, then their LDS stores
+      const uint4* src = reinterpret_cast<const uint4*>(P.log + R0);
+      for (int v0 = 0; v0 < nvec; v0 += 256) {
+        // branch-free: lanes past the end repeat the last vector (same bytes, same place)
+        uint4 t[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) t[i] = src[min(v0 + 64 * i + lane, nvec - 1)];
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+          *reinterpret_cast<uint4*>(rgn + rswz(16u * (uint32_t)min(v0 + 64 * i + lane, nvec - 1))) = t[i];
+      }
+    } else {
+      for (int v = lane; v < nvec; v += 64) {
+        const uint4 val = load16_guarded(P.log, R0 + 16ll * v, log_len);
+        *reinterpret_cast<uint4*>(rgn + rswz(16u * v)) = val;
+      }
+    }
   }
   __syncthreads();
   mark(0);
