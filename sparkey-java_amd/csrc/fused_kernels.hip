@@ -181,17 +181,11 @@ __device__ __forceinline__ uint4 load16_guarded(const uint8_t* log, int64_t a, i
   return *reinterpret_cast<uint4*>(tmp);
 }
 
-// 16-byte-unit XOR swizzle of the region (a bijection on every 256-byte block): lanes reading the
-// same offset of their own chunk fall on different LDS banks.
-__device__ __forceinline__ uint32_t rswz(uint32_t o) {
-  const uint32_t u = o >> 4;
-  return ((u ^ ((u >> 4) & 15u)) << 4) | (o & 15u);
-}
 // 8 bytes at any region offset (two aligned 8-byte reads; the region is allocated in 256 B blocks)
 __device__ __forceinline__ uint64_t rgn_u64(const uint8_t* r, uint32_t o) {
   const uint32_t a = o & ~7u;
-  const uint64_t lo = *reinterpret_cast<const uint64_t*>(r + rswz(a));
-  const uint64_t hi = *reinterpret_cast<const uint64_t*>(r + rswz(a + 8));
+  const uint64_t lo = *reinterpret_cast<const uint64_t*>(r + a);
+  const uint64_t hi = *reinterpret_cast<const uint64_t*>(r + a + 8);
   const uint32_t sh = (o & 7u) * 8u;
   return sh ? (lo >> sh) | (hi << (64 - sh)) : lo;
 }
@@ -213,7 +207,7 @@ __device__ __forceinline__ RecHdr decode_rgn(const uint8_t* r, int64_t R0, int64
     if (first == 0) { h.put = 0; h.klen = second; h.vlen = 0; }
     else { h.put = 1; h.klen = first - 1; h.vlen = second; }
   } else {
-    auto at = [&](int64_t a) -> uint32_t { return r[rswz((uint32_t)(a - R0))]; };
+    auto at = [&](int64_t a) -> uint32_t { return r[(uint32_t)(a - R0)]; };
     h = decode_header(at, p, p + 12);
   }
   if (h.rc == 0 && p + h.hlen > avail) h.rc = kErrCorruptLog;
@@ -228,7 +222,6 @@ __global__ __launch_bounds__(64) void k_frame(BuildParams P) {
   const int64_t C = 1ll << cs;
   const int W = P.fr_w;
   const int64_t LOOK = P.fr_look;
-  const int nwords = P.fr_mask_words;
   const int64_t log_len = (int64_t)P.log_len;
   const uint64_t kf = P.fr_k0;  // chunk of the framing entry
   const uint64_t k0 = kf + wv * (uint64_t)W;
@@ -237,7 +230,6 @@ __global__ __launch_bounds__(64) void k_frame(BuildParams P) {
   const int64_t RLEN = ((int64_t)nw << cs) + LOOK + 16;  // staged bytes [R0, R0 + RLEN)
   const int64_t RUSE = R0 + RLEN - 16;                     // headers decodable in LDS below this
   uint8_t* rgn = lds;
-  unsigned long long* masks = reinterpret_cast<unsigned long long*>(lds + P.fr_rgn_bytes);
   unsigned long long t_prev = P.dbg ? __builtin_amdgcn_s_memtime() : 0;
   auto mark = [&](int i) {  // diagnostic only: cycles per phase, per wave (no atomics)
     if (P.dbg && lane == 0) {
@@ -259,12 +251,12 @@ __global__ __launch_bounds__(64) void k_frame(BuildParams P) {
         for (int i = 0; i < 4; i++) t[i] = src[min(v0 + 64 * i + lane, nvec - 1)];
 #pragma unroll
         for (int i = 0; i < 4; i++)
-          *reinterpret_cast<uint4*>(rgn + rswz(16u * (uint32_t)min(v0 + 64 * i + lane, nvec - 1))) = t[i];
+          *reinterpret_cast<uint4*>(rgn + 16u * (uint32_t)min(v0 + 64 * i + lane, nvec - 1)) = t[i];
       }
     } else {
       for (int v = lane; v < nvec; v += 64) {
         const uint4 val = load16_guarded(P.log, R0 + 16ll * v, log_len);
-        *reinterpret_cast<uint4*>(rgn + rswz(16u * v)) = val;
+        *reinterpret_cast<uint4*>(rgn + 16u * v) = val;
       }
     }
   }
@@ -280,10 +272,11 @@ __global__ __launch_bounds__(64) void k_frame(BuildParams P) {
   const bool passthrough = k > kf && s + P.max_rec_len - 1 >= e;
   const int64_t cand_end = !act || passthrough ? s : (k == kf ? s + 1 : min(e, s + P.max_rec_len));
 
-  // ---- 1 screen: 64 candidate starts per mask word from 9 aligned u64 loads issued together,
-  //      8 per SWAR step (branch-free); masks stay in registers when maxRecLen <= 128 ----
+  // ---- 1 screen: one flag bit per byte of the wave's chunks (is it a plausible record start?),
+  //      lanes on consecutive 8-byte words, 8 positions per SWAR step; a chunk's mask words are
+  //      then its slice of the bitmap.  Masks stay in registers when maxRecLen <= 128. ----
   const int nwl = (int)((min(C, P.max_rec_len) + 63) >> 6);
-  unsigned long long m0 = 0, m1 = 0;
+  unsigned long long* flags = reinterpret_cast<unsigned long long*>(lds + P.fr_rgn_bytes);
   {
     constexpr uint64_t H = 0x8080808080808080ull, L7 = 0x7f7f7f7f7f7f7f7full, ONES = 0x0101010101010101ull;
     // per byte: b <= T with b < 128 (T >= 127: every byte); thresholds replicated once, outside the loop
@@ -293,42 +286,41 @@ __global__ __launch_bounds__(64) void k_frame(BuildParams P) {
     const uint64_t rv = ONES * (uint64_t)(min(P.max_value_len, (int64_t)126) + 1);
     const uint64_t rd = ONES * (uint64_t)(min(P.max_key_len, (int64_t)126) + 1);
     auto le_rep = [&](uint64_t x, uint64_t rep, bool all) -> uint64_t { return all ? H : ~(x | ((x | H) - rep)) & H; };
-    for (int mw = 0; mw < nwl; mw++) {
-      unsigned long long word = 0;
-      const int64_t cw = s + 64ll * mw;
-      if (k == kf) {
-        word = (mw == 0 && cand_end > s) ? 1ull : 0ull;  // the entry chunk: its only start is the entry
-      } else if (cw < cand_end) {
-        const uint32_t o0 = (uint32_t)(cw - R0);  // 8-aligned: chunk starts are multiples of C
-        uint64_t w[9];
-#pragma unroll
-        for (int i = 0; i < 9; i++) w[i] = *reinterpret_cast<const uint64_t*>(rgn + rswz(o0 + 8u * i));
-#pragma unroll
-        for (int q = 0; q < 8; q++) {
-          const uint64_t x = w[q];
-          const uint64_t y = (x >> 8) | (w[q + 1] << 56);
-          const uint64_t z = ~(((x & L7) + L7) | x) & H;  // zero bytes
-          const uint64_t put_first = le_rep(x, rk, allk) & ~z;
-          // a log whose header counts no DELETE has none on its true chain: 0x00 starts no record
-          const uint64_t r = (put_first & le_rep(y, rv, allv)) | (P.no_deletes ? 0ull : (z & le_rep(y, rd, alld)));
-          uint64_t t = (r >> 7) & ONES;  // gather the 8 flags into one byte
-          t |= t >> 7;
-          t |= t >> 14;
-          t |= t >> 28;
-          word |= (t & 0xffull) << (8 * q);
-        }
-        const int64_t valid = cand_end - cw;
-        if (valid < 64) word &= (1ull << valid) - 1ull;
-      }
-      if (nwl <= 2) {
-        if (mw == 0) m0 = word; else m1 = word;
-      } else if (act) {
-        masks[lane * nwords + mw] = word;
-      }
+    const uint64_t* r64 = reinterpret_cast<const uint64_t*>(rgn);
+    uint8_t* fb = reinterpret_cast<uint8_t*>(flags);
+    const int nq = (nw << cs) >> 3;
+    for (int q = lane; q < nq; q += 64) {
+      const uint64_t x = r64[q];
+      const uint64_t y = (x >> 8) | (r64[q + 1] << 56);
+      const uint64_t z = ~(((x & L7) + L7) | x) & H;  // zero bytes
+      const uint64_t put_first = le_rep(x, rk, allk) & ~z;
+      // a log whose header counts no DELETE has none on its true chain: 0x00 starts no record
+      const uint64_t r = (put_first & le_rep(y, rv, allv)) | (P.no_deletes ? 0ull : (z & le_rep(y, rd, alld)));
+      uint64_t t = (r >> 7) & ONES;  // gather the 8 flags into one byte
+      t |= t >> 7;
+      t |= t >> 14;
+      t |= t >> 28;
+      fb[q] = (uint8_t)t;
     }
   }
+  __syncthreads();
+  // mask word wi of this lane's chunk: bit i = candidate start s + 64 wi + i
+  auto masked_word = [&](int wi) -> unsigned long long {
+    if (k == kf) return (wi == 0 && cand_end > s) ? 1ull : 0ull;  // the entry chunk: its only start is the entry
+    const int64_t cw = s + 64ll * wi;
+    if (cw >= cand_end) return 0ull;
+    unsigned long long word = flags[((uint32_t)lane << (cs - 6)) + wi];
+    const int64_t valid = cand_end - cw;
+    if (valid < 64) word &= (1ull << valid) - 1ull;
+    return word;
+  };
+  unsigned long long m0 = 0, m1 = 0;
+  if (nwl <= 2) {
+    m0 = masked_word(0);
+    m1 = nwl > 1 ? masked_word(1) : 0ull;
+  }
   auto mask_word = [&](int wi) -> unsigned long long {
-    return nwl <= 2 ? (wi == 0 ? m0 : m1) : masks[lane * nwords + wi];
+    return nwl <= 2 ? (wi == 0 ? m0 : m1) : masked_word(wi);
   };
   mark(1);
 
@@ -356,6 +348,7 @@ __global__ __launch_bounds__(64) void k_frame(BuildParams P) {
     const uint32_t cpre = incl - cnt_c;
     if (T <= (uint32_t)kCandCap) {
       balanced = true;
+      __syncthreads();  // every lane holds its masks: the list may overwrite the bitmap
       {  // enumerate: lane's candidates in ascending order at cand[cpre ..)
         unsigned long long a0 = has ? m0 : 0ull, a1 = has ? m1 : 0ull;
         uint32_t o = cpre;
@@ -923,8 +916,8 @@ __global__ __launch_bounds__(kPlaceLdsBlock) void k_place_lds(BuildParams P) {
 void launch_frame_fused(const BuildParams& P, hipStream_t s, StageTimer* tm) {
   if (P.fr_nchunks == 0) return;
   const uint64_t nwaves = (P.fr_nchunks + P.fr_w - 1) / P.fr_w;
-  // masks (when they do not fit in registers) or the balanced walk's candidate list
-  const size_t lds = (size_t)P.fr_rgn_bytes + std::max<size_t>((size_t)P.fr_w * P.fr_mask_words * 8, kCandCap * 4);
+  // the screen's bitmap (one bit per chunk byte), later overlaid by the balanced walk's list
+  const size_t lds = (size_t)P.fr_rgn_bytes + std::max<size_t>(((size_t)P.fr_w << P.fr_cshift) / 8 + 8, kCandCap * 4);
   hipLaunchKernelGGL(k_frame, dim3((unsigned)nwaves), dim3(64), lds, s, P);
   scan_exclusive<uint32_t, uint64_t, OpAdd>(P.wcount, P.woff, P.nslabs, (uint64_t*)&P.st->n_records, OpAdd(),
                                             P.scan_scratch_u64, s);
