@@ -214,6 +214,17 @@ __device__ __forceinline__ RecHdr decode_rgn(const uint8_t* r, int64_t R0, int64
   return h;
 }
 
+// Balanced-walk candidate record: start (14 bits, region offset) | exit - start (9) | steps to the
+// exit (8) | survived (1).  A survivor too far to encode is recorded as dead: the exact walk of the
+// entry phase resolves its chunk.
+__device__ __forceinline__ uint32_t pack_cand(int32_t start, int32_t dexit, int32_t steps) {
+  if (steps > 255 || dexit > 511) return (uint32_t)start;
+  return (uint32_t)start | ((uint32_t)dexit << 14) | ((uint32_t)steps << 23) | 0x80000000u;
+}
+__device__ __forceinline__ uint32_t cand_start(uint32_t v) { return v & 0x3fffu; }
+__device__ __forceinline__ uint32_t cand_dexit(uint32_t v) { return (v >> 14) & 0x1ffu; }
+__device__ __forceinline__ int32_t cand_steps(uint32_t v) { return (int32_t)((v >> 23) & 0xffu); }
+
 __global__ __launch_bounds__(64) void k_frame(BuildParams P) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int lane = threadIdx.x;
@@ -332,9 +343,10 @@ __global__ __launch_bounds__(64) void k_frame(BuildParams P) {
   // Balanced walk (C = 128, masks in registers, canonical one-byte VLQs): the wave's candidates go
   // to one LDS list and lane L walks candidates L, L + 64, ..., so the walk takes about the mean
   // work per lane instead of the largest; each lane then folds its own chunk's results.
-  // cand[i] = start | (exit - start) << 14 | steps << 22 | survived << 31 (region offsets).
+  // cand[i]: see pack_cand.
   bool balanced = false;
-  if (P.fr_fast && nwl <= 2) {
+  uint32_t my_cpre = 0, my_ccnt = 0;
+  if (P.fr_fast && nwl <= 2 && RLEN < 16384) {
     uint32_t* cand = reinterpret_cast<uint32_t*>(lds + P.fr_rgn_bytes);
     const bool has = act && cand_end > s;
     const uint32_t cnt_c = has ? (uint32_t)(__builtin_popcountll(m0) + __builtin_popcountll(m1)) : 0u;
@@ -346,6 +358,8 @@ __global__ __launch_bounds__(64) void k_frame(BuildParams P) {
     }
     const uint32_t T = __shfl(incl, 63, 64);
     const uint32_t cpre = incl - cnt_c;
+    my_cpre = cpre;
+    my_ccnt = cnt_c;
     if (T <= (uint32_t)kCandCap) {
       balanced = true;
       __syncthreads();  // every lane holds its masks: the list may overwrite the bitmap
@@ -399,7 +413,7 @@ __global__ __launch_bounds__(64) void k_frame(BuildParams P) {
             rp += 2 + klen + vlen;
             if (rex < 0 && rp >= re) rex = rp;
             if (rp >= rstop) {
-              cand[cur] = (uint32_t)rst | ((uint32_t)(rex - rst) << 14) | ((uint32_t)st << 22) | 0x80000000u;
+              cand[cur] = pack_cand(rst, rex - rst, st);
               rp = -1;
             }
           }
@@ -410,11 +424,11 @@ __global__ __launch_bounds__(64) void k_frame(BuildParams P) {
       for (uint32_t i = 0; i < cnt_c; i++) {
         const uint32_t v = cand[cpre + i];
         if (v & 0x80000000u) {
-          const uint32_t st0 = v & 0x3fffu;
-          const unsigned long long pe = (unsigned long long)(R0 + st0 + ((v >> 14) & 0xffu));
+          const uint32_t st0 = cand_start(v);
+          const unsigned long long pe = (unsigned long long)(R0 + st0 + cand_dexit(v));
           if (nsurv == 0) {
             c_min = (unsigned long long)(R0 + st0);
-            c_min_steps = (int32_t)((v >> 22) & 0x1ffu);
+            c_min_steps = cand_steps(v);
           }
           nsurv++;
           min_exit = min(min_exit, pe);
@@ -519,6 +533,22 @@ __global__ __launch_bounds__(64) void k_frame(BuildParams P) {
     if (lane == 0) { P.dbg[wv * 16 + 9] = sv; P.dbg[wv * 16 + 10] = nc; P.dbg[wv * 16 + 8] = dbg_iters; }
   }
 
+  // balanced walk: the lane's own candidate that starts at p, if it survived -> its steps and exit
+  auto find_surv = [&](int64_t p, int32_t& steps, int64_t& ex) -> bool {
+    if (!balanced) return false;
+    const uint32_t* cand = reinterpret_cast<const uint32_t*>(lds + P.fr_rgn_bytes);
+    const uint32_t want = (uint32_t)(p - R0);
+    for (uint32_t i = 0; i < my_ccnt; i++) {
+      const uint32_t v = cand[my_cpre + i];
+      if (cand_start(v) == want) {
+        if (!(v & 0x80000000u)) return false;
+        steps = cand_steps(v);
+        ex = p + (int64_t)cand_dexit(v);
+        return true;
+      }
+    }
+    return false;
+  };
   // ---- 3 entries ----
   int64_t my_exit = converged ? (int64_t)min_exit : -1;
   if (lane == nw - 1 && converged) granule_store(&P.exit_desc[wv], (unsigned long long)my_exit | kReady);
@@ -552,6 +582,12 @@ __global__ __launch_bounds__(64) void k_frame(BuildParams P) {
     const int64_t prev_exit = __shfl(my_exit, j > 0 ? j - 1 : 0, 64);
     if (lane == j) {
       int64_t p = j == 0 ? ext : prev_exit;
+      int32_t fst = 0;
+      int64_t fex = 0;
+      if (p < e && find_surv(p, fst, fex)) {  // its chain was walked already
+        cnt = fst;
+        p = fex;
+      }
       while (p < e) {
         const RecHdr h = hdr_at(p);
         if (!header_valid(h, p, P.max_key_len, log_len)) {
@@ -571,8 +607,16 @@ __global__ __launch_bounds__(64) void k_frame(BuildParams P) {
   const int64_t entry = lane == 0 ? ext : up;
 
   // ---- 4 counts ----
-  const bool need_walk = converged && !(nsurv == 1 && (unsigned long long)entry == c_min);
+  bool need_walk = converged && !(nsurv == 1 && (unsigned long long)entry == c_min);
   if (converged && !need_walk) cnt = c_min_steps;
+  if (need_walk) {  // the entry's own speculative walk, if it survived, is the verified one
+    int32_t fst = 0;
+    int64_t fex = 0;
+    if (find_surv(entry, fst, fex) && fex == (int64_t)min_exit) {
+      cnt = fst;
+      need_walk = false;
+    }
+  }
   if (__any(need_walk)) {  // several survivors, or an entry the screen pruned: verified walk
     int64_t p = need_walk ? entry : e;
     for (;;) {

@@ -25,6 +25,9 @@ using namespace sk;
 
 namespace {
 
+constexpr int64_t kFrameMinChunk = 256;  // k_frame chunk (one lane) lower bound
+constexpr int64_t kFrameRegion = 8192;   // bytes of chunks per k_frame wave
+
 constexpr uint32_t kLogMagic = 0x49b39c95u;
 constexpr uint32_t kIndexMagic = 0x9a11318fu;
 
@@ -356,15 +359,20 @@ static int setup_params(const LogHdr& lh, const IndexParams& ip, const sparkey_b
   P.fr_entry = entry;
   P.ch_k0 = (uint64_t)entry >> kChunkShift;
   P.nchunks = any ? (uint64_t)((frame_end + kChunk - 1) / kChunk) - P.ch_k0 : 0;
-  // k_frame geometry: chunk C = max(128, nextpow2(maxRecLen)) so every chunk but a short last one
+  // k_frame geometry: chunk C = max(256, nextpow2(maxRecLen)) so every chunk but a short last one
   // holds a record start; 8 KiB of chunks per wave, staged contiguously with max(C, 256) bytes of
   // look-ahead (about 10 KiB of LDS: 16 waves per CU); records longer than 4 KiB -> serial framing.
   {
+    // chunk >= kFrameMinChunk and >= maxRecLen; a wave stages kFrameRegion bytes of chunks
+    // (SPARKEY_FRAME_CMIN / SPARKEY_FRAME_REGION override both, for tuning)
+    int64_t cmin = kFrameMinChunk, region = kFrameRegion;
+    if (const char* v = getenv("SPARKEY_FRAME_CMIN")) cmin = std::max<int64_t>(128, atoll(v));
+    if (const char* v = getenv("SPARKEY_FRAME_REGION")) region = std::max<int64_t>(4096, atoll(v));
     int cs = 7;
-    while ((1ll << cs) < P.max_rec_len) cs++;
+    while ((1ll << cs) < std::max<int64_t>(P.max_rec_len, cmin)) cs++;
     const int64_t C = 1ll << cs;
     P.fr_cshift = cs;
-    P.fr_w = (int32_t)std::max<int64_t>(1, std::min<int64_t>(64, 8192 / C));
+    P.fr_w = (int32_t)std::max<int64_t>(1, std::min<int64_t>(64, region / C));
     P.fr_look = (int32_t)std::max<int64_t>(C, 256);
     P.fr_rgn_bytes = (int32_t)(((int64_t)P.fr_w * C + P.fr_look + 16 + 255) & ~255LL);
     P.fr_mask_words = (int32_t)((std::min<int64_t>(C, P.max_rec_len) + 63) / 64);
