@@ -32,7 +32,7 @@ constexpr int kPart2Block = 1024;                 // k_part2: one workgroup per 
 constexpr int kPart2MaxBits = 14;                 // fine digit of the partition (<= 16384 buckets)
 constexpr uint32_t kPlaceLdsMax = 1536;           // entries of a bucket staged in LDS
 constexpr uint32_t kMaxPartGroup = 64;
-constexpr int kCandCap = 448;                     // k_frame balanced walk: candidates per wave            // slabs per partition tile
+constexpr int kCandCap = 448;                     // k_frame balanced walk: candidates (and listed records) per wave
 
 // One log record as the placement sees it: 16 bytes, AoS so every access is one dwordx4.
 struct alignas(16) Entry {
@@ -151,8 +151,9 @@ struct BuildParams {
   int32_t fr_cshift;
   int32_t fr_w;
   int32_t fr_look;       // speculative walks continue this many bytes past their chunk
-  int32_t fr_rgn_bytes;  // LDS region per wave: W * C + fr_look + 16, rounded up to 256 bytes
-  int32_t fr_mask_words;
+  int32_t fr_rgn_bytes;  // LDS region per wave: W * C + fr_look + 16, rounded up to 1 KiB
+  int32_t fr_mask_words;  // 64-position screen words per chunk: ceil(min(C, maxRecLen) / 64)
+  uint32_t fr_wpc_magic;  // q / (8 * fr_mask_words) == (q * magic) >> 22 for every screened word q
   int32_t fr_fast;  // maxKeyLen + 1 < 128 and maxValueLen < 128: canonical headers are 2 bytes
   int32_t no_deletes;  // the log header counts no DELETE: speculation treats 0x00 as no record start
   uint64_t fr_nchunks;

@@ -214,16 +214,19 @@ __device__ __forceinline__ RecHdr decode_rgn(const uint8_t* r, int64_t R0, int64
   return h;
 }
 
-// Balanced-walk candidate record: start (14 bits, region offset) | exit - start (9) | steps to the
-// exit (8) | survived (1).  A survivor too far to encode is recorded as dead: the exact walk of the
-// entry phase resolves its chunk.
+// Balanced-walk candidate record: start (14 bits, region offset) | exit - chunk end (8) | steps to
+// the exit (9) | survived (1).  The walk only runs with canonical one-byte VLQs (fr_fast), so a
+// record is < 256 bytes and exit - chunk end always fits.  A survivor whose steps do not fit is
+// recorded with steps = 511 and no survived bit: its chunk is then treated as unconverged and walked
+// exactly in the entry phase (a dead candidate has steps 0).
+constexpr uint32_t kCandOverflow = 511u;
 __device__ __forceinline__ uint32_t pack_cand(int32_t start, int32_t dexit, int32_t steps) {
-  if (steps > 255 || dexit > 511) return (uint32_t)start;
-  return (uint32_t)start | ((uint32_t)dexit << 14) | ((uint32_t)steps << 23) | 0x80000000u;
+  if (steps >= (int32_t)kCandOverflow || dexit > 255) return (uint32_t)start | (kCandOverflow << 22);
+  return (uint32_t)start | ((uint32_t)dexit << 14) | ((uint32_t)steps << 22) | 0x80000000u;
 }
 __device__ __forceinline__ uint32_t cand_start(uint32_t v) { return v & 0x3fffu; }
-__device__ __forceinline__ uint32_t cand_dexit(uint32_t v) { return (v >> 14) & 0x1ffu; }
-__device__ __forceinline__ int32_t cand_steps(uint32_t v) { return (int32_t)((v >> 23) & 0xffu); }
+__device__ __forceinline__ uint32_t cand_dexit(uint32_t v) { return (v >> 14) & 0xffu; }
+__device__ __forceinline__ int32_t cand_steps(uint32_t v) { return (int32_t)((v >> 22) & 0x1ffu); }
 
 __global__ __launch_bounds__(64) void k_frame(BuildParams P) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -253,17 +256,15 @@ __global__ __launch_bounds__(64) void k_frame(BuildParams P) {
   // ---- stage: [R0, R0 + RLEN) once, coalesced, 16 bytes per lane per step ----
   {
     const int nvec = (int)((RLEN + 15) >> 4);
-    if (R0 + 16ll * nvec <= log_len) {  // 4 loads in flight per lane, then their LDS stores
+    if (R0 + 16ll * nvec <= log_len) {
+      // every load of the region in flight at once, straight into LDS (global_load_lds_dwordx4:
+      // 1 KiB per wave instruction at rgn + 1024 i; fr_rgn_bytes is a multiple of 1 KiB, lanes past
+      // the end repeat the last vector)
       const uint4* src = reinterpret_cast<const uint4*>(P.log + R0);
-      for (int v0 = 0; v0 < nvec; v0 += 256) {
-        // branch-free: lanes past the end repeat the last vector (same bytes, same place)
-        uint4 t[4];
-#pragma unroll
-        for (int i = 0; i < 4; i++) t[i] = src[min(v0 + 64 * i + lane, nvec - 1)];
-#pragma unroll
-        for (int i = 0; i < 4; i++)
-          *reinterpret_cast<uint4*>(rgn + 16u * (uint32_t)min(v0 + 64 * i + lane, nvec - 1)) = t[i];
-      }
+      for (int v0 = 0; v0 < nvec; v0 += 64)
+        __builtin_amdgcn_global_load_lds(
+            (const __attribute__((address_space(1))) void*)(src + min(v0 + lane, nvec - 1)),
+            (__attribute__((address_space(3))) void*)(rgn + 16u * (uint32_t)v0), 16, 0, 0);
     } else {
       for (int v = lane; v < nvec; v += 64) {
         const uint4 val = load16_guarded(P.log, R0 + 16ll * v, log_len);
@@ -299,19 +300,21 @@ __global__ __launch_bounds__(64) void k_frame(BuildParams P) {
     auto le_rep = [&](uint64_t x, uint64_t rep, bool all) -> uint64_t { return all ? H : ~(x | ((x | H) - rep)) & H; };
     const uint64_t* r64 = reinterpret_cast<const uint64_t*>(rgn);
     uint8_t* fb = reinterpret_cast<uint8_t*>(flags);
-    const int nq = (nw << cs) >> 3;
+    // only each chunk's candidate window [chunk start, + nwl * 64) is screened: byte q of the
+    // bitmap = word q % wpc of chunk q / wpc
+    const int wpc = nwl * 8;
+    const int nq = nw * wpc;
     for (int q = lane; q < nq; q += 64) {
-      const uint64_t x = r64[q];
-      const uint64_t y = (x >> 8) | (r64[q + 1] << 56);
+      const int j = (int)(((uint32_t)q * P.fr_wpc_magic) >> 22);  // q / wpc (exact, checked on the host)
+      const int rw = (j << (cs - 3)) + (q - j * wpc);
+      const uint64_t x = r64[rw];
+      const uint64_t y = (x >> 8) | (r64[rw + 1] << 56);
       const uint64_t z = ~(((x & L7) + L7) | x) & H;  // zero bytes
       const uint64_t put_first = le_rep(x, rk, allk) & ~z;
       // a log whose header counts no DELETE has none on its true chain: 0x00 starts no record
       const uint64_t r = (put_first & le_rep(y, rv, allv)) | (P.no_deletes ? 0ull : (z & le_rep(y, rd, alld)));
-      uint64_t t = (r >> 7) & ONES;  // gather the 8 flags into one byte
-      t |= t >> 7;
-      t |= t >> 14;
-      t |= t >> 28;
-      fb[q] = (uint8_t)t;
+      // gather the 8 flags (bits 7, 15, ..., 63) into one byte: bit 8i -> bit 56 + i, no carries
+      fb[q] = (uint8_t)((((r >> 7) & ONES) * 0x0102040810204080ull) >> 56);
     }
   }
   __syncthreads();
@@ -320,18 +323,21 @@ __global__ __launch_bounds__(64) void k_frame(BuildParams P) {
     if (k == kf) return (wi == 0 && cand_end > s) ? 1ull : 0ull;  // the entry chunk: its only start is the entry
     const int64_t cw = s + 64ll * wi;
     if (cw >= cand_end) return 0ull;
-    unsigned long long word = flags[((uint32_t)lane << (cs - 6)) + wi];
+    unsigned long long word = flags[(uint32_t)lane * (uint32_t)nwl + (uint32_t)wi];
     const int64_t valid = cand_end - cw;
     if (valid < 64) word &= (1ull << valid) - 1ull;
     return word;
   };
-  unsigned long long m0 = 0, m1 = 0;
-  if (nwl <= 2) {
+  unsigned long long m0 = 0, m1 = 0, m2 = 0, m3 = 0;  // masks in registers when nwl <= 4
+  if (nwl <= 4) {
     m0 = masked_word(0);
     m1 = nwl > 1 ? masked_word(1) : 0ull;
+    m2 = nwl > 2 ? masked_word(2) : 0ull;
+    m3 = nwl > 3 ? masked_word(3) : 0ull;
   }
   auto mask_word = [&](int wi) -> unsigned long long {
-    return nwl <= 2 ? (wi == 0 ? m0 : m1) : masked_word(wi);
+    if (nwl > 4) return masked_word(wi);
+    return wi == 0 ? m0 : wi == 1 ? m1 : wi == 2 ? m2 : m3;
   };
   mark(1);
 
@@ -345,11 +351,14 @@ __global__ __launch_bounds__(64) void k_frame(BuildParams P) {
   // work per lane instead of the largest; each lane then folds its own chunk's results.
   // cand[i]: see pack_cand.
   bool balanced = false;
+  bool unenc = false;  // a survivor of this chunk did not fit its candidate record
   uint32_t my_cpre = 0, my_ccnt = 0;
-  if (P.fr_fast && nwl <= 2 && RLEN < 16384) {
+  if (P.fr_fast && nwl <= 4 && RLEN < 16384) {
     uint32_t* cand = reinterpret_cast<uint32_t*>(lds + P.fr_rgn_bytes);
     const bool has = act && cand_end > s;
-    const uint32_t cnt_c = has ? (uint32_t)(__builtin_popcountll(m0) + __builtin_popcountll(m1)) : 0u;
+    const uint32_t cnt_c = has ? (uint32_t)(__builtin_popcountll(m0) + __builtin_popcountll(m1) +
+                                            __builtin_popcountll(m2) + __builtin_popcountll(m3))
+                               : 0u;
     uint32_t incl = cnt_c;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -364,16 +373,22 @@ __global__ __launch_bounds__(64) void k_frame(BuildParams P) {
       balanced = true;
       __syncthreads();  // every lane holds its masks: the list may overwrite the bitmap
       {  // enumerate: lane's candidates in ascending order at cand[cpre ..)
-        unsigned long long a0 = has ? m0 : 0ull, a1 = has ? m1 : 0ull;
+        unsigned long long a0 = has ? m0 : 0ull, a1 = has ? m1 : 0ull, a2 = has ? m2 : 0ull, a3 = has ? m3 : 0ull;
         uint32_t o = cpre;
         const uint32_t base = (uint32_t)(s - R0);
-        while (__any((a0 | a1) != 0ull)) {
+        while (__any((a0 | a1 | a2 | a3) != 0ull)) {
           if (a0) {
             cand[o++] = base + (uint32_t)__builtin_ctzll(a0);
             a0 &= a0 - 1;
           } else if (a1) {
             cand[o++] = base + 64u + (uint32_t)__builtin_ctzll(a1);
             a1 &= a1 - 1;
+          } else if (a2) {
+            cand[o++] = base + 128u + (uint32_t)__builtin_ctzll(a2);
+            a2 &= a2 - 1;
+          } else if (a3) {
+            cand[o++] = base + 192u + (uint32_t)__builtin_ctzll(a3);
+            a3 &= a3 - 1;
           }
         }
       }
@@ -413,7 +428,7 @@ __global__ __launch_bounds__(64) void k_frame(BuildParams P) {
             rp += 2 + klen + vlen;
             if (rex < 0 && rp >= re) rex = rp;
             if (rp >= rstop) {
-              cand[cur] = pack_cand(rst, rex - rst, st);
+              cand[cur] = pack_cand(rst, rex - re, st);
               rp = -1;
             }
           }
@@ -423,9 +438,10 @@ __global__ __launch_bounds__(64) void k_frame(BuildParams P) {
       // fold the lane's own chunk
       for (uint32_t i = 0; i < cnt_c; i++) {
         const uint32_t v = cand[cpre + i];
+        if (!(v & 0x80000000u) && cand_steps(v) == (int32_t)kCandOverflow) unenc = true;
         if (v & 0x80000000u) {
           const uint32_t st0 = cand_start(v);
-          const unsigned long long pe = (unsigned long long)(R0 + st0 + cand_dexit(v));
+          const unsigned long long pe = (unsigned long long)(e + cand_dexit(v));
           if (nsurv == 0) {
             c_min = (unsigned long long)(R0 + st0);
             c_min_steps = cand_steps(v);
@@ -525,7 +541,7 @@ __global__ __launch_bounds__(64) void k_frame(BuildParams P) {
       }
     }
   }
-  const bool converged = act && !passthrough && nsurv > 0 && (long long)min_exit == max_exit;
+  const bool converged = act && !passthrough && !unenc && nsurv > 0 && (long long)min_exit == max_exit;
   mark(2);
   if (P.dbg) {
     const unsigned long long sv = wave_sum_u64(nsurv);
@@ -534,8 +550,10 @@ __global__ __launch_bounds__(64) void k_frame(BuildParams P) {
   }
 
   // balanced walk: the lane's own candidate that starts at p, if it survived -> its steps and exit
+  // (cands_live: the list is overlaid by the record list once phase 5 ran)
+  bool cands_live = true;
   auto find_surv = [&](int64_t p, int32_t& steps, int64_t& ex) -> bool {
-    if (!balanced) return false;
+    if (!balanced || !cands_live) return false;
     const uint32_t* cand = reinterpret_cast<const uint32_t*>(lds + P.fr_rgn_bytes);
     const uint32_t want = (uint32_t)(p - R0);
     for (uint32_t i = 0; i < my_ccnt; i++) {
@@ -543,156 +561,210 @@ __global__ __launch_bounds__(64) void k_frame(BuildParams P) {
       if (cand_start(v) == want) {
         if (!(v & 0x80000000u)) return false;
         steps = cand_steps(v);
-        ex = p + (int64_t)cand_dexit(v);
+        ex = e + (int64_t)cand_dexit(v);
         return true;
       }
     }
     return false;
   };
-  // ---- 3 entries ----
-  int64_t my_exit = converged ? (int64_t)min_exit : -1;
-  if (lane == nw - 1 && converged) granule_store(&P.exit_desc[wv], (unsigned long long)my_exit | kReady);
-  unsigned long long extv = (unsigned long long)P.fr_entry;
-  if (wv > 0 && lane == 0) {
-    const unsigned long long t0 = wall_clock64();
-    for (;;) {
-      const unsigned long long v = granule_load(&P.exit_desc[wv - 1]);
-      if (v & kReady) { extv = v & ~kReady; break; }
-      if (wall_clock64() - t0 > kSpinTicks) {  // should a predecessor never run: serial path
-        atomicOr(&P.st->spec_fail, 2u);
-        extv = (unsigned long long)s;
-        break;
+  // the previous wave's published exit (lane 0 spins, bounded), broadcast
+  auto wait_prev = [&]() -> int64_t {
+    unsigned long long extv = (unsigned long long)P.fr_entry;
+    if (wv > 0 && lane == 0) {
+      const unsigned long long t0 = wall_clock64();
+      for (;;) {
+        const unsigned long long v = granule_load(&P.exit_desc[wv - 1]);
+        if (v & kReady) { extv = v & ~kReady; break; }
+        if (wall_clock64() - t0 > kSpinTicks) {  // should a predecessor never run: serial path
+          atomicOr(&P.st->spec_fail, 2u);
+          extv = (unsigned long long)s;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
       }
-      __builtin_amdgcn_s_sleep(2);
     }
-  }
-  const int64_t ext = (int64_t)__shfl(extv, 0, 64);
-  mark(3);
-  // chunks whose exit depends on their entry, in order (a serial walk each, rare)
-  int32_t cnt = 0;
-  bool bad = false;
+    return (int64_t)__shfl(extv, 0, 64);
+  };
   auto at_glb = [&](int64_t a) -> uint32_t { return (uint32_t)P.log[a]; };
   auto hdr_at = [&](int64_t p) -> RecHdr {
     return p + 16 <= R0 + RLEN ? decode_rgn(rgn, R0, p, log_len) : decode_header(at_glb, p, log_len);
   };
-  unsigned long long pending = __ballot(act && !converged);
-  while (pending) {
-    const int j = __builtin_ctzll(pending);
-    pending &= pending - 1;
-    const int64_t prev_exit = __shfl(my_exit, j > 0 ? j - 1 : 0, 64);
-    if (lane == j) {
-      int64_t p = j == 0 ? ext : prev_exit;
-      int32_t fst = 0;
-      int64_t fex = 0;
-      if (p < e && find_surv(p, fst, fex)) {  // its chain was walked already
-        cnt = fst;
-        p = fex;
-      }
-      while (p < e) {
-        const RecHdr h = hdr_at(p);
-        if (!header_valid(h, p, P.max_key_len, log_len)) {
-          set_error(P.st, p, h.rc ? h.rc : kErrCorruptLog);
-          bad = true;
-          break;
+  // ---- 3 entries ----
+  const int64_t conv_exit = converged ? (int64_t)min_exit : -1;
+  if (lane == nw - 1 && converged) granule_store(&P.exit_desc[wv], (unsigned long long)conv_exit | kReady);
+  // The wave's first entry is the previous wave's published exit.  When every chunk converged and
+  // the first one has a single survivor, that survivor is the entry of any consistent log: the wave
+  // goes on with it and checks the published exit after hashing (phases 3-5 are redone on a
+  // mismatch), so the hand-off latency hides behind the wave's own work.
+  const unsigned long long c_min0 = __shfl(c_min, 0, 64);
+  const unsigned long long nsurv0 = __shfl(nsurv, 0, 64);
+  bool spec = wv > 0 && __all(!act || converged) && nsurv0 == 1;
+  int64_t ext = spec ? (int64_t)c_min0 : wait_prev();
+  mark(3);
+  unsigned long long ndel = 0;
+  for (;;) {
+    int64_t my_exit = conv_exit;
+    // chunks whose exit depends on their entry, in order (a serial walk each, rare)
+    int32_t cnt = 0;
+    bool bad = false;
+    unsigned long long pending = __ballot(act && !converged);
+    while (pending) {
+      const int j = __builtin_ctzll(pending);
+      pending &= pending - 1;
+      const int64_t prev_exit = __shfl(my_exit, j > 0 ? j - 1 : 0, 64);
+      if (lane == j) {
+        int64_t p = j == 0 ? ext : prev_exit;
+        int32_t fst = 0;
+        int64_t fex = 0;
+        if (p < e && find_surv(p, fst, fex)) {  // its chain was walked already
+          cnt = fst;
+          p = fex;
         }
-        cnt++;
-        p = record_end(h, p);
-      }
-      my_exit = max(p, e);
-    }
-  }
-  if (lane == nw - 1 && !converged) granule_store(&P.exit_desc[wv], (unsigned long long)my_exit | kReady);
-  if (lane == nw - 1 && wv + 1 == gridDim.x) P.st->exit = my_exit;  // the framed chain's exit
-  const int64_t up = __shfl_up(my_exit, 1, 64);
-  const int64_t entry = lane == 0 ? ext : up;
-
-  // ---- 4 counts ----
-  bool need_walk = converged && !(nsurv == 1 && (unsigned long long)entry == c_min);
-  if (converged && !need_walk) cnt = c_min_steps;
-  if (need_walk) {  // the entry's own speculative walk, if it survived, is the verified one
-    int32_t fst = 0;
-    int64_t fex = 0;
-    if (find_surv(entry, fst, fex) && fex == (int64_t)min_exit) {
-      cnt = fst;
-      need_walk = false;
-    }
-  }
-  if (__any(need_walk)) {  // several survivors, or an entry the screen pruned: verified walk
-    int64_t p = need_walk ? entry : e;
-    for (;;) {
-      const bool go = need_walk && !bad && p < e;
-      if (!__any(go)) break;
-      if (go) {
-        const RecHdr h = hdr_at(p);
-        if (!header_valid(h, p, P.max_key_len, log_len)) {
-          set_error(P.st, p, h.rc ? h.rc : kErrCorruptLog);
-          bad = true;
-        } else {
+        while (p < e) {
+          const RecHdr h = hdr_at(p);
+          if (!header_valid(h, p, P.max_key_len, log_len)) {
+            set_error(P.st, p, h.rc ? h.rc : kErrCorruptLog);
+            bad = true;
+            break;
+          }
           cnt++;
           p = record_end(h, p);
         }
+        my_exit = max(p, e);
       }
     }
-    if (need_walk && !bad && p != (int64_t)min_exit) atomicOr(&P.st->spec_fail, 1u);
-  }
-  if (!act || bad) cnt = 0;
-  // wave-exclusive scan of the counts
-  unsigned long long incl = (unsigned long long)cnt;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const unsigned long long t = __shfl_up(incl, o, 64);
-    if (lane >= o) incl += t;
-  }
-  const unsigned long long total = __shfl(incl, 63, 64);
-  const unsigned long long local_off = incl - (unsigned long long)cnt;
-  mark(4);
-  // the wave's records go to its own slab; the radix partition compacts the slabs
-  if (total > P.slab_cap) {
-    if (lane == 0) {
-      atomicMax(&P.st->max_wave_count, (unsigned int)min(total, 0xffffffffull));
-      atomicOr(&P.st->overflow, 1u);
-    }
-    return;
-  }
-  if (lane == 0) P.wcount[wv] = (uint32_t)total;
-  const unsigned long long base = wv * (unsigned long long)P.slab_cap;
-  mark(5);
+    if (lane == nw - 1 && !converged) granule_store(&P.exit_desc[wv], (unsigned long long)my_exit | kReady);
+    if (lane == nw - 1 && wv + 1 == gridDim.x) P.st->exit = my_exit;  // the framed chain's exit
+    const int64_t up = __shfl_up(my_exit, 1, 64);
+    const int64_t entry = lane == 0 ? ext : up;
 
-  // ---- 5 hash every record of the chunk, entries in log order ----
-  unsigned long long ndel = 0;
-  {
-    int64_t p = (act && cnt > 0) ? entry : e;
-    uint64_t dst = base + local_off;
-    for (;;) {
-      const bool go = p < e;
-      if (!__any(go)) break;
-      if (go) {
-        const RecHdr h = hdr_at(p);
-        const int64_t kp = p + h.hlen;
-        uint64_t hash;
-        if (kp + h.klen + 16 <= R0 + RLEN) {  // key in the region
-          const RgnKey ld{rgn, (uint32_t)(kp - R0)};
-          hash = P.hash_size == 8 ? murmur64_ld(ld, h.klen, (uint32_t)P.seed)
-                                  : (uint64_t)murmur32_ld(ld, h.klen, (uint32_t)P.seed);
-        } else if (kp + h.klen + 16 <= log_len) {  // key runs past the region: unaligned global reads
-          const GlobalKey ld{P.log + kp};
-          hash = P.hash_size == 8 ? murmur64_ld(ld, h.klen, (uint32_t)P.seed)
-                                  : (uint64_t)murmur32_ld(ld, h.klen, (uint32_t)P.seed);
-        } else {
-          hash = key_hash(P.hash_size, P.log + kp, h.klen, (uint32_t)P.seed);
-        }
-        uint64_t addr = (uint64_t)p << P.ebb;
-        if (!h.put) {
-          addr |= kDelBit;
-          ndel++;
-        }
-        Entry en;
-        en.hash = hash;
-        en.addr = addr;
-        P.ent[dst++] = en;
-        p = record_end(h, p);
+    // ---- 4 counts ----
+    bool need_walk = converged && !(nsurv == 1 && (unsigned long long)entry == c_min);
+    if (converged && !need_walk) cnt = c_min_steps;
+    if (need_walk) {  // the entry's own speculative walk, if it survived, is the verified one
+      int32_t fst = 0;
+      int64_t fex = 0;
+      if (find_surv(entry, fst, fex) && fex == (int64_t)min_exit) {
+        cnt = fst;
+        need_walk = false;
       }
     }
+    if (__any(need_walk)) {  // several survivors, or an entry the screen pruned: verified walk
+      int64_t p = need_walk ? entry : e;
+      for (;;) {
+        const bool go = need_walk && !bad && p < e;
+        if (!__any(go)) break;
+        if (go) {
+          const RecHdr h = hdr_at(p);
+          if (!header_valid(h, p, P.max_key_len, log_len)) {
+            set_error(P.st, p, h.rc ? h.rc : kErrCorruptLog);
+            bad = true;
+          } else {
+            cnt++;
+            p = record_end(h, p);
+          }
+        }
+      }
+      if (need_walk && !bad && p != (int64_t)min_exit) atomicOr(&P.st->spec_fail, 1u);
+    }
+    if (!act || bad) cnt = 0;
+    // wave-exclusive scan of the counts
+    unsigned long long incl = (unsigned long long)cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const unsigned long long t = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += t;
+    }
+    const unsigned long long total = __shfl(incl, 63, 64);
+    const unsigned long long local_off = incl - (unsigned long long)cnt;
+    mark(4);
+    // the wave's records go to its own slab; the radix partition compacts the slabs
+    if (total > P.slab_cap) {
+      if (spec) {  // the guessed entry may be wrong: decide on the published one
+        const int64_t real = wait_prev();
+        spec = false;
+        if (real != ext) {
+          ext = real;
+          continue;
+        }
+      }
+      if (lane == 0) {
+        atomicMax(&P.st->max_wave_count, (unsigned int)min(total, 0xffffffffull));
+        atomicOr(&P.st->overflow, 1u);
+      }
+      return;
+    }
+    if (lane == 0) P.wcount[wv] = (uint32_t)total;
+    const unsigned long long base = wv * (unsigned long long)P.slab_cap;
+    mark(5);
+
+    // ---- 5 hash every record, entries in log order.  The lanes first list their chunks' record
+    //      starts in LDS, then each lane hashes every 64th record of the wave (all lanes busy,
+    //      consecutive entries written together); a wave holding more than kCandCap records hashes
+    //      per chunk instead. ----
+    ndel = 0;
+    auto emit = [&](int64_t p, uint64_t dst) -> int64_t {
+      const RecHdr h = hdr_at(p);
+      const int64_t kp = p + h.hlen;
+      uint64_t hash;
+      if (kp + h.klen + 16 <= R0 + RLEN) {  // key in the region
+        const RgnKey ld{rgn, (uint32_t)(kp - R0)};
+        hash = P.hash_size == 8 ? murmur64_ld(ld, h.klen, (uint32_t)P.seed)
+                                : (uint64_t)murmur32_ld(ld, h.klen, (uint32_t)P.seed);
+      } else if (kp + h.klen + 16 <= log_len) {  // key runs past the region: unaligned global reads
+        const GlobalKey ld{P.log + kp};
+        hash = P.hash_size == 8 ? murmur64_ld(ld, h.klen, (uint32_t)P.seed)
+                                : (uint64_t)murmur32_ld(ld, h.klen, (uint32_t)P.seed);
+      } else {
+        hash = key_hash(P.hash_size, P.log + kp, h.klen, (uint32_t)P.seed);
+      }
+      uint64_t addr = (uint64_t)p << P.ebb;
+      if (!h.put) {
+        addr |= kDelBit;
+        ndel++;
+      }
+      Entry en;
+      en.hash = hash;
+      en.addr = addr;
+      P.ent[dst] = en;
+      return record_end(h, p);
+    };
+    if (total <= (unsigned long long)kCandCap) {  // wave-uniform
+      uint32_t* list = reinterpret_cast<uint32_t*>(lds + P.fr_rgn_bytes);  // overlays the candidate list
+      __syncthreads();
+      cands_live = false;
+      {
+        int64_t p = (act && cnt > 0) ? entry : e;
+        uint32_t o = (uint32_t)local_off;
+        for (;;) {
+          const bool go = p < e;
+          if (!__any(go)) break;
+          if (go) {
+            list[o++] = (uint32_t)(p - R0);
+            p = record_end(hdr_at(p), p);
+          }
+        }
+      }
+      __syncthreads();
+      for (uint32_t i = (uint32_t)lane; i < (uint32_t)total; i += 64) emit(R0 + (int64_t)list[i], base + i);
+    } else {
+      int64_t p = (act && cnt > 0) ? entry : e;
+      uint64_t dst = base + local_off;
+      for (;;) {
+        const bool go = p < e;
+        if (!__any(go)) break;
+        if (go) p = emit(p, dst++);
+      }
+    }
+    if (spec) {  // check the guessed entry against the published exit; redo on a mismatch
+      const int64_t real = wait_prev();
+      spec = false;
+      if (real != ext) {
+        ext = real;
+        continue;
+      }
+    }
+    break;
   }
   ndel = wave_sum_u64(ndel);
   if (ndel && lane == 0) atomicAdd(&P.st->n_deletes, ndel);
@@ -960,12 +1032,13 @@ __global__ __launch_bounds__(kPlaceLdsBlock) void k_place_lds(BuildParams P) {
 void launch_frame_fused(const BuildParams& P, hipStream_t s, StageTimer* tm) {
   if (P.fr_nchunks == 0) return;
   const uint64_t nwaves = (P.fr_nchunks + P.fr_w - 1) / P.fr_w;
-  // the screen's bitmap (one bit per chunk byte), later overlaid by the balanced walk's list
-  const size_t lds = (size_t)P.fr_rgn_bytes + std::max<size_t>(((size_t)P.fr_w << P.fr_cshift) / 8 + 8, kCandCap * 4);
+  // the screen's bitmap (one bit per candidate-window byte), later overlaid by the balanced walk's
+  // candidate list and then by the record list
+  const size_t lds = (size_t)P.fr_rgn_bytes + std::max<size_t>((size_t)P.fr_w * P.fr_mask_words * 8 + 8, kCandCap * 4);
   hipLaunchKernelGGL(k_frame, dim3((unsigned)nwaves), dim3(64), lds, s, P);
+  tm->mark("frame", s);  // the stage is k_frame alone (its rocprof row); the slab scan counts as partition
   scan_exclusive<uint32_t, uint64_t, OpAdd>(P.wcount, P.woff, P.nslabs, (uint64_t*)&P.st->n_records, OpAdd(),
                                             P.scan_scratch_u64, s);
-  tm->mark("frame", s);
 }
 
 void launch_dense_slabs(const BuildParams& P, hipStream_t s) {

@@ -25,8 +25,9 @@ using namespace sk;
 
 namespace {
 
-constexpr int64_t kFrameMinChunk = 256;  // k_frame chunk (one lane) lower bound
+constexpr int64_t kFrameMinChunk = 512;  // k_frame chunk (one lane) lower bound
 constexpr int64_t kFrameRegion = 8192;   // bytes of chunks per k_frame wave
+constexpr int64_t kFrameLook = 128;      // speculative walks continue this far past their chunk
 
 constexpr uint32_t kLogMagic = 0x49b39c95u;
 constexpr uint32_t kIndexMagic = 0x9a11318fu;
@@ -359,23 +360,33 @@ static int setup_params(const LogHdr& lh, const IndexParams& ip, const sparkey_b
   P.fr_entry = entry;
   P.ch_k0 = (uint64_t)entry >> kChunkShift;
   P.nchunks = any ? (uint64_t)((frame_end + kChunk - 1) / kChunk) - P.ch_k0 : 0;
-  // k_frame geometry: chunk C = max(256, nextpow2(maxRecLen)) so every chunk but a short last one
-  // holds a record start; 8 KiB of chunks per wave, staged contiguously with max(C, 256) bytes of
+  // k_frame geometry: chunk C = max(512, nextpow2(maxRecLen)) so every chunk but a short last one
+  // holds a record start; 8 KiB of chunks per wave, staged contiguously with 256 bytes of
   // look-ahead (about 10 KiB of LDS: 16 waves per CU); records longer than 4 KiB -> serial framing.
   {
     // chunk >= kFrameMinChunk and >= maxRecLen; a wave stages kFrameRegion bytes of chunks
     // (SPARKEY_FRAME_CMIN / SPARKEY_FRAME_REGION override both, for tuning)
-    int64_t cmin = kFrameMinChunk, region = kFrameRegion;
+    int64_t cmin = kFrameMinChunk, region = kFrameRegion, look = kFrameLook;
     if (const char* v = getenv("SPARKEY_FRAME_CMIN")) cmin = std::max<int64_t>(128, atoll(v));
-    if (const char* v = getenv("SPARKEY_FRAME_REGION")) region = std::max<int64_t>(4096, atoll(v));
+    if (const char* v = getenv("SPARKEY_FRAME_REGION")) region = std::min<int64_t>(16384, std::max<int64_t>(2048, atoll(v)));
+    if (const char* v = getenv("SPARKEY_FRAME_LOOK")) look = std::min<int64_t>(4096, std::max<int64_t>(16, atoll(v)));
     int cs = 7;
     while ((1ll << cs) < std::max<int64_t>(P.max_rec_len, cmin)) cs++;
     const int64_t C = 1ll << cs;
     P.fr_cshift = cs;
     P.fr_w = (int32_t)std::max<int64_t>(1, std::min<int64_t>(64, region / C));
-    P.fr_look = (int32_t)std::max<int64_t>(C, 256);
-    P.fr_rgn_bytes = (int32_t)(((int64_t)P.fr_w * C + P.fr_look + 16 + 255) & ~255LL);
+    P.fr_look = (int32_t)((look + 15) & ~15LL);
+    P.fr_rgn_bytes = (int32_t)(((int64_t)P.fr_w * C + P.fr_look + 16 + 1023) & ~1023LL);  // whole glds rows
     P.fr_mask_words = (int32_t)((std::min<int64_t>(C, P.max_rec_len) + 63) / 64);
+    if (P.max_rec_len <= 4096) {  // k_frame (fused framing) finds a screened word's chunk as (q * magic) >> 22
+      const uint32_t wpc = 8u * (uint32_t)P.fr_mask_words;
+      P.fr_wpc_magic = (uint32_t)(((1ull << 22) + wpc - 1) / wpc);
+      for (uint32_t q = 0; q < (uint32_t)P.fr_w * wpc; q++)
+        if ((uint32_t)(((uint64_t)q * P.fr_wpc_magic) >> 22) != q / wpc || (uint64_t)q * P.fr_wpc_magic >= (1ull << 32)) {
+          set_err(err, err_len, "k_frame screen geometry out of range");
+          return SPARKEY_E_ARG;
+        }
+    }
     P.fr_fast = lh.max_key_len + 1 < 128 && lh.max_value_len < 128;
     P.no_deletes = lh.num_deletes == 0;
     P.fr_k0 = (uint64_t)entry >> cs;

@@ -209,3 +209,27 @@ def test_header_hides_deletes(native):
     log = bytearray(make_log(key_value_puts(3000), deletes=[b"Key%d" % i for i in range(0, 3000, 5)]))
     struct.pack_into("<q", log, 24, 0)
     check(native, bytes(log), 21)
+
+
+# --- tiny records (2-6 bytes): many records per framing chunk; the speculative framing must stay on
+#     its fast path (a chunk whose candidate walk does not fit its record is walked exactly) ---
+def test_tiny_records_stay_on_fast_framing(native):
+    puts = random_puts(60000, seed=5, kmin=0, kmax=3, vmin=0, vmax=2)
+    got, stats = check(native, make_log(puts), 17, hash_size=8)
+    assert stats.framing_path == 0, stats.as_dict()
+
+
+# --- k_frame geometry overrides (chunk 256..2048 bytes, region, look-ahead): same bytes, fast path ---
+@pytest.mark.parametrize("env", [{"SPARKEY_FRAME_CMIN": "256"}, {"SPARKEY_FRAME_CMIN": "1024"},
+                                 {"SPARKEY_FRAME_CMIN": "2048"}, {"SPARKEY_FRAME_REGION": "16384"},
+                                 {"SPARKEY_FRAME_LOOK": "16"}, {"SPARKEY_FRAME_LOOK": "1024"}])
+def test_frame_geometry_overrides(native, monkeypatch, env):
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    rng = np.random.default_rng(3)
+    puts = [(b"%016d" % i, rng.integers(0, 256, 100, dtype=np.uint8).tobytes()) for i in range(40000)]
+    got, stats = check(native, make_log(puts), 23, hash_size=8)
+    assert stats.framing_path == 0, stats.as_dict()
+    puts = random_puts(30000, seed=9, kmin=0, kmax=3, vmin=0, vmax=2)
+    got, stats = check(native, make_log(puts), 29, hash_size=4)
+    assert stats.framing_path == 0, stats.as_dict()
