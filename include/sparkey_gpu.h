@@ -67,7 +67,8 @@ typedef struct sparkey_build_stats {
   int64_t total_displacement;
   int32_t hash_size;
   int32_t address_size;
-  int32_t placement_path;     /* 0 = parallel canonical placement, 1 = sequential device restatement */
+  int32_t placement_path;     /* 0 = parallel canonical placement, 1 = single-lane exact replay (full tables),
+                                 2 = exact replay over independent slot segments (DELETEs, overwrites) */
   int32_t framing_path;       /* 0 = speculative parallel framing, 1 = serial device walker */
   double device_ms;           /* device time of the build (HIP events), excluding copies */
 } sparkey_build_stats;

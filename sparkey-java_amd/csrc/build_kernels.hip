@@ -525,6 +525,127 @@ __global__ void k_sequential(BuildParams P, int sorted_order) {
 }
 
 // ================================================================================================
+// Exact path in parallel: independent slot segments.
+//
+// occ(S), the set of slots a linear-probing table of the multiset S of wanted slots occupies, does
+// not depend on insertion order, on the Robin-Hood tie rule, on in-place replacement or on
+// backward-shift deletion (every entry sits at w + d with slots w .. w + d all occupied), and it
+// grows with S.  Every table state IndexHash passes through holds a subset of the log's PUT keys, so
+// a slot left empty by the canonical placement of ALL PUT records (duplicates included, DELETEs left
+// out) is empty in every state: no put probe, delete probe or backward shift
+// (IndexHash.java:454-665) ever crosses it.  The runs of occupied slots of that placement --
+// segments -- are therefore independent.  Each one replays its own records, in the reference's
+// order (log order for IN_MEMORY, SortHelper's (wantedSlot, address) for SORTING), with the exact
+// seq_put / seq_delete, on its own slots; a DELETE whose wanted slot is empty there is a no-op in
+// every state.  The result is the reference's table byte for byte.
+// ================================================================================================
+constexpr uint64_t kNoSeg = ~0ull;
+
+__device__ __forceinline__ bool slot_occupied(const BuildParams& P, uint64_t slot) {
+  uint64_t h, a;
+  read_slot(P, slot, h, a);
+  return a != 0;
+}
+
+// One workgroup per slab: every record finds the first slot of the segment holding its wanted slot.
+__global__ __launch_bounds__(64) void k_seg_assign(BuildParams P) {
+  const uint64_t w = blockIdx.x;
+  const uint32_t n = P.wcount[w];
+  for (uint32_t j = threadIdx.x; j < n; j += 64) {
+    const uint64_t idx = w * (uint64_t)P.slab_cap + j;
+    uint64_t s = fast_mod(P.ent[idx].hash, P.mod);
+    uint64_t seg = kNoSeg;
+    if (slot_occupied(P, s)) {
+      for (uint64_t g = 0; g < P.cap; g++) {  // back to the empty slot before the run
+        const uint64_t prev = s ? s - 1 : P.cap - 1;
+        if (!slot_occupied(P, prev)) break;
+        s = prev;
+      }
+      seg = s;
+      atomicAdd(&P.seg_cnt[s], 1u);
+    }
+    P.eseg[idx] = seg;
+  }
+}
+
+// Records grouped by segment (any order inside a segment: the replay sorts them).
+__global__ __launch_bounds__(64) void k_seg_scatter(BuildParams P) {
+  const uint64_t w = blockIdx.x;
+  const uint32_t n = P.wcount[w];
+  for (uint32_t j = threadIdx.x; j < n; j += 64) {
+    const uint64_t idx = w * (uint64_t)P.slab_cap + j;
+    const uint64_t seg = P.eseg[idx];
+    if (seg == kNoSeg) continue;
+    const uint32_t r = atomicSub(&P.seg_cnt[seg], 1u) - 1u;
+    P.ent3[P.seg_off[seg] + r] = P.ent[idx];
+  }
+}
+
+// replay order: IN_MEMORY = address (log order); SORTING = (wantedSlot, address), SortHelper.java:153-171
+__device__ __forceinline__ bool seg_before(const BuildParams& P, const Entry& a, const Entry& b, int sorted_order) {
+  if (sorted_order) {
+    const uint64_t wa = fast_mod(a.hash, P.mod), wb = fast_mod(b.hash, P.mod);
+    if (wa != wb) return wa < wb;
+  }
+  return (a.addr & ~kDelBit) < (b.addr & ~kDelBit);
+}
+
+__device__ void seg_heapsort(const BuildParams& P, Entry* L, uint64_t n, int sorted_order) {
+  auto sift = [&](uint64_t root, uint64_t end) {
+    for (;;) {
+      uint64_t c = 2 * root + 1;
+      if (c >= end) return;
+      if (c + 1 < end && seg_before(P, L[c], L[c + 1], sorted_order)) c++;
+      if (!seg_before(P, L[root], L[c], sorted_order)) return;
+      const Entry t = L[root];
+      L[root] = L[c];
+      L[c] = t;
+      root = c;
+    }
+  };
+  for (uint64_t i = n / 2; i-- > 0;) sift(i, n);
+  for (uint64_t end = n; end-- > 1;) {
+    const Entry t = L[0];
+    L[0] = L[end];
+    L[end] = t;
+    sift(0, end);
+  }
+}
+
+// One thread per slot; the first slot of each segment replays the segment.
+__global__ __launch_bounds__(256) void k_seg_replay(BuildParams P, int sorted_order) {
+  const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= P.cap) return;
+  const uint64_t lo = P.seg_off[s], hi = P.seg_off[s + 1];
+  if (lo == hi) return;
+  Entry* L = P.ent3 + lo;
+  const uint64_t n = hi - lo;
+  seg_heapsort(P, L, n, sorted_order);
+  // the segment's slots: s up to the first empty slot (ring); cleared, then replayed
+  uint64_t t = s;
+  for (uint64_t g = 0; g < P.cap && slot_occupied(P, t); g++) {
+    write_slot(P, t, 0, 0);
+    t = t + 1 == P.cap ? 0 : t + 1;
+  }
+  SeqCtx c;
+  c.P = &P;
+  c.table = P.out + kIndexHeaderSize;
+  c.num_entries = 0;
+  c.garbage = 0;
+  for (uint64_t i = 0; i < n; i++) {
+    const Entry en = L[i];
+    const uint64_t addr = en.addr & ~kDelBit;
+    const int rc = (en.addr & kDelBit) ? seq_delete(c, en.hash, addr) : seq_put(c, en.hash, addr);
+    if (rc) {
+      set_error(P.st, (int64_t)(addr >> P.ebb), rc);
+      break;
+    }
+  }
+  if (c.num_entries) atomicAdd((unsigned long long*)&P.st->num_entries, (unsigned long long)c.num_entries);
+  if (c.garbage) atomicAdd((unsigned long long*)&P.st->garbage, (unsigned long long)c.garbage);
+}
+
+// ================================================================================================
 // host-side launchers (called by the plan in sparkey_gpu.cpp)
 // ================================================================================================
 static inline unsigned grid_for(uint64_t n, unsigned block) { return (unsigned)((n + block - 1) / block); }
@@ -575,6 +696,16 @@ void launch_stats(const BuildParams& P, hipStream_t s, int sequential, StageTime
 
 void launch_sequential(const BuildParams& P, hipStream_t s, int sorted_order) {
   hipLaunchKernelGGL(k_sequential, dim3(1), dim3(64), 0, s, P, sorted_order);
+}
+
+// seg_cnt zeroed and num_entries / garbage reset by the caller; ent3 holds the grouped records
+void launch_segments(const BuildParams& P, hipStream_t s, int sorted_order, StageTimer* tm) {
+  if (P.nslabs) hipLaunchKernelGGL(k_seg_assign, dim3((unsigned)P.nslabs), dim3(64), 0, s, P);
+  scan_exclusive<uint32_t, uint64_t, OpAdd>(P.seg_cnt, P.seg_off, P.cap, P.seg_off + P.cap, OpAdd(),
+                                            P.scan_scratch_u64, s);
+  if (P.nslabs) hipLaunchKernelGGL(k_seg_scatter, dim3((unsigned)P.nslabs), dim3(64), 0, s, P);
+  hipLaunchKernelGGL(k_seg_replay, dim3(grid_for(P.cap, 256)), dim3(256), 0, s, P, sorted_order);
+  tm->mark("exact", s);
 }
 
 }  // namespace sk

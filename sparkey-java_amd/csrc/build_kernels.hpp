@@ -174,6 +174,12 @@ struct BuildParams {
   uint64_t prev_hash;
   SpillEntry* spill;
   uint64_t spill_cap;
+  // exact path over independent slot segments (k_seg_*): the radix partition leaves DELETE records
+  // out of the canonical placement when skip_del is set
+  int32_t skip_del;
+  uint64_t* eseg;     // per slab entry: first slot of its segment, or kNoSeg
+  uint32_t* seg_cnt;  // per slot: records of the segment starting there
+  uint64_t* seg_off;  // exclusive prefix of seg_cnt (cap + 1)
 };
 
 // Per-stage HIP events on the build stream (only when profiling is enabled).
@@ -219,6 +225,8 @@ void launch_place_global(const BuildParams& P, hipStream_t s, int sort_only, int
 void launch_verify(const BuildParams& P, hipStream_t s, StageTimer* tm);
 void launch_stats(const BuildParams& P, hipStream_t s, int sequential, StageTimer* tm);
 void launch_sequential(const BuildParams& P, hipStream_t s, int sorted_order);
+void launch_segments(const BuildParams& P, hipStream_t s, int sorted_order, StageTimer* tm);
+void launch_partition_quiet(const BuildParams& P, hipStream_t s);
 // sharded builds (shard_kernels.hip)
 void launch_dest_counts(const BuildParams& P, hipStream_t s, int world, uint32_t nd, uint64_t* d_out);
 void launch_apply_spill(const BuildParams& P, hipStream_t s, const SpillEntry* in, uint64_t n);

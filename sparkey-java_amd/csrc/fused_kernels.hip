@@ -827,8 +827,11 @@ __global__ __launch_bounds__(kPartBlock) void k_part1_hist(BuildParams P) {
   const uint64_t g0 = (uint64_t)blockIdx.x * P.part_group;
   hist[threadIdx.x] = 0;
   const uint32_t n = load_tile(P, T, g0);
-  for (uint32_t i = threadIdx.x; i < n; i += kPartBlock)
-    atomicAdd(&hist[digit_of(P, bucket_of(P, tile_entry(P, T, g0, i).hash))], 1u);
+  for (uint32_t i = threadIdx.x; i < n; i += kPartBlock) {
+    const Entry& en = tile_entry(P, T, g0, i);
+    if (P.skip_del && (en.addr & kDelBit)) continue;  // exact path: DELETEs stay out of the placement
+    atomicAdd(&hist[digit_of(P, bucket_of(P, en.hash))], 1u);
+  }
   __syncthreads();
   P.p1_hist[(uint64_t)threadIdx.x * P.p1_tiles + blockIdx.x] = hist[threadIdx.x];  // digit-major
 }
@@ -843,7 +846,7 @@ __global__ __launch_bounds__(kPartBlock) void k_part1_scatter(BuildParams P) {
   const uint64_t g0 = (uint64_t)blockIdx.x * P.part_group;
   const int tid = threadIdx.x;
   const uint32_t h = P.p1_hist[(uint64_t)tid * P.p1_tiles + blockIdx.x];
-  lbase[tid] = (uint32_t)block_excl_sum<kPartBlock>(h, sh64, nullptr);
+  lbase[tid] = (uint32_t)block_excl_sum<kPartBlock>(h, sh64, &sh64[kPartBlock / 64]);
   cursor[tid] = 0;
   const uint32_t n = load_tile(P, T, g0);
   Entry v[kPartItems];
@@ -857,14 +860,15 @@ __global__ __launch_bounds__(kPartBlock) void k_part1_scatter(BuildParams P) {
   for (int i = 0; i < kPartItems; i++) {
     const uint32_t idx = (uint32_t)i * kPartBlock + tid;
     d[i] = 0xffffffffu;
-    if (idx < n) {
+    if (idx < n && !(P.skip_del && (v[i].addr & kDelBit))) {
       d[i] = digit_of(P, bucket_of(P, v[i].hash));
       stage[lbase[d[i]] + atomicAdd(&cursor[d[i]], 1u)] = v[i];
     }
   }
   __syncthreads();
+  const uint32_t nkeep = (uint32_t)sh64[kPartBlock / 64];  // the tile's entries in the placement
   // coalesced write-out: LDS position i -> global offset of its digit run
-  for (uint32_t i = tid; i < n; i += kPartBlock) {
+  for (uint32_t i = tid; i < nkeep; i += kPartBlock) {
     const Entry en = stage[i];
     const uint32_t dd = digit_of(P, bucket_of(P, en.hash));
     const uint64_t dst = P.p1_off[(uint64_t)dd * P.p1_tiles + blockIdx.x] + (i - lbase[dd]);
@@ -1050,6 +1054,11 @@ void launch_partition1(const BuildParams& P, hipStream_t s) {
   scan_exclusive<uint32_t, uint64_t, OpAdd>(P.p1_hist, P.p1_off, (uint64_t)P.p1_tiles * 256, P.p1_off_total,
                                             OpAdd(), P.scan_scratch_u64, s);
   hipLaunchKernelGGL(k_part1_scatter, dim3((unsigned)P.p1_tiles), dim3(kPartBlock), 0, s, P);
+}
+
+void launch_partition_quiet(const BuildParams& P, hipStream_t s) {
+  launch_partition1(P, s);
+  hipLaunchKernelGGL(k_part2, dim3(256), dim3(kPart2Block), (size_t)(2u * P.bpp) * sizeof(uint32_t), s, P);
 }
 
 void launch_partition(const BuildParams& P, hipStream_t s, StageTimer* tm) {

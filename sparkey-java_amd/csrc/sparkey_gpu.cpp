@@ -6,6 +6,7 @@
 // the 112-byte header template (IndexHeader.java:125-155) and drive the device pipeline in
 // build_kernels.hip.  Errors map to the reference's exceptions (include/sparkey_gpu.h).
 #include <errno.h>
+#include <stddef.h>
 #include <fcntl.h>
 #include <hip/hip_runtime.h>
 #include <stdio.h>
@@ -242,6 +243,10 @@ struct sparkey_plan {
   uint64_t c_bcount = 0, c_bcursor = 0, c_boff = 0, c_bfun = 0, c_bpre = 0, c_carry = 0;
   uint64_t c_pairs = 0, c_parts = 0, c_su = 0, c_smp = 0, c_bft = 0;
   uint64_t c_desc = 0, c_p1h = 0, c_p1o = 0, c_dbg = 0, c_wcount = 0, c_woff = 0;
+  uint64_t c_eseg = 0, c_seg_cnt = 0, c_seg_off = 0;
+  uint64_t* eseg = nullptr;     // exact path: per slab entry, the first slot of its segment
+  uint32_t* seg_cnt = nullptr;  // exact path: per slot, records of the segment starting there
+  uint64_t* seg_off = nullptr;
   uint8_t* conv = nullptr;
   int64_t* exitp = nullptr;
   int64_t* qpos = nullptr;
@@ -510,6 +515,7 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
   if (rc) return rc;
   P.out = d_out;
   P.st = pl->d_status;
+  P.skip_del = 1;  // DELETEs stay out of the canonical placement (the exact path's segments)
   const bool fused_framing = P.max_rec_len <= 4096;
 
   uint64_t nrec = (uint64_t)std::max<int64_t>(0, lh.num_puts) + (uint64_t)std::max<int64_t>(0, lh.num_deletes);
@@ -571,14 +577,39 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
     set_err(err, err_len, "Corrupt log file: framing did not converge");
     return SPARKEY_E_CORRUPT_LOG;
   }
-  // Logs outside the canonical case go through the exact sequential restatement on the device.
+  // Logs outside the canonical case (DELETEs, duplicate keys) replay the reference's put/delete
+  // exactly: per independent slot segment of the canonical PUT placement (placement_path 2), or,
+  // when that placement left no empty slot, on one lane over the whole table (placement_path 1).
   if (st.n_deletes > 0 || st.dup || st.dup_overflow || st.full || st.n_pairs > P.pair_cap) {
-    placement_path = 1;
+    const bool serial = st.full || getenv("SPARKEY_EXACT_SERIAL") != nullptr;
+    placement_path = serial ? 1 : 2;
     float ms2 = 0.f;
     HIP_TRY(hipEventRecord(pl->ev0, s));
-    if (!ip.in_memory) launch_place_global(P, s, 1, 0);  // (wantedSlot, address) order into ent3
-    HIP_TRY(hipMemsetAsync(d_out + kIndexHeaderSize, 0, (size_t)(ip.index_size - kIndexHeaderSize), s));
-    launch_sequential(P, s, ip.in_memory ? 0 : 1);
+    if (serial) {
+      BuildParams Pd = P;
+      Pd.skip_del = 0;  // the single lane replays every record
+      if (!ip.in_memory) {
+        launch_partition_quiet(Pd, s);
+        launch_place_global(Pd, s, 1, 0);  // (wantedSlot, address) order into ent3
+      }
+      HIP_TRY(hipMemsetAsync(d_out + kIndexHeaderSize, 0, (size_t)(ip.index_size - kIndexHeaderSize), s));
+      launch_sequential(Pd, s, ip.in_memory ? 0 : 1);
+    } else {
+      HIP_TRY(grow(&pl->eseg, pl->c_eseg, P.nslabs * (uint64_t)P.slab_cap));
+      HIP_TRY(grow(&pl->seg_cnt, pl->c_seg_cnt, P.cap));
+      HIP_TRY(grow(&pl->seg_off, pl->c_seg_off, P.cap + 1));
+      const uint64_t scratch = P.cap / kScanTile + 64;
+      if (pl->c_su < scratch + 16) {
+        HIP_TRY(grow(&pl->scan_u64, pl->c_su, scratch + 16));
+        P.scan_scratch_u64 = pl->scan_u64;
+      }
+      P.eseg = pl->eseg;
+      P.seg_cnt = pl->seg_cnt;
+      P.seg_off = pl->seg_off;
+      HIP_TRY(hipMemsetAsync(P.seg_cnt, 0, P.cap * sizeof(uint32_t), s));
+      HIP_TRY(hipMemsetAsync((uint8_t*)pl->d_status + offsetof(Status, num_entries), 0, 2 * sizeof(long long), s));
+      launch_segments(P, s, ip.in_memory ? 0 : 1, &pl->timer);
+    }
     launch_stats(P, s, 1, &pl->timer);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(pl->ev1, s));
@@ -678,7 +709,8 @@ void sparkey_plan_destroy(sparkey_plan* pl) {
   (void)hipSetDevice(pl->device);
   void* bufs[] = {pl->conv, pl->exitp, pl->qpos, pl->tail, pl->G, pl->cnt, pl->off, pl->ent, pl->ent2, pl->ent3,
                   pl->bcount, pl->bcursor, pl->boff, pl->bfun, pl->bpre, pl->bfun_total, pl->carry, pl->pairs,
-                  pl->parts, pl->scan_u64, pl->scan_mp, pl->desc, pl->p1_hist, pl->p1_off, pl->d_status, pl->dbg, pl->wcount, pl->woff, pl->small};
+                  pl->parts, pl->scan_u64, pl->scan_mp, pl->desc, pl->p1_hist, pl->p1_off, pl->d_status, pl->dbg, pl->wcount, pl->woff, pl->small,
+                  pl->eseg, pl->seg_cnt, pl->seg_off};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (pl->h_status) (void)hipHostFree(pl->h_status);
