@@ -5,6 +5,7 @@ header) of a C2-shaped log (10M PUTs per GPU, 16-byte keys, 100-byte values, NON
 resident in HBM, into a device-resident .spi image.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--entries 10000000] [--no-cpu-baseline]
+                    [--workload c2|c3|c5|churn]
 
 N = 1: the C2 log (10M records) built on one GPU; the line carries the per-stage roofline and the
 CPU baseline (the oracle's sequential IN_MEMORY restatement on the host, timed on the same log).
@@ -41,6 +42,7 @@ def stage_bytes(stage, n, data_end, slot, cap):
         "summary": 16 * n,                    # entries read once
         "place": 16 * n + slot * cap,         # entries read once, every slot written once
         "stats": slot * cap,                  # table read once
+        "exact": 3 * 16 * n + 2 * slot * cap,  # entries read, grouped, replayed; segment slots cleared + written
     }.get(stage, 0)
 
 
@@ -52,19 +54,36 @@ def pmc_traffic(stage):
         return None
 
 
+WORKLOADS = {
+    "c2": {"name": "C2: 10M PUTs x (16 B key, 100 B value), CompressionType.NONE, IN_MEMORY", "sorting": False,
+           "path": 0},
+    "c3": {"name": "C3: PUTs x (8-64 B key, 100 B value), CompressionType.NONE, IN_MEMORY", "sorting": False,
+           "path": 0},
+    "c5": {"name": "C5: C3 log, SORTING constructionMethod", "sorting": True, "path": 0},
+    "churn": {"name": "C2 shape with overwrites and DELETEs: keys from a pool of 0.8 n, 10% DELETE records, "
+                      "IN_MEMORY (exact replay over slot segments)", "sorting": False, "path": 2},
+}
+
+
 def single_gpu(args, dev):
     import sparkey
     from sparkey import _native, synth
 
     n = args.entries
+    wl = WORKLOADS[args.workload]
+    method = _native.METHOD_SORTING if wl["sorting"] else _native.METHOD_IN_MEMORY
     t0 = time.time()
-    log_np = synth.fixed_log(n, 16, 100, seed=args.seed, file_id=0x5EED0000)
+    if args.workload == "c2":
+        log_np = synth.fixed_log(n, 16, 100, seed=args.seed, file_id=0x5EED0000)
+    elif args.workload in ("c3", "c5"):
+        log_np = synth.mixed_log(n, 8, 64, 100, seed=args.seed + 2)
+    else:
+        log_np = synth.churn_log(n, int(n * 0.8), 0.1, seed=args.seed + 4)
     gen_s = time.time() - t0
     header = log_np[:84].tobytes()
     log_len = log_np.size
     d_log = torch.from_numpy(log_np).to(dev)
-    opts = _native.make_opts(hash_size=0, hash_seed=HASH_SEED, sparsity=0.0, method=_native.METHOD_IN_MEMORY,
-                             device=dev.index)
+    opts = _native.make_opts(hash_size=0, hash_seed=HASH_SEED, sparsity=0.0, method=method, device=dev.index)
     out_len = _native.index_size(header, opts)
     d_out = torch.empty(out_len, dtype=torch.uint8, device=dev)
     plan = _native.Plan(dev.index, log_len, n)
@@ -98,7 +117,8 @@ def single_gpu(args, dev):
     dom_bytes = stage_bytes(dom, n, log_len, slot, cap) if dom else 0
     achieved = dom_bytes / (stage_ms[dom] * 1e-3) / 1e9 if dom and stage_ms[dom] > 0 else 0.0
     b_alg = (log_len - 84) + 112 + slot * cap
-    assert stats.num_entries == n and stats.placement_path == 0, stats.as_dict()
+    assert stats.placement_path == wl["path"] and stats.framing_path == 0, stats.as_dict()
+    assert wl["path"] != 0 or stats.num_entries == n, stats.as_dict()
 
     # host-to-host rate (north_star): H2D of the log from pinned memory, the build, D2H of the .spi
     pinned = torch.from_numpy(log_np).pin_memory()
@@ -120,16 +140,17 @@ def single_gpu(args, dev):
         oracle.build()
         log_bytes = log_np.tobytes()
         t2 = time.perf_counter()
-        want = oracle.build_index(log_bytes, HASH_SEED, method=oracle.IN_MEMORY)
+        mname = "SORTING" if wl["sorting"] else "IN_MEMORY"
+        want = oracle.build_index(log_bytes, HASH_SEED, method=oracle.SORTING if wl["sorting"] else oracle.IN_MEMORY)
         cpu_s = time.perf_counter() - t2
         got = d_out.cpu().numpy().tobytes()
         cpu = {"value": n / cpu_s, "unit": "keys/s", "cores": 1, "kind": "port",
-               "sample": f"full C2 log ({n} entries), oracle IN_MEMORY sequential restatement (oracle/), 1 thread, "
-                         f"{cpu_s:.2f} s", "bit_identical_to_gpu": got == want}
+               "sample": f"full {args.workload.upper()} log ({n} records), oracle {mname} sequential restatement "
+                         f"(oracle/), 1 thread, {cpu_s:.2f} s", "bit_identical_to_gpu": got == want}
     plan.close()
     return {
         "value": n * args.steps / elapsed, "ms_per_step": ms_per_step,
-        "config": {"workload": "C2: 10M PUTs x (16 B key, 100 B value), CompressionType.NONE, IN_MEMORY",
+        "config": {"workload": wl["name"],
                    "entries": n, "log_bytes": int(log_len), "hash_bytes": stats.hash_size,
                    "address_bytes": stats.address_size, "capacity": int(cap), "spi_bytes": int(out_len),
                    "parallelism": "single"},
@@ -215,6 +236,8 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--entries", type=int, default=10_000_000)
+    ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS),
+                    help="c2 (the headline metric); c3 / c5 / churn are extra single-GPU measurements")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--backend", default="nccl", help="nccl (RCCL); gloo only to rehearse N > 1 ranks on one GPU")

@@ -11,8 +11,6 @@
 //                   order for the SORTING restatement.
 //   k_verify_pairs  equal-hash PUT pairs: same key?  (IndexHash.java:606-636)
 //   k_stats         calculateMaxDisplacement (IndexHash.java:195-245), header patch.
-//   k_sequential    single-lane restatement of put/delete (IndexHash.java:454-665) for logs the
-//                   canonical layout does not cover (DELETEs, duplicate keys, full tables).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -335,317 +333,6 @@ __global__ __launch_bounds__(256) void k_stats_final(BuildParams P, uint32_t npa
 }
 
 // ================================================================================================
-// Exact sequential restatement (IndexHash.put/delete, IndexHash.java:454-665) on the device table,
-// one lane.  IN_MEMORY order: entries in log order (ent).  SORTING order: (wantedSlot, address)
-// per bucket (ent3) -- SortHelper's comparator.  Keys are compared in the log in HBM.
-// ================================================================================================
-struct SeqCtx {
-  const BuildParams* P;
-  uint8_t* table;
-  int64_t num_entries;
-  int64_t garbage;
-};
-
-__device__ uint64_t seq_rd(const uint8_t* p, int n) {
-  uint64_t v = 0;
-  for (int i = 0; i < n; i++) v |= (uint64_t)p[i] << (8 * i);
-  return v;
-}
-__device__ void seq_wr(uint8_t* p, int n, uint64_t v) {
-  for (int i = 0; i < n; i++) p[i] = (uint8_t)(v >> (8 * i));
-}
-__device__ __forceinline__ uint64_t seq_hash(const SeqCtx& c, int64_t slot) {
-  return seq_rd(c.table + slot * c.P->slot_size, c.P->hash_size);
-}
-__device__ __forceinline__ uint64_t seq_addr(const SeqCtx& c, int64_t slot) {
-  return seq_rd(c.table + slot * c.P->slot_size + c.P->hash_size, c.P->addr_size);
-}
-__device__ __forceinline__ void seq_write(SeqCtx& c, int64_t slot, uint64_t h, uint64_t a) {
-  uint8_t* p = c.table + slot * c.P->slot_size;
-  seq_wr(p, c.P->hash_size, h);
-  seq_wr(p + c.P->hash_size, c.P->addr_size, a);
-}
-__device__ __forceinline__ int64_t seq_disp(const SeqCtx& c, int64_t slot, uint64_t hash) {
-  int64_t d = slot - (int64_t)fast_mod(hash, c.P->mod);
-  return d >= 0 ? d : d + (int64_t)c.P->cap;
-}
-__device__ __forceinline__ int32_t vlq_size_i32(int64_t v) {
-  if (v < (1 << 7)) return 1;
-  if (v < (1 << 14)) return 2;
-  if (v < (1 << 21)) return 3;
-  if (v < (1 << 28)) return 4;
-  return 5;
-}
-__device__ __forceinline__ int64_t garbage_of(int32_t k2, int32_t v2) {  // IndexHeader.java:221-228
-  return (int32_t)((uint32_t)k2 + (uint32_t)v2 + (uint32_t)vlq_size_i32((int64_t)k2 + 1) + (uint32_t)vlq_size_i32(v2));
-}
-
-// returns 0, or an error code
-__device__ int seq_put(SeqCtx& c, uint64_t hash, uint64_t address) {
-  const BuildParams& P = *c.P;
-  const int64_t cap = (int64_t)P.cap;
-  if (c.num_entries >= cap) return kErrNoFreeSlots;
-  auto at = [&](int64_t a) -> uint32_t { return P.log[a]; };
-  int64_t slot = (int64_t)fast_mod(hash, P.mod);
-  int64_t displacement = 0, tries = cap;
-  int64_t position = (int64_t)(address >> P.ebb);
-  bool might = true;
-  int32_t own_klen = -1;
-  int64_t own_key = 0;
-  while (--tries >= 0) {
-    const uint64_t hash2 = seq_hash(c, slot);
-    const uint64_t address2 = seq_addr(c, slot);
-    if (address2 == 0) {
-      seq_write(c, slot, hash, address);
-      c.num_entries++;
-      return 0;
-    }
-    const int64_t position2 = (int64_t)(address2 >> P.ebb);
-    if (might && hash == hash2) {
-      if (own_klen == -1) {
-        const RecHdr h = decode_header(at, position, (int64_t)P.log_len);
-        if (h.rc) return h.rc;
-        if (!h.put) return kErrCorruptData;
-        own_klen = h.klen;
-        own_key = position + h.hlen;
-      }
-      const RecHdr h2 = decode_header(at, position2, (int64_t)P.log_len);
-      if (h2.rc) return h2.rc;
-      if (!h2.put) return kErrCorruptData;  // "Invalid data - reference to delete entry"
-      if (own_klen == h2.klen) {
-        bool eq = true;
-        const int64_t k2 = position2 + h2.hlen;
-        for (int32_t j = 0; j < own_klen && eq; j++) eq = P.log[own_key + j] == P.log[k2 + j];
-        if (eq) {
-          seq_write(c, slot, hash, address);
-          c.garbage += garbage_of(h2.klen, h2.vlen);
-          return 0;
-        }
-      }
-    }
-    const int64_t other = seq_disp(c, slot, hash2);
-    if (displacement > other || (displacement == other && (int64_t)address < (int64_t)address2)) {
-      seq_write(c, slot, hash, address);
-      position = position2;
-      address = address2;
-      displacement = other;
-      hash = hash2;
-      might = false;
-    }
-    displacement++;
-    slot++;
-    if (slot >= cap) slot = 0;
-  }
-  return kErrNoFreeSlots;
-}
-
-__device__ int seq_delete(SeqCtx& c, uint64_t hash, uint64_t address) {
-  const BuildParams& P = *c.P;
-  const int64_t cap = (int64_t)P.cap;
-  auto at = [&](int64_t a) -> uint32_t { return P.log[a]; };
-  int64_t slot = (int64_t)fast_mod(hash, P.mod);
-  int64_t displacement = 0;
-  const int64_t position = (int64_t)(address >> P.ebb);
-  int32_t own_klen = -1;
-  int64_t own_key = 0;
-  for (int64_t guard = 0; guard <= cap; guard++) {
-    const uint64_t hash2 = seq_hash(c, slot);
-    const uint64_t address2 = seq_addr(c, slot);
-    if (address2 == 0) return 0;
-    const int64_t position2 = (int64_t)(address2 >> P.ebb);
-    if (hash == hash2) {
-      if (own_klen == -1) {
-        const RecHdr h = decode_header(at, position, (int64_t)P.log_len);
-        if (h.rc) return h.rc;
-        if (h.put) return kErrCorruptData;
-        own_klen = h.klen;
-        own_key = position + h.hlen;
-      }
-      const RecHdr h2 = decode_header(at, position2, (int64_t)P.log_len);
-      if (h2.rc) return h2.rc;
-      if (!h2.put) return kErrCorruptData;
-      if (own_klen == h2.klen) {
-        bool eq = true;
-        const int64_t k2 = position2 + h2.hlen;
-        for (int32_t j = 0; j < own_klen && eq; j++) eq = P.log[own_key + j] == P.log[k2 + j];
-        if (eq) {
-          for (int64_t g2 = 0; g2 < cap; g2++) {  // backward shift, IndexHash.java:503-524
-            int64_t next = slot + 1;
-            if (next == cap) next = 0;
-            const uint64_t hash3 = seq_hash(c, next);
-            const uint64_t pos3 = seq_addr(c, next);
-            if (pos3 == 0) break;
-            if ((int64_t)fast_mod(hash3, P.mod) == next) break;
-            seq_write(c, slot, hash3, pos3);
-            slot = next;
-          }
-          seq_write(c, slot, 0, 0);
-          c.garbage += garbage_of(h2.klen, h2.vlen);
-          c.num_entries--;
-          return 0;
-        }
-      }
-    }
-    const int64_t other = seq_disp(c, slot, hash2);
-    if (displacement > other) return 0;
-    displacement++;
-    slot++;
-    if (slot == cap) slot = 0;
-  }
-  return 0;
-}
-
-__global__ void k_sequential(BuildParams P, int sorted_order) {
-  if (blockIdx.x != 0 || threadIdx.x != 0) return;
-  SeqCtx c;
-  c.P = &P;
-  c.table = P.out + kIndexHeaderSize;
-  c.num_entries = 0;
-  c.garbage = 0;
-  const uint64_t N = min((uint64_t)P.st->n_records, P.max_records);
-  uint64_t w = 0, j = 0;  // IN_MEMORY: log order = slab order
-  for (uint64_t i = 0; i < N; i++) {
-    Entry en;
-    if (sorted_order) {
-      en = P.ent3[i];
-    } else {
-      while (j >= P.wcount[w]) { w++; j = 0; }
-      en = P.ent[w * P.slab_cap + j];
-      j++;
-    }
-    const uint64_t addr = en.addr & ~kDelBit;
-    const int rc = (en.addr & kDelBit) ? seq_delete(c, en.hash, addr) : seq_put(c, en.hash, addr);
-    if (rc) {
-      set_error(P.st, (int64_t)(addr >> P.ebb), rc);
-      break;
-    }
-  }
-  P.st->num_entries = c.num_entries;
-  P.st->garbage = c.garbage;
-}
-
-// ================================================================================================
-// Exact path in parallel: independent slot segments.
-//
-// occ(S), the set of slots a linear-probing table of the multiset S of wanted slots occupies, does
-// not depend on insertion order, on the Robin-Hood tie rule, on in-place replacement or on
-// backward-shift deletion (every entry sits at w + d with slots w .. w + d all occupied), and it
-// grows with S.  Every table state IndexHash passes through holds a subset of the log's PUT keys, so
-// a slot left empty by the canonical placement of ALL PUT records (duplicates included, DELETEs left
-// out) is empty in every state: no put probe, delete probe or backward shift
-// (IndexHash.java:454-665) ever crosses it.  The runs of occupied slots of that placement --
-// segments -- are therefore independent.  Each one replays its own records, in the reference's
-// order (log order for IN_MEMORY, SortHelper's (wantedSlot, address) for SORTING), with the exact
-// seq_put / seq_delete, on its own slots; a DELETE whose wanted slot is empty there is a no-op in
-// every state.  The result is the reference's table byte for byte.
-// ================================================================================================
-constexpr uint64_t kNoSeg = ~0ull;
-
-__device__ __forceinline__ bool slot_occupied(const BuildParams& P, uint64_t slot) {
-  uint64_t h, a;
-  read_slot(P, slot, h, a);
-  return a != 0;
-}
-
-// One workgroup per slab: every record finds the first slot of the segment holding its wanted slot.
-__global__ __launch_bounds__(64) void k_seg_assign(BuildParams P) {
-  const uint64_t w = blockIdx.x;
-  const uint32_t n = P.wcount[w];
-  for (uint32_t j = threadIdx.x; j < n; j += 64) {
-    const uint64_t idx = w * (uint64_t)P.slab_cap + j;
-    uint64_t s = fast_mod(P.ent[idx].hash, P.mod);
-    uint64_t seg = kNoSeg;
-    if (slot_occupied(P, s)) {
-      for (uint64_t g = 0; g < P.cap; g++) {  // back to the empty slot before the run
-        const uint64_t prev = s ? s - 1 : P.cap - 1;
-        if (!slot_occupied(P, prev)) break;
-        s = prev;
-      }
-      seg = s;
-      atomicAdd(&P.seg_cnt[s], 1u);
-    }
-    P.eseg[idx] = seg;
-  }
-}
-
-// Records grouped by segment (any order inside a segment: the replay sorts them).
-__global__ __launch_bounds__(64) void k_seg_scatter(BuildParams P) {
-  const uint64_t w = blockIdx.x;
-  const uint32_t n = P.wcount[w];
-  for (uint32_t j = threadIdx.x; j < n; j += 64) {
-    const uint64_t idx = w * (uint64_t)P.slab_cap + j;
-    const uint64_t seg = P.eseg[idx];
-    if (seg == kNoSeg) continue;
-    const uint32_t r = atomicSub(&P.seg_cnt[seg], 1u) - 1u;
-    P.ent3[P.seg_off[seg] + r] = P.ent[idx];
-  }
-}
-
-// replay order: IN_MEMORY = address (log order); SORTING = (wantedSlot, address), SortHelper.java:153-171
-__device__ __forceinline__ bool seg_before(const BuildParams& P, const Entry& a, const Entry& b, int sorted_order) {
-  if (sorted_order) {
-    const uint64_t wa = fast_mod(a.hash, P.mod), wb = fast_mod(b.hash, P.mod);
-    if (wa != wb) return wa < wb;
-  }
-  return (a.addr & ~kDelBit) < (b.addr & ~kDelBit);
-}
-
-__device__ void seg_heapsort(const BuildParams& P, Entry* L, uint64_t n, int sorted_order) {
-  auto sift = [&](uint64_t root, uint64_t end) {
-    for (;;) {
-      uint64_t c = 2 * root + 1;
-      if (c >= end) return;
-      if (c + 1 < end && seg_before(P, L[c], L[c + 1], sorted_order)) c++;
-      if (!seg_before(P, L[root], L[c], sorted_order)) return;
-      const Entry t = L[root];
-      L[root] = L[c];
-      L[c] = t;
-      root = c;
-    }
-  };
-  for (uint64_t i = n / 2; i-- > 0;) sift(i, n);
-  for (uint64_t end = n; end-- > 1;) {
-    const Entry t = L[0];
-    L[0] = L[end];
-    L[end] = t;
-    sift(0, end);
-  }
-}
-
-// One thread per slot; the first slot of each segment replays the segment.
-__global__ __launch_bounds__(256) void k_seg_replay(BuildParams P, int sorted_order) {
-  const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= P.cap) return;
-  const uint64_t lo = P.seg_off[s], hi = P.seg_off[s + 1];
-  if (lo == hi) return;
-  Entry* L = P.ent3 + lo;
-  const uint64_t n = hi - lo;
-  seg_heapsort(P, L, n, sorted_order);
-  // the segment's slots: s up to the first empty slot (ring); cleared, then replayed
-  uint64_t t = s;
-  for (uint64_t g = 0; g < P.cap && slot_occupied(P, t); g++) {
-    write_slot(P, t, 0, 0);
-    t = t + 1 == P.cap ? 0 : t + 1;
-  }
-  SeqCtx c;
-  c.P = &P;
-  c.table = P.out + kIndexHeaderSize;
-  c.num_entries = 0;
-  c.garbage = 0;
-  for (uint64_t i = 0; i < n; i++) {
-    const Entry en = L[i];
-    const uint64_t addr = en.addr & ~kDelBit;
-    const int rc = (en.addr & kDelBit) ? seq_delete(c, en.hash, addr) : seq_put(c, en.hash, addr);
-    if (rc) {
-      set_error(P.st, (int64_t)(addr >> P.ebb), rc);
-      break;
-    }
-  }
-  if (c.num_entries) atomicAdd((unsigned long long*)&P.st->num_entries, (unsigned long long)c.num_entries);
-  if (c.garbage) atomicAdd((unsigned long long*)&P.st->garbage, (unsigned long long)c.garbage);
-}
-
-// ================================================================================================
 // host-side launchers (called by the plan in sparkey_gpu.cpp)
 // ================================================================================================
 static inline unsigned grid_for(uint64_t n, unsigned block) { return (unsigned)((n + block - 1) / block); }
@@ -692,20 +379,6 @@ void launch_stats(const BuildParams& P, hipStream_t s, int sequential, StageTime
   if (nparts) hipLaunchKernelGGL(k_stats, dim3((unsigned)nparts), dim3(kStatBlock), 0, s, P);
   hipLaunchKernelGGL(k_stats_final, dim3(1), dim3(256), 0, s, P, (uint32_t)nparts, sequential);
   tm->mark("stats", s);
-}
-
-void launch_sequential(const BuildParams& P, hipStream_t s, int sorted_order) {
-  hipLaunchKernelGGL(k_sequential, dim3(1), dim3(64), 0, s, P, sorted_order);
-}
-
-// seg_cnt zeroed and num_entries / garbage reset by the caller; ent3 holds the grouped records
-void launch_segments(const BuildParams& P, hipStream_t s, int sorted_order, StageTimer* tm) {
-  if (P.nslabs) hipLaunchKernelGGL(k_seg_assign, dim3((unsigned)P.nslabs), dim3(64), 0, s, P);
-  scan_exclusive<uint32_t, uint64_t, OpAdd>(P.seg_cnt, P.seg_off, P.cap, P.seg_off + P.cap, OpAdd(),
-                                            P.scan_scratch_u64, s);
-  if (P.nslabs) hipLaunchKernelGGL(k_seg_scatter, dim3((unsigned)P.nslabs), dim3(64), 0, s, P);
-  hipLaunchKernelGGL(k_seg_replay, dim3(grid_for(P.cap, 256)), dim3(256), 0, s, P, sorted_order);
-  tm->mark("exact", s);
 }
 
 }  // namespace sk

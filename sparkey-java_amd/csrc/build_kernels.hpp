@@ -81,6 +81,9 @@ struct Status {
   unsigned int pad2;
   long long exit;                // first record start >= the frame end on the framed chain
   unsigned long long n_spill;    // sharded placement: slots written outside the rank's range
+  unsigned long long n_segs[4];  // exact path: segments per size class (small, mid, large, huge)
+  unsigned int guard;            // exact path: bounds-check bits that tripped (a bug; fails the build)
+  unsigned int pad3;
 };
 
 struct BuildParams {
@@ -180,6 +183,10 @@ struct BuildParams {
   uint64_t* eseg;     // per slab entry: first slot of its segment, or kNoSeg
   uint32_t* seg_cnt;  // per slot: records of the segment starting there
   uint64_t* seg_off;  // exclusive prefix of seg_cnt (cap + 1)
+  int64_t* seg_mark;  // per slot: i + 1 when empty, else 0 (cap + 1: the max at [cap])
+  int64_t* seg_start; // per slot: exclusive max-scan of seg_mark (first slot of its run, 0 = wraps)
+  uint32_t* seg_cls_cnt;  // segment lists: per-workgroup counts [3][blocks], and their scan
+  uint64_t* seg_cls_off;
 };
 
 // Per-stage HIP events on the build stream (only when profiling is enabled).
@@ -224,8 +231,18 @@ void launch_carry(const BuildParams& P, hipStream_t s);
 void launch_place_global(const BuildParams& P, hipStream_t s, int sort_only, int only_big);
 void launch_verify(const BuildParams& P, hipStream_t s, StageTimer* tm);
 void launch_stats(const BuildParams& P, hipStream_t s, int sequential, StageTimer* tm);
+// exact replay (exact_kernels.hip)
 void launch_sequential(const BuildParams& P, hipStream_t s, int sorted_order);
-void launch_segments(const BuildParams& P, hipStream_t s, int sorted_order, StageTimer* tm);
+// Streams the exact path forks its independent segment classes onto (owned by the plan).
+struct SideStreams {
+  hipStream_t s[3];
+  hipEvent_t fork;
+  hipEvent_t join[3];
+};
+void launch_segments(const BuildParams& P, hipStream_t s, int sorted_order, StageTimer* tm, bool check_each,
+                     const SideStreams* side);
+constexpr unsigned kSegDebugWaves[3] = {4096, 2048, 512};   // k_seg_replay_wave grids (mid, large, huge)
+constexpr unsigned kSegDebugWords = (4096 + 2048 + 512) * 8;  // SPARKEY_EXACT_DEBUG: per-wave phase cycles
 void launch_partition_quiet(const BuildParams& P, hipStream_t s);
 // sharded builds (shard_kernels.hip)
 void launch_dest_counts(const BuildParams& P, hipStream_t s, int world, uint32_t nd, uint64_t* d_out);

@@ -934,6 +934,10 @@ __global__ __launch_bounds__(kPart2Block) void k_part2(BuildParams P) {
 // k_place_lds: one bucket per workgroup, entries staged in LDS (buckets above kPlaceLdsMax
 // entries are left to the global-memory k_place, flagged in P.st->big_buckets).
 // ================================================================================================
+__device__ __forceinline__ bool is_put_pair(const Entry& x, const Entry& y) {  // a duplicate-key candidate
+  return x.hash == y.hash && !(x.addr & kDelBit) && !(y.addr & kDelBit);
+}
+
 __global__ __launch_bounds__(kPlaceLdsBlock) void k_place_lds(BuildParams P) {
   __shared__ uint32_t cnt[kBucket];
   __shared__ uint32_t base[kBucket];
@@ -968,7 +972,11 @@ __global__ __launch_bounds__(kPlaceLdsBlock) void k_place_lds(BuildParams P) {
     order[base[w] + atomicAdd((uint32_t*)&aux[w], 1u)] = (uint16_t)i;
   }
   __syncthreads();
-  // equal wanted slots: address order; equal hashes -> duplicate-key candidates
+  // equal wanted slots: address order; equal hashes -> duplicate-key candidates, appended to the
+  // pair list with one atomic per workgroup (not needed once the exact path is certain: the log
+  // holds DELETEs, or the list overflowed)
+  const bool want_pairs = P.st->n_deletes == 0 && P.st->n_pairs <= P.pair_cap;
+  uint32_t npair = 0;
   for (int q = 0; q < kLdsBins; q++) {
     const int s = tid * kLdsBins + q;
     const uint32_t g = cnt[s];
@@ -985,17 +993,33 @@ __global__ __launch_bounds__(kPlaceLdsBlock) void k_place_lds(BuildParams P) {
       while (y > 0 && va < (raw[grp[y - 1]].addr & ~kDelBit)) { grp[y] = grp[y - 1]; y--; }
       grp[y] = vi;
     }
-    for (uint32_t x = 0; x < g; x++)
-      for (uint32_t y = x + 1; y < g; y++) {
-        const Entry ex = raw[grp[x]], ey = raw[grp[y]];
-        if (ex.hash == ey.hash && !(ex.addr & kDelBit) && !(ey.addr & kDelBit)) {
-          const unsigned long long slotn = atomicAdd(&P.st->n_pairs, 1ull);
+    if (want_pairs)
+      for (uint32_t x = 0; x < g; x++)
+        for (uint32_t y = x + 1; y < g; y++) npair += is_put_pair(raw[grp[x]], raw[grp[y]]);
+  }
+  uint64_t pair_total = 0;
+  const uint64_t pair_off = block_excl_sum<kPlaceLdsBlock>(npair, sh64, &pair_total);
+  if (pair_total) {
+    __shared__ unsigned long long pair_base;
+    if (tid == 0) pair_base = atomicAdd(&P.st->n_pairs, (unsigned long long)pair_total);
+    __syncthreads();
+    unsigned long long slotn = pair_base + pair_off;
+    for (int q = 0; q < kLdsBins && npair; q++) {
+      const int s = tid * kLdsBins + q;
+      const uint32_t g = cnt[s];
+      if (g < 2 || g > kGroupMax) continue;
+      const uint16_t* grp = order + base[s];
+      for (uint32_t x = 0; x < g; x++)
+        for (uint32_t y = x + 1; y < g; y++) {
+          const Entry ex = raw[grp[x]], ey = raw[grp[y]];
+          if (!is_put_pair(ex, ey)) continue;
           if (slotn < P.pair_cap) {
             P.pairs[2 * slotn] = ex.addr;
             P.pairs[2 * slotn + 1] = ey.addr;
           }
+          slotn++;
         }
-      }
+    }
   }
   __syncthreads();
   if (P.st->full) return;

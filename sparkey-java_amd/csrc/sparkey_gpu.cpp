@@ -243,7 +243,12 @@ struct sparkey_plan {
   uint64_t c_bcount = 0, c_bcursor = 0, c_boff = 0, c_bfun = 0, c_bpre = 0, c_carry = 0;
   uint64_t c_pairs = 0, c_parts = 0, c_su = 0, c_smp = 0, c_bft = 0;
   uint64_t c_desc = 0, c_p1h = 0, c_p1o = 0, c_dbg = 0, c_wcount = 0, c_woff = 0;
-  uint64_t c_eseg = 0, c_seg_cnt = 0, c_seg_off = 0;
+  uint64_t c_eseg = 0, c_seg_cnt = 0, c_seg_off = 0, c_seg_mark = 0, c_seg_start = 0;
+  uint64_t c_seg_cls_cnt = 0, c_seg_cls_off = 0;
+  uint32_t* seg_cls_cnt = nullptr;
+  uint64_t* seg_cls_off = nullptr;
+  int64_t* seg_mark = nullptr;
+  int64_t* seg_start = nullptr;
   uint64_t* eseg = nullptr;     // exact path: per slab entry, the first slot of its segment
   uint32_t* seg_cnt = nullptr;  // exact path: per slot, records of the segment starting there
   uint64_t* seg_off = nullptr;
@@ -277,6 +282,8 @@ struct sparkey_plan {
   Status* h_status = nullptr;
   unsigned long long* dbg = nullptr;  // SPARKEY_FRAME_DEBUG=1: k_frame phase counters
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  SideStreams side{};  // exact path: concurrent segment classes (created on first use)
+  bool side_ok = false;
   StageTimer timer;
   std::vector<std::string> stage_names;
   std::vector<double> stage_ms;
@@ -598,6 +605,10 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
       HIP_TRY(grow(&pl->eseg, pl->c_eseg, P.nslabs * (uint64_t)P.slab_cap));
       HIP_TRY(grow(&pl->seg_cnt, pl->c_seg_cnt, P.cap));
       HIP_TRY(grow(&pl->seg_off, pl->c_seg_off, P.cap + 1));
+      HIP_TRY(grow(&pl->seg_mark, pl->c_seg_mark, P.cap + 1));
+      HIP_TRY(grow(&pl->seg_start, pl->c_seg_start, P.cap));
+      HIP_TRY(grow(&pl->seg_cls_cnt, pl->c_seg_cls_cnt, 4 * (P.cap / 1024 + 1)));
+      HIP_TRY(grow(&pl->seg_cls_off, pl->c_seg_cls_off, 4 * (P.cap / 1024 + 1) + 1));
       const uint64_t scratch = P.cap / kScanTile + 64;
       if (pl->c_su < scratch + 16) {
         HIP_TRY(grow(&pl->scan_u64, pl->c_su, scratch + 16));
@@ -606,9 +617,51 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
       P.eseg = pl->eseg;
       P.seg_cnt = pl->seg_cnt;
       P.seg_off = pl->seg_off;
+      P.seg_mark = pl->seg_mark;
+      P.seg_start = pl->seg_start;
+      P.seg_cls_cnt = pl->seg_cls_cnt;
+      P.seg_cls_off = pl->seg_cls_off;
       HIP_TRY(hipMemsetAsync(P.seg_cnt, 0, P.cap * sizeof(uint32_t), s));
       HIP_TRY(hipMemsetAsync((uint8_t*)pl->d_status + offsetof(Status, num_entries), 0, 2 * sizeof(long long), s));
-      launch_segments(P, s, ip.in_memory ? 0 : 1, &pl->timer);
+      HIP_TRY(hipMemsetAsync((uint8_t*)pl->d_status + offsetof(Status, n_segs), 0, sizeof(((Status*)0)->n_segs), s));
+      const bool seg_dbg = getenv("SPARKEY_EXACT_DEBUG") != nullptr;
+      if (seg_dbg) {
+        HIP_TRY(grow(&pl->dbg, pl->c_dbg, kSegDebugWords));
+        HIP_TRY(hipMemsetAsync(pl->dbg, 0, kSegDebugWords * sizeof(unsigned long long), s));
+        P.dbg = pl->dbg;
+      } else {
+        P.dbg = nullptr;
+      }
+      const char* dbg_env = getenv("SPARKEY_EXACT_DEBUG");
+      if (!pl->side_ok) {
+        for (int i = 0; i < 3; i++) {
+          HIP_TRY(hipStreamCreateWithFlags(&pl->side.s[i], hipStreamNonBlocking));
+          HIP_TRY(hipEventCreateWithFlags(&pl->side.join[i], hipEventDisableTiming));
+        }
+        HIP_TRY(hipEventCreateWithFlags(&pl->side.fork, hipEventDisableTiming));
+        pl->side_ok = true;
+      }
+      launch_segments(P, s, ip.in_memory ? 0 : 1, &pl->timer, dbg_env && atoi(dbg_env) >= 2, &pl->side);
+      if (seg_dbg) {
+        std::vector<unsigned long long> h(kSegDebugWords);
+        HIP_TRY(hipMemcpyAsync(h.data(), pl->dbg, h.size() * 8, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        static const char* cname[3] = {"mid", "large", "huge"};
+        for (int c = 0, b0 = 0; c < 3; b0 += kSegDebugWaves[c], c++) {
+          const unsigned b1 = b0 + kSegDebugWaves[c];
+          double sum[8] = {0};
+          unsigned long long mx[8] = {0};
+          for (unsigned b = b0; b < b1; b++)
+            for (int i = 0; i < 8; i++) {
+              sum[i] += (double)h[b * 8 + i];
+              mx[i] = std::max(mx[i], h[b * 8 + i]);
+            }
+          fprintf(stderr, "[exact %s] segs %.0f recs %.0f | cycles/seg stage %.0f sort %.0f replay %.0f write %.0f | "
+                          "max wave: segs %llu stage %llu sort %llu replay %llu write %llu\n",
+                  cname[c], sum[4], sum[5], sum[0] / std::max(1.0, sum[4]), sum[1] / std::max(1.0, sum[4]),
+                  sum[2] / std::max(1.0, sum[4]), sum[3] / std::max(1.0, sum[4]), mx[4], mx[0], mx[1], mx[2], mx[3]);
+        }
+      }
     }
     launch_stats(P, s, 1, &pl->timer);
     HIP_TRY(hipGetLastError());
@@ -619,6 +672,10 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
     ms += ms2;
     rc = status_error(st, err, err_len);
     if (rc) return rc;
+    if (st.guard) {
+      set_err(err, err_len, "internal error: exact-path bounds check tripped (bits " + std::to_string(st.guard) + ")");
+      return SPARKEY_E_GPU;
+    }
   }
   if (pl->timer.enabled) {
     pl->stage_names.clear();
@@ -710,13 +767,21 @@ void sparkey_plan_destroy(sparkey_plan* pl) {
   void* bufs[] = {pl->conv, pl->exitp, pl->qpos, pl->tail, pl->G, pl->cnt, pl->off, pl->ent, pl->ent2, pl->ent3,
                   pl->bcount, pl->bcursor, pl->boff, pl->bfun, pl->bpre, pl->bfun_total, pl->carry, pl->pairs,
                   pl->parts, pl->scan_u64, pl->scan_mp, pl->desc, pl->p1_hist, pl->p1_off, pl->d_status, pl->dbg, pl->wcount, pl->woff, pl->small,
-                  pl->eseg, pl->seg_cnt, pl->seg_off};
+                  pl->eseg, pl->seg_cnt, pl->seg_off, pl->seg_mark, pl->seg_start,
+                  pl->seg_cls_cnt, pl->seg_cls_off};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (pl->h_status) (void)hipHostFree(pl->h_status);
   if (pl->ev0) (void)hipEventDestroy(pl->ev0);
   if (pl->ev1) (void)hipEventDestroy(pl->ev1);
   if (pl->own_stream) (void)hipStreamDestroy(pl->own_stream);
+  if (pl->side_ok) {
+    for (int i = 0; i < 3; i++) {
+      (void)hipStreamDestroy(pl->side.s[i]);
+      (void)hipEventDestroy(pl->side.join[i]);
+    }
+    (void)hipEventDestroy(pl->side.fork);
+  }
   delete pl;
 }
 

@@ -4,6 +4,7 @@ LogWriter produces (UncompressedBlockOutput.java:67-72, LogHeader.java:90-115).
   fixed_log(n, 16, 100)      C2: key = LE64(i) || LE64(splitmix64(i ^ seed)) (unique), value = 100 random bytes
   mixed_log(n, 8, 64, 100)   C3: key length uniform in [8, 64], LE64(i) prefix keeps keys unique
   key_value_log(n)           C1: put("key_" + i, "value_" + i) as WriteHashBenchmark.java:52-54
+  churn_log(n, pool, p_del)  C2 shape with overwrites and DELETEs: keys drawn from a pool of `pool`
 """
 from __future__ import annotations
 
@@ -23,9 +24,11 @@ def splitmix64(x: np.ndarray) -> np.ndarray:
 
 
 def _header(n_puts: int, max_key: int, max_val: int, put_size: int, data_end: int, file_id: int,
-            block_size: int) -> bytes:
+            block_size: int, n_deletes: int = 0, delete_size: int = 0) -> bytes:
     h = LogHeader(0, block_size, file_id)
     h.num_puts = n_puts
+    h.num_deletes = n_deletes
+    h.delete_size = delete_size
     h.max_key_len = max_key
     h.max_value_len = max_val
     h.put_size = put_size
@@ -119,3 +122,34 @@ def key_value_log(n: int, file_id: int = 0x0C1C1C1C, block_size: int = 1024) -> 
         put_size += len(rec)
     body = b"".join(parts)
     return _header(n, max_k, max_v, put_size, LOG_HEADER_SIZE + len(body), file_id, block_size) + body
+
+
+def churn_log(n: int, pool: int, p_del: float, key_len: int = 16, value_len: int = 100, seed: int = 5,
+              file_id: int = 0x5EED0005, block_size: int = 0) -> np.ndarray:
+    """n records of C2 shape whose keys are drawn uniformly from `pool` keys (so later PUTs overwrite
+    earlier ones); each record is a DELETE (0x00 VLQ(keyLen) key, UncompressedBlockOutput.java:80-87)
+    with probability p_del.  Key j = LE64(j) || LE64(splitmix64(j ^ seed))."""
+    assert key_len == 16 and value_len < 128
+    rng = np.random.default_rng(seed)
+    kidx = rng.integers(0, pool, size=n).astype(np.uint64)
+    is_del = rng.random(n) < p_del
+    rec = np.where(is_del, 2 + key_len, 2 + key_len + value_len).astype(np.int64)
+    starts = np.zeros(n, dtype=np.int64)
+    if n:
+        np.cumsum(rec[:-1], out=starts[1:])
+    total = int(rec.sum())
+    buf = np.empty(LOG_HEADER_SIZE + total, dtype=np.uint8)
+    body = buf[LOG_HEADER_SIZE:]
+    body[:] = np.frombuffer(rng.bytes(total), dtype=np.uint8)
+    body[starts] = np.where(is_del, 0, key_len + 1).astype(np.uint8)
+    body[starts + 1] = np.where(is_del, key_len, value_len).astype(np.uint8)
+    key = np.concatenate([kidx.view(np.uint8).reshape(n, 8),
+                          splitmix64(kidx ^ np.uint64(seed)).view(np.uint8).reshape(n, 8)], axis=1)
+    for b in range(key_len):
+        body[starts + 2 + b] = key[:, b]
+    n_del = int(is_del.sum())
+    put_size = int(rec[~is_del].sum())
+    buf[:LOG_HEADER_SIZE] = np.frombuffer(
+        _header(n - n_del, key_len, value_len if n > n_del else 0, put_size, LOG_HEADER_SIZE + total, file_id,
+                block_size, n_del, total - put_size), dtype=np.uint8)
+    return buf

@@ -279,3 +279,25 @@ def test_exact_segments_small_tables(native, n, seed, method):
     log = make_log(ops=ops)
     for hs in (4, 8):
         check(native, log, seed, hash_size=hs, method=method)
+
+
+# one hot key written thousands of times: all its records share a wanted slot, so its segment holds
+# more records than a workgroup stages in LDS (the lane-0 HBM replay); warm keys give mid-size ones
+@pytest.mark.parametrize("method", [IN_MEMORY, SORTING])
+def test_exact_segments_hot_keys(native, method):
+    rng = np.random.default_rng(8)
+    ops = []
+    for i in range(20000):
+        r = rng.random()
+        if r < 0.12:
+            ops.append(("put", b"hot", b"v%d" % i))
+        elif r < 0.14:
+            ops.append(("del", b"hot", None))
+        elif r < 0.30:
+            ops.append(("put", b"warm%d" % int(rng.integers(0, 8)), b"w%d" % i))
+        else:
+            ops.append(("put", b"cold%d" % int(rng.integers(0, 12000)), b"c"))
+    log = make_log(ops=ops)
+    for hs in (4, 8):
+        got, stats = check(native, log, 1 + hs, hash_size=hs, method=method)
+        assert stats.placement_path == 2
