@@ -72,3 +72,18 @@ def test_sharded_c2_4_ranks_matches_single(native):
     got, metas = run_threads(log.tobytes(), 4, dict(hash_seed=4242))
     assert all(m["path"] == "sharded" for m in metas)
     assert got == single, diff_report(got, single)
+
+
+@pytest.mark.parametrize("method,n", [(IN_MEMORY, 10_000_000), (SORTING, 4_000_000)])
+def test_churn_full_size(native, method, n):
+    """C2-shaped log with overwrites and DELETEs (keys from a pool of 0.8 n, 10% DELETE records): the
+    exact replay over independent slot segments (placement_path 2), bit-exact against the oracle's
+    sequential IndexHash.put / delete."""
+    from sparkey import synth
+    log = synth.churn_log(n, int(n * 0.8), 0.1, seed=5)
+    got, stats = device_build(native, log, 0x5EED, method=method)
+    want = oracle.build_index(log, 0x5EED, method=method)
+    assert got == want, diff_report(got, want)
+    assert stats.placement_path == 2 and stats.framing_path == 0
+    h = index_header(got)
+    assert h["garbageSize"] > 0 and 0 < h["numEntries"] < n
