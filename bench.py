@@ -117,7 +117,7 @@ def single_gpu(args, dev):
     dom_bytes = stage_bytes(dom, n, log_len, slot, cap) if dom else 0
     achieved = dom_bytes / (stage_ms[dom] * 1e-3) / 1e9 if dom and stage_ms[dom] > 0 else 0.0
     b_alg = (log_len - 84) + 112 + slot * cap
-    assert stats.placement_path == wl["path"] and stats.framing_path == 0, stats.as_dict()
+    assert stats.placement_path == wl["path"] and stats.framing_path in (0, 2), stats.as_dict()
     assert wl["path"] != 0 or stats.num_entries == n, stats.as_dict()
 
     # host-to-host rate (north_star): H2D of the log from pinned memory, the build, D2H of the .spi
@@ -133,6 +133,32 @@ def single_gpu(args, dev):
             host_out.copy_(d_out, non_blocking=True)
             stream.synchronize()
     h2h = n * reps / (time.perf_counter() - t1)
+
+    # the same workload through the general speculative framing (k_frame), when the log's records are
+    # uniform and the default build took k_frame_uniform
+    general = None
+    if stats.framing_path == 2:
+        os.environ["SPARKEY_NO_UNIFORM"] = "1"
+        try:
+            one_build()
+            torch.cuda.synchronize(dev)
+            plan.set_profiling(True)
+            g_acc, g_steps = {}, max(3, args.steps // 2)
+            t_g = time.perf_counter()
+            for _ in range(g_steps):
+                g_stats = one_build()
+                for name, ms in plan.stage_times():
+                    g_acc[name] = g_acc.get(name, 0.0) + ms
+            torch.cuda.synchronize(dev)
+            g_el = time.perf_counter() - t_g
+            plan.set_profiling(False)
+            assert g_stats.framing_path == 0, g_stats.as_dict()
+            g_stage = {k: v / g_steps for k, v in g_acc.items()}
+            general = {"ms_per_step": g_el * 1000.0 / g_steps, "keys_per_s": n * g_steps / g_el,
+                       "stage_ms": g_stage,
+                       "frame_achieved_gbs": stage_bytes("frame", n, log_len, slot, cap) / (g_stage["frame"] * 1e-3) / 1e9}
+        finally:
+            del os.environ["SPARKEY_NO_UNIFORM"]
 
     cpu = None
     if not args.no_cpu_baseline:
@@ -160,6 +186,8 @@ def single_gpu(args, dev):
         "build_hbm_gbs": b_alg / (ms_per_step * 1e-3) / 1e9,
         "build_algorithmic_bytes": b_alg,
         "stage_ms": stage_ms,
+        "framing": {0: "k_frame (speculative)", 1: "serial walk", 2: "k_frame_uniform (uniform records)"}[stats.framing_path],
+        "general_framing": general,
         "host_to_host_keys_per_s": h2h,
         "cpu_baseline": cpu,
         "gen_s": gen_s,

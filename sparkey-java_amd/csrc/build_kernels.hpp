@@ -160,6 +160,9 @@ struct BuildParams {
   int32_t fr_fast;  // maxKeyLen + 1 < 128 and maxValueLen < 128: canonical headers are 2 bytes
   int32_t no_deletes;  // the log header counts no DELETE: speculation treats 0x00 as no record start
   uint64_t fr_nchunks;
+  // uniform-stride framing (k_frame_uniform): uni_n records of uni_rec bytes from fr_entry
+  uint64_t uni_n;
+  int64_t uni_rec;
   // framing window: records start at fr_entry (84 for a whole log) and are framed while they start
   // below data_end (the frame end); k_frame chunks are numbered from fr_k0 = fr_entry >> fr_cshift,
   // serial-path chunks (kChunk) from ch_k0 = fr_entry >> kChunkShift
@@ -221,6 +224,7 @@ void launch_frame_fused(const BuildParams& P, hipStream_t s, StageTimer* tm);
 void launch_partition(const BuildParams& P, hipStream_t s, StageTimer* tm);
 void launch_partition1(const BuildParams& P, hipStream_t s);
 void launch_dense_slabs(const BuildParams& P, hipStream_t s);
+void launch_frame_uniform(const BuildParams& P, hipStream_t s, StageTimer* tm);
 void launch_place_fast(const BuildParams& P, hipStream_t s, StageTimer* tm);
 void launch_place_buckets(const BuildParams& P, hipStream_t s);
 // fallbacks and shared stages (build_kernels.hip)

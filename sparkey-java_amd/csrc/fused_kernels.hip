@@ -772,6 +772,55 @@ __global__ __launch_bounds__(64) void k_frame(BuildParams P) {
 }
 
 // ================================================================================================
+// k_frame_uniform: logs whose header proves that every record has the same size R.  With no DELETE,
+// putSize == numPuts * R (R = the largest PUT record the header allows) and dataEnd - 84 == putSize,
+// every record is at most R bytes and together they fill putSize, so each is exactly R and record i
+// starts at 84 + i * R.  One wave per 64 records stages their bytes into LDS with coalesced
+// global_load_lds, and every lane checks its record's header against (maxKeyLen, maxValueLen) --
+// anything else flags spec_fail and the build reruns the general framing -- then hashes its key.
+// The entries are dense, in log order (the slab layout of the serial path).
+// ================================================================================================
+__global__ __launch_bounds__(64) void k_frame_uniform(BuildParams P) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int lane = threadIdx.x;
+  const uint64_t i0 = (uint64_t)blockIdx.x * 64;
+  const int64_t R = P.uni_rec;
+  const int64_t log_len = (int64_t)P.log_len;
+  const int64_t base = P.fr_entry + (int64_t)i0 * R;
+  const int64_t a0 = base & ~15ll;
+  const int nrec = (int)min((uint64_t)64, P.uni_n - i0);
+  const int64_t want = base + (int64_t)nrec * R + 16 - a0;  // + 16: the 8-byte window reads past a key
+  const int nvec = (int)((want + 15) >> 4);
+  if (a0 + 16ll * nvec <= log_len) {
+    const uint4* src = reinterpret_cast<const uint4*>(P.log + a0);
+    for (int v0 = 0; v0 < nvec; v0 += 64)
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)(src + min(v0 + lane, nvec - 1)),
+          (__attribute__((address_space(3))) void*)(lds + 16u * (uint32_t)v0), 16, 0, 0);
+  } else {
+    for (int v = lane; v < nvec; v += 64) *reinterpret_cast<uint4*>(lds + 16u * v) = load16_guarded(P.log, a0 + 16ll * v, log_len);
+  }
+  __syncthreads();
+  if (blockIdx.x == 0 && lane == 0) P.st->n_records = P.uni_n;
+  if (lane >= nrec) return;
+  const int64_t p = base + (int64_t)lane * R;
+  const uint32_t off = (uint32_t)(p - a0);
+  const uint64_t x = rgn_u64(lds, off);
+  const int32_t klen = (int32_t)(x & 0xff) - 1, vlen = (int32_t)((x >> 8) & 0xff);
+  if ((x & 0x8080ull) != 0 || klen != (int32_t)P.max_key_len || vlen != (int32_t)P.max_value_len) {
+    atomicOr(&P.st->spec_fail, 4u);  // not the uniform log the header describes
+    return;
+  }
+  const RgnKey ld{lds, off + 2u};
+  const uint64_t hash = P.hash_size == 8 ? murmur64_ld(ld, klen, (uint32_t)P.seed)
+                                         : (uint64_t)murmur32_ld(ld, klen, (uint32_t)P.seed);
+  Entry en;
+  en.hash = hash;
+  en.addr = (uint64_t)p << P.ebb;
+  P.ent[i0 + lane] = en;
+}
+
+// ================================================================================================
 // Radix partition of the entries by bucket (bucket = wantedSlot >> kBucketShift).
 // Pass 1: coarse digit = bucket / bpp (< 256; every digit holds bpp buckets, so the digits
 // split the table evenly -- a sharded build gives each rank a run of digits) over tiles of slabs.
@@ -1067,6 +1116,14 @@ void launch_frame_fused(const BuildParams& P, hipStream_t s, StageTimer* tm) {
   tm->mark("frame", s);  // the stage is k_frame alone (its rocprof row); the slab scan counts as partition
   scan_exclusive<uint32_t, uint64_t, OpAdd>(P.wcount, P.woff, P.nslabs, (uint64_t*)&P.st->n_records, OpAdd(),
                                             P.scan_scratch_u64, s);
+}
+
+void launch_frame_uniform(const BuildParams& P, hipStream_t s, StageTimer* tm) {
+  if (P.uni_n == 0) return;
+  const uint64_t nblk = (P.uni_n + 63) / 64;
+  const size_t lds = (size_t)((64 * P.uni_rec + 32 + 1023) & ~1023ll);
+  hipLaunchKernelGGL(k_frame_uniform, dim3((unsigned)nblk), dim3(64), lds, s, P);
+  tm->mark("frame", s);
 }
 
 void launch_dense_slabs(const BuildParams& P, hipStream_t s) {

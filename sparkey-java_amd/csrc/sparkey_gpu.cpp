@@ -16,6 +16,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <cmath>
 #include <string>
 #include <vector>
 
@@ -387,6 +388,24 @@ static int setup_params(const LogHdr& lh, const IndexParams& ip, const sparkey_b
     const int64_t C = 1ll << cs;
     P.fr_cshift = cs;
     P.fr_w = (int32_t)std::max<int64_t>(1, std::min<int64_t>(64, region / C));
+    // Hashing runs one record per lane per round, so a wave holding 69 records pays for 128.  The
+    // header's mean record size (putSize + deleteSize over the record count) picks, among regions of
+    // half to all of kFrameRegion, the W whose expected records per wave (plus a small margin) fill
+    // their rounds best.
+    const int64_t nrec_hdr = std::max<int64_t>(0, lh.num_puts) + std::max<int64_t>(0, lh.num_deletes);
+    const int64_t bytes_hdr = std::max<int64_t>(0, lh.put_size) + std::max<int64_t>(0, lh.delete_size);
+    if (!getenv("SPARKEY_FRAME_REGION") && nrec_hdr > 0 && bytes_hdr > 0 && region / C >= 2) {
+      const double mean = (double)bytes_hdr / (double)nrec_hdr;
+      double best = -1.0;
+      for (int64_t w = std::max<int64_t>(1, region / C / 2); w <= std::min<int64_t>(64, region / C); w++) {
+        const double recs = (double)(w * C) / mean;
+        const double eff = recs / (64.0 * std::ceil((recs + 3.0) / 64.0));
+        if (eff >= best) {
+          best = eff;
+          P.fr_w = (int32_t)w;
+        }
+      }
+    }
     P.fr_look = (int32_t)((look + 15) & ~15LL);
     P.fr_rgn_bytes = (int32_t)(((int64_t)P.fr_w * C + P.fr_look + 16 + 1023) & ~1023LL);  // whole glds rows
     P.fr_mask_words = (int32_t)((std::min<int64_t>(C, P.max_rec_len) + 63) / 64);
@@ -464,6 +483,9 @@ static int launch_framing(sparkey_plan* pl, const BuildParams& P, int framing_pa
     HIP_TRY(hipMemsetAsync(pl->desc, 0, (2 * nwaves + 2) * sizeof(unsigned long long), s));
     HIP_TRY(hipMemsetAsync(pl->wcount, 0, (P.nslabs + 1) * sizeof(uint32_t), s));
     launch_frame_fused(P, s, &pl->timer);
+  } else if (framing_path == 2) {
+    launch_frame_uniform(P, s, &pl->timer);
+    launch_dense_slabs(P, s);
   } else {
     launch_framing_serial(P, s);
     launch_emit(P, s, &pl->timer);
@@ -530,6 +552,17 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
   index_header_template(lh, ip, opts->hash_seed, hdr);
 
   int framing_path = fused_framing ? 0 : 1, placement_path = 0;
+  {  // uniform records (k_frame_uniform): the header proves every record is exactly R bytes
+    const int64_t R = vlq_size_long(lh.max_key_len + 1) + vlq_size_long(lh.max_value_len) + lh.max_key_len +
+                      lh.max_value_len;
+    if (lh.num_deletes == 0 && lh.num_puts > 0 && lh.max_key_len + 1 < 128 && lh.max_value_len < 128 && R <= 256 &&
+        lh.put_size == lh.num_puts * R && lh.data_end - kLogHeaderSize == lh.put_size &&
+        !getenv("SPARKEY_NO_UNIFORM")) {
+      framing_path = 2;
+      P.uni_n = (uint64_t)lh.num_puts;
+      P.uni_rec = R;
+    }
+  }
   float ms = 0.f;
   Status& st = *pl->h_status;
   const uint64_t nwaves = P.fr_nchunks ? (P.fr_nchunks + P.fr_w - 1) / P.fr_w : 0;
@@ -574,6 +607,10 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
     }
     if (framing_path == 0 && (st.spec_fail || st.err != ~0ull)) {  // only the verified serial walk may report
       framing_path = 1;
+      continue;
+    }
+    if (framing_path == 2 && st.spec_fail) {  // a record differs from the header's uniform shape
+      framing_path = fused_framing ? 0 : 1;
       continue;
     }
     break;

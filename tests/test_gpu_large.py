@@ -36,6 +36,17 @@ def test_c2_full_size(native):
     got, stats = device_build(native, log, 0x2545F491)
     want = oracle.build_index(log, 0x2545F491)
     assert got == want, diff_report(got, want)
+    assert stats.placement_path == 0 and stats.framing_path == 2  # uniform records (k_frame_uniform)
+
+
+def test_c2_full_size_general_framing(native, monkeypatch):
+    """The same C2 log through the general speculative framing (k_frame)."""
+    from sparkey import synth
+    monkeypatch.setenv("SPARKEY_NO_UNIFORM", "1")
+    log = synth.fixed_log(10_000_000, 16, 100, seed=1)
+    got, stats = device_build(native, log, 0x2545F491)
+    want = oracle.build_index(log, 0x2545F491)
+    assert got == want, diff_report(got, want)
     assert stats.placement_path == 0 and stats.framing_path == 0
 
 

@@ -224,6 +224,7 @@ def test_tiny_records_stay_on_fast_framing(native):
                                  {"SPARKEY_FRAME_CMIN": "2048"}, {"SPARKEY_FRAME_REGION": "16384"},
                                  {"SPARKEY_FRAME_LOOK": "16"}, {"SPARKEY_FRAME_LOOK": "1024"}])
 def test_frame_geometry_overrides(native, monkeypatch, env):
+    monkeypatch.setenv("SPARKEY_NO_UNIFORM", "1")  # the fixed-size log would take k_frame_uniform
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     rng = np.random.default_rng(3)
@@ -301,3 +302,49 @@ def test_exact_segments_hot_keys(native, method):
     for hs in (4, 8):
         got, stats = check(native, log, 1 + hs, hash_size=hs, method=method)
         assert stats.placement_path == 2
+
+
+# --- uniform records: the header proves every record has the same size (k_frame_uniform) ---
+def _uniform_puts(n, klen, vlen, seed=0, dup_every=0):
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(n):
+        j = i // 2 if dup_every and i % dup_every == 0 else i
+        out.append((j.to_bytes(8, "little")[:klen].ljust(klen, b"k"), rng.integers(0, 256, vlen, dtype=np.uint8).tobytes()))
+    return out
+
+
+@pytest.mark.parametrize("klen,vlen", [(16, 100), (8, 0), (4, 1), (64, 63), (126, 127)])
+@pytest.mark.parametrize("hash_size", [4, 8])
+def test_uniform_records(native, klen, vlen, hash_size):
+    log = make_log(_uniform_puts(30000 if klen >= 4 else 250, klen, vlen, seed=klen))
+    got, stats = check(native, log, 99 + klen, hash_size=hash_size)
+    assert stats.framing_path == 2, stats.as_dict()
+
+
+@pytest.mark.parametrize("method", [IN_MEMORY, SORTING])
+def test_uniform_records_with_overwrites(native, method):
+    log = make_log(_uniform_puts(20000, 16, 20, dup_every=5))
+    got, stats = check(native, log, 5, hash_size=8, method=method)
+    assert stats.framing_path == 2 and stats.placement_path == 2, stats.as_dict()
+
+
+def test_uniform_header_but_record_split_differs(native):
+    """putSize == numPuts * R, yet one record trades a key byte for a value byte (same size): the
+    uniform framing must notice the header mismatch and rerun the general framing."""
+    puts = _uniform_puts(5000, 16, 30)
+    puts[2500] = (puts[2500][0][:15], puts[2500][1] + b"x")
+    import struct
+    log = bytearray(make_log(puts))
+    struct.pack_into("<q", log, 40, 16)  # maxKeyLen stays 16, maxValueLen stays 31 ...
+    struct.pack_into("<q", log, 48, 30)  # ... declare maxValueLen 30 so putSize == n * (2 + 16 + 30)
+    got, stats = check(native, bytes(log), 7, hash_size=8)
+    assert stats.framing_path == 0, stats.as_dict()
+
+
+def test_uniform_disabled_gives_same_bytes(native, monkeypatch):
+    log = make_log(_uniform_puts(40000, 16, 100))
+    a, sa = gpu_build(native, log, 11, 8)
+    monkeypatch.setenv("SPARKEY_NO_UNIFORM", "1")
+    b, sb = gpu_build(native, log, 11, 8)
+    assert sa.framing_path == 2 and sb.framing_path == 0 and a == b
