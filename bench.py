@@ -181,7 +181,8 @@ def single_gpu(args, dev):
                    "address_bytes": stats.address_size, "capacity": int(cap), "spi_bytes": int(out_len),
                    "parallelism": "single"},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(dom),
+                     "frac": achieved / HBM_PEAK_GBS,
+                     "traffic": pmc_traffic("frame_uniform" if dom == "frame" and stats.framing_path == 2 else dom),
                      "algorithmic_bytes_per_launch": dom_bytes, "avg_launch_ms": stage_ms.get(dom) if dom else None},
         "build_hbm_gbs": b_alg / (ms_per_step * 1e-3) / 1e9,
         "build_algorithmic_bytes": b_alg,
