@@ -150,6 +150,15 @@ int sparkey_shard_bin(sparkey_plan* plan, uint8_t* d_send, uint64_t send_cap, vo
  * function f(x) = max(c, x + a). */
 int sparkey_shard_summarize(sparkey_plan* plan, const uint8_t* d_recv, uint64_t n_recv, void* stream,
                             int64_t* fun_out, char* err, size_t err_len);
+/* Entries per coarse digit of this rank's last sparkey_shard_bin (256 values, host side). */
+int sparkey_shard_digit_counts(const sparkey_plan* plan, uint64_t* out256);
+/* sparkey_shard_summarize for an exchange buffer that holds, per source rank in rank order, that
+ * rank's bin output for this rank's digits: digit_counts = the world x 256 matrix of every rank's
+ * sparkey_shard_digit_counts (row = source rank).  The runs are partitioned in place (no first
+ * radix pass over the received entries). */
+int sparkey_shard_summarize_grouped(sparkey_plan* plan, const uint8_t* d_recv, uint64_t n_recv,
+                                    const uint64_t* digit_counts, void* stream, int64_t* fun_out, char* err,
+                                    size_t err_len);
 /* Places the rank's entries given its carry-in into d_slots (the bytes of slot slot_lo onwards);
  * slots past the range go to d_spill as {slot, hash, address, 0} u64 quadruples. */
 int sparkey_shard_place(sparkey_plan* plan, int64_t carry_in, uint8_t* d_slots, uint8_t* d_spill, uint64_t spill_cap,

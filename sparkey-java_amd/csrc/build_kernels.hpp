@@ -147,6 +147,12 @@ struct BuildParams {
   uint64_t* p1_off;
   uint64_t* p1_off_total;
   uint32_t p1_tiles;
+  int32_t p1_hist_ready;  // the framing kernel filled p1_hist (zeroed before it): no k_part1_hist
+  // k_part2 over a sharded build's exchange buffer (null: the pass-1 runs): for each of the rank's
+  // p2_nd coarse digits from p2_d0, p2_nsrc (begin, end) runs of ent3, and the digit's ent2 start
+  const uint64_t* p2_seg;
+  const uint64_t* p2_out;  // p2_nd + 1
+  uint32_t p2_nsrc, p2_d0, p2_nd;
   uint32_t bpp;       // buckets per coarse digit: digit = bucket / bpp (< 256), computed as
   uint64_t dmagic;    // (bucket * dmagic) >> 40, dmagic = ceil(2^40 / bpp), exact for bpp < 2^18
   unsigned long long* dbg;  // diagnostic phase counters (SPARKEY_FRAME_DEBUG=1), else null
@@ -223,6 +229,7 @@ struct StageTimer {
 void launch_frame_fused(const BuildParams& P, hipStream_t s, StageTimer* tm);
 void launch_partition(const BuildParams& P, hipStream_t s, StageTimer* tm);
 void launch_partition1(const BuildParams& P, hipStream_t s);
+void launch_partition2(const BuildParams& P, hipStream_t s, StageTimer* tm);
 void launch_dense_slabs(const BuildParams& P, hipStream_t s);
 void launch_frame_uniform(const BuildParams& P, hipStream_t s, StageTimer* tm);
 void launch_place_fast(const BuildParams& P, hipStream_t s, StageTimer* tm);
@@ -251,6 +258,7 @@ void launch_partition_quiet(const BuildParams& P, hipStream_t s);
 // sharded builds (shard_kernels.hip)
 void launch_dest_counts(const BuildParams& P, hipStream_t s, int world, uint32_t nd, uint64_t* d_out);
 void launch_apply_spill(const BuildParams& P, hipStream_t s, const SpillEntry* in, uint64_t n);
+void launch_digit_starts(const BuildParams& P, hipStream_t s, uint64_t* d_out);
 void launch_fetch_keys(const BuildParams& P, hipStream_t s, const uint64_t* addrs, uint64_t n, uint8_t* rec,
                        uint32_t rec_size);
 void launch_compare_keys(const BuildParams& P, hipStream_t s, const uint8_t* rec, uint64_t npairs, uint32_t rec_size);

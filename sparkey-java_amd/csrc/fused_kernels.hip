@@ -771,6 +771,13 @@ __global__ __launch_bounds__(64) void k_frame(BuildParams P) {
   mark(6);
 }
 
+__device__ __forceinline__ uint32_t bucket_of(const BuildParams& P, uint64_t hash) {
+  return (uint32_t)(fast_mod(hash, P.mod) >> kBucketShift);
+}
+__device__ __forceinline__ uint32_t digit_of(const BuildParams& P, uint32_t bucket) {
+  return (uint32_t)(((uint64_t)bucket * P.dmagic) >> 40);
+}
+
 // ================================================================================================
 // k_frame_uniform: logs whose header proves that every record has the same size R.  With no DELETE,
 // putSize == numPuts * R (R = the largest PUT record the header allows) and dataEnd - 84 == putSize,
@@ -801,7 +808,10 @@ __global__ __launch_bounds__(64) void k_frame_uniform(BuildParams P) {
     for (int v = lane; v < nvec; v += 64) *reinterpret_cast<uint4*>(lds + 16u * v) = load16_guarded(P.log, a0 + 16ll * v, log_len);
   }
   __syncthreads();
-  if (blockIdx.x == 0 && lane == 0) P.st->n_records = P.uni_n;
+  if (blockIdx.x == 0 && lane == 0) {
+    P.st->n_records = P.uni_n;
+    P.st->exit = P.fr_entry + (int64_t)P.uni_n * R;  // the framed chain's exit
+  }
   if (lane >= nrec) return;
   const int64_t p = base + (int64_t)lane * R;
   const uint32_t off = (uint32_t)(p - a0);
@@ -825,13 +835,6 @@ __global__ __launch_bounds__(64) void k_frame_uniform(BuildParams P) {
 // Pass 1: coarse digit = bucket / bpp (< 256; every digit holds bpp buckets, so the digits
 // split the table evenly -- a sharded build gives each rank a run of digits) over tiles of slabs.
 // ================================================================================================
-__device__ __forceinline__ uint32_t bucket_of(const BuildParams& P, uint64_t hash) {
-  return (uint32_t)(fast_mod(hash, P.mod) >> kBucketShift);
-}
-__device__ __forceinline__ uint32_t digit_of(const BuildParams& P, uint32_t bucket) {
-  return (uint32_t)(((uint64_t)bucket * P.dmagic) >> 40);
-}
-
 // A partition tile is part_group (<= 64) consecutive slabs, <= kPartTile entries together.
 // Wave 0 scans the slab counts with shuffles; slab_of maps a tile index to its slab, so every
 // thread then loads its entries with independent reads.
@@ -940,8 +943,22 @@ __global__ __launch_bounds__(kPart2Block) void k_part2(BuildParams P) {
   __shared__ uint64_t sh64[kPart2Block / 64 + 1];
   if (build_aborted(P)) return;
   const uint32_t dpart = blockIdx.x;
-  const uint64_t lo = P.p1_off[(uint64_t)dpart * P.p1_tiles];
-  const uint64_t hi = (dpart + 1 < 256) ? P.p1_off[(uint64_t)(dpart + 1) * P.p1_tiles] : P.p1_off_total[0];
+  // input: the digit's run of the pass-1 output, or (sharded receive) its run in every source rank's
+  // block of the exchange buffer; output: ent2 from `lo` on
+  uint64_t lo, hi;
+  const uint64_t* seg = nullptr;  // nsrc (begin, end) runs of ent3
+  uint32_t nseg = 1;
+  if (P.p2_seg) {
+    if (dpart < P.p2_d0 || dpart >= P.p2_d0 + P.p2_nd) return;
+    const uint32_t k = dpart - P.p2_d0;
+    lo = P.p2_out[k];
+    hi = P.p2_out[k + 1];
+    seg = P.p2_seg + 2ull * k * P.p2_nsrc;
+    nseg = P.p2_nsrc;
+  } else {
+    lo = P.p1_off[(uint64_t)dpart * P.p1_tiles];
+    hi = (dpart + 1 < 256) ? P.p1_off[(uint64_t)(dpart + 1) * P.p1_tiles] : P.p1_off_total[0];
+  }
   const uint32_t nbins = P.bpp;
   const uint32_t b0 = dpart * nbins;
   uint32_t* hist = dyn;
@@ -949,7 +966,10 @@ __global__ __launch_bounds__(kPart2Block) void k_part2(BuildParams P) {
   const int tid = threadIdx.x;
   for (uint32_t b = tid; b < nbins; b += kPart2Block) hist[b] = 0;
   __syncthreads();
-  for (uint64_t i = lo + tid; i < hi; i += kPart2Block) atomicAdd(&hist[bucket_of(P, P.ent3[i].hash) - b0], 1u);
+  for (uint32_t q = 0; q < nseg; q++) {
+    const uint64_t a = seg ? seg[2 * q] : lo, z = seg ? seg[2 * q + 1] : hi;
+    for (uint64_t i = a + tid; i < z; i += kPart2Block) atomicAdd(&hist[bucket_of(P, P.ent3[i].hash) - b0], 1u);
+  }
   __syncthreads();
   // exclusive scan of the bins (per consecutive bins per thread)
   const uint32_t per = (nbins + kPart2Block - 1) / kPart2Block;
@@ -972,10 +992,13 @@ __global__ __launch_bounds__(kPart2Block) void k_part2(BuildParams P) {
     }
   }
   __syncthreads();
-  for (uint64_t i = lo + tid; i < hi; i += kPart2Block) {
-    const Entry en = P.ent3[i];
-    const uint32_t b = bucket_of(P, en.hash) - b0;
-    P.ent2[lo + atomicAdd(&cur[b], 1u)] = en;
+  for (uint32_t q = 0; q < nseg; q++) {
+    const uint64_t a = seg ? seg[2 * q] : lo, z = seg ? seg[2 * q + 1] : hi;
+    for (uint64_t i = a + tid; i < z; i += kPart2Block) {
+      const Entry en = P.ent3[i];
+      const uint32_t b = bucket_of(P, en.hash) - b0;
+      P.ent2[lo + atomicAdd(&cur[b], 1u)] = en;
+    }
   }
 }
 
@@ -1131,7 +1154,7 @@ void launch_dense_slabs(const BuildParams& P, hipStream_t s) {
 }
 
 void launch_partition1(const BuildParams& P, hipStream_t s) {
-  hipLaunchKernelGGL(k_part1_hist, dim3((unsigned)P.p1_tiles), dim3(kPartBlock), 0, s, P);
+  if (!P.p1_hist_ready) hipLaunchKernelGGL(k_part1_hist, dim3((unsigned)P.p1_tiles), dim3(kPartBlock), 0, s, P);
   scan_exclusive<uint32_t, uint64_t, OpAdd>(P.p1_hist, P.p1_off, (uint64_t)P.p1_tiles * 256, P.p1_off_total,
                                             OpAdd(), P.scan_scratch_u64, s);
   hipLaunchKernelGGL(k_part1_scatter, dim3((unsigned)P.p1_tiles), dim3(kPartBlock), 0, s, P);
@@ -1140,6 +1163,11 @@ void launch_partition1(const BuildParams& P, hipStream_t s) {
 void launch_partition_quiet(const BuildParams& P, hipStream_t s) {
   launch_partition1(P, s);
   hipLaunchKernelGGL(k_part2, dim3(256), dim3(kPart2Block), (size_t)(2u * P.bpp) * sizeof(uint32_t), s, P);
+}
+
+void launch_partition2(const BuildParams& P, hipStream_t s, StageTimer* tm) {
+  hipLaunchKernelGGL(k_part2, dim3(256), dim3(kPart2Block), (size_t)(2u * P.bpp) * sizeof(uint32_t), s, P);
+  tm->mark("partition", s);
 }
 
 void launch_partition(const BuildParams& P, hipStream_t s, StageTimer* tm) {

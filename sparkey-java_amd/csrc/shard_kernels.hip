@@ -66,6 +66,12 @@ __global__ void k_dest_counts(BuildParams P, int world, uint32_t nd, uint64_t* o
   out[r] = d < 256 ? P.p1_off[(uint64_t)d * P.p1_tiles] : P.p1_off_total[0];
 }
 
+// the pass-1 start of every coarse digit, and the total (257 values)
+__global__ void k_digit_starts(BuildParams P, uint64_t* out) {
+  const uint32_t d = threadIdx.x;
+  if (d <= 256) out[d] = d < 256 ? P.p1_off[(uint64_t)d * P.p1_tiles] : P.p1_off_total[0];
+}
+
 __global__ void k_apply_spill(BuildParams P, const SpillEntry* in, uint64_t n) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -119,6 +125,10 @@ void launch_find_entry(const BuildParams& P, hipStream_t s, int64_t lo, int64_t 
 
 void launch_dest_counts(const BuildParams& P, hipStream_t s, int world, uint32_t nd, uint64_t* d_out) {
   hipLaunchKernelGGL(k_dest_counts, dim3(1), dim3(320), 0, s, P, world, nd, d_out);
+}
+
+void launch_digit_starts(const BuildParams& P, hipStream_t s, uint64_t* d_out) {
+  hipLaunchKernelGGL(k_digit_starts, dim3(1), dim3(320), 0, s, P, d_out);
 }
 
 void launch_apply_spill(const BuildParams& P, hipStream_t s, const SpillEntry* in, uint64_t n) {

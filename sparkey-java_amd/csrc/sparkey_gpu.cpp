@@ -231,6 +231,7 @@ struct ShardState {
   uint64_t n_local = 0, n_recv = 0;
   BuildParams P;        // placement over the rank's slot range
   BuildParams P_frame;  // the rank's framing (entries in slabs)
+  uint64_t digit_count[256] = {0};  // the last bin's entries per coarse digit
 };
 
 struct sparkey_plan {
@@ -244,7 +245,8 @@ struct sparkey_plan {
   uint64_t c_bcount = 0, c_bcursor = 0, c_boff = 0, c_bfun = 0, c_bpre = 0, c_carry = 0;
   uint64_t c_pairs = 0, c_parts = 0, c_su = 0, c_smp = 0, c_bft = 0;
   uint64_t c_desc = 0, c_p1h = 0, c_p1o = 0, c_dbg = 0, c_wcount = 0, c_woff = 0;
-  uint64_t c_eseg = 0, c_seg_cnt = 0, c_seg_off = 0, c_seg_mark = 0, c_seg_start = 0;
+  uint64_t c_eseg = 0, c_seg_cnt = 0, c_seg_off = 0, c_seg_mark = 0, c_seg_start = 0, c_p2tab = 0;
+  uint64_t* p2tab = nullptr;  // sharded receive: k_part2's run table
   uint64_t c_seg_cls_cnt = 0, c_seg_cls_off = 0;
   uint32_t* seg_cls_cnt = nullptr;
   uint64_t* seg_cls_off = nullptr;
@@ -445,6 +447,19 @@ static int setup_params(const LogHdr& lh, const IndexParams& ip, const sparkey_b
   return SPARKEY_OK;
 }
 
+// R when the header proves that every record of the log is a PUT of exactly R bytes: no DELETE,
+// one-byte VLQs, and putSize == numPuts * R == dataEnd - 84 with R the largest PUT record the header
+// allows (each record is at most R bytes and together they fill putSize).  Else 0.
+// SPARKEY_NO_UNIFORM disables it (tests and the bench's general-framing measurement).
+static int64_t uniform_record_size(const LogHdr& lh) {
+  const int64_t R =
+      vlq_size_long(lh.max_key_len + 1) + vlq_size_long(lh.max_value_len) + lh.max_key_len + lh.max_value_len;
+  if (lh.num_deletes == 0 && lh.num_puts > 0 && lh.max_key_len + 1 < 128 && lh.max_value_len < 128 && R <= 256 &&
+      lh.put_size == lh.num_puts * R && lh.data_end - kLogHeaderSize == lh.put_size && !getenv("SPARKEY_NO_UNIFORM"))
+    return R;
+  return 0;
+}
+
 // Slab layout of the framing output and the workspace it needs (grown on demand).
 static int reserve_for_framing(sparkey_plan* pl, BuildParams& P, int framing_path, uint64_t nrec, uint32_t slab_cap,
                                char* err, size_t err_len) {
@@ -552,16 +567,10 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
   index_header_template(lh, ip, opts->hash_seed, hdr);
 
   int framing_path = fused_framing ? 0 : 1, placement_path = 0;
-  {  // uniform records (k_frame_uniform): the header proves every record is exactly R bytes
-    const int64_t R = vlq_size_long(lh.max_key_len + 1) + vlq_size_long(lh.max_value_len) + lh.max_key_len +
-                      lh.max_value_len;
-    if (lh.num_deletes == 0 && lh.num_puts > 0 && lh.max_key_len + 1 < 128 && lh.max_value_len < 128 && R <= 256 &&
-        lh.put_size == lh.num_puts * R && lh.data_end - kLogHeaderSize == lh.put_size &&
-        !getenv("SPARKEY_NO_UNIFORM")) {
-      framing_path = 2;
-      P.uni_n = (uint64_t)lh.num_puts;
-      P.uni_rec = R;
-    }
+  if (const int64_t R = uniform_record_size(lh)) {  // k_frame_uniform: every record is exactly R bytes
+    framing_path = 2;
+    P.uni_n = (uint64_t)lh.num_puts;
+    P.uni_rec = R;
   }
   float ms = 0.f;
   Status& st = *pl->h_status;
@@ -586,6 +595,7 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
     pl->timer.begin(s);
     HIP_TRY(hipMemcpyAsync(d_out, hdr, kIndexHeaderSize, hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemcpyAsync(pl->d_status, &init, sizeof(Status), hipMemcpyHostToDevice, s));
+    P.p1_hist_ready = 0;  // (a framing kernel filling it with global atomics measured slower)
     rc = launch_framing(pl, P, framing_path, s, err, err_len);
     if (rc) return rc;
     launch_partition(P, s, &pl->timer);
@@ -632,6 +642,7 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
     if (serial) {
       BuildParams Pd = P;
       Pd.skip_del = 0;  // the single lane replays every record
+      Pd.p1_hist_ready = 0;
       if (!ip.in_memory) {
         launch_partition_quiet(Pd, s);
         launch_place_global(Pd, s, 1, 0);  // (wantedSlot, address) order into ent3
@@ -805,7 +816,7 @@ void sparkey_plan_destroy(sparkey_plan* pl) {
                   pl->bcount, pl->bcursor, pl->boff, pl->bfun, pl->bpre, pl->bfun_total, pl->carry, pl->pairs,
                   pl->parts, pl->scan_u64, pl->scan_mp, pl->desc, pl->p1_hist, pl->p1_off, pl->d_status, pl->dbg, pl->wcount, pl->woff, pl->small,
                   pl->eseg, pl->seg_cnt, pl->seg_off, pl->seg_mark, pl->seg_start,
-                  pl->seg_cls_cnt, pl->seg_cls_off};
+                  pl->seg_cls_cnt, pl->seg_cls_off, pl->p2tab};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (pl->h_status) (void)hipHostFree(pl->h_status);
@@ -1108,6 +1119,13 @@ int sparkey_shard_frame(sparkey_plan* pl, int64_t entry, int64_t frame_end, void
   uint64_t nrec = (uint64_t)((double)(std::max<int64_t>(0, sh.lh.num_puts) + std::max<int64_t>(0, sh.lh.num_deletes)) *
                              frac * 1.05) + 4096;
   int framing_path = fused ? 0 : 1;
+  const int64_t R = uniform_record_size(sh.lh);
+  if (R && (entry - kLogHeaderSize) % R == 0) {  // a record start of a uniform log: frame by stride
+    framing_path = 2;
+    P.uni_n = (uint64_t)((frame_end - entry + R - 1) / R);
+    P.uni_rec = R;
+    nrec = P.uni_n;
+  }
   const uint64_t nwaves = P.fr_nchunks ? (P.fr_nchunks + P.fr_w - 1) / P.fr_w : 0;
   uint32_t slab_cap = (uint32_t)std::min<uint64_t>(
       kPartTile, std::max<uint64_t>(64, 2 * ((nrec + std::max<uint64_t>(nwaves, 1) - 1) / std::max<uint64_t>(nwaves, 1)) + 32));
@@ -1134,6 +1152,10 @@ int sparkey_shard_frame(sparkey_plan* pl, int64_t entry, int64_t frame_end, void
     }
     if (framing_path == 0 && (st.spec_fail || st.err != ~0ull)) {
       framing_path = 1;
+      continue;
+    }
+    if (framing_path == 2 && st.spec_fail) {  // not the uniform log its header describes
+      framing_path = fused ? 0 : 1;
       continue;
     }
     break;
@@ -1173,16 +1195,39 @@ int sparkey_shard_bin(sparkey_plan* pl, uint8_t* d_send, uint64_t send_cap, void
   P.max_records = send_cap;
   launch_partition1(P, s);
   launch_dest_counts(P, s, sh.world, (uint32_t)used_digits(P), (uint64_t*)pl->small);
+  launch_digit_starts(P, s, (uint64_t*)pl->small + 64);
   HIP_TRY(hipGetLastError());
-  std::vector<uint64_t> off(sh.world + 1);
-  HIP_TRY(hipMemcpyAsync(off.data(), pl->small, (sh.world + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+  std::vector<uint64_t> off(64 + 257);
+  HIP_TRY(hipMemcpyAsync(off.data(), pl->small, off.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
   for (int r = 0; r < sh.world; r++) counts[r] = off[r + 1] - off[r];
+  for (int d = 0; d < 256; d++) sh.digit_count[d] = off[64 + d + 1] - off[64 + d];
   return SPARKEY_OK;
 }
 
+int sparkey_shard_digit_counts(const sparkey_plan* pl, uint64_t* out256) {
+  if (!pl || !pl->shard.active || !out256) return SPARKEY_E_ARG;
+  for (int d = 0; d < 256; d++) out256[d] = pl->shard.digit_count[d];
+  return SPARKEY_OK;
+}
+
+static int shard_summarize_impl(sparkey_plan* pl, const uint8_t* d_recv, uint64_t n_recv, const uint64_t* digit_counts,
+                                void* stream, int64_t* fun_out, char* err, size_t err_len);
+
 int sparkey_shard_summarize(sparkey_plan* pl, const uint8_t* d_recv, uint64_t n_recv, void* stream, int64_t* fun_out,
                             char* err, size_t err_len) {
+  return shard_summarize_impl(pl, d_recv, n_recv, nullptr, stream, fun_out, err, err_len);
+}
+
+int sparkey_shard_summarize_grouped(sparkey_plan* pl, const uint8_t* d_recv, uint64_t n_recv,
+                                    const uint64_t* digit_counts, void* stream, int64_t* fun_out, char* err,
+                                    size_t err_len) {
+  if (!digit_counts) return SPARKEY_E_ARG;
+  return shard_summarize_impl(pl, d_recv, n_recv, digit_counts, stream, fun_out, err, err_len);
+}
+
+static int shard_summarize_impl(sparkey_plan* pl, const uint8_t* d_recv, uint64_t n_recv, const uint64_t* digit_counts,
+                                void* stream, int64_t* fun_out, char* err, size_t err_len) {
   int rc = shard_check(pl, err, err_len);
   if (rc) return rc;
   ShardState& sh = pl->shard;
@@ -1213,8 +1258,56 @@ int sparkey_shard_summarize(sparkey_plan* pl, const uint8_t* d_recv, uint64_t n_
   init.err = ~0ull;
   init.n_records = n_recv;
   HIP_TRY(hipMemcpyAsync(pl->d_status, &init, sizeof(Status), hipMemcpyHostToDevice, s));
-  launch_dense_slabs(P, s);
-  launch_partition(P, s, &pl->timer);
+  P.p2_seg = nullptr;
+  P.p2_out = nullptr;
+  if (digit_counts) {
+    // the exchange buffer holds, per source rank in rank order, that rank's entries for this rank's
+    // coarse digits in digit order (its pass-1 output): k_part2 reads the runs in place
+    const uint64_t nd = used_digits(P), G = (uint64_t)sh.world;
+    const uint64_t d0 = (nd * (uint64_t)sh.rank) / G, d1 = (nd * (uint64_t)(sh.rank + 1)) / G;
+    const uint64_t nk = d1 - d0;
+    std::vector<uint64_t> tab(2 * nk * G + nk + 1);
+    uint64_t* segs = tab.data();
+    uint64_t* outs = tab.data() + 2 * nk * G;
+    std::vector<uint64_t> blk(G + 1, 0);
+    for (uint64_t r = 0; r < G; r++) {
+      uint64_t m = 0;
+      for (uint64_t d = d0; d < d1; d++) m += digit_counts[r * 256 + d];
+      blk[r + 1] = blk[r] + m;
+    }
+    if (blk[G] != n_recv) {
+      set_err(err, err_len, "digit counts do not add up to the received entries");
+      return SPARKEY_E_ARG;
+    }
+    std::vector<uint64_t> cur(blk.begin(), blk.end() - 1);
+    uint64_t o = 0;
+    for (uint64_t k = 0; k < nk; k++) {
+      outs[k] = o;
+      for (uint64_t r = 0; r < G; r++) {
+        const uint64_t c = digit_counts[r * 256 + d0 + k];
+        segs[2 * (k * G + r)] = cur[r];
+        segs[2 * (k * G + r) + 1] = cur[r] + c;
+        cur[r] += c;
+        o += c;
+      }
+    }
+    outs[nk] = o;
+    HIP_TRY(grow(&pl->p2tab, pl->c_p2tab, tab.size()));
+    HIP_TRY(hipMemcpyAsync(pl->p2tab, tab.data(), tab.size() * sizeof(uint64_t), hipMemcpyHostToDevice, s));
+    P.ent3 = const_cast<Entry*>(reinterpret_cast<const Entry*>(d_recv));
+    P.p2_seg = pl->p2tab;
+    P.p2_out = pl->p2tab + 2 * nk * G;
+    P.p2_nsrc = (uint32_t)G;
+    P.p2_d0 = (uint32_t)d0;
+    P.p2_nd = (uint32_t)nk;
+    launch_partition2(P, s, &pl->timer);
+    P.ent3 = pl->ent3;  // the later steps' scratch (k_place sorts oversized buckets there)
+    P.p2_seg = nullptr;
+    P.p2_out = nullptr;
+  } else {
+    launch_dense_slabs(P, s);
+    launch_partition(P, s, &pl->timer);
+  }
   fun_out[0] = 0;  // identity carry function f(x) = max(0, x + 0) for an empty range
   fun_out[1] = 0;
   if (P.b_hi > P.b_lo) {

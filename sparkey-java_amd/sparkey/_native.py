@@ -126,6 +126,8 @@ _SIGS = {
                             ctypes.c_int),
     "sparkey_shard_bin": ([_vp, _vp, ctypes.c_uint64, _vp, _u64p] + _E, ctypes.c_int),
     "sparkey_shard_summarize": ([_vp, _vp, ctypes.c_uint64, _vp, _i64p] + _E, ctypes.c_int),
+    "sparkey_shard_digit_counts": ([_vp, _u64p], ctypes.c_int),
+    "sparkey_shard_summarize_grouped": ([_vp, _vp, ctypes.c_uint64, _u64p, _vp, _i64p] + _E, ctypes.c_int),
     "sparkey_shard_place": ([_vp, ctypes.c_int64, _vp, _vp, ctypes.c_uint64, _vp, ctypes.POINTER(ShardPlaceResult)]
                             + _E, ctypes.c_int),
     "sparkey_shard_pairs": ([_vp, _u64p, ctypes.c_uint64] + _E, ctypes.c_int),
@@ -296,6 +298,20 @@ class Plan:
     def shard_summarize(self, d_recv: int, n_recv: int, stream: int = 0):
         f = (ctypes.c_int64 * 2)()
         self._call("sparkey_shard_summarize", ctypes.c_void_p(d_recv), n_recv, ctypes.c_void_p(stream), f)
+        return int(f[0]), int(f[1])
+
+    def shard_digit_counts(self):
+        out = (ctypes.c_uint64 * 256)()
+        if _lib.sparkey_shard_digit_counts(self._h, out) != OK:
+            raise ValueError("no sharded build in progress")
+        return [int(v) for v in out]
+
+    def shard_summarize_grouped(self, d_recv: int, n_recv: int, digit_counts, stream: int = 0):
+        """digit_counts: world x 256 (row = source rank), every rank's shard_digit_counts()."""
+        flat = [int(v) for row in digit_counts for v in row]
+        arr = (ctypes.c_uint64 * len(flat))(*flat)
+        f = (ctypes.c_int64 * 2)()
+        self._call("sparkey_shard_summarize_grouped", ctypes.c_void_p(d_recv), n_recv, arr, ctypes.c_void_p(stream), f)
         return int(f[0]), int(f[1])
 
     def shard_place(self, carry_in: int, d_slots: int, d_spill: int, spill_cap: int, stream: int = 0):

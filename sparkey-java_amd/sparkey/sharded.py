@@ -93,6 +93,19 @@ def parse_log_header(header: bytes) -> dict:
     return dict(zip(keys, f))
 
 
+def uniform_record_size(h: dict) -> int:
+    """R when the header proves every record is a PUT of exactly R bytes (no DELETE, one-byte VLQs,
+    putSize == numPuts * R == dataEnd - 84); else 0.  Mirrors uniform_record_size in sparkey_gpu.cpp:
+    the shard entries are then arithmetic (each rank's framing still checks every record header)."""
+    import os
+    k, v = int(h["max_key_len"]), int(h["max_value_len"])
+    r = _vlq_size(k + 1) + _vlq_size(v) + k + v
+    ok = (h["num_deletes"] == 0 and h["num_puts"] > 0 and k + 1 < 128 and v < 128 and r <= 256 and
+          h["put_size"] == h["num_puts"] * r and h["data_end"] - LOG_HEADER_SIZE == h["put_size"] and
+          not os.environ.get("SPARKEY_NO_UNIFORM"))
+    return r if ok else 0
+
+
 def shard_layout(header: bytes, file_len: int, world: int) -> ShardLayout:
     h = parse_log_header(header)
     data_end = max(int(h["data_end"]), LOG_HEADER_SIZE)
@@ -198,8 +211,13 @@ class GpuShardSteps:
     def bin(self, send: torch.Tensor, n: int, world: int):
         return self.plan.shard_bin(send.data_ptr(), n, world, self.stream)
 
-    def summarize(self, recv: torch.Tensor, n: int):
+    def summarize(self, recv: torch.Tensor, n: int, digit_counts=None):
+        if digit_counts is not None:
+            return self.plan.shard_summarize_grouped(recv.data_ptr(), n, digit_counts, self.stream)
         return self.plan.shard_summarize(recv.data_ptr(), n, self.stream)
+
+    def digit_counts(self):
+        return self.plan.shard_digit_counts()
 
     def place(self, carry_in, out: torch.Tensor, out_off: int, spill: torch.Tensor, spill_cap: int):
         return self.plan.shard_place(carry_in, out.data_ptr() + out_off, spill.data_ptr(), spill_cap, self.stream)
@@ -304,13 +322,18 @@ class ShardedBuilder:
         h = parse_log_header(header)
 
         # ---- 1 entries: speculate, frame, verify by induction from c_0 = 84 ----
+        uni = uniform_record_size(h)
         if g == 0:
             c_g = LOG_HEADER_SIZE
         elif lay.small:
             c_g = data_end
+        elif uni:  # uniform records: the first record start at or after lo
+            c_g = min(data_end, LOG_HEADER_SIZE + -(-(lay.lo[g] - LOG_HEADER_SIZE) // uni) * uni)
         else:
             c_g = s.find_entry(lay.lo[g], lay.window)
+        mark("find_entry")
         cs = [int(v) for v in c.allgather_i64([c_g])[:, 0]]
+        mark("gather_entries")
         entries = []
         for r, v in enumerate(cs):
             ok = v >= 0 and (r == 0 or (lay.small and v == data_end) or lay.lo[r] <= v <= data_end)
@@ -364,7 +387,7 @@ class ShardedBuilder:
         out_len = (INDEX_HEADER_SIZE if g == 0 else 0) + (slot_hi - slot_lo) * slot_size
         res = ShardResult(out=None, slot_lo=slot_lo, slot_hi=slot_hi, out_offset=out_off, rounds=rounds,
                           phase_ms=phase)
-        mark("entries+frame")
+        mark("frame+verify")
 
         if n_deletes > 0 or n_total >= _capacity(h, opts):
             return self._gathered(res, header, file_len, buf, buf_lo, buf_hi, lay, opts, slot_size, out_len)
@@ -372,17 +395,22 @@ class ShardedBuilder:
         # ---- 2 exchange: every entry to the owner of its slot range ----
         send = s.alloc(max(1, n_local) * ENTRY_BYTES)
         counts = s.bin(send, n_local, G) if n_local else [0] * G
-        M = c.allgather_i64(counts)                       # M[src][dst]
+        digits = s.digit_counts() if n_local else [0] * 256
+        mark("bin")
+        MD = c.allgather_i64(list(counts) + list(digits))  # per rank: entries per destination, per digit
+        M, D = MD[:, :G], MD[:, G:]                        # M[src][dst], D[src][digit]
         out_splits = [int(M[r][g]) * 2 for r in range(G)]  # int64 elements (2 per entry)
         in_splits = [int(x) * 2 for x in counts]
         recv = c.all_to_all(send.view(torch.int64)[: 2 * max(1, n_local)] if n_local else
                             send.view(torch.int64)[:0], in_splits, out_splits, buf.device)
         n_recv = sum(out_splits) // 2
-        mark("exchange")
+        mark("all_to_all")
 
         # ---- 3 placement ----
-        fun = s.summarize(recv, n_recv)
+        fun = s.summarize(recv, n_recv, D.tolist())  # the runs arrive grouped by digit: no first pass
+        mark("summarize")
         F = [tuple(int(v) for v in row) for row in c.allgather_i64(list(fun))]
+        mark("gather_carry")
         x0 = _compose(F)[0]             # N < capacity: the wrap fixed point is C_total
         carry = x0
         for r in range(g):
@@ -395,6 +423,7 @@ class ShardedBuilder:
             if n_spill <= spill_cap:
                 break
             spill_cap = n_spill
+        mark("place_kernel")
         flags = c.allgather_i64([n_spill, n_pairs, int(non_canon)])
         res.n_spill, res.n_pairs = int(flags[:, 0].sum()), int(flags[:, 1].sum())
         if flags[:, 2].any():
@@ -407,7 +436,7 @@ class ShardedBuilder:
             if allsp is not None:
                 s.apply_spill(allsp, allsp.numel() // 4)
 
-        mark("place")
+        mark("spill")
         # ---- 4 stats: boundary slots, per-range sums, reduce, header ----
         bnd = c.allgather_i64([_signed(v) for v in s.boundary()] + [int(slot_hi > slot_lo)])
         prev_hash, prev_occ = 0, 0
