@@ -5,7 +5,7 @@ header) of a C2-shaped log (10M PUTs per GPU, 16-byte keys, 100-byte values, NON
 resident in HBM, into a device-resident .spi image.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--entries 10000000] [--no-cpu-baseline]
-                    [--workload c2|c3|c5|churn]
+                    [--workload c2|c3|c5|churn|get]
 
 N = 1: the C2 log (10M records) built on one GPU; the line carries the per-stage roofline and the
 CPU baseline (the oracle's sequential IN_MEMORY restatement on the host, timed on the same log).
@@ -62,7 +62,51 @@ WORKLOADS = {
     "c5": {"name": "C5: C3 log, SORTING constructionMethod", "sorting": True, "path": 0},
     "churn": {"name": "C2 shape with overwrites and DELETEs: keys from a pool of 0.8 n, 10% DELETE records, "
                       "IN_MEMORY (exact replay over slot segments)", "sorting": False, "path": 2},
+    "get": {"name": "batched IndexHash.get of every key of the C2 index (log and index resident in HBM)",
+            "sorting": False, "path": 0},
 }
+
+
+def lookups(args, dev):
+    """--workload get: one step = IndexHash.get of all n C2 keys in one batch (sparkey_get_batch)."""
+    import numpy as np
+    import sparkey
+    from sparkey import _native, synth
+    n = args.entries
+    log_np = synth.fixed_log(n, 16, 100, seed=args.seed, file_id=0x5EED0000)
+    header = log_np[:84].tobytes()
+    d_log = torch.from_numpy(log_np).to(dev)
+    opts = _native.make_opts(hash_size=0, hash_seed=HASH_SEED, device=dev.index)
+    out_len = _native.index_size(header, opts)
+    d_index = torch.empty(out_len, dtype=torch.uint8, device=dev)
+    plan = _native.Plan(dev.index, log_np.size, n)
+    plan.build(header, d_log.data_ptr(), log_np.size, d_index.data_ptr(), out_len, opts)
+    keys = torch.from_numpy(np.ascontiguousarray(log_np[84:].reshape(n, 118)[:, 2:18]).reshape(-1)).to(dev)
+    key_off = torch.arange(0, 16 * (n + 1), 16, dtype=torch.int64, device=dev)
+    pos = torch.empty(n, dtype=torch.int64, device=dev)
+    ln = torch.empty(n, dtype=torch.int64, device=dev)
+    stream = torch.cuda.Stream(dev)
+
+    def step():
+        plan.get_batch(d_log.data_ptr(), log_np.size, d_index.data_ptr(), out_len, keys.data_ptr(),
+                       key_off.data_ptr(), n, pos.data_ptr(), ln.data_ptr(), stream.cuda_stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    want = torch.arange(n, dtype=torch.int64, device=dev) * 118 + 84 + 18
+    assert bool((pos == want).all()) and bool((ln == 100).all()), "lookup results differ from the log layout"
+    plan.close()
+    return {"metric": "lookups/s, batched IndexHash.get over the C2 index (extra measurement, not the headline)",
+            "value": n * args.steps / el, "ms_per_step": el * 1000.0 / args.steps, "unit": "lookups/s",
+            "config": {"workload": WORKLOADS["get"]["name"], "entries": n, "log_bytes": int(log_np.size),
+                       "spi_bytes": int(out_len), "parallelism": "single"},
+            "roofline": None, "cpu_baseline": None, "version": sparkey.version()}
 
 
 def single_gpu(args, dev):
@@ -288,10 +332,14 @@ def main():
             dist.init_process_group(args.backend)
         r = sharded(args, dev, world, rank)
         dist.destroy_process_group()
+    elif args.workload == "get":
+        r = lookups(args, dev)
     else:
         r = single_gpu(args, dev)
     if rank == 0:
-        line = {"metric": METRIC, "value": r.pop("value"), "unit": "keys/s", "n_gpus": world, "steps": args.steps,
+        metric = r.pop("metric", METRIC)
+        line = {"metric": metric, "value": r.pop("value"), "unit": r.pop("unit", "keys/s"), "n_gpus": world,
+                "steps": args.steps,
                 "warmup": args.warmup, "ms_per_step": r.pop("ms_per_step"), "higher_is_better": True,
                 "scaling": "weak", "vs_baseline": None, "dtype": "u64", "data": "synthetic"}
         line.update(r)

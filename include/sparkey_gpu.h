@@ -104,6 +104,15 @@ const char* sparkey_plan_stage_name(const sparkey_plan* plan, int32_t i);
 double sparkey_plan_stage_ms(const sparkey_plan* plan, int32_t i);
 void sparkey_plan_destroy(sparkey_plan* plan);
 
+/* Batched IndexHash.get (IndexHash.java:398-452) against a built index and its log, both resident in
+ * device memory: query i is the key d_keys[d_key_off[i] .. d_key_off[i + 1]); d_value_pos[i] = the log
+ * offset of its value (or -1 when absent), d_value_len[i] = its length (or -1).  Runs IndexHash.open's
+ * checks first (identifier match, index size, dataEnd).  A matching slot that points at a DELETE
+ * record is SPARKEY_E_CORRUPT_DATA ("Invalid data - reference to delete entry"). */
+int sparkey_get_batch(sparkey_plan* plan, const uint8_t* d_log, uint64_t log_len, const uint8_t* d_index,
+                      uint64_t index_len, const uint8_t* d_keys, const uint64_t* d_key_off, uint64_t n,
+                      int64_t* d_value_pos, int64_t* d_value_len, void* stream, char* err, size_t err_len);
+
 /* ---- sharded build: one process per GPU, the log's byte range split across ranks ----
  * No reference counterpart (the reference build is single-threaded, Sparkey.java:36); these are
  * the device steps of IndexHash.createNew split at the points where ranks exchange data.  The

@@ -22,6 +22,7 @@
 
 #include "../../include/sparkey_gpu.h"
 #include "build_kernels.hpp"
+#include "lookup.hpp"
 
 using namespace sk;
 
@@ -742,6 +743,96 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
 extern "C" {
 
 const char* sparkey_gpu_version(void) { return "sparkey-mi355x 0.1 (gfx950)"; }
+
+// Batched IndexHash.get (IndexHash.java:398-452): IndexHash.open's checks (IndexHash.java:72-80,
+// 115-121, 352-356), then one lane per query.
+int sparkey_get_batch(sparkey_plan* pl, const uint8_t* d_log, uint64_t log_len, const uint8_t* d_index,
+                      uint64_t index_len, const uint8_t* d_keys, const uint64_t* d_key_off, uint64_t n,
+                      int64_t* d_value_pos, int64_t* d_value_len, void* stream, char* err, size_t err_len) {
+  if (!pl || !d_log || !d_index || (n && (!d_keys || !d_key_off || !d_value_pos || !d_value_len))) {
+    set_err(err, err_len, "null argument");
+    return SPARKEY_E_ARG;
+  }
+  HIP_TRY(hipSetDevice(pl->device));
+  hipStream_t s = stream ? (hipStream_t)stream : pl->own_stream;
+  if (index_len < kIndexHeaderSize || log_len < kLogHeaderSize) {
+    set_err(err, err_len, "Corrupt index file - incorrect size");
+    return SPARKEY_E_CORRUPT_DATA;
+  }
+  uint8_t ih[kIndexHeaderSize], lhb[kLogHeaderSize];
+  HIP_TRY(hipMemcpyAsync(ih, d_index, kIndexHeaderSize, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(lhb, d_log, kLogHeaderSize, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  LogHdr lh;
+  int rc = parse_log_header(lhb, kLogHeaderSize, log_len, &lh, err, err_len);
+  if (rc) return rc;
+  if (rd32(ih) != kIndexMagic) {
+    set_err(err, err_len, "File is not a Sparkey index file");
+    return SPARKEY_E_NOT_LOG;
+  }
+  if (rd32(ih + 4) != 1) {
+    set_err(err, err_len, "Incompatible index file version");
+    return SPARKEY_E_VERSION;
+  }
+  if ((int32_t)rd32(ih + 12) != lh.file_id) {
+    set_err(err, err_len, "Log file did not match index file");
+    return SPARKEY_E_ARG;
+  }
+  const int64_t data_end = (int64_t)rd64(ih + 20);
+  if (data_end > lh.data_end) {
+    set_err(err, err_len, "Corrupt index file: referencing more data than exists in the log file");
+    return SPARKEY_E_CORRUPT_DATA;
+  }
+  LookupParams L;
+  memset(&L, 0, sizeof(L));
+  L.hash_size = (int32_t)rd32(ih + 72);
+  L.addr_size = (int32_t)rd32(ih + 68);
+  L.cap = rd64(ih + 76);
+  L.ebb = (int32_t)rd32(ih + 92);
+  L.seed = rd32(ih + 16);
+  L.max_disp = (int64_t)rd64(ih + 84);
+  if ((L.hash_size != 4 && L.hash_size != 8) || (L.addr_size != 4 && L.addr_size != 8) || L.cap == 0) {
+    set_err(err, err_len, "Corrupt index header");
+    return SPARKEY_E_CORRUPT_DATA;
+  }
+  L.slot_size = L.hash_size + L.addr_size;
+  if (index_len != kIndexHeaderSize + (uint64_t)L.slot_size * L.cap) {
+    set_err(err, err_len, "Corrupt index file - incorrect size. Expected " +
+                              std::to_string(kIndexHeaderSize + (uint64_t)L.slot_size * L.cap) + " but was " +
+                              std::to_string(index_len));
+    return SPARKEY_E_CORRUPT_DATA;
+  }
+  if (lh.compression_type != 0) {
+    set_err(err, err_len, "compressed logs are not supported");
+    return SPARKEY_E_UNSUPPORTED;
+  }
+  L.log = d_log;
+  L.log_len = log_len;
+  L.slots = d_index + kIndexHeaderSize;
+  L.mod = make_fastmod(L.cap);
+  L.keys = d_keys;
+  L.key_off = d_key_off;
+  L.n = n;
+  L.value_pos = d_value_pos;
+  L.value_len = d_value_len;
+  HIP_TRY(grow(&pl->small, pl->c_small, 512));
+  L.err = (unsigned long long*)pl->small + 400;
+  const unsigned long long none = ~0ull;
+  HIP_TRY(hipMemcpyAsync(L.err, &none, sizeof(none), hipMemcpyHostToDevice, s));
+  launch_get(L, s);
+  HIP_TRY(hipGetLastError());
+  unsigned long long e = 0;
+  HIP_TRY(hipMemcpyAsync(&e, L.err, sizeof(e), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  if (e != ~0ull) {
+    const int code = -(int)(e & 0xff);
+    set_err(err, err_len, std::string(code == SPARKEY_E_CORRUPT_DATA ? "Invalid data - reference to delete entry"
+                                                                      : code_message(code)) +
+                              " (query " + std::to_string(e >> 8) + ")");
+    return code;
+  }
+  return SPARKEY_OK;
+}
 
 const char* sparkey_strerror(int code) { return code_message(code); }
 

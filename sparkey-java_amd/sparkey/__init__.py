@@ -1,6 +1,7 @@
 """MI355X-native Sparkey hash-file builder: the com.spotify.sparkey writer API with writeHash() on gfx950.
 
-Importing this package loads libsparkey_gpu.so; there is no CPU fallback.
+Importing this package loads libsparkey_gpu.so; there is no CPU fallback.  Batched GPU lookups over a
+built hash file: sparkey.reader.GpuHashReader.
 """
 from ._native import (BuildStats, Plan, SparkeyGpuError, SparkeyIOError, SparkeyRuntimeError, build_index_file,
                       build_index_mem, index_size, make_opts, version)

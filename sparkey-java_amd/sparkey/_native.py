@@ -140,6 +140,8 @@ _SIGS = {
     "sparkey_shard_stats": ([_vp, ctypes.c_uint64, ctypes.c_int32, _vp, _i64p] + _E, ctypes.c_int),
     "sparkey_index_header": ([_vp, ctypes.POINTER(BuildOpts), ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
                               ctypes.c_int64, ctypes.c_int64, _vp] + _E, ctypes.c_int),
+    "sparkey_get_batch": ([_vp, _vp, ctypes.c_uint64, _vp, ctypes.c_uint64, _vp, _vp, ctypes.c_uint64, _vp, _vp, _vp]
+                          + _E, ctypes.c_int),
 }
 for _name, (_args, _res) in _SIGS.items():
     _f = getattr(_lib, _name)
@@ -255,6 +257,17 @@ class Plan:
         if rc != OK:
             raise_for(rc, err.value.decode(errors="replace"))
         return stats
+
+    def get_batch(self, d_log: int, log_len: int, d_index: int, index_len: int, d_keys: int, d_key_off: int, n: int,
+                  d_value_pos: int, d_value_len: int, stream: int = 0) -> None:
+        """Batched IndexHash.get on device buffers (sparkey_get_batch)."""
+        err = ctypes.create_string_buffer(512)
+        rc = _lib.sparkey_get_batch(self._h, ctypes.c_void_p(d_log), log_len, ctypes.c_void_p(d_index), index_len,
+                                    ctypes.c_void_p(d_keys), ctypes.c_void_p(d_key_off), n,
+                                    ctypes.c_void_p(d_value_pos), ctypes.c_void_p(d_value_len),
+                                    ctypes.c_void_p(stream), err, 512)
+        if rc != OK:
+            raise_for(rc, err.value.decode(errors="replace"))
 
     def set_profiling(self, enabled: bool) -> None:
         _lib.sparkey_plan_set_profiling(self._h, 1 if enabled else 0)

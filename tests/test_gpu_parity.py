@@ -348,3 +348,40 @@ def test_uniform_disabled_gives_same_bytes(native, monkeypatch):
     monkeypatch.setenv("SPARKEY_NO_UNIFORM", "1")
     b, sb = gpu_build(native, log, 11, 8)
     assert sa.framing_path == 2 and sb.framing_path == 0 and a == b
+
+
+# --- batched IndexHash.get on the GPU (sparkey_get_batch) against the oracle's get ---
+def _reader(log, spi):
+    from sparkey.reader import GpuHashReader
+    return GpuHashReader(log, spi)
+
+
+@pytest.mark.parametrize("hash_size", [4, 8])
+def test_get_batch_matches_oracle(native, hash_size):
+    ops = []
+    rng = np.random.default_rng(hash_size)
+    for i in range(20000):
+        k = b"k%d" % int(rng.integers(0, 6000))
+        ops.append(("del", k, None) if rng.random() < 0.15 else ("put", k, b"v%d" % i))
+    log = make_log(ops=ops)
+    spi, _ = gpu_build(native, log, 321, hash_size)
+    keys = [b"k%d" % i for i in range(6500)] + [b"", b"absent", b"k" * 300]
+    r = _reader(log, spi)
+    got = r.get_batch(keys)
+    r.close()
+    want = [oracle.get(spi, log, k) for k in keys]
+    assert got == want
+
+
+def test_get_batch_c1_and_errors(native):
+    log = make_log(key_value_puts(1000, b"key_%d", b"value_%d"), block_size=1024)
+    spi, _ = gpu_build(native, log, 1234)
+    r = _reader(log, spi)
+    assert r.get_batch([b"key_%d" % i for i in range(1000)]) == [b"value_%d" % i for i in range(1000)]
+    assert r.get(b"key_1000") is None
+    r.close()
+    other = make_log(key_value_puts(10), file_id=0x777)
+    with pytest.raises(ValueError):
+        _reader(other, spi).get(b"key_1")          # "Log file did not match index file"
+    with pytest.raises(RuntimeError):
+        _reader(log, spi[:-4]).get(b"key_1")       # "Corrupt index file - incorrect size"
