@@ -437,16 +437,20 @@ class ShardedBuilder:
                 s.apply_spill(allsp, allsp.numel() // 4)
 
         mark("spill")
-        # ---- 4 stats: boundary slots, per-range sums, reduce, header ----
-        bnd = c.allgather_i64([_signed(v) for v in s.boundary()] + [int(slot_hi > slot_lo)])
-        prev_hash, prev_occ = 0, 0
-        for r in range(g - 1, -1, -1):
-            if bnd[r][4]:
-                prev_hash, prev_occ = int(bnd[r][2]) & 0xFFFFFFFFFFFFFFFF, int(bnd[r][3] != 0)
-                break
-        mx, col, tot = s.stats(prev_hash, prev_occ) if slot_hi > slot_lo else (0, 0, 0)
-        S = c.allgather_i64([mx, col, tot])
-        max_disp, collisions, total_disp = int(S[:, 0].max()), int(S[:, 1].sum()), int(S[:, 2].sum())
+        # ---- 4 stats: per-range sums (the first slot is not compared with its predecessor), the
+        #      boundary slots, one gather; the cross-range comparisons are added here ----
+        nonempty = int(slot_hi > slot_lo)
+        bslots = s.boundary()
+        mx, col, tot = s.stats(0, 0) if nonempty else (0, 0, 0)
+        bnd = c.allgather_i64([_signed(v) for v in bslots] + [nonempty, mx, col, tot])
+        max_disp, collisions, total_disp = int(bnd[:, 5].max()), int(bnd[:, 6].sum()), int(bnd[:, 7].sum())
+        prev = None  # (hash, occupied) of the last slot of the previous non-empty range
+        for r in range(G):
+            if not bnd[r][4]:
+                continue
+            if prev is not None and prev[1] and prev[0] == int(bnd[r][0]) & 0xFFFFFFFFFFFFFFFF:
+                collisions += 1  # calculateMaxDisplacement compares every slot with the one before
+            prev = (int(bnd[r][2]) & 0xFFFFFFFFFFFFFFFF, int(bnd[r][3] != 0))
         # wrap quirk (IndexHash.java:239-241): slot 0 and slot cap-1 occupied with equal hashes
         last = max(r for r in range(G) if bnd[r][4])
         if bnd[0][1] != 0 and bnd[last][3] != 0 and bnd[0][0] == bnd[last][2]:
