@@ -5,7 +5,7 @@ header) of a C2-shaped log (10M PUTs per GPU, 16-byte keys, 100-byte values, NON
 resident in HBM, into a device-resident .spi image.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--entries 10000000] [--no-cpu-baseline]
-                    [--workload c2|c3|c5|churn|get]
+                    [--workload c2|c3|c5|churn|get|append]
 
 N = 1: the C2 log (10M records) built on one GPU; the line carries the per-stage roofline and the
 CPU baseline (the oracle's sequential IN_MEMORY restatement on the host, timed on the same log).
@@ -62,9 +62,54 @@ WORKLOADS = {
     "c5": {"name": "C5: C3 log, SORTING constructionMethod", "sorting": True, "path": 0},
     "churn": {"name": "C2 shape with overwrites and DELETEs: keys from a pool of 0.8 n, 10% DELETE records, "
                       "IN_MEMORY (exact replay over slot segments)", "sorting": False, "path": 2},
+    "append": {"name": "GPU log producer (batched LogWriter.put)", "sorting": False, "path": 0},
     "get": {"name": "batched IndexHash.get of every key of the C2 index (log and index resident in HBM)",
             "sorting": False, "path": 0},
 }
+
+
+def appends(args, dev):
+    """--workload append: one step = LogWriter.put of n C2 records in one batch (sparkey_log_append),
+    keys and values already in HBM; the result is checked byte for byte against the C2 log."""
+    import numpy as np
+    import sparkey
+    from sparkey import synth
+    from sparkey.gpu_log import GpuLogAppender, new_log_header
+    n = args.entries
+    log_np = synth.fixed_log(n, 16, 100, seed=args.seed, file_id=0x5EED0000)
+    recs = log_np[84:].reshape(n, 118)
+    keys = torch.from_numpy(np.ascontiguousarray(recs[:, 2:18]).reshape(-1)).to(dev)
+    vals = torch.from_numpy(np.ascontiguousarray(recs[:, 18:]).reshape(-1)).to(dev)
+    koff = torch.arange(0, 16 * (n + 1), 16, dtype=torch.int64, device=dev)
+    voff = torch.arange(0, 100 * (n + 1), 100, dtype=torch.int64, device=dev)
+    kind = torch.ones(n, dtype=torch.uint8, device=dev)
+    out = torch.empty(118 * n, dtype=torch.uint8, device=dev)
+    app = GpuLogAppender(dev.index)
+    stream = torch.cuda.Stream(dev)
+
+    def step():
+        hdr = new_log_header(0x5EED0000)
+        app.append_device(hdr, kind, keys, koff, vals, voff, n, out, out.numel(), stream.cuda_stream)
+        return hdr
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        hdr = step()
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    assert bytes(hdr) == log_np[:84].tobytes(), "header differs from the C2 log's"
+    assert torch.equal(out, torch.from_numpy(log_np[84:]).to(dev)), "records differ from the C2 log"
+    app.close()
+    ms = el * 1000.0 / args.steps
+    return {"metric": "records/s, batched LogWriter.put of the C2 records (extra measurement, not the headline)",
+            "value": n * args.steps / el, "ms_per_step": ms, "unit": "records/s",
+            "config": {"workload": "GPU log producer: 10M PUTs (16 B key, 100 B value) -> the C2 log bytes",
+                       "entries": n, "log_bytes": int(log_np.size), "parallelism": "single"},
+            "hbm_gbs": (116 * n + 118 * n) / (ms * 1e-3) / 1e9,
+            "roofline": None, "cpu_baseline": None, "version": sparkey.version()}
 
 
 def lookups(args, dev):
@@ -334,6 +379,8 @@ def main():
         dist.destroy_process_group()
     elif args.workload == "get":
         r = lookups(args, dev)
+    elif args.workload == "append":
+        r = appends(args, dev)
     else:
         r = single_gpu(args, dev)
     if rank == 0:

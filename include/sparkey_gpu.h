@@ -104,6 +104,20 @@ const char* sparkey_plan_stage_name(const sparkey_plan* plan, int32_t i);
 double sparkey_plan_stage_ms(const sparkey_plan* plan, int32_t i);
 void sparkey_plan_destroy(sparkey_plan* plan);
 
+/* Batched LogWriter.put / delete, NONE compression (LogWriter.java:96-115,
+ * UncompressedBlockOutput.java:34-45, LogHeader.java:161-172).  Op i (d_kind[i]: 1 PUT, 0 DELETE) has
+ * key d_keys[d_key_off[i] .. d_key_off[i + 1]) and, for a PUT, value d_values[d_val_off[i] ..
+ * d_val_off[i + 1]).  Its record (PUT: VLQ(keyLen + 1) VLQ(valueLen) key value; DELETE: 0x00
+ * VLQ(keyLen) key) is written from d_out on, in op order; a DELETE whose key is longer than maxKeyLen
+ * at that point is dropped, as LogWriter.delete does (LogWriter.java:109-114).  header84 (host) is the
+ * log header before the batch and is updated in place (numPuts, numDeletes, putSize, deleteSize,
+ * maxKeyLen, maxValueLen, maxEntriesPerBlock = 1, dataEnd += bytes written).  d_out must hold
+ * out_cap bytes; SPARKEY_E_BUFFER (nothing written) when the records need more. */
+int sparkey_log_append(sparkey_plan* plan, uint8_t* header84, const uint8_t* d_kind, const uint8_t* d_keys,
+                       const uint64_t* d_key_off, const uint8_t* d_values, const uint64_t* d_val_off, uint64_t n,
+                       uint8_t* d_out, uint64_t out_cap, uint64_t* bytes_written, void* stream, char* err,
+                       size_t err_len);
+
 /* Batched IndexHash.get (IndexHash.java:398-452) against a built index and its log, both resident in
  * device memory: query i is the key d_keys[d_key_off[i] .. d_key_off[i + 1]); d_value_pos[i] = the log
  * offset of its value (or -1 when absent), d_value_len[i] = its length (or -1).  Runs IndexHash.open's

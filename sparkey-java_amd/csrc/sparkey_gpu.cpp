@@ -23,6 +23,7 @@
 #include "../../include/sparkey_gpu.h"
 #include "build_kernels.hpp"
 #include "lookup.hpp"
+#include "append.hpp"
 
 using namespace sk;
 
@@ -248,6 +249,13 @@ struct sparkey_plan {
   uint64_t c_desc = 0, c_p1h = 0, c_p1o = 0, c_dbg = 0, c_wcount = 0, c_woff = 0;
   uint64_t c_eseg = 0, c_seg_cnt = 0, c_seg_off = 0, c_seg_mark = 0, c_seg_start = 0, c_p2tab = 0;
   uint64_t* p2tab = nullptr;  // sharded receive: k_part2's run table
+  uint64_t c_app_i64 = 0, c_app_u32 = 0, c_app_u64 = 0, c_app_scan = 0;  // sparkey_log_append workspace
+  int64_t* app_i64 = nullptr;
+  uint32_t* app_u32 = nullptr;
+  uint64_t* app_u64 = nullptr;
+  int64_t* app_scan = nullptr;
+  uint64_t c_app_map = 0;
+  uint32_t* app_map = nullptr;
   uint64_t c_seg_cls_cnt = 0, c_seg_cls_off = 0;
   uint32_t* seg_cls_cnt = nullptr;
   uint64_t* seg_cls_off = nullptr;
@@ -744,6 +752,85 @@ extern "C" {
 
 const char* sparkey_gpu_version(void) { return "sparkey-mi355x 0.1 (gfx950)"; }
 
+// Batched LogWriter.put / delete (LogWriter.java:96-115, UncompressedBlockOutput.java:34-45,
+// LogHeader.java:161-172): records written from d_out on, header84 updated in place.
+int sparkey_log_append(sparkey_plan* pl, uint8_t* header84, const uint8_t* d_kind, const uint8_t* d_keys,
+                       const uint64_t* d_key_off, const uint8_t* d_values, const uint64_t* d_val_off, uint64_t n,
+                       uint8_t* d_out, uint64_t out_cap, uint64_t* bytes_written, void* stream, char* err,
+                       size_t err_len) {
+  if (!pl || !header84 || (n && (!d_kind || !d_keys || !d_key_off || !d_values || !d_val_off || !d_out))) {
+    set_err(err, err_len, "null argument");
+    return SPARKEY_E_ARG;
+  }
+  LogHdr lh;
+  int rc = parse_log_header(header84, kLogHeaderSize, (uint64_t)INT64_MAX, &lh, err, err_len);
+  if (rc) return rc;
+  if (lh.compression_type != 0) {
+    set_err(err, err_len, "compressed logs are not supported");
+    return SPARKEY_E_UNSUPPORTED;
+  }
+  if (bytes_written) *bytes_written = 0;
+  if (n == 0) return SPARKEY_OK;
+  HIP_TRY(hipSetDevice(pl->device));
+  hipStream_t s = stream ? (hipStream_t)stream : pl->own_stream;
+  const uint64_t nblk = (n + 255) / 256;
+  HIP_TRY(grow(&pl->app_i64, pl->c_app_i64, 2 * n + 6 * nblk + 16));
+  HIP_TRY(grow(&pl->app_u32, pl->c_app_u32, n));
+  HIP_TRY(grow(&pl->app_u64, pl->c_app_u64, n + 1));
+  const uint64_t scratch = n / kScanTile + 64;
+  HIP_TRY(grow(&pl->scan_u64, pl->c_su, scratch + 16));
+  HIP_TRY(grow(&pl->app_scan, pl->c_app_scan, scratch + 16));
+  AppendParams A;
+  memset(&A, 0, sizeof(A));
+  A.n = n;
+  A.kind = d_kind;
+  A.keys = d_keys;
+  A.key_off = d_key_off;
+  A.values = d_values;
+  A.val_off = d_val_off;
+  A.max_key_len0 = lh.max_key_len;
+  A.out = d_out;
+  A.keymax = pl->app_i64;
+  A.keymax_pre = pl->app_i64 + n;
+  A.partials = pl->app_i64 + 2 * n;
+  A.sums = pl->app_i64 + 2 * n + 6 * nblk;
+  A.sizes = pl->app_u32;
+  A.off = pl->app_u64;
+  A.total = pl->app_u64 + n;
+  A.scan_u64 = pl->scan_u64;
+  A.scan_i64 = pl->app_scan;
+  // the appended bytes must fit: sizes first, then the write
+  launch_append_sizes(A, s);
+  HIP_TRY(hipGetLastError());
+  int64_t sums[6];
+  uint64_t total = 0;
+  HIP_TRY(hipMemcpyAsync(sums, A.sums, sizeof(sums), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(&total, A.total, sizeof(total), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  if (total > out_cap) {
+    set_err(err, err_len, "output buffer too small: need " + std::to_string(total) + " bytes");
+    return SPARKEY_E_BUFFER;
+  }
+  A.mis = (uint32_t)((uintptr_t)d_out & 15);
+  A.nwords = total ? (total + A.mis + 15) / 16 : 0;
+  HIP_TRY(grow(&pl->app_map, pl->c_app_map, A.nwords + 1));
+  A.map = pl->app_map;
+  launch_append_write(A, s);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(s));
+  // header (LogHeader.put / delete, LogWriter.writeHeader: maxEntriesPerBlock 1, dataEnd = file end)
+  wr64(header84 + 16, (uint64_t)(lh.num_puts + sums[0]));
+  wr64(header84 + 24, (uint64_t)(lh.num_deletes + sums[1]));
+  wr64(header84 + 32, (uint64_t)(lh.data_end + (int64_t)total));
+  wr64(header84 + 40, (uint64_t)std::max<int64_t>(lh.max_key_len, sums[4]));
+  wr64(header84 + 48, (uint64_t)std::max<int64_t>(lh.max_value_len, sums[5]));
+  wr64(header84 + 56, (uint64_t)(lh.delete_size + sums[3]));
+  wr64(header84 + 72, (uint64_t)(lh.put_size + sums[2]));
+  wr32(header84 + 80, 1u);
+  if (bytes_written) *bytes_written = total;
+  return SPARKEY_OK;
+}
+
 // Batched IndexHash.get (IndexHash.java:398-452): IndexHash.open's checks (IndexHash.java:72-80,
 // 115-121, 352-356), then one lane per query.
 int sparkey_get_batch(sparkey_plan* pl, const uint8_t* d_log, uint64_t log_len, const uint8_t* d_index,
@@ -907,7 +994,8 @@ void sparkey_plan_destroy(sparkey_plan* pl) {
                   pl->bcount, pl->bcursor, pl->boff, pl->bfun, pl->bpre, pl->bfun_total, pl->carry, pl->pairs,
                   pl->parts, pl->scan_u64, pl->scan_mp, pl->desc, pl->p1_hist, pl->p1_off, pl->d_status, pl->dbg, pl->wcount, pl->woff, pl->small,
                   pl->eseg, pl->seg_cnt, pl->seg_off, pl->seg_mark, pl->seg_start,
-                  pl->seg_cls_cnt, pl->seg_cls_off, pl->p2tab};
+                  pl->seg_cls_cnt, pl->seg_cls_off, pl->p2tab,
+                  pl->app_i64, pl->app_u32, pl->app_u64, pl->app_scan, pl->app_map};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (pl->h_status) (void)hipHostFree(pl->h_status);

@@ -140,6 +140,8 @@ _SIGS = {
     "sparkey_shard_stats": ([_vp, ctypes.c_uint64, ctypes.c_int32, _vp, _i64p] + _E, ctypes.c_int),
     "sparkey_index_header": ([_vp, ctypes.POINTER(BuildOpts), ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
                               ctypes.c_int64, ctypes.c_int64, _vp] + _E, ctypes.c_int),
+    "sparkey_log_append": ([_vp, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_uint64, _vp, ctypes.c_uint64, _u64p, _vp]
+                           + _E, ctypes.c_int),
     "sparkey_get_batch": ([_vp, _vp, ctypes.c_uint64, _vp, ctypes.c_uint64, _vp, _vp, ctypes.c_uint64, _vp, _vp, _vp]
                           + _E, ctypes.c_int),
 }
@@ -257,6 +259,21 @@ class Plan:
         if rc != OK:
             raise_for(rc, err.value.decode(errors="replace"))
         return stats
+
+    def log_append(self, header84: bytearray, d_kind: int, d_keys: int, d_key_off: int, d_values: int,
+                   d_val_off: int, n: int, d_out: int, out_cap: int, stream: int = 0) -> int:
+        """Batched LogWriter.put / delete on device buffers (sparkey_log_append); header84 is updated in
+        place; returns the bytes written."""
+        hb = (ctypes.c_uint8 * 84).from_buffer(header84)
+        written = ctypes.c_uint64()
+        err = ctypes.create_string_buffer(512)
+        rc = _lib.sparkey_log_append(self._h, hb, ctypes.c_void_p(d_kind), ctypes.c_void_p(d_keys),
+                                     ctypes.c_void_p(d_key_off), ctypes.c_void_p(d_values), ctypes.c_void_p(d_val_off),
+                                     n, ctypes.c_void_p(d_out), out_cap, ctypes.byref(written),
+                                     ctypes.c_void_p(stream), err, 512)
+        if rc != OK:
+            raise_for(rc, err.value.decode(errors="replace"))
+        return int(written.value)
 
     def get_batch(self, d_log: int, log_len: int, d_index: int, index_len: int, d_keys: int, d_key_off: int, n: int,
                   d_value_pos: int, d_value_len: int, stream: int = 0) -> None:

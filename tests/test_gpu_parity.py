@@ -385,3 +385,38 @@ def test_get_batch_c1_and_errors(native):
         _reader(other, spi).get(b"key_1")          # "Log file did not match index file"
     with pytest.raises(RuntimeError):
         _reader(log, spi[:-4]).get(b"key_1")       # "Corrupt index file - incorrect size"
+
+
+# --- batched LogWriter.put / delete on the GPU (sparkey_log_append) against the oracle's LogBuilder ---
+def test_log_append_matches_log_writer(native):
+    from sparkey.gpu_log import DELETE, PUT, GpuLogAppender, new_log_header
+    rng = np.random.default_rng(17)
+    ops = []
+    for i in range(30000):
+        r = rng.random()
+        kl = int(rng.choice([0, 1, 5, 16, 126, 127, 128, 300]))
+        key = bytes(rng.integers(0, 256, kl, dtype=np.uint8))
+        if r < 0.2:
+            ops.append((DELETE, key, None))  # longer than maxKeyLen so far: dropped, as LogWriter.delete does
+        else:
+            vl = int(rng.choice([0, 1, 100, 127, 128, 16383, 16384]))
+            ops.append((PUT, key, bytes(rng.integers(0, 256, vl, dtype=np.uint8))))
+    want = make_log(ops=[("put" if k == PUT else "del", key, v) for k, key, v in ops], file_id=0x51)
+    app = GpuLogAppender()
+    header = new_log_header(0x51)
+    body = app.append(header, ops[:12345]) + app.append(header, ops[12345:])
+    app.close()
+    assert bytes(header) + body == want
+
+
+def test_log_append_then_build(native):
+    """A log written on the GPU builds to the same index as the reference writer's log."""
+    from sparkey.gpu_log import PUT, GpuLogAppender, new_log_header
+    ops = [(PUT, b"key_%d" % i, b"value_%d" % i) for i in range(1000)]
+    app = GpuLogAppender()
+    header = new_log_header(0x0C1C1C1C, 1024)
+    body = app.append(header, ops)  # updates header in place
+    log = bytes(header) + body
+    app.close()
+    assert log == make_log(key_value_puts(1000, b"key_%d", b"value_%d"), file_id=0x0C1C1C1C, block_size=1024)
+    check(native, log, 1234)
