@@ -28,7 +28,7 @@ def _stale(target, deps):
 def build(force: bool = False, verbose: bool = False) -> str:
     os.makedirs(LIB_DIR, exist_ok=True)
     if force or _stale(LIB, SOURCES + HEADERS + [__file__]):
-        cmd = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
+        cmd = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wl,--no-undefined", "-Wall",
                "-I", os.path.join(ROOT, "include")]
         for s in SOURCES:
             cmd += ["-x", "hip", s]

@@ -281,54 +281,27 @@ __global__ __launch_bounds__(kStatBlock) void k_stats(BuildParams P) {
   }
 }
 
-__device__ __forceinline__ void put_le64(uint8_t* p, uint64_t v) {
-#pragma unroll
-  for (int i = 0; i < 8; i++) p[i] = (uint8_t)(v >> (8 * i));
-}
-
-__global__ __launch_bounds__(256) void k_stats_final(BuildParams P, uint32_t nparts, int sequential) {
-  __shared__ unsigned long long s_sum[256], s_col[256];
-  __shared__ long long s_max[256];
+__global__ __launch_bounds__(1024) void k_stats_final(BuildParams P, uint32_t nparts, int sequential) {
+  __shared__ unsigned long long s_sum[16], s_col[16];
+  __shared__ long long s_max[16];
+  const StatPart* parts = P.parts;
   const int tid = threadIdx.x;
   unsigned long long sum = 0, col = 0;
   long long mx = 0;
-  for (uint32_t i = tid; i < nparts; i += 256) {
-    const StatPart sp = P.parts[i];
+  for (uint32_t i = tid; i < nparts; i += 1024) {
+    const StatPart sp = parts[i];
     sum += sp.sum_disp;
     col += sp.collisions;
     mx = max(mx, sp.max_disp);
   }
-  s_sum[tid] = sum; s_col[tid] = col; s_max[tid] = mx;
+  sum = wave_sum_u64(sum);
+  col = wave_sum_u64(col);
+  mx = wave_max_i64(mx);
+  if ((tid & 63) == 0) { s_sum[tid >> 6] = sum; s_col[tid >> 6] = col; s_max[tid >> 6] = mx; }
   __syncthreads();
   if (tid == 0) {
-    sum = s_sum[0]; col = s_col[0]; mx = s_max[0];
-    for (int i = 1; i < 256; i++) { sum += s_sum[i]; col += s_col[i]; mx = max(mx, s_max[i]); }
-    Status* st = P.st;
-    if (P.sharded) {  // partial sums of the rank's slots; the host reduces them and adds the quirk
-      st->max_disp = mx;
-      st->collisions = (long long)col;
-      st->total_disp = (long long)sum;
-      return;
-    }
-    // wrap quirk (IndexHash.java:239-241): slot 0 and slot cap-1 both occupied with equal hashes
-    uint64_t h0, a0, h1, a1;
-    read_slot(P, 0, h0, a0);
-    read_slot(P, P.cap - 1, h1, a1);
-    if (a0 != 0 && a1 != 0 && h0 == h1) col++;
-    long long entries, garbage;
-    if (sequential) { entries = st->num_entries; garbage = st->garbage; }
-    else { entries = (long long)st->n_records; garbage = 0; }
-    st->max_disp = mx;
-    st->collisions = (long long)col;
-    st->total_disp = (long long)sum;
-    st->num_entries = entries;
-    st->garbage = garbage;
-    uint8_t* hdr = P.out;
-    put_le64(hdr + 52, (uint64_t)garbage);
-    put_le64(hdr + 60, (uint64_t)entries);
-    put_le64(hdr + 84, (uint64_t)mx);
-    put_le64(hdr + 96, col);
-    put_le64(hdr + 104, sum);
+    for (int w = 1; w < 16; w++) { s_sum[0] += s_sum[w]; s_col[0] += s_col[w]; s_max[0] = max(s_max[0], s_max[w]); }
+    finish_stats(P, s_sum[0], s_col[0], s_max[0], sequential);
   }
 }
 
@@ -377,7 +350,7 @@ void launch_verify(const BuildParams& P, hipStream_t s, StageTimer* tm) {
 void launch_stats(const BuildParams& P, hipStream_t s, int sequential, StageTimer* tm) {
   const uint64_t nparts = (P.slot_hi - P.slot_lo + kStatSlotsPerBlock - 1) / kStatSlotsPerBlock;
   if (nparts) hipLaunchKernelGGL(k_stats, dim3((unsigned)nparts), dim3(kStatBlock), 0, s, P);
-  hipLaunchKernelGGL(k_stats_final, dim3(1), dim3(256), 0, s, P, (uint32_t)nparts, sequential);
+  hipLaunchKernelGGL(k_stats_final, dim3(1), dim3(1024), 0, s, P, (uint32_t)nparts, sequential);
   tm->mark("stats", s);
 }
 

@@ -30,7 +30,7 @@ constexpr int kPartItems = 16;
 constexpr int kPartTile = kPartBlock * kPartItems;
 constexpr int kPart2Block = 1024;                 // k_part2: one workgroup per coarse digit
 constexpr int kPart2MaxBits = 14;                 // fine digit of the partition (<= 16384 buckets)
-constexpr uint32_t kPlaceLdsMax = 1536;           // entries of a bucket staged in LDS
+constexpr uint32_t kPlaceLdsMax = 1024;           // entries of a bucket staged in LDS (load <= 1/1.3: mean 788)
 constexpr uint32_t kMaxPartGroup = 64;
 constexpr int kCandCap = 448;                     // k_frame balanced walk: candidates (and listed records) per wave
 
@@ -137,6 +137,7 @@ struct BuildParams {
   uint64_t* pairs;
   uint64_t pair_cap;
   StatPart* parts;
+  unsigned long long* place_dbg;  // SPARKEY_PLACE_DEBUG: k_place_lds phase cycles summed over blocks
   uint64_t* scan_scratch_u64;
   MaxPlus* scan_scratch_mp;
   // k_frame granules (zeroed before every launch)

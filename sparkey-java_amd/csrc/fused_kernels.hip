@@ -1010,6 +1010,16 @@ __device__ __forceinline__ bool is_put_pair(const Entry& x, const Entry& y) {  /
   return x.hash == y.hash && !(x.addr & kDelBit) && !(y.addr & kDelBit);
 }
 
+// SPARKEY_PLACE_DEBUG: thread 0's clock at the phase boundaries, summed over blocks
+#define PLACE_MARK(i)                                                   \
+  do {                                                                  \
+    if (P.place_dbg && tid == 0) {                                      \
+      const long long now_ = clock64();                                 \
+      P.place_dbg[8 * (uint64_t)blockIdx.x + (i)] = now_ - t_prev_;      \
+      t_prev_ = now_;                                                   \
+    }                                                                   \
+  } while (0)
+
 __global__ __launch_bounds__(kPlaceLdsBlock) void k_place_lds(BuildParams P) {
   __shared__ uint32_t cnt[kBucket];
   __shared__ uint32_t base[kBucket];
@@ -1019,85 +1029,123 @@ __global__ __launch_bounds__(kPlaceLdsBlock) void k_place_lds(BuildParams P) {
   __shared__ uint16_t order[kPlaceLdsMax];
   __shared__ uint64_t sh64[kPlaceLdsBlock / 64 + 1];
   __shared__ int64_t shm[kPlaceLdsBlock / 64 + 1];
-  if (build_aborted(P)) return;
+  long long t_prev_ = P.place_dbg ? clock64() : 0;
+  const long long t_begin_ = t_prev_;
+  // Every value the block reads besides its entries, in one round trip (block-uniform: scalar loads
+  // issued together) rather than one latency per phase.
+  const Status* st = P.st;
+  const unsigned ovf = st->overflow, full = st->full;
+  const unsigned long long nrec = st->n_records, ndel = st->n_deletes, npairs0 = st->n_pairs;
   const uint64_t b = P.b_lo + blockIdx.x;
-  const uint64_t start = b << kBucketShift;
-  const int64_t bsize = (int64_t)min((uint64_t)kBucket, P.cap - start);
   const uint32_t n = P.bcount[b];
   const uint64_t eoff = P.boff[b];
+  const int64_t x = P.carry[b];
+  if (ovf != 0 || nrec > P.max_records) return;  // build_aborted
+  const uint64_t start = b << kBucketShift;
+  const int64_t bsize = (int64_t)min((uint64_t)kBucket, P.cap - start);
   const int tid = threadIdx.x;
   if (n > kPlaceLdsMax) {
     if (tid == 0) atomicOr(&P.st->big_buckets, 1u);
     return;
   }
+  // the entries' loads are in flight while the histogram is cleared
+  constexpr int kPer = kPlaceLdsMax / kPlaceLdsBlock;
+  static_assert(kPlaceLdsMax % kPlaceLdsBlock == 0, "entries per thread");
+  Entry mine[kPer];
+  uint32_t want[kPer];
+#pragma unroll
+  for (int k = 0; k < kPer; k++) {
+    const uint32_t i = tid + k * kPlaceLdsBlock;
+    if (i < n) mine[k] = P.ent2[eoff + i];
+  }
+  PLACE_MARK(0);
   for (int t = tid; t < kBucket; t += kPlaceLdsBlock) { cnt[t] = 0; aux[t] = 0; }
   __syncthreads();
-  for (uint32_t i = tid; i < n; i += kPlaceLdsBlock) {
-    const Entry en = P.ent2[eoff + i];
-    raw[i] = en;
-    atomicAdd(&cnt[fast_mod(en.hash, P.mod) - start], 1u);
+#pragma unroll
+  for (int k = 0; k < kPer; k++) {
+    const uint32_t i = tid + k * kPlaceLdsBlock;
+    if (i < n) {
+      raw[i] = mine[k];
+      want[k] = (uint32_t)(fast_mod(mine[k].hash, P.mod) - start);
+      atomicAdd(&cnt[want[k]], 1u);
+    }
   }
   __syncthreads();
+  PLACE_MARK(1);
   bucket_scan<kPlaceLdsBlock>(cnt, base, M, sh64, shm, nullptr);
-  for (uint32_t i = tid; i < n; i += kPlaceLdsBlock) {
-    const uint32_t w = (uint32_t)(fast_mod(raw[i].hash, P.mod) - start);
-    order[base[w] + atomicAdd((uint32_t*)&aux[w], 1u)] = (uint16_t)i;
+  // a group's members in arbitrary order (LDS cursors); a lone entry goes straight to its place
+#pragma unroll
+  for (int k = 0; k < kPer; k++) {
+    const uint32_t i = tid + k * kPlaceLdsBlock;
+    if (i < n) {
+      const uint32_t w = want[k];
+      order[base[w] + (cnt[w] > 1 ? atomicAdd((uint32_t*)&aux[w], 1u) : 0u)] = (uint16_t)i;
+    }
   }
   __syncthreads();
-  // equal wanted slots: address order; equal hashes -> duplicate-key candidates, appended to the
-  // pair list with one atomic per workgroup (not needed once the exact path is certain: the log
-  // holds DELETEs, or the list overflowed)
-  const bool want_pairs = P.st->n_deletes == 0 && P.st->n_pairs <= P.pair_cap;
+  PLACE_MARK(2);
+  // Equal wanted slots go in address order (the reference's insertion order): each member counts
+  // the members with smaller addresses -- independent LDS reads, one thread per entry -- and
+  // equal-hash PUT pairs become duplicate-key candidates, counted by their earlier member and
+  // appended to the pair list with one atomic per workgroup (not needed once the exact path is
+  // certain: the log holds DELETEs, or the list overflowed; groups above kGroupMax flag it).
+  const bool want_pairs = ndel == 0 && npairs0 <= P.pair_cap;
+  for (int t = tid; t < kBucket; t += kPlaceLdsBlock) aux[t] = -1;  // (the cursors are done with)
+  uint32_t rank[kPer];
   uint32_t npair = 0;
-  for (int q = 0; q < kLdsBins; q++) {
-    const int s = tid * kLdsBins + q;
-    const uint32_t g = cnt[s];
+#pragma unroll
+  for (int k = 0; k < kPer; k++) {
+    const uint32_t i = tid + k * kPlaceLdsBlock;
+    rank[k] = 0;
+    if (i >= n) continue;
+    const uint32_t w = want[k], g = cnt[w];
     if (g < 2) continue;
-    uint16_t* grp = order + base[s];
-    if (g > kGroupMax) {
-      atomicOr(&P.st->dup_overflow, 1u);
-      continue;
+    const uint16_t* grp = order + base[w];
+    const uint64_t ai = mine[k].addr & ~kDelBit;
+    const bool cp = want_pairs && !(mine[k].addr & kDelBit) && g <= kGroupMax;
+    if (g > kGroupMax && grp[0] == i) atomicOr(&P.st->dup_overflow, 1u);
+    uint32_t r = 0;
+    for (uint32_t u = 0; u < g; u++) {
+      const Entry e = raw[grp[u]];
+      const uint64_t aj = e.addr & ~kDelBit;
+      r += aj < ai;
+      npair += cp && aj > ai && e.hash == mine[k].hash && !(e.addr & kDelBit);
     }
-    for (uint32_t x = 1; x < g; x++) {
-      const uint16_t vi = grp[x];
-      const uint64_t va = raw[vi].addr & ~kDelBit;
-      uint32_t y = x;
-      while (y > 0 && va < (raw[grp[y - 1]].addr & ~kDelBit)) { grp[y] = grp[y - 1]; y--; }
-      grp[y] = vi;
-    }
-    if (want_pairs)
-      for (uint32_t x = 0; x < g; x++)
-        for (uint32_t y = x + 1; y < g; y++) npair += is_put_pair(raw[grp[x]], raw[grp[y]]);
+    rank[k] = r;
   }
-  uint64_t pair_total = 0;
-  const uint64_t pair_off = block_excl_sum<kPlaceLdsBlock>(npair, sh64, &pair_total);
-  if (pair_total) {
+  const bool any_pair = __syncthreads_or(npair != 0);
+#pragma unroll
+  for (int k = 0; k < kPer; k++) {
+    const uint32_t i = tid + k * kPlaceLdsBlock;
+    if (i < n && cnt[want[k]] > 1) order[base[want[k]] + rank[k]] = (uint16_t)i;
+  }
+  if (any_pair) {  // (block-uniform)
+    uint64_t pair_total = 0;
+    const uint64_t pair_off = block_excl_sum<kPlaceLdsBlock>(npair, sh64, &pair_total);  // (syncs the block)
     __shared__ unsigned long long pair_base;
     if (tid == 0) pair_base = atomicAdd(&P.st->n_pairs, (unsigned long long)pair_total);
     __syncthreads();
     unsigned long long slotn = pair_base + pair_off;
-    for (int q = 0; q < kLdsBins && npair; q++) {
-      const int s = tid * kLdsBins + q;
-      const uint32_t g = cnt[s];
-      if (g < 2 || g > kGroupMax) continue;
-      const uint16_t* grp = order + base[s];
-      for (uint32_t x = 0; x < g; x++)
-        for (uint32_t y = x + 1; y < g; y++) {
-          const Entry ex = raw[grp[x]], ey = raw[grp[y]];
-          if (!is_put_pair(ex, ey)) continue;
-          if (slotn < P.pair_cap) {
-            P.pairs[2 * slotn] = ex.addr;
-            P.pairs[2 * slotn + 1] = ey.addr;
-          }
-          slotn++;
+#pragma unroll
+    for (int k = 0; k < kPer; k++) {
+      const uint32_t i = tid + k * kPlaceLdsBlock;
+      if (i >= n || !npair) continue;
+      const uint32_t w = want[k], g = cnt[w];
+      if (g < 2 || g > kGroupMax || (mine[k].addr & kDelBit)) continue;
+      const uint16_t* grp = order + base[w];
+      for (uint32_t u = rank[k] + 1; u < g; u++) {  // the later members, in address order
+        const Entry e = raw[grp[u]];
+        if (!is_put_pair(mine[k], e)) continue;
+        if (slotn < P.pair_cap) {
+          P.pairs[2 * slotn] = mine[k].addr;
+          P.pairs[2 * slotn + 1] = e.addr;
         }
+        slotn++;
+      }
     }
   }
-  __syncthreads();
-  if (P.st->full) return;
-  const int64_t x = P.carry[b];
-  for (int t = tid; t < kBucket; t += kPlaceLdsBlock) aux[t] = -1;
-  __syncthreads();
+  PLACE_MARK(3);
+  if (full) return;
   for (int q = 0; q < kLdsBins; q++) {
     const int s = tid * kLdsBins + q;
     const uint32_t g = cnt[s];
@@ -1115,6 +1163,8 @@ __global__ __launch_bounds__(kPlaceLdsBlock) void k_place_lds(BuildParams P) {
     }
   }
   __syncthreads();
+  PLACE_MARK(4);
+  // every slot of [x, bsize) is this bucket's: an own entry or empty (zero)
   for (int64_t t = x + tid; t < bsize; t += kPlaceLdsBlock) {
     const int32_t j = aux[t];
     if (j >= 0) {
@@ -1124,7 +1174,10 @@ __global__ __launch_bounds__(kPlaceLdsBlock) void k_place_lds(BuildParams P) {
       write_slot(P, start + (uint64_t)t, 0, 0);
     }
   }
+  PLACE_MARK(5);
+  if (P.place_dbg && tid == 0) P.place_dbg[8 * (uint64_t)blockIdx.x + 7] = t_prev_ - t_begin_;
 }
+
 
 // ================================================================================================
 // launchers
@@ -1180,6 +1233,7 @@ void launch_place_buckets(const BuildParams& P, hipStream_t s) {
   if (P.b_hi > P.b_lo) hipLaunchKernelGGL(k_place_lds, dim3((unsigned)(P.b_hi - P.b_lo)), dim3(kPlaceLdsBlock), 0, s, P);
   launch_place_global(P, s, 0, 1);  // buckets above kPlaceLdsMax entries (normally none)
 }
+
 
 void launch_place_fast(const BuildParams& P, hipStream_t s, StageTimer* tm) {
   launch_summary_carry(P, s, tm);

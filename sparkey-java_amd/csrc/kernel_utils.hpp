@@ -126,4 +126,42 @@ __device__ __forceinline__ void read_slot(const BuildParams& P, uint64_t slot, u
 }
 
 
+__device__ __forceinline__ void put_le64(uint8_t* p, uint64_t v) {
+#pragma unroll
+  for (int i = 0; i < 8; i++) p[i] = (uint8_t)(v >> (8 * i));
+}
+
+// The end of calculateMaxDisplacement (IndexHash.java:195-245) from the slot sums: the wrap quirk
+// (IndexHash.java:239-241: slot 0 and slot cap-1 both occupied with equal hashes count once more),
+// Status, and the header fields it writes.  Sharded ranks store their partial sums only; the host
+// reduces them and adds the quirk.
+__device__ inline void finish_stats(const BuildParams& P, unsigned long long sum, unsigned long long col, long long mx,
+                                    int sequential) {
+  Status* st = P.st;
+  if (P.sharded) {
+    st->max_disp = mx;
+    st->collisions = (long long)col;
+    st->total_disp = (long long)sum;
+    return;
+  }
+  uint64_t h0, a0, h1, a1;
+  read_slot(P, 0, h0, a0);
+  read_slot(P, P.cap - 1, h1, a1);
+  if (a0 != 0 && a1 != 0 && h0 == h1) col++;
+  long long entries, garbage;
+  if (sequential) { entries = st->num_entries; garbage = st->garbage; }
+  else { entries = (long long)st->n_records; garbage = 0; }
+  st->max_disp = mx;
+  st->collisions = (long long)col;
+  st->total_disp = (long long)sum;
+  st->num_entries = entries;
+  st->garbage = garbage;
+  uint8_t* hdr = P.out;
+  put_le64(hdr + 52, (uint64_t)garbage);
+  put_le64(hdr + 60, (uint64_t)entries);
+  put_le64(hdr + 84, (uint64_t)mx);
+  put_le64(hdr + 96, col);
+  put_le64(hdr + 104, sum);
+}
+
 }  // namespace sk

@@ -245,6 +245,7 @@ struct sparkey_plan {
   uint64_t c_conv = 0, c_exitp = 0, c_qpos = 0, c_tail = 0, c_G = 0, c_cnt = 0, c_off = 0;
   uint64_t c_ent = 0, c_ent2 = 0, c_ent3 = 0;
   uint64_t c_bcount = 0, c_bcursor = 0, c_boff = 0, c_bfun = 0, c_bpre = 0, c_carry = 0;
+  uint64_t c_pdbg = 0;
   uint64_t c_pairs = 0, c_parts = 0, c_su = 0, c_smp = 0, c_bft = 0;
   uint64_t c_desc = 0, c_p1h = 0, c_p1o = 0, c_dbg = 0, c_wcount = 0, c_woff = 0;
   uint64_t c_eseg = 0, c_seg_cnt = 0, c_seg_off = 0, c_seg_mark = 0, c_seg_start = 0, c_p2tab = 0;
@@ -283,6 +284,7 @@ struct sparkey_plan {
   int64_t* carry = nullptr;
   uint64_t* pairs = nullptr;
   StatPart* parts = nullptr;
+  unsigned long long* pdbg = nullptr;
   uint64_t* scan_u64 = nullptr;
   MaxPlus* scan_mp = nullptr;
   unsigned long long* desc = nullptr;  // k_frame exit granules (memset per build)
@@ -538,6 +540,25 @@ static void print_frame_debug(sparkey_plan* pl, const BuildParams& P) {
           sum[4] / n, sum[5] / n, sum[6] / n, mx[3], sum[8] / n, sum[9] / n, sum[10] / n);
 }
 
+static void print_place_debug(const BuildParams& P) {
+  if (!P.place_dbg) return;
+  const uint64_t nb = P.b_hi - P.b_lo;
+  std::vector<unsigned long long> h(8 * nb);
+  if (hipMemcpy(h.data(), P.place_dbg, h.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return;
+  double sum[8] = {0};
+  uint64_t n = 0;
+  for (uint64_t b = 0; b < nb; b++) {
+    if (!h[8 * b + 7]) continue;
+    n++;
+    for (int i = 0; i < 8; i++) sum[i] += (double)h[8 * b + i];
+  }
+  const double d = n ? (double)n : 1.0;
+  fprintf(stderr, "[k_place_lds] blocks=%llu mean cycles: head %.0f load %.0f scan+order %.0f groups %.0f "
+          "place %.0f write %.0f stats %.0f | total %.0f\n",
+          (unsigned long long)n, sum[0] / d, sum[1] / d, sum[2] / d, sum[3] / d, sum[4] / d, sum[5] / d, sum[6] / d,
+          sum[7] / d);
+}
+
 static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t* d_log, uint64_t log_len,
                       uint8_t* d_out, uint64_t index_cap, const sparkey_build_opts* opts, hipStream_t s,
                       sparkey_build_stats* stats_out, char* err, size_t err_len) {
@@ -596,6 +617,11 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
       HIP_TRY(hipMemsetAsync(pl->dbg, 0, 16 * P.nchunks * sizeof(unsigned long long), s));
       P.dbg = pl->dbg;
     }
+    if (getenv("SPARKEY_PLACE_DEBUG")) {
+      HIP_TRY(grow(&pl->pdbg, pl->c_pdbg, 8 * P.nbuckets));
+      HIP_TRY(hipMemsetAsync(pl->pdbg, 0, 8 * P.nbuckets * sizeof(unsigned long long), s));
+      P.place_dbg = pl->pdbg;
+    }
 
     Status init;
     memset(&init, 0, sizeof(init));
@@ -616,6 +642,7 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
     HIP_TRY(hipStreamSynchronize(s));
     HIP_TRY(hipEventElapsedTime(&ms, pl->ev0, pl->ev1));
     print_frame_debug(pl, P);
+    print_place_debug(P);
     if (framing_path == 0 && st.max_wave_count > slab_cap) {  // a wave overflowed its slab
       slab_cap = (uint32_t)std::min<uint64_t>(kPartTile, ((uint64_t)st.max_wave_count + 63) & ~63ull);
       continue;
@@ -992,7 +1019,7 @@ void sparkey_plan_destroy(sparkey_plan* pl) {
   (void)hipSetDevice(pl->device);
   void* bufs[] = {pl->conv, pl->exitp, pl->qpos, pl->tail, pl->G, pl->cnt, pl->off, pl->ent, pl->ent2, pl->ent3,
                   pl->bcount, pl->bcursor, pl->boff, pl->bfun, pl->bpre, pl->bfun_total, pl->carry, pl->pairs,
-                  pl->parts, pl->scan_u64, pl->scan_mp, pl->desc, pl->p1_hist, pl->p1_off, pl->d_status, pl->dbg, pl->wcount, pl->woff, pl->small,
+                  pl->parts, pl->pdbg, pl->scan_u64, pl->scan_mp, pl->desc, pl->p1_hist, pl->p1_off, pl->d_status, pl->dbg, pl->wcount, pl->woff, pl->small,
                   pl->eseg, pl->seg_cnt, pl->seg_off, pl->seg_mark, pl->seg_start,
                   pl->seg_cls_cnt, pl->seg_cls_off, pl->p2tab,
                   pl->app_i64, pl->app_u32, pl->app_u64, pl->app_scan, pl->app_map};
