@@ -29,6 +29,7 @@ constexpr int kPartBlock = 256;                   // radix partition of the entr
 constexpr int kPartItems = 16;
 constexpr int kPartTile = kPartBlock * kPartItems;
 constexpr int kPart2Block = 1024;                 // k_part2: one workgroup per coarse digit
+constexpr int kPart2Items = 8;                    // k_part2: entries per thread per round
 constexpr int kPart2MaxBits = 14;                 // fine digit of the partition (<= 16384 buckets)
 constexpr uint32_t kPlaceLdsMax = 1024;           // entries of a bucket staged in LDS (load <= 1/1.3: mean 788)
 constexpr uint32_t kMaxPartGroup = 64;
@@ -170,6 +171,7 @@ struct BuildParams {
   // uniform-stride framing (k_frame_uniform): uni_n records of uni_rec bytes from fr_entry
   uint64_t uni_n;
   int64_t uni_rec;
+  uint32_t uni_wbytes;  // LDS staging bytes per wave (set by the launcher)
   // framing window: records start at fr_entry (84 for a whole log) and are framed while they start
   // below data_end (the frame end); k_frame chunks are numbered from fr_k0 = fr_entry >> fr_cshift,
   // serial-path chunks (kChunk) from ch_k0 = fr_entry >> kChunkShift

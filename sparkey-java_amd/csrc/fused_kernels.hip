@@ -787,47 +787,67 @@ __device__ __forceinline__ uint32_t digit_of(const BuildParams& P, uint32_t buck
 // anything else flags spec_fail and the build reruns the general framing -- then hashes its key.
 // The entries are dense, in log order (the slab layout of the serial path).
 // ================================================================================================
-__global__ __launch_bounds__(64) void k_frame_uniform(BuildParams P) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  const int lane = threadIdx.x;
-  const uint64_t i0 = (uint64_t)blockIdx.x * 64;
+__global__ __launch_bounds__(1024) void k_frame_uniform(BuildParams P) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];  // per wave uni_wbytes, then hist[256]
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int W = blockDim.x >> 6;
+  uint8_t* buf = lds + (uint32_t)wave * P.uni_wbytes;
+  uint32_t* hist = reinterpret_cast<uint32_t*>(lds + (uint32_t)W * P.uni_wbytes);
+  const bool with_hist = P.p1_hist_ready != 0;  // this workgroup is partition tile blockIdx.x
+  if (with_hist) {
+    for (int t = threadIdx.x; t < 256; t += blockDim.x) hist[t] = 0;
+    __syncthreads();
+  }
   const int64_t R = P.uni_rec;
   const int64_t log_len = (int64_t)P.log_len;
-  const int64_t base = P.fr_entry + (int64_t)i0 * R;
-  const int64_t a0 = base & ~15ll;
-  const int nrec = (int)min((uint64_t)64, P.uni_n - i0);
-  const int64_t want = base + (int64_t)nrec * R + 16 - a0;  // + 16: the 8-byte window reads past a key
-  const int nvec = (int)((want + 15) >> 4);
-  if (a0 + 16ll * nvec <= log_len) {
-    const uint4* src = reinterpret_cast<const uint4*>(P.log + a0);
-    for (int v0 = 0; v0 < nvec; v0 += 64)
-      __builtin_amdgcn_global_load_lds(
-          (const __attribute__((address_space(1))) void*)(src + min(v0 + lane, nvec - 1)),
-          (__attribute__((address_space(3))) void*)(lds + 16u * (uint32_t)v0), 16, 0, 0);
-  } else {
-    for (int v = lane; v < nvec; v += 64) *reinterpret_cast<uint4*>(lds + 16u * v) = load16_guarded(P.log, a0 + 16ll * v, log_len);
-  }
-  __syncthreads();
-  if (blockIdx.x == 0 && lane == 0) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
     P.st->n_records = P.uni_n;
     P.st->exit = P.fr_entry + (int64_t)P.uni_n * R;  // the framed chain's exit
   }
-  if (lane >= nrec) return;
-  const int64_t p = base + (int64_t)lane * R;
-  const uint32_t off = (uint32_t)(p - a0);
-  const uint64_t x = rgn_u64(lds, off);
-  const int32_t klen = (int32_t)(x & 0xff) - 1, vlen = (int32_t)((x >> 8) & 0xff);
-  if ((x & 0x8080ull) != 0 || klen != (int32_t)P.max_key_len || vlen != (int32_t)P.max_value_len) {
-    atomicOr(&P.st->spec_fail, 4u);  // not the uniform log the header describes
-    return;
+  // the workgroup's kPartTile records, 64 per wave per round, each wave staging its own by LDS-DMA
+  for (int r = 0; r < kPartTile / 64 / W; r++) {
+    const uint64_t i0 = (uint64_t)blockIdx.x * kPartTile + (uint64_t)(r * W + wave) * 64;
+    if (i0 >= P.uni_n) break;  // (wave-uniform)
+    const int64_t base = P.fr_entry + (int64_t)i0 * R;
+    const int64_t a0 = base & ~15ll;
+    const int nrec = (int)min((uint64_t)64, P.uni_n - i0);
+    const int64_t want = base + (int64_t)nrec * R + 16 - a0;  // + 16: the 8-byte window reads past a key
+    const int nvec = (int)((want + 15) >> 4);
+    if (a0 + 16ll * nvec <= log_len) {
+      const uint4* src = reinterpret_cast<const uint4*>(P.log + a0);
+      for (int v0 = 0; v0 < nvec; v0 += 64)
+        __builtin_amdgcn_global_load_lds(
+            (const __attribute__((address_space(1))) void*)(src + min(v0 + lane, nvec - 1)),
+            (__attribute__((address_space(3))) void*)(buf + 16u * (uint32_t)v0), 16, 0, 0);
+      __builtin_amdgcn_s_waitcnt(0);  // this wave's LDS-DMA has landed
+    } else {
+      for (int v = lane; v < nvec; v += 64) *reinterpret_cast<uint4*>(buf + 16u * v) = load16_guarded(P.log, a0 + 16ll * v, log_len);
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (lane < nrec) {
+      const int64_t p = base + (int64_t)lane * R;
+      const uint32_t off = (uint32_t)(p - a0);
+      const uint64_t x = rgn_u64(buf, off);
+      const int32_t klen = (int32_t)(x & 0xff) - 1, vlen = (int32_t)((x >> 8) & 0xff);
+      if ((x & 0x8080ull) != 0 || klen != (int32_t)P.max_key_len || vlen != (int32_t)P.max_value_len) {
+        atomicOr(&P.st->spec_fail, 4u);  // not the uniform log the header describes
+      } else {
+        const RgnKey ld{buf, off + 2u};
+        const uint64_t hash = P.hash_size == 8 ? murmur64_ld(ld, klen, (uint32_t)P.seed)
+                                               : (uint64_t)murmur32_ld(ld, klen, (uint32_t)P.seed);
+        Entry en;
+        en.hash = hash;
+        en.addr = (uint64_t)p << P.ebb;
+        P.ent[i0 + lane] = en;
+        if (with_hist) atomicAdd(&hist[digit_of(P, bucket_of(P, hash))], 1u);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();  // every lane is done with the buffer before the next round's DMA
   }
-  const RgnKey ld{lds, off + 2u};
-  const uint64_t hash = P.hash_size == 8 ? murmur64_ld(ld, klen, (uint32_t)P.seed)
-                                         : (uint64_t)murmur32_ld(ld, klen, (uint32_t)P.seed);
-  Entry en;
-  en.hash = hash;
-  en.addr = (uint64_t)p << P.ebb;
-  P.ent[i0 + lane] = en;
+  if (with_hist) {  // k_part1_hist's output for this tile
+    __syncthreads();
+    for (int t = threadIdx.x; t < 256; t += blockDim.x) P.p1_hist[(uint64_t)t * P.p1_tiles + blockIdx.x] = hist[t];
+  }
 }
 
 // ================================================================================================
@@ -879,10 +899,18 @@ __global__ __launch_bounds__(kPartBlock) void k_part1_hist(BuildParams P) {
   const uint64_t g0 = (uint64_t)blockIdx.x * P.part_group;
   hist[threadIdx.x] = 0;
   const uint32_t n = load_tile(P, T, g0);
-  for (uint32_t i = threadIdx.x; i < n; i += kPartBlock) {
-    const Entry& en = tile_entry(P, T, g0, i);
-    if (P.skip_del && (en.addr & kDelBit)) continue;  // exact path: DELETEs stay out of the placement
-    atomicAdd(&hist[digit_of(P, bucket_of(P, en.hash))], 1u);
+  // every load of the tile in flight at once, then the histogram
+  Entry v[kPartItems];
+#pragma unroll
+  for (int i = 0; i < kPartItems; i++) {
+    const uint32_t idx = (uint32_t)i * kPartBlock + threadIdx.x;
+    if (idx < n) v[i] = tile_entry(P, T, g0, idx);
+  }
+#pragma unroll
+  for (int i = 0; i < kPartItems; i++) {
+    const uint32_t idx = (uint32_t)i * kPartBlock + threadIdx.x;
+    if (idx >= n || (P.skip_del && (v[i].addr & kDelBit))) continue;  // exact path: DELETEs stay out
+    atomicAdd(&hist[digit_of(P, bucket_of(P, v[i].hash))], 1u);
   }
   __syncthreads();
   P.p1_hist[(uint64_t)threadIdx.x * P.p1_tiles + blockIdx.x] = hist[threadIdx.x];  // digit-major
@@ -966,9 +994,22 @@ __global__ __launch_bounds__(kPart2Block) void k_part2(BuildParams P) {
   const int tid = threadIdx.x;
   for (uint32_t b = tid; b < nbins; b += kPart2Block) hist[b] = 0;
   __syncthreads();
+  // (kPart2Items loads per thread in flight: one workgroup per CU needs the memory-level parallelism)
   for (uint32_t q = 0; q < nseg; q++) {
     const uint64_t a = seg ? seg[2 * q] : lo, z = seg ? seg[2 * q + 1] : hi;
-    for (uint64_t i = a + tid; i < z; i += kPart2Block) atomicAdd(&hist[bucket_of(P, P.ent3[i].hash) - b0], 1u);
+    for (uint64_t i0 = a; i0 < z; i0 += (uint64_t)kPart2Block * kPart2Items) {
+      uint64_t h[kPart2Items];
+#pragma unroll
+      for (int k = 0; k < kPart2Items; k++) {
+        const uint64_t i = i0 + (uint64_t)k * kPart2Block + tid;
+        if (i < z) h[k] = P.ent3[i].hash;
+      }
+#pragma unroll
+      for (int k = 0; k < kPart2Items; k++) {
+        const uint64_t i = i0 + (uint64_t)k * kPart2Block + tid;
+        if (i < z) atomicAdd(&hist[bucket_of(P, h[k]) - b0], 1u);
+      }
+    }
   }
   __syncthreads();
   // exclusive scan of the bins (per consecutive bins per thread)
@@ -994,10 +1035,18 @@ __global__ __launch_bounds__(kPart2Block) void k_part2(BuildParams P) {
   __syncthreads();
   for (uint32_t q = 0; q < nseg; q++) {
     const uint64_t a = seg ? seg[2 * q] : lo, z = seg ? seg[2 * q + 1] : hi;
-    for (uint64_t i = a + tid; i < z; i += kPart2Block) {
-      const Entry en = P.ent3[i];
-      const uint32_t b = bucket_of(P, en.hash) - b0;
-      P.ent2[lo + atomicAdd(&cur[b], 1u)] = en;
+    for (uint64_t i0 = a; i0 < z; i0 += (uint64_t)kPart2Block * kPart2Items) {
+      Entry v[kPart2Items];
+#pragma unroll
+      for (int k = 0; k < kPart2Items; k++) {
+        const uint64_t i = i0 + (uint64_t)k * kPart2Block + tid;
+        if (i < z) v[k] = P.ent3[i];
+      }
+#pragma unroll
+      for (int k = 0; k < kPart2Items; k++) {
+        const uint64_t i = i0 + (uint64_t)k * kPart2Block + tid;
+        if (i < z) P.ent2[lo + atomicAdd(&cur[bucket_of(P, v[k].hash) - b0], 1u)] = v[k];
+      }
     }
   }
 }
@@ -1194,11 +1243,22 @@ void launch_frame_fused(const BuildParams& P, hipStream_t s, StageTimer* tm) {
                                             P.scan_scratch_u64, s);
 }
 
+// Waves per workgroup: as many (up to 16) as fit their staging buffers in 150 KB of LDS.
+int frame_uniform_waves(int64_t rec) {
+  const int64_t wbytes = (64 * rec + 32 + 1023) & ~1023ll;
+  int w = 16;
+  while (w > 1 && w * wbytes + 1024 > 150 * 1024) w >>= 1;
+  return w;
+}
+
 void launch_frame_uniform(const BuildParams& P, hipStream_t s, StageTimer* tm) {
   if (P.uni_n == 0) return;
-  const uint64_t nblk = (P.uni_n + 63) / 64;
-  const size_t lds = (size_t)((64 * P.uni_rec + 32 + 1023) & ~1023ll);
-  hipLaunchKernelGGL(k_frame_uniform, dim3((unsigned)nblk), dim3(64), lds, s, P);
+  BuildParams Q = P;
+  const int W = frame_uniform_waves(P.uni_rec);
+  Q.uni_wbytes = (uint32_t)((64 * P.uni_rec + 32 + 1023) & ~1023ll);
+  const uint64_t nblk = (P.uni_n + kPartTile - 1) / kPartTile;
+  const size_t lds = (size_t)W * Q.uni_wbytes + 1024;
+  hipLaunchKernelGGL(k_frame_uniform, dim3((unsigned)nblk), dim3(64 * W), lds, s, Q);
   tm->mark("frame", s);
 }
 

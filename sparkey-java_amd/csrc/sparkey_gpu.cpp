@@ -630,7 +630,8 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
     pl->timer.begin(s);
     HIP_TRY(hipMemcpyAsync(d_out, hdr, kIndexHeaderSize, hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemcpyAsync(pl->d_status, &init, sizeof(Status), hipMemcpyHostToDevice, s));
-    P.p1_hist_ready = 0;  // (a framing kernel filling it with global atomics measured slower)
+    // k_frame_uniform's workgroups are the partition tiles: it leaves k_part1_hist's histogram
+    P.p1_hist_ready = framing_path == 2 && P.slab_cap == (uint32_t)kPartTile && P.part_group == 1 ? 1 : 0;
     rc = launch_framing(pl, P, framing_path, s, err, err_len);
     if (rc) return rc;
     launch_partition(P, s, &pl->timer);
@@ -673,6 +674,7 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
   if (st.n_deletes > 0 || st.dup || st.dup_overflow || st.full || st.n_pairs > P.pair_cap) {
     const bool serial = st.full || getenv("SPARKEY_EXACT_SERIAL") != nullptr;
     placement_path = serial ? 1 : 2;
+    P.p1_hist_ready = 0;  // the exact path's partitions (DELETEs left out) count their own digits
     float ms2 = 0.f;
     HIP_TRY(hipEventRecord(pl->ev0, s));
     if (serial) {
