@@ -918,19 +918,23 @@ __global__ __launch_bounds__(kPartBlock) void k_part1_hist(BuildParams P) {
 
 __global__ __launch_bounds__(kPartBlock) void k_part1_scatter(BuildParams P) {
   __shared__ Entry stage[kPartTile];
+  __shared__ uint8_t sdig[kPartTile];  // digit of each staged entry
   __shared__ uint32_t lbase[256];
   __shared__ uint32_t cursor[256];
+  __shared__ int64_t gdst[256];  // global offset of the digit's run minus its LDS start
   __shared__ uint64_t sh64[kPartBlock / 64 + 1];
   __shared__ SlabTile T;
   if (build_aborted(P)) return;  // the host grows the workspace and redoes the build
   const uint64_t g0 = (uint64_t)blockIdx.x * P.part_group;
   const int tid = threadIdx.x;
   const uint32_t h = P.p1_hist[(uint64_t)tid * P.p1_tiles + blockIdx.x];
-  lbase[tid] = (uint32_t)block_excl_sum<kPartBlock>(h, sh64, &sh64[kPartBlock / 64]);
+  const uint64_t goff = P.p1_off[(uint64_t)tid * P.p1_tiles + blockIdx.x];
+  const uint32_t lb = (uint32_t)block_excl_sum<kPartBlock>(h, sh64, &sh64[kPartBlock / 64]);
+  lbase[tid] = lb;
+  gdst[tid] = (int64_t)goff - (int64_t)lb;
   cursor[tid] = 0;
   const uint32_t n = load_tile(P, T, g0);
   Entry v[kPartItems];
-  uint32_t d[kPartItems];
 #pragma unroll
   for (int i = 0; i < kPartItems; i++) {
     const uint32_t idx = (uint32_t)i * kPartBlock + tid;
@@ -939,20 +943,20 @@ __global__ __launch_bounds__(kPartBlock) void k_part1_scatter(BuildParams P) {
 #pragma unroll
   for (int i = 0; i < kPartItems; i++) {
     const uint32_t idx = (uint32_t)i * kPartBlock + tid;
-    d[i] = 0xffffffffu;
     if (idx < n && !(P.skip_del && (v[i].addr & kDelBit))) {
-      d[i] = digit_of(P, bucket_of(P, v[i].hash));
-      stage[lbase[d[i]] + atomicAdd(&cursor[d[i]], 1u)] = v[i];
+      const uint32_t d = digit_of(P, bucket_of(P, v[i].hash));
+      const uint32_t pos = lbase[d] + atomicAdd(&cursor[d], 1u);
+      stage[pos] = v[i];
+      sdig[pos] = (uint8_t)d;
     }
   }
   __syncthreads();
   const uint32_t nkeep = (uint32_t)sh64[kPartBlock / 64];  // the tile's entries in the placement
   // coalesced write-out: LDS position i -> global offset of its digit run
-  for (uint32_t i = tid; i < nkeep; i += kPartBlock) {
-    const Entry en = stage[i];
-    const uint32_t dd = digit_of(P, bucket_of(P, en.hash));
-    const uint64_t dst = P.p1_off[(uint64_t)dd * P.p1_tiles + blockIdx.x] + (i - lbase[dd]);
-    P.ent3[dst] = en;
+#pragma unroll
+  for (int k = 0; k < kPartItems; k++) {
+    const uint32_t i = (uint32_t)k * kPartBlock + tid;
+    if (i < nkeep) P.ent3[gdst[sdig[i]] + (int64_t)i] = stage[i];
   }
 }
 
