@@ -55,6 +55,8 @@ struct alignas(16) SpillEntry {
   uint64_t pad;
 };
 
+constexpr unsigned kSpecRegionFull = 8u;  // Status.spec_fail: a digit region of ent3 overflowed
+
 struct StatPart {
   unsigned long long sum_disp;
   unsigned long long collisions;
@@ -171,7 +173,11 @@ struct BuildParams {
   // uniform-stride framing (k_frame_uniform): uni_n records of uni_rec bytes from fr_entry
   uint64_t uni_n;
   int64_t uni_rec;
-  uint32_t uni_wbytes;  // LDS staging bytes per wave (set by the launcher)
+  uint32_t uni_wbytes;    // LDS staging bytes per wave (set by the launcher)
+  uint32_t uni_hist_off;  // LDS offset of the digit counts (set by the launcher)
+  // k_frame_uniform as partition pass 1: digit d's entries at ent3[d * p1_region, + p1_fill[d])
+  uint64_t p1_region;   // 0 = off
+  uint32_t* p1_fill;
   // framing window: records start at fr_entry (84 for a whole log) and are framed while they start
   // below data_end (the frame end); k_frame chunks are numbered from fr_k0 = fr_entry >> fr_cshift,
   // serial-path chunks (kChunk) from ch_k0 = fr_entry >> kChunkShift

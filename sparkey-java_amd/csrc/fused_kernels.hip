@@ -17,6 +17,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "build_kernels.hpp"
 #include "device_common.hpp"
 #include "kernel_utils.hpp"
@@ -787,15 +789,24 @@ __device__ __forceinline__ uint32_t digit_of(const BuildParams& P, uint32_t buck
 // anything else flags spec_fail and the build reruns the general framing -- then hashes its key.
 // The entries are dense, in log order (the slab layout of the serial path).
 // ================================================================================================
-__global__ __launch_bounds__(1024) void k_frame_uniform(BuildParams P) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];  // per wave uni_wbytes, then hist[256]
+template <int W>
+__global__ __launch_bounds__(64 * W) void k_frame_uniform(BuildParams P) {
+  // A workgroup frames kSub partition tiles (kSub * kPartTile records), kRounds rounds of 64 records
+  // per wave, each wave staging its own records by LDS-DMA.
+  constexpr int kSub = 1;  // (2 or 4 -- longer runs per region -- measured slower: registers/scratch)
+  constexpr int kTileRounds = kPartTile / 64 / W;
+  constexpr int kRounds = kSub * kTileRounds;
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];  // wave buffers | hist[kSub][256] rbase[256]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int W = blockDim.x >> 6;
   uint8_t* buf = lds + (uint32_t)wave * P.uni_wbytes;
-  uint32_t* hist = reinterpret_cast<uint32_t*>(lds + (uint32_t)W * P.uni_wbytes);
-  const bool with_hist = P.p1_hist_ready != 0;  // this workgroup is partition tile blockIdx.x
+  uint32_t* hist = reinterpret_cast<uint32_t*>(lds + P.uni_hist_off);  // per tile
+  uint32_t* rbase = hist + kSub * 256;
+  // to_regions: the entries go straight to their digit regions of ent3 (partition pass 1 done here);
+  // else with p1_hist_ready each tile's digit counts are k_part1_hist's output
+  const bool to_regions = P.p1_region != 0;
+  const bool with_hist = to_regions || P.p1_hist_ready != 0;
   if (with_hist) {
-    for (int t = threadIdx.x; t < 256; t += blockDim.x) hist[t] = 0;
+    for (int t = threadIdx.x; t < kSub * 256; t += 64 * W) hist[t] = 0;
     __syncthreads();
   }
   const int64_t R = P.uni_rec;
@@ -804,10 +815,14 @@ __global__ __launch_bounds__(1024) void k_frame_uniform(BuildParams P) {
     P.st->n_records = P.uni_n;
     P.st->exit = P.fr_entry + (int64_t)P.uni_n * R;  // the framed chain's exit
   }
-  // the workgroup's kPartTile records, 64 per wave per round, each wave staging its own by LDS-DMA
-  for (int r = 0; r < kPartTile / 64 / W; r++) {
-    const uint64_t i0 = (uint64_t)blockIdx.x * kPartTile + (uint64_t)(r * W + wave) * 64;
-    if (i0 >= P.uni_n) break;  // (wave-uniform)
+  const uint64_t blk0 = (uint64_t)blockIdx.x * (kSub * kPartTile);
+  uint64_t hsh[kRounds];  // (the address follows from the round: record blk0 + (r * W + wave) * 64 + lane)
+  uint32_t dr[kRounds];   // digit << 16 | rank within its tile's digit run, ~0 = none
+#pragma unroll
+  for (int r = 0; r < kRounds; r++) {
+    dr[r] = ~0u;
+    const uint64_t i0 = blk0 + (uint64_t)(r * W + wave) * 64;
+    if (i0 >= P.uni_n) continue;  // (wave-uniform)
     const int64_t base = P.fr_entry + (int64_t)i0 * R;
     const int64_t a0 = base & ~15ll;
     const int nrec = (int)min((uint64_t)64, P.uni_n - i0);
@@ -835,18 +850,88 @@ __global__ __launch_bounds__(1024) void k_frame_uniform(BuildParams P) {
         const RgnKey ld{buf, off + 2u};
         const uint64_t hash = P.hash_size == 8 ? murmur64_ld(ld, klen, (uint32_t)P.seed)
                                                : (uint64_t)murmur32_ld(ld, klen, (uint32_t)P.seed);
-        Entry en;
-        en.hash = hash;
-        en.addr = (uint64_t)p << P.ebb;
-        P.ent[i0 + lane] = en;
-        if (with_hist) atomicAdd(&hist[digit_of(P, bucket_of(P, hash))], 1u);
+        hsh[r] = hash;
+        if (!to_regions) {
+          Entry en;
+          en.hash = hash;
+          en.addr = (uint64_t)p << P.ebb;
+          P.ent[i0 + lane] = en;
+        }
+        if (with_hist) {
+          const uint32_t d = digit_of(P, bucket_of(P, hash));
+          const uint32_t rank = atomicAdd(&hist[(r / kTileRounds) * 256 + d], 1u);
+          dr[r] = (d << 16) | rank;
+        }
       }
     }
     __builtin_amdgcn_wave_barrier();  // every lane is done with the buffer before the next round's DMA
   }
-  if (with_hist) {  // k_part1_hist's output for this tile
+  if (!with_hist) return;
+  __syncthreads();
+  if (!to_regions) {  // k_part1_hist's output for these tiles
+    for (int t = threadIdx.x; t < kSub * 256; t += 64 * W) {
+      const uint64_t tile = (uint64_t)blockIdx.x * kSub + (t >> 8);
+      if (tile < P.p1_tiles) P.p1_hist[(uint64_t)(t & 255) * P.p1_tiles + tile] = hist[t];
+    }
+    return;
+  }
+  // One run per digit region for the workgroup's kSub tiles together (one atomic per non-empty
+  // digit; runs kSub times longer than a tile's, so fewer partial lines at the run ends), then per
+  // tile: its entries grouped by digit in LDS (the staging buffers are free now), each sub-run
+  // written coalesced.
+  Entry* stage = reinterpret_cast<Entry*>(lds);                      // kPartTile entries
+  uint8_t* sdig = lds + kPartTile * sizeof(Entry);                    // digit of each staged entry
+  uint32_t* lbase = reinterpret_cast<uint32_t*>(sdig + kPartTile);   // tile-local run starts
+  __shared__ uint32_t wsum[4];
+  if (threadIdx.x < 256) {
+    const int d = threadIdx.x;
+    uint32_t c = 0;
+#pragma unroll
+    for (int t = 0; t < kSub; t++) c += hist[t * 256 + d];
+    const uint32_t b0 = c ? atomicAdd(&P.p1_fill[d], c) : 0u;
+    if ((uint64_t)b0 + c > P.p1_region) atomicOr(&P.st->spec_fail, kSpecRegionFull);
+    rbase[d] = b0;
+  }
+#pragma unroll
+  for (int t = 0; t < kSub; t++) {
+    uint32_t c = 0, incl = 0;
+    __syncthreads();  // (rbase; the previous tile's write-out is done with stage and rbase)
+    if (t > 0 && threadIdx.x < 256) rbase[threadIdx.x] += hist[(t - 1) * 256 + threadIdx.x];  // this tile's sub-run
+    if (threadIdx.x < 256) {  // waves 0-3: exclusive scan of the tile's 256 digit counts
+      c = hist[t * 256 + threadIdx.x];
+      incl = c;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t v = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += v;
+      }
+      if (lane == 63) wsum[wave] = incl;
+    }
     __syncthreads();
-    for (int t = threadIdx.x; t < 256; t += blockDim.x) P.p1_hist[(uint64_t)t * P.p1_tiles + blockIdx.x] = hist[t];
+    if (threadIdx.x < 256) {
+      uint32_t off = 0;
+      for (int w = 0; w < wave; w++) off += wsum[w];
+      lbase[threadIdx.x] = off + incl - c;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = t * kTileRounds; r < (t + 1) * kTileRounds; r++) {
+      if (dr[r] == ~0u) continue;
+      const uint32_t d = dr[r] >> 16;
+      const uint32_t i = lbase[d] + (dr[r] & 0xffffu);
+      Entry en;
+      en.hash = hsh[r];
+      en.addr = (uint64_t)(P.fr_entry + (int64_t)(blk0 + (uint64_t)(r * W + wave) * 64 + lane) * R) << P.ebb;
+      stage[i] = en;
+      sdig[i] = (uint8_t)d;
+    }
+    __syncthreads();
+    const uint32_t ntile = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    for (uint32_t i = threadIdx.x; i < ntile; i += 64 * W) {
+      const uint32_t d = sdig[i];
+      const uint64_t pos = (uint64_t)rbase[d] + (i - lbase[d]);
+      if (pos < P.p1_region) P.ent3[(uint64_t)d * P.p1_region + pos] = stage[i];
+    }
   }
 }
 
@@ -987,6 +1072,9 @@ __global__ __launch_bounds__(kPart2Block) void k_part2(BuildParams P) {
     hi = P.p2_out[k + 1];
     seg = P.p2_seg + 2ull * k * P.p2_nsrc;
     nseg = P.p2_nsrc;
+  } else if (P.p1_region) {  // k_frame_uniform filled the digit's region of ent3
+    lo = (uint64_t)dpart * P.p1_region;
+    hi = lo + min((uint64_t)P.p1_fill[dpart], P.p1_region);
   } else {
     lo = P.p1_off[(uint64_t)dpart * P.p1_tiles];
     hi = (dpart + 1 < 256) ? P.p1_off[(uint64_t)(dpart + 1) * P.p1_tiles] : P.p1_off_total[0];
@@ -1248,21 +1336,26 @@ void launch_frame_fused(const BuildParams& P, hipStream_t s, StageTimer* tm) {
 }
 
 // Waves per workgroup: as many (up to 16) as fit their staging buffers in 150 KB of LDS.
-int frame_uniform_waves(int64_t rec) {
+int frame_uniform_waves(int64_t rec) {  // (rec <= 256: at least 8 waves fit)
   const int64_t wbytes = (64 * rec + 32 + 1023) & ~1023ll;
-  int w = 16;
-  while (w > 1 && w * wbytes + 1024 > 150 * 1024) w >>= 1;
-  return w;
+  return 16 * wbytes + 2048 <= 150 * 1024 ? 16 : 8;
 }
 
 void launch_frame_uniform(const BuildParams& P, hipStream_t s, StageTimer* tm) {
   if (P.uni_n == 0) return;
   BuildParams Q = P;
-  const int W = frame_uniform_waves(P.uni_rec);
+  int W = frame_uniform_waves(P.uni_rec);
+  if (const char* e = getenv("SPARKEY_FRAME_W")) W = atoi(e) == 8 ? 8 : W;  // (measurements)
   Q.uni_wbytes = (uint32_t)((64 * P.uni_rec + 32 + 1023) & ~1023ll);
-  const uint64_t nblk = (P.uni_n + kPartTile - 1) / kPartTile;
-  const size_t lds = (size_t)W * Q.uni_wbytes + 1024;
-  hipLaunchKernelGGL(k_frame_uniform, dim3((unsigned)nblk), dim3(64 * W), lds, s, Q);
+  const uint64_t per = kPartTile;  // records per workgroup
+  const uint64_t nblk = (P.uni_n + per - 1) / per;
+  // the wave buffers, then the tile regrouped by digit in the same space (entries, digits, run
+  // starts), and hist + rbase after either
+  const size_t body = std::max<size_t>((size_t)W * Q.uni_wbytes, (size_t)kPartTile * (sizeof(Entry) + 1) + 1024);
+  const size_t lds = body + 2048;
+  Q.uni_hist_off = (uint32_t)body;
+  if (W == 16) hipLaunchKernelGGL(k_frame_uniform<16>, dim3((unsigned)nblk), dim3(64 * 16), lds, s, Q);
+  else hipLaunchKernelGGL(k_frame_uniform<8>, dim3((unsigned)nblk), dim3(64 * 8), lds, s, Q);
   tm->mark("frame", s);
 }
 
@@ -1288,7 +1381,7 @@ void launch_partition2(const BuildParams& P, hipStream_t s, StageTimer* tm) {
 }
 
 void launch_partition(const BuildParams& P, hipStream_t s, StageTimer* tm) {
-  launch_partition1(P, s);
+  if (!P.p1_region) launch_partition1(P, s);
   hipLaunchKernelGGL(k_part2, dim3(256), dim3(kPart2Block), (size_t)(2u * P.bpp) * sizeof(uint32_t), s, P);
   tm->mark("partition", s);
 }

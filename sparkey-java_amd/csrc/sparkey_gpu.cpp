@@ -245,7 +245,7 @@ struct sparkey_plan {
   uint64_t c_conv = 0, c_exitp = 0, c_qpos = 0, c_tail = 0, c_G = 0, c_cnt = 0, c_off = 0;
   uint64_t c_ent = 0, c_ent2 = 0, c_ent3 = 0;
   uint64_t c_bcount = 0, c_bcursor = 0, c_boff = 0, c_bfun = 0, c_bpre = 0, c_carry = 0;
-  uint64_t c_pdbg = 0;
+  uint64_t c_pdbg = 0, c_p1_fill = 0;
   uint64_t c_pairs = 0, c_parts = 0, c_su = 0, c_smp = 0, c_bft = 0;
   uint64_t c_desc = 0, c_p1h = 0, c_p1o = 0, c_dbg = 0, c_wcount = 0, c_woff = 0;
   uint64_t c_eseg = 0, c_seg_cnt = 0, c_seg_off = 0, c_seg_mark = 0, c_seg_start = 0, c_p2tab = 0;
@@ -285,6 +285,7 @@ struct sparkey_plan {
   uint64_t* pairs = nullptr;
   StatPart* parts = nullptr;
   unsigned long long* pdbg = nullptr;
+  uint32_t* p1_fill = nullptr;
   uint64_t* scan_u64 = nullptr;
   MaxPlus* scan_mp = nullptr;
   unsigned long long* desc = nullptr;  // k_frame exit granules (memset per build)
@@ -609,7 +610,8 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
   // mean per wave + 32); a wave that holds more grows the slabs and the build is redone
   uint32_t slab_cap = (uint32_t)std::min<uint64_t>(
       kPartTile, std::max<uint64_t>(64, 2 * ((nrec + std::max<uint64_t>(nwaves, 1) - 1) / std::max<uint64_t>(nwaves, 1)) + 32));
-  for (int attempt = 0; attempt < 4; attempt++) {
+  bool use_regions = getenv("SPARKEY_NO_REGIONS") == nullptr;
+  for (int attempt = 0; attempt < 5; attempt++) {
     rc = reserve_for_framing(pl, P, framing_path, nrec, slab_cap, err, err_len);
     if (rc) return rc;
     if (getenv("SPARKEY_FRAME_DEBUG")) {
@@ -630,8 +632,26 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
     pl->timer.begin(s);
     HIP_TRY(hipMemcpyAsync(d_out, hdr, kIndexHeaderSize, hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemcpyAsync(pl->d_status, &init, sizeof(Status), hipMemcpyHostToDevice, s));
-    // k_frame_uniform's workgroups are the partition tiles: it leaves k_part1_hist's histogram
-    P.p1_hist_ready = framing_path == 2 && P.slab_cap == (uint32_t)kPartTile && P.part_group == 1 ? 1 : 0;
+    // k_frame_uniform's workgroups are the partition tiles: it does partition pass 1 itself into
+    // digit regions of ent3 sized for the binomial spread of the digit counts (a region that fills
+    // up redoes the build with the separate pass), or leaves k_part1_hist's histogram
+    const bool tiles = framing_path == 2 && P.slab_cap == (uint32_t)kPartTile && P.part_group == 1;
+    P.p1_region = 0;
+    if (tiles && use_regions) {
+      const double expect = (double)nrec * (double)P.bpp * (double)kBucket / (double)P.cap;
+      uint64_t rc_cap = ((uint64_t)(expect + 8.0 * std::sqrt(expect) + 1024.0) + 63) & ~63ull;
+      if (const char* e = getenv("SPARKEY_REGION_CAP")) rc_cap = std::max<uint64_t>(1, strtoull(e, nullptr, 10));  // (tests)
+      HIP_TRY(grow(&pl->ent2, pl->c_ent2, 256 * rc_cap));
+      HIP_TRY(grow(&pl->ent3, pl->c_ent3, 256 * rc_cap));
+      HIP_TRY(grow(&pl->p1_fill, pl->c_p1_fill, 256));
+      HIP_TRY(hipMemsetAsync(pl->p1_fill, 0, 256 * sizeof(uint32_t), s));
+      P.ent2 = pl->ent2;
+      P.ent3 = pl->ent3;
+      P.max_records = std::min(pl->c_ent2, pl->c_ent3);
+      P.p1_fill = pl->p1_fill;
+      P.p1_region = rc_cap;
+    }
+    P.p1_hist_ready = tiles && !P.p1_region ? 1 : 0;
     rc = launch_framing(pl, P, framing_path, s, err, err_len);
     if (rc) return rc;
     launch_partition(P, s, &pl->timer);
@@ -656,6 +676,10 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
       framing_path = 1;
       continue;
     }
+    if (framing_path == 2 && (st.spec_fail & kSpecRegionFull) && !(st.spec_fail & ~kSpecRegionFull)) {
+      use_regions = false;  // a digit region filled up (skewed hashes): the separate pass 1
+      continue;
+    }
     if (framing_path == 2 && st.spec_fail) {  // a record differs from the header's uniform shape
       framing_path = fused_framing ? 0 : 1;
       continue;
@@ -675,6 +699,11 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
     const bool serial = st.full || getenv("SPARKEY_EXACT_SERIAL") != nullptr;
     placement_path = serial ? 1 : 2;
     P.p1_hist_ready = 0;  // the exact path's partitions (DELETEs left out) count their own digits
+    if (P.p1_region) {  // the exact path replays the entries in log order: frame them into `ent`
+      P.p1_region = 0;
+      rc = launch_framing(pl, P, framing_path, s, err, err_len);
+      if (rc) return rc;
+    }
     float ms2 = 0.f;
     HIP_TRY(hipEventRecord(pl->ev0, s));
     if (serial) {
@@ -1021,7 +1050,7 @@ void sparkey_plan_destroy(sparkey_plan* pl) {
   (void)hipSetDevice(pl->device);
   void* bufs[] = {pl->conv, pl->exitp, pl->qpos, pl->tail, pl->G, pl->cnt, pl->off, pl->ent, pl->ent2, pl->ent3,
                   pl->bcount, pl->bcursor, pl->boff, pl->bfun, pl->bpre, pl->bfun_total, pl->carry, pl->pairs,
-                  pl->parts, pl->pdbg, pl->scan_u64, pl->scan_mp, pl->desc, pl->p1_hist, pl->p1_off, pl->d_status, pl->dbg, pl->wcount, pl->woff, pl->small,
+                  pl->parts, pl->pdbg, pl->p1_fill, pl->scan_u64, pl->scan_mp, pl->desc, pl->p1_hist, pl->p1_off, pl->d_status, pl->dbg, pl->wcount, pl->woff, pl->small,
                   pl->eseg, pl->seg_cnt, pl->seg_off, pl->seg_mark, pl->seg_start,
                   pl->seg_cls_cnt, pl->seg_cls_off, pl->p2tab,
                   pl->app_i64, pl->app_u32, pl->app_u64, pl->app_scan, pl->app_map};

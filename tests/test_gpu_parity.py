@@ -350,6 +350,22 @@ def test_uniform_disabled_gives_same_bytes(native, monkeypatch):
     assert sa.framing_path == 2 and sb.framing_path == 0 and a == b
 
 
+@pytest.mark.parametrize("region_cap", ["60000", "1"])
+def test_uniform_digit_regions(native, monkeypatch, region_cap):
+    """k_frame_uniform as partition pass 1 (entries straight into digit regions of ent3): a region
+    that fills up (forced with a region capacity of 1) redoes the build with the separate pass; both
+    give the reference's bytes, and so does the separate pass by request."""
+    log = make_log(_uniform_puts(50000, 16, 40, seed=3))
+    want, _ = gpu_build(native, log, 21, 8)
+    monkeypatch.setenv("SPARKEY_REGION_CAP", region_cap)
+    got, stats = check(native, log, 21, hash_size=8)
+    assert stats.framing_path == 2 and got == want
+    monkeypatch.delenv("SPARKEY_REGION_CAP")
+    monkeypatch.setenv("SPARKEY_NO_REGIONS", "1")
+    b, _ = gpu_build(native, log, 21, 8)
+    assert b == want
+
+
 # --- batched IndexHash.get on the GPU (sparkey_get_batch) against the oracle's get ---
 def _reader(log, spi):
     from sparkey.reader import GpuHashReader
