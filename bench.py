@@ -32,13 +32,14 @@ PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_pmc_summary.json")
 HASH_SEED = 0x2545F491
 
 
-def stage_bytes(stage, n, data_end, slot, cap):
-    """Algorithmic bytes per launch of each stage."""
+def stage_bytes(stage, n, data_end, slot, cap, passes=2):
+    """Algorithmic bytes per launch of each stage.  passes: partition passes left to
+    the partition stage (1 when the uniform framing wrote the digit regions itself)."""
     log = data_end - 84
     return {
         "frame": log + 16 * n,                # log read once, 16-byte (hash, address) entries written
         "emit": log + 16 * n,                 # serial path: same bytes
-        "partition": 2 * 32 * n,              # two radix passes, entries read + written once each
+        "partition": passes * 32 * n,         # radix passes, entries read + written once each
         "summary": 16 * n,                    # entries read once
         "place": 16 * n + slot * cap,         # entries read once, every slot written once
         "stats": slot * cap,                  # table read once
@@ -203,7 +204,8 @@ def single_gpu(args, dev):
     cap = stats.capacity
     stage_ms = {k: v / args.steps for k, v in stage_acc.items()}
     dom = max(stage_ms, key=lambda k: stage_ms[k]) if stage_ms else None
-    dom_bytes = stage_bytes(dom, n, log_len, slot, cap) if dom else 0
+    passes = stats.partition_passes
+    dom_bytes = stage_bytes(dom, n, log_len, slot, cap, passes) if dom else 0
     achieved = dom_bytes / (stage_ms[dom] * 1e-3) / 1e9 if dom and stage_ms[dom] > 0 else 0.0
     b_alg = (log_len - 84) + 112 + slot * cap
     assert stats.placement_path == wl["path"] and stats.framing_path in (0, 2), stats.as_dict()
@@ -271,7 +273,8 @@ def single_gpu(args, dev):
                    "parallelism": "single"},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS,
-                     "traffic": pmc_traffic("frame_uniform" if dom == "frame" and stats.framing_path == 2 else dom),
+                     "traffic": pmc_traffic({("frame", 2): "frame_uniform", ("partition", 1): "partition_regions"}.get(
+                         (dom, stats.framing_path if dom == "frame" else passes), dom)),
                      "algorithmic_bytes_per_launch": dom_bytes, "avg_launch_ms": stage_ms.get(dom) if dom else None},
         "build_hbm_gbs": b_alg / (ms_per_step * 1e-3) / 1e9,
         "build_algorithmic_bytes": b_alg,

@@ -69,7 +69,11 @@ typedef struct sparkey_build_stats {
   int32_t address_size;
   int32_t placement_path;     /* 0 = parallel canonical placement, 1 = single-lane exact replay (full tables),
                                  2 = exact replay over independent slot segments (DELETEs, overwrites) */
-  int32_t framing_path;       /* 0 = speculative parallel framing, 1 = serial device walker */
+  int32_t framing_path;       /* 0 = speculative parallel framing, 1 = serial device walker,
+                                 2 = uniform-record framing (the header proves one record size) */
+  int32_t partition_passes;   /* passes over the entries of the bucket partition: 2, or 1 when the
+                                 uniform framing wrote the per-digit regions itself */
+  int32_t reserved;
   double device_ms;           /* device time of the build (HIP events), excluding copies */
 } sparkey_build_stats;
 

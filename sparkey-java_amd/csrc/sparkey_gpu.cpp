@@ -338,8 +338,10 @@ static int plan_reserve(sparkey_plan* pl, uint64_t nchunks, uint64_t nrec, uint6
 }
 
 static void fill_stats(sparkey_build_stats* s, const Status& st, const IndexParams& ip, int placement, int framing,
-                       double ms) {
+                       double ms, int partition_passes = 2) {
   if (!s) return;
+  s->partition_passes = partition_passes;
+  s->reserved = 0;
   s->num_records = (int64_t)st.n_records;
   s->num_deletes = (int64_t)st.n_deletes;
   s->num_puts = (int64_t)st.n_records - (int64_t)st.n_deletes;
@@ -610,7 +612,7 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
   // mean per wave + 32); a wave that holds more grows the slabs and the build is redone
   uint32_t slab_cap = (uint32_t)std::min<uint64_t>(
       kPartTile, std::max<uint64_t>(64, 2 * ((nrec + std::max<uint64_t>(nwaves, 1) - 1) / std::max<uint64_t>(nwaves, 1)) + 32));
-  bool use_regions = getenv("SPARKEY_NO_REGIONS") == nullptr;
+  bool use_regions = getenv("SPARKEY_NO_REGIONS") == nullptr, regions_used = false;
   for (int attempt = 0; attempt < 5; attempt++) {
     rc = reserve_for_framing(pl, P, framing_path, nrec, slab_cap, err, err_len);
     if (rc) return rc;
@@ -652,6 +654,7 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
       P.p1_region = rc_cap;
     }
     P.p1_hist_ready = tiles && !P.p1_region ? 1 : 0;
+    regions_used = P.p1_region != 0;
     rc = launch_framing(pl, P, framing_path, s, err, err_len);
     if (rc) return rc;
     launch_partition(P, s, &pl->timer);
@@ -802,7 +805,7 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
       pl->stage_ms.push_back(t);
     }
   }
-  fill_stats(stats_out, st, ip, placement_path, framing_path, ms);
+  fill_stats(stats_out, st, ip, placement_path, framing_path, ms, regions_used ? 1 : 2);
   return SPARKEY_OK;
 }
 

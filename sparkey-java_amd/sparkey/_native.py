@@ -64,7 +64,8 @@ class BuildStats(ctypes.Structure):
                 ("max_displacement", ctypes.c_int64), ("hash_collisions", ctypes.c_int64),
                 ("total_displacement", ctypes.c_int64), ("hash_size", ctypes.c_int32),
                 ("address_size", ctypes.c_int32), ("placement_path", ctypes.c_int32),
-                ("framing_path", ctypes.c_int32), ("device_ms", ctypes.c_double)]
+                ("framing_path", ctypes.c_int32), ("partition_passes", ctypes.c_int32),
+                ("reserved", ctypes.c_int32), ("device_ms", ctypes.c_double)]
 
     def as_dict(self) -> dict:
         return {f: getattr(self, f) for f, _ in self._fields_}
