@@ -143,6 +143,7 @@ __global__ __launch_bounds__(kPlaceBlock) void k_summary(BuildParams P) {
   __shared__ uint64_t sh64[kPlaceBlock / 64 + 1];
   __shared__ int64_t shm[kPlaceBlock / 64 + 1];
   if (build_aborted(P)) return;
+  if (P.p2_sorted && !P.st->need_summary) return;  // k_part2s left every carry function
   const uint64_t b = P.b_lo + blockIdx.x;
   const uint64_t start = b << kBucketShift;
   const int64_t bsize = (int64_t)min((uint64_t)kBucket, P.cap - start);

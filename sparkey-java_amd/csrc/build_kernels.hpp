@@ -30,6 +30,7 @@ constexpr int kPartItems = 16;
 constexpr int kPartTile = kPartBlock * kPartItems;
 constexpr int kPart2Block = 1024;                 // k_part2: one workgroup per coarse digit
 constexpr int kPart2Items = 8;                    // k_part2: entries per thread per round
+constexpr uint32_t kP2SortedMaxBpp = 64;          // k_part2s: buckets per digit (16-bit counts: 2 KB each)
 constexpr int kPart2MaxBits = 14;                 // fine digit of the partition (<= 16384 buckets)
 constexpr uint32_t kPlaceLdsMax = 1024;           // entries of a bucket staged in LDS (load <= 1/1.3: mean 788)
 constexpr uint32_t kMaxPartGroup = 64;
@@ -86,7 +87,7 @@ struct Status {
   unsigned long long n_spill;    // sharded placement: slots written outside the rank's range
   unsigned long long n_segs[4];  // exact path: segments per size class (small, mid, large, huge)
   unsigned int guard;            // exact path: bounds-check bits that tripped (a bug; fails the build)
-  unsigned int pad3;
+  unsigned int need_summary;     // k_part2s left a digit unsummarised (k_summary runs)
 };
 
 struct BuildParams {
@@ -177,6 +178,7 @@ struct BuildParams {
   uint32_t uni_hist_off;  // LDS offset of the digit counts (set by the launcher)
   // k_frame_uniform as partition pass 1: digit d's entries at ent3[d * p1_region, + p1_fill[d])
   uint64_t p1_region;   // 0 = off
+  int32_t p2_sorted;    // k_part2s: entries by wanted slot within the bucket + the carry functions
   uint32_t* p1_fill;
   // framing window: records start at fr_entry (84 for a whole log) and are framed while they start
   // below data_end (the frame end); k_frame chunks are numbered from fr_k0 = fr_entry >> fr_cshift,

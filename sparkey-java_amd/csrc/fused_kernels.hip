@@ -1143,6 +1143,127 @@ __global__ __launch_bounds__(kPart2Block) void k_part2(BuildParams P) {
   }
 }
 
+// Pass 2 for a table of up to kP2SortedMaxBpp buckets per digit (single GPU): the digit's entries
+// are also counted per (bucket, wanted slot) in LDS (16-bit counts), so that the same pass leaves
+// each bucket's max-plus carry function -- k_summary's output: F(x) = max(x + n - bsize,
+// n + mlast - bsize), mlast = max over occupied s of s - base[s] -- without k_summary's read of the
+// entries.  The entries themselves go out grouped by bucket as in k_part2 (each bucket's run written
+// in order: ordering them by wanted slot here scattered the writes and measured 2x slower).  A digit
+// with a bucket of more than 65535 entries (the counts could overflow) asks for the k_summary pass.
+__global__ __launch_bounds__(kPart2Block) void k_part2s(BuildParams P) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t dyn[];  // h[bpp * 512] | btot[bpp] | boffl[bpp]
+  if (build_aborted(P)) return;
+  const uint32_t dpart = blockIdx.x;
+  uint64_t lo, hi;
+  if (P.p1_region) {
+    lo = (uint64_t)dpart * P.p1_region;
+    hi = lo + min((uint64_t)P.p1_fill[dpart], P.p1_region);
+  } else {
+    lo = P.p1_off[(uint64_t)dpart * P.p1_tiles];
+    hi = (dpart + 1 < 256) ? P.p1_off[(uint64_t)(dpart + 1) * P.p1_tiles] : P.p1_off_total[0];
+  }
+  const uint32_t nbins = P.bpp;
+  const uint64_t b0 = (uint64_t)dpart * nbins;
+  uint32_t* h = dyn;
+  uint32_t* btot = dyn + nbins * 512;
+  uint32_t* boffl = btot + nbins;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (uint32_t i = tid; i < nbins * 512 + 2 * nbins; i += kPart2Block) dyn[i] = 0;
+  __syncthreads();
+  for (uint64_t i0 = lo; i0 < hi; i0 += (uint64_t)kPart2Block * kPart2Items) {
+    uint64_t hv[kPart2Items];
+#pragma unroll
+    for (int k = 0; k < kPart2Items; k++) {
+      const uint64_t i = i0 + (uint64_t)k * kPart2Block + tid;
+      if (i < hi) hv[k] = P.ent3[i].hash;
+    }
+#pragma unroll
+    for (int k = 0; k < kPart2Items; k++) {
+      const uint64_t i = i0 + (uint64_t)k * kPart2Block + tid;
+      if (i >= hi) continue;
+      const uint64_t slot = fast_mod(hv[k], P.mod);
+      const uint32_t b = (uint32_t)((slot >> kBucketShift) - b0), sl = (uint32_t)(slot & (kBucket - 1));
+      atomicAdd(&h[(b << 9) + (sl >> 1)], 1u << ((sl & 1) * 16));
+      atomicAdd(&btot[b], 1u);
+    }
+  }
+  __syncthreads();
+  bool big = false;
+  for (uint32_t b = tid; b < nbins; b += kPart2Block) big |= btot[b] > 65535u;
+  const bool summarise = !__syncthreads_or(big);
+  if (!summarise && tid == 0) atomicOr(&P.st->need_summary, 1u);  // (rare)
+  // bucket offsets within the digit (one wave; nbins <= 64)
+  if (wave == 0) {
+    const uint32_t c = (uint32_t)lane < nbins ? btot[lane] : 0u;
+    uint32_t incl = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t t = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += t;
+    }
+    if ((uint32_t)lane < nbins) {
+      boffl[lane] = incl - c;  // then the bucket's cursor
+      const uint64_t bucket = b0 + lane;
+      if (bucket < P.nbuckets) {
+        P.boff[bucket] = lo + incl - c;
+        P.bcount[bucket] = c;
+      }
+    }
+  }
+  // per bucket (one wave each): the carry function from the slot counts
+  for (uint32_t b = wave; summarise && b < nbins; b += kPart2Block / 64) {
+    const uint64_t bucket = b0 + b;
+    if (bucket >= P.nbuckets) continue;
+    const uint32_t* hw = h + (b << 9) + lane * 8;  // this lane's 16 slots: 16 * lane ...
+    uint32_t cnts[16];
+    uint32_t tot = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const uint32_t w = hw[k];
+      cnts[2 * k] = w & 0xffffu;
+      cnts[2 * k + 1] = w >> 16;
+      tot += cnts[2 * k] + cnts[2 * k + 1];
+    }
+    uint32_t incl = tot;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t t = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += t;
+    }
+    uint32_t run = incl - tot;
+    long long mx = -(1ll << 40);
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+      if (cnts[k]) mx = max(mx, (long long)(16 * lane + k) - (long long)run);
+      run += cnts[k];
+    }
+    mx = wave_max_i64(mx);
+    if (lane == 0) {
+      const int64_t n = (int64_t)btot[b];
+      const int64_t bsize = (int64_t)min((uint64_t)kBucket, P.cap - (bucket << kBucketShift));
+      const int64_t mlast = mx < 0 ? 0 : mx;
+      MaxPlus f;
+      f.a = n - bsize;
+      f.c = n ? max((int64_t)0, n + mlast - bsize) : 0;
+      P.bfun[bucket] = f;
+    }
+  }
+  __syncthreads();
+  for (uint64_t i0 = lo; i0 < hi; i0 += (uint64_t)kPart2Block * kPart2Items) {
+    Entry v[kPart2Items];
+#pragma unroll
+    for (int k = 0; k < kPart2Items; k++) {
+      const uint64_t i = i0 + (uint64_t)k * kPart2Block + tid;
+      if (i < hi) v[k] = P.ent3[i];
+    }
+#pragma unroll
+    for (int k = 0; k < kPart2Items; k++) {
+      const uint64_t i = i0 + (uint64_t)k * kPart2Block + tid;
+      if (i < hi) P.ent2[lo + atomicAdd(&boffl[bucket_of(P, v[k].hash) - b0], 1u)] = v[k];
+    }
+  }
+}
+
 // ================================================================================================
 // k_place_lds: one bucket per workgroup, entries staged in LDS (buckets above kPlaceLdsMax
 // entries are left to the global-memory k_place, flagged in P.st->big_buckets).
@@ -1382,7 +1503,10 @@ void launch_partition2(const BuildParams& P, hipStream_t s, StageTimer* tm) {
 
 void launch_partition(const BuildParams& P, hipStream_t s, StageTimer* tm) {
   if (!P.p1_region) launch_partition1(P, s);
-  hipLaunchKernelGGL(k_part2, dim3(256), dim3(kPart2Block), (size_t)(2u * P.bpp) * sizeof(uint32_t), s, P);
+  if (P.p2_sorted)
+    hipLaunchKernelGGL(k_part2s, dim3(256), dim3(kPart2Block), (size_t)(514u * P.bpp) * sizeof(uint32_t), s, P);
+  else
+    hipLaunchKernelGGL(k_part2, dim3(256), dim3(kPart2Block), (size_t)(2u * P.bpp) * sizeof(uint32_t), s, P);
   tm->mark("partition", s);
 }
 

@@ -655,6 +655,8 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
     }
     P.p1_hist_ready = tiles && !P.p1_region ? 1 : 0;
     regions_used = P.p1_region != 0;
+    // k_part2s: pass 2 also sorts each bucket by wanted slot and leaves the carry functions
+    P.p2_sorted = P.bpp <= kP2SortedMaxBpp && !getenv("SPARKEY_NO_P2_SORTED") ? 1 : 0;
     rc = launch_framing(pl, P, framing_path, s, err, err_len);
     if (rc) return rc;
     launch_partition(P, s, &pl->timer);
@@ -702,6 +704,7 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
     const bool serial = st.full || getenv("SPARKEY_EXACT_SERIAL") != nullptr;
     placement_path = serial ? 1 : 2;
     P.p1_hist_ready = 0;  // the exact path's partitions (DELETEs left out) count their own digits
+    P.p2_sorted = 0;
     if (P.p1_region) {  // the exact path replays the entries in log order: frame them into `ent`
       P.p1_region = 0;
       rc = launch_framing(pl, P, framing_path, s, err, err_len);
