@@ -1,0 +1,58 @@
+"""Repeat one device build and compare every result with the first (a race check; one process).
+
+    python tools/repeat_check.py [--reps 8] [--general] [--entries 10000000]
+"""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (os.path.join(ROOT, "sparkey-java_amd"), os.path.join(ROOT, "oracle"), ROOT):
+    sys.path.insert(0, p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=8)
+    ap.add_argument("--entries", type=int, default=10_000_000)
+    ap.add_argument("--general", action="store_true")
+    a = ap.parse_args()
+    if a.general:
+        os.environ["SPARKEY_NO_UNIFORM"] = "1"
+    from sparkey import _native, synth
+    log = synth.fixed_log(a.entries, 16, 100, seed=1)
+    dev = torch.device("cuda", 0)
+    header = log[:84].tobytes()
+    opts = _native.make_opts(hash_seed=0x2545F491)
+    n_out = _native.index_size(header, opts)
+    d_log = torch.from_numpy(log).to(dev)
+    d_out = torch.empty(n_out, dtype=torch.uint8, device=dev)
+    plan = _native.Plan(0)
+    first = None
+    bad = 0
+    for r in range(a.reps):
+        d_out.fill_(0xAB)
+        torch.cuda.synchronize()
+        plan.build(header, d_log.data_ptr(), log.size, d_out.data_ptr(), n_out, opts)
+        out = d_out.cpu().numpy()
+        if first is None:
+            first = out.copy()
+            continue
+        diff = np.nonzero(out != first)[0]
+        if diff.size:
+            bad += 1
+            slots = sorted(set(((diff - 112) // 16).tolist()))[:8]
+            print(f"rep {r}: {diff.size} bytes differ, slots {slots}", flush=True)
+    print(f"reps={a.reps} mismatching={bad}", flush=True)
+    if not a.general or True:
+        import oracle
+        want = np.frombuffer(oracle.build_index(log.tobytes(), 0x2545F491), dtype=np.uint8)
+        print("first == oracle:", bool((first == want).all()), flush=True)
+    plan.close()
+
+
+if __name__ == "__main__":
+    main()
