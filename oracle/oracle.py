@@ -64,6 +64,8 @@ def lib():
                                          ctypes.c_int32, ctypes.c_int32, ctypes.c_int64, u8p,
                                          ctypes.c_int64, ctypes.c_char_p, ctypes.c_int32]
         L.oracle_build_index.restype = ctypes.c_int64
+        L.oracle_snappy_uncompress.argtypes = [u8p, ctypes.c_int64, u8p, ctypes.c_int64]
+        L.oracle_snappy_uncompress.restype = ctypes.c_int64
         L.oracle_get.argtypes = [u8p, ctypes.c_int64, u8p, ctypes.c_int64, u8p, ctypes.c_int32,
                                  ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]
         L.oracle_get.restype = ctypes.c_int32
@@ -163,6 +165,15 @@ def build_index(log: bytes, hash_seed: int, hash_size: int = 0, sparsity: float 
     if rc < 0:
         raise OracleError(rc, err.value.decode())
     return out.raw
+
+
+def snappy_uncompress(data: bytes, cap: int) -> bytes:
+    """Snappy raw-format decompression restated (CompressorType.java:32-34)."""
+    out = ctypes.create_string_buffer(max(cap, 1))
+    rc = lib().oracle_snappy_uncompress(data, len(data), out, cap)
+    if rc < 0:
+        raise OracleError(rc, "snappy uncompress failed")
+    return out.raw[:rc]
 
 
 def get(index: bytes, log: bytes, key: bytes):

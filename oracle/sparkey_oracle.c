@@ -215,7 +215,7 @@ static int32_t parse_log_header(const uint8_t* b, int64_t len, log_header* h) {
   if (h->max_key_len > 0x7fffffffLL || h->max_key_len < 0) return ORACLE_E_HEADER; /* CommonHeader.java:38-40 */
   if (h->max_value_len < 0) return ORACLE_E_HEADER;                     /* CommonHeader.java:41-43 */
   if (h->compression_type < 0 || h->compression_type > 2) return ORACLE_E_CORRUPT_LOG; /* values()[ct] */
-  if (h->compression_type != 0) return ORACLE_E_UNSUPPORTED;            /* NONE only on this path */
+  if (h->compression_type == 2) return ORACLE_E_UNSUPPORTED;            /* ZSTD: not on this path */
   return ORACLE_OK;
 }
 
@@ -341,7 +341,34 @@ typedef struct {
   const uint8_t* log;
   int64_t log_len;
   int32_t ebb_mask;
+  /* SNAPPY logs: `log` is the virtual stream (84 header bytes, then every block's decompressed bytes
+   * back to back); block b starts at file offset blk_pos[b] and at virtual offset blk_voff[b]. */
+  int32_t compressed;
+  int64_t nblk;
+  int64_t* blk_pos;
+  int64_t* blk_voff;
 } build_ctx;
+
+/* The block that holds virtual offset v (largest b with blk_voff[b] <= v). */
+static int64_t block_of(const build_ctx* c, int64_t v) {
+  int64_t lo = 0, hi = c->nblk - 1;
+  while (lo < hi) {
+    int64_t mid = (lo + hi + 1) / 2;
+    if (c->blk_voff[mid] <= v) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+
+/* CompressedRandomReader.seek to a block start: file position -> virtual offset (<0: no such block). */
+static int64_t block_voff(const build_ctx* c, int64_t file_pos) {
+  int64_t lo = 0, hi = c->nblk - 1;
+  while (lo <= hi) {
+    int64_t mid = (lo + hi) / 2;
+    if (c->blk_pos[mid] == file_pos) return c->blk_voff[mid];
+    if (c->blk_pos[mid] < file_pos) lo = mid + 1; else hi = mid - 1;
+  }
+  return -1;
+}
 
 static int32_t calc_entry_block_bits(int32_t max_entries_per_block) { /* IndexHash.java:123-129 */
   int32_t i = 0;
@@ -427,6 +454,11 @@ static int64_t displacement_of(int64_t cap, int64_t slot, uint64_t hash) { /* :6
 
 /* skipStuff (IndexHash.java:550-560) is a no-op for NONE (entryIndex == 0 always). */
 static int32_t skip_stuff(const build_ctx* c, int64_t* pos, int32_t entry_index) {
+  if (c->compressed) { /* the address names a block; entries are counted from its start */
+    int64_t v = block_voff(c, *pos);
+    if (v < 0) return ORACLE_E_CORRUPT_LOG;
+    *pos = v;
+  }
   for (int32_t i = 0; i < entry_index; i++) {
     int32_t k, v;
     int32_t rc = oracle_vlq_read(c->log, c->log_len, pos, &k);
@@ -637,9 +669,12 @@ typedef struct {
 static int32_t next_record(const build_ctx* c, int64_t* pos, int64_t end, int64_t* prev_pos,
                            int32_t* entry_index, log_rec* r) {
   if (*pos >= end) return 0;
-  if (*pos == *prev_pos) (*entry_index)++; else *entry_index = 0;
-  *prev_pos = *pos;
-  r->position = *pos;
+  /* CompressedReader.getBlockPosition (CompressedReader.java:121-126): the block holding the
+   * record's first byte; for NONE the record's own offset */
+  const int64_t bpos = c->compressed ? c->blk_pos[block_of(c, *pos)] : *pos;
+  if (bpos == *prev_pos) (*entry_index)++; else *entry_index = 0;
+  *prev_pos = bpos;
+  r->position = bpos;
   r->entry_index = *entry_index;
   int64_t p = *pos;
   int32_t first, second, rc;
@@ -665,7 +700,7 @@ static int32_t fill_from_log(build_ctx* c) {
   const int32_t ebb = c->ih.entry_block_bits;
   for (;;) {
     log_rec r;
-    int32_t rc = next_record(c, &pos, c->ih.data_end, &prev_pos, &entry_index, &r);
+    int32_t rc = next_record(c, &pos, c->compressed ? c->log_len : c->ih.data_end, &prev_pos, &entry_index, &r);
     if (rc < 0) return rc;
     if (rc == 0) return 0;
     uint64_t address = ((uint64_t)r.position << ebb) | (uint64_t)r.entry_index; /* :283 */
@@ -701,7 +736,7 @@ static int32_t fill_from_log_sorted(build_ctx* c) {
   if (!es) return ORACLE_E_BUFFER;
   for (;;) {
     log_rec r;
-    int32_t rc = next_record(c, &pos, c->ih.data_end, &prev_pos, &entry_index, &r);
+    int32_t rc = next_record(c, &pos, c->compressed ? c->log_len : c->ih.data_end, &prev_pos, &entry_index, &r);
     if (rc < 0) { free(es); return rc; }
     if (rc == 0) break;
     if (n == cap_e) {
@@ -753,6 +788,115 @@ static const char* err_msg(int32_t rc) {
   }
 }
 
+/* Snappy raw-format decompression (the published format snappy-java wraps, CompressorType.java:32-34):
+ * varint uncompressed length, then literal (tag 00), copy-1 (01), copy-2 (10) and copy-4 (11)
+ * elements.  Returns the decompressed length or <0 on a malformed stream or a too-small `out`. */
+int64_t oracle_snappy_uncompress(const uint8_t* in, int64_t n, uint8_t* out, int64_t cap) {
+  int64_t p = 0, ulen = 0;
+  for (int shift = 0;; shift += 7) {
+    if (p >= n || shift > 28) return ORACLE_E_CORRUPT_LOG;
+    uint8_t b = in[p++];
+    ulen |= (int64_t)(b & 0x7f) << shift;
+    if (!(b & 0x80)) break;
+  }
+  if (ulen > cap || ulen > 0xffffffffLL) return ORACLE_E_BUFFER;
+  int64_t o = 0;
+  while (p < n) {
+    const uint8_t t = in[p++];
+    int64_t len, off;
+    if ((t & 3) == 0) {
+      len = (t >> 2) + 1;
+      if (len > 60) {
+        const int nb = (int)len - 60;
+        if (p + nb > n) return ORACLE_E_CORRUPT_LOG;
+        len = 0;
+        for (int i = 0; i < nb; i++) len |= (int64_t)in[p + i] << (8 * i);
+        len += 1;
+        p += nb;
+      }
+      if (p + len > n || o + len > ulen) return ORACLE_E_CORRUPT_LOG;
+      memcpy(out + o, in + p, (size_t)len);
+      p += len;
+      o += len;
+      continue;
+    }
+    if ((t & 3) == 1) {
+      if (p + 1 > n) return ORACLE_E_CORRUPT_LOG;
+      len = ((t >> 2) & 7) + 4;
+      off = ((int64_t)(t >> 5) << 8) | in[p];
+      p += 1;
+    } else if ((t & 3) == 2) {
+      if (p + 2 > n) return ORACLE_E_CORRUPT_LOG;
+      len = (t >> 2) + 1;
+      off = (int64_t)in[p] | ((int64_t)in[p + 1] << 8);
+      p += 2;
+    } else {
+      if (p + 4 > n) return ORACLE_E_CORRUPT_LOG;
+      len = (t >> 2) + 1;
+      off = (int64_t)rd32(in + p);
+      p += 4;
+    }
+    if (off == 0 || off > o || o + len > ulen) return ORACLE_E_CORRUPT_LOG;
+    for (int64_t i = 0; i < len; i++) out[o + i] = out[o - off + i]; /* overlapping copies repeat */
+    o += len;
+  }
+  return o == ulen ? ulen : ORACLE_E_CORRUPT_LOG;
+}
+
+/* The virtual stream of a SNAPPY log: blocks VLQ(compressedSize) || snappy bytes from offset 84 to
+ * dataEnd (CompressedOutputStream.flush, CompressedOutputStream.java:47-58; CompressedReader.fetchBlock,
+ * CompressedReader.java:66-74). */
+static int32_t open_compressed(build_ctx* c, const uint8_t* log, int64_t data_end, uint8_t** vbuf) {
+  int64_t nblk = 0, cap_b = 64, total = 0, p = LOG_HEADER_SIZE;
+  c->blk_pos = (int64_t*)malloc(sizeof(int64_t) * (size_t)cap_b);
+  c->blk_voff = (int64_t*)malloc(sizeof(int64_t) * (size_t)cap_b);
+  int64_t* ulens = (int64_t*)malloc(sizeof(int64_t) * (size_t)cap_b);
+  if (!c->blk_pos || !c->blk_voff || !ulens) { free(ulens); return ORACLE_E_BUFFER; }
+  while (p < data_end) {
+    int64_t q = p;
+    int32_t clen;
+    int32_t rc = oracle_vlq_read(log, data_end, &q, &clen);
+    if (rc) { free(ulens); return rc; }
+    if (clen < 0 || q + clen > data_end) { free(ulens); return ORACLE_E_CORRUPT_LOG; }
+    int64_t ulen = 0, r = q;
+    for (int shift = 0;; shift += 7) {
+      if (r >= q + clen || shift > 28) { free(ulens); return ORACLE_E_CORRUPT_LOG; }
+      ulen |= (int64_t)(log[r] & 0x7f) << shift;
+      if (!(log[r++] & 0x80)) break;
+    }
+    if (nblk == cap_b) {
+      cap_b *= 2;
+      c->blk_pos = (int64_t*)realloc(c->blk_pos, sizeof(int64_t) * (size_t)cap_b);
+      c->blk_voff = (int64_t*)realloc(c->blk_voff, sizeof(int64_t) * (size_t)cap_b);
+      ulens = (int64_t*)realloc(ulens, sizeof(int64_t) * (size_t)cap_b);
+      if (!c->blk_pos || !c->blk_voff || !ulens) { free(ulens); return ORACLE_E_BUFFER; }
+    }
+    c->blk_pos[nblk] = p;
+    c->blk_voff[nblk] = LOG_HEADER_SIZE + total;
+    ulens[nblk] = ulen;
+    total += ulen;
+    nblk++;
+    p = q + clen;
+  }
+  uint8_t* v = (uint8_t*)malloc((size_t)(LOG_HEADER_SIZE + total + 1));
+  if (!v) { free(ulens); return ORACLE_E_BUFFER; }
+  memcpy(v, log, LOG_HEADER_SIZE);
+  for (int64_t b = 0; b < nblk; b++) {
+    int64_t q = c->blk_pos[b];
+    int32_t clen;
+    (void)oracle_vlq_read(log, data_end, &q, &clen);
+    int64_t got = oracle_snappy_uncompress(log + q, clen, v + c->blk_voff[b], ulens[b]);
+    if (got != ulens[b]) { free(ulens); free(v); return ORACLE_E_CORRUPT_LOG; }
+  }
+  free(ulens);
+  c->compressed = 1;
+  c->nblk = nblk;
+  c->log = v;
+  c->log_len = LOG_HEADER_SIZE + total;
+  *vbuf = v;
+  return 0;
+}
+
 /* IndexHash.createNew: IndexHash.java:131-167 */
 int64_t oracle_build_index(const uint8_t* log, int64_t log_len, int32_t hash_size, double sparsity,
                            int32_t seed, int32_t method, int64_t max_memory,
@@ -768,13 +912,21 @@ int64_t oracle_build_index(const uint8_t* log, int64_t log_len, int32_t hash_siz
   c.log = log;
   c.log_len = log_len;
   c.ebb_mask = (1 << c.ih.entry_block_bits) - 1;
+  uint8_t* vbuf = NULL;
+  if (lh.compression_type == 1) {
+    rc = open_compressed(&c, log, lh.data_end, &vbuf);
+    if (rc) { free(c.blk_pos); free(c.blk_voff); set_err(err, err_len, err_msg(rc)); return rc; }
+  }
   const int64_t hash_length = (int64_t)c.slot_size * c.ih.capacity;
   const int64_t total = INDEX_HEADER_SIZE + hash_length;
-  if (out_cap < total) { set_err(err, err_len, "Buffer too small"); return ORACLE_E_BUFFER; }
-  memset(out, 0, (size_t)total);
+  if (out_cap < total) rc = ORACLE_E_BUFFER;
+  if (!rc) memset(out, 0, (size_t)total);
   c.table = out + INDEX_HEADER_SIZE;
   int in_memory = method == 0 ? (hash_length <= max_memory) : (method == 1); /* :155-160 */
-  rc = in_memory ? fill_from_log(&c) : fill_from_log_sorted(&c);
+  if (!rc) rc = in_memory ? fill_from_log(&c) : fill_from_log_sorted(&c);
+  free(vbuf);
+  free(c.blk_pos);
+  free(c.blk_voff);
   if (rc) { set_err(err, err_len, err_msg(rc)); return rc; }
   calc_stats(&c);
   write_index_header(out, &c.ih);

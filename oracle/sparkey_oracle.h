@@ -62,6 +62,9 @@ int64_t oracle_build_index(const uint8_t* log, int64_t log_len, int32_t hash_siz
                            int32_t seed, int32_t method, int64_t max_memory,
                            uint8_t* out, int64_t out_cap, char* err, int32_t err_len);
 
+/* Snappy raw-format block decompression (CompressorType.java:32-34): decompressed length or <0 */
+int64_t oracle_snappy_uncompress(const uint8_t* in, int64_t n, uint8_t* out, int64_t cap);
+
 /* IndexHash.get (IndexHash.java:398-452): 1 found, 0 missing, <0 error */
 int32_t oracle_get(const uint8_t* index, int64_t index_len, const uint8_t* log, int64_t log_len,
                    const uint8_t* key, int32_t klen, int64_t* value_off, int64_t* value_len);
