@@ -1,0 +1,71 @@
+// snappy.hpp -- SNAPPY log front end.
+//
+// A SNAPPY log is 84 header bytes, then blocks VLQ(compressedSize) || Snappy stream from offset 84 to
+// dataEnd (CompressedOutputStream.flush, CompressedOutputStream.java:47-58).  The device front end
+// turns it into the "virtual log": 84 header bytes and every block's decompressed bytes back to back,
+// which is byte for byte the record stream of a NONE log (blocks split records only where the writer
+// splits them, CompressedWriter.java:59-124).  The normal build runs over the virtual log; a last pass
+// rewrites each slot's address from its virtual offset to the reference's
+// (blockPosition << entryBlockBits) | entryIndex (IndexHash.java:270-283,
+// CompressedReader.getBlockPosition CompressedReader.java:121-126).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace sk {
+
+struct SnappyBlock {
+  int64_t file_pos;   // offset of the block's VLQ in the log file (the address's position part)
+  int64_t data;       // offset of the Snappy stream
+  int64_t voff;       // offset of the decompressed bytes in the virtual log
+  uint32_t clen;      // Snappy stream bytes
+  uint32_t ulen;      // decompressed bytes (the stream's preamble)
+};
+
+// per-block result of the decode kernel's record walk (the walk assumes the block starts a record)
+struct SnappyWalk {
+  uint32_t count;     // records started in the block
+  uint32_t flags;     // kWalk* bits
+  int64_t overflow;   // bytes of the last record past the block end
+};
+
+constexpr uint32_t kWalkBadHeader = 1u;    // a record header runs past the block end or a VLQ > 5 bytes
+constexpr uint32_t kWalkTooMany = 2u;      // more records than maxEntriesPerBlock
+constexpr uint32_t kWalkBadStream = 4u;    // malformed Snappy stream
+
+struct SnappyDirResult {
+  uint64_t nblk;
+  uint64_t total;     // decompressed bytes over all blocks
+  int32_t err;        // 0 ok, 1 corrupt block framing, 2 block larger than compressionBlockSize
+  int32_t pad;
+};
+
+struct SnappyParams {
+  const uint8_t* log;
+  int64_t data_end;
+  int64_t max_block;        // compressionBlockSize: the reader's uncompressed buffer
+  SnappyBlock* blocks;
+  uint64_t blk_cap;
+  SnappyDirResult* dir;
+  uint8_t* vlog;            // virtual log (84 header bytes written by the host)
+  SnappyWalk* walk;
+  uint32_t* rec_off;        // [block * mepb + j]: record j's offset inside block
+  uint32_t mepb;            // maxEntriesPerBlock (>= 1)
+  uint32_t lds_bytes;       // k_snappy_lds: staged stream + output bytes
+  // address rewrite
+  const uint8_t* itab;      // internal table (slot layout ihs + ias)
+  uint8_t* otab;            // final table (hs + as)
+  uint64_t cap;
+  int32_t ihs, ias, hs, as;
+  int32_t ebb;
+  uint64_t nblk;
+  int32_t* err;             // rewrite: virtual offset not a record start
+};
+
+void launch_snappy_dir(const SnappyParams& S, hipStream_t s);
+// decode + walk, one wave per block: LDS-staged when lds_bytes > 0, else lane-serial in global memory
+hipError_t launch_snappy_decode(const SnappyParams& S, hipStream_t s);
+void launch_snappy_rewrite(const SnappyParams& S, hipStream_t s);
+
+}  // namespace sk

@@ -1,0 +1,249 @@
+// snappy_kernels.hip -- SNAPPY log front end on the device (snappy.hpp).
+//
+//   k_snappy_dir      block directory: the chain of VLQ(compressedSize) block headers from offset 84 to
+//                     dataEnd (CompressedReader.fetchBlock, CompressedReader.java:66-74), one lane
+//   k_snappy_lds      one wave per block: the Snappy stream staged in LDS, decoded element by element
+//                     into LDS (every lane copies a slice of each literal / match), streamed out to
+//                     the virtual log, then the block's records walked from LDS
+//   k_snappy_global   the same, lane-serial in global memory, for blocks too large for LDS
+//   k_snappy_rewrite  one lane per slot: virtual offset -> (blockPosition << ebb) | entryIndex
+#include "device_common.hpp"
+#include "snappy.hpp"
+
+namespace sk {
+
+namespace {
+
+__device__ __forceinline__ int64_t align16(int64_t x) { return (x + 15) & ~15LL; }
+
+// Snappy raw format: varint uncompressed length, then literal (tag 00), copy-1 (01), copy-2 (10) and
+// copy-4 (11) elements.  Lanes [lane, nlanes) share each element's copy; every lane parses the same
+// tags (uniform control flow).  A match copies out[o + k] = out[o - off + k % off]: only bytes before
+// o are read, so overlapping matches need no ordering between the lanes.  Returns kWalkBadStream on a
+// malformed stream.
+template <bool kSync>
+__device__ uint32_t snappy_decode(const uint8_t* in, int64_t n, int64_t p, uint8_t* out, int64_t ulen, int lane,
+                                  int nlanes) {
+  int64_t o = 0;
+  while (p < n) {
+    const uint32_t t = in[p++];
+    int64_t len, off = 0;
+    if ((t & 3u) == 0) {
+      len = (t >> 2) + 1;
+      if (len > 60) {
+        const int nb = (int)len - 60;
+        if (p + nb > n) return kWalkBadStream;
+        len = 0;
+        for (int i = 0; i < nb; i++) len |= (int64_t)in[p + i] << (8 * i);
+        len += 1;
+        p += nb;
+      }
+      if (p + len > n || o + len > ulen) return kWalkBadStream;
+      for (int64_t k = lane; k < len; k += nlanes) out[o + k] = in[p + k];
+      p += len;
+    } else {
+      if ((t & 3u) == 1) {
+        if (p + 1 > n) return kWalkBadStream;
+        len = ((t >> 2) & 7u) + 4;
+        off = ((int64_t)(t >> 5) << 8) | in[p];
+        p += 1;
+      } else if ((t & 3u) == 2) {
+        if (p + 2 > n) return kWalkBadStream;
+        len = (t >> 2) + 1;
+        off = (int64_t)in[p] | ((int64_t)in[p + 1] << 8);
+        p += 2;
+      } else {
+        if (p + 4 > n) return kWalkBadStream;
+        len = (t >> 2) + 1;
+        off = (int64_t)in[p] | ((int64_t)in[p + 1] << 8) | ((int64_t)in[p + 2] << 16) | ((int64_t)in[p + 3] << 24);
+        p += 4;
+      }
+      if (off == 0 || off > o || o + len > ulen) return kWalkBadStream;
+      for (int64_t k = lane; k < len; k += nlanes) out[o + k] = out[o - off + k % off];
+    }
+    o += len;
+    if (kSync) __syncthreads();
+  }
+  return o == ulen ? 0u : kWalkBadStream;
+}
+
+// The block's records, assuming it starts at a record (SparkeyLogIterator.java:86-138): their offsets
+// go to rec_off, and the last record's bytes past the block end to overflow.
+__device__ void walk_block(const SnappyParams& S, uint64_t b, const uint8_t* buf, int64_t ulen) {
+  auto at = [&](int64_t i) -> uint32_t { return buf[i]; };
+  uint32_t j = 0, flags = 0;
+  int64_t u = 0;
+  while (u < ulen) {
+    if (j < S.mepb) S.rec_off[b * S.mepb + j] = (uint32_t)u;
+    else flags |= kWalkTooMany;
+    j++;
+    const RecHdr h = decode_header(at, u, ulen);
+    if (h.rc || h.klen < 0 || h.vlen < 0) {
+      flags |= kWalkBadHeader;
+      break;
+    }
+    u = record_end(h, u);
+  }
+  SnappyWalk w;
+  w.count = j;
+  w.flags = flags;
+  w.overflow = u - ulen;
+  S.walk[b] = w;
+}
+
+__device__ __forceinline__ int32_t dir_vlq(const uint8_t* log, int64_t& p, int64_t end, int32_t& err) {
+  uint32_t v = 0;
+  for (int i = 0; i < 5; i++) {
+    if (p >= end) { err = 1; return 0; }
+    const uint32_t b = log[p++];
+    if (b < 0x80u) return (int32_t)(v | (b << (7 * i)));
+    v |= (b & 0x7fu) << (7 * i);
+  }
+  err = 1;
+  return 0;
+}
+
+}  // namespace
+
+__global__ void __launch_bounds__(64) k_snappy_dir(SnappyParams S) {
+  if (threadIdx.x != 0) return;
+  int64_t p = 84;
+  uint64_t nb = 0, total = 0;
+  int32_t err = 0;
+  while (p < S.data_end) {
+    int64_t q = p;
+    const int32_t clen = dir_vlq(S.log, q, S.data_end, err);   // Util.readUnsignedVLQInt
+    if (err || clen < 0 || q + clen > S.data_end) { err = 1; break; }
+    int64_t r = q;
+    const int32_t ulen = dir_vlq(S.log, r, q + clen, err);     // the Snappy preamble
+    if (err || ulen < 0) { err = 1; break; }
+    if ((int64_t)ulen > S.max_block) { err = 2; break; }       // the reader's buffer is maxBlockSize
+    if (nb < S.blk_cap) {
+      SnappyBlock B;
+      B.file_pos = p;
+      B.data = q;
+      B.voff = 84 + (int64_t)total;
+      B.clen = (uint32_t)clen;
+      B.ulen = (uint32_t)ulen;
+      S.blocks[nb] = B;
+    }
+    nb++;
+    total += (uint64_t)ulen;
+    p = q + clen;
+  }
+  SnappyDirResult d;
+  d.nblk = nb;
+  d.total = total;
+  d.err = err;
+  d.pad = 0;
+  *S.dir = d;
+}
+
+__global__ void __launch_bounds__(64) k_snappy_lds(SnappyParams S) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const uint64_t b = blockIdx.x;
+  const SnappyBlock B = S.blocks[b];
+  const int lane = threadIdx.x;
+  uint8_t* out = lds;
+  uint8_t* in = lds + align16(S.max_block);
+  const uint8_t* src = S.log + B.data;
+  for (int64_t k = lane; k < (int64_t)B.clen; k += 64) in[k] = src[k];
+  __syncthreads();
+  int64_t p = 0;
+  while (in[p] & 0x80u) p++;                                   // preamble (validated by k_snappy_dir)
+  p++;
+  uint32_t flags = snappy_decode<true>(in, B.clen, p, out, B.ulen, lane, 64);
+  __syncthreads();
+  uint8_t* dst = S.vlog + B.voff;
+  for (int64_t k = lane; k < (int64_t)B.ulen; k += 64) dst[k] = out[k];
+  if (lane == 0) {
+    if (flags) {
+      SnappyWalk w;
+      w.count = 0;
+      w.flags = flags;
+      w.overflow = 0;
+      S.walk[b] = w;
+    } else {
+      walk_block(S, b, out, B.ulen);
+    }
+  }
+}
+
+__global__ void __launch_bounds__(64) k_snappy_global(SnappyParams S) {
+  const uint64_t b = (uint64_t)blockIdx.x * 64 + threadIdx.x;
+  if (b >= S.nblk) return;
+  const SnappyBlock B = S.blocks[b];
+  const uint8_t* in = S.log + B.data;
+  int64_t p = 0;
+  while (in[p] & 0x80u) p++;
+  p++;
+  uint8_t* out = S.vlog + B.voff;
+  const uint32_t flags = snappy_decode<false>(in, B.clen, p, out, B.ulen, 0, 1);
+  if (flags) {
+    SnappyWalk w;
+    w.count = 0;
+    w.flags = flags;
+    w.overflow = 0;
+    S.walk[b] = w;
+  } else {
+    walk_block(S, b, out, B.ulen);
+  }
+}
+
+__global__ void __launch_bounds__(256) k_snappy_rewrite(SnappyParams S) {
+  const uint64_t s = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (s == 0) {  // the internal build's stats: garbageSize, numEntries, maxDisplacement, hashCollisions, totalDisplacement
+    const uint8_t* ih = S.itab - 112;
+    uint8_t* oh = S.otab - 112;
+    for (int i = 52; i < 68; i++) oh[i] = ih[i];
+    for (int i = 84; i < 92; i++) oh[i] = ih[i];
+    for (int i = 96; i < 112; i++) oh[i] = ih[i];
+  }
+  if (s >= S.cap) return;
+  const uint8_t* is = S.itab + s * (uint64_t)(S.ihs + S.ias);
+  uint8_t* os = S.otab + s * (uint64_t)(S.hs + S.as);
+  uint64_t h = 0, a = 0;
+  for (int i = 0; i < S.ihs; i++) h |= (uint64_t)is[i] << (8 * i);
+  for (int i = 0; i < S.ias; i++) a |= (uint64_t)is[S.ihs + i] << (8 * i);
+  uint64_t fa = 0;
+  if (a != 0) {
+    uint64_t lo = 0, hi = S.nblk - 1;                          // the block holding virtual offset a
+    while (lo < hi) {
+      const uint64_t mid = (lo + hi + 1) / 2;
+      if ((uint64_t)S.blocks[mid].voff <= a) lo = mid; else hi = mid - 1;
+    }
+    const SnappyBlock B = S.blocks[lo];
+    const uint32_t rel = (uint32_t)(a - (uint64_t)B.voff);
+    const uint32_t* offs = S.rec_off + lo * S.mepb;
+    uint32_t l = 0, r = min(S.walk[lo].count, S.mepb);         // entryIndex: rank of rel in the block
+    while (l < r) {
+      const uint32_t m = (l + r) / 2;
+      if (offs[m] < rel) l = m + 1; else r = m;
+    }
+    if (l >= min(S.walk[lo].count, S.mepb) || offs[l] != rel) atomicOr(S.err, 1);
+    fa = ((uint64_t)B.file_pos << S.ebb) | l;
+  }
+  for (int i = 0; i < S.hs; i++) os[i] = (uint8_t)(h >> (8 * i));
+  for (int i = 0; i < S.as; i++) os[S.hs + i] = (uint8_t)(fa >> (8 * i));
+}
+
+void launch_snappy_dir(const SnappyParams& S, hipStream_t s) { hipLaunchKernelGGL(k_snappy_dir, 1, 64, 0, s, S); }
+
+hipError_t launch_snappy_decode(const SnappyParams& S, hipStream_t s) {
+  if (S.nblk == 0) return hipSuccess;
+  if (S.lds_bytes) {
+    hipError_t e = hipFuncSetAttribute((const void*)k_snappy_lds, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)S.lds_bytes);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_snappy_lds, dim3((uint32_t)S.nblk), 64, S.lds_bytes, s, S);
+  } else {
+    hipLaunchKernelGGL(k_snappy_global, dim3((uint32_t)((S.nblk + 63) / 64)), 64, 0, s, S);
+  }
+  return hipGetLastError();
+}
+
+void launch_snappy_rewrite(const SnappyParams& S, hipStream_t s) {
+  hipLaunchKernelGGL(k_snappy_rewrite, dim3((uint32_t)((S.cap + 255) / 256)), 256, 0, s, S);
+}
+
+}  // namespace sk

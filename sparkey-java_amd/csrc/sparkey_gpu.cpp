@@ -24,6 +24,7 @@
 #include "build_kernels.hpp"
 #include "lookup.hpp"
 #include "append.hpp"
+#include "snappy.hpp"
 
 using namespace sk;
 
@@ -60,7 +61,8 @@ struct LogHdr {
 };
 
 // LogHeader.read (LogHeader.java:55-88) + CommonHeader bounds (CommonHeader.java:38-43)
-int parse_log_header(const uint8_t* b, uint64_t hdr_len, uint64_t file_len, LogHdr* h, char* err, size_t err_len) {
+int parse_log_header(const uint8_t* b, uint64_t hdr_len, uint64_t file_len, LogHdr* h, char* err, size_t err_len,
+                     bool allow_snappy = false) {
   if (hdr_len < 84 || rd32(b) != kLogMagic) {
     set_err(err, err_len, "File is not a Sparkey log file");
     return SPARKEY_E_NOT_LOG;
@@ -103,8 +105,9 @@ int parse_log_header(const uint8_t* b, uint64_t hdr_len, uint64_t file_len, LogH
     set_err(err, err_len, "Corrupt log file: unknown compression type " + std::to_string(h->compression_type));
     return SPARKEY_E_CORRUPT_LOG;
   }
-  if (h->compression_type != 0) {
-    set_err(err, err_len, "Compressed (SNAPPY/ZSTD) logs are not supported by the GPU builder");
+  if (h->compression_type == 2 || (h->compression_type == 1 && !allow_snappy)) {
+    set_err(err, err_len, h->compression_type == 2 ? "ZSTD logs are not supported by the GPU builder"
+                                                   : "SNAPPY logs are not supported on this entry point");
     return SPARKEY_E_UNSUPPORTED;
   }
   return SPARKEY_OK;
@@ -257,6 +260,16 @@ struct sparkey_plan {
   int64_t* app_scan = nullptr;
   uint64_t c_app_map = 0;
   uint32_t* app_map = nullptr;
+  // SNAPPY front end (snappy.hpp): block directory, per-block walks, record offsets, virtual log,
+  // internal table
+  uint64_t c_sn_blocks = 0, c_sn_dir = 0, c_sn_walk = 0, c_sn_recoff = 0, c_sn_vlog = 0, c_sn_itab = 0, c_sn_err = 0;
+  SnappyBlock* sn_blocks = nullptr;
+  SnappyDirResult* sn_dir = nullptr;
+  SnappyWalk* sn_walk = nullptr;
+  uint32_t* sn_recoff = nullptr;
+  uint8_t* sn_vlog = nullptr;
+  uint8_t* sn_itab = nullptr;
+  int32_t* sn_err = nullptr;
   uint64_t c_seg_cls_cnt = 0, c_seg_cls_off = 0;
   uint32_t* seg_cls_cnt = nullptr;
   uint64_t* seg_cls_off = nullptr;
@@ -564,14 +577,218 @@ static void print_place_debug(const BuildParams& P) {
 
 static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t* d_log, uint64_t log_len,
                       uint8_t* d_out, uint64_t index_cap, const sparkey_build_opts* opts, hipStream_t s,
+                      sparkey_build_stats* stats_out, char* err, size_t err_len);
+
+// SNAPPY logs (snappy.hpp): block directory, decode into the virtual log, the normal
+// build over it into an internal table, then every slot's address rewritten to
+// (blockPosition << entryBlockBits) | entryIndex (IndexHash.java:270-283).
+static int plan_build_snappy(sparkey_plan* pl, const LogHdr& lh, const uint8_t* log_header, const uint8_t* d_log,
+                             uint64_t log_len, uint8_t* d_out, uint64_t index_cap, const sparkey_build_opts* opts,
+                             hipStream_t s, sparkey_build_stats* stats_out, char* err, size_t err_len) {
+  IndexParams ip;
+  int rc = make_index_params(lh, *opts, &ip, err, err_len);
+  if (rc) return rc;
+  if ((uint64_t)ip.index_size > index_cap) {
+    set_err(err, err_len, "index buffer too small: need " + std::to_string(ip.index_size));
+    return SPARKEY_E_BUFFER;
+  }
+  if (!d_log || !d_out) {
+    set_err(err, err_len, "null argument");
+    return SPARKEY_E_ARG;
+  }
+  if (lh.compression_block_size < 0) {  // new byte[maxBlockSize] (CompressedReader.java:40-49)
+    set_err(err, err_len, "Corrupt log file: negative compression block size");
+    return SPARKEY_E_CORRUPT_LOG;
+  }
+  HIP_TRY(hipSetDevice(pl->device));
+  if (!s) s = pl->own_stream;
+  hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+  const bool timed = pl->timer.enabled;
+  if (timed) {
+    for (auto& e : ev) HIP_TRY(hipEventCreate(&e));
+    HIP_TRY(hipEventRecord(ev[0], s));
+  }
+  auto drop_events = [&]() {
+    for (auto& e : ev)
+      if (e) (void)hipEventDestroy(e);
+  };
+  SnappyParams S;
+  memset(&S, 0, sizeof(S));
+  S.log = d_log;
+  S.data_end = lh.data_end;
+  S.max_block = lh.compression_block_size;
+  const uint64_t body = (uint64_t)std::max<int64_t>(0, lh.data_end - kLogHeaderSize);
+  HIP_TRY(grow(&pl->sn_blocks, pl->c_sn_blocks,
+               std::max<uint64_t>(1024, body / (uint64_t)std::max<int64_t>(16, lh.compression_block_size / 16))));
+  HIP_TRY(grow(&pl->sn_dir, pl->c_sn_dir, 1));
+  HIP_TRY(grow(&pl->sn_err, pl->c_sn_err, 1));
+  SnappyDirResult dir;
+  for (int attempt = 0;; attempt++) {
+    S.blocks = pl->sn_blocks;
+    S.blk_cap = pl->c_sn_blocks;
+    S.dir = pl->sn_dir;
+    launch_snappy_dir(S, s);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(&dir, pl->sn_dir, sizeof(dir), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (dir.err || dir.nblk <= S.blk_cap || attempt) break;
+    HIP_TRY(grow(&pl->sn_blocks, pl->c_sn_blocks, dir.nblk));
+  }
+  if (dir.err) {
+    drop_events();
+    set_err(err, err_len, dir.err == 2 ? "Corrupt log file: compressed block larger than the compression block size"
+                                       : "Corrupt log file: bad compressed block header");
+    return SPARKEY_E_CORRUPT_LOG;
+  }
+  const uint64_t nblk = dir.nblk;
+  const uint64_t vlen = (uint64_t)kLogHeaderSize + dir.total;
+  // the virtual log: a NONE header with the same counts, then the decompressed records
+  uint8_t vh[kLogHeaderSize];
+  memcpy(vh, log_header, kLogHeaderSize);
+  wr64(vh + 32, vlen);
+  wr32(vh + 64, 0u);
+  wr32(vh + 80, 1u);
+  HIP_TRY(grow(&pl->sn_vlog, pl->c_sn_vlog, vlen + 4096));
+  HIP_TRY(hipMemcpyAsync(pl->sn_vlog, vh, kLogHeaderSize, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemsetAsync(pl->sn_vlog + vlen, 0, 4096, s));
+  const uint32_t mepb = (uint32_t)std::max<int32_t>(1, lh.max_entries_per_block);
+  HIP_TRY(grow(&pl->sn_walk, pl->c_sn_walk, nblk));
+  HIP_TRY(grow(&pl->sn_recoff, pl->c_sn_recoff, nblk * mepb));
+  S.nblk = nblk;
+  S.vlog = pl->sn_vlog;
+  S.walk = pl->sn_walk;
+  S.rec_off = pl->sn_recoff;
+  S.mepb = mepb;
+  // LDS: the decoded block, then its stream (at most Snappy's maxCompressedLength = 32 + n + n/6)
+  const int64_t mb = lh.compression_block_size;
+  const int64_t lds = ((mb + 15) & ~15LL) + ((32 + mb + mb / 6 + 15) & ~15LL);
+  S.lds_bytes = lds <= 160 * 1024 ? (uint32_t)lds : 0u;
+  if (nblk) {
+    hipError_t e = launch_snappy_decode(S, s);
+    if (e != hipSuccess && S.lds_bytes) {  // the LDS size was refused: lane-serial global decode
+      (void)hipGetLastError();
+      S.lds_bytes = 0;
+      e = launch_snappy_decode(S, s);
+    }
+    if (e != hipSuccess) {
+      drop_events();
+      set_err(err, err_len, std::string("HIP error: ") + hipGetErrorString(e) + " in snappy decode");
+      return SPARKEY_E_GPU;
+    }
+  }
+  // compose the block walks: a block either starts at a record (CompressedWriter flushes after a
+  // spanning record, CompressedWriter.java:71-75) or lies wholly inside the record spanning into it
+  std::vector<SnappyWalk> walks(nblk);
+  std::vector<SnappyBlock> blocks(nblk);
+  if (nblk) {
+    HIP_TRY(hipMemcpyAsync(walks.data(), pl->sn_walk, nblk * sizeof(SnappyWalk), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(blocks.data(), pl->sn_blocks, nblk * sizeof(SnappyBlock), hipMemcpyDeviceToHost, s));
+  }
+  if (timed) HIP_TRY(hipEventRecord(ev[1], s));
+  HIP_TRY(hipStreamSynchronize(s));
+  int64_t carry = 0;
+  for (uint64_t b = 0; b < nblk; b++) {
+    const SnappyWalk& w = walks[b];
+    if (w.flags & kWalkBadStream) {
+      drop_events();
+      set_err(err, err_len, "Corrupt log file: bad snappy stream in block at " + std::to_string(blocks[b].file_pos));
+      return SPARKEY_E_CORRUPT_LOG;
+    }
+    if (carry == 0) {
+      if (w.flags) {
+        drop_events();
+        set_err(err, err_len, (w.flags & kWalkTooMany)
+                                  ? "Corrupt log file: more entries in a block than maxEntriesPerBlock"
+                                  : "Corrupt log file: bad record header in block at " +
+                                        std::to_string(blocks[b].file_pos));
+        return SPARKEY_E_CORRUPT_LOG;
+      }
+      carry = w.overflow;
+    } else if (carry >= (int64_t)blocks[b].ulen) {
+      carry -= blocks[b].ulen;
+    } else {
+      drop_events();
+      set_err(err, err_len, "a record ends inside a later compressed block (not a layout CompressedWriter writes)");
+      return SPARKEY_E_UNSUPPORTED;
+    }
+  }
+  if (carry) {
+    drop_events();
+    set_err(err, err_len, "Corrupt log file: the last record runs past dataEnd");
+    return SPARKEY_E_CORRUPT_LOG;
+  }
+  // the normal build over the virtual log, into an internal table
+  sparkey_build_opts o2 = *opts;
+  o2.method = ip.in_memory ? SPARKEY_METHOD_IN_MEMORY : SPARKEY_METHOD_SORTING;
+  LogHdr vlh;
+  rc = parse_log_header(vh, kLogHeaderSize, vlen, &vlh, err, err_len);
+  IndexParams vip;
+  if (!rc) rc = make_index_params(vlh, o2, &vip, err, err_len);
+  if (rc) {
+    drop_events();
+    return rc;
+  }
+  HIP_TRY(grow(&pl->sn_itab, pl->c_sn_itab, (uint64_t)vip.index_size));
+  rc = plan_build(pl, vh, pl->sn_vlog, vlen, pl->sn_itab, (uint64_t)vip.index_size, &o2, s, stats_out, err, err_len);
+  if (rc) {
+    drop_events();
+    return rc;
+  }
+  if (timed) HIP_TRY(hipEventRecord(ev[2], s));
+  uint8_t hdr[kIndexHeaderSize];
+  index_header_template(lh, ip, opts->hash_seed, hdr);
+  HIP_TRY(hipMemcpyAsync(d_out, hdr, kIndexHeaderSize, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemsetAsync(pl->sn_err, 0, sizeof(int32_t), s));
+  S.itab = pl->sn_itab + kIndexHeaderSize;
+  S.otab = d_out + kIndexHeaderSize;
+  S.cap = ip.cap;
+  S.ihs = vip.hash_size;
+  S.ias = vip.addr_size;
+  S.hs = ip.hash_size;
+  S.as = ip.addr_size;
+  S.ebb = ip.ebb;
+  S.err = pl->sn_err;
+  if (nblk == 0) S.nblk = 1;  // no block: every slot is empty (the search is never reached)
+  launch_snappy_rewrite(S, s);
+  HIP_TRY(hipGetLastError());
+  int32_t rerr = 0;
+  HIP_TRY(hipMemcpyAsync(&rerr, pl->sn_err, sizeof(rerr), hipMemcpyDeviceToHost, s));
+  hipEvent_t ev_end = nullptr;
+  if (timed) {
+    HIP_TRY(hipEventCreate(&ev_end));
+    HIP_TRY(hipEventRecord(ev_end, s));
+  }
+  HIP_TRY(hipStreamSynchronize(s));
+  if (timed) {  // stages of the front end and the rewrite around the inner build's own stages
+    float t0 = 0.f, t1 = 0.f;
+    (void)hipEventElapsedTime(&t0, ev[0], ev[1]);
+    (void)hipEventElapsedTime(&t1, ev[2], ev_end);
+    pl->stage_names.insert(pl->stage_names.begin(), "snappy_decode");
+    pl->stage_ms.insert(pl->stage_ms.begin(), t0);
+    pl->stage_names.push_back("snappy_rewrite");
+    pl->stage_ms.push_back(t1);
+    (void)hipEventDestroy(ev_end);
+  }
+  drop_events();
+  if (rerr) {
+    set_err(err, err_len, "internal error: a slot's record is not a block record start");
+    return SPARKEY_E_CORRUPT_LOG;
+  }
+  return SPARKEY_OK;
+}
+
+static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t* d_log, uint64_t log_len,
+                      uint8_t* d_out, uint64_t index_cap, const sparkey_build_opts* opts, hipStream_t s,
                       sparkey_build_stats* stats_out, char* err, size_t err_len) {
   if (!pl || !log_header || !opts) {
     set_err(err, err_len, "null argument");
     return SPARKEY_E_ARG;
   }
   LogHdr lh;
-  int rc = parse_log_header(log_header, 84, log_len, &lh, err, err_len);
+  int rc = parse_log_header(log_header, 84, log_len, &lh, err, err_len, true);
   if (rc) return rc;
+  if (lh.compression_type == 1)
+    return plan_build_snappy(pl, lh, log_header, d_log, log_len, d_out, index_cap, opts, s, stats_out, err, err_len);
   IndexParams ip;
   rc = make_index_params(lh, *opts, &ip, err, err_len);
   if (rc) return rc;
@@ -1059,7 +1276,8 @@ void sparkey_plan_destroy(sparkey_plan* pl) {
                   pl->parts, pl->pdbg, pl->p1_fill, pl->scan_u64, pl->scan_mp, pl->desc, pl->p1_hist, pl->p1_off, pl->d_status, pl->dbg, pl->wcount, pl->woff, pl->small,
                   pl->eseg, pl->seg_cnt, pl->seg_off, pl->seg_mark, pl->seg_start,
                   pl->seg_cls_cnt, pl->seg_cls_off, pl->p2tab,
-                  pl->app_i64, pl->app_u32, pl->app_u64, pl->app_scan, pl->app_map};
+                  pl->app_i64, pl->app_u32, pl->app_u64, pl->app_scan, pl->app_map,
+                  pl->sn_blocks, pl->sn_dir, pl->sn_walk, pl->sn_recoff, pl->sn_vlog, pl->sn_itab, pl->sn_err};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (pl->h_status) (void)hipHostFree(pl->h_status);
@@ -1080,7 +1298,7 @@ int64_t sparkey_index_size(const uint8_t* log_header, uint64_t header_len, const
   if (!log_header || !opts) return SPARKEY_E_ARG;
   LogHdr lh;
   const uint64_t data_end = header_len >= 40 ? rd64(log_header + 32) : 0;
-  int rc = parse_log_header(log_header, header_len, std::max<uint64_t>(header_len, data_end), &lh, nullptr, 0);
+  int rc = parse_log_header(log_header, header_len, std::max<uint64_t>(header_len, data_end), &lh, nullptr, 0, true);
   if (rc) return rc;
   IndexParams ip;
   rc = make_index_params(lh, *opts, &ip, nullptr, 0);
@@ -1096,7 +1314,7 @@ int sparkey_build_index_mem(const uint8_t* log, uint64_t log_len, uint8_t* index
     return SPARKEY_E_ARG;
   }
   LogHdr lh;
-  int rc = parse_log_header(log, log_len, log_len, &lh, err, err_len);
+  int rc = parse_log_header(log, log_len, log_len, &lh, err, err_len, true);
   if (rc) return rc;
   IndexParams ip;
   rc = make_index_params(lh, *opts, &ip, err, err_len);
@@ -1178,7 +1396,7 @@ int sparkey_build_index_file(const char* log_path, const char* index_out_path, c
   const int64_t isz = sparkey_index_size(hlog, log_len, opts);
   if (isz < 0) {
     LogHdr lh;
-    int rc = parse_log_header(hlog, log_len, log_len, &lh, err, err_len);
+    int rc = parse_log_header(hlog, log_len, log_len, &lh, err, err_len, true);
     (void)hipHostFree(hlog);
     if (!rc) set_err(err, err_len, code_message((int)isz));
     return rc ? rc : (int)isz;

@@ -1,0 +1,89 @@
+"""GPU parity for SNAPPY logs: the HIP front end (block directory, wave-per-block
+Snappy decode, record walk, address rewrite) plus the normal build must give .spi bytes identical to
+the oracle's restatement (CompressedReader block positions, entryIndex addresses; pinned in
+test_compressed_oracle.py).  Bit-exact, IN_MEMORY and SORTING.
+"""
+import random
+import struct
+
+import pytest
+
+import oracle
+from snappy_log import CompressedLog
+from test_compressed_oracle import _compressed, _ops
+
+pytestmark = pytest.mark.gpu
+
+IN_MEMORY, SORTING = 1, 2
+
+
+def check(native, log, seed=4321, method=IN_MEMORY, hash_size=0):
+    want = oracle.build_index(log, seed, hash_size=hash_size, method=method)
+    opts = native.make_opts(hash_size=hash_size, hash_seed=seed, method=method)
+    got, _ = native.build_index_mem(log, opts)
+    assert got == want, "first differing byte %d of %d" % (
+        next((i for i in range(min(len(got), len(want))) if got[i] != want[i]), -1), len(want))
+    return got
+
+
+@pytest.mark.parametrize("block_size", [10, 16, 100, 1024, 4096, 65536, 131072])
+@pytest.mark.parametrize("method", [IN_MEMORY, SORTING])
+def test_unique_puts(native, block_size, method):
+    rng = random.Random(block_size)
+    check(native, _compressed(_ops(rng, 1500, 10 ** 9, 0.0, 200), block_size), method=method)
+
+
+@pytest.mark.parametrize("block_size", [10, 300, 1024, 8192])
+@pytest.mark.parametrize("method", [IN_MEMORY, SORTING])
+def test_overwrites_and_deletes(native, block_size, method):
+    rng = random.Random(block_size + 1)
+    check(native, _compressed(_ops(rng, 3000, 800, 0.2, 120), block_size), method=method)
+
+
+@pytest.mark.parametrize("literal_only", [False, True])
+def test_spanning_records(native, literal_only):
+    rng = random.Random(3)
+    log = _compressed(_ops(rng, 400, 10 ** 9, 0.0, 5000), 512, literal_only=literal_only)
+    check(native, log)
+
+
+@pytest.mark.parametrize("hash_size", [4, 8])
+def test_write_hash_benchmark_snappy(native, hash_size):
+    cl = CompressedLog(1024, file_identifier=77)
+    for i in range(1000):
+        cl.put(b"key_%d" % i, b"value_%d" % i)
+    check(native, cl.finish(), seed=1234, hash_size=hash_size)
+
+
+def test_empty_and_single(native):
+    check(native, CompressedLog(1024).finish())
+    cl = CompressedLog(1024)
+    cl.put(b"k", b"v")
+    check(native, cl.finish())
+
+
+def test_c2_shaped(native):
+    """C2's record shape (16 B keys, 100 B values), 200K records, 64 KiB blocks."""
+    rng = random.Random(9)
+    cl = CompressedLog(65536, file_identifier=5)
+    for i in range(200000):
+        cl.put(struct.pack("<QQ", i, rng.getrandbits(64)), bytes([i & 0xFF]) * 60 + rng.randbytes(40))
+    check(native, cl.finish(), seed=99)
+
+
+def test_errors(native):
+    opts = native.make_opts(hash_seed=1)
+    log = _compressed([("put", b"k%d" % i, b"v" * 50) for i in range(200)], 256)
+    bad = bytearray(log)
+    bad[64] = 2                                                   # ZSTD
+    with pytest.raises(OSError):
+        native.build_index_mem(bytes(bad), opts)
+    bad = bytearray(log)
+    bad[84] = 0xFF                                                # block size VLQ runs on / past dataEnd
+    bad[85] = 0xFF
+    with pytest.raises(OSError):
+        native.build_index_mem(bytes(bad), opts)
+    bad = bytearray(log)
+    struct.pack_into("<i", bad, 68, 16)                           # blocks larger than the block size
+    with pytest.raises(OSError):
+        native.build_index_mem(bytes(bad), opts)

@@ -164,7 +164,7 @@ def test_errors(native):
     with pytest.raises((OSError, RuntimeError)):
         native.build_index_mem(bytes(bad), opts)
     bad = bytearray(log)
-    bad[64] = 1                                                    # SNAPPY: not on this path
+    bad[64] = 1                                                    # SNAPPY flag over NONE bytes: corrupt blocks
     with pytest.raises(OSError):
         native.build_index_mem(bytes(bad), opts)
 
