@@ -32,7 +32,7 @@ PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_pmc_summary.json")
 HASH_SEED = 0x2545F491
 
 
-def stage_bytes(stage, n, data_end, slot, cap, passes=2):
+def stage_bytes(stage, n, data_end, slot, cap, passes=2, comp_end=None):
     """Algorithmic bytes per launch of each stage.  passes: partition passes left to
     the partition stage (1 when the uniform framing wrote the digit regions itself)."""
     log = data_end - 84
@@ -44,6 +44,9 @@ def stage_bytes(stage, n, data_end, slot, cap, passes=2):
         "place": 16 * n + slot * cap,         # entries read once, every slot written once
         "stats": slot * cap,                  # table read once
         "exact": 3 * 16 * n + 2 * slot * cap,  # entries read, grouped, replayed; segment slots cleared + written
+        # SNAPPY (data_end = the virtual log's end): blocks read once, decompressed bytes written once
+        "snappy_decode": (comp_end or data_end) - 84 + log,
+        "snappy_rewrite": 2 * slot * cap,      # internal table read, final table written
     }.get(stage, 0)
 
 
@@ -63,6 +66,8 @@ WORKLOADS = {
     "c5": {"name": "C5: C3 log, SORTING constructionMethod", "sorting": True, "path": 0},
     "churn": {"name": "C2 shape with overwrites and DELETEs: keys from a pool of 0.8 n, 10% DELETE records, "
                       "IN_MEMORY (exact replay over slot segments)", "sorting": False, "path": 2},
+    "snappy": {"name": "C2 records (10M PUTs x (16 B key, 100 B value)), CompressionType.SNAPPY, 64 KiB blocks, "
+                       "IN_MEMORY", "sorting": False, "path": 0},
     "append": {"name": "GPU log producer (batched LogWriter.put)", "sorting": False, "path": 0},
     "get": {"name": "batched IndexHash.get of every key of the C2 index (log and index resident in HBM)",
             "sorting": False, "path": 0},
@@ -167,6 +172,8 @@ def single_gpu(args, dev):
         log_np = synth.fixed_log(n, 16, 100, seed=args.seed, file_id=0x5EED0000)
     elif args.workload in ("c3", "c5"):
         log_np = synth.mixed_log(n, 8, 64, 100, seed=args.seed + 2)
+    elif args.workload == "snappy":
+        log_np = synth.snappy_log(synth.fixed_log(n, 16, 100, seed=args.seed, file_id=0x5EED0000), 118, 65536)
     else:
         log_np = synth.churn_log(n, int(n * 0.8), 0.1, seed=args.seed + 4)
     gen_s = time.time() - t0
@@ -205,7 +212,9 @@ def single_gpu(args, dev):
     stage_ms = {k: v / args.steps for k, v in stage_acc.items()}
     dom = max(stage_ms, key=lambda k: stage_ms[k]) if stage_ms else None
     passes = stats.partition_passes
-    dom_bytes = stage_bytes(dom, n, log_len, slot, cap, passes) if dom else 0
+    # SNAPPY: the inner build's stages run over the virtual log (84 + 118 n bytes for C2 records)
+    frame_end = 84 + 118 * n if args.workload == "snappy" else log_len
+    dom_bytes = stage_bytes(dom, n, frame_end, slot, cap, passes, comp_end=log_len) if dom else 0
     achieved = dom_bytes / (stage_ms[dom] * 1e-3) / 1e9 if dom and stage_ms[dom] > 0 else 0.0
     b_alg = (log_len - 84) + 112 + slot * cap
     assert stats.placement_path == wl["path"] and stats.framing_path in (0, 2), stats.as_dict()
@@ -247,7 +256,7 @@ def single_gpu(args, dev):
             g_stage = {k: v / g_steps for k, v in g_acc.items()}
             general = {"ms_per_step": g_el * 1000.0 / g_steps, "keys_per_s": n * g_steps / g_el,
                        "stage_ms": g_stage,
-                       "frame_achieved_gbs": stage_bytes("frame", n, log_len, slot, cap) / (g_stage["frame"] * 1e-3) / 1e9}
+                       "frame_achieved_gbs": stage_bytes("frame", n, frame_end, slot, cap) / (g_stage["frame"] * 1e-3) / 1e9}
         finally:
             del os.environ["SPARKEY_NO_UNIFORM"]
 
@@ -277,6 +286,8 @@ def single_gpu(args, dev):
                          (dom, stats.framing_path if dom == "frame" else passes), dom)),
                      "algorithmic_bytes_per_launch": dom_bytes, "avg_launch_ms": stage_ms.get(dom) if dom else None},
         "build_hbm_gbs": b_alg / (ms_per_step * 1e-3) / 1e9,
+        "stage_gbs": {k: stage_bytes(k, n, frame_end, slot, cap, passes, comp_end=log_len) / (v * 1e-3) / 1e9
+                      for k, v in stage_ms.items() if v > 0 and stage_bytes(k, n, frame_end, slot, cap, passes)},
         "build_algorithmic_bytes": b_alg,
         "stage_ms": stage_ms,
         "framing": {0: "k_frame (speculative)", 1: "serial walk", 2: "k_frame_uniform (uniform records)"}[stats.framing_path],

@@ -153,3 +153,32 @@ def churn_log(n: int, pool: int, p_del: float, key_len: int = 16, value_len: int
         _header(n - n_del, key_len, value_len if n > n_del else 0, put_size, LOG_HEADER_SIZE + total, file_id,
                 block_size, n_del, total - put_size), dtype=np.uint8)
     return buf
+
+
+def snappy_log(log: np.ndarray, rec: int, block_size: int) -> np.ndarray:
+    """The SNAPPY log a reference writer produces for the same uniform R-byte PUT records (a NONE log
+    from fixed_log): CompressedWriter.smartFlush (CompressedWriter.java:111-118) closes a block when
+    the next record no longer fits, so every block holds block_size // R records; each block is
+    VLQ(compressedSize) || the Snappy stream of its bytes (CompressedOutputStream.java:47-58), here from
+    libsnappy through pyarrow.  Records longer than the block size are not handled here."""
+    import pyarrow as pa
+    from .log_writer import vlq_bytes
+    assert 10 <= rec <= block_size
+    per = block_size // rec
+    hdr = LogHeader.from_bytes(log[:LOG_HEADER_SIZE].tobytes())
+    body = log[LOG_HEADER_SIZE:hdr.data_end]
+    step = per * rec
+    parts = []
+    for o in range(0, body.size, step):
+        comp = pa.compress(body[o:o + step], codec="snappy", asbytes=True)
+        parts.append(vlq_bytes(len(comp)))
+        parts.append(comp)
+    data = b"".join(parts)
+    hdr.compression_type = 1
+    hdr.compression_block_size = block_size
+    hdr.max_entries_per_block = per if body.size else 0
+    hdr.data_end = LOG_HEADER_SIZE + len(data)
+    out = np.empty(hdr.data_end, dtype=np.uint8)
+    out[:LOG_HEADER_SIZE] = np.frombuffer(hdr.to_bytes(), dtype=np.uint8)
+    out[LOG_HEADER_SIZE:] = np.frombuffer(data, dtype=np.uint8)
+    return out

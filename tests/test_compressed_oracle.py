@@ -147,3 +147,16 @@ def test_zstd_is_unsupported():
     clog[64] = 2
     with pytest.raises(oracle.OracleError):
         oracle.build_index(bytes(clog), 1)
+
+
+@pytest.mark.parametrize("block_size", [118, 500, 4096, 65536])
+def test_synth_snappy_log_matches_writer(block_size):
+    """bench's SNAPPY generator (synth.snappy_log) writes what CompressedWriter writes."""
+    from sparkey import synth
+    log = synth.fixed_log(3000, 16, 100, seed=2, file_id=0x777)
+    cl = CompressedLog(block_size, file_identifier=0x777)
+    body = log[84:].tobytes()
+    for i in range(3000):
+        r = body[i * 118:(i + 1) * 118]
+        cl.put(r[2:18], r[18:])
+    assert synth.snappy_log(log, 118, block_size).tobytes() == cl.finish()
