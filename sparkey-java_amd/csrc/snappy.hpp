@@ -43,12 +43,14 @@ struct SnappyDirResult {
 
 struct SnappyParams {
   const uint8_t* log;
+  int64_t log_len;          // readable bytes of `log` (vector loads stay inside)
   int64_t data_end;
   int64_t max_block;        // compressionBlockSize: the reader's uncompressed buffer
   SnappyBlock* blocks;
   uint64_t blk_cap;
   SnappyDirResult* dir;
   uint8_t* vlog;            // virtual log (84 header bytes written by the host)
+  int64_t vlog_len;         // bytes of vlog
   SnappyWalk* walk;
   uint32_t* rec_off;        // [block * mepb + j]: record j's offset inside block
   uint32_t mepb;            // maxEntriesPerBlock (>= 1)

@@ -16,6 +16,26 @@ namespace {
 
 __device__ __forceinline__ int64_t align16(int64_t x) { return (x + 15) & ~15LL; }
 
+// len bytes: one byte per lane per round for short copies (one LDS round trip for the usual
+// <= 64-byte element), 16 consecutive bytes per lane per round for long ones
+__device__ __forceinline__ void copy_bytes(uint8_t* dst, const uint8_t* src, int64_t len, int lane, int nlanes) {
+  if (len <= 4 * nlanes) {
+    for (int64_t k = lane; k < len; k += nlanes) dst[k] = src[k];
+    return;
+  }
+  for (int64_t k = (int64_t)lane * 16; k < len; k += (int64_t)nlanes * 16) {
+    if (k + 16 <= len) {
+      uint8_t t[16];
+#pragma unroll
+      for (int i = 0; i < 16; i++) t[i] = src[k + i];
+#pragma unroll
+      for (int i = 0; i < 16; i++) dst[k + i] = t[i];
+    } else {
+      for (int64_t i = k; i < len; i++) dst[i] = src[i];
+    }
+  }
+}
+
 // Snappy raw format: varint uncompressed length, then literal (tag 00), copy-1 (01), copy-2 (10) and
 // copy-4 (11) elements.  Lanes [lane, nlanes) share each element's copy; every lane parses the same
 // tags (uniform control flow).  A match copies out[o + k] = out[o - off + k % off]: only bytes before
@@ -26,57 +46,70 @@ __device__ uint32_t snappy_decode(const uint8_t* in, int64_t n, int64_t p, uint8
                                   int nlanes) {
   int64_t o = 0;
   while (p < n) {
-    const uint32_t t = in[p++];
+    // the tag and the four bytes after it in one round trip
+    const uint32_t t = in[p];
+    const uint32_t e0 = p + 1 < n ? in[p + 1] : 0u, e1 = p + 2 < n ? in[p + 2] : 0u;
+    const uint32_t e2 = p + 3 < n ? in[p + 3] : 0u, e3 = p + 4 < n ? in[p + 4] : 0u;
+    p++;
     int64_t len, off = 0;
     if ((t & 3u) == 0) {
       len = (t >> 2) + 1;
       if (len > 60) {
         const int nb = (int)len - 60;
         if (p + nb > n) return kWalkBadStream;
-        len = 0;
-        for (int i = 0; i < nb; i++) len |= (int64_t)in[p + i] << (8 * i);
+        len = (int64_t)e0 | (nb > 1 ? (int64_t)e1 << 8 : 0) | (nb > 2 ? (int64_t)e2 << 16 : 0) |
+              (nb > 3 ? (int64_t)e3 << 24 : 0);
         len += 1;
         p += nb;
       }
       if (p + len > n || o + len > ulen) return kWalkBadStream;
-      for (int64_t k = lane; k < len; k += nlanes) out[o + k] = in[p + k];
+      copy_bytes(out + o, in + p, len, lane, nlanes);
       p += len;
     } else {
       if ((t & 3u) == 1) {
         if (p + 1 > n) return kWalkBadStream;
         len = ((t >> 2) & 7u) + 4;
-        off = ((int64_t)(t >> 5) << 8) | in[p];
+        off = ((int64_t)(t >> 5) << 8) | e0;
         p += 1;
       } else if ((t & 3u) == 2) {
         if (p + 2 > n) return kWalkBadStream;
         len = (t >> 2) + 1;
-        off = (int64_t)in[p] | ((int64_t)in[p + 1] << 8);
+        off = (int64_t)e0 | ((int64_t)e1 << 8);
         p += 2;
       } else {
         if (p + 4 > n) return kWalkBadStream;
         len = (t >> 2) + 1;
-        off = (int64_t)in[p] | ((int64_t)in[p + 1] << 8) | ((int64_t)in[p + 2] << 16) | ((int64_t)in[p + 3] << 24);
+        off = (int64_t)e0 | ((int64_t)e1 << 8) | ((int64_t)e2 << 16) | ((int64_t)e3 << 24);
         p += 4;
       }
       if (off == 0 || off > o || o + len > ulen) return kWalkBadStream;
-      for (int64_t k = lane; k < len; k += nlanes) out[o + k] = out[o - off + k % off];
+      if (off >= len) copy_bytes(out + o, out + o - off, len, lane, nlanes);
+      else
+        for (int64_t k = lane; k < len; k += nlanes) out[o + k] = out[o - off + k % off];
     }
     o += len;
-    if (kSync) __syncthreads();
+    if (kSync) __builtin_amdgcn_wave_barrier();  // one-wave workgroup: LDS ops run in order
   }
   return o == ulen ? 0u : kWalkBadStream;
 }
 
 // The block's records, assuming it starts at a record (SparkeyLogIterator.java:86-138): their offsets
-// go to rec_off, and the last record's bytes past the block end to overflow.
-__device__ void walk_block(const SnappyParams& S, uint64_t b, const uint8_t* buf, int64_t ulen) {
+// go to rec_off, and the last record's bytes past the block end to overflow.  The first four header
+// bytes are read together; one-byte VLQs (the common case) decode from them without another trip.
+__device__ __forceinline__ void walk_block(const SnappyParams& S, uint64_t b, const uint8_t* buf, int64_t ulen) {
   auto at = [&](int64_t i) -> uint32_t { return buf[i]; };
   uint32_t j = 0, flags = 0;
   int64_t u = 0;
+  uint32_t* offs = S.rec_off + b * S.mepb;
   while (u < ulen) {
-    if (j < S.mepb) S.rec_off[b * S.mepb + j] = (uint32_t)u;
+    if (j < S.mepb) offs[j] = (uint32_t)u;
     else flags |= kWalkTooMany;
     j++;
+    const uint32_t b0 = buf[u], b1 = u + 1 < ulen ? buf[u + 1] : 0x80u;
+    if (b0 < 0x80u && b1 < 0x80u) {  // VLQ(first) VLQ(second), one byte each
+      u += 2 + (b0 == 0 ? b1 : (b0 - 1) + b1);
+      continue;
+    }
     const RecHdr h = decode_header(at, u, ulen);
     if (h.rc || h.klen < 0 || h.vlen < 0) {
       flags |= kWalkBadHeader;
@@ -91,11 +124,44 @@ __device__ void walk_block(const SnappyParams& S, uint64_t b, const uint8_t* buf
   S.walk[b] = w;
 }
 
-__device__ __forceinline__ int32_t dir_vlq(const uint8_t* log, int64_t& p, int64_t end, int32_t& err) {
+// The 16 bytes from p as two little-endian words, from one pair of aligned 16-byte loads (one memory
+// round trip per hop of the block chain); byte loads near the end of the buffer.
+struct Window {
+  uint64_t lo, hi;
+  __device__ __forceinline__ uint32_t at(int j) const {
+    return (uint32_t)((j < 8 ? lo >> (8 * j) : hi >> (8 * (j - 8))) & 0xffu);
+  }
+};
+
+__device__ __forceinline__ Window load_window(const uint8_t* log, int64_t p, int64_t len) {
+  Window w;
+  const int64_t a = p & ~15LL;
+  if (a + 32 <= len) {
+    const uint4 v0 = *(const uint4*)(log + a);
+    const uint4 v1 = *(const uint4*)(log + a + 16);
+    const uint64_t q0 = v0.x | ((uint64_t)v0.y << 32), q1 = v0.z | ((uint64_t)v0.w << 32);
+    const uint64_t q2 = v1.x | ((uint64_t)v1.y << 32), q3 = v1.z | ((uint64_t)v1.w << 32);
+    const int o = (int)(p - a);
+    const uint64_t s0 = o >= 8 ? q1 : q0, s1 = o >= 8 ? q2 : q1, s2 = o >= 8 ? q3 : q2;
+    const int sh = 8 * (o & 7);
+    w.lo = sh ? (s0 >> sh) | (s1 << (64 - sh)) : s0;
+    w.hi = sh ? (s1 >> sh) | (s2 << (64 - sh)) : s1;
+  } else {
+    w.lo = w.hi = 0;
+    for (int j = 0; j < 16 && p + j < len; j++) {
+      if (j < 8) w.lo |= (uint64_t)log[p + j] << (8 * j);
+      else w.hi |= (uint64_t)log[p + j] << (8 * (j - 8));
+    }
+  }
+  return w;
+}
+
+// Util.readUnsignedVLQInt over the window from byte j; bytes at >= avail are EOF.
+__device__ __forceinline__ int32_t dir_vlq(const Window& w, int& j, int avail, int32_t& err) {
   uint32_t v = 0;
   for (int i = 0; i < 5; i++) {
-    if (p >= end) { err = 1; return 0; }
-    const uint32_t b = log[p++];
+    if (j >= avail) { err = 1; return 0; }
+    const uint32_t b = w.at(j++);
     if (b < 0x80u) return (int32_t)(v | (b << (7 * i)));
     v |= (b & 0x7fu) << (7 * i);
   }
@@ -111,13 +177,16 @@ __global__ void __launch_bounds__(64) k_snappy_dir(SnappyParams S) {
   uint64_t nb = 0, total = 0;
   int32_t err = 0;
   while (p < S.data_end) {
-    int64_t q = p;
-    const int32_t clen = dir_vlq(S.log, q, S.data_end, err);   // Util.readUnsignedVLQInt
+    const Window w = load_window(S.log, p, S.log_len);
+    int j = 0;
+    const int32_t clen = dir_vlq(w, j, (int)min<int64_t>(16, S.data_end - p), err);   // Util.readUnsignedVLQInt
+    const int64_t q = p + j;
     if (err || clen < 0 || q + clen > S.data_end) { err = 1; break; }
-    int64_t r = q;
-    const int32_t ulen = dir_vlq(S.log, r, q + clen, err);     // the Snappy preamble
+    const int32_t ulen = dir_vlq(w, j, (int)min<int64_t>(16, q + clen - p), err);     // the Snappy preamble
     if (err || ulen < 0) { err = 1; break; }
-    if ((int64_t)ulen > S.max_block) { err = 2; break; }       // the reader's buffer is maxBlockSize
+    // the reader's buffers: maxBlockSize decompressed, Snappy.maxCompressedLength(maxBlockSize) compressed
+    // (CompressedReader.java:40-49)
+    if ((int64_t)ulen > S.max_block || (int64_t)clen > 32 + S.max_block + S.max_block / 6) { err = 2; break; }
     if (nb < S.blk_cap) {
       SnappyBlock B;
       B.file_pos = p;
@@ -144,18 +213,43 @@ __global__ void __launch_bounds__(64) k_snappy_lds(SnappyParams S) {
   const uint64_t b = blockIdx.x;
   const SnappyBlock B = S.blocks[b];
   const int lane = threadIdx.x;
-  uint8_t* out = lds;
-  uint8_t* in = lds + align16(S.max_block);
-  const uint8_t* src = S.log + B.data;
-  for (int64_t k = lane; k < (int64_t)B.clen; k += 64) in[k] = src[k];
+  // outb: the decoded block at the alignment of its place in the virtual log; inb: the stream at the
+  // alignment of its place in the log, so that both sides move as 16-byte words
+  uint8_t* outb = lds;
+  uint8_t* inb = lds + align16(S.max_block) + 16;
+  const int64_t ga = B.data & ~15LL;
+  uint8_t* in = inb + (B.data - ga);
+  {
+    const int64_t nw = (B.data - ga + B.clen + 15) / 16;
+#pragma unroll 4
+    for (int64_t w = lane; w < nw; w += 64) {
+      const int64_t g = ga + 16 * w;
+      if (g + 16 <= S.log_len) {
+        *(uint4*)(inb + 16 * w) = *(const uint4*)(S.log + g);
+      } else {
+        for (int i = 0; i < 16 && g + i < S.log_len; i++) inb[16 * w + i] = S.log[g + i];
+      }
+    }
+  }
+  const int64_t oa = B.voff & ~15LL;
+  uint8_t* out = outb + (B.voff - oa);
   __syncthreads();
   int64_t p = 0;
   while (in[p] & 0x80u) p++;                                   // preamble (validated by k_snappy_dir)
   p++;
   uint32_t flags = snappy_decode<true>(in, B.clen, p, out, B.ulen, lane, 64);
   __syncthreads();
-  uint8_t* dst = S.vlog + B.voff;
-  for (int64_t k = lane; k < (int64_t)B.ulen; k += 64) dst[k] = out[k];
+  {
+    const int64_t lo = B.voff - oa, hi = lo + B.ulen;  // the block's bytes in outb coordinates
+    const int64_t nw = (hi + 15) / 16;
+    for (int64_t w = lane; w < nw; w += 64) {
+      if (16 * w >= lo && 16 * w + 16 <= hi) {
+        *(uint4*)(S.vlog + oa + 16 * w) = *(const uint4*)(outb + 16 * w);
+      } else {
+        for (int64_t i = max<int64_t>(16 * w, lo); i < min<int64_t>(16 * w + 16, hi); i++) S.vlog[oa + i] = outb[i];
+      }
+    }
+  }
   if (lane == 0) {
     if (flags) {
       SnappyWalk w;

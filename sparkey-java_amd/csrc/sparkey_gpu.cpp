@@ -615,6 +615,7 @@ static int plan_build_snappy(sparkey_plan* pl, const LogHdr& lh, const uint8_t* 
   SnappyParams S;
   memset(&S, 0, sizeof(S));
   S.log = d_log;
+  S.log_len = (int64_t)log_len;
   S.data_end = lh.data_end;
   S.max_block = lh.compression_block_size;
   const uint64_t body = (uint64_t)std::max<int64_t>(0, lh.data_end - kLogHeaderSize);
@@ -656,12 +657,13 @@ static int plan_build_snappy(sparkey_plan* pl, const LogHdr& lh, const uint8_t* 
   HIP_TRY(grow(&pl->sn_recoff, pl->c_sn_recoff, nblk * mepb));
   S.nblk = nblk;
   S.vlog = pl->sn_vlog;
+  S.vlog_len = (int64_t)vlen;
   S.walk = pl->sn_walk;
   S.rec_off = pl->sn_recoff;
   S.mepb = mepb;
   // LDS: the decoded block, then its stream (at most Snappy's maxCompressedLength = 32 + n + n/6)
   const int64_t mb = lh.compression_block_size;
-  const int64_t lds = ((mb + 15) & ~15LL) + ((32 + mb + mb / 6 + 15) & ~15LL);
+  const int64_t lds = ((mb + 15) & ~15LL) + 16 + ((32 + mb + mb / 6 + 15) & ~15LL) + 32;
   S.lds_bytes = lds <= 160 * 1024 ? (uint32_t)lds : 0u;
   if (nblk) {
     hipError_t e = launch_snappy_decode(S, s);
