@@ -63,6 +63,7 @@ struct SnappyParams {
   int32_t ebb;
   uint64_t nblk;
   int32_t* err;             // rewrite: virtual offset not a record start
+  unsigned long long* dbg;  // SPARKEY_SNAPPY_DEBUG: per block, clock deltas of stage/decode/store/walk
 };
 
 void launch_snappy_dir(const SnappyParams& S, hipStream_t s);

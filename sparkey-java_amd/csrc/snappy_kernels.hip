@@ -17,13 +17,15 @@ namespace {
 __device__ __forceinline__ int64_t align16(int64_t x) { return (x + 15) & ~15LL; }
 
 // len bytes: one byte per lane per round for short copies (one LDS round trip for the usual
-// <= 64-byte element), 16 consecutive bytes per lane per round for long ones
-__device__ __forceinline__ void copy_bytes(uint8_t* dst, const uint8_t* src, int64_t len, int lane, int nlanes) {
+// <= 256-byte element), 16 consecutive bytes per lane per round for long ones.  32-bit indices:
+// blocks are < 2^31 bytes (compressionBlockSize is a Java int).
+__device__ __forceinline__ void copy_bytes(uint8_t* dst, const uint8_t* src, uint32_t len, uint32_t lane,
+                                           uint32_t nlanes) {
   if (len <= 4 * nlanes) {
-    for (int64_t k = lane; k < len; k += nlanes) dst[k] = src[k];
+    for (uint32_t k = lane; k < len; k += nlanes) dst[k] = src[k];
     return;
   }
-  for (int64_t k = (int64_t)lane * 16; k < len; k += (int64_t)nlanes * 16) {
+  for (uint32_t k = lane * 16; k < len; k += nlanes * 16) {
     if (k + 16 <= len) {
       uint8_t t[16];
 #pragma unroll
@@ -31,7 +33,7 @@ __device__ __forceinline__ void copy_bytes(uint8_t* dst, const uint8_t* src, int
 #pragma unroll
       for (int i = 0; i < 16; i++) dst[k + i] = t[i];
     } else {
-      for (int64_t i = k; i < len; i++) dst[i] = src[i];
+      for (uint32_t i = k; i < len; i++) dst[i] = src[i];
     }
   }
 }
@@ -42,50 +44,51 @@ __device__ __forceinline__ void copy_bytes(uint8_t* dst, const uint8_t* src, int
 // o are read, so overlapping matches need no ordering between the lanes.  Returns kWalkBadStream on a
 // malformed stream.
 template <bool kSync>
-__device__ uint32_t snappy_decode(const uint8_t* in, int64_t n, int64_t p, uint8_t* out, int64_t ulen, int lane,
-                                  int nlanes) {
-  int64_t o = 0;
+__device__ __forceinline__ uint32_t snappy_decode(const uint8_t* in, uint32_t n, uint32_t p, uint8_t* out,
+                                                  uint32_t ulen, uint32_t lane, uint32_t nlanes) {
+  uint32_t o = 0;
   while (p < n) {
     // the tag and the four bytes after it in one round trip
     const uint32_t t = in[p];
     const uint32_t e0 = p + 1 < n ? in[p + 1] : 0u, e1 = p + 2 < n ? in[p + 2] : 0u;
     const uint32_t e2 = p + 3 < n ? in[p + 3] : 0u, e3 = p + 4 < n ? in[p + 4] : 0u;
     p++;
-    int64_t len, off = 0;
+    uint32_t len, off = 0;
     if ((t & 3u) == 0) {
       len = (t >> 2) + 1;
       if (len > 60) {
-        const int nb = (int)len - 60;
+        const uint32_t nb = len - 60;
         if (p + nb > n) return kWalkBadStream;
-        len = (int64_t)e0 | (nb > 1 ? (int64_t)e1 << 8 : 0) | (nb > 2 ? (int64_t)e2 << 16 : 0) |
-              (nb > 3 ? (int64_t)e3 << 24 : 0);
-        len += 1;
+        const uint32_t w = e0 | (e1 << 8) | (e2 << 16) | (e3 << 24);
+        const uint64_t lm1 = nb == 4 ? (uint64_t)w : (uint64_t)(w & ((1u << (8 * nb)) - 1u));
+        if (lm1 + 1 > (uint64_t)(n - p - nb)) return kWalkBadStream;
+        len = (uint32_t)lm1 + 1;
         p += nb;
       }
-      if (p + len > n || o + len > ulen) return kWalkBadStream;
+      if (len > n - p || len > ulen - o) return kWalkBadStream;
       copy_bytes(out + o, in + p, len, lane, nlanes);
       p += len;
     } else {
       if ((t & 3u) == 1) {
         if (p + 1 > n) return kWalkBadStream;
         len = ((t >> 2) & 7u) + 4;
-        off = ((int64_t)(t >> 5) << 8) | e0;
+        off = ((t >> 5) << 8) | e0;
         p += 1;
       } else if ((t & 3u) == 2) {
         if (p + 2 > n) return kWalkBadStream;
         len = (t >> 2) + 1;
-        off = (int64_t)e0 | ((int64_t)e1 << 8);
+        off = e0 | (e1 << 8);
         p += 2;
       } else {
         if (p + 4 > n) return kWalkBadStream;
         len = (t >> 2) + 1;
-        off = (int64_t)e0 | ((int64_t)e1 << 8) | ((int64_t)e2 << 16) | ((int64_t)e3 << 24);
+        off = e0 | (e1 << 8) | (e2 << 16) | (e3 << 24);
         p += 4;
       }
-      if (off == 0 || off > o || o + len > ulen) return kWalkBadStream;
+      if (off == 0 || off > o || len > ulen - o) return kWalkBadStream;
       if (off >= len) copy_bytes(out + o, out + o - off, len, lane, nlanes);
       else
-        for (int64_t k = lane; k < len; k += nlanes) out[o + k] = out[o - off + k % off];
+        for (uint32_t k = lane; k < len; k += nlanes) out[o + k] = out[o - off + k % off];
     }
     o += len;
     if (kSync) __builtin_amdgcn_wave_barrier();  // one-wave workgroup: LDS ops run in order
@@ -213,6 +216,14 @@ __global__ void __launch_bounds__(64) k_snappy_lds(SnappyParams S) {
   const uint64_t b = blockIdx.x;
   const SnappyBlock B = S.blocks[b];
   const int lane = threadIdx.x;
+  unsigned long long t_prev = S.dbg ? __builtin_amdgcn_s_memtime() : 0;
+  auto mark = [&](int i) {
+    if (S.dbg && lane == 0) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      S.dbg[b * 4 + i] = t - t_prev;
+      t_prev = t;
+    }
+  };
   // outb: the decoded block at the alignment of its place in the virtual log; inb: the stream at the
   // alignment of its place in the log, so that both sides move as 16-byte words
   uint8_t* outb = lds;
@@ -234,11 +245,13 @@ __global__ void __launch_bounds__(64) k_snappy_lds(SnappyParams S) {
   const int64_t oa = B.voff & ~15LL;
   uint8_t* out = outb + (B.voff - oa);
   __syncthreads();
-  int64_t p = 0;
+  mark(0);
+  uint32_t p = 0;
   while (in[p] & 0x80u) p++;                                   // preamble (validated by k_snappy_dir)
   p++;
-  uint32_t flags = snappy_decode<true>(in, B.clen, p, out, B.ulen, lane, 64);
+  uint32_t flags = snappy_decode<true>(in, B.clen, p, out, B.ulen, (uint32_t)lane, 64u);
   __syncthreads();
+  mark(1);
   {
     const int64_t lo = B.voff - oa, hi = lo + B.ulen;  // the block's bytes in outb coordinates
     const int64_t nw = (hi + 15) / 16;
@@ -258,7 +271,9 @@ __global__ void __launch_bounds__(64) k_snappy_lds(SnappyParams S) {
       w.overflow = 0;
       S.walk[b] = w;
     } else {
+      mark(2);
       walk_block(S, b, out, B.ulen);
+      mark(3);
     }
   }
 }
@@ -268,11 +283,11 @@ __global__ void __launch_bounds__(64) k_snappy_global(SnappyParams S) {
   if (b >= S.nblk) return;
   const SnappyBlock B = S.blocks[b];
   const uint8_t* in = S.log + B.data;
-  int64_t p = 0;
+  uint32_t p = 0;
   while (in[p] & 0x80u) p++;
   p++;
   uint8_t* out = S.vlog + B.voff;
-  const uint32_t flags = snappy_decode<false>(in, B.clen, p, out, B.ulen, 0, 1);
+  const uint32_t flags = snappy_decode<false>(in, B.clen, p, out, B.ulen, 0u, 1u);
   if (flags) {
     SnappyWalk w;
     w.count = 0;

@@ -665,6 +665,12 @@ static int plan_build_snappy(sparkey_plan* pl, const LogHdr& lh, const uint8_t* 
   const int64_t mb = lh.compression_block_size;
   const int64_t lds = ((mb + 15) & ~15LL) + 16 + ((32 + mb + mb / 6 + 15) & ~15LL) + 32;
   S.lds_bytes = lds <= 160 * 1024 ? (uint32_t)lds : 0u;
+  unsigned long long* sdbg = nullptr;
+  if (getenv("SPARKEY_SNAPPY_DEBUG") && nblk) {
+    HIP_TRY(hipMalloc((void**)&sdbg, 4 * nblk * sizeof(unsigned long long)));
+    HIP_TRY(hipMemsetAsync(sdbg, 0, 4 * nblk * sizeof(unsigned long long), s));
+    S.dbg = sdbg;
+  }
   if (nblk) {
     hipError_t e = launch_snappy_decode(S, s);
     if (e != hipSuccess && S.lds_bytes) {  // the LDS size was refused: lane-serial global decode
@@ -688,6 +694,16 @@ static int plan_build_snappy(sparkey_plan* pl, const LogHdr& lh, const uint8_t* 
   }
   if (timed) HIP_TRY(hipEventRecord(ev[1], s));
   HIP_TRY(hipStreamSynchronize(s));
+  if (sdbg) {  // SPARKEY_SNAPPY_DEBUG: mean clock deltas per block
+    std::vector<unsigned long long> h(4 * nblk);
+    HIP_TRY(hipMemcpy(h.data(), sdbg, h.size() * 8, hipMemcpyDeviceToHost));
+    double sum[4] = {0, 0, 0, 0};
+    for (uint64_t b = 0; b < nblk; b++)
+      for (int i = 0; i < 4; i++) sum[i] += (double)h[4 * b + i];
+    fprintf(stderr, "[k_snappy_lds] blocks=%llu lds=%u mean clocks: stage %.0f decode %.0f store %.0f walk %.0f\n",
+            (unsigned long long)nblk, S.lds_bytes, sum[0] / nblk, sum[1] / nblk, sum[2] / nblk, sum[3] / nblk);
+    (void)hipFree(sdbg);
+  }
   int64_t carry = 0;
   for (uint64_t b = 0; b < nblk; b++) {
     const SnappyWalk& w = walks[b];
