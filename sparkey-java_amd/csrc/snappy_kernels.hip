@@ -263,18 +263,13 @@ __global__ void __launch_bounds__(64) k_snappy_lds(SnappyParams S) {
       }
     }
   }
-  if (lane == 0) {
-    if (flags) {
-      SnappyWalk w;
-      w.count = 0;
-      w.flags = flags;
-      w.overflow = 0;
-      S.walk[b] = w;
-    } else {
-      mark(2);
-      walk_block(S, b, out, B.ulen);
-      mark(3);
-    }
+  mark(2);
+  if (lane == 0) {  // the records are walked by k_snappy_walk, many blocks per wave
+    SnappyWalk w;
+    w.count = 0;
+    w.flags = flags;
+    w.overflow = 0;
+    S.walk[b] = w;
   }
 }
 
@@ -288,15 +283,20 @@ __global__ void __launch_bounds__(64) k_snappy_global(SnappyParams S) {
   p++;
   uint8_t* out = S.vlog + B.voff;
   const uint32_t flags = snappy_decode<false>(in, B.clen, p, out, B.ulen, 0u, 1u);
-  if (flags) {
-    SnappyWalk w;
-    w.count = 0;
-    w.flags = flags;
-    w.overflow = 0;
-    S.walk[b] = w;
-  } else {
-    walk_block(S, b, out, B.ulen);
-  }
+  SnappyWalk w;
+  w.count = 0;
+  w.flags = flags;
+  w.overflow = 0;
+  S.walk[b] = w;
+}
+
+// One lane per decoded block: its records from the virtual log (a lone wave per CU walking from LDS
+// paid every load's latency in turn; here the blocks' walks overlap).
+__global__ void __launch_bounds__(64) k_snappy_walk(SnappyParams S) {
+  const uint64_t b = (uint64_t)blockIdx.x * 64 + threadIdx.x;
+  if (b >= S.nblk || S.walk[b].flags) return;
+  const SnappyBlock B = S.blocks[b];
+  walk_block(S, b, S.vlog + B.voff, B.ulen);
 }
 
 __global__ void __launch_bounds__(256) k_snappy_rewrite(SnappyParams S) {
@@ -348,6 +348,9 @@ hipError_t launch_snappy_decode(const SnappyParams& S, hipStream_t s) {
   } else {
     hipLaunchKernelGGL(k_snappy_global, dim3((uint32_t)((S.nblk + 63) / 64)), 64, 0, s, S);
   }
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_snappy_walk, dim3((uint32_t)((S.nblk + 63) / 64)), 64, 0, s, S);
   return hipGetLastError();
 }
 

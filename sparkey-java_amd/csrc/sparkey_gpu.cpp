@@ -700,8 +700,8 @@ static int plan_build_snappy(sparkey_plan* pl, const LogHdr& lh, const uint8_t* 
     double sum[4] = {0, 0, 0, 0};
     for (uint64_t b = 0; b < nblk; b++)
       for (int i = 0; i < 4; i++) sum[i] += (double)h[4 * b + i];
-    fprintf(stderr, "[k_snappy_lds] blocks=%llu lds=%u mean clocks: stage %.0f decode %.0f store %.0f walk %.0f\n",
-            (unsigned long long)nblk, S.lds_bytes, sum[0] / nblk, sum[1] / nblk, sum[2] / nblk, sum[3] / nblk);
+    fprintf(stderr, "[k_snappy_lds] blocks=%llu lds=%u mean clocks: stage %.0f decode %.0f store %.0f\n",
+            (unsigned long long)nblk, S.lds_bytes, sum[0] / nblk, sum[1] / nblk, sum[2] / nblk);
     (void)hipFree(sdbg);
   }
   int64_t carry = 0;
