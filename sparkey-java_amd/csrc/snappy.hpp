@@ -34,11 +34,15 @@ constexpr uint32_t kWalkBadHeader = 1u;    // a record header runs past the bloc
 constexpr uint32_t kWalkTooMany = 2u;      // more records than maxEntriesPerBlock
 constexpr uint32_t kWalkBadStream = 4u;    // malformed Snappy stream
 
+// The directory's state between k_snappy_dir launches (each follows the chain for up to a chunk of
+// blocks, so that the decode of one chunk overlaps the walk along the next).
 struct SnappyDirResult {
-  uint64_t nblk;
-  uint64_t total;     // decompressed bytes over all blocks
-  int32_t err;        // 0 ok, 1 corrupt block framing, 2 block larger than compressionBlockSize
-  int32_t pad;
+  uint64_t nblk;      // blocks found so far
+  uint64_t total;     // their decompressed bytes
+  int64_t p;          // offset of the next block header (0: not started)
+  int32_t err;        // 0 ok, 1 corrupt block framing, 2 block larger than the reader's buffers,
+                      // 3 the decompressed bytes exceed vcap
+  int32_t done;       // the chain reached dataEnd
 };
 
 struct SnappyParams {
@@ -48,6 +52,9 @@ struct SnappyParams {
   int64_t max_block;        // compressionBlockSize: the reader's uncompressed buffer
   SnappyBlock* blocks;
   uint64_t blk_cap;
+  uint64_t dir_limit;       // k_snappy_dir stops at this many blocks
+  int64_t vcap;             // decompressed bytes the virtual log holds (0: unbounded)
+  uint64_t blk_base;        // decode launches: first block
   SnappyDirResult* dir;
   uint8_t* vlog;            // virtual log (84 header bytes written by the host)
   int64_t vlog_len;         // bytes of vlog
@@ -63,12 +70,14 @@ struct SnappyParams {
   int32_t ebb;
   uint64_t nblk;
   int32_t* err;             // rewrite: virtual offset not a record start
-  unsigned long long* dbg;  // SPARKEY_SNAPPY_DEBUG: per block, clock deltas of stage/decode/store/walk
 };
 
 void launch_snappy_dir(const SnappyParams& S, hipStream_t s);
-// decode + walk, one wave per block: LDS-staged when lds_bytes > 0, else lane-serial in global memory
+// blocks [blk_base, blk_base + nblk), one wave per block: LDS-staged when lds_bytes > 0, else
+// lane-serial in global memory
 hipError_t launch_snappy_decode(const SnappyParams& S, hipStream_t s);
+// blocks [0, nblk): their records
+void launch_snappy_walk(const SnappyParams& S, hipStream_t s);
 void launch_snappy_rewrite(const SnappyParams& S, hipStream_t s);
 
 }  // namespace sk

@@ -176,10 +176,11 @@ __device__ __forceinline__ int32_t dir_vlq(const Window& w, int& j, int avail, i
 
 __global__ void __launch_bounds__(64) k_snappy_dir(SnappyParams S) {
   if (threadIdx.x != 0) return;
-  int64_t p = 84;
-  uint64_t nb = 0, total = 0;
+  const SnappyDirResult d0 = *S.dir;
+  int64_t p = d0.p ? d0.p : 84;
+  uint64_t nb = d0.nblk, total = d0.total;
   int32_t err = 0;
-  while (p < S.data_end) {
+  while (p < S.data_end && nb < S.dir_limit) {
     const Window w = load_window(S.log, p, S.log_len);
     int j = 0;
     const int32_t clen = dir_vlq(w, j, (int)min<int64_t>(16, S.data_end - p), err);   // Util.readUnsignedVLQInt
@@ -190,7 +191,8 @@ __global__ void __launch_bounds__(64) k_snappy_dir(SnappyParams S) {
     // the reader's buffers: maxBlockSize decompressed, Snappy.maxCompressedLength(maxBlockSize) compressed
     // (CompressedReader.java:40-49)
     if ((int64_t)ulen > S.max_block || (int64_t)clen > 32 + S.max_block + S.max_block / 6) { err = 2; break; }
-    if (nb < S.blk_cap) {
+    if (S.vcap && (int64_t)(total + (uint64_t)ulen) > S.vcap) { err = 3; break; }
+    {
       SnappyBlock B;
       B.file_pos = p;
       B.data = q;
@@ -206,24 +208,17 @@ __global__ void __launch_bounds__(64) k_snappy_dir(SnappyParams S) {
   SnappyDirResult d;
   d.nblk = nb;
   d.total = total;
+  d.p = p;
   d.err = err;
-  d.pad = 0;
+  d.done = err == 0 && p >= S.data_end;
   *S.dir = d;
 }
 
 __global__ void __launch_bounds__(64) k_snappy_lds(SnappyParams S) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  const uint64_t b = blockIdx.x;
+  const uint64_t b = S.blk_base + blockIdx.x;
   const SnappyBlock B = S.blocks[b];
   const int lane = threadIdx.x;
-  unsigned long long t_prev = S.dbg ? __builtin_amdgcn_s_memtime() : 0;
-  auto mark = [&](int i) {
-    if (S.dbg && lane == 0) {
-      const unsigned long long t = __builtin_amdgcn_s_memtime();
-      S.dbg[b * 4 + i] = t - t_prev;
-      t_prev = t;
-    }
-  };
   // outb: the decoded block at the alignment of its place in the virtual log; inb: the stream at the
   // alignment of its place in the log, so that both sides move as 16-byte words
   uint8_t* outb = lds;
@@ -245,13 +240,11 @@ __global__ void __launch_bounds__(64) k_snappy_lds(SnappyParams S) {
   const int64_t oa = B.voff & ~15LL;
   uint8_t* out = outb + (B.voff - oa);
   __syncthreads();
-  mark(0);
   uint32_t p = 0;
   while (in[p] & 0x80u) p++;                                   // preamble (validated by k_snappy_dir)
   p++;
   uint32_t flags = snappy_decode<true>(in, B.clen, p, out, B.ulen, (uint32_t)lane, 64u);
   __syncthreads();
-  mark(1);
   {
     const int64_t lo = B.voff - oa, hi = lo + B.ulen;  // the block's bytes in outb coordinates
     const int64_t nw = (hi + 15) / 16;
@@ -263,7 +256,6 @@ __global__ void __launch_bounds__(64) k_snappy_lds(SnappyParams S) {
       }
     }
   }
-  mark(2);
   if (lane == 0) {  // the records are walked by k_snappy_walk, many blocks per wave
     SnappyWalk w;
     w.count = 0;
@@ -274,8 +266,8 @@ __global__ void __launch_bounds__(64) k_snappy_lds(SnappyParams S) {
 }
 
 __global__ void __launch_bounds__(64) k_snappy_global(SnappyParams S) {
-  const uint64_t b = (uint64_t)blockIdx.x * 64 + threadIdx.x;
-  if (b >= S.nblk) return;
+  const uint64_t b = S.blk_base + (uint64_t)blockIdx.x * 64 + threadIdx.x;
+  if (b >= S.blk_base + S.nblk) return;
   const SnappyBlock B = S.blocks[b];
   const uint8_t* in = S.log + B.data;
   uint32_t p = 0;
@@ -348,10 +340,11 @@ hipError_t launch_snappy_decode(const SnappyParams& S, hipStream_t s) {
   } else {
     hipLaunchKernelGGL(k_snappy_global, dim3((uint32_t)((S.nblk + 63) / 64)), 64, 0, s, S);
   }
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_snappy_walk, dim3((uint32_t)((S.nblk + 63) / 64)), 64, 0, s, S);
   return hipGetLastError();
+}
+
+void launch_snappy_walk(const SnappyParams& S, hipStream_t s) {
+  if (S.nblk) hipLaunchKernelGGL(k_snappy_walk, dim3((uint32_t)((S.nblk + 63) / 64)), 64, 0, s, S);
 }
 
 void launch_snappy_rewrite(const SnappyParams& S, hipStream_t s) {

@@ -222,6 +222,29 @@ hipError_t grow(T** p, uint64_t& have, uint64_t want) {
   return e;
 }
 
+// grow() that keeps the first `used` elements
+template <class T>
+hipError_t grow_keep(T** p, uint64_t& have, uint64_t want, uint64_t used, hipStream_t s) {
+  if (want <= have && *p) return hipSuccess;
+  T* q = nullptr;
+  hipError_t e = hipMalloc((void**)&q, std::max<uint64_t>(want, 1) * sizeof(T));
+  if (e != hipSuccess) return e;
+  if (*p && used) {
+    e = hipMemcpyAsync(q, *p, std::min(used, have) * sizeof(T), hipMemcpyDeviceToDevice, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) {
+      (void)hipFree(q);
+      return e;
+    }
+  }
+  if (*p) (void)hipFree(*p);
+  *p = q;
+  have = std::max<uint64_t>(want, 1);
+  return hipSuccess;
+}
+
+constexpr uint64_t kSnappyChunk = 2048;  // blocks per k_snappy_dir launch
+
 }  // namespace
 
 // Host state of a sharded build between its steps (sparkey_shard_*).
@@ -270,6 +293,8 @@ struct sparkey_plan {
   uint8_t* sn_vlog = nullptr;
   uint8_t* sn_itab = nullptr;
   int32_t* sn_err = nullptr;
+  hipStream_t sn_stream = nullptr;  // the decode of one directory chunk overlaps the next chunk
+  hipEvent_t sn_ev[2] = {nullptr, nullptr};
   uint64_t c_seg_cls_cnt = 0, c_seg_cls_off = 0;
   uint32_t* seg_cls_cnt = nullptr;
   uint64_t* seg_cls_off = nullptr;
@@ -619,25 +644,89 @@ static int plan_build_snappy(sparkey_plan* pl, const LogHdr& lh, const uint8_t* 
   S.data_end = lh.data_end;
   S.max_block = lh.compression_block_size;
   const uint64_t body = (uint64_t)std::max<int64_t>(0, lh.data_end - kLogHeaderSize);
-  HIP_TRY(grow(&pl->sn_blocks, pl->c_sn_blocks,
-               std::max<uint64_t>(1024, body / (uint64_t)std::max<int64_t>(16, lh.compression_block_size / 16))));
+  // LDS: the decoded block, then its stream (at most Snappy's maxCompressedLength = 32 + n + n/6)
+  const int64_t mb = lh.compression_block_size;
+  const int64_t lds = ((mb + 15) & ~15LL) + 16 + ((32 + mb + mb / 6 + 15) & ~15LL) + 32;
+  S.lds_bytes = lds <= 160 * 1024 ? (uint32_t)lds : 0u;
+  const uint32_t mepb = (uint32_t)std::max<int32_t>(1, lh.max_entries_per_block);
+  S.mepb = mepb;
   HIP_TRY(grow(&pl->sn_dir, pl->c_sn_dir, 1));
   HIP_TRY(grow(&pl->sn_err, pl->c_sn_err, 1));
+  if (pl->c_sn_blocks == 0) {
+    HIP_TRY(grow(&pl->sn_blocks, pl->c_sn_blocks, std::max<uint64_t>(4096, body / (uint64_t)std::max<int64_t>(64, mb / 2))));
+  }
+  HIP_TRY(grow_keep(&pl->sn_walk, pl->c_sn_walk, pl->c_sn_blocks, 0, s));
+  if (!pl->sn_stream) HIP_TRY(hipStreamCreateWithFlags(&pl->sn_stream, hipStreamNonBlocking));
+  if (!pl->sn_ev[0]) {
+    HIP_TRY(hipEventCreateWithFlags(&pl->sn_ev[0], hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&pl->sn_ev[1], hipEventDisableTiming));
+  }
+  hipStream_t s2 = pl->sn_stream;
+  // The block chain is followed kSnappyChunk blocks per k_snappy_dir launch on `s`; each chunk's
+  // blocks are decoded on `s2` while the next chunk is followed.  vcap bounds the virtual log
+  // (dir error 3 past it); decode = false only follows the chain.
   SnappyDirResult dir;
-  for (int attempt = 0;; attempt++) {
-    S.blocks = pl->sn_blocks;
-    S.blk_cap = pl->c_sn_blocks;
-    S.dir = pl->sn_dir;
-    launch_snappy_dir(S, s);
-    HIP_TRY(hipGetLastError());
-    HIP_TRY(hipMemcpyAsync(&dir, pl->sn_dir, sizeof(dir), hipMemcpyDeviceToHost, s));
+  memset(&dir, 0, sizeof(dir));
+  auto pipeline = [&](int64_t vcap, bool decode) -> hipError_t {
+    hipError_t e;
+    if ((e = hipMemsetAsync(pl->sn_dir, 0, sizeof(SnappyDirResult), s)) != hipSuccess) return e;
+    if ((e = hipEventRecord(pl->sn_ev[0], s)) != hipSuccess) return e;
+    if ((e = hipStreamWaitEvent(s2, pl->sn_ev[0], 0)) != hipSuccess) return e;
+    memset(&dir, 0, sizeof(dir));
+    S.vcap = vcap;
+    for (;;) {
+      S.blocks = pl->sn_blocks;
+      S.blk_cap = pl->c_sn_blocks;
+      S.walk = pl->sn_walk;
+      S.dir = pl->sn_dir;
+      const uint64_t before = dir.nblk;
+      S.dir_limit = std::min<uint64_t>(S.blk_cap, before + kSnappyChunk);
+      launch_snappy_dir(S, s);
+      if ((e = hipGetLastError()) != hipSuccess) return e;
+      if ((e = hipMemcpyAsync(&dir, pl->sn_dir, sizeof(dir), hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+      if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+      if (decode && dir.nblk > before) {
+        S.blk_base = before;
+        S.nblk = dir.nblk - before;
+        e = launch_snappy_decode(S, s2);
+        if (e != hipSuccess && S.lds_bytes) {  // the LDS size was refused: lane-serial global decode
+          (void)hipGetLastError();
+          S.lds_bytes = 0;
+          e = launch_snappy_decode(S, s2);
+        }
+        if (e != hipSuccess) return e;
+      }
+      if (dir.err || dir.done) break;
+      if (dir.nblk >= pl->c_sn_blocks) {  // the chain outran the block arrays: grow, keeping them
+        if ((e = hipStreamSynchronize(s2)) != hipSuccess) return e;
+        const uint64_t want = 2 * pl->c_sn_blocks;
+        if ((e = grow_keep(&pl->sn_blocks, pl->c_sn_blocks, want, dir.nblk, s)) != hipSuccess) return e;
+        if ((e = grow_keep(&pl->sn_walk, pl->c_sn_walk, want, dir.nblk, s)) != hipSuccess) return e;
+      }
+    }
+    if ((e = hipEventRecord(pl->sn_ev[1], s2)) != hipSuccess) return e;
+    return hipStreamWaitEvent(s, pl->sn_ev[1], 0);
+  };
+  // the reference writer's logs decompress to exactly putSize + deleteSize record bytes
+  // (LogHeader.put / delete, LogHeader.java:161-172); a header that understates them gets a
+  // directory-only pass to size the virtual log
+  const int64_t hdr_total = std::max<int64_t>(0, lh.put_size) + std::max<int64_t>(0, lh.delete_size);
+  HIP_TRY(grow(&pl->sn_vlog, pl->c_sn_vlog, (uint64_t)hdr_total + kLogHeaderSize + 4096));
+  S.vlog = pl->sn_vlog;
+  HIP_TRY(pipeline(hdr_total, true));
+  if (dir.err == 3) {
     HIP_TRY(hipStreamSynchronize(s));
-    if (dir.err || dir.nblk <= S.blk_cap || attempt) break;
-    HIP_TRY(grow(&pl->sn_blocks, pl->c_sn_blocks, dir.nblk));
+    HIP_TRY(pipeline(0, false));
+    if (!dir.err) {
+      HIP_TRY(grow(&pl->sn_vlog, pl->c_sn_vlog, dir.total + kLogHeaderSize + 4096));
+      S.vlog = pl->sn_vlog;
+      HIP_TRY(pipeline((int64_t)dir.total, true));
+    }
   }
   if (dir.err) {
+    HIP_TRY(hipStreamSynchronize(s));
     drop_events();
-    set_err(err, err_len, dir.err == 2 ? "Corrupt log file: compressed block larger than the compression block size"
+    set_err(err, err_len, dir.err == 2 ? "Corrupt log file: compressed block larger than the reader's buffers"
                                        : "Corrupt log file: bad compressed block header");
     return SPARKEY_E_CORRUPT_LOG;
   }
@@ -649,41 +738,17 @@ static int plan_build_snappy(sparkey_plan* pl, const LogHdr& lh, const uint8_t* 
   wr64(vh + 32, vlen);
   wr32(vh + 64, 0u);
   wr32(vh + 80, 1u);
-  HIP_TRY(grow(&pl->sn_vlog, pl->c_sn_vlog, vlen + 4096));
   HIP_TRY(hipMemcpyAsync(pl->sn_vlog, vh, kLogHeaderSize, hipMemcpyHostToDevice, s));
   HIP_TRY(hipMemsetAsync(pl->sn_vlog + vlen, 0, 4096, s));
-  const uint32_t mepb = (uint32_t)std::max<int32_t>(1, lh.max_entries_per_block);
-  HIP_TRY(grow(&pl->sn_walk, pl->c_sn_walk, nblk));
   HIP_TRY(grow(&pl->sn_recoff, pl->c_sn_recoff, nblk * mepb));
-  S.nblk = nblk;
-  S.vlog = pl->sn_vlog;
-  S.vlog_len = (int64_t)vlen;
+  S.blocks = pl->sn_blocks;
   S.walk = pl->sn_walk;
   S.rec_off = pl->sn_recoff;
-  S.mepb = mepb;
-  // LDS: the decoded block, then its stream (at most Snappy's maxCompressedLength = 32 + n + n/6)
-  const int64_t mb = lh.compression_block_size;
-  const int64_t lds = ((mb + 15) & ~15LL) + 16 + ((32 + mb + mb / 6 + 15) & ~15LL) + 32;
-  S.lds_bytes = lds <= 160 * 1024 ? (uint32_t)lds : 0u;
-  unsigned long long* sdbg = nullptr;
-  if (getenv("SPARKEY_SNAPPY_DEBUG") && nblk) {
-    HIP_TRY(hipMalloc((void**)&sdbg, 4 * nblk * sizeof(unsigned long long)));
-    HIP_TRY(hipMemsetAsync(sdbg, 0, 4 * nblk * sizeof(unsigned long long), s));
-    S.dbg = sdbg;
-  }
-  if (nblk) {
-    hipError_t e = launch_snappy_decode(S, s);
-    if (e != hipSuccess && S.lds_bytes) {  // the LDS size was refused: lane-serial global decode
-      (void)hipGetLastError();
-      S.lds_bytes = 0;
-      e = launch_snappy_decode(S, s);
-    }
-    if (e != hipSuccess) {
-      drop_events();
-      set_err(err, err_len, std::string("HIP error: ") + hipGetErrorString(e) + " in snappy decode");
-      return SPARKEY_E_GPU;
-    }
-  }
+  S.vlog_len = (int64_t)vlen;
+  S.blk_base = 0;
+  S.nblk = nblk;
+  launch_snappy_walk(S, s);
+  HIP_TRY(hipGetLastError());
   // compose the block walks: a block either starts at a record (CompressedWriter flushes after a
   // spanning record, CompressedWriter.java:71-75) or lies wholly inside the record spanning into it
   std::vector<SnappyWalk> walks(nblk);
@@ -694,16 +759,6 @@ static int plan_build_snappy(sparkey_plan* pl, const LogHdr& lh, const uint8_t* 
   }
   if (timed) HIP_TRY(hipEventRecord(ev[1], s));
   HIP_TRY(hipStreamSynchronize(s));
-  if (sdbg) {  // SPARKEY_SNAPPY_DEBUG: mean clock deltas per block
-    std::vector<unsigned long long> h(4 * nblk);
-    HIP_TRY(hipMemcpy(h.data(), sdbg, h.size() * 8, hipMemcpyDeviceToHost));
-    double sum[4] = {0, 0, 0, 0};
-    for (uint64_t b = 0; b < nblk; b++)
-      for (int i = 0; i < 4; i++) sum[i] += (double)h[4 * b + i];
-    fprintf(stderr, "[k_snappy_lds] blocks=%llu lds=%u mean clocks: stage %.0f decode %.0f store %.0f\n",
-            (unsigned long long)nblk, S.lds_bytes, sum[0] / nblk, sum[1] / nblk, sum[2] / nblk);
-    (void)hipFree(sdbg);
-  }
   int64_t carry = 0;
   for (uint64_t b = 0; b < nblk; b++) {
     const SnappyWalk& w = walks[b];
@@ -1302,6 +1357,9 @@ void sparkey_plan_destroy(sparkey_plan* pl) {
   if (pl->ev0) (void)hipEventDestroy(pl->ev0);
   if (pl->ev1) (void)hipEventDestroy(pl->ev1);
   if (pl->own_stream) (void)hipStreamDestroy(pl->own_stream);
+  if (pl->sn_stream) (void)hipStreamDestroy(pl->sn_stream);
+  for (auto& e : pl->sn_ev)
+    if (e) (void)hipEventDestroy(e);
   if (pl->side_ok) {
     for (int i = 0; i < 3; i++) {
       (void)hipStreamDestroy(pl->side.s[i]);
