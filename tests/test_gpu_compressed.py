@@ -87,3 +87,20 @@ def test_errors(native):
     struct.pack_into("<i", bad, 68, 16)                           # blocks larger than the block size
     with pytest.raises(OSError):
         native.build_index_mem(bytes(bad), opts)
+
+
+@pytest.mark.parametrize("delta", [-1000, -1, 0, 5000])
+def test_header_put_size_misstated(native, delta):
+    """The virtual log is sized from putSize + deleteSize; a header that understates them takes the
+    directory-only pass first (the reference never reads putSize here)."""
+    rng = random.Random(11)
+    log = bytearray(_compressed(_ops(rng, 1200, 10 ** 9, 0.1, 150), 700))
+    put_size = struct.unpack_from("<q", log, 72)[0]
+    struct.pack_into("<q", log, 72, max(0, put_size + delta))
+    check(native, bytes(log))
+
+
+def test_many_small_blocks(native):
+    """More blocks than the first directory allocation and many 2048-block chunks."""
+    rng = random.Random(12)
+    check(native, _compressed(_ops(rng, 6000, 10 ** 9, 0.0, 40), 12))
