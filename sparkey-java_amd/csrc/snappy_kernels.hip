@@ -2,9 +2,10 @@
 //
 //   k_snappy_dir      block directory: the chain of VLQ(compressedSize) block headers from offset 84 to
 //                     dataEnd (CompressedReader.fetchBlock, CompressedReader.java:66-74), one lane
-//   k_snappy_lds      one wave per block: the Snappy stream staged in LDS, decoded element by element
-//                     into LDS (every lane copies a slice of each literal / match), streamed out to
-//                     the virtual log, then the block's records walked from LDS
+//   k_snappy_lds      one wave per block: the Snappy stream read through an LDS window, decoded
+//                     element by element into LDS (every lane copies a slice of each literal /
+//                     match), streamed out to the virtual log
+//   k_snappy_walk     one lane per block: the block's records
 //   k_snappy_global   the same, lane-serial in global memory, for blocks too large for LDS
 //   k_snappy_rewrite  one lane per slot: virtual offset -> (blockPosition << ebb) | entryIndex
 #include "device_common.hpp"
@@ -38,20 +39,65 @@ __device__ __forceinline__ void copy_bytes(uint8_t* dst, const uint8_t* src, uin
   }
 }
 
+// Where snappy_decode reads the stream.  FlatIn: the whole stream in one buffer.
+struct FlatIn {
+  const uint8_t* in;
+  __device__ __forceinline__ void ensure(uint32_t, uint32_t) {}
+  __device__ __forceinline__ uint32_t byte(uint32_t q) const { return in[q]; }
+  __device__ __forceinline__ const uint8_t* src(uint32_t q, uint32_t) const { return in + q; }
+};
+
+// RingIn: a kSnappyWindow-byte LDS window over the stream, refilled by the whole wave with aligned
+// 16-byte loads when the parse nears its end; literals that reach past it are copied from global
+// memory directly.  Keeps the LDS per block to the decoded block + the window (two waves per CU at
+// 64 KiB blocks instead of one with the whole stream staged).
+constexpr uint32_t kSnappyWindow = 8192;
+struct RingIn {
+  const uint8_t* g;       // the stream in global memory
+  int64_t readable;       // bytes readable from g (to the end of the log buffer)
+  uint32_t n;             // stream bytes
+  uint8_t* win;           // kSnappyWindow + 16 bytes of LDS
+  int64_t a;              // stream offset of win[0] (16-byte aligned in global memory; may be < 0)
+  int64_t wend;           // stream offset past the window's valid bytes
+  uint32_t lane;
+  __device__ __forceinline__ void refill(uint32_t p) {
+    a = (int64_t)p - (int64_t)(((uintptr_t)(g + p)) & 15);
+#pragma unroll 4
+    for (uint32_t w = lane; w < kSnappyWindow / 16; w += 64) {
+      const int64_t q = a + 16 * (int64_t)w;
+      if (q + 16 <= readable) {
+        *(uint4*)(win + 16 * w) = *(const uint4*)(g + q);
+      } else {
+        for (int i = 0; i < 16 && q + i < readable; i++) win[16 * w + i] = g[q + i];
+      }
+    }
+    wend = min<int64_t>(a + kSnappyWindow, (int64_t)n);
+    __builtin_amdgcn_wave_barrier();
+  }
+  __device__ __forceinline__ void ensure(uint32_t p, uint32_t need) {
+    if ((int64_t)p + need > wend && wend < (int64_t)n) refill(p);
+  }
+  __device__ __forceinline__ uint32_t byte(uint32_t q) const { return win[(int64_t)q - a]; }
+  __device__ __forceinline__ const uint8_t* src(uint32_t q, uint32_t len) const {
+    return (int64_t)q + len <= wend ? win + ((int64_t)q - a) : g + q;
+  }
+};
+
 // Snappy raw format: varint uncompressed length, then literal (tag 00), copy-1 (01), copy-2 (10) and
 // copy-4 (11) elements.  Lanes [lane, nlanes) share each element's copy; every lane parses the same
 // tags (uniform control flow).  A match copies out[o + k] = out[o - off + k % off]: only bytes before
 // o are read, so overlapping matches need no ordering between the lanes.  Returns kWalkBadStream on a
 // malformed stream.
-template <bool kSync>
-__device__ __forceinline__ uint32_t snappy_decode(const uint8_t* in, uint32_t n, uint32_t p, uint8_t* out,
-                                                  uint32_t ulen, uint32_t lane, uint32_t nlanes) {
+template <bool kSync, class In>
+__device__ __forceinline__ uint32_t snappy_decode(In& in, uint32_t n, uint32_t p, uint8_t* out, uint32_t ulen,
+                                                  uint32_t lane, uint32_t nlanes) {
   uint32_t o = 0;
   while (p < n) {
     // the tag and the four bytes after it in one round trip
-    const uint32_t t = in[p];
-    const uint32_t e0 = p + 1 < n ? in[p + 1] : 0u, e1 = p + 2 < n ? in[p + 2] : 0u;
-    const uint32_t e2 = p + 3 < n ? in[p + 3] : 0u, e3 = p + 4 < n ? in[p + 4] : 0u;
+    in.ensure(p, 5);
+    const uint32_t t = in.byte(p);
+    const uint32_t e0 = p + 1 < n ? in.byte(p + 1) : 0u, e1 = p + 2 < n ? in.byte(p + 2) : 0u;
+    const uint32_t e2 = p + 3 < n ? in.byte(p + 3) : 0u, e3 = p + 4 < n ? in.byte(p + 4) : 0u;
     p++;
     uint32_t len, off = 0;
     if ((t & 3u) == 0) {
@@ -66,7 +112,7 @@ __device__ __forceinline__ uint32_t snappy_decode(const uint8_t* in, uint32_t n,
         p += nb;
       }
       if (len > n - p || len > ulen - o) return kWalkBadStream;
-      copy_bytes(out + o, in + p, len, lane, nlanes);
+      copy_bytes(out + o, in.src(p, len), len, lane, nlanes);
       p += len;
     } else {
       if ((t & 3u) == 1) {
@@ -218,32 +264,23 @@ __global__ void __launch_bounds__(64) k_snappy_lds(SnappyParams S) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const uint64_t b = S.blk_base + blockIdx.x;
   const SnappyBlock B = S.blocks[b];
-  const int lane = threadIdx.x;
-  // outb: the decoded block at the alignment of its place in the virtual log; inb: the stream at the
-  // alignment of its place in the log, so that both sides move as 16-byte words
+  const uint32_t lane = threadIdx.x;
+  // outb: the decoded block at the alignment of its place in the virtual log (16-byte stores out);
+  // then the stream window
   uint8_t* outb = lds;
-  uint8_t* inb = lds + align16(S.max_block) + 16;
-  const int64_t ga = B.data & ~15LL;
-  uint8_t* in = inb + (B.data - ga);
-  {
-    const int64_t nw = (B.data - ga + B.clen + 15) / 16;
-#pragma unroll 4
-    for (int64_t w = lane; w < nw; w += 64) {
-      const int64_t g = ga + 16 * w;
-      if (g + 16 <= S.log_len) {
-        *(uint4*)(inb + 16 * w) = *(const uint4*)(S.log + g);
-      } else {
-        for (int i = 0; i < 16 && g + i < S.log_len; i++) inb[16 * w + i] = S.log[g + i];
-      }
-    }
-  }
   const int64_t oa = B.voff & ~15LL;
   uint8_t* out = outb + (B.voff - oa);
-  __syncthreads();
+  RingIn in;
+  in.g = S.log + B.data;
+  in.readable = S.log_len - B.data;
+  in.n = B.clen;
+  in.win = lds + align16(S.max_block) + 16;
+  in.lane = lane;
+  in.refill(0);
   uint32_t p = 0;
-  while (in[p] & 0x80u) p++;                                   // preamble (validated by k_snappy_dir)
+  while (in.byte(p) & 0x80u) p++;                              // preamble (<= 5 bytes, validated by k_snappy_dir)
   p++;
-  uint32_t flags = snappy_decode<true>(in, B.clen, p, out, B.ulen, (uint32_t)lane, 64u);
+  const uint32_t flags = snappy_decode<true>(in, B.clen, p, out, B.ulen, lane, 64u);
   __syncthreads();
   {
     const int64_t lo = B.voff - oa, hi = lo + B.ulen;  // the block's bytes in outb coordinates
@@ -269,9 +306,9 @@ __global__ void __launch_bounds__(64) k_snappy_global(SnappyParams S) {
   const uint64_t b = S.blk_base + (uint64_t)blockIdx.x * 64 + threadIdx.x;
   if (b >= S.blk_base + S.nblk) return;
   const SnappyBlock B = S.blocks[b];
-  const uint8_t* in = S.log + B.data;
+  FlatIn in{S.log + B.data};
   uint32_t p = 0;
-  while (in[p] & 0x80u) p++;
+  while (in.byte(p) & 0x80u) p++;
   p++;
   uint8_t* out = S.vlog + B.voff;
   const uint32_t flags = snappy_decode<false>(in, B.clen, p, out, B.ulen, 0u, 1u);

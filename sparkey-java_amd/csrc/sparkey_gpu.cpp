@@ -644,9 +644,9 @@ static int plan_build_snappy(sparkey_plan* pl, const LogHdr& lh, const uint8_t* 
   S.data_end = lh.data_end;
   S.max_block = lh.compression_block_size;
   const uint64_t body = (uint64_t)std::max<int64_t>(0, lh.data_end - kLogHeaderSize);
-  // LDS: the decoded block, then its stream (at most Snappy's maxCompressedLength = 32 + n + n/6)
+  // LDS: the decoded block, then an 8 KiB window over its stream (k_snappy_lds)
   const int64_t mb = lh.compression_block_size;
-  const int64_t lds = ((mb + 15) & ~15LL) + 16 + ((32 + mb + mb / 6 + 15) & ~15LL) + 32;
+  const int64_t lds = ((mb + 15) & ~15LL) + 16 + 8192 + 16;
   S.lds_bytes = lds <= 160 * 1024 ? (uint32_t)lds : 0u;
   const uint32_t mepb = (uint32_t)std::max<int32_t>(1, lh.max_entries_per_block);
   S.mepb = mepb;
