@@ -5,7 +5,7 @@ header) of a C2-shaped log (10M PUTs per GPU, 16-byte keys, 100-byte values, NON
 resident in HBM, into a device-resident .spi image.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--entries 10000000] [--no-cpu-baseline]
-                    [--workload c2|c3|c5|churn|get|append]
+                    [--workload c2|c3|c5|churn|snappy|get|append]
 
 N = 1: the C2 log (10M records) built on one GPU; the line carries the per-stage roofline and the
 CPU baseline (the oracle's sequential IN_MEMORY restatement on the host, timed on the same log).
