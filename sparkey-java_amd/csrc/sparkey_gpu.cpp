@@ -1562,7 +1562,7 @@ int sparkey_shard_begin(sparkey_plan* pl, const uint8_t* log_header, uint64_t fi
   }
   ShardState& sh = pl->shard;
   sh.active = false;
-  int rc = parse_log_header(log_header, 84, file_len, &sh.lh, err, err_len);
+  int rc = parse_log_header(log_header, 84, file_len, &sh.lh, err, err_len, true);  // SNAPPY: gathered (sharded.py)
   if (rc) return rc;
   rc = make_index_params(sh.lh, *opts, &sh.ip, err, err_len);
   if (rc) return rc;

@@ -19,7 +19,7 @@ device steps of include/sparkey_gpu.h ("sharded build") in between:
   4. stats      calculateMaxDisplacement (IndexHash.java:195-245) per range with the boundary slots
                 exchanged; the totals are reduced and rank 0 writes the 112-byte header.
 
-Logs the canonical layout does not cover (DELETEs, duplicate keys, a full table) are gathered on
+SNAPPY logs, and logs the canonical layout does not cover (DELETEs, duplicate keys, a full table), are gathered on
 every rank and built with the exact single-GPU path (correct, not scaled).
 
 Collectives go through torch.distributed: backend "nccl" (RCCL over xGMI) moves device tensors;
@@ -320,6 +320,14 @@ class ShardedBuilder:
         data_end = lay.data_end
         s.begin(header, file_len, buf, buf_lo, buf_hi, opts, g, G)
         h = parse_log_header(header)
+        if h["compression_type"] == 1:  # SNAPPY: the whole log on every rank, the single-GPU build
+            slot_lo, slot_hi = s.slot_range(g)
+            slot_size = _slot_size(h, opts, data_end)
+            out_off = 0 if g == 0 else INDEX_HEADER_SIZE + slot_lo * slot_size
+            out_len = (INDEX_HEADER_SIZE if g == 0 else 0) + (slot_hi - slot_lo) * slot_size
+            res = ShardResult(out=None, slot_lo=slot_lo, slot_hi=slot_hi, out_offset=out_off, rounds=0,
+                              phase_ms=phase)
+            return self._gathered(res, header, file_len, buf, buf_lo, buf_hi, lay, opts, slot_size, out_len)
 
         # ---- 1 entries: speculate, frame, verify by induction from c_0 = 84 ----
         uni = uniform_record_size(h)

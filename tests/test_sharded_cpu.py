@@ -80,3 +80,14 @@ def test_sharded_understated_header(tmp_path):
     struct.pack_into("<q", log, 48, 10)
     metas = check(bytes(log), 3, tmp_path, seed=9)
     assert metas[0]["rounds"] >= 1
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_snappy_gather(tmp_path, world):
+    """SNAPPY logs are built whole on every rank (the single-GPU path) and sliced by slot range."""
+    from snappy_log import CompressedLog
+    cl = CompressedLog(1024, file_identifier=0x1234567)
+    for i in range(3000):
+        cl.put(b"Key%d" % i, b"Value%d" % i)
+    metas = check(cl.finish(), world, tmp_path, seed=21)
+    assert metas[0]["path"] == "gathered"

@@ -87,3 +87,12 @@ def test_sharded_gpu_matches_single(native):
     single, _ = native.build_index_mem(log, opts)
     got, metas = run_threads(log, 4, dict(hash_seed=99))
     assert got == single, diff_report(got, single)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_sharded_gpu_snappy_gather(native, world):
+    """SNAPPY logs: gathered on every rank, built by the single-GPU SNAPPY path, sliced by slot range."""
+    from sparkey import synth
+    log = synth.snappy_log(synth.fixed_log(100000, 16, 100, seed=6), 118, 16384).tobytes()
+    metas = check(native, log, world, seed=13)
+    assert metas[0]["path"] == "gathered"
