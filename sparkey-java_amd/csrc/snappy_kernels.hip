@@ -95,9 +95,12 @@ __device__ __forceinline__ uint32_t snappy_decode(In& in, uint32_t n, uint32_t p
   while (p < n) {
     // the tag and the four bytes after it in one round trip
     in.ensure(p, 5);
-    const uint32_t t = in.byte(p);
-    const uint32_t e0 = p + 1 < n ? in.byte(p + 1) : 0u, e1 = p + 2 < n ? in.byte(p + 2) : 0u;
-    const uint32_t e2 = p + 3 < n ? in.byte(p + 3) : 0u, e3 = p + 4 < n ? in.byte(p + 4) : 0u;
+    // uniform across the wave: held in scalar registers, so the element's control flow is scalar
+    const uint32_t t = __builtin_amdgcn_readfirstlane(in.byte(p));
+    const uint32_t e0 = __builtin_amdgcn_readfirstlane(p + 1 < n ? in.byte(p + 1) : 0u);
+    const uint32_t e1 = __builtin_amdgcn_readfirstlane(p + 2 < n ? in.byte(p + 2) : 0u);
+    const uint32_t e2 = __builtin_amdgcn_readfirstlane(p + 3 < n ? in.byte(p + 3) : 0u);
+    const uint32_t e3 = __builtin_amdgcn_readfirstlane(p + 4 < n ? in.byte(p + 4) : 0u);
     p++;
     uint32_t len, off = 0;
     if ((t & 3u) == 0) {
