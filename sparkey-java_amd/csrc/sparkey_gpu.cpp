@@ -434,6 +434,14 @@ static int setup_params(const LogHdr& lh, const IndexParams& ip, const sparkey_b
     // chunk >= kFrameMinChunk and >= maxRecLen; a wave stages kFrameRegion bytes of chunks
     // (SPARKEY_FRAME_CMIN / SPARKEY_FRAME_REGION override both, for tuning)
     int64_t cmin = kFrameMinChunk, region = kFrameRegion, look = kFrameLook;
+    {
+      // Records of mixed sizes (the header's mean record well under the largest) take 1 KiB chunks:
+      // measured 7% faster framing on C3 (8-64 B keys, mean 138 B of at most 168 B), while
+      // fixed-size records keep 512 (1 KiB chunks are 8% slower on C2's 118 B records).
+      const int64_t nrec = std::max<int64_t>(0, lh.num_puts) + std::max<int64_t>(0, lh.num_deletes);
+      const int64_t bytes = std::max<int64_t>(0, lh.put_size) + std::max<int64_t>(0, lh.delete_size);
+      if (nrec > 0 && bytes > 0 && 10 * bytes < 9 * nrec * P.max_rec_len) cmin = 1024;
+    }
     if (const char* v = getenv("SPARKEY_FRAME_CMIN")) cmin = std::max<int64_t>(128, atoll(v));
     if (const char* v = getenv("SPARKEY_FRAME_REGION")) region = std::min<int64_t>(16384, std::max<int64_t>(2048, atoll(v)));
     if (const char* v = getenv("SPARKEY_FRAME_LOOK")) look = std::min<int64_t>(4096, std::max<int64_t>(16, atoll(v)));

@@ -14,7 +14,7 @@ for v in "$@"; do
   envs=""
   if [ "$v" = "alt" ]; then envs="SPARKEY_GPU_LIB=$PWD/sparkey-java_amd/lib/alt/libsparkey_gpu.so"; else envs="$v"; fi
   echo "== $v" >> $OUT/sweep.txt
-  env $envs timeout -k 10 120 python -u bench.py --steps 10 --warmup 2 --no-cpu-baseline > $OUT/b$i.log 2>&1 || { echo "FAILED $v" >> $OUT/sweep.txt; exit 1; }
+  env $envs timeout -k 10 120 python -u bench.py --steps 10 --warmup 2 --no-cpu-baseline $BENCH_ARGS > $OUT/b$i.log 2>&1 || { echo "FAILED $v" >> $OUT/sweep.txt; exit 1; }
   python - $OUT/b$i.log >> $OUT/sweep.txt <<'EOF'
 import json, sys
 for line in open(sys.argv[1]):
