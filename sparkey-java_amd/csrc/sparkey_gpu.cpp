@@ -243,7 +243,7 @@ hipError_t grow_keep(T** p, uint64_t& have, uint64_t want, uint64_t used, hipStr
   return hipSuccess;
 }
 
-constexpr uint64_t kSnappyChunk = 2048;  // blocks per k_snappy_dir launch
+constexpr uint64_t kSnappyChunk = 1024;  // blocks per k_snappy_dir launch (swept 256-4096)
 
 }  // namespace
 
@@ -675,6 +675,8 @@ static int plan_build_snappy(sparkey_plan* pl, const LogHdr& lh, const uint8_t* 
   // (dir error 3 past it); decode = false only follows the chain.
   SnappyDirResult dir;
   memset(&dir, 0, sizeof(dir));
+  uint64_t chunk = kSnappyChunk;
+  if (const char* v = getenv("SPARKEY_SNAPPY_CHUNK")) chunk = std::max<uint64_t>(16, strtoull(v, nullptr, 10));  // tuning
   auto pipeline = [&](int64_t vcap, bool decode) -> hipError_t {
     hipError_t e;
     if ((e = hipMemsetAsync(pl->sn_dir, 0, sizeof(SnappyDirResult), s)) != hipSuccess) return e;
@@ -688,7 +690,7 @@ static int plan_build_snappy(sparkey_plan* pl, const LogHdr& lh, const uint8_t* 
       S.walk = pl->sn_walk;
       S.dir = pl->sn_dir;
       const uint64_t before = dir.nblk;
-      S.dir_limit = std::min<uint64_t>(S.blk_cap, before + kSnappyChunk);
+      S.dir_limit = std::min<uint64_t>(S.blk_cap, before + chunk);
       launch_snappy_dir(S, s);
       if ((e = hipGetLastError()) != hipSuccess) return e;
       if ((e = hipMemcpyAsync(&dir, pl->sn_dir, sizeof(dir), hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
