@@ -343,9 +343,18 @@ __global__ void __launch_bounds__(256) k_snappy_rewrite(SnappyParams S) {
   if (s >= S.cap) return;
   const uint8_t* is = S.itab + s * (uint64_t)(S.ihs + S.ias);
   uint8_t* os = S.otab + s * (uint64_t)(S.hs + S.as);
+  // 16-byte slots on both sides (8-byte hash and address; tables start 112 bytes into 16-byte
+  // aligned buffers): one 16-byte load and store per slot
+  const bool wide = S.ihs == 8 && S.ias == 8 && S.hs == 8 && S.as == 8 && !((uintptr_t)S.otab & 15);
   uint64_t h = 0, a = 0;
-  for (int i = 0; i < S.ihs; i++) h |= (uint64_t)is[i] << (8 * i);
-  for (int i = 0; i < S.ias; i++) a |= (uint64_t)is[S.ihs + i] << (8 * i);
+  if (wide) {
+    const uint4 v = *(const uint4*)is;
+    h = v.x | ((uint64_t)v.y << 32);
+    a = v.z | ((uint64_t)v.w << 32);
+  } else {
+    for (int i = 0; i < S.ihs; i++) h |= (uint64_t)is[i] << (8 * i);
+    for (int i = 0; i < S.ias; i++) a |= (uint64_t)is[S.ihs + i] << (8 * i);
+  }
   uint64_t fa = 0;
   if (a != 0) {
     uint64_t lo = 0, hi = S.nblk - 1;                          // the block holding virtual offset a
@@ -363,6 +372,10 @@ __global__ void __launch_bounds__(256) k_snappy_rewrite(SnappyParams S) {
     }
     if (l >= min(S.walk[lo].count, S.mepb) || offs[l] != rel) atomicOr(S.err, 1);
     fa = ((uint64_t)B.file_pos << S.ebb) | l;
+  }
+  if (wide) {
+    *(uint4*)os = make_uint4((uint32_t)h, (uint32_t)(h >> 32), (uint32_t)fa, (uint32_t)(fa >> 32));
+    return;
   }
   for (int i = 0; i < S.hs; i++) os[i] = (uint8_t)(h >> (8 * i));
   for (int i = 0; i < S.as; i++) os[S.hs + i] = (uint8_t)(fa >> (8 * i));

@@ -62,13 +62,15 @@ def test_empty_and_single(native):
     check(native, cl.finish())
 
 
-def test_c2_shaped(native):
-    """C2's record shape (16 B keys, 100 B values), 200K records, 64 KiB blocks."""
+@pytest.mark.parametrize("hash_size", [0, 8])
+def test_c2_shaped(native, hash_size):
+    """C2's record shape (16 B keys, 100 B values), 200K records, 64 KiB blocks (8-byte addresses;
+    hash_size 8 takes the rewrite's 16-byte slot path)."""
     rng = random.Random(9)
     cl = CompressedLog(65536, file_identifier=5)
     for i in range(200000):
         cl.put(struct.pack("<QQ", i, rng.getrandbits(64)), bytes([i & 0xFF]) * 60 + rng.randbytes(40))
-    check(native, cl.finish(), seed=99)
+    check(native, cl.finish(), seed=99, hash_size=hash_size)
 
 
 def test_errors(native):
