@@ -16,7 +16,10 @@ Prints ONE JSON line on rank 0.
 import argparse
 import json
 import os
+import platform
+import shutil
 import sys
+import tempfile
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -28,7 +31,7 @@ import torch  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 METRIC = "keys/s device-resident hash-file build, 10M entries; HBM GB/s vs peak"
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_pmc_summary.json")
+PMC_SUMMARIES = [os.path.join(ROOT, "profiles", f) for f in ("r02_pmc_summary.json", "r01_pmc_summary.json")]
 HASH_SEED = 0x2545F491
 
 
@@ -50,12 +53,39 @@ def stage_bytes(stage, n, data_end, slot, cap, passes=2, comp_end=None):
     }.get(stage, 0)
 
 
-def pmc_traffic(stage):
+def pmc_traffic(workload, stage):
+    """HBM bytes per launch of `stage` on `workload` from the committed rocprofv3 PMC summary
+    (tools/pmc_summary.py), or None when that workload's kernel was not counted."""
+    for path in PMC_SUMMARIES:
+        try:
+            with open(path) as f:
+                pmc = json.load(f)
+        except (OSError, ValueError):
+            continue
+        per = pmc.get("per_launch_hbm_bytes_by_workload", {}).get(workload)
+        if per is None and workload == "c2":
+            per = pmc.get("per_launch_hbm_bytes")
+        if per and stage in per:
+            return per[stage]
+    return None
+
+
+def host_info():
+    """The CPU the baseline ran on: model, logical CPUs of the machine and of this process."""
+    model = platform.processor() or ""
     try:
-        pmc = json.load(open(PMC_SUMMARY))
-        return pmc.get("per_launch_hbm_bytes", {}).get(stage)
-    except Exception:
-        return None
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        usable = os.cpu_count()
+    return {"cpu_model": model, "nproc": os.cpu_count(), "usable_cpus": usable}
 
 
 WORKLOADS = {
@@ -205,6 +235,7 @@ def single_gpu(args, dev):
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t_start
     plan.set_profiling(False)
+    headline_spi = d_out.cpu().numpy().tobytes()  # the headline path's own output (checked below)
 
     ms_per_step = elapsed * 1000.0 / args.steps
     slot = stats.hash_size + stats.address_size
@@ -260,19 +291,51 @@ def single_gpu(args, dev):
         finally:
             del os.environ["SPARKEY_NO_UNIFORM"]
 
-    cpu = None
-    if not args.no_cpu_baseline:
-        import oracle
-        oracle.build()
-        log_bytes = log_np.tobytes()
-        t2 = time.perf_counter()
-        mname = "SORTING" if wl["sorting"] else "IN_MEMORY"
-        want = oracle.build_index(log_bytes, HASH_SEED, method=oracle.SORTING if wl["sorting"] else oracle.IN_MEMORY)
-        cpu_s = time.perf_counter() - t2
-        got = d_out.cpu().numpy().tobytes()
-        cpu = {"value": n / cpu_s, "unit": "keys/s", "cores": 1, "kind": "port",
-               "sample": f"full {args.workload.upper()} log ({n} records), oracle {mname} sequential restatement "
-                         f"(oracle/), 1 thread, {cpu_s:.2f} s", "bit_identical_to_gpu": got == want}
+    # file -> file (north_star: "log file in, hash file out"): sparkey_build_index_file, the entry
+    # point the JNI shim calls, on the same log written to a file; page-cache warm, fsync off (the
+    # writer's default), its per-device context kept across calls
+    file_rate = file_spi = None
+    tmpdir = tempfile.mkdtemp(prefix="sparkey_bench_")
+    log_path, spi_path = os.path.join(tmpdir, "bench.spl"), os.path.join(tmpdir, "bench.spi")
+    try:
+        log_np.tofile(log_path)
+        if args.workload in ("c2", "c3", "c5", "churn", "snappy"):
+            _native.build_index_file(log_path, spi_path, opts)
+            reps_f = 3
+            t_f = time.perf_counter()
+            for _ in range(reps_f):
+                _native.build_index_file(log_path, spi_path, opts)
+            file_rate = n * reps_f / (time.perf_counter() - t_f)
+            with open(spi_path, "rb") as f:
+                file_spi = f.read()
+            _native.release_cached_resources()
+
+        cpu = None
+        if not args.no_cpu_baseline:
+            import oracle
+            oracle.build()
+            mname = "SORTING" if wl["sorting"] else "IN_MEMORY"
+            method_o = oracle.SORTING if wl["sorting"] else oracle.IN_MEMORY
+            t2 = time.perf_counter()
+            want = oracle.build_index(log_np, HASH_SEED, method=method_o)
+            cpu_s = time.perf_counter() - t2
+            # the same restatement file -> file: read the log file, build, write the .spi file
+            t3 = time.perf_counter()
+            with open(log_path, "rb") as f:
+                log_file_bytes = f.read()
+            want_f = oracle.build_index(log_file_bytes, HASH_SEED, method=method_o)
+            with open(spi_path + ".cpu", "wb") as f:
+                f.write(want_f)
+            cpu_file_s = time.perf_counter() - t3
+            del log_file_bytes
+            cpu = {"value": n / cpu_s, "unit": "keys/s", "cores": 1, "kind": "port",
+                   "sample": f"full {args.workload.upper()} log ({n} records), oracle {mname} sequential "
+                             f"restatement (oracle/), 1 thread, {cpu_s:.2f} s", "host": host_info(),
+                   "file_to_file_keys_per_s": n / cpu_file_s,
+                   "bit_identical_to_gpu": headline_spi == want,
+                   "file_bit_identical_to_gpu": None if file_spi is None else file_spi == want_f}
+    finally:
+        shutil.rmtree(tmpdir, ignore_errors=True)
     plan.close()
     return {
         "value": n * args.steps / elapsed, "ms_per_step": ms_per_step,
@@ -282,7 +345,8 @@ def single_gpu(args, dev):
                    "parallelism": "single"},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS,
-                     "traffic": pmc_traffic({("frame", 2): "frame_uniform", ("partition", 1): "partition_regions"}.get(
+                     "traffic": pmc_traffic(args.workload, {("frame", 2): "frame_uniform",
+                                                            ("partition", 1): "partition_regions"}.get(
                          (dom, stats.framing_path if dom == "frame" else passes), dom)),
                      "algorithmic_bytes_per_launch": dom_bytes, "avg_launch_ms": stage_ms.get(dom) if dom else None},
         "build_hbm_gbs": b_alg / (ms_per_step * 1e-3) / 1e9,
@@ -293,6 +357,7 @@ def single_gpu(args, dev):
         "framing": {0: "k_frame (speculative)", 1: "serial walk", 2: "k_frame_uniform (uniform records)"}[stats.framing_path],
         "general_framing": general,
         "host_to_host_keys_per_s": h2h,
+        "file_to_file_keys_per_s": file_rate,
         "cpu_baseline": cpu,
         "gen_s": gen_s,
         "version": sparkey.version(),

@@ -87,6 +87,12 @@ int sparkey_build_index_mem(const uint8_t* log, uint64_t log_len, uint8_t* index
                             const sparkey_build_opts* opts, sparkey_build_stats* stats_out, char* err,
                             size_t err_len);
 
+/* The two entry points above keep a per-device context across calls (build workspace, device
+ * buffers for the log and the .spi, pinned staging, I/O threads), so repeated builds pay no
+ * allocation.  This frees every such context (waiting for calls in flight); the next call builds a
+ * new one.  With SPARKEY_FILE_CACHE=0 in the environment nothing is kept between calls. */
+void sparkey_release_cached_resources(void);
+
 /* .spi size for a log (needs only its 84-byte header): 112 + slotSize * capacity, or < 0. */
 int64_t sparkey_index_size(const uint8_t* log_header, uint64_t header_len, const sparkey_build_opts* opts);
 

@@ -146,7 +146,8 @@ struct BuildParams {
   MaxPlus* scan_scratch_mp;
   // k_frame granules (zeroed before every launch)
   unsigned long long* exit_desc;
-  unsigned long long* cnt_desc;
+  unsigned int* frame_ticket;     // k_frame wave tickets (zeroed with the granules)
+  unsigned long long fr_spin_ticks;  // bound on a wave's wait for its predecessor (100 MHz ticks)
   // radix partition
   uint32_t* p1_hist;  // [256][p1_tiles]
   uint64_t* p1_off;

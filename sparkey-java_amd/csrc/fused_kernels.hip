@@ -142,7 +142,6 @@ __device__ inline uint64_t murmur64_ld(const Ld& ld, int32_t len, uint32_t seed)
 // granules (8-byte {state, value} words) -- relaxed agent-scope atomics, zeroed before the launch
 // ------------------------------------------------------------------------------------------------
 constexpr unsigned long long kReady = 1ull << 63;   // exit granule: bit 63 = published
-constexpr unsigned long long kSpinTicks = 2000000000ull;  // 20 s of the 100 MHz wall clock
 
 __device__ __forceinline__ void granule_store(unsigned long long* g, unsigned long long v) {
   __hip_atomic_store(g, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -233,7 +232,12 @@ __device__ __forceinline__ int32_t cand_steps(uint32_t v) { return (int32_t)((v 
 __global__ __launch_bounds__(64) void k_frame(BuildParams P) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int lane = threadIdx.x;
-  const uint64_t wv = blockIdx.x;
+  // The wave's place in the chain comes from a ticket, not blockIdx.x: a wave that spins on wave
+  // wv - 1's published exit knows that wave already took its ticket, so it is resident and runs to
+  // its publish whatever order the dispatcher admits workgroups in.
+  unsigned int tk = 0;
+  if (lane == 0) tk = atomicAdd(P.frame_ticket, 1u);
+  const uint64_t wv = (uint64_t)__builtin_amdgcn_readfirstlane(tk);
   const int cs = P.fr_cshift;
   const int64_t C = 1ll << cs;
   const int W = P.fr_w;
@@ -577,7 +581,7 @@ __global__ __launch_bounds__(64) void k_frame(BuildParams P) {
       for (;;) {
         const unsigned long long v = granule_load(&P.exit_desc[wv - 1]);
         if (v & kReady) { extv = v & ~kReady; break; }
-        if (wall_clock64() - t0 > kSpinTicks) {  // should a predecessor never run: serial path
+        if (wall_clock64() - t0 >= P.fr_spin_ticks) {  // bounded all the same: serial path
           atomicOr(&P.st->spec_fail, 2u);
           extv = (unsigned long long)s;
           break;

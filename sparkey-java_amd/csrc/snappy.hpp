@@ -53,7 +53,7 @@ struct SnappyParams {
   SnappyBlock* blocks;
   uint64_t blk_cap;
   uint64_t dir_limit;       // k_snappy_dir stops at this many blocks
-  int64_t vcap;             // decompressed bytes the virtual log holds (0: unbounded)
+  int64_t vcap;             // decompressed bytes the virtual log holds (< 0: unbounded)
   uint64_t blk_base;        // decode launches: first block
   SnappyDirResult* dir;
   uint8_t* vlog;            // virtual log (84 header bytes written by the host)

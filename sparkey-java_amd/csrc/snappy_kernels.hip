@@ -240,7 +240,7 @@ __global__ void __launch_bounds__(64) k_snappy_dir(SnappyParams S) {
     // the reader's buffers: maxBlockSize decompressed, Snappy.maxCompressedLength(maxBlockSize) compressed
     // (CompressedReader.java:40-49)
     if ((int64_t)ulen > S.max_block || (int64_t)clen > 32 + S.max_block + S.max_block / 6) { err = 2; break; }
-    if (S.vcap && (int64_t)(total + (uint64_t)ulen) > S.vcap) { err = 3; break; }
+    if (S.vcap >= 0 && (int64_t)(total + (uint64_t)ulen) > S.vcap) { err = 3; break; }
     {
       SnappyBlock B;
       B.file_pos = p;

@@ -545,7 +545,10 @@ static int reserve_for_framing(sparkey_plan* pl, BuildParams& P, int framing_pat
   P.bcount = pl->bcount; P.bcursor = pl->bcursor; P.boff = pl->boff; P.bfun = pl->bfun; P.bpre = pl->bpre;
   P.bfun_total = pl->bfun_total; P.carry = pl->carry; P.pairs = pl->pairs; P.pair_cap = pl->c_pairs / 2;
   P.parts = pl->parts; P.scan_scratch_u64 = pl->scan_u64; P.scan_scratch_mp = pl->scan_mp;
-  P.exit_desc = pl->desc; P.cnt_desc = pl->desc + nwaves;
+  P.exit_desc = pl->desc;
+  P.frame_ticket = reinterpret_cast<unsigned int*>(pl->desc + 2 * nwaves);
+  P.fr_spin_ticks = 2000000000ull;  // 20 s of the 100 MHz wall clock
+  if (const char* v = getenv("SPARKEY_FRAME_SPIN_TICKS")) P.fr_spin_ticks = strtoull(v, nullptr, 10);  // (tests)
   P.p1_hist = pl->p1_hist; P.p1_off = pl->p1_off; P.p1_off_total = pl->p1_off + 256ull * P.p1_tiles;
   return SPARKEY_OK;
 }
@@ -629,22 +632,29 @@ static int plan_build_snappy(sparkey_plan* pl, const LogHdr& lh, const uint8_t* 
     set_err(err, err_len, "null argument");
     return SPARKEY_E_ARG;
   }
+  if (((uintptr_t)d_log & 15) || ((uintptr_t)d_out & 15)) {  // k_snappy_dir reads 16-byte aligned windows
+    set_err(err, err_len, "device buffers must be 16-byte aligned");
+    return SPARKEY_E_ARG;
+  }
   if (lh.compression_block_size < 0) {  // new byte[maxBlockSize] (CompressedReader.java:40-49)
     set_err(err, err_len, "Corrupt log file: negative compression block size");
     return SPARKEY_E_CORRUPT_LOG;
   }
   HIP_TRY(hipSetDevice(pl->device));
   if (!s) s = pl->own_stream;
-  hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+  struct Events {  // destroyed on every return path
+    hipEvent_t e[4] = {nullptr, nullptr, nullptr, nullptr};
+    ~Events() {
+      for (auto& x : e)
+        if (x) (void)hipEventDestroy(x);
+    }
+  } evs;
+  hipEvent_t* ev = evs.e;
   const bool timed = pl->timer.enabled;
   if (timed) {
-    for (auto& e : ev) HIP_TRY(hipEventCreate(&e));
+    for (auto& e : evs.e) HIP_TRY(hipEventCreate(&e));
     HIP_TRY(hipEventRecord(ev[0], s));
   }
-  auto drop_events = [&]() {
-    for (auto& e : ev)
-      if (e) (void)hipEventDestroy(e);
-  };
   SnappyParams S;
   memset(&S, 0, sizeof(S));
   S.log = d_log;
@@ -656,7 +666,11 @@ static int plan_build_snappy(sparkey_plan* pl, const LogHdr& lh, const uint8_t* 
   const int64_t mb = lh.compression_block_size;
   const int64_t lds = ((mb + 15) & ~15LL) + 16 + 8192 + 16;
   S.lds_bytes = lds <= 160 * 1024 ? (uint32_t)lds : 0u;
-  const uint32_t mepb = (uint32_t)std::max<int32_t>(1, lh.max_entries_per_block);
+  // Record offsets per block: maxEntriesPerBlock from the header, bounded by what a block can hold
+  // (every record is at least 2 bytes), so a corrupt header cannot size a huge allocation; a block
+  // with more records than the header allows is still flagged by the walk.
+  const uint32_t mepb = (uint32_t)std::max<int64_t>(
+      1, std::min<int64_t>(lh.max_entries_per_block, (int64_t)lh.compression_block_size / 2 + 1));
   S.mepb = mepb;
   HIP_TRY(grow(&pl->sn_dir, pl->c_sn_dir, 1));
   HIP_TRY(grow(&pl->sn_err, pl->c_sn_err, 1));
@@ -720,13 +734,17 @@ static int plan_build_snappy(sparkey_plan* pl, const LogHdr& lh, const uint8_t* 
   // the reference writer's logs decompress to exactly putSize + deleteSize record bytes
   // (LogHeader.put / delete, LogHeader.java:161-172); a header that understates them gets a
   // directory-only pass to size the virtual log
-  const int64_t hdr_total = std::max<int64_t>(0, lh.put_size) + std::max<int64_t>(0, lh.delete_size);
-  HIP_TRY(grow(&pl->sn_vlog, pl->c_sn_vlog, (uint64_t)hdr_total + kLogHeaderSize + 4096));
+  // (and a header that overstates them beyond what the blocks can decompress to -- Snappy expands at
+  // most 64 bytes per 3-byte copy -- is sized the same way instead of trusted with a huge allocation)
+  const uint64_t ps = (uint64_t)std::max<int64_t>(0, lh.put_size), ds = (uint64_t)std::max<int64_t>(0, lh.delete_size);
+  const uint64_t hdr_total = ps + ds < ps ? UINT64_MAX : ps + ds;
+  const int64_t vcap0 = hdr_total <= 22 * body + 4096 ? (int64_t)hdr_total : 0;
+  HIP_TRY(grow(&pl->sn_vlog, pl->c_sn_vlog, (uint64_t)vcap0 + kLogHeaderSize + 4096));
   S.vlog = pl->sn_vlog;
-  HIP_TRY(pipeline(hdr_total, true));
-  if (dir.err == 3) {
+  HIP_TRY(pipeline(vcap0, true));
+  if (dir.err == 3) {  // more decompressed bytes than vcap0 (putSize = deleteSize = 0 included)
     HIP_TRY(hipStreamSynchronize(s));
-    HIP_TRY(pipeline(0, false));
+    HIP_TRY(pipeline(-1, false));
     if (!dir.err) {
       HIP_TRY(grow(&pl->sn_vlog, pl->c_sn_vlog, dir.total + kLogHeaderSize + 4096));
       S.vlog = pl->sn_vlog;
@@ -735,7 +753,6 @@ static int plan_build_snappy(sparkey_plan* pl, const LogHdr& lh, const uint8_t* 
   }
   if (dir.err) {
     HIP_TRY(hipStreamSynchronize(s));
-    drop_events();
     set_err(err, err_len, dir.err == 2 ? "Corrupt log file: compressed block larger than the reader's buffers"
                                        : "Corrupt log file: bad compressed block header");
     return SPARKEY_E_CORRUPT_LOG;
@@ -773,13 +790,11 @@ static int plan_build_snappy(sparkey_plan* pl, const LogHdr& lh, const uint8_t* 
   for (uint64_t b = 0; b < nblk; b++) {
     const SnappyWalk& w = walks[b];
     if (w.flags & kWalkBadStream) {
-      drop_events();
       set_err(err, err_len, "Corrupt log file: bad snappy stream in block at " + std::to_string(blocks[b].file_pos));
       return SPARKEY_E_CORRUPT_LOG;
     }
     if (carry == 0) {
       if (w.flags) {
-        drop_events();
         set_err(err, err_len, (w.flags & kWalkTooMany)
                                   ? "Corrupt log file: more entries in a block than maxEntriesPerBlock"
                                   : "Corrupt log file: bad record header in block at " +
@@ -790,13 +805,11 @@ static int plan_build_snappy(sparkey_plan* pl, const LogHdr& lh, const uint8_t* 
     } else if (carry >= (int64_t)blocks[b].ulen) {
       carry -= blocks[b].ulen;
     } else {
-      drop_events();
       set_err(err, err_len, "a record ends inside a later compressed block (not a layout CompressedWriter writes)");
       return SPARKEY_E_UNSUPPORTED;
     }
   }
   if (carry) {
-    drop_events();
     set_err(err, err_len, "Corrupt log file: the last record runs past dataEnd");
     return SPARKEY_E_CORRUPT_LOG;
   }
@@ -807,16 +820,10 @@ static int plan_build_snappy(sparkey_plan* pl, const LogHdr& lh, const uint8_t* 
   rc = parse_log_header(vh, kLogHeaderSize, vlen, &vlh, err, err_len);
   IndexParams vip;
   if (!rc) rc = make_index_params(vlh, o2, &vip, err, err_len);
-  if (rc) {
-    drop_events();
-    return rc;
-  }
+  if (rc) return rc;
   HIP_TRY(grow(&pl->sn_itab, pl->c_sn_itab, (uint64_t)vip.index_size));
   rc = plan_build(pl, vh, pl->sn_vlog, vlen, pl->sn_itab, (uint64_t)vip.index_size, &o2, s, stats_out, err, err_len);
-  if (rc) {
-    drop_events();
-    return rc;
-  }
+  if (rc) return rc;
   if (timed) HIP_TRY(hipEventRecord(ev[2], s));
   uint8_t hdr[kIndexHeaderSize];
   index_header_template(lh, ip, opts->hash_seed, hdr);
@@ -836,11 +843,8 @@ static int plan_build_snappy(sparkey_plan* pl, const LogHdr& lh, const uint8_t* 
   HIP_TRY(hipGetLastError());
   int32_t rerr = 0;
   HIP_TRY(hipMemcpyAsync(&rerr, pl->sn_err, sizeof(rerr), hipMemcpyDeviceToHost, s));
-  hipEvent_t ev_end = nullptr;
-  if (timed) {
-    HIP_TRY(hipEventCreate(&ev_end));
-    HIP_TRY(hipEventRecord(ev_end, s));
-  }
+  hipEvent_t ev_end = ev[3];
+  if (timed) HIP_TRY(hipEventRecord(ev_end, s));
   HIP_TRY(hipStreamSynchronize(s));
   if (timed) {  // stages of the front end and the rewrite around the inner build's own stages
     float t0 = 0.f, t1 = 0.f;
@@ -850,9 +854,7 @@ static int plan_build_snappy(sparkey_plan* pl, const LogHdr& lh, const uint8_t* 
     pl->stage_ms.insert(pl->stage_ms.begin(), t0);
     pl->stage_names.push_back("snappy_rewrite");
     pl->stage_ms.push_back(t1);
-    (void)hipEventDestroy(ev_end);
   }
-  drop_events();
   if (rerr) {
     set_err(err, err_len, "internal error: a slot's record is not a block record start");
     return SPARKEY_E_CORRUPT_LOG;
@@ -1110,6 +1112,13 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
   }
   fill_stats(stats_out, st, ip, placement_path, framing_path, ms, regions_used ? 1 : 2);
   return SPARKEY_OK;
+}
+
+// LogHeader.read with the file's real length (file_build.cpp): the dataEnd > file length check
+// (LogHeader.java:81-83) needs it.
+int sk_check_log_header(const uint8_t* b, uint64_t hdr_len, uint64_t file_len, char* err, size_t err_len) {
+  LogHdr lh;
+  return parse_log_header(b, hdr_len, file_len, &lh, err, err_len, true);
 }
 
 extern "C" {
@@ -1390,135 +1399,6 @@ int64_t sparkey_index_size(const uint8_t* log_header, uint64_t header_len, const
   rc = make_index_params(lh, *opts, &ip, nullptr, 0);
   if (rc) return rc;
   return ip.index_size;
-}
-
-int sparkey_build_index_mem(const uint8_t* log, uint64_t log_len, uint8_t* index_out, uint64_t index_cap,
-                            const sparkey_build_opts* opts, sparkey_build_stats* stats_out, char* err,
-                            size_t err_len) {
-  if (!log || !index_out || !opts) {
-    set_err(err, err_len, "null argument");
-    return SPARKEY_E_ARG;
-  }
-  LogHdr lh;
-  int rc = parse_log_header(log, log_len, log_len, &lh, err, err_len, true);
-  if (rc) return rc;
-  IndexParams ip;
-  rc = make_index_params(lh, *opts, &ip, err, err_len);
-  if (rc) return rc;
-  if ((uint64_t)ip.index_size > index_cap) {
-    set_err(err, err_len, "index buffer too small: need " + std::to_string(ip.index_size));
-    return SPARKEY_E_BUFFER;
-  }
-  sparkey_plan* pl = nullptr;
-  rc = sparkey_plan_create(&pl, opts->device, 0, 0, err, err_len);
-  if (rc) return rc;
-  uint8_t* d_log = nullptr;
-  uint8_t* d_out = nullptr;
-  auto cleanup = [&]() {
-    if (d_log) (void)hipFree(d_log);
-    if (d_out) (void)hipFree(d_out);
-    sparkey_plan_destroy(pl);
-  };
-  if (hipMalloc((void**)&d_log, std::max<uint64_t>(log_len, 16)) != hipSuccess ||
-      hipMalloc((void**)&d_out, (size_t)ip.index_size) != hipSuccess) {
-    cleanup();
-    set_err(err, err_len, "hipMalloc failed");
-    return SPARKEY_E_GPU;
-  }
-  if (hipMemcpyAsync(d_log, log, log_len, hipMemcpyHostToDevice, pl->own_stream) != hipSuccess) {
-    cleanup();
-    set_err(err, err_len, "H2D copy failed");
-    return SPARKEY_E_GPU;
-  }
-  rc = plan_build(pl, log, d_log, log_len, d_out, (uint64_t)ip.index_size, opts, pl->own_stream, stats_out, err,
-                  err_len);
-  if (rc == SPARKEY_OK) {
-    if (hipMemcpyAsync(index_out, d_out, (size_t)ip.index_size, hipMemcpyDeviceToHost, pl->own_stream) != hipSuccess ||
-        hipStreamSynchronize(pl->own_stream) != hipSuccess) {
-      set_err(err, err_len, "D2H copy failed");
-      rc = SPARKEY_E_GPU;
-    }
-  }
-  cleanup();
-  return rc;
-}
-
-int sparkey_build_index_file(const char* log_path, const char* index_out_path, const sparkey_build_opts* opts,
-                             int32_t fsync_out, sparkey_build_stats* stats_out, char* err, size_t err_len) {
-  if (!log_path || !index_out_path || !opts) {
-    set_err(err, err_len, "null argument");
-    return SPARKEY_E_ARG;
-  }
-  int fd = open(log_path, O_RDONLY);
-  if (fd < 0) {
-    set_err(err, err_len, std::string("cannot open log file ") + log_path + ": " + strerror(errno));
-    return SPARKEY_E_IO;
-  }
-  struct stat sb;
-  if (fstat(fd, &sb) != 0) {
-    close(fd);
-    set_err(err, err_len, "fstat failed");
-    return SPARKEY_E_IO;
-  }
-  const uint64_t log_len = (uint64_t)sb.st_size;
-  uint8_t* hlog = nullptr;
-  if (hipHostMalloc((void**)&hlog, std::max<uint64_t>(log_len, 16), hipHostMallocDefault) != hipSuccess) {
-    close(fd);
-    set_err(err, err_len, "pinned allocation failed");
-    return SPARKEY_E_GPU;
-  }
-  uint64_t got = 0;
-  while (got < log_len) {
-    const ssize_t r = read(fd, hlog + got, (size_t)std::min<uint64_t>(log_len - got, 1ull << 30));
-    if (r <= 0) break;
-    got += (uint64_t)r;
-  }
-  close(fd);
-  if (got != log_len) {
-    (void)hipHostFree(hlog);
-    set_err(err, err_len, "short read of log file");
-    return SPARKEY_E_IO;
-  }
-  const int64_t isz = sparkey_index_size(hlog, log_len, opts);
-  if (isz < 0) {
-    LogHdr lh;
-    int rc = parse_log_header(hlog, log_len, log_len, &lh, err, err_len, true);
-    (void)hipHostFree(hlog);
-    if (!rc) set_err(err, err_len, code_message((int)isz));
-    return rc ? rc : (int)isz;
-  }
-  uint8_t* hidx = nullptr;
-  if (hipHostMalloc((void**)&hidx, (size_t)isz, hipHostMallocDefault) != hipSuccess) {
-    (void)hipHostFree(hlog);
-    set_err(err, err_len, "pinned allocation failed");
-    return SPARKEY_E_GPU;
-  }
-  int rc = sparkey_build_index_mem(hlog, log_len, hidx, (uint64_t)isz, opts, stats_out, err, err_len);
-  (void)hipHostFree(hlog);
-  if (rc == SPARKEY_OK) {  // FileFlushingData.close: header then slots (+fsync), FileFlushingData.java:20-34
-    int ofd = open(index_out_path, O_WRONLY | O_CREAT | O_TRUNC, 0644);
-    if (ofd < 0) {
-      set_err(err, err_len, std::string("cannot create index file ") + index_out_path + ": " + strerror(errno));
-      rc = SPARKEY_E_IO;
-    } else {
-      uint64_t put = 0;
-      while (put < (uint64_t)isz) {
-        const ssize_t w = write(ofd, hidx + put, (size_t)std::min<uint64_t>((uint64_t)isz - put, 1ull << 30));
-        if (w <= 0) break;
-        put += (uint64_t)w;
-      }
-      if (put != (uint64_t)isz) {
-        set_err(err, err_len, "short write of index file");
-        rc = SPARKEY_E_IO;
-      } else if (fsync_out && fsync(ofd) != 0) {
-        set_err(err, err_len, "fsync failed");
-        rc = SPARKEY_E_IO;
-      }
-      close(ofd);
-    }
-  }
-  (void)hipHostFree(hidx);
-  return rc;
 }
 
 }  // extern "C"

@@ -101,6 +101,8 @@ _lib.sparkey_gpu_version.argtypes = []
 _lib.sparkey_gpu_version.restype = ctypes.c_char_p
 _lib.sparkey_strerror.argtypes = [ctypes.c_int]
 _lib.sparkey_strerror.restype = ctypes.c_char_p
+_lib.sparkey_release_cached_resources.argtypes = []
+_lib.sparkey_release_cached_resources.restype = None
 
 
 
@@ -154,7 +156,7 @@ for _name, (_args, _res) in _SIGS.items():
 EXPORTED = list(_SIGS) + ["sparkey_build_index_file", "sparkey_build_index_mem", "sparkey_index_size", "sparkey_plan_create",
             "sparkey_plan_build_device", "sparkey_plan_set_profiling", "sparkey_plan_stage_count",
             "sparkey_plan_stage_name", "sparkey_plan_stage_ms", "sparkey_plan_destroy", "sparkey_gpu_version",
-            "sparkey_strerror"]
+            "sparkey_strerror", "sparkey_release_cached_resources"]
 
 
 class SparkeyIOError(OSError):
@@ -209,6 +211,11 @@ def build_index_file(log_path: str, index_path: str, opts: BuildOpts, fsync: boo
     if rc != OK:
         raise_for(rc, err.value.decode(errors="replace"))
     return stats
+
+
+def release_cached_resources() -> None:
+    """Frees the per-device contexts the file / host-memory entry points keep across calls."""
+    _lib.sparkey_release_cached_resources()
 
 
 def build_index_mem(log: bytes, opts: BuildOpts):

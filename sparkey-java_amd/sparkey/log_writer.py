@@ -108,13 +108,22 @@ class LogWriter:
 
     @classmethod
     def openExisting(cls, path: str) -> "LogWriter":
+        """LogWriter(File) (LogWriter.java:33-61): header read, file truncated to dataEnd.  A SNAPPY or
+        ZSTD log opens build-only: its header (maxEntriesPerBlock included) is kept as it is, and
+        put/delete raise, since this mirror writes no compressed blocks."""
         with open(path, "rb") as f:
             h = LogHeader.from_bytes(f.read(LOG_HEADER_SIZE))
         with open(path, "r+b") as f:  # LogWriter.java:45-55: truncate to dataEnd
             f.truncate(h.data_end)
         return cls(path, h)
 
+    def _check_appendable(self) -> None:
+        if self.header.compression_type != CompressionType.NONE:
+            raise NotImplementedError("appending to a compressed log is not supported by this writer "
+                                      "(only CompressionType.NONE records are produced)")
+
     def put(self, key: bytes, value: bytes) -> None:
+        self._check_appendable()
         if isinstance(key, str):
             key = key.encode("utf-8")
         if isinstance(value, str):
@@ -128,6 +137,7 @@ class LogWriter:
             self._drain()
 
     def delete(self, key: bytes) -> None:
+        self._check_appendable()
         if isinstance(key, str):
             key = key.encode("utf-8")
         if len(key) > self.header.max_key_len:  # LogWriter.java:110-115
@@ -148,6 +158,13 @@ class LogWriter:
     def flush(self, fsync: bool = False) -> None:
         """LogWriter.flush (LogWriter.java:71-80): data, then the header with dataEnd = file length."""
         self._drain()
+        if self.header.compression_type != CompressionType.NONE:
+            # nothing was appended (put/delete raise): CompressedWriter keeps maxEntriesPerBlock and
+            # the file ends at dataEnd, so the header the reference rewrites is the same bytes
+            if fsync:
+                with open(self.path, "r+b") as f:
+                    os.fsync(f.fileno())
+            return
         self.header.max_entries_per_block = 1  # UncompressedBlockOutput.getMaxEntriesPerBlock
         self.header.data_end = os.path.getsize(self.path)
         with open(self.path, "r+b") as f:

@@ -106,3 +106,16 @@ def test_many_small_blocks(native):
     """More blocks than the first directory allocation and many 2048-block chunks."""
     rng = random.Random(12)
     check(native, _compressed(_ops(rng, 6000, 10 ** 9, 0.0, 40), 12))
+
+
+@pytest.mark.parametrize("put_size,delete_size", [(0, 0), (-5, -1), (1 << 62, 1 << 62), (1 << 62, 0)])
+def test_header_sizes_zero_or_absurd(native, put_size, delete_size):
+    """putSize = deleteSize = 0 on a multi-block log (a zero-sized virtual log must not bound the
+    decode at nothing), negative sizes, and sizes no block chain can decompress to (no huge
+    allocation): all take the directory-only pass and build what the reference builds, which never
+    reads these fields."""
+    rng = random.Random(13)
+    log = bytearray(_compressed(_ops(rng, 2500, 2000, 0.1, 150), 900))
+    struct.pack_into("<q", log, 72, put_size)
+    struct.pack_into("<q", log, 56, delete_size)
+    check(native, bytes(log))

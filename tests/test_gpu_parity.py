@@ -236,6 +236,18 @@ def test_frame_geometry_overrides(native, monkeypatch, env):
     assert stats.framing_path == 0, stats.as_dict()
 
 
+# --- k_frame's bounded wait on the previous wave: a tripped wait reruns the build on the serial path ---
+def test_frame_wait_timeout_falls_back_to_serial(native, monkeypatch):
+    monkeypatch.setenv("SPARKEY_NO_UNIFORM", "1")
+    monkeypatch.setenv("SPARKEY_FRAME_SPIN_TICKS", "0")  # any wait for a predecessor trips at once
+    puts = random_puts(120000, seed=31, kmin=1, kmax=40, vmin=0, vmax=60)
+    got, stats = check(native, make_log(puts), 37, hash_size=8)
+    assert stats.framing_path == 1, stats.as_dict()
+    monkeypatch.delenv("SPARKEY_FRAME_SPIN_TICKS")
+    got2, stats2 = check(native, make_log(puts), 37, hash_size=8)
+    assert stats2.framing_path == 0 and got2 == got
+
+
 # --- exact path (DELETEs, overwrites) over independent slot segments vs the single-lane replay ---
 def _churn_ops(n, nkeys, p_del, seed, klen=(1, 24), vlen=(0, 40)):
     rng = np.random.default_rng(seed)

@@ -15,7 +15,7 @@ mkdir -p $OUT
 ARGS="--steps 5 --warmup 1 --no-cpu-baseline $*"
 run_tests() {
   echo "smoke" && timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 &&
-  echo "pytest" && timeout -k 10 1100 python -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread > $OUT/pytest_gpu.log 2>&1
+  echo "pytest" && timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1
 }
 run_bench() {
   echo "bench" && timeout -k 10 300 python -u bench.py --steps 20 --warmup 3 "$@" > $OUT/bench.log 2>&1 &&

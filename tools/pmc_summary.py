@@ -28,7 +28,7 @@ def read_counters(path):
     return acc
 
 
-def main(src, dst):
+def main(src, dst, workload=None):
     stats = {}
     with open(os.path.join(src, "trace", "run_kernel_stats.csv")) as f:
         for row in csv.DictReader(f):
@@ -71,12 +71,23 @@ def main(src, dst):
         if ok:
             out["per_launch_hbm_bytes"][st] = tot
     os.makedirs(os.path.dirname(dst), exist_ok=True)
+    if workload:  # merge: one summary file holds every workload's counters
+        try:
+            with open(dst) as f:
+                prev = json.load(f)
+        except (OSError, ValueError):
+            prev = {}
+        by = prev.get("per_launch_hbm_bytes_by_workload", {})
+        kern = prev.get("kernels_by_workload", {})
+        by[workload] = out["per_launch_hbm_bytes"]
+        kern[workload] = out["kernels"]
+        out = {"per_launch_hbm_bytes_by_workload": by, "kernels_by_workload": kern}
     with open(dst, "w") as f:
         json.dump(out, f, indent=1)
-    for k, r in out["kernels"].items():
+    for k, r in (out.get("kernels") or out["kernels_by_workload"][workload]).items():
         print(f"{k:28s} {r['avg_us']:9.1f} us  hbm={r.get('hbm_bytes', 0)/1e6:9.1f} MB  "
               f"valu={r.get('SQ_INSTS_VALU', 0):.3g} lds={r.get('SQ_INSTS_LDS', 0):.3g}")
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    main(sys.argv[1], sys.argv[2], sys.argv[3] if len(sys.argv) > 3 else None)
