@@ -300,11 +300,14 @@ def single_gpu(args, dev):
     try:
         log_np.tofile(log_path)
         if args.workload in ("c2", "c3", "c5", "churn", "snappy"):
+            # as SparkeyWriter.writeHash does it: a fresh "-tmp" file, then renamed over the .spi
             _native.build_index_file(log_path, spi_path, opts)
             reps_f = 3
             t_f = time.perf_counter()
-            for _ in range(reps_f):
-                _native.build_index_file(log_path, spi_path, opts)
+            for i in range(reps_f):
+                tmp = f"{spi_path}-tmp{i}"
+                _native.build_index_file(log_path, tmp, opts)
+                os.replace(tmp, spi_path)
             file_rate = n * reps_f / (time.perf_counter() - t_f)
             with open(spi_path, "rb") as f:
                 file_spi = f.read()

@@ -306,6 +306,58 @@ __global__ __launch_bounds__(1024) void k_stats_final(BuildParams P, uint32_t np
   }
 }
 
+// The folded stats (k_place_lds fold_stats): every block left the sums over the slot range it wrote
+// and where that range starts; the ranges tile the ring, so the only pairs left are each range's
+// first slot with the slot before it.  One thread per bucket; the last block to finish (ticket)
+// writes the header.
+constexpr int kStatFoldBlock = 256;
+__global__ __launch_bounds__(kStatFoldBlock) void k_stats_folded(BuildParams P) {
+  __shared__ unsigned long long s_sum[kStatFoldBlock / 64], s_col[kStatFoldBlock / 64], s_max[kStatFoldBlock / 64];
+  __shared__ bool last;
+  if (build_aborted(P)) return;
+  Status* st = P.st;
+  const int tid = threadIdx.x;
+  if (st->big_buckets || st->full) {  // some slots were placed outside k_place_lds: k_stats runs
+    if (tid == 0) st->stats_pending = 1u;
+    return;
+  }
+  unsigned long long sum = 0, col = 0, mx = 0;
+  const uint64_t b = (uint64_t)blockIdx.x * kStatFoldBlock + tid;
+  if (b < P.nbuckets) {
+    const StatPart sp = P.parts[b];
+    sum = sp.sum_disp;
+    col = sp.collisions;
+    mx = (unsigned long long)sp.max_disp;
+    const uint64_t gs = P.bstat_start[b];
+    if (gs != ~0ull && gs != 0) {
+      uint64_t hp, ap, hc, ac;
+      read_slot(P, gs - 1, hp, ap);
+      read_slot(P, gs, hc, ac);
+      col += ap != 0 && hp == hc;
+    }
+  }
+  sum = wave_sum_u64(sum);
+  col = wave_sum_u64(col);
+  mx = (unsigned long long)wave_max_i64((long long)mx);
+  if ((tid & 63) == 0) { s_sum[tid >> 6] = sum; s_col[tid >> 6] = col; s_max[tid >> 6] = mx; }
+  __syncthreads();
+  if (tid == 0) {
+    for (int w = 1; w < kStatFoldBlock / 64; w++) { s_sum[0] += s_sum[w]; s_col[0] += s_col[w]; s_max[0] = max(s_max[0], s_max[w]); }
+    atomicAdd(&st->acc_sum, s_sum[0]);
+    atomicAdd(&st->acc_col, s_col[0]);
+    atomicMax(&st->acc_max, s_max[0]);
+    __threadfence();
+    last = atomicAdd(&st->stats_ticket, 1u) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (last && tid == 0) {
+    __threadfence();
+    const unsigned long long tsum = atomicAdd(&st->acc_sum, 0ull), tcol = atomicAdd(&st->acc_col, 0ull);
+    const unsigned long long tmax = atomicMax(&st->acc_max, 0ull);
+    finish_stats(P, tsum, tcol, (long long)tmax, 0);
+  }
+}
+
 // ================================================================================================
 // host-side launchers (called by the plan in sparkey_gpu.cpp)
 // ================================================================================================
@@ -346,6 +398,12 @@ void launch_place_global(const BuildParams& P, hipStream_t s, int sort_only, int
 void launch_verify(const BuildParams& P, hipStream_t s, StageTimer* tm) {
   hipLaunchKernelGGL(k_verify_pairs, dim3(grid_for(P.pair_cap, 256)), dim3(256), 0, s, P);
   tm->mark("verify", s);
+}
+
+void launch_stats_folded(const BuildParams& P, hipStream_t s, StageTimer* tm) {
+  hipLaunchKernelGGL(k_stats_folded, dim3(grid_for(std::max<uint64_t>(P.nbuckets, 1), kStatFoldBlock)),
+                     dim3(kStatFoldBlock), 0, s, P);
+  tm->mark("stats", s);
 }
 
 void launch_stats(const BuildParams& P, hipStream_t s, int sequential, StageTimer* tm) {

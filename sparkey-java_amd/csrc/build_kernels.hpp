@@ -88,6 +88,10 @@ struct Status {
   unsigned long long n_segs[4];  // exact path: segments per size class (small, mid, large, huge)
   unsigned int guard;            // exact path: bounds-check bits that tripped (a bug; fails the build)
   unsigned int need_summary;     // k_part2s left a digit unsummarised (k_summary runs)
+  unsigned int p2_overflow;      // k_part2s fixed bucket regions: a bucket outgrew its region (redo dense)
+  unsigned int stats_pending;    // folded stats could not cover every slot (big buckets): k_stats runs
+  unsigned int stats_ticket;     // k_stats_folded: blocks done
+  unsigned long long acc_sum, acc_col, acc_max;  // k_stats_folded: totals over its blocks
 };
 
 struct BuildParams {
@@ -179,7 +183,10 @@ struct BuildParams {
   uint32_t uni_hist_off;  // LDS offset of the digit counts (set by the launcher)
   // k_frame_uniform as partition pass 1: digit d's entries at ent3[d * p1_region, + p1_fill[d])
   uint64_t p1_region;   // 0 = off
-  int32_t p2_sorted;    // k_part2s: entries by wanted slot within the bucket + the carry functions
+  int32_t p2_sorted;    // k_part2s: per-(bucket, slot) counts in the same pass + the carry functions
+  int32_t p2_fixed;     // k_part2s in one pass: bucket b's entries at ent2[b * kPlaceLdsMax, + bcount[b])
+  int32_t fold_stats;   // k_place_lds leaves calculateMaxDisplacement's per-bucket parts (no k_stats pass)
+  uint64_t* bstat_start;  // fold_stats: per bucket, the first slot of the range it wrote (~0: none)
   uint32_t* p1_fill;
   // framing window: records start at fr_entry (84 for a whole log) and are framed while they start
   // below data_end (the frame end); k_frame chunks are numbered from fr_k0 = fr_entry >> fr_cshift,
@@ -254,6 +261,7 @@ void launch_carry(const BuildParams& P, hipStream_t s);
 void launch_place_global(const BuildParams& P, hipStream_t s, int sort_only, int only_big);
 void launch_verify(const BuildParams& P, hipStream_t s, StageTimer* tm);
 void launch_stats(const BuildParams& P, hipStream_t s, int sequential, StageTimer* tm);
+void launch_stats_folded(const BuildParams& P, hipStream_t s, StageTimer* tm);
 // exact replay (exact_kernels.hip)
 void launch_sequential(const BuildParams& P, hipStream_t s, int sorted_order);
 // Streams the exact path forks its independent segment classes onto (owned by the plan).

@@ -1172,25 +1172,38 @@ __global__ __launch_bounds__(kPart2Block) void k_part2s(BuildParams P) {
   uint32_t* btot = dyn + nbins * 512;
   uint32_t* boffl = btot + nbins;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // p2_fixed: bucket b's entries go to its region ent2[b * kPlaceLdsMax ..) in this same pass (the
+  // region cursor is the bucket count), so the digit is read once; a bucket that outgrows its region
+  // (more entries than k_place_lds stages anyway) makes the host redo the build with dense runs
+  const bool fixed = P.p2_fixed != 0;
   for (uint32_t i = tid; i < nbins * 512 + 2 * nbins; i += kPart2Block) dyn[i] = 0;
   __syncthreads();
+  bool ovf = false;
   for (uint64_t i0 = lo; i0 < hi; i0 += (uint64_t)kPart2Block * kPart2Items) {
-    uint64_t hv[kPart2Items];
+    Entry v[kPart2Items];
 #pragma unroll
     for (int k = 0; k < kPart2Items; k++) {
       const uint64_t i = i0 + (uint64_t)k * kPart2Block + tid;
-      if (i < hi) hv[k] = P.ent3[i].hash;
+      if (i < hi) {
+        if (fixed) v[k] = P.ent3[i];
+        else v[k].hash = P.ent3[i].hash;
+      }
     }
 #pragma unroll
     for (int k = 0; k < kPart2Items; k++) {
       const uint64_t i = i0 + (uint64_t)k * kPart2Block + tid;
       if (i >= hi) continue;
-      const uint64_t slot = fast_mod(hv[k], P.mod);
+      const uint64_t slot = fast_mod(v[k].hash, P.mod);
       const uint32_t b = (uint32_t)((slot >> kBucketShift) - b0), sl = (uint32_t)(slot & (kBucket - 1));
       atomicAdd(&h[(b << 9) + (sl >> 1)], 1u << ((sl & 1) * 16));
-      atomicAdd(&btot[b], 1u);
+      const uint32_t r = atomicAdd(&btot[b], 1u);
+      if (fixed) {
+        if (r < kPlaceLdsMax) P.ent2[(b0 + b) * (uint64_t)kPlaceLdsMax + r] = v[k];
+        else ovf = true;
+      }
     }
   }
+  if (ovf) atomicOr(&P.st->p2_overflow, 1u);
   __syncthreads();
   bool big = false;
   for (uint32_t b = tid; b < nbins; b += kPart2Block) big |= btot[b] > 65535u;
@@ -1209,7 +1222,7 @@ __global__ __launch_bounds__(kPart2Block) void k_part2s(BuildParams P) {
       boffl[lane] = incl - c;  // then the bucket's cursor
       const uint64_t bucket = b0 + lane;
       if (bucket < P.nbuckets) {
-        P.boff[bucket] = lo + incl - c;
+        P.boff[bucket] = fixed ? bucket * (uint64_t)kPlaceLdsMax : lo + incl - c;
         P.bcount[bucket] = c;
       }
     }
@@ -1252,6 +1265,7 @@ __global__ __launch_bounds__(kPart2Block) void k_part2s(BuildParams P) {
       P.bfun[bucket] = f;
     }
   }
+  if (fixed) return;
   __syncthreads();
   for (uint64_t i0 = lo; i0 < hi; i0 += (uint64_t)kPart2Block * kPart2Items) {
     Entry v[kPart2Items];
@@ -1286,21 +1300,65 @@ __device__ __forceinline__ bool is_put_pair(const Entry& x, const Entry& y) {  /
     }                                                                   \
   } while (0)
 
+// Exclusive sum base[s] of the bucket's 1024 slot counts and the inclusive prefix max M[s] of
+// s - base[s] over occupied slots, 512 threads x 2 slots: wave shuffles, one LDS word per wave and
+// two barriers (the block-generic bucket_scan takes six).
+__device__ __forceinline__ void place_scan512(const uint32_t* cnt, uint32_t* base, int32_t* M, uint32_t* wsum,
+                                              int32_t* wmax) {
+  constexpr int NW = kPlaceLdsBlock / 64;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int s0 = 2 * tid;
+  const uint32_t c0 = cnt[s0], c1 = cnt[s0 + 1];
+  uint32_t incl = c0 + c1;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t t = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += t;
+  }
+  if (lane == 63) wsum[w] = incl;
+  __syncthreads();
+  uint32_t off = 0;
+#pragma unroll
+  for (int i = 0; i < NW; i++) off += i < w ? wsum[i] : 0u;
+  const uint32_t b0 = off + incl - (c0 + c1), b1 = b0 + c0;
+  base[s0] = b0;
+  base[s0 + 1] = b1;
+  constexpr int32_t kNone = -(1 << 20);
+  const int32_t v0 = c0 ? s0 - (int32_t)b0 : kNone, v1 = c1 ? s0 + 1 - (int32_t)b1 : kNone;
+  int32_t m = max(v0, v1);
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int32_t t = __shfl_up(m, o, 64);
+    if (lane >= o) m = max(m, t);
+  }
+  if (lane == 63) wmax[w] = m;
+  __syncthreads();
+  int32_t pre = kNone;
+#pragma unroll
+  for (int i = 0; i < NW; i++) pre = i < w ? max(pre, wmax[i]) : pre;
+  int32_t ex = __shfl_up(m, 1, 64);
+  if (lane == 0) ex = kNone;
+  ex = max(ex, pre);
+  M[s0] = max(ex, v0);
+  M[s0 + 1] = max(max(ex, v0), v1);
+}
+
 __global__ __launch_bounds__(kPlaceLdsBlock) void k_place_lds(BuildParams P) {
-  __shared__ uint32_t cnt[kBucket];
+  __shared__ uint32_t cnt[kBucket];        // entries per wanted slot (their atomics are the group cursors)
   __shared__ uint32_t base[kBucket];
   __shared__ int32_t M[kBucket];
-  __shared__ int32_t aux[kBucket];  // cursors, then slot -> sorted index
-  __shared__ Entry raw[kPlaceLdsMax];
-  __shared__ uint16_t order[kPlaceLdsMax];
+  __shared__ int32_t pos_j[2 * kBucket];   // (position - carry-in) -> sorted index | hash bits << 10, -1 = empty
+  __shared__ Entry buf[kPlaceLdsMax];      // the bucket's entries in (wanted slot, address) order
+  __shared__ uint32_t wsum[kPlaceLdsBlock / 64];
+  __shared__ int32_t wmax[kPlaceLdsBlock / 64];
   __shared__ uint64_t sh64[kPlaceLdsBlock / 64 + 1];
-  __shared__ int64_t shm[kPlaceLdsBlock / 64 + 1];
+  __shared__ int64_t s_pend;
   long long t_prev_ = P.place_dbg ? clock64() : 0;
   const long long t_begin_ = t_prev_;
   // Every value the block reads besides its entries, in one round trip (block-uniform: scalar loads
   // issued together) rather than one latency per phase.
   const Status* st = P.st;
-  const unsigned ovf = st->overflow, full = st->full;
+  const unsigned ovf = st->overflow | st->p2_overflow, full = st->full;
   const unsigned long long nrec = st->n_records, ndel = st->n_deletes, npairs0 = st->n_pairs;
   const uint64_t b = P.b_lo + blockIdx.x;
   const uint32_t n = P.bcount[b];
@@ -1309,55 +1367,52 @@ __global__ __launch_bounds__(kPlaceLdsBlock) void k_place_lds(BuildParams P) {
   if (ovf != 0 || nrec > P.max_records) return;  // build_aborted
   const uint64_t start = b << kBucketShift;
   const int64_t bsize = (int64_t)min((uint64_t)kBucket, P.cap - start);
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63;
   if (n > kPlaceLdsMax) {
     if (tid == 0) atomicOr(&P.st->big_buckets, 1u);
     return;
   }
-  // the entries' loads are in flight while the histogram is cleared
+  // the entries' loads are in flight while the counts are cleared
   constexpr int kPer = kPlaceLdsMax / kPlaceLdsBlock;
   static_assert(kPlaceLdsMax % kPlaceLdsBlock == 0, "entries per thread");
+  static_assert(kBucket == 2 * kPlaceLdsBlock, "place_scan512: two slots per thread");
   Entry mine[kPer];
-  uint32_t want[kPer];
+  uint32_t want[kPer], cur[kPer], rank[kPer];
 #pragma unroll
   for (int k = 0; k < kPer; k++) {
     const uint32_t i = tid + k * kPlaceLdsBlock;
     if (i < n) mine[k] = P.ent2[eoff + i];
   }
   PLACE_MARK(0);
-  for (int t = tid; t < kBucket; t += kPlaceLdsBlock) { cnt[t] = 0; aux[t] = 0; }
+  for (int t = tid; t < kBucket; t += kPlaceLdsBlock) cnt[t] = 0;
+  for (int t = tid; t < 2 * kBucket; t += kPlaceLdsBlock) pos_j[t] = -1;
+  if (tid == 0) s_pend = 0;
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < kPer; k++) {
     const uint32_t i = tid + k * kPlaceLdsBlock;
     if (i < n) {
-      raw[i] = mine[k];
       want[k] = (uint32_t)(fast_mod(mine[k].hash, P.mod) - start);
-      atomicAdd(&cnt[want[k]], 1u);
+      cur[k] = atomicAdd(&cnt[want[k]], 1u);  // an arbitrary place inside the wanted slot's group
     }
   }
   __syncthreads();
   PLACE_MARK(1);
-  bucket_scan<kPlaceLdsBlock>(cnt, base, M, sh64, shm, nullptr);
-  // a group's members in arbitrary order (LDS cursors); a lone entry goes straight to its place
+  place_scan512(cnt, base, M, wsum, wmax);
+  __syncthreads();
 #pragma unroll
   for (int k = 0; k < kPer; k++) {
     const uint32_t i = tid + k * kPlaceLdsBlock;
-    if (i < n) {
-      const uint32_t w = want[k];
-      order[base[w] + (cnt[w] > 1 ? atomicAdd((uint32_t*)&aux[w], 1u) : 0u)] = (uint16_t)i;
-    }
+    if (i < n) buf[base[want[k]] + cur[k]] = mine[k];
   }
   __syncthreads();
   PLACE_MARK(2);
-  // Equal wanted slots go in address order (the reference's insertion order): each member counts
-  // the members with smaller addresses -- independent LDS reads, one thread per entry -- and
-  // equal-hash PUT pairs become duplicate-key candidates, counted by their earlier member and
+  // Equal wanted slots go in address order (the reference's insertion order, and SORTING's
+  // (wantedSlot, address) comparator): each member counts the members with smaller addresses --
+  // independent LDS reads of its group.  Equal-hash PUT pairs become duplicate-key candidates,
   // appended to the pair list with one atomic per workgroup (not needed once the exact path is
   // certain: the log holds DELETEs, or the list overflowed; groups above kGroupMax flag it).
   const bool want_pairs = ndel == 0 && npairs0 <= P.pair_cap;
-  for (int t = tid; t < kBucket; t += kPlaceLdsBlock) aux[t] = -1;  // (the cursors are done with)
-  uint32_t rank[kPer];
   uint32_t npair = 0;
 #pragma unroll
   for (int k = 0; k < kPer; k++) {
@@ -1366,13 +1421,13 @@ __global__ __launch_bounds__(kPlaceLdsBlock) void k_place_lds(BuildParams P) {
     if (i >= n) continue;
     const uint32_t w = want[k], g = cnt[w];
     if (g < 2) continue;
-    const uint16_t* grp = order + base[w];
+    const Entry* grp = buf + base[w];
     const uint64_t ai = mine[k].addr & ~kDelBit;
     const bool cp = want_pairs && !(mine[k].addr & kDelBit) && g <= kGroupMax;
-    if (g > kGroupMax && grp[0] == i) atomicOr(&P.st->dup_overflow, 1u);
+    if (g > kGroupMax && cur[k] == 0) atomicOr(&P.st->dup_overflow, 1u);
     uint32_t r = 0;
     for (uint32_t u = 0; u < g; u++) {
-      const Entry e = raw[grp[u]];
+      const Entry e = grp[u];
       const uint64_t aj = e.addr & ~kDelBit;
       r += aj < ai;
       npair += cp && aj > ai && e.hash == mine[k].hash && !(e.addr & kDelBit);
@@ -1380,12 +1435,7 @@ __global__ __launch_bounds__(kPlaceLdsBlock) void k_place_lds(BuildParams P) {
     rank[k] = r;
   }
   const bool any_pair = __syncthreads_or(npair != 0);
-#pragma unroll
-  for (int k = 0; k < kPer; k++) {
-    const uint32_t i = tid + k * kPlaceLdsBlock;
-    if (i < n && cnt[want[k]] > 1) order[base[want[k]] + rank[k]] = (uint16_t)i;
-  }
-  if (any_pair) {  // (block-uniform)
+  if (any_pair) {  // (block-uniform; the group members are still in their unsorted places)
     uint64_t pair_total = 0;
     const uint64_t pair_off = block_excl_sum<kPlaceLdsBlock>(npair, sh64, &pair_total);  // (syncs the block)
     __shared__ unsigned long long pair_base;
@@ -1398,10 +1448,11 @@ __global__ __launch_bounds__(kPlaceLdsBlock) void k_place_lds(BuildParams P) {
       if (i >= n || !npair) continue;
       const uint32_t w = want[k], g = cnt[w];
       if (g < 2 || g > kGroupMax || (mine[k].addr & kDelBit)) continue;
-      const uint16_t* grp = order + base[w];
-      for (uint32_t u = rank[k] + 1; u < g; u++) {  // the later members, in address order
-        const Entry e = raw[grp[u]];
-        if (!is_put_pair(mine[k], e)) continue;
+      const Entry* grp = buf + base[w];
+      const uint64_t ai = mine[k].addr & ~kDelBit;
+      for (uint32_t u = 0; u < g; u++) {  // every later member with the same hash (pair order is free)
+        const Entry e = grp[u];
+        if ((e.addr & ~kDelBit) <= ai || !is_put_pair(mine[k], e)) continue;
         if (slotn < P.pair_cap) {
           P.pairs[2 * slotn] = mine[k].addr;
           P.pairs[2 * slotn + 1] = e.addr;
@@ -1409,38 +1460,98 @@ __global__ __launch_bounds__(kPlaceLdsBlock) void k_place_lds(BuildParams P) {
         slotn++;
       }
     }
+    __syncthreads();
   }
   PLACE_MARK(3);
   if (full) return;
-  for (int q = 0; q < kLdsBins; q++) {
-    const int s = tid * kLdsBins + q;
-    const uint32_t g = cnt[s];
-    if (!g) continue;
-    const int64_t shift = max(x, (int64_t)M[s]);
-    for (uint32_t r = 0; r < g; r++) {
-      const int64_t j = (int64_t)base[s] + r;
-      const int64_t p = j + shift;
-      if (p < bsize) {
-        aux[p] = (int32_t)j;
-      } else {
-        const Entry en = raw[order[j]];
-        put_slot(P, wrap_slot(start + (uint64_t)p, P.cap), en.hash, en.addr & ~kDelBit);
-      }
-    }
+#pragma unroll
+  for (int k = 0; k < kPer; k++) {  // each group in address order, in place
+    const uint32_t i = tid + k * kPlaceLdsBlock;
+    if (i < n && cnt[want[k]] > 1) buf[base[want[k]] + rank[k]] = mine[k];
   }
+  // Positions: the j-th entry in (wanted, address) order goes to j + max(carry, M(s)), which lies in
+  // [x, x + 2 * kBucket) (j < n <= kBucket, M(s) < bsize).  The block writes the slot range [x, hi):
+  // its own slots from the carry-in on (entries or zero) and the run it spills past the bucket end,
+  // which has no gap (the first spilled entry lands on bsize, each next one on the next slot).
+  const bool fold = P.fold_stats != 0;
+  unsigned long long sum_d = 0;
+  long long max_d = 0;
+  int64_t pend = 0;  // 1 + the last position
+  int64_t pos[kPer];
+#pragma unroll
+  for (int k = 0; k < kPer; k++) {
+    const uint32_t i = tid + k * kPlaceLdsBlock;
+    pos[k] = -1;
+    if (i >= n) continue;
+    const uint32_t w = want[k];
+    const int64_t j = (int64_t)base[w] + rank[k];
+    const int64_t p = j + max(x, (int64_t)M[w]);
+    pos[k] = p;
+    pos_j[p - x] = (int32_t)j | (int32_t)((mine[k].hash & 0x1fffffull) << 10);  // (j < kPlaceLdsMax = 2^10)
+    sum_d += (unsigned long long)(p - w);  // getDisplacement (IndexHash.java:671-678)
+    max_d = max(max_d, (long long)(p - w));
+    pend = max(pend, p + 1);
+  }
+  pend = wave_max_i64(pend);
+  if (lane == 0 && pend > 0) atomicMax((unsigned long long*)&s_pend, (unsigned long long)pend);
   __syncthreads();
   PLACE_MARK(4);
-  // every slot of [x, bsize) is this bucket's: an own entry or empty (zero)
-  for (int64_t t = x + tid; t < bsize; t += kPlaceLdsBlock) {
-    const int32_t j = aux[t];
-    if (j >= 0) {
-      const Entry en = raw[order[j]];
-      write_slot(P, start + (uint64_t)t, en.hash, en.addr & ~kDelBit);
+  const int64_t hi = max(bsize, s_pend);
+  for (int64_t t = x + tid; t < hi; t += kPlaceLdsBlock) {
+    const int32_t v = pos_j[t - x];
+    const uint64_t slot = t < bsize ? start + (uint64_t)t : wrap_slot(start + (uint64_t)t, P.cap);
+    if (v >= 0) {
+      const Entry en = buf[v & 1023];
+      put_slot(P, slot, en.hash, en.addr & ~kDelBit);
     } else {
-      write_slot(P, start + (uint64_t)t, 0, 0);
+      write_slot(P, slot, 0, 0);
     }
   }
   PLACE_MARK(5);
+  if (fold) {  // the block's parts of calculateMaxDisplacement (IndexHash.java:195-245)
+    // adjacent pairs (slot - 1, slot) inside [x, hi), seen from the occupied slot of each pair:
+    // an entry equal to the occupied slot before it, and an entry of hash 0 before an empty slot
+    // (which reads as hash 0)
+    unsigned long long col = 0;
+#pragma unroll
+    for (int k = 0; k < kPer; k++) {
+      const int64_t p = pos[k];
+      if (p < 0) continue;
+      const uint64_t h = mine[k].hash;
+      if (p > x && wrap_slot(start + (uint64_t)p, P.cap) != 0) {
+        const int32_t vp = pos_j[p - 1 - x];  // the hash bits decide; the full hash only confirms
+        if (vp >= 0 && (uint32_t)(vp >> 10) == (uint32_t)(h & 0x1fffffull)) col += buf[vp & 1023].hash == h;
+      }
+      if (h == 0 && p + 1 < hi && pos_j[p + 1 - x] < 0 && wrap_slot(start + (uint64_t)p + 1, P.cap) != 0) col++;
+    }
+    if (x < (1ll << 20)) {  // (block-uniform) every displacement < 2^21: 32-bit DPP reductions
+      sum_d = wave_sum_u32((uint32_t)sum_d);
+      max_d = wave_max_i32((int32_t)max_d);
+    } else {
+      sum_d = wave_sum_u64(sum_d);
+      max_d = wave_max_i64(max_d);
+    }
+    col = wave_sum_u32((uint32_t)col);
+    __shared__ unsigned long long r_sum[kPlaceLdsBlock / 64], r_col[kPlaceLdsBlock / 64];
+    __shared__ long long r_max[kPlaceLdsBlock / 64];
+    if (lane == 0) {
+      r_sum[tid >> 6] = sum_d;
+      r_col[tid >> 6] = col;
+      r_max[tid >> 6] = max_d;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      StatPart sp{0, 0, 0};
+      for (int w = 0; w < kPlaceLdsBlock / 64; w++) {
+        sp.sum_disp += r_sum[w];
+        sp.collisions += r_col[w];
+        sp.max_disp = max(sp.max_disp, r_max[w]);
+      }
+      P.parts[b] = sp;
+      P.bstat_start[b] = hi > x ? wrap_slot(start + (uint64_t)x, P.cap) : ~0ull;
+    }
+  }
+  PLACE_MARK(6);
   if (P.place_dbg && tid == 0) P.place_dbg[8 * (uint64_t)blockIdx.x + 7] = t_prev_ - t_begin_;
 }
 

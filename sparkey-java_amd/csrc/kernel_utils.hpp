@@ -16,7 +16,8 @@ namespace sk {
 // The framing wrote more records than the workspace holds: every later stage of this attempt is
 // skipped (its offsets would run past the buffers) and the host redoes the build with more room.
 __device__ __forceinline__ bool build_aborted(const BuildParams& P) {
-  return P.st->overflow != 0 || P.st->n_records > P.max_records;
+  // (p2_overflow: the fixed bucket regions did not hold a bucket; the host redoes the build)
+  return P.st->overflow != 0 || P.st->n_records > P.max_records || P.st->p2_overflow != 0;
 }
 
 __device__ __forceinline__ void set_error(Status* st, int64_t pos, int code) {
@@ -63,6 +64,26 @@ __device__ __forceinline__ long long wave_max_i64(long long v) {
     v = t > v ? t : v;
   }
   return v;
+}
+// Wave-wide sum / max of 32-bit values by DPP (row shifts, then the row broadcasts of lanes 15
+// and 31), in VALU with no LDS crossbar traffic; the result is read from lane 63.
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);  // row_shr:8
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+__device__ __forceinline__ int32_t wave_max_i32(int32_t v) {  // (v >= 0 lanes only matter: 0 shifts in)
+  v = max(v, __builtin_amdgcn_update_dpp(INT32_MIN, v, 0x111, 0xf, 0xf, false));
+  v = max(v, __builtin_amdgcn_update_dpp(INT32_MIN, v, 0x112, 0xf, 0xf, false));
+  v = max(v, __builtin_amdgcn_update_dpp(INT32_MIN, v, 0x114, 0xf, 0xf, false));
+  v = max(v, __builtin_amdgcn_update_dpp(INT32_MIN, v, 0x118, 0xf, 0xf, false));
+  v = max(v, __builtin_amdgcn_update_dpp(INT32_MIN, v, 0x142, 0xa, 0xf, false));
+  v = max(v, __builtin_amdgcn_update_dpp(INT32_MIN, v, 0x143, 0xc, 0xf, false));
+  return __builtin_amdgcn_readlane(v, 63);
 }
 __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
 #pragma unroll

@@ -271,7 +271,8 @@ struct sparkey_plan {
   uint64_t c_conv = 0, c_exitp = 0, c_qpos = 0, c_tail = 0, c_G = 0, c_cnt = 0, c_off = 0;
   uint64_t c_ent = 0, c_ent2 = 0, c_ent3 = 0;
   uint64_t c_bcount = 0, c_bcursor = 0, c_boff = 0, c_bfun = 0, c_bpre = 0, c_carry = 0;
-  uint64_t c_pdbg = 0, c_p1_fill = 0;
+  uint64_t c_pdbg = 0, c_p1_fill = 0, c_bstat = 0;
+  uint64_t* bstat_start = nullptr;  // folded stats: first slot of each bucket's written range
   uint64_t c_pairs = 0, c_parts = 0, c_su = 0, c_smp = 0, c_bft = 0;
   uint64_t c_desc = 0, c_p1h = 0, c_p1o = 0, c_dbg = 0, c_wcount = 0, c_woff = 0;
   uint64_t c_eseg = 0, c_seg_cnt = 0, c_seg_off = 0, c_seg_mark = 0, c_seg_start = 0, c_p2tab = 0;
@@ -365,7 +366,8 @@ static int plan_reserve(sparkey_plan* pl, uint64_t nchunks, uint64_t nrec, uint6
   HIP_TRY(grow(&pl->carry, pl->c_carry, nbuckets));
   const uint64_t pair_cap = std::max<uint64_t>(1 << 16, std::min<uint64_t>(nrec, 1 << 22));
   HIP_TRY(grow(&pl->pairs, pl->c_pairs, 2 * pair_cap));
-  HIP_TRY(grow(&pl->parts, pl->c_parts, (cap + kStatSlotsPerBlock - 1) / kStatSlotsPerBlock));
+  HIP_TRY(grow(&pl->parts, pl->c_parts, std::max<uint64_t>(nbuckets, (cap + kStatSlotsPerBlock - 1) / kStatSlotsPerBlock)));
+  HIP_TRY(grow(&pl->bstat_start, pl->c_bstat, nbuckets));
   HIP_TRY(grow(&pl->desc, pl->c_desc, 2 * nchunks + 2));
   HIP_TRY(grow(&pl->p1_hist, pl->c_p1h, 256 * p1_tiles));
   HIP_TRY(grow(&pl->p1_off, pl->c_p1o, 256 * p1_tiles + 1));
@@ -545,6 +547,7 @@ static int reserve_for_framing(sparkey_plan* pl, BuildParams& P, int framing_pat
   P.bcount = pl->bcount; P.bcursor = pl->bcursor; P.boff = pl->boff; P.bfun = pl->bfun; P.bpre = pl->bpre;
   P.bfun_total = pl->bfun_total; P.carry = pl->carry; P.pairs = pl->pairs; P.pair_cap = pl->c_pairs / 2;
   P.parts = pl->parts; P.scan_scratch_u64 = pl->scan_u64; P.scan_scratch_mp = pl->scan_mp;
+  P.bstat_start = pl->bstat_start;
   P.exit_desc = pl->desc;
   P.frame_ticket = reinterpret_cast<unsigned int*>(pl->desc + 2 * nwaves);
   P.fr_spin_ticks = 2000000000ull;  // 20 s of the 100 MHz wall clock
@@ -915,6 +918,8 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
   uint32_t slab_cap = (uint32_t)std::min<uint64_t>(
       kPartTile, std::max<uint64_t>(64, 2 * ((nrec + std::max<uint64_t>(nwaves, 1) - 1) / std::max<uint64_t>(nwaves, 1)) + 32));
   bool use_regions = getenv("SPARKEY_NO_REGIONS") == nullptr, regions_used = false;
+  bool use_fixed = getenv("SPARKEY_NO_P2_FIXED") == nullptr;  // k_part2s in one pass (fixed bucket regions)
+  const bool fold = getenv("SPARKEY_NO_FOLD_STATS") == nullptr;  // stats from k_place_lds, no k_stats pass
   for (int attempt = 0; attempt < 5; attempt++) {
     rc = reserve_for_framing(pl, P, framing_path, nrec, slab_cap, err, err_len);
     if (rc) return rc;
@@ -959,11 +964,18 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
     regions_used = P.p1_region != 0;
     // k_part2s: pass 2 also sorts each bucket by wanted slot and leaves the carry functions
     P.p2_sorted = P.bpp <= kP2SortedMaxBpp && !getenv("SPARKEY_NO_P2_SORTED") ? 1 : 0;
+    P.p2_fixed = P.p2_sorted && use_fixed ? 1 : 0;
+    if (P.p2_fixed) {  // bucket b's entries at ent2[b * kPlaceLdsMax ..)
+      HIP_TRY(grow(&pl->ent2, pl->c_ent2, std::max<uint64_t>(P.max_records, P.nbuckets * (uint64_t)kPlaceLdsMax)));
+      P.ent2 = pl->ent2;
+    }
+    P.fold_stats = fold ? 1 : 0;
     rc = launch_framing(pl, P, framing_path, s, err, err_len);
     if (rc) return rc;
     launch_partition(P, s, &pl->timer);
     launch_place_fast(P, s, &pl->timer);
-    launch_stats(P, s, 0, &pl->timer);
+    if (P.fold_stats) launch_stats_folded(P, s, &pl->timer);
+    else launch_stats(P, s, 0, &pl->timer);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(pl->ev1, s));
     HIP_TRY(hipMemcpyAsync(pl->h_status, pl->d_status, sizeof(Status), hipMemcpyDeviceToHost, s));
@@ -983,6 +995,10 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
       framing_path = 1;
       continue;
     }
+    if (st.p2_overflow && P.p2_fixed) {  // a bucket outgrew its fixed region: dense bucket runs
+      use_fixed = false;
+      continue;
+    }
     if (framing_path == 2 && (st.spec_fail & kSpecRegionFull) && !(st.spec_fail & ~kSpecRegionFull)) {
       use_regions = false;  // a digit region filled up (skewed hashes): the separate pass 1
       continue;
@@ -998,6 +1014,18 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
   if (st.overflow || st.spec_fail) {
     set_err(err, err_len, "Corrupt log file: framing did not converge");
     return SPARKEY_E_CORRUPT_LOG;
+  }
+  if (st.stats_pending && !(st.n_deletes > 0 || st.dup || st.dup_overflow || st.full || st.n_pairs > P.pair_cap)) {
+    // folded stats did not cover every slot (a bucket was placed by the global kernel): the pass
+    float ms2 = 0.f;
+    HIP_TRY(hipEventRecord(pl->ev0, s));
+    launch_stats(P, s, 0, &pl->timer);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(pl->ev1, s));
+    HIP_TRY(hipMemcpyAsync(pl->h_status, pl->d_status, sizeof(Status), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    HIP_TRY(hipEventElapsedTime(&ms2, pl->ev0, pl->ev1));
+    ms += ms2;
   }
   // Logs outside the canonical case (DELETEs, duplicate keys) replay the reference's put/delete
   // exactly: per independent slot segment of the canonical PUT placement (placement_path 2), or,
@@ -1366,7 +1394,7 @@ void sparkey_plan_destroy(sparkey_plan* pl) {
   void* bufs[] = {pl->conv, pl->exitp, pl->qpos, pl->tail, pl->G, pl->cnt, pl->off, pl->ent, pl->ent2, pl->ent3,
                   pl->bcount, pl->bcursor, pl->boff, pl->bfun, pl->bpre, pl->bfun_total, pl->carry, pl->pairs,
                   pl->parts, pl->pdbg, pl->p1_fill, pl->scan_u64, pl->scan_mp, pl->desc, pl->p1_hist, pl->p1_off, pl->d_status, pl->dbg, pl->wcount, pl->woff, pl->small,
-                  pl->eseg, pl->seg_cnt, pl->seg_off, pl->seg_mark, pl->seg_start,
+                  pl->eseg, pl->seg_cnt, pl->seg_off, pl->seg_mark, pl->seg_start, pl->bstat_start,
                   pl->seg_cls_cnt, pl->seg_cls_off, pl->p2tab,
                   pl->app_i64, pl->app_u32, pl->app_u64, pl->app_scan, pl->app_map,
                   pl->sn_blocks, pl->sn_dir, pl->sn_walk, pl->sn_recoff, pl->sn_vlog, pl->sn_itab, pl->sn_err};
@@ -1677,6 +1705,7 @@ static int shard_summarize_impl(sparkey_plan* pl, const uint8_t* d_recv, uint64_
   P.bcount = pl->bcount; P.bcursor = pl->bcursor; P.boff = pl->boff; P.bfun = pl->bfun; P.bpre = pl->bpre;
   P.bfun_total = pl->bfun_total; P.carry = pl->carry; P.pairs = pl->pairs; P.pair_cap = pl->c_pairs / 2;
   P.parts = pl->parts; P.scan_scratch_u64 = pl->scan_u64; P.scan_scratch_mp = pl->scan_mp;
+  P.bstat_start = pl->bstat_start;
   P.p1_hist = pl->p1_hist; P.p1_off = pl->p1_off; P.p1_off_total = pl->p1_off + 256ull * P.p1_tiles;
   P.st = pl->d_status;
   sh.n_recv = n_recv;

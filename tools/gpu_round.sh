@@ -19,7 +19,7 @@ run_tests() {
 }
 run_bench() {
   echo "bench" && timeout -k 10 300 python -u bench.py --steps 20 --warmup 3 "$@" > $OUT/bench.log 2>&1 &&
-  echo "frame debug" && SPARKEY_FRAME_DEBUG=1 timeout -k 10 120 python -u bench.py --steps 1 --warmup 0 --no-cpu-baseline "$@" > $OUT/frame_debug.log 2>&1
+  echo "frame debug" && SPARKEY_FRAME_DEBUG=1 SPARKEY_FILE_DEBUG=1 timeout -k 10 120 python -u bench.py --steps 1 --warmup 0 --no-cpu-baseline "$@" > $OUT/frame_debug.log 2>&1
 }
 run_prof() {
   echo "trace" && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof/trace -o run -- python3 bench.py $ARGS > $OUT/trace.log 2>&1 &&
