@@ -248,7 +248,7 @@ def single_gpu(args, dev):
     dom_bytes = stage_bytes(dom, n, frame_end, slot, cap, passes, comp_end=log_len) if dom else 0
     achieved = dom_bytes / (stage_ms[dom] * 1e-3) / 1e9 if dom and stage_ms[dom] > 0 else 0.0
     b_alg = (log_len - 84) + 112 + slot * cap
-    assert stats.placement_path == wl["path"] and stats.framing_path in (0, 2), stats.as_dict()
+    assert stats.placement_path == wl["path"] and stats.framing_path in (0, 2, 3), stats.as_dict()
     assert wl["path"] != 0 or stats.num_entries == n, stats.as_dict()
 
     # host-to-host rate (north_star): H2D of the log from pinned memory, the build, D2H of the .spi
@@ -283,7 +283,7 @@ def single_gpu(args, dev):
             torch.cuda.synchronize(dev)
             g_el = time.perf_counter() - t_g
             plan.set_profiling(False)
-            assert g_stats.framing_path == 0, g_stats.as_dict()
+            assert g_stats.framing_path in (0, 3), g_stats.as_dict()
             g_stage = {k: v / g_steps for k, v in g_acc.items()}
             general = {"ms_per_step": g_el * 1000.0 / g_steps, "keys_per_s": n * g_steps / g_el,
                        "stage_ms": g_stage,
@@ -357,7 +357,8 @@ def single_gpu(args, dev):
                       for k, v in stage_ms.items() if v > 0 and stage_bytes(k, n, frame_end, slot, cap, passes)},
         "build_algorithmic_bytes": b_alg,
         "stage_ms": stage_ms,
-        "framing": {0: "k_frame (speculative)", 1: "serial walk", 2: "k_frame_uniform (uniform records)"}[stats.framing_path],
+        "framing": {0: "k_frame (speculative)", 1: "serial walk", 2: "k_frame_uniform (uniform records)",
+                    3: "k_frame2 (speculative, mixed record sizes)"}[stats.framing_path],
         "general_framing": general,
         "host_to_host_keys_per_s": h2h,
         "file_to_file_keys_per_s": file_rate,

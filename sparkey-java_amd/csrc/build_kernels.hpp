@@ -176,6 +176,10 @@ struct BuildParams {
   int32_t fr_fast;  // maxKeyLen + 1 < 128 and maxValueLen < 128: canonical headers are 2 bytes
   int32_t no_deletes;  // the log header counts no DELETE: speculation treats 0x00 as no record start
   uint64_t fr_nchunks;
+  // k_frame2 (frame2_kernels.hip): segments of 2^fr_cshift bytes, fr_w per wave, f2_lcap listed record
+  // starts per segment, f2_rgn_bytes staged per wave
+  int32_t f2_lcap;
+  int32_t f2_rgn_bytes;
   // uniform-stride framing (k_frame_uniform): uni_n records of uni_rec bytes from fr_entry
   uint64_t uni_n;
   int64_t uni_rec;
@@ -251,6 +255,7 @@ void launch_partition1(const BuildParams& P, hipStream_t s);
 void launch_partition2(const BuildParams& P, hipStream_t s, StageTimer* tm);
 void launch_dense_slabs(const BuildParams& P, hipStream_t s);
 void launch_frame_uniform(const BuildParams& P, hipStream_t s, StageTimer* tm);
+void launch_frame2(const BuildParams& P, hipStream_t s, StageTimer* tm);  // frame2_kernels.hip
 void launch_place_fast(const BuildParams& P, hipStream_t s, StageTimer* tm);
 void launch_place_buckets(const BuildParams& P, hipStream_t s);
 // fallbacks and shared stages (build_kernels.hip)

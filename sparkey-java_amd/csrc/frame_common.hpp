@@ -1,0 +1,218 @@
+// frame_common.hpp -- device helpers shared by the framing kernels (fused_kernels.hip k_frame /
+// k_frame_uniform, frame2_kernels.hip k_frame2): byte access into LDS-staged log regions, MurmurHash3
+// over key bytes read 8 at a time, the inter-wave exit granules and the record-start screen.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "build_kernels.hpp"
+#include "device_common.hpp"
+#include "kernel_utils.hpp"
+
+namespace sk {
+
+// ------------------------------------------------------------------------------------------------
+// LDS byte access
+// ------------------------------------------------------------------------------------------------
+// 8 bytes starting at any offset of an 8-byte-aligned LDS window (two aligned 8-byte reads).
+__device__ __forceinline__ uint64_t lds_u64_at(const uint8_t* win, int off) {
+  const uint64_t* w = reinterpret_cast<const uint64_t*>(win + (off & ~7));
+  const uint64_t lo = w[0];
+  const uint64_t hi = w[1];
+  const int sh = (off & 7) * 8;
+  return sh ? (lo >> sh) | (hi << (64 - sh)) : lo;
+}
+
+// Record header at absolute position p whose bytes lie in the LDS window starting at wb.
+// Fast path: both VLQs one byte (every key < 127 bytes and value < 128 bytes); otherwise the
+// generic Java-int VLQ decoder on the same bytes.
+__device__ __forceinline__ RecHdr decode_lds(const uint8_t* win, int64_t wb, int64_t p, int64_t avail) {
+  const uint64_t x = lds_u64_at(win, (int)(p - wb));
+  RecHdr h;
+  if ((x & 0x8080ull) == 0) {
+    h.rc = 0;
+    h.hlen = 2;
+    const int32_t first = (int32_t)(x & 0xff);
+    const int32_t second = (int32_t)((x >> 8) & 0xff);
+    if (first == 0) { h.put = 0; h.klen = second; h.vlen = 0; }
+    else { h.put = 1; h.klen = first - 1; h.vlen = second; }
+  } else {
+    auto at = [&](int64_t a) -> uint32_t { return win[a - wb]; };
+    h = decode_header(at, p, p + 12);
+  }
+  if (h.rc == 0 && p + h.hlen > avail) h.rc = kErrCorruptLog;
+  return h;
+}
+
+// Key byte loaders for the hashes: u64(o) = the 8 key bytes starting at key offset o (the bytes
+// past the key are read but masked off).
+struct LdsKey {  // key in an 8-byte aligned LDS window
+  const uint8_t* win;
+  int base;
+  __device__ __forceinline__ uint64_t u64(int o) const { return lds_u64_at(win, base + o); }
+};
+struct GlobalKey {  // key in global memory with at least 16 readable bytes past its end
+  const uint8_t* p;
+  __device__ __forceinline__ uint64_t u64(int o) const {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p + o);
+    const uint64_t* q = reinterpret_cast<const uint64_t*>(a & ~(uintptr_t)7);
+    const uint64_t lo = q[0], hi = q[1];
+    const int sh = (int)(a & 7) * 8;
+    return sh ? (lo >> sh) | (hi << (64 - sh)) : lo;
+  }
+};
+
+// MurmurHash3 x86_32 of `len` key bytes (MurmurHash3.java:18-75).
+template <class Ld>
+__device__ inline uint32_t murmur32_ld(const Ld& ld, int32_t len, uint32_t seed) {
+  const uint32_t c1 = 0xcc9e2d51u, c2 = 0x1b873593u;
+  uint32_t h1 = seed;
+  const int32_t nblocks = len >> 2;
+  auto block = [&](uint32_t k1) {
+    k1 *= c1; k1 = rotl32(k1, 15); k1 *= c2;
+    h1 ^= k1; h1 = rotl32(h1, 13); h1 = h1 * 5 + 0xe6546b64u;
+  };
+  int32_t i = 0;
+  for (; i + 1 < nblocks; i += 2) {
+    const uint64_t x = ld.u64(4 * i);
+    block((uint32_t)x);
+    block((uint32_t)(x >> 32));
+  }
+  if (i < nblocks) block((uint32_t)ld.u64(4 * i));
+  const int32_t rem = len & 3;
+  if (rem) {
+    uint32_t k1 = (uint32_t)ld.u64(4 * nblocks) & ((1u << (8 * rem)) - 1u);
+    k1 *= c1; k1 = rotl32(k1, 15); k1 *= c2; h1 ^= k1;
+  }
+  h1 ^= (uint32_t)len;
+  h1 ^= h1 >> 16; h1 *= 0x85ebca6bu; h1 ^= h1 >> 13; h1 *= 0xc2b2ae35u; h1 ^= h1 >> 16;
+  return h1;
+}
+
+// MurmurHash3 x64_128 -> h1 of `len` key bytes (MurmurHash3.java:100-201).
+template <class Ld>
+__device__ inline uint64_t murmur64_ld(const Ld& ld, int32_t len, uint32_t seed) {
+  const uint64_t c1 = 0x87c37b91114253d5ull, c2 = 0x4cf5ad432745937full;
+  uint64_t h1 = (uint64_t)seed, h2 = h1;
+  const int32_t nblocks = len >> 4;
+  for (int32_t i = 0; i < nblocks; i++) {
+    uint64_t k1 = ld.u64(16 * i);
+    uint64_t k2 = ld.u64(16 * i + 8);
+    k1 *= c1; k1 = rotl64(k1, 31); k1 *= c2; h1 ^= k1;
+    h1 = rotl64(h1, 27); h1 += h2; h1 = h1 * 5 + 0x52dce729ull;
+    k2 *= c2; k2 = rotl64(k2, 33); k2 *= c1; h2 ^= k2;
+    h2 = rotl64(h2, 31); h2 += h1; h2 = h2 * 5 + 0x38495ab5ull;
+  }
+  const int32_t rem = len & 15;
+  const int t = 16 * nblocks;
+  if (rem > 8) {
+    uint64_t k2 = ld.u64(t + 8) & ((1ull << (8 * (rem - 8))) - 1ull);
+    k2 *= c2; k2 = rotl64(k2, 33); k2 *= c1; h2 ^= k2;
+  }
+  if (rem > 0) {
+    uint64_t k1 = ld.u64(t);
+    if (rem < 8) k1 &= (1ull << (8 * rem)) - 1ull;
+    k1 *= c1; k1 = rotl64(k1, 31); k1 *= c2; h1 ^= k1;
+  }
+  h1 ^= (uint64_t)(int64_t)len;
+  h2 ^= (uint64_t)(int64_t)len;
+  h1 += h2; h2 += h1;
+  h1 = fmix64(h1); h2 = fmix64(h2);
+  h1 += h2;
+  return h1;
+}
+
+// ------------------------------------------------------------------------------------------------
+// granules (8-byte {state, value} words) -- relaxed agent-scope atomics, zeroed before the launch
+// ------------------------------------------------------------------------------------------------
+constexpr unsigned long long kReady = 1ull << 63;   // exit granule: bit 63 = published
+
+__device__ __forceinline__ void granule_store(unsigned long long* g, unsigned long long v) {
+  __hip_atomic_store(g, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long granule_load(unsigned long long* g) {
+  return __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ bool screen_start(uint32_t b0, uint32_t b1, const BuildParams& P) {
+  // Canonical VLQs (what LogWriter writes).  Pruning a true start only costs speed: the chunk is
+  // then unresolved or disagrees with its verified walk, and is re-walked exactly.
+  if (b0 == 0) return P.max_key_len >= 128 || (int64_t)b1 <= P.max_key_len;  // DELETE, VLQ(keyLen)
+  if (b0 >= 0x80) return P.max_key_len + 1 >= 128;                            // multi-byte keyLen+1
+  if ((int64_t)b0 - 1 > P.max_key_len) return false;
+  return P.max_value_len >= 128 || (int64_t)b1 <= P.max_value_len;            // PUT, VLQ(valueLen)
+}
+
+__device__ __forceinline__ uint4 load16_guarded(const uint8_t* log, int64_t a, int64_t log_len) {
+  if (a + 16 <= log_len) return *reinterpret_cast<const uint4*>(log + a);
+  uint8_t tmp[16];
+#pragma unroll
+  for (int i = 0; i < 16; i++) tmp[i] = (a + i < log_len) ? log[a + i] : 0;
+  return *reinterpret_cast<uint4*>(tmp);
+}
+
+// 8 bytes at any region offset (two aligned 8-byte reads; the region is allocated in 256 B blocks)
+__device__ __forceinline__ uint64_t rgn_u64(const uint8_t* r, uint32_t o) {
+  const uint32_t a = o & ~7u;
+  const uint64_t lo = *reinterpret_cast<const uint64_t*>(r + a);
+  const uint64_t hi = *reinterpret_cast<const uint64_t*>(r + a + 8);
+  const uint32_t sh = (o & 7u) * 8u;
+  return sh ? (lo >> sh) | (hi << (64 - sh)) : lo;
+}
+struct RgnKey {
+  const uint8_t* r;
+  uint32_t base;
+  __device__ __forceinline__ uint64_t u64(int o) const { return rgn_u64(r, base + (uint32_t)o); }
+};
+
+// Record header at absolute position p inside the region (p - R0 + 16 <= region bytes).
+__device__ __forceinline__ RecHdr decode_rgn(const uint8_t* r, int64_t R0, int64_t p, int64_t avail) {
+  const uint64_t x = rgn_u64(r, (uint32_t)(p - R0));
+  RecHdr h;
+  if ((x & 0x8080ull) == 0) {
+    h.rc = 0;
+    h.hlen = 2;
+    const int32_t first = (int32_t)(x & 0xff);
+    const int32_t second = (int32_t)((x >> 8) & 0xff);
+    if (first == 0) { h.put = 0; h.klen = second; h.vlen = 0; }
+    else { h.put = 1; h.klen = first - 1; h.vlen = second; }
+  } else {
+    auto at = [&](int64_t a) -> uint32_t { return r[(uint32_t)(a - R0)]; };
+    h = decode_header(at, p, p + 12);
+  }
+  if (h.rc == 0 && p + h.hlen > avail) h.rc = kErrCorruptLog;
+  return h;
+}
+
+
+// SWAR record-start screen over 8 positions (screen_start bytewise): x = the bytes at p .. p + 7,
+// y = the bytes at p + 1 .. p + 8; bit i of the result = position p + i is a plausible start
+// (canonical VLQs within the header's maxima; 0x00 only when the header counts DELETEs).
+struct Screen8 {
+  uint64_t rk, rv, rd;
+  bool allk, allv, alld, no_del;
+};
+__device__ __forceinline__ Screen8 make_screen8(const BuildParams& P) {
+  constexpr uint64_t ONES = 0x0101010101010101ull;
+  Screen8 S;
+  const int64_t TK = P.max_key_len + 1 >= 128 ? 127 : P.max_key_len + 1;
+  S.allk = P.max_key_len + 1 >= 128;
+  S.allv = P.max_value_len >= 127;
+  S.alld = P.max_key_len >= 127;
+  S.rk = ONES * (uint64_t)(min(TK, (int64_t)126) + 1);
+  S.rv = ONES * (uint64_t)(min(P.max_value_len, (int64_t)126) + 1);
+  S.rd = ONES * (uint64_t)(min(P.max_key_len, (int64_t)126) + 1);
+  S.no_del = P.no_deletes != 0;
+  return S;
+}
+__device__ __forceinline__ uint32_t screen8(uint64_t x, uint64_t y, const Screen8& S) {
+  constexpr uint64_t H = 0x8080808080808080ull, L7 = 0x7f7f7f7f7f7f7f7full, ONES = 0x0101010101010101ull;
+  auto le_rep = [&](uint64_t v, uint64_t rep, bool all) -> uint64_t { return all ? H : ~(v | ((v | H) - rep)) & H; };
+  const uint64_t z = ~(((x & L7) + L7) | x) & H;  // zero bytes
+  const uint64_t put_first = le_rep(x, S.rk, S.allk) & ~z;
+  const uint64_t r = (put_first & le_rep(y, S.rv, S.allv)) | (S.no_del ? 0ull : (z & le_rep(y, S.rd, S.alld)));
+  return (uint32_t)((((r >> 7) & ONES) * 0x0102040810204080ull) >> 56);  // bit 8i -> bit i
+}
+
+}  // namespace sk

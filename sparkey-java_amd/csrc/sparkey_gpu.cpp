@@ -522,11 +522,51 @@ static int64_t uniform_record_size(const LogHdr& lh) {
   return 0;
 }
 
+// Wave geometry of one framing kernel: k_frame (chunks of 2^cshift, w per wave) or k_frame2
+// (segments of 2^cshift, w per wave).
+struct FrameGeom {
+  int32_t cshift, w;
+  uint64_t k0, nchunks;
+};
+static FrameGeom get_geom(const BuildParams& P) { return FrameGeom{P.fr_cshift, P.fr_w, P.fr_k0, P.fr_nchunks}; }
+static void set_geom(BuildParams& P, const FrameGeom& g) {
+  P.fr_cshift = g.cshift;
+  P.fr_w = g.w;
+  P.fr_k0 = g.k0;
+  P.fr_nchunks = g.nchunks;
+}
+
+// k_frame2's geometry (frame2_kernels.hip): segments SEG = max(512, nextpow2(maxRecLen)) bytes,
+// S = 8 KiB / SEG of them per wave (2..32), each listing up to f2_lcap record starts (a log of
+// records far below 16 bytes on average overflows them and is framed by k_frame instead).
+// SPARKEY_FRAME2_SEG / SPARKEY_FRAME2_S override (measurements).
+static FrameGeom frame2_geometry(BuildParams& P, int64_t entry, int64_t frame_end) {
+  int cs = 9;
+  while ((1ll << cs) < P.max_rec_len) cs++;
+  if (const char* v = getenv("SPARKEY_FRAME2_SEG")) {
+    int want = 8;
+    while ((1ll << want) < atoll(v)) want++;
+    cs = std::max(cs, want);
+  }
+  int64_t S = std::max<int64_t>(2, std::min<int64_t>(32, 8192 >> cs));
+  if (const char* v = getenv("SPARKEY_FRAME2_S")) S = std::max<int64_t>(2, std::min<int64_t>(32, atoll(v)));
+  const int64_t SEG = 1ll << cs;
+  P.f2_lcap = (int32_t)((std::min<int64_t>(SEG / 2 + 2, SEG / 16 + 8) + 1) & ~1ll);
+  const int64_t look = std::min<int64_t>(P.max_rec_len, 2048) + 32;
+  P.f2_rgn_bytes = (int32_t)((S * SEG + look + 1023) & ~1023ll);
+  FrameGeom g;
+  g.cshift = cs;
+  g.w = (int32_t)S;
+  g.k0 = (uint64_t)entry >> cs;
+  g.nchunks = frame_end > entry ? (uint64_t)((frame_end + SEG - 1) / SEG) - g.k0 : 0;
+  return g;
+}
+
 // Slab layout of the framing output and the workspace it needs (grown on demand).
 static int reserve_for_framing(sparkey_plan* pl, BuildParams& P, int framing_path, uint64_t nrec, uint32_t slab_cap,
                                char* err, size_t err_len) {
   const uint64_t nwaves = P.fr_nchunks ? (P.fr_nchunks + P.fr_w - 1) / P.fr_w : 0;
-  if (framing_path == 0) {
+  if (framing_path == 0 || framing_path == 3) {
     P.slab_cap = slab_cap;
     P.nslabs = nwaves;
   } else {  // dense entries from the serial framing path, seen as slabs of kPartTile
@@ -560,10 +600,11 @@ static int reserve_for_framing(sparkey_plan* pl, BuildParams& P, int framing_pat
 static int launch_framing(sparkey_plan* pl, const BuildParams& P, int framing_path, hipStream_t s, char* err,
                           size_t err_len) {
   const uint64_t nwaves = P.fr_nchunks ? (P.fr_nchunks + P.fr_w - 1) / P.fr_w : 0;
-  if (framing_path == 0) {
+  if (framing_path == 0 || framing_path == 3) {
     HIP_TRY(hipMemsetAsync(pl->desc, 0, (2 * nwaves + 2) * sizeof(unsigned long long), s));
     HIP_TRY(hipMemsetAsync(pl->wcount, 0, (P.nslabs + 1) * sizeof(uint32_t), s));
-    launch_frame_fused(P, s, &pl->timer);
+    if (framing_path == 3) launch_frame2(P, s, &pl->timer);
+    else launch_frame_fused(P, s, &pl->timer);
   } else if (framing_path == 2) {
     launch_frame_uniform(P, s, &pl->timer);
     launch_dense_slabs(P, s);
@@ -904,7 +945,17 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
   uint8_t hdr[kIndexHeaderSize];
   index_header_template(lh, ip, opts->hash_seed, hdr);
 
-  int framing_path = fused_framing ? 0 : 1, placement_path = 0;
+  // k_frame2 for records of mixed sizes (the header's mean record at least 24 bytes), k_frame for
+  // the rest; both fall back to the serial walk
+  const FrameGeom geom0 = get_geom(P);
+  const FrameGeom geom2 = frame2_geometry(P, kLogHeaderSize, std::max<int64_t>(lh.data_end, kLogHeaderSize));
+  bool use_frame2 = fused_framing && !getenv("SPARKEY_NO_FRAME2");
+  {
+    const int64_t nr = std::max<int64_t>(0, lh.num_puts) + std::max<int64_t>(0, lh.num_deletes);
+    const int64_t by = std::max<int64_t>(0, lh.put_size) + std::max<int64_t>(0, lh.delete_size);
+    if (nr > 0 && by < 24 * nr) use_frame2 = false;
+  }
+  int framing_path = fused_framing ? (use_frame2 ? 3 : 0) : 1, placement_path = 0;
   if (const int64_t R = uniform_record_size(lh)) {  // k_frame_uniform: every record is exactly R bytes
     framing_path = 2;
     P.uni_n = (uint64_t)lh.num_puts;
@@ -912,15 +963,23 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
   }
   float ms = 0.f;
   Status& st = *pl->h_status;
-  const uint64_t nwaves = P.fr_nchunks ? (P.fr_nchunks + P.fr_w - 1) / P.fr_w : 0;
-  // k_frame writes each wave's entries into a slab sized from the header's record count (twice the
-  // mean per wave + 32); a wave that holds more grows the slabs and the build is redone
-  uint32_t slab_cap = (uint32_t)std::min<uint64_t>(
-      kPartTile, std::max<uint64_t>(64, 2 * ((nrec + std::max<uint64_t>(nwaves, 1) - 1) / std::max<uint64_t>(nwaves, 1)) + 32));
+  // the framing kernels write each wave's entries into a slab sized from the header's record count
+  // (twice the mean per wave + 32); a wave that holds more grows the slabs and the build is redone
+  auto slab_for = [&](const FrameGeom& g) -> uint32_t {
+    const uint64_t nw = std::max<uint64_t>(1, g.nchunks ? (g.nchunks + g.w - 1) / g.w : 0);
+    return (uint32_t)std::min<uint64_t>(kPartTile, std::max<uint64_t>(64, 2 * ((nrec + nw - 1) / nw) + 32));
+  };
+  uint32_t slab_cap = slab_for(framing_path == 3 ? geom2 : geom0);
+  int slab_path = framing_path;
   bool use_regions = getenv("SPARKEY_NO_REGIONS") == nullptr, regions_used = false;
   bool use_fixed = getenv("SPARKEY_NO_P2_FIXED") == nullptr;  // k_part2s in one pass (fixed bucket regions)
   const bool fold = getenv("SPARKEY_NO_FOLD_STATS") == nullptr;  // stats from k_place_lds, no k_stats pass
-  for (int attempt = 0; attempt < 5; attempt++) {
+  for (int attempt = 0; attempt < 6; attempt++) {
+    set_geom(P, framing_path == 3 ? geom2 : geom0);
+    if ((framing_path == 0 || framing_path == 3) && framing_path != slab_path) {
+      slab_cap = slab_for(framing_path == 3 ? geom2 : geom0);
+      slab_path = framing_path;
+    }
     rc = reserve_for_framing(pl, P, framing_path, nrec, slab_cap, err, err_len);
     if (rc) return rc;
     if (getenv("SPARKEY_FRAME_DEBUG")) {
@@ -983,15 +1042,19 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
     HIP_TRY(hipEventElapsedTime(&ms, pl->ev0, pl->ev1));
     print_frame_debug(pl, P);
     print_place_debug(P);
-    if (framing_path == 0 && st.max_wave_count > slab_cap) {  // a wave overflowed its slab
+    if ((framing_path == 0 || framing_path == 3) && st.max_wave_count > slab_cap) {  // a wave overflowed its slab
       slab_cap = (uint32_t)std::min<uint64_t>(kPartTile, ((uint64_t)st.max_wave_count + 63) & ~63ull);
+      continue;
+    }
+    if (framing_path == 3 && (st.spec_fail & 16u) && st.err == ~0ull) {  // a segment's record list overflowed
+      framing_path = 0;
       continue;
     }
     if (st.overflow || st.n_records > P.max_records) {  // header under-counts records: grow and redo
       nrec = std::max<uint64_t>(st.n_records, nrec * 2 + 1);
       continue;
     }
-    if (framing_path == 0 && (st.spec_fail || st.err != ~0ull)) {  // only the verified serial walk may report
+    if ((framing_path == 0 || framing_path == 3) && (st.spec_fail || st.err != ~0ull)) {  // only the serial walk reports
       framing_path = 1;
       continue;
     }
@@ -1573,7 +1636,15 @@ int sparkey_shard_frame(sparkey_plan* pl, int64_t entry, int64_t frame_end, void
   const double frac = (double)(frame_end - entry) / (double)std::max<int64_t>(1, data_end - kLogHeaderSize);
   uint64_t nrec = (uint64_t)((double)(std::max<int64_t>(0, sh.lh.num_puts) + std::max<int64_t>(0, sh.lh.num_deletes)) *
                              frac * 1.05) + 4096;
-  int framing_path = fused ? 0 : 1;
+  const FrameGeom geom0 = get_geom(P);
+  const FrameGeom geom2 = frame2_geometry(P, entry, frame_end);
+  bool use_frame2 = fused && !getenv("SPARKEY_NO_FRAME2");
+  {
+    const int64_t nr = std::max<int64_t>(0, sh.lh.num_puts) + std::max<int64_t>(0, sh.lh.num_deletes);
+    const int64_t by = std::max<int64_t>(0, sh.lh.put_size) + std::max<int64_t>(0, sh.lh.delete_size);
+    if (nr > 0 && by < 24 * nr) use_frame2 = false;
+  }
+  int framing_path = fused ? (use_frame2 ? 3 : 0) : 1;
   const int64_t R = uniform_record_size(sh.lh);
   if (R && (entry - kLogHeaderSize) % R == 0) {  // a record start of a uniform log: frame by stride
     framing_path = 2;
@@ -1581,11 +1652,19 @@ int sparkey_shard_frame(sparkey_plan* pl, int64_t entry, int64_t frame_end, void
     P.uni_rec = R;
     nrec = P.uni_n;
   }
-  const uint64_t nwaves = P.fr_nchunks ? (P.fr_nchunks + P.fr_w - 1) / P.fr_w : 0;
-  uint32_t slab_cap = (uint32_t)std::min<uint64_t>(
-      kPartTile, std::max<uint64_t>(64, 2 * ((nrec + std::max<uint64_t>(nwaves, 1) - 1) / std::max<uint64_t>(nwaves, 1)) + 32));
+  auto slab_for = [&](const FrameGeom& g) -> uint32_t {
+    const uint64_t nw = std::max<uint64_t>(1, g.nchunks ? (g.nchunks + g.w - 1) / g.w : 0);
+    return (uint32_t)std::min<uint64_t>(kPartTile, std::max<uint64_t>(64, 2 * ((nrec + nw - 1) / nw) + 32));
+  };
+  uint32_t slab_cap = slab_for(framing_path == 3 ? geom2 : geom0);
+  int slab_path = framing_path;
   Status& st = *pl->h_status;
-  for (int attempt = 0; attempt < 5; attempt++) {
+  for (int attempt = 0; attempt < 6; attempt++) {
+    set_geom(P, framing_path == 3 ? geom2 : geom0);
+    if ((framing_path == 0 || framing_path == 3) && framing_path != slab_path) {
+      slab_cap = slab_for(framing_path == 3 ? geom2 : geom0);
+      slab_path = framing_path;
+    }
     rc = reserve_for_framing(pl, P, framing_path, nrec, slab_cap, err, err_len);
     if (rc) return rc;
     Status init;
@@ -1597,7 +1676,7 @@ int sparkey_shard_frame(sparkey_plan* pl, int64_t entry, int64_t frame_end, void
     if (rc) return rc;
     rc = shard_sync_status(pl, s, err, err_len);
     if (rc) return rc;
-    if (framing_path == 0 && st.max_wave_count > slab_cap) {
+    if ((framing_path == 0 || framing_path == 3) && st.max_wave_count > slab_cap) {
       slab_cap = (uint32_t)std::min<uint64_t>(kPartTile, ((uint64_t)st.max_wave_count + 63) & ~63ull);
       continue;
     }
@@ -1605,7 +1684,11 @@ int sparkey_shard_frame(sparkey_plan* pl, int64_t entry, int64_t frame_end, void
       nrec = std::max<uint64_t>(st.n_records, nrec * 2 + 1);
       continue;
     }
-    if (framing_path == 0 && (st.spec_fail || st.err != ~0ull)) {
+    if (framing_path == 3 && (st.spec_fail & 16u) && st.err == ~0ull) {  // a segment's record list overflowed
+      framing_path = 0;
+      continue;
+    }
+    if ((framing_path == 0 || framing_path == 3) && (st.spec_fail || st.err != ~0ull)) {
       framing_path = 1;
       continue;
     }
