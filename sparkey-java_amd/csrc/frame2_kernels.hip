@@ -63,13 +63,10 @@ __device__ __forceinline__ int32_t spec_step(const uint8_t* rgn, int64_t R0, int
 
 }  // namespace
 
+// One region (wave index wv) of k_frame2; its exit is published before any return.
 template <bool FAST>
-__global__ __launch_bounds__(64) void k_frame2(BuildParams P) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  const int lane = threadIdx.x;
-  unsigned int tk = 0;
-  if (lane == 0) tk = atomicAdd(P.frame_ticket, 1u);
-  const uint64_t wv = (uint64_t)__builtin_amdgcn_readfirstlane(tk);
+__device__ __forceinline__ void frame2_region(const BuildParams& P, const uint64_t wv, uint8_t* lds) {
+  const int lane = threadIdx.x & 63;
   const int SS = P.fr_cshift;
   const int S = P.fr_w;
   const int LCAP = P.f2_lcap;
@@ -104,7 +101,7 @@ __global__ __launch_bounds__(64) void k_frame2(BuildParams P) {
         *reinterpret_cast<uint4*>(rgn + 16u * v) = load16_guarded(P.log, R0 + 16ll * v, log_len);
     }
   }
-  __syncthreads();
+  wave_sync();
   mark(0);
 
   const int64_t lim64 = log_len - R0;
@@ -127,48 +124,73 @@ __global__ __launch_bounds__(64) void k_frame2(BuildParams P) {
   bool found = false;
   unsigned long long nsurv = 0, exmin = ~0ull, cmin = ~0ull;
   long long exmax = -1;
-  for (int pass = 0;; pass++) {
-    // this lane's window [ws, we) and walk bound for this pass
-    int64_t ws = 0, we = 0, bnd = 0;
-    if (walker) {
-      if (pass == 0) { ws = a; we = a + mrl; bnd = b; }
-    } else if (lane >= S && wv > 0) {
-      const int wi = (lane - S) + pass * ncl;
-      if (wi < nwords0) {
-        ws = a0 + 8ll * wi;
-        we = min(ws + 8, a0 + (int64_t)mrl);
-        bnd = b0;
+  // One flat loop, one step per lane per iteration (no nested per-lane loops for the wave to run
+  // through one after another): a lane either screens its next 8-byte word or takes its next
+  // candidate, or advances its walk by one record.  Region offsets in 32 bits.
+  const uint64_t* r64 = reinterpret_cast<const uint64_t*>(rgn);
+  int32_t wpos = 0, wend = 0, rb = 0, pass = 0;
+  if (walker) {
+    wpos = (int32_t)(a - R0);
+    wend = wpos + mrl;
+    rb = (int32_t)(b - R0);
+  } else if (lane >= S && wv > 0 && lane - S < nwords0) {
+    wpos = (int32_t)(a0 - R0) + 8 * (lane - S);
+    wend = min(wpos + 8, (int32_t)(a0 - R0) + mrl);
+    rb = (int32_t)(b0 - R0);
+  }
+  bool done = wpos >= wend;
+  uint32_t msk = 0;
+  int32_t wbase = 0, rp = -1, cs = 0, cnt = 0;
+  uint32_t iters = 0;
+  for (;;) {
+    iters++;
+    if (!done && rp < 0) {
+      if (msk == 0 && wpos >= wend && !walker) {  // a candidate lane's next word
+        const int wi = (lane - S) + (++pass) * ncl;
+        if (wi < nwords0) {
+          wpos = (int32_t)(a0 - R0) + 8 * wi;
+          wend = min(wpos + 8, (int32_t)(a0 - R0) + mrl);
+        }
+      }
+      if (msk == 0) {
+        if (wpos >= wend) {
+          done = true;
+        } else {  // screen one word (windows start 8-byte aligned)
+          const uint64_t x = r64[wpos >> 3], x2 = r64[(wpos >> 3) + 1];
+          msk = screen8(x, (x >> 8) | (x2 << 56), scr);
+          if (wpos + 8 > wend) msk &= (1u << (uint32_t)(wend - wpos)) - 1u;
+          wbase = wpos;
+          wpos += 8;
+        }
+      }
+      if (msk) {
+        cs = wbase + __builtin_ctz(msk);
+        msk &= msk - 1;
+        rp = cs;
+        cnt = 0;
       }
     }
-    if (!__any(ws < we)) break;
-    for (int64_t w = ws; w < we && !found; w += 8) {
-      const uint32_t ro = (uint32_t)(w - R0);
-      const uint64_t x = rgn_u64(rgn, ro), x2 = rgn_u64(rgn, ro + 8);
-      uint32_t msk = screen8(x, (x >> 8) | (x2 << 56), scr);
-      if (w + 8 > we) msk &= (1u << (uint32_t)(we - w)) - 1u;
-      while (msk) {
-        const int i = __builtin_ctz(msk);
-        msk &= msk - 1;
-        const int32_t cs = (int32_t)(w - R0) + i;
-        const int32_t rb = (int32_t)(bnd - R0);
-        int32_t rp = cs;
-        int32_t cnt = 0;
-        while (rp >= 0 && rp < rb) {
-          if (walker && cnt < LCAP) my[cnt] = (uint16_t)rp;
-          cnt++;
-          rp = spec_step<FAST>(rgn, R0, rp, P, lim, mk, mv);
-        }
-        if (rp < 0) continue;  // died: not a start
+    if (!__any(!done)) break;
+    if (rp >= 0) {
+      if (rp >= rb) {  // the chain from cs stayed plausible to the walk bound
         if (walker) {
           found = true;
           xk = R0 + rp;
           m = cnt;
-          break;
+          done = true;
+        } else {
+          nsurv++;
+          exmin = min(exmin, (unsigned long long)(R0 + rp));
+          exmax = max(exmax, (long long)(R0 + rp));
+          cmin = min(cmin, (unsigned long long)(R0 + cs));
         }
-        nsurv++;
-        exmin = min(exmin, (unsigned long long)(R0 + rp));
-        exmax = max(exmax, (long long)(R0 + rp));
-        cmin = min(cmin, (unsigned long long)(R0 + cs));
+        rp = -1;
+      } else if (walker && cnt == LCAP) {  // more starts than a segment lists: not taken
+        rp = -1;
+      } else {
+        if (walker) my[cnt] = (uint16_t)rp;
+        cnt++;
+        rp = spec_step<FAST>(rgn, R0, rp, P, lim, mk, mv);
       }
     }
   }
@@ -231,7 +253,9 @@ __global__ __launch_bounds__(64) void k_frame2(BuildParams P) {
   int64_t X = 0, e0 = 0;
   bool seg0_done = false;
   int32_t m0 = 0;
-  if (wv == 0 || !(ns0 > 0 && (long long)xmin0 == xmax0)) {
+  // (a segment 0 cut short by the frame end may hold no record start at all: its entry can be the
+  // frame end itself, which no candidate screen sees -- it takes the entry)
+  if (wv == 0 || b0 < R0 + (1ll << SS) || !(ns0 > 0 && (long long)xmin0 == xmax0)) {
     e0 = wv == 0 ? P.fr_entry : wait_prev();
     int64_t x0 = 0;
     if (lane == 0) x0 = exact_walk(e0, b0, lists, m0);
@@ -288,9 +312,8 @@ __global__ __launch_bounds__(64) void k_frame2(BuildParams P) {
   const int64_t wexit = __shfl(lane == 0 ? X : xk, last, 64);
   if (lane == 0) {
     granule_store(&P.exit_desc[wv], (unsigned long long)wexit | kReady);
-    if (wv + 1 == gridDim.x) P.st->exit = wexit;
+    if (wv + 1 == (P.fr_nchunks + P.fr_w - 1) / P.fr_w) P.st->exit = wexit;
   }
-  const bool lovf = __any((walker && m > LCAP) || (lane == 0 && m0 > LCAP));
   mark(2);
 
   // ---- D + E: segment 0 from its entry, then every verified record hashed into the slab ----
@@ -315,7 +338,9 @@ __global__ __launch_bounds__(64) void k_frame2(BuildParams P) {
         return;
       }
     }
-    if (lovf || __any(bad)) {  // (a list overflowed: the host redoes the build with k_frame)
+    // every list complete (segment 0's included): else the host redoes the build with k_frame
+    const bool lovf = __any((walker && m > LCAP) || (lane == 0 && m0 > LCAP));
+    if (lovf || __any(bad)) {
       if (lane == 0 && lovf) atomicOr(&P.st->spec_fail, 16u);
       return;
     }
@@ -349,12 +374,18 @@ __global__ __launch_bounds__(64) void k_frame2(BuildParams P) {
       for (uint32_t i = 0; i < cnt; i++) clist[o + i] = src[i];
     }
     if (lane == 0) P.wcount[wv] = total;
-    __syncthreads();
+    wave_sync();
     mark(3);
     const unsigned long long base = wv * (unsigned long long)P.slab_cap;
     ndel = 0;
+    const uint32_t span = (uint32_t)S << SS;
     for (uint32_t r = (uint32_t)lane; r < total; r += 64) {
-      const int64_t p = R0 + (int64_t)clist[r];
+      const uint32_t off = clist[r];
+      if (off >= span) {  // (cannot happen: every listed start lies in the wave's segments)
+        atomicOr(&P.st->spec_fail, 32u);
+        continue;
+      }
+      const int64_t p = R0 + (int64_t)off;
       const RecHdr h = hdr_at(p);
       const int64_t kp = p + h.hlen;
       uint64_t hash;
@@ -383,7 +414,7 @@ __global__ __launch_bounds__(64) void k_frame2(BuildParams P) {
       if (real != e0) {
         e0 = real;
         seg0_done = false;
-        __syncthreads();  // (the list is rewritten)
+        wave_sync();  // (the list is rewritten)
         continue;
       }
     }
@@ -392,18 +423,33 @@ __global__ __launch_bounds__(64) void k_frame2(BuildParams P) {
   ndel = wave_sum_u64(ndel);
   if (ndel && lane == 0) atomicAdd(&P.st->n_deletes, ndel);
   mark(4);
-  if (P.dbg) {
-    const unsigned long long sv = ns0;
-    if (lane == 0) { P.dbg[wv * 16 + 9] = sv; }
+  if (P.dbg && lane == 0) {
+    P.dbg[wv * 16 + 9] = ns0;
+    P.dbg[wv * 16 + 8] = iters;
   }
+}
+
+// kFrameWaves waves per workgroup, one region each, regions by workgroup ticket (see k_frame).
+template <bool FAST>
+__global__ __launch_bounds__(64 * kFrameWaves, 5) void k_frame2(BuildParams P, uint32_t lds_per_wave) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  __shared__ unsigned int tk;
+  if (threadIdx.x == 0) tk = atomicAdd(P.frame_ticket, 1u);
+  __syncthreads();
+  const uint64_t nwaves = (P.fr_nchunks + P.fr_w - 1) / P.fr_w;
+  const uint32_t w = threadIdx.x >> 6;
+  const uint64_t wv = (uint64_t)tk * kFrameWaves + w;
+  if (wv < nwaves) frame2_region<FAST>(P, wv, lds + w * lds_per_wave);
 }
 
 void launch_frame2(const BuildParams& P, hipStream_t s, StageTimer* tm) {
   if (P.fr_nchunks == 0) return;
   const uint64_t nwaves = (P.fr_nchunks + P.fr_w - 1) / P.fr_w;
   const size_t lds = (size_t)P.f2_rgn_bytes + 2 * (size_t)P.fr_w * P.f2_lcap * 2;
-  if (P.fr_fast) hipLaunchKernelGGL(k_frame2<true>, dim3((unsigned)nwaves), dim3(64), lds, s, P);
-  else hipLaunchKernelGGL(k_frame2<false>, dim3((unsigned)nwaves), dim3(64), lds, s, P);
+  const uint32_t per = (uint32_t)((lds + 15) & ~(size_t)15);
+  const dim3 grid((unsigned)((nwaves + kFrameWaves - 1) / kFrameWaves)), block(64 * kFrameWaves);
+  if (P.fr_fast) hipLaunchKernelGGL(k_frame2<true>, grid, block, (size_t)per * kFrameWaves, s, P, per);
+  else hipLaunchKernelGGL(k_frame2<false>, grid, block, (size_t)per * kFrameWaves, s, P, per);
   tm->mark("frame", s);
   scan_exclusive<uint32_t, uint64_t, OpAdd>(P.wcount, P.woff, P.nslabs, (uint64_t*)&P.st->n_records, OpAdd(),
                                             P.scan_scratch_u64, s);

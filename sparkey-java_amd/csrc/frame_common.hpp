@@ -6,6 +6,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "build_kernels.hpp"
 #include "device_common.hpp"
 #include "kernel_utils.hpp"
@@ -185,6 +187,35 @@ __device__ __forceinline__ RecHdr decode_rgn(const uint8_t* r, int64_t R0, int64
   return h;
 }
 
+
+// The framing kernels run several independent waves per workgroup (one log region each): their
+// LDS hand-offs are between the lanes of one wave, so they synchronise the wave, not the workgroup
+// (a wave may spin on another region's exit while its neighbours are elsewhere).  Every LDS access
+// and LDS-DMA of the wave has completed after this.
+__device__ __forceinline__ void wave_sync() {
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// Framing regions per workgroup: one wave each, consecutive regions, one ticket per workgroup.  A
+// region waits only for lower regions' published exits; the ticket order makes every such region
+// belong to a workgroup that is already resident, whatever order the dispatcher admits workgroups
+// in.  One device-scope atomic per workgroup: a ticket per wave measured 88 per microsecond at
+// most, which bounds a launch of 1.7M one-wave workgroups (C3) to 19 ms.
+constexpr int kFrameWaves = 4;
+
+// Workgroups of a persistent launch that the device holds resident at once (occupancy API x CUs,
+// one fewer per CU as margin -- the API can answer one high, MI355X_MICROARCH.md "Residency"), at most
+// `want`.  Host side.
+inline uint64_t resident_grid(const void* kernel, int block, size_t lds, uint64_t want) {
+  int dev = 0, per_cu = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, block, lds) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || per_cu <= 0 || cus <= 0)
+    return std::min<uint64_t>(want, 256);
+  const uint64_t cap = (uint64_t)std::max(1, per_cu - 1) * (uint64_t)cus;
+  return std::max<uint64_t>(1, std::min<uint64_t>(want, cap));
+}
 
 // SWAR record-start screen over 8 positions (screen_start bytewise): x = the bytes at p .. p + 7,
 // y = the bytes at p + 1 .. p + 8; bit i of the result = position p + i is a plausible start

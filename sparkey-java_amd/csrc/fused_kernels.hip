@@ -57,15 +57,10 @@ __device__ __forceinline__ uint32_t cand_start(uint32_t v) { return v & 0x3fffu;
 __device__ __forceinline__ uint32_t cand_dexit(uint32_t v) { return (v >> 14) & 0xffu; }
 __device__ __forceinline__ int32_t cand_steps(uint32_t v) { return (int32_t)((v >> 22) & 0x1ffu); }
 
-__global__ __launch_bounds__(64) void k_frame(BuildParams P) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  const int lane = threadIdx.x;
-  // The wave's place in the chain comes from a ticket, not blockIdx.x: a wave that spins on wave
-  // wv - 1's published exit knows that wave already took its ticket, so it is resident and runs to
-  // its publish whatever order the dispatcher admits workgroups in.
-  unsigned int tk = 0;
-  if (lane == 0) tk = atomicAdd(P.frame_ticket, 1u);
-  const uint64_t wv = (uint64_t)__builtin_amdgcn_readfirstlane(tk);
+// One region (wave index wv) of k_frame; returns once its entries are in the slab (its exit was
+// published before any return).
+__device__ __forceinline__ void frame_region(const BuildParams& P, const uint64_t wv, uint8_t* lds) {
+  const int lane = threadIdx.x & 63;
   const int cs = P.fr_cshift;
   const int64_t C = 1ll << cs;
   const int W = P.fr_w;
@@ -106,7 +101,7 @@ __global__ __launch_bounds__(64) void k_frame(BuildParams P) {
       }
     }
   }
-  __syncthreads();
+  wave_sync();
   mark(0);
 
   const bool act = lane < nw;
@@ -151,7 +146,7 @@ __global__ __launch_bounds__(64) void k_frame(BuildParams P) {
       fb[q] = (uint8_t)((((r >> 7) & ONES) * 0x0102040810204080ull) >> 56);
     }
   }
-  __syncthreads();
+  wave_sync();
   // mask word wi of this lane's chunk: bit i = candidate start s + 64 wi + i
   auto masked_word = [&](int wi) -> unsigned long long {
     if (k == kf) return (wi == 0 && cand_end > s) ? 1ull : 0ull;  // the entry chunk: its only start is the entry
@@ -205,7 +200,7 @@ __global__ __launch_bounds__(64) void k_frame(BuildParams P) {
     my_ccnt = cnt_c;
     if (T <= (uint32_t)kCandCap) {
       balanced = true;
-      __syncthreads();  // every lane holds its masks: the list may overwrite the bitmap
+      wave_sync();  // every lane holds its masks: the list may overwrite the bitmap
       {  // enumerate: lane's candidates in ascending order at cand[cpre ..)
         unsigned long long a0 = has ? m0 : 0ull, a1 = has ? m1 : 0ull, a2 = has ? m2 : 0ull, a3 = has ? m3 : 0ull;
         uint32_t o = cpre;
@@ -226,7 +221,7 @@ __global__ __launch_bounds__(64) void k_frame(BuildParams P) {
           }
         }
       }
-      __syncthreads();
+      wave_sync();
       const int64_t lim64 = log_len - R0;
       const int32_t lim = lim64 > 0x7fffffff ? 0x7fffffff : (int32_t)lim64;
       const int32_t de = (int32_t)min((int64_t)0x7fffffff, P.data_end - R0);
@@ -268,7 +263,7 @@ __global__ __launch_bounds__(64) void k_frame(BuildParams P) {
           }
         }
       }
-      __syncthreads();
+      wave_sync();
       // fold the lane's own chunk
       for (uint32_t i = 0; i < cnt_c; i++) {
         const uint32_t v = cand[cpre + i];
@@ -468,7 +463,7 @@ __global__ __launch_bounds__(64) void k_frame(BuildParams P) {
       }
     }
     if (lane == nw - 1 && !converged) granule_store(&P.exit_desc[wv], (unsigned long long)my_exit | kReady);
-    if (lane == nw - 1 && wv + 1 == gridDim.x) P.st->exit = my_exit;  // the framed chain's exit
+    if (lane == nw - 1 && wv + 1 == (P.fr_nchunks + P.fr_w - 1) / P.fr_w) P.st->exit = my_exit;  // the framed chain's exit
     const int64_t up = __shfl_up(my_exit, 1, 64);
     const int64_t entry = lane == 0 ? ext : up;
 
@@ -565,7 +560,7 @@ __global__ __launch_bounds__(64) void k_frame(BuildParams P) {
     };
     if (total <= (unsigned long long)kCandCap) {  // wave-uniform
       uint32_t* list = reinterpret_cast<uint32_t*>(lds + P.fr_rgn_bytes);  // overlays the candidate list
-      __syncthreads();
+      wave_sync();
       cands_live = false;
       {
         int64_t p = (act && cnt > 0) ? entry : e;
@@ -579,7 +574,7 @@ __global__ __launch_bounds__(64) void k_frame(BuildParams P) {
           }
         }
       }
-      __syncthreads();
+      wave_sync();
       for (uint32_t i = (uint32_t)lane; i < (uint32_t)total; i += 64) emit(R0 + (int64_t)list[i], base + i);
     } else {
       int64_t p = (act && cnt > 0) ? entry : e;
@@ -603,6 +598,19 @@ __global__ __launch_bounds__(64) void k_frame(BuildParams P) {
   ndel = wave_sum_u64(ndel);
   if (ndel && lane == 0) atomicAdd(&P.st->n_deletes, ndel);
   mark(6);
+}
+
+// kFrameWaves waves per workgroup, one region each: the workgroup's ticket t gives regions
+// t * kFrameWaves + wave (frame_common.hpp).
+__global__ __launch_bounds__(64 * kFrameWaves, 5) void k_frame(BuildParams P, uint32_t lds_per_wave) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  __shared__ unsigned int tk;
+  if (threadIdx.x == 0) tk = atomicAdd(P.frame_ticket, 1u);
+  __syncthreads();
+  const uint64_t nwaves = (P.fr_nchunks + P.fr_w - 1) / P.fr_w;
+  const uint32_t w = threadIdx.x >> 6;
+  const uint64_t wv = (uint64_t)tk * kFrameWaves + w;
+  if (wv < nwaves) frame_region(P, wv, lds + w * lds_per_wave);
 }
 
 __device__ __forceinline__ uint32_t bucket_of(const BuildParams& P, uint64_t hash) {
@@ -1393,7 +1401,9 @@ void launch_frame_fused(const BuildParams& P, hipStream_t s, StageTimer* tm) {
   // the screen's bitmap (one bit per candidate-window byte), later overlaid by the balanced walk's
   // candidate list and then by the record list
   const size_t lds = (size_t)P.fr_rgn_bytes + std::max<size_t>((size_t)P.fr_w * P.fr_mask_words * 8 + 8, kCandCap * 4);
-  hipLaunchKernelGGL(k_frame, dim3((unsigned)nwaves), dim3(64), lds, s, P);
+  const uint32_t per = (uint32_t)((lds + 15) & ~(size_t)15);
+  hipLaunchKernelGGL(k_frame, dim3((unsigned)((nwaves + kFrameWaves - 1) / kFrameWaves)), dim3(64 * kFrameWaves),
+                     (size_t)per * kFrameWaves, s, P, per);
   tm->mark("frame", s);  // the stage is k_frame alone (its rocprof row); the slab scan counts as partition
   scan_exclusive<uint32_t, uint64_t, OpAdd>(P.wcount, P.woff, P.nslabs, (uint64_t*)&P.st->n_records, OpAdd(),
                                             P.scan_scratch_u64, s);

@@ -551,6 +551,7 @@ static FrameGeom frame2_geometry(BuildParams& P, int64_t entry, int64_t frame_en
   int64_t S = std::max<int64_t>(2, std::min<int64_t>(32, 8192 >> cs));
   if (const char* v = getenv("SPARKEY_FRAME2_S")) S = std::max<int64_t>(2, std::min<int64_t>(32, atoll(v)));
   const int64_t SEG = 1ll << cs;
+  S = std::max<int64_t>(2, std::min<int64_t>(S, 32768 / SEG));  // the wave's starts are 16-bit LDS offsets
   P.f2_lcap = (int32_t)((std::min<int64_t>(SEG / 2 + 2, SEG / 16 + 8) + 1) & ~1ll);
   const int64_t look = std::min<int64_t>(P.max_rec_len, 2048) + 32;
   P.f2_rgn_bytes = (int32_t)((S * SEG + look + 1023) & ~1023ll);
@@ -949,11 +950,13 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
   // the rest; both fall back to the serial walk
   const FrameGeom geom0 = get_geom(P);
   const FrameGeom geom2 = frame2_geometry(P, kLogHeaderSize, std::max<int64_t>(lh.data_end, kLogHeaderSize));
-  bool use_frame2 = fused_framing && !getenv("SPARKEY_NO_FRAME2");
+  bool use_frame2 = fused_framing && getenv("SPARKEY_FRAME2") != nullptr;  // (measured slower than k_frame so far)
   {
     const int64_t nr = std::max<int64_t>(0, lh.num_puts) + std::max<int64_t>(0, lh.num_deletes);
     const int64_t by = std::max<int64_t>(0, lh.put_size) + std::max<int64_t>(0, lh.delete_size);
-    if (nr > 0 && by < 24 * nr) use_frame2 = false;
+    // (a log with DELETEs lets 0x00 bytes start records: zero-filled values then hold long
+    // plausible chains of 2-byte records, which k_frame's per-chunk screen handles better)
+    if ((nr > 0 && by < 24 * nr) || lh.num_deletes != 0) use_frame2 = false;
   }
   int framing_path = fused_framing ? (use_frame2 ? 3 : 0) : 1, placement_path = 0;
   if (const int64_t R = uniform_record_size(lh)) {  // k_frame_uniform: every record is exactly R bytes
@@ -982,9 +985,10 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
     }
     rc = reserve_for_framing(pl, P, framing_path, nrec, slab_cap, err, err_len);
     if (rc) return rc;
-    if (getenv("SPARKEY_FRAME_DEBUG")) {
-      HIP_TRY(grow(&pl->dbg, pl->c_dbg, 16 * std::max<uint64_t>(P.nchunks, 1)));
-      HIP_TRY(hipMemsetAsync(pl->dbg, 0, 16 * P.nchunks * sizeof(unsigned long long), s));
+    if (getenv("SPARKEY_FRAME_DEBUG")) {  // per-wave phase counters: 16 words per k_frame / k_frame2 wave
+      const uint64_t nw = std::max<uint64_t>(std::max<uint64_t>(P.nchunks, P.fr_nchunks ? (P.fr_nchunks + P.fr_w - 1) / P.fr_w : 0), 1);
+      HIP_TRY(grow(&pl->dbg, pl->c_dbg, 16 * nw));
+      HIP_TRY(hipMemsetAsync(pl->dbg, 0, 16 * nw * sizeof(unsigned long long), s));
       P.dbg = pl->dbg;
     }
     if (getenv("SPARKEY_PLACE_DEBUG")) {
@@ -1054,6 +1058,9 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
       nrec = std::max<uint64_t>(st.n_records, nrec * 2 + 1);
       continue;
     }
+    if (getenv("SPARKEY_FRAME_DEBUG") && (st.spec_fail || st.err != ~0ull))
+      fprintf(stderr, "[framing] path %d: spec_fail %u err %llx (pos %llu)\n", framing_path, st.spec_fail,
+              (unsigned long long)st.err, (unsigned long long)(st.err >> 8));
     if ((framing_path == 0 || framing_path == 3) && (st.spec_fail || st.err != ~0ull)) {  // only the serial walk reports
       framing_path = 1;
       continue;
@@ -1067,7 +1074,7 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
       continue;
     }
     if (framing_path == 2 && st.spec_fail) {  // a record differs from the header's uniform shape
-      framing_path = fused_framing ? 0 : 1;
+      framing_path = fused_framing ? (use_frame2 ? 3 : 0) : 1;
       continue;
     }
     break;
@@ -1638,11 +1645,11 @@ int sparkey_shard_frame(sparkey_plan* pl, int64_t entry, int64_t frame_end, void
                              frac * 1.05) + 4096;
   const FrameGeom geom0 = get_geom(P);
   const FrameGeom geom2 = frame2_geometry(P, entry, frame_end);
-  bool use_frame2 = fused && !getenv("SPARKEY_NO_FRAME2");
+  bool use_frame2 = fused && getenv("SPARKEY_FRAME2") != nullptr;
   {
     const int64_t nr = std::max<int64_t>(0, sh.lh.num_puts) + std::max<int64_t>(0, sh.lh.num_deletes);
     const int64_t by = std::max<int64_t>(0, sh.lh.put_size) + std::max<int64_t>(0, sh.lh.delete_size);
-    if (nr > 0 && by < 24 * nr) use_frame2 = false;
+    if ((nr > 0 && by < 24 * nr) || sh.lh.num_deletes != 0) use_frame2 = false;
   }
   int framing_path = fused ? (use_frame2 ? 3 : 0) : 1;
   const int64_t R = uniform_record_size(sh.lh);
@@ -1693,7 +1700,7 @@ int sparkey_shard_frame(sparkey_plan* pl, int64_t entry, int64_t frame_end, void
       continue;
     }
     if (framing_path == 2 && st.spec_fail) {  // not the uniform log its header describes
-      framing_path = fused ? 0 : 1;
+      framing_path = fused ? (use_frame2 ? 3 : 0) : 1;
       continue;
     }
     break;

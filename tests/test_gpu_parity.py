@@ -191,7 +191,7 @@ def test_records_spanning_chunks(native, vlen):
     log with the serial walker (few records per byte)."""
     puts = [(b"key%d" % i, bytes([i % 251]) * (vlen + (i % 7))) for i in range(300)]
     got, stats = check(native, make_log(puts), 12, hash_size=8)
-    assert stats.framing_path == (3 if vlen + 6 + 16 < 4096 else 1)
+    assert stats.framing_path == (0 if vlen + 6 + 16 < 4096 else 1)
 
 
 def test_understated_max_key_len_is_an_error(native):
@@ -225,7 +225,6 @@ def test_tiny_records_stay_on_fast_framing(native):
                                  {"SPARKEY_FRAME_LOOK": "16"}, {"SPARKEY_FRAME_LOOK": "1024"}])
 def test_frame_geometry_overrides(native, monkeypatch, env):
     monkeypatch.setenv("SPARKEY_NO_UNIFORM", "1")  # the fixed-size log would take k_frame_uniform
-    monkeypatch.setenv("SPARKEY_NO_FRAME2", "1")   # ... and mixed-size logs k_frame2
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     rng = np.random.default_rng(3)
@@ -241,6 +240,7 @@ def test_frame_geometry_overrides(native, monkeypatch, env):
 @pytest.mark.parametrize("seg,nseg", [("512", "2"), ("512", "16"), ("512", "32"), ("1024", "8"), ("2048", "4"),
                                       ("4096", "2"), ("8192", "3")])
 def test_frame2_geometry(native, monkeypatch, seg, nseg):
+    monkeypatch.setenv("SPARKEY_FRAME2", "1")
     monkeypatch.setenv("SPARKEY_FRAME2_SEG", seg)
     monkeypatch.setenv("SPARKEY_FRAME2_S", nseg)
     for seed, (kmin, kmax, vmin, vmax), hs in [(41, (1, 40, 0, 60), 8), (43, (8, 64, 100, 100), 4),
@@ -250,7 +250,7 @@ def test_frame2_geometry(native, monkeypatch, seg, nseg):
         assert stats.framing_path == 3, stats.as_dict()
 
 
-def test_frame2_list_overflow_falls_back_to_k_frame(native):
+def test_frame2_list_overflow_falls_back_to_k_frame(native, monkeypatch):
     """A stretch of 2-3 byte records inside a log of long ones: more starts in a segment than k_frame2
     lists, so the build reruns with k_frame (same bytes)."""
     puts = random_puts(4000, seed=51, kmin=30, kmax=60, vmin=100, vmax=120)
@@ -261,15 +261,28 @@ def test_frame2_list_overflow_falls_back_to_k_frame(native):
         if k not in seen:
             seen.add(k)
             uniq.append((k, v))
+    monkeypatch.setenv("SPARKEY_FRAME2", "1")
     got, stats = check(native, make_log(uniq), 53, hash_size=8)
     assert stats.framing_path == 0, stats.as_dict()
 
 
-def test_frame2_with_deletes_and_overwrites(native):
-    ops = _churn_ops(60000, 20000, 0.1, 57, klen=(8, 40), vlen=(20, 90))
-    got, stats = check(native, make_log(ops=[("put" if o == "put" else "delete", k, v) for o, k, v in ops]), 59,
-                       hash_size=8)
+def test_frame2_with_overwrites(native, monkeypatch):
+    """Overwritten keys (no DELETE): k_frame2 frames, the exact replay places."""
+    rng = np.random.default_rng(57)
+    ops = [("put", b"key-%05d" % int(rng.integers(0, 20000)), rng.integers(0, 256, int(rng.integers(20, 90)),
+                                                                          dtype=np.uint8).tobytes())
+           for _ in range(60000)]
+    monkeypatch.setenv("SPARKEY_FRAME2", "1")
+    got, stats = check(native, make_log(ops=ops), 59, hash_size=8)
     assert stats.framing_path == 3 and stats.placement_path == 2, stats.as_dict()
+
+
+def test_deletes_take_k_frame(native, monkeypatch):
+    monkeypatch.setenv("SPARKEY_FRAME2", "1")
+    """A log with DELETEs (0x00 starts a record) and zero-filled values frames with k_frame."""
+    ops = _churn_ops(60000, 20000, 0.1, 57, klen=(8, 40), vlen=(20, 90))
+    got, stats = check(native, make_log(ops=ops), 59, hash_size=8)
+    assert stats.framing_path == 0 and stats.placement_path == 2, stats.as_dict()
 
 
 # --- k_frame's bounded wait on the previous wave: a tripped wait reruns the build on the serial path ---
@@ -281,7 +294,7 @@ def test_frame_wait_timeout_falls_back_to_serial(native, monkeypatch):
     assert stats.framing_path == 1, stats.as_dict()
     monkeypatch.delenv("SPARKEY_FRAME_SPIN_TICKS")
     got2, stats2 = check(native, make_log(puts), 37, hash_size=8)
-    assert stats2.framing_path == 3 and got2 == got
+    assert stats2.framing_path == 0 and got2 == got
 
 
 # --- exact path (DELETEs, overwrites) over independent slot segments vs the single-lane replay ---
@@ -387,7 +400,7 @@ def test_uniform_header_but_record_split_differs(native):
     struct.pack_into("<q", log, 40, 16)  # maxKeyLen stays 16, maxValueLen stays 31 ...
     struct.pack_into("<q", log, 48, 30)  # ... declare maxValueLen 30 so putSize == n * (2 + 16 + 30)
     got, stats = check(native, bytes(log), 7, hash_size=8)
-    assert stats.framing_path == 3, stats.as_dict()
+    assert stats.framing_path == 0, stats.as_dict()
 
 
 def test_uniform_disabled_gives_same_bytes(native, monkeypatch):
@@ -395,7 +408,7 @@ def test_uniform_disabled_gives_same_bytes(native, monkeypatch):
     a, sa = gpu_build(native, log, 11, 8)
     monkeypatch.setenv("SPARKEY_NO_UNIFORM", "1")
     b, sb = gpu_build(native, log, 11, 8)
-    assert sa.framing_path == 2 and sb.framing_path == 3 and a == b
+    assert sa.framing_path == 2 and sb.framing_path == 0 and a == b
 
 
 @pytest.mark.parametrize("region_cap", ["60000", "1"])
