@@ -251,6 +251,11 @@ def single_gpu(args, dev):
     assert stats.placement_path == wl["path"] and stats.framing_path in (0, 2, 3), stats.as_dict()
     assert wl["path"] != 0 or stats.num_entries == n, stats.as_dict()
 
+    if args.quick:  # (profiling runs: the timed builds only)
+        plan.close()
+        return {"value": n * args.steps / elapsed, "ms_per_step": ms_per_step,
+                "config": {"workload": wl["name"], "entries": n, "log_bytes": int(log_len), "parallelism": "single"},
+                "stage_ms": stage_ms, "roofline": None, "cpu_baseline": None, "version": sparkey.version()}
     # host-to-host rate (north_star): H2D of the log from pinned memory, the build, D2H of the .spi
     pinned = torch.from_numpy(log_np).pin_memory()
     host_out = torch.empty(out_len, dtype=torch.uint8).pin_memory()
@@ -408,6 +413,24 @@ def sharded(args, dev, world, rank):
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
     assert res.path == "sharded" and res.stats["num_entries"] == n_total, (res.path, res.stats)
+    identical = None
+    if args.check:  # the sharded .spi against one single-GPU build of the whole log (rank 0)
+        pieces = [None] * world
+        dist.all_gather_object(pieces, (res.out_offset, res.out.cpu().numpy().tobytes()))
+        if rank == 0:
+            full_log = synth.fixed_log(n_total, 16, 100, seed=args.seed, file_id=0x5EED0000)
+            d_full = torch.from_numpy(full_log).to(dev)
+            size = _native.index_size(full_log[:84].tobytes(), opts)
+            d_spi = torch.empty(size, dtype=torch.uint8, device=dev)
+            p1 = _native.Plan(dev.index, full_log.size, n_total)
+            p1.build(full_log[:84].tobytes(), d_full.data_ptr(), full_log.size, d_spi.data_ptr(), size, opts)
+            single = d_spi.cpu().numpy().tobytes()
+            p1.close()
+            del d_full, d_spi, full_log
+            got = bytearray(size)
+            for off, b in pieces:
+                got[off:off + len(b)] = b
+            identical = bytes(got) == single
     slot = 16
     cap = 1 | int(n_total * 1.3)
     ms_per_step = elapsed * 1000.0 / args.steps
@@ -424,7 +447,7 @@ def sharded(args, dev, world, rank):
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                      "algorithmic_bytes_per_launch": b_alg_per_gpu, "avg_launch_ms": ms_per_step},
         "phase_ms_rank0": {k: v / args.steps for k, v in phase.items()},
-        "entry_rounds": res.rounds, "spilled_slots": res.n_spill,
+        "entry_rounds": res.rounds, "spilled_slots": res.n_spill, "bit_identical_to_single_gpu": identical,
         "cpu_baseline": None,
         "gen_s": gen_s,
         "version": sparkey.version(),
@@ -440,9 +463,11 @@ def main():
     ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS),
                     help="c2 (the headline metric); c3 / c5 / churn are extra single-GPU measurements")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--quick", action="store_true", help="timed device builds only (profiling runs)")
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--backend", default="nccl", help="nccl (RCCL); gloo only to rehearse N > 1 ranks on one GPU")
     ap.add_argument("--sharded", action="store_true", help="the sharded build even at N = 1 (rehearsal)")
+    ap.add_argument("--check", action="store_true", help="sharded: compare the .spi with a single-GPU build")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))

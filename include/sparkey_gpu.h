@@ -142,7 +142,10 @@ int sparkey_get_batch(sparkey_plan* plan, const uint8_t* d_log, uint64_t log_len
  * the device steps of IndexHash.createNew split at the points where ranks exchange data.  The
  * host orchestrator (sparkey-java_amd/sparkey/sharded.py) calls them in this order
  * on every rank and runs the collectives in between.  Every pointer named d_* is device memory;
- * `stream` is a hipStream_t (NULL = the plan's own stream); every step synchronises it. */
+ * `stream` is a hipStream_t (NULL = the plan's own stream).  The steps named *_dev and
+ * sparkey_shard_bin_row only enqueue work: their results stay on the device, in the rows the
+ * collectives exchange, so a build makes three host round trips (after the framing, after the
+ * verification rows, after the final rows).  The other steps synchronise the stream. */
 typedef struct sparkey_shard_frame_result {
   int64_t exit;          /* first record start >= frame_end on the chain framed from `entry` */
   int64_t num_records;   /* records framed (PUT + DELETE) */
@@ -151,13 +154,6 @@ typedef struct sparkey_shard_frame_result {
   int32_t rc;            /* SPARKEY_E_* of an invalid record on this chain; final once the entry is verified */
   int32_t framing_path;  /* 0 speculative k_frame, 1 serial walker */
 } sparkey_shard_frame_result;
-
-typedef struct sparkey_shard_place_result {
-  uint64_t n_spill;       /* slots written past the rank's range (sent to their owners) */
-  uint64_t n_pairs;       /* equal-hash PUT pairs whose keys must be compared */
-  int32_t non_canonical;  /* the canonical layout cannot be proven here (too many equal slots/pairs) */
-  int32_t pad;
-} sparkey_shard_place_result;
 
 /* The rank holds global log bytes [buf_lo, buf_hi) at d_buf (buf_lo 16-byte aligned); file_len is
  * the whole log's length; log_header a host copy of its first 84 bytes. */
@@ -175,27 +171,56 @@ int sparkey_shard_find_entry(sparkey_plan* plan, uint64_t lo, uint64_t window, v
  * IndexHash.java:257-303) into the plan's entry slabs. */
 int sparkey_shard_frame(sparkey_plan* plan, int64_t entry, int64_t frame_end, void* stream,
                         sparkey_shard_frame_result* result, char* err, size_t err_len);
-/* Groups the framed (hash, address) entries (16 B each) by destination rank into d_send;
- * counts[r] = entries for rank r, in rank order. */
-int sparkey_shard_bin(sparkey_plan* plan, uint8_t* d_send, uint64_t send_cap, void* stream, uint64_t* counts,
-                      char* err, size_t err_len);
-/* Partitions the received entries by bucket; fun_out = {c, a} of the rank's slot-range carry
- * function f(x) = max(c, x + a). */
-int sparkey_shard_summarize(sparkey_plan* plan, const uint8_t* d_recv, uint64_t n_recv, void* stream,
-                            int64_t* fun_out, char* err, size_t err_len);
-/* Entries per coarse digit of this rank's last sparkey_shard_bin (256 values, host side). */
-int sparkey_shard_digit_counts(const sparkey_plan* plan, uint64_t* out256);
-/* sparkey_shard_summarize for an exchange buffer that holds, per source rank in rank order, that
- * rank's bin output for this rank's digits: digit_counts = the world x 256 matrix of every rank's
- * sparkey_shard_digit_counts (row = source rank).  The runs are partitioned in place (no first
- * radix pass over the received entries). */
-int sparkey_shard_summarize_grouped(sparkey_plan* plan, const uint8_t* d_recv, uint64_t n_recv,
-                                    const uint64_t* digit_counts, void* stream, int64_t* fun_out, char* err,
-                                    size_t err_len);
-/* Places the rank's entries given its carry-in into d_slots (the bytes of slot slot_lo onwards);
- * slots past the range go to d_spill as {slot, hash, address, 0} u64 quadruples. */
-int sparkey_shard_place(sparkey_plan* plan, int64_t carry_in, uint8_t* d_slots, uint8_t* d_spill, uint64_t spill_cap,
-                        void* stream, sparkey_shard_place_result* result, char* err, size_t err_len);
+/* Entries sparkey_shard_frame_bin_async provisions for [entry, frame_end): the size its send buffer
+ * needs (exact for uniform logs, else from the header's counts); negative on bad arguments. */
+int64_t sparkey_shard_frame_capacity(sparkey_plan* plan, int64_t entry, int64_t frame_end);
+/* sparkey_shard_frame's first attempt + sparkey_shard_bin_row, enqueued without waiting: the row's
+ * scalars come from the device status, and its retry flag (scalar 7) is set when the attempt does not
+ * hold (speculation failed, workspace too small, more entries than send_cap); the host then calls
+ * sparkey_shard_frame + sparkey_shard_bin_row for this range.  d_send NULL with one rank (the
+ * entries stay in the plan; send_cap still bounds them). */
+int sparkey_shard_frame_bin_async(sparkey_plan* plan, int64_t entry, int64_t frame_end, uint8_t* d_send,
+                                  uint64_t send_cap, int64_t* d_row, void* stream, char* err, size_t err_len);
+/* The rank's verification row (int64, 8 + world + 256 values) at d_row: the 8 frame scalars
+ * {entry, frame_end, exit, num_records, num_deletes, rc, err_pos, retry} as given, then the entries bound
+ * for each destination rank, then the entries per coarse digit.  With n > 0 (n = the framed
+ * entries) it also groups the framed (hash, address) entries (16 B each) by destination rank into
+ * d_send, in rank order and within a rank in coarse-digit order; with n = 0 the counts are zero.
+ * With one rank d_send may be NULL: the entries stay in the plan for sparkey_shard_summarize_dev. */
+int sparkey_shard_bin_row(sparkey_plan* plan, uint8_t* d_send, uint64_t send_cap, uint64_t n, const int64_t* scalars,
+                          int64_t* d_row, void* stream, char* err, size_t err_len);
+/* Partitions the received entries by bucket and leaves the rank's slot-range carry function
+ * f(x) = max(c, x + a) at d_fun = {c, a}.  d_digits = &rows[0][8 + world] of the gathered
+ * verification rows (stride int64 apart): the exchange buffer then holds, per source rank in rank
+ * order, that rank's bin output for this rank's digits, partitioned in place (no first radix pass);
+ * NULL = ungrouped entries.  d_recv = NULL (one rank): the entries sparkey_shard_bin_row kept.
+ * fixed_regions = 0 redoes a step whose fixed bucket regions overflowed
+ * (the flags row's "aborted"). */
+int sparkey_shard_summarize_dev(sparkey_plan* plan, const uint8_t* d_recv, uint64_t n_recv, const int64_t* d_digits,
+                                int32_t stride, int32_t fixed_regions, int64_t* d_fun, void* stream, char* err,
+                                size_t err_len);
+/* Places the rank's entries into d_slots (the bytes of slot slot_lo onwards), its carry-in composed
+ * from every rank's carry function d_funs (world x {c, a}); slots past the range go to d_spill as
+ * {slot, hash, address, 0} u64 quadruples.  d_flags (int64, 4 + 4 * inline_cap) = {spilled slots,
+ * equal-hash pairs, non-canonical (too many equal slots or pairs to prove the canonical layout
+ * here), aborted (redo sparkey_shard_summarize_dev with fixed_regions = 0)} and the first
+ * inline_cap spilled slots. */
+int sparkey_shard_place_dev(sparkey_plan* plan, const int64_t* d_funs, uint8_t* d_slots, uint8_t* d_spill,
+                            uint64_t spill_cap, int64_t* d_flags, int32_t inline_cap, void* stream, char* err,
+                            size_t err_len);
+/* Writes the inline spilled slots of every rank's flags row (d_rows: world rows, stride int64 apart)
+ * that fall in this rank's range (a rank that spilled more than inline_cap is left to
+ * sparkey_shard_apply_spill), then calculateMaxDisplacement over the rank's slots with no slot
+ * before the range (IndexHash.java:195-245): d_out (int64 x 12) = {this rank's 4 flags, first slot
+ * hash, address, last slot hash, address, non-empty, max displacement, hash collisions, total
+ * displacement}. */
+int sparkey_shard_finish_dev(sparkey_plan* plan, const int64_t* d_rows, int32_t stride, int32_t inline_cap,
+                             int64_t* d_out, void* stream, char* err, size_t err_len);
+/* Rank 0: the 112-byte .spi header (IndexHeader.java:125-155) at d_header from every rank's
+ * sparkey_shard_finish_dev row (d_fin: world rows, stride int64 apart), adding the comparisons
+ * calculateMaxDisplacement makes across range boundaries and its wrap quirk (IndexHash.java:195-245). */
+int sparkey_shard_header_dev(sparkey_plan* plan, const int64_t* d_fin, int32_t stride, int64_t num_entries,
+                             uint8_t* d_header, void* stream, char* err, size_t err_len);
 /* The equal-hash pairs of the last placement: 2 * n_pairs addresses. */
 int sparkey_shard_pairs(sparkey_plan* plan, uint64_t* h_addrs, uint64_t n_pairs, char* err, size_t err_len);
 int32_t sparkey_shard_key_record_size(const sparkey_plan* plan);

@@ -166,7 +166,7 @@ __global__ void k_carry(BuildParams P) {
   if (build_aborted(P)) return;
   const uint64_t b = P.b_lo + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const MaxPlus tot = *P.bfun_total;
-  int64_t x0 = P.carry_in;
+  int64_t x0 = P.carry_in_ptr ? *P.carry_in_ptr : P.carry_in;
   if (!P.sharded) {
     if (tot.a >= 0) {  // N >= capacity: no empty slot, the canonical layout does not apply
       if (b == 0) atomicOr(&P.st->full, 1u);

@@ -56,6 +56,20 @@ struct alignas(16) SpillEntry {
   uint64_t pad;
 };
 
+// sharded build rows (sharded.py): the frame's scalars {entry, frame end, exit, records, deletes, rc,
+// error position, retry (a speculative attempt that must be redone synchronously)}, and the placement flags {spilled, pairs, non-canonical, aborted} before the
+// inline spilled slots
+constexpr int kShardScalars = 8;
+constexpr int kShardFlags = 4;
+struct ShardScalars {
+  int64_t v[kShardScalars];
+};
+
+constexpr int kIndexHeaderBytes = 112;
+struct IndexHeaderBytes {  // the .spi header template (IndexHeader.asBytes), by value into a kernel
+  uint8_t b[kIndexHeaderBytes];
+};
+
 constexpr unsigned kSpecRegionFull = 8u;  // Status.spec_fail: a digit region of ent3 overflowed
 
 struct StatPart {
@@ -206,6 +220,8 @@ struct BuildParams {
   uint64_t b_lo, b_hi;
   uint64_t slot_lo, slot_hi;
   int64_t carry_in;
+  int32_t abort_on_fail;        // the bin after a speculative framing attempt: skip it when the attempt failed
+  const int64_t* carry_in_ptr;  // non-null: the carry-in is read from device memory (k_shard_carry)
   uint64_t prev_hash;
   SpillEntry* spill;
   uint64_t spill_cap;
@@ -283,10 +299,26 @@ void launch_partition_quiet(const BuildParams& P, hipStream_t s);
 // sharded builds (shard_kernels.hip)
 void launch_dest_counts(const BuildParams& P, hipStream_t s, int world, uint32_t nd, uint64_t* d_out);
 void launch_apply_spill(const BuildParams& P, hipStream_t s, const SpillEntry* in, uint64_t n);
+void launch_region_send(const BuildParams& P, hipStream_t s, int world, uint32_t nd, Entry* send, uint64_t* d_out,
+                        uint64_t send_cap);
 void launch_digit_starts(const BuildParams& P, hipStream_t s, uint64_t* d_out);
 void launch_fetch_keys(const BuildParams& P, hipStream_t s, const uint64_t* addrs, uint64_t n, uint8_t* rec,
                        uint32_t rec_size);
 void launch_compare_keys(const BuildParams& P, hipStream_t s, const uint8_t* rec, uint64_t npairs, uint32_t rec_size);
 void launch_find_entry(const BuildParams& P, hipStream_t s, int64_t lo, int64_t cand_end, int64_t target, int64_t* d_out);
+void launch_shard_row(hipStream_t s, const ShardScalars& sc, const uint64_t* off, int world, int have, int64_t* row);
+void launch_shard_row_async(hipStream_t s, const ShardScalars& sc, const Status* st, int path, uint32_t slab_cap,
+                            uint64_t max_records, uint64_t send_cap, int64_t data_end, const uint64_t* off, int world,
+                            int64_t* row);
+void launch_p2_table(hipStream_t s, const int64_t* dig, int stride, int G, uint32_t d0, uint32_t nk, uint64_t* tab);
+void launch_shard_carry(hipStream_t s, const int64_t* funs, int world, int rank, int64_t* out);
+void launch_shard_flags(const BuildParams& P, hipStream_t s, int64_t* flags, int inline_cap);
+void launch_apply_spill_rows(const BuildParams& P, hipStream_t s, const int64_t* rows, int world, int stride,
+                             int inline_cap);
+void launch_shard_summary_row(const BuildParams& P, hipStream_t s, const int64_t* flags, int64_t* out);
+void launch_status_reset(hipStream_t s, Status* st, uint64_t n_records);
+void launch_p2_table_regions(hipStream_t s, const uint32_t* fill, uint64_t rc, uint32_t d0, uint32_t nk, uint64_t* tab);
+void launch_shard_header(hipStream_t s, const int64_t* fin, int stride, int world, const IndexHeaderBytes& tmpl,
+                         int64_t n_total, uint8_t* out);
 
 }  // namespace sk

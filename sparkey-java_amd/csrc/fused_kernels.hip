@@ -994,8 +994,19 @@ __global__ __launch_bounds__(kPart2Block) void k_part2s(BuildParams P) {
   extern __shared__ __attribute__((aligned(16))) uint32_t dyn[];  // h[bpp * 512] | btot[bpp] | boffl[bpp]
   if (build_aborted(P)) return;
   const uint32_t dpart = blockIdx.x;
+  // input: the digit's run of the pass-1 output, or (sharded receive) its run in every source
+  // rank's block of the exchange buffer; dense output (not p2_fixed) from `lo` on
   uint64_t lo, hi;
-  if (P.p1_region) {
+  const uint64_t* seg = nullptr;  // nseg (begin, end) runs of ent3
+  uint32_t nseg = 1;
+  if (P.p2_seg) {
+    if (dpart < P.p2_d0 || dpart >= P.p2_d0 + P.p2_nd) return;
+    const uint32_t k = dpart - P.p2_d0;
+    lo = P.p2_out[k];
+    hi = P.p2_out[k + 1];
+    seg = P.p2_seg + 2ull * k * P.p2_nsrc;
+    nseg = P.p2_nsrc;
+  } else if (P.p1_region) {
     lo = (uint64_t)dpart * P.p1_region;
     hi = lo + min((uint64_t)P.p1_fill[dpart], P.p1_region);
   } else {
@@ -1015,27 +1026,30 @@ __global__ __launch_bounds__(kPart2Block) void k_part2s(BuildParams P) {
   for (uint32_t i = tid; i < nbins * 512 + 2 * nbins; i += kPart2Block) dyn[i] = 0;
   __syncthreads();
   bool ovf = false;
-  for (uint64_t i0 = lo; i0 < hi; i0 += (uint64_t)kPart2Block * kPart2Items) {
-    Entry v[kPart2Items];
+  for (uint32_t q = 0; q < nseg; q++) {
+    const uint64_t ra = seg ? seg[2 * q] : lo, rz = seg ? seg[2 * q + 1] : hi;
+    for (uint64_t i0 = ra; i0 < rz; i0 += (uint64_t)kPart2Block * kPart2Items) {
+      Entry v[kPart2Items];
 #pragma unroll
-    for (int k = 0; k < kPart2Items; k++) {
-      const uint64_t i = i0 + (uint64_t)k * kPart2Block + tid;
-      if (i < hi) {
-        if (fixed) v[k] = P.ent3[i];
-        else v[k].hash = P.ent3[i].hash;
+      for (int k = 0; k < kPart2Items; k++) {
+        const uint64_t i = i0 + (uint64_t)k * kPart2Block + tid;
+        if (i < rz) {
+          if (fixed) v[k] = P.ent3[i];
+          else v[k].hash = P.ent3[i].hash;
+        }
       }
-    }
 #pragma unroll
-    for (int k = 0; k < kPart2Items; k++) {
-      const uint64_t i = i0 + (uint64_t)k * kPart2Block + tid;
-      if (i >= hi) continue;
-      const uint64_t slot = fast_mod(v[k].hash, P.mod);
-      const uint32_t b = (uint32_t)((slot >> kBucketShift) - b0), sl = (uint32_t)(slot & (kBucket - 1));
-      atomicAdd(&h[(b << 9) + (sl >> 1)], 1u << ((sl & 1) * 16));
-      const uint32_t r = atomicAdd(&btot[b], 1u);
-      if (fixed) {
-        if (r < kPlaceLdsMax) P.ent2[(b0 + b) * (uint64_t)kPlaceLdsMax + r] = v[k];
-        else ovf = true;
+      for (int k = 0; k < kPart2Items; k++) {
+        const uint64_t i = i0 + (uint64_t)k * kPart2Block + tid;
+        if (i >= rz) continue;
+        const uint64_t slot = fast_mod(v[k].hash, P.mod);
+        const uint32_t b = (uint32_t)((slot >> kBucketShift) - b0), sl = (uint32_t)(slot & (kBucket - 1));
+        atomicAdd(&h[(b << 9) + (sl >> 1)], 1u << ((sl & 1) * 16));
+        const uint32_t r = atomicAdd(&btot[b], 1u);
+        if (fixed) {  // (regions from the range's first bucket: a sharded rank holds its range only)
+          if (r < kPlaceLdsMax) P.ent2[(b0 + b - P.b_lo) * (uint64_t)kPlaceLdsMax + r] = v[k];
+          else ovf = true;
+        }
       }
     }
   }
@@ -1058,7 +1072,7 @@ __global__ __launch_bounds__(kPart2Block) void k_part2s(BuildParams P) {
       boffl[lane] = incl - c;  // then the bucket's cursor
       const uint64_t bucket = b0 + lane;
       if (bucket < P.nbuckets) {
-        P.boff[bucket] = fixed ? bucket * (uint64_t)kPlaceLdsMax : lo + incl - c;
+        P.boff[bucket] = fixed ? (bucket - P.b_lo) * (uint64_t)kPlaceLdsMax : lo + incl - c;
         P.bcount[bucket] = c;
       }
     }
@@ -1103,17 +1117,20 @@ __global__ __launch_bounds__(kPart2Block) void k_part2s(BuildParams P) {
   }
   if (fixed) return;
   __syncthreads();
-  for (uint64_t i0 = lo; i0 < hi; i0 += (uint64_t)kPart2Block * kPart2Items) {
-    Entry v[kPart2Items];
+  for (uint32_t q = 0; q < nseg; q++) {
+    const uint64_t ra = seg ? seg[2 * q] : lo, rz = seg ? seg[2 * q + 1] : hi;
+    for (uint64_t i0 = ra; i0 < rz; i0 += (uint64_t)kPart2Block * kPart2Items) {
+      Entry v[kPart2Items];
 #pragma unroll
-    for (int k = 0; k < kPart2Items; k++) {
-      const uint64_t i = i0 + (uint64_t)k * kPart2Block + tid;
-      if (i < hi) v[k] = P.ent3[i];
-    }
+      for (int k = 0; k < kPart2Items; k++) {
+        const uint64_t i = i0 + (uint64_t)k * kPart2Block + tid;
+        if (i < rz) v[k] = P.ent3[i];
+      }
 #pragma unroll
-    for (int k = 0; k < kPart2Items; k++) {
-      const uint64_t i = i0 + (uint64_t)k * kPart2Block + tid;
-      if (i < hi) P.ent2[lo + atomicAdd(&boffl[bucket_of(P, v[k].hash) - b0], 1u)] = v[k];
+      for (int k = 0; k < kPart2Items; k++) {
+        const uint64_t i = i0 + (uint64_t)k * kPart2Block + tid;
+        if (i < rz) P.ent2[lo + atomicAdd(&boffl[bucket_of(P, v[k].hash) - b0], 1u)] = v[k];
+      }
     }
   }
 }
@@ -1450,7 +1467,10 @@ void launch_partition_quiet(const BuildParams& P, hipStream_t s) {
 }
 
 void launch_partition2(const BuildParams& P, hipStream_t s, StageTimer* tm) {
-  hipLaunchKernelGGL(k_part2, dim3(256), dim3(kPart2Block), (size_t)(2u * P.bpp) * sizeof(uint32_t), s, P);
+  if (P.p2_sorted)
+    hipLaunchKernelGGL(k_part2s, dim3(256), dim3(kPart2Block), (size_t)(514u * P.bpp) * sizeof(uint32_t), s, P);
+  else
+    hipLaunchKernelGGL(k_part2, dim3(256), dim3(kPart2Block), (size_t)(2u * P.bpp) * sizeof(uint32_t), s, P);
   tm->mark("partition", s);
 }
 

@@ -17,7 +17,9 @@ namespace sk {
 // skipped (its offsets would run past the buffers) and the host redoes the build with more room.
 __device__ __forceinline__ bool build_aborted(const BuildParams& P) {
   // (p2_overflow: the fixed bucket regions did not hold a bucket; the host redoes the build)
-  return P.st->overflow != 0 || P.st->n_records > P.max_records || P.st->p2_overflow != 0;
+  // (abort_on_fail: a sharded bin right after a speculative framing attempt that did not hold)
+  return P.st->overflow != 0 || P.st->n_records > P.max_records || P.st->p2_overflow != 0 ||
+         (P.abort_on_fail && (P.st->spec_fail != 0 || P.st->err != ~0ull));
 }
 
 __device__ __forceinline__ void set_error(Status* st, int64_t pos, int code) {

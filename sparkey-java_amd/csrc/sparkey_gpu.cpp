@@ -259,7 +259,8 @@ struct ShardState {
   uint64_t n_local = 0, n_recv = 0;
   BuildParams P;        // placement over the rank's slot range
   BuildParams P_frame;  // the rank's framing (entries in slabs)
-  uint64_t digit_count[256] = {0};  // the last bin's entries per coarse digit
+  int local = 0;        // world 1, no send buffer: the binned entries stay in ent3 (1 digit regions, 2 dense)
+  IndexHeaderBytes tmpl;  // the .spi header template
 };
 
 struct sparkey_plan {
@@ -1568,6 +1569,8 @@ int sparkey_shard_begin(sparkey_plan* pl, const uint8_t* log_header, uint64_t fi
   sh.P.st = pl->d_status;
   sh.P.sharded = 1;
   shard_range(sh.P, rank, world, &sh.P.b_lo, &sh.P.b_hi, &sh.P.slot_lo, &sh.P.slot_hi);
+  index_header_template(sh.lh, sh.ip, opts->hash_seed, sh.tmpl.b);
+  sh.local = 0;
   HIP_TRY(grow(&pl->small, pl->c_small, 512));
   sh.active = true;
   return SPARKEY_OK;
@@ -1613,6 +1616,102 @@ int sparkey_shard_find_entry(sparkey_plan* pl, uint64_t lo, uint64_t window, voi
   return SPARKEY_OK;
 }
 
+// One rank's framing set-up: parameters, the framing path and the first geometry (shared by the
+// synchronous sparkey_shard_frame and the speculative sparkey_shard_frame_bin_async).
+struct ShardFrameSetup {
+  BuildParams P;
+  bool fused = false, use_frame2 = false, use_regions = true;
+  int framing_path = 1;
+  uint64_t nrec = 0;
+  FrameGeom geom0, geom2;
+  uint32_t slab_cap = 0;
+  int slab_path = 0;
+};
+
+static uint32_t shard_slab_for(const FrameGeom& g, uint64_t nrec) {
+  const uint64_t nw = std::max<uint64_t>(1, g.nchunks ? (g.nchunks + g.w - 1) / g.w : 0);
+  return (uint32_t)std::min<uint64_t>(kPartTile, std::max<uint64_t>(64, 2 * ((nrec + nw - 1) / nw) + 32));
+}
+
+static int shard_frame_setup(sparkey_plan* pl, int64_t entry, int64_t frame_end, ShardFrameSetup* F, char* err,
+                             size_t err_len) {
+  ShardState& sh = pl->shard;
+  const int64_t data_end = std::max<int64_t>(sh.lh.data_end, kLogHeaderSize);
+  BuildParams& P = F->P;
+  int rc = setup_params(sh.lh, sh.ip, sh.opts, sh.log, sh.buf_hi, entry, frame_end, &P, err, err_len);
+  if (rc) return rc;
+  P.st = pl->d_status;
+  P.sharded = 1;
+  P.b_lo = sh.P.b_lo; P.b_hi = sh.P.b_hi; P.slot_lo = sh.P.slot_lo; P.slot_hi = sh.P.slot_hi;
+  F->fused = P.max_rec_len <= 4096;
+  const double frac = (double)(frame_end - entry) / (double)std::max<int64_t>(1, data_end - kLogHeaderSize);
+  F->nrec = (uint64_t)((double)(std::max<int64_t>(0, sh.lh.num_puts) + std::max<int64_t>(0, sh.lh.num_deletes)) *
+                       frac * 1.05) + 4096;
+  F->geom0 = get_geom(P);
+  F->geom2 = frame2_geometry(P, entry, frame_end);
+  F->use_frame2 = F->fused && getenv("SPARKEY_FRAME2") != nullptr;
+  {
+    const int64_t nr = std::max<int64_t>(0, sh.lh.num_puts) + std::max<int64_t>(0, sh.lh.num_deletes);
+    const int64_t by = std::max<int64_t>(0, sh.lh.put_size) + std::max<int64_t>(0, sh.lh.delete_size);
+    if ((nr > 0 && by < 24 * nr) || sh.lh.num_deletes != 0) F->use_frame2 = false;
+  }
+  F->framing_path = F->fused ? (F->use_frame2 ? 3 : 0) : 1;
+  const int64_t R = uniform_record_size(sh.lh);
+  if (R && (entry - kLogHeaderSize) % R == 0) {  // a record start of a uniform log: frame by stride
+    F->framing_path = 2;
+    P.uni_n = (uint64_t)((frame_end - entry + R - 1) / R);
+    P.uni_rec = R;
+    F->nrec = P.uni_n;
+  }
+  F->slab_cap = shard_slab_for(F->framing_path == 3 ? F->geom2 : F->geom0, F->nrec);
+  F->slab_path = F->framing_path;
+  F->use_regions = getenv("SPARKEY_NO_REGIONS") == nullptr;
+  return SPARKEY_OK;
+}
+
+// Launches one framing attempt of the set-up (status reset first); no synchronisation.
+static int shard_frame_launch(sparkey_plan* pl, ShardFrameSetup* F, hipStream_t s, char* err, size_t err_len) {
+  BuildParams& P = F->P;
+  set_geom(P, F->framing_path == 3 ? F->geom2 : F->geom0);
+  if ((F->framing_path == 0 || F->framing_path == 3) && F->framing_path != F->slab_path) {
+    F->slab_cap = shard_slab_for(F->framing_path == 3 ? F->geom2 : F->geom0, F->nrec);
+    F->slab_path = F->framing_path;
+  }
+  int rc = reserve_for_framing(pl, P, F->framing_path, F->nrec, F->slab_cap, err, err_len);
+  if (rc) return rc;
+  launch_status_reset(s, pl->d_status, 0);
+  // uniform framing also does the bin's partition pass: entries into 256 coarse-digit regions of
+  // ent3 (the bin then only packs them), as on one GPU
+  P.p1_region = 0;
+  if (F->framing_path == 2 && F->use_regions && P.slab_cap == (uint32_t)kPartTile && P.part_group == 1) {
+    const double expect = (double)F->nrec * (double)P.bpp * (double)kBucket / (double)P.cap;
+    const uint64_t rc_cap = ((uint64_t)(expect + 8.0 * std::sqrt(expect) + 1024.0) + 63) & ~63ull;
+    HIP_TRY(grow(&pl->ent3, pl->c_ent3, 256 * rc_cap));
+    HIP_TRY(grow(&pl->p1_fill, pl->c_p1_fill, 256));
+    HIP_TRY(hipMemsetAsync(pl->p1_fill, 0, 256 * sizeof(uint32_t), s));
+    P.ent3 = pl->ent3;
+    P.p1_fill = pl->p1_fill;
+    P.p1_region = rc_cap;
+  }
+  return launch_framing(pl, P, F->framing_path, s, err, err_len);
+}
+
+static int shard_frame_args(sparkey_plan* pl, int64_t entry, int64_t* frame_end, char* err, size_t err_len) {
+  ShardState& sh = pl->shard;
+  const int64_t data_end = std::max<int64_t>(sh.lh.data_end, kLogHeaderSize);
+  *frame_end = std::min<int64_t>(*frame_end, data_end);
+  if (entry < kLogHeaderSize || entry > data_end) {
+    set_err(err, err_len, "shard entry outside the log data");
+    return SPARKEY_E_ARG;
+  }
+  if (entry < *frame_end &&
+      (entry < (int64_t)sh.buf_lo || ((uint64_t)*frame_end > sh.buf_hi && sh.buf_hi < (uint64_t)data_end))) {
+    set_err(err, err_len, "shard frame range outside the shard buffer");
+    return SPARKEY_E_ARG;
+  }
+  return SPARKEY_OK;
+}
+
 int sparkey_shard_frame(sparkey_plan* pl, int64_t entry, int64_t frame_end, void* stream,
                         sparkey_shard_frame_result* res, char* err, size_t err_len) {
   int rc = shard_check(pl, err, err_len);
@@ -1620,92 +1719,50 @@ int sparkey_shard_frame(sparkey_plan* pl, int64_t entry, int64_t frame_end, void
   ShardState& sh = pl->shard;
   hipStream_t s = stream ? (hipStream_t)stream : pl->own_stream;
   const int64_t data_end = std::max<int64_t>(sh.lh.data_end, kLogHeaderSize);
-  frame_end = std::min<int64_t>(frame_end, data_end);
   memset(res, 0, sizeof(*res));
   res->exit = entry;
   sh.n_local = 0;
-  if (entry < kLogHeaderSize || entry > data_end) {
-    set_err(err, err_len, "shard entry outside the log data");
-    return SPARKEY_E_ARG;
-  }
-  if (entry >= frame_end) return SPARKEY_OK;  // owns no record
-  if (entry < (int64_t)sh.buf_lo || ((uint64_t)frame_end > sh.buf_hi && sh.buf_hi < (uint64_t)data_end)) {
-    set_err(err, err_len, "shard frame range outside the shard buffer");
-    return SPARKEY_E_ARG;
-  }
-  BuildParams P;
-  rc = setup_params(sh.lh, sh.ip, sh.opts, sh.log, sh.buf_hi, entry, frame_end, &P, err, err_len);
+  rc = shard_frame_args(pl, entry, &frame_end, err, err_len);
   if (rc) return rc;
-  P.st = pl->d_status;
-  P.sharded = 1;
-  P.b_lo = sh.P.b_lo; P.b_hi = sh.P.b_hi; P.slot_lo = sh.P.slot_lo; P.slot_hi = sh.P.slot_hi;
-  const bool fused = P.max_rec_len <= 4096;
-  const double frac = (double)(frame_end - entry) / (double)std::max<int64_t>(1, data_end - kLogHeaderSize);
-  uint64_t nrec = (uint64_t)((double)(std::max<int64_t>(0, sh.lh.num_puts) + std::max<int64_t>(0, sh.lh.num_deletes)) *
-                             frac * 1.05) + 4096;
-  const FrameGeom geom0 = get_geom(P);
-  const FrameGeom geom2 = frame2_geometry(P, entry, frame_end);
-  bool use_frame2 = fused && getenv("SPARKEY_FRAME2") != nullptr;
-  {
-    const int64_t nr = std::max<int64_t>(0, sh.lh.num_puts) + std::max<int64_t>(0, sh.lh.num_deletes);
-    const int64_t by = std::max<int64_t>(0, sh.lh.put_size) + std::max<int64_t>(0, sh.lh.delete_size);
-    if ((nr > 0 && by < 24 * nr) || sh.lh.num_deletes != 0) use_frame2 = false;
-  }
-  int framing_path = fused ? (use_frame2 ? 3 : 0) : 1;
-  const int64_t R = uniform_record_size(sh.lh);
-  if (R && (entry - kLogHeaderSize) % R == 0) {  // a record start of a uniform log: frame by stride
-    framing_path = 2;
-    P.uni_n = (uint64_t)((frame_end - entry + R - 1) / R);
-    P.uni_rec = R;
-    nrec = P.uni_n;
-  }
-  auto slab_for = [&](const FrameGeom& g) -> uint32_t {
-    const uint64_t nw = std::max<uint64_t>(1, g.nchunks ? (g.nchunks + g.w - 1) / g.w : 0);
-    return (uint32_t)std::min<uint64_t>(kPartTile, std::max<uint64_t>(64, 2 * ((nrec + nw - 1) / nw) + 32));
-  };
-  uint32_t slab_cap = slab_for(framing_path == 3 ? geom2 : geom0);
-  int slab_path = framing_path;
+  if (entry >= frame_end) return SPARKEY_OK;  // owns no record
+  ShardFrameSetup F;
+  rc = shard_frame_setup(pl, entry, frame_end, &F, err, err_len);
+  if (rc) return rc;
+  BuildParams& P = F.P;
   Status& st = *pl->h_status;
   for (int attempt = 0; attempt < 6; attempt++) {
-    set_geom(P, framing_path == 3 ? geom2 : geom0);
-    if ((framing_path == 0 || framing_path == 3) && framing_path != slab_path) {
-      slab_cap = slab_for(framing_path == 3 ? geom2 : geom0);
-      slab_path = framing_path;
-    }
-    rc = reserve_for_framing(pl, P, framing_path, nrec, slab_cap, err, err_len);
-    if (rc) return rc;
-    Status init;
-    memset(&init, 0, sizeof(init));
-    init.err = ~0ull;
-    init.exit = -1;
-    HIP_TRY(hipMemcpyAsync(pl->d_status, &init, sizeof(Status), hipMemcpyHostToDevice, s));
-    rc = launch_framing(pl, P, framing_path, s, err, err_len);
+    rc = shard_frame_launch(pl, &F, s, err, err_len);
     if (rc) return rc;
     rc = shard_sync_status(pl, s, err, err_len);
     if (rc) return rc;
-    if ((framing_path == 0 || framing_path == 3) && st.max_wave_count > slab_cap) {
-      slab_cap = (uint32_t)std::min<uint64_t>(kPartTile, ((uint64_t)st.max_wave_count + 63) & ~63ull);
+    const int path = F.framing_path;
+    if ((path == 0 || path == 3) && st.max_wave_count > F.slab_cap) {
+      F.slab_cap = (uint32_t)std::min<uint64_t>(kPartTile, ((uint64_t)st.max_wave_count + 63) & ~63ull);
       continue;
     }
     if (st.overflow || st.n_records > P.max_records) {
-      nrec = std::max<uint64_t>(st.n_records, nrec * 2 + 1);
+      F.nrec = std::max<uint64_t>(st.n_records, F.nrec * 2 + 1);
       continue;
     }
-    if (framing_path == 3 && (st.spec_fail & 16u) && st.err == ~0ull) {  // a segment's record list overflowed
-      framing_path = 0;
+    if (path == 3 && (st.spec_fail & 16u) && st.err == ~0ull) {  // a segment's record list overflowed
+      F.framing_path = 0;
       continue;
     }
-    if ((framing_path == 0 || framing_path == 3) && (st.spec_fail || st.err != ~0ull)) {
-      framing_path = 1;
+    if ((path == 0 || path == 3) && (st.spec_fail || st.err != ~0ull)) {
+      F.framing_path = 1;
       continue;
     }
-    if (framing_path == 2 && st.spec_fail) {  // not the uniform log its header describes
-      framing_path = fused ? (use_frame2 ? 3 : 0) : 1;
+    if (path == 2 && (st.spec_fail & kSpecRegionFull) && !(st.spec_fail & ~kSpecRegionFull)) {
+      F.use_regions = false;  // a digit region filled up: slabs, and the bin's own pass
+      continue;
+    }
+    if (path == 2 && st.spec_fail) {  // not the uniform log its header describes
+      F.framing_path = F.fused ? (F.use_frame2 ? 3 : 0) : 1;
       continue;
     }
     break;
   }
-  res->framing_path = framing_path;
+  res->framing_path = F.framing_path;
   if (st.err != ~0ull) {  // an invalid record on this chain: final only once the entry is verified
     res->rc = -(int)(st.err & 0xff);
     res->err_pos = (int64_t)(st.err >> 8);
@@ -1723,71 +1780,155 @@ int sparkey_shard_frame(sparkey_plan* pl, int64_t entry, int64_t frame_end, void
   return SPARKEY_OK;
 }
 
-int sparkey_shard_bin(sparkey_plan* pl, uint8_t* d_send, uint64_t send_cap, void* stream, uint64_t* counts,
-                      char* err, size_t err_len) {
+int64_t sparkey_shard_frame_capacity(sparkey_plan* pl, int64_t entry, int64_t frame_end) {
+  char err[8];
+  if (shard_check(pl, err, sizeof(err))) return SPARKEY_E_ARG;
+  if (shard_frame_args(pl, entry, &frame_end, err, sizeof(err))) return SPARKEY_E_ARG;
+  if (entry >= frame_end) return 0;
+  ShardFrameSetup F;
+  if (shard_frame_setup(pl, entry, frame_end, &F, err, sizeof(err))) return SPARKEY_E_ARG;
+  return (int64_t)F.nrec;
+}
+
+// Frames [entry, frame_end) with the first attempt sparkey_shard_frame would make, bins the entries
+// and writes the verification row, all without waiting: the row's retry flag says when the attempt
+// needs sparkey_shard_frame's retries (then nothing else in the row is final).
+int sparkey_shard_frame_bin_async(sparkey_plan* pl, int64_t entry, int64_t frame_end, uint8_t* d_send,
+                                  uint64_t send_cap, int64_t* d_row, void* stream, char* err, size_t err_len) {
   int rc = shard_check(pl, err, err_len);
   if (rc) return rc;
   ShardState& sh = pl->shard;
   hipStream_t s = stream ? (hipStream_t)stream : pl->own_stream;
-  for (int r = 0; r < sh.world; r++) counts[r] = 0;
-  if (sh.n_local == 0) return SPARKEY_OK;
-  if (send_cap < sh.n_local || ((uintptr_t)d_send & 15)) {
-    set_err(err, err_len, "send buffer too small or misaligned: need " + std::to_string(sh.n_local) + " entries");
+  const int64_t data_end = std::max<int64_t>(sh.lh.data_end, kLogHeaderSize);
+  const int64_t fe_in = frame_end;
+  sh.n_local = 0;
+  sh.local = 0;
+  if (!d_row || ((uintptr_t)d_row & 7) || ((uintptr_t)d_send & 15) || (!d_send && sh.world != 1)) {
+    set_err(err, err_len, "bad row or send buffer");
+    return SPARKEY_E_ARG;
+  }
+  rc = shard_frame_args(pl, entry, &frame_end, err, err_len);
+  if (rc) return rc;
+  ShardScalars sc;
+  for (int i = 0; i < kShardScalars; i++) sc.v[i] = 0;
+  sc.v[0] = entry;
+  sc.v[1] = fe_in;
+  sc.v[2] = entry;
+  if (entry >= frame_end) {  // owns no record
+    launch_shard_row(s, sc, (const uint64_t*)pl->small, sh.world, 0, d_row);
+    HIP_TRY(hipGetLastError());
+    return SPARKEY_OK;
+  }
+  ShardFrameSetup F;
+  rc = shard_frame_setup(pl, entry, frame_end, &F, err, err_len);
+  if (rc) return rc;
+  rc = shard_frame_launch(pl, &F, s, err, err_len);
+  if (rc) return rc;
+  BuildParams P = F.P;
+  sh.P_frame = P;
+  P.abort_on_fail = 1;  // the bin skips an attempt that failed (its counts are not used)
+  if (P.p1_region) {
+    launch_region_send(P, s, sh.world, (uint32_t)used_digits(P), reinterpret_cast<Entry*>(d_send),
+                       (uint64_t*)pl->small, send_cap);
+    if (!d_send) sh.local = 1;
+  } else {
+    if (!d_send) {  // (the framing does not use ent3 here: growing it cannot disturb it)
+      HIP_TRY(grow(&pl->ent3, pl->c_ent3, std::max<uint64_t>(F.nrec, 1)));
+      d_send = reinterpret_cast<uint8_t*>(pl->ent3);
+      send_cap = std::min<uint64_t>(send_cap, pl->c_ent3);  // (send_cap still bounds the entries taken)
+      sh.local = 2;
+    }
+    P.ent3 = reinterpret_cast<Entry*>(d_send);
+    P.max_records = send_cap;
+    launch_partition1(P, s);
+    launch_dest_counts(P, s, sh.world, (uint32_t)used_digits(P), (uint64_t*)pl->small);
+    launch_digit_starts(P, s, (uint64_t*)pl->small + 64);
+  }
+  launch_shard_row_async(s, sc, pl->d_status, F.framing_path, F.slab_cap, F.P.max_records, send_cap, data_end,
+                         (const uint64_t*)pl->small, sh.world, d_row);
+  HIP_TRY(hipGetLastError());
+  return SPARKEY_OK;
+}
+
+int sparkey_shard_bin_row(sparkey_plan* pl, uint8_t* d_send, uint64_t send_cap, uint64_t n, const int64_t* scalars,
+                          int64_t* d_row, void* stream, char* err, size_t err_len) {
+  int rc = shard_check(pl, err, err_len);
+  if (rc) return rc;
+  ShardState& sh = pl->shard;
+  hipStream_t s = stream ? (hipStream_t)stream : pl->own_stream;
+  if (!scalars || !d_row || ((uintptr_t)d_row & 7)) {
+    set_err(err, err_len, "bad row arguments");
+    return SPARKEY_E_ARG;
+  }
+  if (!d_send && n && sh.world != 1) {
+    set_err(err, err_len, "a send buffer is needed with more than one rank");
+    return SPARKEY_E_ARG;
+  }
+  if (n && (n != sh.n_local || (d_send && (send_cap < n || ((uintptr_t)d_send & 15))))) {
+    set_err(err, err_len, "send buffer too small or misaligned, or not the framed entries: need " +
+                              std::to_string(sh.n_local) + " entries");
     return SPARKEY_E_BUFFER;
   }
-  BuildParams P = sh.P_frame;
-  P.ent3 = reinterpret_cast<Entry*>(d_send);
-  P.max_records = send_cap;
-  launch_partition1(P, s);
-  launch_dest_counts(P, s, sh.world, (uint32_t)used_digits(P), (uint64_t*)pl->small);
-  launch_digit_starts(P, s, (uint64_t*)pl->small + 64);
+  sh.local = 0;
+  if (n) {
+    BuildParams P = sh.P_frame;
+    if (P.p1_region) {  // the framing filled the digit regions: pack them (or, one rank, leave them)
+      launch_region_send(P, s, sh.world, (uint32_t)used_digits(P), reinterpret_cast<Entry*>(d_send),
+                         (uint64_t*)pl->small, send_cap);
+      if (!d_send) sh.local = 1;
+    } else {
+      if (!d_send) {
+        HIP_TRY(grow(&pl->ent3, pl->c_ent3, n));
+        d_send = reinterpret_cast<uint8_t*>(pl->ent3);
+        send_cap = pl->c_ent3;
+        sh.local = 2;
+      }
+      P.ent3 = reinterpret_cast<Entry*>(d_send);
+      P.max_records = send_cap;
+      launch_partition1(P, s);
+      launch_dest_counts(P, s, sh.world, (uint32_t)used_digits(P), (uint64_t*)pl->small);
+      launch_digit_starts(P, s, (uint64_t*)pl->small + 64);
+    }
+  }
+  ShardScalars sc;
+  for (int i = 0; i < kShardScalars; i++) sc.v[i] = scalars[i];
+  launch_shard_row(s, sc, (const uint64_t*)pl->small, sh.world, n ? 1 : 0, d_row);
   HIP_TRY(hipGetLastError());
-  std::vector<uint64_t> off(64 + 257);
-  HIP_TRY(hipMemcpyAsync(off.data(), pl->small, off.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipStreamSynchronize(s));
-  for (int r = 0; r < sh.world; r++) counts[r] = off[r + 1] - off[r];
-  for (int d = 0; d < 256; d++) sh.digit_count[d] = off[64 + d + 1] - off[64 + d];
   return SPARKEY_OK;
 }
 
-int sparkey_shard_digit_counts(const sparkey_plan* pl, uint64_t* out256) {
-  if (!pl || !pl->shard.active || !out256) return SPARKEY_E_ARG;
-  for (int d = 0; d < 256; d++) out256[d] = pl->shard.digit_count[d];
-  return SPARKEY_OK;
-}
-
-static int shard_summarize_impl(sparkey_plan* pl, const uint8_t* d_recv, uint64_t n_recv, const uint64_t* digit_counts,
-                                void* stream, int64_t* fun_out, char* err, size_t err_len);
-
-int sparkey_shard_summarize(sparkey_plan* pl, const uint8_t* d_recv, uint64_t n_recv, void* stream, int64_t* fun_out,
-                            char* err, size_t err_len) {
-  return shard_summarize_impl(pl, d_recv, n_recv, nullptr, stream, fun_out, err, err_len);
-}
-
-int sparkey_shard_summarize_grouped(sparkey_plan* pl, const uint8_t* d_recv, uint64_t n_recv,
-                                    const uint64_t* digit_counts, void* stream, int64_t* fun_out, char* err,
-                                    size_t err_len) {
-  if (!digit_counts) return SPARKEY_E_ARG;
-  return shard_summarize_impl(pl, d_recv, n_recv, digit_counts, stream, fun_out, err, err_len);
-}
-
-static int shard_summarize_impl(sparkey_plan* pl, const uint8_t* d_recv, uint64_t n_recv, const uint64_t* digit_counts,
-                                void* stream, int64_t* fun_out, char* err, size_t err_len) {
+int sparkey_shard_summarize_dev(sparkey_plan* pl, const uint8_t* d_recv, uint64_t n_recv, const int64_t* d_digits,
+                                int32_t stride, int32_t fixed_regions, int64_t* d_fun, void* stream, char* err,
+                                size_t err_len) {
   int rc = shard_check(pl, err, err_len);
   if (rc) return rc;
   ShardState& sh = pl->shard;
   hipStream_t s = stream ? (hipStream_t)stream : pl->own_stream;
-  if ((uintptr_t)d_recv & 15) {
+  if (((uintptr_t)d_recv & 15) || !d_fun || ((uintptr_t)d_fun & 7)) {
     set_err(err, err_len, "receive buffer must be 16-byte aligned");
     return SPARKEY_E_ARG;
   }
+  const int local = d_recv ? 0 : sh.local;  // no receive buffer: the entries the bin left in ent3
+  if (!d_recv && (n_recv ? !local || !d_digits : false)) {
+    set_err(err, err_len, "no receive buffer and no entries binned in place");
+    return SPARKEY_E_ARG;
+  }
+  if (local) d_recv = reinterpret_cast<const uint8_t*>(pl->ent3);
   BuildParams& P = sh.P;
   P.slab_cap = kPartTile;
   P.nslabs = (std::max<uint64_t>(n_recv, 1) + kPartTile - 1) / kPartTile;
   P.part_group = 1;
   P.p1_tiles = (uint32_t)P.nslabs;
-  rc = plan_reserve(pl, 1, std::max<uint64_t>(n_recv, 1), 1, P.nslabs, P.p1_tiles, P.nbuckets, P.cap, err, err_len);
-  if (rc) return rc;
+  {
+    const Entry* keep = pl->ent3;  // (ent3 holds the local entries: it must not be reallocated)
+    rc = plan_reserve(pl, 1, std::max<uint64_t>(n_recv, 1), 1, P.nslabs, P.p1_tiles, P.nbuckets, P.cap, err,
+                      err_len);
+    if (rc) return rc;
+    if (local && pl->ent3 != keep) {
+      set_err(err, err_len, "internal: local entries moved");
+      return SPARKEY_E_ARG;
+    }
+  }
   P.ent = const_cast<Entry*>(reinterpret_cast<const Entry*>(d_recv));
   P.ent_cap = n_recv;
   P.ent2 = pl->ent2; P.ent3 = pl->ent3; P.max_records = pl->c_ent2;
@@ -1798,106 +1939,120 @@ static int shard_summarize_impl(sparkey_plan* pl, const uint8_t* d_recv, uint64_
   P.bstat_start = pl->bstat_start;
   P.p1_hist = pl->p1_hist; P.p1_off = pl->p1_off; P.p1_off_total = pl->p1_off + 256ull * P.p1_tiles;
   P.st = pl->d_status;
+  P.carry_in_ptr = nullptr;
   sh.n_recv = n_recv;
-  Status init;
-  memset(&init, 0, sizeof(init));
-  init.err = ~0ull;
-  init.n_records = n_recv;
-  HIP_TRY(hipMemcpyAsync(pl->d_status, &init, sizeof(Status), hipMemcpyHostToDevice, s));
+  launch_status_reset(s, pl->d_status, n_recv);
   P.p2_seg = nullptr;
   P.p2_out = nullptr;
-  if (digit_counts) {
+  if (d_digits || local == 1) {
     // the exchange buffer holds, per source rank in rank order, that rank's entries for this rank's
-    // coarse digits in digit order (its pass-1 output): k_part2 reads the runs in place
+    // coarse digits in digit order (its bin output): k_part2 reads the runs in place, its run table
+    // made on the device from the gathered rows
     const uint64_t nd = used_digits(P), G = (uint64_t)sh.world;
     const uint64_t d0 = (nd * (uint64_t)sh.rank) / G, d1 = (nd * (uint64_t)(sh.rank + 1)) / G;
     const uint64_t nk = d1 - d0;
-    std::vector<uint64_t> tab(2 * nk * G + nk + 1);
-    uint64_t* segs = tab.data();
-    uint64_t* outs = tab.data() + 2 * nk * G;
-    std::vector<uint64_t> blk(G + 1, 0);
-    for (uint64_t r = 0; r < G; r++) {
-      uint64_t m = 0;
-      for (uint64_t d = d0; d < d1; d++) m += digit_counts[r * 256 + d];
-      blk[r + 1] = blk[r] + m;
-    }
-    if (blk[G] != n_recv) {
-      set_err(err, err_len, "digit counts do not add up to the received entries");
-      return SPARKEY_E_ARG;
-    }
-    std::vector<uint64_t> cur(blk.begin(), blk.end() - 1);
-    uint64_t o = 0;
-    for (uint64_t k = 0; k < nk; k++) {
-      outs[k] = o;
-      for (uint64_t r = 0; r < G; r++) {
-        const uint64_t c = digit_counts[r * 256 + d0 + k];
-        segs[2 * (k * G + r)] = cur[r];
-        segs[2 * (k * G + r) + 1] = cur[r] + c;
-        cur[r] += c;
-        o += c;
-      }
-    }
-    outs[nk] = o;
-    HIP_TRY(grow(&pl->p2tab, pl->c_p2tab, tab.size()));
-    HIP_TRY(hipMemcpyAsync(pl->p2tab, tab.data(), tab.size() * sizeof(uint64_t), hipMemcpyHostToDevice, s));
+    HIP_TRY(grow(&pl->p2tab, pl->c_p2tab, 2 * nk * G + nk + 1));
+    if (local == 1) launch_p2_table_regions(s, sh.P_frame.p1_fill, sh.P_frame.p1_region, (uint32_t)d0, (uint32_t)nk,
+                                            pl->p2tab);
+    else launch_p2_table(s, d_digits, stride, (int)G, (uint32_t)d0, (uint32_t)nk, pl->p2tab);
     P.ent3 = const_cast<Entry*>(reinterpret_cast<const Entry*>(d_recv));
     P.p2_seg = pl->p2tab;
     P.p2_out = pl->p2tab + 2 * nk * G;
     P.p2_nsrc = (uint32_t)G;
     P.p2_d0 = (uint32_t)d0;
     P.p2_nd = (uint32_t)nk;
+    // k_part2s (tables of at most kP2SortedMaxBpp buckets per digit): one pass into fixed bucket
+    // regions of the rank's range, the carry functions from the same pass.  A bucket that outgrows its
+    // region sets p2_overflow: every later kernel skips, the flags row says "aborted", and the host
+    // redoes the step with fixed_regions = 0 (dense runs)
+    P.p2_sorted = P.bpp <= kP2SortedMaxBpp && !getenv("SPARKEY_NO_P2_SORTED") ? 1 : 0;
+    P.p2_fixed = P.p2_sorted && fixed_regions && !getenv("SPARKEY_NO_P2_FIXED") ? 1 : 0;
+    if (P.p2_fixed) {
+      HIP_TRY(grow(&pl->ent2, pl->c_ent2, std::max<uint64_t>(n_recv, (P.b_hi - P.b_lo) * (uint64_t)kPlaceLdsMax)));
+      P.ent2 = pl->ent2;
+      P.max_records = pl->c_ent2;
+    }
     launch_partition2(P, s, &pl->timer);
     P.ent3 = pl->ent3;  // the later steps' scratch (k_place sorts oversized buckets there)
     P.p2_seg = nullptr;
     P.p2_out = nullptr;
   } else {
+    P.p2_sorted = 0;
+    P.p2_fixed = 0;
     launch_dense_slabs(P, s);
     launch_partition(P, s, &pl->timer);
   }
-  fun_out[0] = 0;  // identity carry function f(x) = max(0, x + 0) for an empty range
-  fun_out[1] = 0;
   if (P.b_hi > P.b_lo) {
     launch_summary_carry(P, s, &pl->timer);
-    HIP_TRY(hipGetLastError());
-    MaxPlus f;
-    HIP_TRY(hipMemcpyAsync(&f, P.bfun_total, sizeof(f), hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
-    fun_out[0] = f.c;
-    fun_out[1] = f.a;
-  } else {
-    HIP_TRY(hipGetLastError());
-    HIP_TRY(hipStreamSynchronize(s));
+    HIP_TRY(hipMemcpyAsync(d_fun, P.bfun_total, sizeof(MaxPlus), hipMemcpyDeviceToDevice, s));
+  } else {  // identity carry function f(x) = max(0, x + 0) for an empty range
+    HIP_TRY(hipMemsetAsync(d_fun, 0, sizeof(MaxPlus), s));
   }
+  HIP_TRY(hipGetLastError());
   return SPARKEY_OK;
 }
 
-int sparkey_shard_place(sparkey_plan* pl, int64_t carry_in, uint8_t* d_slots, uint8_t* d_spill, uint64_t spill_cap,
-                        void* stream, sparkey_shard_place_result* res, char* err, size_t err_len) {
+int sparkey_shard_place_dev(sparkey_plan* pl, const int64_t* d_funs, uint8_t* d_slots, uint8_t* d_spill,
+                            uint64_t spill_cap, int64_t* d_flags, int32_t inline_cap, void* stream, char* err,
+                            size_t err_len) {
   int rc = shard_check(pl, err, err_len);
   if (rc) return rc;
   ShardState& sh = pl->shard;
   hipStream_t s = stream ? (hipStream_t)stream : pl->own_stream;
   BuildParams& P = sh.P;
-  if (((uintptr_t)d_slots & 3) || ((uintptr_t)d_spill & 15)) {
-    set_err(err, err_len, "slot or spill buffer misaligned");
+  if (((uintptr_t)d_slots & 3) || ((uintptr_t)d_spill & 15) || !d_funs || !d_flags || ((uintptr_t)d_flags & 7) ||
+      inline_cap < 0) {
+    set_err(err, err_len, "slot, spill or flags buffer misaligned");
     return SPARKEY_E_ARG;
   }
   P.out = d_slots - kIndexHeaderSize - P.slot_lo * (uint64_t)P.slot_size;  // virtual .spi base
-  P.carry_in = carry_in;
   P.spill = reinterpret_cast<SpillEntry*>(d_spill);
   P.spill_cap = spill_cap;
+  P.carry_in = 0;
+  P.carry_in_ptr = (const int64_t*)((uint64_t*)pl->small + 400);
   HIP_TRY(hipMemsetAsync(&pl->d_status->n_pairs, 0, sizeof(unsigned long long), s));
   HIP_TRY(hipMemsetAsync(&pl->d_status->n_spill, 0, sizeof(unsigned long long), s));
   HIP_TRY(hipMemsetAsync(&pl->d_status->dup_overflow, 0, sizeof(unsigned int), s));
+  launch_shard_carry(s, d_funs, sh.world, sh.rank, (int64_t*)P.carry_in_ptr);
   launch_carry(P, s);
   launch_place_buckets(P, s);
-  rc = shard_sync_status(pl, s, err, err_len);
+  launch_shard_flags(P, s, d_flags, inline_cap);
+  HIP_TRY(hipGetLastError());
+  return SPARKEY_OK;
+}
+
+int sparkey_shard_finish_dev(sparkey_plan* pl, const int64_t* d_rows, int32_t stride, int32_t inline_cap,
+                             int64_t* d_out, void* stream, char* err, size_t err_len) {
+  int rc = shard_check(pl, err, err_len);
   if (rc) return rc;
-  const Status& st = *pl->h_status;
-  memset(res, 0, sizeof(*res));
-  res->n_spill = st.n_spill;
-  res->n_pairs = st.n_pairs;
-  res->non_canonical = (st.dup_overflow || st.n_pairs > P.pair_cap) ? 1 : 0;
+  ShardState& sh = pl->shard;
+  hipStream_t s = stream ? (hipStream_t)stream : pl->own_stream;
+  if (!d_rows || !d_out || ((uintptr_t)d_out & 7) || stride < kShardFlags + 4 * inline_cap) {
+    set_err(err, err_len, "bad flags rows");
+    return SPARKEY_E_ARG;
+  }
+  BuildParams& P = sh.P;
+  launch_apply_spill_rows(P, s, d_rows, sh.world, stride, inline_cap);
+  P.prev_hash = 0;
+  P.prev_occ = 0;
+  if (P.slot_hi > P.slot_lo) launch_stats(P, s, 0, &pl->timer);
+  launch_shard_summary_row(P, s, d_rows + (int64_t)sh.rank * stride, d_out);
+  HIP_TRY(hipGetLastError());
+  return SPARKEY_OK;
+}
+
+int sparkey_shard_header_dev(sparkey_plan* pl, const int64_t* d_fin, int32_t stride, int64_t num_entries,
+                             uint8_t* d_header, void* stream, char* err, size_t err_len) {
+  int rc = shard_check(pl, err, err_len);
+  if (rc) return rc;
+  ShardState& sh = pl->shard;
+  hipStream_t s = stream ? (hipStream_t)stream : pl->own_stream;
+  if (!d_fin || !d_header || stride < kShardFlags + 8) {
+    set_err(err, err_len, "bad finish rows");
+    return SPARKEY_E_ARG;
+  }
+  launch_shard_header(s, d_fin, stride, sh.world, sh.tmpl, num_entries, d_header);
+  HIP_TRY(hipGetLastError());
   return SPARKEY_OK;
 }
 

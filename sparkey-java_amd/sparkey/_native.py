@@ -111,11 +111,6 @@ class ShardFrameResult(ctypes.Structure):
                 ("err_pos", ctypes.c_int64), ("rc", ctypes.c_int32), ("framing_path", ctypes.c_int32)]
 
 
-class ShardPlaceResult(ctypes.Structure):
-    _fields_ = [("n_spill", ctypes.c_uint64), ("n_pairs", ctypes.c_uint64), ("non_canonical", ctypes.c_int32),
-                ("pad", ctypes.c_int32)]
-
-
 _u64p = ctypes.POINTER(ctypes.c_uint64)
 _i64p = ctypes.POINTER(ctypes.c_int64)
 _E = [ctypes.c_char_p, ctypes.c_size_t]
@@ -127,12 +122,15 @@ _SIGS = {
     "sparkey_shard_find_entry": ([_vp, ctypes.c_uint64, ctypes.c_uint64, _vp, _i64p] + _E, ctypes.c_int),
     "sparkey_shard_frame": ([_vp, ctypes.c_int64, ctypes.c_int64, _vp, ctypes.POINTER(ShardFrameResult)] + _E,
                             ctypes.c_int),
-    "sparkey_shard_bin": ([_vp, _vp, ctypes.c_uint64, _vp, _u64p] + _E, ctypes.c_int),
-    "sparkey_shard_summarize": ([_vp, _vp, ctypes.c_uint64, _vp, _i64p] + _E, ctypes.c_int),
-    "sparkey_shard_digit_counts": ([_vp, _u64p], ctypes.c_int),
-    "sparkey_shard_summarize_grouped": ([_vp, _vp, ctypes.c_uint64, _u64p, _vp, _i64p] + _E, ctypes.c_int),
-    "sparkey_shard_place": ([_vp, ctypes.c_int64, _vp, _vp, ctypes.c_uint64, _vp, ctypes.POINTER(ShardPlaceResult)]
-                            + _E, ctypes.c_int),
+    "sparkey_shard_frame_capacity": ([_vp, ctypes.c_int64, ctypes.c_int64], ctypes.c_int64),
+    "sparkey_shard_frame_bin_async": ([_vp, ctypes.c_int64, ctypes.c_int64, _vp, ctypes.c_uint64, _vp, _vp] + _E,
+                                      ctypes.c_int),
+    "sparkey_shard_bin_row": ([_vp, _vp, ctypes.c_uint64, ctypes.c_uint64, _i64p, _vp, _vp] + _E, ctypes.c_int),
+    "sparkey_shard_summarize_dev": ([_vp, _vp, ctypes.c_uint64, _vp, ctypes.c_int32, ctypes.c_int32, _vp, _vp] + _E,
+                                    ctypes.c_int),
+    "sparkey_shard_place_dev": ([_vp, _vp, _vp, _vp, ctypes.c_uint64, _vp, ctypes.c_int32, _vp] + _E, ctypes.c_int),
+    "sparkey_shard_finish_dev": ([_vp, _vp, ctypes.c_int32, ctypes.c_int32, _vp, _vp] + _E, ctypes.c_int),
+    "sparkey_shard_header_dev": ([_vp, _vp, ctypes.c_int32, ctypes.c_int64, _vp, _vp] + _E, ctypes.c_int),
     "sparkey_shard_pairs": ([_vp, _u64p, ctypes.c_uint64] + _E, ctypes.c_int),
     "sparkey_shard_key_record_size": ([_vp], ctypes.c_int32),
     "sparkey_shard_fetch_keys": ([_vp, _vp, ctypes.c_uint64, _vp, ctypes.c_uint32, _vp] + _E, ctypes.c_int),
@@ -328,35 +326,40 @@ class Plan:
         self._call("sparkey_shard_frame", entry, frame_end, ctypes.c_void_p(stream), ctypes.byref(r))
         return r
 
-    def shard_bin(self, d_send: int, send_cap: int, world: int, stream: int = 0):
-        counts = (ctypes.c_uint64 * world)()
-        self._call("sparkey_shard_bin", ctypes.c_void_p(d_send), send_cap, ctypes.c_void_p(stream), counts)
-        return [int(c) for c in counts]
+    def shard_frame_capacity(self, entry: int, frame_end: int) -> int:
+        v = int(_lib.sparkey_shard_frame_capacity(self._h, entry, frame_end))
+        if v < 0:
+            raise ValueError("bad shard frame range")
+        return v
 
-    def shard_summarize(self, d_recv: int, n_recv: int, stream: int = 0):
-        f = (ctypes.c_int64 * 2)()
-        self._call("sparkey_shard_summarize", ctypes.c_void_p(d_recv), n_recv, ctypes.c_void_p(stream), f)
-        return int(f[0]), int(f[1])
+    def shard_frame_bin_async(self, entry: int, frame_end: int, d_send: int, send_cap: int, d_row: int,
+                              stream: int = 0) -> None:
+        self._call("sparkey_shard_frame_bin_async", entry, frame_end, ctypes.c_void_p(d_send or None), send_cap,
+                   ctypes.c_void_p(d_row), ctypes.c_void_p(stream))
 
-    def shard_digit_counts(self):
-        out = (ctypes.c_uint64 * 256)()
-        if _lib.sparkey_shard_digit_counts(self._h, out) != OK:
-            raise ValueError("no sharded build in progress")
-        return [int(v) for v in out]
+    # the *_dev steps and shard_bin_row only enqueue work on `stream` (results stay on the device)
+    def shard_bin_row(self, d_send: int, send_cap: int, n: int, scalars, d_row: int, stream: int = 0) -> None:
+        sc = (ctypes.c_int64 * 8)(*[int(v) for v in scalars])
+        self._call("sparkey_shard_bin_row", ctypes.c_void_p(d_send or None), send_cap, n, sc, ctypes.c_void_p(d_row),
+                   ctypes.c_void_p(stream))
 
-    def shard_summarize_grouped(self, d_recv: int, n_recv: int, digit_counts, stream: int = 0):
-        """digit_counts: world x 256 (row = source rank), every rank's shard_digit_counts()."""
-        flat = [int(v) for row in digit_counts for v in row]
-        arr = (ctypes.c_uint64 * len(flat))(*flat)
-        f = (ctypes.c_int64 * 2)()
-        self._call("sparkey_shard_summarize_grouped", ctypes.c_void_p(d_recv), n_recv, arr, ctypes.c_void_p(stream), f)
-        return int(f[0]), int(f[1])
+    def shard_summarize_dev(self, d_recv: int, n_recv: int, d_digits: int, stride: int, fixed_regions: bool,
+                            d_fun: int, stream: int = 0) -> None:
+        self._call("sparkey_shard_summarize_dev", ctypes.c_void_p(d_recv or None), n_recv, ctypes.c_void_p(d_digits or None),
+                   stride, 1 if fixed_regions else 0, ctypes.c_void_p(d_fun), ctypes.c_void_p(stream))
 
-    def shard_place(self, carry_in: int, d_slots: int, d_spill: int, spill_cap: int, stream: int = 0):
-        r = ShardPlaceResult()
-        self._call("sparkey_shard_place", carry_in, ctypes.c_void_p(d_slots), ctypes.c_void_p(d_spill), spill_cap,
-                   ctypes.c_void_p(stream), ctypes.byref(r))
-        return int(r.n_spill), int(r.n_pairs), bool(r.non_canonical)
+    def shard_place_dev(self, d_funs: int, d_slots: int, d_spill: int, spill_cap: int, d_flags: int, inline_cap: int,
+                        stream: int = 0) -> None:
+        self._call("sparkey_shard_place_dev", ctypes.c_void_p(d_funs), ctypes.c_void_p(d_slots),
+                   ctypes.c_void_p(d_spill), spill_cap, ctypes.c_void_p(d_flags), inline_cap, ctypes.c_void_p(stream))
+
+    def shard_finish_dev(self, d_rows: int, stride: int, inline_cap: int, d_out: int, stream: int = 0) -> None:
+        self._call("sparkey_shard_finish_dev", ctypes.c_void_p(d_rows), stride, inline_cap, ctypes.c_void_p(d_out),
+                   ctypes.c_void_p(stream))
+
+    def shard_header_dev(self, d_fin: int, stride: int, num_entries: int, d_header: int, stream: int = 0) -> None:
+        self._call("sparkey_shard_header_dev", ctypes.c_void_p(d_fin), stride, num_entries, ctypes.c_void_p(d_header),
+                   ctypes.c_void_p(stream))
 
     def shard_pairs(self, n_pairs: int):
         out = (ctypes.c_uint64 * max(1, 2 * n_pairs))()

@@ -28,6 +28,7 @@ Collectives go through torch.distributed: backend "nccl" (RCCL over xGMI) moves 
 from __future__ import annotations
 
 import contextlib
+import os
 import struct
 import time
 from dataclasses import dataclass, field
@@ -39,6 +40,7 @@ LOG_HEADER_SIZE = 84
 INDEX_HEADER_SIZE = 112
 ENTRY_BYTES = 16
 SPILL_BYTES = 32
+SPILL_INLINE = 64  # spilled slots per rank that travel with the placement flags
 _HDR = struct.Struct("<IIIiqqqqqqiiqi")
 
 
@@ -164,6 +166,13 @@ class Comm:
             res.append(piece if piece.device == out_device else piece.to(out_device))
         return res
 
+    def allgather_fixed(self, t: torch.Tensor) -> torch.Tensor:
+        """Every rank's 1-D tensor of the same length -> (world, len), on the collective's device."""
+        t = self._to(t)
+        out = torch.empty(self.world * t.numel(), dtype=t.dtype, device=self.tdev)
+        self.dist.all_gather_into_tensor(out, t, group=self.group)
+        return out.view(self.world, -1)
+
     def barrier(self):
         self.dist.barrier(group=self.group)
 
@@ -208,19 +217,46 @@ class GpuShardSteps:
         return {"exit": r.exit, "n": r.num_records, "ndel": r.num_deletes, "rc": r.rc, "err_pos": r.err_pos,
                 "framing_path": r.framing_path}
 
-    def bin(self, send: torch.Tensor, n: int, world: int):
-        return self.plan.shard_bin(send.data_ptr(), n, world, self.stream)
+    def frame_capacity(self, entry: int, frame_end: int) -> int:
+        return self.plan.shard_frame_capacity(entry, frame_end)
 
-    def summarize(self, recv: torch.Tensor, n: int, digit_counts=None):
-        if digit_counts is not None:
-            return self.plan.shard_summarize_grouped(recv.data_ptr(), n, digit_counts, self.stream)
-        return self.plan.shard_summarize(recv.data_ptr(), n, self.stream)
+    # the next five only enqueue device work on the build stream: their results are device tensors
+    def frame_bin_async(self, entry: int, frame_end: int, send, cap: int, row: torch.Tensor) -> None:
+        self.plan.shard_frame_bin_async(entry, frame_end, 0 if send is None else send.data_ptr(), cap, row.data_ptr(),
+                                        self.stream)
 
-    def digit_counts(self):
-        return self.plan.shard_digit_counts()
+    def bin_row(self, send, n: int, scalars, row: torch.Tensor) -> None:
+        """send None (one rank): the entries stay on the device where the framing left them."""
+        self.plan.shard_bin_row(0 if send is None else send.data_ptr(), 0 if send is None else send.numel() // ENTRY_BYTES,
+                                n, scalars, row.data_ptr(), self.stream)
 
-    def place(self, carry_in, out: torch.Tensor, out_off: int, spill: torch.Tensor, spill_cap: int):
-        return self.plan.shard_place(carry_in, out.data_ptr() + out_off, spill.data_ptr(), spill_cap, self.stream)
+    def summarize(self, recv, n: int, rows: torch.Tensor, digit_col: int, fixed: bool) -> torch.Tensor:
+        """recv None: the entries bin_row kept (one rank)."""
+        fun = torch.empty(2, dtype=torch.int64, device=self.device)
+        rows = rows if rows.device == self.device else rows.to(self.device)
+        self._keep = rows
+        self.plan.shard_summarize_dev(0 if recv is None else recv.data_ptr(), n, rows.data_ptr() + 8 * digit_col,
+                                      rows.shape[1], fixed, fun.data_ptr(), self.stream)
+        return fun
+
+    def write_header(self, fin: torch.Tensor, num_entries: int, out: torch.Tensor) -> None:
+        fin = fin if fin.device == self.device else fin.to(self.device)
+        self._keep_fin = fin
+        self.plan.shard_header_dev(fin.data_ptr(), fin.shape[1], num_entries, out.data_ptr(), self.stream)
+
+    def place(self, funs: torch.Tensor, out: torch.Tensor, out_off: int, spill: torch.Tensor, spill_cap: int,
+              flags: torch.Tensor, inline_cap: int) -> None:
+        funs = funs if funs.device == self.device else funs.to(self.device)
+        self._keep_funs = funs
+        self.plan.shard_place_dev(funs.data_ptr(), out.data_ptr() + out_off, spill.data_ptr(), spill_cap,
+                                  flags.data_ptr(), inline_cap, self.stream)
+
+    def finish(self, rows: torch.Tensor, inline_cap: int) -> torch.Tensor:
+        out = torch.empty(12, dtype=torch.int64, device=self.device)
+        rows = rows if rows.device == self.device else rows.to(self.device)
+        self._keep_rows = rows
+        self.plan.shard_finish_dev(rows.data_ptr(), rows.shape[1], inline_cap, out.data_ptr(), self.stream)
+        return out
 
     def pairs(self, n):
         return np.array(self.plan.shard_pairs(n), dtype=np.uint64)
@@ -340,7 +376,11 @@ class ShardedBuilder:
         else:
             c_g = s.find_entry(lay.lo[g], lay.window)
         mark("find_entry")
-        cs = [int(v) for v in c.allgather_i64([c_g])[:, 0]]
+        if lay.small or uni:  # every rank's entry follows from the header: no gather
+            cs = [LOG_HEADER_SIZE if r == 0 else (data_end if lay.small else
+                  min(data_end, LOG_HEADER_SIZE + -(-(lay.lo[r] - LOG_HEADER_SIZE) // uni) * uni)) for r in range(G)]
+        else:
+            cs = [int(v) for v in c.allgather_i64([c_g])[:, 0]]
         mark("gather_entries")
         entries = []
         for r, v in enumerate(cs):
@@ -354,22 +394,41 @@ class ShardedBuilder:
                 return data_end
             return entries[r + 1] if entries[r + 1] is not None else lay.hi[r]
 
-        mine = None
         todo = {r for r in range(G) if entries[r] is not None}
+        framed = set()  # entries this rank framed speculatively (sparkey_shard_frame_bin_async)
         rounds = 0
+        send = None
+        L = 8 + G + 256  # the verification row: frame scalars, entries per destination, per coarse digit
+        row = torch.empty(L, dtype=torch.int64, device=s.device)
+        if g not in todo:  # (re-framed from the previous rank's exit in a later round)
+            row.zero_()
+            row[:7] = -1
         while True:
             rounds += 1
             if g in todo:
                 fe = frame_end(g)
-                mine = s.frame(entries[g], fe)  # owns nothing when entries[g] >= fe
-                mine["entry"], mine["fe"] = entries[g], fe
-            row = [-1] * 7 if mine is None else [mine["entry"], mine["fe"], mine["exit"], mine["n"], mine["ndel"],
-                                                 mine["rc"], mine["err_pos"]]
-            R = c.allgather_i64(row)
-            todo = set()
+                if entries[g] not in framed:
+                    # framing, bin and row enqueued without waiting; the row says if it held
+                    framed.add(entries[g])
+                    cap = s.frame_capacity(entries[g], fe)
+                    if os.environ.get("SPARKEY_SHARD_SYNC_FRAME"):  # (tests: every attempt is retried)
+                        cap = 0
+                    send = None if G == 1 else s.alloc(max(1, cap) * ENTRY_BYTES)  # (one rank: kept in place)
+                    s.frame_bin_async(entries[g], fe, send, cap, row)
+                else:  # the speculative attempt did not hold: frame with every retry, then bin
+                    mine = s.frame(entries[g], fe)  # owns nothing when entries[g] >= fe
+                    n_mine = int(mine["n"]) if not mine["rc"] and not mine["ndel"] else 0
+                    send = None if G == 1 else s.alloc(max(1, n_mine) * ENTRY_BYTES)
+                    s.bin_row(send, n_mine, [entries[g], fe, mine["exit"], mine["n"], mine["ndel"], mine["rc"],
+                                             mine["err_pos"], 0], row)
+            rows = c.allgather_fixed(row)
+            R = rows.cpu().numpy()
+            todo = {r for r in range(G) if R[r][7]}  # speculative attempts to redo, the entries unchanged
+            if todo:
+                continue
             done = True
             for r in range(G):
-                ent, fe, ex, n, nd, rc, epos = (int(x) for x in R[r])
+                ent, fe, ex, n, nd, rc, epos = (int(x) for x in R[r][:7])
                 if rc:
                     from ._native import raise_for
                     raise_for(rc, f"{_code_text(rc)} (log offset {epos})")
@@ -384,7 +443,7 @@ class ShardedBuilder:
                 break
             if done:
                 break
-        n_local = int(mine["n"]) if mine else 0
+        n_mine = int(R[g][3]) if not R[g][5] and not R[g][4] else 0
         totals = R[:, 3].astype(np.int64)
         n_total = int(totals.sum())
         n_deletes = int(R[:, 4].sum())
@@ -400,57 +459,69 @@ class ShardedBuilder:
         if n_deletes > 0 or n_total >= _capacity(h, opts):
             return self._gathered(res, header, file_len, buf, buf_lo, buf_hi, lay, opts, slot_size, out_len)
 
-        # ---- 2 exchange: every entry to the owner of its slot range ----
-        send = s.alloc(max(1, n_local) * ENTRY_BYTES)
-        counts = s.bin(send, n_local, G) if n_local else [0] * G
-        digits = s.digit_counts() if n_local else [0] * 256
-        mark("bin")
-        MD = c.allgather_i64(list(counts) + list(digits))  # per rank: entries per destination, per digit
-        M, D = MD[:, :G], MD[:, G:]                        # M[src][dst], D[src][digit]
+        # ---- 2 exchange: every entry to the owner of its slot range (binned while framing) ----
+        if send is None and G > 1:
+            send = s.alloc(16)
+        M = R[:, 8:8 + G]                                  # M[src][dst]
         out_splits = [int(M[r][g]) * 2 for r in range(G)]  # int64 elements (2 per entry)
-        in_splits = [int(x) * 2 for x in counts]
-        recv = c.all_to_all(send.view(torch.int64)[: 2 * max(1, n_local)] if n_local else
-                            send.view(torch.int64)[:0], in_splits, out_splits, buf.device)
         n_recv = sum(out_splits) // 2
+        if G == 1:  # nothing to exchange: the entries stay where the framing left them
+            recv = None
+        else:
+            in_splits = [int(x) * 2 for x in M[g]]
+            recv = c.all_to_all(send.view(torch.int64)[: 2 * n_mine], in_splits, out_splits, buf.device)
         mark("all_to_all")
 
-        # ---- 3 placement ----
-        fun = s.summarize(recv, n_recv, D.tolist())  # the runs arrive grouped by digit: no first pass
-        mark("summarize")
-        F = [tuple(int(v) for v in row) for row in c.allgather_i64(list(fun))]
-        mark("gather_carry")
-        x0 = _compose(F)[0]             # N < capacity: the wrap fixed point is C_total
-        carry = x0
-        for r in range(g):
-            carry = _apply(F[r], carry)
+        # ---- 3 placement and stats on the device; the host sees one row per rank at the end ----
         out = s.alloc(out_len)
+        hdr_off = INDEX_HEADER_SIZE if g == 0 else 0
         spill_cap = 4096
+        spill = s.alloc(spill_cap * SPILL_BYTES)
+        flags = torch.empty(4 + 4 * SPILL_INLINE, dtype=torch.int64, device=s.device)
+        fixed = True
         while True:
-            spill = s.alloc(spill_cap * SPILL_BYTES)
-            n_spill, n_pairs, non_canon = s.place(carry, out, INDEX_HEADER_SIZE if g == 0 else 0, spill, spill_cap)
-            if n_spill <= spill_cap:
-                break
-            spill_cap = n_spill
-        mark("place_kernel")
-        flags = c.allgather_i64([n_spill, n_pairs, int(non_canon)])
-        res.n_spill, res.n_pairs = int(flags[:, 0].sum()), int(flags[:, 1].sum())
-        if flags[:, 2].any():
+            # the runs arrive grouped by coarse digit: no first partition pass
+            fun = s.summarize(recv, n_recv, rows, 8 + G, fixed)
+            funs = c.allgather_fixed(fun)                   # every rank's carry function
+            s.place(funs, out, hdr_off, spill, spill_cap, flags, SPILL_INLINE)
+            frows = c.allgather_fixed(flags)                # flags + inline spilled slots of every rank
+            fin = s.finish(frows, SPILL_INLINE)             # spill applied; flags, boundary slots, range stats
+            fins = c.allgather_fixed(fin)
+            if g == 0:  # the header from the same rows (rewritten below if a slow path runs)
+                s.write_header(fins, n_total, out)
+            host = fins.cpu().numpy()
+            F, bnd = host[:, :4], host[:, 4:]
+            if F[:, 3].any() and fixed:  # a bucket outgrew its fixed region on some rank: dense runs
+                fixed = False
+                continue
+            if F[:, 3].any():
+                raise RuntimeError("sharded placement aborted")
+            break
+        mark("place")
+        res.n_spill, res.n_pairs = int(F[:, 0].sum()), int(F[:, 1].sum())
+        if F[:, 2].any():
             return self._gathered(res, header, file_len, buf, buf_lo, buf_hi, lay, opts, slot_size, out_len)
-        if flags[:, 1].sum() > 0 and self._pairs_share_a_key(n_pairs, entries, data_end, buf.device):
+        if F[:, 1].sum() > 0 and self._pairs_share_a_key(int(F[g, 1]), entries, data_end, buf.device):
             return self._gathered(res, header, file_len, buf, buf_lo, buf_hi, lay, opts, slot_size, out_len)
-        if flags[:, 0].sum() > 0:
+        host_header = False
+        if int(F[:, 0].max()) > SPILL_INLINE:  # more spilled slots than the rows carry: exchange them all
+            host_header = True
+            n_spill = int(F[g, 0])
+            if n_spill > spill_cap:
+                spill_cap = n_spill
+                spill = s.alloc(spill_cap * SPILL_BYTES)
+                s.place(funs, out, hdr_off, spill, spill_cap, flags, SPILL_INLINE)
             pieces = c.allgather_var(spill.view(torch.int64), 4 * n_spill, buf.device)
-            allsp = torch.cat([p for p in pieces if p.numel()]) if any(p.numel() for p in pieces) else None
-            if allsp is not None:
-                s.apply_spill(allsp, allsp.numel() // 4)
-
+            allsp = torch.cat([p for p in pieces if p.numel()])
+            s.apply_spill(allsp, allsp.numel() // 4)
+            nonempty = int(slot_hi > slot_lo)
+            bslots = s.boundary()
+            mx, col, tot = s.stats(0, 0) if nonempty else (0, 0, 0)
+            bnd = c.allgather_i64([_signed(v) for v in bslots] + [nonempty, mx, col, tot])
         mark("spill")
-        # ---- 4 stats: per-range sums (the first slot is not compared with its predecessor), the
-        #      boundary slots, one gather; the cross-range comparisons are added here ----
-        nonempty = int(slot_hi > slot_lo)
-        bslots = s.boundary()
-        mx, col, tot = s.stats(0, 0) if nonempty else (0, 0, 0)
-        bnd = c.allgather_i64([_signed(v) for v in bslots] + [nonempty, mx, col, tot])
+
+        # ---- 4 stats: per-range sums (the first slot is not compared with its predecessor) and the
+        #      boundary slots of every rank; the cross-range comparisons are added here ----
         max_disp, collisions, total_disp = int(bnd[:, 5].max()), int(bnd[:, 6].sum()), int(bnd[:, 7].sum())
         prev = None  # (hash, occupied) of the last slot of the previous non-empty range
         for r in range(G):
@@ -465,7 +536,7 @@ class ShardedBuilder:
             collisions += 1
         stats = {"num_entries": n_total, "garbage_size": 0, "max_displacement": max_disp,
                  "hash_collisions": collisions, "total_displacement": total_disp, "placement_path": 0}
-        if g == 0:
+        if g == 0 and host_header:
             hdr = s.index_header(opts, n_total, 0, max_disp, collisions, total_disp)
             out[:INDEX_HEADER_SIZE].copy_(s.from_host(hdr))
         res.out = out

@@ -144,33 +144,58 @@ class CpuShardSteps:
     def _bucket(self, h):
         return (h % self.cap) // KBUCKET
 
-    def bin(self, send, n, world):
-        dest = []
-        nd = (self.nb + self.bpp - 1) // self.bpp
-        for h, a in self.entries:
-            d = self._bucket(h) // self.bpp
-            dest.append(next(r for r in range(world) if nd * r // world <= d < nd * (r + 1) // world))
-        order = sorted(range(len(self.entries)), key=lambda i: dest[i])
-        arr = np.array([self.entries[i] for i in order], dtype=np.uint64).reshape(-1, 2)
-        send.view(torch.int64)[: 2 * len(order)] = torch.from_numpy(arr.view(np.int64).reshape(-1).copy())
-        return [dest.count(r) for r in range(world)]
+    def frame_capacity(self, entry, frame_end):
+        return max(0, frame_end - entry) // 2 + 1  # (a record is at least 2 bytes)
 
-    def digit_counts(self):
-        return [0] * 256  # the simulation's summarize re-sorts what it receives
+    def frame_bin_async(self, entry, frame_end, send, cap, row):
+        if entry >= frame_end:
+            self.entries = []
+            self.bin_row(send, 0, [entry, frame_end, entry, 0, 0, 0, 0, 0], row)
+            return
+        m = self.frame(entry, frame_end)
+        n = m["n"] if not m["rc"] and not m["ndel"] else 0
+        self.bin_row(send, n, [entry, frame_end, m["exit"], m["n"], m["ndel"], m["rc"], m["err_pos"], 0], row)
 
-    def summarize(self, recv, n, digit_counts=None):
-        a = recv[: 2 * n].numpy().view(np.uint64).reshape(-1, 2)
+    def bin_row(self, send, n, scalars, row):
+        world = self.world
+        counts = [0] * world
+        if send is None:  # one rank: the entries stay here
+            self.kept = np.array(self.entries, dtype=np.uint64).reshape(-1, 2)
+            counts = [n]
+        elif n:
+            dest = []
+            nd = (self.nb + self.bpp - 1) // self.bpp
+            for h, a in self.entries:
+                d = self._bucket(h) // self.bpp
+                dest.append(next(r for r in range(world) if nd * r // world <= d < nd * (r + 1) // world))
+            order = sorted(range(len(self.entries)), key=lambda i: dest[i])
+            arr = np.array([self.entries[i] for i in order], dtype=np.uint64).reshape(-1, 2)
+            send.view(torch.int64)[: 2 * len(order)] = torch.from_numpy(arr.view(np.int64).reshape(-1).copy())
+            counts = [dest.count(r) for r in range(world)]
+        row.zero_()  # the per-digit counts stay 0: the simulation's summarize re-sorts what it receives
+        row[:8] = torch.tensor([int(v) for v in scalars], dtype=torch.int64)
+        row[8:8 + world] = torch.tensor(counts, dtype=torch.int64)
+
+    def summarize(self, recv, n, rows, digit_col, fixed):
+        a = self.kept[:n] if recv is None else recv[: 2 * n].numpy().view(np.uint64).reshape(-1, 2)
         self.mine = sorted(((int(h) % self.cap, int(ad), int(h)) for h, ad in a), key=lambda t: (t[0], t[1] & ~DEL))
         size = self.slot_hi - self.slot_lo
         if size == 0:
-            return 0, 0
+            return torch.zeros(2, dtype=torch.int64)
         n = len(self.mine)
         c = 0
         for j, (w, _, _) in enumerate(self.mine):
             c = max(c, w + n - j - self.slot_hi)
-        return c, n - size
+        return torch.tensor([c, n - size], dtype=torch.int64)
 
-    def place(self, carry_in, out, out_off, spill, spill_cap):
+    def place(self, funs, out, out_off, spill, spill_cap, flags, inline_cap):
+        F = [(int(c), int(a)) for c, a in funs.reshape(-1, 2).tolist()]
+        c0, a0 = F[0]
+        for fc, fa in F[1:]:
+            c0, a0 = max(fc, c0 + fa), a0 + fa
+        carry_in = c0
+        for r in range(self.rank):
+            carry_in = max(F[r][0], carry_in + F[r][1])
         self.out, self.out_off = out, out_off
         nxt = self.slot_lo + carry_in
         sp = []
@@ -181,15 +206,32 @@ class CpuShardSteps:
                 self._write(pos, h, addr & ~DEL)
             else:
                 sp.append((pos % self.cap, h, addr & ~DEL, 0))
-        if sp and len(sp) <= spill_cap:
-            arr = np.array(sp, dtype=np.uint64)
-            spill.view(torch.int64)[: 4 * len(sp)] = torch.from_numpy(arr.view(np.int64).reshape(-1).copy())
+        if sp:
+            arr = np.array(sp[:spill_cap], dtype=np.uint64)
+            spill.view(torch.int64)[: 4 * len(arr)] = torch.from_numpy(arr.view(np.int64).reshape(-1).copy())
         groups = {}
         for w, addr, h in self.mine:
             if not addr & DEL:
                 groups.setdefault(h, []).append(addr)
         self._pairs = [(x, y) for g in groups.values() for i, x in enumerate(g) for y in g[i + 1:]]
-        return len(sp), len(self._pairs), False
+        flags.zero_()
+        flags[:4] = torch.tensor([len(sp), len(self._pairs), 0, 0], dtype=torch.int64)
+        k = min(len(sp), spill_cap, inline_cap)
+        if k:
+            arr = np.array(sp[:k], dtype=np.uint64)
+            flags[4: 4 + 4 * k] = torch.from_numpy(arr.view(np.int64).reshape(-1).copy())
+
+    def finish(self, rows, inline_cap):
+        for row in rows.reshape(self.world, -1):
+            n = int(row[0])
+            if 0 < n <= inline_cap:
+                self.apply_spill(row[4: 4 + 4 * n], n)
+        nonempty = int(self.slot_hi > self.slot_lo)
+        b = self.boundary()
+        mx, col, tot = self.stats(0, 0) if nonempty else (0, 0, 0)
+        v = [x - (1 << 64) if x >= (1 << 63) else x for x in b] + [nonempty, mx, col, tot]
+        own = [int(x) for x in rows.reshape(self.world, -1)[self.rank, :4]]
+        return torch.tensor(own + v, dtype=torch.int64)
 
     def _write(self, slot, h, a):
         off = self.out_off + (slot - self.slot_lo) * self.S
@@ -255,6 +297,21 @@ class CpuShardSteps:
                 mx = max(mx, d)
             ph, po = h, a != 0
         return mx, col, tot
+
+    def write_header(self, fin, num_entries, out):
+        f = fin.reshape(self.world, -1)[:, 4:].tolist()
+        mx, col, tot = max(r[5] for r in f), sum(r[6] for r in f), sum(r[7] for r in f)
+        prev, last = None, None
+        for r, b in enumerate(f):
+            if not b[4]:
+                continue
+            if prev is not None and prev[1] and prev[0] == b[0]:
+                col += 1
+            prev, last = (b[2], b[3] != 0), r
+        if last is not None and f[0][1] != 0 and f[last][3] != 0 and f[0][0] == f[last][2]:
+            col += 1
+        hdr = self.index_header(self.opts, num_entries, 0, mx, col, tot)
+        out[:INDEX_HEADER_SIZE] = torch.frombuffer(bytearray(hdr), dtype=torch.uint8)
 
     def index_header(self, opts, num_entries, garbage, max_disp, collisions, total_disp):
         return _native.index_header(self.header, opts, num_entries, garbage, max_disp, collisions, total_disp)

@@ -129,6 +129,13 @@ class ThreadComm:
         self._exchange(None)
         return out
 
+    def allgather_fixed(self, t):
+        import torch
+        res = self._exchange(t.clone())
+        out = torch.stack([x.to(t.device) for x in res])
+        self._exchange(None)
+        return out
+
     def barrier(self):
         self._exchange(None)
 

@@ -22,7 +22,7 @@ def check(log, world, tmp_path, seed=7, hash_size=0, method=IN_MEMORY, sparsity=
     return metas
 
 
-@pytest.mark.parametrize("world", [2, 3, 4])
+@pytest.mark.parametrize("world", [1, 2, 3, 4])
 def test_sharded_key_value(tmp_path, world):
     log = make_log(key_value_puts(3000))
     metas = check(log, world, tmp_path)

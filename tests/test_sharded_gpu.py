@@ -24,13 +24,13 @@ def check(native, log, world, seed=7, hash_size=0, method=IN_MEMORY, sparsity=0.
     return metas
 
 
-@pytest.mark.parametrize("world", [2, 3, 4])
+@pytest.mark.parametrize("world", [1, 2, 3, 4])
 def test_sharded_gpu_key_value(native, world):
     metas = check(native, make_log(key_value_puts(20000)), world)
     assert metas[0]["path"] == "sharded"
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [1, 2, 4])
 def test_sharded_gpu_c2_shape(native, world):
     """C2's record shape (16 B keys, 100 B values, fused framing) at 300K records."""
     from sparkey import synth
@@ -80,13 +80,16 @@ def test_sharded_gpu_understated_header(native):
     check(native, bytes(log), 3, seed=9)
 
 
-def test_sharded_gpu_matches_single(native):
+@pytest.mark.parametrize("world", [1, 4])
+def test_sharded_gpu_matches_single(native, world):
+    """Mixed record sizes (k_frame, the bin's own partition pass; one rank: entries kept in place)."""
     from sparkey import synth
     log = synth.mixed_log(100000, 8, 64, 100, seed=4).tobytes()
     opts = native.make_opts(hash_seed=99)
     single, _ = native.build_index_mem(log, opts)
-    got, metas = run_threads(log, 4, dict(hash_seed=99))
+    got, metas = run_threads(log, world, dict(hash_seed=99))
     assert got == single, diff_report(got, single)
+    assert metas[0]["path"] == "sharded"
 
 
 @pytest.mark.parametrize("world", [2, 4])
@@ -96,3 +99,12 @@ def test_sharded_gpu_snappy_gather(native, world):
     log = synth.snappy_log(synth.fixed_log(100000, 16, 100, seed=6), 118, 16384).tobytes()
     metas = check(native, log, world, seed=13)
     assert metas[0]["path"] == "gathered"
+
+
+@pytest.mark.parametrize("world", [1, 3])
+def test_sharded_gpu_speculative_retry(native, world, monkeypatch):
+    """Every speculative frame+bin attempt flagged for a retry (a send buffer of 0 entries): the
+    ranks re-frame synchronously and the result is unchanged."""
+    monkeypatch.setenv("SPARKEY_SHARD_SYNC_FRAME", "1")
+    metas = check(native, make_log(key_value_puts(20000)), world)
+    assert metas[0]["path"] == "sharded" and metas[0]["rounds"] >= 2

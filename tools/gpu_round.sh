@@ -12,7 +12,7 @@ MODE=${2:-all}
 shift 2 2>/dev/null
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
-ARGS="--steps 5 --warmup 1 --no-cpu-baseline $*"
+ARGS="--steps 5 --warmup 1 --no-cpu-baseline --quick $*"
 run_tests() {
   echo "smoke" && timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 &&
   echo "pytest" && timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1
@@ -24,10 +24,10 @@ run_bench() {
 run_prof() {
   echo "trace" && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof/trace -o run -- python3 bench.py $ARGS > $OUT/trace.log 2>&1 &&
   echo "pmc" &&
-  timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/prof/fetch -o run -- python3 bench.py $ARGS > $OUT/fetch.log 2>&1 &&
-  timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/prof/write -o run -- python3 bench.py $ARGS > $OUT/write.log 2>&1 &&
-  timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU --output-format csv -d $OUT/prof/sq -o run -- python3 bench.py $ARGS > $OUT/sq.log 2>&1 &&
-  timeout -s KILL 120 rocprofv3 --pmc SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE --output-format csv -d $OUT/prof/sq2 -o run -- python3 bench.py $ARGS > $OUT/sq2.log 2>&1
+  timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/prof/fetch -o run -- python3 bench.py $ARGS > $OUT/fetch.log 2>&1 &&
+  timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/prof/write -o run -- python3 bench.py $ARGS > $OUT/write.log 2>&1 &&
+  timeout -s KILL 200 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU --output-format csv -d $OUT/prof/sq -o run -- python3 bench.py $ARGS > $OUT/sq.log 2>&1 &&
+  timeout -s KILL 200 rocprofv3 --pmc SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE --output-format csv -d $OUT/prof/sq2 -o run -- python3 bench.py $ARGS > $OUT/sq2.log 2>&1
 }
 case $MODE in
   tests) run_tests ;;
