@@ -161,12 +161,28 @@ __global__ __launch_bounds__(kPlaceBlock) void k_summary(BuildParams P) {
 }
 
 // carry[b] = (F_{b-1} o ... o F_0)(x0), x0 = fixed point of the whole ring = C_total when N < cap.
-// Sharded: the prefix starts at b_lo and x0 is the rank's carry-in (composed on the host).
+// Sharded: the prefix starts at b_lo and x0 is the rank's carry-in: given, or composed here from every
+// rank's carry function (the ring's fixed point (N < capacity), then the ranks before this one).
 __global__ void k_carry(BuildParams P) {
+  if (P.carry_funs && blockIdx.x == 0 && threadIdx.x == 0) {  // (the placement's counters, before k_place)
+    P.st->n_pairs = 0;
+    P.st->n_spill = 0;
+    P.st->dup_overflow = 0;
+  }
   if (build_aborted(P)) return;
   const uint64_t b = P.b_lo + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const MaxPlus tot = *P.bfun_total;
-  int64_t x0 = P.carry_in_ptr ? *P.carry_in_ptr : P.carry_in;
+  int64_t x0 = P.carry_in;
+  if (P.carry_funs) {
+    const int64_t* f = P.carry_funs;
+    int64_t c = f[0], a = f[1];
+    for (int r = 1; r < P.carry_world; r++) {
+      c = max(f[2 * r], c + f[2 * r + 1]);
+      a += f[2 * r + 1];
+    }
+    x0 = c;
+    for (int r = 0; r < P.carry_rank; r++) x0 = max(f[2 * r], x0 + f[2 * r + 1]);
+  }
   if (!P.sharded) {
     if (tot.a >= 0) {  // N >= capacity: no empty slot, the canonical layout does not apply
       if (b == 0) atomicOr(&P.st->full, 1u);
@@ -225,6 +241,7 @@ __global__ __launch_bounds__(kStatBlock) void k_stats(BuildParams P) {
   __shared__ unsigned long long red_col[kStatBlock / 64];
   __shared__ long long red_max[kStatBlock / 64];
   if (build_aborted(P)) return;
+  if (P.stats_if_pending && !P.st->stats_pending) return;  // (the folded stats covered every slot)
   const int tid = threadIdx.x;
   const uint64_t blk0 = P.slot_lo + (uint64_t)blockIdx.x * kStatSlotsPerBlock;
   uint64_t prev_hash = 0;
@@ -285,6 +302,7 @@ __global__ __launch_bounds__(kStatBlock) void k_stats(BuildParams P) {
 __global__ __launch_bounds__(1024) void k_stats_final(BuildParams P, uint32_t nparts, int sequential) {
   __shared__ unsigned long long s_sum[16], s_col[16];
   __shared__ long long s_max[16];
+  if (P.stats_if_pending && !P.st->stats_pending) return;
   const StatPart* parts = P.parts;
   const int tid = threadIdx.x;
   unsigned long long sum = 0, col = 0;
@@ -358,6 +376,68 @@ __global__ __launch_bounds__(kStatFoldBlock) void k_stats_folded(BuildParams P) 
   }
 }
 
+// The folded stats of a sharded rank (after its spilled-in slots were written).  Every entry's
+// displacement was summed by the rank that placed it (max and sum are global); the adjacent pairs
+// (s - 1, s) with s in (slot_lo, slot_hi) are: inside one block's written range (k_place_lds counted
+// those whose s this rank owns), at the start gs of a block of this rank other than b_lo (read here),
+// or in the spilled-in run [slot_lo, slot_lo + carry[b_lo]] (read here by block 0).  The pair at
+// slot_lo and the wrap quirk are the host's (sharded.py), as with k_stats.
+__global__ __launch_bounds__(kStatFoldBlock) void k_stats_folded_shard(BuildParams P) {
+  __shared__ unsigned long long s_sum[kStatFoldBlock / 64], s_col[kStatFoldBlock / 64], s_max[kStatFoldBlock / 64];
+  __shared__ bool last;
+  if (build_aborted(P)) return;
+  Status* st = P.st;
+  const int tid = threadIdx.x;
+  if (st->big_buckets || st->full) {  // some slots were placed outside k_place_lds: k_stats runs
+    if (tid == 0) st->stats_pending = 1u;
+    return;
+  }
+  unsigned long long sum = 0, col = 0, mx = 0;
+  const uint64_t b = P.b_lo + (uint64_t)blockIdx.x * kStatFoldBlock + tid;
+  if (b < P.b_hi) {
+    const StatPart sp = P.parts[b];
+    sum = sp.sum_disp;
+    col = sp.collisions;
+    mx = (unsigned long long)sp.max_disp;
+    const uint64_t gs = (b << kBucketShift) + (uint64_t)P.carry[b];  // (unwrapped)
+    if (b > P.b_lo && P.bstat_start[b] != ~0ull && gs < P.slot_hi) {
+      uint64_t hp, ap, hc, ac;
+      read_slot(P, gs - 1, hp, ap);
+      read_slot(P, gs, hc, ac);
+      col += ap != 0 && hp == hc;
+    }
+  }
+  if (blockIdx.x == 0 && P.b_hi > P.b_lo) {  // the spilled-in run
+    const uint64_t end = min(P.slot_lo + (uint64_t)P.carry[P.b_lo], P.slot_hi - 1);
+    for (uint64_t s = P.slot_lo + 1 + tid; s <= end; s += kStatFoldBlock) {
+      uint64_t hp, ap, hc, ac;
+      read_slot(P, s - 1, hp, ap);
+      read_slot(P, s, hc, ac);
+      col += ap != 0 && hp == hc;
+    }
+  }
+  sum = wave_sum_u64(sum);
+  col = wave_sum_u64(col);
+  mx = (unsigned long long)wave_max_i64((long long)mx);
+  if ((tid & 63) == 0) { s_sum[tid >> 6] = sum; s_col[tid >> 6] = col; s_max[tid >> 6] = mx; }
+  __syncthreads();
+  if (tid == 0) {
+    for (int w = 1; w < kStatFoldBlock / 64; w++) { s_sum[0] += s_sum[w]; s_col[0] += s_col[w]; s_max[0] = max(s_max[0], s_max[w]); }
+    atomicAdd(&st->acc_sum, s_sum[0]);
+    atomicAdd(&st->acc_col, s_col[0]);
+    atomicMax(&st->acc_max, s_max[0]);
+    __threadfence();
+    last = atomicAdd(&st->stats_ticket, 1u) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (last && tid == 0) {
+    __threadfence();
+    const unsigned long long tsum = atomicAdd(&st->acc_sum, 0ull), tcol = atomicAdd(&st->acc_col, 0ull);
+    const unsigned long long tmax = atomicMax(&st->acc_max, 0ull);
+    finish_stats(P, tsum, tcol, (long long)tmax, 0);
+  }
+}
+
 // ================================================================================================
 // host-side launchers (called by the plan in sparkey_gpu.cpp)
 // ================================================================================================
@@ -404,6 +484,12 @@ void launch_stats_folded(const BuildParams& P, hipStream_t s, StageTimer* tm) {
   hipLaunchKernelGGL(k_stats_folded, dim3(grid_for(std::max<uint64_t>(P.nbuckets, 1), kStatFoldBlock)),
                      dim3(kStatFoldBlock), 0, s, P);
   tm->mark("stats", s);
+}
+
+void launch_stats_folded_shard(const BuildParams& P, hipStream_t s) {
+  const uint64_t nb = P.b_hi - P.b_lo;
+  hipLaunchKernelGGL(k_stats_folded_shard, dim3(grid_for(std::max<uint64_t>(nb, 1), kStatFoldBlock)),
+                     dim3(kStatFoldBlock), 0, s, P);
 }
 
 void launch_stats(const BuildParams& P, hipStream_t s, int sequential, StageTimer* tm) {

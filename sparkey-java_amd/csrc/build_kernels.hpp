@@ -204,6 +204,7 @@ struct BuildParams {
   int32_t p2_sorted;    // k_part2s: per-(bucket, slot) counts in the same pass + the carry functions
   int32_t p2_fixed;     // k_part2s in one pass: bucket b's entries at ent2[b * kPlaceLdsMax, + bcount[b])
   int32_t fold_stats;   // k_place_lds leaves calculateMaxDisplacement's per-bucket parts (no k_stats pass)
+  int32_t stats_if_pending;  // k_stats / k_stats_final only when the folded stats left stats_pending
   uint64_t* bstat_start;  // fold_stats: per bucket, the first slot of the range it wrote (~0: none)
   uint32_t* p1_fill;
   // framing window: records start at fr_entry (84 for a whole log) and are framed while they start
@@ -221,7 +222,10 @@ struct BuildParams {
   uint64_t slot_lo, slot_hi;
   int64_t carry_in;
   int32_t abort_on_fail;        // the bin after a speculative framing attempt: skip it when the attempt failed
-  const int64_t* carry_in_ptr;  // non-null: the carry-in is read from device memory (k_shard_carry)
+  // sharded: the carry-in composed on the device from every rank's carry function (world x {c, a});
+  // k_carry then also clears the placement's status counters
+  const int64_t* carry_funs;
+  int32_t carry_world, carry_rank;
   uint64_t prev_hash;
   SpillEntry* spill;
   uint64_t spill_cap;
@@ -283,6 +287,7 @@ void launch_place_global(const BuildParams& P, hipStream_t s, int sort_only, int
 void launch_verify(const BuildParams& P, hipStream_t s, StageTimer* tm);
 void launch_stats(const BuildParams& P, hipStream_t s, int sequential, StageTimer* tm);
 void launch_stats_folded(const BuildParams& P, hipStream_t s, StageTimer* tm);
+void launch_stats_folded_shard(const BuildParams& P, hipStream_t s);
 // exact replay (exact_kernels.hip)
 void launch_sequential(const BuildParams& P, hipStream_t s, int sorted_order);
 // Streams the exact path forks its independent segment classes onto (owned by the plan).
@@ -310,14 +315,15 @@ void launch_shard_row(hipStream_t s, const ShardScalars& sc, const uint64_t* off
 void launch_shard_row_async(hipStream_t s, const ShardScalars& sc, const Status* st, int path, uint32_t slab_cap,
                             uint64_t max_records, uint64_t send_cap, int64_t data_end, const uint64_t* off, int world,
                             int64_t* row);
-void launch_p2_table(hipStream_t s, const int64_t* dig, int stride, int G, uint32_t d0, uint32_t nk, uint64_t* tab);
-void launch_shard_carry(hipStream_t s, const int64_t* funs, int world, int rank, int64_t* out);
+void launch_p2_table(hipStream_t s, const int64_t* dig, int stride, int G, uint32_t d0, uint32_t nk, uint64_t* tab,
+                     Status* st, uint64_t n_records);
 void launch_shard_flags(const BuildParams& P, hipStream_t s, int64_t* flags, int inline_cap);
 void launch_apply_spill_rows(const BuildParams& P, hipStream_t s, const int64_t* rows, int world, int stride,
                              int inline_cap);
 void launch_shard_summary_row(const BuildParams& P, hipStream_t s, const int64_t* flags, int64_t* out);
-void launch_status_reset(hipStream_t s, Status* st, uint64_t n_records);
-void launch_p2_table_regions(hipStream_t s, const uint32_t* fill, uint64_t rc, uint32_t d0, uint32_t nk, uint64_t* tab);
+void launch_status_reset(hipStream_t s, Status* st, uint64_t n_records, uint32_t* fill = nullptr, int nfill = 0);
+void launch_p2_table_regions(hipStream_t s, const uint32_t* fill, uint64_t rc, uint32_t d0, uint32_t nk, uint64_t* tab,
+                             Status* st, uint64_t n_records);
 void launch_shard_header(hipStream_t s, const int64_t* fin, int stride, int world, const IndexHeaderBytes& tmpl,
                          int64_t n_total, uint8_t* out);
 

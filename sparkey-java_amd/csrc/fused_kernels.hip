@@ -1365,17 +1365,22 @@ __global__ __launch_bounds__(kPlaceLdsBlock) void k_place_lds(BuildParams P) {
     // adjacent pairs (slot - 1, slot) inside [x, hi), seen from the occupied slot of each pair:
     // an entry equal to the occupied slot before it, and an entry of hash 0 before an empty slot
     // (which reads as hash 0)
+    // (sharded: only pairs whose later slot this rank owns -- the rest are the next rank's, counted
+    // from its spilled-in slots by k_stats_folded_shard)
+    const uint64_t lim = P.sharded ? P.slot_hi : ~0ull;
     unsigned long long col = 0;
 #pragma unroll
     for (int k = 0; k < kPer; k++) {
       const int64_t p = pos[k];
       if (p < 0) continue;
       const uint64_t h = mine[k].hash;
-      if (p > x && wrap_slot(start + (uint64_t)p, P.cap) != 0) {
+      if (p > x && wrap_slot(start + (uint64_t)p, P.cap) != 0 && start + (uint64_t)p < lim) {
         const int32_t vp = pos_j[p - 1 - x];  // the hash bits decide; the full hash only confirms
         if (vp >= 0 && (uint32_t)(vp >> 10) == (uint32_t)(h & 0x1fffffull)) col += buf[vp & 1023].hash == h;
       }
-      if (h == 0 && p + 1 < hi && pos_j[p + 1 - x] < 0 && wrap_slot(start + (uint64_t)p + 1, P.cap) != 0) col++;
+      if (h == 0 && p + 1 < hi && pos_j[p + 1 - x] < 0 && wrap_slot(start + (uint64_t)p + 1, P.cap) != 0 &&
+          start + (uint64_t)p + 1 < lim)
+        col++;
     }
     if (x < (1ll << 20)) {  // (block-uniform) every displacement < 2^21: 32-bit DPP reductions
       sum_d = wave_sum_u32((uint32_t)sum_d);

@@ -18,6 +18,16 @@
 
 namespace sk {
 
+// a fresh status block: no error, no exit yet, n_records given
+__device__ inline void status_reset(Status* st, uint64_t n_records) {
+  Status z;
+  memset(&z, 0, sizeof(z));
+  z.err = ~0ull;
+  z.exit = -1;
+  z.n_records = n_records;
+  *st = z;
+}
+
 // Every plausible start in [lo, cand_end) walks its chain with the speculative rules of k_frame
 // (IndexHash's iterator rules plus the header's maxKeyLen / maxValueLen) to the first record start
 // >= target.  If every surviving chain reaches the same start, that start is on the true chain
@@ -212,9 +222,10 @@ __global__ __launch_bounds__(256) void k_shard_row_async(ShardScalars sc, const 
 // dig = &rows[0][first digit column]; source r's count of digit d is dig[r * stride + d].
 // One thread per digit (nk <= 256); per source rank one block scan over the digits.
 __global__ __launch_bounds__(256) void k_p2_table(const int64_t* dig, int stride, int G, uint32_t d0, uint32_t nk,
-                                                  uint64_t* tab) {
+                                                  uint64_t* tab, Status* st, uint64_t n_records) {
   __shared__ uint64_t wsum[4];
   const uint32_t k = threadIdx.x;
+  if (k == 0) status_reset(st, n_records);
   const int lane = k & 63, w = k >> 6;
   uint64_t* segs = tab;
   uint64_t* outs = tab + 2ull * nk * G;
@@ -258,9 +269,10 @@ __global__ __launch_bounds__(256) void k_p2_table(const int64_t* dig, int stride
 // One rank (world 1): k_part2's runs are the framing's digit regions of ent3 where they lie (region d
 // at d * rc, fill[d] entries), no send buffer in between.
 __global__ __launch_bounds__(256) void k_p2_table_regions(const uint32_t* fill, uint64_t rc, uint32_t d0, uint32_t nk,
-                                                          uint64_t* tab) {
+                                                          uint64_t* tab, Status* st, uint64_t n_records) {
   __shared__ uint64_t wsum[4];
   const uint32_t k = threadIdx.x;
+  if (k == 0) status_reset(st, n_records);
   const int lane = k & 63, w = k >> 6;
   const uint64_t c = k < nk ? min((uint64_t)fill[d0 + k], rc) : 0;
   uint64_t incl = c;
@@ -320,21 +332,6 @@ __global__ void k_shard_header(const int64_t* fin, int stride, int world, IndexH
   put_le64(out + 84, (uint64_t)mx);
   put_le64(out + 96, col);
   put_le64(out + 104, tot);
-}
-
-// The rank's carry-in from every rank's carry function (funs = world x {c, a}): x0 = the fixed point
-// of the whole ring (N < capacity), then the functions of the ranks before this one.
-__global__ void k_shard_carry(const int64_t* funs, int world, int rank, int64_t* out) {
-  if (threadIdx.x != 0) return;
-  int64_t c = funs[0], a = funs[1];
-  for (int r = 1; r < world; r++) {
-    const int64_t fc = funs[2 * r], fa = funs[2 * r + 1];
-    c = max(fc, c + fa);
-    a = a + fa;
-  }
-  int64_t x = c;
-  for (int r = 0; r < rank; r++) x = max(funs[2 * r], x + funs[2 * r + 1]);
-  *out = x;
 }
 
 // flags = {spilled slots, equal-hash pairs, non-canonical, aborted, up to inline_cap spilled slots
@@ -397,14 +394,9 @@ __global__ void k_shard_summary_row(BuildParams P, const int64_t* flags, int64_t
   out[7] = ne ? P.st->total_disp : 0;
 }
 
-__global__ void k_status_reset(Status* st, uint64_t n_records) {
-  if (threadIdx.x != 0) return;
-  Status z;
-  memset(&z, 0, sizeof(z));
-  z.err = ~0ull;
-  z.exit = -1;
-  z.n_records = n_records;
-  *st = z;
+__global__ void k_status_reset(Status* st, uint64_t n_records, uint32_t* fill, int nfill) {
+  if (threadIdx.x == 0) status_reset(st, n_records);
+  for (int i = threadIdx.x; i < nfill; i += blockDim.x) fill[i] = 0;
 }
 
 void launch_shard_row(hipStream_t s, const ShardScalars& sc, const uint64_t* off, int world, int have, int64_t* row) {
@@ -418,21 +410,19 @@ void launch_shard_row_async(hipStream_t s, const ShardScalars& sc, const Status*
                      data_end, off, world, row);
 }
 
-void launch_p2_table(hipStream_t s, const int64_t* dig, int stride, int G, uint32_t d0, uint32_t nk, uint64_t* tab) {
-  hipLaunchKernelGGL(k_p2_table, dim3(1), dim3(256), 0, s, dig, stride, G, d0, nk, tab);
+void launch_p2_table(hipStream_t s, const int64_t* dig, int stride, int G, uint32_t d0, uint32_t nk, uint64_t* tab,
+                     Status* st, uint64_t n_records) {
+  hipLaunchKernelGGL(k_p2_table, dim3(1), dim3(256), 0, s, dig, stride, G, d0, nk, tab, st, n_records);
 }
 
-void launch_p2_table_regions(hipStream_t s, const uint32_t* fill, uint64_t rc, uint32_t d0, uint32_t nk, uint64_t* tab) {
-  hipLaunchKernelGGL(k_p2_table_regions, dim3(1), dim3(256), 0, s, fill, rc, d0, nk, tab);
+void launch_p2_table_regions(hipStream_t s, const uint32_t* fill, uint64_t rc, uint32_t d0, uint32_t nk, uint64_t* tab,
+                             Status* st, uint64_t n_records) {
+  hipLaunchKernelGGL(k_p2_table_regions, dim3(1), dim3(256), 0, s, fill, rc, d0, nk, tab, st, n_records);
 }
 
 void launch_shard_header(hipStream_t s, const int64_t* fin, int stride, int world, const IndexHeaderBytes& tmpl,
                          int64_t n_total, uint8_t* out) {
   hipLaunchKernelGGL(k_shard_header, dim3(1), dim3(64), 0, s, fin, stride, world, tmpl, n_total, out);
-}
-
-void launch_shard_carry(hipStream_t s, const int64_t* funs, int world, int rank, int64_t* out) {
-  hipLaunchKernelGGL(k_shard_carry, dim3(1), dim3(64), 0, s, funs, world, rank, out);
 }
 
 void launch_shard_flags(const BuildParams& P, hipStream_t s, int64_t* flags, int inline_cap) {
@@ -448,8 +438,8 @@ void launch_shard_summary_row(const BuildParams& P, hipStream_t s, const int64_t
   hipLaunchKernelGGL(k_shard_summary_row, dim3(1), dim3(64), 0, s, P, flags, out);
 }
 
-void launch_status_reset(hipStream_t s, Status* st, uint64_t n_records) {
-  hipLaunchKernelGGL(k_status_reset, dim3(1), dim3(64), 0, s, st, n_records);
+void launch_status_reset(hipStream_t s, Status* st, uint64_t n_records, uint32_t* fill, int nfill) {
+  hipLaunchKernelGGL(k_status_reset, dim3(1), dim3(256), 0, s, st, n_records, fill, nfill);
 }
 
 void launch_find_entry(const BuildParams& P, hipStream_t s, int64_t lo, int64_t cand_end, int64_t target,

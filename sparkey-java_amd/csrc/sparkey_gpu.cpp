@@ -609,7 +609,7 @@ static int launch_framing(sparkey_plan* pl, const BuildParams& P, int framing_pa
     else launch_frame_fused(P, s, &pl->timer);
   } else if (framing_path == 2) {
     launch_frame_uniform(P, s, &pl->timer);
-    launch_dense_slabs(P, s);
+    if (!(P.sharded && P.p1_region)) launch_dense_slabs(P, s);  // (a sharded rank reads only the regions)
   } else {
     launch_framing_serial(P, s);
     launch_emit(P, s, &pl->timer);
@@ -1679,7 +1679,6 @@ static int shard_frame_launch(sparkey_plan* pl, ShardFrameSetup* F, hipStream_t 
   }
   int rc = reserve_for_framing(pl, P, F->framing_path, F->nrec, F->slab_cap, err, err_len);
   if (rc) return rc;
-  launch_status_reset(s, pl->d_status, 0);
   // uniform framing also does the bin's partition pass: entries into 256 coarse-digit regions of
   // ent3 (the bin then only packs them), as on one GPU
   P.p1_region = 0;
@@ -1688,11 +1687,11 @@ static int shard_frame_launch(sparkey_plan* pl, ShardFrameSetup* F, hipStream_t 
     const uint64_t rc_cap = ((uint64_t)(expect + 8.0 * std::sqrt(expect) + 1024.0) + 63) & ~63ull;
     HIP_TRY(grow(&pl->ent3, pl->c_ent3, 256 * rc_cap));
     HIP_TRY(grow(&pl->p1_fill, pl->c_p1_fill, 256));
-    HIP_TRY(hipMemsetAsync(pl->p1_fill, 0, 256 * sizeof(uint32_t), s));
     P.ent3 = pl->ent3;
     P.p1_fill = pl->p1_fill;
     P.p1_region = rc_cap;
   }
+  launch_status_reset(s, pl->d_status, 0, P.p1_region ? pl->p1_fill : nullptr, P.p1_region ? 256 : 0);
   return launch_framing(pl, P, F->framing_path, s, err, err_len);
 }
 
@@ -1915,6 +1914,16 @@ int sparkey_shard_summarize_dev(sparkey_plan* pl, const uint8_t* d_recv, uint64_
   }
   if (local) d_recv = reinterpret_cast<const uint8_t*>(pl->ent3);
   BuildParams& P = sh.P;
+  const bool grouped = d_digits || local == 1;
+  const uint64_t nd = used_digits(P), G = (uint64_t)sh.world;
+  const uint64_t d0 = (nd * (uint64_t)sh.rank) / G, d1 = (nd * (uint64_t)(sh.rank + 1)) / G;
+  const uint64_t nk = d1 - d0;
+  if (grouped) {  // the run table (and the status reset) first: the device starts while the host sets up
+    HIP_TRY(grow(&pl->p2tab, pl->c_p2tab, 2 * nk * G + nk + 1));
+    if (local == 1) launch_p2_table_regions(s, sh.P_frame.p1_fill, sh.P_frame.p1_region, (uint32_t)d0, (uint32_t)nk,
+                                            pl->p2tab, pl->d_status, n_recv);
+    else launch_p2_table(s, d_digits, stride, (int)G, (uint32_t)d0, (uint32_t)nk, pl->p2tab, pl->d_status, n_recv);
+  }
   P.slab_cap = kPartTile;
   P.nslabs = (std::max<uint64_t>(n_recv, 1) + kPartTile - 1) / kPartTile;
   P.part_group = 1;
@@ -1939,22 +1948,14 @@ int sparkey_shard_summarize_dev(sparkey_plan* pl, const uint8_t* d_recv, uint64_
   P.bstat_start = pl->bstat_start;
   P.p1_hist = pl->p1_hist; P.p1_off = pl->p1_off; P.p1_off_total = pl->p1_off + 256ull * P.p1_tiles;
   P.st = pl->d_status;
-  P.carry_in_ptr = nullptr;
+  P.carry_funs = nullptr;
   sh.n_recv = n_recv;
-  launch_status_reset(s, pl->d_status, n_recv);
   P.p2_seg = nullptr;
   P.p2_out = nullptr;
-  if (d_digits || local == 1) {
+  if (grouped) {
     // the exchange buffer holds, per source rank in rank order, that rank's entries for this rank's
     // coarse digits in digit order (its bin output): k_part2 reads the runs in place, its run table
-    // made on the device from the gathered rows
-    const uint64_t nd = used_digits(P), G = (uint64_t)sh.world;
-    const uint64_t d0 = (nd * (uint64_t)sh.rank) / G, d1 = (nd * (uint64_t)(sh.rank + 1)) / G;
-    const uint64_t nk = d1 - d0;
-    HIP_TRY(grow(&pl->p2tab, pl->c_p2tab, 2 * nk * G + nk + 1));
-    if (local == 1) launch_p2_table_regions(s, sh.P_frame.p1_fill, sh.P_frame.p1_region, (uint32_t)d0, (uint32_t)nk,
-                                            pl->p2tab);
-    else launch_p2_table(s, d_digits, stride, (int)G, (uint32_t)d0, (uint32_t)nk, pl->p2tab);
+    // made on the device from the gathered rows (above)
     P.ent3 = const_cast<Entry*>(reinterpret_cast<const Entry*>(d_recv));
     P.p2_seg = pl->p2tab;
     P.p2_out = pl->p2tab + 2 * nk * G;
@@ -1979,6 +1980,7 @@ int sparkey_shard_summarize_dev(sparkey_plan* pl, const uint8_t* d_recv, uint64_
   } else {
     P.p2_sorted = 0;
     P.p2_fixed = 0;
+    launch_status_reset(s, pl->d_status, n_recv);
     launch_dense_slabs(P, s);
     launch_partition(P, s, &pl->timer);
   }
@@ -2009,12 +2011,11 @@ int sparkey_shard_place_dev(sparkey_plan* pl, const int64_t* d_funs, uint8_t* d_
   P.spill = reinterpret_cast<SpillEntry*>(d_spill);
   P.spill_cap = spill_cap;
   P.carry_in = 0;
-  P.carry_in_ptr = (const int64_t*)((uint64_t*)pl->small + 400);
-  HIP_TRY(hipMemsetAsync(&pl->d_status->n_pairs, 0, sizeof(unsigned long long), s));
-  HIP_TRY(hipMemsetAsync(&pl->d_status->n_spill, 0, sizeof(unsigned long long), s));
-  HIP_TRY(hipMemsetAsync(&pl->d_status->dup_overflow, 0, sizeof(unsigned int), s));
-  launch_shard_carry(s, d_funs, sh.world, sh.rank, (int64_t*)P.carry_in_ptr);
-  launch_carry(P, s);
+  P.carry_funs = d_funs;
+  P.carry_world = sh.world;
+  P.carry_rank = sh.rank;
+  P.fold_stats = getenv("SPARKEY_NO_FOLD_STATS") ? 0 : 1;  // k_place_lds leaves the stats parts
+  launch_carry(P, s);  // (also clears the placement's counters)
   launch_place_buckets(P, s);
   launch_shard_flags(P, s, d_flags, inline_cap);
   HIP_TRY(hipGetLastError());
@@ -2035,7 +2036,16 @@ int sparkey_shard_finish_dev(sparkey_plan* pl, const int64_t* d_rows, int32_t st
   launch_apply_spill_rows(P, s, d_rows, sh.world, stride, inline_cap);
   P.prev_hash = 0;
   P.prev_occ = 0;
-  if (P.slot_hi > P.slot_lo) launch_stats(P, s, 0, &pl->timer);
+  if (P.slot_hi > P.slot_lo) {
+    if (P.fold_stats) {  // the parts k_place_lds left; k_stats only if some bucket bypassed it
+      launch_stats_folded_shard(P, s);
+      BuildParams Q = P;
+      Q.stats_if_pending = 1;
+      launch_stats(Q, s, 0, &pl->timer);
+    } else {
+      launch_stats(P, s, 0, &pl->timer);
+    }
+  }
   launch_shard_summary_row(P, s, d_rows + (int64_t)sh.rank * stride, d_out);
   HIP_TRY(hipGetLastError());
   return SPARKEY_OK;

@@ -188,10 +188,12 @@ class GpuShardSteps:
         self.n = _native
         self.device = device
         self.plan = plan if plan is not None else _native.Plan(device.index or 0)
-        # every torch op and every C-ABI step of the build runs in order on this one stream
+        # every torch op and every C-ABI step of the build runs in order on this one stream (its own:
+        # the C-ABI reads a NULL stream as the plan's stream, so the default stream cannot be shared)
         self.tstream = torch.cuda.Stream(device)
         self.stream = self.tstream.cuda_stream
         self.header = None
+        self._fun = self._fin = None  # device results kept across builds (each build ends synchronised)
 
     def stream_ctx(self):
         return torch.cuda.stream(self.tstream)
@@ -232,7 +234,9 @@ class GpuShardSteps:
 
     def summarize(self, recv, n: int, rows: torch.Tensor, digit_col: int, fixed: bool) -> torch.Tensor:
         """recv None: the entries bin_row kept (one rank)."""
-        fun = torch.empty(2, dtype=torch.int64, device=self.device)
+        if self._fun is None:
+            self._fun = torch.empty(2, dtype=torch.int64, device=self.device)
+        fun = self._fun
         rows = rows if rows.device == self.device else rows.to(self.device)
         self._keep = rows
         self.plan.shard_summarize_dev(0 if recv is None else recv.data_ptr(), n, rows.data_ptr() + 8 * digit_col,
@@ -252,7 +256,9 @@ class GpuShardSteps:
                                   flags.data_ptr(), inline_cap, self.stream)
 
     def finish(self, rows: torch.Tensor, inline_cap: int) -> torch.Tensor:
-        out = torch.empty(12, dtype=torch.int64, device=self.device)
+        if self._fin is None:
+            self._fin = torch.empty(12, dtype=torch.int64, device=self.device)
+        out = self._fin
         rows = rows if rows.device == self.device else rows.to(self.device)
         self._keep_rows = rows
         self.plan.shard_finish_dev(rows.data_ptr(), rows.shape[1], inline_cap, out.data_ptr(), self.stream)
@@ -335,6 +341,16 @@ class ShardedBuilder:
         self.s = steps
         self.c = comm
         self._ebb = 0
+        self._geo = {}
+        self._bufs = {}
+
+    def _buf(self, name: str, n: int, dtype=torch.int64) -> torch.Tensor:
+        """A scratch tensor kept across builds (each build ends synchronised on the host)."""
+        t = self._bufs.get(name)
+        if t is None or t.numel() != n or t.dtype != dtype:
+            t = torch.empty(n, dtype=dtype, device=self.s.device)
+            self._bufs[name] = t
+        return t
 
     def build(self, header: bytes, file_len: int, buf: torch.Tensor, buf_lo: int, buf_hi: int, opts) -> ShardResult:
         ctx = self.s.stream_ctx() if hasattr(self.s, "stream_ctx") else contextlib.nullcontext()
@@ -352,10 +368,16 @@ class ShardedBuilder:
             clock[0] = t
 
         g, G = c.rank, c.world
-        lay = shard_layout(header, file_len, G)
+        key = (bytes(header[:LOG_HEADER_SIZE]), file_len, G)
+        geo = self._geo.get(key)
+        if geo is None:  # the host-side geometry of this log, kept for the next build of it
+            lay = shard_layout(header, file_len, G)
+            h = parse_log_header(header)
+            self._geo = {key: (lay, h, uniform_record_size(h))}
+            geo = self._geo[key]
+        lay, h, uni = geo
         data_end = lay.data_end
         s.begin(header, file_len, buf, buf_lo, buf_hi, opts, g, G)
-        h = parse_log_header(header)
         if h["compression_type"] == 1:  # SNAPPY: the whole log on every rank, the single-GPU build
             slot_lo, slot_hi = s.slot_range(g)
             slot_size = _slot_size(h, opts, data_end)
@@ -366,7 +388,6 @@ class ShardedBuilder:
             return self._gathered(res, header, file_len, buf, buf_lo, buf_hi, lay, opts, slot_size, out_len)
 
         # ---- 1 entries: speculate, frame, verify by induction from c_0 = 84 ----
-        uni = uniform_record_size(h)
         if g == 0:
             c_g = LOG_HEADER_SIZE
         elif lay.small:
@@ -399,7 +420,7 @@ class ShardedBuilder:
         rounds = 0
         send = None
         L = 8 + G + 256  # the verification row: frame scalars, entries per destination, per coarse digit
-        row = torch.empty(L, dtype=torch.int64, device=s.device)
+        row = self._buf("row", L)
         if g not in todo:  # (re-framed from the previous rank's exit in a later round)
             row.zero_()
             row[:7] = -1
@@ -410,10 +431,11 @@ class ShardedBuilder:
                 if entries[g] not in framed:
                     # framing, bin and row enqueued without waiting; the row says if it held
                     framed.add(entries[g])
-                    cap = s.frame_capacity(entries[g], fe)
+                    # (one rank: the entries stay in place, bounded by the plan's own workspace)
+                    cap = (1 << 62) if G == 1 else s.frame_capacity(entries[g], fe)
                     if os.environ.get("SPARKEY_SHARD_SYNC_FRAME"):  # (tests: every attempt is retried)
                         cap = 0
-                    send = None if G == 1 else s.alloc(max(1, cap) * ENTRY_BYTES)  # (one rank: kept in place)
+                    send = None if G == 1 else s.alloc(max(1, cap) * ENTRY_BYTES)
                     s.frame_bin_async(entries[g], fe, send, cap, row)
                 else:  # the speculative attempt did not hold: frame with every retry, then bin
                     mine = s.frame(entries[g], fe)  # owns nothing when entries[g] >= fe
@@ -421,8 +443,11 @@ class ShardedBuilder:
                     send = None if G == 1 else s.alloc(max(1, n_mine) * ENTRY_BYTES)
                     s.bin_row(send, n_mine, [entries[g], fe, mine["exit"], mine["n"], mine["ndel"], mine["rc"],
                                              mine["err_pos"], 0], row)
+            mark("frame_launch")
             rows = c.allgather_fixed(row)
+            mark("rows_gather")
             R = rows.cpu().numpy()
+            mark("rows_wait")
             todo = {r for r in range(G) if R[r][7]}  # speculative attempts to redo, the entries unchanged
             if todo:
                 continue
@@ -476,17 +501,23 @@ class ShardedBuilder:
         out = s.alloc(out_len)
         hdr_off = INDEX_HEADER_SIZE if g == 0 else 0
         spill_cap = 4096
-        spill = s.alloc(spill_cap * SPILL_BYTES)
-        flags = torch.empty(4 + 4 * SPILL_INLINE, dtype=torch.int64, device=s.device)
+        spill = self._buf("spill", spill_cap * SPILL_BYTES, torch.uint8)
+        flags = self._buf("flags", 4 + 4 * SPILL_INLINE)
         fixed = True
         while True:
             # the runs arrive grouped by coarse digit: no first partition pass
             fun = s.summarize(recv, n_recv, rows, 8 + G, fixed)
+            mark("summarize")
             funs = c.allgather_fixed(fun)                   # every rank's carry function
+            mark("funs_gather")
             s.place(funs, out, hdr_off, spill, spill_cap, flags, SPILL_INLINE)
+            mark("place_launch")
             frows = c.allgather_fixed(flags)                # flags + inline spilled slots of every rank
+            mark("flags_gather")
             fin = s.finish(frows, SPILL_INLINE)             # spill applied; flags, boundary slots, range stats
+            mark("finish_launch")
             fins = c.allgather_fixed(fin)
+            mark("fins_gather")
             if g == 0:  # the header from the same rows (rewritten below if a slow path runs)
                 s.write_header(fins, n_total, out)
             host = fins.cpu().numpy()
