@@ -248,7 +248,7 @@ def single_gpu(args, dev):
     dom_bytes = stage_bytes(dom, n, frame_end, slot, cap, passes, comp_end=log_len) if dom else 0
     achieved = dom_bytes / (stage_ms[dom] * 1e-3) / 1e9 if dom and stage_ms[dom] > 0 else 0.0
     b_alg = (log_len - 84) + 112 + slot * cap
-    assert stats.placement_path == wl["path"] and stats.framing_path in (0, 2, 3), stats.as_dict()
+    assert stats.placement_path == wl["path"] and stats.framing_path in (0, 2, 3, 4), stats.as_dict()
     assert wl["path"] != 0 or stats.num_entries == n, stats.as_dict()
 
     if args.quick:  # (profiling runs: the timed builds only)
@@ -363,7 +363,8 @@ def single_gpu(args, dev):
         "build_algorithmic_bytes": b_alg,
         "stage_ms": stage_ms,
         "framing": {0: "k_frame (speculative)", 1: "serial walk", 2: "k_frame_uniform (uniform records)",
-                    3: "k_frame2 (speculative, mixed record sizes)"}[stats.framing_path],
+                    3: "k_frame2 (speculative, mixed record sizes)",
+                    4: "k_frame3 (short/long walks, one-byte VLQs)"}[stats.framing_path],
         "general_framing": general,
         "host_to_host_keys_per_s": h2h,
         "file_to_file_keys_per_s": file_rate,

@@ -175,11 +175,8 @@ __global__ void k_carry(BuildParams P) {
   int64_t x0 = P.carry_in;
   if (P.carry_funs) {
     const int64_t* f = P.carry_funs;
-    int64_t c = f[0], a = f[1];
-    for (int r = 1; r < P.carry_world; r++) {
-      c = max(f[2 * r], c + f[2 * r + 1]);
-      a += f[2 * r + 1];
-    }
+    int64_t c = f[0];  // the composed function's constant: the fixed point when N < capacity
+    for (int r = 1; r < P.carry_world; r++) c = max(f[2 * r], c + f[2 * r + 1]);
     x0 = c;
     for (int r = 0; r < P.carry_rank; r++) x0 = max(f[2 * r], x0 + f[2 * r + 1]);
   }

@@ -194,6 +194,7 @@ struct BuildParams {
   // starts per segment, f2_rgn_bytes staged per wave
   int32_t f2_lcap;
   int32_t f2_rgn_bytes;
+  int32_t f3_short;  // k_frame3 (frame3_kernels.hip): steps of the short walk
   // uniform-stride framing (k_frame_uniform): uni_n records of uni_rec bytes from fr_entry
   uint64_t uni_n;
   int64_t uni_rec;
@@ -276,6 +277,12 @@ void launch_partition2(const BuildParams& P, hipStream_t s, StageTimer* tm);
 void launch_dense_slabs(const BuildParams& P, hipStream_t s);
 void launch_frame_uniform(const BuildParams& P, hipStream_t s, StageTimer* tm);
 void launch_frame2(const BuildParams& P, hipStream_t s, StageTimer* tm);  // frame2_kernels.hip
+void launch_frame3(const BuildParams& P, hipStream_t s, StageTimer* tm);  // frame3_kernels.hip
+bool frame3_fits(const BuildParams& P, double mean_record, double pass);
+uint32_t frame3_lds_per_wave(const BuildParams& P);
+// framing paths: 0 k_frame, 1 serial walk, 2 k_frame_uniform, 3 k_frame2, 4 k_frame3; the
+// speculative ones with per-wave slabs
+__host__ __device__ inline bool slab_framing(int path) { return path == 0 || path == 3 || path == 4; }
 void launch_place_fast(const BuildParams& P, hipStream_t s, StageTimer* tm);
 void launch_place_buckets(const BuildParams& P, hipStream_t s);
 // fallbacks and shared stages (build_kernels.hip)

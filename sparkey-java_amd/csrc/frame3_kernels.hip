@@ -1,0 +1,607 @@
+// frame3_kernels.hip -- k_frame3: framing + MurmurHash3 of logs whose records differ in size and
+// whose VLQs are all one byte (every key < 127 bytes, every value < 128 bytes: fr_fast).
+//
+// The log is a chain of varint-framed records (SparkeyLogIterator.java:86-138): where a record
+// starts depends on every record before it.  One wave owns W chunks of C = 2^fr_cshift bytes
+// (C >= maxRecLen), staged once into LDS with LOOK bytes past the last one, like k_frame
+// (fused_kernels.hip).  k_frame walks every candidate start of a chunk to the chunk end and then
+// walks the verified chain a second time to list its records; here the walks are split so that
+// all 64 lanes stay busy and every chain is walked once:
+//
+//   1 screen     plausible record starts in each chunk's first maxRecLen bytes (SWAR, 8 per step),
+//                as in k_frame; the candidates of all chunks go to one position-sorted LDS list,
+//                one 64-bit mask word per lane.
+//   2 short walk every candidate K records on (K = 2..4), lanes taking candidates lane, lane + 64, ...:
+//                a false start survives a step with the probability that two random bytes look like
+//                a header (about 1 in 10 for 8-64 B keys: K = 2, 1 in 100 survives), and K grows
+//                with that probability (the header's maxima).  A
+//                surviving candidate marks the starts it reached inside its chunk: a candidate
+//                reached from another one lies on that one's chain (its records are a suffix of the
+//                other's), so only the unreached survivors -- the chain heads -- walk on.  The true
+//                starts of a chunk form one chain: only the first is a head.
+//   3 long walk  each head (about one per chunk: the true chain, rarely a false one) walks to its
+//                chunk end + LOOK on its own lane, listing its record starts.  Its exit is the first
+//                start at or past the chunk end.
+//   4 resolve    chunk j's entry is chunk j-1's exit: a head whose list holds it gives the chunk's
+//                records (that list from the entry on) and its exit (the true start of a chunk
+//                always survives, as a head or on one's list: it is a plausible start of a valid
+//                chain).  A chunk whose heads all reach one exit knows it without its entry, so the
+//                wave's exit is usually published before the wave waits for its predecessor's; the
+//                first entry is taken speculatively when chunk 0 has a single head (checked at the
+//                end).
+//   5 hash       the chosen lists back to back, every lane on every 64th record: MurmurHash3 of the
+//                key out of LDS (MurmurHash3.java:18-201), 16-byte (hash, address) entries in log
+//                order into the wave's slab.
+//
+// Anything outside what the lists can hold (too many candidates, survivors or records per chunk),
+// a chunk whose entry no survivor starts at (the header understates its maxima, or the log is
+// corrupt), or a wait that does not end, makes the host redo the framing with k_frame or the
+// serial walker (Status.spec_fail).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "build_kernels.hpp"
+#include "device_common.hpp"
+#include "frame_common.hpp"
+#include "kernel_utils.hpp"
+#include "scan.hpp"
+
+namespace sk {
+
+namespace {
+
+constexpr int kF3CandCap = 512;  // candidates per wave (u16 region offsets)
+constexpr int kF3SurvCap = 64;   // chain heads after the short walk per wave (one long walk per lane)
+constexpr int kF3Lcap = 16;      // record starts a survivor lists inside its chunk
+constexpr int kF3RecCap = 512;   // records per wave hashed from the LDS list (else: slab overflow)
+constexpr int kF3ShortMax = 4;   // steps of the short walk: P.f3_short (2..4, from the header's maxima)
+constexpr unsigned kF3Caps = 64u;  // Status.spec_fail: a list cap was exceeded (k_frame redoes it)
+
+// Scratch after the staged region (bytes): candidate list, later the wave's record list; head
+// starts / exits / counts / per-chunk choice; the heads' record lists, earlier the screen bitmap and
+// then the short walk's reached-start bitmap (one bit per region byte).
+constexpr int kF3OffMeta = 2 * kF3CandCap;
+constexpr int kF3OffLists = kF3OffMeta + kF3SurvCap * 5 + 128;
+constexpr int kF3ListBytes = kF3SurvCap * kF3Lcap * 2;
+
+// One record step from region offset rp (screen rules, canonical one-byte VLQs): the next start,
+// or -1 when the bytes at rp are no plausible header.
+__device__ __forceinline__ int32_t f3_step(const uint8_t* rgn, int32_t rp, int32_t lim, int32_t mk, int32_t mv,
+                                           bool nodel) {
+  const int32_t b0 = rgn[rp], b1 = rgn[rp + 1];
+  const int32_t klen = b0 ? b0 - 1 : b1;
+  const int32_t vlen = b0 ? b1 : 0;
+  const bool ok = ((b0 | b1) & 0x80) == 0 && (b0 || !nodel) && klen <= mk && vlen <= mv && rp + 2 + klen <= lim;
+  return ok ? rp + 2 + klen + vlen : -1;
+}
+
+}  // namespace
+
+// One region (wave index wv) of k_frame3; its exit is published before any return.
+__device__ __forceinline__ void frame3_region(const BuildParams& P, const uint64_t wv, uint8_t* lds) {
+  const int lane = threadIdx.x & 63;
+  const int cs = P.fr_cshift;
+  const int W = P.fr_w;
+  const int64_t LOOK = P.fr_look;
+  const int64_t log_len = (int64_t)P.log_len;
+  const uint64_t kf = P.fr_k0;
+  const uint64_t k0 = kf + wv * (uint64_t)W;
+  const int nw = (int)min((uint64_t)W, kf + P.fr_nchunks - k0);
+  const int64_t R0 = (int64_t)(k0 << cs);
+  const int64_t RLEN = ((int64_t)nw << cs) + LOOK + 16;
+  uint8_t* rgn = lds;
+  uint8_t* scr = lds + P.fr_rgn_bytes;
+  uint16_t* cand = reinterpret_cast<uint16_t*>(scr);             // candidates, then the record list
+  uint16_t* s_start = reinterpret_cast<uint16_t*>(scr + kF3OffMeta);
+  uint16_t* s_exit = s_start + kF3SurvCap;                          // 0xffff: died in the long walk
+  uint8_t* s_cnt = reinterpret_cast<uint8_t*>(s_exit + kF3SurvCap);
+  int8_t* s_sel = reinterpret_cast<int8_t*>(s_cnt + kF3SurvCap);    // per chunk: chosen head, entry index
+  uint16_t* lists = reinterpret_cast<uint16_t*>(scr + kF3OffLists);
+  unsigned long long t_prev = P.dbg ? __builtin_amdgcn_s_memtime() : 0;
+  auto mark = [&](int i) {  // diagnostic only: cycles per phase, per wave (no atomics)
+    if (P.dbg && lane == 0) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      P.dbg[wv * 16 + i] = t - t_prev;
+      t_prev = t;
+    }
+  };
+  // the previous wave's published exit (lane 0 spins, bounded), broadcast
+  auto wait_prev = [&]() -> int64_t {
+    unsigned long long extv = (unsigned long long)P.fr_entry;
+    if (wv > 0 && lane == 0) {
+      const unsigned long long t0 = wall_clock64();
+      for (;;) {
+        const unsigned long long v = granule_load(&P.exit_desc[wv - 1]);
+        if (v & kReady) { extv = v & ~kReady; break; }
+        if (wall_clock64() - t0 >= P.fr_spin_ticks) {  // bounded all the same: serial path
+          atomicOr(&P.st->spec_fail, 2u);
+          extv = (unsigned long long)R0;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+    }
+    return (int64_t)__shfl(extv, 0, 64);
+  };
+  // every return below publishes the wave's exit first (successors wait on it): on a failure, any
+  // value (the host redoes the framing)
+  auto fail = [&](unsigned bits) {
+    if (lane == 0) {
+      atomicOr(&P.st->spec_fail, bits);
+      granule_store(&P.exit_desc[wv], (unsigned long long)R0 | kReady);
+    }
+  };
+
+  // ---- stage [R0, R0 + RLEN): every 1 KiB row in flight at once, straight into LDS ----
+  {
+    const int nvec = (int)((RLEN + 15) >> 4);
+    if (R0 + 16ll * nvec <= log_len) {
+      const uint4* src = reinterpret_cast<const uint4*>(P.log + R0);
+      for (int v0 = 0; v0 < nvec; v0 += 64)
+        __builtin_amdgcn_global_load_lds(
+            (const __attribute__((address_space(1))) void*)(src + min(v0 + lane, nvec - 1)),
+            (__attribute__((address_space(3))) void*)(rgn + 16u * (uint32_t)v0), 16, 0, 0);
+    } else {
+      for (int v = lane; v < nvec; v += 64)
+        *reinterpret_cast<uint4*>(rgn + 16u * v) = load16_guarded(P.log, R0 + 16ll * v, log_len);
+    }
+  }
+  wave_sync();
+  mark(0);
+
+  // region offsets (32-bit) of the wave's bounds
+  const int32_t de = (int32_t)min((int64_t)0x7fffffff, P.data_end - R0);  // records start below this
+  const int32_t ruse = (int32_t)(RLEN - 16);                              // headers readable below this
+  const int64_t lim64 = log_len - R0;
+  const int32_t lim = lim64 > 0x7fffffff ? 0x7fffffff : (int32_t)lim64;
+  const int32_t mk = (int32_t)P.max_key_len, mv = (int32_t)P.max_value_len;
+  const int32_t mrl = (int32_t)P.max_rec_len;
+  const int32_t look = (int32_t)LOOK;
+  const bool nodel = P.no_deletes != 0;
+  const int32_t ent0 = (int32_t)(P.fr_entry - R0);  // (wave 0) the frame's entry
+  const int32_t C = 1 << cs;
+  auto chunk_end = [&](int32_t j) -> int32_t { return min((j + 1) * C, de); };
+
+  // ---- 1 screen: one flag bit per byte of each chunk's candidate window ----
+  const int nwl = (int)((min(C, mrl) + 63) >> 6);  // 64-position words per chunk
+  unsigned long long* flags = reinterpret_cast<unsigned long long*>(scr + kF3OffLists);
+  {
+    const Screen8 scn = make_screen8(P);
+    const uint64_t* r64 = reinterpret_cast<const uint64_t*>(rgn);
+    uint8_t* fb = reinterpret_cast<uint8_t*>(flags);
+    const int wpc = nwl * 8;
+    const int nq = nw * wpc;
+    for (int q = lane; q < nq; q += 64) {
+      const int j = (int)(((uint32_t)q * P.fr_wpc_magic) >> 22);  // q / wpc (exact, checked on the host)
+      const int rw = (j << (cs - 3)) + (q - j * wpc);
+      const uint64_t x = r64[rw];
+      fb[q] = (uint8_t)screen8(x, (x >> 8) | (r64[rw + 1] << 56), scn);
+    }
+  }
+  wave_sync();
+  mark(1);
+
+  // ---- candidates, position order: word q = chunk q / nwl, positions 64 (q % nwl) + bit ----
+  int32_t T = 0;
+  bool over = false;
+  {
+    const int nq = nw * nwl;
+    for (int q0 = 0; q0 < nq; q0 += 64) {
+      const int q = q0 + lane;
+      unsigned long long m = 0;
+      int32_t base = 0;
+      if (q < nq) {
+        const int j = q / nwl, wi = q - j * nwl;
+        const int32_t s = j * C;
+        const int32_t e = chunk_end(j);
+        if (wv == 0 && j == 0) {  // the frame's entry chunk: its only start is the entry
+          m = (wi == 0 && ent0 < e) ? 1ull : 0ull;
+          base = ent0;
+        } else {
+          base = s + 64 * wi;
+          const int32_t cend = min(e, s + mrl);
+          if (base < cend) {
+            m = flags[q];
+            const int32_t valid = cend - base;
+            if (valid < 64) m &= (1ull << valid) - 1ull;
+          }
+        }
+      }
+      const uint32_t c = (uint32_t)__builtin_popcountll(m);
+      uint32_t incl = c;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += t;
+      }
+      const int32_t tot = (int32_t)__shfl(incl, 63, 64);
+      if (T + tot > kF3CandCap) {
+        over = true;
+        break;
+      }
+      uint32_t o = (uint32_t)T + incl - c;
+      while (m) {
+        cand[o++] = (uint16_t)(base + __builtin_ctzll(m));
+        m &= m - 1;
+      }
+      T += tot;
+    }
+  }
+  if (over) {
+    fail(kF3Caps);
+    return;
+  }
+  wave_sync();
+
+  // ---- 2 short walk: each candidate K records on (or to its stop); a survivor marks the starts it
+  //      reached inside its chunk (bit 15 of its list entry: alive).  More heads than the lanes
+  //      (rare: a stretch of bytes that look like headers) walk one step more. ----
+  uint32_t* reached = reinterpret_cast<uint32_t*>(scr + kF3OffLists);  // (the screen bitmap is dead)
+  int32_t S = 0;
+  for (int K = P.f3_short;; K++) {
+    for (int32_t i = lane; i < (ruse + 31) / 32 + 1; i += 64) reached[i] = 0u;
+    wave_sync();
+    for (int32_t i = lane; i < T; i += 64) {
+      const int32_t st = cand[i] & 0x7fff;
+      const int32_t j = st >> cs;
+      const int32_t e = chunk_end(j);
+      const int32_t stop = min(min(e + look, de), ruse);
+      int32_t p = st, q[kF3ShortMax];
+      bool alive = true;
+#pragma unroll
+      for (int t = 0; t < kF3ShortMax; t++) {
+        q[t] = -1;
+        if (t >= K || !alive || p >= stop) continue;
+        p = f3_step(rgn, p, lim, mk, mv, nodel);
+        if (p < 0) alive = false;
+        else q[t] = p;
+      }
+      for (int t = kF3ShortMax; t < K && alive && p < stop; t++) {  // (a second pass, rare)
+        p = f3_step(rgn, p, lim, mk, mv, nodel);
+        alive = p >= 0;
+      }
+      cand[i] = (uint16_t)(st | (alive ? 0x8000 : 0));
+      if (alive) {
+#pragma unroll
+        for (int t = 0; t < kF3ShortMax; t++)
+          if (q[t] >= 0 && q[t] < e) atomicOr(&reached[q[t] >> 5], 1u << (q[t] & 31));
+      }
+    }
+    wave_sync();
+    // heads: alive and reached from no other survivor, compacted in position order
+    S = 0;
+    over = false;
+    for (int32_t i0 = 0; i0 < T; i0 += 64) {
+      const int32_t i = i0 + lane;
+      bool head = false;
+      int32_t st = 0;
+      if (i < T) {
+        const int32_t v = cand[i];
+        st = v & 0x7fff;
+        head = (v & 0x8000) && !((reached[st >> 5] >> (st & 31)) & 1u);
+      }
+      const unsigned long long bal = __ballot(head);
+      const int32_t before = (int32_t)__builtin_popcountll(bal & ((1ull << lane) - 1ull));
+      const int32_t n = (int32_t)__builtin_popcountll(bal);
+      if (S + n > kF3SurvCap) {
+        over = true;
+        break;
+      }
+      if (head) s_start[S + before] = (uint16_t)st;
+      S += n;
+    }
+    if (!over) break;
+    if (K >= 8) {
+      fail(kF3Caps);
+      return;
+    }
+    wave_sync();
+  }
+  wave_sync();
+  mark(2);
+
+  // ---- 3 long walk: head `lane` to its chunk end + LOOK, listing its starts in the chunk ----
+  bool lovf = false;
+  if (lane < S) {
+    int32_t p = s_start[lane];
+    const int32_t j = p >> cs;
+    const int32_t e = chunk_end(j);
+    const int32_t stop = min(min(e + look, de), ruse);
+    uint16_t* my = lists + lane * kF3Lcap;
+    int32_t cnt = 0, ex = -1;
+    bool alive = true;
+    for (;;) {
+      if (p >= e && ex < 0) ex = p;
+      if (p >= stop) break;
+      if (p < e) {
+        if (cnt < kF3Lcap) my[cnt] = (uint16_t)p;
+        cnt++;
+      }
+      p = f3_step(rgn, p, lim, mk, mv, nodel);
+      if (p < 0) {
+        alive = false;
+        break;
+      }
+    }
+    if (cnt > kF3Lcap) lovf = true;
+    s_exit[lane] = alive && ex >= 0 ? (uint16_t)ex : (uint16_t)0xffff;
+    s_cnt[lane] = (uint8_t)min(cnt, 255);
+  }
+  if (__any(lovf)) {
+    fail(kF3Caps);
+    return;
+  }
+  wave_sync();
+  mark(3);
+
+  // ---- 4 resolve, lane j = chunk j.  Heads are in position order: chunk j's are a contiguous run
+  //      [c_first[j], c_last[j]].  A chunk whose alive heads all reach one exit is converged: its
+  //      exit is known without its entry.  An entry is known from a converged predecessor, or from
+  //      the predecessor's own entry (the head whose list holds it gives the exit); the frame's
+  //      first entry is the previous wave's exit. ----
+  uint8_t* c_first = reinterpret_cast<uint8_t*>(s_sel);
+  uint8_t* c_last = c_first + 64;
+  {
+    if (lane < nw) c_first[lane] = 0xff;
+    wave_sync();
+    const int32_t hc = lane < S ? ((int32_t)s_start[lane] >> cs) : 127;
+    const int32_t pc = __shfl_up(hc, 1, 64), nc = __shfl_down(hc, 1, 64);
+    if (lane < S && (lane == 0 || pc != hc)) c_first[hc] = (uint8_t)lane;
+    if (lane < S && (lane == S - 1 || nc != hc)) c_last[hc] = (uint8_t)lane;
+    wave_sync();
+  }
+  constexpr int32_t UNK = -2;
+  int32_t hf = 0, hl = -1;  // this chunk's heads
+  bool conv = false;
+  int32_t cx = UNK;
+  if (lane < nw && c_first[lane] != 0xff) {
+    hf = c_first[lane];
+    hl = c_last[lane];
+    bool any = false;
+    conv = true;
+    for (int32_t h = hf; h <= hl; h++) {
+      const int32_t ex = s_exit[h];
+      if (ex == 0xffff) continue;
+      if (!any) { cx = ex; any = true; }
+      else if (ex != cx) conv = false;
+    }
+    conv = conv && any;
+  }
+  // the head holding entry e of this chunk -> its exit (sel/at: head, index of e in its list); a
+  // chunk entered at or past its end holds no record; -1: no head holds e
+  auto find = [&](int32_t e, int32_t& sel, int32_t& at) -> int32_t {
+    sel = -1;
+    at = 0;
+    if (e >= chunk_end(lane)) return e;
+    for (int32_t g = hf; g <= hl; g++) {
+      const int32_t st = s_start[g];
+      if (st > e) break;
+      if (s_exit[g] == 0xffff) continue;
+      if (st == e) {
+        sel = g;
+        return s_exit[g];
+      }
+      const int32_t n = min((int32_t)s_cnt[g], kF3Lcap);
+      for (int32_t k = 1; k < n; k++) {
+        const int32_t v = lists[g * kF3Lcap + k];
+        if (v >= e) {
+          if (v == e) {
+            sel = g;
+            at = k;
+            return s_exit[g];
+          }
+          break;
+        }
+      }
+    }
+    return -1;
+  };
+  // entries forward from whatever is known (converged chunks; chunk 0's entry e0 when given).  The
+  // chunks resolved without e0 (pre = true) keep their result when e0 arrives or changes.
+  int32_t ent = UNK, sel = -1, at = 0, myx = UNK;
+  bool bad = false, pre = false;
+  auto resolve = [&](int32_t e0) {
+    if (!pre) {
+      ent = lane == 0 ? e0 : UNK;
+      myx = UNK;
+      sel = -1;
+      at = 0;
+      bad = false;
+    }
+    for (;;) {
+      if (lane < nw && myx == UNK && ent != UNK) {
+        myx = find(ent, sel, at);
+        if (myx < 0) bad = true;
+      }
+      const int32_t kx = myx >= 0 ? myx : (conv ? cx : UNK);
+      const int32_t inx = __shfl_up(kx, 1, 64);
+      const bool take = lane >= 1 && lane < nw && ent == UNK && inx != UNK;
+      if (take) ent = inx;
+      if (!__any(take || (lane < nw && myx == UNK && ent != UNK && !bad))) break;
+    }
+  };
+  // early exit: the wave's exit known without the first entry
+  resolve(UNK);
+  pre = lane < nw && ent != UNK && !bad;
+  int32_t early = -1;
+  {
+    const int32_t lastx = __shfl(myx >= 0 ? myx : (conv ? cx : UNK), nw - 1, 64);
+    if (wv > 0 && lastx >= 0) {
+      early = lastx;
+      if (lane == 0) granule_store(&P.exit_desc[wv], (unsigned long long)(R0 + early) | kReady);
+    }
+  }
+  // the first entry: the previous wave's exit; with one alive head in chunk 0, speculatively its start
+  int32_t spec_e0 = -1;
+  if (lane == 0 && wv > 0) {
+    int32_t n0 = 0;
+    for (int32_t h = hf; h <= hl; h++)
+      if (s_exit[h] != 0xffff) {
+        n0++;
+        spec_e0 = s_start[h];
+      }
+    if (n0 != 1) spec_e0 = -1;
+  }
+  spec_e0 = __shfl(spec_e0, 0, 64);
+  bool spec = spec_e0 >= 0;
+  int64_t ext = wv == 0 ? P.fr_entry : (spec ? R0 + spec_e0 : wait_prev());
+  mark(4);
+  unsigned long long ndel = 0;
+  for (;;) {
+    const int64_t e0 = ext - R0;
+    resolve(e0 < 0 || e0 > 0x7fff ? UNK : (int32_t)e0);
+    // every chunk resolved, and each exit the next chunk's entry
+    const int32_t nxt = __shfl_down(ent, 1, 64);
+    const bool broken = lane < nw && (bad || myx < 0 || (lane + 1 < nw && nxt != myx));
+    const int32_t wexit = __shfl(myx, nw - 1, 64);
+    if (__any(broken) || (early >= 0 && early != wexit)) {
+      if (spec) {  // the guessed entry may be wrong: decide on the published one
+        const int64_t real = wait_prev();
+        spec = false;
+        if (real != ext) {
+          ext = real;
+          continue;
+        }
+      }
+      if (early < 0) fail(1u);
+      else if (lane == 0) atomicOr(&P.st->spec_fail, 1u);
+      return;
+    }
+    if (early < 0 && lane == 0) granule_store(&P.exit_desc[wv], (unsigned long long)(R0 + wexit) | kReady);
+    if (lane == 0 && wv + 1 == (P.fr_nchunks + P.fr_w - 1) / P.fr_w) P.st->exit = R0 + wexit;
+    // ---- counts: chunk `lane`'s records, their wave scan ----
+    const uint32_t cnt = sel >= 0 ? (uint32_t)(s_cnt[sel] - at) : 0u;
+    uint32_t incl = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t t = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += t;
+    }
+    const uint32_t total = __shfl(incl, 63, 64);
+    if (total > (uint32_t)kF3RecCap) {  // (the host ruled this out from the header's mean record)
+      if (lane == 0) atomicOr(&P.st->spec_fail, kF3Caps);
+      return;
+    }
+    if (total > P.slab_cap) {
+      if (spec) {
+        const int64_t real = wait_prev();
+        spec = false;
+        if (real != ext) {
+          ext = real;
+          continue;
+        }
+      }
+      if (lane == 0) {
+        atomicMax(&P.st->max_wave_count, total);
+        atomicOr(&P.st->overflow, 1u);
+      }
+      return;
+    }
+    if (lane == 0) P.wcount[wv] = total;
+    {  // the chosen lists back to back (the candidate list is dead), four independent reads a step
+      const uint32_t o = incl - cnt;
+      const uint16_t* src = lists + sel * kF3Lcap + at;
+      for (uint32_t i = 0; i < cnt; i += 4) {
+        uint16_t v[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) v[u] = i + u < cnt ? src[i + u] : 0;
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+          if (i + u < cnt) cand[o + i + u] = v[u];
+      }
+    }
+    wave_sync();
+    mark(5);
+    // ---- 5 hash ----
+    const unsigned long long base = wv * (unsigned long long)P.slab_cap;
+    ndel = 0;
+    for (uint32_t r = (uint32_t)lane; r < total; r += 64) {
+      const int64_t p = R0 + (int64_t)cand[r];
+      const RecHdr h = decode_rgn(rgn, R0, p, log_len);
+      const int64_t kp = p + h.hlen;
+      uint64_t hash;
+      if (kp + h.klen + 16 <= R0 + RLEN) {  // key in the region
+        const RgnKey ld{rgn, (uint32_t)(kp - R0)};
+        hash = P.hash_size == 8 ? murmur64_ld(ld, h.klen, (uint32_t)P.seed) : (uint64_t)murmur32_ld(ld, h.klen, (uint32_t)P.seed);
+      } else if (kp + h.klen + 16 <= log_len) {
+        const GlobalKey ld{P.log + kp};
+        hash = P.hash_size == 8 ? murmur64_ld(ld, h.klen, (uint32_t)P.seed) : (uint64_t)murmur32_ld(ld, h.klen, (uint32_t)P.seed);
+      } else {
+        hash = key_hash(P.hash_size, P.log + kp, h.klen, (uint32_t)P.seed);
+      }
+      uint64_t addr = (uint64_t)p << P.ebb;
+      if (!h.put) {
+        addr |= kDelBit;
+        ndel++;
+      }
+      Entry en;
+      en.hash = hash;
+      en.addr = addr;
+      P.ent[base + r] = en;
+    }
+    if (spec) {  // check the guessed entry against the published exit; redo on a mismatch
+      const int64_t real = wait_prev();
+      spec = false;
+      if (real != ext) {
+        ext = real;
+        wave_sync();  // (the record list is rewritten)
+        continue;
+      }
+    }
+    break;
+  }
+  ndel = wave_sum_u64(ndel);
+  if (ndel && lane == 0) atomicAdd(&P.st->n_deletes, ndel);
+  mark(6);
+  if (P.dbg && lane == 0) {
+    P.dbg[wv * 16 + 8] = (unsigned long long)T;
+    P.dbg[wv * 16 + 9] = (unsigned long long)S;
+    P.dbg[wv * 16 + 10] = early >= 0 ? 0ull : 1ull;
+  }
+}
+
+// kFrameWaves waves per workgroup, one region each, regions by workgroup ticket (see k_frame).
+__global__ __launch_bounds__(64 * kFrameWaves) void k_frame3(BuildParams P, uint32_t lds_per_wave) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  __shared__ unsigned int tk;
+  if (threadIdx.x == 0) tk = atomicAdd(P.frame_ticket, 1u);
+  __syncthreads();
+  const uint64_t nwaves = (P.fr_nchunks + P.fr_w - 1) / P.fr_w;
+  const uint32_t w = threadIdx.x >> 6;
+  const uint64_t wv = (uint64_t)tk * kFrameWaves + w;
+  if (wv < nwaves) frame3_region(P, wv, lds + w * lds_per_wave);
+}
+
+// LDS per wave: the staged region, then the scratch (candidates / record list, survivor data, lists
+// or the screen bitmap).
+uint32_t frame3_lds_per_wave(const BuildParams& P) {
+  const size_t bitmap = (size_t)P.fr_w * (size_t)((std::min<int64_t>(1ll << P.fr_cshift, P.max_rec_len) + 63) / 64) * 8;
+  const size_t reached = (size_t)((((int64_t)P.fr_w << P.fr_cshift) + P.fr_look + 31) / 32 + 1) * 4;
+  const size_t scratch = (size_t)kF3OffLists + std::max<size_t>(std::max<size_t>(bitmap, reached), (size_t)kF3ListBytes);
+  return (uint32_t)(((size_t)P.fr_rgn_bytes + scratch + 15) & ~(size_t)15);
+}
+
+bool frame3_fits(const BuildParams& P, double mean_record, double pass) {
+  // every chunk's records must fit a head's list, a wave's records the record list, and a wave's
+  // candidates (pass = the chance that a random byte pair passes the screen) the candidate list
+  const double C = (double)(1ll << P.fr_cshift);
+  if (!P.fr_fast || P.max_rec_len > 4096 || P.fr_cshift < 7) return false;
+  if (mean_record <= 0.0 || C / mean_record > 0.6 * kF3Lcap) return false;
+  if ((double)P.fr_w * C / mean_record > 0.6 * kF3RecCap) return false;
+  if ((double)P.fr_w * (double)std::min<int64_t>(1ll << P.fr_cshift, P.max_rec_len) * pass > 0.6 * kF3CandCap)
+    return false;
+  return ((int64_t)P.fr_w << P.fr_cshift) + P.fr_look + 16 < 32768;  // 15-bit region offsets
+}
+
+void launch_frame3(const BuildParams& P, hipStream_t s, StageTimer* tm) {
+  if (P.fr_nchunks == 0) return;
+  const uint64_t nwaves = (P.fr_nchunks + P.fr_w - 1) / P.fr_w;
+  const uint32_t per = frame3_lds_per_wave(P);
+  hipLaunchKernelGGL(k_frame3, dim3((unsigned)((nwaves + kFrameWaves - 1) / kFrameWaves)), dim3(64 * kFrameWaves),
+                     (size_t)per * kFrameWaves, s, P, per);
+  tm->mark("frame", s);
+  scan_exclusive<uint32_t, uint64_t, OpAdd>(P.wcount, P.woff, P.nslabs, (uint64_t*)&P.st->n_records, OpAdd(),
+                                            P.scan_scratch_u64, s);
+}
+
+}  // namespace sk

@@ -1424,8 +1424,10 @@ void launch_frame_fused(const BuildParams& P, hipStream_t s, StageTimer* tm) {
   // candidate list and then by the record list
   const size_t lds = (size_t)P.fr_rgn_bytes + std::max<size_t>((size_t)P.fr_w * P.fr_mask_words * 8 + 8, kCandCap * 4);
   const uint32_t per = (uint32_t)((lds + 15) & ~(size_t)15);
+  // (SPARKEY_FRAME_LDS_PAD: extra LDS per workgroup, to measure the phases at lower occupancy)
+  const size_t pad = getenv("SPARKEY_FRAME_LDS_PAD") ? (size_t)atoll(getenv("SPARKEY_FRAME_LDS_PAD")) : 0;
   hipLaunchKernelGGL(k_frame, dim3((unsigned)((nwaves + kFrameWaves - 1) / kFrameWaves)), dim3(64 * kFrameWaves),
-                     (size_t)per * kFrameWaves, s, P, per);
+                     (size_t)per * kFrameWaves + pad, s, P, per);
   tm->mark("frame", s);  // the stage is k_frame alone (its rocprof row); the slab scan counts as partition
   scan_exclusive<uint32_t, uint64_t, OpAdd>(P.wcount, P.woff, P.nslabs, (uint64_t*)&P.st->n_records, OpAdd(),
                                             P.scan_scratch_u64, s);

@@ -197,7 +197,7 @@ __global__ __launch_bounds__(256) void k_shard_row_async(ShardScalars sc, const 
   const int t = threadIdx.x;
   const unsigned long long e = st->err;
   const unsigned long long n = st->n_records, nd = st->n_deletes;
-  const bool spec = path == 0 || path == 3;
+  const bool spec = slab_framing(path);
   const bool retry = (spec && st->max_wave_count > slab_cap) || st->overflow || n > max_records ||
                      st->spec_fail != 0 || (path != 1 && e != ~0ull) || n > send_cap;
   const int rc = e != ~0ull ? -(int)(e & 0xff) : 0;

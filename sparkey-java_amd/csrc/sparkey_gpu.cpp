@@ -514,6 +514,49 @@ static int setup_params(const LogHdr& lh, const IndexParams& ip, const sparkey_b
 // one-byte VLQs, and putSize == numPuts * R == dataEnd - 84 with R the largest PUT record the header
 // allows (each record is at most R bytes and together they fill putSize).  Else 0.
 // SPARKEY_NO_UNIFORM disables it (tests and the bench's general-framing measurement).
+// k_frame3 (frame3_kernels.hip) frames the log when its VLQs are one byte and the header's mean
+// record lets a chunk's records and a wave's records fit k_frame3's lists (SPARKEY_NO_FRAME3: k_frame).
+// Its chunk: the power of two >= maxRecLen near 4 mean records (a long walk of about four steps, and
+// a chunk's candidate window a small part of it), SPARKEY_FRAME3_C overrides; 8 KiB of chunks per
+// wave (SPARKEY_FRAME_REGION).  The geometry is set on P when k_frame3 is chosen (k_frame can frame
+// with it too, which its fallback does).
+static bool want_frame3(BuildParams& P, const LogHdr& lh, int64_t entry, int64_t frame_end) {
+  if (getenv("SPARKEY_NO_FRAME3") || !P.fr_fast || P.max_rec_len > 4096) return false;
+  const int64_t nr = std::max<int64_t>(0, lh.num_puts) + std::max<int64_t>(0, lh.num_deletes);
+  const int64_t by = std::max<int64_t>(0, lh.put_size) + std::max<int64_t>(0, lh.delete_size);
+  if (nr <= 0 || by <= 0) return false;
+  const double mean = (double)by / (double)nr;
+  int64_t want = std::max<int64_t>(std::max<int64_t>(P.max_rec_len, 128), (int64_t)std::ceil(4.0 * mean));
+  if (const char* v = getenv("SPARKEY_FRAME3_C")) want = std::max<int64_t>(P.max_rec_len, atoll(v));
+  int cs = 7;
+  while ((1ll << cs) < want) cs++;
+  while (cs > 7 && (double)(1ll << cs) / mean > 8.0 && (1ll << (cs - 1)) >= P.max_rec_len) cs--;
+  int64_t region = 8192;
+  if (const char* v = getenv("SPARKEY_FRAME_REGION")) region = std::min<int64_t>(16384, std::max<int64_t>(2048, atoll(v)));
+  BuildParams Q = P;
+  const int64_t C = 1ll << cs;
+  Q.fr_cshift = cs;
+  Q.fr_w = (int32_t)std::max<int64_t>(1, std::min<int64_t>(64, region / C));
+  Q.fr_rgn_bytes = (int32_t)(((int64_t)Q.fr_w * C + Q.fr_look + 16 + 1023) & ~1023LL);
+  Q.fr_mask_words = (int32_t)((std::min<int64_t>(C, Q.max_rec_len) + 63) / 64);
+  const uint32_t wpc = 8u * (uint32_t)Q.fr_mask_words;
+  Q.fr_wpc_magic = (uint32_t)(((1ull << 22) + wpc - 1) / wpc);
+  for (uint32_t q = 0; q < (uint32_t)Q.fr_w * wpc; q++)
+    if ((uint32_t)(((uint64_t)q * Q.fr_wpc_magic) >> 22) != q / wpc || (uint64_t)q * Q.fr_wpc_magic >= (1ull << 32))
+      return false;
+  Q.fr_k0 = (uint64_t)entry >> cs;
+  Q.fr_nchunks = frame_end > entry ? (uint64_t)((frame_end + C - 1) / C) - Q.fr_k0 : 0;
+  // a random byte pair passes the screen with about p = (maxKeyLen + 1) / 256 * (maxValueLen + 1) / 256
+  // (more with DELETEs); the short walk's K steps leave p^K of the false starts
+  const double pk = std::min(1.0, (double)(Q.max_key_len + 1) / 256.0) * std::min(1.0, (double)(Q.max_value_len + 1) / 256.0) +
+                    (Q.no_deletes ? 0.0 : std::min(1.0, (double)(Q.max_key_len + 1) / 256.0) / 256.0);
+  if (!frame3_fits(Q, mean, pk)) return false;
+  Q.f3_short = pk < 0.12 ? 2 : pk < 0.3 ? 3 : 4;
+  if (const char* v = getenv("SPARKEY_FRAME3_SHORT")) Q.f3_short = std::max(1, std::min(4, atoi(v)));
+  P = Q;
+  return true;
+}
+
 static int64_t uniform_record_size(const LogHdr& lh) {
   const int64_t R =
       vlq_size_long(lh.max_key_len + 1) + vlq_size_long(lh.max_value_len) + lh.max_key_len + lh.max_value_len;
@@ -568,7 +611,7 @@ static FrameGeom frame2_geometry(BuildParams& P, int64_t entry, int64_t frame_en
 static int reserve_for_framing(sparkey_plan* pl, BuildParams& P, int framing_path, uint64_t nrec, uint32_t slab_cap,
                                char* err, size_t err_len) {
   const uint64_t nwaves = P.fr_nchunks ? (P.fr_nchunks + P.fr_w - 1) / P.fr_w : 0;
-  if (framing_path == 0 || framing_path == 3) {
+  if (slab_framing(framing_path)) {
     P.slab_cap = slab_cap;
     P.nslabs = nwaves;
   } else {  // dense entries from the serial framing path, seen as slabs of kPartTile
@@ -602,10 +645,11 @@ static int reserve_for_framing(sparkey_plan* pl, BuildParams& P, int framing_pat
 static int launch_framing(sparkey_plan* pl, const BuildParams& P, int framing_path, hipStream_t s, char* err,
                           size_t err_len) {
   const uint64_t nwaves = P.fr_nchunks ? (P.fr_nchunks + P.fr_w - 1) / P.fr_w : 0;
-  if (framing_path == 0 || framing_path == 3) {
+  if (slab_framing(framing_path)) {
     HIP_TRY(hipMemsetAsync(pl->desc, 0, (2 * nwaves + 2) * sizeof(unsigned long long), s));
     HIP_TRY(hipMemsetAsync(pl->wcount, 0, (P.nslabs + 1) * sizeof(uint32_t), s));
     if (framing_path == 3) launch_frame2(P, s, &pl->timer);
+    else if (framing_path == 4) launch_frame3(P, s, &pl->timer);
     else launch_frame_fused(P, s, &pl->timer);
   } else if (framing_path == 2) {
     launch_frame_uniform(P, s, &pl->timer);
@@ -949,8 +993,6 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
 
   // k_frame2 for records of mixed sizes (the header's mean record at least 24 bytes), k_frame for
   // the rest; both fall back to the serial walk
-  const FrameGeom geom0 = get_geom(P);
-  const FrameGeom geom2 = frame2_geometry(P, kLogHeaderSize, std::max<int64_t>(lh.data_end, kLogHeaderSize));
   bool use_frame2 = fused_framing && getenv("SPARKEY_FRAME2") != nullptr;  // (measured slower than k_frame so far)
   {
     const int64_t nr = std::max<int64_t>(0, lh.num_puts) + std::max<int64_t>(0, lh.num_deletes);
@@ -959,7 +1001,13 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
     // plausible chains of 2-byte records, which k_frame's per-chunk screen handles better)
     if ((nr > 0 && by < 24 * nr) || lh.num_deletes != 0) use_frame2 = false;
   }
-  int framing_path = fused_framing ? (use_frame2 ? 3 : 0) : 1, placement_path = 0;
+  // k_frame3 for one-byte-VLQ logs whose chunks hold a few records each (its lists' sizes)
+  const bool use_frame3 = fused_framing && !use_frame2 &&
+                          want_frame3(P, lh, kLogHeaderSize, std::max<int64_t>(lh.data_end, kLogHeaderSize));
+  const FrameGeom geom0 = get_geom(P);
+  const FrameGeom geom2 = frame2_geometry(P, kLogHeaderSize, std::max<int64_t>(lh.data_end, kLogHeaderSize));
+  const int spec_path = fused_framing ? (use_frame2 ? 3 : (use_frame3 ? 4 : 0)) : 1;
+  int framing_path = spec_path, placement_path = 0;
   if (const int64_t R = uniform_record_size(lh)) {  // k_frame_uniform: every record is exactly R bytes
     framing_path = 2;
     P.uni_n = (uint64_t)lh.num_puts;
@@ -980,7 +1028,7 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
   const bool fold = getenv("SPARKEY_NO_FOLD_STATS") == nullptr;  // stats from k_place_lds, no k_stats pass
   for (int attempt = 0; attempt < 6; attempt++) {
     set_geom(P, framing_path == 3 ? geom2 : geom0);
-    if ((framing_path == 0 || framing_path == 3) && framing_path != slab_path) {
+    if (slab_framing(framing_path) && framing_path != slab_path) {
       slab_cap = slab_for(framing_path == 3 ? geom2 : geom0);
       slab_path = framing_path;
     }
@@ -1047,7 +1095,7 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
     HIP_TRY(hipEventElapsedTime(&ms, pl->ev0, pl->ev1));
     print_frame_debug(pl, P);
     print_place_debug(P);
-    if ((framing_path == 0 || framing_path == 3) && st.max_wave_count > slab_cap) {  // a wave overflowed its slab
+    if (slab_framing(framing_path) && st.max_wave_count > slab_cap) {  // a wave overflowed its slab
       slab_cap = (uint32_t)std::min<uint64_t>(kPartTile, ((uint64_t)st.max_wave_count + 63) & ~63ull);
       continue;
     }
@@ -1062,6 +1110,10 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
     if (getenv("SPARKEY_FRAME_DEBUG") && (st.spec_fail || st.err != ~0ull))
       fprintf(stderr, "[framing] path %d: spec_fail %u err %llx (pos %llu)\n", framing_path, st.spec_fail,
               (unsigned long long)st.err, (unsigned long long)(st.err >> 8));
+    if (framing_path == 4 && (st.spec_fail || st.err != ~0ull)) {  // k_frame3's lists or speculation: k_frame
+      framing_path = 0;
+      continue;
+    }
     if ((framing_path == 0 || framing_path == 3) && (st.spec_fail || st.err != ~0ull)) {  // only the serial walk reports
       framing_path = 1;
       continue;
@@ -1075,7 +1127,7 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
       continue;
     }
     if (framing_path == 2 && st.spec_fail) {  // a record differs from the header's uniform shape
-      framing_path = fused_framing ? (use_frame2 ? 3 : 0) : 1;
+      framing_path = spec_path;
       continue;
     }
     break;
@@ -1620,7 +1672,8 @@ int sparkey_shard_find_entry(sparkey_plan* pl, uint64_t lo, uint64_t window, voi
 // synchronous sparkey_shard_frame and the speculative sparkey_shard_frame_bin_async).
 struct ShardFrameSetup {
   BuildParams P;
-  bool fused = false, use_frame2 = false, use_regions = true;
+  bool fused = false, use_frame2 = false, use_frame3 = false, use_regions = true;
+  int spec_path() const { return fused ? (use_frame2 ? 3 : (use_frame3 ? 4 : 0)) : 1; }
   int framing_path = 1;
   uint64_t nrec = 0;
   FrameGeom geom0, geom2;
@@ -1647,15 +1700,16 @@ static int shard_frame_setup(sparkey_plan* pl, int64_t entry, int64_t frame_end,
   const double frac = (double)(frame_end - entry) / (double)std::max<int64_t>(1, data_end - kLogHeaderSize);
   F->nrec = (uint64_t)((double)(std::max<int64_t>(0, sh.lh.num_puts) + std::max<int64_t>(0, sh.lh.num_deletes)) *
                        frac * 1.05) + 4096;
-  F->geom0 = get_geom(P);
-  F->geom2 = frame2_geometry(P, entry, frame_end);
   F->use_frame2 = F->fused && getenv("SPARKEY_FRAME2") != nullptr;
   {
     const int64_t nr = std::max<int64_t>(0, sh.lh.num_puts) + std::max<int64_t>(0, sh.lh.num_deletes);
     const int64_t by = std::max<int64_t>(0, sh.lh.put_size) + std::max<int64_t>(0, sh.lh.delete_size);
     if ((nr > 0 && by < 24 * nr) || sh.lh.num_deletes != 0) F->use_frame2 = false;
   }
-  F->framing_path = F->fused ? (F->use_frame2 ? 3 : 0) : 1;
+  F->use_frame3 = F->fused && !F->use_frame2 && want_frame3(P, sh.lh, entry, frame_end);
+  F->geom0 = get_geom(P);
+  F->geom2 = frame2_geometry(P, entry, frame_end);
+  F->framing_path = F->spec_path();
   const int64_t R = uniform_record_size(sh.lh);
   if (R && (entry - kLogHeaderSize) % R == 0) {  // a record start of a uniform log: frame by stride
     F->framing_path = 2;
@@ -1673,7 +1727,7 @@ static int shard_frame_setup(sparkey_plan* pl, int64_t entry, int64_t frame_end,
 static int shard_frame_launch(sparkey_plan* pl, ShardFrameSetup* F, hipStream_t s, char* err, size_t err_len) {
   BuildParams& P = F->P;
   set_geom(P, F->framing_path == 3 ? F->geom2 : F->geom0);
-  if ((F->framing_path == 0 || F->framing_path == 3) && F->framing_path != F->slab_path) {
+  if (slab_framing(F->framing_path) && F->framing_path != F->slab_path) {
     F->slab_cap = shard_slab_for(F->framing_path == 3 ? F->geom2 : F->geom0, F->nrec);
     F->slab_path = F->framing_path;
   }
@@ -1735,7 +1789,7 @@ int sparkey_shard_frame(sparkey_plan* pl, int64_t entry, int64_t frame_end, void
     rc = shard_sync_status(pl, s, err, err_len);
     if (rc) return rc;
     const int path = F.framing_path;
-    if ((path == 0 || path == 3) && st.max_wave_count > F.slab_cap) {
+    if (slab_framing(path) && st.max_wave_count > F.slab_cap) {
       F.slab_cap = (uint32_t)std::min<uint64_t>(kPartTile, ((uint64_t)st.max_wave_count + 63) & ~63ull);
       continue;
     }
@@ -1744,6 +1798,10 @@ int sparkey_shard_frame(sparkey_plan* pl, int64_t entry, int64_t frame_end, void
       continue;
     }
     if (path == 3 && (st.spec_fail & 16u) && st.err == ~0ull) {  // a segment's record list overflowed
+      F.framing_path = 0;
+      continue;
+    }
+    if (path == 4 && (st.spec_fail || st.err != ~0ull)) {
       F.framing_path = 0;
       continue;
     }
@@ -1756,7 +1814,7 @@ int sparkey_shard_frame(sparkey_plan* pl, int64_t entry, int64_t frame_end, void
       continue;
     }
     if (path == 2 && st.spec_fail) {  // not the uniform log its header describes
-      F.framing_path = F.fused ? (F.use_frame2 ? 3 : 0) : 1;
+      F.framing_path = F.spec_path();
       continue;
     }
     break;

@@ -12,6 +12,7 @@ from helpers import diff_report, index_header, key_value_puts, make_log, random_
 pytestmark = pytest.mark.gpu
 
 IN_MEMORY, SORTING = 1, 2
+SPEC = (0, 4)  # the speculative framing of mixed-size records: k_frame, or k_frame3 (one-byte VLQs)
 
 
 def gpu_build(native, log, seed, hash_size=0, method=IN_MEMORY, sparsity=0.0):
@@ -191,7 +192,7 @@ def test_records_spanning_chunks(native, vlen):
     log with the serial walker (few records per byte)."""
     puts = [(b"key%d" % i, bytes([i % 251]) * (vlen + (i % 7))) for i in range(300)]
     got, stats = check(native, make_log(puts), 12, hash_size=8)
-    assert stats.framing_path == (0 if vlen + 6 + 16 < 4096 else 1)
+    assert stats.framing_path in (SPEC if vlen + 6 + 16 < 4096 else (1,))
 
 
 def test_understated_max_key_len_is_an_error(native):
@@ -225,6 +226,7 @@ def test_tiny_records_stay_on_fast_framing(native):
                                  {"SPARKEY_FRAME_LOOK": "16"}, {"SPARKEY_FRAME_LOOK": "1024"}])
 def test_frame_geometry_overrides(native, monkeypatch, env):
     monkeypatch.setenv("SPARKEY_NO_UNIFORM", "1")  # the fixed-size log would take k_frame_uniform
+    monkeypatch.setenv("SPARKEY_NO_FRAME3", "1")   # k_frame's geometry (k_frame3: test_frame3_geometry)
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     rng = np.random.default_rng(3)
@@ -263,7 +265,7 @@ def test_frame2_list_overflow_falls_back_to_k_frame(native, monkeypatch):
             uniq.append((k, v))
     monkeypatch.setenv("SPARKEY_FRAME2", "1")
     got, stats = check(native, make_log(uniq), 53, hash_size=8)
-    assert stats.framing_path == 0, stats.as_dict()
+    assert stats.framing_path in SPEC, stats.as_dict()
 
 
 def test_frame2_with_overwrites(native, monkeypatch):
@@ -282,7 +284,7 @@ def test_deletes_take_k_frame(native, monkeypatch):
     """A log with DELETEs (0x00 starts a record) and zero-filled values frames with k_frame."""
     ops = _churn_ops(60000, 20000, 0.1, 57, klen=(8, 40), vlen=(20, 90))
     got, stats = check(native, make_log(ops=ops), 59, hash_size=8)
-    assert stats.framing_path == 0 and stats.placement_path == 2, stats.as_dict()
+    assert stats.framing_path in SPEC and stats.placement_path == 2, stats.as_dict()
 
 
 # --- k_frame's bounded wait on the previous wave: a tripped wait reruns the build on the serial path ---
@@ -294,7 +296,7 @@ def test_frame_wait_timeout_falls_back_to_serial(native, monkeypatch):
     assert stats.framing_path == 1, stats.as_dict()
     monkeypatch.delenv("SPARKEY_FRAME_SPIN_TICKS")
     got2, stats2 = check(native, make_log(puts), 37, hash_size=8)
-    assert stats2.framing_path == 0 and got2 == got
+    assert stats2.framing_path in SPEC and got2 == got
 
 
 # --- exact path (DELETEs, overwrites) over independent slot segments vs the single-lane replay ---
@@ -400,7 +402,7 @@ def test_uniform_header_but_record_split_differs(native):
     struct.pack_into("<q", log, 40, 16)  # maxKeyLen stays 16, maxValueLen stays 31 ...
     struct.pack_into("<q", log, 48, 30)  # ... declare maxValueLen 30 so putSize == n * (2 + 16 + 30)
     got, stats = check(native, bytes(log), 7, hash_size=8)
-    assert stats.framing_path == 0, stats.as_dict()
+    assert stats.framing_path in SPEC, stats.as_dict()
 
 
 def test_uniform_disabled_gives_same_bytes(native, monkeypatch):
@@ -408,7 +410,7 @@ def test_uniform_disabled_gives_same_bytes(native, monkeypatch):
     a, sa = gpu_build(native, log, 11, 8)
     monkeypatch.setenv("SPARKEY_NO_UNIFORM", "1")
     b, sb = gpu_build(native, log, 11, 8)
-    assert sa.framing_path == 2 and sb.framing_path == 0 and a == b
+    assert sa.framing_path == 2 and sb.framing_path in SPEC and a == b
 
 
 @pytest.mark.parametrize("region_cap", ["60000", "1"])
@@ -497,3 +499,68 @@ def test_log_append_then_build(native):
     app.close()
     assert log == make_log(key_value_puts(1000, b"key_%d", b"value_%d"), file_id=0x0C1C1C1C, block_size=1024)
     check(native, log, 1234)
+
+
+# --- k_frame3: the short/long walk framing of one-byte-VLQ logs ---
+@pytest.mark.parametrize("env", [{}, {"SPARKEY_FRAME3_C": "256"}, {"SPARKEY_FRAME3_C": "512"},
+                                 {"SPARKEY_FRAME3_C": "2048"}, {"SPARKEY_FRAME_REGION": "16384"},
+                                 {"SPARKEY_FRAME_LOOK": "16"}, {"SPARKEY_FRAME_LOOK": "1024"}])
+def test_frame3_geometry(native, monkeypatch, env):
+    """Chunk sizes, regions and look-aheads: the same bytes; k_frame3 frames in the default geometry
+    (a geometry whose lists cannot hold a chunk's records reruns with k_frame)."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    for seed, (kmin, kmax, vmin, vmax), hs in [(61, (8, 64, 100, 100), 8), (63, (1, 40, 20, 60), 4),
+                                               (67, (10, 100, 0, 60), 8)]:
+        puts = random_puts(25000, seed=seed, kmin=kmin, kmax=kmax, vmin=vmin, vmax=vmax)
+        got, stats = check(native, make_log(puts), seed, hash_size=hs)
+        assert stats.framing_path == 4 if not env else stats.framing_path in SPEC, stats.as_dict()
+
+
+def test_frame3_matches_k_frame(native, monkeypatch):
+    """The same mixed log through k_frame3 and k_frame: identical bytes (and the oracle's)."""
+    puts = random_puts(60000, seed=71, kmin=8, kmax=64, vmin=100, vmax=100)
+    log = make_log(puts)
+    a, sa = check(native, log, 71, hash_size=8)
+    monkeypatch.setenv("SPARKEY_NO_FRAME3", "1")
+    b, sb = gpu_build(native, log, 71, 8)
+    assert sa.framing_path == 4 and sb.framing_path == 0 and a == b
+
+
+def test_frame3_with_deletes_and_overwrites(native):
+    """DELETE records (0x00 then starts a record) and overwritten keys through k_frame3; the exact
+    replay places."""
+    ops = _churn_ops(60000, 20000, 0.1, 73, klen=(8, 40), vlen=(20, 90))
+    got, stats = check(native, make_log(ops=ops), 73, hash_size=8)
+    assert stats.framing_path in SPEC and stats.placement_path == 2, stats.as_dict()
+
+
+def test_frame3_list_caps_fall_back(native):
+    """A stretch of 2-3 byte records in a log of long ones: more records in a chunk than k_frame3's
+    lists hold, so the build reruns with k_frame (same bytes)."""
+    puts = random_puts(4000, seed=75, kmin=30, kmax=60, vmin=100, vmax=120)
+    puts += [(bytes([i & 0xFF, i >> 8]), b"") for i in range(3000)]
+    puts += random_puts(4000, seed=76, kmin=30, kmax=60, vmin=100, vmax=120)
+    seen, uniq = set(), []
+    for k, v in puts:
+        if k not in seen:
+            seen.add(k)
+            uniq.append((k, v))
+    got, stats = check(native, make_log(uniq), 77, hash_size=8)
+    assert stats.framing_path in SPEC, stats.as_dict()
+
+
+def test_frame3_understated_header(native):
+    """maxValueLen understated: the screen prunes true starts, k_frame3's chain finds no survivor at
+    some entry, the build reruns (k_frame, then the serial walk) and still matches the oracle."""
+    import struct
+    log = bytearray(make_log(random_puts(20000, seed=79, kmin=8, kmax=64, vmin=90, vmax=110)))
+    struct.pack_into("<q", log, 48, 95)
+    check(native, bytes(log), 79, hash_size=8)
+
+
+def test_frame3_wait_timeout(native, monkeypatch):
+    monkeypatch.setenv("SPARKEY_FRAME_SPIN_TICKS", "0")
+    puts = random_puts(120000, seed=81, kmin=8, kmax=64, vmin=100, vmax=100)
+    got, stats = check(native, make_log(puts), 83, hash_size=8)
+    assert stats.framing_path == 1, stats.as_dict()
