@@ -195,6 +195,8 @@ struct BuildParams {
   int32_t f2_lcap;
   int32_t f2_rgn_bytes;
   int32_t f3_short;  // k_frame3 (frame3_kernels.hip): steps of the short walk
+  int32_t f3_cover;  // k_frame3: mark the starts the short walk reached (windows hold several true starts)
+  int32_t f3_stop;   // SPARKEY_FRAME3_STOP: k_frame3 gives up after this phase (instruction counts by phase)
   // uniform-stride framing (k_frame_uniform): uni_n records of uni_rec bytes from fr_entry
   uint64_t uni_n;
   int64_t uni_rec;

@@ -54,7 +54,6 @@ constexpr int kF3CandCap = 512;  // candidates per wave (u16 region offsets)
 constexpr int kF3SurvCap = 64;   // chain heads after the short walk per wave (one long walk per lane)
 constexpr int kF3Lcap = 16;      // record starts a survivor lists inside its chunk
 constexpr int kF3RecCap = 512;   // records per wave hashed from the LDS list (else: slab overflow)
-constexpr int kF3ShortMax = 4;   // steps of the short walk: P.f3_short (2..4, from the header's maxima)
 constexpr unsigned kF3Caps = 64u;  // Status.spec_fail: a list cap was exceeded (k_frame redoes it)
 
 // Scratch after the staged region (bytes): candidate list, later the wave's record list; head
@@ -148,6 +147,7 @@ __device__ __forceinline__ void frame3_region(const BuildParams& P, const uint64
   }
   wave_sync();
   mark(0);
+  if (P.f3_stop == 0) { fail(kF3Caps); return; }  // (SPARKEY_FRAME3_STOP: measurements)
 
   // region offsets (32-bit) of the wave's bounds
   const int32_t de = (int32_t)min((int64_t)0x7fffffff, P.data_end - R0);  // records start below this
@@ -180,6 +180,7 @@ __device__ __forceinline__ void frame3_region(const BuildParams& P, const uint64
   }
   wave_sync();
   mark(1);
+  if (P.f3_stop == 1) { fail(kF3Caps); return; }  // (SPARKEY_FRAME3_STOP: measurements)
 
   // ---- candidates, position order: word q = chunk q / nwl, positions 64 (q % nwl) + bit ----
   int32_t T = 0;
@@ -237,58 +238,70 @@ __device__ __forceinline__ void frame3_region(const BuildParams& P, const uint64
   //      reached inside its chunk (bit 15 of its list entry: alive).  More heads than the lanes
   //      (rare: a stretch of bytes that look like headers) walk one step more. ----
   uint32_t* reached = reinterpret_cast<uint32_t*>(scr + kF3OffLists);  // (the screen bitmap is dead)
+  const bool cover = P.f3_cover != 0;  // (windows that hold several true starts: mark the reached ones)
   int32_t S = 0;
   for (int K = P.f3_short;; K++) {
-    for (int32_t i = lane; i < (ruse + 31) / 32 + 1; i += 64) reached[i] = 0u;
-    wave_sync();
-    for (int32_t i = lane; i < T; i += 64) {
-      const int32_t st = cand[i] & 0x7fff;
-      const int32_t j = st >> cs;
-      const int32_t e = chunk_end(j);
-      const int32_t stop = min(min(e + look, de), ruse);
-      int32_t p = st, q[kF3ShortMax];
-      bool alive = true;
-#pragma unroll
-      for (int t = 0; t < kF3ShortMax; t++) {
-        q[t] = -1;
-        if (t >= K || !alive || p >= stop) continue;
-        p = f3_step(rgn, p, lim, mk, mv, nodel);
-        if (p < 0) alive = false;
-        else q[t] = p;
-      }
-      for (int t = kF3ShortMax; t < K && alive && p < stop; t++) {  // (a second pass, rare)
-        p = f3_step(rgn, p, lim, mk, mv, nodel);
-        alive = p >= 0;
-      }
-      cand[i] = (uint16_t)(st | (alive ? 0x8000 : 0));
-      if (alive) {
-#pragma unroll
-        for (int t = 0; t < kF3ShortMax; t++)
-          if (q[t] >= 0 && q[t] < e) atomicOr(&reached[q[t] >> 5], 1u << (q[t] & 31));
-      }
+    if (cover) {
+      for (int32_t i = lane; i < (ruse + 31) / 32 + 1; i += 64) reached[i] = 0u;
+      wave_sync();
     }
-    wave_sync();
-    // heads: alive and reached from no other survivor, compacted in position order
+    // without marks, a round's survivors are its heads: walk and compact in one pass
     S = 0;
     over = false;
     for (int32_t i0 = 0; i0 < T; i0 += 64) {
       const int32_t i = i0 + lane;
-      bool head = false;
+      bool alive = false;
       int32_t st = 0;
       if (i < T) {
-        const int32_t v = cand[i];
-        st = v & 0x7fff;
-        head = (v & 0x8000) && !((reached[st >> 5] >> (st & 31)) & 1u);
+        st = cand[i] & 0x7fff;
+        const int32_t e = chunk_end(st >> cs);
+        const int32_t stop = min(min(e + look, de), ruse);
+        int32_t p = st;
+        alive = true;
+        for (int t = 0; t < K && p < stop; t++) {
+          p = f3_step(rgn, p, lim, mk, mv, nodel);
+          if (p < 0) {
+            alive = false;
+            break;
+          }
+          // (a start reached by a candidate that dies later dies too: marking it is harmless)
+          if (cover && p < e) atomicOr(&reached[p >> 5], 1u << (p & 31));
+        }
+        if (cover) cand[i] = (uint16_t)(st | (alive ? 0x8000 : 0));
       }
-      const unsigned long long bal = __ballot(head);
+      if (cover) continue;
+      const unsigned long long bal = __ballot(alive);
       const int32_t before = (int32_t)__builtin_popcountll(bal & ((1ull << lane) - 1ull));
       const int32_t n = (int32_t)__builtin_popcountll(bal);
       if (S + n > kF3SurvCap) {
         over = true;
         break;
       }
-      if (head) s_start[S + before] = (uint16_t)st;
+      if (alive) s_start[S + before] = (uint16_t)st;
       S += n;
+    }
+    if (cover) {
+      wave_sync();
+      // heads: alive and reached from no other survivor, compacted in position order
+      for (int32_t i0 = 0; i0 < T; i0 += 64) {
+        const int32_t i = i0 + lane;
+        bool head = false;
+        int32_t st = 0;
+        if (i < T) {
+          const int32_t v = cand[i];
+          st = v & 0x7fff;
+          head = (v & 0x8000) && !((reached[st >> 5] >> (st & 31)) & 1u);
+        }
+        const unsigned long long bal = __ballot(head);
+        const int32_t before = (int32_t)__builtin_popcountll(bal & ((1ull << lane) - 1ull));
+        const int32_t n = (int32_t)__builtin_popcountll(bal);
+        if (S + n > kF3SurvCap) {
+          over = true;
+          break;
+        }
+        if (head) s_start[S + before] = (uint16_t)st;
+        S += n;
+      }
     }
     if (!over) break;
     if (K >= 8) {
@@ -299,6 +312,7 @@ __device__ __forceinline__ void frame3_region(const BuildParams& P, const uint64
   }
   wave_sync();
   mark(2);
+  if (P.f3_stop == 2) { fail(kF3Caps); return; }  // (SPARKEY_FRAME3_STOP: measurements)
 
   // ---- 3 long walk: head `lane` to its chunk end + LOOK, listing its starts in the chunk ----
   bool lovf = false;
@@ -333,6 +347,7 @@ __device__ __forceinline__ void frame3_region(const BuildParams& P, const uint64
   }
   wave_sync();
   mark(3);
+  if (P.f3_stop == 3) { fail(kF3Caps); return; }  // (SPARKEY_FRAME3_STOP: measurements)
 
   // ---- 4 resolve, lane j = chunk j.  Heads are in position order: chunk j's are a contiguous run
   //      [c_first[j], c_last[j]].  A chunk whose alive heads all reach one exit is converged: its
@@ -446,6 +461,7 @@ __device__ __forceinline__ void frame3_region(const BuildParams& P, const uint64
   bool spec = spec_e0 >= 0;
   int64_t ext = wv == 0 ? P.fr_entry : (spec ? R0 + spec_e0 : wait_prev());
   mark(4);
+  if (P.f3_stop == 4) { fail(kF3Caps); return; }  // (SPARKEY_FRAME3_STOP: measurements)
   unsigned long long ndel = 0;
   for (;;) {
     const int64_t e0 = ext - R0;
@@ -512,6 +528,7 @@ __device__ __forceinline__ void frame3_region(const BuildParams& P, const uint64
     }
     wave_sync();
     mark(5);
+  if (P.f3_stop == 5) { fail(kF3Caps); return; }  // (SPARKEY_FRAME3_STOP: measurements)
     // ---- 5 hash ----
     const unsigned long long base = wv * (unsigned long long)P.slab_cap;
     ndel = 0;
