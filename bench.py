@@ -5,7 +5,7 @@ header) of a C2-shaped log (10M PUTs per GPU, 16-byte keys, 100-byte values, NON
 resident in HBM, into a device-resident .spi image.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--entries 10000000] [--no-cpu-baseline]
-                    [--workload c2|c3|c5|churn|snappy|get|append]
+                    [--workload c2|c3|c5|churn|snappy|zstd|get|append]
 
 N = 1: the C2 log (10M records) built on one GPU; the line carries the per-stage roofline and the
 CPU baseline (the oracle's sequential IN_MEMORY restatement on the host, timed on the same log).
@@ -50,6 +50,8 @@ def stage_bytes(stage, n, data_end, slot, cap, passes=2, comp_end=None):
         # SNAPPY (data_end = the virtual log's end): blocks read once, decompressed bytes written once
         "snappy_decode": (comp_end or data_end) - 84 + log,
         "snappy_rewrite": 2 * slot * cap,      # internal table read, final table written
+        "zstd_decode": (comp_end or data_end) - 84 + log,   # (as SNAPPY)
+        "zstd_rewrite": 2 * slot * cap,
     }.get(stage, 0)
 
 
@@ -98,6 +100,8 @@ WORKLOADS = {
                       "IN_MEMORY (exact replay over slot segments)", "sorting": False, "path": 2},
     "snappy": {"name": "C2 records (10M PUTs x (16 B key, 100 B value)), CompressionType.SNAPPY, 64 KiB blocks, "
                        "IN_MEMORY", "sorting": False, "path": 0},
+    "zstd": {"name": "C2 records (10M PUTs x (16 B key, 100 B value)), CompressionType.ZSTD (level 3), 64 KiB "
+                     "blocks, IN_MEMORY", "sorting": False, "path": 0},
     "append": {"name": "GPU log producer (batched LogWriter.put)", "sorting": False, "path": 0},
     "get": {"name": "batched IndexHash.get of every key of the C2 index (log and index resident in HBM)",
             "sorting": False, "path": 0},
@@ -202,8 +206,9 @@ def single_gpu(args, dev):
         log_np = synth.fixed_log(n, 16, 100, seed=args.seed, file_id=0x5EED0000)
     elif args.workload in ("c3", "c5"):
         log_np = synth.mixed_log(n, 8, 64, 100, seed=args.seed + 2)
-    elif args.workload == "snappy":
-        log_np = synth.snappy_log(synth.fixed_log(n, 16, 100, seed=args.seed, file_id=0x5EED0000), 118, 65536)
+    elif args.workload in ("snappy", "zstd"):
+        log_np = synth.snappy_log(synth.fixed_log(n, 16, 100, seed=args.seed, file_id=0x5EED0000), 118, 65536,
+                                  codec=args.workload)
     else:
         log_np = synth.churn_log(n, int(n * 0.8), 0.1, seed=args.seed + 4)
     gen_s = time.time() - t0
@@ -244,7 +249,7 @@ def single_gpu(args, dev):
     dom = max(stage_ms, key=lambda k: stage_ms[k]) if stage_ms else None
     passes = stats.partition_passes
     # SNAPPY: the inner build's stages run over the virtual log (84 + 118 n bytes for C2 records)
-    frame_end = 84 + 118 * n if args.workload == "snappy" else log_len
+    frame_end = 84 + 118 * n if args.workload in ("snappy", "zstd") else log_len
     dom_bytes = stage_bytes(dom, n, frame_end, slot, cap, passes, comp_end=log_len) if dom else 0
     achieved = dom_bytes / (stage_ms[dom] * 1e-3) / 1e9 if dom and stage_ms[dom] > 0 else 0.0
     b_alg = (log_len - 84) + 112 + slot * cap
@@ -304,7 +309,7 @@ def single_gpu(args, dev):
     log_path, spi_path = os.path.join(tmpdir, "bench.spl"), os.path.join(tmpdir, "bench.spi")
     try:
         log_np.tofile(log_path)
-        if args.workload in ("c2", "c3", "c5", "churn", "snappy"):
+        if args.workload in ("c2", "c3", "c5", "churn", "snappy", "zstd"):
             # as SparkeyWriter.writeHash does it: a fresh "-tmp" file, then renamed over the .spi
             _native.build_index_file(log_path, spi_path, opts)
             reps_f = 3

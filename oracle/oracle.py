@@ -20,6 +20,30 @@ SORTING = 2
 AUTO = 0
 
 
+def zstd_decompress(data: bytes) -> bytes:
+    """One ZSTD block through libzstd (pyarrow's bundled copy; zstd-jni wraps the same library,
+    CompressorType.java:42-56).  Streaming, so frames without a content size decode too."""
+    import pyarrow as pa
+    return pa.CompressedInputStream(pa.BufferReader(data), "zstd").read()
+
+
+_DECODER = ctypes.CFUNCTYPE(ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64)
+
+
+def _zstd_block(src, n, dst, cap):
+    try:
+        out = zstd_decompress(ctypes.string_at(src, n))
+    except Exception:
+        return -1
+    if len(out) > cap:
+        return -1
+    ctypes.memmove(dst, out, len(out))
+    return len(out)
+
+
+_zstd_cb = _DECODER(_zstd_block)
+
+
 def build() -> str:
     """Compiles the oracle with gcc (make); returns the .so path."""
     subprocess.run(["make", "-s", "-C", _HERE], check=True)
@@ -69,6 +93,9 @@ def lib():
         L.oracle_get.argtypes = [u8p, ctypes.c_int64, u8p, ctypes.c_int64, u8p, ctypes.c_int32,
                                  ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]
         L.oracle_get.restype = ctypes.c_int32
+        L.oracle_set_zstd_decoder.argtypes = [_DECODER]
+        L.oracle_set_zstd_decoder.restype = None
+        L.oracle_set_zstd_decoder(_zstd_cb)
         _lib = L
     return _lib
 

@@ -193,6 +193,11 @@ typedef struct {
   int32_t max_entries_per_block;
 } log_header;
 
+/* ZSTD block decoder (oracle_set_zstd_decoder); NULL: ZSTD logs are unsupported */
+static oracle_block_decoder g_zstd = NULL;
+
+void oracle_set_zstd_decoder(oracle_block_decoder fn) { g_zstd = fn; }
+
 static int32_t parse_log_header(const uint8_t* b, int64_t len, log_header* h) {
   if (len < LOG_HEADER_SIZE) return ORACLE_E_NOT_LOG;
   if (rd32(b + 0) != LOG_MAGIC) return ORACLE_E_NOT_LOG;               /* :57-60 */
@@ -215,7 +220,7 @@ static int32_t parse_log_header(const uint8_t* b, int64_t len, log_header* h) {
   if (h->max_key_len > 0x7fffffffLL || h->max_key_len < 0) return ORACLE_E_HEADER; /* CommonHeader.java:38-40 */
   if (h->max_value_len < 0) return ORACLE_E_HEADER;                     /* CommonHeader.java:41-43 */
   if (h->compression_type < 0 || h->compression_type > 2) return ORACLE_E_CORRUPT_LOG; /* values()[ct] */
-  if (h->compression_type == 2) return ORACLE_E_UNSUPPORTED;            /* ZSTD: not on this path */
+  if (h->compression_type == 2 && !g_zstd) return ORACLE_E_UNSUPPORTED; /* ZSTD: needs a decoder */
   return ORACLE_OK;
 }
 
@@ -843,6 +848,52 @@ int64_t oracle_snappy_uncompress(const uint8_t* in, int64_t n, uint8_t* out, int
   return o == ulen ? ulen : ORACLE_E_CORRUPT_LOG;
 }
 
+/* ZSTD: every block decoded into a buffer of maxBlockSize bytes (CompressedReader.java:40-49,
+ * CompressorType.java:42-56: the decompressed length is what the decoder returns), appended to the
+ * virtual stream. */
+static int32_t open_zstd(build_ctx* c, const uint8_t* log, int64_t data_end, int64_t max_block, uint8_t** vbuf) {
+  int64_t nblk = 0, cap_b = 64, total = 0, vcap = 1 << 16, p = LOG_HEADER_SIZE;
+  c->blk_pos = (int64_t*)malloc(sizeof(int64_t) * (size_t)cap_b);
+  c->blk_voff = (int64_t*)malloc(sizeof(int64_t) * (size_t)cap_b);
+  uint8_t* v = (uint8_t*)malloc((size_t)vcap);
+  uint8_t* tmp = (uint8_t*)malloc((size_t)max_block + 1);
+  if (!c->blk_pos || !c->blk_voff || !v || !tmp) { free(v); free(tmp); return ORACLE_E_BUFFER; }
+  memcpy(v, log, LOG_HEADER_SIZE);
+  while (p < data_end) {
+    int64_t q = p;
+    int32_t clen;
+    int32_t rc = oracle_vlq_read(log, data_end, &q, &clen);
+    if (rc) { free(v); free(tmp); return rc; }
+    if (clen < 0 || q + clen > data_end) { free(v); free(tmp); return ORACLE_E_CORRUPT_LOG; }
+    const int64_t got = g_zstd(log + q, clen, tmp, max_block);
+    if (got < 0 || got > max_block) { free(v); free(tmp); return ORACLE_E_CORRUPT_LOG; }
+    if (nblk == cap_b) {
+      cap_b *= 2;
+      c->blk_pos = (int64_t*)realloc(c->blk_pos, sizeof(int64_t) * (size_t)cap_b);
+      c->blk_voff = (int64_t*)realloc(c->blk_voff, sizeof(int64_t) * (size_t)cap_b);
+      if (!c->blk_pos || !c->blk_voff) { free(v); free(tmp); return ORACLE_E_BUFFER; }
+    }
+    while (LOG_HEADER_SIZE + total + got + 1 > vcap) {
+      vcap *= 2;
+      v = (uint8_t*)realloc(v, (size_t)vcap);
+      if (!v) { free(tmp); return ORACLE_E_BUFFER; }
+    }
+    c->blk_pos[nblk] = p;
+    c->blk_voff[nblk] = LOG_HEADER_SIZE + total;
+    memcpy(v + LOG_HEADER_SIZE + total, tmp, (size_t)got);
+    total += got;
+    nblk++;
+    p = q + clen;
+  }
+  free(tmp);
+  c->compressed = 1;
+  c->nblk = nblk;
+  c->log = v;
+  c->log_len = LOG_HEADER_SIZE + total;
+  *vbuf = v;
+  return 0;
+}
+
 /* The virtual stream of a SNAPPY log: blocks VLQ(compressedSize) || snappy bytes from offset 84 to
  * dataEnd (CompressedOutputStream.flush, CompressedOutputStream.java:47-58; CompressedReader.fetchBlock,
  * CompressedReader.java:66-74). */
@@ -913,8 +964,10 @@ int64_t oracle_build_index(const uint8_t* log, int64_t log_len, int32_t hash_siz
   c.log_len = log_len;
   c.ebb_mask = (1 << c.ih.entry_block_bits) - 1;
   uint8_t* vbuf = NULL;
-  if (lh.compression_type == 1) {
-    rc = open_compressed(&c, log, lh.data_end, &vbuf);
+  if (lh.compression_type != 0) {
+    if (lh.compression_block_size < 0) rc = ORACLE_E_CORRUPT_LOG;
+    else if (lh.compression_type == 2) rc = open_zstd(&c, log, lh.data_end, lh.compression_block_size, &vbuf);
+    else rc = open_compressed(&c, log, lh.data_end, &vbuf);
     if (rc) { free(c.blk_pos); free(c.blk_voff); set_err(err, err_len, err_msg(rc)); return rc; }
   }
   const int64_t hash_length = (int64_t)c.slot_size * c.ih.capacity;

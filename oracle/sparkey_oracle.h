@@ -65,6 +65,11 @@ int64_t oracle_build_index(const uint8_t* log, int64_t log_len, int32_t hash_siz
 /* Snappy raw-format block decompression (CompressorType.java:32-34): decompressed length or <0 */
 int64_t oracle_snappy_uncompress(const uint8_t* in, int64_t n, uint8_t* out, int64_t cap);
 
+/* ZSTD blocks (CompressorType.java:42-56) are decoded by libzstd, the library zstd-jni wraps, which
+ * the caller registers (oracle.py: pyarrow's bundled libzstd): decompressed length or <0. */
+typedef int64_t (*oracle_block_decoder)(const uint8_t* in, int64_t n, uint8_t* out, int64_t cap);
+void oracle_set_zstd_decoder(oracle_block_decoder fn);
+
 /* IndexHash.get (IndexHash.java:398-452): 1 found, 0 missing, <0 error */
 int32_t oracle_get(const uint8_t* index, int64_t index_len, const uint8_t* log, int64_t log_len,
                    const uint8_t* key, int32_t klen, int64_t* value_off, int64_t* value_len);

@@ -73,6 +73,10 @@ struct SnappyParams {
 };
 
 void launch_snappy_dir(const SnappyParams& S, hipStream_t s);
+// ZSTD logs (zstd_kernels.hip): the same directory with sizes from the frame headers, and the decode
+void launch_zstd_dir(const SnappyParams& S, hipStream_t s);
+hipError_t launch_zstd_decode(const SnappyParams& S, hipStream_t s);
+uint32_t zstd_lds_bytes(int64_t max_block);  // dynamic LDS of the in-LDS decode (0: too large, global)
 // blocks [blk_base, blk_base + nblk), one wave per block: LDS-staged when lds_bytes > 0, else
 // lane-serial in global memory
 hipError_t launch_snappy_decode(const SnappyParams& S, hipStream_t s);

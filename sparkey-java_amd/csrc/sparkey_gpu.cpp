@@ -105,8 +105,8 @@ int parse_log_header(const uint8_t* b, uint64_t hdr_len, uint64_t file_len, LogH
     set_err(err, err_len, "Corrupt log file: unknown compression type " + std::to_string(h->compression_type));
     return SPARKEY_E_CORRUPT_LOG;
   }
-  if (h->compression_type == 2 || (h->compression_type == 1 && !allow_snappy)) {
-    set_err(err, err_len, h->compression_type == 2 ? "ZSTD logs are not supported by the GPU builder"
+  if (h->compression_type != 0 && !allow_snappy) {
+    set_err(err, err_len, h->compression_type == 2 ? "ZSTD logs are not supported on this entry point"
                                                    : "SNAPPY logs are not supported on this entry point");
     return SPARKEY_E_UNSUPPORTED;
   }
@@ -711,9 +711,11 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
                       uint8_t* d_out, uint64_t index_cap, const sparkey_build_opts* opts, hipStream_t s,
                       sparkey_build_stats* stats_out, char* err, size_t err_len);
 
-// SNAPPY logs (snappy.hpp): block directory, decode into the virtual log, the normal
-// build over it into an internal table, then every slot's address rewritten to
-// (blockPosition << entryBlockBits) | entryIndex (IndexHash.java:270-283).
+// SNAPPY and ZSTD logs (snappy.hpp): block directory, decode into the virtual log, the
+// normal build over it into an internal table, then every slot's address rewritten to
+// (blockPosition << entryBlockBits) | entryIndex (IndexHash.java:270-283).  The two codecs differ only
+// in the directory (a Snappy preamble / a Zstandard Frame_Content_Size gives each block's size) and
+// the decode kernel (snappy_kernels.hip / zstd_kernels.hip).
 static int plan_build_snappy(sparkey_plan* pl, const LogHdr& lh, const uint8_t* log_header, const uint8_t* d_log,
                              uint64_t log_len, uint8_t* d_out, uint64_t index_cap, const sparkey_build_opts* opts,
                              hipStream_t s, sparkey_build_stats* stats_out, char* err, size_t err_len) {
@@ -758,10 +760,16 @@ static int plan_build_snappy(sparkey_plan* pl, const LogHdr& lh, const uint8_t* 
   S.data_end = lh.data_end;
   S.max_block = lh.compression_block_size;
   const uint64_t body = (uint64_t)std::max<int64_t>(0, lh.data_end - kLogHeaderSize);
-  // LDS: the decoded block, then an 8 KiB window over its stream (k_snappy_lds)
+  const bool zstd = lh.compression_type == 2;
+  const char* codec = zstd ? "zstd" : "snappy";
   const int64_t mb = lh.compression_block_size;
-  const int64_t lds = ((mb + 15) & ~15LL) + 16 + 8192 + 16;
-  S.lds_bytes = lds <= 160 * 1024 ? (uint32_t)lds : 0u;
+  if (zstd) {  // LDS: the decoded block, then the whole frame (k_zstd_decode)
+    S.lds_bytes = zstd_lds_bytes(mb);
+  } else {  // LDS: the decoded block, then an 8 KiB window over its stream (k_snappy_lds)
+    const int64_t lds = ((mb + 15) & ~15LL) + 16 + 8192 + 16;
+    S.lds_bytes = lds <= 160 * 1024 ? (uint32_t)lds : 0u;
+  }
+  auto decode_launch = [&](hipStream_t st) { return zstd ? launch_zstd_decode(S, st) : launch_snappy_decode(S, st); };
   // Record offsets per block: maxEntriesPerBlock from the header, bounded by what a block can hold
   // (every record is at least 2 bytes), so a corrupt header cannot size a huge allocation; a block
   // with more records than the header allows is still flagged by the walk.
@@ -801,18 +809,21 @@ static int plan_build_snappy(sparkey_plan* pl, const LogHdr& lh, const uint8_t* 
       S.dir = pl->sn_dir;
       const uint64_t before = dir.nblk;
       S.dir_limit = std::min<uint64_t>(S.blk_cap, before + chunk);
-      launch_snappy_dir(S, s);
+      if (zstd)
+        launch_zstd_dir(S, s);
+      else
+        launch_snappy_dir(S, s);
       if ((e = hipGetLastError()) != hipSuccess) return e;
       if ((e = hipMemcpyAsync(&dir, pl->sn_dir, sizeof(dir), hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
       if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
       if (decode && dir.nblk > before) {
         S.blk_base = before;
         S.nblk = dir.nblk - before;
-        e = launch_snappy_decode(S, s2);
-        if (e != hipSuccess && S.lds_bytes) {  // the LDS size was refused: lane-serial global decode
+        e = decode_launch(s2);
+        if (e != hipSuccess && S.lds_bytes) {  // the LDS size was refused: decode in global memory
           (void)hipGetLastError();
           S.lds_bytes = 0;
-          e = launch_snappy_decode(S, s2);
+          e = decode_launch(s2);
         }
         if (e != hipSuccess) return e;
       }
@@ -831,7 +842,8 @@ static int plan_build_snappy(sparkey_plan* pl, const LogHdr& lh, const uint8_t* 
   // (LogHeader.put / delete, LogHeader.java:161-172); a header that understates them gets a
   // directory-only pass to size the virtual log
   // (and a header that overstates them beyond what the blocks can decompress to -- Snappy expands at
-  // most 64 bytes per 3-byte copy -- is sized the same way instead of trusted with a huge allocation)
+  // most 64 bytes per 3-byte copy -- is sized the same way instead of trusted with a huge allocation;
+  // ZSTD logs use the same bound: one compressing better takes the directory-only pass)
   const uint64_t ps = (uint64_t)std::max<int64_t>(0, lh.put_size), ds = (uint64_t)std::max<int64_t>(0, lh.delete_size);
   const uint64_t hdr_total = ps + ds < ps ? UINT64_MAX : ps + ds;
   const int64_t vcap0 = hdr_total <= 22 * body + 4096 ? (int64_t)hdr_total : 0;
@@ -849,8 +861,10 @@ static int plan_build_snappy(sparkey_plan* pl, const LogHdr& lh, const uint8_t* 
   }
   if (dir.err) {
     HIP_TRY(hipStreamSynchronize(s));
-    set_err(err, err_len, dir.err == 2 ? "Corrupt log file: compressed block larger than the reader's buffers"
-                                       : "Corrupt log file: bad compressed block header");
+    set_err(err, err_len, dir.err == 2   ? "Corrupt log file: compressed block larger than the reader's buffers"
+                          : dir.err == 4 ? "ZSTD block frame without a content size (not a layout the reference writes)"
+                                         : "Corrupt log file: bad compressed block header");
+    if (dir.err == 4) return SPARKEY_E_UNSUPPORTED;
     return SPARKEY_E_CORRUPT_LOG;
   }
   const uint64_t nblk = dir.nblk;
@@ -886,7 +900,8 @@ static int plan_build_snappy(sparkey_plan* pl, const LogHdr& lh, const uint8_t* 
   for (uint64_t b = 0; b < nblk; b++) {
     const SnappyWalk& w = walks[b];
     if (w.flags & kWalkBadStream) {
-      set_err(err, err_len, "Corrupt log file: bad snappy stream in block at " + std::to_string(blocks[b].file_pos));
+      set_err(err, err_len, std::string("Corrupt log file: bad ") + codec + " stream in block at " +
+                                std::to_string(blocks[b].file_pos));
       return SPARKEY_E_CORRUPT_LOG;
     }
     if (carry == 0) {
@@ -946,9 +961,9 @@ static int plan_build_snappy(sparkey_plan* pl, const LogHdr& lh, const uint8_t* 
     float t0 = 0.f, t1 = 0.f;
     (void)hipEventElapsedTime(&t0, ev[0], ev[1]);
     (void)hipEventElapsedTime(&t1, ev[2], ev_end);
-    pl->stage_names.insert(pl->stage_names.begin(), "snappy_decode");
+    pl->stage_names.insert(pl->stage_names.begin(), std::string(codec) + "_decode");
     pl->stage_ms.insert(pl->stage_ms.begin(), t0);
-    pl->stage_names.push_back("snappy_rewrite");
+    pl->stage_names.push_back(std::string(codec) + "_rewrite");
     pl->stage_ms.push_back(t1);
   }
   if (rerr) {
@@ -968,7 +983,7 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
   LogHdr lh;
   int rc = parse_log_header(log_header, 84, log_len, &lh, err, err_len, true);
   if (rc) return rc;
-  if (lh.compression_type == 1)
+  if (lh.compression_type != 0)
     return plan_build_snappy(pl, lh, log_header, d_log, log_len, d_out, index_cap, opts, s, stats_out, err, err_len);
   IndexParams ip;
   rc = make_index_params(lh, *opts, &ip, err, err_len);

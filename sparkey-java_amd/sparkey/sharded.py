@@ -378,7 +378,7 @@ class ShardedBuilder:
         lay, h, uni = geo
         data_end = lay.data_end
         s.begin(header, file_len, buf, buf_lo, buf_hi, opts, g, G)
-        if h["compression_type"] == 1:  # SNAPPY: the whole log on every rank, the single-GPU build
+        if h["compression_type"] != 0:  # SNAPPY / ZSTD: the whole log on every rank, the single-GPU build
             slot_lo, slot_hi = s.slot_range(g)
             slot_size = _slot_size(h, opts, data_end)
             out_off = 0 if g == 0 else INDEX_HEADER_SIZE + slot_lo * slot_size

@@ -155,12 +155,13 @@ def churn_log(n: int, pool: int, p_del: float, key_len: int = 16, value_len: int
     return buf
 
 
-def snappy_log(log: np.ndarray, rec: int, block_size: int) -> np.ndarray:
+def snappy_log(log: np.ndarray, rec: int, block_size: int, codec: str = "snappy") -> np.ndarray:
     """The SNAPPY log a reference writer produces for the same uniform R-byte PUT records (a NONE log
     from fixed_log): CompressedWriter.smartFlush (CompressedWriter.java:111-118) closes a block when
     the next record no longer fits, so every block holds block_size // R records; each block is
     VLQ(compressedSize) || the Snappy stream of its bytes (CompressedOutputStream.java:47-58), here from
-    libsnappy through pyarrow.  Records longer than the block size are not handled here."""
+    libsnappy through pyarrow.  codec="zstd": a ZSTD log, each block one Zstandard frame from libzstd at
+    level 3 (CompressorType.java:42-56).  Records longer than the block size are not handled here."""
     import pyarrow as pa
     from .log_writer import vlq_bytes
     assert 10 <= rec <= block_size
@@ -170,11 +171,12 @@ def snappy_log(log: np.ndarray, rec: int, block_size: int) -> np.ndarray:
     step = per * rec
     parts = []
     for o in range(0, body.size, step):
-        comp = pa.compress(body[o:o + step], codec="snappy", asbytes=True)
+        comp = (pa.Codec("zstd", compression_level=3).compress(body[o:o + step], asbytes=True) if codec == "zstd"
+                else pa.compress(body[o:o + step], codec="snappy", asbytes=True))
         parts.append(vlq_bytes(len(comp)))
         parts.append(comp)
     data = b"".join(parts)
-    hdr.compression_type = 1
+    hdr.compression_type = 2 if codec == "zstd" else 1
     hdr.compression_block_size = block_size
     hdr.max_entries_per_block = per if body.size else 0
     hdr.data_end = LOG_HEADER_SIZE + len(data)

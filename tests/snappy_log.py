@@ -1,4 +1,4 @@
-"""Test-input generator: SNAPPY-compressed Sparkey logs, in memory.
+"""Test-input generator: SNAPPY- and ZSTD-compressed Sparkey logs, in memory.
 
 Restates the reference's compressed append path so that a log built here has the block layout the
 reference writes for the same puts/deletes, block size and file identifier:
@@ -11,7 +11,8 @@ reference writes for the same puts/deletes, block size and file identifier:
     (LogWriter.java:77-81): maxEntriesPerBlock = the most records started in one block.
 The block bytes come from libsnappy through pyarrow (the C++ library snappy-java wraps); any valid
 Snappy stream gives the same index, since the index depends only on the decompressed bytes and the
-block boundaries.  `literal_only=True` writes raw literal-only Snappy streams instead (the format's
+block boundaries.  codec="zstd" writes ZSTD logs: each block one Zstandard frame from libzstd at level 3
+(pyarrow), what zstd-jni's Zstd.compress writes (CompressorType.java:42-56).  `literal_only=True` writes raw literal-only Snappy streams instead (the format's
 simplest valid encoding), and `encoder=` accepts any callable bytes -> snappy bytes.
 """
 from __future__ import annotations
@@ -46,6 +47,18 @@ def snappy_literal_only(data: bytes) -> bytes:
     return bytes(out)
 
 
+def zstd_compress(data: bytes, level: int = 3) -> bytes:
+    """One Zstandard frame, as zstd-jni's Zstd.compress at the reference's level 3
+    (CompressorType.java:42-56); libzstd through pyarrow."""
+    import pyarrow as pa
+    return pa.Codec("zstd", compression_level=level).compress(data, asbytes=True)
+
+
+def zstd_decompress(data: bytes) -> bytes:
+    import pyarrow as pa
+    return pa.CompressedInputStream(pa.BufferReader(data), "zstd").read()
+
+
 def snappy_decompress(data: bytes, ulen: int) -> bytes:
     import pyarrow as pa
     return pa.decompress(data, ulen, codec="snappy", asbytes=True)
@@ -54,12 +67,14 @@ def snappy_decompress(data: bytes, ulen: int) -> bytes:
 class CompressedLog:
     """LogWriter over a SNAPPY CompressedWriter, kept in memory; `finish()` returns the .spl bytes."""
 
-    def __init__(self, block_size: int, file_identifier: int = 12345, literal_only: bool = False, encoder=None):
+    def __init__(self, block_size: int, file_identifier: int = 12345, literal_only: bool = False, encoder=None,
+                 codec: str = "snappy"):
         if block_size < 10:  # CompressedOutputStream.java:33-35
             raise OSError("Too small block size - won't be able to fit keylen + valuelen in a single block")
-        self.header = LogHeader(CompressionType.SNAPPY, block_size, file_identifier)
+        zstd = codec == "zstd"
+        self.header = LogHeader(CompressionType.ZSTD if zstd else CompressionType.SNAPPY, block_size, file_identifier)
         self.block_size = block_size
-        self.encoder = encoder or (snappy_literal_only if literal_only else snappy_compress)
+        self.encoder = encoder or (zstd_compress if zstd else snappy_literal_only if literal_only else snappy_compress)
         self.out = bytearray()
         self.pending = bytearray()
         self.cur_entries = 0
@@ -149,9 +164,12 @@ def iterate_compressed(log: bytes):
     while p < end:
         clen, q = _vlq(log, p)
         raw = log[q:q + clen]
-        ulen, _ = _vlq(raw, 0)
         starts.append((len(stream), p))
-        stream += snappy_decompress(raw, ulen)
+        if hdr.compression_type == CompressionType.ZSTD:
+            stream += zstd_decompress(raw)
+        else:
+            ulen, _ = _vlq(raw, 0)
+            stream += snappy_decompress(raw, ulen)
         p = q + clen
     starts.append((len(stream), end))
     u = 0

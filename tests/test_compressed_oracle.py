@@ -1,4 +1,4 @@
-"""Oracle pinning for SNAPPY logs.
+"""Oracle pinning for SNAPPY and ZSTD logs.
 
 The reference's compressed tests need snappy-java and a JVM, neither of which is here, and the
 reference ships no compressed fixture; so the compressed oracle is pinned by two properties:
@@ -51,8 +51,8 @@ def _ops(rng, n, nkeys, p_del, vmax):
     return ops
 
 
-def _compressed(ops, block_size, literal_only=False):
-    cl = CompressedLog(block_size, file_identifier=0x1234567, literal_only=literal_only)
+def _compressed(ops, block_size, literal_only=False, codec="snappy"):
+    cl = CompressedLog(block_size, file_identifier=0x1234567, literal_only=literal_only, codec=codec)
     for op, k, v in ops:
         if op == "put":
             cl.put(k, v)
@@ -93,8 +93,8 @@ def _vlq(b, p):
             return v, p
 
 
-def check_equivalent(ops, block_size, method, literal_only=False, hash_size=0):
-    clog = _compressed(ops, block_size, literal_only)
+def check_equivalent(ops, block_size, method, literal_only=False, hash_size=0, codec="snappy"):
+    clog = _compressed(ops, block_size, literal_only, codec)
     nlog = make_log(ops=ops)
     ci = oracle.build_index(clog, 4321, hash_size=hash_size, method=method)
     ni = oracle.build_index(nlog, 4321, hash_size=hash_size, method=method)
@@ -142,21 +142,50 @@ def test_write_hash_benchmark_snappy():
     assert struct.unpack_from("<i", ci, 92)[0] == (mepb - 1).bit_length()
 
 
-def test_zstd_is_unsupported():
-    clog = bytearray(_compressed([("put", b"a", b"b")], 64))
-    clog[64] = 2
+# ---- ZSTD (CompressorType.java:42-56): blocks decoded by libzstd, the library zstd-jni wraps ----
+
+def test_zstd_frames_round_trip():
+    """The generator's frames are what zstd-jni writes: single frames with a content size, level 3."""
+    from snappy_log import zstd_compress
+    rng = random.Random(9)
+    for n in (1, 10, 100, 4096, 65536, 131072):
+        d = bytes(rng.randrange(4) for _ in range(n // 2)) + bytes(rng.randrange(256) for _ in range(n - n // 2))
+        z = zstd_compress(d)
+        assert struct.unpack_from("<I", z, 0)[0] == 0xFD2FB528
+        assert z[4] >> 6 or z[4] & 0x20                          # Frame_Content_Size present
+        assert oracle.zstd_decompress(z) == d
+
+
+@pytest.mark.parametrize("block_size", [10, 100, 1024, 65536, 131072])
+@pytest.mark.parametrize("method", [IN_MEMORY, SORTING])
+def test_zstd_unique_puts(block_size, method):
+    rng = random.Random(block_size + 7)
+    check_equivalent(_ops(rng, 1500, 10 ** 9, 0.0, 200), block_size, method, codec="zstd")
+
+
+@pytest.mark.parametrize("block_size", [10, 300, 4096])
+def test_zstd_overwrites_deletes_and_spanning_records(block_size):
+    rng = random.Random(block_size + 8)
+    check_equivalent(_ops(rng, 1500, 400, 0.2, 3000 if block_size == 300 else 120), block_size, IN_MEMORY,
+                     codec="zstd")
+
+
+def test_zstd_corrupt_block_is_rejected():
+    clog = bytearray(_compressed([("put", b"k%d" % i, b"v" * 50) for i in range(40)], 256, codec="zstd"))
+    clog[84 + 1 + 8] ^= 0xFF                                      # inside the first frame's first block
     with pytest.raises(oracle.OracleError):
         oracle.build_index(bytes(clog), 1)
 
 
+@pytest.mark.parametrize("codec", ["snappy", "zstd"])
 @pytest.mark.parametrize("block_size", [118, 500, 4096, 65536])
-def test_synth_snappy_log_matches_writer(block_size):
-    """bench's SNAPPY generator (synth.snappy_log) writes what CompressedWriter writes."""
+def test_synth_snappy_log_matches_writer(block_size, codec):
+    """bench's SNAPPY / ZSTD generator (synth.snappy_log) writes what CompressedWriter writes."""
     from sparkey import synth
     log = synth.fixed_log(3000, 16, 100, seed=2, file_id=0x777)
-    cl = CompressedLog(block_size, file_identifier=0x777)
+    cl = CompressedLog(block_size, file_identifier=0x777, codec=codec)
     body = log[84:].tobytes()
     for i in range(3000):
         r = body[i * 118:(i + 1) * 118]
         cl.put(r[2:18], r[18:])
-    assert synth.snappy_log(log, 118, block_size).tobytes() == cl.finish()
+    assert synth.snappy_log(log, 118, block_size, codec=codec).tobytes() == cl.finish()
