@@ -35,7 +35,7 @@ extern "C" {
 #define SPARKEY_E_CORRUPT_DATA (-5)   /* RuntimeException "Corrupt data" / "reference to delete entry" IndexHash.java:484,494,613,624 */
 #define SPARKEY_E_VLQ (-6)            /* RuntimeException "Too long VLQ value" Util.java:181,217 */
 #define SPARKEY_E_HEADER (-7)         /* IOException "Too large max key len" CommonHeader.java:38-43 */
-#define SPARKEY_E_UNSUPPORTED (-8)    /* ZSTD logs (SNAPPY logs are built: DESIGN.md §2.7) */
+#define SPARKEY_E_UNSUPPORTED (-8)    /* compressed layouts the reference never writes */
 #define SPARKEY_E_IO (-9)             /* IOException from file open/read/write */
 #define SPARKEY_E_GPU (-10)           /* HIP runtime error or no gfx950 device */
 #define SPARKEY_E_ARG (-11)           /* IllegalArgumentException (bad hash size etc.) */
