@@ -209,11 +209,7 @@ __global__ __launch_bounds__(kPlaceBlock) void k_place(BuildParams P, int sort_o
 
 // Equal-hash pairs: do they share the key?  (the reference compares key bytes in the log,
 // IndexHash.java:619-629)
-__global__ void k_verify_pairs(BuildParams P) {
-  if (build_aborted(P)) return;
-  const unsigned long long np = min(P.st->n_pairs, (unsigned long long)P.pair_cap);
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= np) return;
+__device__ void verify_pair(const BuildParams& P, uint64_t i) {
   const int64_t p1 = (int64_t)(P.pairs[2 * i] >> P.ebb);
   const int64_t p2 = (int64_t)(P.pairs[2 * i + 1] >> P.ebb);
   auto at = [&](int64_t a) -> uint32_t { return P.log[a]; };
@@ -225,6 +221,13 @@ __global__ void k_verify_pairs(BuildParams P) {
   for (int32_t j = 0; j < h1.klen; j++)
     if (k1[j] != k2[j]) return;
   atomicOr(&P.st->dup, 1u);
+}
+
+__global__ void k_verify_pairs(BuildParams P) {
+  if (build_aborted(P)) return;
+  const unsigned long long np = min(P.st->n_pairs, (unsigned long long)P.pair_cap);
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < np) verify_pair(P, i);
 }
 
 // ================================================================================================
@@ -332,6 +335,11 @@ __global__ __launch_bounds__(kStatFoldBlock) void k_stats_folded(BuildParams P) 
   if (build_aborted(P)) return;
   Status* st = P.st;
   const int tid = threadIdx.x;
+  if (P.fused_carry) {  // k_verify_pairs' work (no launch of its own)
+    const unsigned long long np = min(st->n_pairs, (unsigned long long)P.pair_cap);
+    for (uint64_t i = (uint64_t)blockIdx.x * kStatFoldBlock + tid; i < np; i += (uint64_t)gridDim.x * kStatFoldBlock)
+      verify_pair(P, i);
+  }
   if (st->big_buckets || st->full) {  // some slots were placed outside k_place_lds: k_stats runs
     if (tid == 0) st->stats_pending = 1u;
     return;

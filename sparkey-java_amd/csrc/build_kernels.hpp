@@ -106,6 +106,8 @@ struct Status {
   unsigned int stats_pending;    // folded stats could not cover every slot (big buckets): k_stats runs
   unsigned int stats_ticket;     // k_stats_folded: blocks done
   unsigned long long acc_sum, acc_col, acc_max;  // k_stats_folded: totals over its blocks
+  unsigned int p2_ticket;        // fused_carry: k_part2s blocks done (the last composes the digits)
+  unsigned int pad3;
 };
 
 struct BuildParams {
@@ -155,6 +157,14 @@ struct BuildParams {
   MaxPlus* bfun;
   MaxPlus* bpre;
   MaxPlus* bfun_total;
+  // fused_carry (single GPU, k_part2s in one pass): k_part2s leaves bpre = each bucket's exclusive
+  // prefix function inside its digit and dfun = each digit's composed function; its last block
+  // composes the 256 digits around the ring into dcarry (each digit's carry-in), and k_place_lds
+  // takes carry = bpre[b](dcarry[digit]) -- no k_summary / scan / k_carry launches
+  MaxPlus* dfun;         // (as 256 packed words, see part2_fused_carry)
+  int64_t* dcarry;
+  int32_t fused_carry;
+  uint32_t epoch;        // fused_carry: this build's number (1 .. 2^22 - 1), tags the dfun words
   int64_t* carry;
   uint64_t* pairs;
   uint64_t pair_cap;

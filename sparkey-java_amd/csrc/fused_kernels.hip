@@ -983,6 +983,95 @@ __global__ __launch_bounds__(kPart2Block) void k_part2(BuildParams P) {
   }
 }
 
+__device__ __forceinline__ MaxPlus shfl_up_mp(MaxPlus f, int o) {
+  MaxPlus t;
+  t.c = __shfl_up(f.c, o, 64);
+  t.a = __shfl_up(f.a, o, 64);
+  return t;
+}
+
+// fused_carry: the digit's bucket functions -> each bucket's exclusive prefix inside the digit (bpre)
+// and the digit's composed function (dfun); the last block to finish composes the 256 digits around
+// the ring: x0 = the composed function's constant (the carry into slot 0 when some slot stays
+// empty), each digit's carry-in dcarry[d] = (digits before d)(x0), or `full` when no slot stays empty
+// (k_carry's rules, evaluated per digit instead of per bucket).
+// A digit's function travels as one 64-bit word, (epoch << 42) | c << 21 | (a + 2^20), stored with a
+// relaxed agent-scope atomic; the last block reads each word until it carries this build's epoch.
+// That needs no release fence (on gfx950 one writes the XCD's whole L2 back: 256 of them measured
+// 0.11 ms).  With fixed bucket regions |a|, c <= 64 buckets x 1024 entries < 2^20; a digit past that
+// overflowed its regions and the build is redone (the clamp only keeps the epoch bits intact).
+constexpr int kDfunShift = 21;
+__device__ __forceinline__ uint64_t pack_dfun(MaxPlus f, uint32_t epoch) {
+  const int64_t lim = (1ll << 20) - 1;
+  const uint64_t c = (uint64_t)min(max(f.c, (int64_t)0), lim), a = (uint64_t)(min(max(f.a, -lim), lim) + (1ll << 20));
+  return ((uint64_t)epoch << (2 * kDfunShift)) | (c << kDfunShift) | a;
+}
+
+__device__ void part2_fused_carry(const BuildParams& P, const MaxPlus* s_fun, uint32_t nbins, uint64_t b0,
+                                  uint32_t dpart) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const OpMaxPlus op;
+  __shared__ bool s_last;
+  uint64_t* dword = (uint64_t*)P.dfun;  // (256 packed words)
+  __syncthreads();
+  if (wave == 0) {
+    MaxPlus f = (uint32_t)lane < nbins ? s_fun[lane] : MaxPlus{0, 0};
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const MaxPlus t = shfl_up_mp(f, o);
+      if (lane >= o) f = op(t, f);
+    }
+    MaxPlus ex = shfl_up_mp(f, 1);
+    if (lane == 0) ex = MaxPlus{0, 0};
+    const uint64_t bucket = b0 + lane;
+    if ((uint32_t)lane < nbins && bucket < P.nbuckets) P.bpre[bucket] = ex;
+    if (lane == 63) __hip_atomic_store(&dword[dpart], pack_dfun(f, P.epoch), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (tid == 0) s_last = atomicAdd(&P.st->p2_ticket, 1u) == gridDim.x - 1;
+  __syncthreads();
+  if (!s_last || wave != 0) return;
+  static_assert(kPart2Block >= 64, "one wave composes the digits");
+  MaxPlus g[4], agg{0, 0};
+#pragma unroll
+  for (int k = 0; k < 4; k++) {  // lane l: digits 4l .. 4l + 3 (every block stored its word before its ticket)
+    uint64_t v;
+    for (uint32_t spin = 0;; spin++) {  // (bounded: a word that never arrives is a bug, reported as such)
+      v = __hip_atomic_load(&dword[4 * lane + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if ((uint32_t)(v >> (2 * kDfunShift)) == P.epoch) break;
+      if (spin > (1u << 24)) {
+        atomicOr(&P.st->guard, 0x40u);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    g[k].c = (int64_t)((v >> kDfunShift) & ((1ull << kDfunShift) - 1));
+    g[k].a = (int64_t)(v & ((1ull << kDfunShift) - 1)) - (1ll << 20);
+    agg = op(agg, g[k]);
+  }
+  MaxPlus incl = agg;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const MaxPlus t = shfl_up_mp(incl, o);
+    if (lane >= o) incl = op(t, incl);
+  }
+  MaxPlus run = shfl_up_mp(incl, 1);
+  if (lane == 0) run = MaxPlus{0, 0};
+  MaxPlus tot;
+  tot.c = __shfl(incl.c, 63, 64);
+  tot.a = __shfl(incl.a, 63, 64);
+  if (tot.a >= 0) {  // N >= capacity: no empty slot, the canonical layout does not apply
+    if (lane == 0) atomicOr(&P.st->full, 1u);
+    return;
+  }
+  const int64_t x0 = tot.c;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    P.dcarry[4 * lane + k] = max(run.c, x0 + run.a);
+    run = op(run, g[k]);
+  }
+}
+
 // Pass 2 for a table of up to kP2SortedMaxBpp buckets per digit (single GPU): the digit's entries
 // are also counted per (bucket, wanted slot) in LDS (16-bit counts), so that the same pass leaves
 // each bucket's max-plus carry function -- k_summary's output: F(x) = max(x + n - bsize,
@@ -1015,6 +1104,7 @@ __global__ __launch_bounds__(kPart2Block) void k_part2s(BuildParams P) {
   }
   const uint32_t nbins = P.bpp;
   const uint64_t b0 = (uint64_t)dpart * nbins;
+  __shared__ MaxPlus s_fun[kP2SortedMaxBpp];  // (fused_carry) the digit's bucket functions
   uint32_t* h = dyn;
   uint32_t* btot = dyn + nbins * 512;
   uint32_t* boffl = btot + nbins;
@@ -1024,6 +1114,7 @@ __global__ __launch_bounds__(kPart2Block) void k_part2s(BuildParams P) {
   // (more entries than k_place_lds stages anyway) makes the host redo the build with dense runs
   const bool fixed = P.p2_fixed != 0;
   for (uint32_t i = tid; i < nbins * 512 + 2 * nbins; i += kPart2Block) dyn[i] = 0;
+  if (tid < (int)kP2SortedMaxBpp) s_fun[tid] = MaxPlus{0, 0};
   __syncthreads();
   bool ovf = false;
   for (uint32_t q = 0; q < nseg; q++) {
@@ -1113,7 +1204,12 @@ __global__ __launch_bounds__(kPart2Block) void k_part2s(BuildParams P) {
       f.a = n - bsize;
       f.c = n ? max((int64_t)0, n + mlast - bsize) : 0;
       P.bfun[bucket] = f;
+      s_fun[b] = f;
     }
+  }
+  if (P.fused_carry) {
+    part2_fused_carry(P, s_fun, nbins, b0, dpart);
+    return;
   }
   if (fixed) return;
   __syncthreads();
@@ -1216,8 +1312,15 @@ __global__ __launch_bounds__(kPlaceLdsBlock) void k_place_lds(BuildParams P) {
   const uint64_t b = P.b_lo + blockIdx.x;
   const uint32_t n = P.bcount[b];
   const uint64_t eoff = P.boff[b];
-  const int64_t x = P.carry[b];
+  int64_t x;
+  if (P.fused_carry) {
+    const MaxPlus pre = P.bpre[b];
+    x = max(pre.c, P.dcarry[b / P.bpp] + pre.a);
+  } else {
+    x = P.carry[b];
+  }
   if (ovf != 0 || nrec > P.max_records) return;  // build_aborted
+  if (P.fused_carry && threadIdx.x == 0) P.carry[b] = x;  // (for the global-memory placement's readers)
   const uint64_t start = b << kBucketShift;
   const int64_t bsize = (int64_t)min((uint64_t)kBucket, P.cap - start);
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1492,15 +1595,17 @@ void launch_partition(const BuildParams& P, hipStream_t s, StageTimer* tm) {
 
 void launch_place_buckets(const BuildParams& P, hipStream_t s) {
   if (P.b_hi > P.b_lo) hipLaunchKernelGGL(k_place_lds, dim3((unsigned)(P.b_hi - P.b_lo)), dim3(kPlaceLdsBlock), 0, s, P);
-  launch_place_global(P, s, 0, 1);  // buckets above kPlaceLdsMax entries (normally none)
+  // buckets above kPlaceLdsMax entries (normally none; never with fixed bucket regions, whose
+  // overflow redoes the build with dense runs)
+  if (!P.p2_fixed) launch_place_global(P, s, 0, 1);
 }
 
 
 void launch_place_fast(const BuildParams& P, hipStream_t s, StageTimer* tm) {
-  launch_summary_carry(P, s, tm);
+  if (!P.fused_carry) launch_summary_carry(P, s, tm);
   launch_place_buckets(P, s);
   tm->mark("place", s);
-  launch_verify(P, s, tm);
+  if (!P.fused_carry) launch_verify(P, s, tm);  // (fused_carry: k_stats_folded verifies the pairs)
 }
 
 }  // namespace sk

@@ -20,21 +20,29 @@ __device__ __forceinline__ int64_t align16(int64_t x) { return (x + 15) & ~15LL;
 // len bytes: one byte per lane per round for short copies (one LDS round trip for the usual
 // <= 256-byte element), 16 consecutive bytes per lane per round for long ones.  32-bit indices:
 // blocks are < 2^31 bytes (compressionBlockSize is a Java int).
+// kVol: src is output in global memory written by this wave (volatile loads, past the vector L1).
+template <bool kVol = false>
+__device__ __forceinline__ uint8_t ld_byte(const uint8_t* p) {
+  if (kVol) return *(const volatile uint8_t*)p;
+  return *p;
+}
+
+template <bool kVol = false>
 __device__ __forceinline__ void copy_bytes(uint8_t* dst, const uint8_t* src, uint32_t len, uint32_t lane,
                                            uint32_t nlanes) {
   if (len <= 4 * nlanes) {
-    for (uint32_t k = lane; k < len; k += nlanes) dst[k] = src[k];
+    for (uint32_t k = lane; k < len; k += nlanes) dst[k] = ld_byte<kVol>(src + k);
     return;
   }
   for (uint32_t k = lane * 16; k < len; k += nlanes * 16) {
     if (k + 16 <= len) {
       uint8_t t[16];
 #pragma unroll
-      for (int i = 0; i < 16; i++) t[i] = src[k + i];
+      for (int i = 0; i < 16; i++) t[i] = ld_byte<kVol>(src + k + i);
 #pragma unroll
       for (int i = 0; i < 16; i++) dst[k + i] = t[i];
     } else {
-      for (uint32_t i = k; i < len; i++) dst[i] = src[i];
+      for (uint32_t i = k; i < len; i++) dst[i] = ld_byte<kVol>(src + i);
     }
   }
 }
@@ -88,10 +96,14 @@ struct RingIn {
 // tags (uniform control flow).  A match copies out[o + k] = out[o - off + k % off]: only bytes before
 // o are read, so overlapping matches need no ordering between the lanes.  Returns kWalkBadStream on a
 // malformed stream.
-template <bool kSync, class In>
+// kGlobal: `out` is global memory (k_snappy_gw): a match reads what the wave stored, so its source
+// must be complete first -- the wave waits for its stores when the source reaches past `safe`, the
+// output offset below which every store is known complete.
+template <bool kSync, class In, bool kGlobal = false>
 __device__ __forceinline__ uint32_t snappy_decode(In& in, uint32_t n, uint32_t p, uint8_t* out, uint32_t ulen,
                                                   uint32_t lane, uint32_t nlanes) {
   uint32_t o = 0;
+  uint32_t safe = 0;
   while (p < n) {
     // the tag and the four bytes after it in one round trip
     in.ensure(p, 5);
@@ -135,9 +147,13 @@ __device__ __forceinline__ uint32_t snappy_decode(In& in, uint32_t n, uint32_t p
         p += 4;
       }
       if (off == 0 || off > o || len > ulen - o) return kWalkBadStream;
-      if (off >= len) copy_bytes(out + o, out + o - off, len, lane, nlanes);
+      if (kGlobal && o - off + min(off, len) > safe) {
+        __builtin_amdgcn_s_waitcnt(0);
+        safe = o;
+      }
+      if (off >= len) copy_bytes<kGlobal>(out + o, out + o - off, len, lane, nlanes);
       else
-        for (uint32_t k = lane; k < len; k += nlanes) out[o + k] = out[o - off + k % off];
+        for (uint32_t k = lane; k < len; k += nlanes) out[o + k] = ld_byte<kGlobal>(out + o - off + k % off);
     }
     o += len;
     if (kSync) __builtin_amdgcn_wave_barrier();  // one-wave workgroup: LDS ops run in order
@@ -305,6 +321,34 @@ __global__ void __launch_bounds__(64) k_snappy_lds(SnappyParams S) {
   }
 }
 
+// One wave per block as k_snappy_lds, decoding straight into the virtual log: only the stream window
+// is in LDS (8 KiB per wave instead of the whole decoded block), so many more blocks decode at once;
+// matches read back through L2.
+__global__ void __launch_bounds__(64) k_snappy_gw(SnappyParams S) {
+  __shared__ __attribute__((aligned(16))) uint8_t win[kSnappyWindow + 16];
+  const uint64_t b = S.blk_base + blockIdx.x;
+  const SnappyBlock B = S.blocks[b];
+  const uint32_t lane = threadIdx.x;
+  RingIn in;
+  in.g = S.log + B.data;
+  in.readable = S.log_len - B.data;
+  in.n = B.clen;
+  in.win = win;
+  in.lane = lane;
+  in.refill(0);
+  uint32_t p = 0;
+  while (in.byte(p) & 0x80u) p++;
+  p++;
+  const uint32_t flags = snappy_decode<true, RingIn, true>(in, B.clen, p, S.vlog + B.voff, B.ulen, lane, 64u);
+  if (lane == 0) {
+    SnappyWalk w;
+    w.count = 0;
+    w.flags = flags;
+    w.overflow = 0;
+    S.walk[b] = w;
+  }
+}
+
 __global__ void __launch_bounds__(64) k_snappy_global(SnappyParams S) {
   const uint64_t b = S.blk_base + (uint64_t)blockIdx.x * 64 + threadIdx.x;
   if (b >= S.blk_base + S.nblk) return;
@@ -385,7 +429,10 @@ void launch_snappy_dir(const SnappyParams& S, hipStream_t s) { hipLaunchKernelGG
 
 hipError_t launch_snappy_decode(const SnappyParams& S, hipStream_t s) {
   if (S.nblk == 0) return hipSuccess;
-  if (S.lds_bytes) {
+  static const bool gw = getenv("SPARKEY_SNAPPY_LDS") == nullptr;  // (A/B: the decoded block in LDS)
+  if (gw) {
+    hipLaunchKernelGGL(k_snappy_gw, dim3((uint32_t)S.nblk), 64, 0, s, S);
+  } else if (S.lds_bytes) {
     hipError_t e = hipFuncSetAttribute((const void*)k_snappy_lds, hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)S.lds_bytes);
     if (e != hipSuccess) return e;

@@ -322,6 +322,10 @@ struct sparkey_plan {
   MaxPlus* bpre = nullptr;
   MaxPlus* bfun_total = nullptr;
   int64_t* carry = nullptr;
+  MaxPlus* dfun = nullptr;     // fused_carry: per coarse digit
+  int64_t* dcarry = nullptr;
+  uint64_t c_dfun = 0, c_dcarry = 0;
+  uint32_t epoch = 0;          // fused_carry builds so far (tags the dfun words)
   uint64_t* pairs = nullptr;
   StatPart* parts = nullptr;
   unsigned long long* pdbg = nullptr;
@@ -365,6 +369,11 @@ static int plan_reserve(sparkey_plan* pl, uint64_t nchunks, uint64_t nrec, uint6
   HIP_TRY(grow(&pl->bpre, pl->c_bpre, nbuckets));
   HIP_TRY(grow(&pl->bfun_total, pl->c_bft, 1));
   HIP_TRY(grow(&pl->carry, pl->c_carry, nbuckets));
+  if (!pl->dfun) {
+    HIP_TRY(grow(&pl->dfun, pl->c_dfun, 256));
+    HIP_TRY(hipMemset(pl->dfun, 0, 256 * sizeof(MaxPlus)));  // epoch 0: no build's
+  }
+  HIP_TRY(grow(&pl->dcarry, pl->c_dcarry, 256));
   const uint64_t pair_cap = std::max<uint64_t>(1 << 16, std::min<uint64_t>(nrec, 1 << 22));
   HIP_TRY(grow(&pl->pairs, pl->c_pairs, 2 * pair_cap));
   HIP_TRY(grow(&pl->parts, pl->c_parts, std::max<uint64_t>(nbuckets, (cap + kStatSlotsPerBlock - 1) / kStatSlotsPerBlock)));
@@ -659,7 +668,7 @@ static int launch_framing(sparkey_plan* pl, const BuildParams& P, int framing_pa
     else launch_frame_fused(P, s, &pl->timer);
   } else if (framing_path == 2) {
     launch_frame_uniform(P, s, &pl->timer);
-    if (!(P.sharded && P.p1_region)) launch_dense_slabs(P, s);  // (a sharded rank reads only the regions)
+    if (!P.p1_region) launch_dense_slabs(P, s);  // (with digit regions nothing reads the slab counts)
   } else {
     launch_framing_serial(P, s);
     launch_emit(P, s, &pl->timer);
@@ -1103,6 +1112,14 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
       P.ent2 = pl->ent2;
     }
     P.fold_stats = fold ? 1 : 0;
+    // the carry composition inside k_part2s (its fixed-region pass), no summary / scan / carry kernels
+    P.fused_carry = P.p2_fixed && P.fold_stats && !getenv("SPARKEY_NO_FUSED_CARRY") ? 1 : 0;
+    P.dfun = pl->dfun;
+    P.dcarry = pl->dcarry;
+    if (P.fused_carry) {
+      pl->epoch = pl->epoch % ((1u << 22) - 1) + 1;
+      P.epoch = pl->epoch;
+    }
     rc = launch_framing(pl, P, framing_path, s, err, err_len);
     if (rc) return rc;
     launch_partition(P, s, &pl->timer);
@@ -1155,6 +1172,10 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
   }
   rc = status_error(st, err, err_len);
   if (rc) return rc;
+  if (st.guard) {
+    set_err(err, err_len, "internal error: placement check tripped (bits " + std::to_string(st.guard) + ")");
+    return SPARKEY_E_GPU;
+  }
   if (st.overflow || st.spec_fail) {
     set_err(err, err_len, "Corrupt log file: framing did not converge");
     return SPARKEY_E_CORRUPT_LOG;
@@ -1537,7 +1558,7 @@ void sparkey_plan_destroy(sparkey_plan* pl) {
   (void)hipSetDevice(pl->device);
   void* bufs[] = {pl->conv, pl->exitp, pl->qpos, pl->tail, pl->G, pl->cnt, pl->off, pl->ent, pl->ent2, pl->ent3,
                   pl->bcount, pl->bcursor, pl->boff, pl->bfun, pl->bpre, pl->bfun_total, pl->carry, pl->pairs,
-                  pl->parts, pl->pdbg, pl->p1_fill, pl->scan_u64, pl->scan_mp, pl->desc, pl->p1_hist, pl->p1_off, pl->d_status, pl->dbg, pl->wcount, pl->woff, pl->small,
+                  pl->dfun, pl->dcarry, pl->parts, pl->pdbg, pl->p1_fill, pl->scan_u64, pl->scan_mp, pl->desc, pl->p1_hist, pl->p1_off, pl->d_status, pl->dbg, pl->wcount, pl->woff, pl->small,
                   pl->eseg, pl->seg_cnt, pl->seg_off, pl->seg_mark, pl->seg_start, pl->bstat_start,
                   pl->seg_cls_cnt, pl->seg_cls_off, pl->p2tab,
                   pl->app_i64, pl->app_u32, pl->app_u64, pl->app_scan, pl->app_map,
