@@ -239,6 +239,40 @@ int sparkey_shard_boundary(sparkey_plan* plan, void* stream, uint64_t* out, char
  * its range: out = {max displacement, hash collisions, total displacement}. */
 int sparkey_shard_stats(sparkey_plan* plan, uint64_t prev_hash, int32_t prev_occ, void* stream, int64_t* out,
                         char* err, size_t err_len);
+/* ---- sharded exact path: logs with DELETE records or duplicate keys ----
+ * IndexHash.put / delete (IndexHash.java:454-665) replayed across ranks.  The bins above carry PUT
+ * records only, so sparkey_shard_place_dev + sparkey_shard_finish_dev leave the canonical placement of
+ * every PUT record; a slot it leaves empty is never crossed by a probe or a backward shift, so the ring
+ * splits at such slots into exact ranges that replay independently.  Rank r's exact range starts at
+ * the first empty slot of its slot range (if any) and runs to the next rank's start. */
+/* The first slot of the rank's range the placement left empty, or -1. */
+int sparkey_shard_first_empty(sparkey_plan* plan, void* stream, int64_t* slot_out, char* err, size_t err_len);
+/* Bytes per exchange record: {hash, address, the record's header VLQs and key, zero padded}; 0 when
+ * the header's maxKeyLen is above 4096 (such logs take the gathered path). */
+int32_t sparkey_shard_exact_record_size(const sparkey_plan* plan);
+/* Frames [entry, frame_end) again (PUT and DELETE records) and counts the records per exact owner:
+ * starts[world] = each rank's exact range start (-1: none; increasing otherwise), counts_out[world]. */
+int sparkey_shard_exact_frame(sparkey_plan* plan, int64_t entry, int64_t frame_end, const int64_t* starts,
+                              void* stream, uint64_t* counts_out, char* err, size_t err_len);
+/* The framed records as exchange records into d_send (sum(counts) x record size bytes), grouped by
+ * owner in rank order, log order within each owner. */
+int sparkey_shard_exact_pack(sparkey_plan* plan, uint8_t* d_send, uint64_t send_bytes, void* stream, char* err,
+                             size_t err_len);
+typedef struct sparkey_shard_exact_result {
+  int64_t num_entries;   /* entries the replay left in this rank's exact range */
+  int64_t garbage_size;  /* IndexHash's garbageSize contributions of the replay */
+  int64_t err_pos;       /* log offset of the failing record when rc != 0 */
+  int32_t rc;            /* SPARKEY_E_* raised by put / delete (e.g. a reference to a delete entry) */
+  int32_t reserved;
+} sparkey_shard_exact_result;
+/* Replays the n received exchange records (every source rank's, in rank order: log order) with the
+ * reference's put / delete on a local table of the reference's geometry. */
+int sparkey_shard_exact_build(sparkey_plan* plan, const uint8_t* d_recv, uint64_t n, void* stream,
+                              sparkey_shard_exact_result* result, char* err, size_t err_len);
+/* Slots [a, b) of the replay in the .spi slot layout, log addresses restored: packed at d_dst, or
+ * (d_dst NULL) into the rank's own slice, the buffer sparkey_shard_place_dev wrote. */
+int sparkey_shard_exact_extract(sparkey_plan* plan, uint64_t a, uint64_t b, uint8_t* d_dst, void* stream, char* err,
+                                size_t err_len);
 /* The 112-byte .spi header (IndexHeader.java:125-155) for the given totals. */
 int sparkey_index_header(const uint8_t* log_header, const sparkey_build_opts* opts, int64_t num_entries,
                          int64_t garbage_size, int64_t max_displacement, int64_t hash_collisions,

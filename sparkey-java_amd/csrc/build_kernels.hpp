@@ -345,5 +345,15 @@ void launch_p2_table_regions(hipStream_t s, const uint32_t* fill, uint64_t rc, u
                              Status* st, uint64_t n_records);
 void launch_shard_header(hipStream_t s, const int64_t* fin, int stride, int world, const IndexHeaderBytes& tmpl,
                          int64_t n_total, uint8_t* out);
+// sharded exact path (shard_exact_kernels.hip)
+void launch_first_empty(const BuildParams& P, hipStream_t s, unsigned long long* out);
+void launch_ex_count(const BuildParams& P, hipStream_t s, const int64_t* starts, int world, uint32_t* cnt,
+                     unsigned long long* totals);
+void launch_ex_offsets(hipStream_t s, const uint32_t* cnt, uint64_t* off, uint64_t n, uint64_t* scratch);
+void launch_ex_scatter(const BuildParams& P, hipStream_t s, const int64_t* starts, int world, const uint64_t* off,
+                       uint8_t* send, uint32_t rs);
+void launch_ex_ent(hipStream_t s, const uint8_t* recv, uint64_t n, uint32_t rs, Entry* ent);
+void launch_ex_extract(const BuildParams& L, const BuildParams& G, hipStream_t s, const uint8_t* recv, uint64_t n,
+                       uint32_t rs, uint64_t a, uint64_t b);
 
 }  // namespace sk

@@ -196,12 +196,12 @@ __global__ __launch_bounds__(256) void k_shard_row_async(ShardScalars sc, const 
                                                          const uint64_t* off, int world, int64_t* row) {
   const int t = threadIdx.x;
   const unsigned long long e = st->err;
-  const unsigned long long n = st->n_records, nd = st->n_deletes;
+  const unsigned long long n = st->n_records, nd = st->n_deletes;  // (nd: the row's scalar 4)
   const bool spec = slab_framing(path);
   const bool retry = (spec && st->max_wave_count > slab_cap) || st->overflow || n > max_records ||
                      st->spec_fail != 0 || (path != 1 && e != ~0ull) || n > send_cap;
   const int rc = e != ~0ull ? -(int)(e & 0xff) : 0;
-  const bool have = !retry && !rc && nd == 0 && n > 0;
+  const bool have = !retry && !rc && n > 0;  // (the bin skips DELETE records)
   if (t == 0) {
     row[0] = sc.v[0];
     row[1] = sc.v[1];

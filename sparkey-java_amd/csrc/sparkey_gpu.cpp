@@ -243,6 +243,7 @@ hipError_t grow_keep(T** p, uint64_t& have, uint64_t want, uint64_t used, hipStr
   return hipSuccess;
 }
 
+constexpr int64_t kExactMaxKey = 4096;     // sharded exact path: longest key its exchange records carry
 constexpr uint64_t kSnappyChunk = 1024;  // blocks per k_snappy_dir launch (swept 256-4096)
 
 }  // namespace
@@ -261,6 +262,15 @@ struct ShardState {
   BuildParams P_frame;  // the rank's framing (entries in slabs)
   int local = 0;        // world 1, no send buffer: the binned entries stay in ent3 (1 digit regions, 2 dense)
   IndexHeaderBytes tmpl;  // the .spi header template
+  // exact path (sparkey_shard_exact_*): the exact ranges' starts, the exchange record size, the
+  // records packed, and the replay over the received records (its local table and receive buffer)
+  std::vector<int64_t> ex_starts;
+  uint32_t ex_rs = 0;
+  uint64_t ex_total = 0;
+  bool ex_framed = false, ex_built = false;
+  BuildParams ex_L;
+  const uint8_t* ex_recv = nullptr;
+  uint64_t ex_n = 0;
 };
 
 struct sparkey_plan {
@@ -298,6 +308,13 @@ struct sparkey_plan {
   hipStream_t sn_stream = nullptr;  // the decode of one directory chunk overlaps the next chunk
   hipEvent_t sn_ev[2] = {nullptr, nullptr};
   uint64_t c_seg_cls_cnt = 0, c_seg_cls_off = 0;
+  // sharded exact path: the local replay table (the .spi layout with 8-byte addresses), the exact
+  // ranges' starts, per-(owner, slab) record counts and their scan
+  uint64_t c_xtab = 0, c_ex_starts = 0, c_ex_cnt = 0, c_ex_off = 0;
+  uint8_t* xtab = nullptr;
+  int64_t* ex_starts = nullptr;
+  uint32_t* ex_cnt = nullptr;
+  uint64_t* ex_off = nullptr;
   uint32_t* seg_cls_cnt = nullptr;
   uint64_t* seg_cls_off = nullptr;
   int64_t* seg_mark = nullptr;
@@ -982,6 +999,73 @@ static int plan_build_snappy(sparkey_plan* pl, const LogHdr& lh, const uint8_t* 
   return SPARKEY_OK;
 }
 
+// The exact path's segment replay (exact_kernels.hip) after the canonical placement of the PUT
+// records in P.out: segments, their records grouped, replayed per size class.  Enqueued only.
+static int run_exact_segments(sparkey_plan* pl, BuildParams& P, bool in_memory, hipStream_t s, char* err,
+                              size_t err_len) {
+  HIP_TRY(grow(&pl->eseg, pl->c_eseg, P.nslabs * (uint64_t)P.slab_cap));
+  HIP_TRY(grow(&pl->seg_cnt, pl->c_seg_cnt, P.cap));
+  HIP_TRY(grow(&pl->seg_off, pl->c_seg_off, P.cap + 1));
+  HIP_TRY(grow(&pl->seg_mark, pl->c_seg_mark, P.cap + 1));
+  HIP_TRY(grow(&pl->seg_start, pl->c_seg_start, P.cap));
+  HIP_TRY(grow(&pl->seg_cls_cnt, pl->c_seg_cls_cnt, 4 * (P.cap / 1024 + 1)));
+  HIP_TRY(grow(&pl->seg_cls_off, pl->c_seg_cls_off, 4 * (P.cap / 1024 + 1) + 1));
+  const uint64_t scratch = P.cap / kScanTile + 64;
+  if (pl->c_su < scratch + 16) {
+    HIP_TRY(grow(&pl->scan_u64, pl->c_su, scratch + 16));
+    P.scan_scratch_u64 = pl->scan_u64;
+  }
+  P.eseg = pl->eseg;
+  P.seg_cnt = pl->seg_cnt;
+  P.seg_off = pl->seg_off;
+  P.seg_mark = pl->seg_mark;
+  P.seg_start = pl->seg_start;
+  P.seg_cls_cnt = pl->seg_cls_cnt;
+  P.seg_cls_off = pl->seg_cls_off;
+  HIP_TRY(hipMemsetAsync(P.seg_cnt, 0, P.cap * sizeof(uint32_t), s));
+  HIP_TRY(hipMemsetAsync((uint8_t*)pl->d_status + offsetof(Status, num_entries), 0, 2 * sizeof(long long), s));
+  HIP_TRY(hipMemsetAsync((uint8_t*)pl->d_status + offsetof(Status, n_segs), 0, sizeof(((Status*)0)->n_segs), s));
+  const char* dbg_env = getenv("SPARKEY_EXACT_DEBUG");
+  const bool seg_dbg = dbg_env != nullptr;
+  if (seg_dbg) {
+    HIP_TRY(grow(&pl->dbg, pl->c_dbg, kSegDebugWords));
+    HIP_TRY(hipMemsetAsync(pl->dbg, 0, kSegDebugWords * sizeof(unsigned long long), s));
+    P.dbg = pl->dbg;
+  } else {
+    P.dbg = nullptr;
+  }
+  if (!pl->side_ok) {
+    for (int i = 0; i < 3; i++) {
+      HIP_TRY(hipStreamCreateWithFlags(&pl->side.s[i], hipStreamNonBlocking));
+      HIP_TRY(hipEventCreateWithFlags(&pl->side.join[i], hipEventDisableTiming));
+    }
+    HIP_TRY(hipEventCreateWithFlags(&pl->side.fork, hipEventDisableTiming));
+    pl->side_ok = true;
+  }
+  launch_segments(P, s, in_memory ? 0 : 1, &pl->timer, dbg_env && atoi(dbg_env) >= 2, &pl->side);
+  if (seg_dbg) {
+    std::vector<unsigned long long> h(kSegDebugWords);
+    HIP_TRY(hipMemcpyAsync(h.data(), pl->dbg, h.size() * 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    static const char* cname[3] = {"mid", "large", "huge"};
+    for (int c = 0, b0 = 0; c < 3; b0 += kSegDebugWaves[c], c++) {
+      const unsigned b1 = b0 + kSegDebugWaves[c];
+      double sum[8] = {0};
+      unsigned long long mx[8] = {0};
+      for (unsigned b = b0; b < b1; b++)
+        for (int i = 0; i < 8; i++) {
+          sum[i] += (double)h[b * 8 + i];
+          mx[i] = std::max(mx[i], h[b * 8 + i]);
+        }
+      fprintf(stderr, "[exact %s] segs %.0f recs %.0f | cycles/seg stage %.0f sort %.0f replay %.0f write %.0f | "
+                      "max wave: segs %llu stage %llu sort %llu replay %llu write %llu\n",
+              cname[c], sum[4], sum[5], sum[0] / std::max(1.0, sum[4]), sum[1] / std::max(1.0, sum[4]),
+              sum[2] / std::max(1.0, sum[4]), sum[3] / std::max(1.0, sum[4]), mx[4], mx[0], mx[1], mx[2], mx[3]);
+    }
+  }
+  return SPARKEY_OK;
+}
+
 static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t* d_log, uint64_t log_len,
                       uint8_t* d_out, uint64_t index_cap, const sparkey_build_opts* opts, hipStream_t s,
                       sparkey_build_stats* stats_out, char* err, size_t err_len) {
@@ -1218,66 +1302,8 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
       HIP_TRY(hipMemsetAsync(d_out + kIndexHeaderSize, 0, (size_t)(ip.index_size - kIndexHeaderSize), s));
       launch_sequential(Pd, s, ip.in_memory ? 0 : 1);
     } else {
-      HIP_TRY(grow(&pl->eseg, pl->c_eseg, P.nslabs * (uint64_t)P.slab_cap));
-      HIP_TRY(grow(&pl->seg_cnt, pl->c_seg_cnt, P.cap));
-      HIP_TRY(grow(&pl->seg_off, pl->c_seg_off, P.cap + 1));
-      HIP_TRY(grow(&pl->seg_mark, pl->c_seg_mark, P.cap + 1));
-      HIP_TRY(grow(&pl->seg_start, pl->c_seg_start, P.cap));
-      HIP_TRY(grow(&pl->seg_cls_cnt, pl->c_seg_cls_cnt, 4 * (P.cap / 1024 + 1)));
-      HIP_TRY(grow(&pl->seg_cls_off, pl->c_seg_cls_off, 4 * (P.cap / 1024 + 1) + 1));
-      const uint64_t scratch = P.cap / kScanTile + 64;
-      if (pl->c_su < scratch + 16) {
-        HIP_TRY(grow(&pl->scan_u64, pl->c_su, scratch + 16));
-        P.scan_scratch_u64 = pl->scan_u64;
-      }
-      P.eseg = pl->eseg;
-      P.seg_cnt = pl->seg_cnt;
-      P.seg_off = pl->seg_off;
-      P.seg_mark = pl->seg_mark;
-      P.seg_start = pl->seg_start;
-      P.seg_cls_cnt = pl->seg_cls_cnt;
-      P.seg_cls_off = pl->seg_cls_off;
-      HIP_TRY(hipMemsetAsync(P.seg_cnt, 0, P.cap * sizeof(uint32_t), s));
-      HIP_TRY(hipMemsetAsync((uint8_t*)pl->d_status + offsetof(Status, num_entries), 0, 2 * sizeof(long long), s));
-      HIP_TRY(hipMemsetAsync((uint8_t*)pl->d_status + offsetof(Status, n_segs), 0, sizeof(((Status*)0)->n_segs), s));
-      const bool seg_dbg = getenv("SPARKEY_EXACT_DEBUG") != nullptr;
-      if (seg_dbg) {
-        HIP_TRY(grow(&pl->dbg, pl->c_dbg, kSegDebugWords));
-        HIP_TRY(hipMemsetAsync(pl->dbg, 0, kSegDebugWords * sizeof(unsigned long long), s));
-        P.dbg = pl->dbg;
-      } else {
-        P.dbg = nullptr;
-      }
-      const char* dbg_env = getenv("SPARKEY_EXACT_DEBUG");
-      if (!pl->side_ok) {
-        for (int i = 0; i < 3; i++) {
-          HIP_TRY(hipStreamCreateWithFlags(&pl->side.s[i], hipStreamNonBlocking));
-          HIP_TRY(hipEventCreateWithFlags(&pl->side.join[i], hipEventDisableTiming));
-        }
-        HIP_TRY(hipEventCreateWithFlags(&pl->side.fork, hipEventDisableTiming));
-        pl->side_ok = true;
-      }
-      launch_segments(P, s, ip.in_memory ? 0 : 1, &pl->timer, dbg_env && atoi(dbg_env) >= 2, &pl->side);
-      if (seg_dbg) {
-        std::vector<unsigned long long> h(kSegDebugWords);
-        HIP_TRY(hipMemcpyAsync(h.data(), pl->dbg, h.size() * 8, hipMemcpyDeviceToHost, s));
-        HIP_TRY(hipStreamSynchronize(s));
-        static const char* cname[3] = {"mid", "large", "huge"};
-        for (int c = 0, b0 = 0; c < 3; b0 += kSegDebugWaves[c], c++) {
-          const unsigned b1 = b0 + kSegDebugWaves[c];
-          double sum[8] = {0};
-          unsigned long long mx[8] = {0};
-          for (unsigned b = b0; b < b1; b++)
-            for (int i = 0; i < 8; i++) {
-              sum[i] += (double)h[b * 8 + i];
-              mx[i] = std::max(mx[i], h[b * 8 + i]);
-            }
-          fprintf(stderr, "[exact %s] segs %.0f recs %.0f | cycles/seg stage %.0f sort %.0f replay %.0f write %.0f | "
-                          "max wave: segs %llu stage %llu sort %llu replay %llu write %llu\n",
-                  cname[c], sum[4], sum[5], sum[0] / std::max(1.0, sum[4]), sum[1] / std::max(1.0, sum[4]),
-                  sum[2] / std::max(1.0, sum[4]), sum[3] / std::max(1.0, sum[4]), mx[4], mx[0], mx[1], mx[2], mx[3]);
-        }
-      }
+      rc = run_exact_segments(pl, P, ip.in_memory, s, err, err_len);
+      if (rc) return rc;
     }
     launch_stats(P, s, 1, &pl->timer);
     HIP_TRY(hipGetLastError());
@@ -1562,7 +1588,8 @@ void sparkey_plan_destroy(sparkey_plan* pl) {
                   pl->eseg, pl->seg_cnt, pl->seg_off, pl->seg_mark, pl->seg_start, pl->bstat_start,
                   pl->seg_cls_cnt, pl->seg_cls_off, pl->p2tab,
                   pl->app_i64, pl->app_u32, pl->app_u64, pl->app_scan, pl->app_map,
-                  pl->sn_blocks, pl->sn_dir, pl->sn_walk, pl->sn_recoff, pl->sn_vlog, pl->sn_itab, pl->sn_err};
+                  pl->sn_blocks, pl->sn_dir, pl->sn_walk, pl->sn_recoff, pl->sn_vlog, pl->sn_itab, pl->sn_err,
+                  pl->xtab, pl->ex_starts, pl->ex_cnt, pl->ex_off};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (pl->h_status) (void)hipHostFree(pl->h_status);
@@ -1665,6 +1692,9 @@ int sparkey_shard_begin(sparkey_plan* pl, const uint8_t* log_header, uint64_t fi
   shard_range(sh.P, rank, world, &sh.P.b_lo, &sh.P.b_hi, &sh.P.slot_lo, &sh.P.slot_hi);
   index_header_template(sh.lh, sh.ip, opts->hash_seed, sh.tmpl.b);
   sh.local = 0;
+  sh.ex_framed = sh.ex_built = false;
+  sh.ex_recv = nullptr;
+  sh.ex_n = 0;
   HIP_TRY(grow(&pl->small, pl->c_small, 512));
   sh.active = true;
   return SPARKEY_OK;
@@ -1737,6 +1767,7 @@ static int shard_frame_setup(sparkey_plan* pl, int64_t entry, int64_t frame_end,
   if (rc) return rc;
   P.st = pl->d_status;
   P.sharded = 1;
+  P.skip_del = 1;  // the bin carries PUT records only (their canonical placement); DELETEs: the exact path
   P.b_lo = sh.P.b_lo; P.b_hi = sh.P.b_hi; P.slot_lo = sh.P.slot_lo; P.slot_hi = sh.P.slot_hi;
   F->fused = P.max_rec_len <= 4096;
   const double frac = (double)(frame_end - entry) / (double)std::max<int64_t>(1, data_end - kLogHeaderSize);
@@ -1807,12 +1838,14 @@ static int shard_frame_args(sparkey_plan* pl, int64_t entry, int64_t* frame_end,
   return SPARKEY_OK;
 }
 
-int sparkey_shard_frame(sparkey_plan* pl, int64_t entry, int64_t frame_end, void* stream,
-                        sparkey_shard_frame_result* res, char* err, size_t err_len) {
-  int rc = shard_check(pl, err, err_len);
-  if (rc) return rc;
+}  // extern "C"
+
+// sparkey_shard_frame's body; allow_regions = false keeps the entries in slabs in log order (the
+// exact path packs them from there) where uniform framing would write digit regions
+static int shard_frame_sync(sparkey_plan* pl, int64_t entry, int64_t frame_end, hipStream_t s,
+                            sparkey_shard_frame_result* res, bool allow_regions, char* err, size_t err_len) {
   ShardState& sh = pl->shard;
-  hipStream_t s = stream ? (hipStream_t)stream : pl->own_stream;
+  int rc;
   const int64_t data_end = std::max<int64_t>(sh.lh.data_end, kLogHeaderSize);
   memset(res, 0, sizeof(*res));
   res->exit = entry;
@@ -1823,6 +1856,7 @@ int sparkey_shard_frame(sparkey_plan* pl, int64_t entry, int64_t frame_end, void
   ShardFrameSetup F;
   rc = shard_frame_setup(pl, entry, frame_end, &F, err, err_len);
   if (rc) return rc;
+  F.use_regions = F.use_regions && allow_regions;
   BuildParams& P = F.P;
   Status& st = *pl->h_status;
   for (int attempt = 0; attempt < 6; attempt++) {
@@ -1877,6 +1911,16 @@ int sparkey_shard_frame(sparkey_plan* pl, int64_t entry, int64_t frame_end, void
   sh.P_frame = P;
   sh.n_local = st.n_records;
   return SPARKEY_OK;
+}
+
+extern "C" {
+
+int sparkey_shard_frame(sparkey_plan* pl, int64_t entry, int64_t frame_end, void* stream,
+                        sparkey_shard_frame_result* res, char* err, size_t err_len) {
+  int rc = shard_check(pl, err, err_len);
+  if (rc) return rc;
+  hipStream_t s = stream ? (hipStream_t)stream : pl->own_stream;
+  return shard_frame_sync(pl, entry, frame_end, s, res, true, err, err_len);
 }
 
 int64_t sparkey_shard_frame_capacity(sparkey_plan* pl, int64_t entry, int64_t frame_end) {
@@ -2260,6 +2304,237 @@ int sparkey_shard_stats(sparkey_plan* pl, uint64_t prev_hash, int32_t prev_occ, 
   out[0] = pl->h_status->max_disp;
   out[1] = pl->h_status->collisions;
   out[2] = pl->h_status->total_disp;
+  return SPARKEY_OK;
+}
+
+// ---- sharded exact path ----
+
+int sparkey_shard_first_empty(sparkey_plan* pl, void* stream, int64_t* slot_out, char* err, size_t err_len) {
+  int rc = shard_check(pl, err, err_len);
+  if (rc) return rc;
+  hipStream_t s = stream ? (hipStream_t)stream : pl->own_stream;
+  const BuildParams& P = pl->shard.P;
+  if (!slot_out || !P.out) {
+    set_err(err, err_len, "no placement to search (sparkey_shard_place_dev first)");
+    return SPARKEY_E_ARG;
+  }
+  unsigned long long* d = reinterpret_cast<unsigned long long*>(pl->small) + 400;
+  HIP_TRY(hipMemsetAsync(d, 0xff, sizeof(unsigned long long), s));
+  launch_first_empty(P, s, d);
+  HIP_TRY(hipGetLastError());
+  unsigned long long v = ~0ull;
+  HIP_TRY(hipMemcpyAsync(&v, d, sizeof(v), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  *slot_out = v == ~0ull ? -1 : (int64_t)v;
+  return SPARKEY_OK;
+}
+
+int32_t sparkey_shard_exact_record_size(const sparkey_plan* pl) {
+  if (!pl || !pl->shard.active) return SPARKEY_E_ARG;
+  const int64_t k = pl->shard.lh.max_key_len;
+  if (k < 0 || k > kExactMaxKey) return 0;
+  return (int32_t)(16 + ((10 + k + 7) & ~7LL));  // {hash, address} + two VLQs (<= 5 bytes each) + key
+}
+
+int sparkey_shard_exact_frame(sparkey_plan* pl, int64_t entry, int64_t frame_end, const int64_t* starts, void* stream,
+                              uint64_t* counts_out, char* err, size_t err_len) {
+  int rc = shard_check(pl, err, err_len);
+  if (rc) return rc;
+  ShardState& sh = pl->shard;
+  hipStream_t s = stream ? (hipStream_t)stream : pl->own_stream;
+  const int W = sh.world;
+  sh.ex_framed = false;
+  sh.ex_built = false;
+  if (!starts || !counts_out) {
+    set_err(err, err_len, "null argument");
+    return SPARKEY_E_ARG;
+  }
+  sh.ex_rs = (uint32_t)sparkey_shard_exact_record_size(pl);
+  if (!sh.ex_rs) {
+    set_err(err, err_len, "keys too long for the exact exchange records");
+    return SPARKEY_E_UNSUPPORTED;
+  }
+  sh.ex_starts.assign(starts, starts + W);
+  int64_t prev = -1;
+  bool any = false;
+  for (int r = 0; r < W; r++) {
+    const int64_t e = starts[r];
+    if (e < 0) continue;
+    if ((uint64_t)e >= sh.ip.cap || e <= prev) {
+      set_err(err, err_len, "exact range starts must increase with the rank and lie in the table");
+      return SPARKEY_E_ARG;
+    }
+    prev = e;
+    any = true;
+  }
+  if (!any) {
+    set_err(err, err_len, "no exact range (no empty slot)");
+    return SPARKEY_E_ARG;
+  }
+  for (int r = 0; r < W; r++) counts_out[r] = 0;
+  sparkey_shard_frame_result fr;
+  rc = shard_frame_sync(pl, entry, frame_end, s, &fr, false, err, err_len);
+  if (rc) return rc;
+  if (fr.rc) {
+    set_err(err, err_len, std::string(code_message(fr.rc)) + " (log offset " + std::to_string(fr.err_pos) + ")");
+    return fr.rc;
+  }
+  sh.ex_total = 0;
+  sh.ex_framed = true;
+  if (!sh.n_local) return SPARKEY_OK;
+  BuildParams& P = sh.P_frame;
+  HIP_TRY(grow(&pl->ex_starts, pl->c_ex_starts, (uint64_t)W + 1));
+  HIP_TRY(grow(&pl->ex_cnt, pl->c_ex_cnt, (uint64_t)W * P.nslabs));
+  HIP_TRY(grow(&pl->ex_off, pl->c_ex_off, (uint64_t)W * P.nslabs + 1));
+  const uint64_t scratch = ((uint64_t)W * P.nslabs) / kScanTile + 80;
+  HIP_TRY(grow(&pl->scan_u64, pl->c_su, std::max<uint64_t>(pl->c_su, scratch)));
+  HIP_TRY(hipMemcpyAsync(pl->ex_starts, starts, W * sizeof(int64_t), hipMemcpyHostToDevice, s));
+  unsigned long long* tot = reinterpret_cast<unsigned long long*>(pl->small);
+  HIP_TRY(hipMemsetAsync(tot, 0, W * sizeof(unsigned long long), s));
+  launch_ex_count(P, s, pl->ex_starts, W, pl->ex_cnt, tot);
+  launch_ex_offsets(s, pl->ex_cnt, pl->ex_off, (uint64_t)W * P.nslabs, pl->scan_u64);
+  HIP_TRY(hipGetLastError());
+  std::vector<unsigned long long> h(W);
+  HIP_TRY(hipMemcpyAsync(h.data(), tot, W * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  for (int r = 0; r < W; r++) {
+    counts_out[r] = h[r];
+    sh.ex_total += h[r];
+  }
+  if (sh.ex_total != sh.n_local) {
+    set_err(err, err_len, "internal: exact counts do not cover the framed records");
+    return SPARKEY_E_GPU;
+  }
+  return SPARKEY_OK;
+}
+
+int sparkey_shard_exact_pack(sparkey_plan* pl, uint8_t* d_send, uint64_t send_bytes, void* stream, char* err,
+                             size_t err_len) {
+  int rc = shard_check(pl, err, err_len);
+  if (rc) return rc;
+  ShardState& sh = pl->shard;
+  hipStream_t s = stream ? (hipStream_t)stream : pl->own_stream;
+  if (!sh.ex_framed) {
+    set_err(err, err_len, "sparkey_shard_exact_frame first");
+    return SPARKEY_E_ARG;
+  }
+  if (!sh.ex_total) return SPARKEY_OK;
+  if (!d_send || ((uintptr_t)d_send & 15) || send_bytes < sh.ex_total * sh.ex_rs) {
+    set_err(err, err_len, "send buffer too small or misaligned: need " + std::to_string(sh.ex_total * sh.ex_rs));
+    return SPARKEY_E_BUFFER;
+  }
+  launch_ex_scatter(sh.P_frame, s, pl->ex_starts, sh.world, pl->ex_off, d_send, sh.ex_rs);
+  HIP_TRY(hipGetLastError());
+  return SPARKEY_OK;
+}
+
+int sparkey_shard_exact_build(sparkey_plan* pl, const uint8_t* d_recv, uint64_t n, void* stream,
+                              sparkey_shard_exact_result* res, char* err, size_t err_len) {
+  int rc = shard_check(pl, err, err_len);
+  if (rc) return rc;
+  ShardState& sh = pl->shard;
+  hipStream_t s = stream ? (hipStream_t)stream : pl->own_stream;
+  if (!res || (n && (!d_recv || ((uintptr_t)d_recv & 15))) || !sh.ex_rs) {
+    set_err(err, err_len, "bad exact build arguments");
+    return SPARKEY_E_ARG;
+  }
+  memset(res, 0, sizeof(*res));
+  sh.ex_built = false;
+  sh.ex_recv = d_recv;
+  sh.ex_n = n;
+  BuildParams& L = sh.ex_L;
+  memset(&L, 0, sizeof(L));
+  if (n) {
+    // the local replay: the reference's table geometry (capacity, hash size) with 8-byte addresses,
+    // which are offsets into the receive buffer
+    IndexParams ipl = sh.ip;
+    ipl.addr_size = 8;
+    ipl.ebb = 0;
+    ipl.slot_size = ipl.hash_size + 8;
+    ipl.index_size = kIndexHeaderSize + (int64_t)ipl.cap * ipl.slot_size;
+    rc = setup_params(sh.lh, ipl, sh.opts, d_recv, n * (uint64_t)sh.ex_rs, kLogHeaderSize, kLogHeaderSize, &L, err,
+                      err_len);
+    if (rc) return rc;
+    L.st = pl->d_status;
+    rc = reserve_for_framing(pl, L, 1, n, kPartTile, err, err_len);
+    if (rc) return rc;
+    HIP_TRY(grow(&pl->xtab, pl->c_xtab, (uint64_t)ipl.index_size));
+    L.out = pl->xtab;
+    HIP_TRY(hipMemsetAsync(pl->xtab, 0, (size_t)ipl.index_size, s));
+    launch_status_reset(s, pl->d_status, n);
+    launch_ex_ent(s, d_recv, n, sh.ex_rs, L.ent);
+    launch_dense_slabs(L, s);
+    // canonical placement of the PUT records (the segments), then the replay per segment
+    L.skip_del = 1;
+    L.p1_region = 0;
+    L.p1_hist_ready = 0;
+    L.p2_sorted = 0;
+    L.p2_fixed = 0;
+    L.fold_stats = 0;
+    L.fused_carry = 0;
+    launch_partition(L, s, &pl->timer);
+    launch_place_fast(L, s, &pl->timer);
+    rc = run_exact_segments(pl, L, ipl.in_memory, s, err, err_len);
+    if (rc) return rc;
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(pl->h_status, pl->d_status, sizeof(Status), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    const Status& st = *pl->h_status;
+    if (st.guard) {
+      set_err(err, err_len, "internal error: exact-path bounds check tripped (bits " + std::to_string(st.guard) + ")");
+      return SPARKEY_E_GPU;
+    }
+    if (st.err != ~0ull) {  // an error at a local record offset: report the record's log position
+      const uint64_t q = (uint64_t)(st.err >> 8);
+      res->rc = -(int32_t)(st.err & 0xff);
+      res->err_pos = -1;
+      if (q >= 16 && (q - 16) % sh.ex_rs == 0 && (q - 16) / sh.ex_rs < n) {
+        uint64_t a = 0;
+        HIP_TRY(hipMemcpy(&a, d_recv + (q - 16) + 8, sizeof(a), hipMemcpyDeviceToHost));
+        res->err_pos = (int64_t)((a & ~kDelBit) >> sh.ip.ebb);
+      }
+    }
+    res->num_entries = st.num_entries;
+    res->garbage_size = st.garbage;
+  }
+  // the stats steps read the plan's workspace through sh.P: it may have moved
+  sh.P.parts = pl->parts;
+  sh.P.scan_scratch_u64 = pl->scan_u64;
+  sh.P.scan_scratch_mp = pl->scan_mp;
+  sh.P.st = pl->d_status;
+  sh.ex_built = true;
+  return SPARKEY_OK;
+}
+
+int sparkey_shard_exact_extract(sparkey_plan* pl, uint64_t a, uint64_t b, uint8_t* d_dst, void* stream, char* err,
+                                size_t err_len) {
+  int rc = shard_check(pl, err, err_len);
+  if (rc) return rc;
+  ShardState& sh = pl->shard;
+  hipStream_t s = stream ? (hipStream_t)stream : pl->own_stream;
+  if (!sh.ex_built || a > b || b > sh.ip.cap) {
+    set_err(err, err_len, "bad exact extract arguments");
+    return SPARKEY_E_ARG;
+  }
+  if (a == b) return SPARKEY_OK;
+  BuildParams G = sh.P;  // the .spi slot layout
+  if (d_dst) {
+    if (((uintptr_t)d_dst & 3) || (G.slot_size == 16 && ((uintptr_t)d_dst & 15)) || (G.slot_size == 8 && ((uintptr_t)d_dst & 7))) {
+      set_err(err, err_len, "misaligned destination");
+      return SPARKEY_E_ARG;
+    }
+    G.out = d_dst - kIndexHeaderSize - a * (uint64_t)G.slot_size;
+  } else if (!G.out || a < G.slot_lo || b > G.slot_hi) {
+    set_err(err, err_len, "slots outside the rank's range (or no slice placed)");
+    return SPARKEY_E_ARG;
+  }
+  BuildParams L = sh.ex_L;
+  if (!sh.ex_n) {
+    L = sh.P;
+    L.out = nullptr;  // nothing received: the range is empty
+  }
+  launch_ex_extract(L, G, s, sh.ex_recv, sh.ex_n, sh.ex_rs, a, b);
+  HIP_TRY(hipGetLastError());
   return SPARKEY_OK;
 }
 

@@ -111,6 +111,11 @@ class ShardFrameResult(ctypes.Structure):
                 ("err_pos", ctypes.c_int64), ("rc", ctypes.c_int32), ("framing_path", ctypes.c_int32)]
 
 
+class ShardExactResult(ctypes.Structure):
+    _fields_ = [("num_entries", ctypes.c_int64), ("garbage_size", ctypes.c_int64), ("err_pos", ctypes.c_int64),
+                ("rc", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
 _u64p = ctypes.POINTER(ctypes.c_uint64)
 _i64p = ctypes.POINTER(ctypes.c_int64)
 _E = [ctypes.c_char_p, ctypes.c_size_t]
@@ -139,6 +144,12 @@ _SIGS = {
     "sparkey_shard_apply_spill": ([_vp, _vp, ctypes.c_uint64, _vp] + _E, ctypes.c_int),
     "sparkey_shard_boundary": ([_vp, _vp, _u64p] + _E, ctypes.c_int),
     "sparkey_shard_stats": ([_vp, ctypes.c_uint64, ctypes.c_int32, _vp, _i64p] + _E, ctypes.c_int),
+    "sparkey_shard_first_empty": ([_vp, _vp, _i64p] + _E, ctypes.c_int),
+    "sparkey_shard_exact_record_size": ([_vp], ctypes.c_int32),
+    "sparkey_shard_exact_frame": ([_vp, ctypes.c_int64, ctypes.c_int64, _i64p, _vp, _u64p] + _E, ctypes.c_int),
+    "sparkey_shard_exact_pack": ([_vp, _vp, ctypes.c_uint64, _vp] + _E, ctypes.c_int),
+    "sparkey_shard_exact_build": ([_vp, _vp, ctypes.c_uint64, _vp, ctypes.POINTER(ShardExactResult)] + _E, ctypes.c_int),
+    "sparkey_shard_exact_extract": ([_vp, ctypes.c_uint64, ctypes.c_uint64, _vp, _vp] + _E, ctypes.c_int),
     "sparkey_index_header": ([_vp, ctypes.POINTER(BuildOpts), ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
                               ctypes.c_int64, ctypes.c_int64, _vp] + _E, ctypes.c_int),
     "sparkey_log_append": ([_vp, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_uint64, _vp, ctypes.c_uint64, _u64p, _vp]
@@ -391,6 +402,34 @@ class Plan:
         out = (ctypes.c_int64 * 3)()
         self._call("sparkey_shard_stats", prev_hash, prev_occ, ctypes.c_void_p(stream), out)
         return int(out[0]), int(out[1]), int(out[2])
+
+    # ---- sharded exact path (logs with DELETEs or duplicate keys) ----
+    def shard_first_empty(self, stream: int = 0) -> int:
+        v = ctypes.c_int64()
+        self._call("sparkey_shard_first_empty", ctypes.c_void_p(stream), ctypes.byref(v))
+        return v.value
+
+    def shard_exact_record_size(self) -> int:
+        return int(_lib.sparkey_shard_exact_record_size(self._h))
+
+    def shard_exact_frame(self, entry: int, frame_end: int, starts, stream: int = 0):
+        world = len(starts)
+        st = (ctypes.c_int64 * world)(*[int(v) for v in starts])
+        counts = (ctypes.c_uint64 * world)()
+        self._call("sparkey_shard_exact_frame", entry, frame_end, st, ctypes.c_void_p(stream), counts)
+        return [int(x) for x in counts]
+
+    def shard_exact_pack(self, d_send: int, send_bytes: int, stream: int = 0) -> None:
+        self._call("sparkey_shard_exact_pack", ctypes.c_void_p(d_send or None), send_bytes, ctypes.c_void_p(stream))
+
+    def shard_exact_build(self, d_recv: int, n: int, stream: int = 0) -> ShardExactResult:
+        r = ShardExactResult()
+        self._call("sparkey_shard_exact_build", ctypes.c_void_p(d_recv or None), n, ctypes.c_void_p(stream),
+                   ctypes.byref(r))
+        return r
+
+    def shard_exact_extract(self, a: int, b: int, d_dst: int = 0, stream: int = 0) -> None:
+        self._call("sparkey_shard_exact_extract", a, b, ctypes.c_void_p(d_dst or None), ctypes.c_void_p(stream))
 
     def stage_times(self):
         n = _lib.sparkey_plan_stage_count(self._h)

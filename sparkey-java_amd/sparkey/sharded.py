@@ -19,8 +19,12 @@ device steps of include/sparkey_gpu.h ("sharded build") in between:
   4. stats      calculateMaxDisplacement (IndexHash.java:195-245) per range with the boundary slots
                 exchanged; the totals are reduced and rank 0 writes the 112-byte header.
 
-SNAPPY logs, and logs the canonical layout does not cover (DELETEs, duplicate keys, a full table), are gathered on
-every rank and built with the exact single-GPU path (correct, not scaled).
+Logs the canonical layout does not cover (DELETEs, duplicate keys) take the sharded exact path
+(_exact): the canonical placement of the PUT records splits the ring at empty slots
+into exact ranges, every record goes to the owner of its range with its header and key, and each
+owner replays IndexHash.put / delete (IndexHash.java:454-665) on its range.  SNAPPY / ZSTD logs, keys
+over 4 KiB and tables the PUT records fill are gathered on every rank and built with the single-GPU
+path (correct, not scaled).
 
 Collectives go through torch.distributed: backend "nccl" (RCCL over xGMI) moves device tensors;
 "gloo" (CPU tests, several ranks on one GPU) stages them through host memory.
@@ -288,6 +292,27 @@ class GpuShardSteps:
     def index_header(self, opts, num_entries, garbage, max_disp, collisions, total_disp) -> bytes:
         return self.n.index_header(self.header, opts, num_entries, garbage, max_disp, collisions, total_disp)
 
+    # exact path (DELETEs, duplicate keys): include/sparkey_gpu.h "sharded exact path"
+    def first_empty(self) -> int:
+        return self.plan.shard_first_empty(self.stream)
+
+    def exact_record_size(self) -> int:
+        return self.plan.shard_exact_record_size()
+
+    def exact_frame(self, entry: int, frame_end: int, starts) -> list:
+        return self.plan.shard_exact_frame(entry, frame_end, starts, self.stream)
+
+    def exact_pack(self, send: torch.Tensor) -> None:
+        self.plan.shard_exact_pack(send.data_ptr(), send.numel(), self.stream)
+
+    def exact_build(self, recv: torch.Tensor, n: int) -> dict:
+        self._keep_recv = recv  # the replay's log: read again by exact_extract
+        r = self.plan.shard_exact_build(recv.data_ptr() if n else 0, n, self.stream)
+        return {"rc": r.rc, "err_pos": r.err_pos, "num_entries": r.num_entries, "garbage": r.garbage_size}
+
+    def exact_extract(self, a: int, b: int, dst: torch.Tensor = None, dst_off: int = 0) -> None:
+        self.plan.shard_exact_extract(a, b, 0 if dst is None else dst.data_ptr() + dst_off, self.stream)
+
     def full_build(self, log: torch.Tensor, file_len: int, out: torch.Tensor, opts):
         st = self.plan.build(self.header, log.data_ptr(), file_len, out.data_ptr(), out.numel(), opts, self.stream)
         return {"num_entries": st.num_entries, "garbage_size": st.garbage_size, "max_displacement": st.max_displacement,
@@ -439,7 +464,7 @@ class ShardedBuilder:
                     s.frame_bin_async(entries[g], fe, send, cap, row)
                 else:  # the speculative attempt did not hold: frame with every retry, then bin
                     mine = s.frame(entries[g], fe)  # owns nothing when entries[g] >= fe
-                    n_mine = int(mine["n"]) if not mine["rc"] and not mine["ndel"] else 0
+                    n_mine = int(mine["n"]) if not mine["rc"] else 0
                     send = None if G == 1 else s.alloc(max(1, n_mine) * ENTRY_BYTES)
                     s.bin_row(send, n_mine, [entries[g], fe, mine["exit"], mine["n"], mine["ndel"], mine["rc"],
                                              mine["err_pos"], 0], row)
@@ -468,7 +493,6 @@ class ShardedBuilder:
                 break
             if done:
                 break
-        n_mine = int(R[g][3]) if not R[g][5] and not R[g][4] else 0
         totals = R[:, 3].astype(np.int64)
         n_total = int(totals.sum())
         n_deletes = int(R[:, 4].sum())
@@ -481,13 +505,15 @@ class ShardedBuilder:
                           phase_ms=phase)
         mark("frame+verify")
 
-        if n_deletes > 0 or n_total >= _capacity(h, opts):
+        if n_total - n_deletes >= _capacity(h, opts):  # the PUT records may fill the table: one lane's replay
             return self._gathered(res, header, file_len, buf, buf_lo, buf_hi, lay, opts, slot_size, out_len)
 
-        # ---- 2 exchange: every entry to the owner of its slot range (binned while framing) ----
+        # ---- 2 exchange: every PUT entry to the owner of its slot range (binned while framing; the bins
+        #      leave DELETE records out: they only matter to the exact path) ----
         if send is None and G > 1:
             send = s.alloc(16)
         M = R[:, 8:8 + G]                                  # M[src][dst]
+        n_mine = int(M[g].sum())
         out_splits = [int(M[r][g]) * 2 for r in range(G)]  # int64 elements (2 per entry)
         n_recv = sum(out_splits) // 2
         if G == 1:  # nothing to exchange: the entries stay where the framing left them
@@ -530,11 +556,11 @@ class ShardedBuilder:
             break
         mark("place")
         res.n_spill, res.n_pairs = int(F[:, 0].sum()), int(F[:, 1].sum())
-        if F[:, 2].any():
-            return self._gathered(res, header, file_len, buf, buf_lo, buf_hi, lay, opts, slot_size, out_len)
-        if F[:, 1].sum() > 0 and self._pairs_share_a_key(int(F[g, 1]), entries, data_end, buf.device):
-            return self._gathered(res, header, file_len, buf, buf_lo, buf_hi, lay, opts, slot_size, out_len)
-        host_header = False
+        # DELETE records, or equal-hash pairs this step cannot prove distinct: the exact path
+        exact = n_deletes > 0 or bool(F[:, 2].any())
+        if not exact and F[:, 1].sum() > 0:
+            exact = self._pairs_share_a_key(int(F[g, 1]), entries, data_end, buf.device)
+        host_header = exact
         if int(F[:, 0].max()) > SPILL_INLINE:  # more spilled slots than the rows carry: exchange them all
             host_header = True
             n_spill = int(F[g, 0])
@@ -545,26 +571,19 @@ class ShardedBuilder:
             pieces = c.allgather_var(spill.view(torch.int64), 4 * n_spill, buf.device)
             allsp = torch.cat([p for p in pieces if p.numel()])
             s.apply_spill(allsp, allsp.numel() // 4)
-            nonempty = int(slot_hi > slot_lo)
-            bslots = s.boundary()
-            mx, col, tot = s.stats(0, 0) if nonempty else (0, 0, 0)
-            bnd = c.allgather_i64([_signed(v) for v in bslots] + [nonempty, mx, col, tot])
+            if not exact:
+                bnd = self._range_stats(slot_lo, slot_hi)
         mark("spill")
+        if exact:  # the ring splits at the slots the PUT placement left empty (now complete on every rank)
+            done = self._exact(res, out, hdr_off, entries, frame_end, opts, h, slot_lo, slot_hi, slot_size, buf.device)
+            if done is not None:
+                mark("exact")
+                return done
+            return self._gathered(res, header, file_len, buf, buf_lo, buf_hi, lay, opts, slot_size, out_len)
 
         # ---- 4 stats: per-range sums (the first slot is not compared with its predecessor) and the
         #      boundary slots of every rank; the cross-range comparisons are added here ----
-        max_disp, collisions, total_disp = int(bnd[:, 5].max()), int(bnd[:, 6].sum()), int(bnd[:, 7].sum())
-        prev = None  # (hash, occupied) of the last slot of the previous non-empty range
-        for r in range(G):
-            if not bnd[r][4]:
-                continue
-            if prev is not None and prev[1] and prev[0] == int(bnd[r][0]) & 0xFFFFFFFFFFFFFFFF:
-                collisions += 1  # calculateMaxDisplacement compares every slot with the one before
-            prev = (int(bnd[r][2]) & 0xFFFFFFFFFFFFFFFF, int(bnd[r][3] != 0))
-        # wrap quirk (IndexHash.java:239-241): slot 0 and slot cap-1 occupied with equal hashes
-        last = max(r for r in range(G) if bnd[r][4])
-        if bnd[0][1] != 0 and bnd[last][3] != 0 and bnd[0][0] == bnd[last][2]:
-            collisions += 1
+        max_disp, collisions, total_disp = _combine_stats(bnd)
         stats = {"num_entries": n_total, "garbage_size": 0, "max_displacement": max_disp,
                  "hash_collisions": collisions, "total_displacement": total_disp, "placement_path": 0}
         if g == 0 and host_header:
@@ -573,6 +592,107 @@ class ShardedBuilder:
         res.out = out
         res.stats = stats
         mark("stats")
+        return res
+
+    def _range_stats(self, slot_lo, slot_hi) -> np.ndarray:
+        """Every rank's {boundary slots, non-empty, max displacement, collisions, total displacement}."""
+        s, c = self.s, self.c
+        nonempty = int(slot_hi > slot_lo)
+        bslots = s.boundary()
+        mx, col, tot = s.stats(0, 0) if nonempty else (0, 0, 0)
+        return c.allgather_i64([_signed(v) for v in bslots] + [nonempty, mx, col, tot])
+
+    # ---- the sharded exact path (DESIGN.md §6.1) ----
+    def _exact(self, res, out, hdr_off, entries, frame_end, opts, h, slot_lo, slot_hi, slot_size, device):
+        """IndexHash.put / delete (IndexHash.java:454-665) replayed on exact ranges: the ring splits at the
+        slots the canonical placement of all PUT records leaves empty (no probe or backward shift crosses
+        one), rank r's range running from the first such slot of its slot range to the next rank's.
+        Returns None when the log needs the gathered path (no empty slot, keys over 4 KiB)."""
+        s, c = self.s, self.c
+        g, G = c.rank, c.world
+        cap = _capacity(h, opts)
+        E = [int(v) for v in c.allgather_i64([s.first_empty()])[:, 0]]
+        have = [r for r in range(G) if E[r] >= 0]
+        rs = s.exact_record_size()
+        if not have or rs <= 0:
+            return None
+        ranges = {}
+        for i, r in enumerate(have):
+            a, b = E[r], E[have[(i + 1) % len(have)]]
+            ranges[r] = (a, b + cap if b <= a else b)
+        # every record (PUT and DELETE) with its header and key to the owner of its wanted slot's range
+        counts = s.exact_frame(entries[g], frame_end(g), E)
+        n_send = sum(counts)
+        send = s.alloc(max(1, n_send) * rs)
+        s.exact_pack(send)
+        M = c.allgather_i64(counts)  # M[src][dst]
+        n_recv = int(sum(M[r][g] for r in range(G)))
+        if G == 1:
+            recv = send
+        else:
+            recv = c.all_to_all(send[: n_send * rs], [x * rs for x in counts], [int(M[r][g]) * rs for r in range(G)],
+                                device)
+        rep = s.exact_build(recv, n_recv)
+        rows = c.allgather_i64([rep["rc"], rep["err_pos"], rep["num_entries"], rep["garbage"]])
+        bad = sorted((int(x[1]), int(x[0])) for x in rows if x[0])
+        if bad:
+            from ._native import raise_for
+            raise_for(bad[0][1], f"{_code_text(bad[0][1])} (log offset {bad[0][0]})")
+        # the replayed slots to the ranks whose slices hold them (mostly a rank's own slice; the run
+        # before the first empty slot of a slice was replayed by the previous range's owner)
+        slices = [s.slot_range(r) for r in range(G)]
+
+        def pieces(r):
+            if r not in ranges:
+                return []
+            a, b = ranges[r]
+            segs = [(a, min(b, cap))] + ([(0, b - cap)] if b > cap else [])
+            got = []
+            for q in range(G):
+                lo, hi = slices[q]
+                for x, y in segs:
+                    u, v = max(x, lo), min(y, hi)
+                    if u < v:
+                        got.append((q, u, v))
+            return got
+
+        mine = pieces(g)
+        for q, u, v in mine:
+            if q == g:
+                s.exact_extract(u, v, out, hdr_off + (u - slot_lo) * slot_size)
+        if G > 1:
+            to = [0] * G
+            for q, u, v in mine:
+                if q != g:
+                    to[q] += (v - u) * slot_size
+            send2 = s.alloc(max(1, sum(to)))
+            at = [sum(to[:q]) for q in range(G)]
+            for q, u, v in mine:
+                if q != g:
+                    s.exact_extract(u, v, send2, at[q])
+                    at[q] += (v - u) * slot_size
+            frm = [sum((v - u) * slot_size for q, u, v in pieces(r) if q == g) if r != g else 0 for r in range(G)]
+            recv2 = c.all_to_all(send2[: sum(to)], to, frm, device)
+            at2 = 0
+            for r in range(G):
+                if r == g:
+                    continue
+                for q, u, v in pieces(r):
+                    if q == g:
+                        nb = (v - u) * slot_size
+                        o = hdr_off + (u - slot_lo) * slot_size
+                        out[o: o + nb].copy_(recv2[at2: at2 + nb])
+                        at2 += nb
+        bnd = self._range_stats(slot_lo, slot_hi)
+        max_disp, collisions, total_disp = _combine_stats(bnd)
+        n_entries, garbage = int(rows[:, 2].sum()), int(rows[:, 3].sum())
+        if g == 0:
+            hdr = s.index_header(opts, n_entries, garbage, max_disp, collisions, total_disp)
+            out[:INDEX_HEADER_SIZE].copy_(s.from_host(hdr))
+        res.out = out
+        res.stats = {"num_entries": n_entries, "garbage_size": garbage, "max_displacement": max_disp,
+                     "hash_collisions": collisions, "total_displacement": total_disp, "placement_path": 2}
+        res.path = "exact"
         return res
 
     # equal-hash pairs: fetch both keys from the ranks that hold the records, compare on device
@@ -632,6 +752,24 @@ class ShardedBuilder:
         res.stats = stats
         res.path = "gathered"
         return res
+
+
+def _combine_stats(bnd):
+    """calculateMaxDisplacement (IndexHash.java:195-245) from every rank's range row: the per-range sums
+    plus the comparisons across range boundaries and the wrap quirk."""
+    max_disp, collisions, total_disp = int(bnd[:, 5].max()), int(bnd[:, 6].sum()), int(bnd[:, 7].sum())
+    prev = None  # (hash, occupied) of the last slot of the previous non-empty range
+    for r in range(bnd.shape[0]):
+        if not bnd[r][4]:
+            continue
+        if prev is not None and prev[1] and prev[0] == int(bnd[r][0]) & 0xFFFFFFFFFFFFFFFF:
+            collisions += 1  # calculateMaxDisplacement compares every slot with the one before
+        prev = (int(bnd[r][2]) & 0xFFFFFFFFFFFFFFFF, int(bnd[r][3] != 0))
+    # wrap quirk (IndexHash.java:239-241): slot 0 and slot cap-1 occupied with equal hashes
+    last = max(r for r in range(bnd.shape[0]) if bnd[r][4])
+    if bnd[0][1] != 0 and bnd[last][3] != 0 and bnd[0][0] == bnd[last][2]:
+        collisions += 1
+    return max_disp, collisions, total_disp
 
 
 _CODE_TEXT = {-1: "File is not a Sparkey log file", -2: "Incompatible version", -3: "Corrupt log file",

@@ -58,6 +58,7 @@ class CpuShardSteps:
         self.seed = opts.hash_seed
         self.slot_lo, self.slot_hi = self.slot_range(rank)
         self.entries = []
+        self._tab = None
 
     # log access by global position
     def byte(self, p):
@@ -153,23 +154,25 @@ class CpuShardSteps:
             self.bin_row(send, 0, [entry, frame_end, entry, 0, 0, 0, 0, 0], row)
             return
         m = self.frame(entry, frame_end)
-        n = m["n"] if not m["rc"] and not m["ndel"] else 0
+        n = m["n"] if not m["rc"] else 0
         self.bin_row(send, n, [entry, frame_end, m["exit"], m["n"], m["ndel"], m["rc"], m["err_pos"], 0], row)
 
     def bin_row(self, send, n, scalars, row):
+        """The bin carries PUT entries only (DELETEs matter to the exact path alone)."""
         world = self.world
         counts = [0] * world
+        puts = [e for e in self.entries if not e[1] & DEL] if n else []
         if send is None:  # one rank: the entries stay here
-            self.kept = np.array(self.entries, dtype=np.uint64).reshape(-1, 2)
-            counts = [n]
-        elif n:
+            self.kept = np.array(puts, dtype=np.uint64).reshape(-1, 2)
+            counts = [len(puts)]
+        elif puts:
             dest = []
             nd = (self.nb + self.bpp - 1) // self.bpp
-            for h, a in self.entries:
+            for h, a in puts:
                 d = self._bucket(h) // self.bpp
                 dest.append(next(r for r in range(world) if nd * r // world <= d < nd * (r + 1) // world))
-            order = sorted(range(len(self.entries)), key=lambda i: dest[i])
-            arr = np.array([self.entries[i] for i in order], dtype=np.uint64).reshape(-1, 2)
+            order = sorted(range(len(puts)), key=lambda i: dest[i])
+            arr = np.array([puts[i] for i in order], dtype=np.uint64).reshape(-1, 2)
             send.view(torch.int64)[: 2 * len(order)] = torch.from_numpy(arr.view(np.int64).reshape(-1).copy())
             counts = [dest.count(r) for r in range(world)]
         row.zero_()  # the per-digit counts stay 0: the simulation's summarize re-sorts what it receives
@@ -315,6 +318,134 @@ class CpuShardSteps:
 
     def index_header(self, opts, num_entries, garbage, max_disp, collisions, total_disp):
         return _native.index_header(self.header, opts, num_entries, garbage, max_disp, collisions, total_disp)
+
+    # ---- exact path (DELETEs, duplicate keys) ----
+    def first_empty(self):
+        for slot in range(self.slot_lo, self.slot_hi):
+            if self._read(slot)[1] == 0:
+                return slot
+        return -1
+
+    def exact_record_size(self):
+        k = self.h["max_key_len"]
+        return 0 if k > 4096 else 16 + ((10 + k + 7) & ~7)
+
+    def _owner(self, w, starts):
+        own, last = -1, -1
+        for r, e in enumerate(starts):
+            if e < 0:
+                continue
+            last = r
+            if e <= w:
+                own = r
+        return own if own >= 0 else last
+
+    def exact_frame(self, entry, frame_end, starts):
+        m = self.frame(entry, frame_end)
+        assert not m["rc"]
+        self._ex = []  # (owner, hash, address, header + key bytes) in log order
+        for h, a in self.entries:
+            p = (a & ~DEL) >> self.ebb
+            klen, vlen, hlen, put = self._hdr(p)
+            self._ex.append((self._owner(h % self.cap, starts), h, a, self._bytes(p, hlen + klen)))
+        return [sum(1 for e in self._ex if e[0] == r) for r in range(self.world)]
+
+    def exact_pack(self, send):
+        rs = self.exact_record_size()
+        recs = sorted(self._ex, key=lambda e: e[0])  # stable: log order within each owner
+        b = bytearray()
+        for _, h, a, body in recs:
+            b += int(h).to_bytes(8, "little") + int(a).to_bytes(8, "little") + body + bytes(rs - 16 - len(body))
+        if b:
+            send[: len(b)] = torch.frombuffer(b, dtype=torch.uint8)
+
+    def exact_build(self, recv, n):
+        """IndexHash.put / delete (IndexHash.java:454-665) over the received records, sequentially."""
+        rs = self.exact_record_size()
+        raw = recv[: n * rs].numpy().tobytes()
+        recs = []
+        for i in range(n):
+            r = raw[i * rs: (i + 1) * rs]
+            h, a = int.from_bytes(r[:8], "little"), int.from_bytes(r[8:16], "little")
+            first, q = _vlq(r, 16, rs)
+            second, q2 = _vlq(r, q, rs)
+            put = first != 0
+            klen, vlen = (first - 1, second) if put else (second, 0)
+            recs.append((h, a & ~DEL, put, klen, vlen, r[q2: q2 + klen]))
+        if self.opts.method == 2:  # SORTING: SortHelper's (wantedSlot, address) order
+            recs.sort(key=lambda t: (t[0] % self.cap, t[1]))
+        info = {t[1]: t for t in recs}
+        cap = self.cap
+        tab = [None] * cap  # (hash, address)
+        st = {"n": 0, "garbage": 0}
+
+        def vsz(v):
+            return next(n for n in range(1, 5) if v < 1 << (7 * n)) if v < 1 << 28 else 5
+
+        def gar(k, v):  # IndexHeader.java:221-228
+            return k + v + vsz(k + 1) + vsz(v)
+
+        for h, a, put, klen, vlen, key in recs:
+            slot, disp = h % cap, 0
+            if put:
+                hh, aa, might = h, a, True
+                for _ in range(cap):
+                    cur = tab[slot]
+                    if cur is None:
+                        tab[slot] = (hh, aa)
+                        st["n"] += 1
+                        break
+                    if might and cur[0] == hh:
+                        o = info[cur[1]]
+                        if not o[2]:
+                            return {"rc": -5, "err_pos": a >> self.ebb, "num_entries": 0, "garbage": 0}
+                        if o[3] == klen and o[5] == key:
+                            tab[slot] = (hh, aa)
+                            st["garbage"] += gar(o[3], o[4])
+                            break
+                    d2 = (slot - cur[0] % cap) % cap
+                    if disp > d2 or (disp == d2 and aa < cur[1]):
+                        tab[slot] = (hh, aa)
+                        hh, aa = cur
+                        disp = d2
+                        might = False
+                    disp += 1
+                    slot = (slot + 1) % cap
+            else:
+                for _ in range(cap + 1):
+                    cur = tab[slot]
+                    if cur is None:
+                        break
+                    if cur[0] == h:
+                        o = info[cur[1]]
+                        if not o[2]:
+                            return {"rc": -5, "err_pos": a >> self.ebb, "num_entries": 0, "garbage": 0}
+                        if o[3] == klen and o[5] == key:
+                            for _ in range(cap):
+                                nx = (slot + 1) % cap
+                                c = tab[nx]
+                                if c is None or c[0] % cap == nx:
+                                    break
+                                tab[slot] = c
+                                slot = nx
+                            tab[slot] = None
+                            st["garbage"] += gar(o[3], o[4])
+                            st["n"] -= 1
+                            break
+                    if disp > (slot - cur[0] % cap) % cap:
+                        break
+                    disp += 1
+                    slot = (slot + 1) % cap
+        self._tab = tab
+        return {"rc": 0, "err_pos": 0, "num_entries": st["n"], "garbage": st["garbage"]}
+
+    def exact_extract(self, a, b, dst=None, dst_off=0):
+        for slot in range(a, b):
+            cur = self._tab[slot] if self._tab is not None else None
+            h, ad = cur if cur is not None else (0, 0)
+            bts = (h & ((1 << (8 * self.hs)) - 1)).to_bytes(self.hs, "little") + ad.to_bytes(self.asz, "little")
+            o = dst_off + (slot - a) * self.S
+            dst[o: o + self.S] = torch.frombuffer(bytearray(bts), dtype=torch.uint8)
 
     def full_build(self, log, file_len, out, opts):
         b = log[:file_len].numpy().tobytes()

@@ -60,17 +60,45 @@ def test_sharded_hash_collision_pairs(tmp_path):
     assert metas[0]["n_pairs"] > 0 and metas[0]["path"] == "sharded"
 
 
-def test_sharded_duplicates_gather(tmp_path):
+@pytest.mark.parametrize("world", [1, 2, 3])
+def test_sharded_duplicates_exact(tmp_path, world):
+    """Overwritten keys: the sharded exact path (no gathering), equal to the oracle."""
     puts = key_value_puts(2000) + [(b"Key%d" % i, b"again") for i in range(0, 2000, 17)]
-    metas = check(make_log(puts), 2, tmp_path, seed=5)
-    assert metas[0]["path"] == "gathered"
+    metas = check(make_log(puts), world, tmp_path, seed=5)
+    assert all(m["path"] == "exact" for m in metas)
 
 
 @pytest.mark.parametrize("method", [IN_MEMORY, SORTING])
-def test_sharded_deletes_gather(tmp_path, method):
+@pytest.mark.parametrize("world", [2, 4])
+def test_sharded_deletes_exact(tmp_path, method, world):
     log = make_log(key_value_puts(2000), deletes=[b"Key%d" % i for i in range(0, 2000, 7)])
-    metas = check(log, 2, tmp_path, seed=-5, method=method)
-    assert metas[0]["path"] == "gathered"
+    metas = check(log, world, tmp_path, seed=-5, method=method)
+    assert all(m["path"] == "exact" for m in metas)
+    assert metas[0]["stats"]["garbage_size"] > 0
+
+
+def test_sharded_churn_exact(tmp_path):
+    """Interleaved puts, overwrites and deletes of a small key space (long segments that cross the
+    slot-range boundaries), 3 ranks, dense table."""
+    import random
+    rnd = random.Random(3)
+    lb = oracle.LogBuilder(7, 0)
+    for i in range(5000):
+        k = b"k%d" % rnd.randrange(1500)
+        if rnd.random() < 0.2:
+            lb.delete(k)
+        else:
+            lb.put(k, b"v" * rnd.randrange(0, 40))
+    metas = check(lb.finish(), 3, tmp_path, seed=77, sparsity=1.3)
+    assert all(m["path"] == "exact" for m in metas)
+
+
+def test_sharded_delete_of_absent_keys(tmp_path):
+    """DELETE records of keys never put (no-ops in every state) and deletes before the puts."""
+    puts = key_value_puts(1500)
+    log = make_log(puts, deletes=[b"Nope%d" % i for i in range(300)] + [b"Key%d" % i for i in range(0, 1500, 5)])
+    metas = check(log, 2, tmp_path, seed=12)
+    assert all(m["path"] == "exact" for m in metas)
 
 
 def test_sharded_understated_header(tmp_path):

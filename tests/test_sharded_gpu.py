@@ -62,16 +62,61 @@ def test_sharded_gpu_small_log(native):
 
 
 @pytest.mark.parametrize("method", [IN_MEMORY, SORTING])
-def test_sharded_gpu_deletes_gather(native, method):
+@pytest.mark.parametrize("world", [1, 2, 4])
+def test_sharded_gpu_deletes_exact(native, method, world):
+    """DELETE records: the sharded exact path (exact ranges replayed by their owners), no gathering."""
     log = make_log(key_value_puts(5000), deletes=[b"Key%d" % i for i in range(0, 5000, 7)])
-    metas = check(native, log, 2, seed=-5, method=method)
-    assert metas[0]["path"] == "gathered"
+    metas = check(native, log, world, seed=-5, method=method)
+    assert all(m["path"] == "exact" for m in metas)
 
 
-def test_sharded_gpu_duplicates_gather(native):
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_gpu_duplicates_exact(native, world):
     puts = key_value_puts(5000) + [(b"Key%d" % i, b"again") for i in range(0, 5000, 13)]
-    metas = check(native, make_log(puts), 2, seed=5)
-    assert metas[0]["path"] == "gathered"
+    metas = check(native, make_log(puts), world, seed=5)
+    assert all(m["path"] == "exact" for m in metas)
+
+
+def _churn_log(n, keys, seed, del_frac=0.2, vmax=40):
+    import random
+    rnd = random.Random(seed)
+    lb = oracle.LogBuilder(7, 0)
+    for _ in range(n):
+        k = b"k%d" % rnd.randrange(keys)
+        if rnd.random() < del_frac:
+            lb.delete(k)
+        else:
+            lb.put(k, b"v" * rnd.randrange(0, vmax))
+    return lb.finish()
+
+
+@pytest.mark.parametrize("method", [IN_MEMORY, SORTING])
+@pytest.mark.parametrize("world", [2, 4])
+def test_sharded_gpu_churn_exact(native, method, world):
+    """Puts, overwrites and deletes over a small key space at sparsity 1.3: long segments crossing the
+    slot-range boundaries (and the ring's wrap), equal to the oracle and to the single-GPU build."""
+    log = _churn_log(60000, 20000, seed=world, del_frac=0.25)
+    metas = check(native, log, world, seed=31, method=method, sparsity=1.3)
+    assert all(m["path"] == "exact" for m in metas)
+    single, st = native.build_index_mem(log, native.make_opts(hash_seed=31, method=method, sparsity=1.3))
+    got, _ = run_threads(log, world, dict(hash_seed=31, method=method, sparsity=1.3))
+    assert got == single and st.placement_path == 2
+
+
+def test_sharded_gpu_c2_shape_overwrites(native):
+    """C2's record shape (uniform framing) with every 10th key written twice: the uniform log's exact
+    path, 4 ranks."""
+    from sparkey import synth
+    base = synth.fixed_log(200000, 16, 100, seed=8).tobytes()
+    recs = [base[84 + 118 * i: 84 + 118 * (i + 1)] for i in range(0, 200000, 10)]
+    lb = oracle.LogBuilder(0x2545F491, 0)
+    for i in range(200000):
+        r = base[84 + 118 * i: 84 + 118 * (i + 1)]
+        lb.put(r[2:18], r[18:])
+    for r in recs:
+        lb.put(r[2:18], r[18:][::-1])
+    metas = check(native, lb.finish(), 4, seed=0x2545F491)
+    assert all(m["path"] == "exact" for m in metas)
 
 
 def test_sharded_gpu_understated_header(native):
