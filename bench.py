@@ -393,12 +393,22 @@ def sharded(args, dev, world, rank):
     from sparkey.sharded import Comm, GpuShardSteps, ShardedBuilder, shard_layout
 
     n_total = args.entries * world
-    file_len = 84 + n_total * 118
-    header, _ = synth.fixed_log_range(n_total, 0, 84, 16, 100, seed=args.seed, file_id=0x5EED0000)
+    churn = args.workload == "churn"  # overwrites + DELETEs: the sharded exact path
+    full_log = None
+    t0 = time.time()
+    if churn:  # (every rank makes the whole log, then keeps its byte range)
+        full_log = synth.churn_log(n_total, int(n_total * 0.8), 0.1, seed=args.seed + 4)
+        file_len = int(full_log.size)
+        header = full_log[:84].tobytes()
+    else:
+        file_len = 84 + n_total * 118
+        header, _ = synth.fixed_log_range(n_total, 0, 84, 16, 100, seed=args.seed, file_id=0x5EED0000)
     lay = shard_layout(header, file_len, world)
     lo, hi = lay.buffer_range(rank)
-    t0 = time.time()
-    _, part = synth.fixed_log_range(n_total, lo, hi, 16, 100, seed=args.seed, file_id=0x5EED0000)
+    if churn:
+        part = full_log[lo:hi]
+    else:
+        _, part = synth.fixed_log_range(n_total, lo, hi, 16, 100, seed=args.seed, file_id=0x5EED0000)
     gen_s = time.time() - t0
     buf = torch.from_numpy(part).to(dev)
     del part
@@ -425,13 +435,17 @@ def sharded(args, dev, world, rank):
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.backend == "nccl" else "cpu")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
-    assert res.path == "sharded" and res.stats["num_entries"] == n_total, (res.path, res.stats)
+    if churn:
+        assert res.path == "exact", (res.path, res.stats)
+    else:
+        assert res.path == "sharded" and res.stats["num_entries"] == n_total, (res.path, res.stats)
     identical = None
     if args.check:  # the sharded .spi against one single-GPU build of the whole log (rank 0)
         pieces = [None] * world
         dist.all_gather_object(pieces, (res.out_offset, res.out.cpu().numpy().tobytes()))
         if rank == 0:
-            full_log = synth.fixed_log(n_total, 16, 100, seed=args.seed, file_id=0x5EED0000)
+            if full_log is None:
+                full_log = synth.fixed_log(n_total, 16, 100, seed=args.seed, file_id=0x5EED0000)
             d_full = torch.from_numpy(full_log).to(dev)
             size = _native.index_size(full_log[:84].tobytes(), opts)
             d_spi = torch.empty(size, dtype=torch.uint8, device=dev)
@@ -445,14 +459,17 @@ def sharded(args, dev, world, rank):
                 got[off:off + len(b)] = b
             identical = bytes(got) == single
     slot = 16
-    cap = 1 | int(n_total * 1.3)
+    from sparkey.sharded import parse_log_header
+    cap = 1 | int(parse_log_header(header)["num_puts"] * 1.3)
     ms_per_step = elapsed * 1000.0 / args.steps
     b_alg_per_gpu = ((file_len - 84) + 112 + slot * cap) / world
     achieved = b_alg_per_gpu / (ms_per_step * 1e-3) / 1e9
     return {
         "value": n_total * args.steps / elapsed, "ms_per_step": ms_per_step,
-        "config": {"workload": f"C2 shape, {args.entries} PUTs per GPU x {world} GPUs = {n_total} in ONE index "
-                               "(16 B key, 100 B value, NONE, IN_MEMORY)",
+        "config": {"workload": (f"churn: {args.entries} records per GPU x {world} GPUs = {n_total} (keys from a pool "
+                                f"of 0.8 n, 10% DELETEs) in ONE index, sharded exact path" if churn else
+                                f"C2 shape, {args.entries} PUTs per GPU x {world} GPUs = {n_total} in ONE index "
+                                "(16 B key, 100 B value, NONE, IN_MEMORY)"),
                    "entries": n_total, "entries_per_gpu": args.entries, "log_bytes": file_len, "capacity": cap,
                    "spi_bytes": 112 + slot * cap,
                    "parallelism": f"log byte-range sharded x{world}, RCCL all_to_all of (hash, address) entries"},

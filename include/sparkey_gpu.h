@@ -250,10 +250,12 @@ int sparkey_shard_first_empty(sparkey_plan* plan, void* stream, int64_t* slot_ou
 /* Bytes per exchange record: {hash, address, the record's header VLQs and key, zero padded}; 0 when
  * the header's maxKeyLen is above 4096 (such logs take the gathered path). */
 int32_t sparkey_shard_exact_record_size(const sparkey_plan* plan);
-/* Frames [entry, frame_end) again (PUT and DELETE records) and counts the records per exact owner:
- * starts[world] = each rank's exact range start (-1: none; increasing otherwise), counts_out[world]. */
-int sparkey_shard_exact_frame(sparkey_plan* plan, int64_t entry, int64_t frame_end, const int64_t* starts,
-                              void* stream, uint64_t* counts_out, char* err, size_t err_len);
+/* The records of [entry, frame_end) (PUT and DELETE; n_records of them per the verification row, -1:
+ * unknown) counted per exact owner: starts[world] = each rank's exact range start (-1: none;
+ * increasing otherwise), counts_out[world].  Reuses the slabs the canonical step's framing left when
+ * they still hold those records, else frames the range again. */
+int sparkey_shard_exact_frame(sparkey_plan* plan, int64_t entry, int64_t frame_end, int64_t n_records,
+                              const int64_t* starts, void* stream, uint64_t* counts_out, char* err, size_t err_len);
 /* The framed records as exchange records into d_send (sum(counts) x record size bytes), grouped by
  * owner in rank order, log order within each owner. */
 int sparkey_shard_exact_pack(sparkey_plan* plan, uint8_t* d_send, uint64_t send_bytes, void* stream, char* err,

@@ -348,8 +348,7 @@ void launch_shard_header(hipStream_t s, const int64_t* fin, int stride, int worl
 // sharded exact path (shard_exact_kernels.hip)
 void launch_first_empty(const BuildParams& P, hipStream_t s, unsigned long long* out);
 void launch_ex_count(const BuildParams& P, hipStream_t s, const int64_t* starts, int world, uint32_t* cnt,
-                     unsigned long long* totals);
-void launch_ex_offsets(hipStream_t s, const uint32_t* cnt, uint64_t* off, uint64_t n, uint64_t* scratch);
+                     uint64_t* off, uint64_t* scratch, unsigned long long* totals);
 void launch_ex_scatter(const BuildParams& P, hipStream_t s, const int64_t* starts, int world, const uint64_t* off,
                        uint8_t* send, uint32_t rs);
 void launch_ex_ent(hipStream_t s, const uint8_t* recv, uint64_t n, uint32_t rs, Entry* ent);

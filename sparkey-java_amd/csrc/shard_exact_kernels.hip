@@ -26,10 +26,12 @@ constexpr int kExMaxWorld = 256;
 
 __global__ __launch_bounds__(256) void k_first_empty(BuildParams P, unsigned long long* out) {
   const uint64_t slot = P.slot_lo + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (slot >= P.slot_hi) return;
-  uint64_t h, a;
-  read_slot(P, slot, h, a);
-  if (a == 0) atomicMin(out, (unsigned long long)slot);
+  uint64_t h, a = 1;
+  if (slot < P.slot_hi) read_slot(P, slot, h, a);
+  const uint64_t empty = __ballot(a == 0);  // one atomic per wave (slots rise with the lane) ...
+  if (empty && (threadIdx.x & 63) == (unsigned)(__ffsll((unsigned long long)empty) - 1) &&
+      slot < __hip_atomic_load(out, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))  // ... and none behind a found one
+    atomicMin(out, (unsigned long long)slot);
 }
 
 // the rank owning wanted slot w: the last rank whose exact range starts at or before w, else (w before
@@ -45,44 +47,63 @@ __device__ __forceinline__ int exact_owner(const int64_t* starts, int world, uin
   return own >= 0 ? own : last;
 }
 
-// one workgroup per slab: cnt[owner * nslabs + slab], and the totals per owner
-__global__ __launch_bounds__(256) void k_ex_count(BuildParams P, const int64_t* starts, int world, uint32_t* cnt,
-                                                  unsigned long long* totals) {
+constexpr int kExWaves = 4;  // k_ex_count / k_ex_scatter: one wave per slab, four slabs per workgroup
+
+// one wave per slab: cnt[owner * nslabs + slab]
+__global__ __launch_bounds__(64 * kExWaves) void k_ex_count(BuildParams P, const int64_t* starts, int world,
+                                                            uint32_t* cnt) {
   __shared__ int64_t sE[kExMaxWorld];
-  __shared__ uint32_t c[kExMaxWorld];
-  const uint64_t w = blockIdx.x;
-  for (int r = threadIdx.x; r < world; r += blockDim.x) {
-    sE[r] = starts[r];
-    c[r] = 0;
+  __shared__ uint32_t c[kExWaves][kExMaxWorld];
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint64_t w = (uint64_t)blockIdx.x * kExWaves + wv;
+  for (int r = threadIdx.x; r < world; r += blockDim.x) sE[r] = starts[r];
+  for (int r = lane; r < world; r += 64) c[wv][r] = 0;
+  __syncthreads();
+  if (w < P.nslabs) {
+    const uint32_t n = P.wcount[w];
+    for (uint32_t j = lane; j < n; j += 64) {
+      const Entry en = P.ent[w * P.slab_cap + j];
+      atomicAdd(&c[wv][exact_owner(sE, world, fast_mod(en.hash, P.mod))], 1u);
+    }
   }
   __syncthreads();
-  const uint32_t n = P.wcount[w];
-  for (uint32_t j = threadIdx.x; j < n; j += blockDim.x) {
-    const Entry en = P.ent[w * P.slab_cap + j];
-    atomicAdd(&c[exact_owner(sE, world, fast_mod(en.hash, P.mod))], 1u);
-  }
-  __syncthreads();
-  for (int r = threadIdx.x; r < world; r += blockDim.x) {
-    cnt[(uint64_t)r * P.nslabs + w] = c[r];
-    if (c[r]) atomicAdd(&totals[r], (unsigned long long)c[r]);
-  }
+  if (w < P.nslabs)
+    for (int r = lane; r < world; r += 64) cnt[(uint64_t)r * P.nslabs + w] = c[wv][r];
+}
+
+// records per owner from the scanned counts (off: world * nslabs + 1, owner-major)
+__global__ void k_ex_totals(const uint64_t* off, uint64_t nslabs, int world, unsigned long long* totals) {
+  for (int r = threadIdx.x; r < world; r += blockDim.x)
+    totals[r] = off[(uint64_t)(r + 1) * nslabs] - off[(uint64_t)r * nslabs];
+}
+
+// little-endian word of the 8 log bytes from p (p + 8 <= the buffer's end + 16), from aligned dwords
+__device__ __forceinline__ uint64_t log_word(const uint8_t* log, int64_t p) {
+  const int64_t a = p & ~3ll;
+  const uint32_t* q = reinterpret_cast<const uint32_t*>(log + a);
+  const uint32_t sh = (uint32_t)(p - a) * 8u;
+  const uint64_t lo = (uint64_t)q[0] | ((uint64_t)q[1] << 32);
+  const uint64_t hi = q[2];
+  return sh ? (lo >> sh) | (hi << (64 - sh)) : lo;
 }
 
 // one wave per slab: each 64-record step ranks its records per owner with ballots (log order kept),
 // then every lane writes its exchange record: {hash, address, the record's header VLQs and key}
-__global__ __launch_bounds__(64) void k_ex_scatter(BuildParams P, const int64_t* starts, int world, const uint64_t* off,
-                                                   uint8_t* send, uint32_t rs) {
+__global__ __launch_bounds__(64 * kExWaves) void k_ex_scatter(BuildParams P, const int64_t* starts, int world,
+                                                              const uint64_t* off, uint8_t* send, uint32_t rs) {
   __shared__ int64_t sE[kExMaxWorld];
-  __shared__ uint64_t base[kExMaxWorld];
-  const uint64_t w = blockIdx.x;
-  const int lane = threadIdx.x;
-  for (int r = lane; r < world; r += 64) {
-    sE[r] = starts[r];
-    base[r] = off[(uint64_t)r * P.nslabs + w];
-  }
+  __shared__ uint64_t base_all[kExWaves][kExMaxWorld];
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint64_t w = (uint64_t)blockIdx.x * kExWaves + wv;
+  uint64_t* base = base_all[wv];
+  for (int r = threadIdx.x; r < world; r += blockDim.x) sE[r] = starts[r];
+  if (w < P.nslabs)
+    for (int r = lane; r < world; r += 64) base[r] = off[(uint64_t)r * P.nslabs + w];
   __syncthreads();
+  if (w >= P.nslabs) return;
   const uint32_t n = P.wcount[w];
   const uint64_t lt = (1ull << lane) - 1;
+  const uint32_t body = rs - 16;  // multiple of 8
   for (uint32_t j0 = 0; j0 < n; j0 += 64) {
     const uint32_t j = j0 + lane;
     const bool active = j < n;
@@ -106,14 +127,23 @@ __global__ __launch_bounds__(64) void k_ex_scatter(BuildParams P, const int64_t*
       todo &= ~m;
     }
     if (!active) continue;
-    uint8_t* r = send + pos * rs;
-    reinterpret_cast<uint64_t*>(r)[0] = en.hash;
-    reinterpret_cast<uint64_t*>(r)[1] = en.addr;
+    uint64_t* r = reinterpret_cast<uint64_t*>(send + pos * rs);
+    r[0] = en.hash;
+    r[1] = en.addr;
     const int64_t p = (int64_t)((en.addr & ~kDelBit) >> P.ebb);
     auto at = [&](int64_t a) -> uint32_t { return P.log[a]; };
     const RecHdr h = decode_header(at, p, (int64_t)P.log_len);
-    const uint32_t len = h.rc ? 0u : (uint32_t)min<int64_t>((int64_t)(h.hlen + h.klen), (int64_t)rs - 16);
-    for (uint32_t q = 0; q < rs - 16; q++) r[16 + q] = q < len ? P.log[p + q] : 0;
+    const uint32_t len = h.rc ? 0u : (uint32_t)min<int64_t>((int64_t)(h.hlen + h.klen), (int64_t)body);
+    for (uint32_t q = 0; q < body; q += 8) {
+      uint64_t v = 0;
+      if (q < len) {
+        v = p + q + 12 <= (int64_t)P.log_len ? log_word(P.log, p + q) : 0;
+        if (p + q + 12 > (int64_t)P.log_len)  // (the buffer's last bytes: one at a time)
+          for (uint32_t k = 0; k < 8 && q + k < len; k++) v |= (uint64_t)P.log[p + q + k] << (8 * k);
+        if (len - q < 8) v &= (1ull << (8 * (len - q))) - 1;
+      }
+      r[2 + q / 8] = v;
+    }
   }
 }
 
@@ -156,17 +186,20 @@ void launch_first_empty(const BuildParams& P, hipStream_t s, unsigned long long*
 }
 
 void launch_ex_count(const BuildParams& P, hipStream_t s, const int64_t* starts, int world, uint32_t* cnt,
-                     unsigned long long* totals) {
-  if (P.nslabs) hipLaunchKernelGGL(k_ex_count, dim3((unsigned)P.nslabs), dim3(256), 0, s, P, starts, world, cnt, totals);
-}
-
-void launch_ex_offsets(hipStream_t s, const uint32_t* cnt, uint64_t* off, uint64_t n, uint64_t* scratch) {
+                     uint64_t* off, uint64_t* scratch, unsigned long long* totals) {
+  if (!P.nslabs) return;
+  hipLaunchKernelGGL(k_ex_count, dim3((unsigned)((P.nslabs + kExWaves - 1) / kExWaves)), dim3(64 * kExWaves), 0, s, P,
+                     starts, world, cnt);
+  const uint64_t n = (uint64_t)world * P.nslabs;
   scan_exclusive<uint32_t, uint64_t, OpAdd>(cnt, off, n, off + n, OpAdd(), scratch, s);
+  hipLaunchKernelGGL(k_ex_totals, dim3(1), dim3(256), 0, s, off, P.nslabs, world, totals);
 }
 
 void launch_ex_scatter(const BuildParams& P, hipStream_t s, const int64_t* starts, int world, const uint64_t* off,
                        uint8_t* send, uint32_t rs) {
-  if (P.nslabs) hipLaunchKernelGGL(k_ex_scatter, dim3((unsigned)P.nslabs), dim3(64), 0, s, P, starts, world, off, send, rs);
+  if (P.nslabs)
+    hipLaunchKernelGGL(k_ex_scatter, dim3((unsigned)((P.nslabs + kExWaves - 1) / kExWaves)), dim3(64 * kExWaves), 0, s,
+                       P, starts, world, off, send, rs);
 }
 
 void launch_ex_ent(hipStream_t s, const uint8_t* recv, uint64_t n, uint32_t rs, Entry* ent) {

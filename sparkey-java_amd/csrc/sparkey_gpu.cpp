@@ -265,6 +265,10 @@ struct ShardState {
   // exact path (sparkey_shard_exact_*): the exact ranges' starts, the exchange record size, the
   // records packed, and the replay over the received records (its local table and receive buffer)
   std::vector<int64_t> ex_starts;
+  // the framing's log-order slabs (P_frame) still hold [slabs_entry, slabs_end): the exact path packs
+  // them without framing again (cleared by the steps that reuse the slab counts)
+  bool slabs_ok = false;
+  int64_t slabs_entry = 0, slabs_end = 0;
   uint32_t ex_rs = 0;
   uint64_t ex_total = 0;
   bool ex_framed = false, ex_built = false;
@@ -1693,6 +1697,7 @@ int sparkey_shard_begin(sparkey_plan* pl, const uint8_t* log_header, uint64_t fi
   index_header_template(sh.lh, sh.ip, opts->hash_seed, sh.tmpl.b);
   sh.local = 0;
   sh.ex_framed = sh.ex_built = false;
+  sh.slabs_ok = false;
   sh.ex_recv = nullptr;
   sh.ex_n = 0;
   HIP_TRY(grow(&pl->small, pl->c_small, 512));
@@ -1850,6 +1855,7 @@ static int shard_frame_sync(sparkey_plan* pl, int64_t entry, int64_t frame_end, 
   memset(res, 0, sizeof(*res));
   res->exit = entry;
   sh.n_local = 0;
+  sh.slabs_ok = false;
   rc = shard_frame_args(pl, entry, &frame_end, err, err_len);
   if (rc) return rc;
   if (entry >= frame_end) return SPARKEY_OK;  // owns no record
@@ -1910,6 +1916,9 @@ static int shard_frame_sync(sparkey_plan* pl, int64_t entry, int64_t frame_end, 
   res->num_deletes = (int64_t)st.n_deletes;
   sh.P_frame = P;
   sh.n_local = st.n_records;
+  sh.slabs_ok = P.p1_region == 0;
+  sh.slabs_entry = entry;
+  sh.slabs_end = frame_end;
   return SPARKEY_OK;
 }
 
@@ -1946,6 +1955,7 @@ int sparkey_shard_frame_bin_async(sparkey_plan* pl, int64_t entry, int64_t frame
   const int64_t fe_in = frame_end;
   sh.n_local = 0;
   sh.local = 0;
+  sh.slabs_ok = false;
   if (!d_row || ((uintptr_t)d_row & 7) || ((uintptr_t)d_send & 15) || (!d_send && sh.world != 1)) {
     set_err(err, err_len, "bad row or send buffer");
     return SPARKEY_E_ARG;
@@ -1969,6 +1979,9 @@ int sparkey_shard_frame_bin_async(sparkey_plan* pl, int64_t entry, int64_t frame
   if (rc) return rc;
   BuildParams P = F.P;
   sh.P_frame = P;
+  sh.slabs_ok = P.p1_region == 0;  // (a failed attempt is redone by sparkey_shard_frame)
+  sh.slabs_entry = entry;
+  sh.slabs_end = frame_end;
   P.abort_on_fail = 1;  // the bin skips an attempt that failed (its counts are not used)
   if (P.p1_region) {
     launch_region_send(P, s, sh.world, (uint32_t)used_digits(P), reinterpret_cast<Entry*>(d_send),
@@ -2124,6 +2137,7 @@ int sparkey_shard_summarize_dev(sparkey_plan* pl, const uint8_t* d_recv, uint64_
   } else {
     P.p2_sorted = 0;
     P.p2_fixed = 0;
+    sh.slabs_ok = false;  // (the slab counts are rewritten below)
     launch_status_reset(s, pl->d_status, n_recv);
     launch_dense_slabs(P, s);
     launch_partition(P, s, &pl->timer);
@@ -2336,8 +2350,10 @@ int32_t sparkey_shard_exact_record_size(const sparkey_plan* pl) {
   return (int32_t)(16 + ((10 + k + 7) & ~7LL));  // {hash, address} + two VLQs (<= 5 bytes each) + key
 }
 
-int sparkey_shard_exact_frame(sparkey_plan* pl, int64_t entry, int64_t frame_end, const int64_t* starts, void* stream,
-                              uint64_t* counts_out, char* err, size_t err_len) {
+static int exact_count(sparkey_plan* pl, hipStream_t s, uint64_t* counts_out, char* err, size_t err_len);
+
+int sparkey_shard_exact_frame(sparkey_plan* pl, int64_t entry, int64_t frame_end, int64_t n_records,
+                              const int64_t* starts, void* stream, uint64_t* counts_out, char* err, size_t err_len) {
   int rc = shard_check(pl, err, err_len);
   if (rc) return rc;
   ShardState& sh = pl->shard;
@@ -2372,15 +2388,46 @@ int sparkey_shard_exact_frame(sparkey_plan* pl, int64_t entry, int64_t frame_end
     return SPARKEY_E_ARG;
   }
   for (int r = 0; r < W; r++) counts_out[r] = 0;
-  sparkey_shard_frame_result fr;
-  rc = shard_frame_sync(pl, entry, frame_end, s, &fr, false, err, err_len);
-  if (rc) return rc;
-  if (fr.rc) {
-    set_err(err, err_len, std::string(code_message(fr.rc)) + " (log offset " + std::to_string(fr.err_pos) + ")");
-    return fr.rc;
+  {
+    int64_t fe = frame_end;
+    rc = shard_frame_args(pl, entry, &fe, err, err_len);
+    if (rc) return rc;
+    frame_end = fe;
   }
-  sh.ex_total = 0;
+  // the canonical step's framing left its slabs in place: no second framing (the counts below check it)
+  bool reuse = sh.slabs_ok && n_records >= 0 && entry == sh.slabs_entry && frame_end == sh.slabs_end &&
+               sh.P_frame.ent == pl->ent && sh.P_frame.wcount == pl->wcount && !getenv("SPARKEY_EXACT_REFRAME");
+  for (int pass = 0; pass < 2; pass++) {
+    if (reuse) {
+      sh.n_local = entry < frame_end ? (uint64_t)n_records : 0;
+    } else {
+      sparkey_shard_frame_result fr;
+      rc = shard_frame_sync(pl, entry, frame_end, s, &fr, false, err, err_len);
+      if (rc) return rc;
+      if (fr.rc) {
+        set_err(err, err_len, std::string(code_message(fr.rc)) + " (log offset " + std::to_string(fr.err_pos) + ")");
+        return fr.rc;
+      }
+    }
+    rc = exact_count(pl, s, counts_out, err, err_len);
+    if (rc) return rc;
+    if (sh.ex_total == sh.n_local) break;
+    if (!reuse) {
+      set_err(err, err_len, "internal: exact counts do not cover the framed records");
+      return SPARKEY_E_GPU;
+    }
+    reuse = false;  // the slabs did not hold the records: frame again
+  }
   sh.ex_framed = true;
+  return SPARKEY_OK;
+}
+
+// records per exact owner of the framed slabs (sh.P_frame), and the scanned (owner, slab) offsets
+static int exact_count(sparkey_plan* pl, hipStream_t s, uint64_t* counts_out, char* err, size_t err_len) {
+  ShardState& sh = pl->shard;
+  const int W = sh.world;
+  sh.ex_total = 0;
+  for (int r = 0; r < W; r++) counts_out[r] = 0;
   if (!sh.n_local) return SPARKEY_OK;
   BuildParams& P = sh.P_frame;
   HIP_TRY(grow(&pl->ex_starts, pl->c_ex_starts, (uint64_t)W + 1));
@@ -2388,11 +2435,9 @@ int sparkey_shard_exact_frame(sparkey_plan* pl, int64_t entry, int64_t frame_end
   HIP_TRY(grow(&pl->ex_off, pl->c_ex_off, (uint64_t)W * P.nslabs + 1));
   const uint64_t scratch = ((uint64_t)W * P.nslabs) / kScanTile + 80;
   HIP_TRY(grow(&pl->scan_u64, pl->c_su, std::max<uint64_t>(pl->c_su, scratch)));
-  HIP_TRY(hipMemcpyAsync(pl->ex_starts, starts, W * sizeof(int64_t), hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(pl->ex_starts, sh.ex_starts.data(), W * sizeof(int64_t), hipMemcpyHostToDevice, s));
   unsigned long long* tot = reinterpret_cast<unsigned long long*>(pl->small);
-  HIP_TRY(hipMemsetAsync(tot, 0, W * sizeof(unsigned long long), s));
-  launch_ex_count(P, s, pl->ex_starts, W, pl->ex_cnt, tot);
-  launch_ex_offsets(s, pl->ex_cnt, pl->ex_off, (uint64_t)W * P.nslabs, pl->scan_u64);
+  launch_ex_count(P, s, pl->ex_starts, W, pl->ex_cnt, pl->ex_off, pl->scan_u64, tot);
   HIP_TRY(hipGetLastError());
   std::vector<unsigned long long> h(W);
   HIP_TRY(hipMemcpyAsync(h.data(), tot, W * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
@@ -2400,10 +2445,6 @@ int sparkey_shard_exact_frame(sparkey_plan* pl, int64_t entry, int64_t frame_end
   for (int r = 0; r < W; r++) {
     counts_out[r] = h[r];
     sh.ex_total += h[r];
-  }
-  if (sh.ex_total != sh.n_local) {
-    set_err(err, err_len, "internal: exact counts do not cover the framed records");
-    return SPARKEY_E_GPU;
   }
   return SPARKEY_OK;
 }
@@ -2473,7 +2514,8 @@ int sparkey_shard_exact_build(sparkey_plan* pl, const uint8_t* d_recv, uint64_t 
     L.fold_stats = 0;
     L.fused_carry = 0;
     launch_partition(L, s, &pl->timer);
-    launch_place_fast(L, s, &pl->timer);
+    launch_summary_carry(L, s, &pl->timer);
+    launch_place_buckets(L, s);  // (no pair verification: the replay compares the keys itself)
     rc = run_exact_segments(pl, L, ipl.in_memory, s, err, err_len);
     if (rc) return rc;
     HIP_TRY(hipGetLastError());

@@ -146,7 +146,8 @@ _SIGS = {
     "sparkey_shard_stats": ([_vp, ctypes.c_uint64, ctypes.c_int32, _vp, _i64p] + _E, ctypes.c_int),
     "sparkey_shard_first_empty": ([_vp, _vp, _i64p] + _E, ctypes.c_int),
     "sparkey_shard_exact_record_size": ([_vp], ctypes.c_int32),
-    "sparkey_shard_exact_frame": ([_vp, ctypes.c_int64, ctypes.c_int64, _i64p, _vp, _u64p] + _E, ctypes.c_int),
+    "sparkey_shard_exact_frame": ([_vp, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, _i64p, _vp, _u64p] + _E,
+                                  ctypes.c_int),
     "sparkey_shard_exact_pack": ([_vp, _vp, ctypes.c_uint64, _vp] + _E, ctypes.c_int),
     "sparkey_shard_exact_build": ([_vp, _vp, ctypes.c_uint64, _vp, ctypes.POINTER(ShardExactResult)] + _E, ctypes.c_int),
     "sparkey_shard_exact_extract": ([_vp, ctypes.c_uint64, ctypes.c_uint64, _vp, _vp] + _E, ctypes.c_int),
@@ -412,11 +413,11 @@ class Plan:
     def shard_exact_record_size(self) -> int:
         return int(_lib.sparkey_shard_exact_record_size(self._h))
 
-    def shard_exact_frame(self, entry: int, frame_end: int, starts, stream: int = 0):
+    def shard_exact_frame(self, entry: int, frame_end: int, n_records: int, starts, stream: int = 0):
         world = len(starts)
         st = (ctypes.c_int64 * world)(*[int(v) for v in starts])
         counts = (ctypes.c_uint64 * world)()
-        self._call("sparkey_shard_exact_frame", entry, frame_end, st, ctypes.c_void_p(stream), counts)
+        self._call("sparkey_shard_exact_frame", entry, frame_end, n_records, st, ctypes.c_void_p(stream), counts)
         return [int(x) for x in counts]
 
     def shard_exact_pack(self, d_send: int, send_bytes: int, stream: int = 0) -> None:

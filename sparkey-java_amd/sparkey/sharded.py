@@ -299,8 +299,8 @@ class GpuShardSteps:
     def exact_record_size(self) -> int:
         return self.plan.shard_exact_record_size()
 
-    def exact_frame(self, entry: int, frame_end: int, starts) -> list:
-        return self.plan.shard_exact_frame(entry, frame_end, starts, self.stream)
+    def exact_frame(self, entry: int, frame_end: int, n_records: int, starts) -> list:
+        return self.plan.shard_exact_frame(entry, frame_end, n_records, starts, self.stream)
 
     def exact_pack(self, send: torch.Tensor) -> None:
         self.plan.shard_exact_pack(send.data_ptr(), send.numel(), self.stream)
@@ -575,7 +575,8 @@ class ShardedBuilder:
                 bnd = self._range_stats(slot_lo, slot_hi)
         mark("spill")
         if exact:  # the ring splits at the slots the PUT placement left empty (now complete on every rank)
-            done = self._exact(res, out, hdr_off, entries, frame_end, opts, h, slot_lo, slot_hi, slot_size, buf.device)
+            done = self._exact(res, out, hdr_off, entries, frame_end, int(R[g][3]), opts, h, slot_lo, slot_hi,
+                               slot_size, buf.device)
             if done is not None:
                 mark("exact")
                 return done
@@ -603,7 +604,7 @@ class ShardedBuilder:
         return c.allgather_i64([_signed(v) for v in bslots] + [nonempty, mx, col, tot])
 
     # ---- the sharded exact path ----
-    def _exact(self, res, out, hdr_off, entries, frame_end, opts, h, slot_lo, slot_hi, slot_size, device):
+    def _exact(self, res, out, hdr_off, entries, frame_end, n_records, opts, h, slot_lo, slot_hi, slot_size, device):
         """IndexHash.put / delete (IndexHash.java:454-665) replayed on exact ranges: the ring splits at the
         slots the canonical placement of all PUT records leaves empty (no probe or backward shift crosses
         one), rank r's range running from the first such slot of its slot range to the next rank's.
@@ -621,7 +622,7 @@ class ShardedBuilder:
             a, b = E[r], E[have[(i + 1) % len(have)]]
             ranges[r] = (a, b + cap if b <= a else b)
         # every record (PUT and DELETE) with its header and key to the owner of its wanted slot's range
-        counts = s.exact_frame(entries[g], frame_end(g), E)
+        counts = s.exact_frame(entries[g], frame_end(g), n_records, E)
         n_send = sum(counts)
         send = s.alloc(max(1, n_send) * rs)
         s.exact_pack(send)

@@ -340,7 +340,7 @@ class CpuShardSteps:
                 own = r
         return own if own >= 0 else last
 
-    def exact_frame(self, entry, frame_end, starts):
+    def exact_frame(self, entry, frame_end, n_records, starts):
         m = self.frame(entry, frame_end)
         assert not m["rc"]
         self._ex = []  # (owner, hash, address, header + key bytes) in log order
