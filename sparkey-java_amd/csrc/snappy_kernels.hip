@@ -425,6 +425,255 @@ __global__ void __launch_bounds__(256) k_snappy_rewrite(SnappyParams S) {
   for (int i = 0; i < S.as; i++) os[S.hs + i] = (uint8_t)(fa >> (8 * i));
 }
 
+// ------------------------------------------------------------------------------------------------
+// Parallel block directory: anchors on the block chain found by speculation, the
+// chain between them walked from every anchor at once, every link checked.
+// ------------------------------------------------------------------------------------------------
+namespace {
+
+// One hop of the chain from p with k_snappy_dir's checks (the same errors): {next, data, clen, ulen}.
+// win(p) gives the 16 bytes from p (global memory, or the screen's LDS copy).
+struct DirHop {
+  int64_t next, data;
+  int32_t clen, ulen;
+  int32_t err;  // 0, 1 bad framing, 2 larger than the reader's buffers
+};
+
+template <class Win>
+__device__ __forceinline__ DirHop dir_hop(const SnappyParams& S, int64_t p, const Win& win) {
+  DirHop h{0, 0, 0, 0, 0};
+  const Window w = win(p);
+  int j = 0;
+  int32_t err = 0;
+  const int32_t clen = dir_vlq(w, j, (int)min<int64_t>(16, S.data_end - p), err);
+  const int64_t q = p + j;
+  if (err || clen < 0 || q + clen > S.data_end) { h.err = 1; return h; }
+  const int32_t ulen = dir_vlq(w, j, (int)min<int64_t>(16, q + clen - p), err);
+  if (err || ulen < 0) { h.err = 1; return h; }
+  if ((int64_t)ulen > S.max_block || (int64_t)clen > 32 + S.max_block + S.max_block / 6) { h.err = 2; return h; }
+  h.next = q + clen;
+  h.data = q;
+  h.clen = clen;
+  h.ulen = ulen;
+  return h;
+}
+
+// A screen for speculative block starts (never needed for correctness: every link is checked): the
+// header hop, then the stream's first ten elements (within 320 bytes) -- a literal first, copy
+// offsets within what is already out, nothing past the decompressed size or the stream end.
+template <class Win>
+__device__ __forceinline__ bool snappy_head_plausible(const SnappyParams& S, const DirHop& h, const Win& win) {
+  if (h.err) return false;
+  int64_t pos;  // past the preamble's varint
+  {
+    const Window w = win(h.data);
+    int j = 0;
+    while (j < 5 && (w.at(j) & 0x80u)) j++;
+    pos = h.data + j + 1;
+  }
+  const int64_t end = h.data + h.clen;
+  if (h.ulen == 0) return pos == end;
+  const int64_t lim = pos + 320;  // the elements checked start in the next 320 bytes
+  uint32_t o = 0;
+  for (int e = 0; e < 10; e++) {
+    if (pos >= end) return o == (uint32_t)h.ulen;
+    if (o >= (uint32_t)h.ulen) return false;  // the output is complete but the stream goes on
+    if (pos >= lim) return true;
+    const Window w = win(pos);
+    const uint32_t t = w.at(0);
+    uint32_t len, off = 0;
+    if ((t & 3u) == 0) {
+      len = (t >> 2) + 1;
+      int64_t q = pos + 1;
+      if (len > 60) {
+        const uint32_t nb = len - 60;
+        uint32_t v = 0;
+        for (uint32_t k = 0; k < nb; k++) v |= w.at(1 + (int)k) << (8 * k);
+        len = v + 1;
+        q += nb;
+      }
+      if (len == 0 || (uint64_t)len > (uint64_t)(h.ulen - o) || q + len > end) return false;
+      pos = q + len;
+    } else {
+      if ((t & 3u) == 1) {
+        len = ((t >> 2) & 7u) + 4;
+        off = ((t >> 5) << 8) | w.at(1);
+        pos += 2;
+      } else if ((t & 3u) == 2) {
+        len = (t >> 2) + 1;
+        off = w.at(1) | (w.at(2) << 8);
+        pos += 3;
+      } else {
+        len = (t >> 2) + 1;
+        off = w.at(1) | (w.at(2) << 8) | (w.at(3) << 16) | (w.at(4) << 24);
+        pos += 5;
+      }
+      if (off == 0 || off > o || len > (uint32_t)h.ulen - o || pos > end) return false;
+    }
+    o += len;
+  }
+  return true;
+}
+
+// a start that passes the screen, and whose next block (if any) passes it too
+template <class Win>
+__device__ __forceinline__ bool block_start_plausible(const SnappyParams& S, int64_t p, const Win& win, DirHop& h) {
+  h = dir_hop(S, p, win);
+  if (!snappy_head_plausible(S, h, win)) return false;
+  if (h.next >= S.data_end) return true;
+  const DirHop h2 = dir_hop(S, h.next, win);
+  return snappy_head_plausible(S, h2, win);
+}
+
+struct GlobalWin {
+  const SnappyParams* S;
+  __device__ __forceinline__ Window operator()(int64_t p) const { return load_window(S->log, p, S->log_len); }
+};
+
+// the screen's window: the staged bytes [base, base + n) from LDS (aligned dwords, funnel-shifted),
+// anything else from global memory
+struct StagedWin {
+  const SnappyParams* S;
+  const uint32_t* lds;  // base is 16-byte aligned
+  int64_t base, n;
+  __device__ __forceinline__ Window operator()(int64_t p) const {
+    const int64_t r = p - base;
+    if (r < 0 || r + 24 > n) return load_window(S->log, p, S->log_len);
+    const uint32_t i = (uint32_t)(r >> 2), sh = (uint32_t)(r & 3) * 8u;
+    uint32_t d[5];
+#pragma unroll
+    for (int k = 0; k < 5; k++) d[k] = lds[i + k];
+    const uint64_t q0 = d[0] | ((uint64_t)d[1] << 32), q1 = d[2] | ((uint64_t)d[3] << 32);
+    const uint64_t q2 = d[4];
+    Window w;
+    w.lo = sh ? (q0 >> sh) | (q1 << (64 - sh)) : q0;
+    w.hi = sh ? (q1 >> sh) | (q2 << (64 - sh)) : q1;
+    return w;
+  }
+};
+
+constexpr int kDirCand = kSdirCand;  // candidate starts per window
+
+}  // namespace
+
+// Window k = [84 + k A, 84 + k A + H), H = the longest hop (so it holds a true start unless it runs
+// past dataEnd): its plausible starts whose next block is plausible too, into cand[k].  The window's
+// bytes (and 384 past it, for the screen's look-ahead) are staged in LDS first.
+__global__ __launch_bounds__(256) void k_sdir_screen(SnappyParams S, int64_t A, int64_t H, int64_t* cand,
+                                                     int32_t* ncand) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t stage[];
+  __shared__ int32_t n;
+  const uint64_t k = blockIdx.x;
+  if (threadIdx.x == 0) n = 0;
+  const int64_t w0 = 84 + (int64_t)k * A;
+  const int64_t w1 = min(w0 + H, S.data_end);
+  const int64_t base = w0 & ~15LL;
+  const int64_t nst = min<int64_t>(((w1 - base + 384 + 15) & ~15LL), ((S.log_len - base) & ~15LL));
+  for (int64_t v = threadIdx.x; v < nst / 16; v += blockDim.x)
+    reinterpret_cast<uint4*>(stage)[v] = *reinterpret_cast<const uint4*>(S.log + base + 16 * v);
+  __syncthreads();
+  const StagedWin win{&S, stage, base, nst};
+  for (int64_t p = w0 + threadIdx.x; p < w1; p += blockDim.x) {
+    DirHop h;
+    if (!block_start_plausible(S, p, win, h)) continue;
+    const int32_t i = atomicAdd(&n, 1);
+    if (i < kDirCand) cand[k * kDirCand + i] = p;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) ncand[k] = n;
+}
+
+// Window k's anchor: the first chain position at or past its end that every candidate chain reaching
+// that far (plausible at every hop) agrees on -- the window's true start is a candidate when the
+// stream is well formed -- else -1.
+__global__ __launch_bounds__(64) void k_sdir_anchor(SnappyParams S, int64_t A, int64_t H, const int64_t* cand,
+                                                    const int32_t* ncand, int64_t* anchor) {
+  const uint64_t k = blockIdx.x;
+  const int lane = threadIdx.x;
+  const int64_t wend = 84 + (int64_t)k * A + H;
+  const int32_t nc = ncand[k];
+  const GlobalWin win{&S};
+  int64_t x = -1;
+  if (nc <= kDirCand && lane < nc) {
+    int64_t p = cand[k * kDirCand + lane];
+    while (p < wend && p < S.data_end) {
+      DirHop h;
+      if (!block_start_plausible(S, p, win, h)) { p = -1; break; }
+      p = h.next;
+    }
+    x = p;
+  }
+  const unsigned long long alive = __ballot(x >= 0);
+  int64_t first = -1;
+  if (alive) first = __shfl(x, __ffsll(alive) - 1, 64);
+  const bool agree = !__any(x >= 0 && x != first);
+  if (lane == 0) anchor[k] = (alive && agree && nc <= kDirCand) ? first : -1;
+}
+
+// Link i: the chain from ends[i] to ends[i + 1], every hop with k_snappy_dir's checks.  emit = 0:
+// its blocks and decompressed bytes (cnt, usum); emit = 1: its blocks into S.blocks from boff[i],
+// virtual offsets from 84 + uoff[i].  fail[0] |= 1 when a link does not land on its end.
+__global__ __launch_bounds__(64) void k_sdir_link(SnappyParams S, const int64_t* ends, uint64_t nlinks, int emit,
+                                                  uint64_t* cnt, uint64_t* usum, const uint64_t* boff,
+                                                  const uint64_t* uoff, int32_t* fail) {
+  const uint64_t i = (uint64_t)blockIdx.x * 64 + threadIdx.x;
+  if (i >= nlinks) return;
+  int64_t p = ends[i];
+  const int64_t e = ends[i + 1];
+  uint64_t nb = 0, us = 0;
+  uint64_t bi = emit ? boff[i] : 0;
+  const uint64_t v0 = emit ? uoff[i] : 0;
+  const GlobalWin win{&S};
+  while (p < e) {
+    const DirHop h = dir_hop(S, p, win);
+    if (h.err) {
+      atomicOr(fail, 1 << h.err);
+      return;
+    }
+    if (emit) {
+      if (bi >= S.blk_cap) {
+        atomicOr(fail, 8);
+        return;
+      }
+      SnappyBlock B;
+      B.file_pos = p;
+      B.data = h.data;
+      B.voff = 84 + (int64_t)(v0 + us);
+      B.clen = (uint32_t)h.clen;
+      B.ulen = (uint32_t)h.ulen;
+      S.blocks[bi++] = B;
+    }
+    nb++;
+    us += (uint64_t)h.ulen;
+    p = h.next;
+  }
+  if (p != e) atomicOr(fail, 1);
+  if (!emit) {
+    cnt[i] = nb;
+    usum[i] = us;
+  }
+}
+
+void launch_sdir_screen(const SnappyParams& S, hipStream_t s, int64_t A, int64_t H, uint64_t nwin, int64_t* cand,
+                        int32_t* ncand) {
+  const size_t lds = sdir_screen_lds(H);
+  if (!nwin) return;
+  (void)hipFuncSetAttribute((const void*)k_sdir_screen, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL(k_sdir_screen, dim3((unsigned)nwin), 256, lds, s, S, A, H, cand, ncand);
+}
+
+void launch_sdir_anchor(const SnappyParams& S, hipStream_t s, int64_t A, int64_t H, uint64_t nwin, const int64_t* cand,
+                        const int32_t* ncand, int64_t* anchor) {
+  if (nwin) hipLaunchKernelGGL(k_sdir_anchor, dim3((unsigned)nwin), 64, 0, s, S, A, H, cand, ncand, anchor);
+}
+
+void launch_sdir_link(const SnappyParams& S, hipStream_t s, const int64_t* ends, uint64_t nlinks, int emit,
+                      uint64_t* cnt, uint64_t* usum, const uint64_t* boff, const uint64_t* uoff, int32_t* fail) {
+  if (nlinks)
+    hipLaunchKernelGGL(k_sdir_link, dim3((unsigned)((nlinks + 63) / 64)), 64, 0, s, S, ends, nlinks, emit, cnt, usum,
+                       boff, uoff, fail);
+}
+
 void launch_snappy_dir(const SnappyParams& S, hipStream_t s) { hipLaunchKernelGGL(k_snappy_dir, 1, 64, 0, s, S); }
 
 hipError_t launch_snappy_decode(const SnappyParams& S, hipStream_t s) {

@@ -309,6 +309,8 @@ struct sparkey_plan {
   uint8_t* sn_vlog = nullptr;
   uint8_t* sn_itab = nullptr;
   int32_t* sn_err = nullptr;
+  uint64_t c_sn_par = 0;
+  uint8_t* sn_par = nullptr;        // the parallel directory's scratch (candidates, anchors, links)
   hipStream_t sn_stream = nullptr;  // the decode of one directory chunk overlaps the next chunk
   hipEvent_t sn_ev[2] = {nullptr, nullptr};
   uint64_t c_seg_cls_cnt = 0, c_seg_cls_off = 0;
@@ -746,6 +748,90 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
 // (blockPosition << entryBlockBits) | entryIndex (IndexHash.java:270-283).  The two codecs differ only
 // in the directory (a Snappy preamble / a Zstandard Frame_Content_Size gives each block's size) and
 // the decode kernel (snappy_kernels.hip / zstd_kernels.hip).
+// The SNAPPY block directory in parallel: windows of the longest hop every A bytes,
+// their plausible block starts chained to an anchor each (the first chain position past the window,
+// where the candidates agree), then every link of the chain 84 -> anchors -> dataEnd walked from its
+// start at once with k_snappy_dir's checks; a link that does not land on its end, or any check that
+// fails, leaves the directory to the serial chain (*ok = false), which reports errors exactly.
+static int snappy_par_dir(sparkey_plan* pl, SnappyParams& S, hipStream_t s, SnappyDirResult* dir, bool* ok, char* err,
+                          size_t err_len) {
+  *ok = false;
+  const int64_t body = S.data_end - kLogHeaderSize;
+  if (body <= 0 || S.max_block <= 0) return SPARKEY_OK;
+  const int64_t H = 32 + S.max_block + S.max_block / 6 + 5;  // the longest hop: VLQ + maxCompressedLength
+  if (sdir_screen_lds(H) > 150 * 1024) return SPARKEY_OK;   // (blocks over ~128 KiB: the serial chain)
+  int64_t A = std::max<int64_t>(16 * H, body / (1 << 20) + 1);  // (screen 1/16 of the log; links of ~16 blocks)
+  if (const char* v = getenv("SPARKEY_SNAPPY_DIR_A")) A = std::max<int64_t>(H, atoll(v));  // (tests, tuning)
+  const uint64_t nwin = body > H ? (uint64_t)((body - H - 1) / A + 1) : 0;
+  const uint64_t maxl = nwin + 1;  // links
+  const uint64_t bytes = nwin * (kSdirCand * 8 + 4 + 8) + (maxl + 1) * 8 + 4 * maxl * 8 + 64;
+  HIP_TRY(grow(&pl->sn_par, pl->c_sn_par, bytes));
+  uint8_t* q = pl->sn_par;
+  auto carve = [&](uint64_t n) { uint8_t* r = q; q += (n + 15) & ~15ull; return r; };
+  int64_t* cand = (int64_t*)carve(nwin * kSdirCand * 8);
+  int32_t* ncand = (int32_t*)carve(nwin * 4);
+  int64_t* anchor = (int64_t*)carve(nwin * 8);
+  int64_t* ends = (int64_t*)carve((maxl + 1) * 8);
+  uint64_t* cnt = (uint64_t*)carve(maxl * 8);
+  uint64_t* usum = (uint64_t*)carve(maxl * 8);
+  uint64_t* boff = (uint64_t*)carve(maxl * 8);
+  uint64_t* uoff = (uint64_t*)carve(maxl * 8);
+  int32_t* fail = (int32_t*)carve(16);
+  HIP_TRY(hipMemsetAsync(fail, 0, 4, s));
+  launch_sdir_screen(S, s, A, H, nwin, cand, ncand);
+  launch_sdir_anchor(S, s, A, H, nwin, cand, ncand, anchor);
+  HIP_TRY(hipGetLastError());
+  std::vector<int64_t> anc(nwin);
+  if (nwin) HIP_TRY(hipMemcpyAsync(anc.data(), anchor, nwin * 8, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  std::vector<int64_t> e;
+  e.push_back(kLogHeaderSize);
+  for (int64_t x : anc)
+    if (x > e.back() && x < S.data_end) e.push_back(x);
+  e.push_back(S.data_end);
+  const uint64_t nl = e.size() - 1;
+  HIP_TRY(hipMemcpyAsync(ends, e.data(), e.size() * 8, hipMemcpyHostToDevice, s));
+  launch_sdir_link(S, s, ends, nl, 0, cnt, usum, nullptr, nullptr, fail);
+  HIP_TRY(hipGetLastError());
+  std::vector<uint64_t> hc(nl), hu(nl);
+  int32_t hf = 0;
+  HIP_TRY(hipMemcpyAsync(hc.data(), cnt, nl * 8, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(hu.data(), usum, nl * 8, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(&hf, fail, 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  if (hf) return SPARKEY_OK;
+  std::vector<uint64_t> bo(nl), uo(nl);
+  uint64_t nb = 0, tot = 0;
+  for (uint64_t i = 0; i < nl; i++) {
+    bo[i] = nb;
+    uo[i] = tot;
+    nb += hc[i];
+    tot += hu[i];
+  }
+  HIP_TRY(grow(&pl->sn_blocks, pl->c_sn_blocks, std::max<uint64_t>(nb, 1)));
+  HIP_TRY(grow(&pl->sn_walk, pl->c_sn_walk, pl->c_sn_blocks));
+  S.blocks = pl->sn_blocks;
+  S.blk_cap = pl->c_sn_blocks;
+  S.walk = pl->sn_walk;
+  HIP_TRY(hipMemcpyAsync(boff, bo.data(), nl * 8, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(uoff, uo.data(), nl * 8, hipMemcpyHostToDevice, s));
+  launch_sdir_link(S, s, ends, nl, 1, cnt, usum, boff, uoff, fail);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(&hf, fail, 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  if (hf) return SPARKEY_OK;
+  if (getenv("SPARKEY_SNAPPY_DIR_DEBUG"))
+    fprintf(stderr, "[snappy dir] parallel: %llu blocks, %llu windows, %llu links\n", (unsigned long long)nb,
+            (unsigned long long)nwin, (unsigned long long)nl);
+  memset(dir, 0, sizeof(*dir));
+  dir->nblk = nb;
+  dir->total = tot;
+  dir->p = S.data_end;
+  dir->done = 1;
+  *ok = true;
+  return SPARKEY_OK;
+}
+
 static int plan_build_snappy(sparkey_plan* pl, const LogHdr& lh, const uint8_t* log_header, const uint8_t* d_log,
                              uint64_t log_len, uint8_t* d_out, uint64_t index_cap, const sparkey_build_opts* opts,
                              hipStream_t s, sparkey_build_stats* stats_out, char* err, size_t err_len) {
@@ -877,10 +963,31 @@ static int plan_build_snappy(sparkey_plan* pl, const LogHdr& lh, const uint8_t* 
   const uint64_t ps = (uint64_t)std::max<int64_t>(0, lh.put_size), ds = (uint64_t)std::max<int64_t>(0, lh.delete_size);
   const uint64_t hdr_total = ps + ds < ps ? UINT64_MAX : ps + ds;
   const int64_t vcap0 = hdr_total <= 22 * body + 4096 ? (int64_t)hdr_total : 0;
-  HIP_TRY(grow(&pl->sn_vlog, pl->c_sn_vlog, (uint64_t)vcap0 + kLogHeaderSize + 4096));
-  S.vlog = pl->sn_vlog;
-  HIP_TRY(pipeline(vcap0, true));
-  if (dir.err == 3) {  // more decompressed bytes than vcap0 (putSize = deleteSize = 0 included)
+  bool par = false;  // SNAPPY: the directory in parallel, then every block decoded in one launch
+  if (!zstd && !getenv("SPARKEY_SNAPPY_SERIAL_DIR")) {
+    rc = snappy_par_dir(pl, S, s, &dir, &par, err, err_len);
+    if (rc) return rc;
+  }
+  if (par) {
+    HIP_TRY(grow(&pl->sn_vlog, pl->c_sn_vlog, dir.total + kLogHeaderSize + 4096));
+    S.vlog = pl->sn_vlog;
+    S.blocks = pl->sn_blocks;
+    S.walk = pl->sn_walk;
+    S.blk_base = 0;
+    S.nblk = dir.nblk;
+    hipError_t e = decode_launch(s);
+    if (e != hipSuccess && S.lds_bytes) {  // the LDS size was refused: decode in global memory
+      (void)hipGetLastError();
+      S.lds_bytes = 0;
+      e = decode_launch(s);
+    }
+    HIP_TRY(e);
+  } else {
+    HIP_TRY(grow(&pl->sn_vlog, pl->c_sn_vlog, (uint64_t)vcap0 + kLogHeaderSize + 4096));
+    S.vlog = pl->sn_vlog;
+    HIP_TRY(pipeline(vcap0, true));
+  }
+  if (!par && dir.err == 3) {  // more decompressed bytes than vcap0 (putSize = deleteSize = 0 included)
     HIP_TRY(hipStreamSynchronize(s));
     HIP_TRY(pipeline(-1, false));
     if (!dir.err) {
@@ -1593,7 +1700,7 @@ void sparkey_plan_destroy(sparkey_plan* pl) {
                   pl->seg_cls_cnt, pl->seg_cls_off, pl->p2tab,
                   pl->app_i64, pl->app_u32, pl->app_u64, pl->app_scan, pl->app_map,
                   pl->sn_blocks, pl->sn_dir, pl->sn_walk, pl->sn_recoff, pl->sn_vlog, pl->sn_itab, pl->sn_err,
-                  pl->xtab, pl->ex_starts, pl->ex_cnt, pl->ex_off};
+                  pl->xtab, pl->ex_starts, pl->ex_cnt, pl->ex_off, pl->sn_par};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (pl->h_status) (void)hipHostFree(pl->h_status);
