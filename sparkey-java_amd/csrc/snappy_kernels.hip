@@ -321,25 +321,130 @@ __global__ void __launch_bounds__(64) k_snappy_lds(SnappyParams S) {
   }
 }
 
-// One wave per block as k_snappy_lds, decoding straight into the virtual log: only the stream window
-// is in LDS (8 KiB per wave instead of the whole decoded block), so many more blocks decode at once;
-// matches read back through L2.
+// k_snappy_gw: one wave per block, decoding straight into the virtual log.  In LDS only a window over
+// the stream (refilled with aligned 16-byte loads as the parse nears its end) and a ring of the last
+// kSnappyRing output bytes, from which matches copy (a longer-range match waits for the wave's stores
+// and reads global memory): 12 KiB per wave instead of the whole decoded block, so many blocks decode
+// at once.  Every LDS access indexes the __shared__ arrays themselves (never a pointer that may point
+// to global memory as well), so the loads are ds_* and do not wait for the wave's global stores.
+constexpr uint32_t kSnappyRing = 4096;
 __global__ void __launch_bounds__(64) k_snappy_gw(SnappyParams S) {
   __shared__ __attribute__((aligned(16))) uint8_t win[kSnappyWindow + 16];
+  __shared__ __attribute__((aligned(16))) uint8_t ring[kSnappyRing];
+  constexpr uint32_t RM = kSnappyRing - 1;
   const uint64_t b = S.blk_base + blockIdx.x;
   const SnappyBlock B = S.blocks[b];
   const uint32_t lane = threadIdx.x;
-  RingIn in;
-  in.g = S.log + B.data;
-  in.readable = S.log_len - B.data;
-  in.n = B.clen;
-  in.win = win;
-  in.lane = lane;
-  in.refill(0);
+  const uint8_t* g = S.log + B.data;
+  const int64_t readable = S.log_len - B.data;
+  const uint32_t n = B.clen, ulen = B.ulen;
+  uint8_t* out = S.vlog + B.voff;
+  int64_t wa = 0, wend = 0;  // the window holds stream bytes [wa, wend)
+  auto refill = [&](uint32_t p) {
+    wa = (int64_t)p - (int64_t)(((uintptr_t)(g + p)) & 15);
+#pragma unroll 4
+    for (uint32_t w = lane; w < kSnappyWindow / 16; w += 64) {
+      const int64_t q = wa + 16 * (int64_t)w;
+      if (q + 16 <= readable) {
+        *(uint4*)(win + 16 * w) = *(const uint4*)(g + q);
+      } else {
+        for (int i = 0; i < 16 && q + i < readable; i++) win[16 * w + i] = g[q + i];
+      }
+    }
+    wend = min<int64_t>(wa + kSnappyWindow, (int64_t)n);
+    __builtin_amdgcn_wave_barrier();
+  };
+  auto byte = [&](uint32_t q) -> uint32_t { return win[(int64_t)q - wa]; };
+  refill(0);
   uint32_t p = 0;
-  while (in.byte(p) & 0x80u) p++;
+  while (byte(p) & 0x80u) p++;  // preamble (<= 5 bytes, validated by the directory)
   p++;
-  const uint32_t flags = snappy_decode<true, RingIn, true>(in, B.clen, p, S.vlog + B.voff, B.ulen, lane, 64u);
+  uint32_t o = 0, flags = 0;
+  while (p < n) {
+    if ((int64_t)p + 5 > wend && wend < (int64_t)n) refill(p);
+    const uint32_t t = __builtin_amdgcn_readfirstlane(byte(p));
+    const uint32_t e0 = __builtin_amdgcn_readfirstlane(p + 1 < n ? byte(p + 1) : 0u);
+    const uint32_t e1 = __builtin_amdgcn_readfirstlane(p + 2 < n ? byte(p + 2) : 0u);
+    const uint32_t e2 = __builtin_amdgcn_readfirstlane(p + 3 < n ? byte(p + 3) : 0u);
+    const uint32_t e3 = __builtin_amdgcn_readfirstlane(p + 4 < n ? byte(p + 4) : 0u);
+    p++;
+    uint32_t len, off = 0;
+    if ((t & 3u) == 0) {
+      len = (t >> 2) + 1;
+      if (len > 60) {
+        const uint32_t nb = len - 60;
+        if (p + nb > n) { flags = kWalkBadStream; break; }
+        const uint32_t w = e0 | (e1 << 8) | (e2 << 16) | (e3 << 24);
+        const uint64_t lm1 = nb == 4 ? (uint64_t)w : (uint64_t)(w & ((1u << (8 * nb)) - 1u));
+        if (lm1 + 1 > (uint64_t)(n - p - nb)) { flags = kWalkBadStream; break; }
+        len = (uint32_t)lm1 + 1;
+        p += nb;
+      }
+      if (len > n - p || len > ulen - o) { flags = kWalkBadStream; break; }
+      if ((int64_t)p + len <= wend) {  // from the window
+        const int64_t r = (int64_t)p - wa;
+        for (uint32_t k = lane; k < len; k += 64) {
+          const uint8_t v = win[r + k];
+          out[o + k] = v;
+          ring[(o + k) & RM] = v;
+        }
+      } else {  // reaches past the window: from global memory
+        for (uint32_t k = lane; k < len; k += 64) {
+          const uint8_t v = g[p + k];
+          out[o + k] = v;
+          ring[(o + k) & RM] = v;
+        }
+      }
+      p += len;
+    } else {
+      if ((t & 3u) == 1) {
+        if (p + 1 > n) { flags = kWalkBadStream; break; }
+        len = ((t >> 2) & 7u) + 4;
+        off = ((t >> 5) << 8) | e0;
+        p += 1;
+      } else if ((t & 3u) == 2) {
+        if (p + 2 > n) { flags = kWalkBadStream; break; }
+        len = (t >> 2) + 1;
+        off = e0 | (e1 << 8);
+        p += 2;
+      } else {
+        if (p + 4 > n) { flags = kWalkBadStream; break; }
+        len = (t >> 2) + 1;
+        off = e0 | (e1 << 8) | (e2 << 16) | (e3 << 24);
+        p += 4;
+      }
+      if (off == 0 || off > o || len > ulen - o) { flags = kWalkBadStream; break; }
+      if (off + len <= kSnappyRing) {  // out[o + k] = out[o - off + k % off]: sources < o, in the ring
+        for (uint32_t k0 = 0; k0 < len; k0 += 64) {
+          const uint32_t k = k0 + lane;
+          uint8_t v = 0;
+          if (k < len) v = ring[(o - off + (off >= len ? k : k % off)) & RM];
+          __builtin_amdgcn_wave_barrier();
+          if (k < len) {
+            out[o + k] = v;
+            ring[(o + k) & RM] = v;
+          }
+          __builtin_amdgcn_wave_barrier();
+        }
+      } else {
+        __builtin_amdgcn_s_waitcnt(0);  // the wave's own stores of the source first
+        for (uint32_t k0 = 0; k0 < len; k0 += 64) {
+          const uint32_t k = k0 + lane;
+          uint8_t v = 0;
+          if (k < len) v = *(const volatile uint8_t*)(out + o - off + (off >= len ? k : k % off));
+          __builtin_amdgcn_s_waitcnt(0);
+          if (k < len) {
+            out[o + k] = v;
+            ring[(o + k) & RM] = v;
+          }
+          __builtin_amdgcn_s_waitcnt(0);
+        }
+      }
+    }
+    o += len;
+    __builtin_amdgcn_wave_barrier();  // one-wave workgroup: LDS ops run in order
+  }
+  if (!flags && o != ulen) flags = kWalkBadStream;
   if (lane == 0) {
     SnappyWalk w;
     w.count = 0;
@@ -559,7 +664,7 @@ constexpr int kDirCand = kSdirCand;  // candidate starts per window
 // Window k = [84 + k A, 84 + k A + H), H = the longest hop (so it holds a true start unless it runs
 // past dataEnd): its plausible starts whose next block is plausible too, into cand[k].  The window's
 // bytes (and 384 past it, for the screen's look-ahead) are staged in LDS first.
-__global__ __launch_bounds__(256) void k_sdir_screen(SnappyParams S, int64_t A, int64_t H, int64_t* cand,
+__global__ __launch_bounds__(1024) void k_sdir_screen(SnappyParams S, int64_t A, int64_t H, int64_t* cand,
                                                      int32_t* ncand) {
   extern __shared__ __attribute__((aligned(16))) uint32_t stage[];
   __shared__ int32_t n;
@@ -659,7 +764,7 @@ void launch_sdir_screen(const SnappyParams& S, hipStream_t s, int64_t A, int64_t
   const size_t lds = sdir_screen_lds(H);
   if (!nwin) return;
   (void)hipFuncSetAttribute((const void*)k_sdir_screen, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL(k_sdir_screen, dim3((unsigned)nwin), 256, lds, s, S, A, H, cand, ncand);
+  hipLaunchKernelGGL(k_sdir_screen, dim3((unsigned)nwin), 1024, lds, s, S, A, H, cand, ncand);
 }
 
 void launch_sdir_anchor(const SnappyParams& S, hipStream_t s, int64_t A, int64_t H, uint64_t nwin, const int64_t* cand,

@@ -760,7 +760,7 @@ static int snappy_par_dir(sparkey_plan* pl, SnappyParams& S, hipStream_t s, Snap
   if (body <= 0 || S.max_block <= 0) return SPARKEY_OK;
   const int64_t H = 32 + S.max_block + S.max_block / 6 + 5;  // the longest hop: VLQ + maxCompressedLength
   if (sdir_screen_lds(H) > 150 * 1024) return SPARKEY_OK;   // (blocks over ~128 KiB: the serial chain)
-  int64_t A = std::max<int64_t>(16 * H, body / (1 << 20) + 1);  // (screen 1/16 of the log; links of ~16 blocks)
+  int64_t A = std::max<int64_t>(32 * H, body / (1 << 20) + 1);  // (screen 1/32 of the log; links of ~32 blocks)
   if (const char* v = getenv("SPARKEY_SNAPPY_DIR_A")) A = std::max<int64_t>(H, atoll(v));  // (tests, tuning)
   const uint64_t nwin = body > H ? (uint64_t)((body - H - 1) / A + 1) : 0;
   const uint64_t maxl = nwin + 1;  // links
