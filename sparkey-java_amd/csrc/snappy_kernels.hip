@@ -328,8 +328,10 @@ __global__ void __launch_bounds__(64) k_snappy_lds(SnappyParams S) {
 // at once.  Every LDS access indexes the __shared__ arrays themselves (never a pointer that may point
 // to global memory as well), so the loads are ds_* and do not wait for the wave's global stores.
 constexpr uint32_t kSnappyRing = 4096;
+constexpr uint32_t kGwWindow = 4096;  // k_snappy_gw's stream window (8 KiB of LDS per wave with the ring)
+template <int kExp>
 __global__ void __launch_bounds__(64) k_snappy_gw(SnappyParams S) {
-  __shared__ __attribute__((aligned(16))) uint8_t win[kSnappyWindow + 16];
+  __shared__ __attribute__((aligned(16))) uint8_t win[kGwWindow + 16];
   __shared__ __attribute__((aligned(16))) uint8_t ring[kSnappyRing];
   constexpr uint32_t RM = kSnappyRing - 1;
   const uint64_t b = S.blk_base + blockIdx.x;
@@ -343,7 +345,7 @@ __global__ void __launch_bounds__(64) k_snappy_gw(SnappyParams S) {
   auto refill = [&](uint32_t p) {
     wa = (int64_t)p - (int64_t)(((uintptr_t)(g + p)) & 15);
 #pragma unroll 4
-    for (uint32_t w = lane; w < kSnappyWindow / 16; w += 64) {
+    for (uint32_t w = lane; w < kGwWindow / 16; w += 64) {
       const int64_t q = wa + 16 * (int64_t)w;
       if (q + 16 <= readable) {
         *(uint4*)(win + 16 * w) = *(const uint4*)(g + q);
@@ -351,7 +353,7 @@ __global__ void __launch_bounds__(64) k_snappy_gw(SnappyParams S) {
         for (int i = 0; i < 16 && q + i < readable; i++) win[16 * w + i] = g[q + i];
       }
     }
-    wend = min<int64_t>(wa + kSnappyWindow, (int64_t)n);
+    wend = min<int64_t>(wa + kGwWindow, (int64_t)n);
     __builtin_amdgcn_wave_barrier();
   };
   auto byte = [&](uint32_t q) -> uint32_t { return win[(int64_t)q - wa]; };
@@ -362,11 +364,24 @@ __global__ void __launch_bounds__(64) k_snappy_gw(SnappyParams S) {
   uint32_t o = 0, flags = 0;
   while (p < n) {
     if ((int64_t)p + 5 > wend && wend < (int64_t)n) refill(p);
-    const uint32_t t = __builtin_amdgcn_readfirstlane(byte(p));
-    const uint32_t e0 = __builtin_amdgcn_readfirstlane(p + 1 < n ? byte(p + 1) : 0u);
-    const uint32_t e1 = __builtin_amdgcn_readfirstlane(p + 2 < n ? byte(p + 2) : 0u);
-    const uint32_t e2 = __builtin_amdgcn_readfirstlane(p + 3 < n ? byte(p + 3) : 0u);
-    const uint32_t e3 = __builtin_amdgcn_readfirstlane(p + 4 < n ? byte(p + 4) : 0u);
+    // the tag and the four bytes after it: one aligned 8-byte LDS read (the window has 16 bytes of
+    // slack; bytes at or past the stream end are not used: every use is bounds-checked against n)
+    uint32_t t, e0, e1, e2, e3;
+    {
+      const uint32_t r = (uint32_t)((int64_t)p - wa);
+      const uint32_t a4 = r & ~3u, sh = (r & 3u) * 8u;
+      const uint32_t d0 = __builtin_amdgcn_readfirstlane(*reinterpret_cast<const uint32_t*>(win + a4));
+      const uint32_t d1 = __builtin_amdgcn_readfirstlane(*reinterpret_cast<const uint32_t*>(win + a4 + 4));
+      const uint32_t d2 = __builtin_amdgcn_readfirstlane(*reinterpret_cast<const uint32_t*>(win + a4 + 8));
+      const uint64_t lo = ((uint64_t)d1 << 32 | d0) >> sh;
+      const uint32_t hi = sh ? (d2 << (32 - sh)) : 0u;
+      const uint64_t v = lo | ((uint64_t)hi << 32);
+      t = (uint32_t)v & 0xffu;
+      e0 = (uint32_t)(v >> 8) & 0xffu;
+      e1 = (uint32_t)(v >> 16) & 0xffu;
+      e2 = (uint32_t)(v >> 24) & 0xffu;
+      e3 = (uint32_t)(v >> 32) & 0xffu;
+    }
     p++;
     uint32_t len, off = 0;
     if ((t & 3u) == 0) {
@@ -385,7 +400,7 @@ __global__ void __launch_bounds__(64) k_snappy_gw(SnappyParams S) {
         const int64_t r = (int64_t)p - wa;
         for (uint32_t k = lane; k < len; k += 64) {
           const uint8_t v = win[r + k];
-          out[o + k] = v;
+          if (kExp != 1) out[o + k] = v;
           ring[(o + k) & RM] = v;
         }
       } else {  // reaches past the window: from global memory
@@ -421,7 +436,7 @@ __global__ void __launch_bounds__(64) k_snappy_gw(SnappyParams S) {
           if (k < len) v = ring[(o - off + (off >= len ? k : k % off)) & RM];
           __builtin_amdgcn_wave_barrier();
           if (k < len) {
-            out[o + k] = v;
+            if (kExp != 1) out[o + k] = v;
             ring[(o + k) & RM] = v;
           }
           __builtin_amdgcn_wave_barrier();
@@ -784,8 +799,11 @@ void launch_snappy_dir(const SnappyParams& S, hipStream_t s) { hipLaunchKernelGG
 hipError_t launch_snappy_decode(const SnappyParams& S, hipStream_t s) {
   if (S.nblk == 0) return hipSuccess;
   static const bool gw = getenv("SPARKEY_SNAPPY_LDS") == nullptr;  // (A/B: the decoded block in LDS)
-  if (gw) {
-    hipLaunchKernelGGL(k_snappy_gw, dim3((uint32_t)S.nblk), 64, 0, s, S);
+  static const int exp = getenv("SPARKEY_SNAPPY_EXP") ? atoi(getenv("SPARKEY_SNAPPY_EXP")) : 0;  // (measurements)
+  if (gw && exp == 1) {
+    hipLaunchKernelGGL(k_snappy_gw<1>, dim3((uint32_t)S.nblk), 64, 0, s, S);
+  } else if (gw) {
+    hipLaunchKernelGGL(k_snappy_gw<0>, dim3((uint32_t)S.nblk), 64, 0, s, S);
   } else if (S.lds_bytes) {
     hipError_t e = hipFuncSetAttribute((const void*)k_snappy_lds, hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)S.lds_bytes);
