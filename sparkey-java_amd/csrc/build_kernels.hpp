@@ -212,6 +212,7 @@ struct BuildParams {
   int64_t uni_rec;
   uint32_t uni_wbytes;    // LDS staging bytes per wave (set by the launcher)
   uint32_t uni_hist_off;  // LDS offset of the digit counts (set by the launcher)
+  uint32_t uni_nt;        // framing kernels: non-temporal LDS-DMA of the log (SPARKEY_FRAME_NO_NT: default policy)
   // k_frame_uniform as partition pass 1: digit d's entries at ent3[d * p1_region, + p1_fill[d])
   uint64_t p1_region;   // 0 = off
   int32_t p2_sorted;    // k_part2s: per-(bucket, slot) counts in the same pass + the carry functions

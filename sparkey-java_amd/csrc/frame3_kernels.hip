@@ -136,10 +136,17 @@ __device__ __forceinline__ void frame3_region(const BuildParams& P, const uint64
     const int nvec = (int)((RLEN + 15) >> 4);
     if (R0 + 16ll * nvec <= log_len) {
       const uint4* src = reinterpret_cast<const uint4*>(P.log + R0);
-      for (int v0 = 0; v0 < nvec; v0 += 64)
-        __builtin_amdgcn_global_load_lds(
-            (const __attribute__((address_space(1))) void*)(src + min(v0 + lane, nvec - 1)),
-            (__attribute__((address_space(3))) void*)(rgn + 16u * (uint32_t)v0), 16, 0, 0);
+      if (P.uni_nt) {  // non-temporal: the log is read once
+        for (int v0 = 0; v0 < nvec; v0 += 64)
+          __builtin_amdgcn_global_load_lds(
+              (const __attribute__((address_space(1))) void*)(src + min(v0 + lane, nvec - 1)),
+              (__attribute__((address_space(3))) void*)(rgn + 16u * (uint32_t)v0), 16, 0, 2);
+      } else {
+        for (int v0 = 0; v0 < nvec; v0 += 64)
+          __builtin_amdgcn_global_load_lds(
+              (const __attribute__((address_space(1))) void*)(src + min(v0 + lane, nvec - 1)),
+              (__attribute__((address_space(3))) void*)(rgn + 16u * (uint32_t)v0), 16, 0, 0);
+      }
     } else {
       for (int v = lane; v < nvec; v += 64)
         *reinterpret_cast<uint4*>(rgn + 16u * v) = load16_guarded(P.log, R0 + 16ll * v, log_len);

@@ -90,10 +90,17 @@ __device__ __forceinline__ void frame_region(const BuildParams& P, const uint64_
       // 1 KiB per wave instruction at rgn + 1024 i; fr_rgn_bytes is a multiple of 1 KiB, lanes past
       // the end repeat the last vector)
       const uint4* src = reinterpret_cast<const uint4*>(P.log + R0);
-      for (int v0 = 0; v0 < nvec; v0 += 64)
-        __builtin_amdgcn_global_load_lds(
-            (const __attribute__((address_space(1))) void*)(src + min(v0 + lane, nvec - 1)),
-            (__attribute__((address_space(3))) void*)(rgn + 16u * (uint32_t)v0), 16, 0, 0);
+      if (P.uni_nt) {  // non-temporal: the log is read once
+        for (int v0 = 0; v0 < nvec; v0 += 64)
+          __builtin_amdgcn_global_load_lds(
+              (const __attribute__((address_space(1))) void*)(src + min(v0 + lane, nvec - 1)),
+              (__attribute__((address_space(3))) void*)(rgn + 16u * (uint32_t)v0), 16, 0, 2);
+      } else {
+        for (int v0 = 0; v0 < nvec; v0 += 64)
+          __builtin_amdgcn_global_load_lds(
+              (const __attribute__((address_space(1))) void*)(src + min(v0 + lane, nvec - 1)),
+              (__attribute__((address_space(3))) void*)(rgn + 16u * (uint32_t)v0), 16, 0, 0);
+      }
     } else {
       for (int v = lane; v < nvec; v += 64) {
         const uint4 val = load16_guarded(P.log, R0 + 16ll * v, log_len);
@@ -629,7 +636,35 @@ __device__ __forceinline__ uint32_t digit_of(const BuildParams& P, uint32_t buck
 // anything else flags spec_fail and the build reruns the general framing -- then hashes its key.
 // The entries are dense, in log order (the slab layout of the serial path).
 // ================================================================================================
-template <int W>
+// s_waitcnt vmcnt(n) for n in 0..16 (gfx9 encoding: vmcnt in bits 3:0 and 15:14, expcnt and lgkmcnt
+// left at their maxima)
+__device__ __forceinline__ void wait_vmcnt_le(int n) {
+#define SK_VM(v) __builtin_amdgcn_s_waitcnt(((v) & 0xF) | (((v) >> 4) << 14) | (0x7 << 4) | (0xF << 8))
+  switch (n) {
+    case 1: SK_VM(1); break;
+    case 2: SK_VM(2); break;
+    case 3: SK_VM(3); break;
+    case 4: SK_VM(4); break;
+    case 5: SK_VM(5); break;
+    case 6: SK_VM(6); break;
+    case 7: SK_VM(7); break;
+    case 8: SK_VM(8); break;
+    case 9: SK_VM(9); break;
+    case 10: SK_VM(10); break;
+    case 11: SK_VM(11); break;
+    case 12: SK_VM(12); break;
+    case 13: SK_VM(13); break;
+    case 14: SK_VM(14); break;
+    case 15: SK_VM(15); break;
+    case 16: SK_VM(16); break;
+    default: __builtin_amdgcn_s_waitcnt(0); break;
+  }
+#undef SK_VM
+}
+
+// W waves per workgroup; DB: each wave double-buffers its staging, the next round's LDS-DMA in flight
+// while it hashes the current one (the only global loads of the rounds, so vmcnt counts just them).
+template <int W, bool DB>
 __global__ __launch_bounds__(64 * W) void k_frame_uniform(BuildParams P) {
   // A workgroup frames kSub partition tiles (kSub * kPartTile records), kRounds rounds of 64 records
   // per wave, each wave staging its own records by LDS-DMA.
@@ -638,7 +673,7 @@ __global__ __launch_bounds__(64 * W) void k_frame_uniform(BuildParams P) {
   constexpr int kRounds = kSub * kTileRounds;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];  // wave buffers | hist[kSub][256] rbase[256]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  uint8_t* buf = lds + (uint32_t)wave * P.uni_wbytes;
+  uint8_t* buf0 = lds + (uint32_t)wave * P.uni_wbytes * (DB ? 2u : 1u);
   uint32_t* hist = reinterpret_cast<uint32_t*>(lds + P.uni_hist_off);  // per tile
   uint32_t* rbase = hist + kSub * 256;
   // to_regions: the entries go straight to their digit regions of ent3 (partition pass 1 done here);
@@ -658,11 +693,11 @@ __global__ __launch_bounds__(64 * W) void k_frame_uniform(BuildParams P) {
   const uint64_t blk0 = (uint64_t)blockIdx.x * (kSub * kPartTile);
   uint64_t hsh[kRounds];  // (the address follows from the round: record blk0 + (r * W + wave) * 64 + lane)
   uint32_t dr[kRounds];   // digit << 16 | rank within its tile's digit run, ~0 = none
-#pragma unroll
-  for (int r = 0; r < kRounds; r++) {
-    dr[r] = ~0u;
+  // stage round r's records into b: LDS-DMA (returns the load instructions in flight), or guarded
+  // loads near the end of the buffer (synchronous, returns 0)
+  auto stage_round = [&](int r, uint8_t* b) -> int {
     const uint64_t i0 = blk0 + (uint64_t)(r * W + wave) * 64;
-    if (i0 >= P.uni_n) continue;  // (wave-uniform)
+    if (i0 >= P.uni_n) return 0;  // (wave-uniform)
     const int64_t base = P.fr_entry + (int64_t)i0 * R;
     const int64_t a0 = base & ~15ll;
     const int nrec = (int)min((uint64_t)64, P.uni_n - i0);
@@ -670,14 +705,40 @@ __global__ __launch_bounds__(64 * W) void k_frame_uniform(BuildParams P) {
     const int nvec = (int)((want + 15) >> 4);
     if (a0 + 16ll * nvec <= log_len) {
       const uint4* src = reinterpret_cast<const uint4*>(P.log + a0);
-      for (int v0 = 0; v0 < nvec; v0 += 64)
-        __builtin_amdgcn_global_load_lds(
-            (const __attribute__((address_space(1))) void*)(src + min(v0 + lane, nvec - 1)),
-            (__attribute__((address_space(3))) void*)(buf + 16u * (uint32_t)v0), 16, 0, 0);
-      __builtin_amdgcn_s_waitcnt(0);  // this wave's LDS-DMA has landed
-    } else {
-      for (int v = lane; v < nvec; v += 64) *reinterpret_cast<uint4*>(buf + 16u * v) = load16_guarded(P.log, a0 + 16ll * v, log_len);
+      if (P.uni_nt) {  // non-temporal: the log is read once
+        for (int v0 = 0; v0 < nvec; v0 += 64)
+          __builtin_amdgcn_global_load_lds(
+              (const __attribute__((address_space(1))) void*)(src + min(v0 + lane, nvec - 1)),
+              (__attribute__((address_space(3))) void*)(b + 16u * (uint32_t)v0), 16, 0, 2);
+      } else {
+        for (int v0 = 0; v0 < nvec; v0 += 64)
+          __builtin_amdgcn_global_load_lds(
+              (const __attribute__((address_space(1))) void*)(src + min(v0 + lane, nvec - 1)),
+              (__attribute__((address_space(3))) void*)(b + 16u * (uint32_t)v0), 16, 0, 0);
+      }
+      return (nvec + 63) / 64;
     }
+    for (int v = lane; v < nvec; v += 64) *reinterpret_cast<uint4*>(b + 16u * v) = load16_guarded(P.log, a0 + 16ll * v, log_len);
+    return 0;
+  };
+  if (DB) stage_round(0, buf0);
+#pragma unroll
+  for (int r = 0; r < kRounds; r++) {
+    dr[r] = ~0u;
+    uint8_t* buf = DB ? buf0 + (r & 1) * P.uni_wbytes : buf0;
+    const uint64_t i0 = blk0 + (uint64_t)(r * W + wave) * 64;
+    if (DB) {
+      // the next round's records in flight while this one is hashed; then wait for this one's only
+      const int nxt = r + 1 < kRounds ? stage_round(r + 1, buf0 + ((r + 1) & 1) * P.uni_wbytes) : 0;
+      wait_vmcnt_le(nxt);
+    } else {
+      stage_round(r, buf);
+      __builtin_amdgcn_s_waitcnt(0);  // this wave's LDS-DMA has landed
+    }
+    if (i0 >= P.uni_n) continue;  // (wave-uniform)
+    const int64_t base = P.fr_entry + (int64_t)i0 * R;
+    const int64_t a0 = base & ~15ll;
+    const int nrec = (int)min((uint64_t)64, P.uni_n - i0);
     __builtin_amdgcn_wave_barrier();
     if (lane < nrec) {
       const int64_t p = base + (int64_t)lane * R;
@@ -1456,9 +1517,22 @@ __global__ __launch_bounds__(kPlaceLdsBlock) void k_place_lds(BuildParams P) {
   for (int64_t t = x + tid; t < hi; t += kPlaceLdsBlock) {
     const int32_t v = pos_j[t - x];
     const uint64_t slot = t < bsize ? start + (uint64_t)t : wrap_slot(start + (uint64_t)t, P.cap);
+    uint64_t hh = 0, aa = 0;
     if (v >= 0) {
       const Entry en = buf[v & 1023];
-      put_slot(P, slot, en.hash, en.addr & ~kDelBit);
+      hh = en.hash;
+      aa = en.addr & ~kDelBit;
+    }
+    if (P.slot_size == 16 && !P.sharded && P.uni_nt) {  // the table is written once: non-temporal stores
+      typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+      u32x4 w;
+      w.x = (uint32_t)hh;
+      w.y = (uint32_t)(hh >> 32);
+      w.z = (uint32_t)aa;
+      w.w = (uint32_t)(aa >> 32);
+      __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(P.out + kIndexHeaderSize + slot * 16ull));
+    } else if (v >= 0) {
+      put_slot(P, slot, hh, aa);
     } else {
       write_slot(P, slot, 0, 0);
     }
@@ -1546,17 +1620,26 @@ void launch_frame_uniform(const BuildParams& P, hipStream_t s, StageTimer* tm) {
   if (P.uni_n == 0) return;
   BuildParams Q = P;
   int W = frame_uniform_waves(P.uni_rec);
-  if (const char* e = getenv("SPARKEY_FRAME_W")) W = atoi(e) == 8 ? 8 : W;  // (measurements)
+  // default: 4 waves per workgroup, double-buffered (two workgroups per CU, each wave's next DMA in
+  // flight while it hashes); SPARKEY_FRAME_W=16 / 8: single-buffered, one workgroup per CU
+  bool db = true;
+  if (const char* e = getenv("SPARKEY_FRAME_W")) {  // (measurements)
+    W = atoi(e) == 8 ? 8 : 16;
+    db = false;
+  }
+  if (db) W = 4;
   Q.uni_wbytes = (uint32_t)((64 * P.uni_rec + 32 + 1023) & ~1023ll);
+  Q.uni_nt = getenv("SPARKEY_FRAME_NO_NT") ? 0u : 1u;  // (the log is read once: measured 10% faster)
   const uint64_t per = kPartTile;  // records per workgroup
   const uint64_t nblk = (P.uni_n + per - 1) / per;
   // the wave buffers, then the tile regrouped by digit in the same space (entries, digits, run
   // starts), and hist + rbase after either
-  const size_t body = std::max<size_t>((size_t)W * Q.uni_wbytes, (size_t)kPartTile * (sizeof(Entry) + 1) + 1024);
+  const size_t body = std::max<size_t>((size_t)W * Q.uni_wbytes * (db ? 2 : 1), (size_t)kPartTile * (sizeof(Entry) + 1) + 1024);
   const size_t lds = body + 2048;
   Q.uni_hist_off = (uint32_t)body;
-  if (W == 16) hipLaunchKernelGGL(k_frame_uniform<16>, dim3((unsigned)nblk), dim3(64 * 16), lds, s, Q);
-  else hipLaunchKernelGGL(k_frame_uniform<8>, dim3((unsigned)nblk), dim3(64 * 8), lds, s, Q);
+  if (db) hipLaunchKernelGGL((k_frame_uniform<4, true>), dim3((unsigned)nblk), dim3(64 * 4), lds, s, Q);
+  else if (W == 16) hipLaunchKernelGGL((k_frame_uniform<16, false>), dim3((unsigned)nblk), dim3(64 * 16), lds, s, Q);
+  else hipLaunchKernelGGL((k_frame_uniform<8, false>), dim3((unsigned)nblk), dim3(64 * 8), lds, s, Q);
   tm->mark("frame", s);
 }
 

@@ -521,6 +521,7 @@ static int setup_params(const LogHdr& lh, const IndexParams& ip, const sparkey_b
     P.fr_nchunks = any ? (uint64_t)((frame_end + C - 1) / C) - P.fr_k0 : 0;
   }
   P.emit_extra = lh.max_key_len + 32 <= kEmitExtra ? (int32_t)((lh.max_key_len + 32 + 15) & ~15LL) : 32;
+  P.uni_nt = getenv("SPARKEY_FRAME_NO_NT") ? 0u : 1u;  // framing stages the log non-temporally (read once)
   P.hash_size = ip.hash_size;
   P.addr_size = ip.addr_size;
   P.slot_size = ip.slot_size;
