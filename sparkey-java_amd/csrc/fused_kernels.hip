@@ -1367,6 +1367,18 @@ __global__ __launch_bounds__(kPlaceLdsBlock) void k_place_lds(BuildParams P) {
   const long long t_begin_ = t_prev_;
   // Every value the block reads besides its entries, in one round trip (block-uniform: scalar loads
   // issued together) rather than one latency per phase.
+  constexpr int kPer = kPlaceLdsMax / kPlaceLdsBlock;
+  static_assert(kPlaceLdsMax % kPlaceLdsBlock == 0, "entries per thread");
+  static_assert(kBucket == 2 * kPlaceLdsBlock, "place_scan512: two slots per thread");
+  Entry mine[kPer];
+  // fixed bucket regions: the bucket's region is known without its count, so the entry loads go out
+  // together with the head's (one round trip, not two; slots past the count are never used)
+  const bool fixed = P.p2_fixed != 0;
+  if (fixed) {
+    const uint64_t e0 = (uint64_t)blockIdx.x * kPlaceLdsMax;
+#pragma unroll
+    for (int k = 0; k < kPer; k++) mine[k] = P.ent2[e0 + threadIdx.x + k * kPlaceLdsBlock];
+  }
   const Status* st = P.st;
   const unsigned ovf = st->overflow | st->p2_overflow, full = st->full;
   const unsigned long long nrec = st->n_records, ndel = st->n_deletes, npairs0 = st->n_pairs;
@@ -1390,15 +1402,13 @@ __global__ __launch_bounds__(kPlaceLdsBlock) void k_place_lds(BuildParams P) {
     return;
   }
   // the entries' loads are in flight while the counts are cleared
-  constexpr int kPer = kPlaceLdsMax / kPlaceLdsBlock;
-  static_assert(kPlaceLdsMax % kPlaceLdsBlock == 0, "entries per thread");
-  static_assert(kBucket == 2 * kPlaceLdsBlock, "place_scan512: two slots per thread");
-  Entry mine[kPer];
   uint32_t want[kPer], cur[kPer], rank[kPer];
+  if (!fixed) {
 #pragma unroll
-  for (int k = 0; k < kPer; k++) {
-    const uint32_t i = tid + k * kPlaceLdsBlock;
-    if (i < n) mine[k] = P.ent2[eoff + i];
+    for (int k = 0; k < kPer; k++) {
+      const uint32_t i = tid + k * kPlaceLdsBlock;
+      if (i < n) mine[k] = P.ent2[eoff + i];
+    }
   }
   PLACE_MARK(0);
   for (int t = tid; t < kBucket; t += kPlaceLdsBlock) cnt[t] = 0;

@@ -76,11 +76,12 @@ void launch_snappy_dir(const SnappyParams& S, hipStream_t s);
 // the parallel directory (SNAPPY): window screen, anchors, links (count, then emit)
 constexpr int kSdirCand = 32;
 inline size_t sdir_screen_lds(int64_t H) { return (size_t)((H + 15 + 384 + 15) & ~15LL) + 16; }  // staged window
-void launch_sdir_screen(const SnappyParams& S, hipStream_t s, int64_t A, int64_t H, uint64_t nwin, int64_t* cand,
-                        int32_t* ncand);
-void launch_sdir_anchor(const SnappyParams& S, hipStream_t s, int64_t A, int64_t H, uint64_t nwin, const int64_t* cand,
-                        const int32_t* ncand, int64_t* anchor);
-void launch_sdir_link(const SnappyParams& S, hipStream_t s, const int64_t* ends, uint64_t nlinks, int emit,
+// (codec 0 SNAPPY, 1 ZSTD)
+void launch_sdir_screen(const SnappyParams& S, hipStream_t s, int codec, int64_t A, int64_t H, uint64_t nwin,
+                        int64_t* cand, int32_t* ncand);
+void launch_sdir_anchor(const SnappyParams& S, hipStream_t s, int codec, int64_t A, int64_t H, uint64_t nwin,
+                        const int64_t* cand, const int32_t* ncand, int64_t* anchor);
+void launch_sdir_link(const SnappyParams& S, hipStream_t s, int codec, const int64_t* ends, uint64_t nlinks, int emit,
                       uint64_t* cnt, uint64_t* usum, const uint64_t* boff, const uint64_t* uoff, int32_t* fail);
 // ZSTD logs (zstd_kernels.hip): the same directory with sizes from the frame headers, and the decode
 void launch_zstd_dir(const SnappyParams& S, hipStream_t s);

@@ -635,14 +635,66 @@ __device__ __forceinline__ bool snappy_head_plausible(const SnappyParams& S, con
   return true;
 }
 
-// a start that passes the screen, and whose next block (if any) passes it too
+// One hop of a ZSTD log's chain with k_zstd_dir's checks (its error codes: 1 framing, 2 larger than
+// the reader's buffers, 4 no content size): VLQ(compressedSize), then the frame header's magic,
+// descriptor, [window], [dictionary id] and Frame_Content_Size (RFC 8878 §3.1.1.1).
 template <class Win>
+__device__ __forceinline__ DirHop zstd_hop(const SnappyParams& S, int64_t p, const Win& win) {
+  DirHop h{0, 0, 0, 0, 0};
+  const Window w0 = win(p), w1 = win(p + 16);
+  auto at = [&](int j) -> uint32_t { return j < 16 ? w0.at(j) : w1.at(j - 16); };
+  const int avail = (int)min<int64_t>(32, S.data_end - p);
+  uint32_t v = 0;
+  int j = 0;
+  int32_t clen = -1;
+  for (int i = 0; i < 5; i++) {
+    if (j >= avail) { h.err = 1; return h; }
+    const uint32_t b = at(j++);
+    if (b < 0x80u) { clen = (int32_t)(v | (b << (7 * i))); break; }
+    v |= (b & 0x7fu) << (7 * i);
+  }
+  const int64_t q = p + j;
+  if (clen < 0 || q + clen > S.data_end || clen < 6) { h.err = 1; return h; }
+  const uint32_t magic = at(j) | (at(j + 1) << 8) | (at(j + 2) << 16) | (at(j + 3) << 24);
+  if (magic != 0xFD2FB528u) { h.err = 1; return h; }
+  const uint32_t fhd = at(j + 4);
+  const uint32_t fcs_flag = fhd >> 6, single = (fhd >> 5) & 1, did_flag = fhd & 3;
+  const uint32_t did_bytes = did_flag == 0 ? 0 : did_flag == 1 ? 1 : did_flag == 2 ? 2 : 4;
+  const uint32_t fcs_bytes = fcs_flag == 0 ? (single ? 1u : 0u) : fcs_flag == 1 ? 2u : fcs_flag == 2 ? 4u : 8u;
+  const int f = j + 5 + (single ? 0 : 1) + (int)did_bytes;
+  if (fcs_bytes == 0) { h.err = 4; return h; }
+  if ((int64_t)p + f + fcs_bytes > q + clen) { h.err = 1; return h; }
+  uint64_t fcs = 0;
+  for (uint32_t i = 0; i < fcs_bytes; i++) fcs |= (uint64_t)at(f + (int)i) << (8 * i);
+  if (fcs_bytes == 2) fcs += 256;
+  const int64_t mb = S.max_block;
+  const int64_t bound = mb + (mb >> 8) + (mb < (128 << 10) ? (((128 << 10) - mb) >> 11) : 0);
+  if ((int64_t)fcs > S.max_block || (int64_t)clen > bound) { h.err = 2; return h; }
+  h.next = q + clen;
+  h.data = q;
+  h.clen = clen;
+  h.ulen = (int32_t)fcs;
+  return h;
+}
+
+// the codec's hop (kCodec 0 SNAPPY, 1 ZSTD) and its screen
+template <int kCodec, class Win>
+__device__ __forceinline__ DirHop codec_hop(const SnappyParams& S, int64_t p, const Win& win) {
+  return kCodec == 1 ? zstd_hop(S, p, win) : dir_hop(S, p, win);
+}
+template <int kCodec, class Win>
+__device__ __forceinline__ bool codec_plausible(const SnappyParams& S, const DirHop& h, const Win& win) {
+  return kCodec == 1 ? h.err == 0 : snappy_head_plausible(S, h, win);  // (the ZSTD magic is the screen)
+}
+
+// a start that passes the screen, and whose next block (if any) passes it too
+template <int kCodec, class Win>
 __device__ __forceinline__ bool block_start_plausible(const SnappyParams& S, int64_t p, const Win& win, DirHop& h) {
-  h = dir_hop(S, p, win);
-  if (!snappy_head_plausible(S, h, win)) return false;
+  h = codec_hop<kCodec>(S, p, win);
+  if (!codec_plausible<kCodec>(S, h, win)) return false;
   if (h.next >= S.data_end) return true;
-  const DirHop h2 = dir_hop(S, h.next, win);
-  return snappy_head_plausible(S, h2, win);
+  const DirHop h2 = codec_hop<kCodec>(S, h.next, win);
+  return codec_plausible<kCodec>(S, h2, win);
 }
 
 struct GlobalWin {
@@ -679,6 +731,7 @@ constexpr int kDirCand = kSdirCand;  // candidate starts per window
 // Window k = [84 + k A, 84 + k A + H), H = the longest hop (so it holds a true start unless it runs
 // past dataEnd): its plausible starts whose next block is plausible too, into cand[k].  The window's
 // bytes (and 384 past it, for the screen's look-ahead) are staged in LDS first.
+template <int kCodec>
 __global__ __launch_bounds__(1024) void k_sdir_screen(SnappyParams S, int64_t A, int64_t H, int64_t* cand,
                                                      int32_t* ncand) {
   extern __shared__ __attribute__((aligned(16))) uint32_t stage[];
@@ -695,7 +748,7 @@ __global__ __launch_bounds__(1024) void k_sdir_screen(SnappyParams S, int64_t A,
   const StagedWin win{&S, stage, base, nst};
   for (int64_t p = w0 + threadIdx.x; p < w1; p += blockDim.x) {
     DirHop h;
-    if (!block_start_plausible(S, p, win, h)) continue;
+    if (!block_start_plausible<kCodec>(S, p, win, h)) continue;
     const int32_t i = atomicAdd(&n, 1);
     if (i < kDirCand) cand[k * kDirCand + i] = p;
   }
@@ -706,6 +759,7 @@ __global__ __launch_bounds__(1024) void k_sdir_screen(SnappyParams S, int64_t A,
 // Window k's anchor: the first chain position at or past its end that every candidate chain reaching
 // that far (plausible at every hop) agrees on -- the window's true start is a candidate when the
 // stream is well formed -- else -1.
+template <int kCodec>
 __global__ __launch_bounds__(64) void k_sdir_anchor(SnappyParams S, int64_t A, int64_t H, const int64_t* cand,
                                                     const int32_t* ncand, int64_t* anchor) {
   const uint64_t k = blockIdx.x;
@@ -718,7 +772,7 @@ __global__ __launch_bounds__(64) void k_sdir_anchor(SnappyParams S, int64_t A, i
     int64_t p = cand[k * kDirCand + lane];
     while (p < wend && p < S.data_end) {
       DirHop h;
-      if (!block_start_plausible(S, p, win, h)) { p = -1; break; }
+      if (!block_start_plausible<kCodec>(S, p, win, h)) { p = -1; break; }
       p = h.next;
     }
     x = p;
@@ -733,6 +787,7 @@ __global__ __launch_bounds__(64) void k_sdir_anchor(SnappyParams S, int64_t A, i
 // Link i: the chain from ends[i] to ends[i + 1], every hop with k_snappy_dir's checks.  emit = 0:
 // its blocks and decompressed bytes (cnt, usum); emit = 1: its blocks into S.blocks from boff[i],
 // virtual offsets from 84 + uoff[i].  fail[0] |= 1 when a link does not land on its end.
+template <int kCodec>
 __global__ __launch_bounds__(64) void k_sdir_link(SnappyParams S, const int64_t* ends, uint64_t nlinks, int emit,
                                                   uint64_t* cnt, uint64_t* usum, const uint64_t* boff,
                                                   const uint64_t* uoff, int32_t* fail) {
@@ -745,7 +800,7 @@ __global__ __launch_bounds__(64) void k_sdir_link(SnappyParams S, const int64_t*
   const uint64_t v0 = emit ? uoff[i] : 0;
   const GlobalWin win{&S};
   while (p < e) {
-    const DirHop h = dir_hop(S, p, win);
+    const DirHop h = codec_hop<kCodec>(S, p, win);
     if (h.err) {
       atomicOr(fail, 1 << h.err);
       return;
@@ -774,24 +829,32 @@ __global__ __launch_bounds__(64) void k_sdir_link(SnappyParams S, const int64_t*
   }
 }
 
-void launch_sdir_screen(const SnappyParams& S, hipStream_t s, int64_t A, int64_t H, uint64_t nwin, int64_t* cand,
-                        int32_t* ncand) {
+void launch_sdir_screen(const SnappyParams& S, hipStream_t s, int codec, int64_t A, int64_t H, uint64_t nwin,
+                        int64_t* cand, int32_t* ncand) {
   const size_t lds = sdir_screen_lds(H);
   if (!nwin) return;
-  (void)hipFuncSetAttribute((const void*)k_sdir_screen, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL(k_sdir_screen, dim3((unsigned)nwin), 1024, lds, s, S, A, H, cand, ncand);
+  if (codec == 1) {
+    (void)hipFuncSetAttribute((const void*)k_sdir_screen<1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(k_sdir_screen<1>, dim3((unsigned)nwin), 1024, lds, s, S, A, H, cand, ncand);
+  } else {
+    (void)hipFuncSetAttribute((const void*)k_sdir_screen<0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(k_sdir_screen<0>, dim3((unsigned)nwin), 1024, lds, s, S, A, H, cand, ncand);
+  }
 }
 
-void launch_sdir_anchor(const SnappyParams& S, hipStream_t s, int64_t A, int64_t H, uint64_t nwin, const int64_t* cand,
-                        const int32_t* ncand, int64_t* anchor) {
-  if (nwin) hipLaunchKernelGGL(k_sdir_anchor, dim3((unsigned)nwin), 64, 0, s, S, A, H, cand, ncand, anchor);
+void launch_sdir_anchor(const SnappyParams& S, hipStream_t s, int codec, int64_t A, int64_t H, uint64_t nwin,
+                        const int64_t* cand, const int32_t* ncand, int64_t* anchor) {
+  if (!nwin) return;
+  if (codec == 1) hipLaunchKernelGGL(k_sdir_anchor<1>, dim3((unsigned)nwin), 64, 0, s, S, A, H, cand, ncand, anchor);
+  else hipLaunchKernelGGL(k_sdir_anchor<0>, dim3((unsigned)nwin), 64, 0, s, S, A, H, cand, ncand, anchor);
 }
 
-void launch_sdir_link(const SnappyParams& S, hipStream_t s, const int64_t* ends, uint64_t nlinks, int emit,
+void launch_sdir_link(const SnappyParams& S, hipStream_t s, int codec, const int64_t* ends, uint64_t nlinks, int emit,
                       uint64_t* cnt, uint64_t* usum, const uint64_t* boff, const uint64_t* uoff, int32_t* fail) {
-  if (nlinks)
-    hipLaunchKernelGGL(k_sdir_link, dim3((unsigned)((nlinks + 63) / 64)), 64, 0, s, S, ends, nlinks, emit, cnt, usum,
-                       boff, uoff, fail);
+  if (!nlinks) return;
+  const dim3 g((unsigned)((nlinks + 63) / 64));
+  if (codec == 1) hipLaunchKernelGGL(k_sdir_link<1>, g, 64, 0, s, S, ends, nlinks, emit, cnt, usum, boff, uoff, fail);
+  else hipLaunchKernelGGL(k_sdir_link<0>, g, 64, 0, s, S, ends, nlinks, emit, cnt, usum, boff, uoff, fail);
 }
 
 void launch_snappy_dir(const SnappyParams& S, hipStream_t s) { hipLaunchKernelGGL(k_snappy_dir, 1, 64, 0, s, S); }

@@ -754,12 +754,15 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
 // where the candidates agree), then every link of the chain 84 -> anchors -> dataEnd walked from its
 // start at once with k_snappy_dir's checks; a link that does not land on its end, or any check that
 // fails, leaves the directory to the serial chain (*ok = false), which reports errors exactly.
-static int snappy_par_dir(sparkey_plan* pl, SnappyParams& S, hipStream_t s, SnappyDirResult* dir, bool* ok, char* err,
-                          size_t err_len) {
+static int snappy_par_dir(sparkey_plan* pl, SnappyParams& S, hipStream_t s, int codec, SnappyDirResult* dir, bool* ok,
+                          char* err, size_t err_len) {
   *ok = false;
   const int64_t body = S.data_end - kLogHeaderSize;
   if (body <= 0 || S.max_block <= 0) return SPARKEY_OK;
-  const int64_t H = 32 + S.max_block + S.max_block / 6 + 5;  // the longest hop: VLQ + maxCompressedLength
+  // the longest hop: VLQ + the reader's compressed buffer (Snappy.maxCompressedLength, ZSTD_compressBound)
+  const int64_t mb = S.max_block;
+  const int64_t H = 5 + (codec == 1 ? mb + (mb >> 8) + (mb < (128 << 10) ? (((128 << 10) - mb) >> 11) : 0)
+                                    : 32 + mb + mb / 6);
   if (sdir_screen_lds(H) > 150 * 1024) return SPARKEY_OK;   // (blocks over ~128 KiB: the serial chain)
   int64_t A = std::max<int64_t>(32 * H, body / (1 << 20) + 1);  // (screen 1/32 of the log; links of ~32 blocks)
   if (const char* v = getenv("SPARKEY_SNAPPY_DIR_A")) A = std::max<int64_t>(H, atoll(v));  // (tests, tuning)
@@ -779,8 +782,8 @@ static int snappy_par_dir(sparkey_plan* pl, SnappyParams& S, hipStream_t s, Snap
   uint64_t* uoff = (uint64_t*)carve(maxl * 8);
   int32_t* fail = (int32_t*)carve(16);
   HIP_TRY(hipMemsetAsync(fail, 0, 4, s));
-  launch_sdir_screen(S, s, A, H, nwin, cand, ncand);
-  launch_sdir_anchor(S, s, A, H, nwin, cand, ncand, anchor);
+  launch_sdir_screen(S, s, codec, A, H, nwin, cand, ncand);
+  launch_sdir_anchor(S, s, codec, A, H, nwin, cand, ncand, anchor);
   HIP_TRY(hipGetLastError());
   std::vector<int64_t> anc(nwin);
   if (nwin) HIP_TRY(hipMemcpyAsync(anc.data(), anchor, nwin * 8, hipMemcpyDeviceToHost, s));
@@ -792,7 +795,7 @@ static int snappy_par_dir(sparkey_plan* pl, SnappyParams& S, hipStream_t s, Snap
   e.push_back(S.data_end);
   const uint64_t nl = e.size() - 1;
   HIP_TRY(hipMemcpyAsync(ends, e.data(), e.size() * 8, hipMemcpyHostToDevice, s));
-  launch_sdir_link(S, s, ends, nl, 0, cnt, usum, nullptr, nullptr, fail);
+  launch_sdir_link(S, s, codec, ends, nl, 0, cnt, usum, nullptr, nullptr, fail);
   HIP_TRY(hipGetLastError());
   std::vector<uint64_t> hc(nl), hu(nl);
   int32_t hf = 0;
@@ -816,13 +819,13 @@ static int snappy_par_dir(sparkey_plan* pl, SnappyParams& S, hipStream_t s, Snap
   S.walk = pl->sn_walk;
   HIP_TRY(hipMemcpyAsync(boff, bo.data(), nl * 8, hipMemcpyHostToDevice, s));
   HIP_TRY(hipMemcpyAsync(uoff, uo.data(), nl * 8, hipMemcpyHostToDevice, s));
-  launch_sdir_link(S, s, ends, nl, 1, cnt, usum, boff, uoff, fail);
+  launch_sdir_link(S, s, codec, ends, nl, 1, cnt, usum, boff, uoff, fail);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpyAsync(&hf, fail, 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
   if (hf) return SPARKEY_OK;
   if (getenv("SPARKEY_SNAPPY_DIR_DEBUG"))
-    fprintf(stderr, "[snappy dir] parallel: %llu blocks, %llu windows, %llu links\n", (unsigned long long)nb,
+    fprintf(stderr, "[%s dir] parallel: %llu blocks, %llu windows, %llu links\n", codec ? "zstd" : "snappy", (unsigned long long)nb,
             (unsigned long long)nwin, (unsigned long long)nl);
   memset(dir, 0, sizeof(*dir));
   dir->nblk = nb;
@@ -881,7 +884,9 @@ static int plan_build_snappy(sparkey_plan* pl, const LogHdr& lh, const uint8_t* 
   const char* codec = zstd ? "zstd" : "snappy";
   const int64_t mb = lh.compression_block_size;
   if (zstd) {  // LDS: the decoded block, then the whole frame (k_zstd_decode)
-    S.lds_bytes = zstd_lds_bytes(mb);
+    // decoded straight into the virtual log (LDS for the entropy tables only: many waves per CU)
+    // measured 3x faster than the block and frame in LDS (one wave per CU); SPARKEY_ZSTD_LDS=1: that
+    S.lds_bytes = getenv("SPARKEY_ZSTD_LDS") ? zstd_lds_bytes(mb) : 0u;
   } else {  // LDS: the decoded block, then an 8 KiB window over its stream (k_snappy_lds)
     const int64_t lds = ((mb + 15) & ~15LL) + 16 + 8192 + 16;
     S.lds_bytes = lds <= 160 * 1024 ? (uint32_t)lds : 0u;
@@ -964,9 +969,9 @@ static int plan_build_snappy(sparkey_plan* pl, const LogHdr& lh, const uint8_t* 
   const uint64_t ps = (uint64_t)std::max<int64_t>(0, lh.put_size), ds = (uint64_t)std::max<int64_t>(0, lh.delete_size);
   const uint64_t hdr_total = ps + ds < ps ? UINT64_MAX : ps + ds;
   const int64_t vcap0 = hdr_total <= 22 * body + 4096 ? (int64_t)hdr_total : 0;
-  bool par = false;  // SNAPPY: the directory in parallel, then every block decoded in one launch
-  if (!zstd && !getenv("SPARKEY_SNAPPY_SERIAL_DIR")) {
-    rc = snappy_par_dir(pl, S, s, &dir, &par, err, err_len);
+  bool par = false;  // the directory in parallel, then every block decoded in one launch
+  if (!getenv("SPARKEY_SNAPPY_SERIAL_DIR")) {
+    rc = snappy_par_dir(pl, S, s, zstd ? 1 : 0, &dir, &par, err, err_len);
     if (rc) return rc;
   }
   if (par) {
