@@ -730,6 +730,8 @@ __global__ void __launch_bounds__(64) k_zstd_dir(SnappyParams S) {
 
 // One wave per block: its frame into the virtual log at voff, decoded in LDS when the block fits
 // (lds_bytes > 0), then stored 16 bytes a lane; else straight into the virtual log.
+// (one instantiation per mode: the global-memory decode alone needs fewer registers, so more waves)
+template <bool kInLds>
 __global__ void __launch_bounds__(64) k_zstd_decode(SnappyParams S) {
   __shared__ ZWork W;
   extern __shared__ __attribute__((aligned(16))) uint8_t dyn[];
@@ -738,7 +740,7 @@ __global__ void __launch_bounds__(64) k_zstd_decode(SnappyParams S) {
   const int lane = (int)threadIdx.x;
   ZIn in{S.log + B.data, B.clen};
   int64_t got;
-  if (S.lds_bytes) {
+  if (kInLds) {
     // the block at the alignment of its place in the virtual log (16-byte stores out), then its
     // frame's bytes (every bit read of the entropy decoding stays in LDS)
     const int64_t oa = B.voff & ~15LL;
@@ -795,11 +797,13 @@ uint32_t zstd_lds_bytes(int64_t max_block) {
 hipError_t launch_zstd_decode(const SnappyParams& S, hipStream_t s) {
   if (S.nblk == 0) return hipSuccess;
   if (S.lds_bytes) {
-    hipError_t e = hipFuncSetAttribute((const void*)k_zstd_decode, hipFuncAttributeMaxDynamicSharedMemorySize,
+    hipError_t e = hipFuncSetAttribute((const void*)k_zstd_decode<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)S.lds_bytes);
     if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_zstd_decode<true>, dim3((uint32_t)S.nblk), 64, S.lds_bytes, s, S);
+  } else {
+    hipLaunchKernelGGL(k_zstd_decode<false>, dim3((uint32_t)S.nblk), 64, 0, s, S);
   }
-  hipLaunchKernelGGL(k_zstd_decode, dim3((uint32_t)S.nblk), 64, S.lds_bytes, s, S);
   return hipGetLastError();
 }
 
