@@ -365,7 +365,9 @@ def single_gpu(args, dev):
                    "parallelism": "single"},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS,
-                     "traffic": pmc_traffic(args.workload, {("frame", 2): "frame_uniform",
+                     # (counters are keyed by workload and size: "c3" is the 10M run, "c3_100000000" 100M)
+                     "traffic": pmc_traffic(args.workload if n == 10_000_000 else f"{args.workload}_{n}",
+                                            {("frame", 2): "frame_uniform",
                                                             ("partition", 1): "partition_regions"}.get(
                          (dom, stats.framing_path if dom == "frame" else passes), dom)),
                      "algorithmic_bytes_per_launch": dom_bytes, "avg_launch_ms": stage_ms.get(dom) if dom else None},

@@ -56,7 +56,8 @@ def main(src, dst, workload=None):
             rec[c] = sum(vals) / len(vals)
         out["kernels"][k] = rec
     # stage name (bench.py) -> kernels in that stage
-    stage_kernels = {"frame": ["k_frame"], "frame_uniform": ["k_frame_uniform"], "partition": ["k_part1_hist", "k_part1_scatter", "k_part2", "k_scan_tiles"],
+    stage_kernels = {"frame": ["k_frame", "k_frame_uniform", "k_frame2", "k_frame3"], "frame_uniform": ["k_frame_uniform"],
+                     "partition": ["k_part1_hist", "k_part1_scatter", "k_part2", "k_part2s", "k_scan_tiles"],
                      "partition_regions": ["k_part2"],
                      "place": ["k_place_lds", "k_place"], "stats": ["k_stats", "k_stats_final"],
                      "summary": ["k_summary", "k_carry"], "verify": ["k_verify_pairs"]}
