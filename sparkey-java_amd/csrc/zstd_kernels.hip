@@ -64,6 +64,11 @@ struct ZWork {
   uint16_t next[64];
   uint8_t w[256];           // Huffman weights
   uint32_t rank[kHufMaxBits + 2];
+  // literal / match length codes: baseline | extra bits << 24 (the __constant__ tables, copied here:
+  // a constant-memory load indexed by a decoded symbol is a vector memory load, which waits for the
+  // wave's outstanding global stores and sat on every sequence's dependent path)
+  uint32_t llc[36];
+  uint32_t mlc[53];
 };
 
 enum : int32_t { kZOk = 0, kZCorrupt = -1, kZUnsupported = -2 };
@@ -584,8 +589,9 @@ __device__ int64_t zstd_decode(ZWork& W, const ZIn& in, uint8_t* out, uint32_t c
             const uint32_t ofc = eo.sym, mlc = em.sym, llc = el.sym;
             if (ofc > 31 || mlc > 52 || llc > 35) return kZCorrupt;
             uint32_t ofv = (1u << ofc) + br.read((int)ofc);
-            const uint32_t ml = kMLBase[mlc] + br.read(kMLBits[mlc]);
-            const uint32_t ll = kLLBase[llc] + br.read(kLLBits[llc]);
+            const uint32_t mlx = W.mlc[mlc], llx = W.llc[llc];
+            const uint32_t ml = (mlx & 0xFFFFFFu) + br.read((int)(mlx >> 24));
+            const uint32_t ll = (llx & 0xFFFFFFu) + br.read((int)(llx >> 24));
             uint32_t off;
             if (ofv > 3) {
               off = ofv - 3;
@@ -734,6 +740,9 @@ __global__ void __launch_bounds__(64) k_zstd_dir(SnappyParams S) {
 template <bool kInLds>
 __global__ void __launch_bounds__(64) k_zstd_decode(SnappyParams S) {
   __shared__ ZWork W;
+  if (threadIdx.x < 36) W.llc[threadIdx.x] = kLLBase[threadIdx.x] | ((uint32_t)kLLBits[threadIdx.x] << 24);
+  if (threadIdx.x < 53) W.mlc[threadIdx.x] = kMLBase[threadIdx.x] | ((uint32_t)kMLBits[threadIdx.x] << 24);
+  __builtin_amdgcn_wave_barrier();
   extern __shared__ __attribute__((aligned(16))) uint8_t dyn[];
   const uint64_t b = S.blk_base + blockIdx.x;
   const SnappyBlock B = S.blocks[b];
