@@ -387,6 +387,24 @@ __device__ __forceinline__ uint8_t out_at(const uint8_t* p) {
 // a later step only reads below what earlier steps wrote, see the file comment).
 template <bool kLds>
 __device__ __forceinline__ void wave_copy(uint8_t* dst, const uint8_t* src, uint32_t n, int lane, bool src_out) {
+  if (!kLds && !src_out) {  // from the frame (never written here): four steps' loads, then one wait
+    for (uint32_t i0 = 0; i0 < n; i0 += 256) {
+      uint8_t v[4];
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const uint32_t k = i0 + 64u * q + (uint32_t)lane;
+        v[q] = k < n ? src[k] : (uint8_t)0;
+      }
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const uint32_t k = i0 + 64u * q + (uint32_t)lane;
+        if (k < n) dst[k] = v[q];
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
+    return;
+  }
   for (uint32_t i = 0; i < n; i += 64) {
     const uint32_t k = i + (uint32_t)lane;
     uint8_t v = 0;
