@@ -284,7 +284,7 @@ def single_gpu(args, dev):
 
     # the same workload through the general speculative framing (k_frame), when the log's records are
     # uniform and the default build took k_frame_uniform
-    general = None
+    general = general_spi = None
     if stats.framing_path == 2:
         os.environ["SPARKEY_NO_UNIFORM"] = "1"
         try:
@@ -301,6 +301,7 @@ def single_gpu(args, dev):
             g_el = time.perf_counter() - t_g
             plan.set_profiling(False)
             assert g_stats.framing_path in (0, 3, 4), g_stats.as_dict()
+            general_spi = d_out.cpu().numpy().tobytes()  # (compared with the headline build below)
             g_stage = {k: v / g_steps for k, v in g_acc.items()}
             general = {"ms_per_step": g_el * 1000.0 / g_steps, "keys_per_s": n * g_steps / g_el,
                        "stage_ms": g_stage,
@@ -357,6 +358,16 @@ def single_gpu(args, dev):
     finally:
         shutil.rmtree(tmpdir, ignore_errors=True)
     plan.close()
+    parity = None
+    if args.workload == "c2" and not args.no_parity:
+        del d_log, d_out
+        torch.cuda.empty_cache()
+        parity = parity_checks(args, dev, headline_spi, general_spi)
+        if cpu is not None:
+            parity["c2_device_bit_identical_to_oracle"] = cpu["bit_identical_to_gpu"]
+            parity["c2_file_to_file_bit_identical_to_oracle"] = cpu["file_bit_identical_to_gpu"]
+    if general is not None:
+        general["bit_identical_to_headline"] = general_spi == headline_spi
     return {
         "value": n * args.steps / elapsed, "ms_per_step": ms_per_step,
         "config": {"workload": wl["name"],
@@ -383,21 +394,76 @@ def single_gpu(args, dev):
         "host_to_host_keys_per_s": h2h,
         "file_to_file_keys_per_s": file_rate,
         "cpu_baseline": cpu,
+        "parity": parity,
         "gen_s": gen_s,
         "version": sparkey.version(),
     }
 
 
+def parity_checks(args, dev, headline_spi, general_spi):
+    """Outside every timed region (N = 1, default workload): the device paths the headline does not
+    take, each checked byte for byte -- the general framing of the C2 log against the headline build,
+    and the C3-shaped (k_frame3), C5 (SORTING), exact-path, SNAPPY and ZSTD builds against the oracle.
+    Returns {check: bool} plus the sizes used."""
+    import oracle
+    from sparkey import _native, synth
+    oracle.build()
+    out = {"c2_general_framing_equals_headline": None if general_spi is None else general_spi == headline_spi}
+    n3 = args.parity_c3_entries
+
+    def gpu_vs_oracle(log_np, seed, method, want_path=None):
+        header = log_np[:84].tobytes()
+        opts = _native.make_opts(hash_size=0, hash_seed=seed, method=method, device=dev.index)
+        size = _native.index_size(header, opts)
+        d_log = torch.from_numpy(log_np).to(dev)
+        d_out = torch.empty(size, dtype=torch.uint8, device=dev)
+        plan = _native.Plan(dev.index, log_np.size, 0)
+        try:
+            st = plan.build(header, d_log.data_ptr(), log_np.size, d_out.data_ptr(), size, opts)
+            got = d_out.cpu().numpy().tobytes()
+        finally:
+            plan.close()
+        del d_log, d_out
+        want = oracle.build_index(log_np, seed, method=method)
+        return got == want and (want_path is None or st.framing_path == want_path), st
+
+    t0 = time.time()
+    c3 = synth.mixed_log(n3, 8, 64, 100, seed=args.seed + 2)
+    ok, st = gpu_vs_oracle(c3, HASH_SEED, _native.METHOD_IN_MEMORY)
+    out[f"c3_{n3}_in_memory"] = ok
+    out["c3_framing_path"] = st.framing_path
+    ok, _ = gpu_vs_oracle(c3, HASH_SEED, _native.METHOD_SORTING)
+    out[f"c5_{n3}_sorting"] = ok
+    del c3
+    churn = synth.churn_log(1_000_000, 800_000, 0.1, seed=args.seed + 4)
+    for name, method in (("in_memory", _native.METHOD_IN_MEMORY), ("sorting", _native.METHOD_SORTING)):
+        ok, st = gpu_vs_oracle(churn, HASH_SEED, method)
+        out[f"churn_1000000_exact_{name}"] = ok and st.placement_path == 2
+    del churn
+    for codec in ("snappy", "zstd"):
+        clog = synth.snappy_log(synth.fixed_log(1_000_000, 16, 100, seed=args.seed, file_id=0x5EED0000), 118, 65536,
+                                codec=codec)
+        ok, _ = gpu_vs_oracle(clog, HASH_SEED, _native.METHOD_IN_MEMORY)
+        out[f"{codec}_1000000"] = ok
+    out["seconds"] = round(time.time() - t0, 1)
+    return out
+
+
 def sharded(args, dev, world, rank):
+    """N > 1 (one process per GPU): ONE index over a log of N x 10M C2 records whose byte range is split
+    across the ranks.  Each rank runs sparkey_shard_build -- the C++ orchestrator behind the C-ABI
+    (csrc/shard_host.cpp) -- over its own RCCL communicator (unique id from rank 0 via
+    torch.distributed, whose gloo group only carries the control messages: id, barrier, timing max).
+    --orchestrator python runs sparkey/sharded.py's ShardedBuilder over torch.distributed instead."""
     import torch.distributed as dist
     import sparkey
     from sparkey import _native, synth
-    from sparkey.sharded import Comm, GpuShardSteps, ShardedBuilder, shard_layout
 
     n_total = args.entries * world
     churn = args.workload == "churn"  # overwrites + DELETEs: the sharded exact path (DESIGN.md §6.1)
     full_log = None
     t0 = time.time()
+    opts = _native.make_opts(hash_size=0, hash_seed=HASH_SEED, method=_native.METHOD_IN_MEMORY, device=dev.index)
     if churn:  # (every rank makes the whole log, then keeps its byte range)
         full_log = synth.churn_log(n_total, int(n_total * 0.8), 0.1, seed=args.seed + 4)
         file_len = int(full_log.size)
@@ -405,8 +471,7 @@ def sharded(args, dev, world, rank):
     else:
         file_len = 84 + n_total * 118
         header, _ = synth.fixed_log_range(n_total, 0, 84, 16, 100, seed=args.seed, file_id=0x5EED0000)
-    lay = shard_layout(header, file_len, world)
-    lo, hi = lay.buffer_range(rank)
+    lo, hi, out_off, out_len = _native.shard_geometry(header, file_len, opts, rank, world)
     if churn:
         part = full_log[lo:hi]
     else:
@@ -414,37 +479,54 @@ def sharded(args, dev, world, rank):
     gen_s = time.time() - t0
     buf = torch.from_numpy(part).to(dev)
     del part
-    opts = _native.make_opts(hash_size=0, hash_seed=HASH_SEED, method=_native.METHOD_IN_MEMORY, device=dev.index)
-    steps = GpuShardSteps(dev, _native.Plan(dev.index, hi - lo, 2 * args.entries))
-    builder = ShardedBuilder(steps, Comm(device=dev))
+    plan = _native.Plan(dev.index, hi - lo, 2 * args.entries)
+    stream = torch.cuda.Stream(dev)
+    phases = {}
+    if args.orchestrator == "python":
+        from sparkey.sharded import Comm, GpuShardSteps, ShardedBuilder
+        builder = ShardedBuilder(GpuShardSteps(dev, plan), Comm(device=dev))
 
-    def one_build():
-        return builder.build(header, file_len, buf, lo, hi, opts)
+        def one_build():
+            r = builder.build(header, file_len, buf, lo, hi, opts)
+            for k, v in r.phase_ms.items():
+                phases[k] = phases.get(k, 0.0) + v
+            return r.out, {"sharded": {"sharded": 1, "exact": 2, "gathered": 3}[r.path],
+                           "num_entries": r.stats["num_entries"]}
+    else:
+        uid = [_native.shard_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        comm = _native.ShardComm(uid[0], rank, world, dev.index)
+        d_out = torch.empty(max(16, out_len), dtype=torch.uint8, device=dev)
+
+        def one_build():
+            st = comm.build(plan, header, file_len, buf.data_ptr(), lo, hi, opts, d_out.data_ptr(), out_len,
+                            stream.cuda_stream)
+            for k, v in comm.phases():
+                phases[k] = phases.get(k, 0.0) + v
+            return d_out[:out_len], {"sharded": st.sharded, "num_entries": st.num_entries}
 
     for _ in range(args.warmup):
-        res = one_build()
+        out, info = one_build()
+    phases.clear()
     dist.barrier()
     torch.cuda.synchronize(dev)
     t_start = time.perf_counter()
-    phase = {}
     for _ in range(args.steps):
-        res = one_build()
-        for k, v in res.phase_ms.items():
-            phase[k] = phase.get(k, 0.0) + v
+        out, info = one_build()
     torch.cuda.synchronize(dev)
     dist.barrier()
     elapsed = time.perf_counter() - t_start
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.backend == "nccl" else "cpu")
+    t = torch.tensor([elapsed], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
     if churn:
-        assert res.path == "exact", (res.path, res.stats)
+        assert info["sharded"] == 2, info
     else:
-        assert res.path == "sharded" and res.stats["num_entries"] == n_total, (res.path, res.stats)
+        assert info["sharded"] == 1 and info["num_entries"] == n_total, info
     identical = None
     if args.check:  # the sharded .spi against one single-GPU build of the whole log (rank 0)
         pieces = [None] * world
-        dist.all_gather_object(pieces, (res.out_offset, res.out.cpu().numpy().tobytes()))
+        dist.all_gather_object(pieces, (out_off, out.cpu().numpy().tobytes()))
         if rank == 0:
             if full_log is None:
                 full_log = synth.fixed_log(n_total, 16, 100, seed=args.seed, file_id=0x5EED0000)
@@ -466,6 +548,7 @@ def sharded(args, dev, world, rank):
     ms_per_step = elapsed * 1000.0 / args.steps
     b_alg_per_gpu = ((file_len - 84) + 112 + slot * cap) / world
     achieved = b_alg_per_gpu / (ms_per_step * 1e-3) / 1e9
+    plan.close()
     return {
         "value": n_total * args.steps / elapsed, "ms_per_step": ms_per_step,
         "config": {"workload": (f"churn: {args.entries} records per GPU x {world} GPUs = {n_total} (keys from a pool "
@@ -474,12 +557,14 @@ def sharded(args, dev, world, rank):
                                 "(16 B key, 100 B value, NONE, IN_MEMORY)"),
                    "entries": n_total, "entries_per_gpu": args.entries, "log_bytes": file_len, "capacity": cap,
                    "spi_bytes": 112 + slot * cap,
-                   "parallelism": f"log byte-range sharded x{world}, RCCL all_to_all of (hash, address) entries"},
+                   "parallelism": f"log byte-range sharded x{world}, RCCL all_to_all of (hash, address) entries",
+                   "orchestrator": "C++ sparkey_shard_build (C-ABI)" if args.orchestrator == "cpp"
+                   else "Python ShardedBuilder"},
         "roofline": {"bound": "hbm", "kernel": "whole sharded build per GPU", "achieved": achieved,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                      "algorithmic_bytes_per_launch": b_alg_per_gpu, "avg_launch_ms": ms_per_step},
-        "phase_ms_rank0": {k: v / args.steps for k, v in phase.items()},
-        "entry_rounds": res.rounds, "spilled_slots": res.n_spill, "bit_identical_to_single_gpu": identical,
+        "phase_ms_rank0": {k: v / args.steps for k, v in phases.items()},
+        "bit_identical_to_single_gpu": identical,
         "cpu_baseline": None,
         "gen_s": gen_s,
         "version": sparkey.version(),
@@ -496,10 +581,14 @@ def main():
                     help="c2 (the headline metric); c3 / c5 / churn are extra single-GPU measurements")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--quick", action="store_true", help="timed device builds only (profiling runs)")
+    ap.add_argument("--no-parity", action="store_true", help="skip the N = 1 parity leg (other device paths)")
+    ap.add_argument("--parity-c3-entries", type=int, default=10_000_000)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--backend", default="nccl", help="nccl (RCCL); gloo only to rehearse N > 1 ranks on one GPU")
     ap.add_argument("--sharded", action="store_true", help="the sharded build even at N = 1 (rehearsal)")
     ap.add_argument("--check", action="store_true", help="sharded: compare the .spi with a single-GPU build")
+    ap.add_argument("--orchestrator", default="cpp", choices=["cpp", "python"],
+                    help="sharded: the C-ABI's sparkey_shard_build (C++) or sparkey/sharded.py over torch.distributed")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -511,10 +600,10 @@ def main():
     dev = torch.device("cuda", local_rank)
     if world > 1 or args.sharded:
         import torch.distributed as dist
-        if args.backend == "nccl":
+        if args.backend == "nccl" and args.orchestrator == "python":
             dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group(args.backend)
+        else:  # (the C++ orchestrator moves the data over its own RCCL communicator)
+            dist.init_process_group("gloo")
         r = sharded(args, dev, world, rank)
         dist.destroy_process_group()
     elif args.workload == "get":

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define SPARKEY_GPU_ABI_VERSION 1
+#define SPARKEY_GPU_ABI_VERSION 2
 
 /* Error codes -> the reference's exception (see INTEGRATION.md for the JNI mapping). */
 #define SPARKEY_OK 0
@@ -40,6 +40,11 @@ extern "C" {
 #define SPARKEY_E_GPU (-10)           /* HIP runtime error or no gfx950 device */
 #define SPARKEY_E_ARG (-11)           /* IllegalArgumentException (bad hash size etc.) */
 #define SPARKEY_E_BUFFER (-12)        /* caller buffer too small */
+#define SPARKEY_E_CORRUPT_RECORD (-13) /* RuntimeException: a record the log iterator cannot read -- EOF inside its
+                                          header VLQs (EOFException wrapped, SparkeyLogIterator.java:117,134-136), a key
+                                          longer than maxKeyLen or negative (IndexOutOfBoundsException from
+                                          stream.read(keyBuf, 0, keyLen), :130), a compressed block that fails to
+                                          decode while iterating (CompressedReader.fetchBlock, CompressedReader.java:51-60) */
 
 /* ConstructionMethod (SparkeyWriter.java ConstructionMethod enum) */
 #define SPARKEY_METHOD_AUTO 0
@@ -52,7 +57,11 @@ typedef struct sparkey_build_opts {
   double sparsity;     /* clamped to >= 1.3 like IndexHash.java:135-137 */
   int64_t max_memory;  /* already resolved (>= 10 MiB); only decides AUTO */
   int32_t method;      /* SPARKEY_METHOD_* */
-  int32_t device;      /* HIP device ordinal */
+  int32_t device;      /* HIP device ordinal (the first one when num_gpus > 1) */
+  int32_t num_gpus;    /* 0 or 1: one GPU.  N > 1: the log's byte range sharded over devices device .. device + N - 1
+                          of this process, one thread per GPU, RCCL over xGMI between them; the
+                          .spi bytes are the single-GPU build's.  Only sparkey_build_index_file / _mem read it. */
+  int32_t reserved;    /* 0 */
 } sparkey_build_opts;
 
 typedef struct sparkey_build_stats {
@@ -73,8 +82,10 @@ typedef struct sparkey_build_stats {
                                  2 = uniform-record framing (the header proves one record size) */
   int32_t partition_passes;   /* passes over the entries of the bucket partition: 2, or 1 when the
                                  uniform framing wrote the per-digit regions itself */
-  int32_t reserved;
-  double device_ms;           /* device time of the build (HIP events), excluding copies */
+  int32_t sharded;            /* multi-GPU builds: 1 sharded canonical placement, 2 sharded exact path, 3 the log
+                                 gathered on every rank and built whole (compressed logs, full tables); else 0 */
+  double device_ms;           /* device time of the build (HIP events), excluding copies; sharded: the rank's
+                                 wall time of sparkey_shard_build */
 } sparkey_build_stats;
 
 /* file -> file.  What the JNI shim calls in place of IndexHash.createNew; the Java side keeps
@@ -279,6 +290,37 @@ int sparkey_shard_exact_extract(sparkey_plan* plan, uint64_t a, uint64_t b, uint
 int sparkey_index_header(const uint8_t* log_header, const sparkey_build_opts* opts, int64_t num_entries,
                          int64_t garbage_size, int64_t max_displacement, int64_t hash_collisions,
                          int64_t total_displacement, uint8_t* out, char* err, size_t err_len);
+
+/* ---- one rank of the sharded build, whole (the orchestration of the steps above) ----
+ * sparkey_build_index_file / _mem with opts.num_gpus > 1 run N such ranks as threads of the calling
+ * process.  A multi-process host (one process per GPU, e.g. bench.py under torch.distributed.run) runs
+ * one per process: rank 0 makes an RCCL unique id, hands it to every rank out of band, and each rank
+ * creates its communicator and calls sparkey_shard_build with the same log header and options. */
+typedef struct sparkey_shard_comm sparkey_shard_comm;
+#define SPARKEY_SHARD_UNIQUE_ID_BYTES 128
+int sparkey_shard_comm_unique_id(uint8_t* id_out /* 128 bytes */, char* err, size_t err_len);
+/* RCCL communicator of rank `rank` of `world` on `device` (collective: every rank calls it). */
+int sparkey_shard_comm_create(sparkey_shard_comm** comm_out, const uint8_t* id, int32_t rank, int32_t world,
+                              int32_t device, char* err, size_t err_len);
+void sparkey_shard_comm_destroy(sparkey_shard_comm* comm);
+/* What rank `rank` must hold of the log (global bytes [*buf_lo, *buf_hi), buf_lo 4 KiB aligned) and the
+ * part of the .spi it produces (bytes [*out_off, *out_off + *out_len) of the file: rank 0 the header and
+ * its slots, every other rank its slots). */
+int sparkey_shard_geometry(const uint8_t* log_header, uint64_t file_len, const sparkey_build_opts* opts, int32_t rank,
+                           int32_t world, uint64_t* buf_lo, uint64_t* buf_hi, uint64_t* out_off, uint64_t* out_len,
+                           char* err, size_t err_len);
+/* The rank's whole build: d_buf holds global log bytes [buf_lo, buf_hi) (sparkey_shard_geometry), d_out
+ * receives the rank's part of the .spi (out_cap >= *out_len).  Synchronises `stream` (NULL: a private
+ * stream) before returning; stats_out holds the whole index's header fields on every rank.  Errors are
+ * the single-GPU build's (the lowest log offset over the ranks). */
+int sparkey_shard_build(sparkey_plan* plan, sparkey_shard_comm* comm, const uint8_t* log_header, uint64_t file_len,
+                        const uint8_t* d_buf, uint64_t buf_lo, uint64_t buf_hi, const sparkey_build_opts* opts,
+                        uint8_t* d_out, uint64_t out_cap, void* stream, sparkey_build_stats* stats_out, char* err,
+                        size_t err_len);
+/* Host wall time per phase of the last sparkey_shard_build on this communicator. */
+int32_t sparkey_shard_phase_count(const sparkey_shard_comm* comm);
+const char* sparkey_shard_phase_name(const sparkey_shard_comm* comm, int32_t i);
+double sparkey_shard_phase_ms(const sparkey_shard_comm* comm, int32_t i);
 
 const char* sparkey_gpu_version(void);
 const char* sparkey_strerror(int code);

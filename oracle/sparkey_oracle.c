@@ -684,15 +684,20 @@ static int32_t next_record(const build_ctx* c, int64_t* pos, int64_t end, int64_
   int64_t p = *pos;
   int32_t first, second, rc;
   if (p >= c->log_len) return 0;                                         /* EOF on first VLQ: stop */
+  /* EOF inside the header VLQs: EOFException, wrapped in RuntimeException by hasNext
+   * (SparkeyLogIterator.java:117,134-136) */
   rc = oracle_vlq_read(c->log, c->log_len, &p, &first);
-  if (rc) return rc;
+  if (rc) return rc == ORACLE_E_CORRUPT_LOG ? ORACLE_E_CORRUPT_RECORD : rc;
   rc = oracle_vlq_read(c->log, c->log_len, &p, &second);
-  if (rc) return rc;
+  if (rc) return rc == ORACLE_E_CORRUPT_LOG ? ORACLE_E_CORRUPT_RECORD : rc;
   if (first == 0) { r->is_put = 0; r->key_len = second; r->value_len = 0; }
   else { r->is_put = 1; r->key_len = first - 1; r->value_len = second; }
-  if (r->key_len < 0 || r->value_len < 0) return ORACLE_E_CORRUPT_LOG;
-  if (r->key_len > c->ih.max_key_len) return ORACLE_E_CORRUPT_LOG;      /* keyBuf overflow in Java */
-  if (p + r->key_len > c->log_len) return ORACLE_E_CORRUPT_LOG;
+  /* stream.read(keyBuf, 0, keyLen) (:130): IndexOutOfBoundsException for a negative key length or one
+   * above maxKeyLen (the buffer's size); a negative value length and a key past the end of the file
+   * are not reference-pinned and are rejected the same way */
+  if (r->key_len < 0 || r->value_len < 0) return ORACLE_E_CORRUPT_RECORD;
+  if (r->key_len > c->ih.max_key_len) return ORACLE_E_CORRUPT_RECORD;
+  if (p + r->key_len > c->log_len) return ORACLE_E_CORRUPT_RECORD;
   r->key = c->log + p;
   *pos = p + r->key_len + r->value_len;
   return 1;
@@ -789,6 +794,7 @@ static const char* err_msg(int32_t rc) {
     case ORACLE_E_HEADER: return "Too large max key len";
     case ORACLE_E_UNSUPPORTED: return "Unsupported compression type";
     case ORACLE_E_BUFFER: return "Buffer too small";
+    case ORACLE_E_CORRUPT_RECORD: return "Corrupt log record";
     default: return "Error";
   }
 }
@@ -965,9 +971,13 @@ int64_t oracle_build_index(const uint8_t* log, int64_t log_len, int32_t hash_siz
   c.ebb_mask = (1 << c.ih.entry_block_bits) - 1;
   uint8_t* vbuf = NULL;
   if (lh.compression_type != 0) {
-    if (lh.compression_block_size < 0) rc = ORACLE_E_CORRUPT_LOG;
+    /* every block is fetched and decoded inside the iterator (CompressedReader.fetchBlock,
+     * CompressedReader.java:51-60; a negative maxBlockSize fails in its constructor, :40-49), so a
+     * bad block is a RuntimeException there */
+    if (lh.compression_block_size < 0) rc = ORACLE_E_CORRUPT_RECORD;
     else if (lh.compression_type == 2) rc = open_zstd(&c, log, lh.data_end, lh.compression_block_size, &vbuf);
     else rc = open_compressed(&c, log, lh.data_end, &vbuf);
+    if (rc == ORACLE_E_CORRUPT_LOG) rc = ORACLE_E_CORRUPT_RECORD;
     if (rc) { free(c.blk_pos); free(c.blk_voff); set_err(err, err_len, err_msg(rc)); return rc; }
   }
   const int64_t hash_length = (int64_t)c.slot_size * c.ih.capacity;

@@ -34,6 +34,7 @@ extern "C" {
 #define ORACLE_E_UNSUPPORTED (-8)
 #define ORACLE_E_ARG (-11)
 #define ORACLE_E_BUFFER (-12)
+#define ORACLE_E_CORRUPT_RECORD (-13) /* RuntimeException from the log iterator (SPARKEY_E_CORRUPT_RECORD) */
 
 /* MurmurHash3.java:18-75 */
 uint32_t oracle_murmur3_x86_32(const uint8_t* data, int32_t len, int32_t seed);

@@ -10,10 +10,11 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 LIB_DIR = os.path.join(HERE, "lib")
 LIB = os.path.join(LIB_DIR, "libsparkey_gpu.so")
+OBJ_DIR = os.path.join(HERE, "build", "obj")
 SOURCES = [os.path.join(HERE, "csrc", f) for f in ("build_kernels.hip", "fused_kernels.hip", "frame2_kernels.hip", "frame3_kernels.hip", "exact_kernels.hip", "shard_kernels.hip", "shard_exact_kernels.hip",
-                                                      "lookup_kernels.hip", "append_kernels.hip", "snappy_kernels.hip", "zstd_kernels.hip", "sparkey_gpu.cpp", "file_build.cpp")]
+                                                      "lookup_kernels.hip", "append_kernels.hip", "snappy_kernels.hip", "zstd_kernels.hip", "sparkey_gpu.cpp", "file_build.cpp", "shard_host.cpp")]
 HEADERS = [os.path.join(HERE, "csrc", f) for f in ("snappy.hpp", "frame_common.hpp", "build_kernels.hpp", "device_common.hpp", "kernel_utils.hpp", "scan.hpp", "place_common.hpp",
-                                                      "lookup.hpp", "append.hpp")] + [
+                                                      "lookup.hpp", "append.hpp", "shard_host.hpp")] + [
     os.path.join(ROOT, "include", "sparkey_gpu.h")]
 ARCH = os.environ.get("SPARKEY_GPU_ARCH", "gfx950")
 
@@ -25,14 +26,33 @@ def _stale(target, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
+def _compile(src, obj, verbose):
+    cmd = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall", "-I", os.path.join(ROOT, "include"),
+           "-c", "-x", "hip", src, "-o", obj + ".tmp"]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True)
+    os.replace(obj + ".tmp", obj)
+
+
 def build(force: bool = False, verbose: bool = False) -> str:
-    os.makedirs(LIB_DIR, exist_ok=True)
-    if force or _stale(LIB, SOURCES + HEADERS + [__file__]):
-        cmd = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wl,--no-undefined", "-Wall",
-               "-I", os.path.join(ROOT, "include")]
-        for s in SOURCES:
-            cmd += ["-x", "hip", s]
-        cmd += ["-o", LIB + ".tmp"]
+    """One object per source (compiled in parallel, each only when it or a header changed), then one
+    link.  No -fgpu-rdc: every kernel is launched from its own translation unit."""
+    from concurrent.futures import ThreadPoolExecutor
+    os.makedirs(OBJ_DIR, exist_ok=True)
+    jobs = []
+    for s in SOURCES:
+        obj = os.path.join(OBJ_DIR, os.path.basename(s) + ".o")
+        if force or _stale(obj, [s] + HEADERS + [__file__]):
+            jobs.append((s, obj))
+    if jobs:
+        workers = max(1, min(len(jobs), int(os.environ.get("MAX_JOBS", "0")) or (os.cpu_count() or 4)))
+        with ThreadPoolExecutor(workers) as ex:
+            for f in [ex.submit(_compile, s, o, verbose) for s, o in jobs]:
+                f.result()
+    objs = [os.path.join(OBJ_DIR, os.path.basename(s) + ".o") for s in SOURCES]
+    if force or jobs or _stale(LIB, objs):
+        cmd = ["hipcc", f"--offload-arch={ARCH}", "-fPIC", "-shared", "-Wl,--no-undefined"] + objs + ["-o", LIB + ".tmp"]
         if verbose:
             print(" ".join(cmd))
         subprocess.run(cmd, check=True)

@@ -54,7 +54,7 @@ __global__ void k_walk(BuildParams P, int serial) {
     }
     const RecHdr h = decode_header(at, p, (int64_t)P.log_len);
     if (!header_valid(h, p, P.max_key_len, (int64_t)P.log_len)) {
-      set_error(P.st, p, h.rc ? h.rc : kErrCorruptLog);
+      set_error(P.st, p, h.rc ? h.rc : kErrCorruptRecord);
       for (; m < nc; m++) P.cnt[m] = 0;
       return;
     }
@@ -89,7 +89,7 @@ __global__ __launch_bounds__(64) void k_emit(BuildParams P) {
     while (p < e) {
       const RecHdr h = decode_header(at, p, (int64_t)P.log_len);
       if (!header_valid(h, p, P.max_key_len, (int64_t)P.log_len)) {
-        set_error(P.st, p, h.rc ? h.rc : kErrCorruptLog);
+        set_error(P.st, p, h.rc ? h.rc : kErrCorruptRecord);
         bad = true;
         break;
       }

@@ -19,6 +19,7 @@ constexpr int kErrCorruptLog = -3;
 constexpr int kErrNoFreeSlots = -4;
 constexpr int kErrCorruptData = -5;
 constexpr int kErrVlq = -6;
+constexpr int kErrCorruptRecord = -13;  // SPARKEY_E_CORRUPT_RECORD: the iterator cannot read a record
 
 // ---------------------------------------------------------------------------------------------
 // wantedSlot = Long.remainderUnsigned(hash, capacity)   (IndexHash.java:667-669)
@@ -160,7 +161,7 @@ __device__ __forceinline__ uint64_t key_hash(int hash_size, P key, int32_t len, 
 // (SparkeyLogIterator.java:86-138).
 // ---------------------------------------------------------------------------------------------
 struct RecHdr {
-  int32_t rc;     // 0 ok, kErrVlq, kErrCorruptLog (EOF inside the header)
+  int32_t rc;     // 0 ok, kErrVlq, kErrCorruptRecord (EOF inside the header)
   int32_t put;    // 1 PUT, 0 DELETE
   int32_t hlen;   // header bytes
   int32_t klen;   // Java int (may be negative on corrupt input)
@@ -173,7 +174,7 @@ __device__ __forceinline__ int32_t read_vlq(At at, int64_t& p, int64_t avail, in
   uint32_t v = 0;
 #pragma unroll
   for (int i = 0; i < 5; i++) {
-    if (p >= avail) { rc = kErrCorruptLog; return 0; }
+    if (p >= avail) { rc = kErrCorruptRecord; return 0; }
     const uint32_t b = at(p);
     p++;
     if (b < 0x80u) return (int32_t)(v | (b << (7 * i)));

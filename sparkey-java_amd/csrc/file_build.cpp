@@ -31,6 +31,7 @@
 #include <vector>
 
 #include "../../include/sparkey_gpu.h"
+#include "shard_host.hpp"
 
 // LogHeader.read's checks with the file's length (sparkey_gpu.cpp), message into err.
 int sk_check_log_header(const uint8_t* b, uint64_t hdr_len, uint64_t file_len, char* err, size_t err_len);
@@ -247,8 +248,14 @@ int for_each_slot_piece(FileCtx* c, uint64_t total, Fn&& fn) {
 }
 
 // [off, off + len) of fd into buf by the pool, kPieceBytes per task.
-bool pool_pread(FileCtx* c, int fd, uint8_t* buf, uint64_t off, uint64_t len) {
-  std::atomic<bool> ok{true};
+// The first failure of a pool task: its errno, or kShortRead when the file ended early (it shrank
+// after fstat).  errno is per thread, so the failing task records it for the caller's message.
+constexpr int kShortRead = -1;
+
+std::string io_error(int e) { return e == kShortRead ? std::string("the log file ended early (truncated)") : strerror(e); }
+
+bool pool_pread(FileCtx* c, int fd, uint8_t* buf, uint64_t off, uint64_t len, int* err_no) {
+  std::atomic<int> fail{0};
   const int ntask = (int)((len + kPieceBytes - 1) / kPieceBytes);
   c->pool->run(ntask, [&](int t) {
     uint64_t a = (uint64_t)t * kPieceBytes;
@@ -257,17 +264,19 @@ bool pool_pread(FileCtx* c, int fd, uint8_t* buf, uint64_t off, uint64_t len) {
       const ssize_t r = pread(fd, buf + a, (size_t)(b - a), (off_t)(off + a));
       if (r < 0 && errno == EINTR) continue;
       if (r <= 0) {
-        ok = false;
+        int expect = 0;
+        fail.compare_exchange_strong(expect, r == 0 ? kShortRead : errno);
         return;
       }
       a += (uint64_t)r;
     }
   });
-  return ok;
+  *err_no = fail.load();
+  return *err_no == 0;
 }
 
-bool pool_pwrite(FileCtx* c, int fd, const uint8_t* buf, uint64_t off, uint64_t len) {
-  std::atomic<bool> ok{true};
+bool pool_pwrite(FileCtx* c, int fd, const uint8_t* buf, uint64_t off, uint64_t len, int* err_no) {
+  std::atomic<int> fail{0};
   const int ntask = (int)((len + kPieceBytes - 1) / kPieceBytes);
   c->pool->run(ntask, [&](int t) {
     uint64_t a = (uint64_t)t * kPieceBytes;
@@ -276,18 +285,20 @@ bool pool_pwrite(FileCtx* c, int fd, const uint8_t* buf, uint64_t off, uint64_t 
       const ssize_t w = pwrite(fd, buf + a, (size_t)(b - a), (off_t)(off + a));
       if (w < 0 && errno == EINTR) continue;
       if (w <= 0) {
-        ok = false;
+        int expect = 0;
+        fail.compare_exchange_strong(expect, w == 0 ? ENOSPC : errno);
         return;
       }
       a += (uint64_t)w;
     }
   });
-  return ok;
+  *err_no = fail.load();
+  return *err_no == 0;
 }
 
-// d_out[0, isz) -> fd, through the staging ring: the copy of piece i + 1 runs while piece i is
-// written.
-int write_index(FileCtx* c, int fd, uint64_t isz, char* err, size_t err_len) {
+// d_out[0, isz) -> fd at file offset file_off, through the staging ring: the copy of piece i + 1 runs
+// while piece i is written.
+int write_index(FileCtx* c, int fd, uint64_t isz, char* err, size_t err_len, uint64_t file_off = 0) {
   const uint64_t n = (isz + kSlotBytes - 1) / kSlotBytes;
   auto issue = [&](uint64_t i) -> bool {
     const int k = (int)(i % kSlots);
@@ -311,12 +322,65 @@ int write_index(FileCtx* c, int fd, uint64_t isz, char* err, size_t err_len) {
       return SPARKEY_E_GPU;
     }
     const uint64_t off = i * kSlotBytes, len = std::min(kSlotBytes, isz - off);
-    if (!pool_pwrite(c, fd, c->slot[k], off, len)) {
-      set_err(err, err_len, std::string("write of the index file failed: ") + strerror(errno));
+    int e = 0;
+    if (!pool_pwrite(c, fd, c->slot[k], file_off + off, len, &e)) {
+      set_err(err, err_len, std::string("write of the index file failed: ") + io_error(e));
       return SPARKEY_E_IO;
     }
   }
   return SPARKEY_OK;
+}
+
+// Log bytes [file_off, file_off + len) of fd -> c->d_log[0, len), through the staging ring (the pool
+// reads piece i + 1 while piece i is copied).
+int read_log_range(FileCtx* c, int fd, uint64_t file_off, uint64_t len, char* err, size_t err_len) {
+  const int rc = for_each_slot_piece(c, len, [&](int k, uint64_t off, uint64_t n) -> int {
+    int e = 0;
+    if (!pool_pread(c, fd, c->slot[k], file_off + off, n, &e)) {
+      set_err(err, err_len, std::string("read of the log file failed: ") + io_error(e));
+      return SPARKEY_E_IO;
+    }
+    if (hipMemcpyAsync(c->d_log + off, c->slot[k], n, hipMemcpyHostToDevice, c->s) != hipSuccess ||
+        hipEventRecord(c->ev[k], c->s) != hipSuccess) {
+      set_err(err, err_len, "H2D copy failed");
+      return SPARKEY_E_GPU;
+    }
+    return SPARKEY_OK;
+  });
+  if (rc) (void)hipStreamSynchronize(c->s);
+  return rc;
+}
+
+struct CtxHold {  // acquire_ctx / release_ctx around one rank's work
+  FileCtx* c = nullptr;
+  ~CtxHold() { release_ctx(c); }
+};
+
+// One rank of a multi-GPU build (opts.num_gpus > 1): its log bytes in through `load`, the sharded build,
+// its part of the .spi out through `store`.  Runs on the rank's own thread (shard_run_threads).
+template <class Load, class Store>
+int shard_rank(int rank, int world, int device, sparkey_shard_comm* comm, const uint8_t* hdr, uint64_t log_len,
+               const sparkey_build_opts* opts, sparkey_build_stats* stats_out, char* err, size_t err_len, Load&& load,
+               Store&& store) {
+  uint64_t blo, bhi, ooff, olen;
+  int rc = sparkey_shard_geometry(hdr, log_len, opts, rank, world, &blo, &bhi, &ooff, &olen, err, err_len);
+  if (rc) return rc;
+  CtxHold h;
+  h.c = acquire_ctx(device, err, err_len, &rc);
+  if (!h.c) return rc;
+  FileCtx* c = h.c;
+  if (hipSetDevice(device) != hipSuccess) {
+    set_err(err, err_len, "hipSetDevice failed");
+    return SPARKEY_E_GPU;
+  }
+  rc = c->reserve(bhi - blo + 16, olen, err, err_len);
+  if (!rc) rc = load(c, blo, bhi - blo);
+  sparkey_build_stats st;
+  if (!rc) rc = sparkey_shard_build(c->plan, comm, hdr, log_len, c->d_log, blo, bhi, opts, c->d_out, olen, c->s, &st, err,
+                                    err_len);
+  if (!rc) rc = store(c, ooff, olen);
+  if (!rc && rank == 0 && stats_out) *stats_out = st;
+  return rc;
 }
 
 }  // namespace
@@ -358,6 +422,33 @@ int sparkey_build_index_file(const char* log_path, const char* index_out_path, c
     set_err(err, err_len, sparkey_strerror((int)isz));
     return (int)isz;
   }
+  if (opts->num_gpus > 1) {  // every rank reads its byte range and writes its part of the .spi itself
+    const int ofd = open(index_out_path, O_WRONLY | O_CREAT | O_TRUNC, 0644);
+    if (ofd < 0) {
+      set_err(err, err_len, std::string("cannot create index file ") + index_out_path + ": " + strerror(errno));
+      return SPARKEY_E_IO;
+    }
+    rc = ftruncate(ofd, (off_t)isz) == 0 ? SPARKEY_OK : SPARKEY_E_IO;
+    if (rc) set_err(err, err_len, std::string("cannot size the index file: ") + strerror(errno));
+    if (!rc)
+      rc = shard_run_threads(*opts, [&](int rank, int world, int device, sparkey_shard_comm* comm, char* e, size_t el) {
+        return shard_rank(
+            rank, world, device, comm, hdr, log_len, opts, stats_out, e, el,
+            [&](FileCtx* c, uint64_t lo, uint64_t n) { return read_log_range(c, fd, lo, n, e, el); },
+            [&](FileCtx* c, uint64_t off, uint64_t n) { return write_index(c, ofd, n, e, el, off); });
+      }, err, err_len);
+    if (!rc && fsync_out && fsync(ofd) != 0) {
+      set_err(err, err_len, std::string("fsync of the index file failed: ") + strerror(errno));
+      rc = SPARKEY_E_IO;
+    }
+    if (close(ofd) != 0 && !rc) {
+      set_err(err, err_len, std::string("close of the index file failed: ") + strerror(errno));
+      rc = SPARKEY_E_IO;
+    }
+    if (rc) unlink(index_out_path);
+    if (dbg) fprintf(stderr, "[file] %d GPUs: %.2f ms\n", opts->num_gpus, now_ms() - t0);
+    return rc;
+  }
   FileCtx* c = acquire_ctx(opts->device, err, err_len, &rc);
   if (!c) return rc;
   struct Releaser {
@@ -372,22 +463,8 @@ int sparkey_build_index_file(const char* log_path, const char* index_out_path, c
   if (rc) return rc;
   const double t1 = now_ms();
   // log -> pinned slots (pool) -> device, piece by piece
-  rc = for_each_slot_piece(c, log_len, [&](int k, uint64_t off, uint64_t len) -> int {
-    if (!pool_pread(c, fd, c->slot[k], off, len)) {
-      set_err(err, err_len, std::string("read of the log file failed: ") + strerror(errno));
-      return SPARKEY_E_IO;
-    }
-    if (hipMemcpyAsync(c->d_log + off, c->slot[k], len, hipMemcpyHostToDevice, c->s) != hipSuccess ||
-        hipEventRecord(c->ev[k], c->s) != hipSuccess) {
-      set_err(err, err_len, "H2D copy failed");
-      return SPARKEY_E_GPU;
-    }
-    return SPARKEY_OK;
-  });
-  if (rc) {
-    (void)hipStreamSynchronize(c->s);
-    return rc;
-  }
+  rc = read_log_range(c, fd, 0, log_len, err, err_len);
+  if (rc) return rc;
   const double t2 = now_ms();
   rc = sparkey_plan_build_device(c->plan, hdr, c->d_log, log_len, c->d_out, (uint64_t)isz, opts, c->s, stats_out, err,
                                  err_len);
@@ -438,6 +515,26 @@ int sparkey_build_index_mem(const uint8_t* log, uint64_t log_len, uint8_t* index
     set_err(err, err_len, "index buffer too small: need " + std::to_string(isz));
     return SPARKEY_E_BUFFER;
   }
+  if (opts->num_gpus > 1)
+    return shard_run_threads(*opts, [&](int rank, int world, int device, sparkey_shard_comm* comm, char* e, size_t el) {
+      return shard_rank(
+          rank, world, device, comm, log, log_len, opts, stats_out, e, el,
+          [&](FileCtx* c, uint64_t lo, uint64_t n) {
+            if (hipMemcpyAsync(c->d_log, log + lo, n, hipMemcpyHostToDevice, c->s) != hipSuccess) {
+              set_err(e, el, "H2D copy failed");
+              return (int)SPARKEY_E_GPU;
+            }
+            return (int)SPARKEY_OK;
+          },
+          [&](FileCtx* c, uint64_t off, uint64_t n) {
+            if (hipMemcpyAsync(index_out + off, c->d_out, n, hipMemcpyDeviceToHost, c->s) != hipSuccess ||
+                hipStreamSynchronize(c->s) != hipSuccess) {
+              set_err(e, el, "D2H copy failed");
+              return (int)SPARKEY_E_GPU;
+            }
+            return (int)SPARKEY_OK;
+          });
+    }, err, err_len);
   FileCtx* c = acquire_ctx(opts->device, err, err_len, &rc);
   if (!c) return rc;
   struct Releaser {
@@ -475,6 +572,7 @@ int sparkey_build_index_mem(const uint8_t* log, uint64_t log_len, uint8_t* index
 }
 
 void sparkey_release_cached_resources(void) {
+  shard_release_groups();
   std::lock_guard<std::mutex> g(g_mu);
   for (auto& kv : g_cache) {
     kv.second->mu.lock();  // waits for a call in flight

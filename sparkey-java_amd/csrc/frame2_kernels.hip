@@ -237,7 +237,7 @@ __device__ __forceinline__ void frame2_region(const BuildParams& P, const uint64
     while (q < end) {
       const RecHdr h = hdr_at(q);
       if (!header_valid(h, q, P.max_key_len, log_len)) {
-        set_error(P.st, q, h.rc ? h.rc : kErrCorruptLog);
+        set_error(P.st, q, h.rc ? h.rc : kErrCorruptRecord);
         bad = true;
         return end;
       }

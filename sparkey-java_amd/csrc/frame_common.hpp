@@ -43,7 +43,7 @@ __device__ __forceinline__ RecHdr decode_lds(const uint8_t* win, int64_t wb, int
     auto at = [&](int64_t a) -> uint32_t { return win[a - wb]; };
     h = decode_header(at, p, p + 12);
   }
-  if (h.rc == 0 && p + h.hlen > avail) h.rc = kErrCorruptLog;
+  if (h.rc == 0 && p + h.hlen > avail) h.rc = kErrCorruptRecord;
   return h;
 }
 
@@ -183,7 +183,7 @@ __device__ __forceinline__ RecHdr decode_rgn(const uint8_t* r, int64_t R0, int64
     auto at = [&](int64_t a) -> uint32_t { return r[(uint32_t)(a - R0)]; };
     h = decode_header(at, p, p + 12);
   }
-  if (h.rc == 0 && p + h.hlen > avail) h.rc = kErrCorruptLog;
+  if (h.rc == 0 && p + h.hlen > avail) h.rc = kErrCorruptRecord;
   return h;
 }
 

@@ -459,7 +459,7 @@ __device__ __forceinline__ void frame_region(const BuildParams& P, const uint64_
         while (p < e) {
           const RecHdr h = hdr_at(p);
           if (!header_valid(h, p, P.max_key_len, log_len)) {
-            set_error(P.st, p, h.rc ? h.rc : kErrCorruptLog);
+            set_error(P.st, p, h.rc ? h.rc : kErrCorruptRecord);
             bad = true;
             break;
           }
@@ -493,7 +493,7 @@ __device__ __forceinline__ void frame_region(const BuildParams& P, const uint64_
         if (go) {
           const RecHdr h = hdr_at(p);
           if (!header_valid(h, p, P.max_key_len, log_len)) {
-            set_error(P.st, p, h.rc ? h.rc : kErrCorruptLog);
+            set_error(P.st, p, h.rc ? h.rc : kErrCorruptRecord);
             bad = true;
           } else {
             cnt++;

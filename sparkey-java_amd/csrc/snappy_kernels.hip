@@ -862,10 +862,7 @@ void launch_snappy_dir(const SnappyParams& S, hipStream_t s) { hipLaunchKernelGG
 hipError_t launch_snappy_decode(const SnappyParams& S, hipStream_t s) {
   if (S.nblk == 0) return hipSuccess;
   static const bool gw = getenv("SPARKEY_SNAPPY_LDS") == nullptr;  // (A/B: the decoded block in LDS)
-  static const int exp = getenv("SPARKEY_SNAPPY_EXP") ? atoi(getenv("SPARKEY_SNAPPY_EXP")) : 0;  // (measurements)
-  if (gw && exp == 1) {
-    hipLaunchKernelGGL(k_snappy_gw<1>, dim3((uint32_t)S.nblk), 64, 0, s, S);
-  } else if (gw) {
+  if (gw) {
     hipLaunchKernelGGL(k_snappy_gw<0>, dim3((uint32_t)S.nblk), 64, 0, s, S);
   } else if (S.lds_bytes) {
     hipError_t e = hipFuncSetAttribute((const void*)k_snappy_lds, hipFuncAttributeMaxDynamicSharedMemorySize,

@@ -197,6 +197,7 @@ const char* code_message(int code) {
     case SPARKEY_E_GPU: return "GPU error";
     case SPARKEY_E_ARG: return "Illegal argument";
     case SPARKEY_E_BUFFER: return "Buffer too small";
+    case SPARKEY_E_CORRUPT_RECORD: return "Corrupt log record";
     default: return "Unknown error";
   }
 }
@@ -414,7 +415,7 @@ static void fill_stats(sparkey_build_stats* s, const Status& st, const IndexPara
                        double ms, int partition_passes = 2) {
   if (!s) return;
   s->partition_passes = partition_passes;
-  s->reserved = 0;
+  s->sharded = 0;
   s->num_records = (int64_t)st.n_records;
   s->num_deletes = (int64_t)st.n_deletes;
   s->num_puts = (int64_t)st.n_records - (int64_t)st.n_deletes;
@@ -856,7 +857,7 @@ static int plan_build_snappy(sparkey_plan* pl, const LogHdr& lh, const uint8_t* 
   }
   if (lh.compression_block_size < 0) {  // new byte[maxBlockSize] (CompressedReader.java:40-49)
     set_err(err, err_len, "Corrupt log file: negative compression block size");
-    return SPARKEY_E_CORRUPT_LOG;
+    return SPARKEY_E_CORRUPT_RECORD;
   }
   HIP_TRY(hipSetDevice(pl->device));
   if (!s) s = pl->own_stream;
@@ -1008,7 +1009,7 @@ static int plan_build_snappy(sparkey_plan* pl, const LogHdr& lh, const uint8_t* 
                           : dir.err == 4 ? "ZSTD block frame without a content size (not a layout the reference writes)"
                                          : "Corrupt log file: bad compressed block header");
     if (dir.err == 4) return SPARKEY_E_UNSUPPORTED;
-    return SPARKEY_E_CORRUPT_LOG;
+    return SPARKEY_E_CORRUPT_RECORD;  // (CompressedReader.fetchBlock fails inside the iterator)
   }
   const uint64_t nblk = dir.nblk;
   const uint64_t vlen = (uint64_t)kLogHeaderSize + dir.total;
@@ -1045,7 +1046,7 @@ static int plan_build_snappy(sparkey_plan* pl, const LogHdr& lh, const uint8_t* 
     if (w.flags & kWalkBadStream) {
       set_err(err, err_len, std::string("Corrupt log file: bad ") + codec + " stream in block at " +
                                 std::to_string(blocks[b].file_pos));
-      return SPARKEY_E_CORRUPT_LOG;
+      return SPARKEY_E_CORRUPT_RECORD;
     }
     if (carry == 0) {
       if (w.flags) {
@@ -1053,7 +1054,7 @@ static int plan_build_snappy(sparkey_plan* pl, const LogHdr& lh, const uint8_t* 
                                   ? "Corrupt log file: more entries in a block than maxEntriesPerBlock"
                                   : "Corrupt log file: bad record header in block at " +
                                         std::to_string(blocks[b].file_pos));
-        return SPARKEY_E_CORRUPT_LOG;
+        return SPARKEY_E_CORRUPT_RECORD;
       }
       carry = w.overflow;
     } else if (carry >= (int64_t)blocks[b].ulen) {
@@ -1065,7 +1066,7 @@ static int plan_build_snappy(sparkey_plan* pl, const LogHdr& lh, const uint8_t* 
   }
   if (carry) {
     set_err(err, err_len, "Corrupt log file: the last record runs past dataEnd");
-    return SPARKEY_E_CORRUPT_LOG;
+    return SPARKEY_E_CORRUPT_RECORD;
   }
   // the normal build over the virtual log, into an internal table
   sparkey_build_opts o2 = *opts;
@@ -1237,9 +1238,11 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
                           want_frame3(P, lh, kLogHeaderSize, std::max<int64_t>(lh.data_end, kLogHeaderSize));
   const FrameGeom geom0 = get_geom(P);
   const FrameGeom geom2 = frame2_geometry(P, kLogHeaderSize, std::max<int64_t>(lh.data_end, kLogHeaderSize));
-  const int spec_path = fused_framing ? (use_frame2 ? 3 : (use_frame3 ? 4 : 0)) : 1;
+  // SPARKEY_SERIAL_FRAMING forces the exact serial walk (smoke() and tests check every framing path)
+  const bool force_serial = getenv("SPARKEY_SERIAL_FRAMING") != nullptr;
+  const int spec_path = fused_framing && !force_serial ? (use_frame2 ? 3 : (use_frame3 ? 4 : 0)) : 1;
   int framing_path = spec_path, placement_path = 0;
-  if (const int64_t R = uniform_record_size(lh)) {  // k_frame_uniform: every record is exactly R bytes
+  if (const int64_t R = force_serial ? 0 : uniform_record_size(lh)) {  // k_frame_uniform: every record is exactly R bytes
     framing_path = 2;
     P.uni_n = (uint64_t)lh.num_puts;
     P.uni_rec = R;
@@ -1762,15 +1765,26 @@ static int shard_sync_status(sparkey_plan* pl, hipStream_t s, char* err, size_t 
 // the nd = ceil(nbuckets / bpp) coarse digits in use split evenly: rank r owns digits
 // [nd r / world, nd (r + 1) / world) -> buckets -> slots
 static uint64_t used_digits(const BuildParams& P) { return (P.nbuckets + P.bpp - 1) / P.bpp; }
-static void shard_range(const BuildParams& P, int rank, int world, uint64_t* b_lo, uint64_t* b_hi, uint64_t* s_lo,
-                        uint64_t* s_hi) {
-  const uint64_t nd = used_digits(P);
+// buckets and slots of `rank`: an even split of the coarse digits (bucket / bpp) that hold buckets
+static void digit_split(uint64_t cap, uint64_t nbuckets, uint64_t bpp, int rank, int world, uint64_t* b_lo,
+                        uint64_t* b_hi, uint64_t* s_lo, uint64_t* s_hi) {
+  const uint64_t nd = (nbuckets + bpp - 1) / bpp;
   const uint64_t d0 = (nd * (uint64_t)rank) / (uint64_t)world;
   const uint64_t d1 = (nd * (uint64_t)(rank + 1)) / (uint64_t)world;
-  *b_lo = std::min<uint64_t>(P.nbuckets, d0 * P.bpp);
-  *b_hi = std::min<uint64_t>(P.nbuckets, d1 * P.bpp);
-  *s_lo = std::min<uint64_t>(P.cap, *b_lo << kBucketShift);
-  *s_hi = std::min<uint64_t>(P.cap, *b_hi << kBucketShift);
+  *b_lo = std::min<uint64_t>(nbuckets, d0 * bpp);
+  *b_hi = std::min<uint64_t>(nbuckets, d1 * bpp);
+  *s_lo = std::min<uint64_t>(cap, *b_lo << kBucketShift);
+  *s_hi = std::min<uint64_t>(cap, *b_hi << kBucketShift);
+}
+static void shard_range(const BuildParams& P, int rank, int world, uint64_t* b_lo, uint64_t* b_hi, uint64_t* s_lo,
+                        uint64_t* s_hi) {
+  digit_split(P.cap, P.nbuckets, P.bpp, rank, world, b_lo, b_hi, s_lo, s_hi);
+}
+void shard_slot_split(uint64_t cap, int world, int rank, uint64_t* lo, uint64_t* hi) {
+  const uint64_t nb = (cap + kBucket - 1) / kBucket;  // (setup_params: nbuckets, bpp)
+  const uint64_t bpp = std::max<uint64_t>(1, (nb + 255) / 256);
+  uint64_t b0, b1;
+  digit_split(cap, nb, bpp, rank, world, &b0, &b1, lo, hi);
 }
 
 extern "C" {

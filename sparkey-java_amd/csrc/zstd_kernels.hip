@@ -383,6 +383,52 @@ __device__ __forceinline__ uint8_t out_at(const uint8_t* p) {
   return *(const volatile uint8_t*)p;
 }
 
+// XXH64 (seed 0) of n decoded bytes, one lane (only checksummed frames take it; zstd-jni's default
+// frames carry no checksum).  The published algorithm: 4 accumulators over 32-byte stripes, merged,
+// then the 8/4/1-byte tail and the avalanche.
+template <bool kLds>
+__device__ uint64_t xxh64_out(const uint8_t* p, uint32_t n) {
+  constexpr uint64_t P1 = 0x9E3779B185EBCA87ull, P2 = 0xC2B2AE3D27D4EB4Full, P3 = 0x165667B19E3779F9ull,
+                     P4 = 0x85EBCA77C2B2AE63ull, P5 = 0x27D4EB2F165667C5ull;
+  auto rotl = [](uint64_t x, int r) { return (x << r) | (x >> (64 - r)); };
+  auto rd64 = [&](uint32_t i) {
+    uint64_t v = 0;
+    for (int k = 0; k < 8; k++) v |= (uint64_t)out_at<kLds>(p + i + k) << (8 * k);
+    return v;
+  };
+  auto round = [&](uint64_t acc, uint64_t in) { return rotl(acc + in * P2, 31) * P1; };
+  uint32_t i = 0;
+  uint64_t h;
+  if (n >= 32) {
+    uint64_t v1 = P1 + P2, v2 = P2, v3 = 0, v4 = 0 - P1;
+    for (; i + 32 <= n; i += 32) {
+      v1 = round(v1, rd64(i));
+      v2 = round(v2, rd64(i + 8));
+      v3 = round(v3, rd64(i + 16));
+      v4 = round(v4, rd64(i + 24));
+    }
+    h = rotl(v1, 1) + rotl(v2, 7) + rotl(v3, 12) + rotl(v4, 18);
+    for (uint64_t v : {v1, v2, v3, v4}) h = (h ^ round(0, v)) * P1 + P4;
+  } else {
+    h = P5;
+  }
+  h += n;
+  for (; i + 8 <= n; i += 8) h = rotl(h ^ round(0, rd64(i)), 27) * P1 + P4;
+  if (i + 4 <= n) {
+    uint64_t w = 0;
+    for (int k = 0; k < 4; k++) w |= (uint64_t)out_at<kLds>(p + i + k) << (8 * k);
+    h = rotl(h ^ (w * P1), 23) * P2 + P3;
+    i += 4;
+  }
+  for (; i < n; i++) h = rotl(h ^ (out_at<kLds>(p + i) * P5), 11) * P1;
+  h ^= h >> 33;
+  h *= P2;
+  h ^= h >> 29;
+  h *= P3;
+  h ^= h >> 32;
+  return h;
+}
+
 // Copies n bytes src -> dst with the wave, 64 a step (every step's loads complete before its stores;
 // a later step only reads below what earlier steps wrote, see the file comment).
 template <bool kLds>
@@ -451,8 +497,12 @@ __device__ int64_t zstd_decode(ZWork& W, const ZIn& in, uint8_t* out, uint32_t c
   bool have_ll = false, have_ml = false, have_of = false, have_huf = false;
   while (ip < in.n) {
     const uint32_t magic = in.le32(ip);
-    if ((magic & 0xFFFFFFF0u) == 0x184D2A50u) {  // skippable frame
-      ip += 8 + in.le32(ip + 4);
+    if (ip + 4 > in.n) return kZCorrupt;  // a partial frame header
+    if ((magic & 0xFFFFFFF0u) == 0x184D2A50u) {  // skippable frame: its size must lie inside the block
+      if (ip + 8 > in.n) return kZCorrupt;
+      const uint32_t skip = in.le32(ip + 4);
+      if (skip > in.n - ip - 8) return kZCorrupt;
+      ip += 8 + skip;
       continue;
     }
     if (magic != kZstdMagic) return kZCorrupt;
@@ -676,8 +726,15 @@ __device__ int64_t zstd_decode(ZWork& W, const ZIn& in, uint8_t* out, uint32_t c
       }
       if (last) break;
     }
-    if (checksum) ip += 4;
     if (fcs_bytes && op - frame_start != fcs) return kZCorrupt;
+    if (checksum) {  // Content_Checksum: low 32 bits of XXH64(frame output, seed 0), as libzstd checks it
+      if (ip + 4 > in.n) return kZCorrupt;
+      uint32_t want = 0;
+      if (lane == 0) want = (uint32_t)xxh64_out<kLds>(out + frame_start, op - frame_start);
+      want = (uint32_t)__shfl((int)want, 0);
+      if (want != in.le32(ip)) return kZCorrupt;
+      ip += 4;
+    }
   }
   return (int64_t)op;
 }

@@ -6,7 +6,8 @@
  *   IOException       LogHeader.read (LogHeader.java:57-83), "No free slots in the hash"
  *                     (IndexHash.java:574-576,664), CommonHeader (CommonHeader.java:38-43), file I/O
  *   RuntimeException  "Corrupt data" / "Invalid data - reference to delete entry"
- *                     (IndexHash.java:484,494,613,624), "Too long VLQ value" (Util.java:181,217)
+ *                     (IndexHash.java:484,494,613,624), "Too long VLQ value" (Util.java:181,217),
+ *                     records the log iterator cannot read (SparkeyLogIterator.java:117-136)
  *   IllegalArgumentException  bad hash size / options
  *
  * Built by sparkey-java_amd/build.py only when $JAVA_HOME/include/jni.h exists (this image has no
@@ -22,6 +23,7 @@ static void throw_for(JNIEnv* env, int rc, const char* msg) {
   switch (rc) {
     case SPARKEY_E_CORRUPT_DATA:
     case SPARKEY_E_VLQ:
+    case SPARKEY_E_CORRUPT_RECORD:
     case SPARKEY_E_GPU:
       cls = "java/lang/RuntimeException";
       break;
@@ -39,14 +41,17 @@ static void throw_for(JNIEnv* env, int rc, const char* msg) {
 /*
  * private static native void createNew0(String indexFile, String logFile, int hashSize, double sparsity,
  *                                       boolean fsync, int hashSeed, long maxMemory, int method,
- *                                       int device, long[] statsOut);
+ *                                       int device, int numGpus, long[] statsOut);
  * hashSize: 0 = auto (hashType == null), 4 or 8.  method: ConstructionMethod.ordinal() (AUTO 0,
- * IN_MEMORY 1, SORTING 2).  statsOut (nullable, length >= 9): numRecords, numPuts, numDeletes,
- * numEntries, capacity, garbageSize, maxDisplacement, hashCollisions, totalDisplacement.
+ * IN_MEMORY 1, SORTING 2).  numGpus: 0 or 1 = one GPU (`device`); N > 1 = the log sharded over GPUs
+ * device .. device + N - 1 of this process (sparkey_build_opts.num_gpus).  statsOut (nullable, length
+ * >= 9): numRecords, numPuts, numDeletes, numEntries, capacity, garbageSize, maxDisplacement,
+ * hashCollisions, totalDisplacement.
  */
 JNIEXPORT void JNICALL Java_com_spotify_sparkey_GpuIndexHash_createNew0(
     JNIEnv* env, jclass cls, jstring index_file, jstring log_file, jint hash_size, jdouble sparsity,
-    jboolean fsync, jint hash_seed, jlong max_memory, jint method, jint device, jlongArray stats_out) {
+    jboolean fsync, jint hash_seed, jlong max_memory, jint method, jint device, jint num_gpus,
+    jlongArray stats_out) {
   (void)cls;
   const char* idx = (*env)->GetStringUTFChars(env, index_file, NULL);
   const char* log = (*env)->GetStringUTFChars(env, log_file, NULL);
@@ -63,6 +68,7 @@ JNIEXPORT void JNICALL Java_com_spotify_sparkey_GpuIndexHash_createNew0(
   opts.max_memory = max_memory;
   opts.method = method;
   opts.device = device;
+  opts.num_gpus = num_gpus;
   sparkey_build_stats st;
   memset(&st, 0, sizeof(st));
   char err[512];

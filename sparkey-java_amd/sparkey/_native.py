@@ -47,6 +47,7 @@ E_IO = -9
 E_GPU = -10
 E_ARG = -11
 E_BUFFER = -12
+E_CORRUPT_RECORD = -13  # RuntimeException from the log iterator (SparkeyLogIterator.java:117-136)
 
 METHOD_AUTO = 0
 METHOD_IN_MEMORY = 1
@@ -55,7 +56,8 @@ METHOD_SORTING = 2
 
 class BuildOpts(ctypes.Structure):
     _fields_ = [("hash_size", ctypes.c_int32), ("hash_seed", ctypes.c_int32), ("sparsity", ctypes.c_double),
-                ("max_memory", ctypes.c_int64), ("method", ctypes.c_int32), ("device", ctypes.c_int32)]
+                ("max_memory", ctypes.c_int64), ("method", ctypes.c_int32), ("device", ctypes.c_int32),
+                ("num_gpus", ctypes.c_int32), ("reserved", ctypes.c_int32)]
 
 
 class BuildStats(ctypes.Structure):
@@ -65,7 +67,7 @@ class BuildStats(ctypes.Structure):
                 ("total_displacement", ctypes.c_int64), ("hash_size", ctypes.c_int32),
                 ("address_size", ctypes.c_int32), ("placement_path", ctypes.c_int32),
                 ("framing_path", ctypes.c_int32), ("partition_passes", ctypes.c_int32),
-                ("reserved", ctypes.c_int32), ("device_ms", ctypes.c_double)]
+                ("sharded", ctypes.c_int32), ("device_ms", ctypes.c_double)]
 
     def as_dict(self) -> dict:
         return {f: getattr(self, f) for f, _ in self._fields_}
@@ -103,6 +105,83 @@ _lib.sparkey_strerror.argtypes = [ctypes.c_int]
 _lib.sparkey_strerror.restype = ctypes.c_char_p
 _lib.sparkey_release_cached_resources.argtypes = []
 _lib.sparkey_release_cached_resources.restype = None
+_lib.sparkey_shard_comm_unique_id.argtypes = [_vp, ctypes.c_char_p, ctypes.c_size_t]
+_lib.sparkey_shard_comm_unique_id.restype = ctypes.c_int
+_lib.sparkey_shard_comm_create.argtypes = [ctypes.POINTER(_vp), _vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                           ctypes.c_char_p, ctypes.c_size_t]
+_lib.sparkey_shard_comm_create.restype = ctypes.c_int
+_lib.sparkey_shard_comm_destroy.argtypes = [_vp]
+_lib.sparkey_shard_comm_destroy.restype = None
+_lib.sparkey_shard_geometry.argtypes = [_vp, ctypes.c_uint64, ctypes.POINTER(BuildOpts), ctypes.c_int32, ctypes.c_int32,
+                                        ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
+                                        ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
+                                        ctypes.c_char_p, ctypes.c_size_t]
+_lib.sparkey_shard_geometry.restype = ctypes.c_int
+_lib.sparkey_shard_build.argtypes = [_vp, _vp, _vp, ctypes.c_uint64, _vp, ctypes.c_uint64, ctypes.c_uint64,
+                                     ctypes.POINTER(BuildOpts), _vp, ctypes.c_uint64, _vp, ctypes.POINTER(BuildStats),
+                                     ctypes.c_char_p, ctypes.c_size_t]
+_lib.sparkey_shard_build.restype = ctypes.c_int
+_lib.sparkey_shard_phase_count.argtypes = [_vp]
+_lib.sparkey_shard_phase_count.restype = ctypes.c_int32
+_lib.sparkey_shard_phase_name.argtypes = [_vp, ctypes.c_int32]
+_lib.sparkey_shard_phase_name.restype = ctypes.c_char_p
+_lib.sparkey_shard_phase_ms.argtypes = [_vp, ctypes.c_int32]
+_lib.sparkey_shard_phase_ms.restype = ctypes.c_double
+
+
+def shard_unique_id() -> bytes:
+    """An RCCL unique id (128 bytes) for sparkey_shard_comm_create; made on one rank, sent to all."""
+    buf = ctypes.create_string_buffer(128)
+    err = ctypes.create_string_buffer(512)
+    rc = _lib.sparkey_shard_comm_unique_id(buf, err, 512)
+    if rc != OK:
+        raise_for(rc, err.value.decode(errors="replace"))
+    return buf.raw
+
+
+def shard_geometry(log_header: bytes, file_len: int, opts, rank: int, world: int):
+    """(buf_lo, buf_hi, out_off, out_len): the log bytes rank `rank` holds and the .spi bytes it makes."""
+    v = [ctypes.c_uint64() for _ in range(4)]
+    err = ctypes.create_string_buffer(512)
+    rc = _lib.sparkey_shard_geometry(log_header, file_len, ctypes.byref(opts), rank, world,
+                                     *[ctypes.byref(x) for x in v], err, 512)
+    if rc != OK:
+        raise_for(rc, err.value.decode(errors="replace"))
+    return tuple(int(x.value) for x in v)
+
+
+class ShardComm:
+    """RCCL communicator of one rank of the sharded build (sparkey_shard_comm_create)."""
+
+    def __init__(self, unique_id: bytes, rank: int, world: int, device: int):
+        h = ctypes.c_void_p()
+        err = ctypes.create_string_buffer(512)
+        rc = _lib.sparkey_shard_comm_create(ctypes.byref(h), unique_id, rank, world, device, err, 512)
+        if rc != OK:
+            raise_for(rc, err.value.decode(errors="replace"))
+        self._h = h
+
+    def build(self, plan, log_header: bytes, file_len: int, d_buf: int, buf_lo: int, buf_hi: int, opts,
+              d_out: int, out_cap: int, stream: int = 0) -> BuildStats:
+        """One rank's whole sharded build (sparkey_shard_build)."""
+        stats = BuildStats()
+        err = ctypes.create_string_buffer(512)
+        rc = _lib.sparkey_shard_build(plan._h, self._h, log_header, file_len, ctypes.c_void_p(d_buf), buf_lo, buf_hi,
+                                      ctypes.byref(opts), ctypes.c_void_p(d_out), out_cap, ctypes.c_void_p(stream),
+                                      ctypes.byref(stats), err, 512)
+        if rc != OK:
+            raise_for(rc, err.value.decode(errors="replace"))
+        return stats
+
+    def phases(self):
+        n = _lib.sparkey_shard_phase_count(self._h)
+        return [(_lib.sparkey_shard_phase_name(self._h, i).decode(), _lib.sparkey_shard_phase_ms(self._h, i))
+                for i in range(n)]
+
+    def close(self) -> None:
+        if self._h:
+            _lib.sparkey_shard_comm_destroy(self._h)
+            self._h = None
 
 
 
@@ -166,7 +245,9 @@ for _name, (_args, _res) in _SIGS.items():
 EXPORTED = list(_SIGS) + ["sparkey_build_index_file", "sparkey_build_index_mem", "sparkey_index_size", "sparkey_plan_create",
             "sparkey_plan_build_device", "sparkey_plan_set_profiling", "sparkey_plan_stage_count",
             "sparkey_plan_stage_name", "sparkey_plan_stage_ms", "sparkey_plan_destroy", "sparkey_gpu_version",
-            "sparkey_strerror", "sparkey_release_cached_resources"]
+            "sparkey_strerror", "sparkey_release_cached_resources", "sparkey_shard_comm_unique_id",
+            "sparkey_shard_comm_create", "sparkey_shard_comm_destroy", "sparkey_shard_geometry", "sparkey_shard_build",
+            "sparkey_shard_phase_count", "sparkey_shard_phase_name", "sparkey_shard_phase_ms"]
 
 
 class SparkeyIOError(OSError):
@@ -182,7 +263,7 @@ class SparkeyGpuError(RuntimeError):
 
 
 _IO_CODES = {E_NOT_LOG, E_VERSION, E_CORRUPT_LOG, E_NO_FREE_SLOTS, E_HEADER, E_IO, E_UNSUPPORTED}
-_RUNTIME_CODES = {E_CORRUPT_DATA, E_VLQ}
+_RUNTIME_CODES = {E_CORRUPT_DATA, E_VLQ, E_CORRUPT_RECORD}
 
 
 def raise_for(code: int, msg: str):
@@ -201,9 +282,12 @@ def raise_for(code: int, msg: str):
     raise err
 
 
-def make_opts(hash_size=0, hash_seed=0, sparsity=0.0, max_memory=1 << 62, method=METHOD_IN_MEMORY, device=0):
+def make_opts(hash_size=0, hash_seed=0, sparsity=0.0, max_memory=1 << 62, method=METHOD_IN_MEMORY, device=0,
+              num_gpus=0):
+    """num_gpus > 1: sparkey_build_index_file / _mem shard the log over devices device .. device + num_gpus - 1
+    (SPARKEY_SHARD_TRANSPORT=threads-one-device: every rank on `device`, for tests on one GPU)."""
     return BuildOpts(hash_size, ctypes.c_int32(hash_seed).value, float(sparsity), int(max_memory), int(method),
-                     int(device))
+                     int(device), int(num_gpus), 0)
 
 
 def index_size(log_header: bytes, opts: BuildOpts) -> int:

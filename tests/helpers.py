@@ -77,3 +77,31 @@ def random_puts(n, seed=0, kmin=1, kmax=40, vmin=0, vmax=60, unique=True):
                 res.append((k, v))
         out = res
     return out
+
+
+# The reference's exception class per error code (include/sparkey_gpu.h; the JNI shim's mapping)
+_RUNTIME = {-5, -6, -10, -13}
+_ILLEGAL = {-11, -12}
+
+
+def java_class(code: int) -> str:
+    return "RuntimeException" if code in _RUNTIME else "IllegalArgumentException" if code in _ILLEGAL else "IOException"
+
+
+def same_error(native, log: bytes, seed: int = 1, **opts_kw):
+    """The oracle rejects the log and the GPU build rejects it with the same Java exception class."""
+    import oracle
+    try:
+        oracle.build_index(log, seed, **{k: v for k, v in opts_kw.items() if k in ("hash_size", "method")})
+    except oracle.OracleError as e:
+        want = e.code
+    else:
+        raise AssertionError("the oracle accepts the log")
+    try:
+        native.build_index_mem(log, native.make_opts(hash_seed=seed, **opts_kw))
+    except (OSError, RuntimeError, ValueError) as e:
+        got = getattr(e, "code", None)
+    else:
+        raise AssertionError("the GPU build accepts a log the oracle rejects (code %d)" % want)
+    assert java_class(got) == java_class(want), (got, want)
+    return got, want

@@ -4,10 +4,12 @@ scenarios (CorrectnessTest, LargeFilesTest, IndexHashTest, WriteHashBenchmark) a
 Integer/byte work: the bar is bit-exact.
 """
 import numpy as np
+import os
+
 import pytest
 
 import oracle
-from helpers import diff_report, index_header, key_value_puts, make_log, random_puts
+from helpers import diff_report, index_header, key_value_puts, make_log, random_puts, same_error
 
 pytestmark = pytest.mark.gpu
 
@@ -162,12 +164,10 @@ def test_errors(native):
         native.build_index_mem(trunc, opts)                        # dataEnd > file length
     bad = bytearray(log)
     bad[84] = 0xFF                                                 # corrupt first record header
-    with pytest.raises((OSError, RuntimeError)):
-        native.build_index_mem(bytes(bad), opts)
+    same_error(native, bytes(bad))
     bad = bytearray(log)
     bad[64] = 1                                                    # SNAPPY flag over NONE bytes: corrupt blocks
-    with pytest.raises(OSError):
-        native.build_index_mem(bytes(bad), opts)
+    same_error(native, bytes(bad))
 
 
 # --- framing edge cases: the speculative framing must fall back to the exact serial walk ---
@@ -199,8 +199,16 @@ def test_understated_max_key_len_is_an_error(native):
     import struct
     log = bytearray(make_log(key_value_puts(100)))
     struct.pack_into("<q", log, 40, 3)  # maxKeyLen := 3 < real key lengths: the reference throws
-    with pytest.raises((OSError, RuntimeError)):
-        native.build_index_mem(bytes(log), native.make_opts(hash_seed=1))
+    got, want = same_error(native, bytes(log))  # IndexOutOfBoundsException (SparkeyLogIterator.java:130)
+    assert got == want == native.E_CORRUPT_RECORD
+    for env in ({"SPARKEY_NO_UNIFORM": "1"}, {"SPARKEY_NO_FRAME3": "1"}, {"SPARKEY_SERIAL_FRAMING": "1"}):
+        os.environ.update(env)
+        try:
+            got, _ = same_error(native, bytes(log))
+        finally:
+            for k in env:
+                del os.environ[k]
+        assert got == native.E_CORRUPT_RECORD, env
 
 
 def test_header_hides_deletes(native):

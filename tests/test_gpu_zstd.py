@@ -11,6 +11,7 @@ import struct
 import pytest
 
 import oracle
+from helpers import same_error
 
 from snappy_log import CompressedLog, zstd_compress
 from test_compressed_oracle import _compressed, _ops
@@ -121,12 +122,10 @@ def test_errors(native):
     log = _compressed(ops, 256, codec="zstd")
     bad = bytearray(log)
     bad[84 + 1] ^= 0x01                                           # first frame's magic
-    with pytest.raises(OSError):
-        native.build_index_mem(bytes(bad), opts)
+    same_error(native, bytes(bad))
     bad = bytearray(log)
     struct.pack_into("<i", bad, 68, 16)                           # frames larger than the block size
-    with pytest.raises(OSError):
-        native.build_index_mem(bytes(bad), opts)
+    same_error(native, bytes(bad))
     cl = CompressedLog(256, codec="zstd", encoder=_streamed_frame)
     for _, k, v in ops:
         cl.put(k, v)
@@ -151,8 +150,7 @@ def test_errors(native):
         p = q + n
     assert n < 128
     bad[p] = n - 1
-    with pytest.raises(OSError):
-        native.build_index_mem(bytes(bad), opts)
+    same_error(native, bytes(bad))
 
 
 @pytest.mark.parametrize("block_size", [1024, 16384])
@@ -170,3 +168,104 @@ def test_parallel_directory_zstd(native, block_size, spacing, monkeypatch, capfd
     monkeypatch.setenv("SPARKEY_SNAPPY_SERIAL_DIR", "1")
     serial, _ = native.build_index_mem(log, native.make_opts(hash_seed=77))
     assert got == serial
+
+
+def _checksummed(data: bytes) -> bytes:
+    """zstd_compress's frame with Content_Checksum set: FHD bit 2 and the low 32 bits of XXH64(data)
+    appended (RFC 8878 §3.1.1), which libzstd verifies on decode."""
+    import xxhash
+    f = bytearray(zstd_compress(data))
+    assert struct.unpack_from("<I", f, 0)[0] == 0xFD2FB528 and not f[4] & 4
+    f[4] |= 4
+    return bytes(f) + struct.pack("<I", xxhash.xxh64(data).intdigest() & 0xFFFFFFFF)
+
+
+def _zlog_enc(ops, block_size, encoder):
+    cl = CompressedLog(block_size, file_identifier=0x2468, codec="zstd", encoder=encoder)
+    for op, k, v in ops:
+        if op == "put":
+            cl.put(k, v)
+        else:
+            cl.delete(k)
+    return cl.finish()
+
+
+def _frames(log: bytes):
+    """(frame offset, frame length) of every block of a compressed log (VLQ size prefix per block)."""
+    data_end = struct.unpack_from("<q", log, 32)[0]
+    p, out = 84, []
+    while p < data_end:
+        n, shift = 0, 0
+        while True:
+            c = log[p]
+            p += 1
+            n |= (c & 0x7F) << shift
+            shift += 7
+            if c < 0x80:
+                break
+        out.append((p, n))
+        p += n
+    return out
+
+
+def _same_outcome(native, log, seed=4321):
+    """The GPU build and the oracle (libzstd) either both reject the log or build the same bytes."""
+    try:
+        want = oracle.build_index(log, seed)
+    except oracle.OracleError:
+        want = None
+    opts = native.make_opts(hash_seed=seed)
+    if want is None:
+        with pytest.raises((OSError, RuntimeError)):
+            native.build_index_mem(log, opts)
+    else:
+        got, _ = native.build_index_mem(log, opts)
+        assert got == want
+    return want is not None
+
+
+@pytest.mark.parametrize("block_size", [512, 8192])
+def test_checksummed_frames(native, block_size):
+    """Frames carrying Content_Checksum build like the oracle; one flipped checksum byte is rejected
+    (libzstd rejects it too)."""
+    rng = random.Random(block_size + 3)
+    ops = _ops(rng, 800, 10 ** 9, 0.1, 120)
+    log = _zlog_enc(ops, block_size, _checksummed)
+    check(native, log)
+    frames = _frames(log)
+    for off, n in (frames[0], frames[len(frames) // 2], frames[-1]):
+        bad = bytearray(log)
+        bad[off + n - 2] ^= 0x10                      # inside the 4 checksum bytes
+        same_error(native, bytes(bad), 4321)
+
+
+def test_skippable_frames(native):
+    """A skippable frame after a block's frame is skipped; one whose size runs past the block (or wraps
+    the 32-bit offset: 0xFFFFFFF8) is a corrupt log, not a hang."""
+    rng = random.Random(21)
+    ops = _ops(rng, 600, 10 ** 9, 0.0, 100)
+    good = _zlog_enc(ops, 1024, lambda d: zstd_compress(d) + struct.pack("<II", 0x184D2A53, 3) + b"abc")
+    check(native, good)
+    for size in (0xFFFFFFF8, 0xFFFFFFFF, 4):
+        bad = _zlog_enc(ops, 1024, lambda d, s=size: zstd_compress(d) + struct.pack("<II", 0x184D2A50, s))
+        same_error(native, bad, 4321)
+
+
+def test_byte_flips_inside_frames(native):
+    """Single flipped bytes at random positions inside frames: the GPU build rejects exactly the logs
+    the oracle (libzstd) rejects, and otherwise builds the oracle's bytes."""
+    rng = random.Random(77)
+    ops = []
+    for i in range(1500):
+        v = (b"value-%d-" % (i % 23)) * rng.randrange(1, 12) + rng.randbytes(rng.randrange(0, 40))
+        ops.append(("put", b"key_%d" % rng.randrange(1200), v))
+    log = _zlog(ops, 4096, level=9)
+    frames = _frames(log)
+    ok = 0
+    for t in range(40):
+        off, n = frames[rng.randrange(len(frames))]
+        pos = off + rng.randrange(n)
+        bad = bytearray(log)
+        bad[pos] ^= 1 << rng.randrange(8)
+        ok += _same_outcome(native, bytes(bad))
+    assert ok < 40  # (most flips break the stream; the point is that both sides agree)

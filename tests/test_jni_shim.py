@@ -1,0 +1,148 @@
+"""The JNI shim (sparkey-java_amd/jni/sparkey_gpu_jni.c) compiled against a test-only stand-in jni.h
+(tests/jni/jni.h; this image has no JDK) and driven by a recording JNIEnv (tests/jni/harness.c):
+
+  * argument conversion: every Java argument reaches sparkey_build_index_file's options unchanged, and
+    the stats long[] is filled in the documented order (or left alone when null / too short);
+  * exception mapping: every SPARKEY_E_* code throws the reference's class (IOException for LogHeader /
+    file errors, RuntimeException for the iterator's and put/delete's, IllegalArgumentException for
+    options), with the C-ABI's message;
+  * against the real library: the errors decided before any device work (CPU), and a real build (GPU).
+
+The reference classes: LogHeader.java:57-83 and CommonHeader.java:38-43 (IOException),
+SparkeyLogIterator.java:117-136 and IndexHash.java:484,494,613,624 (RuntimeException), Util.java:181,217.
+"""
+import json
+import os
+import struct
+import subprocess
+
+import pytest
+
+import oracle
+from helpers import key_value_puts, make_log
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+JNI = os.path.join(ROOT, "tests", "jni")
+SHIM = os.path.join(ROOT, "sparkey-java_amd", "jni", "sparkey_gpu_jni.c")
+LIBDIR = os.path.join(ROOT, "sparkey-java_amd", "lib")
+
+IOE, RTE, IAE = "java/io/IOException", "java/lang/RuntimeException", "java/lang/IllegalArgumentException"
+EXPECTED = {-1: IOE, -2: IOE, -3: IOE, -4: IOE, -5: RTE, -6: RTE, -7: IOE, -8: IOE, -9: IOE, -10: RTE, -11: IAE,
+            -12: IAE, -13: RTE}
+
+
+def _cc(out, *srcs, libs=()):
+    cmd = ["gcc", "-O1", "-Wall", "-Werror", "-I", JNI, "-I", os.path.join(ROOT, "include"), *srcs, "-o", out, *libs]
+    subprocess.run(cmd, check=True, capture_output=True)
+    return out
+
+
+@pytest.fixture(scope="module")
+def fake_harness(tmp_path_factory):
+    d = tmp_path_factory.mktemp("jni")
+    return _cc(str(d / "harness_fake"), os.path.join(JNI, "harness.c"), SHIM, os.path.join(JNI, "fake_sparkey.c"))
+
+
+@pytest.fixture(scope="module")
+def real_harness(tmp_path_factory, native):
+    d = tmp_path_factory.mktemp("jni_real")
+    return _cc(str(d / "harness_real"), os.path.join(JNI, "harness.c"), SHIM,
+               libs=["-L", LIBDIR, "-lsparkey_gpu", "-Wl,-rpath," + LIBDIR])
+
+
+def _run(harness, args, env=None):
+    e = dict(os.environ)
+    e["LD_LIBRARY_PATH"] = "/opt/rocm/lib:" + e.get("LD_LIBRARY_PATH", "")
+    e.update(env or {})
+    p = subprocess.run([harness] + [str(a) for a in args], capture_output=True, text=True, env=e, timeout=300)
+    assert p.returncode == 0, p.stderr
+    lines = [json.loads(x) for x in p.stdout.splitlines() if x.startswith("{")]
+    call = next((x["call"] for x in lines if "call" in x), None)
+    return call, lines[-1]
+
+
+def _args(log="in.spl", index="out.spi", hash_size=8, sparsity=2.5, fsync=1, seed=-12345, max_memory=1 << 40,
+          method=2, device=3, num_gpus=4, stats_len=9):
+    return [log, index, hash_size, sparsity, fsync, seed, max_memory, method, device, num_gpus, stats_len]
+
+
+def test_argument_conversion(fake_harness):
+    call, res = _run(fake_harness, _args())
+    assert call == {"log": "in.spl", "index": "out.spi", "hash_size": 8, "hash_seed": -12345, "sparsity": 2.5,
+                    "max_memory": 1 << 40, "method": 2, "device": 3, "num_gpus": 4, "fsync": 1}
+    assert res["exception"] is None
+    assert res["stats"] == [11, 10, 1, 9, 13, 5, 2, 1, 7]        # numRecords .. totalDisplacement
+    assert res["strings_acquired"] == res["strings_released"] == 2
+    call, _ = _run(fake_harness, _args(hash_size=0, sparsity=0.0, fsync=0, method=0, device=0, num_gpus=0))
+    assert (call["hash_size"], call["sparsity"], call["fsync"], call["method"], call["num_gpus"]) == (0, 0.0, 0, 0, 0)
+
+
+@pytest.mark.parametrize("stats_len", [-1, 0, 8, 12])
+def test_stats_array_lengths(fake_harness, stats_len):
+    _, res = _run(fake_harness, _args(stats_len=stats_len))
+    assert res["exception"] is None
+    if stats_len >= 9:
+        assert res["stats"][:9] == [11, 10, 1, 9, 13, 5, 2, 1, 7] and res["stats"][9:] == [-1] * (stats_len - 9)
+    else:  # null or too short: left alone
+        assert res["stats"] == [-1] * max(0, stats_len)
+
+
+@pytest.mark.parametrize("code", sorted(EXPECTED))
+def test_exception_class_per_code(fake_harness, code):
+    _, res = _run(fake_harness, _args(), env={"FAKE_RC": str(code)})
+    assert res["exception"] == {"class": EXPECTED[code], "message": "fake failure %d" % code}
+    assert res["stats"] == [-1] * 9                               # nothing written on failure
+    assert res["strings_acquired"] == res["strings_released"] == 2
+
+
+def test_real_library_errors_before_device_work(real_harness, tmp_path):
+    """Decided from the log file and its header (LogHeader.read, IndexHash.createNew's options):
+    no GPU is touched, so these run on the CPU too."""
+    out = str(tmp_path / "x.spi")
+    _, res = _run(real_harness, _args(log=str(tmp_path / "missing.spl"), index=out))
+    assert res["exception"]["class"] == IOE and "cannot open log file" in res["exception"]["message"]
+    (tmp_path / "junk.spl").write_bytes(b"\0" * 200)
+    _, res = _run(real_harness, _args(log=str(tmp_path / "junk.spl"), index=out))
+    assert res["exception"] == {"class": IOE, "message": "File is not a Sparkey log file"} or (
+        res["exception"]["class"] == IOE and "not a Sparkey log" in res["exception"]["message"])
+    log = make_log(key_value_puts(50))
+    (tmp_path / "cut.spl").write_bytes(log[:-10])                   # dataEnd > file length (LogHeader.java:81-83)
+    _, res = _run(real_harness, _args(log=str(tmp_path / "cut.spl"), index=out))
+    assert res["exception"]["class"] == IOE and "expected at least" in res["exception"]["message"]
+    (tmp_path / "ok.spl").write_bytes(log)
+    _, res = _run(real_harness, _args(log=str(tmp_path / "ok.spl"), index=out, hash_size=5))
+    assert res["exception"]["class"] == IAE  # (no Java caller can pass it: HashType is an enum)
+    assert not os.path.exists(out)
+
+
+@pytest.mark.gpu
+def test_real_library_build_through_the_shim(real_harness, tmp_path):
+    """One real build through the shim: the .spi equals the oracle's and statsOut carries its header."""
+    log = make_log(key_value_puts(5000))
+    lp, sp = str(tmp_path / "a.spl"), str(tmp_path / "a.spi")
+    with open(lp, "wb") as f:
+        f.write(log)
+    _, res = _run(real_harness, _args(log=lp, index=sp, hash_size=0, sparsity=0.0, seed=77, method=1, device=0,
+                                      num_gpus=0))
+    assert res["exception"] is None
+    want = oracle.build_index(log, 77)
+    assert open(sp, "rb").read() == want
+    h = struct.unpack_from("<qqqqq", want, 44)                      # numPuts, garbage, numEntries (+ sizes)
+    assert res["stats"][1] == 5000 and res["stats"][3] == h[2] and res["stats"][4] == struct.unpack_from("<q", want, 76)[0]
+
+
+@pytest.mark.gpu
+def test_real_library_iterator_error_is_runtime(real_harness, tmp_path):
+    """A key longer than the header's maxKeyLen: IndexOutOfBoundsException from stream.read(keyBuf, 0,
+    keyLen) in the reference (SparkeyLogIterator.java:130), a RuntimeException through the shim."""
+    log = bytearray(make_log(key_value_puts(100)))
+    struct.pack_into("<q", log, 40, 3)                              # maxKeyLen := 3 (keys are 4-6 bytes)
+    lp = str(tmp_path / "k.spl")
+    with open(lp, "wb") as f:
+        f.write(bytes(log))
+    with pytest.raises(oracle.OracleError) as e:
+        oracle.build_index(bytes(log), 5)
+    assert e.value.code == -13
+    _, res = _run(real_harness, _args(log=lp, index=str(tmp_path / "k.spi"), hash_size=0, seed=5, method=1, device=0,
+                                      num_gpus=0))
+    assert res["exception"]["class"] == RTE and "Corrupt log record" in res["exception"]["message"]
