@@ -903,7 +903,11 @@ static int32_t open_zstd(build_ctx* c, const uint8_t* log, int64_t data_end, int
 /* The virtual stream of a SNAPPY log: blocks VLQ(compressedSize) || snappy bytes from offset 84 to
  * dataEnd (CompressedOutputStream.flush, CompressedOutputStream.java:47-58; CompressedReader.fetchBlock,
  * CompressedReader.java:66-74). */
-static int32_t open_compressed(build_ctx* c, const uint8_t* log, int64_t data_end, uint8_t** vbuf) {
+static int32_t open_compressed(build_ctx* c, const uint8_t* log, int64_t data_end, int64_t max_block, uint8_t** vbuf) {
+  /* the reader's buffers (CompressedReader.java:40-49): compressedBuf holds
+   * Snappy.maxCompressedLength(maxBlockSize) = 32 + n + n / 6 bytes, uncompressedBuf maxBlockSize; a
+   * block that does not fit fails inside fetchBlock (:51-60) */
+  const int64_t max_comp = 32 + max_block + max_block / 6;
   int64_t nblk = 0, cap_b = 64, total = 0, p = LOG_HEADER_SIZE;
   c->blk_pos = (int64_t*)malloc(sizeof(int64_t) * (size_t)cap_b);
   c->blk_voff = (int64_t*)malloc(sizeof(int64_t) * (size_t)cap_b);
@@ -914,13 +918,14 @@ static int32_t open_compressed(build_ctx* c, const uint8_t* log, int64_t data_en
     int32_t clen;
     int32_t rc = oracle_vlq_read(log, data_end, &q, &clen);
     if (rc) { free(ulens); return rc; }
-    if (clen < 0 || q + clen > data_end) { free(ulens); return ORACLE_E_CORRUPT_LOG; }
+    if (clen < 0 || q + clen > data_end || clen > max_comp) { free(ulens); return ORACLE_E_CORRUPT_LOG; }
     int64_t ulen = 0, r = q;
     for (int shift = 0;; shift += 7) {
       if (r >= q + clen || shift > 28) { free(ulens); return ORACLE_E_CORRUPT_LOG; }
       ulen |= (int64_t)(log[r] & 0x7f) << shift;
       if (!(log[r++] & 0x80)) break;
     }
+    if (ulen > max_block) { free(ulens); return ORACLE_E_CORRUPT_LOG; }
     if (nblk == cap_b) {
       cap_b *= 2;
       c->blk_pos = (int64_t*)realloc(c->blk_pos, sizeof(int64_t) * (size_t)cap_b);
@@ -976,7 +981,7 @@ int64_t oracle_build_index(const uint8_t* log, int64_t log_len, int32_t hash_siz
      * bad block is a RuntimeException there */
     if (lh.compression_block_size < 0) rc = ORACLE_E_CORRUPT_RECORD;
     else if (lh.compression_type == 2) rc = open_zstd(&c, log, lh.data_end, lh.compression_block_size, &vbuf);
-    else rc = open_compressed(&c, log, lh.data_end, &vbuf);
+    else rc = open_compressed(&c, log, lh.data_end, lh.compression_block_size, &vbuf);
     if (rc == ORACLE_E_CORRUPT_LOG) rc = ORACLE_E_CORRUPT_RECORD;
     if (rc) { free(c.blk_pos); free(c.blk_voff); set_err(err, err_len, err_msg(rc)); return rc; }
   }

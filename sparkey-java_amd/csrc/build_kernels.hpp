@@ -207,6 +207,9 @@ struct BuildParams {
   int32_t f3_short;  // k_frame3 (frame3_kernels.hip): steps of the short walk
   int32_t f3_cover;  // k_frame3: mark the starts the short walk reached (windows hold several true starts)
   int32_t f3_stop;   // SPARKEY_FRAME3_STOP: k_frame3 gives up after this phase (instruction counts by phase)
+  int32_t f3_rgn;    // k_frame3: staged region bytes per wave (W * C + fr_look + 16, 16-byte multiple)
+  int32_t f3_cand_cap;  // k_frame3: candidates (and records) per wave its LDS list holds (<= 512)
+  int32_t f3_surv_cap;  // k_frame3: chain heads per wave after the short walk (<= 64, one long walk per lane)
   // uniform-stride framing (k_frame_uniform): uni_n records of uni_rec bytes from fr_entry
   uint64_t uni_n;
   int64_t uni_rec;
@@ -291,7 +294,7 @@ void launch_dense_slabs(const BuildParams& P, hipStream_t s);
 void launch_frame_uniform(const BuildParams& P, hipStream_t s, StageTimer* tm);
 void launch_frame2(const BuildParams& P, hipStream_t s, StageTimer* tm);  // frame2_kernels.hip
 void launch_frame3(const BuildParams& P, hipStream_t s, StageTimer* tm);  // frame3_kernels.hip
-bool frame3_fits(const BuildParams& P, double mean_record, double pass);
+bool frame3_fits(BuildParams& P, double mean_record, double pass);
 uint32_t frame3_lds_per_wave(const BuildParams& P);
 // framing paths: 0 k_frame, 1 serial walk, 2 k_frame_uniform, 3 k_frame2, 4 k_frame3; the
 // speculative ones with per-wave slabs

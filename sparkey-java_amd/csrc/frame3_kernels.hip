@@ -50,18 +50,18 @@ namespace sk {
 
 namespace {
 
-constexpr int kF3CandCap = 512;  // candidates per wave (u16 region offsets)
-constexpr int kF3SurvCap = 64;   // chain heads after the short walk per wave (one long walk per lane)
 constexpr int kF3Lcap = 16;      // record starts a survivor lists inside its chunk
-constexpr int kF3RecCap = 512;   // records per wave hashed from the LDS list (else: slab overflow)
 constexpr unsigned kF3Caps = 64u;  // Status.spec_fail: a list cap was exceeded (k_frame redoes it)
 
-// Scratch after the staged region (bytes): candidate list, later the wave's record list; head
-// starts / exits / counts / per-chunk choice; the heads' record lists, earlier the screen bitmap and
-// then the short walk's reached-start bitmap (one bit per region byte).
-constexpr int kF3OffMeta = 2 * kF3CandCap;
-constexpr int kF3OffLists = kF3OffMeta + kF3SurvCap * 5 + 128;
-constexpr int kF3ListBytes = kF3SurvCap * kF3Lcap * 2;
+// Scratch after the staged region (bytes), sized on the host so that four waves of a workgroup and
+// four workgroups fit a CU's LDS where the log allows (P.f3_cand_cap candidates, P.f3_surv_cap heads):
+// candidate list, later the wave's record list (u16 each); head starts / exits / counts / per-chunk
+// choice; the heads' record lists, earlier the screen bitmap and then the short walk's reached-start
+// bitmap (one bit per region byte).
+__host__ __device__ __forceinline__ int f3_off_meta(int cand_cap) { return 2 * cand_cap; }
+__host__ __device__ __forceinline__ int f3_off_lists(int cand_cap, int surv_cap) {
+  return (f3_off_meta(cand_cap) + surv_cap * 5 + 128 + 7) & ~7;
+}
 
 // One record step from region offset rp (screen rules, canonical one-byte VLQs): the next start,
 // or -1 when the bytes at rp are no plausible header.
@@ -88,10 +88,12 @@ __device__ __forceinline__ void frame3_region(const BuildParams& P, const uint64
   const int nw = (int)min((uint64_t)W, kf + P.fr_nchunks - k0);
   const int64_t R0 = (int64_t)(k0 << cs);
   const int64_t RLEN = ((int64_t)nw << cs) + LOOK + 16;
+  const int kF3CandCap = P.f3_cand_cap, kF3SurvCap = P.f3_surv_cap, kF3RecCap = P.f3_cand_cap;
+  const int kF3OffLists = f3_off_lists(kF3CandCap, kF3SurvCap);
   uint8_t* rgn = lds;
-  uint8_t* scr = lds + P.fr_rgn_bytes;
+  uint8_t* scr = lds + P.f3_rgn;
   uint16_t* cand = reinterpret_cast<uint16_t*>(scr);             // candidates, then the record list
-  uint16_t* s_start = reinterpret_cast<uint16_t*>(scr + kF3OffMeta);
+  uint16_t* s_start = reinterpret_cast<uint16_t*>(scr + f3_off_meta(kF3CandCap));
   uint16_t* s_exit = s_start + kF3SurvCap;                          // 0xffff: died in the long walk
   uint8_t* s_cnt = reinterpret_cast<uint8_t*>(s_exit + kF3SurvCap);
   int8_t* s_sel = reinterpret_cast<int8_t*>(s_cnt + kF3SurvCap);    // per chunk: chosen head, entry index
@@ -131,21 +133,24 @@ __device__ __forceinline__ void frame3_region(const BuildParams& P, const uint64
     }
   };
 
-  // ---- stage [R0, R0 + RLEN): every 1 KiB row in flight at once, straight into LDS ----
+  // ---- stage [R0, R0 + RLEN): every 1 KiB row in flight at once, straight into LDS (the last row's
+  //      lanes past the region masked off: the region is a 16-byte multiple, not whole rows) ----
   {
     const int nvec = (int)((RLEN + 15) >> 4);
     if (R0 + 16ll * nvec <= log_len) {
       const uint4* src = reinterpret_cast<const uint4*>(P.log + R0);
       if (P.uni_nt) {  // non-temporal: the log is read once
         for (int v0 = 0; v0 < nvec; v0 += 64)
-          __builtin_amdgcn_global_load_lds(
-              (const __attribute__((address_space(1))) void*)(src + min(v0 + lane, nvec - 1)),
-              (__attribute__((address_space(3))) void*)(rgn + 16u * (uint32_t)v0), 16, 0, 2);
+          if (v0 + lane < nvec)
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + v0 + lane),
+                                             (__attribute__((address_space(3))) void*)(rgn + 16u * (uint32_t)v0), 16,
+                                             0, 2);
       } else {
         for (int v0 = 0; v0 < nvec; v0 += 64)
-          __builtin_amdgcn_global_load_lds(
-              (const __attribute__((address_space(1))) void*)(src + min(v0 + lane, nvec - 1)),
-              (__attribute__((address_space(3))) void*)(rgn + 16u * (uint32_t)v0), 16, 0, 0);
+          if (v0 + lane < nvec)
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + v0 + lane),
+                                             (__attribute__((address_space(3))) void*)(rgn + 16u * (uint32_t)v0), 16,
+                                             0, 0);
       }
     } else {
       for (int v = lane; v < nvec; v += 64)
@@ -600,21 +605,40 @@ __global__ __launch_bounds__(64 * kFrameWaves) void k_frame3(BuildParams P, uint
 // or the screen bitmap).
 uint32_t frame3_lds_per_wave(const BuildParams& P) {
   const size_t bitmap = (size_t)P.fr_w * (size_t)((std::min<int64_t>(1ll << P.fr_cshift, P.max_rec_len) + 63) / 64) * 8;
-  const size_t reached = (size_t)((((int64_t)P.fr_w << P.fr_cshift) + P.fr_look + 31) / 32 + 1) * 4;
-  const size_t scratch = (size_t)kF3OffLists + std::max<size_t>(std::max<size_t>(bitmap, reached), (size_t)kF3ListBytes);
-  return (uint32_t)(((size_t)P.fr_rgn_bytes + scratch + 15) & ~(size_t)15);
+  const size_t reached = P.f3_cover ? (size_t)((((int64_t)P.fr_w << P.fr_cshift) + P.fr_look + 31) / 32 + 1) * 4 : 0;
+  const size_t lists = (size_t)P.f3_surv_cap * kF3Lcap * 2;
+  const size_t scratch =
+      (size_t)f3_off_lists(P.f3_cand_cap, P.f3_surv_cap) + std::max<size_t>(std::max<size_t>(bitmap, reached), lists);
+  return (uint32_t)(((size_t)P.f3_rgn + scratch + 15) & ~(size_t)15);
 }
 
-bool frame3_fits(const BuildParams& P, double mean_record, double pass) {
-  // every chunk's records must fit a head's list, a wave's records the record list, and a wave's
-  // candidates (pass = the chance that a random byte pair passes the screen) the candidate list
+// The LDS layout of k_frame3 for this geometry (P.fr_w, fr_cshift, fr_look, f3_cover set): the region
+// and the list caps.  The candidate cap is 2.2x the expected candidates of a wave (pass = the chance
+// that a random byte pair passes the screen) plus 32, and at least 1.7x its expected records + 32;
+// when that allows, it is trimmed so that 16 waves (4 workgroups) fit a CU.  False when the lists
+// cannot hold what the header's mean record implies (k_frame frames such logs).
+bool frame3_fits(BuildParams& P, double mean_record, double pass) {
   const double C = (double)(1ll << P.fr_cshift);
   if (!P.fr_fast || P.max_rec_len > 4096 || P.fr_cshift < 7) return false;
   if (mean_record <= 0.0 || C / mean_record > 0.6 * kF3Lcap) return false;
-  if ((double)P.fr_w * C / mean_record > 0.6 * kF3RecCap) return false;
-  if ((double)P.fr_w * (double)std::min<int64_t>(1ll << P.fr_cshift, P.max_rec_len) * pass > 0.6 * kF3CandCap)
-    return false;
-  return ((int64_t)P.fr_w << P.fr_cshift) + P.fr_look + 16 < 32768;  // 15-bit region offsets
+  if (((int64_t)P.fr_w << P.fr_cshift) + P.fr_look + 16 >= 32768) return false;  // 15-bit region offsets
+  P.f3_rgn = (int32_t)((((int64_t)P.fr_w << P.fr_cshift) + P.fr_look + 16 + 15) & ~15ll);
+  const double recs = (double)P.fr_w * C / mean_record;
+  const double cands = (double)P.fr_w * (double)std::min<int64_t>(1ll << P.fr_cshift, P.max_rec_len) * pass + P.fr_w;
+  const int need = (int)std::ceil(std::max(2.2 * cands + 32.0, 1.7 * recs + 32.0));
+  if (need > 512) return false;
+  // heads: about one per chunk plus a few false survivors; one long walk per lane
+  P.f3_surv_cap = std::min(64, std::max(32, (2 * P.fr_w + 8 + 7) & ~7));
+  P.f3_cand_cap = 512;
+  // the largest cap >= need (16-multiple) that keeps 4 workgroups of 4 waves (+16 B static) in 160 KiB
+  // of LDS with 512-byte allocation granules
+  for (int cap = 512; cap >= need; cap -= 16) {
+    P.f3_cand_cap = cap;
+    const uint64_t wg = ((uint64_t)frame3_lds_per_wave(P) * kFrameWaves + 16 + 511) & ~511ull;
+    if (wg * 4 <= 160 * 1024) return true;
+  }
+  P.f3_cand_cap = 512;  // (fewer waves per CU)
+  return true;
 }
 
 void launch_frame3(const BuildParams& P, hipStream_t s, StageTimer* tm) {

@@ -584,15 +584,15 @@ static bool want_frame3(BuildParams& P, const LogHdr& lh, int64_t entry, int64_t
   // (more with DELETEs); the short walk's K steps leave p^K of the false starts
   const double pk = std::min(1.0, (double)(Q.max_key_len + 1) / 256.0) * std::min(1.0, (double)(Q.max_value_len + 1) / 256.0) +
                     (Q.no_deletes ? 0.0 : std::min(1.0, (double)(Q.max_key_len + 1) / 256.0) / 256.0);
-  if (!frame3_fits(Q, mean, pk)) return false;
-  Q.f3_short = pk < 0.12 ? 2 : pk < 0.3 ? 3 : 4;
-  if (const char* v = getenv("SPARKEY_FRAME3_SHORT")) Q.f3_short = std::max(1, std::min(4, atoi(v)));
-  Q.f3_stop = getenv("SPARKEY_FRAME3_STOP") ? atoi(getenv("SPARKEY_FRAME3_STOP")) : -1;
   // a candidate window (maxRecLen bytes) holds about maxRecLen / mean true starts, all on one chain:
   // when that is well above one, the starts reached by others are marked so that only chain heads
   // walk on (SPARKEY_FRAME3_COVER=0/1 forces it)
   Q.f3_cover = (double)Q.max_rec_len > 1.5 * mean ? 1 : 0;
   if (const char* v = getenv("SPARKEY_FRAME3_COVER")) Q.f3_cover = atoi(v) ? 1 : 0;
+  if (!frame3_fits(Q, mean, pk)) return false;
+  Q.f3_short = pk < 0.12 ? 2 : pk < 0.3 ? 3 : 4;
+  if (const char* v = getenv("SPARKEY_FRAME3_SHORT")) Q.f3_short = std::max(1, std::min(4, atoi(v)));
+  Q.f3_stop = getenv("SPARKEY_FRAME3_STOP") ? atoi(getenv("SPARKEY_FRAME3_STOP")) : -1;
   P = Q;
   return true;
 }
