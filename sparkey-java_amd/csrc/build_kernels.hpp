@@ -218,6 +218,8 @@ struct BuildParams {
   uint32_t uni_nt;        // framing kernels: non-temporal LDS-DMA of the log (SPARKEY_FRAME_NO_NT: default policy)
   // k_frame_uniform as partition pass 1: digit d's entries at ent3[d * p1_region, + p1_fill[d])
   uint64_t p1_region;   // 0 = off
+  int32_t p1_kernel;    // with p1_region: k_part1_regions fills the regions from the slabs (else the framing did)
+  int32_t p1_pad;
   int32_t p2_sorted;    // k_part2s: per-(bucket, slot) counts in the same pass + the carry functions
   int32_t p2_fixed;     // k_part2s in one pass: bucket b's entries at ent2[b * kPlaceLdsMax, + bcount[b])
   int32_t fold_stats;   // k_place_lds leaves calculateMaxDisplacement's per-bucket parts (no k_stats pass)
@@ -295,10 +297,12 @@ void launch_frame_uniform(const BuildParams& P, hipStream_t s, StageTimer* tm);
 void launch_frame2(const BuildParams& P, hipStream_t s, StageTimer* tm);  // frame2_kernels.hip
 void launch_frame3(const BuildParams& P, hipStream_t s, StageTimer* tm);  // frame3_kernels.hip
 bool frame3_fits(BuildParams& P, double mean_record, double pass);
+void launch_frame_lane(const BuildParams& P, hipStream_t s, StageTimer* tm);  // frame_lane_kernels.hip
+bool frame_lane_supported(const BuildParams& P);
 uint32_t frame3_lds_per_wave(const BuildParams& P);
 // framing paths: 0 k_frame, 1 serial walk, 2 k_frame_uniform, 3 k_frame2, 4 k_frame3; the
 // speculative ones with per-wave slabs
-__host__ __device__ inline bool slab_framing(int path) { return path == 0 || path == 3 || path == 4; }
+__host__ __device__ inline bool slab_framing(int path) { return path == 0 || path == 3 || path == 4 || path == 5; }
 void launch_place_fast(const BuildParams& P, hipStream_t s, StageTimer* tm);
 void launch_place_buckets(const BuildParams& P, hipStream_t s);
 // fallbacks and shared stages (build_kernels.hip)

@@ -122,7 +122,8 @@ __device__ __forceinline__ void frame3_region(const BuildParams& P, const uint64
         __builtin_amdgcn_s_sleep(2);
       }
     }
-    return (int64_t)__shfl(extv, 0, 64);
+    return (int64_t)(((unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(extv >> 32)) << 32) |
+                     (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)extv));
   };
   // every return below publishes the wave's exit first (successors wait on it): on a failure, any
   // value (the host redoes the framing)
@@ -221,13 +222,8 @@ __device__ __forceinline__ void frame3_region(const BuildParams& P, const uint64
         }
       }
       const uint32_t c = (uint32_t)__builtin_popcountll(m);
-      uint32_t incl = c;
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t t = __shfl_up(incl, o, 64);
-        if (lane >= o) incl += t;
-      }
-      const int32_t tot = (int32_t)__shfl(incl, 63, 64);
+      const uint32_t incl = wave_incl_sum_u32(c);
+      const int32_t tot = __builtin_amdgcn_readlane((int)incl, 63);
       if (T + tot > kF3CandCap) {
         over = true;
         break;
@@ -372,7 +368,7 @@ __device__ __forceinline__ void frame3_region(const BuildParams& P, const uint64
     if (lane < nw) c_first[lane] = 0xff;
     wave_sync();
     const int32_t hc = lane < S ? ((int32_t)s_start[lane] >> cs) : 127;
-    const int32_t pc = __shfl_up(hc, 1, 64), nc = __shfl_down(hc, 1, 64);
+    const int32_t pc = wave_prev_i32(hc, -1), nc = wave_next_i32(hc, -1);
     if (lane < S && (lane == 0 || pc != hc)) c_first[hc] = (uint8_t)lane;
     if (lane < S && (lane == S - 1 || nc != hc)) c_last[hc] = (uint8_t)lane;
     wave_sync();
@@ -441,7 +437,7 @@ __device__ __forceinline__ void frame3_region(const BuildParams& P, const uint64
         if (myx < 0) bad = true;
       }
       const int32_t kx = myx >= 0 ? myx : (conv ? cx : UNK);
-      const int32_t inx = __shfl_up(kx, 1, 64);
+      const int32_t inx = wave_prev_i32(kx, UNK);
       const bool take = lane >= 1 && lane < nw && ent == UNK && inx != UNK;
       if (take) ent = inx;
       if (!__any(take || (lane < nw && myx == UNK && ent != UNK && !bad))) break;
@@ -452,7 +448,7 @@ __device__ __forceinline__ void frame3_region(const BuildParams& P, const uint64
   pre = lane < nw && ent != UNK && !bad;
   int32_t early = -1;
   {
-    const int32_t lastx = __shfl(myx >= 0 ? myx : (conv ? cx : UNK), nw - 1, 64);
+    const int32_t lastx = __builtin_amdgcn_readlane(myx >= 0 ? myx : (conv ? cx : UNK), nw - 1);
     if (wv > 0 && lastx >= 0) {
       early = lastx;
       if (lane == 0) granule_store(&P.exit_desc[wv], (unsigned long long)(R0 + early) | kReady);
@@ -469,7 +465,7 @@ __device__ __forceinline__ void frame3_region(const BuildParams& P, const uint64
       }
     if (n0 != 1) spec_e0 = -1;
   }
-  spec_e0 = __shfl(spec_e0, 0, 64);
+  spec_e0 = __builtin_amdgcn_readfirstlane(spec_e0);
   bool spec = spec_e0 >= 0;
   int64_t ext = wv == 0 ? P.fr_entry : (spec ? R0 + spec_e0 : wait_prev());
   mark(4);
@@ -479,9 +475,9 @@ __device__ __forceinline__ void frame3_region(const BuildParams& P, const uint64
     const int64_t e0 = ext - R0;
     resolve(e0 < 0 || e0 > 0x7fff ? UNK : (int32_t)e0);
     // every chunk resolved, and each exit the next chunk's entry
-    const int32_t nxt = __shfl_down(ent, 1, 64);
+    const int32_t nxt = wave_next_i32(ent, UNK);
     const bool broken = lane < nw && (bad || myx < 0 || (lane + 1 < nw && nxt != myx));
-    const int32_t wexit = __shfl(myx, nw - 1, 64);
+    const int32_t wexit = __builtin_amdgcn_readlane(myx, nw - 1);
     if (__any(broken) || (early >= 0 && early != wexit)) {
       if (spec) {  // the guessed entry may be wrong: decide on the published one
         const int64_t real = wait_prev();
@@ -499,13 +495,8 @@ __device__ __forceinline__ void frame3_region(const BuildParams& P, const uint64
     if (lane == 0 && wv + 1 == (P.fr_nchunks + P.fr_w - 1) / P.fr_w) P.st->exit = R0 + wexit;
     // ---- counts: chunk `lane`'s records, their wave scan ----
     const uint32_t cnt = sel >= 0 ? (uint32_t)(s_cnt[sel] - at) : 0u;
-    uint32_t incl = cnt;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t t = __shfl_up(incl, o, 64);
-      if (lane >= o) incl += t;
-    }
-    const uint32_t total = __shfl(incl, 63, 64);
+    const uint32_t incl = wave_incl_sum_u32(cnt);
+    const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
     if (total > (uint32_t)kF3RecCap) {  // (the host ruled this out from the header's mean record)
       if (lane == 0) atomicOr(&P.st->spec_fail, kF3Caps);
       return;
@@ -624,9 +615,9 @@ bool frame3_fits(BuildParams& P, double mean_record, double pass) {
   if (((int64_t)P.fr_w << P.fr_cshift) + P.fr_look + 16 >= 32768) return false;  // 15-bit region offsets
   P.f3_rgn = (int32_t)((((int64_t)P.fr_w << P.fr_cshift) + P.fr_look + 16 + 15) & ~15ll);
   const double recs = (double)P.fr_w * C / mean_record;
-  const double cands = (double)P.fr_w * (double)std::min<int64_t>(1ll << P.fr_cshift, P.max_rec_len) * pass + P.fr_w;
-  const int need = (int)std::ceil(std::max(2.2 * cands + 32.0, 1.7 * recs + 32.0));
-  if (need > 512) return false;
+  const double false_cands = (double)P.fr_w * (double)std::min<int64_t>(1ll << P.fr_cshift, P.max_rec_len) * pass;
+  if (recs > 0.6 * 512 || false_cands > 0.6 * 512) return false;
+  const int need = std::min(512, (int)std::ceil(std::max(2.2 * (false_cands + P.fr_w) + 32.0, 1.7 * recs + 32.0)));
   // heads: about one per chunk plus a few false survivors; one long walk per lane
   P.f3_surv_cap = std::min(64, std::max(32, (2 * P.fr_w + 8 + 7) & ~7));
   P.f3_cand_cap = 512;

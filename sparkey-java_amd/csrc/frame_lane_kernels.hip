@@ -1,0 +1,387 @@
+// frame_lane_kernels.hip -- k_frame_lane: framing + MurmurHash3 with ONE LANE PER REGION of the log.
+//
+// The log is a chain of varint-framed records (SparkeyLogIterator.java:86-138): where record i + 1
+// starts depends on every record before it.  The wave-per-region framings (k_frame, k_frame3) spend
+// their lanes on that dependence: most of a wave's instructions screen, walk and resolve candidate
+// starts, and only one of its phases hashes.  Here a lane owns a whole region of R bytes and walks
+// its records itself, one dependent header load per record, hashing each key as it goes; the 64 lanes
+// of a wave (and every wave of the grid) walk 64 different regions at once, so the dependent loads of
+// thousands of lanes are in flight together and the HBM stream, not the chain, sets the pace.
+//
+//   entry   region r > 0 starts at s = base + r * R.  Its entry is the first record start >= s.  The
+//           lane screens [s, s + maxRecLen) 16 positions at a time (SWAR, the header maxima) and walks
+//           each plausible position kLaneTrial records on; the first that survives is its entry.
+//   walk    from the entry while records start below the region end: decode the header (one-byte
+//           VLQs from registers, else the reference's VLQ rules from memory), load the key's 16-byte
+//           chunks, prefetch the next header, MurmurHash3 the key (MurmurHash3.java:18-201) from
+//           registers, write the (hash, address) entry into the region's slab.  The walk applies the
+//           reference iterator's rules (SparkeyLogIterator.java:117-136); its exit is the first record
+//           start at or past the region end.
+//   fix     region r's records are right when its walk started at region r - 1's exit (by induction
+//           from the frame's verified entry).  k_frame_lane_flags + k_frame_lane_act re-walk, from
+//           r - 1's exit, every region whose start disagrees (the screened candidate was a false start,
+//           or the walk failed); two such passes settle what the speculation leaves in practice, and a
+//           final check pass flags any disagreement left: the host then redoes the framing with
+//           k_frame3 / k_frame / the serial walker.  A walk error on the verified chain leaves its
+//           region without an exit, so it reaches the serial walker too, which reports it.
+//
+// Per region r (P.qpos / P.exitp / P.tail / P.wcount, one word each): the position its walk started
+// from, its exit (-1: the walk failed), its DELETE count and its record count; entries in slab r of
+// P.ent (slab_cap each).  Regions are the framing's "chunks" with fr_w = 1 (fr_cshift = log2 R).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "build_kernels.hpp"
+#include "device_common.hpp"
+#include "frame_common.hpp"
+#include "kernel_utils.hpp"
+#include "scan.hpp"
+
+namespace sk {
+
+namespace {
+
+constexpr int kLaneTrial = 4;     // records a candidate entry must survive
+constexpr int kLaneMaxChunks = 10;  // 16-byte chunks of a record's header + key (+ 8 bytes): maxKeyLen <= 126
+
+__device__ __forceinline__ uint4 chunk_at(const BuildParams& P, int64_t a) {  // the 16 bytes at a (16-aligned)
+  return load16_guarded(P.log, a, (int64_t)P.log_len);
+}
+
+__device__ __forceinline__ uint64_t lo64(const uint4& c) { return (uint64_t)c.x | ((uint64_t)c.y << 32); }
+__device__ __forceinline__ uint64_t hi64(const uint4& c) { return (uint64_t)c.z | ((uint64_t)c.w << 32); }
+
+// 8 bytes at byte offset o (0..15) of the 32 bytes c0 ++ c1
+__device__ __forceinline__ uint64_t bytes8(const uint4& c0, const uint4& c1, int o) {
+  const uint64_t w0 = (o & 8) ? hi64(c0) : lo64(c0);
+  const uint64_t w1 = (o & 8) ? lo64(c1) : hi64(c0);
+  const int sh = (o & 7) * 8;
+  return sh ? (w0 >> sh) | (w1 << (64 - sh)) : w0;
+}
+
+// half h (8 bytes) of the chunk array: chunk h / 2, low or high half (h a compile-time index once
+// unrolled; clamped to the array, since the selects below also form indices the lane never uses)
+template <int N>
+__device__ __forceinline__ uint64_t half_of(const uint4 (&c)[N], int h) {
+  h = h < 2 * N ? h : 2 * N - 1;
+  return (h & 1) ? hi64(c[h >> 1]) : lo64(c[h >> 1]);
+}
+
+// The key's 8-byte word j (key bytes 8j .. 8j + 7), the key starting at byte ko (0..31) of the chunk
+// array: aligned halves (ko >> 3) + j and + j + 1, funnel-shifted.  ko >> 3 is lane-variable (0..3):
+// a select among four static halves.
+template <int N>
+__device__ __forceinline__ uint64_t key_word(const uint4 (&c)[N], int ko, int j) {
+  const int q = ko >> 3;
+  // (every half index below is static once j is; q picks among them by value selects, so the array
+  // stays in registers)
+  const uint64_t h0 = half_of(c, j), h1 = half_of(c, j + 1), h2 = half_of(c, j + 2), h3 = half_of(c, j + 3),
+                 h4 = half_of(c, j + 4);
+  const bool q1 = q & 1, q2 = q & 2;
+  const uint64_t a = q2 ? (q1 ? h3 : h2) : (q1 ? h1 : h0);
+  const uint64_t b = q2 ? (q1 ? h4 : h3) : (q1 ? h2 : h1);
+  const int sh = (ko & 7) * 8;
+  return sh ? (a >> sh) | (b << (64 - sh)) : a;
+}
+
+// MurmurHash3 x64_128 -> h1 (MurmurHash3.java:100-201) of a key whose bytes are in the chunk array
+// from byte ko on (ko + len + 8 <= 16 N); the loops run to the static bound with the lane's own length
+// as the guard, so every chunk index is static.
+template <int N>
+__device__ __forceinline__ uint64_t lane_murmur64(const uint4 (&c)[N], int ko, int32_t len, uint32_t seed) {
+  constexpr int kMaxBlocks = N - 1;  // (len < 16 N - 8 - ko)
+  const uint64_t c1 = 0x87c37b91114253d5ull, c2 = 0x4cf5ad432745937full;
+  uint64_t h1 = (uint64_t)seed, h2 = h1;
+  const int32_t nblocks = len >> 4;
+#pragma unroll
+  for (int i = 0; i < kMaxBlocks; i++) {
+    if (i < nblocks) {
+      uint64_t k1 = key_word(c, ko, 2 * i);
+      uint64_t k2 = key_word(c, ko, 2 * i + 1);
+      k1 *= c1; k1 = rotl64(k1, 31); k1 *= c2; h1 ^= k1;
+      h1 = rotl64(h1, 27); h1 += h2; h1 = h1 * 5 + 0x52dce729ull;
+      k2 *= c2; k2 = rotl64(k2, 33); k2 *= c1; h2 ^= k2;
+      h2 = rotl64(h2, 31); h2 += h1; h2 = h2 * 5 + 0x38495ab5ull;
+    }
+  }
+  const int32_t rem = len & 15;
+  uint64_t t1 = 0, t2 = 0;  // the tail's two words: word 2 * nblocks and the next (lane-variable block)
+#pragma unroll
+  for (int i = 0; i <= kMaxBlocks; i++) {
+    if (i == nblocks) {
+      t1 = key_word(c, ko, 2 * i);
+      t2 = key_word(c, ko, 2 * i + 1);
+    }
+  }
+  if (rem > 8) {
+    uint64_t k2 = t2 & ((1ull << (8 * (rem - 8))) - 1ull);
+    k2 *= c2; k2 = rotl64(k2, 33); k2 *= c1; h2 ^= k2;
+  }
+  if (rem > 0) {
+    uint64_t k1 = t1;
+    if (rem < 8) k1 &= (1ull << (8 * rem)) - 1ull;
+    k1 *= c1; k1 = rotl64(k1, 31); k1 *= c2; h1 ^= k1;
+  }
+  h1 ^= (uint64_t)(int64_t)len;
+  h2 ^= (uint64_t)(int64_t)len;
+  h1 += h2; h2 += h1;
+  h1 = fmix64(h1); h2 = fmix64(h2);
+  h1 += h2;
+  return h1;
+}
+
+// MurmurHash3 x86_32 (MurmurHash3.java:18-75), same conventions.
+template <int N>
+__device__ __forceinline__ uint32_t lane_murmur32(const uint4 (&c)[N], int ko, int32_t len, uint32_t seed) {
+  constexpr int kMaxWords = 2 * N - 1;  // 8-byte words the key (and its tail word) can span
+  const uint32_t c1 = 0xcc9e2d51u, c2 = 0x1b873593u;
+  uint32_t h1 = seed;
+  const int32_t nblocks = len >> 2;
+  auto block = [&](uint32_t k1) {
+    k1 *= c1; k1 = rotl32(k1, 15); k1 *= c2;
+    h1 ^= k1; h1 = rotl32(h1, 13); h1 = h1 * 5 + 0xe6546b64u;
+  };
+  uint32_t tail = 0;
+#pragma unroll
+  for (int j = 0; j < kMaxWords; j++) {
+    if (2 * j < nblocks || 2 * j == nblocks) {
+      const uint64_t w = key_word(c, ko, j);
+      if (2 * j < nblocks) block((uint32_t)w);
+      if (2 * j + 1 < nblocks) block((uint32_t)(w >> 32));
+      if (2 * j == nblocks) tail = (uint32_t)w;
+      if (2 * j + 1 == nblocks) tail = (uint32_t)(w >> 32);
+    }
+  }
+  const int32_t rem = len & 3;
+  if (rem) {
+    uint32_t k1 = tail & ((1u << (8 * rem)) - 1u);
+    k1 *= c1; k1 = rotl32(k1, 15); k1 *= c2; h1 ^= k1;
+  }
+  h1 ^= (uint32_t)len;
+  h1 ^= h1 >> 16; h1 *= 0x85ebca6bu; h1 ^= h1 >> 13; h1 *= 0xc2b2ae35u; h1 ^= h1 >> 16;
+  return h1;
+}
+
+// Plausible record start at byte o of c0 ++ c1 (the screen's rules: one-byte VLQs, the header's
+// maxima, no DELETE when the header counts none); returns the record's length, or 0.
+__device__ __forceinline__ int32_t plausible_len(const BuildParams& P, uint64_t x) {
+  const int32_t b0 = (int32_t)(x & 0xff), b1 = (int32_t)((x >> 8) & 0xff);
+  if ((b0 | b1) & 0x80) return 0;
+  if (b0 == 0) {
+    if (P.no_deletes || b1 > P.max_key_len) return 0;
+    return 2 + b1;
+  }
+  if (b0 - 1 > P.max_key_len || b1 > P.max_value_len) return 0;
+  return 1 + b0 + b1;
+}
+
+// A candidate start walked kLaneTrial records on by the screen's rules (it may run past lim: a chain
+// that reaches the frame end survives).
+__device__ __forceinline__ bool survives(const BuildParams& P, int64_t q, int64_t lim) {
+#pragma unroll 1
+  for (int t = 0; t < kLaneTrial && q < lim; t++) {
+    const int64_t a = q & ~15ll;
+    const int o = (int)(q & 15);
+    const uint4 c0 = chunk_at(P, a);
+    const uint4 c1 = o >= 15 ? chunk_at(P, a + 16) : make_uint4(0, 0, 0, 0);
+    const int32_t L = plausible_len(P, bytes8(c0, c1, o));
+    if (!L) return false;
+    q += L;
+  }
+  return true;
+}
+
+// The first record start >= s that survives the trial walk (s's region has one: R >= maxRecLen), or -1.
+__device__ __forceinline__ int64_t find_entry(const BuildParams& P, int64_t s, int64_t frame_end) {
+  const int64_t wend = min(s + P.max_rec_len, frame_end);  // a true start lies in [s, wend)
+  const Screen8 scn = make_screen8(P);
+  int64_t a = s & ~15ll;
+#pragma unroll 1
+  for (; a < wend; a += 16) {
+    const uint4 c0 = chunk_at(P, a), c1 = chunk_at(P, a + 16);
+    const uint64_t x0 = lo64(c0), x1 = hi64(c0), x2 = lo64(c1);
+    uint32_t m = screen8(x0, (x0 >> 8) | (x1 << 56), scn) | (screen8(x1, (x1 >> 8) | (x2 << 56), scn) << 8);
+    if (a < s) m &= ~0u << (int)(s - a);
+    if (wend - a < 16) m &= (1u << (int)(wend - a)) - 1u;
+#pragma unroll 1
+    while (m) {
+      const int o = __builtin_ctz(m);
+      m &= m - 1;
+      const int64_t c = a + o;
+      const int32_t L = plausible_len(P, bytes8(c0, c1, o));
+      if (L && survives(P, c + L, frame_end)) return c;
+    }
+  }
+  return -1;
+}
+
+// Walks region r from `entry` (see the file comment); writes its slab and per-region words.
+// Returns false when the walk failed (an invalid record, or a header that is not one-byte VLQs
+// beyond what the fast loader holds: the serial walker takes those).
+template <int N>
+__device__ bool walk_region(const BuildParams& P, uint64_t r, int64_t entry, int64_t rend) {
+  const int64_t log_len = (int64_t)P.log_len;
+  const uint64_t slab0 = r * (uint64_t)P.slab_cap;
+  uint32_t n = 0, nd = 0;
+  int64_t p = entry;
+  bool ok = true;
+  uint4 c[N];
+  if (p < rend) {
+    const int64_t a = p & ~15ll;
+    c[0] = chunk_at(P, a);
+    c[1] = chunk_at(P, a + 16);
+  }
+#pragma unroll 1
+  while (p < rend) {
+    const int o = (int)(p & 15);
+    const uint64_t x = bytes8(c[0], c[1], o);
+    int32_t klen, vlen, hlen;
+    bool put;
+    if ((x & 0x8080ull) == 0) {  // one-byte VLQs (every key < 127 bytes, value < 128)
+      const int32_t b0 = (int32_t)(x & 0xff), b1 = (int32_t)((x >> 8) & 0xff);
+      hlen = 2;
+      put = b0 != 0;
+      klen = put ? b0 - 1 : b1;
+      vlen = put ? b1 : 0;
+    } else {  // the reference's VLQ rules (Util.readUnsignedVLQInt), from memory
+      auto at = [&](int64_t i) -> uint32_t { return P.log[i]; };
+      const RecHdr h = decode_header(at, p, log_len);
+      if (h.rc) { ok = false; break; }
+      hlen = h.hlen; klen = h.klen; vlen = h.vlen; put = h.put != 0;
+    }
+    RecHdr hh;
+    hh.rc = 0; hh.hlen = hlen; hh.klen = klen; hh.vlen = vlen; hh.put = put;
+    if (!header_valid(hh, p, P.max_key_len, log_len) || o + hlen + klen + 8 > 16 * N) { ok = false; break; }
+    const int64_t pn = p + hlen + klen + vlen;
+    // the key's remaining chunks, then the next header's two (prefetch: its latency under the hash)
+    const int64_t a = p & ~15ll;
+    const int nch = (o + hlen + klen + 8 + 15) >> 4;  // chunks holding the header, the key, 8 slack bytes
+#pragma unroll
+    for (int k = 2; k < N; k++)
+      if (k < nch) c[k] = chunk_at(P, a + 16 * k);
+    uint4 n0 = make_uint4(0, 0, 0, 0), n1 = n0;
+    if (pn < rend) {
+      const int64_t an = pn & ~15ll;
+      n0 = chunk_at(P, an);
+      n1 = chunk_at(P, an + 16);
+    }
+    const int ko = o + hlen;
+    const uint64_t hash = P.hash_size == 8 ? lane_murmur64(c, ko, klen, (uint32_t)P.seed)
+                                           : (uint64_t)lane_murmur32(c, ko, klen, (uint32_t)P.seed);
+    uint64_t addr = (uint64_t)p << P.ebb;
+    if (!put) {
+      addr |= kDelBit;
+      nd++;
+    }
+    if (n < P.slab_cap) {
+      Entry en;
+      en.hash = hash;
+      en.addr = addr;
+      P.ent[slab0 + n] = en;
+    }
+    n++;
+    p = pn;
+    c[0] = n0;
+    c[1] = n1;
+  }
+  if (n > P.slab_cap) {  // the host grows the slabs and redoes the build
+    atomicMax(&P.st->max_wave_count, n);
+  }
+  P.qpos[r] = entry;
+  P.exitp[r] = ok ? p : -1;
+  P.tail[r] = nd;
+  P.wcount[r] = n;
+  return ok;
+}
+
+}  // namespace
+
+// Regions of the frame: region k (k from fr_k0) covers [k << fr_cshift, (k + 1) << fr_cshift) of the
+// log, clipped to [fr_entry, frame end).
+template <int N>
+__global__ __launch_bounds__(256) void k_frame_lane(BuildParams P) {
+  const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= P.fr_nchunks) return;
+  const int64_t frame_end = P.data_end;
+  const int64_t s = r == 0 ? P.fr_entry : (int64_t)((P.fr_k0 + r) << P.fr_cshift);
+  const int64_t rend = min((int64_t)((P.fr_k0 + r + 1) << P.fr_cshift), frame_end);
+  int64_t entry = r == 0 ? s : find_entry(P, s, frame_end);
+  if (entry < 0) {  // no surviving candidate: the fix pass walks it from the previous exit
+    P.qpos[r] = -2;
+    P.exitp[r] = -1;
+    P.tail[r] = 0;
+    P.wcount[r] = 0;
+    return;
+  }
+  walk_region<N>(P, r, entry, rend);
+}
+
+// The fix (see the file comment), in passes of two launches so that no region is read while it is
+// rewritten.  k_frame_lane_flags: P.conv[r] = 1 when region r's walk started at region r - 1's exit (region
+// 0: at the frame's entry) and ended with an exit.  check = 1 (the last pass): any region left without
+// the flag sets spec_fail (the host reruns the framing another way); the DELETE counts are summed and
+// the frame's exit recorded.
+__global__ __launch_bounds__(256) void k_frame_lane_flags(BuildParams P, int check) {
+  const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t nreg = P.fr_nchunks;
+  bool good = true;
+  uint32_t nd = 0;
+  if (r < nreg) {
+    good = P.exitp[r] >= 0 && (r == 0 || (P.exitp[r - 1] >= 0 && P.exitp[r - 1] == P.qpos[r]));
+    P.conv[r] = good ? 1 : 0;
+    nd = P.tail[r];
+    if (check && r + 1 == nreg) P.st->exit = P.exitp[r];
+  }
+  if (!check) return;
+  const bool any_bad = __any(!good);
+  const unsigned long long ndw = wave_sum_u64((unsigned long long)nd);
+  if ((threadIdx.x & 63) == 0) {
+    if (any_bad) atomicOr(&P.st->spec_fail, 1u);
+    if (ndw) atomicAdd(&P.st->n_deletes, ndw);
+  }
+}
+
+// k_frame_lane_act: region r without the flag whose predecessor has it (so region r - 1 is not
+// rewritten in this pass) is walked again from region r - 1's exit.
+template <int N>
+__global__ __launch_bounds__(256) void k_frame_lane_act(BuildParams P) {
+  const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r == 0 || r >= P.fr_nchunks || P.conv[r] || !P.conv[r - 1]) return;
+  const int64_t rend = min((int64_t)((P.fr_k0 + r + 1) << P.fr_cshift), P.data_end);
+  walk_region<N>(P, r, P.exitp[r - 1], rend);
+}
+
+// Chunks (16 bytes) a record's header + key + 8 slack bytes can span at the header maxima.
+static int lane_chunks(const BuildParams& P) {
+  const int64_t need = 15 + 2 + P.max_key_len + 8;
+  return (int)((need + 15) / 16);
+}
+
+bool frame_lane_supported(const BuildParams& P) {
+  return P.fr_fast && lane_chunks(P) <= kLaneMaxChunks && P.max_rec_len <= (1ll << P.fr_cshift);
+}
+
+template <int N>
+static void launch_lane_n(const BuildParams& P, hipStream_t s, StageTimer* tm) {
+  const unsigned g = (unsigned)((P.fr_nchunks + 255) / 256);
+  hipLaunchKernelGGL(k_frame_lane<N>, dim3(g), dim3(256), 0, s, P);
+  for (int pass = 0; pass < 2; pass++) {
+    hipLaunchKernelGGL(k_frame_lane_flags, dim3(g), dim3(256), 0, s, P, 0);
+    hipLaunchKernelGGL(k_frame_lane_act<N>, dim3(g), dim3(256), 0, s, P);
+  }
+  hipLaunchKernelGGL(k_frame_lane_flags, dim3(g), dim3(256), 0, s, P, 1);
+  tm->mark("frame", s);
+}
+
+void launch_frame_lane(const BuildParams& P, hipStream_t s, StageTimer* tm) {
+  if (P.fr_nchunks == 0) return;
+  // the chunk array holds a record's header and key: its size is static (registers)
+  const int n = lane_chunks(P);
+  if (n <= 4) launch_lane_n<4>(P, s, tm);
+  else if (n <= 6) launch_lane_n<6>(P, s, tm);
+  else launch_lane_n<kLaneMaxChunks>(P, s, tm);
+  scan_exclusive<uint32_t, uint64_t, OpAdd>(P.wcount, P.woff, P.nslabs, (uint64_t*)&P.st->n_records, OpAdd(),
+                                            P.scan_scratch_u64, s);
+}
+
+}  // namespace sk

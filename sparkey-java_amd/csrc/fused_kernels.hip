@@ -946,6 +946,69 @@ __global__ __launch_bounds__(kPartBlock) void k_part1_scatter(BuildParams P) {
   }
 }
 
+// Pass 1 in one kernel, into fixed-capacity digit regions (P.p1_region, as k_frame_uniform writes
+// them): the tile's digit counts in LDS, one atomic per non-empty digit on the region's fill cursor,
+// the tile's entries grouped by digit in LDS and written as one run per digit.  No histogram pass over
+// the entries and no global scan (k_part1_hist + k_part1_scatter read every entry twice).  A region
+// that fills up flags kSpecRegionFull: the host redoes the build with the two-pass partition.
+__global__ __launch_bounds__(kPartBlock) void k_part1_regions(BuildParams P) {
+  __shared__ Entry stage[kPartTile];
+  __shared__ uint8_t sdig[kPartTile];  // digit of each staged entry
+  __shared__ uint32_t cnt[256];
+  __shared__ uint32_t lbase[256];
+  __shared__ int64_t gdst[256];        // global index of the digit's run minus its LDS start
+  __shared__ uint64_t lim[256];        // end of the digit's region
+  __shared__ uint64_t sh64[kPartBlock / 64 + 1];
+  __shared__ SlabTile T;
+  if (build_aborted(P)) return;
+  const uint64_t g0 = (uint64_t)blockIdx.x * P.part_group;
+  const int tid = threadIdx.x;
+  cnt[tid] = 0;
+  const uint32_t n = load_tile(P, T, g0);  // (its barriers order the clear)
+  Entry v[kPartItems];
+  uint32_t dg[kPartItems];
+#pragma unroll
+  for (int i = 0; i < kPartItems; i++) {
+    const uint32_t idx = (uint32_t)i * kPartBlock + tid;
+    if (idx < n) v[i] = tile_entry(P, T, g0, idx);
+  }
+#pragma unroll
+  for (int i = 0; i < kPartItems; i++) {
+    const uint32_t idx = (uint32_t)i * kPartBlock + tid;
+    dg[i] = ~0u;
+    if (idx < n && !(P.skip_del && (v[i].addr & kDelBit))) {  // exact path: DELETEs stay out
+      dg[i] = digit_of(P, bucket_of(P, v[i].hash));
+      dg[i] |= atomicAdd(&cnt[dg[i]], 1u) << 8;  // rank inside the tile's digit run
+    }
+  }
+  __syncthreads();
+  const uint32_t c = cnt[tid];
+  lbase[tid] = (uint32_t)block_excl_sum<kPartBlock>(c, sh64, &sh64[kPartBlock / 64]);
+  const uint64_t b0 = c ? atomicAdd(&P.p1_fill[tid], c) : 0u;
+  if (b0 + c > P.p1_region) atomicOr(&P.st->spec_fail, kSpecRegionFull);
+  gdst[tid] = (int64_t)((uint64_t)tid * P.p1_region + b0) - (int64_t)lbase[tid];
+  lim[tid] = (uint64_t)(tid + 1) * P.p1_region;
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < kPartItems; i++) {
+    if (dg[i] == ~0u) continue;
+    const uint32_t d = dg[i] & 255u, pos = lbase[d] + (dg[i] >> 8);
+    stage[pos] = v[i];
+    sdig[pos] = (uint8_t)d;
+  }
+  __syncthreads();
+  const uint32_t nkeep = (uint32_t)sh64[kPartBlock / 64];
+#pragma unroll
+  for (int k = 0; k < kPartItems; k++) {
+    const uint32_t i = (uint32_t)k * kPartBlock + tid;
+    if (i < nkeep) {
+      const uint32_t d = sdig[i];
+      const uint64_t at = (uint64_t)(gdst[d] + (int64_t)i);
+      if (at < lim[d]) P.ent3[at] = stage[i];
+    }
+  }
+}
+
 // Dense entries (serial framing path) seen as slabs of kPartTile.
 __global__ void k_dense_slabs(BuildParams P) {
   const uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1679,6 +1742,7 @@ void launch_partition2(const BuildParams& P, hipStream_t s, StageTimer* tm) {
 
 void launch_partition(const BuildParams& P, hipStream_t s, StageTimer* tm) {
   if (!P.p1_region) launch_partition1(P, s);
+  else if (P.p1_kernel) hipLaunchKernelGGL(k_part1_regions, dim3((unsigned)P.p1_tiles), dim3(kPartBlock), 0, s, P);
   if (P.p2_sorted)
     hipLaunchKernelGGL(k_part2s, dim3(256), dim3(kPart2Block), (size_t)(514u * P.bpp) * sizeof(uint32_t), s, P);
   else

@@ -78,6 +78,25 @@ __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
   v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31
   return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
 }
+// Inclusive prefix sum over the wave's lanes by the same DPP steps (each lane keeps its prefix): a
+// scan in ~12 VALU cycles, where shuffles cost six LDS-crossbar round trips (ds_bpermute).
+__device__ __forceinline__ uint32_t wave_incl_sum_u32(uint32_t v) {
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);  // row_shr:8
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31
+  return v;
+}
+// Lane i gets lane i - 1's value, lane 0 gets `first` (DPP wave_shr:1); lane i gets lane i + 1's,
+// lane 63 gets `last` (wave_shl:1).  No LDS crossbar.
+__device__ __forceinline__ int32_t wave_prev_i32(int32_t v, int32_t first) {
+  return __builtin_amdgcn_update_dpp(first, v, 0x138, 0xf, 0xf, false);
+}
+__device__ __forceinline__ int32_t wave_next_i32(int32_t v, int32_t last) {
+  return __builtin_amdgcn_update_dpp(last, v, 0x130, 0xf, 0xf, false);
+}
 __device__ __forceinline__ int32_t wave_max_i32(int32_t v) {  // (v >= 0 lanes only matter: 0 shifts in)
   v = max(v, __builtin_amdgcn_update_dpp(INT32_MIN, v, 0x111, 0xf, 0xf, false));
   v = max(v, __builtin_amdgcn_update_dpp(INT32_MIN, v, 0x112, 0xf, 0xf, false));

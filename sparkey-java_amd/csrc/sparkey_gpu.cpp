@@ -624,6 +624,25 @@ static void set_geom(BuildParams& P, const FrameGeom& g) {
 // S = 8 KiB / SEG of them per wave (2..32), each listing up to f2_lcap record starts (a log of
 // records far below 16 bytes on average overflows them and is framed by k_frame instead).
 // SPARKEY_FRAME2_SEG / SPARKEY_FRAME2_S override (measurements).
+// k_frame_lane's regions: R = max(8 KiB, the power of two >= maxRecLen) bytes per lane
+// (SPARKEY_LANE_REGION overrides), numbered from entry >> log2 R; none when the log's records do not
+// suit it (frame_lane_supported) or SPARKEY_NO_LANE is set.
+static FrameGeom lane_geometry(const BuildParams& P, int64_t entry, int64_t frame_end) {
+  FrameGeom g{0, 1, 0, 0};
+  if (getenv("SPARKEY_NO_LANE") || frame_end <= entry) return g;
+  int64_t want = 8192;
+  if (const char* v = getenv("SPARKEY_LANE_REGION")) want = std::max<int64_t>(256, atoll(v));
+  int cs = 8;
+  while ((1ll << cs) < std::max<int64_t>(want, P.max_rec_len)) cs++;
+  BuildParams Q = P;
+  Q.fr_cshift = cs;
+  if (!frame_lane_supported(Q)) return g;
+  g.cshift = cs;
+  g.k0 = (uint64_t)entry >> cs;
+  g.nchunks = (uint64_t)((frame_end + (1ll << cs) - 1) >> cs) - g.k0;
+  return g;
+}
+
 static FrameGeom frame2_geometry(BuildParams& P, int64_t entry, int64_t frame_end) {
   int cs = 9;
   while ((1ll << cs) < P.max_rec_len) cs++;
@@ -690,6 +709,7 @@ static int launch_framing(sparkey_plan* pl, const BuildParams& P, int framing_pa
     HIP_TRY(hipMemsetAsync(pl->wcount, 0, (P.nslabs + 1) * sizeof(uint32_t), s));
     if (framing_path == 3) launch_frame2(P, s, &pl->timer);
     else if (framing_path == 4) launch_frame3(P, s, &pl->timer);
+    else if (framing_path == 5) launch_frame_lane(P, s, &pl->timer);
     else launch_frame_fused(P, s, &pl->timer);
   } else if (framing_path == 2) {
     launch_frame_uniform(P, s, &pl->timer);
@@ -1238,9 +1258,12 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
                           want_frame3(P, lh, kLogHeaderSize, std::max<int64_t>(lh.data_end, kLogHeaderSize));
   const FrameGeom geom0 = get_geom(P);
   const FrameGeom geom2 = frame2_geometry(P, kLogHeaderSize, std::max<int64_t>(lh.data_end, kLogHeaderSize));
+  // k_frame_lane (frame_lane_kernels.hip): one lane per region of R bytes walks and hashes its records
+  const FrameGeom geom5 = lane_geometry(P, kLogHeaderSize, std::max<int64_t>(lh.data_end, kLogHeaderSize));
+  const bool use_lane = fused_framing && !use_frame2 && geom5.nchunks > 0;
   // SPARKEY_SERIAL_FRAMING forces the exact serial walk (smoke() and tests check every framing path)
   const bool force_serial = getenv("SPARKEY_SERIAL_FRAMING") != nullptr;
-  const int spec_path = fused_framing && !force_serial ? (use_frame2 ? 3 : (use_frame3 ? 4 : 0)) : 1;
+  const int spec_path = fused_framing && !force_serial ? (use_frame2 ? 3 : (use_lane ? 5 : (use_frame3 ? 4 : 0))) : 1;
   int framing_path = spec_path, placement_path = 0;
   if (const int64_t R = force_serial ? 0 : uniform_record_size(lh)) {  // k_frame_uniform: every record is exactly R bytes
     framing_path = 2;
@@ -1255,15 +1278,16 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
     const uint64_t nw = std::max<uint64_t>(1, g.nchunks ? (g.nchunks + g.w - 1) / g.w : 0);
     return (uint32_t)std::min<uint64_t>(kPartTile, std::max<uint64_t>(64, 2 * ((nrec + nw - 1) / nw) + 32));
   };
-  uint32_t slab_cap = slab_for(framing_path == 3 ? geom2 : geom0);
+  auto geom_of = [&](int path) -> const FrameGeom& { return path == 3 ? geom2 : path == 5 ? geom5 : geom0; };
+  uint32_t slab_cap = slab_for(geom_of(framing_path));
   int slab_path = framing_path;
   bool use_regions = getenv("SPARKEY_NO_REGIONS") == nullptr, regions_used = false;
   bool use_fixed = getenv("SPARKEY_NO_P2_FIXED") == nullptr;  // k_part2s in one pass (fixed bucket regions)
   const bool fold = getenv("SPARKEY_NO_FOLD_STATS") == nullptr;  // stats from k_place_lds, no k_stats pass
   for (int attempt = 0; attempt < 6; attempt++) {
-    set_geom(P, framing_path == 3 ? geom2 : geom0);
+    set_geom(P, geom_of(framing_path));
     if (slab_framing(framing_path) && framing_path != slab_path) {
-      slab_cap = slab_for(framing_path == 3 ? geom2 : geom0);
+      slab_cap = slab_for(geom_of(framing_path));
       slab_path = framing_path;
     }
     rc = reserve_for_framing(pl, P, framing_path, nrec, slab_cap, err, err_len);
@@ -1291,8 +1315,12 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
     // digit regions of ent3 sized for the binomial spread of the digit counts (a region that fills
     // up redoes the build with the separate pass), or leaves k_part1_hist's histogram
     const bool tiles = framing_path == 2 && P.slab_cap == (uint32_t)kPartTile && P.part_group == 1;
+    // the other framings' slabs: pass 1 into the same fixed digit regions by k_part1_regions (one read
+    // of the entries instead of k_part1_hist + k_part1_scatter's two)
+    const bool slab_regions = !tiles && !getenv("SPARKEY_NO_P1_REGIONS");
     P.p1_region = 0;
-    if (tiles && use_regions) {
+    P.p1_kernel = 0;
+    if ((tiles || slab_regions) && use_regions) {
       const double expect = (double)nrec * (double)P.bpp * (double)kBucket / (double)P.cap;
       uint64_t rc_cap = ((uint64_t)(expect + 8.0 * std::sqrt(expect) + 1024.0) + 63) & ~63ull;
       if (const char* e = getenv("SPARKEY_REGION_CAP")) rc_cap = std::max<uint64_t>(1, strtoull(e, nullptr, 10));  // (tests)
@@ -1305,9 +1333,10 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
       P.max_records = std::min(pl->c_ent2, pl->c_ent3);
       P.p1_fill = pl->p1_fill;
       P.p1_region = rc_cap;
+      P.p1_kernel = tiles ? 0 : 1;
     }
     P.p1_hist_ready = tiles && !P.p1_region ? 1 : 0;
-    regions_used = P.p1_region != 0;
+    regions_used = P.p1_region != 0 && !P.p1_kernel;  // (partition passes: 1 when the framing did pass 1)
     // k_part2s: pass 2 also sorts each bucket by wanted slot and leaves the carry functions
     P.p2_sorted = P.bpp <= kP2SortedMaxBpp && !getenv("SPARKEY_NO_P2_SORTED") ? 1 : 0;
     P.p2_fixed = P.p2_sorted && use_fixed ? 1 : 0;
@@ -1352,11 +1381,17 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
     if (getenv("SPARKEY_FRAME_DEBUG") && (st.spec_fail || st.err != ~0ull))
       fprintf(stderr, "[framing] path %d: spec_fail %u err %llx (pos %llu)\n", framing_path, st.spec_fail,
               (unsigned long long)st.err, (unsigned long long)(st.err >> 8));
-    if (framing_path == 4 && (st.spec_fail || st.err != ~0ull)) {  // k_frame3's lists or speculation: k_frame
+    // (a digit region filled by k_part1_regions is the partition's business, not the framing's)
+    const unsigned fspec = st.spec_fail & ~(P.p1_kernel ? kSpecRegionFull : 0u);
+    if (framing_path == 5 && (fspec || st.err != ~0ull)) {  // regions left unresolved: k_frame3 / k_frame
+      framing_path = use_frame3 ? 4 : 0;
+      continue;
+    }
+    if (framing_path == 4 && (fspec || st.err != ~0ull)) {  // k_frame3's lists or speculation: k_frame
       framing_path = 0;
       continue;
     }
-    if ((framing_path == 0 || framing_path == 3) && (st.spec_fail || st.err != ~0ull)) {  // only the serial walk reports
+    if ((framing_path == 0 || framing_path == 3) && (fspec || st.err != ~0ull)) {  // only the serial walk reports
       framing_path = 1;
       continue;
     }
@@ -1364,8 +1399,8 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
       use_fixed = false;
       continue;
     }
-    if (framing_path == 2 && (st.spec_fail & kSpecRegionFull) && !(st.spec_fail & ~kSpecRegionFull)) {
-      use_regions = false;  // a digit region filled up (skewed hashes): the separate pass 1
+    if ((st.spec_fail & kSpecRegionFull) && (P.p1_kernel || !(st.spec_fail & ~kSpecRegionFull))) {
+      use_regions = false;  // a digit region filled up (skewed hashes): the two-pass partition
       continue;
     }
     if (framing_path == 2 && st.spec_fail) {  // a record differs from the header's uniform shape
