@@ -260,7 +260,7 @@ def single_gpu(args, dev):
     dom_bytes = stage_bytes(dom, n, frame_end, slot, cap, passes, comp_end=log_len) if dom else 0
     achieved = dom_bytes / (stage_ms[dom] * 1e-3) / 1e9 if dom and stage_ms[dom] > 0 else 0.0
     b_alg = (log_len - 84) + 112 + slot * cap
-    assert stats.placement_path == wl["path"] and stats.framing_path in (0, 2, 3, 4), stats.as_dict()
+    assert stats.placement_path == wl["path"] and stats.framing_path in (0, 2, 3, 4, 5), stats.as_dict()
     assert wl["path"] != 0 or stats.num_entries == n, stats.as_dict()
 
     if args.quick:  # (profiling runs: the timed builds only)
@@ -300,7 +300,7 @@ def single_gpu(args, dev):
             torch.cuda.synchronize(dev)
             g_el = time.perf_counter() - t_g
             plan.set_profiling(False)
-            assert g_stats.framing_path in (0, 3, 4), g_stats.as_dict()
+            assert g_stats.framing_path in (0, 3, 4, 5), g_stats.as_dict()
             general_spi = d_out.cpu().numpy().tobytes()  # (compared with the headline build below)
             g_stage = {k: v / g_steps for k, v in g_acc.items()}
             general = {"ms_per_step": g_el * 1000.0 / g_steps, "keys_per_s": n * g_steps / g_el,
@@ -313,6 +313,7 @@ def single_gpu(args, dev):
     # point the JNI shim calls, on the same log written to a file; page-cache warm, fsync off (the
     # writer's default), its per-device context kept across calls
     file_rate = file_spi = None
+    file_phases = None
     tmpdir = tempfile.mkdtemp(prefix="sparkey_bench_")
     log_path, spi_path = os.path.join(tmpdir, "bench.spl"), os.path.join(tmpdir, "bench.spi")
     try:
@@ -322,9 +323,12 @@ def single_gpu(args, dev):
             _native.build_index_file(log_path, spi_path, opts)
             reps_f = 3
             t_f = time.perf_counter()
+            file_phases = {}
             for i in range(reps_f):
                 tmp = f"{spi_path}-tmp{i}"
                 _native.build_index_file(log_path, tmp, opts)
+                for k, v in _native.file_last_phases().items():
+                    file_phases[k] = file_phases.get(k, 0.0) + v / reps_f
                 os.replace(tmp, spi_path)
             file_rate = n * reps_f / (time.perf_counter() - t_f)
             with open(spi_path, "rb") as f:
@@ -389,10 +393,12 @@ def single_gpu(args, dev):
         "stage_ms": stage_ms,
         "framing": {0: "k_frame (speculative)", 1: "serial walk", 2: "k_frame_uniform (uniform records)",
                     3: "k_frame2 (speculative, mixed record sizes)",
-                    4: "k_frame3 (short/long walks, one-byte VLQs)"}[stats.framing_path],
+                    4: "k_frame3 (short/long walks, one-byte VLQs)",
+                    5: "k_frame_lane (one lane per log region, one-byte VLQs)"}[stats.framing_path],
         "general_framing": general,
         "host_to_host_keys_per_s": h2h,
         "file_to_file_keys_per_s": file_rate,
+        "file_to_file_phase_ms": file_phases,
         "cpu_baseline": cpu,
         "parity": parity,
         "gen_s": gen_s,

@@ -104,6 +104,11 @@ int sparkey_build_index_mem(const uint8_t* log, uint64_t log_len, uint8_t* index
  * new one.  With SPARKEY_FILE_CACHE=0 in the environment nothing is kept between calls. */
 void sparkey_release_cached_resources(void);
 
+/* Wall time of the calling thread's last single-GPU sparkey_build_index_file by phase (diagnostics):
+ * {open + header checks, log read + H2D, device build, D2H + index write, fsync + close}, in ms.
+ * Copies min(n, 5) values; returns that count. */
+int32_t sparkey_file_last_phases(double* ms_out, int32_t n);
+
 /* .spi size for a log (needs only its 84-byte header): 112 + slotSize * capacity, or < 0. */
 int64_t sparkey_index_size(const uint8_t* log_header, uint64_t header_len, const sparkey_build_opts* opts);
 

@@ -12,6 +12,7 @@
 // released by sparkey_release_cached_resources(), or never kept with SPARKEY_FILE_CACHE=0.
 #include <errno.h>
 #include <fcntl.h>
+#include <sched.h>
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -32,6 +33,9 @@
 
 #include "../../include/sparkey_gpu.h"
 #include "shard_host.hpp"
+
+// Phases of the calling thread's last sparkey_build_index_file (sparkey_file_last_phases).
+thread_local double t_file_phase[5] = {0, 0, 0, 0, 0};
 
 // LogHeader.read's checks with the file's length (sparkey_gpu.cpp), message into err.
 int sk_check_log_header(const uint8_t* b, uint64_t hdr_len, uint64_t file_len, char* err, size_t err_len);
@@ -160,8 +164,12 @@ struct FileCtx {
         return SPARKEY_E_GPU;
       }
     }
-    const unsigned hc = std::thread::hardware_concurrency();
-    int nt = (int)std::min<unsigned>(8u, hc ? hc : 4u) - 1;  // the calling thread works too
+    // the CPUs this process may run on (a container's share, not the machine's), at most 16
+    cpu_set_t cs;
+    unsigned hc = 0;
+    if (sched_getaffinity(0, sizeof(cs), &cs) == 0) hc = (unsigned)CPU_COUNT(&cs);
+    if (!hc) hc = std::thread::hardware_concurrency();
+    int nt = (int)std::min<unsigned>(16u, hc ? hc : 4u) - 1;  // the calling thread works too
     if (const char* v = getenv("SPARKEY_FILE_THREADS")) nt = std::max(0, atoi(v) - 1);
     pool = new WorkerPool(std::max(0, nt));
     return SPARKEY_OK;
@@ -491,9 +499,15 @@ int sparkey_build_index_file(const char* log_path, const char* index_out_path, c
     unlink(index_out_path);
     return rc;
   }
+  const double t5 = now_ms();
+  t_file_phase[0] = t1 - t0;
+  t_file_phase[1] = t2 - t1;
+  t_file_phase[2] = t3 - t2;
+  t_file_phase[3] = t4 - t3;
+  t_file_phase[4] = t5 - t4;
   if (dbg)
-    fprintf(stderr, "[file] open+header %.2f ms, read+H2D %.2f ms, build %.2f ms, D2H+write %.2f ms, fsync %.2f ms\n",
-            t1 - t0, t2 - t1, t3 - t2, t4 - t3, now_ms() - t4);
+    fprintf(stderr, "[file] open+header %.2f ms, read+H2D %.2f ms, build %.2f ms, D2H+write %.2f ms, fsync+close %.2f ms\n",
+            t1 - t0, t2 - t1, t3 - t2, t4 - t3, t5 - t4);
   return SPARKEY_OK;
 }
 
@@ -569,6 +583,12 @@ int sparkey_build_index_mem(const uint8_t* log, uint64_t log_len, uint8_t* index
     return SPARKEY_E_GPU;
   }
   return SPARKEY_OK;
+}
+
+int32_t sparkey_file_last_phases(double* ms_out, int32_t n) {
+  const int32_t k = n < 5 ? n : 5;
+  for (int32_t i = 0; i < k; i++) ms_out[i] = t_file_phase[i];
+  return k;
 }
 
 void sparkey_release_cached_resources(void) {

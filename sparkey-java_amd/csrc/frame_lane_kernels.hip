@@ -20,8 +20,8 @@
 //   fix     region r's records are right when its walk started at region r - 1's exit (by induction
 //           from the frame's verified entry).  k_frame_lane_flags + k_frame_lane_act re-walk, from
 //           r - 1's exit, every region whose start disagrees (the screened candidate was a false start,
-//           or the walk failed); two such passes settle what the speculation leaves in practice, and a
-//           final check pass flags any disagreement left: the host then redoes the framing with
+//           or the walk failed); kLanePasses such passes settle what the speculation leaves in practice,
+//           and a final check pass flags any disagreement left: the host then redoes the framing with
 //           k_frame3 / k_frame / the serial walker.  A walk error on the verified chain leaves its
 //           region without an exit, so it reaches the serial walker too, which reports it.
 //
@@ -42,6 +42,7 @@ namespace sk {
 namespace {
 
 constexpr int kLaneTrial = 4;     // records a candidate entry must survive
+constexpr int kLanePasses = 4;    // fix passes (one settles what C3-like logs leave; pathological ones need more)
 constexpr int kLaneMaxChunks = 10;  // 16-byte chunks of a record's header + key (+ 8 bytes): maxKeyLen <= 126
 
 __device__ __forceinline__ uint4 chunk_at(const BuildParams& P, int64_t a) {  // the 16 bytes at a (16-aligned)
@@ -215,16 +216,13 @@ __device__ __forceinline__ int64_t find_entry(const BuildParams& P, int64_t s, i
   return -1;
 }
 
-// Walks region r from `entry` (see the file comment); writes its slab and per-region words.
-// Returns false when the walk failed (an invalid record, or a header that is not one-byte VLQs
-// beyond what the fast loader holds: the serial walker takes those).
-template <int N>
-__device__ bool walk_region(const BuildParams& P, uint64_t r, int64_t entry, int64_t rend) {
+// Walks the records from p while they start below rend: for each, emit(position, hash, put) (false:
+// stop there).  Returns the first record start >= rend, the position emit stopped at, or -1 at a
+// record the reference's iterator rejects (SparkeyLogIterator.java:117-136) or one whose header and
+// key do not fit the chunk array (a header VLQ longer than one byte the header maxima ruled out).
+template <int N, class Emit>
+__device__ int64_t walk_records(const BuildParams& P, int64_t p, int64_t rend, Emit&& emit) {
   const int64_t log_len = (int64_t)P.log_len;
-  const uint64_t slab0 = r * (uint64_t)P.slab_cap;
-  uint32_t n = 0, nd = 0;
-  int64_t p = entry;
-  bool ok = true;
   uint4 c[N];
   if (p < rend) {
     const int64_t a = p & ~15ll;
@@ -246,12 +244,12 @@ __device__ bool walk_region(const BuildParams& P, uint64_t r, int64_t entry, int
     } else {  // the reference's VLQ rules (Util.readUnsignedVLQInt), from memory
       auto at = [&](int64_t i) -> uint32_t { return P.log[i]; };
       const RecHdr h = decode_header(at, p, log_len);
-      if (h.rc) { ok = false; break; }
+      if (h.rc) return -1;
       hlen = h.hlen; klen = h.klen; vlen = h.vlen; put = h.put != 0;
     }
     RecHdr hh;
     hh.rc = 0; hh.hlen = hlen; hh.klen = klen; hh.vlen = vlen; hh.put = put;
-    if (!header_valid(hh, p, P.max_key_len, log_len) || o + hlen + klen + 8 > 16 * N) { ok = false; break; }
+    if (!header_valid(hh, p, P.max_key_len, log_len) || o + hlen + klen + 8 > 16 * N) return -1;
     const int64_t pn = p + hlen + klen + vlen;
     // the key's remaining chunks, then the next header's two (prefetch: its latency under the hash)
     const int64_t a = p & ~15ll;
@@ -268,30 +266,112 @@ __device__ bool walk_region(const BuildParams& P, uint64_t r, int64_t entry, int
     const int ko = o + hlen;
     const uint64_t hash = P.hash_size == 8 ? lane_murmur64(c, ko, klen, (uint32_t)P.seed)
                                            : (uint64_t)lane_murmur32(c, ko, klen, (uint32_t)P.seed);
-    uint64_t addr = (uint64_t)p << P.ebb;
-    if (!put) {
-      addr |= kDelBit;
-      nd++;
-    }
-    if (n < P.slab_cap) {
-      Entry en;
-      en.hash = hash;
-      en.addr = addr;
-      P.ent[slab0 + n] = en;
-    }
-    n++;
+    if (!emit(p, hash, put)) return p;
     p = pn;
     c[0] = n0;
     c[1] = n1;
   }
-  if (n > P.slab_cap) {  // the host grows the slabs and redoes the build
-    atomicMax(&P.st->max_wave_count, n);
-  }
+  return p;
+}
+
+__device__ __forceinline__ uint64_t entry_addr(const BuildParams& P, int64_t p, bool put) {
+  return ((uint64_t)p << P.ebb) | (put ? 0ull : kDelBit);
+}
+__device__ __forceinline__ int64_t entry_pos(const BuildParams& P, uint64_t addr) {
+  return (int64_t)((addr & ~kDelBit) >> P.ebb);
+}
+
+// Walks region r from `entry` (see the file comment): its slab and per-region words.
+template <int N>
+__device__ void walk_region(const BuildParams& P, uint64_t r, int64_t entry, int64_t rend) {
+  const uint64_t slab0 = r * (uint64_t)P.slab_cap;
+  uint32_t n = 0, nd = 0;
+  const int64_t ex = walk_records<N>(P, entry, rend, [&](int64_t p, uint64_t hash, bool put) {
+    if (n < P.slab_cap) {
+      Entry en;
+      en.hash = hash;
+      en.addr = entry_addr(P, p, put);
+      P.ent[slab0 + n] = en;
+    }
+    nd += put ? 0u : 1u;
+    n++;
+    return true;
+  });
+  if (n > P.slab_cap) atomicMax(&P.st->max_wave_count, n);  // the host grows the slabs and redoes the build
   P.qpos[r] = entry;
-  P.exitp[r] = ok ? p : -1;
+  P.exitp[r] = ex;
   P.tail[r] = nd;
   P.wcount[r] = n;
-  return ok;
+}
+
+constexpr int kPatchMax = 16;  // records a fix may put in front of the original walk's suffix
+
+// Region r again from x, the verified previous exit.  A screened entry that was a false start almost
+// always joins the true chain within a record or two, so the original walk's records are right from
+// the first position both walks reach: the new records before it replace the original's before it (the
+// suffix is moved in the slab) and the exit stands.  A walk that meets no original position within
+// kPatchMax records, or an original walk without an exit, is redone whole.
+template <int N>
+__device__ void fix_region(const BuildParams& P, uint64_t r, int64_t x, int64_t rend) {
+  const uint64_t slab0 = r * (uint64_t)P.slab_cap;
+  const int64_t old_exit = P.exitp[r];
+  const uint32_t n0 = P.wcount[r];
+  if (old_exit < 0 || P.qpos[r] < 0 || n0 > P.slab_cap) {
+    walk_region<N>(P, r, x, rend);
+    return;
+  }
+  Entry nb[kPatchMax];
+  int k = 0;
+  uint32_t i = 0, nd_old = 0, nd_new = 0;
+  bool merged = false, full = false;
+  int64_t ipos = n0 ? entry_pos(P, P.ent[slab0].addr) : INT64_MAX;
+  const int64_t ex = walk_records<N>(P, x, rend, [&](int64_t p, uint64_t hash, bool put) {
+    while (i < n0 && ipos < p) {  // the original's records before p: replaced
+      nd_old += (P.ent[slab0 + i].addr & kDelBit) ? 1u : 0u;
+      i++;
+      ipos = i < n0 ? entry_pos(P, P.ent[slab0 + i].addr) : INT64_MAX;
+    }
+    if (ipos == p) {  // both walks reach p: the original is right from here on
+      merged = true;
+      return false;
+    }
+    if (k == kPatchMax) {
+      full = true;
+      return false;
+    }
+    nb[k].hash = hash;
+    nb[k].addr = entry_addr(P, p, put);
+    nd_new += put ? 0u : 1u;
+    k++;
+    return true;
+  });
+  if (full || ex < 0) {  // no meeting point close by (or a bad record): the whole region again
+    walk_region<N>(P, r, x, rend);
+    return;
+  }
+  uint32_t n;
+  if (merged) {  // new prefix nb[0, k) + original [i, n0)
+    n = (uint32_t)k + (n0 - i);
+    if (n > P.slab_cap) {
+      atomicMax(&P.st->max_wave_count, n);
+      P.wcount[r] = n;
+      return;
+    }
+    if ((uint32_t)k > i) {
+      for (uint32_t t = n0; t-- > i;) P.ent[slab0 + t + (k - i)] = P.ent[slab0 + t];
+    } else if ((uint32_t)k < i) {
+      for (uint32_t t = i; t < n0; t++) P.ent[slab0 + t - (i - k)] = P.ent[slab0 + t];
+    }
+    P.tail[r] = P.tail[r] - nd_old + nd_new;
+  } else {  // the walk reached the region end within kPatchMax records: nb is the region
+    n = (uint32_t)k;
+    P.exitp[r] = ex;
+    P.tail[r] = nd_new;
+  }
+  for (int t = 0; t < kPatchMax; t++)
+    if (t < k) P.ent[slab0 + t] = nb[t];
+  P.qpos[r] = x;
+  P.wcount[r] = n;
 }
 
 }  // namespace
@@ -341,14 +421,24 @@ __global__ __launch_bounds__(256) void k_frame_lane_flags(BuildParams P, int che
   }
 }
 
-// k_frame_lane_act: region r without the flag whose predecessor has it (so region r - 1 is not
-// rewritten in this pass) is walked again from region r - 1's exit.
+// k_frame_lane_act: a run of regions without the flag (region r - 1 before it has the flag, so no thread
+// of this pass rewrites it) is fixed by one thread, region by region, from region r - 1's exit: every
+// region of the run belongs to that thread only.
 template <int N>
 __global__ __launch_bounds__(256) void k_frame_lane_act(BuildParams P) {
   const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (r == 0 || r >= P.fr_nchunks || P.conv[r] || !P.conv[r - 1]) return;
-  const int64_t rend = min((int64_t)((P.fr_k0 + r + 1) << P.fr_cshift), P.data_end);
-  walk_region<N>(P, r, P.exitp[r - 1], rend);
+  const uint64_t nreg = P.fr_nchunks;
+  if (r == 0 || r >= nreg || P.conv[r] || !P.conv[r - 1] || P.exitp[r - 1] < 0) return;
+#pragma unroll 1
+  for (uint64_t q = r; q < nreg; q++) {
+    const int64_t rend = min((int64_t)((P.fr_k0 + q + 1) << P.fr_cshift), P.data_end);
+    const int64_t old_exit = P.exitp[q];
+    fix_region<N>(P, q, P.exitp[q - 1], rend);
+    if (P.exitp[q] < 0 || q + 1 >= nreg) break;
+    // on into the next region when it is part of this run, or when this fix moved the exit it agreed
+    // with and the region after it is no other run's head (whose thread reads the next region's exit)
+    if (P.conv[q + 1] && !(P.exitp[q] != old_exit && (q + 2 >= nreg || P.conv[q + 2]))) break;
+  }
 }
 
 // Chunks (16 bytes) a record's header + key + 8 slack bytes can span at the header maxima.
@@ -365,7 +455,7 @@ template <int N>
 static void launch_lane_n(const BuildParams& P, hipStream_t s, StageTimer* tm) {
   const unsigned g = (unsigned)((P.fr_nchunks + 255) / 256);
   hipLaunchKernelGGL(k_frame_lane<N>, dim3(g), dim3(256), 0, s, P);
-  for (int pass = 0; pass < 2; pass++) {
+  for (int pass = 0; pass < kLanePasses; pass++) {
     hipLaunchKernelGGL(k_frame_lane_flags, dim3(g), dim3(256), 0, s, P, 0);
     hipLaunchKernelGGL(k_frame_lane_act<N>, dim3(g), dim3(256), 0, s, P);
   }

@@ -129,6 +129,17 @@ _lib.sparkey_shard_phase_ms.argtypes = [_vp, ctypes.c_int32]
 _lib.sparkey_shard_phase_ms.restype = ctypes.c_double
 
 
+_lib.sparkey_file_last_phases.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.c_int32]
+_lib.sparkey_file_last_phases.restype = ctypes.c_int32
+
+
+def file_last_phases() -> dict:
+    """Phases (ms) of this thread's last single-GPU build_index_file."""
+    v = (ctypes.c_double * 5)()
+    _lib.sparkey_file_last_phases(v, 5)
+    return dict(zip(("open_header", "read_h2d", "build", "d2h_write", "fsync_close"), [float(x) for x in v]))
+
+
 def shard_unique_id() -> bytes:
     """An RCCL unique id (128 bytes) for sparkey_shard_comm_create; made on one rank, sent to all."""
     buf = ctypes.create_string_buffer(128)
@@ -247,7 +258,8 @@ EXPORTED = list(_SIGS) + ["sparkey_build_index_file", "sparkey_build_index_mem",
             "sparkey_plan_stage_name", "sparkey_plan_stage_ms", "sparkey_plan_destroy", "sparkey_gpu_version",
             "sparkey_strerror", "sparkey_release_cached_resources", "sparkey_shard_comm_unique_id",
             "sparkey_shard_comm_create", "sparkey_shard_comm_destroy", "sparkey_shard_geometry", "sparkey_shard_build",
-            "sparkey_shard_phase_count", "sparkey_shard_phase_name", "sparkey_shard_phase_ms"]
+            "sparkey_shard_phase_count", "sparkey_shard_phase_name", "sparkey_shard_phase_ms",
+            "sparkey_file_last_phases"]
 
 
 class SparkeyIOError(OSError):

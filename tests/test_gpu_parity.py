@@ -299,6 +299,7 @@ def test_deletes_take_k_frame(native, monkeypatch):
 # --- k_frame's bounded wait on the previous wave: a tripped wait reruns the build on the serial path ---
 def test_frame_wait_timeout_falls_back_to_serial(native, monkeypatch):
     monkeypatch.setenv("SPARKEY_NO_UNIFORM", "1")
+    monkeypatch.setenv("SPARKEY_NO_LANE", "1")  # (k_frame_lane has no waits)
     monkeypatch.setenv("SPARKEY_FRAME_SPIN_TICKS", "0")  # any wait for a predecessor trips at once
     puts = random_puts(120000, seed=31, kmin=1, kmax=40, vmin=0, vmax=60)
     got, stats = check(native, make_log(puts), 37, hash_size=8)
