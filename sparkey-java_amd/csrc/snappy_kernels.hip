@@ -495,6 +495,43 @@ __global__ void __launch_bounds__(64) k_snappy_walk(SnappyParams S) {
   walk_block(S, b, S.vlog + B.voff, B.ulen);
 }
 
+// The last index i in [0, n) with pred(i) (pred true on a prefix), -1 if none: from a guess g, gallop
+// away until the answer is bracketed, then bisect.
+template <class Pred>
+__device__ __forceinline__ int64_t gallop_last(int64_t n, int64_t g, Pred pred) {
+  int64_t lo, hi;  // lo == -1 or pred(lo); hi == n or !pred(hi); lo < hi
+  int64_t step = 1;
+  if (pred(g)) {
+    lo = g;
+    hi = n;
+    while (lo + step < n) {
+      if (!pred(lo + step)) {
+        hi = lo + step;
+        break;
+      }
+      lo += step;
+      step <<= 1;
+    }
+  } else {
+    hi = g;
+    lo = -1;
+    while (hi - step >= 0) {
+      if (pred(hi - step)) {
+        lo = hi - step;
+        break;
+      }
+      hi -= step;
+      step <<= 1;
+    }
+  }
+  while (hi - lo > 1) {
+    const int64_t m = lo + (hi - lo) / 2;
+    if (pred(m)) lo = m;
+    else hi = m;
+  }
+  return lo;
+}
+
 __global__ void __launch_bounds__(256) k_snappy_rewrite(SnappyParams S) {
   const uint64_t s = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   if (s == 0) {  // the internal build's stats: garbageSize, numEntries, maxDisplacement, hashCollisions, totalDisplacement
@@ -521,20 +558,25 @@ __global__ void __launch_bounds__(256) k_snappy_rewrite(SnappyParams S) {
   }
   uint64_t fa = 0;
   if (a != 0) {
-    uint64_t lo = 0, hi = S.nblk - 1;                          // the block holding virtual offset a
-    while (lo < hi) {
-      const uint64_t mid = (lo + hi + 1) / 2;
-      if ((uint64_t)S.blocks[mid].voff <= a) lo = mid; else hi = mid - 1;
-    }
+    // the block holding virtual offset a: the last block whose voff <= a.  Blocks hold about the same
+    // number of bytes, so the search starts at the proportional guess and gallops from there (a few
+    // dependent loads where a binary search over every block took ~15)
+    const uint64_t vbody = S.vlog_len > 84 ? (uint64_t)S.vlog_len - 84 : 1;
+    const int64_t nb = (int64_t)S.nblk;
+    const int64_t g0 = min(nb - 1, (int64_t)((double)(a - min(a, (uint64_t)84)) / (double)vbody * (double)nb));
+    const int64_t lo = max((int64_t)0, gallop_last(nb, g0, [&](int64_t b) { return (uint64_t)S.blocks[b].voff <= a; }));
     const SnappyBlock B = S.blocks[lo];
     const uint32_t rel = (uint32_t)(a - (uint64_t)B.voff);
     const uint32_t* offs = S.rec_off + lo * S.mepb;
-    uint32_t l = 0, r = min(S.walk[lo].count, S.mepb);         // entryIndex: rank of rel in the block
-    while (l < r) {
-      const uint32_t m = (l + r) / 2;
-      if (offs[m] < rel) l = m + 1; else r = m;
+    const uint32_t cnt = min(S.walk[lo].count, S.mepb);
+    // entryIndex: the rank of rel among the block's record offsets (records of about one size: the
+    // proportional guess again), the first offset >= rel
+    uint32_t l = cnt;
+    if (cnt) {
+      const int64_t g = min((int64_t)cnt - 1, (int64_t)((double)rel / (double)max(B.ulen, 1u) * (double)cnt));
+      l = (uint32_t)(gallop_last((int64_t)cnt, g, [&](int64_t i) { return offs[i] < rel; }) + 1);
     }
-    if (l >= min(S.walk[lo].count, S.mepb) || offs[l] != rel) atomicOr(S.err, 1);
+    if (l >= cnt || offs[l] != rel) atomicOr(S.err, 1);
     fa = ((uint64_t)B.file_pos << S.ebb) | l;
   }
   if (wide) {
