@@ -326,6 +326,11 @@ int sparkey_shard_build(sparkey_plan* plan, sparkey_shard_comm* comm, const uint
 int32_t sparkey_shard_phase_count(const sparkey_shard_comm* comm);
 const char* sparkey_shard_phase_name(const sparkey_shard_comm* comm, int32_t i);
 double sparkey_shard_phase_ms(const sparkey_shard_comm* comm, int32_t i);
+/* The same for rank `rank` of this process's last multi-GPU build (sparkey_build_index_mem / _file with
+ * opts.num_gpus > 1).  Diagnostics: a concurrent multi-GPU build replaces them. */
+int32_t sparkey_multi_phase_count(int32_t rank);
+const char* sparkey_multi_phase_name(int32_t rank, int32_t i);
+double sparkey_multi_phase_ms(int32_t rank, int32_t i);
 
 const char* sparkey_gpu_version(void);
 const char* sparkey_strerror(int code);

@@ -26,9 +26,12 @@ constexpr int kErrCorruptRecord = -13;  // SPARKEY_E_CORRUPT_RECORD: the iterato
 // q = mulhi(x, floor(2^64 / cap)) is floor(x / cap) or one less, so one conditional subtract
 // gives the exact remainder (checked exhaustively against '%' in tests/test_fastmod.py).
 // ---------------------------------------------------------------------------------------------
+// A table window (the sharded exact path's range-local replay) sets `base`: slots
+// are then numbered from `base` around the ring, local = (wanted - base) mod cap.
 struct FastMod {
-  uint64_t cap;  // capacity (odd, >= 1)
-  uint64_t m;    // floor(2^64 / cap); 0 when cap == 1
+  uint64_t cap;   // capacity (odd, >= 1)
+  uint64_t m;     // floor(2^64 / cap); 0 when cap == 1
+  uint64_t base;  // first slot of the window (0: the whole table)
 };
 
 __host__ __device__ inline uint64_t mulhi_u64(uint64_t a, uint64_t b) {
@@ -40,13 +43,24 @@ __host__ __device__ inline uint64_t fast_mod(uint64_t x, FastMod f) {
   const uint64_t q = mulhi_u64(x, f.m);
   uint64_t r = x - q * f.cap;
   if (r >= f.cap) r -= f.cap;
-  return r;
+  return r >= f.base ? r - f.base : r + f.cap - f.base;
 }
 
-inline FastMod make_fastmod(uint64_t cap) {
+// the table slot of window slot `local` (the reference's wantedSlot for an entry's local wanted slot)
+__host__ __device__ inline uint64_t window_to_table(uint64_t local, FastMod f) {
+  const uint64_t s = local + f.base;
+  return s >= f.cap ? s - f.cap : s;
+}
+// the window slot of table slot `slot`
+__host__ __device__ inline uint64_t table_to_window(uint64_t slot, FastMod f) {
+  return slot >= f.base ? slot - f.base : slot + f.cap - f.base;
+}
+
+inline FastMod make_fastmod(uint64_t cap, uint64_t base = 0) {
   FastMod f;
   f.cap = cap;
   f.m = cap <= 1 ? 0 : (uint64_t)(((unsigned __int128)1 << 64) / cap);
+  f.base = base;
   return f;
 }
 

@@ -438,10 +438,12 @@ __global__ __launch_bounds__(kClsBlock) void k_seg_classify(BuildParams P, int w
   if (blockIdx.x == 0 && tid < kSegClasses) P.st->n_segs[tid] = off[(uint64_t)(tid + 1) * nblk] - off[(uint64_t)tid * nblk];
 }
 
-// replay order: IN_MEMORY = address (log order); SORTING = (wantedSlot, address)
+// replay order: IN_MEMORY = address (log order); SORTING = (wantedSlot, address), the table's wanted
+// slot (a window's run may wrap the table's end)
 __device__ __forceinline__ bool seg_before(const BuildParams& P, const Entry& a, const Entry& b, int sorted_order) {
   if (sorted_order) {
-    const uint64_t wa = fast_mod(a.hash, P.mod), wb = fast_mod(b.hash, P.mod);
+    const uint64_t wa = window_to_table(fast_mod(a.hash, P.mod), P.mod);
+    const uint64_t wb = window_to_table(fast_mod(b.hash, P.mod), P.mod);
     if (wa != wb) return wa < wb;
   }
   return (a.addr & ~kDelBit) < (b.addr & ~kDelBit);

@@ -283,12 +283,24 @@ bool pool_pread(FileCtx* c, int fd, uint8_t* buf, uint64_t off, uint64_t len, in
   return *err_no == 0;
 }
 
+// Buffered writes to one file serialize on its inode lock: on the GPU box (overlayfs) one thread
+// writes a new 208 MB file at 8.5 GB/s and 2-32 threads at 7.0-8.0 (tools/io_probe.c,
+// DESIGN.md §5), so the index goes out from the calling thread unless SPARKEY_FILE_WRITE_THREADS > 1.
+int write_threads() {
+  static const int n = [] {
+    const char* v = getenv("SPARKEY_FILE_WRITE_THREADS");
+    return v ? std::max(1, atoi(v)) : 1;
+  }();
+  return n;
+}
+
 bool pool_pwrite(FileCtx* c, int fd, const uint8_t* buf, uint64_t off, uint64_t len, int* err_no) {
   std::atomic<int> fail{0};
-  const int ntask = (int)((len + kPieceBytes - 1) / kPieceBytes);
-  c->pool->run(ntask, [&](int t) {
-    uint64_t a = (uint64_t)t * kPieceBytes;
-    const uint64_t b = std::min(len, a + kPieceBytes);
+  const uint64_t piece = write_threads() > 1 ? kPieceBytes : std::max<uint64_t>(len, 1);
+  const int ntask = (int)((len + piece - 1) / piece);
+  auto task = [&](int t) {
+    uint64_t a = (uint64_t)t * piece;
+    const uint64_t b = std::min(len, a + piece);
     while (a < b) {
       const ssize_t w = pwrite(fd, buf + a, (size_t)(b - a), (off_t)(off + a));
       if (w < 0 && errno == EINTR) continue;
@@ -299,7 +311,9 @@ bool pool_pwrite(FileCtx* c, int fd, const uint8_t* buf, uint64_t off, uint64_t 
       }
       a += (uint64_t)w;
     }
-  });
+  };
+  if (ntask == 1) task(0);
+  else c->pool->run(ntask, task);
   *err_no = fail.load();
   return *err_no == 0;
 }

@@ -30,6 +30,10 @@
 // P.ent (slab_cap each).  Regions are the framing's "chunks" with fr_w = 1 (fr_cshift = log2 R).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+#include <vector>
 
 #include "build_kernels.hpp"
 #include "device_common.hpp"
@@ -218,8 +222,8 @@ __device__ __forceinline__ int64_t find_entry(const BuildParams& P, int64_t s, i
 
 // Walks the records from p while they start below rend: for each, emit(position, hash, put) (false:
 // stop there).  Returns the first record start >= rend, the position emit stopped at, or -1 at a
-// record the reference's iterator rejects (SparkeyLogIterator.java:117-136) or one whose header and
-// key do not fit the chunk array (a header VLQ longer than one byte the header maxima ruled out).
+// record the reference's iterator rejects (SparkeyLogIterator.java:117-136) or one outside the
+// header's maxima (below).
 template <int N, class Emit>
 __device__ int64_t walk_records(const BuildParams& P, int64_t p, int64_t rend, Emit&& emit) {
   const int64_t log_len = (int64_t)P.log_len;
@@ -233,23 +237,20 @@ __device__ int64_t walk_records(const BuildParams& P, int64_t p, int64_t rend, E
   while (p < rend) {
     const int o = (int)(p & 15);
     const uint64_t x = bytes8(c[0], c[1], o);
-    int32_t klen, vlen, hlen;
-    bool put;
-    if ((x & 0x8080ull) == 0) {  // one-byte VLQs (every key < 127 bytes, value < 128)
-      const int32_t b0 = (int32_t)(x & 0xff), b1 = (int32_t)((x >> 8) & 0xff);
-      hlen = 2;
-      put = b0 != 0;
-      klen = put ? b0 - 1 : b1;
-      vlen = put ? b1 : 0;
-    } else {  // the reference's VLQ rules (Util.readUnsignedVLQInt), from memory
-      auto at = [&](int64_t i) -> uint32_t { return P.log[i]; };
-      const RecHdr h = decode_header(at, p, log_len);
-      if (h.rc) return -1;
-      hlen = h.hlen; klen = h.klen; vlen = h.vlen; put = h.put != 0;
-    }
-    RecHdr hh;
-    hh.rc = 0; hh.hlen = hlen; hh.klen = klen; hh.vlen = vlen; hh.put = put;
-    if (!header_valid(hh, p, P.max_key_len, log_len) || o + hlen + klen + 8 > 16 * N) return -1;
+    // The header's maxima make every VLQ of the log one byte (frame_lane_supported): a longer one, a
+    // value over maxValueLen or a DELETE in a log that counts none cannot be on the true chain of a
+    // log the header describes, so the walk stops there as on a record the iterator rejects.  (On a
+    // false chain such a record would send the walk anywhere; on the verified chain the region keeps
+    // no exit and the host's serial walker decides, by the reference's rules.)
+    if (x & 0x8080ull) return -1;
+    const int32_t b0 = (int32_t)(x & 0xff), b1 = (int32_t)((x >> 8) & 0xff);
+    const int32_t hlen = 2;
+    const bool put = b0 != 0;
+    const int32_t klen = put ? b0 - 1 : b1;
+    const int32_t vlen = put ? b1 : 0;
+    if (klen > P.max_key_len || vlen > P.max_value_len || (!put && P.no_deletes) || p + hlen + klen > log_len ||
+        o + hlen + klen + 8 > 16 * N)
+      return -1;
     const int64_t pn = p + hlen + klen + vlen;
     // the key's remaining chunks, then the next header's two (prefetch: its latency under the hash)
     const int64_t a = p & ~15ll;
@@ -451,13 +452,46 @@ bool frame_lane_supported(const BuildParams& P) {
   return P.fr_fast && lane_chunks(P) <= kLaneMaxChunks && P.max_rec_len <= (1ll << P.fr_cshift);
 }
 
+// SPARKEY_LANE_DEBUG: regions without the flag before each fix pass (stderr; synchronizes)
+static void lane_debug(const BuildParams& P, hipStream_t s, int pass) {
+  std::vector<uint8_t> conv(P.fr_nchunks);
+  std::vector<int64_t> qp(P.fr_nchunks), ex(P.fr_nchunks);
+  if (hipMemcpyAsync(conv.data(), P.conv, conv.size(), hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipMemcpyAsync(qp.data(), P.qpos, qp.size() * 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipMemcpyAsync(ex.data(), P.exitp, ex.size() * 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess)
+    return;
+  uint64_t bad = 0, runs = 0, nofound = 0, failed = 0, first = ~0ull;
+  for (uint64_t r = 0; r < conv.size(); r++) {
+    if (!conv[r]) {
+      bad++;
+      if (r > 0 && conv[r - 1]) runs++;
+      if (first == ~0ull) first = r;
+    }
+    nofound += qp[r] == -2;
+    failed += ex[r] < 0;
+  }
+  fprintf(stderr, "[lane] pass %d: %llu of %llu regions unflagged, %llu run heads, %llu without entry, %llu without exit, first %lld\n",
+          pass, (unsigned long long)bad, (unsigned long long)conv.size(), (unsigned long long)runs,
+          (unsigned long long)nofound, (unsigned long long)failed, first == ~0ull ? -1ll : (long long)first);
+  if (first != ~0ull && first > 0)
+    fprintf(stderr, "[lane]   region %lld: qpos %lld exit %lld; previous exit %lld\n", (long long)first,
+            (long long)qp[first], (long long)ex[first], (long long)ex[first - 1]);
+}
+
 template <int N>
 static void launch_lane_n(const BuildParams& P, hipStream_t s, StageTimer* tm) {
   const unsigned g = (unsigned)((P.fr_nchunks + 255) / 256);
+  const bool dbg = getenv("SPARKEY_LANE_DEBUG") != nullptr;
   hipLaunchKernelGGL(k_frame_lane<N>, dim3(g), dim3(256), 0, s, P);
   for (int pass = 0; pass < kLanePasses; pass++) {
     hipLaunchKernelGGL(k_frame_lane_flags, dim3(g), dim3(256), 0, s, P, 0);
+    if (dbg) lane_debug(P, s, pass);
     hipLaunchKernelGGL(k_frame_lane_act<N>, dim3(g), dim3(256), 0, s, P);
+  }
+  if (dbg) {
+    hipLaunchKernelGGL(k_frame_lane_flags, dim3(g), dim3(256), 0, s, P, 0);
+    lane_debug(P, s, kLanePasses);
   }
   hipLaunchKernelGGL(k_frame_lane_flags, dim3(g), dim3(256), 0, s, P, 1);
   tm->mark("frame", s);

@@ -158,15 +158,20 @@ __global__ void k_ex_ent(const uint8_t* recv, uint64_t n, uint32_t rs, Entry* en
   ent[i] = e;
 }
 
-// slots [a, b) of the local replay (L: the local table, addresses = receive-buffer offsets) written in
-// the .spi layout through G (the rank's own slice, or a packed piece for another rank), addresses
-// mapped back to the log's: the log address sits 8 bytes before the record's header
+// table slots [a, b) of the local replay (L: the window of the rank's exact range, addresses =
+// receive-buffer offsets) written in the .spi layout through G (the rank's own slice, or a packed
+// piece for another rank), addresses mapped back to the log's: the log address sits 8 bytes before
+// the record's header
 __global__ void k_ex_extract(BuildParams L, BuildParams G, const uint8_t* recv, uint64_t n, uint32_t rs, uint64_t a,
                              uint64_t b) {
   const uint64_t slot = a + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (slot >= b) return;
   uint64_t h = 0, la = 0, ga = 0;
-  if (L.out) read_slot(L, slot, h, la);
+  if (L.out) {
+    const uint64_t w = table_to_window(slot, L.mod);
+    if (w < L.cap) read_slot(L, w, h, la);
+    else atomicOr(&L.st->guard, 4u);
+  }
   if (la) {
     const uint64_t q = la - 16;
     if (la < 16 || q % rs != 0 || q / rs >= n) {

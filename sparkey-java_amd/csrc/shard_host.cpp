@@ -1225,6 +1225,7 @@ struct Group {  // communicators for one device list, kept across calls
 
 std::mutex g_groups_mu;
 std::map<std::pair<std::vector<int>, bool>, Group*> g_groups;
+std::vector<std::vector<std::pair<std::string, double>>> g_multi_phases;  // per rank, the last build's
 
 Group* get_group(const std::vector<int>& devs, bool threads, std::string* why) {
   std::lock_guard<std::mutex> l(g_groups_mu);
@@ -1313,6 +1314,11 @@ int shard_run_threads(const sparkey_build_opts& o, const ShardRankFn& fn, char* 
       if (rcs[r]) gr->comms[r]->coll->abort();
     });
   for (auto& t : ts) t.join();
+  {
+    std::lock_guard<std::mutex> g2(g_groups_mu);
+    g_multi_phases.resize(n);
+    for (int r = 0; r < n; r++) g_multi_phases[r] = gr->comms[r]->phase;
+  }
   // the first rank's own error (not "another rank failed")
   for (int r = 0; r < n; r++)
     if (rcs[r] && msgs[r].find("another rank") == std::string::npos) {
@@ -1330,6 +1336,23 @@ int shard_run_threads(const sparkey_build_opts& o, const ShardRankFn& fn, char* 
     }
   return SPARKEY_OK;
 }
+
+extern "C" {
+int32_t sparkey_multi_phase_count(int32_t rank) {
+  std::lock_guard<std::mutex> l(g_groups_mu);
+  return rank >= 0 && rank < (int32_t)g_multi_phases.size() ? (int32_t)g_multi_phases[rank].size() : 0;
+}
+const char* sparkey_multi_phase_name(int32_t rank, int32_t i) {
+  std::lock_guard<std::mutex> l(g_groups_mu);
+  if (rank < 0 || rank >= (int32_t)g_multi_phases.size() || i < 0 || i >= (int32_t)g_multi_phases[rank].size()) return "";
+  return g_multi_phases[rank][i].first.c_str();
+}
+double sparkey_multi_phase_ms(int32_t rank, int32_t i) {
+  std::lock_guard<std::mutex> l(g_groups_mu);
+  if (rank < 0 || rank >= (int32_t)g_multi_phases.size() || i < 0 || i >= (int32_t)g_multi_phases[rank].size()) return 0.0;
+  return g_multi_phases[rank][i].second;
+}
+}  // extern "C"
 
 void shard_release_groups() {
   std::lock_guard<std::mutex> l(g_groups_mu);

@@ -2648,9 +2648,23 @@ int sparkey_shard_exact_build(sparkey_plan* pl, const uint8_t* d_recv, uint64_t 
   BuildParams& L = sh.ex_L;
   memset(&L, 0, sizeof(L));
   if (n) {
-    // the local replay: the reference's table geometry (capacity, hash size) with 8-byte addresses,
-    // which are offsets into the receive buffer
+    // the local replay runs on a window of the table: the rank's exact range [a, b) (b the next
+    // range's start around the ring; the whole ring when this is the only range), slots numbered
+    // from a.  Every record received wants a slot in it and no probe leaves it (b stays empty), so
+    // the window's table, segments and placement scratch are O(b - a), about cap / world.  Slots
+    // carry 8-byte addresses: offsets into the receive buffer.
+    const int W = sh.world;
+    const int64_t a = sh.ex_starts[sh.rank];
+    if (a < 0) {
+      set_err(err, err_len, "records received by a rank without an exact range");
+      return SPARKEY_E_GPU;
+    }
+    int64_t b = -1;
+    for (int k = 1; k <= W && b < 0; k++) b = sh.ex_starts[(sh.rank + k) % W];
+    const uint64_t cap = sh.ip.cap;
+    const uint64_t len = b == a ? cap : ((uint64_t)b + cap - (uint64_t)a) % cap;
     IndexParams ipl = sh.ip;
+    ipl.cap = getenv("SPARKEY_EXACT_FULL_TABLE") ? cap : len;
     ipl.addr_size = 8;
     ipl.ebb = 0;
     ipl.slot_size = ipl.hash_size + 8;
@@ -2658,6 +2672,8 @@ int sparkey_shard_exact_build(sparkey_plan* pl, const uint8_t* d_recv, uint64_t 
     rc = setup_params(sh.lh, ipl, sh.opts, d_recv, n * (uint64_t)sh.ex_rs, kLogHeaderSize, kLogHeaderSize, &L, err,
                       err_len);
     if (rc) return rc;
+    L.mod = make_fastmod(cap, ipl.cap == cap ? 0 : (uint64_t)a);
+    L.slot_hi = ipl.cap;
     L.st = pl->d_status;
     rc = reserve_for_framing(pl, L, 1, n, kPartTile, err, err_len);
     if (rc) return rc;

@@ -127,6 +127,12 @@ _lib.sparkey_shard_phase_name.argtypes = [_vp, ctypes.c_int32]
 _lib.sparkey_shard_phase_name.restype = ctypes.c_char_p
 _lib.sparkey_shard_phase_ms.argtypes = [_vp, ctypes.c_int32]
 _lib.sparkey_shard_phase_ms.restype = ctypes.c_double
+_lib.sparkey_multi_phase_count.argtypes = [ctypes.c_int32]
+_lib.sparkey_multi_phase_count.restype = ctypes.c_int32
+_lib.sparkey_multi_phase_name.argtypes = [ctypes.c_int32, ctypes.c_int32]
+_lib.sparkey_multi_phase_name.restype = ctypes.c_char_p
+_lib.sparkey_multi_phase_ms.argtypes = [ctypes.c_int32, ctypes.c_int32]
+_lib.sparkey_multi_phase_ms.restype = ctypes.c_double
 
 
 _lib.sparkey_file_last_phases.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.c_int32]
@@ -138,6 +144,12 @@ def file_last_phases() -> dict:
     v = (ctypes.c_double * 5)()
     _lib.sparkey_file_last_phases(v, 5)
     return dict(zip(("open_header", "read_h2d", "build", "d2h_write", "fsync_close"), [float(x) for x in v]))
+
+
+def multi_last_phases(rank: int) -> list:
+    """[(phase, ms)] of rank `rank` of this process's last num_gpus > 1 build."""
+    return [(_lib.sparkey_multi_phase_name(rank, i).decode(), _lib.sparkey_multi_phase_ms(rank, i))
+            for i in range(_lib.sparkey_multi_phase_count(rank))]
 
 
 def shard_unique_id() -> bytes:
@@ -259,6 +271,7 @@ EXPORTED = list(_SIGS) + ["sparkey_build_index_file", "sparkey_build_index_mem",
             "sparkey_strerror", "sparkey_release_cached_resources", "sparkey_shard_comm_unique_id",
             "sparkey_shard_comm_create", "sparkey_shard_comm_destroy", "sparkey_shard_geometry", "sparkey_shard_build",
             "sparkey_shard_phase_count", "sparkey_shard_phase_name", "sparkey_shard_phase_ms",
+            "sparkey_multi_phase_count", "sparkey_multi_phase_name", "sparkey_multi_phase_ms",
             "sparkey_file_last_phases"]
 
 

@@ -573,6 +573,7 @@ def test_frame3_understated_header(native):
 
 def test_frame3_wait_timeout(native, monkeypatch):
     monkeypatch.setenv("SPARKEY_FRAME_SPIN_TICKS", "0")
+    monkeypatch.setenv("SPARKEY_NO_LANE", "1")  # (k_frame_lane has no waits)
     puts = random_puts(120000, seed=81, kmin=8, kmax=64, vmin=100, vmax=100)
     got, stats = check(native, make_log(puts), 83, hash_size=8)
     assert stats.framing_path == 1, stats.as_dict()

@@ -75,7 +75,7 @@ class LaneModel:
                 return -1
             put = b0 != 0
             klen, vlen = (b0 - 1, b1) if put else (b1, 0)
-            if klen > self.mk or p + 2 + klen > len(self.log):
+            if klen > self.mk or vlen > self.mv or (not put and self.nodel) or p + 2 + klen > len(self.log):
                 return -1
             if not emit(p):
                 return p
