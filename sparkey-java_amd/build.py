@@ -40,6 +40,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
     link.  No -fgpu-rdc: every kernel is launched from its own translation unit."""
     from concurrent.futures import ThreadPoolExecutor
     os.makedirs(OBJ_DIR, exist_ok=True)
+    os.makedirs(LIB_DIR, exist_ok=True)  # lib/ holds only built files, so a fresh checkout lacks it
     jobs = []
     for s in SOURCES:
         obj = os.path.join(OBJ_DIR, os.path.basename(s) + ".o")
