@@ -170,6 +170,7 @@ struct BuildParams {
   uint64_t pair_cap;
   StatPart* parts;
   unsigned long long* place_dbg;  // SPARKEY_PLACE_DEBUG: k_place_lds phase cycles summed over blocks
+  unsigned long long* part_dbg;   // SPARKEY_PART2_DEBUG: k_part2s phase cycles, 8 words per digit
   uint64_t* scan_scratch_u64;
   MaxPlus* scan_scratch_mp;
   // k_frame granules (zeroed before every launch)
@@ -197,6 +198,7 @@ struct BuildParams {
   int32_t fr_rgn_bytes;  // LDS region per wave: W * C + fr_look + 16, rounded up to 1 KiB
   int32_t fr_mask_words;  // 64-position screen words per chunk: ceil(min(C, maxRecLen) / 64)
   uint32_t fr_wpc_magic;  // q / (8 * fr_mask_words) == (q * magic) >> 22 for every screened word q
+  int32_t place_nt;  // k_place_reg: non-temporal slot stores (SPARKEY_PLACE_NT, measurements)
   int32_t fr_fast;  // maxKeyLen + 1 < 128 and maxValueLen < 128: canonical headers are 2 bytes
   int32_t no_deletes;  // the log header counts no DELETE: speculation treats 0x00 as no record start
   uint64_t fr_nchunks;

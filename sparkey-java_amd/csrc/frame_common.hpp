@@ -192,6 +192,18 @@ __device__ __forceinline__ RecHdr decode_rgn(const uint8_t* r, int64_t R0, int64
 // LDS hand-offs are between the lanes of one wave, so they synchronise the wave, not the workgroup
 // (a wave may spin on another region's exit while its neighbours are elsewhere).  Every LDS access
 // and LDS-DMA of the wave has completed after this.
+// s_waitcnt vmcnt(n) for a run-time n (0..63; more waits for everything): gfx9 encoding, vmcnt in bits
+// 3:0 and 15:14, expcnt and lgkmcnt left at their maxima
+__device__ __forceinline__ void wait_vmcnt_upto(int n) {
+#define SK_VMW(v) \
+  case v: __builtin_amdgcn_s_waitcnt(((v) & 0xF) | (((v) >> 4) << 14) | (0x7 << 4) | (0xF << 8)); break;
+  switch (n) {
+    SK_VMW(0) SK_VMW(1) SK_VMW(2) SK_VMW(3) SK_VMW(4) SK_VMW(5) SK_VMW(6) SK_VMW(7) SK_VMW(8) SK_VMW(9) SK_VMW(10) SK_VMW(11) SK_VMW(12) SK_VMW(13) SK_VMW(14) SK_VMW(15) SK_VMW(16) SK_VMW(17) SK_VMW(18) SK_VMW(19) SK_VMW(20) SK_VMW(21) SK_VMW(22) SK_VMW(23) SK_VMW(24) SK_VMW(25) SK_VMW(26) SK_VMW(27) SK_VMW(28) SK_VMW(29) SK_VMW(30) SK_VMW(31) SK_VMW(32) SK_VMW(33) SK_VMW(34) SK_VMW(35) SK_VMW(36) SK_VMW(37) SK_VMW(38) SK_VMW(39) SK_VMW(40) SK_VMW(41) SK_VMW(42) SK_VMW(43) SK_VMW(44) SK_VMW(45) SK_VMW(46) SK_VMW(47) SK_VMW(48) SK_VMW(49) SK_VMW(50) SK_VMW(51) SK_VMW(52) SK_VMW(53) SK_VMW(54) SK_VMW(55) SK_VMW(56) SK_VMW(57) SK_VMW(58) SK_VMW(59) SK_VMW(60) SK_VMW(61) SK_VMW(62) SK_VMW(63)
+    default: __builtin_amdgcn_s_waitcnt(0); break;
+  }
+#undef SK_VMW
+}
+
 __device__ __forceinline__ void wave_sync() {
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_wave_barrier();

@@ -45,7 +45,6 @@ namespace sk {
 
 namespace {
 
-constexpr int kLaneTrial = 4;     // records a candidate entry must survive
 constexpr int kLanePasses = 4;    // fix passes (one settles what C3-like logs leave; pathological ones need more)
 constexpr int kLaneMaxChunks = 10;  // 16-byte chunks of a record's header + key (+ 8 bytes): maxKeyLen <= 126
 
@@ -180,46 +179,6 @@ __device__ __forceinline__ int32_t plausible_len(const BuildParams& P, uint64_t 
   return 1 + b0 + b1;
 }
 
-// A candidate start walked kLaneTrial records on by the screen's rules (it may run past lim: a chain
-// that reaches the frame end survives).
-__device__ __forceinline__ bool survives(const BuildParams& P, int64_t q, int64_t lim) {
-#pragma unroll 1
-  for (int t = 0; t < kLaneTrial && q < lim; t++) {
-    const int64_t a = q & ~15ll;
-    const int o = (int)(q & 15);
-    const uint4 c0 = chunk_at(P, a);
-    const uint4 c1 = o >= 15 ? chunk_at(P, a + 16) : make_uint4(0, 0, 0, 0);
-    const int32_t L = plausible_len(P, bytes8(c0, c1, o));
-    if (!L) return false;
-    q += L;
-  }
-  return true;
-}
-
-// The first record start >= s that survives the trial walk (s's region has one: R >= maxRecLen), or -1.
-__device__ __forceinline__ int64_t find_entry(const BuildParams& P, int64_t s, int64_t frame_end) {
-  const int64_t wend = min(s + P.max_rec_len, frame_end);  // a true start lies in [s, wend)
-  const Screen8 scn = make_screen8(P);
-  int64_t a = s & ~15ll;
-#pragma unroll 1
-  for (; a < wend; a += 16) {
-    const uint4 c0 = chunk_at(P, a), c1 = chunk_at(P, a + 16);
-    const uint64_t x0 = lo64(c0), x1 = hi64(c0), x2 = lo64(c1);
-    uint32_t m = screen8(x0, (x0 >> 8) | (x1 << 56), scn) | (screen8(x1, (x1 >> 8) | (x2 << 56), scn) << 8);
-    if (a < s) m &= ~0u << (int)(s - a);
-    if (wend - a < 16) m &= (1u << (int)(wend - a)) - 1u;
-#pragma unroll 1
-    while (m) {
-      const int o = __builtin_ctz(m);
-      m &= m - 1;
-      const int64_t c = a + o;
-      const int32_t L = plausible_len(P, bytes8(c0, c1, o));
-      if (L && survives(P, c + L, frame_end)) return c;
-    }
-  }
-  return -1;
-}
-
 // Walks the records from p while they start below rend: for each, emit(position, hash, put) (false:
 // stop there).  Returns the first record start >= rend, the position emit stopped at, or -1 at a
 // record the reference's iterator rejects (SparkeyLogIterator.java:117-136) or one outside the
@@ -351,6 +310,24 @@ __device__ void fix_region(const BuildParams& P, uint64_t r, int64_t x, int64_t 
     return;
   }
   uint32_t n;
+  if (merged && i == 0 && r > 0) {
+    // The walk from x reached the region's first record: nb is the run between the previous region's
+    // exit and this region's entry.  It follows the previous region's records in the log, so it goes
+    // at the end of that region's slab (this region's slab is right as it is).
+    const uint64_t pslab = (r - 1) * (uint64_t)P.slab_cap;
+    const uint32_t pn = P.wcount[r - 1];
+    if (pn + (uint32_t)k > P.slab_cap) {
+      atomicMax(&P.st->max_wave_count, pn + (uint32_t)k);
+      P.wcount[r - 1] = pn + (uint32_t)k;
+      return;
+    }
+    for (int t = 0; t < kPatchMax; t++)
+      if (t < k) P.ent[pslab + pn + t] = nb[t];
+    P.wcount[r - 1] = pn + (uint32_t)k;
+    P.tail[r - 1] += nd_new;
+    P.exitp[r - 1] = P.qpos[r];
+    return;
+  }
   if (merged) {  // new prefix nb[0, k) + original [i, n0)
     n = (uint32_t)k + (n0 - i);
     if (n > P.slab_cap) {
@@ -377,24 +354,281 @@ __device__ void fix_region(const BuildParams& P, uint64_t r, int64_t x, int64_t 
 
 }  // namespace
 
-// Regions of the frame: region k (k from fr_k0) covers [k << fr_cshift, (k + 1) << fr_cshift) of the
-// log, clipped to [fr_entry, frame end).
-template <int N>
-__global__ __launch_bounds__(256) void k_frame_lane(BuildParams P) {
-  const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= P.fr_nchunks) return;
-  const int64_t frame_end = P.data_end;
-  const int64_t s = r == 0 ? P.fr_entry : (int64_t)((P.fr_k0 + r) << P.fr_cshift);
-  const int64_t rend = min((int64_t)((P.fr_k0 + r + 1) << P.fr_cshift), frame_end);
-  int64_t entry = r == 0 ? s : find_entry(P, s, frame_end);
-  if (entry < 0) {  // no surviving candidate: the fix pass walks it from the previous exit
-    P.qpos[r] = -2;
-    P.exitp[r] = -1;
-    P.tail[r] = 0;
-    P.wcount[r] = 0;
-    return;
+// ------------------------------------------------------------------------------------------------
+// k_frame_lane: the ring.  Lane L of a wave walks region r = 64 w + L, but the wave loads the log
+// for all 64 lanes together: slice k of a lane's stream is bytes [b + kZ, b + (k + 1)Z) of its
+// region (b = region start rounded down to 16), and one slice of every lane is 64 Z bytes fetched by
+// 64 Z / 1024 LDS-DMA instructions in which Z / 16 consecutive lanes fetch the Z bytes of one region
+// -- whole lines, 1 KiB per instruction, as coalesced as a contiguous copy.  The ring holds kRingNS
+// slices per lane (512 bytes: slot-major, lane-minor, Z bytes each); the wave refills the slots the
+// slowest lane has left, and each lane walks as far as the landed bytes allow.
+// ------------------------------------------------------------------------------------------------
+constexpr int kRingWin = 512;     // bytes of a lane's stream the ring holds
+constexpr int kLaneTail = 768;    // bytes a lane streams past its region end (the walk on to the next entry)
+constexpr int kConvMax = 12;      // record starts of the first surviving chain kept for the join test
+
+template <int Z>
+struct Ring {
+  static constexpr int NS = kRingWin / Z;  // slots
+  static constexpr int SLOT = 64 * Z;      // bytes of one slot (a slice of every lane)
+  const uint8_t* lds;
+  uint32_t lane_off;  // lane * Z
+  __device__ __forceinline__ uint64_t al8(int32_t a) const {  // a: stream offset, multiple of 8
+    const uint32_t u = (uint32_t)a;
+    return *reinterpret_cast<const uint64_t*>(lds + ((u / Z) % NS) * SLOT + lane_off + (u % Z));
   }
-  walk_region<N>(P, r, entry, rend);
+  __device__ __forceinline__ uint64_t u64(int32_t a) const {  // the 8 bytes at stream offset a
+    const int32_t a0 = a & ~7;
+    const uint64_t lo = al8(a0), hi = al8(a0 + 8);
+    const int sh = (a & 7) * 8;
+    return sh ? (lo >> sh) | (hi << (64 - sh)) : lo;
+  }
+};
+
+template <int Z>
+struct RingKey {  // a key at stream offset base (murmur*_ld's loader)
+  const Ring<Z>& R;
+  int32_t base;
+  __device__ __forceinline__ uint64_t u64(int o) const { return R.u64(base + o); }
+};
+
+// The entry of a region: a record start m at or after its start, on the log's true chain whatever
+// the record before the region is.  Candidates are the plausible starts in [so, so + span) (the screen
+// of §2.1; the true first start is one of them).  A = the first candidate whose chain stays plausible
+// through the ring's first 512 bytes (or to the frame end); every later candidate must die or join
+// A's chain (land on one of its starts) inside that window.  The true first start is A or a joiner,
+// so the true chain runs through m = the last join point (A when none joins).  Returns -1 when that
+// cannot be decided inside the window (the fix pass walks the region from the previous exit).
+template <int Z>
+__device__ int32_t ring_entry(const BuildParams& P, const Ring<Z>& R, int32_t so, int32_t span, int32_t deo) {
+  constexpr int32_t hlim = kRingWin - 16;  // headers readable below this (16 bytes from the 8-aligned offset)
+  int32_t ca[kConvMax];
+  int nca = 0;
+  int32_t A = -1, mj = -1, alast = -1;
+  bool undecided = false;
+  const Screen8 scn = make_screen8(P);
+  const int32_t cend = min(so + span, deo);
+#pragma unroll 1
+  for (int32_t a = so & ~15; a < cend; a += 16) {
+    const uint64_t x0 = R.al8(a), x1 = R.al8(a + 8), x2 = R.al8(a + 16);
+    uint32_t m = screen8(x0, (x0 >> 8) | (x1 << 56), scn) | (screen8(x1, (x1 >> 8) | (x2 << 56), scn) << 8);
+    if (a < so) m &= ~0u << (int)(so - a);
+    if (cend - a < 16) m &= (1u << (int)(cend - a)) - 1u;
+#pragma unroll 1
+    while (m) {
+      const int32_t c = a + (int32_t)__builtin_ctz(m);
+      m &= m - 1;
+      if (A < 0) {  // the chain of c through the window
+        int32_t p = c;
+        int n = 0;
+        bool alive = true;
+#pragma unroll 1
+        while (p < deo && p < hlim && n < kConvMax) {  // (tiny records: the list's first kConvMax starts)
+          const int32_t L = plausible_len(P, R.u64(p));
+          if (!L) {
+            alive = false;
+            break;
+          }
+#pragma unroll
+          for (int k = 0; k < kConvMax; k++)
+            if (k == n) ca[k] = p;
+          n++;
+          alast = p;
+          p += L;
+        }
+        if (alive) {
+          A = c;
+          nca = n;
+        }
+      } else {  // c dies, or joins A's chain, or stays undecided
+        int32_t p = c;
+#pragma unroll 1
+        for (;;) {
+          bool on = false;
+#pragma unroll
+          for (int k = 0; k < kConvMax; k++) on |= k < nca && ca[k] == p;
+          if (on) {
+            mj = max(mj, p);
+            break;
+          }
+          if (p >= deo || p >= hlim || (nca == kConvMax && p > alast)) {  // undecided: A, speculatively
+            undecided = true;
+            break;
+          }
+          const int32_t L = plausible_len(P, R.u64(p));
+          if (!L) break;
+          p += L;
+        }
+      }
+    }
+  }
+  // (undecided: the boundary check after the walk decides, and the fix pass repairs a wrong guess)
+  (void)undecided;
+  return A < 0 ? -1 : max(A, mj);
+}
+
+// Regions of the frame: region k (k from fr_k0) covers [k << fr_cshift, (k + 1) << fr_cshift) of the
+// log, clipped to [fr_entry, frame end).  One wave per 64 regions.
+template <int Z>
+__global__ __launch_bounds__(64) void k_frame_lane(BuildParams P) {
+  using RingT = Ring<Z>;
+  constexpr int NS = RingT::NS;
+  constexpr int LPR = Z / 16;     // lanes fetching one row (region) of a slice
+  constexpr int RPI = 64 / LPR;   // rows per DMA instruction
+  constexpr int NI = 64 / RPI;    // DMA instructions per slice
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int lane = threadIdx.x;
+  const uint64_t nreg = P.fr_nchunks;
+  const uint64_t r0 = (uint64_t)blockIdx.x * 64;
+  const uint64_t r = r0 + lane;
+  const bool active = r < nreg;
+  const int64_t log_len = (int64_t)P.log_len, frame_end = P.data_end;
+  const int cs = P.fr_cshift;
+  auto reg_start = [&](uint64_t q) -> int64_t { return q == 0 ? P.fr_entry : (int64_t)((P.fr_k0 + q) << cs); };
+  auto reg_end = [&](uint64_t q) -> int64_t { return min((int64_t)((P.fr_k0 + q + 1) << cs), frame_end); };
+  // the wave's base (its first region's 16-aligned start): every row base below is 32-bit from it
+  const int64_t Wb = reg_start(r0) & ~15ll;
+  // this lane's region [s, e), its stream base b (16-aligned) and streamed bytes [b, se)
+  const int64_t s = active ? reg_start(r) : Wb, e = active ? reg_end(r) : Wb;
+  const int64_t b = s & ~15ll;
+  const int64_t se = active ? min(e + kLaneTail, log_len) : b;
+  // per DMA instruction i: the row this lane fetches for (LPR lanes a row), its base and stream length
+  int32_t rowb[NI], rowl[NI];
+#pragma unroll
+  for (int i = 0; i < NI; i++) {
+    const uint64_t q = r0 + (uint64_t)(RPI * i + lane / LPR);
+    rowb[i] = 0;
+    rowl[i] = 0;
+    if (q < nreg) {
+      const int64_t qb = reg_start(q) & ~15ll;
+      rowb[i] = (int32_t)(qb - Wb);
+      rowl[i] = (int32_t)(min(reg_end(q) + kLaneTail, log_len) - qb);
+    }
+  }
+  unsigned long long streaming = __ballot(active);  // rows whose lanes still walk
+  // Slice k of every row into its slot: NI instructions, always all of them (the wait below counts
+  // them), lanes of finished or absent rows fetching the log's first line into their unused cells.
+  auto issue = [&](int k) {
+    uint8_t* slot = lds + (uint32_t)(k % NS) * RingT::SLOT;
+    const int32_t off = k * Z + (lane % LPR) * 16;
+#pragma unroll
+    for (int i = 0; i < NI; i++) {
+      const int row = RPI * i + lane / LPR;
+      const bool need = off < rowl[i] && ((streaming >> row) & 1ull);
+      const int64_t a = Wb + rowb[i] + off;
+      const bool tail = need && a + 16 > log_len;  // (the log's last bytes: a guarded copy instead)
+      if (!tail)
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(P.log + (need ? a : 0)),
+                                         (__attribute__((address_space(3))) void*)(slot + i * 1024), 16, 0, 2);
+      if (tail) *reinterpret_cast<uint4*>(slot + i * 1024 + lane * 16) = load16_guarded(P.log, a, log_len);
+    }
+  };
+  // prologue: the ring's NS slices (the entry phase reads all of them)
+#pragma unroll 1
+  for (int k = 0; k < NS; k++) issue(k);
+  __builtin_amdgcn_s_waitcnt(0);
+  __builtin_amdgcn_wave_barrier();
+  const RingT R{lds, (uint32_t)lane * Z};
+  const int32_t so = (int32_t)(s - b), eo = (int32_t)(e - b);
+  const int32_t deo = (int32_t)min((int64_t)0x3fffffff, frame_end - b);
+  const int32_t slim = (int32_t)(se - b);  // streamed bytes of this lane
+  const int32_t lo_max = (int32_t)min((int64_t)0x3fffffff, log_len - b);
+  int32_t m = -1;
+  if (active) m = r == 0 ? so : ring_entry<Z>(P, R, so, (int32_t)min((int64_t)P.max_rec_len, e - s), deo);
+  // the next region's entry (lane + 1; the wave's last lane leaves that boundary to the fix pass):
+  // the lane walks on past its region end to it, so that the boundary agrees without a fix
+  const int32_t mn = __shfl(m, (lane + 1) & 63, 64);
+  int32_t tgt = -1;  // (stream offset)
+  if (active && lane < 63 && r + 1 < nreg && mn >= 0) tgt = (int32_t)((reg_start(r + 1) & ~15ll) + mn - b);
+  const uint64_t slab0 = r * (uint64_t)P.slab_cap;
+  uint32_t n = 0, nd = 0;
+  int32_t pos = m, ex = -1;
+  bool done = !active || m < 0, failed = false;
+  int kb = 0, kl = NS, kland = NS;  // ring: slices [kb, kb + NS); issued below kl, landed below kland
+#pragma unroll 1
+  for (;;) {
+    const int32_t hv = kland * Z;  // landed stream bytes
+    const bool all_in = hv >= slim;
+    // every lane walks the records whose bytes have landed (a lane whose next key has not: blocked
+    // until the next slice)
+    bool blocked = false;
+#pragma unroll 1
+    for (;;) {
+      bool go = false;
+      if (!done && !blocked) {
+        if (pos >= eo && pos >= tgt) {  // past the region end, at (or past) the next region's entry
+          done = true;
+          ex = pos;
+        } else if ((pos & ~7) + 16 > slim) {  // the stream ends (a walk to the next entry longer than the tail)
+          done = true;
+          ex = pos >= eo ? pos : -1;
+        } else if ((pos & ~7) + 16 <= hv) {
+          go = true;
+        } else {
+          blocked = true;
+        }
+      }
+      if (!__any(go)) break;
+      if (go) {
+        const uint64_t x = R.u64(pos);
+        const int32_t b0 = (int32_t)(x & 0xff), b1 = (int32_t)((x >> 8) & 0xff);
+        const bool put = b0 != 0;
+        const int32_t klen = put ? b0 - 1 : b1;
+        const int32_t vlen = put ? b1 : 0;
+        const int32_t kend = pos + 2 + klen;
+        // The header's maxima make every VLQ of the log one byte (frame_lane_supported): anything else
+        // ends the walk, as a record the iterator rejects would (SparkeyLogIterator.java:117-136); the
+        // fix pass and then the serial walker decide on such a region.
+        if ((x & 0x8080ull) || klen > P.max_key_len || vlen > P.max_value_len || (!put && P.no_deletes) ||
+            kend > lo_max) {
+          done = true;
+          failed = true;
+        } else if (kend + 16 > slim && slim < lo_max) {  // the key runs past the stream (a long walk on)
+          done = true;
+          ex = pos >= eo ? pos : -1;
+        } else if (all_in || ((kend + 16) & ~7) + 8 <= hv) {
+          const RingKey<Z> ld{R, pos + 2};
+          const uint64_t hash = P.hash_size == 8 ? murmur64_ld(ld, klen, (uint32_t)P.seed)
+                                                 : (uint64_t)murmur32_ld(ld, klen, (uint32_t)P.seed);
+          if (n < P.slab_cap) {
+            Entry en;
+            en.hash = hash;
+            en.addr = ((uint64_t)(b + pos) << P.ebb) | (put ? 0ull : kDelBit);
+            P.ent[slab0 + n] = en;
+          }
+          n++;
+          nd += put ? 0u : 1u;
+          pos = kend + vlen;
+        } else {
+          blocked = true;  // (the key's bytes have not all landed: the lane waits for the next slice)
+        }
+      }
+    }
+    streaming = __ballot(!done);
+    if (!streaming) break;
+    // slots below the slowest lane's slice are free: refill them, then wait for the next slice
+    int32_t kmin = done ? 0x7fffffff : pos / Z;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) kmin = min(kmin, __shfl_xor(kmin, o, 64));
+    kb = max(kb, (int)kmin);
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the ring's reads are done before its slots refill
+#pragma unroll 1
+    while (kl < kb + NS) issue(kl++);
+    if (kland < kl) {
+      wait_vmcnt_upto((kl - kland - 1) * NI);  // loads complete in order: the later slices stay in flight
+      kland++;
+    } else {  // (unreachable: the slowest lane's next record always lies in a full ring)
+      if (!done) failed = true;
+      break;
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  if (!active) return;
+  if (n > P.slab_cap) atomicMax(&P.st->max_wave_count, n);  // the host grows the slabs and redoes the build
+  P.qpos[r] = m < 0 ? -2 : b + m;
+  P.exitp[r] = (m < 0 || failed || ex < 0) ? -1 : b + ex;
+  P.tail[r] = m < 0 ? 0 : nd;
+  P.wcount[r] = m < 0 ? 0 : n;
 }
 
 // The fix (see the file comment), in passes of two launches so that no region is read while it is
@@ -448,8 +682,11 @@ static int lane_chunks(const BuildParams& P) {
   return (int)((need + 15) / 16);
 }
 
+// One-byte VLQs (the ring walk decodes 2-byte headers), records within a region, and an entry screen
+// (maxRecLen positions plus the 16-byte reads past them) inside the ring's first 512 bytes.
 bool frame_lane_supported(const BuildParams& P) {
-  return P.fr_fast && lane_chunks(P) <= kLaneMaxChunks && P.max_rec_len <= (1ll << P.fr_cshift);
+  return P.fr_fast && lane_chunks(P) <= kLaneMaxChunks && P.max_rec_len <= (1ll << P.fr_cshift) &&
+         P.max_rec_len + 15 + 32 <= kRingWin - 16;
 }
 
 // SPARKEY_LANE_DEBUG: regions without the flag before each fix pass (stderr; synchronizes)
@@ -483,7 +720,15 @@ template <int N>
 static void launch_lane_n(const BuildParams& P, hipStream_t s, StageTimer* tm) {
   const unsigned g = (unsigned)((P.fr_nchunks + 255) / 256);
   const bool dbg = getenv("SPARKEY_LANE_DEBUG") != nullptr;
-  hipLaunchKernelGGL(k_frame_lane<N>, dim3(g), dim3(256), 0, s, P);
+  // the ring kernel: one wave per 64 regions, 512 bytes of LDS per lane; slices of 128 bytes (or 64:
+  // SPARKEY_LANE_Z=64, a measurement)
+  const unsigned gw = (unsigned)((P.fr_nchunks + 63) / 64);
+  static const int z = [] {
+    const char* v = getenv("SPARKEY_LANE_Z");
+    return v && atoi(v) == 64 ? 64 : 128;
+  }();
+  if (z == 64) hipLaunchKernelGGL(k_frame_lane<64>, dim3(gw), dim3(64), 64 * kRingWin, s, P);
+  else hipLaunchKernelGGL(k_frame_lane<128>, dim3(gw), dim3(64), 64 * kRingWin, s, P);
   for (int pass = 0; pass < kLanePasses; pass++) {
     hipLaunchKernelGGL(k_frame_lane_flags, dim3(g), dim3(256), 0, s, P, 0);
     if (dbg) lane_debug(P, s, pass);

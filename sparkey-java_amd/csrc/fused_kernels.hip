@@ -1237,9 +1237,18 @@ __global__ __launch_bounds__(kPart2Block) void k_part2s(BuildParams P) {
   // region cursor is the bucket count), so the digit is read once; a bucket that outgrows its region
   // (more entries than k_place_lds stages anyway) makes the host redo the build with dense runs
   const bool fixed = P.p2_fixed != 0;
+  long long t_prev2 = P.part_dbg ? clock64() : 0;
+  auto mark2 = [&](int i) {  // (SPARKEY_PART2_DEBUG: thread 0's cycles per phase)
+    if (P.part_dbg && tid == 0) {
+      const long long now = clock64();
+      P.part_dbg[8 * (uint64_t)dpart + i] = now - t_prev2;
+      t_prev2 = now;
+    }
+  };
   for (uint32_t i = tid; i < nbins * 512 + 2 * nbins; i += kPart2Block) dyn[i] = 0;
   if (tid < (int)kP2SortedMaxBpp) s_fun[tid] = MaxPlus{0, 0};
   __syncthreads();
+  mark2(0);
   bool ovf = false;
   for (uint32_t q = 0; q < nseg; q++) {
     const uint64_t ra = seg ? seg[2 * q] : lo, rz = seg ? seg[2 * q + 1] : hi;
@@ -1269,7 +1278,9 @@ __global__ __launch_bounds__(kPart2Block) void k_part2s(BuildParams P) {
     }
   }
   if (ovf) atomicOr(&P.st->p2_overflow, 1u);
+  mark2(1);
   __syncthreads();
+  mark2(2);
   bool big = false;
   for (uint32_t b = tid; b < nbins; b += kPart2Block) big |= btot[b] > 65535u;
   const bool summarise = !__syncthreads_or(big);
@@ -1331,8 +1342,10 @@ __global__ __launch_bounds__(kPart2Block) void k_part2s(BuildParams P) {
       s_fun[b] = f;
     }
   }
+  mark2(3);
   if (P.fused_carry) {
     part2_fused_carry(P, s_fun, nbins, b0, dpart);
+    mark2(4);
     return;
   }
   if (fixed) return;
@@ -1665,6 +1678,295 @@ __global__ __launch_bounds__(kPlaceLdsBlock) void k_place_lds(BuildParams P) {
 
 
 // ================================================================================================
+// k_place_reg: k_place_lds's placement with the entries kept in registers and stored straight to
+// their slots.  Per bucket: the 16-bit count of each wanted slot (its atomic is the entry's place
+// in its group), one scan for base[s] (entries wanted before s) and M[s] (the prefix max of
+// s - base[s] over occupied s), the entries copied to base[w] + cursor so that each group of equal
+// wanted slots lies together, then every entry's rank in its group by address (IndexHash.java:647-650,
+// SortHelper's (wantedSlot, address) order) and its position j + max(carry, M[w]).  The block writes
+// its slots [x, hi): its entries from registers, zeros where its occupancy bitmap is clear.  22.5 KiB
+// of LDS (k_place_lds: 36 KiB), 4 waves: 7 blocks per CU in flight against k_place_lds's 4.
+// ================================================================================================
+constexpr int kPlaceRegBlock = 256;
+constexpr int kPlaceRegPer = kPlaceLdsMax / kPlaceRegBlock;
+
+__global__ __launch_bounds__(kPlaceRegBlock) void k_place_reg(BuildParams P) {
+  constexpr int NW = kPlaceRegBlock / 64;
+  static_assert(kBucket == 4 * kPlaceRegBlock, "four wanted slots per thread in the scan");
+  __shared__ uint32_t cnt[kBucket / 2];          // 16-bit entry count per wanted slot
+  __shared__ uint32_t meta[kBucket];             // base[s] | (M[s] + 32768) << 16
+  __shared__ Entry buf[kPlaceLdsMax];            // each group's members together (any order inside)
+  __shared__ uint32_t occ[2 * kBucket / 32];     // slots [x, x + 2 kBucket) holding this block's entries
+  __shared__ uint32_t wsum[NW];
+  __shared__ int32_t wmax[NW];
+  __shared__ uint64_t sh64[NW + 1];
+  __shared__ unsigned long long pair_base;
+  __shared__ unsigned long long r_sum[NW], r_col[NW];
+  __shared__ long long r_max[NW];
+  __shared__ int32_t s_pend;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const Status* st = P.st;
+  const unsigned ovf = st->overflow | st->p2_overflow, full = st->full;
+  const unsigned long long nrec = st->n_records, ndel = st->n_deletes, npairs0 = st->n_pairs;
+  const uint64_t b = P.b_lo + blockIdx.x;
+  const uint32_t n = P.bcount[b];
+  const uint64_t eoff = P.boff[b];
+  int64_t x;
+  if (P.fused_carry) {
+    const MaxPlus pre = P.bpre[b];
+    x = max(pre.c, P.dcarry[b / P.bpp] + pre.a);
+  } else {
+    x = P.carry[b];
+  }
+  if (ovf != 0 || nrec > P.max_records) return;  // build_aborted
+  if (P.fused_carry && tid == 0) P.carry[b] = x;  // (for the global-memory placement's readers)
+  const uint64_t start = b << kBucketShift;
+  const int64_t bsize = (int64_t)min((uint64_t)kBucket, P.cap - start);
+  if (n > kPlaceLdsMax) {
+    if (tid == 0) atomicOr(&P.st->big_buckets, 1u);
+    return;
+  }
+  Entry mine[kPlaceRegPer];
+#pragma unroll
+  for (int k = 0; k < kPlaceRegPer; k++) {
+    const uint32_t i = tid + k * kPlaceRegBlock;
+    if (i < n) mine[k] = P.ent2[eoff + i];
+  }
+  // (the loads are in flight while the counts are cleared)
+  for (int t = tid; t < kBucket / 2; t += kPlaceRegBlock) cnt[t] = 0;
+  if (tid < 2 * kBucket / 32) occ[tid] = 0;
+  if (tid == 0) s_pend = 0;
+  __syncthreads();
+  uint32_t want[kPlaceRegPer], cur[kPlaceRegPer];
+#pragma unroll
+  for (int k = 0; k < kPlaceRegPer; k++) {
+    const uint32_t i = tid + k * kPlaceRegBlock;
+    if (i < n) {
+      want[k] = (uint32_t)(fast_mod(mine[k].hash, P.mod) - start);
+      const uint32_t sh = (want[k] & 1u) * 16u;
+      cur[k] = (atomicAdd(&cnt[want[k] >> 1], 1u << sh) >> sh) & 0xffffu;
+    }
+  }
+  __syncthreads();
+  // scan of slots 4 tid .. 4 tid + 3: base (exclusive count) and M (prefix max of s - base[s] over
+  // occupied s), one barrier: a wave's max of (s - its local base) needs only the waves' sums after it
+  {
+    const uint32_t w0 = cnt[2 * tid], w1 = cnt[2 * tid + 1];
+    const uint32_t c[4] = {w0 & 0xffffu, w0 >> 16, w1 & 0xffffu, w1 >> 16};
+    const uint32_t tot = c[0] + c[1] + c[2] + c[3];
+    uint32_t incl = tot;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t t = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += t;
+    }
+    constexpr int32_t kNone = -(1 << 20);
+    uint32_t lb[4];
+    int32_t v = kNone;  // max over this thread's occupied slots of s - (wave-local base)
+    {
+      uint32_t run = incl - tot;
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        lb[i] = run;
+        if (c[i]) v = max(v, (int32_t)(4 * tid + i) - (int32_t)run);
+        run += c[i];
+      }
+    }
+    int32_t mi = v;  // inclusive wave prefix max
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int32_t t = __shfl_up(mi, o, 64);
+      if (lane >= o) mi = max(mi, t);
+    }
+    if (lane == 63) {
+      wsum[wv] = incl;
+      wmax[wv] = mi;
+    }
+    __syncthreads();
+    uint32_t off = 0;
+    int32_t pre = kNone;
+#pragma unroll
+    for (int u = 0; u < NW; u++) {
+      if (u < wv) {
+        pre = max(pre, wmax[u] == kNone ? kNone : wmax[u] - (int32_t)off);
+        off += wsum[u];
+      }
+    }
+    int32_t ex = __shfl_up(mi, 1, 64);  // exclusive wave prefix max (wave-local), then block-level
+    if (lane == 0) ex = kNone;
+    int32_t m = max(pre, ex == kNone ? kNone : ex - (int32_t)off);
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const uint32_t base = off + lb[i];
+      if (c[i]) m = max(m, (int32_t)(4 * tid + i) - (int32_t)base);
+      const int32_t mc = max(m, -32768);
+      meta[4 * tid + i] = base | ((uint32_t)(mc + 32768) << 16);
+    }
+  }
+  __syncthreads();
+  uint32_t bw[kPlaceRegPer], g[kPlaceRegPer];
+#pragma unroll
+  for (int k = 0; k < kPlaceRegPer; k++) {
+    const uint32_t i = tid + k * kPlaceRegBlock;
+    if (i < n) {
+      bw[k] = meta[want[k]] & 0xffffu;
+      g[k] = (cnt[want[k] >> 1] >> ((want[k] & 1u) * 16u)) & 0xffffu;
+      buf[bw[k] + cur[k]] = mine[k];
+    }
+  }
+  __syncthreads();
+  // Equal wanted slots in address order: each member counts the members with smaller addresses.
+  // Equal-hash PUT pairs are duplicate-key candidates for the pair list (as k_place_lds).
+  const bool want_pairs = ndel == 0 && npairs0 <= P.pair_cap;
+  uint32_t npair = 0;
+  uint32_t rank[kPlaceRegPer];
+  bool same_prev[kPlaceRegPer];  // the member ranked just before this one has its hash
+#pragma unroll
+  for (int k = 0; k < kPlaceRegPer; k++) {
+    const uint32_t i = tid + k * kPlaceRegBlock;
+    rank[k] = 0;
+    same_prev[k] = false;
+    if (i >= n || g[k] < 2) continue;
+    const Entry* grp = buf + bw[k];
+    const uint64_t ai = mine[k].addr & ~kDelBit;
+    const bool cp = want_pairs && !(mine[k].addr & kDelBit) && g[k] <= kGroupMax;
+    if (g[k] > kGroupMax && cur[k] == 0) atomicOr(&P.st->dup_overflow, 1u);
+    uint32_t r = 0;
+    uint64_t best = 0;
+    bool have = false;
+    for (uint32_t u = 0; u < g[k]; u++) {
+      const Entry e = grp[u];
+      const uint64_t aj = e.addr & ~kDelBit;
+      if (aj < ai) {
+        r++;
+        if (!have || aj > best) {
+          best = aj;
+          have = true;
+          same_prev[k] = e.hash == mine[k].hash;
+        }
+      }
+      npair += cp && aj > ai && e.hash == mine[k].hash && !(e.addr & kDelBit);
+    }
+    rank[k] = r;
+  }
+  const bool any_pair = __syncthreads_or(npair != 0);
+  if (any_pair) {  // (block-uniform)
+    uint64_t pair_total = 0;
+    const uint64_t pair_off = block_excl_sum<kPlaceRegBlock>(npair, sh64, &pair_total);
+    if (tid == 0) pair_base = atomicAdd(&P.st->n_pairs, (unsigned long long)pair_total);
+    __syncthreads();
+    unsigned long long slotn = pair_base + pair_off;
+#pragma unroll
+    for (int k = 0; k < kPlaceRegPer; k++) {
+      const uint32_t i = tid + k * kPlaceRegBlock;
+      if (i >= n || !npair || g[k] < 2 || g[k] > kGroupMax || (mine[k].addr & kDelBit)) continue;
+      const Entry* grp = buf + bw[k];
+      const uint64_t ai = mine[k].addr & ~kDelBit;
+      for (uint32_t u = 0; u < g[k]; u++) {
+        const Entry e = grp[u];
+        if ((e.addr & ~kDelBit) <= ai || !is_put_pair(mine[k], e)) continue;
+        if (slotn < P.pair_cap) {
+          P.pairs[2 * slotn] = mine[k].addr;
+          P.pairs[2 * slotn + 1] = e.addr;
+        }
+        slotn++;
+      }
+    }
+  }
+  if (full) return;
+  // positions, the entries' slots, the occupancy bitmap and the displacements
+  // (scattered slot stores go through L2, which merges each line's slots: non-temporal ones would
+  // reach memory as partial lines; P.place_nt = 1 measures that)
+  const bool nt16 = P.slot_size == 16 && !P.sharded && P.uni_nt && P.place_nt;
+  const uint64_t lim = P.sharded ? P.slot_hi : ~0ull;
+  unsigned long long sum_d = 0, col = 0;
+  long long max_d = 0;
+  int32_t pend = 0;
+  int64_t pos[kPlaceRegPer];
+#pragma unroll
+  for (int k = 0; k < kPlaceRegPer; k++) {
+    const uint32_t i = tid + k * kPlaceRegBlock;
+    pos[k] = -1;
+    if (i >= n) continue;
+    const int32_t M = (int32_t)(meta[want[k]] >> 16) - 32768;
+    const int64_t p = (int64_t)(bw[k] + rank[k]) + max(x, (int64_t)M);
+    pos[k] = p;
+    const uint64_t slot = p < bsize ? start + (uint64_t)p : wrap_slot(start + (uint64_t)p, P.cap);
+    const uint64_t hh = mine[k].hash, aa = mine[k].addr & ~kDelBit;
+    if (nt16) {
+      typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+      u32x4 w;
+      w.x = (uint32_t)hh;
+      w.y = (uint32_t)(hh >> 32);
+      w.z = (uint32_t)aa;
+      w.w = (uint32_t)(aa >> 32);
+      __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(P.out + kIndexHeaderSize + slot * 16ull));
+    } else {
+      put_slot(P, slot, hh, aa);
+    }
+    atomicOr(&occ[(uint32_t)(p - x) >> 5], 1u << ((uint32_t)(p - x) & 31u));
+    sum_d += (unsigned long long)(p - want[k]);  // getDisplacement (IndexHash.java:671-678)
+    max_d = max(max_d, (long long)(p - want[k]));
+    pend = max(pend, (int32_t)(p + 1));
+    // the pair (slot - 1, slot) inside the block's range: equal hashes lie in one group, ranked
+    // next to each other (calculateMaxDisplacement, IndexHash.java:195-245)
+    if (same_prev[k] && wrap_slot(start + (uint64_t)p, P.cap) != 0 && start + (uint64_t)p < lim) col++;
+  }
+  pend = wave_max_i32(pend);
+  if (lane == 0 && pend > 0) atomicMax(&s_pend, pend);
+  __syncthreads();
+  const int64_t hi = max(bsize, (int64_t)s_pend);
+  // zeros where no entry landed (only inside the bucket: the run spilled past it has no gap)
+  for (int64_t t = x + tid; t < hi; t += kPlaceRegBlock) {
+    const uint32_t d = (uint32_t)(t - x);
+    if ((occ[d >> 5] >> (d & 31u)) & 1u) continue;
+    const uint64_t slot = start + (uint64_t)t;
+    if (nt16) {
+      typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+      const u32x4 z = {0u, 0u, 0u, 0u};
+      __builtin_nontemporal_store(z, reinterpret_cast<u32x4*>(P.out + kIndexHeaderSize + slot * 16ull));
+    } else {
+      write_slot(P, slot, 0, 0);
+    }
+  }
+  if (!P.fold_stats) return;
+  // an entry of hash 0 before an empty slot of the range (an empty slot reads as hash 0)
+#pragma unroll
+  for (int k = 0; k < kPlaceRegPer; k++) {
+    const int64_t p = pos[k];
+    if (p < 0 || mine[k].hash != 0 || p + 1 >= hi) continue;
+    const uint32_t d = (uint32_t)(p + 1 - x);
+    if (!((occ[d >> 5] >> (d & 31u)) & 1u) && wrap_slot(start + (uint64_t)p + 1, P.cap) != 0 &&
+        start + (uint64_t)p + 1 < lim)
+      col++;
+  }
+  if (x < (1ll << 20)) {  // (block-uniform) every displacement < 2^21: 32-bit DPP reductions
+    sum_d = wave_sum_u32((uint32_t)sum_d);
+    max_d = wave_max_i32((int32_t)max_d);
+  } else {
+    sum_d = wave_sum_u64(sum_d);
+    max_d = wave_max_i64(max_d);
+  }
+  col = wave_sum_u32((uint32_t)col);
+  if (lane == 0) {
+    r_sum[wv] = sum_d;
+    r_col[wv] = col;
+    r_max[wv] = max_d;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    StatPart sp{0, 0, 0};
+    for (int w = 0; w < NW; w++) {
+      sp.sum_disp += r_sum[w];
+      sp.collisions += r_col[w];
+      sp.max_disp = max(sp.max_disp, r_max[w]);
+    }
+    P.parts[b] = sp;
+    P.bstat_start[b] = hi > x ? wrap_slot(start + (uint64_t)x, P.cap) : ~0ull;
+  }
+}
+
+// ================================================================================================
 // launchers
 // ================================================================================================
 void launch_frame_fused(const BuildParams& P, hipStream_t s, StageTimer* tm) {
@@ -1751,7 +2053,14 @@ void launch_partition(const BuildParams& P, hipStream_t s, StageTimer* tm) {
 }
 
 void launch_place_buckets(const BuildParams& P, hipStream_t s) {
-  if (P.b_hi > P.b_lo) hipLaunchKernelGGL(k_place_lds, dim3((unsigned)(P.b_hi - P.b_lo)), dim3(kPlaceLdsBlock), 0, s, P);
+  // k_place_reg (SPARKEY_PLACE_LDS=1: k_place_lds, the round-2 kernel, for measurements)
+  static const bool lds_kernel = getenv("SPARKEY_PLACE_REG") == nullptr;
+  if (P.b_hi > P.b_lo) {
+    if (lds_kernel || P.place_dbg)
+      hipLaunchKernelGGL(k_place_lds, dim3((unsigned)(P.b_hi - P.b_lo)), dim3(kPlaceLdsBlock), 0, s, P);
+    else
+      hipLaunchKernelGGL(k_place_reg, dim3((unsigned)(P.b_hi - P.b_lo)), dim3(kPlaceRegBlock), 0, s, P);
+  }
   // buckets above kPlaceLdsMax entries (normally none; never with fixed bucket regions, whose
   // overflow redoes the build with dense runs)
   if (!P.p2_fixed) launch_place_global(P, s, 0, 1);

@@ -523,6 +523,7 @@ static int setup_params(const LogHdr& lh, const IndexParams& ip, const sparkey_b
   }
   P.emit_extra = lh.max_key_len + 32 <= kEmitExtra ? (int32_t)((lh.max_key_len + 32 + 15) & ~15LL) : 32;
   P.uni_nt = getenv("SPARKEY_FRAME_NO_NT") ? 0u : 1u;  // framing stages the log non-temporally (read once)
+  P.place_nt = getenv("SPARKEY_PLACE_NT") ? 1 : 0;
   P.hash_size = ip.hash_size;
   P.addr_size = ip.addr_size;
   P.slot_size = ip.slot_size;
@@ -626,10 +627,12 @@ static void set_geom(BuildParams& P, const FrameGeom& g) {
 // SPARKEY_FRAME2_SEG / SPARKEY_FRAME2_S override (measurements).
 // k_frame_lane's regions: R = max(8 KiB, the power of two >= maxRecLen) bytes per lane
 // (SPARKEY_LANE_REGION overrides), numbered from entry >> log2 R; none when the log's records do not
-// suit it (frame_lane_supported) or SPARKEY_NO_LANE is set.
+// suit it (frame_lane_supported), unless SPARKEY_FRAME_LANE is set: on the C3 shape the ring walk
+// measured 1.16 ms per 10M records against k_frame3's 0.90, so k_frame3 frames
+// these logs by default.
 static FrameGeom lane_geometry(const BuildParams& P, int64_t entry, int64_t frame_end) {
   FrameGeom g{0, 1, 0, 0};
-  if (getenv("SPARKEY_NO_LANE") || frame_end <= entry) return g;
+  if (!getenv("SPARKEY_FRAME_LANE") || getenv("SPARKEY_NO_LANE") || frame_end <= entry) return g;
   int64_t want = 8192;
   if (const char* v = getenv("SPARKEY_LANE_REGION")) want = std::max<int64_t>(256, atoll(v));
   int cs = 8;
@@ -740,6 +743,22 @@ static void print_frame_debug(sparkey_plan* pl, const BuildParams& P) {
           "%.2f\n",
           (unsigned long long)nwv, 1 << P.fr_cshift, P.fr_w, sum[0] / n, sum[1] / n, sum[2] / n, sum[3] / n,
           sum[4] / n, sum[5] / n, sum[6] / n, mx[3], sum[8] / n, sum[9] / n, sum[10] / n);
+}
+
+static void print_part2_debug(const BuildParams& P) {
+  if (!P.part_dbg) return;
+  std::vector<unsigned long long> h(8 * 256);
+  if (hipMemcpy(h.data(), P.part_dbg, h.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return;
+  double sum[8] = {0};
+  unsigned long long mx[8] = {0};
+  for (int d = 0; d < 256; d++)
+    for (int i = 0; i < 8; i++) {
+      sum[i] += (double)h[8 * d + i];
+      mx[i] = std::max(mx[i], h[8 * d + i]);
+    }
+  fprintf(stderr, "[k_part2s] digits=256 mean cycles: clear %.0f count+scatter %.0f barrier %.0f functions %.0f "
+          "carry %.0f | max: clear %llu count+scatter %llu barrier %llu functions %llu carry %llu\n",
+          sum[0] / 256, sum[1] / 256, sum[2] / 256, sum[3] / 256, sum[4] / 256, mx[0], mx[1], mx[2], mx[3], mx[4]);
 }
 
 static void print_place_debug(const BuildParams& P) {
@@ -1303,6 +1322,11 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
       HIP_TRY(hipMemsetAsync(pl->pdbg, 0, 8 * P.nbuckets * sizeof(unsigned long long), s));
       P.place_dbg = pl->pdbg;
     }
+    if (getenv("SPARKEY_PART2_DEBUG")) {
+      HIP_TRY(grow(&pl->dbg, pl->c_dbg, 8 * 256));
+      HIP_TRY(hipMemsetAsync(pl->dbg, 0, 8 * 256 * sizeof(unsigned long long), s));
+      P.part_dbg = pl->dbg;
+    }
 
     Status init;
     memset(&init, 0, sizeof(init));
@@ -1366,6 +1390,7 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
     HIP_TRY(hipEventElapsedTime(&ms, pl->ev0, pl->ev1));
     print_frame_debug(pl, P);
     print_place_debug(P);
+    print_part2_debug(P);
     if (slab_framing(framing_path) && st.max_wave_count > slab_cap) {  // a wave overflowed its slab
       slab_cap = (uint32_t)std::min<uint64_t>(kPartTile, ((uint64_t)st.max_wave_count + 63) & ~63ull);
       continue;

@@ -584,6 +584,7 @@ def test_frame3_wait_timeout(native, monkeypatch):
 @pytest.mark.parametrize("region", [None, "256", "512", "4096", "65536"])
 def test_lane_geometry(native, monkeypatch, region):
     """Region sizes from a few records to many: the oracle's bytes, on k_frame_lane."""
+    monkeypatch.setenv("SPARKEY_FRAME_LANE", "1")  # (opt-in: k_frame3 frames these logs by default)
     if region:
         monkeypatch.setenv("SPARKEY_LANE_REGION", region)
     for seed, (kmin, kmax, vmin, vmax), hs in [(81, (8, 64, 100, 100), 8), (83, (1, 40, 20, 60), 4),
@@ -596,6 +597,7 @@ def test_lane_geometry(native, monkeypatch, region):
 def test_lane_matches_frame3(native, monkeypatch):
     puts = random_puts(60000, seed=91, kmin=8, kmax=64, vmin=100, vmax=100)
     log = make_log(puts)
+    monkeypatch.setenv("SPARKEY_FRAME_LANE", "1")
     a, sa = check(native, log, 91, hash_size=8)
     monkeypatch.setenv("SPARKEY_NO_LANE", "1")
     b, sb = gpu_build(native, log, 91, 8)
@@ -607,6 +609,7 @@ def test_lane_false_entries_fixed(native, monkeypatch, region):
     """Values whose bytes all look like record headers (small bytes), tiny records and DELETE records:
     many screened entries are false starts that survive the trial walk; the fix passes re-walk those
     regions from the previous region's exit and the bytes stay the oracle's."""
+    monkeypatch.setenv("SPARKEY_FRAME_LANE", "1")
     monkeypatch.setenv("SPARKEY_LANE_REGION", region)
     rng = np.random.default_rng(int(region))
     puts = [(b"k%d" % i, rng.integers(1, 9, int(rng.integers(0, 40)), dtype=np.uint8).tobytes()) for i in range(30000)]
@@ -617,10 +620,11 @@ def test_lane_false_entries_fixed(native, monkeypatch, region):
     assert stats.framing_path in SPEC and stats.placement_path == 2, stats.as_dict()
 
 
-def test_lane_errors_reported_like_serial(native):
+def test_lane_errors_reported_like_serial(native, monkeypatch):
     """A corrupt record in the middle of a log: the lane framing leaves its region unresolved, the
     serial walk reports the reference's error at the record's offset."""
     import struct
+    monkeypatch.setenv("SPARKEY_FRAME_LANE", "1")
     log = bytearray(make_log(random_puts(20000, seed=95, kmin=8, kmax=40, vmin=10, vmax=90)))
     # corrupt the header of a record near the middle: key length above maxKeyLen
     p, mid = 84, len(log) // 2

@@ -1,7 +1,10 @@
 """A record-for-record model of k_frame_lane (sparkey-java_amd/csrc/frame_lane_kernels.hip), checked
-against the log's true record chain (SparkeyLogIterator.java:86-138) on the CPU: the entry screen and
-trial walk, the per-region walks, and the fix passes (flags snapshot, one thread per run of disagreeing
-regions, patching a false entry where both walks meet).  The GPU parity tests check the kernel itself
+against the log's true record chain (SparkeyLogIterator.java:86-138) on the CPU: the ring entry (the
+first surviving candidate of the region's first maxRecLen bytes, and the last point where the later
+candidates join its chain, all inside the ring's first 512 bytes), the per-lane walks on to the next
+lane's entry, and the fix passes (flags snapshot, one thread per run of disagreeing regions: the run
+between the previous exit and a region's first record appended to the previous slab, or a patched
+prefix where a false entry's walk meets the true one).  The GPU parity tests check the kernel itself
 against the oracle; this model checks the algorithm on many more logs and region sizes than a GPU run
 would, and that the kernel's four fix passes settle them."""
 import struct
@@ -11,8 +14,10 @@ import pytest
 
 from helpers import make_log, random_puts
 
-TRIAL = 4        # kLaneTrial
 PATCH_MAX = 16   # kPatchMax
+RING_WIN = 512   # kRingWin
+LANE_TAIL = 768  # kLaneTail
+CONV_MAX = 12    # kConvMax
 
 
 def true_chain(log):
@@ -51,22 +56,38 @@ class LaneModel:
             return 0 if (self.nodel or b1 > self.mk) else 2 + b1
         return 0 if (b0 - 1 > self.mk or b1 > self.mv) else 1 + b0 + b1
 
-    def survives(self, q):
-        for _ in range(TRIAL):
-            if q >= self.de:
-                break
-            n = self.plausible_len(q)
-            if not n:
-                return False
-            q += n
-        return True
-
-    def find_entry(self, s):
-        for c in range(s, min(s + self.mrl, self.de)):
-            n = self.plausible_len(c)
-            if n and self.survives(c + n):
-                return c
-        return -1
+    def ring_entry(self, s, e):  # ring_entry: positions relative to the 16-aligned stream base b
+        b = s & ~15
+        hlim = b + RING_WIN - 16
+        cend = min(s + min(self.mrl, e - s), self.de)
+        A, mj, ca = -1, -1, []
+        for c in range(s, cend):
+            if not self.plausible_len(c):
+                continue
+            if A < 0:
+                p, chain, alive = c, [], True
+                while p < self.de and p < hlim and len(chain) < CONV_MAX:
+                    n = self.plausible_len(p)
+                    if not n:
+                        alive = False
+                        break
+                    chain.append(p)
+                    p += n
+                if alive:
+                    A, ca = c, chain
+            else:
+                p = c
+                while True:
+                    if p in ca:
+                        mj = max(mj, p)
+                        break
+                    if p >= self.de or p >= hlim or (len(ca) == CONV_MAX and p > ca[-1]):
+                        break  # undecided: A, speculatively
+                    n = self.plausible_len(p)
+                    if not n:
+                        break
+                    p += n
+        return -1 if A < 0 else max(A, mj)
 
     def walk(self, p, rend, emit):  # walk_records (one-byte VLQ logs; header_valid)
         while p < rend:
@@ -110,21 +131,54 @@ class LaneModel:
         ex = self.walk(x, self.rend(r), emit)
         if st["full"] or ex < 0:
             return self.walk_region(r, x)
+        if st["merged"] and st["i"] == 0 and r > 0:  # the run before the first record: the previous slab's end
+            self.slab[r - 1] = self.slab[r - 1] + st["nb"]
+            self.exitp[r - 1] = self.qpos[r]
+            return
         if st["merged"]:
             self.slab[r] = st["nb"] + old[st["i"]:]
         else:
             self.slab[r], self.exitp[r] = st["nb"], ex
         self.qpos[r] = x
 
+    def lane_walk(self, r, m, tgt):  # the ring walk: records from m below the region end, then on to tgt
+        s = 84 if r == 0 else (self.k0 + r) * self.R
+        e, b = self.rend(r), s & ~15
+        slim = min(e + LANE_TAIL, len(self.log))
+        recs, p, ex = [], m, -1
+        while True:
+            if p >= e and p >= tgt:
+                ex = p
+                break
+            if (p & ~7) + 16 > slim:
+                ex = p if p >= e else -1
+                break
+            b0, b1 = self.log[p], self.log[p + 1]
+            put = b0 != 0
+            klen, vlen = (b0 - 1, b1) if put else (b1, 0)
+            if (b0 | b1) & 0x80 or klen > self.mk or vlen > self.mv or (not put and self.nodel) or \
+                    p + 2 + klen > len(self.log):
+                ex = -1
+                break
+            if p + 2 + klen + 16 > slim and slim < len(self.log):
+                ex = p if p >= e else -1
+                break
+            recs.append(p)
+            p += 2 + klen + vlen
+        self.qpos[r], self.exitp[r], self.slab[r] = m, ex, recs
+
     def run(self, passes=4):
         self.qpos, self.exitp, self.slab = [0] * self.nreg, [0] * self.nreg, [[] for _ in range(self.nreg)]
+        ms = []
         for r in range(self.nreg):
             s = 84 if r == 0 else (self.k0 + r) * self.R
-            e = s if r == 0 else self.find_entry(s)
-            if e < 0:
+            ms.append(s if r == 0 else self.ring_entry(s, self.rend(r)))
+        for r in range(self.nreg):  # lane r % 64 of wave r // 64
+            if ms[r] < 0:
                 self.qpos[r], self.exitp[r], self.slab[r] = -2, -1, []
-            else:
-                self.walk_region(r, e)
+                continue
+            nxt = ms[r + 1] if r % 64 != 63 and r + 1 < self.nreg else -1
+            self.lane_walk(r, ms[r], nxt if nxt >= 0 else -1)
         bad0 = sum(not f for f in self.flags())
         for _ in range(passes):
             conv = self.flags()  # k_frame_lane_flags: a snapshot
