@@ -485,6 +485,31 @@ void launch_verify(const BuildParams& P, hipStream_t s, StageTimer* tm) {
   tm->mark("verify", s);
 }
 
+// The build's first launch: the .spi header (from the host's template), the status block reset
+// (err = none) and n words of the digit regions' fill cursors cleared -- one kernel in place of two
+// host-to-device copies and a memset per build.
+struct BuildInit {
+  uint8_t hdr[kIndexHeaderBytes];
+};
+__global__ __launch_bounds__(256) void k_build_init(uint8_t* out, BuildInit h, Status* st, uint32_t* fill, uint32_t n) {
+  const int t = threadIdx.x;
+  if (t < kIndexHeaderBytes / 4) {
+    const uint32_t w = (uint32_t)h.hdr[4 * t] | ((uint32_t)h.hdr[4 * t + 1] << 8) | ((uint32_t)h.hdr[4 * t + 2] << 16) |
+                       ((uint32_t)h.hdr[4 * t + 3] << 24);
+    reinterpret_cast<uint32_t*>(out)[t] = w;
+  }
+  constexpr int kWords = (int)(sizeof(Status) / 4);
+  uint32_t* sw = reinterpret_cast<uint32_t*>(st);
+  for (int i = t; i < kWords; i += 256) sw[i] = i < 2 ? ~0u : 0u;  // err (the first 8 bytes) = ~0
+  for (uint32_t i = t; i < n; i += 256) fill[i] = 0;
+}
+
+void launch_build_init(uint8_t* out, const uint8_t* hdr, Status* st, uint32_t* fill, uint32_t n, hipStream_t s) {
+  BuildInit h;
+  for (int i = 0; i < kIndexHeaderBytes; i++) h.hdr[i] = hdr[i];
+  hipLaunchKernelGGL(k_build_init, dim3(1), dim3(256), 0, s, out, h, st, fill, n);
+}
+
 void launch_stats_folded(const BuildParams& P, hipStream_t s, StageTimer* tm) {
   hipLaunchKernelGGL(k_stats_folded, dim3(grid_for(std::max<uint64_t>(P.nbuckets, 1), kStatFoldBlock)),
                      dim3(kStatFoldBlock), 0, s, P);

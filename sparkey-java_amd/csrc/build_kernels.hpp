@@ -198,7 +198,6 @@ struct BuildParams {
   int32_t fr_rgn_bytes;  // LDS region per wave: W * C + fr_look + 16, rounded up to 1 KiB
   int32_t fr_mask_words;  // 64-position screen words per chunk: ceil(min(C, maxRecLen) / 64)
   uint32_t fr_wpc_magic;  // q / (8 * fr_mask_words) == (q * magic) >> 22 for every screened word q
-  int32_t place_nt;  // k_place_reg: non-temporal slot stores (SPARKEY_PLACE_NT, measurements)
   int32_t fr_fast;  // maxKeyLen + 1 < 128 and maxValueLen < 128: canonical headers are 2 bytes
   int32_t no_deletes;  // the log header counts no DELETE: speculation treats 0x00 as no record start
   uint64_t fr_nchunks;
@@ -316,6 +315,7 @@ void launch_place_global(const BuildParams& P, hipStream_t s, int sort_only, int
 void launch_verify(const BuildParams& P, hipStream_t s, StageTimer* tm);
 void launch_stats(const BuildParams& P, hipStream_t s, int sequential, StageTimer* tm);
 void launch_stats_folded(const BuildParams& P, hipStream_t s, StageTimer* tm);
+void launch_build_init(uint8_t* out, const uint8_t* hdr, Status* st, uint32_t* fill, uint32_t n, hipStream_t s);
 void launch_stats_folded_shard(const BuildParams& P, hipStream_t s);
 // exact replay (exact_kernels.hip)
 void launch_sequential(const BuildParams& P, hipStream_t s, int sorted_order);

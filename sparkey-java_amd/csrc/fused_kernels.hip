@@ -1250,18 +1250,28 @@ __global__ __launch_bounds__(kPart2Block) void k_part2s(BuildParams P) {
   __syncthreads();
   mark2(0);
   bool ovf = false;
+  // (software-pipelined: the next round's entries are in flight while this round's are counted and
+  // stored -- one workgroup per CU, so nothing else hides the load latency; measured 5 rounds of
+  // ~31K cycles each at C2 without it, SPARKEY_PART2_DEBUG)
+  auto load_round = [&](Entry (&v)[kPart2Items], uint64_t i0, uint64_t rz) {
+#pragma unroll
+    for (int k = 0; k < kPart2Items; k++) {
+      const uint64_t i = i0 + (uint64_t)k * kPart2Block + tid;
+      if (i < rz) {
+        if (fixed) v[k] = P.ent3[i];
+        else v[k].hash = P.ent3[i].hash;
+      }
+    }
+  };
   for (uint32_t q = 0; q < nseg; q++) {
     const uint64_t ra = seg ? seg[2 * q] : lo, rz = seg ? seg[2 * q + 1] : hi;
+    Entry nx[kPart2Items];
+    if (ra < rz) load_round(nx, ra, rz);
     for (uint64_t i0 = ra; i0 < rz; i0 += (uint64_t)kPart2Block * kPart2Items) {
       Entry v[kPart2Items];
 #pragma unroll
-      for (int k = 0; k < kPart2Items; k++) {
-        const uint64_t i = i0 + (uint64_t)k * kPart2Block + tid;
-        if (i < rz) {
-          if (fixed) v[k] = P.ent3[i];
-          else v[k].hash = P.ent3[i].hash;
-        }
-      }
+      for (int k = 0; k < kPart2Items; k++) v[k] = nx[k];
+      if (i0 + (uint64_t)kPart2Block * kPart2Items < rz) load_round(nx, i0 + (uint64_t)kPart2Block * kPart2Items, rz);
 #pragma unroll
       for (int k = 0; k < kPart2Items; k++) {
         const uint64_t i = i0 + (uint64_t)k * kPart2Block + tid;
@@ -1366,6 +1376,165 @@ __global__ __launch_bounds__(kPart2Block) void k_part2s(BuildParams P) {
       }
     }
   }
+}
+
+// k_part2st: k_part2s's fixed-region pass with its stores staged.  k_part2s stores every entry on
+// its own (one L2 request per 16 bytes: 100K of its 160K cycles per digit at C2,
+// profiles/r03/k_part2s_phases_c2.log).  Here each round of kP2Stage entries is grouped by bucket in
+// LDS and leaves as one run per bucket.  The slot counts are 8-bit (4 per word), which frees the LDS
+// for the stage; a count that would pass 255 flags p2_overflow, and the host redoes the build with
+// dense runs (k_part2s's two-pass path).  Single GPU, fixed regions only.
+constexpr int kP2StagePer = 5;
+constexpr int kP2Stage = kPart2Block * kP2StagePer;
+
+__global__ __launch_bounds__(kPart2Block) void k_part2st(BuildParams P) {
+  // h8[bpp * 256] | btot[bpp] | rcnt[bpp] | roff[bpp] | gbase[bpp] | stage[kP2Stage] | sbin[kP2Stage]
+  extern __shared__ __attribute__((aligned(16))) uint32_t dyn[];
+  if (build_aborted(P)) return;
+  const uint32_t dpart = blockIdx.x;
+  const uint64_t lo = (uint64_t)dpart * P.p1_region;
+  const uint64_t hi = lo + min((uint64_t)P.p1_fill[dpart], P.p1_region);
+  const uint32_t nbins = P.bpp;
+  const uint64_t b0 = (uint64_t)dpart * nbins;
+  __shared__ MaxPlus s_fun[kP2SortedMaxBpp];
+  uint32_t* h = dyn;
+  uint32_t* btot = dyn + nbins * 256;
+  uint32_t* rcnt = btot + nbins;
+  uint32_t* roff = rcnt + nbins;
+  uint32_t* gbase = roff + nbins;
+  Entry* stage = reinterpret_cast<Entry*>(dyn + ((nbins * 260 + 3) & ~3u));
+  uint8_t* sbin = reinterpret_cast<uint8_t*>(stage + kP2Stage);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  long long t_prev2 = P.part_dbg ? clock64() : 0;
+  auto mark2 = [&](int i) {  // (SPARKEY_PART2_DEBUG: thread 0's cycles per phase)
+    if (P.part_dbg && tid == 0) {
+      const long long now = clock64();
+      P.part_dbg[8 * (uint64_t)dpart + i] = now - t_prev2;
+      t_prev2 = now;
+    }
+  };
+  for (uint32_t i = tid; i < nbins * 260; i += kPart2Block) dyn[i] = 0;
+  if (tid < (int)kP2SortedMaxBpp) s_fun[tid] = MaxPlus{0, 0};
+  __syncthreads();
+  mark2(0);
+  bool ovf = false;
+  auto load_round = [&](Entry (&v)[kP2StagePer], uint64_t i0) {
+#pragma unroll
+    for (int k = 0; k < kP2StagePer; k++) {
+      const uint64_t i = i0 + (uint64_t)k * kPart2Block + tid;
+      if (i < hi) v[k] = P.ent3[i];
+    }
+  };
+  Entry nx[kP2StagePer];
+  if (lo < hi) load_round(nx, lo);
+  for (uint64_t i0 = lo; i0 < hi; i0 += kP2Stage) {
+    Entry v[kP2StagePer];
+#pragma unroll
+    for (int k = 0; k < kP2StagePer; k++) v[k] = nx[k];
+    if (i0 + kP2Stage < hi) load_round(nx, i0 + kP2Stage);  // (in flight through this round)
+    uint32_t bk[kP2StagePer], rk[kP2StagePer];
+#pragma unroll
+    for (int k = 0; k < kP2StagePer; k++) {
+      const uint64_t i = i0 + (uint64_t)k * kPart2Block + tid;
+      bk[k] = ~0u;
+      if (i >= hi) continue;
+      const uint64_t slot = fast_mod(v[k].hash, P.mod);
+      const uint32_t b = (uint32_t)((slot >> kBucketShift) - b0), sl = (uint32_t)(slot & (kBucket - 1));
+      const uint32_t sh = (sl & 3u) * 8u;
+      if (((atomicAdd(&h[(b << 8) + (sl >> 2)], 1u << sh) >> sh) & 0xffu) == 0xffu) ovf = true;  // (8-bit count full)
+      bk[k] = b;
+      rk[k] = atomicAdd(&rcnt[b], 1u);
+    }
+    __syncthreads();
+    if (wave == 0) {  // the round's run offsets, and each bucket's region cursor before the round
+      const uint32_t c = (uint32_t)lane < nbins ? rcnt[lane] : 0u;
+      uint32_t incl = c;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += t;
+      }
+      if ((uint32_t)lane < nbins) {
+        roff[lane] = incl - c;
+        gbase[lane] = btot[lane];
+        btot[lane] += c;
+        rcnt[lane] = 0;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kP2StagePer; k++) {
+      if (bk[k] == ~0u) continue;
+      const uint32_t at = roff[bk[k]] + rk[k];
+      stage[at] = v[k];
+      sbin[at] = (uint8_t)bk[k];
+    }
+    __syncthreads();
+    // the runs: consecutive lanes on consecutive entries of a bucket's region
+    const uint32_t nround = (uint32_t)min((uint64_t)kP2Stage, hi - i0);
+    for (uint32_t i = tid; i < nround; i += kPart2Block) {
+      const uint32_t b = sbin[i];
+      const uint32_t r = gbase[b] + (i - roff[b]);
+      if (r < kPlaceLdsMax) P.ent2[(b0 + b - P.b_lo) * (uint64_t)kPlaceLdsMax + r] = stage[i];
+      else ovf = true;
+    }
+    __syncthreads();  // (the stage and the offsets are rewritten next round)
+  }
+  if (ovf) atomicOr(&P.st->p2_overflow, 1u);
+  mark2(1);
+  mark2(2);
+  // bucket offsets (fixed regions) and counts
+  if (wave == 0 && (uint32_t)lane < nbins) {
+    const uint64_t bucket = b0 + lane;
+    if (bucket < P.nbuckets) {
+      P.boff[bucket] = (bucket - P.b_lo) * (uint64_t)kPlaceLdsMax;
+      P.bcount[bucket] = btot[lane];
+    }
+  }
+  // per bucket (one wave each): the carry function from the slot counts
+  for (uint32_t b = wave; b < nbins; b += kPart2Block / 64) {
+    const uint64_t bucket = b0 + b;
+    if (bucket >= P.nbuckets) continue;
+    const uint32_t* hw = h + (b << 8) + lane * 4;  // this lane's 16 slots: 16 * lane ...
+    uint32_t cnts[16];
+    uint32_t tot = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const uint32_t w = hw[k];
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        cnts[4 * k + q] = (w >> (8 * q)) & 0xffu;
+        tot += cnts[4 * k + q];
+      }
+    }
+    uint32_t incl = tot;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t t = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += t;
+    }
+    uint32_t run = incl - tot;
+    long long mx = -(1ll << 40);
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+      if (cnts[k]) mx = max(mx, (long long)(16 * lane + k) - (long long)run);
+      run += cnts[k];
+    }
+    mx = wave_max_i64(mx);
+    if (lane == 0) {
+      const int64_t n = (int64_t)btot[b];
+      const int64_t bsize = (int64_t)min((uint64_t)kBucket, P.cap - (bucket << kBucketShift));
+      const int64_t mlast = mx < 0 ? 0 : mx;
+      MaxPlus f;
+      f.a = n - bsize;
+      f.c = n ? max((int64_t)0, n + mlast - bsize) : 0;
+      P.bfun[bucket] = f;
+      s_fun[b] = f;
+    }
+  }
+  mark2(3);
+  part2_fused_carry(P, s_fun, nbins, b0, dpart);
+  mark2(4);
 }
 
 // ================================================================================================
@@ -1684,8 +1853,9 @@ __global__ __launch_bounds__(kPlaceLdsBlock) void k_place_lds(BuildParams P) {
 // s - base[s] over occupied s), the entries copied to base[w] + cursor so that each group of equal
 // wanted slots lies together, then every entry's rank in its group by address (IndexHash.java:647-650,
 // SortHelper's (wantedSlot, address) order) and its position j + max(carry, M[w]).  The block writes
-// its slots [x, hi): its entries from registers, zeros where its occupancy bitmap is clear.  22.5 KiB
-// of LDS (k_place_lds: 36 KiB), 4 waves: 7 blocks per CU in flight against k_place_lds's 4.
+// its slots [x, hi) in order (coalesced: scattered 16-byte stores cost one L2 request each, which
+// measured 2.4x slower), entries out of LDS through a slot -> entry map.  27 KiB of LDS (k_place_lds:
+// 36 KiB), 4 waves per block, 5 blocks per CU; the fixed regions' entry loads go out before the head.
 // ================================================================================================
 constexpr int kPlaceRegBlock = 256;
 constexpr int kPlaceRegPer = kPlaceLdsMax / kPlaceRegBlock;
@@ -1696,7 +1866,7 @@ __global__ __launch_bounds__(kPlaceRegBlock) void k_place_reg(BuildParams P) {
   __shared__ uint32_t cnt[kBucket / 2];          // 16-bit entry count per wanted slot
   __shared__ uint32_t meta[kBucket];             // base[s] | (M[s] + 32768) << 16
   __shared__ Entry buf[kPlaceLdsMax];            // each group's members together (any order inside)
-  __shared__ uint32_t occ[2 * kBucket / 32];     // slots [x, x + 2 kBucket) holding this block's entries
+  __shared__ int16_t slot_of[2 * kBucket];       // slot x + t -> its entry's buf index, -1: empty
   __shared__ uint32_t wsum[NW];
   __shared__ int32_t wmax[NW];
   __shared__ uint64_t sh64[NW + 1];
@@ -1705,6 +1875,15 @@ __global__ __launch_bounds__(kPlaceRegBlock) void k_place_reg(BuildParams P) {
   __shared__ long long r_max[NW];
   __shared__ int32_t s_pend;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  // fixed bucket regions: the region is known without the count, so the entry loads go out first,
+  // in the same round trip as the head's scalar loads (slots past the count are never used)
+  Entry mine[kPlaceRegPer];
+  const bool fixed = P.p2_fixed != 0;
+  if (fixed) {
+    const uint64_t e0 = (uint64_t)blockIdx.x * kPlaceLdsMax;
+#pragma unroll
+    for (int k = 0; k < kPlaceRegPer; k++) mine[k] = P.ent2[e0 + tid + k * kPlaceRegBlock];
+  }
   const Status* st = P.st;
   const unsigned ovf = st->overflow | st->p2_overflow, full = st->full;
   const unsigned long long nrec = st->n_records, ndel = st->n_deletes, npairs0 = st->n_pairs;
@@ -1726,15 +1905,16 @@ __global__ __launch_bounds__(kPlaceRegBlock) void k_place_reg(BuildParams P) {
     if (tid == 0) atomicOr(&P.st->big_buckets, 1u);
     return;
   }
-  Entry mine[kPlaceRegPer];
+  if (!fixed) {
 #pragma unroll
-  for (int k = 0; k < kPlaceRegPer; k++) {
-    const uint32_t i = tid + k * kPlaceRegBlock;
-    if (i < n) mine[k] = P.ent2[eoff + i];
+    for (int k = 0; k < kPlaceRegPer; k++) {
+      const uint32_t i = tid + k * kPlaceRegBlock;
+      if (i < n) mine[k] = P.ent2[eoff + i];
+    }
   }
   // (the loads are in flight while the counts are cleared)
   for (int t = tid; t < kBucket / 2; t += kPlaceRegBlock) cnt[t] = 0;
-  if (tid < 2 * kBucket / 32) occ[tid] = 0;
+  for (int t = tid; t < kBucket; t += kPlaceRegBlock) reinterpret_cast<uint32_t*>(slot_of)[t] = 0xffffffffu;
   if (tid == 0) s_pend = 0;
   __syncthreads();
   uint32_t want[kPlaceRegPer], cur[kPlaceRegPer];
@@ -1875,9 +2055,7 @@ __global__ __launch_bounds__(kPlaceRegBlock) void k_place_reg(BuildParams P) {
   }
   if (full) return;
   // positions, the entries' slots, the occupancy bitmap and the displacements
-  // (scattered slot stores go through L2, which merges each line's slots: non-temporal ones would
-  // reach memory as partial lines; P.place_nt = 1 measures that)
-  const bool nt16 = P.slot_size == 16 && !P.sharded && P.uni_nt && P.place_nt;
+  const bool nt16 = P.slot_size == 16 && !P.sharded && P.uni_nt;
   const uint64_t lim = P.sharded ? P.slot_hi : ~0ull;
   unsigned long long sum_d = 0, col = 0;
   long long max_d = 0;
@@ -1891,20 +2069,7 @@ __global__ __launch_bounds__(kPlaceRegBlock) void k_place_reg(BuildParams P) {
     const int32_t M = (int32_t)(meta[want[k]] >> 16) - 32768;
     const int64_t p = (int64_t)(bw[k] + rank[k]) + max(x, (int64_t)M);
     pos[k] = p;
-    const uint64_t slot = p < bsize ? start + (uint64_t)p : wrap_slot(start + (uint64_t)p, P.cap);
-    const uint64_t hh = mine[k].hash, aa = mine[k].addr & ~kDelBit;
-    if (nt16) {
-      typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-      u32x4 w;
-      w.x = (uint32_t)hh;
-      w.y = (uint32_t)(hh >> 32);
-      w.z = (uint32_t)aa;
-      w.w = (uint32_t)(aa >> 32);
-      __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(P.out + kIndexHeaderSize + slot * 16ull));
-    } else {
-      put_slot(P, slot, hh, aa);
-    }
-    atomicOr(&occ[(uint32_t)(p - x) >> 5], 1u << ((uint32_t)(p - x) & 31u));
+    slot_of[p - x] = (int16_t)(bw[k] + cur[k]);  // (where the entry sits in buf)
     sum_d += (unsigned long long)(p - want[k]);  // getDisplacement (IndexHash.java:671-678)
     max_d = max(max_d, (long long)(p - want[k]));
     pend = max(pend, (int32_t)(p + 1));
@@ -1916,15 +2081,27 @@ __global__ __launch_bounds__(kPlaceRegBlock) void k_place_reg(BuildParams P) {
   if (lane == 0 && pend > 0) atomicMax(&s_pend, pend);
   __syncthreads();
   const int64_t hi = max(bsize, (int64_t)s_pend);
-  // zeros where no entry landed (only inside the bucket: the run spilled past it has no gap)
+  // the block's slots [x, hi) in order, consecutive lanes on consecutive slots: its entries out of
+  // buf, zeros where none landed (the run spilled past the bucket has no gap)
   for (int64_t t = x + tid; t < hi; t += kPlaceRegBlock) {
-    const uint32_t d = (uint32_t)(t - x);
-    if ((occ[d >> 5] >> (d & 31u)) & 1u) continue;
-    const uint64_t slot = start + (uint64_t)t;
-    if (nt16) {
+    const int32_t v = slot_of[t - x];
+    const uint64_t slot = t < bsize ? start + (uint64_t)t : wrap_slot(start + (uint64_t)t, P.cap);
+    uint64_t hh = 0, aa = 0;
+    if (v >= 0) {
+      const Entry en = buf[v];
+      hh = en.hash;
+      aa = en.addr & ~kDelBit;
+    }
+    if (nt16) {  // the table is written once: non-temporal stores
       typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-      const u32x4 z = {0u, 0u, 0u, 0u};
-      __builtin_nontemporal_store(z, reinterpret_cast<u32x4*>(P.out + kIndexHeaderSize + slot * 16ull));
+      u32x4 w;
+      w.x = (uint32_t)hh;
+      w.y = (uint32_t)(hh >> 32);
+      w.z = (uint32_t)aa;
+      w.w = (uint32_t)(aa >> 32);
+      __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(P.out + kIndexHeaderSize + slot * 16ull));
+    } else if (v >= 0) {
+      put_slot(P, slot, hh, aa);
     } else {
       write_slot(P, slot, 0, 0);
     }
@@ -1935,8 +2112,7 @@ __global__ __launch_bounds__(kPlaceRegBlock) void k_place_reg(BuildParams P) {
   for (int k = 0; k < kPlaceRegPer; k++) {
     const int64_t p = pos[k];
     if (p < 0 || mine[k].hash != 0 || p + 1 >= hi) continue;
-    const uint32_t d = (uint32_t)(p + 1 - x);
-    if (!((occ[d >> 5] >> (d & 31u)) & 1u) && wrap_slot(start + (uint64_t)p + 1, P.cap) != 0 &&
+    if (slot_of[p + 1 - x] < 0 && wrap_slot(start + (uint64_t)p + 1, P.cap) != 0 &&
         start + (uint64_t)p + 1 < lim)
       col++;
   }
@@ -2042,10 +2218,19 @@ void launch_partition2(const BuildParams& P, hipStream_t s, StageTimer* tm) {
   tm->mark("partition", s);
 }
 
+// k_part2st's dynamic LDS (the 8-bit counts, the bucket words, the stage and its bucket bytes)
+static size_t part2st_lds(uint32_t bpp) {
+  return (size_t)((bpp * 260 + 3) & ~3u) * 4 + (size_t)kP2Stage * (sizeof(Entry) + 1);
+}
+
 void launch_partition(const BuildParams& P, hipStream_t s, StageTimer* tm) {
   if (!P.p1_region) launch_partition1(P, s);
   else if (P.p1_kernel) hipLaunchKernelGGL(k_part1_regions, dim3((unsigned)P.p1_tiles), dim3(kPartBlock), 0, s, P);
-  if (P.p2_sorted)
+  static const bool no_staged = getenv("SPARKEY_NO_P2_STAGED") != nullptr;  // (k_part2s: measurements)
+  if (P.p2_sorted && P.p2_fixed && P.fused_carry && P.p1_region && !P.p2_seg && !no_staged &&
+      part2st_lds(P.bpp) <= 150 * 1024)
+    hipLaunchKernelGGL(k_part2st, dim3(256), dim3(kPart2Block), part2st_lds(P.bpp), s, P);
+  else if (P.p2_sorted)
     hipLaunchKernelGGL(k_part2s, dim3(256), dim3(kPart2Block), (size_t)(514u * P.bpp) * sizeof(uint32_t), s, P);
   else
     hipLaunchKernelGGL(k_part2, dim3(256), dim3(kPart2Block), (size_t)(2u * P.bpp) * sizeof(uint32_t), s, P);
@@ -2053,8 +2238,8 @@ void launch_partition(const BuildParams& P, hipStream_t s, StageTimer* tm) {
 }
 
 void launch_place_buckets(const BuildParams& P, hipStream_t s) {
-  // k_place_reg (SPARKEY_PLACE_LDS=1: k_place_lds, the round-2 kernel, for measurements)
-  static const bool lds_kernel = getenv("SPARKEY_PLACE_REG") == nullptr;
+  // k_place_reg (SPARKEY_PLACE_LDS=1: k_place_lds, the round-2 kernel: 0.170 against 0.154 ms on C2)
+  static const bool lds_kernel = getenv("SPARKEY_PLACE_LDS") != nullptr;
   if (P.b_hi > P.b_lo) {
     if (lds_kernel || P.place_dbg)
       hipLaunchKernelGGL(k_place_lds, dim3((unsigned)(P.b_hi - P.b_lo)), dim3(kPlaceLdsBlock), 0, s, P);

@@ -523,7 +523,6 @@ static int setup_params(const LogHdr& lh, const IndexParams& ip, const sparkey_b
   }
   P.emit_extra = lh.max_key_len + 32 <= kEmitExtra ? (int32_t)((lh.max_key_len + 32 + 15) & ~15LL) : 32;
   P.uni_nt = getenv("SPARKEY_FRAME_NO_NT") ? 0u : 1u;  // framing stages the log non-temporally (read once)
-  P.place_nt = getenv("SPARKEY_PLACE_NT") ? 1 : 0;
   P.hash_size = ip.hash_size;
   P.addr_size = ip.addr_size;
   P.slot_size = ip.slot_size;
@@ -1328,13 +1327,8 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
       P.part_dbg = pl->dbg;
     }
 
-    Status init;
-    memset(&init, 0, sizeof(init));
-    init.err = ~0ull;
     HIP_TRY(hipEventRecord(pl->ev0, s));
     pl->timer.begin(s);
-    HIP_TRY(hipMemcpyAsync(d_out, hdr, kIndexHeaderSize, hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(pl->d_status, &init, sizeof(Status), hipMemcpyHostToDevice, s));
     // k_frame_uniform's workgroups are the partition tiles: it does partition pass 1 itself into
     // digit regions of ent3 sized for the binomial spread of the digit counts (a region that fills
     // up redoes the build with the separate pass), or leaves k_part1_hist's histogram
@@ -1351,7 +1345,6 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
       HIP_TRY(grow(&pl->ent2, pl->c_ent2, 256 * rc_cap));
       HIP_TRY(grow(&pl->ent3, pl->c_ent3, 256 * rc_cap));
       HIP_TRY(grow(&pl->p1_fill, pl->c_p1_fill, 256));
-      HIP_TRY(hipMemsetAsync(pl->p1_fill, 0, 256 * sizeof(uint32_t), s));
       P.ent2 = pl->ent2;
       P.ent3 = pl->ent3;
       P.max_records = std::min(pl->c_ent2, pl->c_ent3);
@@ -1359,6 +1352,8 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
       P.p1_region = rc_cap;
       P.p1_kernel = tiles ? 0 : 1;
     }
+    // the header, the status reset and the region cursors in one launch
+    launch_build_init(d_out, hdr, pl->d_status, P.p1_region ? pl->p1_fill : nullptr, P.p1_region ? 256u : 0u, s);
     P.p1_hist_ready = tiles && !P.p1_region ? 1 : 0;
     regions_used = P.p1_region != 0 && !P.p1_kernel;  // (partition passes: 1 when the framing did pass 1)
     // k_part2s: pass 2 also sorts each bucket by wanted slot and leaves the carry functions

@@ -89,6 +89,17 @@ def test_overwrite_single_key(native):
     check(native, log, 5)
 
 
+@pytest.mark.parametrize("hash_size", [4, 8])
+def test_many_equal_wanted_slots(native, hash_size):
+    """More than 255 entries wanting one slot (one key put 600 times among 20000 others): k_part2st's
+    8-bit slot count would overflow, so the build redoes its partition with dense runs; the exact path
+    then replays the overwrites.  The oracle's bytes either way."""
+    puts = [(b"k%d" % i, b"v%d" % i) for i in range(20000)]
+    puts[5000:5000] = [(b"hot", b"x%d" % i) for i in range(600)]
+    got, stats = check(native, make_log(puts), 31, hash_size=hash_size, expect_path=2)
+    assert index_header(got)["garbageSize"] > 0
+
+
 # --- LargeFilesTest: values larger than a framing chunk (LargeFilesTest.java:28-50) ---
 def test_large_values(native):
     value = b"value"
