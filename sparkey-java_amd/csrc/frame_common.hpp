@@ -258,4 +258,123 @@ __device__ __forceinline__ uint32_t screen8(uint64_t x, uint64_t y, const Screen
   return (uint32_t)((((r >> 7) & ONES) * 0x0102040810204080ull) >> 56);  // bit 8i -> bit i
 }
 
+// ------------------------------------------------------------------------------------------------
+// Records held in registers: an array of N aligned 16-byte chunks, a lane-variable byte offset
+// resolved by value selects (never by indexing registers), MurmurHash3 over it.
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t lo64(const uint4& c) { return (uint64_t)c.x | ((uint64_t)c.y << 32); }
+__device__ __forceinline__ uint64_t hi64(const uint4& c) { return (uint64_t)c.z | ((uint64_t)c.w << 32); }
+
+// 8 bytes at byte offset o (0..15) of the 32 bytes c0 ++ c1
+__device__ __forceinline__ uint64_t bytes8(const uint4& c0, const uint4& c1, int o) {
+  const uint64_t w0 = (o & 8) ? hi64(c0) : lo64(c0);
+  const uint64_t w1 = (o & 8) ? lo64(c1) : hi64(c0);
+  const int sh = (o & 7) * 8;
+  return sh ? (w0 >> sh) | (w1 << (64 - sh)) : w0;
+}
+
+// half h (8 bytes) of the chunk array: chunk h / 2, low or high half (h a compile-time index once
+// unrolled; clamped to the array, since the selects below also form indices the lane never uses)
+template <int N>
+__device__ __forceinline__ uint64_t half_of(const uint4 (&c)[N], int h) {
+  h = h < 2 * N ? h : 2 * N - 1;
+  return (h & 1) ? hi64(c[h >> 1]) : lo64(c[h >> 1]);
+}
+
+// The key's 8-byte word j (key bytes 8j .. 8j + 7), the key starting at byte ko (0..31) of the chunk
+// array: aligned halves (ko >> 3) + j and + j + 1, funnel-shifted.  ko >> 3 is lane-variable (0..3):
+// a select among four static halves.
+template <int N>
+__device__ __forceinline__ uint64_t key_word(const uint4 (&c)[N], int ko, int j) {
+  const int q = ko >> 3;
+  // (every half index below is static once j is; q picks among them by value selects, so the array
+  // stays in registers)
+  const uint64_t h0 = half_of(c, j), h1 = half_of(c, j + 1), h2 = half_of(c, j + 2), h3 = half_of(c, j + 3),
+                 h4 = half_of(c, j + 4);
+  const bool q1 = q & 1, q2 = q & 2;
+  const uint64_t a = q2 ? (q1 ? h3 : h2) : (q1 ? h1 : h0);
+  const uint64_t b = q2 ? (q1 ? h4 : h3) : (q1 ? h2 : h1);
+  const int sh = (ko & 7) * 8;
+  return sh ? (a >> sh) | (b << (64 - sh)) : a;
+}
+
+// MurmurHash3 x64_128 -> h1 (MurmurHash3.java:100-201) of a key whose bytes are in the chunk array
+// from byte ko on (ko + len + 8 <= 16 N); the loops run to the static bound with the lane's own length
+// as the guard, so every chunk index is static.
+template <int N>
+__device__ __forceinline__ uint64_t lane_murmur64(const uint4 (&c)[N], int ko, int32_t len, uint32_t seed) {
+  constexpr int kMaxBlocks = N - 1;  // (len < 16 N - 8 - ko)
+  const uint64_t c1 = 0x87c37b91114253d5ull, c2 = 0x4cf5ad432745937full;
+  uint64_t h1 = (uint64_t)seed, h2 = h1;
+  const int32_t nblocks = len >> 4;
+#pragma unroll
+  for (int i = 0; i < kMaxBlocks; i++) {
+    if (i < nblocks) {
+      uint64_t k1 = key_word(c, ko, 2 * i);
+      uint64_t k2 = key_word(c, ko, 2 * i + 1);
+      k1 *= c1; k1 = rotl64(k1, 31); k1 *= c2; h1 ^= k1;
+      h1 = rotl64(h1, 27); h1 += h2; h1 = h1 * 5 + 0x52dce729ull;
+      k2 *= c2; k2 = rotl64(k2, 33); k2 *= c1; h2 ^= k2;
+      h2 = rotl64(h2, 31); h2 += h1; h2 = h2 * 5 + 0x38495ab5ull;
+    }
+  }
+  const int32_t rem = len & 15;
+  uint64_t t1 = 0, t2 = 0;  // the tail's two words: word 2 * nblocks and the next (lane-variable block)
+#pragma unroll
+  for (int i = 0; i <= kMaxBlocks; i++) {
+    if (i == nblocks) {
+      t1 = key_word(c, ko, 2 * i);
+      t2 = key_word(c, ko, 2 * i + 1);
+    }
+  }
+  if (rem > 8) {
+    uint64_t k2 = t2 & ((1ull << (8 * (rem - 8))) - 1ull);
+    k2 *= c2; k2 = rotl64(k2, 33); k2 *= c1; h2 ^= k2;
+  }
+  if (rem > 0) {
+    uint64_t k1 = t1;
+    if (rem < 8) k1 &= (1ull << (8 * rem)) - 1ull;
+    k1 *= c1; k1 = rotl64(k1, 31); k1 *= c2; h1 ^= k1;
+  }
+  h1 ^= (uint64_t)(int64_t)len;
+  h2 ^= (uint64_t)(int64_t)len;
+  h1 += h2; h2 += h1;
+  h1 = fmix64(h1); h2 = fmix64(h2);
+  h1 += h2;
+  return h1;
+}
+
+// MurmurHash3 x86_32 (MurmurHash3.java:18-75), same conventions.
+template <int N>
+__device__ __forceinline__ uint32_t lane_murmur32(const uint4 (&c)[N], int ko, int32_t len, uint32_t seed) {
+  constexpr int kMaxWords = 2 * N - 1;  // 8-byte words the key (and its tail word) can span
+  const uint32_t c1 = 0xcc9e2d51u, c2 = 0x1b873593u;
+  uint32_t h1 = seed;
+  const int32_t nblocks = len >> 2;
+  auto block = [&](uint32_t k1) {
+    k1 *= c1; k1 = rotl32(k1, 15); k1 *= c2;
+    h1 ^= k1; h1 = rotl32(h1, 13); h1 = h1 * 5 + 0xe6546b64u;
+  };
+  uint32_t tail = 0;
+#pragma unroll
+  for (int j = 0; j < kMaxWords; j++) {
+    if (2 * j < nblocks || 2 * j == nblocks) {
+      const uint64_t w = key_word(c, ko, j);
+      if (2 * j < nblocks) block((uint32_t)w);
+      if (2 * j + 1 < nblocks) block((uint32_t)(w >> 32));
+      if (2 * j == nblocks) tail = (uint32_t)w;
+      if (2 * j + 1 == nblocks) tail = (uint32_t)(w >> 32);
+    }
+  }
+  const int32_t rem = len & 3;
+  if (rem) {
+    uint32_t k1 = tail & ((1u << (8 * rem)) - 1u);
+    k1 *= c1; k1 = rotl32(k1, 15); k1 *= c2; h1 ^= k1;
+  }
+  h1 ^= (uint32_t)len;
+  h1 ^= h1 >> 16; h1 *= 0x85ebca6bu; h1 ^= h1 >> 13; h1 *= 0xc2b2ae35u; h1 ^= h1 >> 16;
+  return h1;
+}
+
+
 }  // namespace sk

@@ -1860,7 +1860,8 @@ __global__ __launch_bounds__(kPlaceLdsBlock) void k_place_lds(BuildParams P) {
 constexpr int kPlaceRegBlock = 256;
 constexpr int kPlaceRegPer = kPlaceLdsMax / kPlaceRegBlock;
 
-__global__ __launch_bounds__(kPlaceRegBlock) void k_place_reg(BuildParams P) {
+// One bucket of k_place_reg: bucket b_lo + bi; pre[] holds its fixed-region entries when `fixed`.
+__device__ __forceinline__ void place_reg_bucket(const BuildParams& P, uint64_t bi, const Entry (&pre)[kPlaceRegPer]) {
   constexpr int NW = kPlaceRegBlock / 64;
   static_assert(kBucket == 4 * kPlaceRegBlock, "four wanted slots per thread in the scan");
   __shared__ uint32_t cnt[kBucket / 2];          // 16-bit entry count per wanted slot
@@ -1875,19 +1876,16 @@ __global__ __launch_bounds__(kPlaceRegBlock) void k_place_reg(BuildParams P) {
   __shared__ long long r_max[NW];
   __shared__ int32_t s_pend;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  // fixed bucket regions: the region is known without the count, so the entry loads go out first,
-  // in the same round trip as the head's scalar loads (slots past the count are never used)
   Entry mine[kPlaceRegPer];
   const bool fixed = P.p2_fixed != 0;
   if (fixed) {
-    const uint64_t e0 = (uint64_t)blockIdx.x * kPlaceLdsMax;
 #pragma unroll
-    for (int k = 0; k < kPlaceRegPer; k++) mine[k] = P.ent2[e0 + tid + k * kPlaceRegBlock];
+    for (int k = 0; k < kPlaceRegPer; k++) mine[k] = pre[k];
   }
   const Status* st = P.st;
   const unsigned ovf = st->overflow | st->p2_overflow, full = st->full;
   const unsigned long long nrec = st->n_records, ndel = st->n_deletes, npairs0 = st->n_pairs;
-  const uint64_t b = P.b_lo + blockIdx.x;
+  const uint64_t b = P.b_lo + bi;
   const uint32_t n = P.bcount[b];
   const uint64_t eoff = P.boff[b];
   int64_t x;
@@ -2140,6 +2138,19 @@ __global__ __launch_bounds__(kPlaceRegBlock) void k_place_reg(BuildParams P) {
     P.parts[b] = sp;
     P.bstat_start[b] = hi > x ? wrap_slot(start + (uint64_t)x, P.cap) : ~0ull;
   }
+}
+
+
+// k_place_reg: one block per bucket; the fixed regions' entry loads go out before the head's scalar
+// loads (slots past the count are never used), in one round trip.
+__global__ __launch_bounds__(kPlaceRegBlock) void k_place_reg(BuildParams P) {
+  Entry pre[kPlaceRegPer];
+  if (P.p2_fixed) {
+    const uint64_t e0 = (uint64_t)blockIdx.x * kPlaceLdsMax;
+#pragma unroll
+    for (int k = 0; k < kPlaceRegPer; k++) pre[k] = P.ent2[e0 + threadIdx.x + k * kPlaceRegBlock];
+  }
+  place_reg_bucket(P, blockIdx.x, pre);
 }
 
 // ================================================================================================
