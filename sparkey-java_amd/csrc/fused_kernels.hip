@@ -1196,6 +1196,137 @@ __device__ void part2_fused_carry(const BuildParams& P, const MaxPlus* s_fun, ui
   }
 }
 
+// k_part2d: k_part2 (dense bucket runs, tables of more than kP2SortedMaxBpp buckets per digit) with its
+// scatter pass staged as in k_part2st: each round of kP2dPer entries a thread is grouped by bucket in
+// LDS and leaves as one run per bucket, instead of one L2 request per 16-byte entry.  The round's
+// bucket counts are double-buffered so that only the scan needs a barrier of its own.  Single GPU.
+constexpr int kP2dPer = 6;
+
+__global__ __launch_bounds__(kPart2Block) void k_part2d(BuildParams P) {
+  // hist[nb] | cur[nb] | rc0[nb] | rc1[nb] | roff[nb] | gbase[nb] | stage[kPart2Block * kP2dPer]
+  extern __shared__ __attribute__((aligned(16))) uint32_t dyn[];
+  __shared__ uint64_t sh64[kPart2Block / 64 + 1];
+  if (build_aborted(P)) return;
+  const uint32_t dpart = blockIdx.x;
+  uint64_t lo, hi;
+  if (P.p1_region) {
+    lo = (uint64_t)dpart * P.p1_region;
+    hi = lo + min((uint64_t)P.p1_fill[dpart], P.p1_region);
+  } else {
+    lo = P.p1_off[(uint64_t)dpart * P.p1_tiles];
+    hi = (dpart + 1 < 256) ? P.p1_off[(uint64_t)(dpart + 1) * P.p1_tiles] : P.p1_off_total[0];
+  }
+  const uint32_t nbins = P.bpp;
+  const uint32_t b0 = dpart * nbins;
+  uint32_t* hist = dyn;
+  uint32_t* cur = hist + nbins;
+  uint32_t* rc[2] = {cur + nbins, cur + 2 * nbins};
+  uint32_t* roff = cur + 3 * nbins;
+  uint32_t* gbase = cur + 4 * nbins;
+  Entry* stage = reinterpret_cast<Entry*>(dyn + ((6 * nbins + 3) & ~3u));
+  constexpr uint32_t kRound = kPart2Block * kP2dPer;
+  const int tid = threadIdx.x;
+  for (uint32_t b = tid; b < 6 * nbins; b += kPart2Block) dyn[b] = 0;
+  __syncthreads();
+  // pass A: the bucket histogram (hashes only)
+  for (uint64_t i0 = lo; i0 < hi; i0 += (uint64_t)kPart2Block * kPart2Items) {
+    uint64_t h[kPart2Items];
+#pragma unroll
+    for (int k = 0; k < kPart2Items; k++) {
+      const uint64_t i = i0 + (uint64_t)k * kPart2Block + tid;
+      if (i < hi) h[k] = P.ent3[i].hash;
+    }
+#pragma unroll
+    for (int k = 0; k < kPart2Items; k++) {
+      const uint64_t i = i0 + (uint64_t)k * kPart2Block + tid;
+      if (i < hi) atomicAdd(&hist[bucket_of(P, h[k]) - b0], 1u);
+    }
+  }
+  __syncthreads();
+  // bucket offsets: consecutive bins per thread
+  const uint32_t per = (nbins + kPart2Block - 1) / kPart2Block;
+  {
+    uint64_t local = 0;
+    for (uint32_t q = 0; q < per; q++) {
+      const uint32_t b = tid * per + q;
+      if (b < nbins) local += hist[b];
+    }
+    uint64_t run = block_excl_sum<kPart2Block>(local, sh64, nullptr);
+    for (uint32_t q = 0; q < per; q++) {
+      const uint32_t b = tid * per + q;
+      if (b < nbins) {
+        const uint64_t bucket = (uint64_t)b0 + b;
+        if (bucket < P.nbuckets) {
+          P.boff[bucket] = lo + run;
+          P.bcount[bucket] = hist[b];
+        }
+        cur[b] = (uint32_t)run;
+        run += hist[b];
+      }
+    }
+  }
+  __syncthreads();
+  // pass B: rounds of kRound entries, grouped by bucket in the stage
+  auto load_round = [&](Entry (&v)[kP2dPer], uint64_t i0) {
+#pragma unroll
+    for (int k = 0; k < kP2dPer; k++) {
+      const uint64_t i = i0 + (uint64_t)k * kPart2Block + tid;
+      if (i < hi) v[k] = P.ent3[i];
+    }
+  };
+  Entry nx[kP2dPer];
+  if (lo < hi) load_round(nx, lo);
+  int par = 0;
+  for (uint64_t i0 = lo; i0 < hi; i0 += kRound, par ^= 1) {
+    Entry v[kP2dPer];
+#pragma unroll
+    for (int k = 0; k < kP2dPer; k++) v[k] = nx[k];
+    if (i0 + kRound < hi) load_round(nx, i0 + kRound);
+    uint32_t* rcnt = rc[par];
+    uint32_t bk[kP2dPer], rk[kP2dPer];
+#pragma unroll
+    for (int k = 0; k < kP2dPer; k++) {
+      const uint64_t i = i0 + (uint64_t)k * kPart2Block + tid;
+      bk[k] = ~0u;
+      if (i >= hi) continue;
+      bk[k] = bucket_of(P, v[k].hash) - b0;
+      rk[k] = atomicAdd(&rcnt[bk[k]], 1u);
+    }
+    __syncthreads();
+    {  // the round's run offsets; each bin's region cursor moves past the round; the other parity's
+       // counts are cleared for the next round
+      uint64_t local = 0;
+      for (uint32_t q = 0; q < per; q++) {
+        const uint32_t b = tid * per + q;
+        if (b < nbins) local += rcnt[b];
+      }
+      uint64_t run = block_excl_sum<kPart2Block>(local, sh64, nullptr);
+      for (uint32_t q = 0; q < per; q++) {
+        const uint32_t b = tid * per + q;
+        if (b < nbins) {
+          roff[b] = (uint32_t)run;
+          gbase[b] = cur[b];
+          cur[b] += rcnt[b];
+          run += rcnt[b];
+          rc[par ^ 1][b] = 0;
+        }
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kP2dPer; k++)
+      if (bk[k] != ~0u) stage[roff[bk[k]] + rk[k]] = v[k];
+    __syncthreads();
+    const uint32_t nround = (uint32_t)min((uint64_t)kRound, hi - i0);
+    for (uint32_t i = tid; i < nround; i += kPart2Block) {
+      const Entry e = stage[i];
+      const uint32_t b = bucket_of(P, e.hash) - b0;
+      P.ent2[lo + gbase[b] + (i - roff[b])] = e;
+    }
+    __syncthreads();  // (the stage, roff and gbase are rewritten next round)
+  }
+}
+
 // Pass 2 for a table of up to kP2SortedMaxBpp buckets per digit (single GPU): the digit's entries
 // are also counted per (bucket, wanted slot) in LDS (16-bit counts), so that the same pass leaves
 // each bucket's max-plus carry function -- k_summary's output: F(x) = max(x + n - bsize,
@@ -1384,11 +1515,10 @@ __global__ __launch_bounds__(kPart2Block) void k_part2s(BuildParams P) {
 // LDS and leaves as one run per bucket.  The slot counts are 8-bit (4 per word), which frees the LDS
 // for the stage; a count that would pass 255 flags p2_overflow, and the host redoes the build with
 // dense runs (k_part2s's two-pass path).  Single GPU, fixed regions only.
-constexpr int kP2StagePer = 5;
-constexpr int kP2Stage = kPart2Block * kP2StagePer;
-
+template <int kP2StagePer>
 __global__ __launch_bounds__(kPart2Block) void k_part2st(BuildParams P) {
-  // h8[bpp * 256] | btot[bpp] | rcnt[bpp] | roff[bpp] | gbase[bpp] | stage[kP2Stage] | sbin[kP2Stage]
+  constexpr int kP2Stage = kPart2Block * kP2StagePer;
+  // h8[bpp * 256] | btot[bpp] | rcnt[bpp] | roff[bpp] | gbase[bpp] | stage[kP2Stage]
   extern __shared__ __attribute__((aligned(16))) uint32_t dyn[];
   if (build_aborted(P)) return;
   const uint32_t dpart = blockIdx.x;
@@ -1403,7 +1533,6 @@ __global__ __launch_bounds__(kPart2Block) void k_part2st(BuildParams P) {
   uint32_t* roff = rcnt + nbins;
   uint32_t* gbase = roff + nbins;
   Entry* stage = reinterpret_cast<Entry*>(dyn + ((nbins * 260 + 3) & ~3u));
-  uint8_t* sbin = reinterpret_cast<uint8_t*>(stage + kP2Stage);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   long long t_prev2 = P.part_dbg ? clock64() : 0;
   auto mark2 = [&](int i) {  // (SPARKEY_PART2_DEBUG: thread 0's cycles per phase)
@@ -1465,17 +1594,16 @@ __global__ __launch_bounds__(kPart2Block) void k_part2st(BuildParams P) {
 #pragma unroll
     for (int k = 0; k < kP2StagePer; k++) {
       if (bk[k] == ~0u) continue;
-      const uint32_t at = roff[bk[k]] + rk[k];
-      stage[at] = v[k];
-      sbin[at] = (uint8_t)bk[k];
+      stage[roff[bk[k]] + rk[k]] = v[k];
     }
     __syncthreads();
     // the runs: consecutive lanes on consecutive entries of a bucket's region
     const uint32_t nround = (uint32_t)min((uint64_t)kP2Stage, hi - i0);
     for (uint32_t i = tid; i < nround; i += kPart2Block) {
-      const uint32_t b = sbin[i];
+      const Entry e = stage[i];
+      const uint32_t b = (uint32_t)((fast_mod(e.hash, P.mod) >> kBucketShift) - b0);
       const uint32_t r = gbase[b] + (i - roff[b]);
-      if (r < kPlaceLdsMax) P.ent2[(b0 + b - P.b_lo) * (uint64_t)kPlaceLdsMax + r] = stage[i];
+      if (r < kPlaceLdsMax) P.ent2[(b0 + b - P.b_lo) * (uint64_t)kPlaceLdsMax + r] = e;
       else ovf = true;
     }
     __syncthreads();  // (the stage and the offsets are rewritten next round)
@@ -2229,20 +2357,33 @@ void launch_partition2(const BuildParams& P, hipStream_t s, StageTimer* tm) {
   tm->mark("partition", s);
 }
 
-// k_part2st's dynamic LDS (the 8-bit counts, the bucket words, the stage and its bucket bytes)
-static size_t part2st_lds(uint32_t bpp) {
-  return (size_t)((bpp * 260 + 3) & ~3u) * 4 + (size_t)kP2Stage * (sizeof(Entry) + 1);
+// k_part2d's dynamic LDS (six words a bucket, the stage)
+static size_t part2d_lds(uint32_t bpp) {
+  return (size_t)((6 * bpp + 3) & ~3u) * 4 + (size_t)kPart2Block * kP2dPer * sizeof(Entry);
+}
+
+// k_part2st's dynamic LDS (the 8-bit counts, the bucket words, the stage of `per` entries a thread)
+static size_t part2st_lds(uint32_t bpp, int per) {
+  return (size_t)((bpp * 260 + 3) & ~3u) * 4 + (size_t)kPart2Block * per * sizeof(Entry);
 }
 
 void launch_partition(const BuildParams& P, hipStream_t s, StageTimer* tm) {
   if (!P.p1_region) launch_partition1(P, s);
   else if (P.p1_kernel) hipLaunchKernelGGL(k_part1_regions, dim3((unsigned)P.p1_tiles), dim3(kPartBlock), 0, s, P);
   static const bool no_staged = getenv("SPARKEY_NO_P2_STAGED") != nullptr;  // (k_part2s: measurements)
-  if (P.p2_sorted && P.p2_fixed && P.fused_carry && P.p1_region && !P.p2_seg && !no_staged &&
-      part2st_lds(P.bpp) <= 150 * 1024)
-    hipLaunchKernelGGL(k_part2st, dim3(256), dim3(kPart2Block), part2st_lds(P.bpp), s, P);
+  // the largest stage (entries a thread per round) that fits: fewer rounds, fewer barriers
+  constexpr size_t kLdsMax = 158 * 1024;
+  const bool staged = P.p2_sorted && P.p2_fixed && P.fused_carry && P.p1_region && !P.p2_seg && !no_staged;
+  if (staged && part2st_lds(P.bpp, 6) <= kLdsMax)
+    hipLaunchKernelGGL(k_part2st<6>, dim3(256), dim3(kPart2Block), part2st_lds(P.bpp, 6), s, P);
+  else if (staged && part2st_lds(P.bpp, 5) <= kLdsMax)
+    hipLaunchKernelGGL(k_part2st<5>, dim3(256), dim3(kPart2Block), part2st_lds(P.bpp, 5), s, P);
+  else if (staged && part2st_lds(P.bpp, 4) <= kLdsMax)
+    hipLaunchKernelGGL(k_part2st<4>, dim3(256), dim3(kPart2Block), part2st_lds(P.bpp, 4), s, P);
   else if (P.p2_sorted)
     hipLaunchKernelGGL(k_part2s, dim3(256), dim3(kPart2Block), (size_t)(514u * P.bpp) * sizeof(uint32_t), s, P);
+  else if (!P.p2_seg && !no_staged && part2d_lds(P.bpp) <= kLdsMax)
+    hipLaunchKernelGGL(k_part2d, dim3(256), dim3(kPart2Block), part2d_lds(P.bpp), s, P);
   else
     hipLaunchKernelGGL(k_part2, dim3(256), dim3(kPart2Block), (size_t)(2u * P.bpp) * sizeof(uint32_t), s, P);
   tm->mark("partition", s);

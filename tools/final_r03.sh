@@ -14,10 +14,10 @@ mkdir -p $OUT
 Q="--steps 5 --warmup 1 --no-cpu-baseline --quick"
 pmc() {  # $1 = tag, rest = bench args
   local t=$1; shift
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/$t/trace -o run -- python3 bench.py "$@" > $OUT/$t.trace.log 2>&1 &&
-  timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/$t/fetch -o run -- python3 bench.py "$@" > $OUT/$t.fetch.log 2>&1 &&
-  timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/$t/write -o run -- python3 bench.py "$@" > $OUT/$t.write.log 2>&1 &&
-  timeout -s KILL 200 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU --output-format csv -d $OUT/$t/sq -o run -- python3 bench.py "$@" > $OUT/$t.sq.log 2>&1
+  timeout -k 10 420 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/$t/trace -o run -- python3 bench.py "$@" > $OUT/$t.trace.log 2>&1 &&
+  timeout -s KILL 420 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/$t/fetch -o run -- python3 bench.py "$@" > $OUT/$t.fetch.log 2>&1 &&
+  timeout -s KILL 420 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/$t/write -o run -- python3 bench.py "$@" > $OUT/$t.write.log 2>&1 &&
+  timeout -s KILL 420 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU --output-format csv -d $OUT/$t/sq -o run -- python3 bench.py "$@" > $OUT/$t.sq.log 2>&1
 }
 rc=0
 for st in $STEPS; do
