@@ -590,7 +590,9 @@ static bool want_frame3(BuildParams& P, const LogHdr& lh, int64_t entry, int64_t
   Q.f3_cover = (double)Q.max_rec_len > 1.5 * mean ? 1 : 0;
   if (const char* v = getenv("SPARKEY_FRAME3_COVER")) Q.f3_cover = atoi(v) ? 1 : 0;
   if (!frame3_fits(Q, mean, pk)) return false;
-  Q.f3_short = pk < 0.12 ? 2 : pk < 0.3 ? 3 : 4;
+  // (C3's shape, pk 0.1: K = 3 measured 0.870 ms against K = 2's 0.903 per 10M records,
+  // profiles/r03/k_frame3_sweep_c3_10m.txt)
+  Q.f3_short = pk < 0.05 ? 2 : pk < 0.3 ? 3 : 4;
   if (const char* v = getenv("SPARKEY_FRAME3_SHORT")) Q.f3_short = std::max(1, std::min(4, atoi(v)));
   Q.f3_stop = getenv("SPARKEY_FRAME3_STOP") ? atoi(getenv("SPARKEY_FRAME3_STOP")) : -1;
   P = Q;
@@ -1459,11 +1461,16 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
     placement_path = serial ? 1 : 2;
     P.p1_hist_ready = 0;  // the exact path's partitions (DELETEs left out) count their own digits
     P.p2_sorted = 0;
-    if (P.p1_region) {  // the exact path replays the entries in log order: frame them into `ent`
+    // The exact path replays the entries in log order, from the framing's slabs (`ent`).  The slab
+    // framings left them there (k_part1_regions only read them); the uniform framing wrote straight
+    // into the digit regions, so it frames again into `ent`.
+    if (P.p1_region && !P.p1_kernel) {
       P.p1_region = 0;
       rc = launch_framing(pl, P, framing_path, s, err, err_len);
       if (rc) return rc;
     }
+    P.p1_region = 0;
+    P.p1_kernel = 0;
     float ms2 = 0.f;
     HIP_TRY(hipEventRecord(pl->ev0, s));
     if (serial) {
