@@ -503,7 +503,7 @@ def sharded(args, dev, world, rank):
             for k, v in r.phase_ms.items():
                 phases[k] = phases.get(k, 0.0) + v
             return r.out, {"sharded": {"sharded": 1, "exact": 2, "gathered": 3}[r.path],
-                           "num_entries": r.stats["num_entries"]}
+                           "num_entries": r.stats["num_entries"], "out_offset": r.out_offset}
     else:
         uid = [_native.shard_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
@@ -538,7 +538,8 @@ def sharded(args, dev, world, rank):
     identical = None
     if args.check:  # the sharded .spi against one single-GPU build of the whole log (rank 0)
         pieces = [None] * world
-        dist.all_gather_object(pieces, (out_off, out.cpu().numpy().tobytes()))
+        # (the Python orchestrator's slot split is its own: its result carries the file offset)
+        dist.all_gather_object(pieces, (info.get("out_offset", out_off), out.cpu().numpy().tobytes()))
         if rank == 0:
             if full_log is None:
                 full_log = synth.fixed_log(n_total, 16, 100, seed=args.seed, file_id=0x5EED0000)
@@ -554,6 +555,11 @@ def sharded(args, dev, world, rank):
             for off, b in pieces:
                 got[off:off + len(b)] = b
             identical = bytes(got) == single
+            if not identical:  # where the pieces sit and the first byte that differs
+                d = next((i for i in range(0, size, 1 << 20) if got[i:i + (1 << 20)] != single[i:i + (1 << 20)]), 0)
+                d = next((j for j in range(d, min(size, d + (1 << 20))) if got[j] != single[j]), -1)
+                identical = {"identical": False, "size": size, "pieces": [(o, len(b)) for o, b in pieces],
+                             "first_diff": d, "slot": (d - 112) // 16 if d >= 112 else None}
     slot = 16
     from sparkey.sharded import parse_log_header
     cap = 1 | int(parse_log_header(header)["num_puts"] * 1.3)

@@ -52,9 +52,10 @@ namespace {
 
 constexpr int kF3Lcap = 16;      // record starts a survivor lists inside its chunk
 constexpr unsigned kF3Caps = 64u;  // Status.spec_fail: a list cap was exceeded (k_frame redoes it)
+constexpr int kF3WavesPerSimd = 6;  // k_frame3's occupancy bound (its VGPR budget)
 
 // Scratch after the staged region (bytes), sized on the host so that four waves of a workgroup and
-// four workgroups fit a CU's LDS where the log allows (P.f3_cand_cap candidates, P.f3_surv_cap heads):
+// kF3WavesPerSimd workgroups fit a CU's LDS where the log allows (P.f3_cand_cap candidates, P.f3_surv_cap heads):
 // candidate list, later the wave's record list (u16 each); head starts / exits / counts / per-chunk
 // choice; the heads' record lists, earlier the screen bitmap and then the short walk's reached-start
 // bitmap (one bit per region byte).
@@ -87,7 +88,9 @@ __device__ __forceinline__ void frame3_region(const BuildParams& P, const uint64
   const uint64_t k0 = kf + wv * (uint64_t)W;
   const int nw = (int)min((uint64_t)W, kf + P.fr_nchunks - k0);
   const int64_t R0 = (int64_t)(k0 << cs);
-  const int64_t RLEN = ((int64_t)nw << cs) + LOOK + 16;
+  // the staged bytes: the chunks, then at least max(LOOK, maxRecLen) + 16 more, so that every key a
+  // listed record holds lies in LDS (records start inside the chunks)
+  const int64_t RLEN = (int64_t)P.f3_rgn - ((int64_t)(W - nw) << cs);
   const int kF3CandCap = P.f3_cand_cap, kF3SurvCap = P.f3_surv_cap, kF3RecCap = P.f3_cand_cap;
   const int kF3OffLists = f3_off_lists(kF3CandCap, kF3SurvCap);
   uint8_t* rgn = lds;
@@ -539,16 +542,9 @@ __device__ __forceinline__ void frame3_region(const BuildParams& P, const uint64
       const int64_t p = R0 + (int64_t)cand[r];
       const RecHdr h = decode_rgn(rgn, R0, p, log_len);
       const int64_t kp = p + h.hlen;
-      uint64_t hash;
-      if (kp + h.klen + 16 <= R0 + RLEN) {  // key in the region
-        const RgnKey ld{rgn, (uint32_t)(kp - R0)};
-        hash = P.hash_size == 8 ? murmur64_ld(ld, h.klen, (uint32_t)P.seed) : (uint64_t)murmur32_ld(ld, h.klen, (uint32_t)P.seed);
-      } else if (kp + h.klen + 16 <= log_len) {
-        const GlobalKey ld{P.log + kp};
-        hash = P.hash_size == 8 ? murmur64_ld(ld, h.klen, (uint32_t)P.seed) : (uint64_t)murmur32_ld(ld, h.klen, (uint32_t)P.seed);
-      } else {
-        hash = key_hash(P.hash_size, P.log + kp, h.klen, (uint32_t)P.seed);
-      }
+      const RgnKey ld{rgn, (uint32_t)(kp - R0)};  // (in the region: see RLEN)
+      const uint64_t hash = P.hash_size == 8 ? murmur64_ld(ld, h.klen, (uint32_t)P.seed)
+                                             : (uint64_t)murmur32_ld(ld, h.klen, (uint32_t)P.seed);
       uint64_t addr = (uint64_t)p << P.ebb;
       if (!h.put) {
         addr |= kDelBit;
@@ -580,8 +576,10 @@ __device__ __forceinline__ void frame3_region(const BuildParams& P, const uint64
   }
 }
 
-// kFrameWaves waves per workgroup, one region each, regions by workgroup ticket (see k_frame).
-__global__ __launch_bounds__(64 * kFrameWaves) void k_frame3(BuildParams P, uint32_t lds_per_wave) {
+// kFrameWaves waves per workgroup, one region each, regions by workgroup ticket (see k_frame).  The
+// walks wait on LDS reads, one after the other: kF3WavesPerSimd waves (80 VGPRs) hide them where a
+// CU's LDS holds as many regions (frame3_fits).
+__global__ __launch_bounds__(64 * kFrameWaves, kF3WavesPerSimd) void k_frame3(BuildParams P, uint32_t lds_per_wave) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   __shared__ unsigned int tk;
   if (threadIdx.x == 0) tk = atomicAdd(P.frame_ticket, 1u);
@@ -606,14 +604,15 @@ uint32_t frame3_lds_per_wave(const BuildParams& P) {
 // The LDS layout of k_frame3 for this geometry (P.fr_w, fr_cshift, fr_look, f3_cover set): the region
 // and the list caps.  The candidate cap is 2.2x the expected candidates of a wave (pass = the chance
 // that a random byte pair passes the screen) plus 32, and at least 1.7x its expected records + 32;
-// when that allows, it is trimmed so that 16 waves (4 workgroups) fit a CU.  False when the lists
+// when that allows, it is trimmed so that as many workgroups as the VGPRs allow fit a CU.  False when the lists
 // cannot hold what the header's mean record implies (k_frame frames such logs).
 bool frame3_fits(BuildParams& P, double mean_record, double pass) {
   const double C = (double)(1ll << P.fr_cshift);
   if (!P.fr_fast || P.max_rec_len > 4096 || P.fr_cshift < 7) return false;
   if (mean_record <= 0.0 || C / mean_record > 0.6 * kF3Lcap) return false;
-  if (((int64_t)P.fr_w << P.fr_cshift) + P.fr_look + 16 >= 32768) return false;  // 15-bit region offsets
-  P.f3_rgn = (int32_t)((((int64_t)P.fr_w << P.fr_cshift) + P.fr_look + 16 + 15) & ~15ll);
+  const int64_t tail = std::max<int64_t>(P.fr_look, P.max_rec_len);  // (the keys of the last chunk's records)
+  if (((int64_t)P.fr_w << P.fr_cshift) + tail + 16 >= 32768) return false;  // 15-bit region offsets
+  P.f3_rgn = (int32_t)((((int64_t)P.fr_w << P.fr_cshift) + tail + 16 + 15) & ~15ll);
   const double recs = (double)P.fr_w * C / mean_record;
   const double false_cands = (double)P.fr_w * (double)std::min<int64_t>(1ll << P.fr_cshift, P.max_rec_len) * pass;
   if (recs > 0.6 * 512 || false_cands > 0.6 * 512) return false;
@@ -621,13 +620,14 @@ bool frame3_fits(BuildParams& P, double mean_record, double pass) {
   // heads: about one per chunk plus a few false survivors; one long walk per lane
   P.f3_surv_cap = std::min(64, std::max(32, (2 * P.fr_w + 8 + 7) & ~7));
   P.f3_cand_cap = 512;
-  // the largest cap >= need (16-multiple) that keeps 4 workgroups of 4 waves (+16 B static) in 160 KiB
-  // of LDS with 512-byte allocation granules
-  for (int cap = 512; cap >= need; cap -= 16) {
-    P.f3_cand_cap = cap;
-    const uint64_t wg = ((uint64_t)frame3_lds_per_wave(P) * kFrameWaves + 16 + 511) & ~511ull;
-    if (wg * 4 <= 160 * 1024) return true;
-  }
+  // the largest cap >= need (16-multiple) that keeps the most workgroups of 4 waves (+16 B static, up
+  // to kF3WavesPerSimd of them) in 160 KiB of LDS with 512-byte allocation granules
+  for (int wgs = kF3WavesPerSimd; wgs >= 1; wgs--)
+    for (int cap = 512; cap >= need; cap -= 16) {
+      P.f3_cand_cap = cap;
+      const uint64_t wg = ((uint64_t)frame3_lds_per_wave(P) * kFrameWaves + 16 + 511) & ~511ull;
+      if (wg * wgs <= 160 * 1024) return true;
+    }
   P.f3_cand_cap = 512;  // (fewer waves per CU)
   return true;
 }

@@ -590,7 +590,7 @@ class ShardedBuilder:
         if g == 0 and host_header:
             hdr = s.index_header(opts, n_total, 0, max_disp, collisions, total_disp)
             out[:INDEX_HEADER_SIZE].copy_(s.from_host(hdr))
-        res.out = out
+        res.out = out[:out_len]  # (the allocation is rounded up)
         res.stats = stats
         mark("stats")
         return res
@@ -690,7 +690,7 @@ class ShardedBuilder:
         if g == 0:
             hdr = s.index_header(opts, n_entries, garbage, max_disp, collisions, total_disp)
             out[:INDEX_HEADER_SIZE].copy_(s.from_host(hdr))
-        res.out = out
+        res.out = out[:hdr_off + (slot_hi - slot_lo) * slot_size]  # (the allocation is rounded up)
         res.stats = {"num_entries": n_entries, "garbage_size": garbage, "max_displacement": max_disp,
                      "hash_collisions": collisions, "total_displacement": total_disp, "placement_path": 2}
         res.path = "exact"
@@ -749,7 +749,7 @@ class ShardedBuilder:
         lo = 0 if g == 0 else INDEX_HEADER_SIZE + res.slot_lo * slot_size
         out = s.alloc(out_len)
         out[:out_len].copy_(full[lo: lo + out_len])
-        res.out = out
+        res.out = out[:out_len]
         res.stats = stats
         res.path = "gathered"
         return res

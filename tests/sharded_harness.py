@@ -85,7 +85,8 @@ def run_world(log: bytes, world: int, opts_kw: dict, tmpdir: str, kind: str = "c
         data = open(os.path.join(tmpdir, f"rank{r}.bin"), "rb").read()
         want = (INDEX_HEADER_SIZE if r == 0 else 0) + (meta["slot_hi"] - meta["slot_lo"]) * (size - INDEX_HEADER_SIZE) \
             // max(1, _capacity(h, opts))
-        spi[meta["offset"]: meta["offset"] + want] = data[:want]
+        assert len(data) == want, (r, len(data), want)  # ShardResult.out: exactly the rank's bytes
+        spi[meta["offset"]: meta["offset"] + want] = data
         metas.append(meta)
     return bytes(spi), metas
 
@@ -189,7 +190,8 @@ def run_threads(log: bytes, world: int, opts_kw: dict, device=None):
     for r in range(world):
         res, data = results[r]
         want = (INDEX_HEADER_SIZE if r == 0 else 0) + (res.slot_hi - res.slot_lo) * S
-        spi[res.out_offset: res.out_offset + want] = data[:want]
+        assert len(data) == want, (r, len(data), want)  # ShardResult.out: exactly the rank's bytes
+        spi[res.out_offset: res.out_offset + want] = data
         metas.append({"path": res.path, "rounds": res.rounds, "n_pairs": res.n_pairs, "n_spill": res.n_spill,
                       "stats": res.stats})
     return bytes(spi), metas
