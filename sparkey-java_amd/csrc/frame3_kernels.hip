@@ -91,7 +91,7 @@ __device__ __forceinline__ void frame3_region(const BuildParams& P, const uint64
   // the staged bytes: the chunks, then at least max(LOOK, maxRecLen) + 16 more, so that every key a
   // listed record holds lies in LDS (records start inside the chunks)
   const int64_t RLEN = (int64_t)P.f3_rgn - ((int64_t)(W - nw) << cs);
-  const int kF3CandCap = P.f3_cand_cap, kF3SurvCap = P.f3_surv_cap, kF3RecCap = P.f3_cand_cap;
+  const int kF3CandCap = P.f3_cand_cap, kF3SurvCap = P.f3_surv_cap;
   const int kF3OffLists = f3_off_lists(kF3CandCap, kF3SurvCap);
   uint8_t* rgn = lds;
   uint8_t* scr = lds + P.f3_rgn;
@@ -244,6 +244,7 @@ __device__ __forceinline__ void frame3_region(const BuildParams& P, const uint64
     return;
   }
   wave_sync();
+  mark(7);  // (the candidate list: reported after the other phases)
 
   // ---- 2 short walk: each candidate K records on (or to its stop); a survivor marks the starts it
   //      reached inside its chunk (bit 15 of its list entry: alive).  More heads than the lanes
@@ -500,10 +501,6 @@ __device__ __forceinline__ void frame3_region(const BuildParams& P, const uint64
     const uint32_t cnt = sel >= 0 ? (uint32_t)(s_cnt[sel] - at) : 0u;
     const uint32_t incl = wave_incl_sum_u32(cnt);
     const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-    if (total > (uint32_t)kF3RecCap) {  // (the host ruled this out from the header's mean record)
-      if (lane == 0) atomicOr(&P.st->spec_fail, kF3Caps);
-      return;
-    }
     if (total > P.slab_cap) {
       if (spec) {
         const int64_t real = wait_prev();
@@ -520,26 +517,23 @@ __device__ __forceinline__ void frame3_region(const BuildParams& P, const uint64
       return;
     }
     if (lane == 0) P.wcount[wv] = total;
-    {  // the chosen lists back to back (the candidate list is dead), four independent reads a step
-      const uint32_t o = incl - cnt;
-      const uint16_t* src = lists + sel * kF3Lcap + at;
-      for (uint32_t i = 0; i < cnt; i += 4) {
-        uint16_t v[4];
-#pragma unroll
-        for (int u = 0; u < 4; u++) v[u] = i + u < cnt ? src[i + u] : 0;
-#pragma unroll
-        for (int u = 0; u < 4; u++)
-          if (i + u < cnt) cand[o + i + u] = v[u];
-      }
-    }
-    wave_sync();
+    // record r of the wave is entry r - base[j] of chunk j's chosen list (base: the scan of the
+    // counts; the last chunk whose base is <= r, so empty chunks are passed over)
+    const int32_t cbase = (int32_t)(incl - cnt);
+    const int32_t csrc = sel >= 0 ? sel * kF3Lcap + at : 0;
     mark(5);
-  if (P.f3_stop == 5) { fail(kF3Caps); return; }  // (SPARKEY_FRAME3_STOP: measurements)
+    if (P.f3_stop == 5) { fail(kF3Caps); return; }  // (SPARKEY_FRAME3_STOP: measurements)
     // ---- 5 hash ----
     const unsigned long long base = wv * (unsigned long long)P.slab_cap;
     ndel = 0;
     for (uint32_t r = (uint32_t)lane; r < total; r += 64) {
-      const int64_t p = R0 + (int64_t)cand[r];
+      int32_t src = 0;
+      for (int j = 0; j < nw; j++) {  // (wave-uniform)
+        const int32_t bj = __builtin_amdgcn_readlane(cbase, j);
+        const int32_t sj = __builtin_amdgcn_readlane(csrc, j);
+        if ((int32_t)r >= bj) src = sj + ((int32_t)r - bj);
+      }
+      const int64_t p = R0 + (int64_t)lists[src];
       const RecHdr h = decode_rgn(rgn, R0, p, log_len);
       const int64_t kp = p + h.hlen;
       const RgnKey ld{rgn, (uint32_t)(kp - R0)};  // (in the region: see RLEN)
@@ -560,7 +554,6 @@ __device__ __forceinline__ void frame3_region(const BuildParams& P, const uint64
       spec = false;
       if (real != ext) {
         ext = real;
-        wave_sync();  // (the record list is rewritten)
         continue;
       }
     }

@@ -741,9 +741,9 @@ static void print_frame_debug(sparkey_plan* pl, const BuildParams& P) {
   const double n = (double)nwv;
   fprintf(stderr, "[k_frame] waves=%llu C=%d W=%d mean cycles: stage %.0f screen %.0f walk %.0f entry %.0f "
           "counts %.0f slab %.0f hash %.0f | max entry %llu | walk iters %.1f survivors/wave %.1f unconverged/wave "
-          "%.2f\n",
+          "%.2f | slot 7 %.0f\n",
           (unsigned long long)nwv, 1 << P.fr_cshift, P.fr_w, sum[0] / n, sum[1] / n, sum[2] / n, sum[3] / n,
-          sum[4] / n, sum[5] / n, sum[6] / n, mx[3], sum[8] / n, sum[9] / n, sum[10] / n);
+          sum[4] / n, sum[5] / n, sum[6] / n, mx[3], sum[8] / n, sum[9] / n, sum[10] / n, sum[7] / n);
 }
 
 static void print_part2_debug(const BuildParams& P) {
