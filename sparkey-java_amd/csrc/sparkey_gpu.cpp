@@ -595,6 +595,7 @@ static bool want_frame3(BuildParams& P, const LogHdr& lh, int64_t entry, int64_t
   Q.f3_short = pk < 0.05 ? 2 : pk < 0.3 ? 3 : 4;
   if (const char* v = getenv("SPARKEY_FRAME3_SHORT")) Q.f3_short = std::max(1, std::min(4, atoi(v)));
   Q.f3_stop = getenv("SPARKEY_FRAME3_STOP") ? atoi(getenv("SPARKEY_FRAME3_STOP")) : -1;
+  Q.f3_noticket = getenv("SPARKEY_FRAME3_TICKET") ? 0 : 1;  // (frame3_kernels.hip: regions by workgroup id)
   P = Q;
   return true;
 }

@@ -526,6 +526,8 @@ def test_log_append_then_build(native):
 @pytest.mark.parametrize("env", [{}, {"SPARKEY_FRAME3_C": "256"}, {"SPARKEY_FRAME3_C": "512"},
                                  {"SPARKEY_FRAME3_C": "2048"}, {"SPARKEY_FRAME_REGION": "16384"},
                                  {"SPARKEY_FRAME_REGION": "4096"}, {"SPARKEY_FRAME_REGION": "6144"},
+                                 {"SPARKEY_FRAME3_WG": "4"}, {"SPARKEY_FRAME3_WG": "4", "SPARKEY_FRAME3_TICKET": "1"},
+                                 {"SPARKEY_FRAME3_TICKET": "1"},
                                  {"SPARKEY_FRAME_LOOK": "16"}, {"SPARKEY_FRAME_LOOK": "1024"}])
 def test_frame3_geometry(native, monkeypatch, env):
     """Chunk sizes, regions and look-aheads: the same bytes; k_frame3 frames in the default geometry
