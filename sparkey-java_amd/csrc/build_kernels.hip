@@ -510,6 +510,22 @@ void launch_build_init(uint8_t* out, const uint8_t* hdr, Status* st, uint32_t* f
   hipLaunchKernelGGL(k_build_init, dim3(1), dim3(256), 0, s, out, h, st, fill, n);
 }
 
+// The framing's spread DELETE counters into st->n_deletes, cleared for the next framing launch.
+__global__ __launch_bounds__(64) void k_sum_deletes(BuildParams P) {
+  const int lane = threadIdx.x;
+  unsigned long long v = 0;
+  for (int i = lane; i < kDelParts; i += 64) {
+    v += P.del_parts[i * 16];
+    P.del_parts[i * 16] = 0;
+  }
+  v = wave_sum_u64(v);
+  if (lane == 0 && v) atomicAdd(&P.st->n_deletes, v);
+}
+
+void launch_sum_deletes(const BuildParams& P, hipStream_t s) {
+  if (P.del_parts) hipLaunchKernelGGL(k_sum_deletes, dim3(1), dim3(64), 0, s, P);
+}
+
 void launch_stats_folded(const BuildParams& P, hipStream_t s, StageTimer* tm) {
   hipLaunchKernelGGL(k_stats_folded, dim3(grid_for(std::max<uint64_t>(P.nbuckets, 1), kStatFoldBlock)),
                      dim3(kStatFoldBlock), 0, s, P);

@@ -176,6 +176,10 @@ struct BuildParams {
   // k_frame granules (zeroed before every launch)
   unsigned long long* exit_desc;
   unsigned int* frame_ticket;     // k_frame wave tickets (zeroed with the granules)
+  // the framing kernels' DELETE counts: kDelParts counters 128 B apart (wave wv adds to wv % kDelParts),
+  // summed into st->n_deletes by launch_sum_deletes -- one device-wide counter serialised 131K atomics
+  // per 10M-record churn log (1.0 ms of k_frame3's 1.65)
+  unsigned long long* del_parts;
   unsigned long long fr_spin_ticks;  // bound on a wave's wait for its predecessor (100 MHz ticks)
   // radix partition
   uint32_t* p1_hist;  // [256][p1_tiles]
@@ -317,6 +321,8 @@ void launch_verify(const BuildParams& P, hipStream_t s, StageTimer* tm);
 void launch_stats(const BuildParams& P, hipStream_t s, int sequential, StageTimer* tm);
 void launch_stats_folded(const BuildParams& P, hipStream_t s, StageTimer* tm);
 void launch_build_init(uint8_t* out, const uint8_t* hdr, Status* st, uint32_t* fill, uint32_t n, hipStream_t s);
+constexpr int kDelParts = 64;
+void launch_sum_deletes(const BuildParams& P, hipStream_t s);
 void launch_stats_folded_shard(const BuildParams& P, hipStream_t s);
 // exact replay (exact_kernels.hip)
 void launch_sequential(const BuildParams& P, hipStream_t s, int sorted_order);

@@ -421,7 +421,7 @@ __device__ __forceinline__ void frame2_region(const BuildParams& P, const uint64
     break;
   }
   ndel = wave_sum_u64(ndel);
-  if (ndel && lane == 0) atomicAdd(&P.st->n_deletes, ndel);
+  if (ndel && lane == 0) add_deletes(P, wv, ndel);
   mark(4);
   if (P.dbg && lane == 0) {
     P.dbg[wv * 16 + 9] = ns0;

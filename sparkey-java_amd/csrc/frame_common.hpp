@@ -188,6 +188,13 @@ __device__ __forceinline__ RecHdr decode_rgn(const uint8_t* r, int64_t R0, int64
 }
 
 
+// A framing wave's DELETE count: into one of kDelParts spread counters (build_kernels.hpp) when the
+// plan gives them, else straight into the status block.
+__device__ __forceinline__ void add_deletes(const BuildParams& P, uint64_t wv, unsigned long long n) {
+  if (P.del_parts) atomicAdd(&P.del_parts[(wv % kDelParts) * 16], n);
+  else atomicAdd(&P.st->n_deletes, n);
+}
+
 // The framing kernels run several independent waves per workgroup (one log region each): their
 // LDS hand-offs are between the lanes of one wave, so they synchronise the wave, not the workgroup
 // (a wave may spin on another region's exit while its neighbours are elsewhere).  Every LDS access

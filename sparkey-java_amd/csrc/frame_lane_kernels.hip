@@ -538,7 +538,7 @@ __global__ __launch_bounds__(256) void k_frame_lane_flags(BuildParams P, int che
   const unsigned long long ndw = wave_sum_u64((unsigned long long)nd);
   if ((threadIdx.x & 63) == 0) {
     if (any_bad) atomicOr(&P.st->spec_fail, 1u);
-    if (ndw) atomicAdd(&P.st->n_deletes, ndw);
+    if (ndw) add_deletes(P, blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6), ndw);
   }
 }
 

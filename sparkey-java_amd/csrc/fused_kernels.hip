@@ -603,20 +603,27 @@ __device__ __forceinline__ void frame_region(const BuildParams& P, const uint64_
     break;
   }
   ndel = wave_sum_u64(ndel);
-  if (ndel && lane == 0) atomicAdd(&P.st->n_deletes, ndel);
+  if (ndel && lane == 0) add_deletes(P, wv, ndel);
   mark(6);
 }
 
-// kFrameWaves waves per workgroup, one region each: the workgroup's ticket t gives regions
-// t * kFrameWaves + wave (frame_common.hpp).
-__global__ __launch_bounds__(64 * kFrameWaves, 5) void k_frame(BuildParams P, uint32_t lds_per_wave) {
+// NW waves per workgroup, one region each.  Default (frame3_kernels.hip's measurements): one wave per
+// workgroup, region = workgroup id (in-order dispatch starts the predecessor first; the spin on its
+// exit is bounded).  TICKET: regions by a device-wide ticket per workgroup, 4 waves each
+// (SPARKEY_FRAME_TICKET, the round-2 launch).
+template <int NW, bool TICKET>
+__global__ __launch_bounds__(64 * NW, 5) void k_frame(BuildParams P, uint32_t lds_per_wave) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  __shared__ unsigned int tk;
-  if (threadIdx.x == 0) tk = atomicAdd(P.frame_ticket, 1u);
-  __syncthreads();
+  uint32_t tk = blockIdx.x;
+  if (TICKET) {
+    __shared__ unsigned int s_tk;
+    if (threadIdx.x == 0) s_tk = atomicAdd(P.frame_ticket, 1u);
+    __syncthreads();
+    tk = s_tk;
+  }
   const uint64_t nwaves = (P.fr_nchunks + P.fr_w - 1) / P.fr_w;
   const uint32_t w = threadIdx.x >> 6;
-  const uint64_t wv = (uint64_t)tk * kFrameWaves + w;
+  const uint64_t wv = (uint64_t)tk * NW + w;
   if (wv < nwaves) frame_region(P, wv, lds + w * lds_per_wave);
 }
 
@@ -2293,8 +2300,11 @@ void launch_frame_fused(const BuildParams& P, hipStream_t s, StageTimer* tm) {
   const uint32_t per = (uint32_t)((lds + 15) & ~(size_t)15);
   // (SPARKEY_FRAME_LDS_PAD: extra LDS per workgroup, to measure the phases at lower occupancy)
   const size_t pad = getenv("SPARKEY_FRAME_LDS_PAD") ? (size_t)atoll(getenv("SPARKEY_FRAME_LDS_PAD")) : 0;
-  hipLaunchKernelGGL(k_frame, dim3((unsigned)((nwaves + kFrameWaves - 1) / kFrameWaves)), dim3(64 * kFrameWaves),
-                     (size_t)per * kFrameWaves + pad, s, P, per);
+  if (getenv("SPARKEY_FRAME_TICKET"))
+    hipLaunchKernelGGL((k_frame<kFrameWaves, true>), dim3((unsigned)((nwaves + kFrameWaves - 1) / kFrameWaves)),
+                       dim3(64 * kFrameWaves), (size_t)per * kFrameWaves + pad, s, P, per);
+  else
+    hipLaunchKernelGGL((k_frame<1, false>), dim3((unsigned)nwaves), dim3(64), (size_t)per + pad, s, P, per);
   tm->mark("frame", s);  // the stage is k_frame alone (its rocprof row); the slab scan counts as partition
   scan_exclusive<uint32_t, uint64_t, OpAdd>(P.wcount, P.woff, P.nslabs, (uint64_t*)&P.st->n_records, OpAdd(),
                                             P.scan_scratch_u64, s);

@@ -293,6 +293,7 @@ struct sparkey_plan {
   uint64_t c_desc = 0, c_p1h = 0, c_p1o = 0, c_dbg = 0, c_wcount = 0, c_woff = 0;
   uint64_t c_eseg = 0, c_seg_cnt = 0, c_seg_off = 0, c_seg_mark = 0, c_seg_start = 0, c_p2tab = 0;
   uint64_t* p2tab = nullptr;  // sharded receive: k_part2's run table
+  unsigned long long* delp = nullptr;  // the framing kernels' spread DELETE counters (kDelParts x 128 B)
   uint64_t c_app_i64 = 0, c_app_u32 = 0, c_app_u64 = 0, c_app_scan = 0;  // sparkey_log_append workspace
   int64_t* app_i64 = nullptr;
   uint32_t* app_u32 = nullptr;
@@ -699,6 +700,8 @@ static int reserve_for_framing(sparkey_plan* pl, BuildParams& P, int framing_pat
   P.bstat_start = pl->bstat_start;
   P.exit_desc = pl->desc;
   P.frame_ticket = reinterpret_cast<unsigned int*>(pl->desc + 2 * nwaves);
+  if (!pl->delp) HIP_TRY(hipMalloc(&pl->delp, (size_t)kDelParts * 16 * sizeof(unsigned long long)));
+  P.del_parts = pl->delp;
   P.fr_spin_ticks = 2000000000ull;  // 20 s of the 100 MHz wall clock
   if (const char* v = getenv("SPARKEY_FRAME_SPIN_TICKS")) P.fr_spin_ticks = strtoull(v, nullptr, 10);  // (tests)
   P.p1_hist = pl->p1_hist; P.p1_off = pl->p1_off; P.p1_off_total = pl->p1_off + 256ull * P.p1_tiles;
@@ -712,10 +715,12 @@ static int launch_framing(sparkey_plan* pl, const BuildParams& P, int framing_pa
   if (slab_framing(framing_path)) {
     HIP_TRY(hipMemsetAsync(pl->desc, 0, (2 * nwaves + 2) * sizeof(unsigned long long), s));
     HIP_TRY(hipMemsetAsync(pl->wcount, 0, (P.nslabs + 1) * sizeof(uint32_t), s));
+    if (P.del_parts) HIP_TRY(hipMemsetAsync(P.del_parts, 0, (size_t)kDelParts * 16 * sizeof(unsigned long long), s));
     if (framing_path == 3) launch_frame2(P, s, &pl->timer);
     else if (framing_path == 4) launch_frame3(P, s, &pl->timer);
     else if (framing_path == 5) launch_frame_lane(P, s, &pl->timer);
     else launch_frame_fused(P, s, &pl->timer);
+    launch_sum_deletes(P, s);  // (the spread DELETE counters into the status block)
   } else if (framing_path == 2) {
     launch_frame_uniform(P, s, &pl->timer);
     if (!P.p1_region) launch_dense_slabs(P, s);  // (with digit regions nothing reads the slab counts)
@@ -1772,7 +1777,7 @@ void sparkey_plan_destroy(sparkey_plan* pl) {
                   pl->seg_cls_cnt, pl->seg_cls_off, pl->p2tab,
                   pl->app_i64, pl->app_u32, pl->app_u64, pl->app_scan, pl->app_map,
                   pl->sn_blocks, pl->sn_dir, pl->sn_walk, pl->sn_recoff, pl->sn_vlog, pl->sn_itab, pl->sn_err,
-                  pl->xtab, pl->ex_starts, pl->ex_cnt, pl->ex_off, pl->sn_par};
+                  pl->xtab, pl->ex_starts, pl->ex_cnt, pl->ex_off, pl->sn_par, pl->delp};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (pl->h_status) (void)hipHostFree(pl->h_status);
