@@ -30,6 +30,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <cstdlib>
+
 #include "build_kernels.hpp"
 #include "device_common.hpp"
 #include "frame_common.hpp"
@@ -429,16 +431,21 @@ __device__ __forceinline__ void frame2_region(const BuildParams& P, const uint64
   }
 }
 
-// kFrameWaves waves per workgroup, one region each, regions by workgroup ticket (see k_frame).
-template <bool FAST>
-__global__ __launch_bounds__(64 * kFrameWaves, 5) void k_frame2(BuildParams P, uint32_t lds_per_wave) {
+// One wave per workgroup, region = workgroup id, as k_frame (fused_kernels.hip); TICKET: the 4-wave
+// ticket launch (SPARKEY_FRAME_TICKET).
+template <bool FAST, int NW, bool TICKET>
+__global__ __launch_bounds__(64 * NW, 5) void k_frame2(BuildParams P, uint32_t lds_per_wave) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  __shared__ unsigned int tk;
-  if (threadIdx.x == 0) tk = atomicAdd(P.frame_ticket, 1u);
-  __syncthreads();
+  uint32_t tk = blockIdx.x;
+  if (TICKET) {
+    __shared__ unsigned int s_tk;
+    if (threadIdx.x == 0) s_tk = atomicAdd(P.frame_ticket, 1u);
+    __syncthreads();
+    tk = s_tk;
+  }
   const uint64_t nwaves = (P.fr_nchunks + P.fr_w - 1) / P.fr_w;
   const uint32_t w = threadIdx.x >> 6;
-  const uint64_t wv = (uint64_t)tk * kFrameWaves + w;
+  const uint64_t wv = (uint64_t)tk * NW + w;
   if (wv < nwaves) frame2_region<FAST>(P, wv, lds + w * lds_per_wave);
 }
 
@@ -447,9 +454,15 @@ void launch_frame2(const BuildParams& P, hipStream_t s, StageTimer* tm) {
   const uint64_t nwaves = (P.fr_nchunks + P.fr_w - 1) / P.fr_w;
   const size_t lds = (size_t)P.f2_rgn_bytes + 2 * (size_t)P.fr_w * P.f2_lcap * 2;
   const uint32_t per = (uint32_t)((lds + 15) & ~(size_t)15);
-  const dim3 grid((unsigned)((nwaves + kFrameWaves - 1) / kFrameWaves)), block(64 * kFrameWaves);
-  if (P.fr_fast) hipLaunchKernelGGL(k_frame2<true>, grid, block, (size_t)per * kFrameWaves, s, P, per);
-  else hipLaunchKernelGGL(k_frame2<false>, grid, block, (size_t)per * kFrameWaves, s, P, per);
+  if (getenv("SPARKEY_FRAME_TICKET")) {
+    const dim3 grid((unsigned)((nwaves + kFrameWaves - 1) / kFrameWaves)), block(64 * kFrameWaves);
+    if (P.fr_fast) hipLaunchKernelGGL((k_frame2<true, kFrameWaves, true>), grid, block, (size_t)per * kFrameWaves, s, P, per);
+    else hipLaunchKernelGGL((k_frame2<false, kFrameWaves, true>), grid, block, (size_t)per * kFrameWaves, s, P, per);
+  } else {
+    const dim3 grid((unsigned)nwaves), block(64);
+    if (P.fr_fast) hipLaunchKernelGGL((k_frame2<true, 1, false>), grid, block, (size_t)per, s, P, per);
+    else hipLaunchKernelGGL((k_frame2<false, 1, false>), grid, block, (size_t)per, s, P, per);
+  }
   tm->mark("frame", s);
   scan_exclusive<uint32_t, uint64_t, OpAdd>(P.wcount, P.woff, P.nslabs, (uint64_t*)&P.st->n_records, OpAdd(),
                                             P.scan_scratch_u64, s);
