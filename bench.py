@@ -1,17 +1,19 @@
 """Benchmark: device-resident Sparkey hash-file (.spi) builds on MI355X.
 
 One step = one full IndexHash.createNew-equivalent build (framing, MurmurHash3, placement, stats,
-header) of a C2-shaped log (10M PUTs per GPU, 16-byte keys, 100-byte values, NONE) already
-resident in HBM, into a device-resident .spi image.
+header) of a C2-shaped log (16-byte keys, 100-byte values, NONE) already resident in HBM, into a
+device-resident .spi image.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--entries 10000000] [--no-cpu-baseline]
-                    [--workload c2|c3|c5|churn|snappy|zstd|get|append]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--entries N] [--no-cpu-baseline]
+                    [--workload c2|c3|c4|c5|churn|snappy|zstd|get|append]
 
 N = 1: the C2 log (10M records) built on one GPU; the line carries the per-stage roofline and the
 CPU baseline (the oracle's sequential IN_MEMORY restatement on the host, timed on the same log).
-N > 1 (torch.distributed.run, one rank per GPU, RCCL): ONE index over a log of N x 10M C2 records
-whose byte range is split across the ranks -- weak scaling, 10M records per GPU.
-Prints ONE JSON line on rank 0.
+--workload c4: BASELINE's configs[3] size, 1B records, on one GPU.
+N > 1 (torch.distributed.run, one rank per GPU, RCCL): ONE index over a log of N x 125M C2-shaped
+records (C4 -- 1B records -- at N = 8) whose byte range is split across the ranks, each
+rank generating its range in HBM -- weak scaling, 125M records per GPU; afterwards every rank's slice
+is checked against one single-GPU build of the whole log.  Prints ONE JSON line on rank 0.
 """
 import argparse
 import json
@@ -104,6 +106,8 @@ WORKLOADS = {
     "zstd": {"name": "C2 records (10M PUTs x (16 B key, 100 B value)), CompressionType.ZSTD (level 3), 64 KiB "
                      "blocks, IN_MEMORY", "sorting": False, "path": 0},
     "append": {"name": "GPU log producer (batched LogWriter.put)", "sorting": False, "path": 0},
+    "c4": {"name": "C4: 1B PUTs x (16 B key, 100 B value), CompressionType.NONE, IN_MEMORY, one GPU (118 GB log "
+                   "in HBM)", "sorting": False, "path": 0},
     "get": {"name": "batched IndexHash.get of every key of the C2 index (log and index resident in HBM)",
             "sorting": False, "path": 0},
 }
@@ -261,7 +265,7 @@ def single_gpu(args, dev):
     dom_bytes = stage_bytes(dom, n, frame_end, slot, cap, passes, comp_end=log_len) if dom else 0
     achieved = dom_bytes / (stage_ms[dom] * 1e-3) / 1e9 if dom and stage_ms[dom] > 0 else 0.0
     b_alg = (log_len - 84) + 112 + slot * cap
-    assert stats.placement_path == wl["path"] and stats.framing_path in (0, 2, 3, 4, 5), stats.as_dict()
+    assert stats.placement_path == wl["path"] and stats.framing_path in (0, 2, 4), stats.as_dict()
     assert wl["path"] != 0 or stats.num_entries == n, stats.as_dict()
 
     if args.quick:  # (profiling runs: the timed builds only)
@@ -287,7 +291,7 @@ def single_gpu(args, dev):
     # uniform and the default build took k_frame_uniform
     general = general_spi = None
     if stats.framing_path == 2:
-        os.environ["SPARKEY_NO_UNIFORM"] = "1"
+        _native.debug_set("no_uniform", 1)
         try:
             one_build()
             torch.cuda.synchronize(dev)
@@ -301,14 +305,14 @@ def single_gpu(args, dev):
             torch.cuda.synchronize(dev)
             g_el = time.perf_counter() - t_g
             plan.set_profiling(False)
-            assert g_stats.framing_path in (0, 3, 4, 5), g_stats.as_dict()
+            assert g_stats.framing_path in (0, 4), g_stats.as_dict()
             general_spi = d_out.cpu().numpy().tobytes()  # (compared with the headline build below)
             g_stage = {k: v / g_steps for k, v in g_acc.items()}
             general = {"ms_per_step": g_el * 1000.0 / g_steps, "keys_per_s": n * g_steps / g_el,
                        "stage_ms": g_stage,
                        "frame_achieved_gbs": stage_bytes("frame", n, frame_end, slot, cap) / (g_stage["frame"] * 1e-3) / 1e9}
         finally:
-            del os.environ["SPARKEY_NO_UNIFORM"]
+            _native.debug_set("no_uniform", None)
 
     # file -> file (north_star: "log file in, hash file out"): sparkey_build_index_file, the entry
     # point the JNI shim calls, on the same log written to a file; page-cache warm, fsync off (the
@@ -398,9 +402,7 @@ def single_gpu(args, dev):
         "build_algorithmic_bytes": b_alg,
         "stage_ms": stage_ms,
         "framing": {0: "k_frame (speculative)", 1: "serial walk", 2: "k_frame_uniform (uniform records)",
-                    3: "k_frame2 (speculative, mixed record sizes)",
-                    4: "k_frame3 (short/long walks, one-byte VLQs)",
-                    5: "k_frame_lane (one lane per log region, one-byte VLQs)"}[stats.framing_path],
+                    4: "k_frame3 (short/long walks, one-byte VLQs)"}[stats.framing_path],
         "general_framing": general,
         "host_to_host_keys_per_s": h2h,
         "file_to_file_keys_per_s": file_rate,
@@ -410,6 +412,114 @@ def single_gpu(args, dev):
         "gen_s": gen_s,
         "version": sparkey.version(),
     }
+
+
+def single_gpu_c4(args, dev):
+    """--workload c4: BASELINE.json configs[3]'s 1B records (16 B key, 100 B value) on ONE GPU -- a
+    118 GB log generated in HBM (sparkey/synth_device.py), a 20.8 GB .spi.  Timed like the C2 line;
+    checked by the header's numEntries and IndexHash.get of every 1000th key (sparkey_get_batch), and
+    the CPU baseline's bit-identity on a bounded C2-shaped sample of the same records."""
+    import sparkey
+    from sparkey import _native, synth_device
+    n = args.entries
+    t0 = time.time()
+    d_log = synth_device.fixed_log(n, 16, 100, seed=args.seed, file_id=0x5EED0000, device=dev)
+    torch.cuda.synchronize(dev)
+    gen_s = time.time() - t0
+    header = d_log[:84].cpu().numpy().tobytes()
+    log_len = d_log.numel()
+    opts = _native.make_opts(hash_size=0, hash_seed=HASH_SEED, sparsity=0.0, method=_native.METHOD_IN_MEMORY,
+                             device=dev.index)
+    out_len = _native.index_size(header, opts)
+    d_out = torch.empty(out_len, dtype=torch.uint8, device=dev)
+    plan = _native.Plan(dev.index)
+    stream = torch.cuda.Stream(dev)
+
+    def one_build():
+        return plan.build(header, d_log.data_ptr(), log_len, d_out.data_ptr(), out_len, opts, stream.cuda_stream)
+
+    for _ in range(args.warmup):
+        stats = one_build()
+    torch.cuda.synchronize(dev)
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        stats = one_build()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t_start
+    plan.set_profiling(True)
+    stage_acc, n_prof = {}, max(1, min(args.steps, 5))
+    for _ in range(n_prof):
+        one_build()
+        for name, ms in plan.stage_times():
+            stage_acc[name] = stage_acc.get(name, 0.0) + ms
+    plan.set_profiling(False)
+    stage_ms = {k: v / n_prof for k, v in stage_acc.items()}
+    slot = stats.hash_size + stats.address_size
+    cap = stats.capacity
+    passes = stats.partition_passes
+    dom = max(stage_ms, key=lambda k: stage_ms[k])
+    dom_bytes = stage_bytes(dom, n, log_len, slot, cap, passes)
+    achieved = dom_bytes / (stage_ms[dom] * 1e-3) / 1e9
+    b_alg = (log_len - 84) + 112 + slot * cap
+    ms_per_step = elapsed * 1000.0 / args.steps
+    assert stats.num_entries == n and stats.placement_path == 0, stats.as_dict()
+    # IndexHash.get of every 1000th key: the value of record i sits at 84 + 118 i + 18, 100 bytes
+    idx = torch.arange(0, n, 1000, dtype=torch.int64, device=dev)
+    keys = synth_device.fixed_keys(idx, seed=args.seed).reshape(-1)
+    key_off = torch.arange(0, 16 * (idx.numel() + 1), 16, dtype=torch.int64, device=dev)
+    pos = torch.empty(idx.numel(), dtype=torch.int64, device=dev)
+    vlen = torch.empty(idx.numel(), dtype=torch.int64, device=dev)
+    plan.get_batch(d_log.data_ptr(), log_len, d_out.data_ptr(), out_len, keys.data_ptr(), key_off.data_ptr(),
+                   idx.numel(), pos.data_ptr(), vlen.data_ptr())
+    gets_ok = bool((pos == idx * 118 + 84 + 18).all()) and bool((vlen == 100).all())
+    hdr = d_out[:112].cpu().numpy().tobytes()
+    plan.close()
+    del d_log, d_out, keys, key_off, pos, vlen
+    torch.cuda.empty_cache()
+    cpu = None
+    if not args.no_cpu_baseline:  # a bounded sample: the first 50M of the same records as their own log
+        import oracle
+        oracle.build()
+        m = 50_000_000
+        d_s = synth_device.fixed_log(m, 16, 100, seed=args.seed, file_id=0x5EED0000, device=dev)
+        s_hdr = d_s[:84].cpu().numpy().tobytes()
+        s_len = _native.index_size(s_hdr, opts)
+        d_so = torch.empty(s_len, dtype=torch.uint8, device=dev)
+        p2 = _native.Plan(dev.index)
+        p2.build(s_hdr, d_s.data_ptr(), d_s.numel(), d_so.data_ptr(), s_len, opts)
+        p2.close()
+        gpu_sample = d_so.cpu().numpy()
+        host = d_s.cpu().numpy()
+        del d_s, d_so
+        t2 = time.perf_counter()
+        want = oracle.build_index(host, HASH_SEED)
+        cpu_s = time.perf_counter() - t2
+        cpu = {"value": m / cpu_s, "unit": "keys/s", "cores": 1, "kind": "port",
+               "sample": f"the first {m} of the C4 records as their own log, oracle IN_MEMORY sequential "
+                         f"restatement (oracle/), 1 thread, {cpu_s:.2f} s", "host": host_info(),
+               "bit_identical_to_gpu_on_sample": bool(np_equal(gpu_sample, want))}
+    return {
+        "value": n * args.steps / elapsed, "ms_per_step": ms_per_step,
+        "config": {"workload": WORKLOADS["c4"]["name"], "entries": n, "log_bytes": int(log_len),
+                   "hash_bytes": stats.hash_size, "address_bytes": stats.address_size, "capacity": int(cap),
+                   "spi_bytes": int(out_len), "parallelism": "single"},
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS,
+                     "traffic": pmc_traffic(f"c4_{n}", {("frame", 2): "frame_uniform", ("partition", 1):
+                                                        "partition_regions"}.get(
+                         (dom, stats.framing_path if dom == "frame" else passes), dom)),
+                     "algorithmic_bytes_per_launch": dom_bytes, "avg_launch_ms": stage_ms[dom]},
+        "build_hbm_gbs": b_alg / (ms_per_step * 1e-3) / 1e9,
+        "build_algorithmic_bytes": b_alg,
+        "stage_ms": stage_ms,
+        "checks": {"num_entries": int.from_bytes(hdr[60:68], "little"), "gets_every_1000th_key_ok": gets_ok},
+        "cpu_baseline": cpu, "gen_s": gen_s, "version": sparkey.version(),
+    }
+
+
+def np_equal(a, b_bytes):
+    import numpy as np
+    return a.size == len(b_bytes) and np.array_equal(a, np.frombuffer(b_bytes, dtype=np.uint8))
 
 
 def parity_checks(args, dev, headline_spi, general_spi):
@@ -461,15 +571,34 @@ def parity_checks(args, dev, headline_spi, general_spi):
     return out
 
 
+def block_sums(t, block=1 << 28):
+    """Per 256 MiB block of a device byte tensor: (sum of its int64 words, sum of word * (2 * position
+    + 1)), wrapping mod 2^64, plus the bytes after the last whole word -- a checksum of checksums that
+    compares two .spi images without moving them to the host."""
+    n8 = t.numel() // 8
+    words = t[: n8 * 8].view(torch.int64)
+    out = []
+    for a in range(0, n8, block // 8):
+        w = words[a: a + block // 8]
+        pos = torch.arange(a, a + w.numel(), dtype=torch.int64, device=t.device) * 2 + 1
+        out.append((int(w.sum()), int((w * pos).sum())))
+    return out, t[n8 * 8:].cpu().numpy().tobytes()
+
+
 def sharded(args, dev, world, rank):
-    """N > 1 (one process per GPU): ONE index over a log of N x 10M C2 records whose byte range is split
-    across the ranks.  Each rank runs sparkey_shard_build -- the C++ orchestrator behind the C-ABI
+    """N > 1 (one process per GPU): ONE index over a log of N x entries C2-shaped records (C4 at N = 8 with
+    the default 125M per GPU: 1B records) whose byte range is split across the ranks; each rank generates
+    its range in HBM.  Each rank runs sparkey_shard_build -- the C++ orchestrator behind the C-ABI
     (csrc/shard_host.cpp) -- over its own RCCL communicator (unique id from rank 0 via
     torch.distributed, whose gloo group only carries the control messages: id, barrier, timing max).
-    --orchestrator python runs sparkey/sharded.py's ShardedBuilder over torch.distributed instead."""
+    --backend gloo: the same C++ orchestrator with its collectives over gloo on host buffers
+    (sparkey_shard_comm_create_host), every rank on one GPU (a rehearsal).  --orchestrator python runs
+    sparkey/sharded.py's ShardedBuilder over torch.distributed instead.  After the timed region
+    (--check, on by default): rank 0 builds the whole log on one GPU and compares every rank's slice
+    of the .spi with it, by per-block checksums."""
     import torch.distributed as dist
     import sparkey
-    from sparkey import _native, synth
+    from sparkey import _native, synth, synth_device
 
     n_total = args.entries * world
     churn = args.workload == "churn"  # overwrites + DELETEs: the sharded exact path (DESIGN.md §6.1)
@@ -485,15 +614,18 @@ def sharded(args, dev, world, rank):
         header, _ = synth.fixed_log_range(n_total, 0, 84, 16, 100, seed=args.seed, file_id=0x5EED0000)
     lo, hi, out_off, out_len = _native.shard_geometry(header, file_len, opts, rank, world)
     if churn:
-        part = full_log[lo:hi]
-    else:
-        _, part = synth.fixed_log_range(n_total, lo, hi, 16, 100, seed=args.seed, file_id=0x5EED0000)
+        buf = torch.from_numpy(full_log[lo:hi]).to(dev)
+    else:  # the rank's byte range, generated in HBM
+        _, buf = synth_device.fixed_log_range(n_total, lo, hi, 16, 100, seed=args.seed, file_id=0x5EED0000,
+                                              device=dev)
+    torch.cuda.synchronize(dev)
     gen_s = time.time() - t0
-    buf = torch.from_numpy(part).to(dev)
-    del part
     plan = _native.Plan(dev.index, hi - lo, 2 * args.entries)
     stream = torch.cuda.Stream(dev)
     phases = {}
+    shared_gpu = args.backend == "gloo"  # (the rehearsal: every rank on one GPU)
+    if shared_gpu:
+        _native.debug_set("frame_ticket", 1)  # builds share the device: framing regions by ticket
     if args.orchestrator == "python":
         from sparkey.sharded import Comm, GpuShardSteps, ShardedBuilder
         builder = ShardedBuilder(GpuShardSteps(dev, plan), Comm(device=dev))
@@ -505,9 +637,12 @@ def sharded(args, dev, world, rank):
             return r.out, {"sharded": {"sharded": 1, "exact": 2, "gathered": 3}[r.path],
                            "num_entries": r.stats["num_entries"], "out_offset": r.out_offset}
     else:
-        uid = [_native.shard_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        comm = _native.ShardComm(uid[0], rank, world, dev.index)
+        if shared_gpu:  # gloo on host buffers between the processes (sparkey_shard_comm_create_host)
+            comm = _native.ShardComm(None, rank, world, dev.index)
+        else:
+            uid = [_native.shard_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(uid, src=0)
+            comm = _native.ShardComm(uid[0], rank, world, dev.index)
         d_out = torch.empty(max(16, out_len), dtype=torch.uint8, device=dev)
 
         def one_build():
@@ -536,53 +671,71 @@ def sharded(args, dev, world, rank):
     else:
         assert info["sharded"] == 1 and info["num_entries"] == n_total, info
     identical = None
-    if args.check:  # the sharded .spi against one single-GPU build of the whole log (rank 0)
+    check_s = None
+    if not args.no_check:  # every rank's slice against ONE single-GPU build of the whole log (rank 0)
+        t_c = time.time()
+        mine = (info.get("out_offset", out_off), int(out.numel()), block_sums(out))
+        del out
         pieces = [None] * world
-        # (the Python orchestrator's slot split is its own: its result carries the file offset)
-        dist.all_gather_object(pieces, (info.get("out_offset", out_off), out.cpu().numpy().tobytes()))
+        dist.all_gather_object(pieces, mine)
+        plan.close()
+        if shared_gpu or rank == 0:
+            del buf
+            torch.cuda.empty_cache()
         if rank == 0:
-            if full_log is None:
-                full_log = synth.fixed_log(n_total, 16, 100, seed=args.seed, file_id=0x5EED0000)
-            d_full = torch.from_numpy(full_log).to(dev)
-            size = _native.index_size(full_log[:84].tobytes(), opts)
+            if full_log is not None:
+                d_full = torch.from_numpy(full_log).to(dev)
+            else:
+                d_full = synth_device.fixed_log(n_total, 16, 100, seed=args.seed, file_id=0x5EED0000, device=dev)
+            size = _native.index_size(header, opts)
             d_spi = torch.empty(size, dtype=torch.uint8, device=dev)
-            p1 = _native.Plan(dev.index, full_log.size, n_total)
-            p1.build(full_log[:84].tobytes(), d_full.data_ptr(), full_log.size, d_spi.data_ptr(), size, opts)
-            single = d_spi.cpu().numpy().tobytes()
+            p1 = _native.Plan(dev.index)
+            p1.build(header, d_full.data_ptr(), d_full.numel(), d_spi.data_ptr(), size, opts)
             p1.close()
-            del d_full, d_spi, full_log
-            got = bytearray(size)
-            for off, b in pieces:
-                got[off:off + len(b)] = b
-            identical = bytes(got) == single
-            if not identical:  # where the pieces sit and the first byte that differs
-                d = next((i for i in range(0, size, 1 << 20) if got[i:i + (1 << 20)] != single[i:i + (1 << 20)]), 0)
-                d = next((j for j in range(d, min(size, d + (1 << 20))) if got[j] != single[j]), -1)
-                identical = {"identical": False, "size": size, "pieces": [(o, len(b)) for o, b in pieces],
-                             "first_diff": d, "slot": (d - 112) // 16 if d >= 112 else None}
+            del d_full
+            bad = [r for r, (off, ln, sums) in enumerate(pieces) if block_sums(d_spi[off:off + ln]) != sums]
+            covered = sorted((off, ln) for off, ln, _ in pieces)
+            contiguous = covered[0][0] == 0 and all(a + la == b for (a, la), (b, _) in zip(covered, covered[1:])) \
+                and covered[-1][0] + covered[-1][1] == size
+            identical = not bad and contiguous
+            if not identical:
+                identical = {"identical": False, "ranks_differing": bad, "slices_cover_the_file": contiguous}
+            del d_spi
+            torch.cuda.empty_cache()
+        check_s = round(time.time() - t_c, 1)
+        dist.barrier()
+    else:
+        plan.close()
+    if shared_gpu:
+        _native.debug_set("frame_ticket", None)
     slot = 16
     from sparkey.sharded import parse_log_header
     cap = 1 | int(parse_log_header(header)["num_puts"] * 1.3)
     ms_per_step = elapsed * 1000.0 / args.steps
     b_alg_per_gpu = ((file_len - 84) + 112 + slot * cap) / world
     achieved = b_alg_per_gpu / (ms_per_step * 1e-3) / 1e9
-    plan.close()
+    c4 = n_total == 1_000_000_000 and not churn
     return {
         "value": n_total * args.steps / elapsed, "ms_per_step": ms_per_step,
         "config": {"workload": (f"churn: {args.entries} records per GPU x {world} GPUs = {n_total} (keys from a pool "
                                 f"of 0.8 n, 10% DELETEs) in ONE index, sharded exact path" if churn else
+                                ("C4: " if c4 else "") +
                                 f"C2 shape, {args.entries} PUTs per GPU x {world} GPUs = {n_total} in ONE index "
                                 "(16 B key, 100 B value, NONE, IN_MEMORY)"),
                    "entries": n_total, "entries_per_gpu": args.entries, "log_bytes": file_len, "capacity": cap,
                    "spi_bytes": 112 + slot * cap,
-                   "parallelism": f"log byte-range sharded x{world}, RCCL all_to_all of (hash, address) entries",
+                   "parallelism": f"log byte-range sharded x{world}, " +
+                   ("gloo on host buffers, every rank on one GPU (rehearsal)" if shared_gpu else
+                    "RCCL all_to_all of (hash, address) entries"),
                    "orchestrator": "C++ sparkey_shard_build (C-ABI)" if args.orchestrator == "cpp"
                    else "Python ShardedBuilder"},
         "roofline": {"bound": "hbm", "kernel": "whole sharded build per GPU", "achieved": achieved,
-                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                     "traffic": pmc_traffic(f"sharded_rank_{args.entries}", "build"),
                      "algorithmic_bytes_per_launch": b_alg_per_gpu, "avg_launch_ms": ms_per_step},
         "phase_ms_rank0": {k: v / args.steps for k, v in phases.items()},
         "bit_identical_to_single_gpu": identical,
+        "check_s": check_s,
         "cpu_baseline": None,
         "gen_s": gen_s,
         "version": sparkey.version(),
@@ -594,7 +747,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--entries", type=int, default=10_000_000)
+    ap.add_argument("--entries", type=int, default=None,
+                    help="records (per GPU at N > 1); default 10M at N = 1 (C2), 125M per GPU at N > 1 (C4 at N = 8), "
+                         "1B for --workload c4")
     ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS),
                     help="c2 (the headline metric); c3 / c5 / churn are extra single-GPU measurements")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -604,12 +759,15 @@ def main():
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--backend", default="nccl", help="nccl (RCCL); gloo only to rehearse N > 1 ranks on one GPU")
     ap.add_argument("--sharded", action="store_true", help="the sharded build even at N = 1 (rehearsal)")
-    ap.add_argument("--check", action="store_true", help="sharded: compare the .spi with a single-GPU build")
+    ap.add_argument("--no-check", action="store_true",
+                    help="sharded: skip comparing the .spi with a single-GPU build (done after the timed region)")
     ap.add_argument("--orchestrator", default="cpp", choices=["cpp", "python"],
                     help="sharded: the C-ABI's sparkey_shard_build (C++) or sparkey/sharded.py over torch.distributed")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.entries is None:
+        args.entries = 1_000_000_000 if args.workload == "c4" else (125_000_000 if world > 1 else 10_000_000)
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if args.backend == "gloo":
@@ -628,6 +786,8 @@ def main():
         r = lookups(args, dev)
     elif args.workload == "append":
         r = appends(args, dev)
+    elif args.workload == "c4":
+        r = single_gpu_c4(args, dev)
     else:
         r = single_gpu(args, dev)
     if rank == 0:

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define SPARKEY_GPU_ABI_VERSION 2
+#define SPARKEY_GPU_ABI_VERSION 3
 
 /* Error codes -> the reference's exception (see INTEGRATION.md for the JNI mapping). */
 #define SPARKEY_OK 0
@@ -143,6 +143,19 @@ int sparkey_log_append(sparkey_plan* plan, uint8_t* header84, const uint8_t* d_k
                        const uint64_t* d_key_off, const uint8_t* d_values, const uint64_t* d_val_off, uint64_t n,
                        uint8_t* d_out, uint64_t out_cap, uint64_t* bytes_written, void* stream, char* err,
                        size_t err_len);
+
+/* Batched HashType.hash (HashType.java:44-46, 70-72: MurmurHash3 x86_32 for hash_size 4, x64_128 -> h1 for
+ * hash_size 8, MurmurHash3.java:18-201) of n keys resident in device memory: key i is
+ * d_keys[d_key_off[i] .. d_key_off[i + 1]); d_hash[i] = its hash (4-byte hashes zero-extended).  With
+ * capacity > 0 and d_slot non-NULL, d_slot[i] = IndexHash.getWantedSlot = Long.remainderUnsigned(hash,
+ * capacity) (IndexHash.java:667-669).  These are the device functions every build kernel hashes with. */
+int sparkey_hash_batch(sparkey_plan* plan, const uint8_t* d_keys, const uint64_t* d_key_off, uint64_t n,
+                       int32_t hash_size, int32_t hash_seed, uint64_t capacity, uint64_t* d_hash, uint64_t* d_slot,
+                       void* stream, char* err, size_t err_len);
+/* d_slot[i] = Long.remainderUnsigned(d_hash[i], capacity) (IndexHash.java:667-669), capacity >= 1, by the
+ * build kernels' multiply-high remainder. */
+int sparkey_wanted_slot_batch(sparkey_plan* plan, const uint64_t* d_hash, uint64_t n, uint64_t capacity,
+                              uint64_t* d_slot, void* stream, char* err, size_t err_len);
 
 /* Batched IndexHash.get (IndexHash.java:398-452) against a built index and its log, both resident in
  * device memory: query i is the key d_keys[d_key_off[i] .. d_key_off[i + 1]); d_value_pos[i] = the log
@@ -307,6 +320,19 @@ int sparkey_shard_comm_unique_id(uint8_t* id_out /* 128 bytes */, char* err, siz
 /* RCCL communicator of rank `rank` of `world` on `device` (collective: every rank calls it). */
 int sparkey_shard_comm_create(sparkey_shard_comm** comm_out, const uint8_t* id, int32_t rank, int32_t world,
                               int32_t device, char* err, size_t err_len);
+/* Collectives supplied by the host program instead of RCCL (e.g. the JVM's own transport, or gloo to
+ * rehearse several ranks that share one GPU).  The library stages every device buffer through pinned
+ * host memory and calls these on the rank's thread; each returns 0 on success.
+ *   all_gather: every rank's `bytes` bytes at `send` -> `recv` (world * bytes, in rank order)
+ *   all_to_all: send_bytes[r] bytes to rank r from consecutive runs of `send` in rank order;
+ *               recv_bytes[r] bytes from rank r into consecutive runs of `recv` in rank order */
+typedef struct sparkey_shard_transport {
+  void* ctx;
+  int (*all_gather)(void* ctx, const void* send, void* recv, uint64_t bytes);
+  int (*all_to_all)(void* ctx, const void* send, const uint64_t* send_bytes, void* recv, const uint64_t* recv_bytes);
+} sparkey_shard_transport;
+int sparkey_shard_comm_create_host(sparkey_shard_comm** comm_out, const sparkey_shard_transport* transport,
+                                   int32_t rank, int32_t world, int32_t device, char* err, size_t err_len);
 void sparkey_shard_comm_destroy(sparkey_shard_comm* comm);
 /* What rank `rank` must hold of the log (global bytes [*buf_lo, *buf_hi), buf_lo 4 KiB aligned) and the
  * part of the .spi it produces (bytes [*out_off, *out_off + *out_len) of the file: rank 0 the header and
@@ -322,6 +348,15 @@ int sparkey_shard_build(sparkey_plan* plan, sparkey_shard_comm* comm, const uint
                         const uint8_t* d_buf, uint64_t buf_lo, uint64_t buf_hi, const sparkey_build_opts* opts,
                         uint8_t* d_out, uint64_t out_cap, void* stream, sparkey_build_stats* stats_out, char* err,
                         size_t err_len);
+/* The multi-GPU build with the log already in device memory: opts->num_gpus ranks as threads of this
+ * process (devices opts->device .. + num_gpus - 1, RCCL between them; the shard_transport switch can put
+ * them all on opts->device).  d_bufs[r] holds global log bytes [buf_lo, buf_hi) of rank r and d_outs[r]
+ * receives bytes [out_off, out_off + out_len) of the .spi, both as sparkey_shard_geometry gives them for
+ * (rank r, num_gpus); log_header is a host copy of the first 84 bytes, file_len the log's length.  The
+ * buffers may alias one full log and one full .spi.  stats_out: the whole index's header fields. */
+int sparkey_build_index_sharded_device(const uint8_t* log_header, uint64_t file_len, const uint8_t* const* d_bufs,
+                                       uint8_t* const* d_outs, const sparkey_build_opts* opts,
+                                       sparkey_build_stats* stats_out, char* err, size_t err_len);
 /* Host wall time per phase of the last sparkey_shard_build on this communicator. */
 int32_t sparkey_shard_phase_count(const sparkey_shard_comm* comm);
 const char* sparkey_shard_phase_name(const sparkey_shard_comm* comm, int32_t i);
@@ -334,6 +369,15 @@ double sparkey_multi_phase_ms(int32_t rank, int32_t i);
 
 const char* sparkey_gpu_version(void);
 const char* sparkey_strerror(int code);
+
+/* ---- test and diagnostic switches (csrc/knobs.hpp) ----
+ * No switch changes the bytes of a build; each forces a device path or geometry the default choice
+ * would not take (e.g. "no_uniform", "serial_framing", "shard_transport").  value < 0 unsets.  Process
+ * wide; set them only while no build runs.  SPARKEY_DEBUG="name=value,..." in the environment sets
+ * them once at the first read.  Returns SPARKEY_E_ARG for an unknown name. */
+int sparkey_debug_set(const char* name, int64_t value);
+/* The switch's value, -1 when unset, SPARKEY_E_ARG for an unknown name. */
+int64_t sparkey_debug_get(const char* name);
 
 #ifdef __cplusplus
 }

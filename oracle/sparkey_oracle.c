@@ -683,11 +683,14 @@ static int32_t next_record(const build_ctx* c, int64_t* pos, int64_t end, int64_
   r->entry_index = *entry_index;
   int64_t p = *pos;
   int32_t first, second, rc;
-  if (p >= c->log_len) return 0;                                         /* EOF on first VLQ: stop */
-  /* EOF inside the header VLQs: EOFException, wrapped in RuntimeException by hasNext
-   * (SparkeyLogIterator.java:117,134-136) */
+  /* EOF anywhere inside the first VLQ (its first byte, or after a continuation byte): hasNext catches
+   * the EOFException of that read and ends the iteration without an error (SparkeyLogIterator.java:
+   * 111-115).  "Too long VLQ value" there is a RuntimeException, not caught (Util.java:217). */
   rc = oracle_vlq_read(c->log, c->log_len, &p, &first);
-  if (rc) return rc == ORACLE_E_CORRUPT_LOG ? ORACLE_E_CORRUPT_RECORD : rc;
+  if (rc == ORACLE_E_CORRUPT_LOG) return 0;
+  if (rc) return rc;
+  /* EOF inside the second VLQ: EOFException, wrapped in RuntimeException by hasNext
+   * (SparkeyLogIterator.java:117,134-136) */
   rc = oracle_vlq_read(c->log, c->log_len, &p, &second);
   if (rc) return rc == ORACLE_E_CORRUPT_LOG ? ORACLE_E_CORRUPT_RECORD : rc;
   if (first == 0) { r->is_put = 0; r->key_len = second; r->value_len = 0; }

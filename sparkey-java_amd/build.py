@@ -11,10 +11,13 @@ ROOT = os.path.dirname(HERE)
 LIB_DIR = os.path.join(HERE, "lib")
 LIB = os.path.join(LIB_DIR, "libsparkey_gpu.so")
 OBJ_DIR = os.path.join(HERE, "build", "obj")
-SOURCES = [os.path.join(HERE, "csrc", f) for f in ("build_kernels.hip", "fused_kernels.hip", "frame2_kernels.hip", "frame3_kernels.hip", "frame_lane_kernels.hip", "exact_kernels.hip", "shard_kernels.hip", "shard_exact_kernels.hip",
-                                                      "lookup_kernels.hip", "append_kernels.hip", "snappy_kernels.hip", "zstd_kernels.hip", "sparkey_gpu.cpp", "file_build.cpp", "shard_host.cpp")]
-HEADERS = [os.path.join(HERE, "csrc", f) for f in ("snappy.hpp", "frame_common.hpp", "build_kernels.hpp", "device_common.hpp", "kernel_utils.hpp", "scan.hpp", "place_common.hpp",
-                                                      "lookup.hpp", "append.hpp", "shard_host.hpp")] + [
+SOURCES = [os.path.join(HERE, "csrc", f) for f in (
+    "build_kernels.hip", "fused_kernels.hip", "frame3_kernels.hip", "exact_kernels.hip", "shard_kernels.hip",
+    "shard_exact_kernels.hip", "lookup_kernels.hip", "append_kernels.hip", "snappy_kernels.hip", "zstd_kernels.hip",
+    "sparkey_gpu.cpp", "file_build.cpp", "shard_host.cpp", "knobs.cpp")]
+HEADERS = [os.path.join(HERE, "csrc", f) for f in (
+    "snappy.hpp", "frame_common.hpp", "build_kernels.hpp", "device_common.hpp", "kernel_utils.hpp", "scan.hpp",
+    "place_common.hpp", "lookup.hpp", "append.hpp", "shard_host.hpp", "knobs.hpp")] + [
     os.path.join(ROOT, "include", "sparkey_gpu.h")]
 ARCH = os.environ.get("SPARKEY_GPU_ARCH", "gfx950")
 

@@ -1,6 +1,6 @@
 // build_kernels.hip -- gfx950 kernels of the Sparkey .spi build (IndexHash.createNew on MI355X).
 //
-// The fast path lives in fused_kernels.hip (k_frame, radix partition, k_place_lds).  This file
+// The fast path lives in fused_kernels.hip (k_frame, radix partition, k_place_reg).  This file
 // holds the exact fallbacks and the shared stages:
 //   k_walk(serial)  one thread walks the whole record chain (SparkeyLogIterator.java:86-138) when
 //                   speculative framing disagreed with the verified chain (inconsistent headers).
@@ -53,8 +53,17 @@ __global__ void k_walk(BuildParams P, int serial) {
       em = chunk_end(P.ch_k0 + m, P.data_end);
     }
     const RecHdr h = decode_header(at, p, (int64_t)P.log_len);
+    if (h.rc == kEndOfLog) {  // EOF inside the first VLQ: the iteration ends here, no error
+      P.cnt[m] = c;
+      for (m++; m < nc; m++) {
+        P.G[m] = p;
+        P.cnt[m] = 0;
+      }
+      if (serial) P.st->exit = P.data_end;
+      return;
+    }
     if (!header_valid(h, p, P.max_key_len, (int64_t)P.log_len)) {
-      set_error(P.st, p, h.rc ? h.rc : kErrCorruptRecord);
+      set_error(P.st, p, header_error(h));
       for (; m < nc; m++) P.cnt[m] = 0;
       return;
     }
@@ -88,8 +97,9 @@ __global__ __launch_bounds__(64) void k_emit(BuildParams P) {
     bool bad = false;
     while (p < e) {
       const RecHdr h = decode_header(at, p, (int64_t)P.log_len);
+      if (h.rc == kEndOfLog) break;  // the iteration ends (k_walk ended the chain at the same byte)
       if (!header_valid(h, p, P.max_key_len, (int64_t)P.log_len)) {
-        set_error(P.st, p, h.rc ? h.rc : kErrCorruptRecord);
+        set_error(P.st, p, header_error(h));
         bad = true;
         break;
       }
@@ -192,7 +202,7 @@ __global__ void k_carry(BuildParams P) {
   P.carry[b] = max(pre.c, x0 + pre.a);
 }
 
-// Global-memory placement of every bucket (buckets too big for k_place_lds), or, with
+// Global-memory placement of every bucket (buckets too big for k_place_reg), or, with
 // sort_only, the (wantedSlot, address) order of every bucket into ent3 for the SORTING restatement.
 __global__ __launch_bounds__(kPlaceBlock) void k_place(BuildParams P, int sort_only, int only_big) {
   __shared__ uint32_t cnt[kBucket];
@@ -324,7 +334,7 @@ __global__ __launch_bounds__(1024) void k_stats_final(BuildParams P, uint32_t np
   }
 }
 
-// The folded stats (k_place_lds fold_stats): every block left the sums over the slot range it wrote
+// The folded stats (k_place_reg fold_stats): every block left the sums over the slot range it wrote
 // and where that range starts; the ranges tile the ring, so the only pairs left are each range's
 // first slot with the slot before it.  One thread per bucket; the last block to finish (ticket)
 // writes the header.
@@ -340,7 +350,7 @@ __global__ __launch_bounds__(kStatFoldBlock) void k_stats_folded(BuildParams P) 
     for (uint64_t i = (uint64_t)blockIdx.x * kStatFoldBlock + tid; i < np; i += (uint64_t)gridDim.x * kStatFoldBlock)
       verify_pair(P, i);
   }
-  if (st->big_buckets || st->full) {  // some slots were placed outside k_place_lds: k_stats runs
+  if (st->big_buckets || st->full) {  // some slots were placed outside k_place_reg: k_stats runs
     if (tid == 0) st->stats_pending = 1u;
     return;
   }
@@ -383,7 +393,7 @@ __global__ __launch_bounds__(kStatFoldBlock) void k_stats_folded(BuildParams P) 
 
 // The folded stats of a sharded rank (after its spilled-in slots were written).  Every entry's
 // displacement was summed by the rank that placed it (max and sum are global); the adjacent pairs
-// (s - 1, s) with s in (slot_lo, slot_hi) are: inside one block's written range (k_place_lds counted
+// (s - 1, s) with s in (slot_lo, slot_hi) are: inside one block's written range (k_place_reg counted
 // those whose s this rank owns), at the start gs of a block of this rank other than b_lo (read here),
 // or in the spilled-in run [slot_lo, slot_lo + carry[b_lo]] (read here by block 0).  The pair at
 // slot_lo and the wrap quirk are the host's (sharded.py), as with k_stats.
@@ -393,7 +403,7 @@ __global__ __launch_bounds__(kStatFoldBlock) void k_stats_folded_shard(BuildPara
   if (build_aborted(P)) return;
   Status* st = P.st;
   const int tid = threadIdx.x;
-  if (st->big_buckets || st->full) {  // some slots were placed outside k_place_lds: k_stats runs
+  if (st->big_buckets || st->full) {  // some slots were placed outside k_place_reg: k_stats runs
     if (tid == 0) st->stats_pending = 1u;
     return;
   }

@@ -16,8 +16,6 @@ constexpr int kEmitExtra = 1024 + 16;             // bytes staged past a chunk f
 constexpr int kBucketShift = 10;                  // placement bucket: 1024 slots
 constexpr int kBucket = 1 << kBucketShift;
 constexpr int kPlaceBlock = 256;
-constexpr int kPlaceLdsBlock = 512;              // k_place_lds: one bucket per workgroup
-constexpr int kLdsBins = kBucket / kPlaceLdsBlock;
 constexpr int kBinsPerThread = kBucket / kPlaceBlock;
 constexpr uint32_t kGroupMax = 64;                // equal-wanted-slot group sorted by insertion
 constexpr int kScanBlock = 256;
@@ -159,7 +157,7 @@ struct BuildParams {
   MaxPlus* bfun_total;
   // fused_carry (single GPU, k_part2s in one pass): k_part2s leaves bpre = each bucket's exclusive
   // prefix function inside its digit and dfun = each digit's composed function; its last block
-  // composes the 256 digits around the ring into dcarry (each digit's carry-in), and k_place_lds
+  // composes the 256 digits around the ring into dcarry (each digit's carry-in), and k_place_reg
   // takes carry = bpre[b](dcarry[digit]) -- no k_summary / scan / k_carry launches
   MaxPlus* dfun;         // (as 256 packed words, see part2_fused_carry)
   int64_t* dcarry;
@@ -169,8 +167,7 @@ struct BuildParams {
   uint64_t* pairs;
   uint64_t pair_cap;
   StatPart* parts;
-  unsigned long long* place_dbg;  // SPARKEY_PLACE_DEBUG: k_place_lds phase cycles summed over blocks
-  unsigned long long* part_dbg;   // SPARKEY_PART2_DEBUG: k_part2s phase cycles, 8 words per digit
+  unsigned long long* part_dbg;   // part2_debug switch: k_part2s phase cycles, 8 words per digit
   uint64_t* scan_scratch_u64;
   MaxPlus* scan_scratch_mp;
   // k_frame granules (zeroed before every launch)
@@ -194,7 +191,7 @@ struct BuildParams {
   uint32_t p2_nsrc, p2_d0, p2_nd;
   uint32_t bpp;       // buckets per coarse digit: digit = bucket / bpp (< 256), computed as
   uint64_t dmagic;    // (bucket * dmagic) >> 40, dmagic = ceil(2^40 / bpp), exact for bpp < 2^18
-  unsigned long long* dbg;  // diagnostic phase counters (SPARKEY_FRAME_DEBUG=1), else null
+  unsigned long long* dbg;  // diagnostic phase counters (frame_debug switch), else null
   // k_frame geometry (chunk C = 2^fr_cshift bytes, fr_w chunks per wave)
   int32_t fr_cshift;
   int32_t fr_w;
@@ -205,30 +202,27 @@ struct BuildParams {
   int32_t fr_fast;  // maxKeyLen + 1 < 128 and maxValueLen < 128: canonical headers are 2 bytes
   int32_t no_deletes;  // the log header counts no DELETE: speculation treats 0x00 as no record start
   uint64_t fr_nchunks;
-  // k_frame2 (frame2_kernels.hip): segments of 2^fr_cshift bytes, fr_w per wave, f2_lcap listed record
-  // starts per segment, f2_rgn_bytes staged per wave
-  int32_t f2_lcap;
-  int32_t f2_rgn_bytes;
   int32_t f3_short;  // k_frame3 (frame3_kernels.hip): steps of the short walk
   int32_t f3_cover;  // k_frame3: mark the starts the short walk reached (windows hold several true starts)
-  int32_t f3_stop;   // SPARKEY_FRAME3_STOP: k_frame3 gives up after this phase (instruction counts by phase)
+  int32_t f3_stop;   // frame3_stop switch: k_frame3 gives up after this phase (instruction counts by phase)
   int32_t f3_rgn;    // k_frame3: staged region bytes per wave (W * C + fr_look + 16, 16-byte multiple)
   int32_t f3_cand_cap;  // k_frame3: candidates (and records) per wave its LDS list holds (<= 512)
   int32_t f3_surv_cap;  // k_frame3: chain heads per wave after the short walk (<= 64, one long walk per lane)
-  int32_t f3_noticket;  // k_frame3: regions by workgroup id, not by ticket (SPARKEY_FRAME3_TICKET: 0)
+  int32_t fr_ticket;    // k_frame / k_frame3: regions by device-wide ticket, not by workgroup id (builds that
+                        // share the device, or the frame_ticket switch)
   // uniform-stride framing (k_frame_uniform): uni_n records of uni_rec bytes from fr_entry
   uint64_t uni_n;
   int64_t uni_rec;
   uint32_t uni_wbytes;    // LDS staging bytes per wave (set by the launcher)
   uint32_t uni_hist_off;  // LDS offset of the digit counts (set by the launcher)
-  uint32_t uni_nt;        // framing kernels: non-temporal LDS-DMA of the log (SPARKEY_FRAME_NO_NT: default policy)
+  uint32_t uni_nt;        // framing kernels: non-temporal LDS-DMA of the log (read once)
   // k_frame_uniform as partition pass 1: digit d's entries at ent3[d * p1_region, + p1_fill[d])
   uint64_t p1_region;   // 0 = off
   int32_t p1_kernel;    // with p1_region: k_part1_regions fills the regions from the slabs (else the framing did)
   int32_t p1_pad;
   int32_t p2_sorted;    // k_part2s: per-(bucket, slot) counts in the same pass + the carry functions
   int32_t p2_fixed;     // k_part2s in one pass: bucket b's entries at ent2[b * kPlaceLdsMax, + bcount[b])
-  int32_t fold_stats;   // k_place_lds leaves calculateMaxDisplacement's per-bucket parts (no k_stats pass)
+  int32_t fold_stats;   // k_place_reg leaves calculateMaxDisplacement's per-bucket parts (no k_stats pass)
   int32_t stats_if_pending;  // k_stats / k_stats_final only when the folded stats left stats_pending
   uint64_t* bstat_start;  // fold_stats: per bucket, the first slot of the range it wrote (~0: none)
   uint32_t* p1_fill;
@@ -300,15 +294,12 @@ void launch_partition1(const BuildParams& P, hipStream_t s);
 void launch_partition2(const BuildParams& P, hipStream_t s, StageTimer* tm);
 void launch_dense_slabs(const BuildParams& P, hipStream_t s);
 void launch_frame_uniform(const BuildParams& P, hipStream_t s, StageTimer* tm);
-void launch_frame2(const BuildParams& P, hipStream_t s, StageTimer* tm);  // frame2_kernels.hip
 void launch_frame3(const BuildParams& P, hipStream_t s, StageTimer* tm);  // frame3_kernels.hip
 bool frame3_fits(BuildParams& P, double mean_record, double pass);
-void launch_frame_lane(const BuildParams& P, hipStream_t s, StageTimer* tm);  // frame_lane_kernels.hip
-bool frame_lane_supported(const BuildParams& P);
 uint32_t frame3_lds_per_wave(const BuildParams& P);
-// framing paths: 0 k_frame, 1 serial walk, 2 k_frame_uniform, 3 k_frame2, 4 k_frame3; the
-// speculative ones with per-wave slabs
-__host__ __device__ inline bool slab_framing(int path) { return path == 0 || path == 3 || path == 4 || path == 5; }
+// framing paths: 0 k_frame, 1 serial walk, 2 k_frame_uniform, 4 k_frame3 (3 and 5 were the k_frame2 and
+// k_frame_lane experiments, measured slower and removed); the speculative ones with per-wave slabs
+__host__ __device__ inline bool slab_framing(int path) { return path == 0 || path == 4; }
 void launch_place_fast(const BuildParams& P, hipStream_t s, StageTimer* tm);
 void launch_place_buckets(const BuildParams& P, hipStream_t s);
 // fallbacks and shared stages (build_kernels.hip)

@@ -20,11 +20,15 @@ constexpr int kErrNoFreeSlots = -4;
 constexpr int kErrCorruptData = -5;
 constexpr int kErrVlq = -6;
 constexpr int kErrCorruptRecord = -13;  // SPARKEY_E_CORRUPT_RECORD: the iterator cannot read a record
+// RecHdr.rc of a record whose first VLQ runs into the end of the file: SparkeyLogIterator.hasNext
+// catches that EOFException and ends the iteration without an error (SparkeyLogIterator.java:111-115).
+constexpr int kEndOfLog = 1;
 
 // ---------------------------------------------------------------------------------------------
 // wantedSlot = Long.remainderUnsigned(hash, capacity)   (IndexHash.java:667-669)
 // q = mulhi(x, floor(2^64 / cap)) is floor(x / cap) or one less, so one conditional subtract
-// gives the exact remainder (checked exhaustively against '%' in tests/test_fastmod.py).
+// gives the exact remainder (tests/test_fastmod.py checks it against '%' on the host -- boundary values,
+// random hashes, the BASELINE capacities and every odd capacity below 4096 -- and on the device).
 // ---------------------------------------------------------------------------------------------
 // A table window (the sharded exact path's range-local replay) sets `base`: slots
 // are then numbered from `base` around the ring, local = (wanted - base) mod cap.
@@ -175,7 +179,7 @@ __device__ __forceinline__ uint64_t key_hash(int hash_size, P key, int32_t len, 
 // (SparkeyLogIterator.java:86-138).
 // ---------------------------------------------------------------------------------------------
 struct RecHdr {
-  int32_t rc;     // 0 ok, kErrVlq, kErrCorruptRecord (EOF inside the header)
+  int32_t rc;     // 0 ok, kErrVlq, kErrCorruptRecord (EOF inside the second VLQ), kEndOfLog (EOF inside the first)
   int32_t put;    // 1 PUT, 0 DELETE
   int32_t hlen;   // header bytes
   int32_t klen;   // Java int (may be negative on corrupt input)
@@ -204,7 +208,10 @@ __device__ __forceinline__ RecHdr decode_header(At at, int64_t p, int64_t avail)
   h.rc = 0;
   int64_t q = p;
   const int32_t first = read_vlq(at, q, avail, h.rc);
-  if (h.rc) return h;
+  if (h.rc) {
+    if (h.rc == kErrCorruptRecord) h.rc = kEndOfLog;
+    return h;
+  }
   const int32_t second = read_vlq(at, q, avail, h.rc);
   if (h.rc) return h;
   h.hlen = (int32_t)(q - p);
@@ -212,6 +219,10 @@ __device__ __forceinline__ RecHdr decode_header(At at, int64_t p, int64_t avail)
   else { h.put = 1; h.klen = first - 1; h.vlen = second; }
   return h;
 }
+
+// The error code of a record header the iterator rejects (kEndOfLog ends the chain instead, where the
+// caller walks the verified chain; anywhere else it is a corrupt record).
+__device__ __forceinline__ int32_t header_error(const RecHdr& h) { return h.rc < 0 ? h.rc : kErrCorruptRecord; }
 
 // What the reference's iterator accepts on the real record chain (else it throws):
 // key fits its keyBuf of maxKeyLen bytes and lies inside the file.

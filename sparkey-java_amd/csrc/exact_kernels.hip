@@ -183,12 +183,12 @@ __device__ int replay_put(Replay<Tab>& r, uint64_t hash, uint64_t address, uint3
     if (might && hash == hash2) {  // same hash: same key?  (IndexHash.java:606-636)
       if (!have_mine) {
         mine = r.tab.rec(my_id, my_addr);
-        if (mine.rc) return mine.rc;
+        if (mine.rc) return header_error(mine);
         if (!mine.put) return kErrCorruptData;
         have_mine = true;
       }
       const RecHdr other = r.tab.rec(id2, address2);
-      if (other.rc) return other.rc;
+      if (other.rc) return header_error(other);
       if (!other.put) return kErrCorruptData;  // "Invalid data - reference to delete entry"
       if (mine.klen == other.klen && r.tab.same_key(my_id, mine, my_addr, id2, other, address2)) {
         r.tab.set(slot, hash, address, wanted, id);  // replace in place
@@ -229,12 +229,12 @@ __device__ int replay_delete(Replay<Tab>& r, uint64_t hash, uint64_t address, ui
     if (hash == hash2) {
       if (!have_mine) {
         mine = r.tab.rec(id, address);
-        if (mine.rc) return mine.rc;
+        if (mine.rc) return header_error(mine);
         if (mine.put) return kErrCorruptData;
         have_mine = true;
       }
       const RecHdr other = r.tab.rec(id2, address2);
-      if (other.rc) return other.rc;
+      if (other.rc) return header_error(other);
       if (!other.put) return kErrCorruptData;
       if (mine.klen == other.klen && r.tab.same_key(id, mine, address, id2, other, address2)) {
         for (int64_t g2 = 0; g2 < cap; g2++) {  // backward shift, IndexHash.java:503-524
@@ -615,9 +615,9 @@ __device__ int wave_put(const BuildParams& P, SegLds<CAP, KEYB>& L, const Entry&
           if (might && o.h == C.h) {
             const RecHdr& mine = L.rec(P, C.id);
             const RecHdr& other = L.rec(P, o.id);
-            if (mine.rc) e_rc = mine.rc;
+            if (mine.rc) e_rc = header_error(mine);
             else if (!mine.put) e_rc = kErrCorruptData;
-            else if (other.rc) e_rc = other.rc;
+            else if (other.rc) e_rc = header_error(other);
             else if (!other.put) e_rc = kErrCorruptData;
             if (e_rc) ev = 2;
             else if (mine.klen == other.klen && L.same_key(P, C.id, o.id)) ev = 3;
@@ -721,9 +721,9 @@ __device__ int wave_delete(const BuildParams& P, SegLds<CAP, KEYB>& L, const Ent
         if (o.h == h) {
           const RecHdr& mine = L.rec(P, id);
           const RecHdr& other = L.rec(P, o.id);
-          if (mine.rc) e_rc = mine.rc;
+          if (mine.rc) e_rc = header_error(mine);
           else if (mine.put) e_rc = kErrCorruptData;
-          else if (other.rc) e_rc = other.rc;
+          else if (other.rc) e_rc = header_error(other);
           else if (!other.put) e_rc = kErrCorruptData;
           if (e_rc) ev = 2;
           else if (mine.klen == other.klen && L.same_key(P, id, o.id)) ev = 3;

@@ -32,7 +32,11 @@
 #include <vector>
 
 #include "../../include/sparkey_gpu.h"
+#include "knobs.hpp"
 #include "shard_host.hpp"
+
+using sk::Knob;
+using sk::knob;
 
 // Phases of the calling thread's last sparkey_build_index_file (sparkey_file_last_phases).
 thread_local double t_file_phase[5] = {0, 0, 0, 0, 0};
@@ -170,7 +174,7 @@ struct FileCtx {
     if (sched_getaffinity(0, sizeof(cs), &cs) == 0) hc = (unsigned)CPU_COUNT(&cs);
     if (!hc) hc = std::thread::hardware_concurrency();
     int nt = (int)std::min<unsigned>(16u, hc ? hc : 4u) - 1;  // the calling thread works too
-    if (const char* v = getenv("SPARKEY_FILE_THREADS")) nt = std::max(0, atoi(v) - 1);
+    if (sk::knob_set(sk::Knob::FileThreads)) nt = (int)std::max<int64_t>(0, sk::knob(sk::Knob::FileThreads) - 1);
     pool = new WorkerPool(std::max(0, nt));
     return SPARKEY_OK;
   }
@@ -285,14 +289,8 @@ bool pool_pread(FileCtx* c, int fd, uint8_t* buf, uint64_t off, uint64_t len, in
 
 // Buffered writes to one file serialize on its inode lock: on the GPU box (overlayfs) one thread
 // writes a new 208 MB file at 8.5 GB/s and 2-32 threads at 7.0-8.0 (tools/io_probe.c,
-// DESIGN.md §5), so the index goes out from the calling thread unless SPARKEY_FILE_WRITE_THREADS > 1.
-int write_threads() {
-  static const int n = [] {
-    const char* v = getenv("SPARKEY_FILE_WRITE_THREADS");
-    return v ? std::max(1, atoi(v)) : 1;
-  }();
-  return n;
-}
+// DESIGN.md §5), so the index goes out from the calling thread unless the file_write_threads switch > 1.
+int write_threads() { return (int)std::max<int64_t>(1, sk::knob(sk::Knob::FileWriteThreads)); }
 
 bool pool_pwrite(FileCtx* c, int fd, const uint8_t* buf, uint64_t off, uint64_t len, int* err_no) {
   std::atomic<int> fail{0};
@@ -379,27 +377,34 @@ struct CtxHold {  // acquire_ctx / release_ctx around one rank's work
 };
 
 // One rank of a multi-GPU build (opts.num_gpus > 1): its log bytes in through `load`, the sharded build,
-// its part of the .spi out through `store`.  Runs on the rank's own thread (shard_run_threads).
+// its part of the .spi out through `store`.  Runs on the rank's own thread (shard_run_threads).  A rank
+// whose context or load fails still enters the build with that code, so every rank returns it
+// (shard_build_rank) instead of the others waiting for this one in a collective.
 template <class Load, class Store>
-int shard_rank(int rank, int world, int device, sparkey_shard_comm* comm, const uint8_t* hdr, uint64_t log_len,
-               const sparkey_build_opts* opts, sparkey_build_stats* stats_out, char* err, size_t err_len, Load&& load,
-               Store&& store) {
-  uint64_t blo, bhi, ooff, olen;
+int shard_rank(int rank, int world, int device, sparkey_shard_comm* comm, bool shared_device, const uint8_t* hdr,
+               uint64_t log_len, const sparkey_build_opts* opts, sparkey_build_stats* stats_out, char* err,
+               size_t err_len, Load&& load, Store&& store) {
+  uint64_t blo = 0, bhi = 0, ooff = 0, olen = 0;
   int rc = sparkey_shard_geometry(hdr, log_len, opts, rank, world, &blo, &bhi, &ooff, &olen, err, err_len);
-  if (rc) return rc;
+  if (rc) return rc;  // (the same on every rank: they all return here)
   CtxHold h;
   h.c = acquire_ctx(device, err, err_len, &rc);
-  if (!h.c) return rc;
   FileCtx* c = h.c;
-  if (hipSetDevice(device) != hipSuccess) {
+  if (!rc && hipSetDevice(device) != hipSuccess) {
     set_err(err, err_len, "hipSetDevice failed");
-    return SPARKEY_E_GPU;
+    rc = SPARKEY_E_GPU;
   }
-  rc = c->reserve(bhi - blo + 16, olen, err, err_len);
+  if (!rc) rc = c->reserve(bhi - blo + 16, olen, err, err_len);
+  if (!rc && knob(Knob::ShardFailRank) == rank) {  // (tests: one rank fails on its own)
+    set_err(err, err_len, "rank " + std::to_string(rank) + ": injected load failure");
+    rc = SPARKEY_E_IO;
+  }
   if (!rc) rc = load(c, blo, bhi - blo);
+  if (c) sk_plan_set_shared_device(c->plan, shared_device);
   sparkey_build_stats st;
-  if (!rc) rc = sparkey_shard_build(c->plan, comm, hdr, log_len, c->d_log, blo, bhi, opts, c->d_out, olen, c->s, &st, err,
-                                    err_len);
+  rc = shard_build_rank(c ? c->plan : nullptr, comm, hdr, log_len, c ? c->d_log : nullptr, blo, bhi, opts,
+                        c ? c->d_out : nullptr, olen, c ? (void*)c->s : nullptr, &st, rc, err, err_len);
+  if (c) sk_plan_set_shared_device(c->plan, false);
   if (!rc) rc = store(c, ooff, olen);
   if (!rc && rank == 0 && stats_out) *stats_out = st;
   return rc;
@@ -415,7 +420,7 @@ int sparkey_build_index_file(const char* log_path, const char* index_out_path, c
     set_err(err, err_len, "null argument");
     return SPARKEY_E_ARG;
   }
-  const bool dbg = getenv("SPARKEY_FILE_DEBUG") != nullptr;
+  const bool dbg = sk::knob_on(sk::Knob::FileDebug);
   const double t0 = now_ms();
   const int fd = open(log_path, O_RDONLY);
   if (fd < 0) {
@@ -453,9 +458,10 @@ int sparkey_build_index_file(const char* log_path, const char* index_out_path, c
     rc = ftruncate(ofd, (off_t)isz) == 0 ? SPARKEY_OK : SPARKEY_E_IO;
     if (rc) set_err(err, err_len, std::string("cannot size the index file: ") + strerror(errno));
     if (!rc)
-      rc = shard_run_threads(*opts, [&](int rank, int world, int device, sparkey_shard_comm* comm, char* e, size_t el) {
+      rc = shard_run_threads(*opts, [&](int rank, int world, int device, sparkey_shard_comm* comm, bool same, char* e,
+                                        size_t el) {
         return shard_rank(
-            rank, world, device, comm, hdr, log_len, opts, stats_out, e, el,
+            rank, world, device, comm, same, hdr, log_len, opts, stats_out, e, el,
             [&](FileCtx* c, uint64_t lo, uint64_t n) { return read_log_range(c, fd, lo, n, e, el); },
             [&](FileCtx* c, uint64_t off, uint64_t n) { return write_index(c, ofd, n, e, el, off); });
       }, err, err_len);
@@ -544,9 +550,10 @@ int sparkey_build_index_mem(const uint8_t* log, uint64_t log_len, uint8_t* index
     return SPARKEY_E_BUFFER;
   }
   if (opts->num_gpus > 1)
-    return shard_run_threads(*opts, [&](int rank, int world, int device, sparkey_shard_comm* comm, char* e, size_t el) {
+    return shard_run_threads(*opts, [&](int rank, int world, int device, sparkey_shard_comm* comm, bool same, char* e,
+                                        size_t el) {
       return shard_rank(
-          rank, world, device, comm, log, log_len, opts, stats_out, e, el,
+          rank, world, device, comm, same, log, log_len, opts, stats_out, e, el,
           [&](FileCtx* c, uint64_t lo, uint64_t n) {
             if (hipMemcpyAsync(c->d_log, log + lo, n, hipMemcpyHostToDevice, c->s) != hipSuccess) {
               set_err(e, el, "H2D copy failed");
@@ -597,6 +604,45 @@ int sparkey_build_index_mem(const uint8_t* log, uint64_t log_len, uint8_t* index
     return SPARKEY_E_GPU;
   }
   return SPARKEY_OK;
+}
+
+// The multi-GPU build over device-resident log ranges (include/sparkey_gpu.h): every rank reads its
+// range in place and writes its part of the .spi in place.
+int sparkey_build_index_sharded_device(const uint8_t* log_header, uint64_t file_len, const uint8_t* const* d_bufs,
+                                       uint8_t* const* d_outs, const sparkey_build_opts* opts,
+                                       sparkey_build_stats* stats_out, char* err, size_t err_len) {
+  if (!log_header || !d_bufs || !d_outs || !opts || opts->num_gpus < 1) {
+    set_err(err, err_len, "null argument or num_gpus < 1");
+    return SPARKEY_E_ARG;
+  }
+  int rc = sk_check_log_header(log_header, 84, file_len, err, err_len);
+  if (rc) return rc;
+  sparkey_build_opts o = *opts;
+  o.num_gpus = std::max(1, opts->num_gpus);
+  return shard_run_threads(o, [&](int rank, int world, int device, sparkey_shard_comm* comm, bool same, char* e,
+                                  size_t el) {
+    uint64_t blo = 0, bhi = 0, ooff = 0, olen = 0;
+    int r = sparkey_shard_geometry(log_header, file_len, &o, rank, world, &blo, &bhi, &ooff, &olen, e, el);
+    if (r) return r;
+    CtxHold h;
+    h.c = acquire_ctx(device, e, el, &r);
+    FileCtx* c = h.c;
+    if (!r && hipSetDevice(device) != hipSuccess) {
+      set_err(e, el, "hipSetDevice failed");
+      r = SPARKEY_E_GPU;
+    }
+    if (!r && (!d_bufs[rank] || !d_outs[rank])) {
+      set_err(e, el, "null device buffer for rank " + std::to_string(rank));
+      r = SPARKEY_E_ARG;
+    }
+    if (c) sk_plan_set_shared_device(c->plan, same);
+    sparkey_build_stats st;
+    r = shard_build_rank(c ? c->plan : nullptr, comm, log_header, file_len, d_bufs[rank], blo, bhi, &o, d_outs[rank],
+                         olen, c ? (void*)c->s : nullptr, &st, r, e, el);
+    if (c) sk_plan_set_shared_device(c->plan, false);
+    if (!r && rank == 0 && stats_out) *stats_out = st;
+    return r;
+  }, err, err_len);
 }
 
 int32_t sparkey_file_last_phases(double* ms_out, int32_t n) {

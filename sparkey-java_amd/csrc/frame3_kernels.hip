@@ -571,42 +571,25 @@ __device__ __forceinline__ void frame3_region(const BuildParams& P, const uint64
   }
 }
 
-// NW waves per workgroup, one region each.  The waves share nothing, so the default is one wave per
-// workgroup: each region's LDS is freed as soon as its wave ends (4-wave workgroups averaged 2.8
-// resident waves per SIMD of the 4 their LDS allowed, SQ_WAVE_CYCLES / GRBM_GUI_ACTIVE).  Region i is
-// workgroup i: a wave spins on its predecessor's exit, which the in-order dispatch has started before
-// it (the spin is bounded all the same: the host redoes a framing whose wait ran out).  A ticket from
-// one device-wide counter per workgroup (SPARKEY_FRAME3_TICKET, as k_frame) serialises 168K atomics
-// per 10M C3 records: 1.98 ms with one-wave workgroups.  C3 10M on one box: one wave, no ticket
-// 0.746 ms; 4 waves, ticket 0.856; 4 waves, no ticket 0.834; 8 waves 1.27.
-// kF3WavesPerSimd waves (80 VGPRs) where a CU's LDS holds as many regions (frame3_fits).
-template <int NW>
-__global__ __launch_bounds__(64 * NW, kF3WavesPerSimd) void k_frame3(BuildParams P, uint32_t lds_per_wave) {
+// One wave per workgroup, one region each: the waves share nothing, and each region's LDS is freed
+// as soon as its wave ends (4-wave workgroups averaged 2.8 resident waves per SIMD of the 4 their
+// LDS allowed, SQ_WAVE_CYCLES / GRBM_GUI_ACTIVE).  Region i is workgroup i: a wave spins on its
+// predecessor's exit, which the in-order dispatch has started before it (the spin is bounded all the
+// same: the host redoes a framing whose wait ran out).  Builds that share the device take a ticket
+// from one device-wide counter instead (fr_ticket): no wave then waits on one that is not resident.
+// C3 10M on one box: one wave, no ticket 0.746 ms; 4 waves, ticket 0.856; 4 waves, no ticket 0.834;
+// 8 waves 1.27.  kF3WavesPerSimd waves (80 VGPRs) where a CU's LDS holds as many regions
+// (frame3_fits).
+__global__ __launch_bounds__(64, kF3WavesPerSimd) void k_frame3(BuildParams P, uint32_t lds_per_wave) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  uint32_t tk;
-  if (P.f3_noticket) {
-    tk = blockIdx.x;
-  } else if (NW == 1) {
+  uint32_t tk = blockIdx.x;
+  if (P.fr_ticket) {
     uint32_t t = 0;
     if (threadIdx.x == 0) t = atomicAdd(P.frame_ticket, 1u);
     tk = (uint32_t)__builtin_amdgcn_readfirstlane((int)t);
-  } else {
-    __shared__ unsigned int s_tk;
-    if (threadIdx.x == 0) s_tk = atomicAdd(P.frame_ticket, 1u);
-    __syncthreads();
-    tk = s_tk;
   }
   const uint64_t nwaves = (P.fr_nchunks + P.fr_w - 1) / P.fr_w;
-  const uint32_t w = threadIdx.x >> 6;
-  const uint64_t wv = (uint64_t)tk * NW + w;
-  if (wv < nwaves) frame3_region(P, wv, lds + w * lds_per_wave);
-}
-
-// waves per k_frame3 workgroup: 1 (SPARKEY_FRAME3_WG=2 / 4 / 8: measurements)
-static int f3_wg_waves() {
-  const char* v = getenv("SPARKEY_FRAME3_WG");
-  const int n = v ? atoi(v) : 1;
-  return n == 2 || n == 4 || n == 8 ? n : 1;
+  if (tk < nwaves) frame3_region(P, tk, lds);
 }
 
 // LDS per wave: the staged region, then the scratch (candidates / record list, survivor data, lists
@@ -641,11 +624,10 @@ bool frame3_fits(BuildParams& P, double mean_record, double pass) {
   P.f3_cand_cap = 512;
   // the largest cap >= need (16-multiple) that keeps the most waves (up to kF3WavesPerSimd per SIMD) in
   // 160 KiB of LDS: workgroups of NW waves, + 16 B static each, in 512-byte allocation granules
-  const int NW = f3_wg_waves();
-  for (int wgs = 4 * kF3WavesPerSimd / NW; wgs >= 1; wgs--)
+  for (int wgs = 4 * kF3WavesPerSimd; wgs >= 1; wgs--)
     for (int cap = 512; cap >= need; cap -= 16) {
       P.f3_cand_cap = cap;
-      const uint64_t wg = ((uint64_t)frame3_lds_per_wave(P) * NW + 16 + 511) & ~511ull;
+      const uint64_t wg = ((uint64_t)frame3_lds_per_wave(P) + 16 + 511) & ~511ull;
       if (wg * wgs <= 160 * 1024) return true;
     }
   P.f3_cand_cap = 512;  // (fewer waves per CU)
@@ -656,12 +638,7 @@ void launch_frame3(const BuildParams& P, hipStream_t s, StageTimer* tm) {
   if (P.fr_nchunks == 0) return;
   const uint64_t nwaves = (P.fr_nchunks + P.fr_w - 1) / P.fr_w;
   const uint32_t per = frame3_lds_per_wave(P);
-  const int NW = f3_wg_waves();
-  const dim3 grid((unsigned)((nwaves + NW - 1) / NW)), block(64 * NW);
-  if (NW == 8) hipLaunchKernelGGL(k_frame3<8>, grid, block, (size_t)per * 8, s, P, per);
-  else if (NW == 4) hipLaunchKernelGGL(k_frame3<4>, grid, block, (size_t)per * 4, s, P, per);
-  else if (NW == 2) hipLaunchKernelGGL(k_frame3<2>, grid, block, (size_t)per * 2, s, P, per);
-  else hipLaunchKernelGGL(k_frame3<1>, grid, block, (size_t)per, s, P, per);
+  hipLaunchKernelGGL(k_frame3, dim3((unsigned)nwaves), dim3(64), (size_t)per, s, P, per);
   tm->mark("frame", s);
   scan_exclusive<uint32_t, uint64_t, OpAdd>(P.wcount, P.woff, P.nslabs, (uint64_t*)&P.st->n_records, OpAdd(),
                                             P.scan_scratch_u64, s);

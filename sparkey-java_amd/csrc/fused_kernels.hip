@@ -4,10 +4,15 @@
 //                    speculative framing -> wave exit published at once -> entry from the previous
 //                    wave's exit -> MurmurHash3 of every key out of LDS -> (hash, address) entries
 //                    in log order into the wave's slab.
-//   k_part1_hist/    coarse radix partition of the entries by the top 8 bits of their bucket id
-//   k_part1_scatter  (bucket = wantedSlot >> 10), LDS-staged so every write run is contiguous.
-//   k_part2          one workgroup per coarse partition: fine split into buckets + bucket offsets.
-//   k_place_lds      per bucket, everything in LDS: counting sort by wanted slot, address order
+//   k_frame_uniform  the same for logs whose header proves one record size (stride framing), also
+//                    partition pass 1 into fixed per-digit regions.
+//   k_part1_regions  partition pass 1 of the speculative framings' slabs into the digit regions
+//                    (digit = the top 8 bits of the bucket id, bucket = wantedSlot >> 10).
+//   k_part1_hist/    the two-pass partition (histogram, then LDS-staged scatter) for the serial walk's
+//   k_part1_scatter  dense entries and for hash distributions that overflow a digit region.
+//   k_part2st/s/d/   one workgroup per coarse digit: fine split into buckets (st/s: fixed bucket
+//   k_part2          regions, slot counts and carry functions in the same pass; d: dense, staged).
+//   k_place_reg      per bucket, entries in registers: counting sort by wanted slot, address order
 //                    inside equal slots, canonical positions, every slot of the bucket written once.
 //
 // The only inter-workgroup hand-off in k_frame (a wave's exit -> the next wave's entry) uses 8-byte
@@ -459,7 +464,7 @@ __device__ __forceinline__ void frame_region(const BuildParams& P, const uint64_
         while (p < e) {
           const RecHdr h = hdr_at(p);
           if (!header_valid(h, p, P.max_key_len, log_len)) {
-            set_error(P.st, p, h.rc ? h.rc : kErrCorruptRecord);
+            set_error(P.st, p, header_error(h));
             bad = true;
             break;
           }
@@ -493,7 +498,7 @@ __device__ __forceinline__ void frame_region(const BuildParams& P, const uint64_
         if (go) {
           const RecHdr h = hdr_at(p);
           if (!header_valid(h, p, P.max_key_len, log_len)) {
-            set_error(P.st, p, h.rc ? h.rc : kErrCorruptRecord);
+            set_error(P.st, p, header_error(h));
             bad = true;
           } else {
             cnt++;
@@ -607,24 +612,20 @@ __device__ __forceinline__ void frame_region(const BuildParams& P, const uint64_
   mark(6);
 }
 
-// NW waves per workgroup, one region each.  Default (frame3_kernels.hip's measurements): one wave per
-// workgroup, region = workgroup id (in-order dispatch starts the predecessor first; the spin on its
-// exit is bounded).  TICKET: regions by a device-wide ticket per workgroup, 4 waves each
-// (SPARKEY_FRAME_TICKET, the round-2 launch).
-template <int NW, bool TICKET>
-__global__ __launch_bounds__(64 * NW, 5) void k_frame(BuildParams P, uint32_t lds_per_wave) {
+// One wave per workgroup, region = workgroup id (frame3_kernels.hip's measurements: in-order dispatch
+// starts the predecessor first; the spin on its exit is bounded).  fr_ticket: regions by a device-wide
+// ticket per workgroup, for builds that share the device.
+__global__ __launch_bounds__(64, 5) void k_frame(BuildParams P, uint32_t lds_per_wave) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   uint32_t tk = blockIdx.x;
-  if (TICKET) {
-    __shared__ unsigned int s_tk;
-    if (threadIdx.x == 0) s_tk = atomicAdd(P.frame_ticket, 1u);
-    __syncthreads();
-    tk = s_tk;
+  if (P.fr_ticket) {
+    uint32_t t = 0;
+    if (threadIdx.x == 0) t = atomicAdd(P.frame_ticket, 1u);
+    tk = (uint32_t)__builtin_amdgcn_readfirstlane((int)t);
   }
   const uint64_t nwaves = (P.fr_nchunks + P.fr_w - 1) / P.fr_w;
-  const uint32_t w = threadIdx.x >> 6;
-  const uint64_t wv = (uint64_t)tk * NW + w;
-  if (wv < nwaves) frame_region(P, wv, lds + w * lds_per_wave);
+  (void)lds_per_wave;
+  if (tk < nwaves) frame_region(P, tk, lds);
 }
 
 __device__ __forceinline__ uint32_t bucket_of(const BuildParams& P, uint64_t hash) {
@@ -1373,7 +1374,7 @@ __global__ __launch_bounds__(kPart2Block) void k_part2s(BuildParams P) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   // p2_fixed: bucket b's entries go to its region ent2[b * kPlaceLdsMax ..) in this same pass (the
   // region cursor is the bucket count), so the digit is read once; a bucket that outgrows its region
-  // (more entries than k_place_lds stages anyway) makes the host redo the build with dense runs
+  // (more entries than k_place_reg stages anyway) makes the host redo the build with dense runs
   const bool fixed = P.p2_fixed != 0;
   long long t_prev2 = P.part_dbg ? clock64() : 0;
   auto mark2 = [&](int i) {  // (SPARKEY_PART2_DEBUG: thread 0's cycles per phase)
@@ -1673,324 +1674,23 @@ __global__ __launch_bounds__(kPart2Block) void k_part2st(BuildParams P) {
 }
 
 // ================================================================================================
-// k_place_lds: one bucket per workgroup, entries staged in LDS (buckets above kPlaceLdsMax
-// entries are left to the global-memory k_place, flagged in P.st->big_buckets).
+// Placement: one bucket per workgroup (buckets above kPlaceLdsMax entries are left to the
+// global-memory k_place, flagged in P.st->big_buckets).
 // ================================================================================================
 __device__ __forceinline__ bool is_put_pair(const Entry& x, const Entry& y) {  // a duplicate-key candidate
   return x.hash == y.hash && !(x.addr & kDelBit) && !(y.addr & kDelBit);
 }
 
-// SPARKEY_PLACE_DEBUG: thread 0's clock at the phase boundaries, summed over blocks
-#define PLACE_MARK(i)                                                   \
-  do {                                                                  \
-    if (P.place_dbg && tid == 0) {                                      \
-      const long long now_ = clock64();                                 \
-      P.place_dbg[8 * (uint64_t)blockIdx.x + (i)] = now_ - t_prev_;      \
-      t_prev_ = now_;                                                   \
-    }                                                                   \
-  } while (0)
-
-// Exclusive sum base[s] of the bucket's 1024 slot counts and the inclusive prefix max M[s] of
-// s - base[s] over occupied slots, 512 threads x 2 slots: wave shuffles, one LDS word per wave and
-// two barriers (the block-generic bucket_scan takes six).
-__device__ __forceinline__ void place_scan512(const uint32_t* cnt, uint32_t* base, int32_t* M, uint32_t* wsum,
-                                              int32_t* wmax) {
-  constexpr int NW = kPlaceLdsBlock / 64;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int s0 = 2 * tid;
-  const uint32_t c0 = cnt[s0], c1 = cnt[s0 + 1];
-  uint32_t incl = c0 + c1;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t t = __shfl_up(incl, o, 64);
-    if (lane >= o) incl += t;
-  }
-  if (lane == 63) wsum[w] = incl;
-  __syncthreads();
-  uint32_t off = 0;
-#pragma unroll
-  for (int i = 0; i < NW; i++) off += i < w ? wsum[i] : 0u;
-  const uint32_t b0 = off + incl - (c0 + c1), b1 = b0 + c0;
-  base[s0] = b0;
-  base[s0 + 1] = b1;
-  constexpr int32_t kNone = -(1 << 20);
-  const int32_t v0 = c0 ? s0 - (int32_t)b0 : kNone, v1 = c1 ? s0 + 1 - (int32_t)b1 : kNone;
-  int32_t m = max(v0, v1);
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int32_t t = __shfl_up(m, o, 64);
-    if (lane >= o) m = max(m, t);
-  }
-  if (lane == 63) wmax[w] = m;
-  __syncthreads();
-  int32_t pre = kNone;
-#pragma unroll
-  for (int i = 0; i < NW; i++) pre = i < w ? max(pre, wmax[i]) : pre;
-  int32_t ex = __shfl_up(m, 1, 64);
-  if (lane == 0) ex = kNone;
-  ex = max(ex, pre);
-  M[s0] = max(ex, v0);
-  M[s0 + 1] = max(max(ex, v0), v1);
-}
-
-__global__ __launch_bounds__(kPlaceLdsBlock) void k_place_lds(BuildParams P) {
-  __shared__ uint32_t cnt[kBucket];        // entries per wanted slot (their atomics are the group cursors)
-  __shared__ uint32_t base[kBucket];
-  __shared__ int32_t M[kBucket];
-  __shared__ int32_t pos_j[2 * kBucket];   // (position - carry-in) -> sorted index | hash bits << 10, -1 = empty
-  __shared__ Entry buf[kPlaceLdsMax];      // the bucket's entries in (wanted slot, address) order
-  __shared__ uint32_t wsum[kPlaceLdsBlock / 64];
-  __shared__ int32_t wmax[kPlaceLdsBlock / 64];
-  __shared__ uint64_t sh64[kPlaceLdsBlock / 64 + 1];
-  __shared__ int64_t s_pend;
-  long long t_prev_ = P.place_dbg ? clock64() : 0;
-  const long long t_begin_ = t_prev_;
-  // Every value the block reads besides its entries, in one round trip (block-uniform: scalar loads
-  // issued together) rather than one latency per phase.
-  constexpr int kPer = kPlaceLdsMax / kPlaceLdsBlock;
-  static_assert(kPlaceLdsMax % kPlaceLdsBlock == 0, "entries per thread");
-  static_assert(kBucket == 2 * kPlaceLdsBlock, "place_scan512: two slots per thread");
-  Entry mine[kPer];
-  // fixed bucket regions: the bucket's region is known without its count, so the entry loads go out
-  // together with the head's (one round trip, not two; slots past the count are never used)
-  const bool fixed = P.p2_fixed != 0;
-  if (fixed) {
-    const uint64_t e0 = (uint64_t)blockIdx.x * kPlaceLdsMax;
-#pragma unroll
-    for (int k = 0; k < kPer; k++) mine[k] = P.ent2[e0 + threadIdx.x + k * kPlaceLdsBlock];
-  }
-  const Status* st = P.st;
-  const unsigned ovf = st->overflow | st->p2_overflow, full = st->full;
-  const unsigned long long nrec = st->n_records, ndel = st->n_deletes, npairs0 = st->n_pairs;
-  const uint64_t b = P.b_lo + blockIdx.x;
-  const uint32_t n = P.bcount[b];
-  const uint64_t eoff = P.boff[b];
-  int64_t x;
-  if (P.fused_carry) {
-    const MaxPlus pre = P.bpre[b];
-    x = max(pre.c, P.dcarry[b / P.bpp] + pre.a);
-  } else {
-    x = P.carry[b];
-  }
-  if (ovf != 0 || nrec > P.max_records) return;  // build_aborted
-  if (P.fused_carry && threadIdx.x == 0) P.carry[b] = x;  // (for the global-memory placement's readers)
-  const uint64_t start = b << kBucketShift;
-  const int64_t bsize = (int64_t)min((uint64_t)kBucket, P.cap - start);
-  const int tid = threadIdx.x, lane = tid & 63;
-  if (n > kPlaceLdsMax) {
-    if (tid == 0) atomicOr(&P.st->big_buckets, 1u);
-    return;
-  }
-  // the entries' loads are in flight while the counts are cleared
-  uint32_t want[kPer], cur[kPer], rank[kPer];
-  if (!fixed) {
-#pragma unroll
-    for (int k = 0; k < kPer; k++) {
-      const uint32_t i = tid + k * kPlaceLdsBlock;
-      if (i < n) mine[k] = P.ent2[eoff + i];
-    }
-  }
-  PLACE_MARK(0);
-  for (int t = tid; t < kBucket; t += kPlaceLdsBlock) cnt[t] = 0;
-  for (int t = tid; t < 2 * kBucket; t += kPlaceLdsBlock) pos_j[t] = -1;
-  if (tid == 0) s_pend = 0;
-  __syncthreads();
-#pragma unroll
-  for (int k = 0; k < kPer; k++) {
-    const uint32_t i = tid + k * kPlaceLdsBlock;
-    if (i < n) {
-      want[k] = (uint32_t)(fast_mod(mine[k].hash, P.mod) - start);
-      cur[k] = atomicAdd(&cnt[want[k]], 1u);  // an arbitrary place inside the wanted slot's group
-    }
-  }
-  __syncthreads();
-  PLACE_MARK(1);
-  place_scan512(cnt, base, M, wsum, wmax);
-  __syncthreads();
-#pragma unroll
-  for (int k = 0; k < kPer; k++) {
-    const uint32_t i = tid + k * kPlaceLdsBlock;
-    if (i < n) buf[base[want[k]] + cur[k]] = mine[k];
-  }
-  __syncthreads();
-  PLACE_MARK(2);
-  // Equal wanted slots go in address order (the reference's insertion order, and SORTING's
-  // (wantedSlot, address) comparator): each member counts the members with smaller addresses --
-  // independent LDS reads of its group.  Equal-hash PUT pairs become duplicate-key candidates,
-  // appended to the pair list with one atomic per workgroup (not needed once the exact path is
-  // certain: the log holds DELETEs, or the list overflowed; groups above kGroupMax flag it).
-  const bool want_pairs = ndel == 0 && npairs0 <= P.pair_cap;
-  uint32_t npair = 0;
-#pragma unroll
-  for (int k = 0; k < kPer; k++) {
-    const uint32_t i = tid + k * kPlaceLdsBlock;
-    rank[k] = 0;
-    if (i >= n) continue;
-    const uint32_t w = want[k], g = cnt[w];
-    if (g < 2) continue;
-    const Entry* grp = buf + base[w];
-    const uint64_t ai = mine[k].addr & ~kDelBit;
-    const bool cp = want_pairs && !(mine[k].addr & kDelBit) && g <= kGroupMax;
-    if (g > kGroupMax && cur[k] == 0) atomicOr(&P.st->dup_overflow, 1u);
-    uint32_t r = 0;
-    for (uint32_t u = 0; u < g; u++) {
-      const Entry e = grp[u];
-      const uint64_t aj = e.addr & ~kDelBit;
-      r += aj < ai;
-      npair += cp && aj > ai && e.hash == mine[k].hash && !(e.addr & kDelBit);
-    }
-    rank[k] = r;
-  }
-  const bool any_pair = __syncthreads_or(npair != 0);
-  if (any_pair) {  // (block-uniform; the group members are still in their unsorted places)
-    uint64_t pair_total = 0;
-    const uint64_t pair_off = block_excl_sum<kPlaceLdsBlock>(npair, sh64, &pair_total);  // (syncs the block)
-    __shared__ unsigned long long pair_base;
-    if (tid == 0) pair_base = atomicAdd(&P.st->n_pairs, (unsigned long long)pair_total);
-    __syncthreads();
-    unsigned long long slotn = pair_base + pair_off;
-#pragma unroll
-    for (int k = 0; k < kPer; k++) {
-      const uint32_t i = tid + k * kPlaceLdsBlock;
-      if (i >= n || !npair) continue;
-      const uint32_t w = want[k], g = cnt[w];
-      if (g < 2 || g > kGroupMax || (mine[k].addr & kDelBit)) continue;
-      const Entry* grp = buf + base[w];
-      const uint64_t ai = mine[k].addr & ~kDelBit;
-      for (uint32_t u = 0; u < g; u++) {  // every later member with the same hash (pair order is free)
-        const Entry e = grp[u];
-        if ((e.addr & ~kDelBit) <= ai || !is_put_pair(mine[k], e)) continue;
-        if (slotn < P.pair_cap) {
-          P.pairs[2 * slotn] = mine[k].addr;
-          P.pairs[2 * slotn + 1] = e.addr;
-        }
-        slotn++;
-      }
-    }
-    __syncthreads();
-  }
-  PLACE_MARK(3);
-  if (full) return;
-#pragma unroll
-  for (int k = 0; k < kPer; k++) {  // each group in address order, in place
-    const uint32_t i = tid + k * kPlaceLdsBlock;
-    if (i < n && cnt[want[k]] > 1) buf[base[want[k]] + rank[k]] = mine[k];
-  }
-  // Positions: the j-th entry in (wanted, address) order goes to j + max(carry, M(s)), which lies in
-  // [x, x + 2 * kBucket) (j < n <= kBucket, M(s) < bsize).  The block writes the slot range [x, hi):
-  // its own slots from the carry-in on (entries or zero) and the run it spills past the bucket end,
-  // which has no gap (the first spilled entry lands on bsize, each next one on the next slot).
-  const bool fold = P.fold_stats != 0;
-  unsigned long long sum_d = 0;
-  long long max_d = 0;
-  int64_t pend = 0;  // 1 + the last position
-  int64_t pos[kPer];
-#pragma unroll
-  for (int k = 0; k < kPer; k++) {
-    const uint32_t i = tid + k * kPlaceLdsBlock;
-    pos[k] = -1;
-    if (i >= n) continue;
-    const uint32_t w = want[k];
-    const int64_t j = (int64_t)base[w] + rank[k];
-    const int64_t p = j + max(x, (int64_t)M[w]);
-    pos[k] = p;
-    pos_j[p - x] = (int32_t)j | (int32_t)((mine[k].hash & 0x1fffffull) << 10);  // (j < kPlaceLdsMax = 2^10)
-    sum_d += (unsigned long long)(p - w);  // getDisplacement (IndexHash.java:671-678)
-    max_d = max(max_d, (long long)(p - w));
-    pend = max(pend, p + 1);
-  }
-  pend = wave_max_i64(pend);
-  if (lane == 0 && pend > 0) atomicMax((unsigned long long*)&s_pend, (unsigned long long)pend);
-  __syncthreads();
-  PLACE_MARK(4);
-  const int64_t hi = max(bsize, s_pend);
-  for (int64_t t = x + tid; t < hi; t += kPlaceLdsBlock) {
-    const int32_t v = pos_j[t - x];
-    const uint64_t slot = t < bsize ? start + (uint64_t)t : wrap_slot(start + (uint64_t)t, P.cap);
-    uint64_t hh = 0, aa = 0;
-    if (v >= 0) {
-      const Entry en = buf[v & 1023];
-      hh = en.hash;
-      aa = en.addr & ~kDelBit;
-    }
-    if (P.slot_size == 16 && !P.sharded && P.uni_nt) {  // the table is written once: non-temporal stores
-      typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-      u32x4 w;
-      w.x = (uint32_t)hh;
-      w.y = (uint32_t)(hh >> 32);
-      w.z = (uint32_t)aa;
-      w.w = (uint32_t)(aa >> 32);
-      __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(P.out + kIndexHeaderSize + slot * 16ull));
-    } else if (v >= 0) {
-      put_slot(P, slot, hh, aa);
-    } else {
-      write_slot(P, slot, 0, 0);
-    }
-  }
-  PLACE_MARK(5);
-  if (fold) {  // the block's parts of calculateMaxDisplacement (IndexHash.java:195-245)
-    // adjacent pairs (slot - 1, slot) inside [x, hi), seen from the occupied slot of each pair:
-    // an entry equal to the occupied slot before it, and an entry of hash 0 before an empty slot
-    // (which reads as hash 0)
-    // (sharded: only pairs whose later slot this rank owns -- the rest are the next rank's, counted
-    // from its spilled-in slots by k_stats_folded_shard)
-    const uint64_t lim = P.sharded ? P.slot_hi : ~0ull;
-    unsigned long long col = 0;
-#pragma unroll
-    for (int k = 0; k < kPer; k++) {
-      const int64_t p = pos[k];
-      if (p < 0) continue;
-      const uint64_t h = mine[k].hash;
-      if (p > x && wrap_slot(start + (uint64_t)p, P.cap) != 0 && start + (uint64_t)p < lim) {
-        const int32_t vp = pos_j[p - 1 - x];  // the hash bits decide; the full hash only confirms
-        if (vp >= 0 && (uint32_t)(vp >> 10) == (uint32_t)(h & 0x1fffffull)) col += buf[vp & 1023].hash == h;
-      }
-      if (h == 0 && p + 1 < hi && pos_j[p + 1 - x] < 0 && wrap_slot(start + (uint64_t)p + 1, P.cap) != 0 &&
-          start + (uint64_t)p + 1 < lim)
-        col++;
-    }
-    if (x < (1ll << 20)) {  // (block-uniform) every displacement < 2^21: 32-bit DPP reductions
-      sum_d = wave_sum_u32((uint32_t)sum_d);
-      max_d = wave_max_i32((int32_t)max_d);
-    } else {
-      sum_d = wave_sum_u64(sum_d);
-      max_d = wave_max_i64(max_d);
-    }
-    col = wave_sum_u32((uint32_t)col);
-    __shared__ unsigned long long r_sum[kPlaceLdsBlock / 64], r_col[kPlaceLdsBlock / 64];
-    __shared__ long long r_max[kPlaceLdsBlock / 64];
-    if (lane == 0) {
-      r_sum[tid >> 6] = sum_d;
-      r_col[tid >> 6] = col;
-      r_max[tid >> 6] = max_d;
-    }
-    __syncthreads();
-    if (tid == 0) {
-      StatPart sp{0, 0, 0};
-      for (int w = 0; w < kPlaceLdsBlock / 64; w++) {
-        sp.sum_disp += r_sum[w];
-        sp.collisions += r_col[w];
-        sp.max_disp = max(sp.max_disp, r_max[w]);
-      }
-      P.parts[b] = sp;
-      P.bstat_start[b] = hi > x ? wrap_slot(start + (uint64_t)x, P.cap) : ~0ull;
-    }
-  }
-  PLACE_MARK(6);
-  if (P.place_dbg && tid == 0) P.place_dbg[8 * (uint64_t)blockIdx.x + 7] = t_prev_ - t_begin_;
-}
-
-
 // ================================================================================================
-// k_place_reg: k_place_lds's placement with the entries kept in registers and stored straight to
-// their slots.  Per bucket: the 16-bit count of each wanted slot (its atomic is the entry's place
+// k_place_reg: the canonical placement of one bucket, its entries kept in registers.  Per bucket: the 16-bit count of each wanted slot (its atomic is the entry's place
 // in its group), one scan for base[s] (entries wanted before s) and M[s] (the prefix max of
 // s - base[s] over occupied s), the entries copied to base[w] + cursor so that each group of equal
 // wanted slots lies together, then every entry's rank in its group by address (IndexHash.java:647-650,
 // SortHelper's (wantedSlot, address) order) and its position j + max(carry, M[w]).  The block writes
 // its slots [x, hi) in order (coalesced: scattered 16-byte stores cost one L2 request each, which
-// measured 2.4x slower), entries out of LDS through a slot -> entry map.  27 KiB of LDS (k_place_lds:
-// 36 KiB), 4 waves per block, 5 blocks per CU; the fixed regions' entry loads go out before the head.
+// measured 2.4x slower), entries out of LDS through a slot -> entry map.  27 KiB of LDS (the round-2
+// kernel that staged the bucket in LDS took 36 KiB and 0.170 against 0.154 ms on C2), 4 waves per
+// block, 5 blocks per CU; the fixed regions' entry loads go out before the head.
 // ================================================================================================
 constexpr int kPlaceRegBlock = 256;
 constexpr int kPlaceRegPer = kPlaceLdsMax / kPlaceRegBlock;
@@ -2129,7 +1829,7 @@ __device__ __forceinline__ void place_reg_bucket(const BuildParams& P, uint64_t 
   }
   __syncthreads();
   // Equal wanted slots in address order: each member counts the members with smaller addresses.
-  // Equal-hash PUT pairs are duplicate-key candidates for the pair list (as k_place_lds).
+  // Equal-hash PUT pairs are duplicate-key candidates for the pair list (as k_place_reg).
   const bool want_pairs = ndel == 0 && npairs0 <= P.pair_cap;
   uint32_t npair = 0;
   uint32_t rank[kPlaceRegPer];
@@ -2298,38 +1998,21 @@ void launch_frame_fused(const BuildParams& P, hipStream_t s, StageTimer* tm) {
   // candidate list and then by the record list
   const size_t lds = (size_t)P.fr_rgn_bytes + std::max<size_t>((size_t)P.fr_w * P.fr_mask_words * 8 + 8, kCandCap * 4);
   const uint32_t per = (uint32_t)((lds + 15) & ~(size_t)15);
-  // (SPARKEY_FRAME_LDS_PAD: extra LDS per workgroup, to measure the phases at lower occupancy)
-  const size_t pad = getenv("SPARKEY_FRAME_LDS_PAD") ? (size_t)atoll(getenv("SPARKEY_FRAME_LDS_PAD")) : 0;
-  if (getenv("SPARKEY_FRAME_TICKET"))
-    hipLaunchKernelGGL((k_frame<kFrameWaves, true>), dim3((unsigned)((nwaves + kFrameWaves - 1) / kFrameWaves)),
-                       dim3(64 * kFrameWaves), (size_t)per * kFrameWaves + pad, s, P, per);
-  else
-    hipLaunchKernelGGL((k_frame<1, false>), dim3((unsigned)nwaves), dim3(64), (size_t)per + pad, s, P, per);
+  hipLaunchKernelGGL(k_frame, dim3((unsigned)nwaves), dim3(64), (size_t)per, s, P, per);
   tm->mark("frame", s);  // the stage is k_frame alone (its rocprof row); the slab scan counts as partition
   scan_exclusive<uint32_t, uint64_t, OpAdd>(P.wcount, P.woff, P.nslabs, (uint64_t*)&P.st->n_records, OpAdd(),
                                             P.scan_scratch_u64, s);
 }
 
-// Waves per workgroup: as many (up to 16) as fit their staging buffers in 150 KB of LDS.
-int frame_uniform_waves(int64_t rec) {  // (rec <= 256: at least 8 waves fit)
-  const int64_t wbytes = (64 * rec + 32 + 1023) & ~1023ll;
-  return 16 * wbytes + 2048 <= 150 * 1024 ? 16 : 8;
-}
-
 void launch_frame_uniform(const BuildParams& P, hipStream_t s, StageTimer* tm) {
   if (P.uni_n == 0) return;
   BuildParams Q = P;
-  int W = frame_uniform_waves(P.uni_rec);
-  // default: 4 waves per workgroup, double-buffered (two workgroups per CU, each wave's next DMA in
-  // flight while it hashes); SPARKEY_FRAME_W=16 / 8: single-buffered, one workgroup per CU
-  bool db = true;
-  if (const char* e = getenv("SPARKEY_FRAME_W")) {  // (measurements)
-    W = atoi(e) == 8 ? 8 : 16;
-    db = false;
-  }
-  if (db) W = 4;
+  // 4 waves per workgroup, double-buffered: two workgroups per CU, each wave's next DMA in flight while
+  // it hashes (single-buffered 16- and 8-wave workgroups, one per CU, measured slower)
+  constexpr int W = 4;
+  constexpr bool db = true;
   Q.uni_wbytes = (uint32_t)((64 * P.uni_rec + 32 + 1023) & ~1023ll);
-  Q.uni_nt = getenv("SPARKEY_FRAME_NO_NT") ? 0u : 1u;  // (the log is read once: measured 10% faster)
+  Q.uni_nt = 1u;  // (the log is read once: non-temporal staging measured 10% faster)
   const uint64_t per = kPartTile;  // records per workgroup
   const uint64_t nblk = (P.uni_n + per - 1) / per;
   // the wave buffers, then the tile regrouped by digit in the same space (entries, digits, run
@@ -2337,9 +2020,7 @@ void launch_frame_uniform(const BuildParams& P, hipStream_t s, StageTimer* tm) {
   const size_t body = std::max<size_t>((size_t)W * Q.uni_wbytes * (db ? 2 : 1), (size_t)kPartTile * (sizeof(Entry) + 1) + 1024);
   const size_t lds = body + 2048;
   Q.uni_hist_off = (uint32_t)body;
-  if (db) hipLaunchKernelGGL((k_frame_uniform<4, true>), dim3((unsigned)nblk), dim3(64 * 4), lds, s, Q);
-  else if (W == 16) hipLaunchKernelGGL((k_frame_uniform<16, false>), dim3((unsigned)nblk), dim3(64 * 16), lds, s, Q);
-  else hipLaunchKernelGGL((k_frame_uniform<8, false>), dim3((unsigned)nblk), dim3(64 * 8), lds, s, Q);
+  hipLaunchKernelGGL((k_frame_uniform<W, db>), dim3((unsigned)nblk), dim3(64 * W), lds, s, Q);
   tm->mark("frame", s);
 }
 
@@ -2380,10 +2061,9 @@ static size_t part2st_lds(uint32_t bpp, int per) {
 void launch_partition(const BuildParams& P, hipStream_t s, StageTimer* tm) {
   if (!P.p1_region) launch_partition1(P, s);
   else if (P.p1_kernel) hipLaunchKernelGGL(k_part1_regions, dim3((unsigned)P.p1_tiles), dim3(kPartBlock), 0, s, P);
-  static const bool no_staged = getenv("SPARKEY_NO_P2_STAGED") != nullptr;  // (k_part2s: measurements)
   // the largest stage (entries a thread per round) that fits: fewer rounds, fewer barriers
   constexpr size_t kLdsMax = 158 * 1024;
-  const bool staged = P.p2_sorted && P.p2_fixed && P.fused_carry && P.p1_region && !P.p2_seg && !no_staged;
+  const bool staged = P.p2_sorted && P.p2_fixed && P.fused_carry && P.p1_region && !P.p2_seg;
   if (staged && part2st_lds(P.bpp, 6) <= kLdsMax)
     hipLaunchKernelGGL(k_part2st<6>, dim3(256), dim3(kPart2Block), part2st_lds(P.bpp, 6), s, P);
   else if (staged && part2st_lds(P.bpp, 5) <= kLdsMax)
@@ -2392,7 +2072,7 @@ void launch_partition(const BuildParams& P, hipStream_t s, StageTimer* tm) {
     hipLaunchKernelGGL(k_part2st<4>, dim3(256), dim3(kPart2Block), part2st_lds(P.bpp, 4), s, P);
   else if (P.p2_sorted)
     hipLaunchKernelGGL(k_part2s, dim3(256), dim3(kPart2Block), (size_t)(514u * P.bpp) * sizeof(uint32_t), s, P);
-  else if (!P.p2_seg && !no_staged && part2d_lds(P.bpp) <= kLdsMax)
+  else if (!P.p2_seg && part2d_lds(P.bpp) <= kLdsMax)
     hipLaunchKernelGGL(k_part2d, dim3(256), dim3(kPart2Block), part2d_lds(P.bpp), s, P);
   else
     hipLaunchKernelGGL(k_part2, dim3(256), dim3(kPart2Block), (size_t)(2u * P.bpp) * sizeof(uint32_t), s, P);
@@ -2400,14 +2080,8 @@ void launch_partition(const BuildParams& P, hipStream_t s, StageTimer* tm) {
 }
 
 void launch_place_buckets(const BuildParams& P, hipStream_t s) {
-  // k_place_reg (SPARKEY_PLACE_LDS=1: k_place_lds, the round-2 kernel: 0.170 against 0.154 ms on C2)
-  static const bool lds_kernel = getenv("SPARKEY_PLACE_LDS") != nullptr;
-  if (P.b_hi > P.b_lo) {
-    if (lds_kernel || P.place_dbg)
-      hipLaunchKernelGGL(k_place_lds, dim3((unsigned)(P.b_hi - P.b_lo)), dim3(kPlaceLdsBlock), 0, s, P);
-    else
-      hipLaunchKernelGGL(k_place_reg, dim3((unsigned)(P.b_hi - P.b_lo)), dim3(kPlaceRegBlock), 0, s, P);
-  }
+  if (P.b_hi > P.b_lo)
+    hipLaunchKernelGGL(k_place_reg, dim3((unsigned)(P.b_hi - P.b_lo)), dim3(kPlaceRegBlock), 0, s, P);
   // buckets above kPlaceLdsMax entries (normally none; never with fixed bucket regions, whose
   // overflow redoes the build with dense runs)
   if (!P.p2_fixed) launch_place_global(P, s, 0, 1);

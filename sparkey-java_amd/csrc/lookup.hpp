@@ -26,5 +26,8 @@ struct LookupParams {
 };
 
 void launch_get(const LookupParams& L, hipStream_t s);
+// sparkey_hash_batch: L.keys / key_off / n / hash_size / seed / mod (mod.cap == 0: no slots)
+void launch_hash_batch(const LookupParams& L, uint64_t* hash_out, uint64_t* slot_out, hipStream_t s);
+void launch_slot_batch(const uint64_t* hash, uint64_t n, const FastMod& mod, uint64_t* slot_out, hipStream_t s);
 
 }  // namespace sk

@@ -44,7 +44,7 @@ __global__ __launch_bounds__(256) void k_get(LookupParams L) {
       const int64_t p = (int64_t)(addr2 >> L.ebb);
       const RecHdr h = decode_header(at, p, (int64_t)L.log_len);
       if (h.rc) {
-        atomicMin(L.err, ((unsigned long long)i << 8) | (unsigned long long)(-h.rc));
+        atomicMin(L.err, ((unsigned long long)i << 8) | (unsigned long long)(-header_error(h)));
         break;
       }
       if (!h.put) {  // "Invalid data - reference to delete entry"
@@ -72,6 +72,32 @@ __global__ __launch_bounds__(256) void k_get(LookupParams L) {
 void launch_get(const LookupParams& L, hipStream_t s) {
   if (L.n == 0) return;
   hipLaunchKernelGGL(k_get, dim3((unsigned)((L.n + 255) / 256)), dim3(256), 0, s, L);
+}
+
+// HashType.hash + getWantedSlot per key (sparkey_hash_batch): the same key_hash / fast_mod the build
+// kernels call, one lane per key.
+__global__ __launch_bounds__(256) void k_hash_batch(LookupParams L, uint64_t* hash_out, uint64_t* slot_out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= L.n) return;
+  const uint64_t k0 = L.key_off[i];
+  const uint64_t h = key_hash(L.hash_size, L.keys + k0, (int32_t)(L.key_off[i + 1] - k0), L.seed);
+  hash_out[i] = h;
+  if (slot_out) slot_out[i] = fast_mod(h, L.mod);
+}
+
+__global__ __launch_bounds__(256) void k_slot_batch(const uint64_t* hash, uint64_t n, FastMod mod, uint64_t* slot_out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) slot_out[i] = fast_mod(hash[i], mod);
+}
+
+void launch_hash_batch(const LookupParams& L, uint64_t* hash_out, uint64_t* slot_out, hipStream_t s) {
+  if (L.n == 0) return;
+  hipLaunchKernelGGL(k_hash_batch, dim3((unsigned)((L.n + 255) / 256)), dim3(256), 0, s, L, hash_out, slot_out);
+}
+
+void launch_slot_batch(const uint64_t* hash, uint64_t n, const FastMod& mod, uint64_t* slot_out, hipStream_t s) {
+  if (n == 0) return;
+  hipLaunchKernelGGL(k_slot_batch, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, hash, n, mod, slot_out);
 }
 
 }  // namespace sk

@@ -42,6 +42,7 @@
 #include <rccl/rccl.h>  // types only: librccl is opened at run time (shared with torch's copy when loaded)
 
 #include "../../include/sparkey_gpu.h"
+#include "knobs.hpp"
 #include "shard_host.hpp"
 
 namespace {
@@ -274,6 +275,68 @@ class ThreadColl : public Coll {
 };
 
 // ---------------------------------------------------------------------------------------------
+// collectives supplied by the host program (sparkey_shard_comm_create_host): every buffer is staged
+// through pinned host memory and handed to the caller's functions, which move it between the ranks
+// (torch.distributed gloo for the one-GPU multi-process rehearsal, or a JVM's own transport).
+// ---------------------------------------------------------------------------------------------
+class HostColl : public Coll {
+ public:
+  HostColl(const sparkey_shard_transport& t, int r, int w) : t_(t) {
+    rank = r;
+    world = w;
+  }
+  ~HostColl() override {
+    if (h_) (void)hipHostFree(h_);
+  }
+  int all_gather(const void* d_send, void* d_recv, size_t bytes, hipStream_t s, std::string* why) override {
+    uint8_t* h = stage((uint64_t)bytes * (world + 1));
+    if (!h) return err(why, "pinned staging allocation failed");
+    int rc = copy(h, d_send, bytes, hipMemcpyDeviceToHost, s, why);
+    if (rc) return rc;
+    if (t_.all_gather(t_.ctx, h, h + bytes, bytes) != 0) return err(why, "host transport all_gather failed");
+    return copy(d_recv, h + bytes, (uint64_t)bytes * world, hipMemcpyHostToDevice, s, why);
+  }
+  int all_to_all(const uint8_t* d_send, const uint64_t* send_bytes, uint8_t* d_recv, const uint64_t* recv_bytes,
+                 hipStream_t s, std::string* why) override {
+    uint64_t sb = 0, rb = 0;
+    for (int r = 0; r < world; r++) {
+      sb += send_bytes[r];
+      rb += recv_bytes[r];
+    }
+    uint8_t* h = stage(sb + rb);
+    if (!h) return err(why, "pinned staging allocation failed");
+    int rc = copy(h, d_send, sb, hipMemcpyDeviceToHost, s, why);
+    if (rc) return rc;
+    if (t_.all_to_all(t_.ctx, h, send_bytes, h + sb, recv_bytes) != 0) return err(why, "host transport all_to_all failed");
+    return copy(d_recv, h + sb, rb, hipMemcpyHostToDevice, s, why);
+  }
+
+ private:
+  static int err(std::string* why, const char* m) {
+    *why = m;
+    return SPARKEY_E_GPU;
+  }
+  uint8_t* stage(uint64_t n) {
+    n = std::max<uint64_t>(n, 64);
+    if (h_ && cap_ >= n) return h_;
+    if (h_) (void)hipHostFree(h_);
+    h_ = nullptr;
+    cap_ = 0;
+    if (hipHostMalloc((void**)&h_, n, hipHostMallocDefault) != hipSuccess) return nullptr;
+    cap_ = n;
+    return h_;
+  }
+  static int copy(void* dst, const void* src, uint64_t n, hipMemcpyKind k, hipStream_t s, std::string* why) {
+    if (n && (hipMemcpyAsync(dst, src, n, k, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess))
+      return err(why, "staging copy failed");
+    return SPARKEY_OK;
+  }
+  sparkey_shard_transport t_;
+  uint8_t* h_ = nullptr;
+  uint64_t cap_ = 0;
+};
+
+// ---------------------------------------------------------------------------------------------
 // log geometry (sharded.py shard_layout)
 // ---------------------------------------------------------------------------------------------
 uint32_t rd32(const uint8_t* p) {
@@ -326,7 +389,7 @@ Layout make_layout(const uint8_t* h, int world) {
   // uniform records (sparkey_gpu.cpp uniform_record_size): the shard entries are arithmetic
   const int64_t r = vlq_size(L.max_key_len + 1) + vlq_size(L.max_value_len) + L.max_key_len + L.max_value_len;
   L.uni = (L.num_deletes == 0 && L.num_puts > 0 && L.max_key_len + 1 < 128 && L.max_value_len < 128 && r <= 256 &&
-           L.put_size == L.num_puts * r && L.data_end - kLogHeader == L.put_size && !getenv("SPARKEY_NO_UNIFORM"))
+           L.put_size == L.num_puts * r && L.data_end - kLogHeader == L.put_size && !sk::knob_on(sk::Knob::NoUniform))
               ? r
               : 0;
   return L;
@@ -408,14 +471,37 @@ class Rank {
   Rank(sparkey_plan* pl, sparkey_shard_comm* cm, hipStream_t s, char* err, size_t err_len)
       : pl_(pl), cm_(cm), c_(cm->coll.get()), s_(s), err_(err), err_len_(err_len), g_(c_->rank), G_(c_->world) {}
 
+  // rc0 != 0: this rank already failed (e.g. loading its log range); it still meets the other ranks at
+  // the first checkpoint so that every rank returns the error instead of waiting for it
   int run(const uint8_t* hdr, uint64_t file_len, const uint8_t* d_buf, uint64_t buf_lo, uint64_t buf_hi,
-          const sparkey_build_opts& o, uint8_t* d_out, uint64_t out_cap, sparkey_build_stats* st);
+          const sparkey_build_opts& o, uint8_t* d_out, uint64_t out_cap, sparkey_build_stats* st, int rc0);
 
  private:
   // ---- helpers ----
   int fail(int rc, const std::string& msg) {
     set_err(err_, err_len_, msg);
     return rc;
+  }
+  // Every rank fails together: a rank whose own step failed does not return on its own,
+  // it posts its code at the next exchange (a checkpoint, or a field of a row every rank gathers
+  // anyway) and all ranks return from the same place.  `codes[r]` is rank r's code (0 = fine).
+  int fail_together(const std::vector<int64_t>& codes, int own) {
+    for (int r = 0; r < G_; r++)
+      if (codes[r]) {
+        if (r == g_) return own ? own : (int)codes[r];  // (its own message is in err_)
+        if (own) return own;
+        return fail((int)codes[r], std::string("another rank of the sharded build failed (rank ") + std::to_string(r) +
+                                       ": " + code_text((int)codes[r]) + ")");
+      }
+    return SPARKEY_OK;
+  }
+  // a checkpoint: every rank's local code gathered; non-zero anywhere -> every rank fails
+  int agree(int own) {
+    if (G_ == 1) return own;
+    std::vector<int64_t> codes;
+    const int rc = gather_i64({own}, &codes);
+    if (rc) return rc;
+    return fail_together(codes, own);
   }
   int gpu(hipError_t e, const char* what) {
     if (e == hipSuccess) return SPARKEY_OK;
@@ -810,48 +896,62 @@ int Rank::gathered(const uint8_t* hdr, uint64_t file_len, const uint8_t* d_buf, 
 }
 
 int Rank::run(const uint8_t* hdr, uint64_t file_len, const uint8_t* d_buf, uint64_t buf_lo, uint64_t buf_hi,
-              const sparkey_build_opts& o, uint8_t* d_out, uint64_t out_cap, sparkey_build_stats* st) {
+              const sparkey_build_opts& o, uint8_t* d_out, uint64_t out_cap, sparkey_build_stats* st, int rc0) {
   cm_->phase.clear();
   clock_ = now_ms();
   hdr_ = hdr;
   L_ = make_layout(hdr, G_);
   geo_ = make_geo(L_, hdr, o);
   const int64_t data_end = L_.data_end;
-  int rc = sparkey_shard_begin(pl_, hdr, file_len, d_buf, buf_lo, buf_hi, &o, g_, G_, err_, err_len_);
-  if (rc) return rc;
-  uint64_t slot_lo = 0, slot_hi = 0;
-  sparkey_shard_slot_range(pl_, g_, &slot_lo, &slot_hi);
-  const uint64_t ss = (uint64_t)geo_.slot;
-  const uint64_t hdr_off = g_ == 0 ? kIndexHeader : 0;
-  const uint64_t out_len = hdr_off + (slot_hi - slot_lo) * ss;
-  if (out_cap < out_len) return fail(SPARKEY_E_BUFFER, "shard output buffer too small: need " + std::to_string(out_len));
   memset(st, 0, sizeof(*st));
   st->capacity = (int64_t)geo_.cap;
   st->hash_size = geo_.hash_size;
   st->address_size = geo_.addr_size;
   st->num_puts = L_.num_puts;
   st->num_deletes = L_.num_deletes;
-  if (L_.compression != 0) return gathered(hdr, file_len, d_buf, buf_lo, o, d_out, slot_lo, out_len, st);
+  uint64_t slot_lo = 0, slot_hi = 0;
+  const uint64_t ss = (uint64_t)geo_.slot;
+  const uint64_t hdr_off = g_ == 0 ? kIndexHeader : 0;
+  uint64_t out_len = 0;
+  if (!rc0) rc0 = sparkey_shard_begin(pl_, hdr, file_len, d_buf, buf_lo, buf_hi, &o, g_, G_, err_, err_len_);
+  if (!rc0) {
+    sparkey_shard_slot_range(pl_, g_, &slot_lo, &slot_hi);
+    out_len = hdr_off + (slot_hi - slot_lo) * ss;
+    if (out_cap < out_len) rc0 = fail(SPARKEY_E_BUFFER, "shard output buffer too small: need " + std::to_string(out_len));
+  }
+  const int RL = 8 + G_ + 256;  // the verification row
+  uint8_t* row = rc0 ? nullptr : cm_->row.ensure((uint64_t)RL * 8);
+  if (!rc0 && !row) rc0 = fail(SPARKEY_E_GPU, "hipMalloc failed");
 
   // ---- 1 entries: speculate, frame, verify by induction from c_0 = 84 ----
   auto uni_entry = [&](int r) {
     return std::min<int64_t>(data_end, kLogHeader + (L_.lo[r] - kLogHeader + L_.uni - 1) / L_.uni * L_.uni);
   };
-  int64_t c_g;
-  if (g_ == 0) c_g = kLogHeader;
-  else if (L_.small) c_g = data_end;
-  else if (L_.uni) c_g = uni_entry(g_);
-  else {
-    rc = sparkey_shard_find_entry(pl_, (uint64_t)L_.lo[g_], (uint64_t)L_.window, s_, &c_g, err_, err_len_);
-    if (rc) return rc;
+  int64_t c_g = -1;
+  if (!rc0) {
+    if (g_ == 0) c_g = kLogHeader;
+    else if (L_.small || L_.compression != 0) c_g = data_end;
+    else if (L_.uni) c_g = uni_entry(g_);
+    else rc0 = sparkey_shard_find_entry(pl_, (uint64_t)L_.lo[g_], (uint64_t)L_.window, s_, &c_g, err_, err_len_);
   }
+  // the first checkpoint: every rank's entry and code (a rank that failed so far fails them all)
   std::vector<int64_t> cs(G_);
-  if (L_.small || L_.uni) {
-    for (int r = 0; r < G_; r++) cs[r] = r == 0 ? kLogHeader : (L_.small ? data_end : uni_entry(r));
-  } else {
-    rc = gather_i64({c_g}, &cs);
+  if (G_ > 1) {
+    std::vector<int64_t> ce;
+    int rc = gather_i64({c_g, rc0}, &ce);
     if (rc) return rc;
+    std::vector<int64_t> codes(G_);
+    for (int r = 0; r < G_; r++) {
+      cs[r] = ce[2 * r];
+      codes[r] = ce[2 * r + 1];
+    }
+    rc = fail_together(codes, rc0);
+    if (rc) return rc;
+  } else {
+    if (rc0) return rc0;
+    cs[0] = c_g;
   }
+  if (L_.compression != 0) return gathered(hdr, file_len, d_buf, buf_lo, o, d_out, slot_lo, out_len, st);
   mark("entries");
   entries_.assign(G_, 0);
   valid_.assign(G_, false);
@@ -873,9 +973,7 @@ int Rank::run(const uint8_t* hdr, uint64_t file_len, const uint8_t* d_buf, uint6
   for (int r = 0; r < G_; r++) todo[r] = valid_[r];
   std::vector<int64_t> framed;
   int rounds = 0;
-  const int RL = 8 + G_ + 256;  // the verification row
-  uint8_t* row = cm_->row.ensure((uint64_t)RL * 8);
-  if (!row) return fail(SPARKEY_E_GPU, "hipMalloc failed");
+  int rc = SPARKEY_OK;
   if (!todo[g_]) {  // (re-framed from the previous rank's exit in a later round)
     std::vector<int64_t> init(RL, 0);
     for (int i = 0; i < 7; i++) init[i] = -1;
@@ -885,48 +983,67 @@ int Rank::run(const uint8_t* hdr, uint64_t file_len, const uint8_t* d_buf, uint6
   uint8_t* send = nullptr;
   uint64_t send_cap = 0;
   std::vector<int64_t> R((size_t)G_ * RL);
-  const bool sync_frame = getenv("SPARKEY_SHARD_SYNC_FRAME") != nullptr;  // (tests: every attempt retried)
+  const bool sync_frame = sk::knob_on(sk::Knob::ShardSyncFrame);  // (tests: every attempt retried)
+  // a rank whose framing step fails posts a row with retry = -2 and its code (every rank then fails)
+  auto post_failure = [&](int code) -> int {
+    std::vector<int64_t> f(RL, 0);
+    f[5] = code;
+    f[6] = -1;
+    f[7] = -2;
+    const int e = gpu(hipMemcpyAsync(row, f.data(), (uint64_t)RL * 8, hipMemcpyHostToDevice, s_), "H2D");
+    return e ? e : gpu(hipStreamSynchronize(s_), "sync");
+  };
+  int own = SPARKEY_OK;  // this rank's failed step, posted in its row
   for (;;) {
     rounds++;
-    if (todo[g_]) {
+    if (todo[g_] && !own) {
       const int64_t fend = fe(g_);
       if (std::find(framed.begin(), framed.end(), entries_[g_]) == framed.end()) {
         framed.push_back(entries_[g_]);
         uint64_t cap = 1ull << 62;  // (one rank: the entries stay in place, bounded by the plan's workspace)
         if (G_ > 1) {
           const int64_t c = sparkey_shard_frame_capacity(pl_, entries_[g_], fend);
-          if (c < 0) return fail(SPARKEY_E_ARG, "bad shard frame range");
-          cap = (uint64_t)c;
+          if (c < 0) own = fail(SPARKEY_E_ARG, "bad shard frame range");
+          cap = (uint64_t)std::max<int64_t>(0, c);
         }
         if (sync_frame) cap = 0;
         send = nullptr;
         send_cap = cap;
-        if (G_ > 1) {
+        if (G_ > 1 && !own) {
           send = cm_->send.ensure(std::max<uint64_t>(1, cap) * kEntryBytes);
-          if (!send) return fail(SPARKEY_E_GPU, "hipMalloc failed");
+          if (!send) own = fail(SPARKEY_E_GPU, "hipMalloc failed");
         }
-        rc = sparkey_shard_frame_bin_async(pl_, entries_[g_], fend, send, cap, (int64_t*)row, s_, err_, err_len_);
-        if (rc) return rc;
+        if (!own) own = sparkey_shard_frame_bin_async(pl_, entries_[g_], fend, send, cap, (int64_t*)row, s_, err_, err_len_);
       } else {  // the speculative attempt did not hold: frame with every retry, then bin
         sparkey_shard_frame_result fr;
-        rc = sparkey_shard_frame(pl_, entries_[g_], fend, s_, &fr, err_, err_len_);
-        if (rc) return rc;
+        memset(&fr, 0, sizeof(fr));
+        own = sparkey_shard_frame(pl_, entries_[g_], fend, s_, &fr, err_, err_len_);
         const uint64_t n_mine = fr.rc ? 0 : (uint64_t)fr.num_records;
         send = nullptr;
         send_cap = 0;
-        if (G_ > 1) {
+        if (G_ > 1 && !own) {
           send = cm_->send.ensure(std::max<uint64_t>(1, n_mine) * kEntryBytes);
-          if (!send) return fail(SPARKEY_E_GPU, "hipMalloc failed");
+          if (!send) own = fail(SPARKEY_E_GPU, "hipMalloc failed");
           send_cap = cm_->send.cap / kEntryBytes;
         }
         const int64_t sc[8] = {entries_[g_], fend, fr.exit, fr.num_records, fr.num_deletes, fr.rc, fr.err_pos, 0};
-        rc = sparkey_shard_bin_row(pl_, send, send_cap, n_mine, sc, (int64_t*)row, s_, err_, err_len_);
-        if (rc) return rc;
+        if (!own) own = sparkey_shard_bin_row(pl_, send, send_cap, n_mine, sc, (int64_t*)row, s_, err_, err_len_);
       }
+    }
+    if (own) {
+      rc = post_failure(own);
+      if (rc) return rc;
     }
     rc = all_gather(row, cm_->rows, (uint64_t)RL * 8);
     if (!rc) rc = to_host(R.data(), cm_->rows.p, (uint64_t)G_ * RL * 8);
     if (rc) return rc;
+    {
+      std::vector<int64_t> codes(G_, 0);
+      for (int r = 0; r < G_; r++)
+        if (R[(size_t)r * RL + 7] == -2) codes[r] = R[(size_t)r * RL + 5] ? R[(size_t)r * RL + 5] : SPARKEY_E_GPU;
+      rc = fail_together(codes, own);
+      if (rc) return rc;
+    }
     bool any = false;
     for (int r = 0; r < G_; r++) {
       todo[r] = R[(size_t)r * RL + 7] != 0;  // speculative attempts to redo, the entries unchanged
@@ -960,10 +1077,6 @@ int Rank::run(const uint8_t* hdr, uint64_t file_len, const uint8_t* d_buf, uint6
     return gathered(hdr, file_len, d_buf, buf_lo, o, d_out, slot_lo, out_len, st);
 
   // ---- 2 exchange: every PUT entry to the owner of its slot range ----
-  if (!send && G_ > 1) {
-    send = cm_->send.ensure(16);
-    if (!send) return fail(SPARKEY_E_GPU, "hipMalloc failed");
-  }
   std::vector<uint64_t> sb(G_), rb(G_);
   uint64_t n_recv = 0;
   for (int r = 0; r < G_; r++) {
@@ -971,10 +1084,25 @@ int Rank::run(const uint8_t* hdr, uint64_t file_len, const uint8_t* d_buf, uint6
     rb[r] = (uint64_t)R[(size_t)r * RL + 8 + g_] * kEntryBytes;
     n_recv += (uint64_t)R[(size_t)r * RL + 8 + g_];
   }
+  // every buffer the exchange and the placement need, then one checkpoint: a rank that cannot
+  // allocate them fails every rank here instead of leaving the others inside a collective
+  const int FL = 4 + 4 * kSpillInline;
+  uint64_t spill_cap = 4096;
+  uint8_t* rv = nullptr;
+  if (G_ > 1) {
+    if (!send) send = cm_->send.ensure(16);
+    rv = cm_->recv.ensure(std::max<uint64_t>(1, n_recv) * kEntryBytes);
+  }
+  uint8_t* spill = cm_->spill.ensure(spill_cap * kSpillBytes);
+  uint8_t* flags = cm_->flags.ensure((uint64_t)FL * 8);
+  uint8_t* fun = cm_->fun.ensure(16);
+  uint8_t* fin = cm_->fin.ensure(12 * 8);
+  const bool have = (G_ == 1 || (send && rv)) && spill && flags && fun && fin && cm_->funs.ensure(16ull * G_) &&
+                    cm_->frows.ensure((uint64_t)FL * 8 * G_) && cm_->fins.ensure(12ull * 8 * G_);
+  rc = agree(have ? SPARKEY_OK : fail(SPARKEY_E_GPU, "hipMalloc failed"));
+  if (rc) return rc;
   const uint8_t* recv = nullptr;
   if (G_ > 1) {
-    uint8_t* rv = cm_->recv.ensure(std::max<uint64_t>(1, n_recv) * kEntryBytes);
-    if (!rv) return fail(SPARKEY_E_GPU, "hipMalloc failed");
     std::string why;
     rc = coll_rc(c_->all_to_all(send, sb.data(), rv, rb.data(), s_, &why), why);
     if (rc) return rc;
@@ -983,27 +1111,34 @@ int Rank::run(const uint8_t* hdr, uint64_t file_len, const uint8_t* d_buf, uint6
   mark("all_to_all");
 
   // ---- 3 placement and stats on the device; the host sees one row per rank at the end ----
-  uint64_t spill_cap = 4096;
-  uint8_t* spill = cm_->spill.ensure(spill_cap * kSpillBytes);
-  uint8_t* flags = cm_->flags.ensure((4 + 4 * kSpillInline) * 8);
-  uint8_t* fun = cm_->fun.ensure(16);
-  uint8_t* fin = cm_->fin.ensure(12 * 8);
-  if (!spill || !flags || !fun || !fin) return fail(SPARKEY_E_GPU, "hipMalloc failed");
-  const int FL = 4 + 4 * kSpillInline;
+  // A rank whose step fails posts neutral rows (the identity carry function, no spilled slots) so
+  // that the others' steps stay in bounds, and its code in its finish row: every rank then fails.
   std::vector<int64_t> F((size_t)G_ * 12);
   bool fixed = true;
   for (;;) {
     const int64_t* digits = (const int64_t*)cm_->rows.p + (8 + G_);  // &rows[0][8 + G]
-    rc = sparkey_shard_summarize_dev(pl_, recv, n_recv, digits, RL, fixed ? 1 : 0, (int64_t*)fun, s_, err_, err_len_);
+    int lrc = sparkey_shard_summarize_dev(pl_, recv, n_recv, digits, RL, fixed ? 1 : 0, (int64_t*)fun, s_, err_, err_len_);
+    if (lrc) rc = gpu(hipMemsetAsync(fun, 0, 16, s_), "memset");
     if (!rc) rc = all_gather(fun, cm_->funs, 16);
-    if (!rc)
-      rc = sparkey_shard_place_dev(pl_, (const int64_t*)cm_->funs.p, d_out + hdr_off, spill, spill_cap, (int64_t*)flags,
-                                   kSpillInline, s_, err_, err_len_);
+    if (rc) return rc;
+    if (!lrc)
+      lrc = sparkey_shard_place_dev(pl_, (const int64_t*)cm_->funs.p, d_out + hdr_off, spill, spill_cap, (int64_t*)flags,
+                                    kSpillInline, s_, err_, err_len_);
+    if (lrc) rc = gpu(hipMemsetAsync(flags, 0, (uint64_t)FL * 8, s_), "memset");
     if (!rc) rc = all_gather(flags, cm_->frows, (uint64_t)FL * 8);
-    if (!rc) rc = sparkey_shard_finish_dev(pl_, (const int64_t*)cm_->frows.p, FL, kSpillInline, (int64_t*)fin, s_, err_, err_len_);
+    if (rc) return rc;
+    if (!lrc) lrc = sparkey_shard_finish_dev(pl_, (const int64_t*)cm_->frows.p, FL, kSpillInline, (int64_t*)fin, s_, err_, err_len_);
+    if (lrc) {
+      int64_t f[12] = {0};
+      f[3] = lrc;  // (a negative "aborted" flag: this rank failed)
+      rc = gpu(hipMemcpyAsync(fin, f, sizeof(f), hipMemcpyHostToDevice, s_), "H2D");
+    }
     if (!rc) rc = all_gather(fin, cm_->fins, 12 * 8);
-    if (!rc && g_ == 0) rc = sparkey_shard_header_dev(pl_, (const int64_t*)cm_->fins.p, 12, n_total, d_out, s_, err_, err_len_);
     if (!rc) rc = to_host(F.data(), cm_->fins.p, (uint64_t)G_ * 12 * 8);
+    if (rc) return rc;
+    std::vector<int64_t> codes(G_, 0);
+    for (int r = 0; r < G_; r++) codes[r] = F[(size_t)r * 12 + 3] < 0 ? F[(size_t)r * 12 + 3] : 0;
+    rc = fail_together(codes, lrc);
     if (rc) return rc;
     bool aborted = false;
     for (int r = 0; r < G_; r++) aborted = aborted || F[(size_t)r * 12 + 3] != 0;
@@ -1012,6 +1147,8 @@ int Rank::run(const uint8_t* hdr, uint64_t file_len, const uint8_t* d_buf, uint6
       continue;
     }
     if (aborted) return fail(SPARKEY_E_GPU, "sharded placement aborted");
+    if (g_ == 0) rc = sparkey_shard_header_dev(pl_, (const int64_t*)cm_->fins.p, 12, n_total, d_out, s_, err_, err_len_);
+    if (rc) return rc;
     break;
   }
   mark("place");
@@ -1084,6 +1221,39 @@ int Rank::run(const uint8_t* hdr, uint64_t file_len, const uint8_t* d_buf, uint6
 
 }  // namespace
 
+// One rank's sparkey_shard_build; rc0 != 0 (its log range could not be loaded, err holds why): the rank
+// still meets the others at the first checkpoint so that they all return the error.
+int shard_build_rank(sparkey_plan* plan, sparkey_shard_comm* comm, const uint8_t* log_header, uint64_t file_len,
+                     const uint8_t* d_buf, uint64_t buf_lo, uint64_t buf_hi, const sparkey_build_opts* opts,
+                     uint8_t* d_out, uint64_t out_cap, void* stream, sparkey_build_stats* stats_out, int rc0, char* err,
+                     size_t err_len) {
+  if (hipSetDevice(comm->device) != hipSuccess && !rc0) {
+    set_err(err, err_len, "hipSetDevice failed");
+    rc0 = SPARKEY_E_GPU;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  hipStream_t own = nullptr;
+  if (!s) {
+    if (hipStreamCreateWithFlags(&own, hipStreamNonBlocking) != hipSuccess) {
+      set_err(err, err_len, "hipStreamCreate failed");
+      own = nullptr;
+      if (!rc0) rc0 = SPARKEY_E_GPU;
+    }
+    s = own;
+  }
+  sparkey_build_stats st;
+  memset(&st, 0, sizeof(st));
+  const double t0 = now_ms();
+  Rank rank(plan, comm, s, err, err_len);
+  int rc = rank.run(log_header, file_len, d_buf, buf_lo, buf_hi, *opts, d_out, out_cap, &st, rc0);
+  if (rc) comm->coll->abort();  // (thread transport: release the other ranks)
+  if (s) (void)hipStreamSynchronize(s);
+  if (own) (void)hipStreamDestroy(own);
+  st.device_ms = now_ms() - t0;
+  if (stats_out) *stats_out = st;
+  return rc;
+}
+
 // ---------------------------------------------------------------------------------------------
 // C-ABI
 // ---------------------------------------------------------------------------------------------
@@ -1136,6 +1306,23 @@ int sparkey_shard_comm_create(sparkey_shard_comm** out, const uint8_t* id128, in
   return SPARKEY_OK;
 }
 
+int sparkey_shard_comm_create_host(sparkey_shard_comm** out, const sparkey_shard_transport* t, int32_t rank,
+                                   int32_t world, int32_t device, char* err, size_t err_len) {
+  if (!out || !t || !t->all_gather || !t->all_to_all || world < 1 || rank < 0 || rank >= world) {
+    set_err(err, err_len, "bad communicator arguments");
+    return SPARKEY_E_ARG;
+  }
+  if (hipSetDevice(device) != hipSuccess) {
+    set_err(err, err_len, "hipSetDevice failed");
+    return SPARKEY_E_GPU;
+  }
+  auto* cm = new sparkey_shard_comm();
+  cm->coll.reset(new HostColl(*t, rank, world));
+  cm->device = device;
+  *out = cm;
+  return SPARKEY_OK;
+}
+
 void sparkey_shard_comm_destroy(sparkey_shard_comm* cm) {
   if (!cm) return;
   (void)hipSetDevice(cm->device);
@@ -1172,30 +1359,8 @@ int sparkey_shard_build(sparkey_plan* plan, sparkey_shard_comm* comm, const uint
     set_err(err, err_len, "null argument");
     return SPARKEY_E_ARG;
   }
-  if (hipSetDevice(comm->device) != hipSuccess) {
-    set_err(err, err_len, "hipSetDevice failed");
-    return SPARKEY_E_GPU;
-  }
-  hipStream_t s = (hipStream_t)stream;
-  hipStream_t own = nullptr;
-  if (!s) {
-    if (hipStreamCreateWithFlags(&own, hipStreamNonBlocking) != hipSuccess) {
-      set_err(err, err_len, "hipStreamCreate failed");
-      return SPARKEY_E_GPU;
-    }
-    s = own;
-  }
-  sparkey_build_stats st;
-  memset(&st, 0, sizeof(st));
-  const double t0 = now_ms();
-  Rank rank(plan, comm, s, err, err_len);
-  int rc = rank.run(log_header, file_len, d_buf, buf_lo, buf_hi, *opts, d_out, out_cap, &st);
-  if (rc) comm->coll->abort();  // (thread transport: release the other ranks)
-  (void)hipStreamSynchronize(s);
-  if (own) (void)hipStreamDestroy(own);
-  st.device_ms = now_ms() - t0;
-  if (stats_out) *stats_out = st;
-  return rc;
+  return shard_build_rank(plan, comm, log_header, file_len, d_buf, buf_lo, buf_hi, opts, d_out, out_cap, stream,
+                          stats_out, SPARKEY_OK, err, err_len);
 }
 
 int32_t sparkey_shard_phase_count(const sparkey_shard_comm* comm) { return comm ? (int32_t)comm->phase.size() : 0; }
@@ -1223,16 +1388,19 @@ struct Group {  // communicators for one device list, kept across calls
   }
 };
 
+// Groups are shared: a build holds its group for its whole length, so sparkey_release_cached_resources
+// (which empties the map) never frees a group under a running build, and a failed group is dropped
+// from the map and freed when its last build ends.
 std::mutex g_groups_mu;
-std::map<std::pair<std::vector<int>, bool>, Group*> g_groups;
+std::map<std::pair<std::vector<int>, bool>, std::shared_ptr<Group>> g_groups;
 std::vector<std::vector<std::pair<std::string, double>>> g_multi_phases;  // per rank, the last build's
 
-Group* get_group(const std::vector<int>& devs, bool threads, std::string* why) {
+std::shared_ptr<Group> get_group(const std::vector<int>& devs, bool threads, std::string* why) {
   std::lock_guard<std::mutex> l(g_groups_mu);
   auto key = std::make_pair(devs, threads);
   auto it = g_groups.find(key);
   if (it != g_groups.end()) return it->second;
-  auto* gr = new Group();
+  auto gr = std::make_shared<Group>();
   gr->devices = devs;
   gr->threads = threads;
   const int n = (int)devs.size();
@@ -1246,15 +1414,11 @@ Group* get_group(const std::vector<int>& devs, bool threads, std::string* why) {
     }
   } else {
     const RcclApi* api = rccl_api(why);
-    if (!api) {
-      delete gr;
-      return nullptr;
-    }
+    if (!api) return nullptr;
     std::vector<ncclComm_t> cs(n);
     const ncclResult_t r = api->CommInitAll(cs.data(), n, devs.data());
     if (r != ncclSuccess) {
       *why = std::string("ncclCommInitAll: ") + api->GetErrorString(r);
-      delete gr;
       return nullptr;
     }
     for (int q = 0; q < n; q++) {
@@ -1272,10 +1436,9 @@ Group* get_group(const std::vector<int>& devs, bool threads, std::string* why) {
 
 int shard_devices(const sparkey_build_opts& o, std::vector<int>* devs, bool* threads, char* err, size_t err_len) {
   const int n = o.num_gpus;
-  const char* tr = getenv("SPARKEY_SHARD_TRANSPORT");
-  *threads = tr && strcmp(tr, "threads") == 0;
-  const bool same = tr && strcmp(tr, "threads-one-device") == 0;  // (tests: every rank on opts.device)
-  if (same) *threads = true;
+  const int64_t tr = sk::knob(sk::Knob::ShardTransport);  // (tests: 1 threads, 2 threads on opts.device)
+  *threads = tr == 1 || tr == 2;
+  const bool same = tr == 2;
   int count = 0;
   if (hipGetDeviceCount(&count) != hipSuccess) count = 0;
   devs->clear();
@@ -1295,13 +1458,14 @@ int shard_run_threads(const sparkey_build_opts& o, const ShardRankFn& fn, char* 
   int rc = shard_devices(o, &devs, &threads, err, err_len);
   if (rc) return rc;
   std::string why;
-  Group* gr = get_group(devs, threads, &why);
+  const std::shared_ptr<Group> gr = get_group(devs, threads, &why);
   if (!gr) {
     set_err(err, err_len, why);
     return SPARKEY_E_GPU;
   }
   std::lock_guard<std::mutex> l(gr->mu);
   const int n = (int)devs.size();
+  const bool same = n > 1 && devs[0] == devs[1];  // every rank on one device (tests)
   std::vector<int> rcs(n, SPARKEY_OK);
   std::vector<std::string> msgs(n);
   std::vector<std::thread> ts;
@@ -1309,7 +1473,7 @@ int shard_run_threads(const sparkey_build_opts& o, const ShardRankFn& fn, char* 
     ts.emplace_back([&, r] {
       char e[512] = {0};
       (void)hipSetDevice(devs[r]);
-      rcs[r] = fn(r, n, devs[r], gr->comms[r], e, sizeof(e));
+      rcs[r] = fn(r, n, devs[r], gr->comms[r], same, e, sizeof(e));
       msgs[r] = e;
       if (rcs[r]) gr->comms[r]->coll->abort();
     });
@@ -1319,22 +1483,23 @@ int shard_run_threads(const sparkey_build_opts& o, const ShardRankFn& fn, char* 
     g_multi_phases.resize(n);
     for (int r = 0; r < n; r++) g_multi_phases[r] = gr->comms[r]->phase;
   }
-  // the first rank's own error (not "another rank failed")
-  for (int r = 0; r < n; r++)
+  rc = SPARKEY_OK;
+  for (int r = 0; r < n && !rc; r++)  // the first rank's own error (not "another rank failed")
     if (rcs[r] && msgs[r].find("another rank") == std::string::npos) {
       set_err(err, err_len, msgs[r]);
-      if (threads) {  // a failed thread group is not reused (its barrier is aborted)
-        std::lock_guard<std::mutex> g2(g_groups_mu);
-        g_groups.erase(std::make_pair(devs, threads));
-      }
-      return rcs[r];
+      rc = rcs[r];
     }
-  for (int r = 0; r < n; r++)
+  for (int r = 0; r < n && !rc; r++)
     if (rcs[r]) {
       set_err(err, err_len, msgs[r]);
-      return rcs[r];
+      rc = rcs[r];
     }
-  return SPARKEY_OK;
+  if (rc) {  // a failed group is not reused (a thread group's barrier is aborted; fresh communicators)
+    std::lock_guard<std::mutex> g2(g_groups_mu);
+    auto it = g_groups.find(std::make_pair(devs, threads));
+    if (it != g_groups.end() && it->second == gr) g_groups.erase(it);
+  }
+  return rc;
 }
 
 extern "C" {
@@ -1343,9 +1508,11 @@ int32_t sparkey_multi_phase_count(int32_t rank) {
   return rank >= 0 && rank < (int32_t)g_multi_phases.size() ? (int32_t)g_multi_phases[rank].size() : 0;
 }
 const char* sparkey_multi_phase_name(int32_t rank, int32_t i) {
+  thread_local std::string name;  // (a copy: a concurrent build may replace the phases)
   std::lock_guard<std::mutex> l(g_groups_mu);
   if (rank < 0 || rank >= (int32_t)g_multi_phases.size() || i < 0 || i >= (int32_t)g_multi_phases[rank].size()) return "";
-  return g_multi_phases[rank][i].first.c_str();
+  name = g_multi_phases[rank][i].first;
+  return name.c_str();
 }
 double sparkey_multi_phase_ms(int32_t rank, int32_t i) {
   std::lock_guard<std::mutex> l(g_groups_mu);
@@ -1355,7 +1522,10 @@ double sparkey_multi_phase_ms(int32_t rank, int32_t i) {
 }  // extern "C"
 
 void shard_release_groups() {
-  std::lock_guard<std::mutex> l(g_groups_mu);
-  for (auto& kv : g_groups) delete kv.second;
-  g_groups.clear();
+  std::map<std::pair<std::vector<int>, bool>, std::shared_ptr<Group>> old;
+  {
+    std::lock_guard<std::mutex> l(g_groups_mu);
+    old.swap(g_groups);
+  }
+  // (each group is freed here, or by the build still holding it when that build ends)
 }

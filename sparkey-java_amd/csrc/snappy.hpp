@@ -33,6 +33,8 @@ struct SnappyWalk {
 constexpr uint32_t kWalkBadHeader = 1u;    // a record header runs past the block end or a VLQ > 5 bytes
 constexpr uint32_t kWalkTooMany = 2u;      // more records than maxEntriesPerBlock
 constexpr uint32_t kWalkBadStream = 4u;    // malformed Snappy stream
+constexpr uint32_t kWalkEofFirst = 8u;     // the block ends inside a record's first VLQ: the iterator ends there
+                                           // when it is the log's last block (SparkeyLogIterator.java:111-115)
 
 // The directory's state between k_snappy_dir launches (each follows the chain for up to a chunk of
 // blocks, so that the decode of one chunk overlaps the walk along the next).

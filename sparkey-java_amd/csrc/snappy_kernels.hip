@@ -10,6 +10,7 @@
 //   k_snappy_rewrite  one lane per slot: virtual offset -> (blockPosition << ebb) | entryIndex
 #include "device_common.hpp"
 #include "snappy.hpp"
+#include "knobs.hpp"
 
 namespace sk {
 
@@ -179,6 +180,12 @@ __device__ __forceinline__ void walk_block(const SnappyParams& S, uint64_t b, co
       continue;
     }
     const RecHdr h = decode_header(at, u, ulen);
+    if (h.rc == kEndOfLog) {  // (not a record: the host accepts this only in the last block)
+      flags |= kWalkEofFirst;
+      j--;
+      u = ulen;
+      break;
+    }
     if (h.rc || h.klen < 0 || h.vlen < 0) {
       flags |= kWalkBadHeader;
       break;
@@ -903,7 +910,7 @@ void launch_snappy_dir(const SnappyParams& S, hipStream_t s) { hipLaunchKernelGG
 
 hipError_t launch_snappy_decode(const SnappyParams& S, hipStream_t s) {
   if (S.nblk == 0) return hipSuccess;
-  static const bool gw = getenv("SPARKEY_SNAPPY_LDS") == nullptr;  // (A/B: the decoded block in LDS)
+  const bool gw = !knob_on(Knob::SnappyLds);  // (A/B: the decoded block in LDS)
   if (gw) {
     hipLaunchKernelGGL(k_snappy_gw<0>, dim3((uint32_t)S.nblk), 64, 0, s, S);
   } else if (S.lds_bytes) {

@@ -25,6 +25,7 @@
 #include "lookup.hpp"
 #include "append.hpp"
 #include "snappy.hpp"
+#include "knobs.hpp"
 
 using namespace sk;
 
@@ -280,6 +281,7 @@ struct ShardState {
 
 struct sparkey_plan {
   int device = 0;
+  bool shared_device = false;  // other builds run on this device concurrently (threads-one-device ranks)
   ShardState shard;
   uint64_t c_small = 0;
   uint64_t* small = nullptr;  // a few words of device scratch
@@ -287,7 +289,7 @@ struct sparkey_plan {
   uint64_t c_conv = 0, c_exitp = 0, c_qpos = 0, c_tail = 0, c_G = 0, c_cnt = 0, c_off = 0;
   uint64_t c_ent = 0, c_ent2 = 0, c_ent3 = 0;
   uint64_t c_bcount = 0, c_bcursor = 0, c_boff = 0, c_bfun = 0, c_bpre = 0, c_carry = 0;
-  uint64_t c_pdbg = 0, c_p1_fill = 0, c_bstat = 0;
+  uint64_t c_p1_fill = 0, c_bstat = 0;
   uint64_t* bstat_start = nullptr;  // folded stats: first slot of each bucket's written range
   uint64_t c_pairs = 0, c_parts = 0, c_su = 0, c_smp = 0, c_bft = 0;
   uint64_t c_desc = 0, c_p1h = 0, c_p1o = 0, c_dbg = 0, c_wcount = 0, c_woff = 0;
@@ -353,7 +355,6 @@ struct sparkey_plan {
   uint32_t epoch = 0;          // fused_carry builds so far (tags the dfun words)
   uint64_t* pairs = nullptr;
   StatPart* parts = nullptr;
-  unsigned long long* pdbg = nullptr;
   uint32_t* p1_fill = nullptr;
   uint64_t* scan_u64 = nullptr;
   MaxPlus* scan_mp = nullptr;
@@ -479,9 +480,9 @@ static int setup_params(const LogHdr& lh, const IndexParams& ip, const sparkey_b
       const int64_t bytes = std::max<int64_t>(0, lh.put_size) + std::max<int64_t>(0, lh.delete_size);
       if (nrec > 0 && bytes > 0 && 10 * bytes < 9 * nrec * P.max_rec_len) cmin = 1024;
     }
-    if (const char* v = getenv("SPARKEY_FRAME_CMIN")) cmin = std::max<int64_t>(128, atoll(v));
-    if (const char* v = getenv("SPARKEY_FRAME_REGION")) region = std::min<int64_t>(16384, std::max<int64_t>(2048, atoll(v)));
-    if (const char* v = getenv("SPARKEY_FRAME_LOOK")) look = std::min<int64_t>(4096, std::max<int64_t>(16, atoll(v)));
+    if (knob_set(Knob::FrameCmin)) cmin = std::max<int64_t>(128, knob(Knob::FrameCmin));
+    if (knob_set(Knob::FrameRegion)) region = std::min<int64_t>(16384, std::max<int64_t>(2048, knob(Knob::FrameRegion)));
+    if (knob_set(Knob::FrameLook)) look = std::min<int64_t>(4096, std::max<int64_t>(16, knob(Knob::FrameLook)));
     int cs = 7;
     while ((1ll << cs) < std::max<int64_t>(P.max_rec_len, cmin)) cs++;
     const int64_t C = 1ll << cs;
@@ -493,7 +494,7 @@ static int setup_params(const LogHdr& lh, const IndexParams& ip, const sparkey_b
     // their rounds best.
     const int64_t nrec_hdr = std::max<int64_t>(0, lh.num_puts) + std::max<int64_t>(0, lh.num_deletes);
     const int64_t bytes_hdr = std::max<int64_t>(0, lh.put_size) + std::max<int64_t>(0, lh.delete_size);
-    if (!getenv("SPARKEY_FRAME_REGION") && nrec_hdr > 0 && bytes_hdr > 0 && region / C >= 2) {
+    if (!knob_set(Knob::FrameRegion) && nrec_hdr > 0 && bytes_hdr > 0 && region / C >= 2) {
       const double mean = (double)bytes_hdr / (double)nrec_hdr;
       double best = -1.0;
       for (int64_t w = std::max<int64_t>(1, region / C / 2); w <= std::min<int64_t>(64, region / C); w++) {
@@ -523,7 +524,7 @@ static int setup_params(const LogHdr& lh, const IndexParams& ip, const sparkey_b
     P.fr_nchunks = any ? (uint64_t)((frame_end + C - 1) / C) - P.fr_k0 : 0;
   }
   P.emit_extra = lh.max_key_len + 32 <= kEmitExtra ? (int32_t)((lh.max_key_len + 32 + 15) & ~15LL) : 32;
-  P.uni_nt = getenv("SPARKEY_FRAME_NO_NT") ? 0u : 1u;  // framing stages the log non-temporally (read once)
+  P.uni_nt = 1u;  // framing stages the log non-temporally (read once: measured 10% faster)
   P.hash_size = ip.hash_size;
   P.addr_size = ip.addr_size;
   P.slot_size = ip.slot_size;
@@ -556,18 +557,18 @@ static int setup_params(const LogHdr& lh, const IndexParams& ip, const sparkey_b
 // wave (SPARKEY_FRAME_REGION).  The geometry is set on P when k_frame3 is chosen (k_frame can frame
 // with it too, which its fallback does).
 static bool want_frame3(BuildParams& P, const LogHdr& lh, int64_t entry, int64_t frame_end) {
-  if (getenv("SPARKEY_NO_FRAME3") || !P.fr_fast || P.max_rec_len > 4096) return false;
+  if (knob_on(Knob::NoFrame3) || !P.fr_fast || P.max_rec_len > 4096) return false;
   const int64_t nr = std::max<int64_t>(0, lh.num_puts) + std::max<int64_t>(0, lh.num_deletes);
   const int64_t by = std::max<int64_t>(0, lh.put_size) + std::max<int64_t>(0, lh.delete_size);
   if (nr <= 0 || by <= 0) return false;
   const double mean = (double)by / (double)nr;
   int64_t want = std::max<int64_t>(std::max<int64_t>(P.max_rec_len, 128), (int64_t)std::ceil(4.0 * mean));
-  if (const char* v = getenv("SPARKEY_FRAME3_C")) want = std::max<int64_t>(P.max_rec_len, atoll(v));
+  if (knob_set(Knob::Frame3C)) want = std::max<int64_t>(P.max_rec_len, knob(Knob::Frame3C));
   int cs = 7;
   while ((1ll << cs) < want) cs++;
   while (cs > 7 && (double)(1ll << cs) / mean > 8.0 && (1ll << (cs - 1)) >= P.max_rec_len) cs--;
   int64_t region = 8192;
-  if (const char* v = getenv("SPARKEY_FRAME_REGION")) region = std::min<int64_t>(16384, std::max<int64_t>(2048, atoll(v)));
+  if (knob_set(Knob::FrameRegion)) region = std::min<int64_t>(16384, std::max<int64_t>(2048, knob(Knob::FrameRegion)));
   BuildParams Q = P;
   const int64_t C = 1ll << cs;
   Q.fr_cshift = cs;
@@ -589,14 +590,13 @@ static bool want_frame3(BuildParams& P, const LogHdr& lh, int64_t entry, int64_t
   // when that is well above one, the starts reached by others are marked so that only chain heads
   // walk on (SPARKEY_FRAME3_COVER=0/1 forces it)
   Q.f3_cover = (double)Q.max_rec_len > 1.5 * mean ? 1 : 0;
-  if (const char* v = getenv("SPARKEY_FRAME3_COVER")) Q.f3_cover = atoi(v) ? 1 : 0;
+  if (knob_set(Knob::Frame3Cover)) Q.f3_cover = knob(Knob::Frame3Cover) ? 1 : 0;
   if (!frame3_fits(Q, mean, pk)) return false;
   // (C3's shape, pk 0.1: K = 3 measured 0.870 ms against K = 2's 0.903 per 10M records,
   // profiles/r03/k_frame3_sweep_c3_10m.txt)
   Q.f3_short = pk < 0.05 ? 2 : pk < 0.3 ? 3 : 4;
-  if (const char* v = getenv("SPARKEY_FRAME3_SHORT")) Q.f3_short = std::max(1, std::min(4, atoi(v)));
-  Q.f3_stop = getenv("SPARKEY_FRAME3_STOP") ? atoi(getenv("SPARKEY_FRAME3_STOP")) : -1;
-  Q.f3_noticket = getenv("SPARKEY_FRAME3_TICKET") ? 0 : 1;  // (frame3_kernels.hip: regions by workgroup id)
+  if (knob_set(Knob::Frame3Short)) Q.f3_short = (int32_t)std::max<int64_t>(1, std::min<int64_t>(4, knob(Knob::Frame3Short)));
+  Q.f3_stop = (int32_t)knob(Knob::Frame3Stop);
   P = Q;
   return true;
 }
@@ -605,13 +605,12 @@ static int64_t uniform_record_size(const LogHdr& lh) {
   const int64_t R =
       vlq_size_long(lh.max_key_len + 1) + vlq_size_long(lh.max_value_len) + lh.max_key_len + lh.max_value_len;
   if (lh.num_deletes == 0 && lh.num_puts > 0 && lh.max_key_len + 1 < 128 && lh.max_value_len < 128 && R <= 256 &&
-      lh.put_size == lh.num_puts * R && lh.data_end - kLogHeaderSize == lh.put_size && !getenv("SPARKEY_NO_UNIFORM"))
+      lh.put_size == lh.num_puts * R && lh.data_end - kLogHeaderSize == lh.put_size && !knob_on(Knob::NoUniform))
     return R;
   return 0;
 }
 
-// Wave geometry of one framing kernel: k_frame (chunks of 2^cshift, w per wave) or k_frame2
-// (segments of 2^cshift, w per wave).
+// Wave geometry of one framing kernel: chunks of 2^cshift bytes, w per wave.
 struct FrameGeom {
   int32_t cshift, w;
   uint64_t k0, nchunks;
@@ -622,54 +621,6 @@ static void set_geom(BuildParams& P, const FrameGeom& g) {
   P.fr_w = g.w;
   P.fr_k0 = g.k0;
   P.fr_nchunks = g.nchunks;
-}
-
-// k_frame2's geometry (frame2_kernels.hip): segments SEG = max(512, nextpow2(maxRecLen)) bytes,
-// S = 8 KiB / SEG of them per wave (2..32), each listing up to f2_lcap record starts (a log of
-// records far below 16 bytes on average overflows them and is framed by k_frame instead).
-// SPARKEY_FRAME2_SEG / SPARKEY_FRAME2_S override (measurements).
-// k_frame_lane's regions: R = max(8 KiB, the power of two >= maxRecLen) bytes per lane
-// (SPARKEY_LANE_REGION overrides), numbered from entry >> log2 R; none when the log's records do not
-// suit it (frame_lane_supported), unless SPARKEY_FRAME_LANE is set: on the C3 shape the ring walk
-// measured 1.16 ms per 10M records against k_frame3's 0.90, so k_frame3 frames
-// these logs by default.
-static FrameGeom lane_geometry(const BuildParams& P, int64_t entry, int64_t frame_end) {
-  FrameGeom g{0, 1, 0, 0};
-  if (!getenv("SPARKEY_FRAME_LANE") || getenv("SPARKEY_NO_LANE") || frame_end <= entry) return g;
-  int64_t want = 8192;
-  if (const char* v = getenv("SPARKEY_LANE_REGION")) want = std::max<int64_t>(256, atoll(v));
-  int cs = 8;
-  while ((1ll << cs) < std::max<int64_t>(want, P.max_rec_len)) cs++;
-  BuildParams Q = P;
-  Q.fr_cshift = cs;
-  if (!frame_lane_supported(Q)) return g;
-  g.cshift = cs;
-  g.k0 = (uint64_t)entry >> cs;
-  g.nchunks = (uint64_t)((frame_end + (1ll << cs) - 1) >> cs) - g.k0;
-  return g;
-}
-
-static FrameGeom frame2_geometry(BuildParams& P, int64_t entry, int64_t frame_end) {
-  int cs = 9;
-  while ((1ll << cs) < P.max_rec_len) cs++;
-  if (const char* v = getenv("SPARKEY_FRAME2_SEG")) {
-    int want = 8;
-    while ((1ll << want) < atoll(v)) want++;
-    cs = std::max(cs, want);
-  }
-  int64_t S = std::max<int64_t>(2, std::min<int64_t>(32, 8192 >> cs));
-  if (const char* v = getenv("SPARKEY_FRAME2_S")) S = std::max<int64_t>(2, std::min<int64_t>(32, atoll(v)));
-  const int64_t SEG = 1ll << cs;
-  S = std::max<int64_t>(2, std::min<int64_t>(S, 32768 / SEG));  // the wave's starts are 16-bit LDS offsets
-  P.f2_lcap = (int32_t)((std::min<int64_t>(SEG / 2 + 2, SEG / 16 + 8) + 1) & ~1ll);
-  const int64_t look = std::min<int64_t>(P.max_rec_len, 2048) + 32;
-  P.f2_rgn_bytes = (int32_t)((S * SEG + look + 1023) & ~1023ll);
-  FrameGeom g;
-  g.cshift = cs;
-  g.w = (int32_t)S;
-  g.k0 = (uint64_t)entry >> cs;
-  g.nchunks = frame_end > entry ? (uint64_t)((frame_end + SEG - 1) / SEG) - g.k0 : 0;
-  return g;
 }
 
 // Slab layout of the framing output and the workspace it needs (grown on demand).
@@ -702,8 +653,12 @@ static int reserve_for_framing(sparkey_plan* pl, BuildParams& P, int framing_pat
   P.frame_ticket = reinterpret_cast<unsigned int*>(pl->desc + 2 * nwaves);
   if (!pl->delp) HIP_TRY(hipMalloc(&pl->delp, (size_t)kDelParts * 16 * sizeof(unsigned long long)));
   P.del_parts = pl->delp;
-  P.fr_spin_ticks = 2000000000ull;  // 20 s of the 100 MHz wall clock
-  if (const char* v = getenv("SPARKEY_FRAME_SPIN_TICKS")) P.fr_spin_ticks = strtoull(v, nullptr, 10);  // (tests)
+  // a wave waits for its predecessor's exit at most 2 s of the 100 MHz wall clock; the host then
+  // redoes the framing on the serial walk (correct, slower).  With one wave per workgroup the
+  // predecessor is a lower workgroup id, which the dispatcher starts first; builds that share a
+  // device (fr_ticket) take regions by ticket instead, so no wave waits on one not yet started.
+  P.fr_spin_ticks = knob_set(Knob::FrameSpinTicks) ? (uint64_t)knob(Knob::FrameSpinTicks) : 200000000ull;
+  P.fr_ticket = pl->shared_device || knob_on(Knob::FrameTicket) ? 1 : 0;
   P.p1_hist = pl->p1_hist; P.p1_off = pl->p1_off; P.p1_off_total = pl->p1_off + 256ull * P.p1_tiles;
   return SPARKEY_OK;
 }
@@ -716,9 +671,7 @@ static int launch_framing(sparkey_plan* pl, const BuildParams& P, int framing_pa
     HIP_TRY(hipMemsetAsync(pl->desc, 0, (2 * nwaves + 2) * sizeof(unsigned long long), s));
     HIP_TRY(hipMemsetAsync(pl->wcount, 0, (P.nslabs + 1) * sizeof(uint32_t), s));
     if (P.del_parts) HIP_TRY(hipMemsetAsync(P.del_parts, 0, (size_t)kDelParts * 16 * sizeof(unsigned long long), s));
-    if (framing_path == 3) launch_frame2(P, s, &pl->timer);
-    else if (framing_path == 4) launch_frame3(P, s, &pl->timer);
-    else if (framing_path == 5) launch_frame_lane(P, s, &pl->timer);
+    if (framing_path == 4) launch_frame3(P, s, &pl->timer);
     else launch_frame_fused(P, s, &pl->timer);
     launch_sum_deletes(P, s);  // (the spread DELETE counters into the status block)
   } else if (framing_path == 2) {
@@ -768,25 +721,6 @@ static void print_part2_debug(const BuildParams& P) {
           sum[0] / 256, sum[1] / 256, sum[2] / 256, sum[3] / 256, sum[4] / 256, mx[0], mx[1], mx[2], mx[3], mx[4]);
 }
 
-static void print_place_debug(const BuildParams& P) {
-  if (!P.place_dbg) return;
-  const uint64_t nb = P.b_hi - P.b_lo;
-  std::vector<unsigned long long> h(8 * nb);
-  if (hipMemcpy(h.data(), P.place_dbg, h.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return;
-  double sum[8] = {0};
-  uint64_t n = 0;
-  for (uint64_t b = 0; b < nb; b++) {
-    if (!h[8 * b + 7]) continue;
-    n++;
-    for (int i = 0; i < 8; i++) sum[i] += (double)h[8 * b + i];
-  }
-  const double d = n ? (double)n : 1.0;
-  fprintf(stderr, "[k_place_lds] blocks=%llu mean cycles: head %.0f load %.0f scan+order %.0f groups %.0f "
-          "place %.0f write %.0f stats %.0f | total %.0f\n",
-          (unsigned long long)n, sum[0] / d, sum[1] / d, sum[2] / d, sum[3] / d, sum[4] / d, sum[5] / d, sum[6] / d,
-          sum[7] / d);
-}
-
 static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t* d_log, uint64_t log_len,
                       uint8_t* d_out, uint64_t index_cap, const sparkey_build_opts* opts, hipStream_t s,
                       sparkey_build_stats* stats_out, char* err, size_t err_len);
@@ -812,7 +746,7 @@ static int snappy_par_dir(sparkey_plan* pl, SnappyParams& S, hipStream_t s, int 
                                     : 32 + mb + mb / 6);
   if (sdir_screen_lds(H) > 150 * 1024) return SPARKEY_OK;   // (blocks over ~128 KiB: the serial chain)
   int64_t A = std::max<int64_t>(32 * H, body / (1 << 20) + 1);  // (screen 1/32 of the log; links of ~32 blocks)
-  if (const char* v = getenv("SPARKEY_SNAPPY_DIR_A")) A = std::max<int64_t>(H, atoll(v));  // (tests, tuning)
+  if (knob_set(Knob::SnappyDirA)) A = std::max<int64_t>(H, knob(Knob::SnappyDirA));  // (tests, tuning)
   const uint64_t nwin = body > H ? (uint64_t)((body - H - 1) / A + 1) : 0;
   const uint64_t maxl = nwin + 1;  // links
   const uint64_t bytes = nwin * (kSdirCand * 8 + 4 + 8) + (maxl + 1) * 8 + 4 * maxl * 8 + 64;
@@ -871,7 +805,7 @@ static int snappy_par_dir(sparkey_plan* pl, SnappyParams& S, hipStream_t s, int 
   HIP_TRY(hipMemcpyAsync(&hf, fail, 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
   if (hf) return SPARKEY_OK;
-  if (getenv("SPARKEY_SNAPPY_DIR_DEBUG"))
+  if (knob_on(Knob::SnappyDirDebug))
     fprintf(stderr, "[%s dir] parallel: %llu blocks, %llu windows, %llu links\n", codec ? "zstd" : "snappy", (unsigned long long)nb,
             (unsigned long long)nwin, (unsigned long long)nl);
   memset(dir, 0, sizeof(*dir));
@@ -933,7 +867,7 @@ static int plan_build_snappy(sparkey_plan* pl, const LogHdr& lh, const uint8_t* 
   if (zstd) {  // LDS: the decoded block, then the whole frame (k_zstd_decode)
     // decoded straight into the virtual log (LDS for the entropy tables only: many waves per CU)
     // measured 3x faster than the block and frame in LDS (one wave per CU); SPARKEY_ZSTD_LDS=1: that
-    S.lds_bytes = getenv("SPARKEY_ZSTD_LDS") ? zstd_lds_bytes(mb) : 0u;
+    S.lds_bytes = knob_on(Knob::ZstdLds) ? zstd_lds_bytes(mb) : 0u;
   } else {  // LDS: the decoded block, then an 8 KiB window over its stream (k_snappy_lds)
     const int64_t lds = ((mb + 15) & ~15LL) + 16 + 8192 + 16;
     S.lds_bytes = lds <= 160 * 1024 ? (uint32_t)lds : 0u;
@@ -963,7 +897,7 @@ static int plan_build_snappy(sparkey_plan* pl, const LogHdr& lh, const uint8_t* 
   SnappyDirResult dir;
   memset(&dir, 0, sizeof(dir));
   uint64_t chunk = kSnappyChunk;
-  if (const char* v = getenv("SPARKEY_SNAPPY_CHUNK")) chunk = std::max<uint64_t>(16, strtoull(v, nullptr, 10));  // tuning
+  if (knob_set(Knob::SnappyChunk)) chunk = std::max<uint64_t>(16, (uint64_t)knob(Knob::SnappyChunk));  // tuning
   auto pipeline = [&](int64_t vcap, bool decode) -> hipError_t {
     hipError_t e;
     if ((e = hipMemsetAsync(pl->sn_dir, 0, sizeof(SnappyDirResult), s)) != hipSuccess) return e;
@@ -1017,7 +951,7 @@ static int plan_build_snappy(sparkey_plan* pl, const LogHdr& lh, const uint8_t* 
   const uint64_t hdr_total = ps + ds < ps ? UINT64_MAX : ps + ds;
   const int64_t vcap0 = hdr_total <= 22 * body + 4096 ? (int64_t)hdr_total : 0;
   bool par = false;  // the directory in parallel, then every block decoded in one launch
-  if (!getenv("SPARKEY_SNAPPY_SERIAL_DIR")) {
+  if (!knob_on(Knob::SnappySerialDir)) {
     rc = snappy_par_dir(pl, S, s, zstd ? 1 : 0, &dir, &par, err, err_len);
     if (rc) return rc;
   }
@@ -1094,8 +1028,9 @@ static int plan_build_snappy(sparkey_plan* pl, const LogHdr& lh, const uint8_t* 
                                 std::to_string(blocks[b].file_pos));
       return SPARKEY_E_CORRUPT_RECORD;
     }
+    const bool last = b + 1 == nblk;
     if (carry == 0) {
-      if (w.flags) {
+      if (w.flags & ~(last ? kWalkEofFirst : 0u)) {
         set_err(err, err_len, (w.flags & kWalkTooMany)
                                   ? "Corrupt log file: more entries in a block than maxEntriesPerBlock"
                                   : "Corrupt log file: bad record header in block at " +
@@ -1189,8 +1124,8 @@ static int run_exact_segments(sparkey_plan* pl, BuildParams& P, bool in_memory, 
   HIP_TRY(hipMemsetAsync(P.seg_cnt, 0, P.cap * sizeof(uint32_t), s));
   HIP_TRY(hipMemsetAsync((uint8_t*)pl->d_status + offsetof(Status, num_entries), 0, 2 * sizeof(long long), s));
   HIP_TRY(hipMemsetAsync((uint8_t*)pl->d_status + offsetof(Status, n_segs), 0, sizeof(((Status*)0)->n_segs), s));
-  const char* dbg_env = getenv("SPARKEY_EXACT_DEBUG");
-  const bool seg_dbg = dbg_env != nullptr;
+  const int64_t dbg_level = knob(Knob::ExactDebug);
+  const bool seg_dbg = dbg_level > 0;
   if (seg_dbg) {
     HIP_TRY(grow(&pl->dbg, pl->c_dbg, kSegDebugWords));
     HIP_TRY(hipMemsetAsync(pl->dbg, 0, kSegDebugWords * sizeof(unsigned long long), s));
@@ -1206,7 +1141,7 @@ static int run_exact_segments(sparkey_plan* pl, BuildParams& P, bool in_memory, 
     HIP_TRY(hipEventCreateWithFlags(&pl->side.fork, hipEventDisableTiming));
     pl->side_ok = true;
   }
-  launch_segments(P, s, in_memory ? 0 : 1, &pl->timer, dbg_env && atoi(dbg_env) >= 2, &pl->side);
+  launch_segments(P, s, in_memory ? 0 : 1, &pl->timer, dbg_level >= 2, &pl->side);
   if (seg_dbg) {
     std::vector<unsigned long long> h(kSegDebugWords);
     HIP_TRY(hipMemcpyAsync(h.data(), pl->dbg, h.size() * 8, hipMemcpyDeviceToHost, s));
@@ -1269,27 +1204,13 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
   uint8_t hdr[kIndexHeaderSize];
   index_header_template(lh, ip, opts->hash_seed, hdr);
 
-  // k_frame2 for records of mixed sizes (the header's mean record at least 24 bytes), k_frame for
-  // the rest; both fall back to the serial walk
-  bool use_frame2 = fused_framing && getenv("SPARKEY_FRAME2") != nullptr;  // (measured slower than k_frame so far)
-  {
-    const int64_t nr = std::max<int64_t>(0, lh.num_puts) + std::max<int64_t>(0, lh.num_deletes);
-    const int64_t by = std::max<int64_t>(0, lh.put_size) + std::max<int64_t>(0, lh.delete_size);
-    // (a log with DELETEs lets 0x00 bytes start records: zero-filled values then hold long
-    // plausible chains of 2-byte records, which k_frame's per-chunk screen handles better)
-    if ((nr > 0 && by < 24 * nr) || lh.num_deletes != 0) use_frame2 = false;
-  }
-  // k_frame3 for one-byte-VLQ logs whose chunks hold a few records each (its lists' sizes)
-  const bool use_frame3 = fused_framing && !use_frame2 &&
-                          want_frame3(P, lh, kLogHeaderSize, std::max<int64_t>(lh.data_end, kLogHeaderSize));
+  // k_frame3 for one-byte-VLQ logs whose chunks hold a few records each (its lists' sizes), k_frame
+  // for the rest; both fall back to the serial walk, which alone reports errors
+  const bool use_frame3 = fused_framing && want_frame3(P, lh, kLogHeaderSize, std::max<int64_t>(lh.data_end, kLogHeaderSize));
   const FrameGeom geom0 = get_geom(P);
-  const FrameGeom geom2 = frame2_geometry(P, kLogHeaderSize, std::max<int64_t>(lh.data_end, kLogHeaderSize));
-  // k_frame_lane (frame_lane_kernels.hip): one lane per region of R bytes walks and hashes its records
-  const FrameGeom geom5 = lane_geometry(P, kLogHeaderSize, std::max<int64_t>(lh.data_end, kLogHeaderSize));
-  const bool use_lane = fused_framing && !use_frame2 && geom5.nchunks > 0;
-  // SPARKEY_SERIAL_FRAMING forces the exact serial walk (smoke() and tests check every framing path)
-  const bool force_serial = getenv("SPARKEY_SERIAL_FRAMING") != nullptr;
-  const int spec_path = fused_framing && !force_serial ? (use_frame2 ? 3 : (use_lane ? 5 : (use_frame3 ? 4 : 0))) : 1;
+  // the serial_framing switch forces the exact serial walk (smoke() and the tests check every path)
+  const bool force_serial = knob_on(Knob::SerialFraming);
+  const int spec_path = fused_framing && !force_serial ? (use_frame3 ? 4 : 0) : 1;
   int framing_path = spec_path, placement_path = 0;
   if (const int64_t R = force_serial ? 0 : uniform_record_size(lh)) {  // k_frame_uniform: every record is exactly R bytes
     framing_path = 2;
@@ -1304,32 +1225,20 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
     const uint64_t nw = std::max<uint64_t>(1, g.nchunks ? (g.nchunks + g.w - 1) / g.w : 0);
     return (uint32_t)std::min<uint64_t>(kPartTile, std::max<uint64_t>(64, 2 * ((nrec + nw - 1) / nw) + 32));
   };
-  auto geom_of = [&](int path) -> const FrameGeom& { return path == 3 ? geom2 : path == 5 ? geom5 : geom0; };
-  uint32_t slab_cap = slab_for(geom_of(framing_path));
-  int slab_path = framing_path;
-  bool use_regions = getenv("SPARKEY_NO_REGIONS") == nullptr, regions_used = false;
-  bool use_fixed = getenv("SPARKEY_NO_P2_FIXED") == nullptr;  // k_part2s in one pass (fixed bucket regions)
-  const bool fold = getenv("SPARKEY_NO_FOLD_STATS") == nullptr;  // stats from k_place_lds, no k_stats pass
+  uint32_t slab_cap = slab_for(geom0);
+  bool use_regions = !knob_on(Knob::NoRegions), regions_used = false;
+  bool use_fixed = true;  // k_part2st / k_part2s in one pass into fixed bucket regions
+  set_geom(P, geom0);
   for (int attempt = 0; attempt < 6; attempt++) {
-    set_geom(P, geom_of(framing_path));
-    if (slab_framing(framing_path) && framing_path != slab_path) {
-      slab_cap = slab_for(geom_of(framing_path));
-      slab_path = framing_path;
-    }
     rc = reserve_for_framing(pl, P, framing_path, nrec, slab_cap, err, err_len);
     if (rc) return rc;
-    if (getenv("SPARKEY_FRAME_DEBUG")) {  // per-wave phase counters: 16 words per k_frame / k_frame2 wave
+    if (knob_on(Knob::FrameDebug)) {  // per-wave phase counters: 16 words per k_frame / k_frame3 wave
       const uint64_t nw = std::max<uint64_t>(std::max<uint64_t>(P.nchunks, P.fr_nchunks ? (P.fr_nchunks + P.fr_w - 1) / P.fr_w : 0), 1);
       HIP_TRY(grow(&pl->dbg, pl->c_dbg, 16 * nw));
       HIP_TRY(hipMemsetAsync(pl->dbg, 0, 16 * nw * sizeof(unsigned long long), s));
       P.dbg = pl->dbg;
     }
-    if (getenv("SPARKEY_PLACE_DEBUG")) {
-      HIP_TRY(grow(&pl->pdbg, pl->c_pdbg, 8 * P.nbuckets));
-      HIP_TRY(hipMemsetAsync(pl->pdbg, 0, 8 * P.nbuckets * sizeof(unsigned long long), s));
-      P.place_dbg = pl->pdbg;
-    }
-    if (getenv("SPARKEY_PART2_DEBUG")) {
+    if (knob_on(Knob::Part2Debug)) {
       HIP_TRY(grow(&pl->dbg, pl->c_dbg, 8 * 256));
       HIP_TRY(hipMemsetAsync(pl->dbg, 0, 8 * 256 * sizeof(unsigned long long), s));
       P.part_dbg = pl->dbg;
@@ -1343,13 +1252,13 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
     const bool tiles = framing_path == 2 && P.slab_cap == (uint32_t)kPartTile && P.part_group == 1;
     // the other framings' slabs: pass 1 into the same fixed digit regions by k_part1_regions (one read
     // of the entries instead of k_part1_hist + k_part1_scatter's two)
-    const bool slab_regions = !tiles && !getenv("SPARKEY_NO_P1_REGIONS");
+    const bool slab_regions = !tiles;
     P.p1_region = 0;
     P.p1_kernel = 0;
     if ((tiles || slab_regions) && use_regions) {
       const double expect = (double)nrec * (double)P.bpp * (double)kBucket / (double)P.cap;
       uint64_t rc_cap = ((uint64_t)(expect + 8.0 * std::sqrt(expect) + 1024.0) + 63) & ~63ull;
-      if (const char* e = getenv("SPARKEY_REGION_CAP")) rc_cap = std::max<uint64_t>(1, strtoull(e, nullptr, 10));  // (tests)
+      if (knob_set(Knob::RegionCap)) rc_cap = std::max<uint64_t>(1, (uint64_t)knob(Knob::RegionCap));  // (tests)
       HIP_TRY(grow(&pl->ent2, pl->c_ent2, 256 * rc_cap));
       HIP_TRY(grow(&pl->ent3, pl->c_ent3, 256 * rc_cap));
       HIP_TRY(grow(&pl->p1_fill, pl->c_p1_fill, 256));
@@ -1365,15 +1274,16 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
     P.p1_hist_ready = tiles && !P.p1_region ? 1 : 0;
     regions_used = P.p1_region != 0 && !P.p1_kernel;  // (partition passes: 1 when the framing did pass 1)
     // k_part2s: pass 2 also sorts each bucket by wanted slot and leaves the carry functions
-    P.p2_sorted = P.bpp <= kP2SortedMaxBpp && !getenv("SPARKEY_NO_P2_SORTED") ? 1 : 0;
+    P.p2_sorted = P.bpp <= kP2SortedMaxBpp ? 1 : 0;
     P.p2_fixed = P.p2_sorted && use_fixed ? 1 : 0;
     if (P.p2_fixed) {  // bucket b's entries at ent2[b * kPlaceLdsMax ..)
       HIP_TRY(grow(&pl->ent2, pl->c_ent2, std::max<uint64_t>(P.max_records, P.nbuckets * (uint64_t)kPlaceLdsMax)));
       P.ent2 = pl->ent2;
     }
-    P.fold_stats = fold ? 1 : 0;
-    // the carry composition inside k_part2s (its fixed-region pass), no summary / scan / carry kernels
-    P.fused_carry = P.p2_fixed && P.fold_stats && !getenv("SPARKEY_NO_FUSED_CARRY") ? 1 : 0;
+    P.fold_stats = 1;  // the stats parts from the placement (k_stats only for buckets it could not place)
+    // the carry composition inside k_part2st / k_part2s (their fixed-region pass), no summary / scan /
+    // carry kernels
+    P.fused_carry = P.p2_fixed ? 1 : 0;
     P.dfun = pl->dfun;
     P.dcarry = pl->dcarry;
     if (P.fused_carry) {
@@ -1392,34 +1302,25 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
     HIP_TRY(hipStreamSynchronize(s));
     HIP_TRY(hipEventElapsedTime(&ms, pl->ev0, pl->ev1));
     print_frame_debug(pl, P);
-    print_place_debug(P);
     print_part2_debug(P);
     if (slab_framing(framing_path) && st.max_wave_count > slab_cap) {  // a wave overflowed its slab
       slab_cap = (uint32_t)std::min<uint64_t>(kPartTile, ((uint64_t)st.max_wave_count + 63) & ~63ull);
-      continue;
-    }
-    if (framing_path == 3 && (st.spec_fail & 16u) && st.err == ~0ull) {  // a segment's record list overflowed
-      framing_path = 0;
       continue;
     }
     if (st.overflow || st.n_records > P.max_records) {  // header under-counts records: grow and redo
       nrec = std::max<uint64_t>(st.n_records, nrec * 2 + 1);
       continue;
     }
-    if (getenv("SPARKEY_FRAME_DEBUG") && (st.spec_fail || st.err != ~0ull))
+    if (knob_on(Knob::FrameDebug) && (st.spec_fail || st.err != ~0ull))
       fprintf(stderr, "[framing] path %d: spec_fail %u err %llx (pos %llu)\n", framing_path, st.spec_fail,
               (unsigned long long)st.err, (unsigned long long)(st.err >> 8));
     // (a digit region filled by k_part1_regions is the partition's business, not the framing's)
     const unsigned fspec = st.spec_fail & ~(P.p1_kernel ? kSpecRegionFull : 0u);
-    if (framing_path == 5 && (fspec || st.err != ~0ull)) {  // regions left unresolved: k_frame3 / k_frame
-      framing_path = use_frame3 ? 4 : 0;
-      continue;
-    }
     if (framing_path == 4 && (fspec || st.err != ~0ull)) {  // k_frame3's lists or speculation: k_frame
       framing_path = 0;
       continue;
     }
-    if ((framing_path == 0 || framing_path == 3) && (fspec || st.err != ~0ull)) {  // only the serial walk reports
+    if (framing_path == 0 && (fspec || st.err != ~0ull)) {  // only the serial walk reports
       framing_path = 1;
       continue;
     }
@@ -1463,7 +1364,7 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
   // exactly: per independent slot segment of the canonical PUT placement (placement_path 2), or,
   // when that placement left no empty slot, on one lane over the whole table (placement_path 1).
   if (st.n_deletes > 0 || st.dup || st.dup_overflow || st.full || st.n_pairs > P.pair_cap) {
-    const bool serial = st.full || getenv("SPARKEY_EXACT_SERIAL") != nullptr;
+    const bool serial = st.full || knob_on(Knob::ExactSerial);
     placement_path = serial ? 1 : 2;
     P.p1_hist_ready = 0;  // the exact path's partitions (DELETEs left out) count their own digits
     P.p2_sorted = 0;
@@ -1523,6 +1424,11 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
 
 // LogHeader.read with the file's real length (file_build.cpp): the dataEnd > file length check
 // (LogHeader.java:81-83) needs it.
+// Ranks of one sharded build that share a device (file_build.cpp): framing takes regions by ticket.
+void sk_plan_set_shared_device(sparkey_plan* pl, bool shared) {
+  if (pl) pl->shared_device = shared;
+}
+
 int sk_check_log_header(const uint8_t* b, uint64_t hdr_len, uint64_t file_len, char* err, size_t err_len) {
   LogHdr lh;
   return parse_log_header(b, hdr_len, file_len, &lh, err, err_len, true);
@@ -1701,6 +1607,48 @@ int sparkey_get_batch(sparkey_plan* pl, const uint8_t* d_log, uint64_t log_len, 
   return SPARKEY_OK;
 }
 
+// Batched HashType.hash (+ getWantedSlot) on device keys: the build kernels' own device functions.
+int sparkey_hash_batch(sparkey_plan* pl, const uint8_t* d_keys, const uint64_t* d_key_off, uint64_t n,
+                       int32_t hash_size, int32_t hash_seed, uint64_t capacity, uint64_t* d_hash, uint64_t* d_slot,
+                       void* stream, char* err, size_t err_len) {
+  if (!pl || (n && (!d_keys || !d_key_off || !d_hash))) {
+    set_err(err, err_len, "null argument");
+    return SPARKEY_E_ARG;
+  }
+  if (hash_size != 4 && hash_size != 8) {
+    set_err(err, err_len, "Can't support hash size " + std::to_string(hash_size));
+    return SPARKEY_E_ARG;
+  }
+  HIP_TRY(hipSetDevice(pl->device));
+  hipStream_t s = stream ? (hipStream_t)stream : pl->own_stream;
+  LookupParams L;
+  memset(&L, 0, sizeof(L));
+  L.keys = d_keys;
+  L.key_off = d_key_off;
+  L.n = n;
+  L.hash_size = hash_size;
+  L.seed = (uint32_t)hash_seed;
+  if (capacity) L.mod = make_fastmod(capacity);
+  launch_hash_batch(L, d_hash, capacity ? d_slot : nullptr, s);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(s));
+  return SPARKEY_OK;
+}
+
+int sparkey_wanted_slot_batch(sparkey_plan* pl, const uint64_t* d_hash, uint64_t n, uint64_t capacity,
+                              uint64_t* d_slot, void* stream, char* err, size_t err_len) {
+  if (!pl || capacity == 0 || (n && (!d_hash || !d_slot))) {
+    set_err(err, err_len, "null argument or zero capacity");
+    return SPARKEY_E_ARG;
+  }
+  HIP_TRY(hipSetDevice(pl->device));
+  hipStream_t s = stream ? (hipStream_t)stream : pl->own_stream;
+  launch_slot_batch(d_hash, n, make_fastmod(capacity), d_slot, s);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(s));
+  return SPARKEY_OK;
+}
+
 const char* sparkey_strerror(int code) { return code_message(code); }
 
 int sparkey_plan_create(sparkey_plan** plan_out, int32_t device, uint64_t max_log_bytes, uint64_t max_records,
@@ -1772,7 +1720,7 @@ void sparkey_plan_destroy(sparkey_plan* pl) {
   (void)hipSetDevice(pl->device);
   void* bufs[] = {pl->conv, pl->exitp, pl->qpos, pl->tail, pl->G, pl->cnt, pl->off, pl->ent, pl->ent2, pl->ent3,
                   pl->bcount, pl->bcursor, pl->boff, pl->bfun, pl->bpre, pl->bfun_total, pl->carry, pl->pairs,
-                  pl->dfun, pl->dcarry, pl->parts, pl->pdbg, pl->p1_fill, pl->scan_u64, pl->scan_mp, pl->desc, pl->p1_hist, pl->p1_off, pl->d_status, pl->dbg, pl->wcount, pl->woff, pl->small,
+                  pl->dfun, pl->dcarry, pl->parts, pl->p1_fill, pl->scan_u64, pl->scan_mp, pl->desc, pl->p1_hist, pl->p1_off, pl->d_status, pl->dbg, pl->wcount, pl->woff, pl->small,
                   pl->eseg, pl->seg_cnt, pl->seg_off, pl->seg_mark, pl->seg_start, pl->bstat_start,
                   pl->seg_cls_cnt, pl->seg_cls_off, pl->p2tab,
                   pl->app_i64, pl->app_u32, pl->app_u64, pl->app_scan, pl->app_map,
@@ -1944,11 +1892,11 @@ int sparkey_shard_find_entry(sparkey_plan* pl, uint64_t lo, uint64_t window, voi
 // synchronous sparkey_shard_frame and the speculative sparkey_shard_frame_bin_async).
 struct ShardFrameSetup {
   BuildParams P;
-  bool fused = false, use_frame2 = false, use_frame3 = false, use_regions = true;
-  int spec_path() const { return fused ? (use_frame2 ? 3 : (use_frame3 ? 4 : 0)) : 1; }
+  bool fused = false, use_frame3 = false, use_regions = true;
+  int spec_path() const { return fused && !knob_on(Knob::SerialFraming) ? (use_frame3 ? 4 : 0) : 1; }
   int framing_path = 1;
   uint64_t nrec = 0;
-  FrameGeom geom0, geom2;
+  FrameGeom geom0;
   uint32_t slab_cap = 0;
   int slab_path = 0;
 };
@@ -1973,15 +1921,8 @@ static int shard_frame_setup(sparkey_plan* pl, int64_t entry, int64_t frame_end,
   const double frac = (double)(frame_end - entry) / (double)std::max<int64_t>(1, data_end - kLogHeaderSize);
   F->nrec = (uint64_t)((double)(std::max<int64_t>(0, sh.lh.num_puts) + std::max<int64_t>(0, sh.lh.num_deletes)) *
                        frac * 1.05) + 4096;
-  F->use_frame2 = F->fused && getenv("SPARKEY_FRAME2") != nullptr;
-  {
-    const int64_t nr = std::max<int64_t>(0, sh.lh.num_puts) + std::max<int64_t>(0, sh.lh.num_deletes);
-    const int64_t by = std::max<int64_t>(0, sh.lh.put_size) + std::max<int64_t>(0, sh.lh.delete_size);
-    if ((nr > 0 && by < 24 * nr) || sh.lh.num_deletes != 0) F->use_frame2 = false;
-  }
-  F->use_frame3 = F->fused && !F->use_frame2 && want_frame3(P, sh.lh, entry, frame_end);
+  F->use_frame3 = F->fused && want_frame3(P, sh.lh, entry, frame_end);
   F->geom0 = get_geom(P);
-  F->geom2 = frame2_geometry(P, entry, frame_end);
   F->framing_path = F->spec_path();
   const int64_t R = uniform_record_size(sh.lh);
   if (R && (entry - kLogHeaderSize) % R == 0) {  // a record start of a uniform log: frame by stride
@@ -1990,18 +1931,18 @@ static int shard_frame_setup(sparkey_plan* pl, int64_t entry, int64_t frame_end,
     P.uni_rec = R;
     F->nrec = P.uni_n;
   }
-  F->slab_cap = shard_slab_for(F->framing_path == 3 ? F->geom2 : F->geom0, F->nrec);
+  F->slab_cap = shard_slab_for(F->geom0, F->nrec);
   F->slab_path = F->framing_path;
-  F->use_regions = getenv("SPARKEY_NO_REGIONS") == nullptr;
+  F->use_regions = !knob_on(Knob::NoRegions);
   return SPARKEY_OK;
 }
 
 // Launches one framing attempt of the set-up (status reset first); no synchronisation.
 static int shard_frame_launch(sparkey_plan* pl, ShardFrameSetup* F, hipStream_t s, char* err, size_t err_len) {
   BuildParams& P = F->P;
-  set_geom(P, F->framing_path == 3 ? F->geom2 : F->geom0);
+  set_geom(P, F->geom0);
   if (slab_framing(F->framing_path) && F->framing_path != F->slab_path) {
-    F->slab_cap = shard_slab_for(F->framing_path == 3 ? F->geom2 : F->geom0, F->nrec);
+    F->slab_cap = shard_slab_for(F->geom0, F->nrec);
     F->slab_path = F->framing_path;
   }
   int rc = reserve_for_framing(pl, P, F->framing_path, F->nrec, F->slab_cap, err, err_len);
@@ -2074,15 +2015,11 @@ static int shard_frame_sync(sparkey_plan* pl, int64_t entry, int64_t frame_end, 
       F.nrec = std::max<uint64_t>(st.n_records, F.nrec * 2 + 1);
       continue;
     }
-    if (path == 3 && (st.spec_fail & 16u) && st.err == ~0ull) {  // a segment's record list overflowed
-      F.framing_path = 0;
-      continue;
-    }
     if (path == 4 && (st.spec_fail || st.err != ~0ull)) {
       F.framing_path = 0;
       continue;
     }
-    if ((path == 0 || path == 3) && (st.spec_fail || st.err != ~0ull)) {
+    if (path == 0 && (st.spec_fail || st.err != ~0ull)) {
       F.framing_path = 1;
       continue;
     }
@@ -2318,8 +2255,8 @@ int sparkey_shard_summarize_dev(sparkey_plan* pl, const uint8_t* d_recv, uint64_
     // regions of the rank's range, the carry functions from the same pass.  A bucket that outgrows its
     // region sets p2_overflow: every later kernel skips, the flags row says "aborted", and the host
     // redoes the step with fixed_regions = 0 (dense runs)
-    P.p2_sorted = P.bpp <= kP2SortedMaxBpp && !getenv("SPARKEY_NO_P2_SORTED") ? 1 : 0;
-    P.p2_fixed = P.p2_sorted && fixed_regions && !getenv("SPARKEY_NO_P2_FIXED") ? 1 : 0;
+    P.p2_sorted = P.bpp <= kP2SortedMaxBpp ? 1 : 0;
+    P.p2_fixed = P.p2_sorted && fixed_regions ? 1 : 0;
     if (P.p2_fixed) {
       HIP_TRY(grow(&pl->ent2, pl->c_ent2, std::max<uint64_t>(n_recv, (P.b_hi - P.b_lo) * (uint64_t)kPlaceLdsMax)));
       P.ent2 = pl->ent2;
@@ -2367,7 +2304,7 @@ int sparkey_shard_place_dev(sparkey_plan* pl, const int64_t* d_funs, uint8_t* d_
   P.carry_funs = d_funs;
   P.carry_world = sh.world;
   P.carry_rank = sh.rank;
-  P.fold_stats = getenv("SPARKEY_NO_FOLD_STATS") ? 0 : 1;  // k_place_lds leaves the stats parts
+  P.fold_stats = 1;  // k_place_reg leaves the stats parts
   launch_carry(P, s);  // (also clears the placement's counters)
   launch_place_buckets(P, s);
   launch_shard_flags(P, s, d_flags, inline_cap);
@@ -2390,7 +2327,7 @@ int sparkey_shard_finish_dev(sparkey_plan* pl, const int64_t* d_rows, int32_t st
   P.prev_hash = 0;
   P.prev_occ = 0;
   if (P.slot_hi > P.slot_lo) {
-    if (P.fold_stats) {  // the parts k_place_lds left; k_stats only if some bucket bypassed it
+    if (P.fold_stats) {  // the parts k_place_reg left; k_stats only if some bucket bypassed it
       launch_stats_folded_shard(P, s);
       BuildParams Q = P;
       Q.stats_if_pending = 1;
@@ -2591,7 +2528,7 @@ int sparkey_shard_exact_frame(sparkey_plan* pl, int64_t entry, int64_t frame_end
   }
   // the canonical step's framing left its slabs in place: no second framing (the counts below check it)
   bool reuse = sh.slabs_ok && n_records >= 0 && entry == sh.slabs_entry && frame_end == sh.slabs_end &&
-               sh.P_frame.ent == pl->ent && sh.P_frame.wcount == pl->wcount && !getenv("SPARKEY_EXACT_REFRAME");
+               sh.P_frame.ent == pl->ent && sh.P_frame.wcount == pl->wcount && !knob_on(Knob::ExactReframe);
   for (int pass = 0; pass < 2; pass++) {
     if (reuse) {
       sh.n_local = entry < frame_end ? (uint64_t)n_records : 0;
@@ -2697,7 +2634,7 @@ int sparkey_shard_exact_build(sparkey_plan* pl, const uint8_t* d_recv, uint64_t 
     const uint64_t cap = sh.ip.cap;
     const uint64_t len = b == a ? cap : ((uint64_t)b + cap - (uint64_t)a) % cap;
     IndexParams ipl = sh.ip;
-    ipl.cap = getenv("SPARKEY_EXACT_FULL_TABLE") ? cap : len;
+    ipl.cap = knob_on(Knob::ExactFullTable) ? cap : len;
     ipl.addr_size = 8;
     ipl.ebb = 0;
     ipl.slot_size = ipl.hash_size + 8;

@@ -110,6 +110,21 @@ _lib.sparkey_shard_comm_unique_id.restype = ctypes.c_int
 _lib.sparkey_shard_comm_create.argtypes = [ctypes.POINTER(_vp), _vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                            ctypes.c_char_p, ctypes.c_size_t]
 _lib.sparkey_shard_comm_create.restype = ctypes.c_int
+_AG_FN = ctypes.CFUNCTYPE(ctypes.c_int, _vp, _vp, _vp, ctypes.c_uint64)
+_A2A_FN = ctypes.CFUNCTYPE(ctypes.c_int, _vp, _vp, ctypes.POINTER(ctypes.c_uint64), _vp, ctypes.POINTER(ctypes.c_uint64))
+
+
+class ShardTransport(ctypes.Structure):
+    _fields_ = [("ctx", _vp), ("all_gather", _AG_FN), ("all_to_all", _A2A_FN)]
+
+
+_lib.sparkey_shard_comm_create_host.argtypes = [ctypes.POINTER(_vp), ctypes.POINTER(ShardTransport), ctypes.c_int32,
+                                                ctypes.c_int32, ctypes.c_int32, ctypes.c_char_p, ctypes.c_size_t]
+_lib.sparkey_shard_comm_create_host.restype = ctypes.c_int
+_lib.sparkey_build_index_sharded_device.argtypes = [_vp, ctypes.c_uint64, ctypes.POINTER(_vp), ctypes.POINTER(_vp),
+                                                    ctypes.POINTER(BuildOpts), ctypes.POINTER(BuildStats),
+                                                    ctypes.c_char_p, ctypes.c_size_t]
+_lib.sparkey_build_index_sharded_device.restype = ctypes.c_int
 _lib.sparkey_shard_comm_destroy.argtypes = [_vp]
 _lib.sparkey_shard_comm_destroy.restype = None
 _lib.sparkey_shard_geometry.argtypes = [_vp, ctypes.c_uint64, ctypes.POINTER(BuildOpts), ctypes.c_int32, ctypes.c_int32,
@@ -137,6 +152,42 @@ _lib.sparkey_multi_phase_ms.restype = ctypes.c_double
 
 _lib.sparkey_file_last_phases.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.c_int32]
 _lib.sparkey_file_last_phases.restype = ctypes.c_int32
+_lib.sparkey_debug_set.argtypes = [ctypes.c_char_p, ctypes.c_int64]
+_lib.sparkey_debug_set.restype = ctypes.c_int
+_lib.sparkey_debug_get.argtypes = [ctypes.c_char_p]
+_lib.sparkey_debug_get.restype = ctypes.c_int64
+
+
+def debug_set(name: str, value) -> None:
+    """Sets a test / diagnostic switch (csrc/knobs.hpp; None or a negative value unsets it).  No switch
+    changes a build's bytes: each forces a device path or geometry the default choice would not take."""
+    v = -1 if value is None or value is False else (1 if value is True else int(value))
+    if _lib.sparkey_debug_set(name.encode(), v) != OK:
+        raise ValueError(f"unknown switch {name!r}")
+
+
+def debug_get(name: str) -> int:
+    v = int(_lib.sparkey_debug_get(name.encode()))
+    if v == E_ARG:
+        raise ValueError(f"unknown switch {name!r}")
+    return v
+
+
+class debug:
+    """with debug(no_uniform=1, serial_framing=1): ... -- switches set for the block, restored after."""
+
+    def __init__(self, **kv):
+        self.kv = kv
+
+    def __enter__(self):
+        self.old = {k: debug_get(k) for k in self.kv}
+        for k, v in self.kv.items():
+            debug_set(k, v)
+        return self
+
+    def __exit__(self, *a):
+        for k, v in self.old.items():
+            debug_set(k, v)
 
 
 def file_last_phases() -> dict:
@@ -162,6 +213,61 @@ def shard_unique_id() -> bytes:
     return buf.raw
 
 
+def _torch_transport(group=None) -> ShardTransport:
+    """sparkey_shard_transport over torch.distributed (the default group, or `group`) on host buffers."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    def view(ptr, n):
+        if n == 0:
+            return torch.empty(0, dtype=torch.uint8)
+        return torch.from_numpy(np.ctypeslib.as_array((ctypes.c_uint8 * n).from_address(ptr)))
+
+    def all_gather(ctx, send, recv, nbytes):
+        try:
+            w = dist.get_world_size(group)
+            if nbytes:
+                dist.all_gather_into_tensor(view(recv, nbytes * w), view(send, nbytes).clone(), group=group)
+            return 0
+        except Exception:  # noqa: BLE001  (reported to the library as a failed collective)
+            return 1
+
+    def all_to_all(ctx, send, send_bytes, recv, recv_bytes):
+        try:
+            w = dist.get_world_size(group)
+            sb = [int(send_bytes[r]) for r in range(w)]
+            rb = [int(recv_bytes[r]) for r in range(w)]
+            inp = view(send, sum(sb)).clone()
+            out = torch.empty(sum(rb), dtype=torch.uint8)
+            dist.all_to_all_single(out, inp, rb, sb, group=group)
+            if sum(rb):
+                view(recv, sum(rb)).copy_(out)
+            return 0
+        except Exception:  # noqa: BLE001
+            return 1
+
+    t = ShardTransport(None, _AG_FN(all_gather), _A2A_FN(all_to_all))
+    t._keep = (all_gather, all_to_all)
+    return t
+
+
+def build_index_sharded_device(log_header: bytes, file_len: int, d_bufs, d_outs, opts: BuildOpts) -> BuildStats:
+    """The multi-GPU build over device-resident log ranges (sparkey_build_index_sharded_device):
+    d_bufs[r] / d_outs[r] are device addresses of rank r's log range and .spi part
+    (shard_geometry(..., r, opts.num_gpus))."""
+    n = len(d_bufs)
+    bufs = (_vp * n)(*[ctypes.c_void_p(int(x)) for x in d_bufs])
+    outs = (_vp * n)(*[ctypes.c_void_p(int(x)) for x in d_outs])
+    stats = BuildStats()
+    err = ctypes.create_string_buffer(512)
+    rc = _lib.sparkey_build_index_sharded_device(log_header, file_len, bufs, outs, ctypes.byref(opts),
+                                                 ctypes.byref(stats), err, 512)
+    if rc != OK:
+        raise_for(rc, err.value.decode(errors="replace"))
+    return stats
+
+
 def shard_geometry(log_header: bytes, file_len: int, opts, rank: int, world: int):
     """(buf_lo, buf_hi, out_off, out_len): the log bytes rank `rank` holds and the .spi bytes it makes."""
     v = [ctypes.c_uint64() for _ in range(4)]
@@ -174,12 +280,20 @@ def shard_geometry(log_header: bytes, file_len: int, opts, rank: int, world: int
 
 
 class ShardComm:
-    """RCCL communicator of one rank of the sharded build (sparkey_shard_comm_create)."""
+    """Communicator of one rank of the sharded build: RCCL (sparkey_shard_comm_create), or, with
+    `group`, the collectives of a torch.distributed process group on host buffers
+    (sparkey_shard_comm_create_host: e.g. gloo, to rehearse several ranks on one GPU)."""
 
-    def __init__(self, unique_id: bytes, rank: int, world: int, device: int):
+    def __init__(self, unique_id: bytes, rank: int, world: int, device: int, group=None):
         h = ctypes.c_void_p()
         err = ctypes.create_string_buffer(512)
-        rc = _lib.sparkey_shard_comm_create(ctypes.byref(h), unique_id, rank, world, device, err, 512)
+        self._transport = None
+        if group is not None or unique_id is None:
+            self._transport = _torch_transport(group)
+            rc = _lib.sparkey_shard_comm_create_host(ctypes.byref(h), ctypes.byref(self._transport), rank, world, device,
+                                                     err, 512)
+        else:
+            rc = _lib.sparkey_shard_comm_create(ctypes.byref(h), unique_id, rank, world, device, err, 512)
         if rc != OK:
             raise_for(rc, err.value.decode(errors="replace"))
         self._h = h
@@ -259,6 +373,9 @@ _SIGS = {
                            + _E, ctypes.c_int),
     "sparkey_get_batch": ([_vp, _vp, ctypes.c_uint64, _vp, ctypes.c_uint64, _vp, _vp, ctypes.c_uint64, _vp, _vp, _vp]
                           + _E, ctypes.c_int),
+    "sparkey_hash_batch": ([_vp, _vp, _vp, ctypes.c_uint64, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint64, _vp, _vp,
+                            _vp] + _E, ctypes.c_int),
+    "sparkey_wanted_slot_batch": ([_vp, _vp, ctypes.c_uint64, ctypes.c_uint64, _vp, _vp] + _E, ctypes.c_int),
 }
 for _name, (_args, _res) in _SIGS.items():
     _f = getattr(_lib, _name)
@@ -272,7 +389,8 @@ EXPORTED = list(_SIGS) + ["sparkey_build_index_file", "sparkey_build_index_mem",
             "sparkey_shard_comm_create", "sparkey_shard_comm_destroy", "sparkey_shard_geometry", "sparkey_shard_build",
             "sparkey_shard_phase_count", "sparkey_shard_phase_name", "sparkey_shard_phase_ms",
             "sparkey_multi_phase_count", "sparkey_multi_phase_name", "sparkey_multi_phase_ms",
-            "sparkey_file_last_phases"]
+            "sparkey_file_last_phases", "sparkey_debug_set", "sparkey_debug_get", "sparkey_shard_comm_create_host",
+            "sparkey_build_index_sharded_device"]
 
 
 class SparkeyIOError(OSError):
@@ -310,7 +428,7 @@ def raise_for(code: int, msg: str):
 def make_opts(hash_size=0, hash_seed=0, sparsity=0.0, max_memory=1 << 62, method=METHOD_IN_MEMORY, device=0,
               num_gpus=0):
     """num_gpus > 1: sparkey_build_index_file / _mem shard the log over devices device .. device + num_gpus - 1
-    (SPARKEY_SHARD_TRANSPORT=threads-one-device: every rank on `device`, for tests on one GPU)."""
+    (the shard_transport switch = 2: every rank on `device`, for tests on one GPU)."""
     return BuildOpts(hash_size, ctypes.c_int32(hash_seed).value, float(sparsity), int(max_memory), int(method),
                      int(device), int(num_gpus), 0)
 
@@ -410,6 +528,24 @@ class Plan:
                                     ctypes.c_void_p(d_keys), ctypes.c_void_p(d_key_off), n,
                                     ctypes.c_void_p(d_value_pos), ctypes.c_void_p(d_value_len),
                                     ctypes.c_void_p(stream), err, 512)
+        if rc != OK:
+            raise_for(rc, err.value.decode(errors="replace"))
+
+    def hash_batch(self, d_keys: int, d_key_off: int, n: int, hash_size: int, seed: int, capacity: int, d_hash: int,
+                   d_slot: int = 0, stream: int = 0) -> None:
+        """Batched HashType.hash (+ getWantedSlot when capacity > 0) on device keys (sparkey_hash_batch)."""
+        err = ctypes.create_string_buffer(512)
+        rc = _lib.sparkey_hash_batch(self._h, ctypes.c_void_p(d_keys), ctypes.c_void_p(d_key_off), n, hash_size,
+                                     ctypes.c_int32(seed).value, capacity, ctypes.c_void_p(d_hash),
+                                     ctypes.c_void_p(d_slot or None), ctypes.c_void_p(stream), err, 512)
+        if rc != OK:
+            raise_for(rc, err.value.decode(errors="replace"))
+
+    def wanted_slot_batch(self, d_hash: int, n: int, capacity: int, d_slot: int, stream: int = 0) -> None:
+        """Long.remainderUnsigned(hash, capacity) per hash on the device (sparkey_wanted_slot_batch)."""
+        err = ctypes.create_string_buffer(512)
+        rc = _lib.sparkey_wanted_slot_batch(self._h, ctypes.c_void_p(d_hash), n, capacity, ctypes.c_void_p(d_slot),
+                                            ctypes.c_void_p(stream), err, 512)
         if rc != OK:
             raise_for(rc, err.value.decode(errors="replace"))
 

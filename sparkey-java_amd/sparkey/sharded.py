@@ -32,7 +32,6 @@ Collectives go through torch.distributed: backend "nccl" (RCCL over xGMI) moves 
 from __future__ import annotations
 
 import contextlib
-import os
 import struct
 import time
 from dataclasses import dataclass, field
@@ -99,16 +98,25 @@ def parse_log_header(header: bytes) -> dict:
     return dict(zip(keys, f))
 
 
+def _switch(name: str) -> bool:
+    """The library's test switch `name` (sparkey_debug_get), False where the library is not loaded
+    (the CPU simulation of the device steps)."""
+    try:
+        from . import _native
+    except ImportError:
+        return False
+    return _native.debug_get(name) > 0
+
+
 def uniform_record_size(h: dict) -> int:
     """R when the header proves every record is a PUT of exactly R bytes (no DELETE, one-byte VLQs,
     putSize == numPuts * R == dataEnd - 84); else 0.  Mirrors uniform_record_size in sparkey_gpu.cpp:
     the shard entries are then arithmetic (each rank's framing still checks every record header)."""
-    import os
     k, v = int(h["max_key_len"]), int(h["max_value_len"])
     r = _vlq_size(k + 1) + _vlq_size(v) + k + v
     ok = (h["num_deletes"] == 0 and h["num_puts"] > 0 and k + 1 < 128 and v < 128 and r <= 256 and
           h["put_size"] == h["num_puts"] * r and h["data_end"] - LOG_HEADER_SIZE == h["put_size"] and
-          not os.environ.get("SPARKEY_NO_UNIFORM"))
+          not _switch("no_uniform"))
     return r if ok else 0
 
 
@@ -458,7 +466,7 @@ class ShardedBuilder:
                     framed.add(entries[g])
                     # (one rank: the entries stay in place, bounded by the plan's own workspace)
                     cap = (1 << 62) if G == 1 else s.frame_capacity(entries[g], fe)
-                    if os.environ.get("SPARKEY_SHARD_SYNC_FRAME"):  # (tests: every attempt is retried)
+                    if _switch("shard_sync_frame"):  # (tests: every attempt is retried)
                         cap = 0
                     send = None if G == 1 else s.alloc(max(1, cap) * ENTRY_BYTES)
                     s.frame_bin_async(entries[g], fe, send, cap, row)

@@ -27,3 +27,19 @@ def native():
     sk_build.build()
     from sparkey import _native
     return _native
+
+
+@pytest.fixture
+def switch(native):
+    """switch(name=value, ...): sets the library's test switches (sparkey_debug_set) for this test;
+    every switch it touched is unset again at teardown."""
+    touched = set()
+
+    def set_(**kv):
+        for k, v in kv.items():
+            native.debug_set(k, v)
+            touched.add(k)
+
+    yield set_
+    for k in touched:
+        native.debug_set(k, None)

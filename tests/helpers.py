@@ -105,3 +105,11 @@ def same_error(native, log: bytes, seed: int = 1, **opts_kw):
         raise AssertionError("the GPU build accepts a log the oracle rejects (code %d)" % want)
     assert java_class(got) == java_class(want), (got, want)
     return got, want
+
+
+def with_trailing_bytes(log: bytes, tail: bytes) -> bytes:
+    """The log with `tail` appended and dataEnd moved to the file's end: the iterator then reads `tail`
+    as the start of one more record."""
+    out = bytearray(log) + tail
+    struct.pack_into("<q", out, 32, len(out))
+    return bytes(out)

@@ -122,17 +122,17 @@ def test_header_sizes_zero_or_absurd(native, put_size, delete_size):
 
 @pytest.mark.parametrize("block_size", [1024, 4096, 16384])
 @pytest.mark.parametrize("spacing", ["default", "min"])
-def test_parallel_directory(native, block_size, spacing, monkeypatch, capfd):
+def test_parallel_directory(native, block_size, spacing, switch, capfd):
     """The parallel block directory (windows, anchors, checked links) gives the serial chain's
-    directory: the same .spi as the oracle and as SPARKEY_SNAPPY_SERIAL_DIR, with the anchors as
+    directory: the same .spi as the oracle and as the serial chain (snappy_serial_dir), with the anchors as
     dense as the window length allows or at the default spacing."""
     from sparkey import synth
     log = synth.snappy_log(synth.fixed_log(30000, 16, 100, seed=block_size), 118, block_size).tobytes()
     if spacing == "min":
-        monkeypatch.setenv("SPARKEY_SNAPPY_DIR_A", "1")
-    monkeypatch.setenv("SPARKEY_SNAPPY_DIR_DEBUG", "1")
+        switch(snappy_dir_a=1)
+    switch(snappy_dir_debug=1)
     got = check(native, log, seed=99)
     assert "[snappy dir] parallel" in capfd.readouterr().err
-    monkeypatch.setenv("SPARKEY_SNAPPY_SERIAL_DIR", "1")
+    switch(snappy_serial_dir=1)
     serial, _ = native.build_index_mem(log, native.make_opts(hash_seed=99))
     assert got == serial

@@ -4,7 +4,6 @@ scenarios (CorrectnessTest, LargeFilesTest, IndexHashTest, WriteHashBenchmark) a
 Integer/byte work: the bar is bit-exact.
 """
 import numpy as np
-import os
 
 import pytest
 
@@ -14,7 +13,7 @@ from helpers import diff_report, index_header, key_value_puts, make_log, random_
 pytestmark = pytest.mark.gpu
 
 IN_MEMORY, SORTING = 1, 2
-SPEC = (0, 4, 5)  # the speculative framings of mixed-size records: k_frame, k_frame3, k_frame_lane (one-byte VLQs)
+SPEC = (0, 4)  # the speculative framings of mixed-size records: k_frame, k_frame3 (one-byte VLQs)
 
 
 def gpu_build(native, log, seed, hash_size=0, method=IN_MEMORY, sparsity=0.0):
@@ -212,14 +211,10 @@ def test_understated_max_key_len_is_an_error(native):
     struct.pack_into("<q", log, 40, 3)  # maxKeyLen := 3 < real key lengths: the reference throws
     got, want = same_error(native, bytes(log))  # IndexOutOfBoundsException (SparkeyLogIterator.java:130)
     assert got == want == native.E_CORRUPT_RECORD
-    for env in ({"SPARKEY_NO_UNIFORM": "1"}, {"SPARKEY_NO_FRAME3": "1"}, {"SPARKEY_SERIAL_FRAMING": "1"}):
-        os.environ.update(env)
-        try:
+    for sw in ({"no_uniform": 1}, {"no_frame3": 1}, {"serial_framing": 1}):
+        with native.debug(**sw):
             got, _ = same_error(native, bytes(log))
-        finally:
-            for k in env:
-                del os.environ[k]
-        assert got == native.E_CORRUPT_RECORD, env
+        assert got == native.E_CORRUPT_RECORD, sw
 
 
 def test_header_hides_deletes(native):
@@ -236,19 +231,17 @@ def test_header_hides_deletes(native):
 def test_tiny_records_stay_on_fast_framing(native):
     puts = random_puts(60000, seed=5, kmin=0, kmax=3, vmin=0, vmax=2)
     got, stats = check(native, make_log(puts), 17, hash_size=8)
-    assert stats.framing_path in (0, 5), stats.as_dict()
+    assert stats.framing_path == 0, stats.as_dict()
 
 
 # --- k_frame geometry overrides (chunk 256..2048 bytes, region, look-ahead): same bytes, fast path ---
-@pytest.mark.parametrize("env", [{"SPARKEY_FRAME_CMIN": "256"}, {"SPARKEY_FRAME_CMIN": "1024"},
-                                 {"SPARKEY_FRAME_CMIN": "2048"}, {"SPARKEY_FRAME_REGION": "16384"},
-                                 {"SPARKEY_FRAME_LOOK": "16"}, {"SPARKEY_FRAME_LOOK": "1024"}])
-def test_frame_geometry_overrides(native, monkeypatch, env):
-    monkeypatch.setenv("SPARKEY_NO_UNIFORM", "1")  # the fixed-size log would take k_frame_uniform
-    monkeypatch.setenv("SPARKEY_NO_FRAME3", "1")   # k_frame's geometry (k_frame3: test_frame3_geometry)
-    monkeypatch.setenv("SPARKEY_NO_LANE", "1")     # (k_frame_lane: test_lane_geometry)
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
+@pytest.mark.parametrize("sw", [{"frame_cmin": 256}, {"frame_cmin": 1024}, {"frame_cmin": 2048},
+                                {"frame_region": 16384}, {"frame_look": 16}, {"frame_look": 1024},
+                                {"frame_ticket": 1}])
+def test_frame_geometry_overrides(native, switch, sw):
+    switch(no_uniform=1)  # the fixed-size log would take k_frame_uniform
+    switch(no_frame3=1)   # k_frame's geometry (k_frame3: test_frame3_geometry)
+    switch(**sw)
     rng = np.random.default_rng(3)
     puts = [(b"%016d" % i, rng.integers(0, 256, 100, dtype=np.uint8).tobytes()) for i in range(40000)]
     got, stats = check(native, make_log(puts), 23, hash_size=8)
@@ -258,64 +251,20 @@ def test_frame_geometry_overrides(native, monkeypatch, env):
     assert stats.framing_path == 0, stats.as_dict()
 
 
-# --- k_frame2 geometry (segment bytes, segments per wave): same bytes on the mixed-record path ---
-@pytest.mark.parametrize("seg,nseg", [("512", "2"), ("512", "16"), ("512", "32"), ("1024", "8"), ("2048", "4"),
-                                      ("4096", "2"), ("8192", "3")])
-def test_frame2_geometry(native, monkeypatch, seg, nseg):
-    monkeypatch.setenv("SPARKEY_FRAME2", "1")
-    monkeypatch.setenv("SPARKEY_FRAME2_SEG", seg)
-    monkeypatch.setenv("SPARKEY_FRAME2_S", nseg)
-    for seed, (kmin, kmax, vmin, vmax), hs in [(41, (1, 40, 0, 60), 8), (43, (8, 64, 100, 100), 4),
-                                               (47, (1, 200, 0, 300), 8)]:
-        puts = random_puts(25000, seed=seed, kmin=kmin, kmax=kmax, vmin=vmin, vmax=vmax)
-        got, stats = check(native, make_log(puts), seed, hash_size=hs)
-        assert stats.framing_path == 3, stats.as_dict()
-
-
-def test_frame2_list_overflow_falls_back_to_k_frame(native, monkeypatch):
-    """A stretch of 2-3 byte records inside a log of long ones: more starts in a segment than k_frame2
-    lists, so the build reruns with k_frame (same bytes)."""
-    puts = random_puts(4000, seed=51, kmin=30, kmax=60, vmin=100, vmax=120)
-    puts += [(bytes([i & 0xFF, i >> 8]), b"") for i in range(3000)]
-    puts += random_puts(4000, seed=52, kmin=30, kmax=60, vmin=100, vmax=120)
-    seen, uniq = set(), []
-    for k, v in puts:
-        if k not in seen:
-            seen.add(k)
-            uniq.append((k, v))
-    monkeypatch.setenv("SPARKEY_FRAME2", "1")
-    got, stats = check(native, make_log(uniq), 53, hash_size=8)
-    assert stats.framing_path in SPEC, stats.as_dict()
-
-
-def test_frame2_with_overwrites(native, monkeypatch):
-    """Overwritten keys (no DELETE): k_frame2 frames, the exact replay places."""
-    rng = np.random.default_rng(57)
-    ops = [("put", b"key-%05d" % int(rng.integers(0, 20000)), rng.integers(0, 256, int(rng.integers(20, 90)),
-                                                                          dtype=np.uint8).tobytes())
-           for _ in range(60000)]
-    monkeypatch.setenv("SPARKEY_FRAME2", "1")
-    got, stats = check(native, make_log(ops=ops), 59, hash_size=8)
-    assert stats.framing_path == 3 and stats.placement_path == 2, stats.as_dict()
-
-
-def test_deletes_take_k_frame(native, monkeypatch):
-    monkeypatch.setenv("SPARKEY_FRAME2", "1")
-    """A log with DELETEs (0x00 starts a record) and zero-filled values frames with k_frame."""
+def test_deletes_take_k_frame(native):
+    """A log with DELETEs (0x00 starts a record) and zero-filled values frames speculatively."""
     ops = _churn_ops(60000, 20000, 0.1, 57, klen=(8, 40), vlen=(20, 90))
     got, stats = check(native, make_log(ops=ops), 59, hash_size=8)
     assert stats.framing_path in SPEC and stats.placement_path == 2, stats.as_dict()
 
 
 # --- k_frame's bounded wait on the previous wave: a tripped wait reruns the build on the serial path ---
-def test_frame_wait_timeout_falls_back_to_serial(native, monkeypatch):
-    monkeypatch.setenv("SPARKEY_NO_UNIFORM", "1")
-    monkeypatch.setenv("SPARKEY_NO_LANE", "1")  # (k_frame_lane has no waits)
-    monkeypatch.setenv("SPARKEY_FRAME_SPIN_TICKS", "0")  # any wait for a predecessor trips at once
+def test_frame_wait_timeout_falls_back_to_serial(native, switch):
+    switch(no_uniform=1, frame_spin_ticks=0)  # any wait for a predecessor trips at once
     puts = random_puts(120000, seed=31, kmin=1, kmax=40, vmin=0, vmax=60)
     got, stats = check(native, make_log(puts), 37, hash_size=8)
     assert stats.framing_path == 1, stats.as_dict()
-    monkeypatch.delenv("SPARKEY_FRAME_SPIN_TICKS")
+    switch(frame_spin_ticks=None)
     got2, stats2 = check(native, make_log(puts), 37, hash_size=8)
     assert stats2.framing_path in SPEC and got2 == got
 
@@ -344,10 +293,10 @@ def test_exact_segments_churn(native, method, n, nkeys, p_del):
 
 
 @pytest.mark.parametrize("method", [IN_MEMORY, SORTING])
-def test_exact_segments_equal_serial_replay(native, monkeypatch, method):
+def test_exact_segments_equal_serial_replay(native, switch, method):
     log = make_log(ops=_churn_ops(30000, 8000, 0.25, seed=3))
     seg, st1 = gpu_build(native, log, 77, 4, method)
-    monkeypatch.setenv("SPARKEY_EXACT_SERIAL", "1")
+    switch(exact_serial=1)
     ser, st2 = gpu_build(native, log, 77, 4, method)
     assert st1.placement_path == 2 and st2.placement_path == 1
     assert seg == ser, diff_report(seg, ser)
@@ -426,26 +375,25 @@ def test_uniform_header_but_record_split_differs(native):
     assert stats.framing_path in SPEC, stats.as_dict()
 
 
-def test_uniform_disabled_gives_same_bytes(native, monkeypatch):
+def test_uniform_disabled_gives_same_bytes(native, switch):
     log = make_log(_uniform_puts(40000, 16, 100))
     a, sa = gpu_build(native, log, 11, 8)
-    monkeypatch.setenv("SPARKEY_NO_UNIFORM", "1")
+    switch(no_uniform=1)
     b, sb = gpu_build(native, log, 11, 8)
     assert sa.framing_path == 2 and sb.framing_path in SPEC and a == b
 
 
-@pytest.mark.parametrize("region_cap", ["60000", "1"])
-def test_uniform_digit_regions(native, monkeypatch, region_cap):
+@pytest.mark.parametrize("region_cap", [60000, 1])
+def test_uniform_digit_regions(native, switch, region_cap):
     """k_frame_uniform as partition pass 1 (entries straight into digit regions of ent3): a region
     that fills up (forced with a region capacity of 1) redoes the build with the separate pass; both
     give the reference's bytes, and so does the separate pass by request."""
     log = make_log(_uniform_puts(50000, 16, 40, seed=3))
     want, _ = gpu_build(native, log, 21, 8)
-    monkeypatch.setenv("SPARKEY_REGION_CAP", region_cap)
+    switch(region_cap=region_cap)
     got, stats = check(native, log, 21, hash_size=8)
     assert stats.framing_path == 2 and got == want
-    monkeypatch.delenv("SPARKEY_REGION_CAP")
-    monkeypatch.setenv("SPARKEY_NO_REGIONS", "1")
+    switch(region_cap=None, no_regions=1)
     b, _ = gpu_build(native, log, 21, 8)
     assert b == want
 
@@ -523,18 +471,15 @@ def test_log_append_then_build(native):
 
 
 # --- k_frame3: the short/long walk framing of one-byte-VLQ logs ---
-@pytest.mark.parametrize("env", [{}, {"SPARKEY_FRAME3_C": "256"}, {"SPARKEY_FRAME3_C": "512"},
-                                 {"SPARKEY_FRAME3_C": "2048"}, {"SPARKEY_FRAME_REGION": "16384"},
-                                 {"SPARKEY_FRAME_REGION": "4096"}, {"SPARKEY_FRAME_REGION": "6144"},
-                                 {"SPARKEY_FRAME3_WG": "4"}, {"SPARKEY_FRAME3_WG": "4", "SPARKEY_FRAME3_TICKET": "1"},
-                                 {"SPARKEY_FRAME3_TICKET": "1"},
-                                 {"SPARKEY_FRAME_LOOK": "16"}, {"SPARKEY_FRAME_LOOK": "1024"}])
-def test_frame3_geometry(native, monkeypatch, env):
-    """Chunk sizes, regions and look-aheads: the same bytes; k_frame3 frames in the default geometry
-    (a geometry whose lists cannot hold a chunk's records reruns with k_frame)."""
-    monkeypatch.setenv("SPARKEY_NO_LANE", "1")
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
+@pytest.mark.parametrize("sw", [{}, {"frame3_c": 256}, {"frame3_c": 512}, {"frame3_c": 2048},
+                                {"frame_region": 16384}, {"frame_region": 4096}, {"frame_region": 6144},
+                                {"frame_ticket": 1}, {"frame3_short": 2}, {"frame3_cover": 1},
+                                {"frame_look": 16}, {"frame_look": 1024}])
+def test_frame3_geometry(native, switch, sw):
+    """Chunk sizes, regions, look-aheads and the ticket launch: the same bytes; k_frame3 frames in the
+    default geometry (a geometry whose lists cannot hold a chunk's records reruns with k_frame)."""
+    switch(**sw)
+    env = sw
     for seed, (kmin, kmax, vmin, vmax), hs in [(61, (8, 64, 100, 100), 8), (63, (1, 40, 20, 60), 4),
                                                (67, (10, 100, 0, 60), 8)]:
         puts = random_puts(25000, seed=seed, kmin=kmin, kmax=kmax, vmin=vmin, vmax=vmax)
@@ -542,13 +487,12 @@ def test_frame3_geometry(native, monkeypatch, env):
         assert stats.framing_path == 4 if not env else stats.framing_path in SPEC, stats.as_dict()
 
 
-def test_frame3_matches_k_frame(native, monkeypatch):
+def test_frame3_matches_k_frame(native, switch):
     """The same mixed log through k_frame3 and k_frame: identical bytes (and the oracle's)."""
     puts = random_puts(60000, seed=71, kmin=8, kmax=64, vmin=100, vmax=100)
     log = make_log(puts)
-    monkeypatch.setenv("SPARKEY_NO_LANE", "1")
     a, sa = check(native, log, 71, hash_size=8)
-    monkeypatch.setenv("SPARKEY_NO_FRAME3", "1")
+    switch(no_frame3=1)
     b, sb = gpu_build(native, log, 71, 8)
     assert sa.framing_path == 4 and sb.framing_path == 0 and a == b
 
@@ -585,65 +529,26 @@ def test_frame3_understated_header(native):
     check(native, bytes(log), 79, hash_size=8)
 
 
-def test_frame3_wait_timeout(native, monkeypatch):
-    monkeypatch.setenv("SPARKEY_FRAME_SPIN_TICKS", "0")
-    monkeypatch.setenv("SPARKEY_NO_LANE", "1")  # (k_frame_lane has no waits)
+def test_frame3_wait_timeout(native, switch):
+    switch(frame_spin_ticks=0)
     puts = random_puts(120000, seed=81, kmin=8, kmax=64, vmin=100, vmax=100)
     got, stats = check(native, make_log(puts), 83, hash_size=8)
     assert stats.framing_path == 1, stats.as_dict()
 
 
-# --- k_frame_lane: one lane per region walks and hashes its records; regions whose screened entry
-#     was a false start are walked again from the previous region's exit ---
-@pytest.mark.parametrize("region", [None, "256", "512", "4096", "65536"])
-def test_lane_geometry(native, monkeypatch, region):
-    """Region sizes from a few records to many: the oracle's bytes, on k_frame_lane."""
-    monkeypatch.setenv("SPARKEY_FRAME_LANE", "1")  # (opt-in: k_frame3 frames these logs by default)
-    if region:
-        monkeypatch.setenv("SPARKEY_LANE_REGION", region)
-    for seed, (kmin, kmax, vmin, vmax), hs in [(81, (8, 64, 100, 100), 8), (83, (1, 40, 20, 60), 4),
-                                               (87, (10, 100, 0, 60), 8), (89, (0, 126, 0, 127), 8)]:
-        puts = random_puts(20000, seed=seed, kmin=kmin, kmax=kmax, vmin=vmin, vmax=vmax)
-        got, stats = check(native, make_log(puts), seed, hash_size=hs)
-        assert stats.framing_path == 5, stats.as_dict()
+# --- EOF inside the last record's first VLQ ends the iteration quietly (SparkeyLogIterator.java:
+#     111-115); inside the second VLQ it is a RuntimeException (:117,134-136) ---
+@pytest.mark.parametrize("tail", [b"\x80", b"\xff\xff\xff", b"\x81\x82\x83\x84"])
+@pytest.mark.parametrize("sw", [{}, {"no_frame3": 1}, {"serial_framing": 1}])
+def test_eof_inside_first_vlq(native, switch, tail, sw):
+    from helpers import with_trailing_bytes
+    switch(**sw)
+    for base in (make_log(key_value_puts(3000)), make_log(random_puts(5000, seed=7, kmin=8, kmax=64, vmin=90,
+                                                                       vmax=110))):
+        check(native, with_trailing_bytes(base, tail), 19, hash_size=8)
 
 
-def test_lane_matches_frame3(native, monkeypatch):
-    puts = random_puts(60000, seed=91, kmin=8, kmax=64, vmin=100, vmax=100)
-    log = make_log(puts)
-    monkeypatch.setenv("SPARKEY_FRAME_LANE", "1")
-    a, sa = check(native, log, 91, hash_size=8)
-    monkeypatch.setenv("SPARKEY_NO_LANE", "1")
-    b, sb = gpu_build(native, log, 91, 8)
-    assert sa.framing_path == 5 and sb.framing_path == 4 and a == b
-
-
-@pytest.mark.parametrize("region", ["256", "1024", "8192"])
-def test_lane_false_entries_fixed(native, monkeypatch, region):
-    """Values whose bytes all look like record headers (small bytes), tiny records and DELETE records:
-    many screened entries are false starts that survive the trial walk; the fix passes re-walk those
-    regions from the previous region's exit and the bytes stay the oracle's."""
-    monkeypatch.setenv("SPARKEY_FRAME_LANE", "1")
-    monkeypatch.setenv("SPARKEY_LANE_REGION", region)
-    rng = np.random.default_rng(int(region))
-    puts = [(b"k%d" % i, rng.integers(1, 9, int(rng.integers(0, 40)), dtype=np.uint8).tobytes()) for i in range(30000)]
-    got, stats = check(native, make_log(puts), 7, hash_size=8)
-    assert stats.framing_path in SPEC, stats.as_dict()
-    ops = _churn_ops(40000, 9000, 0.2, 93, klen=(1, 12), vlen=(0, 6))
-    got, stats = check(native, make_log(ops=ops), 93, hash_size=4)
-    assert stats.framing_path in SPEC and stats.placement_path == 2, stats.as_dict()
-
-
-def test_lane_errors_reported_like_serial(native, monkeypatch):
-    """A corrupt record in the middle of a log: the lane framing leaves its region unresolved, the
-    serial walk reports the reference's error at the record's offset."""
-    import struct
-    monkeypatch.setenv("SPARKEY_FRAME_LANE", "1")
-    log = bytearray(make_log(random_puts(20000, seed=95, kmin=8, kmax=40, vmin=10, vmax=90)))
-    # corrupt the header of a record near the middle: key length above maxKeyLen
-    p, mid = 84, len(log) // 2
-    while p < mid:
-        p += 1 + log[p] + log[p + 1]
-    log[p] = 127
-    got, want = same_error(native, bytes(log))
-    assert got == want
+def test_eof_inside_second_vlq(native):
+    from helpers import with_trailing_bytes
+    got, want = same_error(native, with_trailing_bytes(make_log(key_value_puts(300)), b"\x05\x80"))
+    assert got == want == native.E_CORRUPT_RECORD

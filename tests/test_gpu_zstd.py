@@ -155,17 +155,17 @@ def test_errors(native):
 
 @pytest.mark.parametrize("block_size", [1024, 16384])
 @pytest.mark.parametrize("spacing", ["default", "min"])
-def test_parallel_directory_zstd(native, block_size, spacing, monkeypatch, capfd):
+def test_parallel_directory_zstd(native, block_size, spacing, switch, capfd):
     """The parallel block directory on ZSTD logs (frame magic as the screen) equals the serial chain."""
     from sparkey import synth
     log = synth.snappy_log(synth.fixed_log(20000, 16, 100, seed=block_size), 118, block_size, codec="zstd").tobytes()
     if spacing == "min":
-        monkeypatch.setenv("SPARKEY_SNAPPY_DIR_A", "1")
-    monkeypatch.setenv("SPARKEY_SNAPPY_DIR_DEBUG", "1")
+        switch(snappy_dir_a=1)
+    switch(snappy_dir_debug=1)
     got, _ = native.build_index_mem(log, native.make_opts(hash_seed=77))
     assert got == oracle.build_index(log, 77)
     assert "[zstd dir] parallel" in capfd.readouterr().err
-    monkeypatch.setenv("SPARKEY_SNAPPY_SERIAL_DIR", "1")
+    switch(snappy_serial_dir=1)
     serial, _ = native.build_index_mem(log, native.make_opts(hash_seed=77))
     assert got == serial
 

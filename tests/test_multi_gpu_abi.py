@@ -1,7 +1,7 @@
 """Multi-GPU builds through the drop-in boundary: sparkey_build_index_mem / _file with
 opts.num_gpus = N (the C++ orchestrator, sparkey-java_amd/csrc/shard_host.cpp, N ranks as threads).
 On a one-GPU box the ranks share cuda:0 through the in-process transport
-(SPARKEY_SHARD_TRANSPORT=threads-one-device); the RCCL transport runs at N = 1 here (one rank,
+(the shard_transport switch = 2, threads on one device); the RCCL transport runs at N = 1 here (one rank,
 sparkey_shard_build over an RCCL communicator) and at N > 1 in the driver's multi-GPU bench.
 Every .spi must equal the oracle's (the reference's single-threaded IndexHash.createNew,
 IndexHash.java:131-167) byte for byte."""
@@ -19,8 +19,8 @@ IN_MEMORY, SORTING = 1, 2
 
 
 @pytest.fixture(autouse=True)
-def one_device(monkeypatch):
-    monkeypatch.setenv("SPARKEY_SHARD_TRANSPORT", "threads-one-device")
+def one_device(switch):
+    switch(shard_transport=2)
 
 
 def check(native, log, n, seed=7, method=IN_MEMORY, hash_size=0, sharded=None):
@@ -111,12 +111,12 @@ def test_file_to_file(native, tmp_path):
     assert st.sharded == 1 and st.num_entries == 100000
 
 
-def test_rccl_one_rank(native, monkeypatch):
+def test_rccl_one_rank(native, switch):
     """sparkey_shard_build over an RCCL communicator (world 1 on a one-GPU box): the multi-process path
     bench.py takes at N > 1."""
     import torch
     from sparkey import synth
-    monkeypatch.delenv("SPARKEY_SHARD_TRANSPORT")
+    switch(shard_transport=None)
     log = synth.fixed_log(200000, 16, 100, seed=6).tobytes()
     opts = native.make_opts(hash_seed=3)
     uid = native.shard_unique_id()
@@ -134,3 +134,41 @@ def test_rccl_one_rank(native, monkeypatch):
     finally:
         plan.close()
         comm.close()
+
+
+@pytest.mark.parametrize("fail_rank", [0, 2])
+def test_one_rank_failing_fails_every_rank(native, switch, fail_rank):
+    """One rank fails on its own (its load, forced by the shard_fail_rank switch): every rank returns
+    from the same checkpoint with the error (no rank waits in a collective for it), and the next build
+    through a fresh group is correct (ranks fail together)."""
+    from sparkey import synth
+    log = synth.fixed_log(60000, 16, 100, seed=2).tobytes()
+    switch(shard_fail_rank=fail_rank)
+    with pytest.raises(OSError) as e:
+        native.build_index_mem(log, native.make_opts(hash_seed=5, num_gpus=3))
+    assert "injected load failure" in str(e.value) or "another rank" in str(e.value)
+    switch(shard_fail_rank=None)
+    check(native, log, 3, seed=5, sharded=1)
+
+
+@pytest.mark.parametrize("n", [2, 4])
+def test_sharded_device_entry(native, n):
+    """sparkey_build_index_sharded_device: every rank reads its range of ONE device log in place and
+    writes its part of ONE device .spi in place."""
+    import torch
+    from sparkey import synth
+    for log in (synth.fixed_log(300000, 16, 100, seed=4).tobytes(), make_log(random_puts(50000, seed=3))):
+        opts = native.make_opts(hash_seed=11, num_gpus=n)
+        size = native.index_size(log[:84], opts)
+        d_log = torch.frombuffer(bytearray(log), dtype=torch.uint8).to("cuda:0")
+        d_spi = torch.empty(size, dtype=torch.uint8, device="cuda:0")
+        bufs, outs = [], []
+        for r in range(n):
+            lo, hi, off, ln = native.shard_geometry(log[:84], len(log), opts, r, n)
+            bufs.append(d_log.data_ptr() + lo)
+            outs.append(d_spi.data_ptr() + off)
+        st = native.build_index_sharded_device(log[:84], len(log), bufs, outs, opts)
+        got = d_spi.cpu().numpy().tobytes()
+        want = oracle.build_index(log, 11)
+        assert got == want, diff_report(got, want)
+        assert st.sharded == 1

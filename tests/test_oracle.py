@@ -165,3 +165,27 @@ def test_canonical_layout_matches_sequential(oracle_mod):
         want = oracle.build_index(log, seed, hash_size=hs, method=oracle.IN_MEMORY)
         got = canonical_table(log, seed, hs)
         assert got == want[112:]
+
+
+@pytest.mark.parametrize("tail", [b"\x80", b"\xff\xff", b"\x81\x82\x83\x84"])
+def test_eof_inside_first_vlq_ends_iteration(oracle_mod, tail):
+    """dataEnd == file length and the last record's first VLQ cut after continuation bytes: hasNext
+    catches the EOFException and ends the iteration (SparkeyLogIterator.java:111-115), so the index
+    holds the earlier records and no error is raised."""
+    from helpers import index_header, key_value_puts, make_log, with_trailing_bytes
+    base = make_log(key_value_puts(500))
+    log = with_trailing_bytes(base, tail)
+    for method in (oracle.IN_MEMORY, oracle.SORTING):
+        got = oracle.build_index(log, 42, method=method)
+        want = oracle.build_index(base, 42, method=method)
+        assert got[112:] == want[112:]  # the same slots; only the header's dataEnd differs
+        assert index_header(got)["dataEnd"] == len(log) and index_header(got)["numEntries"] == 500
+
+
+def test_eof_inside_second_vlq_is_an_error(oracle_mod):
+    """EOF inside the second VLQ is wrapped in a RuntimeException (SparkeyLogIterator.java:117,134-136)."""
+    from helpers import key_value_puts, make_log, with_trailing_bytes
+    log = with_trailing_bytes(make_log(key_value_puts(50)), b"\x05\x80")
+    with pytest.raises(oracle.OracleError) as e:
+        oracle.build_index(log, 42)
+    assert e.value.code == -13  # ORACLE_E_CORRUPT_RECORD

@@ -147,17 +147,17 @@ def test_sharded_gpu_snappy_gather(native, world):
 
 
 @pytest.mark.parametrize("world", [1, 3])
-def test_sharded_gpu_speculative_retry(native, world, monkeypatch):
+def test_sharded_gpu_speculative_retry(native, world, switch):
     """Every speculative frame+bin attempt flagged for a retry (a send buffer of 0 entries): the
     ranks re-frame synchronously and the result is unchanged."""
-    monkeypatch.setenv("SPARKEY_SHARD_SYNC_FRAME", "1")
+    switch(shard_sync_frame=1)
     metas = check(native, make_log(key_value_puts(20000)), world)
     assert metas[0]["path"] == "sharded" and metas[0]["rounds"] >= 2
 
 
 @pytest.mark.parametrize("world", [1, 3])
-def test_sharded_gpu_exact_reframe(native, world, monkeypatch):
+def test_sharded_gpu_exact_reframe(native, world, switch):
     """The exact path framing its byte range again instead of reusing the canonical step's slabs."""
-    monkeypatch.setenv("SPARKEY_EXACT_REFRAME", "1")
+    switch(exact_reframe=1)
     metas = check(native, _churn_log(30000, 10000, seed=9), world, seed=4, sparsity=1.3)
     assert all(m["path"] == "exact" for m in metas)

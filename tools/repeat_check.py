@@ -20,9 +20,9 @@ def main():
     ap.add_argument("--entries", type=int, default=10_000_000)
     ap.add_argument("--general", action="store_true")
     a = ap.parse_args()
-    if a.general:
-        os.environ["SPARKEY_NO_UNIFORM"] = "1"
     from sparkey import _native, synth
+    if a.general:
+        _native.debug_set("no_uniform", 1)
     log = synth.fixed_log(a.entries, 16, 100, seed=1)
     dev = torch.device("cuda", 0)
     header = log[:84].tobytes()

@@ -1,6 +1,6 @@
 """Sharded exact-path rehearsal on ONE GPU: the churn log (overwrites + DELETEs) built
 by sparkey_build_index_mem with opts.num_gpus = N ranks as threads of this process on cuda:0
-(SPARKEY_SHARD_TRANSPORT=threads-one-device), against the single-GPU device build of the same log.
+(the shard_transport switch = 2), against the single-GPU device build of the same log.
 Prints per-rank phase times (host wall, sparkey_multi_phase_*) and checks the .spi is identical.
 
     python tools/shard_rehearsal.py --entries 10000000 --ranks 1,2,4 [--reps 3]
@@ -27,9 +27,9 @@ def main():
     import torch
     from sparkey import _native, synth
 
-    os.environ["SPARKEY_SHARD_TRANSPORT"] = "threads-one-device"
+    _native.debug_set("shard_transport", 2)
     if args.full_table:
-        os.environ["SPARKEY_EXACT_FULL_TABLE"] = "1"
+        _native.debug_set("exact_full_table", 1)
     n = args.entries
     t0 = time.time()
     log = synth.churn_log(n, int(n * 0.8), 0.1, seed=9)
