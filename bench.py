@@ -98,6 +98,8 @@ WORKLOADS = {
            "path": 0},
     "c3": {"name": "C3: PUTs x (8-64 B key, 100 B value), CompressionType.NONE, IN_MEMORY", "sorting": False,
            "path": 0},
+    "c1x": {"name": "WriteHashBenchmark's data at its 10M parameter: put(\"key_\" + i, \"value_\" + i), block size "
+                    "1024, CompressionType.NONE, IN_MEMORY (WriteHashBenchmark.java:43-76)", "sorting": False, "path": 0},
     "c5": {"name": "C5: C3 log, SORTING constructionMethod", "sorting": True, "path": 0},
     "churn": {"name": "C2 shape with overwrites and DELETEs: keys from a pool of 0.8 n, 10% DELETE records, "
                       "IN_MEMORY (exact replay over slot segments)", "sorting": False, "path": 2},
@@ -211,6 +213,8 @@ def single_gpu(args, dev):
         log_np = synth.fixed_log(n, 16, 100, seed=args.seed, file_id=0x5EED0000)
     elif args.workload in ("c3", "c5"):
         log_np = synth.mixed_log(n, 8, 64, 100, seed=args.seed + 2)
+    elif args.workload == "c1x":
+        log_np = synth.key_value_log_np(n)
     elif args.workload in ("snappy", "zstd"):
         log_np = synth.snappy_log(synth.fixed_log(n, 16, 100, seed=args.seed, file_id=0x5EED0000), 118, 65536,
                                   codec=args.workload)
@@ -323,7 +327,7 @@ def single_gpu(args, dev):
     log_path, spi_path = os.path.join(tmpdir, "bench.spl"), os.path.join(tmpdir, "bench.spi")
     try:
         log_np.tofile(log_path)
-        if args.workload in ("c2", "c3", "c5", "churn", "snappy", "zstd"):
+        if args.workload in ("c1x", "c2", "c3", "c5", "churn", "snappy", "zstd"):
             # as SparkeyWriter.writeHash does it: a fresh "-tmp" file, then renamed over the .spi
             # (each timed call writes a new file; replacing the old .spi -- an unlink of ~200 MB of
             # page cache, ~20 ms on the box -- happens after the clock stops)

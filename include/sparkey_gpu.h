@@ -78,8 +78,9 @@ typedef struct sparkey_build_stats {
   int32_t address_size;
   int32_t placement_path;     /* 0 = parallel canonical placement, 1 = single-lane exact replay (full tables),
                                  2 = exact replay over independent slot segments (DELETEs, overwrites) */
-  int32_t framing_path;       /* 0 = speculative parallel framing, 1 = serial device walker,
-                                 2 = uniform-record framing (the header proves one record size) */
+  int32_t framing_path;       /* 0 = speculative parallel framing (k_frame), 1 = serial device walker,
+                                 2 = uniform-record framing (the header proves one record size),
+                                 4 = one-byte-VLQ framing (k_frame3), 5 = one chunk per lane (k_frame4) */
   int32_t partition_passes;   /* passes over the entries of the bucket partition: 2, or 1 when the
                                  uniform framing wrote the per-digit regions itself */
   int32_t sharded;            /* multi-GPU builds: 1 sharded canonical placement, 2 sharded exact path, 3 the log

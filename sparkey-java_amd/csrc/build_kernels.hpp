@@ -208,6 +208,8 @@ struct BuildParams {
   int32_t f3_rgn;    // k_frame3: staged region bytes per wave (W * C + fr_look + 16, 16-byte multiple)
   int32_t f3_cand_cap;  // k_frame3: candidates (and records) per wave its LDS list holds (<= 512)
   int32_t f3_surv_cap;  // k_frame3: chain heads per wave after the short walk (<= 64, one long walk per lane)
+  int32_t f4_rgn;  // k_frame4 (frame4_kernels.hip): staged region bytes per wave (64 C + maxRecLen + 32)
+  int32_t f4_m;    // k_frame4: chunks from a wave's start to its converge target (m C >= maxRecLen)
   int32_t fr_ticket;    // k_frame / k_frame3: regions by device-wide ticket, not by workgroup id (builds that
                         // share the device, or the frame_ticket switch)
   // uniform-stride framing (k_frame_uniform): uni_n records of uni_rec bytes from fr_entry
@@ -296,10 +298,13 @@ void launch_dense_slabs(const BuildParams& P, hipStream_t s);
 void launch_frame_uniform(const BuildParams& P, hipStream_t s, StageTimer* tm);
 void launch_frame3(const BuildParams& P, hipStream_t s, StageTimer* tm);  // frame3_kernels.hip
 bool frame3_fits(BuildParams& P, double mean_record, double pass);
+void launch_frame4(const BuildParams& P, hipStream_t s, StageTimer* tm);  // frame4_kernels.hip
+bool frame4_geometry(BuildParams& P, double mean_record, int64_t want_c, int64_t entry, int64_t frame_end);
+uint32_t frame4_lds(const BuildParams& P);
 uint32_t frame3_lds_per_wave(const BuildParams& P);
 // framing paths: 0 k_frame, 1 serial walk, 2 k_frame_uniform, 4 k_frame3 (3 and 5 were the k_frame2 and
 // k_frame_lane experiments, measured slower and removed); the speculative ones with per-wave slabs
-__host__ __device__ inline bool slab_framing(int path) { return path == 0 || path == 4; }
+__host__ __device__ inline bool slab_framing(int path) { return path == 0 || path == 4 || path == 5; }
 void launch_place_fast(const BuildParams& P, hipStream_t s, StageTimer* tm);
 void launch_place_buckets(const BuildParams& P, hipStream_t s);
 // fallbacks and shared stages (build_kernels.hip)

@@ -623,6 +623,24 @@ static void set_geom(BuildParams& P, const FrameGeom& g) {
   P.fr_nchunks = g.nchunks;
 }
 
+// k_frame4 (frame4_kernels.hip): one chunk per lane, for the logs k_frame3 frames (one-byte VLQs,
+// records of at most 256 bytes).  The frame4 switch turns it on (1) or off (0).  Its geometry is
+// returned apart from P's (k_frame3 / k_frame, its fallbacks, keep theirs); f4_* are set on P.
+static bool want_frame4(BuildParams& P, const LogHdr& lh, int64_t entry, int64_t frame_end, FrameGeom* g) {
+  if (knob(Knob::Frame4) != 1 || !P.fr_fast || P.max_rec_len > 256) return false;
+  const int64_t nr = std::max<int64_t>(0, lh.num_puts) + std::max<int64_t>(0, lh.num_deletes);
+  const int64_t by = std::max<int64_t>(0, lh.put_size) + std::max<int64_t>(0, lh.delete_size);
+  if (nr <= 0 || by <= 0) return false;
+  BuildParams Q = P;
+  if (!frame4_geometry(Q, (double)by / (double)nr, knob_set(Knob::Frame4C) ? knob(Knob::Frame4C) : 0, entry,
+                       frame_end))
+    return false;
+  *g = get_geom(Q);
+  P.f4_rgn = Q.f4_rgn;
+  P.f4_m = Q.f4_m;
+  return true;
+}
+
 // Slab layout of the framing output and the workspace it needs (grown on demand).
 static int reserve_for_framing(sparkey_plan* pl, BuildParams& P, int framing_path, uint64_t nrec, uint32_t slab_cap,
                                char* err, size_t err_len) {
@@ -671,7 +689,8 @@ static int launch_framing(sparkey_plan* pl, const BuildParams& P, int framing_pa
     HIP_TRY(hipMemsetAsync(pl->desc, 0, (2 * nwaves + 2) * sizeof(unsigned long long), s));
     HIP_TRY(hipMemsetAsync(pl->wcount, 0, (P.nslabs + 1) * sizeof(uint32_t), s));
     if (P.del_parts) HIP_TRY(hipMemsetAsync(P.del_parts, 0, (size_t)kDelParts * 16 * sizeof(unsigned long long), s));
-    if (framing_path == 4) launch_frame3(P, s, &pl->timer);
+    if (framing_path == 5) launch_frame4(P, s, &pl->timer);
+    else if (framing_path == 4) launch_frame3(P, s, &pl->timer);
     else launch_frame_fused(P, s, &pl->timer);
     launch_sum_deletes(P, s);  // (the spread DELETE counters into the status block)
   } else if (framing_path == 2) {
@@ -1208,9 +1227,11 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
   // for the rest; both fall back to the serial walk, which alone reports errors
   const bool use_frame3 = fused_framing && want_frame3(P, lh, kLogHeaderSize, std::max<int64_t>(lh.data_end, kLogHeaderSize));
   const FrameGeom geom0 = get_geom(P);
+  FrameGeom geom4{};
+  const bool use_frame4 = use_frame3 && want_frame4(P, lh, kLogHeaderSize, std::max<int64_t>(lh.data_end, kLogHeaderSize), &geom4);
   // the serial_framing switch forces the exact serial walk (smoke() and the tests check every path)
   const bool force_serial = knob_on(Knob::SerialFraming);
-  const int spec_path = fused_framing && !force_serial ? (use_frame3 ? 4 : 0) : 1;
+  const int spec_path = fused_framing && !force_serial ? (use_frame4 ? 5 : use_frame3 ? 4 : 0) : 1;
   int framing_path = spec_path, placement_path = 0;
   if (const int64_t R = force_serial ? 0 : uniform_record_size(lh)) {  // k_frame_uniform: every record is exactly R bytes
     framing_path = 2;
@@ -1225,11 +1246,17 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
     const uint64_t nw = std::max<uint64_t>(1, g.nchunks ? (g.nchunks + g.w - 1) / g.w : 0);
     return (uint32_t)std::min<uint64_t>(kPartTile, std::max<uint64_t>(64, 2 * ((nrec + nw - 1) / nw) + 32));
   };
-  uint32_t slab_cap = slab_for(geom0);
+  auto geom_for = [&](int path) -> const FrameGeom& { return path == 5 ? geom4 : geom0; };
+  int slab_path = framing_path;  // (the framing the slab size was chosen for)
+  uint32_t slab_cap = slab_for(geom_for(framing_path));
   bool use_regions = !knob_on(Knob::NoRegions), regions_used = false;
   bool use_fixed = true;  // k_part2st / k_part2s in one pass into fixed bucket regions
-  set_geom(P, geom0);
-  for (int attempt = 0; attempt < 6; attempt++) {
+  for (int attempt = 0; attempt < 7; attempt++) {
+    set_geom(P, geom_for(framing_path));
+    if (slab_framing(framing_path) && framing_path != slab_path) {
+      slab_cap = slab_for(geom_for(framing_path));
+      slab_path = framing_path;
+    }
     rc = reserve_for_framing(pl, P, framing_path, nrec, slab_cap, err, err_len);
     if (rc) return rc;
     if (knob_on(Knob::FrameDebug)) {  // per-wave phase counters: 16 words per k_frame / k_frame3 wave
@@ -1316,6 +1343,10 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
               (unsigned long long)st.err, (unsigned long long)(st.err >> 8));
     // (a digit region filled by k_part1_regions is the partition's business, not the framing's)
     const unsigned fspec = st.spec_fail & ~(P.p1_kernel ? kSpecRegionFull : 0u);
+    if (framing_path == 5 && (fspec || st.err != ~0ull)) {  // k_frame4's lists: k_frame3 (or k_frame)
+      framing_path = use_frame3 ? 4 : 0;
+      continue;
+    }
     if (framing_path == 4 && (fspec || st.err != ~0ull)) {  // k_frame3's lists or speculation: k_frame
       framing_path = 0;
       continue;
@@ -1892,11 +1923,14 @@ int sparkey_shard_find_entry(sparkey_plan* pl, uint64_t lo, uint64_t window, voi
 // synchronous sparkey_shard_frame and the speculative sparkey_shard_frame_bin_async).
 struct ShardFrameSetup {
   BuildParams P;
-  bool fused = false, use_frame3 = false, use_regions = true;
-  int spec_path() const { return fused && !knob_on(Knob::SerialFraming) ? (use_frame3 ? 4 : 0) : 1; }
+  bool fused = false, use_frame3 = false, use_frame4 = false, use_regions = true;
+  int spec_path() const {
+    return fused && !knob_on(Knob::SerialFraming) ? (use_frame4 ? 5 : use_frame3 ? 4 : 0) : 1;
+  }
   int framing_path = 1;
   uint64_t nrec = 0;
-  FrameGeom geom0;
+  FrameGeom geom0, geom4{};
+  const FrameGeom& geom(int path) const { return path == 5 ? geom4 : geom0; }
   uint32_t slab_cap = 0;
   int slab_path = 0;
 };
@@ -1923,6 +1957,7 @@ static int shard_frame_setup(sparkey_plan* pl, int64_t entry, int64_t frame_end,
                        frac * 1.05) + 4096;
   F->use_frame3 = F->fused && want_frame3(P, sh.lh, entry, frame_end);
   F->geom0 = get_geom(P);
+  F->use_frame4 = F->use_frame3 && want_frame4(P, sh.lh, entry, frame_end, &F->geom4);
   F->framing_path = F->spec_path();
   const int64_t R = uniform_record_size(sh.lh);
   if (R && (entry - kLogHeaderSize) % R == 0) {  // a record start of a uniform log: frame by stride
@@ -1931,7 +1966,7 @@ static int shard_frame_setup(sparkey_plan* pl, int64_t entry, int64_t frame_end,
     P.uni_rec = R;
     F->nrec = P.uni_n;
   }
-  F->slab_cap = shard_slab_for(F->geom0, F->nrec);
+  F->slab_cap = shard_slab_for(F->geom(F->framing_path), F->nrec);
   F->slab_path = F->framing_path;
   F->use_regions = !knob_on(Knob::NoRegions);
   return SPARKEY_OK;
@@ -1940,9 +1975,9 @@ static int shard_frame_setup(sparkey_plan* pl, int64_t entry, int64_t frame_end,
 // Launches one framing attempt of the set-up (status reset first); no synchronisation.
 static int shard_frame_launch(sparkey_plan* pl, ShardFrameSetup* F, hipStream_t s, char* err, size_t err_len) {
   BuildParams& P = F->P;
-  set_geom(P, F->geom0);
+  set_geom(P, F->geom(F->framing_path));
   if (slab_framing(F->framing_path) && F->framing_path != F->slab_path) {
-    F->slab_cap = shard_slab_for(F->geom0, F->nrec);
+    F->slab_cap = shard_slab_for(F->geom(F->framing_path), F->nrec);
     F->slab_path = F->framing_path;
   }
   int rc = reserve_for_framing(pl, P, F->framing_path, F->nrec, F->slab_cap, err, err_len);
@@ -2001,7 +2036,7 @@ static int shard_frame_sync(sparkey_plan* pl, int64_t entry, int64_t frame_end, 
   F.use_regions = F.use_regions && allow_regions;
   BuildParams& P = F.P;
   Status& st = *pl->h_status;
-  for (int attempt = 0; attempt < 6; attempt++) {
+  for (int attempt = 0; attempt < 7; attempt++) {
     rc = shard_frame_launch(pl, &F, s, err, err_len);
     if (rc) return rc;
     rc = shard_sync_status(pl, s, err, err_len);
@@ -2013,6 +2048,10 @@ static int shard_frame_sync(sparkey_plan* pl, int64_t entry, int64_t frame_end, 
     }
     if (st.overflow || st.n_records > P.max_records) {
       F.nrec = std::max<uint64_t>(st.n_records, F.nrec * 2 + 1);
+      continue;
+    }
+    if (path == 5 && (st.spec_fail || st.err != ~0ull)) {
+      F.framing_path = F.use_frame3 ? 4 : 0;
       continue;
     }
     if (path == 4 && (st.spec_fail || st.err != ~0ull)) {

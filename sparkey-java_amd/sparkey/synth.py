@@ -4,6 +4,7 @@ LogWriter produces (UncompressedBlockOutput.java:67-72, LogHeader.java:90-115).
   fixed_log(n, 16, 100)      C2: key = LE64(i) || LE64(splitmix64(i ^ seed)) (unique), value = 100 random bytes
   mixed_log(n, 8, 64, 100)   C3: key length uniform in [8, 64], LE64(i) prefix keeps keys unique
   key_value_log(n)           C1: put("key_" + i, "value_" + i) as WriteHashBenchmark.java:52-54
+  key_value_log_np(n)        the same bytes built with numpy (WriteHashBenchmark's 10M)
   churn_log(n, pool, p_del)  C2 shape with overwrites and DELETEs: keys drawn from a pool of `pool`
 """
 from __future__ import annotations
@@ -122,6 +123,41 @@ def key_value_log(n: int, file_id: int = 0x0C1C1C1C, block_size: int = 1024) -> 
         put_size += len(rec)
     body = b"".join(parts)
     return _header(n, max_k, max_v, put_size, LOG_HEADER_SIZE + len(body), file_id, block_size) + body
+
+
+def key_value_log_np(n: int, file_id: int = 0x0C1C1C1C, block_size: int = 1024) -> np.ndarray:
+    """key_value_log(n) built with numpy (the same bytes, fast at WriteHashBenchmark's 10M): records with
+    the same number of decimal digits in i have one size, so each digit-count group is one 2-D array."""
+    parts = [np.frombuffer(b"", dtype=np.uint8)]
+    put_size = max_k = max_v = 0
+    lo, d = 0, 1
+    while lo < n:
+        hi = min(n, 10 ** d)
+        m = hi - lo
+        kl, vl = 4 + d, 6 + d
+        rec = np.empty((m, 2 + kl + vl), dtype=np.uint8)
+        rec[:, 0] = kl + 1
+        rec[:, 1] = vl
+        i = np.arange(lo, hi, dtype=np.int64)
+        digits = np.empty((m, d), dtype=np.uint8)
+        x = i.copy()
+        for k in range(d - 1, -1, -1):
+            digits[:, k] = (x % 10 + 48).astype(np.uint8)
+            x //= 10
+        rec[:, 2:6] = np.frombuffer(b"key_", dtype=np.uint8)
+        rec[:, 6:6 + d] = digits
+        rec[:, 6 + d:12 + d] = np.frombuffer(b"value_", dtype=np.uint8)
+        rec[:, 12 + d:] = digits
+        parts.append(rec.reshape(-1))
+        put_size += rec.size
+        max_k, max_v = max(max_k, kl), max(max_v, vl)
+        lo, d = hi, d + 1
+    body = np.concatenate(parts)
+    out = np.empty(LOG_HEADER_SIZE + body.size, dtype=np.uint8)
+    out[:LOG_HEADER_SIZE] = np.frombuffer(_header(n, max_k, max_v, put_size, LOG_HEADER_SIZE + body.size, file_id,
+                                                  block_size), dtype=np.uint8)
+    out[LOG_HEADER_SIZE:] = body
+    return out
 
 
 def churn_log(n: int, pool: int, p_del: float, key_len: int = 16, value_len: int = 100, seed: int = 5,

@@ -189,3 +189,12 @@ def test_eof_inside_second_vlq_is_an_error(oracle_mod):
     with pytest.raises(oracle.OracleError) as e:
         oracle.build_index(log, 42)
     assert e.value.code == -13  # ORACLE_E_CORRUPT_RECORD
+
+
+def test_key_value_log_np_matches_writer(oracle_mod):
+    """WriteHashBenchmark's data (put("key_" + i, "value_" + i), block size 1024) from the numpy generator
+    equals the LogWriter restatement's bytes across the digit-count boundaries."""
+    from sparkey import synth
+    for n in (0, 1, 10, 11, 1000, 10001):
+        assert synth.key_value_log_np(n).tobytes() == make_log(key_value_puts(n, b"key_%d", b"value_%d"),
+                                                               file_id=0x0C1C1C1C, block_size=1024)
