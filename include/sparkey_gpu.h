@@ -80,9 +80,10 @@ typedef struct sparkey_build_stats {
                                  2 = exact replay over independent slot segments (DELETEs, overwrites) */
   int32_t framing_path;       /* 0 = speculative parallel framing (k_frame), 1 = serial device walker,
                                  2 = uniform-record framing (the header proves one record size),
-                                 4 = one-byte-VLQ framing (k_frame3), 5 = one chunk per lane (k_frame4) */
-  int32_t partition_passes;   /* passes over the entries of the bucket partition: 2, or 1 when the
-                                 uniform framing wrote the per-digit regions itself */
+                                 4 = one-byte-VLQ framing (k_frame3) */
+  int32_t partition_passes;   /* passes over the entries of the bucket partition: 2; 1 when the
+                                 uniform framing wrote the per-digit regions itself; 0 when it wrote
+                                 every entry straight into its placement bucket */
   int32_t sharded;            /* multi-GPU builds: 1 sharded canonical placement, 2 sharded exact path, 3 the log
                                  gathered on every rank and built whole (compressed logs, full tables); else 0 */
   double device_ms;           /* device time of the build (HIP events), excluding copies; sharded: the rank's

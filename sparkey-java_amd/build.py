@@ -12,7 +12,7 @@ LIB_DIR = os.path.join(HERE, "lib")
 LIB = os.path.join(LIB_DIR, "libsparkey_gpu.so")
 OBJ_DIR = os.path.join(HERE, "build", "obj")
 SOURCES = [os.path.join(HERE, "csrc", f) for f in (
-    "build_kernels.hip", "fused_kernels.hip", "frame3_kernels.hip", "frame4_kernels.hip", "exact_kernels.hip", "shard_kernels.hip",
+    "build_kernels.hip", "fused_kernels.hip", "frame3_kernels.hip", "exact_kernels.hip", "shard_kernels.hip",
     "shard_exact_kernels.hip", "lookup_kernels.hip", "append_kernels.hip", "snappy_kernels.hip", "zstd_kernels.hip",
     "sparkey_gpu.cpp", "file_build.cpp", "shard_host.cpp", "knobs.cpp")]
 HEADERS = [os.path.join(HERE, "csrc", f) for f in (

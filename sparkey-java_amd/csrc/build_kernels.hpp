@@ -105,7 +105,7 @@ struct Status {
   unsigned int stats_ticket;     // k_stats_folded: blocks done
   unsigned long long acc_sum, acc_col, acc_max;  // k_stats_folded: totals over its blocks
   unsigned int p2_ticket;        // fused_carry: k_part2s blocks done (the last composes the digits)
-  unsigned int pad3;
+  unsigned int lb_fail;          // k_place_reg look-back: a wait ran out or a repair did not close (redo)
 };
 
 struct BuildParams {
@@ -147,6 +147,8 @@ struct BuildParams {
   uint64_t* woff;        // exclusive prefix of wcount (+ total at [nslabs])
   uint32_t slab_cap;
   uint32_t part_group;   // slabs per partition tile
+  uint32_t p1r_group;    // k_part1_regions: slabs per tile (<= 2 kPartTile entries, taken kPartTile at a time)
+  uint32_t p1r_tiles;
   uint64_t nslabs;
   // buckets
   uint32_t* bcount;
@@ -208,8 +210,6 @@ struct BuildParams {
   int32_t f3_rgn;    // k_frame3: staged region bytes per wave (W * C + fr_look + 16, 16-byte multiple)
   int32_t f3_cand_cap;  // k_frame3: candidates (and records) per wave its LDS list holds (<= 512)
   int32_t f3_surv_cap;  // k_frame3: chain heads per wave after the short walk (<= 64, one long walk per lane)
-  int32_t f4_rgn;  // k_frame4 (frame4_kernels.hip): staged region bytes per wave (64 C + maxRecLen + 32)
-  int32_t f4_m;    // k_frame4: chunks from a wave's start to its converge target (m C >= maxRecLen)
   int32_t fr_ticket;    // k_frame / k_frame3: regions by device-wide ticket, not by workgroup id (builds that
                         // share the device, or the frame_ticket switch)
   // uniform-stride framing (k_frame_uniform): uni_n records of uni_rec bytes from fr_entry
@@ -223,6 +223,11 @@ struct BuildParams {
   int32_t p1_kernel;    // with p1_region: k_part1_regions fills the regions from the slabs (else the framing did)
   int32_t p1_pad;
   int32_t p2_sorted;    // k_part2s: per-(bucket, slot) counts in the same pass + the carry functions
+  int32_t p1_bucket;    // k_frame_uniform writes each entry into its bucket's fixed region (no partition);
+                        // bcount[] is the atomic cursor, zeroed before the framing
+  int32_t lookback;     // k_place_reg composes the bucket carries itself (decoupled look-back over
+                        // lb_desc, no k_summary / scan / k_carry); k_place_fix repairs the wrap
+  unsigned long long* lb_desc;  // per bucket: flag << 62 | carry constant << 32 | (int32) slope
   int32_t p2_fixed;     // k_part2s in one pass: bucket b's entries at ent2[b * kPlaceLdsMax, + bcount[b])
   int32_t fold_stats;   // k_place_reg leaves calculateMaxDisplacement's per-bucket parts (no k_stats pass)
   int32_t stats_if_pending;  // k_stats / k_stats_final only when the folded stats left stats_pending
@@ -292,19 +297,17 @@ struct StageTimer {
 // fast path (fused_kernels.hip)
 void launch_frame_fused(const BuildParams& P, hipStream_t s, StageTimer* tm);
 void launch_partition(const BuildParams& P, hipStream_t s, StageTimer* tm);
+bool part2f_fits(uint32_t bpp);  // k_part2f's LDS for this many buckets a digit
 void launch_partition1(const BuildParams& P, hipStream_t s);
 void launch_partition2(const BuildParams& P, hipStream_t s, StageTimer* tm);
 void launch_dense_slabs(const BuildParams& P, hipStream_t s);
 void launch_frame_uniform(const BuildParams& P, hipStream_t s, StageTimer* tm);
 void launch_frame3(const BuildParams& P, hipStream_t s, StageTimer* tm);  // frame3_kernels.hip
 bool frame3_fits(BuildParams& P, double mean_record, double pass);
-void launch_frame4(const BuildParams& P, hipStream_t s, StageTimer* tm);  // frame4_kernels.hip
-bool frame4_geometry(BuildParams& P, double mean_record, int64_t want_c, int64_t entry, int64_t frame_end);
-uint32_t frame4_lds(const BuildParams& P);
 uint32_t frame3_lds_per_wave(const BuildParams& P);
 // framing paths: 0 k_frame, 1 serial walk, 2 k_frame_uniform, 4 k_frame3 (3 and 5 were the k_frame2 and
 // k_frame_lane experiments, measured slower and removed); the speculative ones with per-wave slabs
-__host__ __device__ inline bool slab_framing(int path) { return path == 0 || path == 4 || path == 5; }
+__host__ __device__ inline bool slab_framing(int path) { return path == 0 || path == 4; }
 void launch_place_fast(const BuildParams& P, hipStream_t s, StageTimer* tm);
 void launch_place_buckets(const BuildParams& P, hipStream_t s);
 // fallbacks and shared stages (build_kernels.hip)

@@ -477,6 +477,11 @@ __device__ __forceinline__ void frame3_region(const BuildParams& P, const uint64
   mark(4);
   if (P.f3_stop == 4) { fail(kF3Caps); return; }  // (SPARKEY_FRAME3_STOP: measurements)
   unsigned long long ndel = 0;
+  // p1_bucket: the entries go to the slab as always, and once the wave's entry is verified, from there
+  // (this lane's own stores) straight to their buckets' regions, an atomic each -- so that a round redone
+  // after a wrong guess of the entry does not count twice
+  uint32_t total = 0;
+  unsigned long long base = 0;
   for (;;) {
     const int64_t e0 = ext - R0;
     resolve(e0 < 0 || e0 > 0x7fff ? UNK : (int32_t)e0);
@@ -502,7 +507,7 @@ __device__ __forceinline__ void frame3_region(const BuildParams& P, const uint64
     // ---- counts: chunk `lane`'s records, their wave scan ----
     const uint32_t cnt = sel >= 0 ? (uint32_t)(s_cnt[sel] - at) : 0u;
     const uint32_t incl = wave_incl_sum_u32(cnt);
-    const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
     if (total > P.slab_cap) {
       if (spec) {
         const int64_t real = wait_prev();
@@ -526,7 +531,7 @@ __device__ __forceinline__ void frame3_region(const BuildParams& P, const uint64
     mark(5);
     if (P.f3_stop == 5) { fail(kF3Caps); return; }  // (SPARKEY_FRAME3_STOP: measurements)
     // ---- 5 hash ----
-    const unsigned long long base = wv * (unsigned long long)P.slab_cap;
+    base = wv * (unsigned long long)P.slab_cap;
     ndel = 0;
     for (uint32_t r = (uint32_t)lane; r < total; r += 64) {
       int32_t src = 0;
@@ -560,6 +565,18 @@ __device__ __forceinline__ void frame3_region(const BuildParams& P, const uint64
       }
     }
     break;
+  }
+  if (P.p1_bucket) {  // the verified entries into their buckets (PUTs: DELETEs stay out of the placement)
+    bool ovf = false;
+    for (uint32_t r = (uint32_t)lane; r < total; r += 64) {
+      const Entry en = P.ent[base + r];
+      if (en.addr & kDelBit) continue;
+      const uint32_t b = bucket_of(P, en.hash);
+      const uint32_t a = atomicAdd(&P.bcount[b], 1u);
+      if (a < kPlaceLdsMax) P.ent2[(uint64_t)b * kPlaceLdsMax + a] = en;
+      else ovf = true;
+    }
+    if (ovf) atomicOr(&P.st->p2_overflow, 1u);
   }
   ndel = wave_sum_u64(ndel);
   if (ndel && lane == 0) add_deletes(P, wv, ndel);

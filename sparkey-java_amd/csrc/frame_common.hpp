@@ -128,6 +128,14 @@ __device__ inline uint64_t murmur64_ld(const Ld& ld, int32_t len, uint32_t seed)
 // ------------------------------------------------------------------------------------------------
 // granules (8-byte {state, value} words) -- relaxed agent-scope atomics, zeroed before the launch
 // ------------------------------------------------------------------------------------------------
+// Placement bucket of a hash (its wanted slot >> kBucketShift) and the bucket's coarse partition digit.
+__device__ __forceinline__ uint32_t bucket_of(const BuildParams& P, uint64_t hash) {
+  return (uint32_t)(fast_mod(hash, P.mod) >> kBucketShift);
+}
+__device__ __forceinline__ uint32_t digit_of(const BuildParams& P, uint32_t bucket) {
+  return (uint32_t)(((uint64_t)bucket * P.dmagic) >> 40);
+}
+
 constexpr unsigned long long kReady = 1ull << 63;   // exit granule: bit 63 = published
 
 __device__ __forceinline__ void granule_store(unsigned long long* g, unsigned long long v) {

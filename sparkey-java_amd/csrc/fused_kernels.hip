@@ -628,12 +628,6 @@ __global__ __launch_bounds__(64, 5) void k_frame(BuildParams P, uint32_t lds_per
   if (tk < nwaves) frame_region(P, tk, lds);
 }
 
-__device__ __forceinline__ uint32_t bucket_of(const BuildParams& P, uint64_t hash) {
-  return (uint32_t)(fast_mod(hash, P.mod) >> kBucketShift);
-}
-__device__ __forceinline__ uint32_t digit_of(const BuildParams& P, uint32_t bucket) {
-  return (uint32_t)(((uint64_t)bucket * P.dmagic) >> 40);
-}
 
 // ================================================================================================
 // k_frame_uniform: logs whose header proves that every record has the same size R.  With no DELETE,
@@ -688,6 +682,8 @@ __global__ __launch_bounds__(64 * W) void k_frame_uniform(BuildParams P) {
   // else with p1_hist_ready each tile's digit counts are k_part1_hist's output
   const bool to_regions = P.p1_region != 0;
   const bool with_hist = to_regions || P.p1_hist_ready != 0;
+  // to_buckets (P.p1_bucket): no partition at all -- each entry goes straight to its placement bucket's
+  // fixed region (ent2[bucket * kPlaceLdsMax ..), its place from an atomic on the bucket's count)
   if (with_hist) {
     for (int t = threadIdx.x; t < kSub * 256; t += 64 * W) hist[t] = 0;
     __syncthreads();
@@ -760,7 +756,9 @@ __global__ __launch_bounds__(64 * W) void k_frame_uniform(BuildParams P) {
         const uint64_t hash = P.hash_size == 8 ? murmur64_ld(ld, klen, (uint32_t)P.seed)
                                                : (uint64_t)murmur32_ld(ld, klen, (uint32_t)P.seed);
         hsh[r] = hash;
-        if (!to_regions) {
+        if (P.p1_bucket) {
+          dr[r] = (uint32_t)bucket_of(P, hash);
+        } else if (!to_regions) {
           Entry en;
           en.hash = hash;
           en.addr = (uint64_t)p << P.ebb;
@@ -774,6 +772,28 @@ __global__ __launch_bounds__(64 * W) void k_frame_uniform(BuildParams P) {
       }
     }
     __builtin_amdgcn_wave_barrier();  // every lane is done with the buffer before the next round's DMA
+  }
+  if (P.p1_bucket) {
+    // the tile's places: every atomic in flight at once (one round trip), then the entries
+    uint32_t at[kRounds];
+#pragma unroll
+    for (int r = 0; r < kRounds; r++)
+      if (dr[r] != ~0u) at[r] = atomicAdd(&P.bcount[dr[r]], 1u);
+    bool ovf = false;
+#pragma unroll
+    for (int r = 0; r < kRounds; r++) {
+      if (dr[r] == ~0u) continue;
+      if (at[r] >= kPlaceLdsMax) {
+        ovf = true;
+        continue;
+      }
+      Entry en;
+      en.hash = hsh[r];
+      en.addr = (uint64_t)(P.fr_entry + (int64_t)(blk0 + (uint64_t)(r * W + wave) * 64 + lane) * R) << P.ebb;
+      P.ent2[(uint64_t)dr[r] * kPlaceLdsMax + at[r]] = en;
+    }
+    if (ovf) atomicOr(&P.st->p2_overflow, 1u);
+    return;
   }
   if (!with_hist) return;
   __syncthreads();
@@ -852,13 +872,17 @@ __global__ __launch_bounds__(64 * W) void k_frame_uniform(BuildParams P) {
 // A partition tile is part_group (<= 64) consecutive slabs, <= kPartTile entries together.
 // Wave 0 scans the slab counts with shuffles; slab_of maps a tile index to its slab, so every
 // thread then loads its entries with independent reads.
-struct SlabTile {
+template <int kMaxEntries>
+struct SlabTileN {
   uint32_t pre[kMaxPartGroup + 1];  // entry prefix over the tile's slabs
-  uint8_t slab_of[kPartTile];
+  uint8_t slab_of[kMaxEntries];
 };
+using SlabTile = SlabTileN<kPartTile>;
 
-__device__ __forceinline__ uint32_t load_tile(const BuildParams& P, SlabTile& T, uint64_t g0) {
-  const uint32_t ng = (uint32_t)min((uint64_t)P.part_group, P.nslabs > g0 ? P.nslabs - g0 : 0);
+template <int kMaxEntries>
+__device__ __forceinline__ uint32_t load_tile(const BuildParams& P, SlabTileN<kMaxEntries>& T, uint64_t g0,
+                                              uint32_t group) {
+  const uint32_t ng = (uint32_t)min((uint64_t)group, P.nslabs > g0 ? P.nslabs - g0 : 0);
   const int tid = threadIdx.x;
   if (tid < 64) {
     const uint32_t c = (uint32_t)tid < ng ? P.wcount[g0 + tid] : 0u;
@@ -881,8 +905,45 @@ __device__ __forceinline__ uint32_t load_tile(const BuildParams& P, SlabTile& T,
   return T.pre[64];
 }
 
-__device__ __forceinline__ const Entry& tile_entry(const BuildParams& P, const SlabTile& T, uint64_t g0, uint32_t i) {
+template <int kMaxEntries>
+__device__ __forceinline__ const Entry& tile_entry(const BuildParams& P, const SlabTileN<kMaxEntries>& T, uint64_t g0,
+                                                   uint32_t i) {
   const uint32_t g = T.slab_of[i];
+  return P.ent[(g0 + g) * (uint64_t)P.slab_cap + (i - T.pre[g])];
+}
+
+// k_part1_regions' tiles (up to 2 kPartTile entries): the slab of entry i found from the slab of
+// entry 32 * (i / 32) (slabs hold ~60 entries: at most a step or two), 256 bytes where a byte per entry
+// would take 8 KiB of the LDS that two workgroups per CU need.
+struct SlabTileR {
+  uint32_t pre[kMaxPartGroup + 1];
+  uint8_t first[2 * kPartTile / 32];
+};
+
+__device__ __forceinline__ uint32_t load_tile_r(const BuildParams& P, SlabTileR& T, uint64_t g0, uint32_t group) {
+  const uint32_t ng = (uint32_t)min((uint64_t)group, P.nslabs > g0 ? P.nslabs - g0 : 0);
+  const int tid = threadIdx.x;
+  if (tid < 64) {
+    const uint32_t c = (uint32_t)tid < ng ? P.wcount[g0 + tid] : 0u;
+    uint32_t incl = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t t = __shfl_up(incl, o, 64);
+      if (tid >= o) incl += t;
+    }
+    T.pre[tid] = incl - c;
+    if (tid == 63) T.pre[64] = incl;
+    // slab g covers the 32-entry groups whose first entry it holds
+    if ((uint32_t)tid < ng)
+      for (uint32_t k = (incl - c + 31) / 32; k < (incl + 31) / 32 && k < 2 * kPartTile / 32; k++) T.first[k] = (uint8_t)tid;
+  }
+  __syncthreads();
+  return T.pre[64];
+}
+
+__device__ __forceinline__ const Entry& tile_entry_r(const BuildParams& P, const SlabTileR& T, uint64_t g0, uint32_t i) {
+  uint32_t g = T.first[i >> 5];
+  while (T.pre[g + 1] <= i) g++;
   return P.ent[(g0 + g) * (uint64_t)P.slab_cap + (i - T.pre[g])];
 }
 
@@ -892,7 +953,7 @@ __global__ __launch_bounds__(kPartBlock) void k_part1_hist(BuildParams P) {
   if (build_aborted(P)) return;
   const uint64_t g0 = (uint64_t)blockIdx.x * P.part_group;
   hist[threadIdx.x] = 0;
-  const uint32_t n = load_tile(P, T, g0);
+  const uint32_t n = load_tile(P, T, g0, P.part_group);
   // every load of the tile in flight at once, then the histogram
   Entry v[kPartItems];
 #pragma unroll
@@ -927,7 +988,7 @@ __global__ __launch_bounds__(kPartBlock) void k_part1_scatter(BuildParams P) {
   lbase[tid] = lb;
   gdst[tid] = (int64_t)goff - (int64_t)lb;
   cursor[tid] = 0;
-  const uint32_t n = load_tile(P, T, g0);
+  const uint32_t n = load_tile(P, T, g0, P.part_group);
   Entry v[kPartItems];
 #pragma unroll
   for (int i = 0; i < kPartItems; i++) {
@@ -965,54 +1026,57 @@ __global__ __launch_bounds__(kPartBlock) void k_part1_regions(BuildParams P) {
   __shared__ uint32_t cnt[256];
   __shared__ uint32_t lbase[256];
   __shared__ int64_t gdst[256];        // global index of the digit's run minus its LDS start
-  __shared__ uint64_t lim[256];        // end of the digit's region
   __shared__ uint64_t sh64[kPartBlock / 64 + 1];
-  __shared__ SlabTile T;
+  __shared__ SlabTileR T;              // (p1r_group slabs: at most 2 kPartTile entries, host-checked)
   if (build_aborted(P)) return;
-  const uint64_t g0 = (uint64_t)blockIdx.x * P.part_group;
+  const uint64_t g0 = (uint64_t)blockIdx.x * P.p1r_group;
   const int tid = threadIdx.x;
-  cnt[tid] = 0;
-  const uint32_t n = load_tile(P, T, g0);  // (its barriers order the clear)
-  Entry v[kPartItems];
-  uint32_t dg[kPartItems];
+  const uint32_t ntile = load_tile_r(P, T, g0, P.p1r_group);
+  // kPartTile entries at a time (the second round is for the tiles that came out above the mean)
+  for (uint32_t base = 0; base < ntile; base += kPartTile) {
+    const uint32_t n = min((uint32_t)kPartTile, ntile - base);
+    cnt[tid] = 0;
+    Entry v[kPartItems];
+    uint32_t dg[kPartItems];
 #pragma unroll
-  for (int i = 0; i < kPartItems; i++) {
-    const uint32_t idx = (uint32_t)i * kPartBlock + tid;
-    if (idx < n) v[i] = tile_entry(P, T, g0, idx);
-  }
-#pragma unroll
-  for (int i = 0; i < kPartItems; i++) {
-    const uint32_t idx = (uint32_t)i * kPartBlock + tid;
-    dg[i] = ~0u;
-    if (idx < n && !(P.skip_del && (v[i].addr & kDelBit))) {  // exact path: DELETEs stay out
-      dg[i] = digit_of(P, bucket_of(P, v[i].hash));
-      dg[i] |= atomicAdd(&cnt[dg[i]], 1u) << 8;  // rank inside the tile's digit run
+    for (int i = 0; i < kPartItems; i++) {
+      const uint32_t idx = (uint32_t)i * kPartBlock + tid;
+      if (idx < n) v[i] = tile_entry_r(P, T, g0, base + idx);
     }
-  }
-  __syncthreads();
-  const uint32_t c = cnt[tid];
-  lbase[tid] = (uint32_t)block_excl_sum<kPartBlock>(c, sh64, &sh64[kPartBlock / 64]);
-  const uint64_t b0 = c ? atomicAdd(&P.p1_fill[tid], c) : 0u;
-  if (b0 + c > P.p1_region) atomicOr(&P.st->spec_fail, kSpecRegionFull);
-  gdst[tid] = (int64_t)((uint64_t)tid * P.p1_region + b0) - (int64_t)lbase[tid];
-  lim[tid] = (uint64_t)(tid + 1) * P.p1_region;
-  __syncthreads();
+    __syncthreads();  // (the clear; the previous round is done with stage and gdst)
 #pragma unroll
-  for (int i = 0; i < kPartItems; i++) {
-    if (dg[i] == ~0u) continue;
-    const uint32_t d = dg[i] & 255u, pos = lbase[d] + (dg[i] >> 8);
-    stage[pos] = v[i];
-    sdig[pos] = (uint8_t)d;
-  }
-  __syncthreads();
-  const uint32_t nkeep = (uint32_t)sh64[kPartBlock / 64];
+    for (int i = 0; i < kPartItems; i++) {
+      const uint32_t idx = (uint32_t)i * kPartBlock + tid;
+      dg[i] = ~0u;
+      if (idx < n && !(P.skip_del && (v[i].addr & kDelBit))) {  // exact path: DELETEs stay out
+        dg[i] = digit_of(P, bucket_of(P, v[i].hash));
+        dg[i] |= atomicAdd(&cnt[dg[i]], 1u) << 8;  // rank inside the tile's digit run
+      }
+    }
+    __syncthreads();
+    const uint32_t c = cnt[tid];
+    lbase[tid] = (uint32_t)block_excl_sum<kPartBlock>(c, sh64, &sh64[kPartBlock / 64]);
+    const uint64_t b0 = c ? atomicAdd(&P.p1_fill[tid], c) : 0u;
+    if (b0 + c > P.p1_region) atomicOr(&P.st->spec_fail, kSpecRegionFull);
+    gdst[tid] = (int64_t)((uint64_t)tid * P.p1_region + b0) - (int64_t)lbase[tid];
+    __syncthreads();
 #pragma unroll
-  for (int k = 0; k < kPartItems; k++) {
-    const uint32_t i = (uint32_t)k * kPartBlock + tid;
-    if (i < nkeep) {
-      const uint32_t d = sdig[i];
-      const uint64_t at = (uint64_t)(gdst[d] + (int64_t)i);
-      if (at < lim[d]) P.ent3[at] = stage[i];
+    for (int i = 0; i < kPartItems; i++) {
+      if (dg[i] == ~0u) continue;
+      const uint32_t d = dg[i] & 255u, pos = lbase[d] + (dg[i] >> 8);
+      stage[pos] = v[i];
+      sdig[pos] = (uint8_t)d;
+    }
+    __syncthreads();
+    const uint32_t nkeep = (uint32_t)sh64[kPartBlock / 64];
+#pragma unroll
+    for (int k = 0; k < kPartItems; k++) {
+      const uint32_t i = (uint32_t)k * kPartBlock + tid;
+      if (i < nkeep) {
+        const uint32_t d = sdig[i];
+        const uint64_t at = (uint64_t)(gdst[d] + (int64_t)i);
+        if (at < (uint64_t)(d + 1) * P.p1_region) P.ent3[at] = stage[i];
+      }
     }
   }
 }
@@ -1332,6 +1396,103 @@ __global__ __launch_bounds__(kPart2Block) void k_part2d(BuildParams P) {
       P.ent2[lo + gbase[b] + (i - roff[b])] = e;
     }
     __syncthreads();  // (the stage, roff and gbase are rewritten next round)
+  }
+}
+
+// k_part2f: k_part2d's staged scatter in ONE read of the digit's entries, into fixed bucket regions
+// (bucket b's entries at ent2[b * kPlaceLdsMax ..), as k_part2st writes them) for tables of more than
+// kP2SortedMaxBpp buckets per digit: no histogram pass, the bucket counts are the cursors at the end.
+// A bucket past kPlaceLdsMax entries flags p2_overflow (the host redoes the build with k_part2d's dense
+// runs; kPlaceLdsMax is 8 standard deviations over the mean bucket at the table's load).  The carry
+// functions are k_summary's (no slot counts here: bpp x 1024 of them do not fit the LDS).  Single GPU.
+__global__ __launch_bounds__(kPart2Block) void k_part2f(BuildParams P) {
+  // cur[nb] | rc0[nb] | rc1[nb] | roff[nb] | gbase[nb] | stage[kPart2Block * kP2dPer]
+  extern __shared__ __attribute__((aligned(16))) uint32_t dyn[];
+  __shared__ uint64_t sh64[kPart2Block / 64 + 1];
+  if (build_aborted(P)) return;
+  const uint32_t dpart = blockIdx.x;
+  const uint64_t lo = (uint64_t)dpart * P.p1_region;
+  const uint64_t hi = lo + min((uint64_t)P.p1_fill[dpart], P.p1_region);
+  const uint32_t nbins = P.bpp;
+  const uint32_t b0 = dpart * nbins;
+  uint32_t* cur = dyn;
+  uint32_t* rc[2] = {cur + nbins, cur + 2 * nbins};
+  uint32_t* roff = cur + 3 * nbins;
+  uint32_t* gbase = cur + 4 * nbins;
+  Entry* stage = reinterpret_cast<Entry*>(dyn + ((6 * nbins + 3) & ~3u));
+  constexpr uint32_t kRound = kPart2Block * kP2dPer;
+  const int tid = threadIdx.x;
+  for (uint32_t b = tid; b < 5 * nbins; b += kPart2Block) dyn[b] = 0;
+  __syncthreads();
+  const uint32_t per = (nbins + kPart2Block - 1) / kPart2Block;
+  bool ovf = false;
+  auto load_round = [&](Entry (&v)[kP2dPer], uint64_t i0) {
+#pragma unroll
+    for (int k = 0; k < kP2dPer; k++) {
+      const uint64_t i = i0 + (uint64_t)k * kPart2Block + tid;
+      if (i < hi) v[k] = P.ent3[i];
+    }
+  };
+  Entry nx[kP2dPer];
+  if (lo < hi) load_round(nx, lo);
+  int par = 0;
+  for (uint64_t i0 = lo; i0 < hi; i0 += kRound, par ^= 1) {
+    Entry v[kP2dPer];
+#pragma unroll
+    for (int k = 0; k < kP2dPer; k++) v[k] = nx[k];
+    if (i0 + kRound < hi) load_round(nx, i0 + kRound);  // (in flight through this round)
+    uint32_t* rcnt = rc[par];
+    uint32_t bk[kP2dPer], rk[kP2dPer];
+#pragma unroll
+    for (int k = 0; k < kP2dPer; k++) {
+      const uint64_t i = i0 + (uint64_t)k * kPart2Block + tid;
+      bk[k] = ~0u;
+      if (i >= hi) continue;
+      bk[k] = bucket_of(P, v[k].hash) - b0;
+      rk[k] = atomicAdd(&rcnt[bk[k]], 1u);
+    }
+    __syncthreads();
+    {  // the round's run offsets; each bucket's cursor moves past the round; the other parity's counts
+       // are cleared for the next round
+      uint64_t local = 0;
+      for (uint32_t q = 0; q < per; q++) {
+        const uint32_t b = tid * per + q;
+        if (b < nbins) local += rcnt[b];
+      }
+      uint64_t run = block_excl_sum<kPart2Block>(local, sh64, nullptr);
+      for (uint32_t q = 0; q < per; q++) {
+        const uint32_t b = tid * per + q;
+        if (b < nbins) {
+          roff[b] = (uint32_t)run;
+          gbase[b] = cur[b];
+          cur[b] += rcnt[b];
+          run += rcnt[b];
+          rc[par ^ 1][b] = 0;
+        }
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kP2dPer; k++)
+      if (bk[k] != ~0u) stage[roff[bk[k]] + rk[k]] = v[k];
+    __syncthreads();
+    const uint32_t nround = (uint32_t)min((uint64_t)kRound, hi - i0);
+    for (uint32_t i = tid; i < nround; i += kPart2Block) {
+      const Entry e = stage[i];
+      const uint32_t b = bucket_of(P, e.hash) - b0;
+      const uint32_t r = gbase[b] + (i - roff[b]);
+      if (r < kPlaceLdsMax) P.ent2[((uint64_t)b0 + b - P.b_lo) * kPlaceLdsMax + r] = e;
+      else ovf = true;
+    }
+    __syncthreads();  // (the stage, roff and gbase are rewritten next round)
+  }
+  if (ovf) atomicOr(&P.st->p2_overflow, 1u);
+  for (uint32_t b = tid; b < nbins; b += kPart2Block) {
+    const uint64_t bucket = (uint64_t)b0 + b;
+    if (bucket < P.nbuckets) {
+      P.boff[bucket] = (bucket - P.b_lo) * (uint64_t)kPlaceLdsMax;
+      P.bcount[bucket] = cur[b];
+    }
   }
 }
 
@@ -1695,8 +1856,72 @@ __device__ __forceinline__ bool is_put_pair(const Entry& x, const Entry& y) {  /
 constexpr int kPlaceRegBlock = 256;
 constexpr int kPlaceRegPer = kPlaceLdsMax / kPlaceRegBlock;
 
+// Look-back descriptors (P.lookback): bucket b's carry function F_b as 64 bits, flag 1 = F_b alone,
+// 2 = the inclusive prefix F_0 ... F_b.  The slope a (entries - slots) fits 32 bits and the constant c
+// 30 (the host allows the mode for capacity < 2^31 and fewer than 2^30 records).
+constexpr unsigned long long kLbAgg = 1ull << 62, kLbPre = 2ull << 62;
+__device__ __forceinline__ unsigned long long lb_pack(unsigned long long flag, MaxPlus f) {
+  const int64_t c = min(max(f.c, (int64_t)0), (int64_t)((1 << 30) - 1));
+  return flag | ((unsigned long long)c << 32) | (unsigned long long)(uint32_t)(int32_t)f.a;
+}
+__device__ __forceinline__ MaxPlus lb_unpack(unsigned long long w) {
+  MaxPlus f;
+  f.c = (int64_t)((w >> 32) & 0x3fffffffull);
+  f.a = (int64_t)(int32_t)(uint32_t)w;
+  return f;
+}
+
+// The exclusive carry prefix of bucket b (wave 0 of its block): publishes F_b, reads the descriptors
+// of the buckets before it 64 at a time (each lane one, spinning until it is published) back to the
+// nearest inclusive prefix, composes them in bucket order, and publishes b's inclusive prefix.  Blocks
+// start in bucket order, so every descriptor waited on belongs to a block that is running or done (the
+// wait is bounded all the same: lb_fail, and the host redoes the build with k_summary's carries).
+__device__ __forceinline__ MaxPlus lookback_prefix(const BuildParams& P, uint64_t b, MaxPlus f, int lane) {
+  const OpMaxPlus op;
+  unsigned long long* D = P.lb_desc;
+  if (lane == 0) __hip_atomic_store(&D[b], lb_pack(kLbAgg, f), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  MaxPlus ex{0, 0};
+  int64_t i = (int64_t)b - 1;
+  bool timed_out = false;
+  const unsigned long long t0 = wall_clock64();
+  while (i >= 0) {
+    const int64_t j = i - lane;
+    unsigned long long w = kLbPre;  // (lanes before bucket 0: the identity, as a prefix)
+    if (j >= 0) {
+      for (;;) {
+        w = __hip_atomic_load(&D[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (w >> 62) break;
+        if (wall_clock64() - t0 >= 200000000ull) {  // 2 s
+          timed_out = true;
+          w = kLbPre;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+    const unsigned long long pre = __ballot((w >> 62) == 2);
+    const int k = pre ? __builtin_ctzll(pre) : 63;  // the nearest inclusive prefix, or all 64
+    MaxPlus acc{0, 0};
+    for (int t = k; t >= 0; t--) {  // buckets i - k .. i in order
+      const unsigned long long wt = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(w >> 32), t) << 32) |
+                                    (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)w, t);
+      const MaxPlus g = lb_unpack(wt);
+      acc = t == k ? g : op(acc, g);
+    }
+    ex = op(acc, ex);
+    if (pre) break;
+    i -= 64;
+  }
+  if (__any(timed_out) && lane == 0) atomicOr(&P.st->lb_fail, 1u);
+  if (lane == 0) __hip_atomic_store(&D[b], lb_pack(kLbPre, op(ex, f)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return ex;
+}
+
 // One bucket of k_place_reg: bucket b_lo + bi; pre[] holds its fixed-region entries when `fixed`.
-__device__ __forceinline__ void place_reg_bucket(const BuildParams& P, uint64_t bi, const Entry (&pre)[kPlaceRegPer]) {
+// repair_x >= 0 (k_place_fix): place it again with that carry, without the pair list.
+template <bool kLookback>
+__device__ __forceinline__ void place_reg_bucket(const BuildParams& P, uint64_t bi, const Entry (&pre)[kPlaceRegPer],
+                                                 int64_t repair_x = -1) {
   constexpr int NW = kPlaceRegBlock / 64;
   static_assert(kBucket == 4 * kPlaceRegBlock, "four wanted slots per thread in the scan");
   __shared__ uint32_t cnt[kBucket / 2];          // 16-bit entry count per wanted slot
@@ -1723,18 +1948,21 @@ __device__ __forceinline__ void place_reg_bucket(const BuildParams& P, uint64_t 
   const uint64_t b = P.b_lo + bi;
   const uint32_t n = P.bcount[b];
   const uint64_t eoff = P.boff[b];
-  int64_t x;
-  if (P.fused_carry) {
+  const bool lookback = kLookback && repair_x < 0;  // (a kernel of its own: the look-back's registers)
+  int64_t x = 0;
+  if (repair_x >= 0) {
+    x = repair_x;
+  } else if (P.fused_carry) {
     const MaxPlus pre = P.bpre[b];
     x = max(pre.c, P.dcarry[b / P.bpp] + pre.a);
-  } else {
+  } else if (!lookback) {
     x = P.carry[b];
   }
-  if (ovf != 0 || nrec > P.max_records) return;  // build_aborted
-  if (P.fused_carry && tid == 0) P.carry[b] = x;  // (for the global-memory placement's readers)
+  if (ovf != 0 || nrec > P.max_records) return;  // build_aborted (every block alike: no look-back waits)
+  if ((P.fused_carry || repair_x >= 0) && tid == 0) P.carry[b] = x;  // (for the global-memory placement's readers)
   const uint64_t start = b << kBucketShift;
   const int64_t bsize = (int64_t)min((uint64_t)kBucket, P.cap - start);
-  if (n > kPlaceLdsMax) {
+  if (n > kPlaceLdsMax) {  // (never with fixed regions, the look-back's layout: p2_overflow above)
     if (tid == 0) atomicOr(&P.st->big_buckets, 1u);
     return;
   }
@@ -1817,6 +2045,23 @@ __device__ __forceinline__ void place_reg_bucket(const BuildParams& P, uint64_t 
     }
   }
   __syncthreads();
+  if (lookback) {  // the carry into the bucket from the buckets before it, assuming none wraps into bucket 0
+    __shared__ int64_t s_x;
+    if (wv == 0) {
+      const int32_t mlast = (int32_t)(meta[kBucket - 1] >> 16) - 32768;  // max over occupied s of s - base[s]
+      MaxPlus f;
+      f.a = (int64_t)n - bsize;
+      f.c = n ? max((int64_t)0, (int64_t)n + (int64_t)mlast - bsize) : 0;
+      const MaxPlus ex = lookback_prefix(P, b, f, lane);
+      if (lane == 0) {
+        s_x = max(ex.c, ex.a);  // (x0 = 0; k_place_fix places again what the real x0 changes)
+        P.bpre[b] = ex;
+        P.carry[b] = s_x;
+      }
+    }
+    __syncthreads();
+    x = s_x;
+  }
   uint32_t bw[kPlaceRegPer], g[kPlaceRegPer];
 #pragma unroll
   for (int k = 0; k < kPlaceRegPer; k++) {
@@ -1830,7 +2075,7 @@ __device__ __forceinline__ void place_reg_bucket(const BuildParams& P, uint64_t 
   __syncthreads();
   // Equal wanted slots in address order: each member counts the members with smaller addresses.
   // Equal-hash PUT pairs are duplicate-key candidates for the pair list (as k_place_reg).
-  const bool want_pairs = ndel == 0 && npairs0 <= P.pair_cap;
+  const bool want_pairs = ndel == 0 && npairs0 <= P.pair_cap && repair_x < 0;
   uint32_t npair = 0;
   uint32_t rank[kPlaceRegPer];
   bool same_prev[kPlaceRegPer];  // the member ranked just before this one has its hash
@@ -1978,6 +2223,7 @@ __device__ __forceinline__ void place_reg_bucket(const BuildParams& P, uint64_t 
 
 // k_place_reg: one block per bucket; the fixed regions' entry loads go out before the head's scalar
 // loads (slots past the count are never used), in one round trip.
+template <bool kLookback>
 __global__ __launch_bounds__(kPlaceRegBlock) void k_place_reg(BuildParams P) {
   Entry pre[kPlaceRegPer];
   if (P.p2_fixed) {
@@ -1985,7 +2231,42 @@ __global__ __launch_bounds__(kPlaceRegBlock) void k_place_reg(BuildParams P) {
 #pragma unroll
     for (int k = 0; k < kPlaceRegPer; k++) pre[k] = P.ent2[e0 + threadIdx.x + k * kPlaceRegBlock];
   }
-  place_reg_bucket(P, blockIdx.x, pre);
+  place_reg_bucket<kLookback>(P, blockIdx.x, pre);
+}
+
+// k_place_fix (P.lookback): the carry into bucket 0 is the ring's fixed point x0, the constant of all
+// the buckets' functions composed (when some slot stays empty); k_place_reg assumed 0.  Blocks
+// 0 .. kPlaceFixBuckets - 1 take buckets 0 .. kPlaceFixBuckets - 1: one whose carry x0 changes is placed
+// again (a carry that x0 leaves alone leaves every later one alone too: x0 + pre.a <= pre.c stays true
+// as buckets are composed on); the last block places the last bucket again, whose spill into bucket 0's
+// slots raced with bucket 0's first placement.  A change past the first kPlaceFixBuckets buckets flags
+// lb_fail (the host redoes the build with k_summary's carries).  A table with no empty slot flags
+// `full` (k_carry's rule), and the exact path builds it.
+constexpr int kPlaceFixBuckets = 16;
+__global__ __launch_bounds__(kPlaceRegBlock) void k_place_fix(BuildParams P) {
+  if (build_aborted(P)) return;
+  const uint64_t nb = P.nbuckets;
+  const MaxPlus tot = lb_unpack(P.lb_desc[nb - 1]);
+  if (tot.a >= 0) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(&P.st->full, 1u);
+    return;
+  }
+  const int64_t x0 = tot.c;
+  if (x0 == 0) return;  // (the common case: nothing wraps)
+  const bool tail = blockIdx.x == kPlaceFixBuckets;
+  const uint64_t b = tail ? nb - 1 : blockIdx.x;
+  if (b >= nb || (tail && nb - 1 < kPlaceFixBuckets)) return;  // (small tables: the last bucket is a block's)
+  const MaxPlus ex = P.bpre[b];
+  const int64_t x = max(ex.c, x0 + ex.a);
+  const bool last = b == nb - 1;
+  if (!last && x == P.carry[b]) return;
+  if (!tail && b == kPlaceFixBuckets - 1 && !last && threadIdx.x == 0) atomicOr(&P.st->lb_fail, 1u);
+  Entry pre[kPlaceRegPer];
+  const uint64_t e0 = b * kPlaceLdsMax;
+#pragma unroll
+  for (int k = 0; k < kPlaceRegPer; k++) pre[k] = P.ent2[e0 + threadIdx.x + k * kPlaceRegBlock];
+  __syncthreads();  // (every thread read carry[b] before the placement rewrites it)
+  place_reg_bucket<false>(P, b, pre, x);
 }
 
 // ================================================================================================
@@ -2017,7 +2298,8 @@ void launch_frame_uniform(const BuildParams& P, hipStream_t s, StageTimer* tm) {
   const uint64_t nblk = (P.uni_n + per - 1) / per;
   // the wave buffers, then the tile regrouped by digit in the same space (entries, digits, run
   // starts), and hist + rbase after either
-  const size_t body = std::max<size_t>((size_t)W * Q.uni_wbytes * (db ? 2 : 1), (size_t)kPartTile * (sizeof(Entry) + 1) + 1024);
+  const size_t bufs = (size_t)W * Q.uni_wbytes * (db ? 2 : 1);
+  const size_t body = P.p1_bucket ? bufs : std::max<size_t>(bufs, (size_t)kPartTile * (sizeof(Entry) + 1) + 1024);
   const size_t lds = body + 2048;
   Q.uni_hist_off = (uint32_t)body;
   hipLaunchKernelGGL((k_frame_uniform<W, db>), dim3((unsigned)nblk), dim3(64 * W), lds, s, Q);
@@ -2053,14 +2335,17 @@ static size_t part2d_lds(uint32_t bpp) {
   return (size_t)((6 * bpp + 3) & ~3u) * 4 + (size_t)kPart2Block * kP2dPer * sizeof(Entry);
 }
 
+bool part2f_fits(uint32_t bpp) { return part2d_lds(bpp) <= 158 * 1024; }
+
 // k_part2st's dynamic LDS (the 8-bit counts, the bucket words, the stage of `per` entries a thread)
 static size_t part2st_lds(uint32_t bpp, int per) {
   return (size_t)((bpp * 260 + 3) & ~3u) * 4 + (size_t)kPart2Block * per * sizeof(Entry);
 }
 
 void launch_partition(const BuildParams& P, hipStream_t s, StageTimer* tm) {
+  if (P.p1_bucket) return;  // (the framing wrote the bucket regions)
   if (!P.p1_region) launch_partition1(P, s);
-  else if (P.p1_kernel) hipLaunchKernelGGL(k_part1_regions, dim3((unsigned)P.p1_tiles), dim3(kPartBlock), 0, s, P);
+  else if (P.p1_kernel) hipLaunchKernelGGL(k_part1_regions, dim3((unsigned)P.p1r_tiles), dim3(kPartBlock), 0, s, P);
   // the largest stage (entries a thread per round) that fits: fewer rounds, fewer barriers
   constexpr size_t kLdsMax = 158 * 1024;
   const bool staged = P.p2_sorted && P.p2_fixed && P.fused_carry && P.p1_region && !P.p2_seg;
@@ -2072,6 +2357,8 @@ void launch_partition(const BuildParams& P, hipStream_t s, StageTimer* tm) {
     hipLaunchKernelGGL(k_part2st<4>, dim3(256), dim3(kPart2Block), part2st_lds(P.bpp, 4), s, P);
   else if (P.p2_sorted)
     hipLaunchKernelGGL(k_part2s, dim3(256), dim3(kPart2Block), (size_t)(514u * P.bpp) * sizeof(uint32_t), s, P);
+  else if (P.p2_fixed && P.p1_region && !P.p2_seg && part2d_lds(P.bpp) <= kLdsMax)
+    hipLaunchKernelGGL(k_part2f, dim3(256), dim3(kPart2Block), part2d_lds(P.bpp), s, P);
   else if (!P.p2_seg && part2d_lds(P.bpp) <= kLdsMax)
     hipLaunchKernelGGL(k_part2d, dim3(256), dim3(kPart2Block), part2d_lds(P.bpp), s, P);
   else
@@ -2081,7 +2368,8 @@ void launch_partition(const BuildParams& P, hipStream_t s, StageTimer* tm) {
 
 void launch_place_buckets(const BuildParams& P, hipStream_t s) {
   if (P.b_hi > P.b_lo)
-    hipLaunchKernelGGL(k_place_reg, dim3((unsigned)(P.b_hi - P.b_lo)), dim3(kPlaceRegBlock), 0, s, P);
+    hipLaunchKernelGGL(P.lookback ? k_place_reg<true> : k_place_reg<false>, dim3((unsigned)(P.b_hi - P.b_lo)),
+                       dim3(kPlaceRegBlock), 0, s, P);
   // buckets above kPlaceLdsMax entries (normally none; never with fixed bucket regions, whose
   // overflow redoes the build with dense runs)
   if (!P.p2_fixed) launch_place_global(P, s, 0, 1);
@@ -2089,8 +2377,10 @@ void launch_place_buckets(const BuildParams& P, hipStream_t s) {
 
 
 void launch_place_fast(const BuildParams& P, hipStream_t s, StageTimer* tm) {
-  if (!P.fused_carry) launch_summary_carry(P, s, tm);
+  if (P.lookback) (void)hipMemsetAsync(P.lb_desc, 0, P.nbuckets * sizeof(unsigned long long), s);
+  else if (!P.fused_carry) launch_summary_carry(P, s, tm);
   launch_place_buckets(P, s);
+  if (P.lookback) hipLaunchKernelGGL(k_place_fix, dim3(kPlaceFixBuckets + 1), dim3(kPlaceRegBlock), 0, s, P);
   tm->mark("place", s);
   if (!P.fused_carry) launch_verify(P, s, tm);  // (fused_carry: k_stats_folded verifies the pairs)
 }

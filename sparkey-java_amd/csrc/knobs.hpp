@@ -23,13 +23,13 @@ enum class Knob : int {
   Frame3Short,      // k_frame3: steps of the short walk
   Frame3Cover,      // k_frame3: mark reached starts (0 / 1)
   Frame3Stop,       // k_frame3: stop after this phase (instruction counts by phase)
-  Frame4,           // k_frame4: 0 off (k_frame3 frames one-byte-VLQ logs), 1 on
-  Frame4C,          // k_frame4: chunk per lane (bytes)
   FrameTicket,      // k_frame / k_frame3: regions by device-wide ticket, not by workgroup id
   FrameSpinTicks,   // bound on a wave's wait for its predecessor (100 MHz ticks)
   FrameDebug,       // k_frame / k_frame3 per-wave phase counters to stderr
   Part2Debug,       // k_part2s phase counters to stderr
   NoRegions,        // partition pass 1 into digit regions off (two-pass histogram partition)
+  NoLookback,       // k_place_reg's look-back carries off (k_summary, scan, k_carry)
+  NoBuckets,        // uniform framing into the bucket regions off (partition pass 1 into digit regions)
   RegionCap,        // digit region capacity (entries; tests force overflows)
   ExactSerial,      // the exact path on one lane over the whole table
   ExactDebug,       // exact path phase counters (2: synchronise each class)

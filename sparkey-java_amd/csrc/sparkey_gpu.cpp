@@ -623,24 +623,6 @@ static void set_geom(BuildParams& P, const FrameGeom& g) {
   P.fr_nchunks = g.nchunks;
 }
 
-// k_frame4 (frame4_kernels.hip): one chunk per lane, for the logs k_frame3 frames (one-byte VLQs,
-// records of at most 256 bytes).  The frame4 switch turns it on (1) or off (0).  Its geometry is
-// returned apart from P's (k_frame3 / k_frame, its fallbacks, keep theirs); f4_* are set on P.
-static bool want_frame4(BuildParams& P, const LogHdr& lh, int64_t entry, int64_t frame_end, FrameGeom* g) {
-  if (knob(Knob::Frame4) != 1 || !P.fr_fast || P.max_rec_len > 256) return false;
-  const int64_t nr = std::max<int64_t>(0, lh.num_puts) + std::max<int64_t>(0, lh.num_deletes);
-  const int64_t by = std::max<int64_t>(0, lh.put_size) + std::max<int64_t>(0, lh.delete_size);
-  if (nr <= 0 || by <= 0) return false;
-  BuildParams Q = P;
-  if (!frame4_geometry(Q, (double)by / (double)nr, knob_set(Knob::Frame4C) ? knob(Knob::Frame4C) : 0, entry,
-                       frame_end))
-    return false;
-  *g = get_geom(Q);
-  P.f4_rgn = Q.f4_rgn;
-  P.f4_m = Q.f4_m;
-  return true;
-}
-
 // Slab layout of the framing output and the workspace it needs (grown on demand).
 static int reserve_for_framing(sparkey_plan* pl, BuildParams& P, int framing_path, uint64_t nrec, uint32_t slab_cap,
                                char* err, size_t err_len) {
@@ -654,6 +636,17 @@ static int reserve_for_framing(sparkey_plan* pl, BuildParams& P, int framing_pat
   }
   P.part_group = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(kMaxPartGroup, kPartTile / P.slab_cap));
   P.p1_tiles = (uint32_t)std::max<uint64_t>(1, (P.nslabs + P.part_group - 1) / P.part_group);
+  // k_part1_regions' tiles: slabs of the mean count (the header's records over the slabs) to fill
+  // 0.9 kPartTile, at most 2 kPartTile entries whatever the counts (its two rounds); the slabs are sized
+  // for twice the mean, which left its tiles 40% full (an atomic per digit and tile on the fill cursors)
+  {
+    const double mean = (double)std::max<uint64_t>(nrec, 1) / (double)std::max<uint64_t>(P.nslabs, 1);
+    uint64_t g = (uint64_t)std::max(1.0, 0.9 * kPartTile / std::max(1.0, mean));
+    g = std::min<uint64_t>(g, std::min<uint64_t>(kMaxPartGroup, 2 * kPartTile / std::max<uint32_t>(P.slab_cap, 1)));
+    P.p1r_group = (uint32_t)std::max<uint64_t>(std::max<uint64_t>(g, 1), P.part_group);
+    if ((uint64_t)P.p1r_group * P.slab_cap > 2ull * kPartTile) P.p1r_group = P.part_group;
+    P.p1r_tiles = (uint32_t)std::max<uint64_t>(1, (P.nslabs + P.p1r_group - 1) / P.p1r_group);
+  }
   const uint64_t ent_cap = std::max<uint64_t>(1, P.nslabs * P.slab_cap);
   int rc = plan_reserve(pl, std::max<uint64_t>(P.nchunks, nwaves), std::max<uint64_t>(nrec, 1), ent_cap, P.nslabs,
                         P.p1_tiles, P.nbuckets, P.cap, err, err_len);
@@ -689,13 +682,12 @@ static int launch_framing(sparkey_plan* pl, const BuildParams& P, int framing_pa
     HIP_TRY(hipMemsetAsync(pl->desc, 0, (2 * nwaves + 2) * sizeof(unsigned long long), s));
     HIP_TRY(hipMemsetAsync(pl->wcount, 0, (P.nslabs + 1) * sizeof(uint32_t), s));
     if (P.del_parts) HIP_TRY(hipMemsetAsync(P.del_parts, 0, (size_t)kDelParts * 16 * sizeof(unsigned long long), s));
-    if (framing_path == 5) launch_frame4(P, s, &pl->timer);
-    else if (framing_path == 4) launch_frame3(P, s, &pl->timer);
+    if (framing_path == 4) launch_frame3(P, s, &pl->timer);
     else launch_frame_fused(P, s, &pl->timer);
     launch_sum_deletes(P, s);  // (the spread DELETE counters into the status block)
   } else if (framing_path == 2) {
     launch_frame_uniform(P, s, &pl->timer);
-    if (!P.p1_region) launch_dense_slabs(P, s);  // (with digit regions nothing reads the slab counts)
+    if (!P.p1_region && !P.p1_bucket) launch_dense_slabs(P, s);  // (with regions nothing reads the slab counts)
   } else {
     launch_framing_serial(P, s);
     launch_emit(P, s, &pl->timer);
@@ -1227,11 +1219,9 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
   // for the rest; both fall back to the serial walk, which alone reports errors
   const bool use_frame3 = fused_framing && want_frame3(P, lh, kLogHeaderSize, std::max<int64_t>(lh.data_end, kLogHeaderSize));
   const FrameGeom geom0 = get_geom(P);
-  FrameGeom geom4{};
-  const bool use_frame4 = use_frame3 && want_frame4(P, lh, kLogHeaderSize, std::max<int64_t>(lh.data_end, kLogHeaderSize), &geom4);
   // the serial_framing switch forces the exact serial walk (smoke() and the tests check every path)
   const bool force_serial = knob_on(Knob::SerialFraming);
-  const int spec_path = fused_framing && !force_serial ? (use_frame4 ? 5 : use_frame3 ? 4 : 0) : 1;
+  const int spec_path = fused_framing && !force_serial ? (use_frame3 ? 4 : 0) : 1;
   int framing_path = spec_path, placement_path = 0;
   if (const int64_t R = force_serial ? 0 : uniform_record_size(lh)) {  // k_frame_uniform: every record is exactly R bytes
     framing_path = 2;
@@ -1246,17 +1236,13 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
     const uint64_t nw = std::max<uint64_t>(1, g.nchunks ? (g.nchunks + g.w - 1) / g.w : 0);
     return (uint32_t)std::min<uint64_t>(kPartTile, std::max<uint64_t>(64, 2 * ((nrec + nw - 1) / nw) + 32));
   };
-  auto geom_for = [&](int path) -> const FrameGeom& { return path == 5 ? geom4 : geom0; };
-  int slab_path = framing_path;  // (the framing the slab size was chosen for)
-  uint32_t slab_cap = slab_for(geom_for(framing_path));
-  bool use_regions = !knob_on(Knob::NoRegions), regions_used = false;
+  uint32_t slab_cap = slab_for(geom0);
+  bool use_regions = !knob_on(Knob::NoRegions), regions_used = false, buckets_used = false;
   bool use_fixed = true;  // k_part2st / k_part2s in one pass into fixed bucket regions
-  for (int attempt = 0; attempt < 7; attempt++) {
-    set_geom(P, geom_for(framing_path));
-    if (slab_framing(framing_path) && framing_path != slab_path) {
-      slab_cap = slab_for(geom_for(framing_path));
-      slab_path = framing_path;
-    }
+  bool use_lookback = !knob_on(Knob::NoLookback);
+  bool use_buckets = !knob_on(Knob::NoBuckets);
+  for (int attempt = 0; attempt < 8; attempt++) {
+    set_geom(P, geom0);
     rc = reserve_for_framing(pl, P, framing_path, nrec, slab_cap, err, err_len);
     if (rc) return rc;
     if (knob_on(Knob::FrameDebug)) {  // per-wave phase counters: 16 words per k_frame / k_frame3 wave
@@ -1280,9 +1266,14 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
     // the other framings' slabs: pass 1 into the same fixed digit regions by k_part1_regions (one read
     // of the entries instead of k_part1_hist + k_part1_scatter's two)
     const bool slab_regions = !tiles;
+    // k_frame_uniform / k_frame3 where the look-back applies: each entry straight into its placement
+    // bucket's fixed region (an atomic on the bucket's count), no partition pass at all
+    const bool to_buckets = (tiles || framing_path == 4) && use_buckets && use_fixed && use_lookback && P.b_lo == 0 &&
+                            P.cap < (1ull << 31) && nrec < (1ull << 30);
+    P.p1_bucket = to_buckets ? 1 : 0;
     P.p1_region = 0;
     P.p1_kernel = 0;
-    if ((tiles || slab_regions) && use_regions) {
+    if ((tiles || slab_regions) && use_regions && !to_buckets) {
       const double expect = (double)nrec * (double)P.bpp * (double)kBucket / (double)P.cap;
       uint64_t rc_cap = ((uint64_t)(expect + 8.0 * std::sqrt(expect) + 1024.0) + 63) & ~63ull;
       if (knob_set(Knob::RegionCap)) rc_cap = std::max<uint64_t>(1, (uint64_t)knob(Knob::RegionCap));  // (tests)
@@ -1298,19 +1289,28 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
     }
     // the header, the status reset and the region cursors in one launch
     launch_build_init(d_out, hdr, pl->d_status, P.p1_region ? pl->p1_fill : nullptr, P.p1_region ? 256u : 0u, s);
-    P.p1_hist_ready = tiles && !P.p1_region ? 1 : 0;
+    P.p1_hist_ready = tiles && !P.p1_region && !to_buckets ? 1 : 0;
     regions_used = P.p1_region != 0 && !P.p1_kernel;  // (partition passes: 1 when the framing did pass 1)
+    buckets_used = to_buckets;                         // (0 when it wrote the buckets)
     // k_part2s: pass 2 also sorts each bucket by wanted slot and leaves the carry functions
-    P.p2_sorted = P.bpp <= kP2SortedMaxBpp ? 1 : 0;
-    P.p2_fixed = P.p2_sorted && use_fixed ? 1 : 0;
+    P.p2_sorted = P.bpp <= kP2SortedMaxBpp && !to_buckets ? 1 : 0;
+    // fixed bucket regions: k_part2st (fused carry) up to kP2SortedMaxBpp buckets a digit, k_part2f past
+    // that (from the digit regions of pass 1)
+    P.p2_fixed = use_fixed && (to_buckets || P.p2_sorted || (P.p1_region && part2f_fits(P.bpp))) ? 1 : 0;
     if (P.p2_fixed) {  // bucket b's entries at ent2[b * kPlaceLdsMax ..)
       HIP_TRY(grow(&pl->ent2, pl->c_ent2, std::max<uint64_t>(P.max_records, P.nbuckets * (uint64_t)kPlaceLdsMax)));
       P.ent2 = pl->ent2;
     }
+    if (to_buckets) HIP_TRY(hipMemsetAsync(P.bcount, 0, P.nbuckets * sizeof(uint32_t), s));  // (the cursors)
     P.fold_stats = 1;  // the stats parts from the placement (k_stats only for buckets it could not place)
     // the carry composition inside k_part2st / k_part2s (their fixed-region pass), no summary / scan /
     // carry kernels
-    P.fused_carry = P.p2_fixed ? 1 : 0;
+    P.fused_carry = P.p2_fixed && P.p2_sorted ? 1 : 0;
+    // past kP2SortedMaxBpp buckets a digit (k_part2f), k_place_reg composes the carries itself by a
+    // look-back over the buckets (k_summary's read of every entry, the scan and k_carry go)
+    P.lookback = !P.fused_carry && P.p2_fixed && use_lookback && P.b_lo == 0 && P.cap < (1ull << 31) &&
+                         std::max<uint64_t>(nrec, P.max_records) < (1ull << 30) ? 1 : 0;
+    P.lb_desc = reinterpret_cast<unsigned long long*>(pl->bfun);  // (bfun: 16 bytes a bucket, unused then)
     P.dfun = pl->dfun;
     P.dcarry = pl->dcarry;
     if (P.fused_carry) {
@@ -1343,10 +1343,6 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
               (unsigned long long)st.err, (unsigned long long)(st.err >> 8));
     // (a digit region filled by k_part1_regions is the partition's business, not the framing's)
     const unsigned fspec = st.spec_fail & ~(P.p1_kernel ? kSpecRegionFull : 0u);
-    if (framing_path == 5 && (fspec || st.err != ~0ull)) {  // k_frame4's lists: k_frame3 (or k_frame)
-      framing_path = use_frame3 ? 4 : 0;
-      continue;
-    }
     if (framing_path == 4 && (fspec || st.err != ~0ull)) {  // k_frame3's lists or speculation: k_frame
       framing_path = 0;
       continue;
@@ -1357,6 +1353,10 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
     }
     if (st.p2_overflow && P.p2_fixed) {  // a bucket outgrew its fixed region: dense bucket runs
       use_fixed = false;
+      continue;
+    }
+    if (st.lb_fail && P.lookback) {  // the look-back's wait or its wrap repair gave up: k_summary's carries
+      use_lookback = false;
       continue;
     }
     if ((st.spec_fail & kSpecRegionFull) && (P.p1_kernel || !(st.spec_fail & ~kSpecRegionFull))) {
@@ -1402,7 +1402,9 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
     // The exact path replays the entries in log order, from the framing's slabs (`ent`).  The slab
     // framings left them there (k_part1_regions only read them); the uniform framing wrote straight
     // into the digit regions, so it frames again into `ent`.
-    if (P.p1_region && !P.p1_kernel) {
+    const bool reframe = (P.p1_region && !P.p1_kernel) || (P.p1_bucket && framing_path == 2);
+    P.p1_bucket = 0;  // (k_frame3 left its slabs as well)
+    if (reframe) {
       P.p1_region = 0;
       rc = launch_framing(pl, P, framing_path, s, err, err_len);
       if (rc) return rc;
@@ -1449,7 +1451,7 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
       pl->stage_ms.push_back(t);
     }
   }
-  fill_stats(stats_out, st, ip, placement_path, framing_path, ms, regions_used ? 1 : 2);
+  fill_stats(stats_out, st, ip, placement_path, framing_path, ms, buckets_used ? 0 : regions_used ? 1 : 2);
   return SPARKEY_OK;
 }
 
@@ -1923,14 +1925,11 @@ int sparkey_shard_find_entry(sparkey_plan* pl, uint64_t lo, uint64_t window, voi
 // synchronous sparkey_shard_frame and the speculative sparkey_shard_frame_bin_async).
 struct ShardFrameSetup {
   BuildParams P;
-  bool fused = false, use_frame3 = false, use_frame4 = false, use_regions = true;
-  int spec_path() const {
-    return fused && !knob_on(Knob::SerialFraming) ? (use_frame4 ? 5 : use_frame3 ? 4 : 0) : 1;
-  }
+  bool fused = false, use_frame3 = false, use_regions = true;
+  int spec_path() const { return fused && !knob_on(Knob::SerialFraming) ? (use_frame3 ? 4 : 0) : 1; }
   int framing_path = 1;
   uint64_t nrec = 0;
-  FrameGeom geom0, geom4{};
-  const FrameGeom& geom(int path) const { return path == 5 ? geom4 : geom0; }
+  FrameGeom geom0;
   uint32_t slab_cap = 0;
   int slab_path = 0;
 };
@@ -1957,7 +1956,6 @@ static int shard_frame_setup(sparkey_plan* pl, int64_t entry, int64_t frame_end,
                        frac * 1.05) + 4096;
   F->use_frame3 = F->fused && want_frame3(P, sh.lh, entry, frame_end);
   F->geom0 = get_geom(P);
-  F->use_frame4 = F->use_frame3 && want_frame4(P, sh.lh, entry, frame_end, &F->geom4);
   F->framing_path = F->spec_path();
   const int64_t R = uniform_record_size(sh.lh);
   if (R && (entry - kLogHeaderSize) % R == 0) {  // a record start of a uniform log: frame by stride
@@ -1966,7 +1964,7 @@ static int shard_frame_setup(sparkey_plan* pl, int64_t entry, int64_t frame_end,
     P.uni_rec = R;
     F->nrec = P.uni_n;
   }
-  F->slab_cap = shard_slab_for(F->geom(F->framing_path), F->nrec);
+  F->slab_cap = shard_slab_for(F->geom0, F->nrec);
   F->slab_path = F->framing_path;
   F->use_regions = !knob_on(Knob::NoRegions);
   return SPARKEY_OK;
@@ -1975,9 +1973,9 @@ static int shard_frame_setup(sparkey_plan* pl, int64_t entry, int64_t frame_end,
 // Launches one framing attempt of the set-up (status reset first); no synchronisation.
 static int shard_frame_launch(sparkey_plan* pl, ShardFrameSetup* F, hipStream_t s, char* err, size_t err_len) {
   BuildParams& P = F->P;
-  set_geom(P, F->geom(F->framing_path));
+  set_geom(P, F->geom0);
   if (slab_framing(F->framing_path) && F->framing_path != F->slab_path) {
-    F->slab_cap = shard_slab_for(F->geom(F->framing_path), F->nrec);
+    F->slab_cap = shard_slab_for(F->geom0, F->nrec);
     F->slab_path = F->framing_path;
   }
   int rc = reserve_for_framing(pl, P, F->framing_path, F->nrec, F->slab_cap, err, err_len);
@@ -2048,10 +2046,6 @@ static int shard_frame_sync(sparkey_plan* pl, int64_t entry, int64_t frame_end, 
     }
     if (st.overflow || st.n_records > P.max_records) {
       F.nrec = std::max<uint64_t>(st.n_records, F.nrec * 2 + 1);
-      continue;
-    }
-    if (path == 5 && (st.spec_fail || st.err != ~0ull)) {
-      F.framing_path = F.use_frame3 ? 4 : 0;
       continue;
     }
     if (path == 4 && (st.spec_fail || st.err != ~0ull)) {
@@ -2256,6 +2250,8 @@ int sparkey_shard_summarize_dev(sparkey_plan* pl, const uint8_t* d_recv, uint64_
   P.nslabs = (std::max<uint64_t>(n_recv, 1) + kPartTile - 1) / kPartTile;
   P.part_group = 1;
   P.p1_tiles = (uint32_t)P.nslabs;
+  P.p1r_group = 1;
+  P.p1r_tiles = P.p1_tiles;
   {
     const Entry* keep = pl->ent3;  // (ent3 holds the local entries: it must not be reallocated)
     rc = plan_reserve(pl, 1, std::max<uint64_t>(n_recv, 1), 1, P.nslabs, P.p1_tiles, P.nbuckets, P.cap, err,

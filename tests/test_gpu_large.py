@@ -69,6 +69,31 @@ def test_c3_100m_mixed_keys(native, c3_log, c3_want):
     assert stats.framing_path in (0, 4) and stats.placement_path == 0
 
 
+@pytest.mark.parametrize("sw", [{}, {"no_buckets": 1}, {"no_buckets": 1, "no_lookback": 1}])
+def test_mixed_20m_fixed_bucket_regions(native, switch, sw):
+    """20M mixed records: 25,391 placement buckets, 100 a digit.  By default k_frame3 writes every entry
+    straight into its bucket's fixed region and k_place_reg composes the carries by look-back; with the
+    bucket regions off, pass 1 goes to digit regions and pass 2 is k_part2f (past k_part2st's 64 buckets
+    a digit: one read into the fixed bucket regions), with the look-back or k_summary's carries."""
+    from sparkey import synth
+    switch(**sw)
+    log = synth.mixed_log(20_000_000, 8, 64, 100, seed=11)
+    got, stats = device_build(native, log, 91)
+    want = _want_20m(log)
+    assert got == want, diff_report(got, want)
+    assert stats.placement_path == 0
+    assert stats.partition_passes == (2 if sw else 0), stats.as_dict()
+
+
+_W20 = {}
+
+
+def _want_20m(log):
+    if "w" not in _W20:
+        _W20["w"] = oracle.build_index(log, 91)
+    return _W20["w"]
+
+
 def test_c5_100m_sorting(native, c3_log, c3_want):
     """SORTING on the C3 log: identical to IN_MEMORY for unique keys (TestSparkeyWriter.java:9-36)."""
     got, stats = device_build(native, c3_log, 77, method=SORTING)

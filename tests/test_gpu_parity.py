@@ -552,3 +552,40 @@ def test_eof_inside_second_vlq(native):
     from helpers import with_trailing_bytes
     got, want = same_error(native, with_trailing_bytes(make_log(key_value_puts(300)), b"\x05\x80"))
     assert got == want == native.E_CORRUPT_RECORD
+
+
+# --- the look-back placement's wrap (k_place_fix): runs that spill past the table's last slot ---
+@pytest.mark.parametrize("spill,mixed", [(40, False), (900, False), (900, True), (0, False)])
+def test_lookback_wrap_repair(native, switch, spill, mixed):
+    """Keys whose wanted slots crowd the last 4-45 slots of the table (and no other key wants the last
+    bucket): their run spills past the end into bucket 0 (the ring's carry x0 > 0; IndexHash.java:562-665
+    wraps the probe), which k_place_reg's look-back assumed empty.  k_place_fix places the first buckets
+    again (x0 = 900 pushes bucket 0's own run into bucket 1 and on) and the last one, whose spill raced
+    with bucket 0's first placement.  Uniform records go straight into the bucket regions
+    (k_frame_uniform), mixed ones through k_frame3; the bytes are the oracle's, and again with the
+    look-back off (k_summary's carries)."""
+    n = 3000
+    cap = 1 | int(n * 1.3)
+    seed = 77
+    window = max(4, spill // 20)  # (groups of equal wanted slots stay under kGroupMax = 64)
+    crowd, rest, i = [], [], 0
+    while len(crowd) < spill or len(rest) < n - spill:
+        k = b"w%07d" % i
+        i += 1
+        slot = oracle.key_hash(4, k, seed) % cap
+        if slot >= cap - window:
+            if len(crowd) < spill:
+                crowd.append(k)
+        elif slot < cap - 1100 and len(rest) < n - spill:
+            rest.append(k)
+    keys = rest[: (n - spill) // 2] + crowd + rest[(n - spill) // 2:]
+    rng = np.random.default_rng(spill)
+    puts = [(k, b"v%05d" % j + (bytes(int(rng.integers(0, 20))) if mixed else b"")) for j, k in enumerate(keys)]
+    log = make_log(puts)
+    got, stats = check(native, log, seed, hash_size=4)
+    assert stats.capacity == cap and stats.placement_path == 0, stats.as_dict()
+    assert stats.framing_path == (4 if mixed else 2), stats.as_dict()
+    assert stats.partition_passes == 0, stats.as_dict()  # (the framing wrote the bucket regions)
+    switch(no_lookback=1)
+    got2, _ = gpu_build(native, log, seed, 4)
+    assert got2 == got

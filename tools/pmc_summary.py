@@ -59,9 +59,9 @@ def main(src, dst, workload=None):
     stage_kernels = {"frame": ["k_frame", "k_frame_uniform", "k_frame2", "k_frame3", "k_frame_lane", "k_frame_lane_act",
                                "k_frame_lane_flags"], "frame_uniform": ["k_frame_uniform"],
                      "partition": ["k_part1_hist", "k_part1_scatter", "k_part1_regions", "k_part2", "k_part2s", "k_part2st", "k_part2d",
-                                   "k_scan_tiles"],
-                     "partition_regions": ["k_part2", "k_part2s", "k_part2st", "k_part2d"],
-                     "place": ["k_place_lds", "k_place_reg", "k_place_reg_persist", "k_place"],
+                                   "k_part2f", "k_scan_tiles"],
+                     "partition_regions": ["k_part2", "k_part2s", "k_part2st", "k_part2d", "k_part2f"],
+                     "place": ["k_place_lds", "k_place_reg", "k_place_reg_persist", "k_place", "k_place_fix"],
                      "stats": ["k_stats", "k_stats_final", "k_stats_folded"],
                      "summary": ["k_summary", "k_carry"], "verify": ["k_verify_pairs"]}
     for st, ks in stage_kernels.items():
@@ -74,6 +74,12 @@ def main(src, dst, workload=None):
                 ok = True
         if ok:
             out["per_launch_hbm_bytes"][st] = tot
+    # the whole build: every kernel's bytes per dispatch times its dispatches per build (one k_build_init
+    # a single-GPU build; a sharded rank counts its frame launches)
+    ref = next((k for k in ("k_build_init", "k_frame_uniform", "k_frame3", "k_frame") if k in out["kernels"]), None)
+    if ref and all("hbm_bytes" in r for k, r in out["kernels"].items() if r["total_ns"] > 0.01 * out["kernels"][ref]["total_ns"]):
+        nb = out["kernels"][ref]["calls"]
+        out["per_launch_hbm_bytes"]["build"] = sum(r.get("hbm_bytes", 0.0) * r["calls"] / nb for r in out["kernels"].values())
     os.makedirs(os.path.dirname(dst), exist_ok=True)
     if workload:  # merge: one summary file holds every workload's counters
         try:
