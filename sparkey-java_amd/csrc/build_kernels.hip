@@ -158,7 +158,8 @@ __global__ __launch_bounds__(kPlaceBlock) void k_summary(BuildParams P) {
   const uint64_t start = b << kBucketShift;
   const int64_t bsize = (int64_t)min((uint64_t)kBucket, P.cap - start);
   const uint32_t n = P.bcount[b];
-  const uint64_t eoff = P.boff[b];
+  // (the framing's bucket regions: bucket b at b * kPlaceLdsMax, no offsets written)
+  const uint64_t eoff = P.p1_bucket ? (b - P.b_lo) * (uint64_t)kPlaceLdsMax : P.boff[b];
   bucket_histogram(P, b, n, eoff, start, cnt);
   uint32_t mlast = 0;
   bucket_scan(cnt, base, M, sh64, shm, &mlast);

@@ -105,7 +105,7 @@ struct Status {
   unsigned int stats_ticket;     // k_stats_folded: blocks done
   unsigned long long acc_sum, acc_col, acc_max;  // k_stats_folded: totals over its blocks
   unsigned int p2_ticket;        // fused_carry: k_part2s blocks done (the last composes the digits)
-  unsigned int lb_fail;          // k_place_reg look-back: a wait ran out or a repair did not close (redo)
+  unsigned int pad3;
 };
 
 struct BuildParams {
@@ -223,11 +223,8 @@ struct BuildParams {
   int32_t p1_kernel;    // with p1_region: k_part1_regions fills the regions from the slabs (else the framing did)
   int32_t p1_pad;
   int32_t p2_sorted;    // k_part2s: per-(bucket, slot) counts in the same pass + the carry functions
-  int32_t p1_bucket;    // k_frame_uniform writes each entry into its bucket's fixed region (no partition);
+  int32_t p1_bucket;    // k_frame3 writes each entry into its bucket's fixed region (no partition);
                         // bcount[] is the atomic cursor, zeroed before the framing
-  int32_t lookback;     // k_place_reg composes the bucket carries itself (decoupled look-back over
-                        // lb_desc, no k_summary / scan / k_carry); k_place_fix repairs the wrap
-  unsigned long long* lb_desc;  // per bucket: flag << 62 | carry constant << 32 | (int32) slope
   int32_t p2_fixed;     // k_part2s in one pass: bucket b's entries at ent2[b * kPlaceLdsMax, + bcount[b])
   int32_t fold_stats;   // k_place_reg leaves calculateMaxDisplacement's per-bucket parts (no k_stats pass)
   int32_t stats_if_pending;  // k_stats / k_stats_final only when the folded stats left stats_pending

@@ -682,8 +682,7 @@ __global__ __launch_bounds__(64 * W) void k_frame_uniform(BuildParams P) {
   // else with p1_hist_ready each tile's digit counts are k_part1_hist's output
   const bool to_regions = P.p1_region != 0;
   const bool with_hist = to_regions || P.p1_hist_ready != 0;
-  // to_buckets (P.p1_bucket): no partition at all -- each entry goes straight to its placement bucket's
-  // fixed region (ent2[bucket * kPlaceLdsMax ..), its place from an atomic on the bucket's count)
+
   if (with_hist) {
     for (int t = threadIdx.x; t < kSub * 256; t += 64 * W) hist[t] = 0;
     __syncthreads();
@@ -756,9 +755,7 @@ __global__ __launch_bounds__(64 * W) void k_frame_uniform(BuildParams P) {
         const uint64_t hash = P.hash_size == 8 ? murmur64_ld(ld, klen, (uint32_t)P.seed)
                                                : (uint64_t)murmur32_ld(ld, klen, (uint32_t)P.seed);
         hsh[r] = hash;
-        if (P.p1_bucket) {
-          dr[r] = (uint32_t)bucket_of(P, hash);
-        } else if (!to_regions) {
+        if (!to_regions) {
           Entry en;
           en.hash = hash;
           en.addr = (uint64_t)p << P.ebb;
@@ -772,28 +769,6 @@ __global__ __launch_bounds__(64 * W) void k_frame_uniform(BuildParams P) {
       }
     }
     __builtin_amdgcn_wave_barrier();  // every lane is done with the buffer before the next round's DMA
-  }
-  if (P.p1_bucket) {
-    // the tile's places: every atomic in flight at once (one round trip), then the entries
-    uint32_t at[kRounds];
-#pragma unroll
-    for (int r = 0; r < kRounds; r++)
-      if (dr[r] != ~0u) at[r] = atomicAdd(&P.bcount[dr[r]], 1u);
-    bool ovf = false;
-#pragma unroll
-    for (int r = 0; r < kRounds; r++) {
-      if (dr[r] == ~0u) continue;
-      if (at[r] >= kPlaceLdsMax) {
-        ovf = true;
-        continue;
-      }
-      Entry en;
-      en.hash = hsh[r];
-      en.addr = (uint64_t)(P.fr_entry + (int64_t)(blk0 + (uint64_t)(r * W + wave) * 64 + lane) * R) << P.ebb;
-      P.ent2[(uint64_t)dr[r] * kPlaceLdsMax + at[r]] = en;
-    }
-    if (ovf) atomicOr(&P.st->p2_overflow, 1u);
-    return;
   }
   if (!with_hist) return;
   __syncthreads();
@@ -1856,72 +1831,8 @@ __device__ __forceinline__ bool is_put_pair(const Entry& x, const Entry& y) {  /
 constexpr int kPlaceRegBlock = 256;
 constexpr int kPlaceRegPer = kPlaceLdsMax / kPlaceRegBlock;
 
-// Look-back descriptors (P.lookback): bucket b's carry function F_b as 64 bits, flag 1 = F_b alone,
-// 2 = the inclusive prefix F_0 ... F_b.  The slope a (entries - slots) fits 32 bits and the constant c
-// 30 (the host allows the mode for capacity < 2^31 and fewer than 2^30 records).
-constexpr unsigned long long kLbAgg = 1ull << 62, kLbPre = 2ull << 62;
-__device__ __forceinline__ unsigned long long lb_pack(unsigned long long flag, MaxPlus f) {
-  const int64_t c = min(max(f.c, (int64_t)0), (int64_t)((1 << 30) - 1));
-  return flag | ((unsigned long long)c << 32) | (unsigned long long)(uint32_t)(int32_t)f.a;
-}
-__device__ __forceinline__ MaxPlus lb_unpack(unsigned long long w) {
-  MaxPlus f;
-  f.c = (int64_t)((w >> 32) & 0x3fffffffull);
-  f.a = (int64_t)(int32_t)(uint32_t)w;
-  return f;
-}
-
-// The exclusive carry prefix of bucket b (wave 0 of its block): publishes F_b, reads the descriptors
-// of the buckets before it 64 at a time (each lane one, spinning until it is published) back to the
-// nearest inclusive prefix, composes them in bucket order, and publishes b's inclusive prefix.  Blocks
-// start in bucket order, so every descriptor waited on belongs to a block that is running or done (the
-// wait is bounded all the same: lb_fail, and the host redoes the build with k_summary's carries).
-__device__ __forceinline__ MaxPlus lookback_prefix(const BuildParams& P, uint64_t b, MaxPlus f, int lane) {
-  const OpMaxPlus op;
-  unsigned long long* D = P.lb_desc;
-  if (lane == 0) __hip_atomic_store(&D[b], lb_pack(kLbAgg, f), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  MaxPlus ex{0, 0};
-  int64_t i = (int64_t)b - 1;
-  bool timed_out = false;
-  const unsigned long long t0 = wall_clock64();
-  while (i >= 0) {
-    const int64_t j = i - lane;
-    unsigned long long w = kLbPre;  // (lanes before bucket 0: the identity, as a prefix)
-    if (j >= 0) {
-      for (;;) {
-        w = __hip_atomic_load(&D[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (w >> 62) break;
-        if (wall_clock64() - t0 >= 200000000ull) {  // 2 s
-          timed_out = true;
-          w = kLbPre;
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
-    }
-    const unsigned long long pre = __ballot((w >> 62) == 2);
-    const int k = pre ? __builtin_ctzll(pre) : 63;  // the nearest inclusive prefix, or all 64
-    MaxPlus acc{0, 0};
-    for (int t = k; t >= 0; t--) {  // buckets i - k .. i in order
-      const unsigned long long wt = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(w >> 32), t) << 32) |
-                                    (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)w, t);
-      const MaxPlus g = lb_unpack(wt);
-      acc = t == k ? g : op(acc, g);
-    }
-    ex = op(acc, ex);
-    if (pre) break;
-    i -= 64;
-  }
-  if (__any(timed_out) && lane == 0) atomicOr(&P.st->lb_fail, 1u);
-  if (lane == 0) __hip_atomic_store(&D[b], lb_pack(kLbPre, op(ex, f)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  return ex;
-}
-
 // One bucket of k_place_reg: bucket b_lo + bi; pre[] holds its fixed-region entries when `fixed`.
-// repair_x >= 0 (k_place_fix): place it again with that carry, without the pair list.
-template <bool kLookback>
-__device__ __forceinline__ void place_reg_bucket(const BuildParams& P, uint64_t bi, const Entry (&pre)[kPlaceRegPer],
-                                                 int64_t repair_x = -1) {
+__device__ __forceinline__ void place_reg_bucket(const BuildParams& P, uint64_t bi, const Entry (&pre)[kPlaceRegPer]) {
   constexpr int NW = kPlaceRegBlock / 64;
   static_assert(kBucket == 4 * kPlaceRegBlock, "four wanted slots per thread in the scan");
   __shared__ uint32_t cnt[kBucket / 2];          // 16-bit entry count per wanted slot
@@ -1948,21 +1859,18 @@ __device__ __forceinline__ void place_reg_bucket(const BuildParams& P, uint64_t 
   const uint64_t b = P.b_lo + bi;
   const uint32_t n = P.bcount[b];
   const uint64_t eoff = P.boff[b];
-  const bool lookback = kLookback && repair_x < 0;  // (a kernel of its own: the look-back's registers)
-  int64_t x = 0;
-  if (repair_x >= 0) {
-    x = repair_x;
-  } else if (P.fused_carry) {
+  int64_t x;
+  if (P.fused_carry) {
     const MaxPlus pre = P.bpre[b];
     x = max(pre.c, P.dcarry[b / P.bpp] + pre.a);
-  } else if (!lookback) {
+  } else {
     x = P.carry[b];
   }
-  if (ovf != 0 || nrec > P.max_records) return;  // build_aborted (every block alike: no look-back waits)
-  if ((P.fused_carry || repair_x >= 0) && tid == 0) P.carry[b] = x;  // (for the global-memory placement's readers)
+  if (ovf != 0 || nrec > P.max_records) return;  // build_aborted
+  if (P.fused_carry && tid == 0) P.carry[b] = x;  // (for the global-memory placement's readers)
   const uint64_t start = b << kBucketShift;
   const int64_t bsize = (int64_t)min((uint64_t)kBucket, P.cap - start);
-  if (n > kPlaceLdsMax) {  // (never with fixed regions, the look-back's layout: p2_overflow above)
+  if (n > kPlaceLdsMax) {  // (never with fixed regions: p2_overflow above)
     if (tid == 0) atomicOr(&P.st->big_buckets, 1u);
     return;
   }
@@ -2045,23 +1953,6 @@ __device__ __forceinline__ void place_reg_bucket(const BuildParams& P, uint64_t 
     }
   }
   __syncthreads();
-  if (lookback) {  // the carry into the bucket from the buckets before it, assuming none wraps into bucket 0
-    __shared__ int64_t s_x;
-    if (wv == 0) {
-      const int32_t mlast = (int32_t)(meta[kBucket - 1] >> 16) - 32768;  // max over occupied s of s - base[s]
-      MaxPlus f;
-      f.a = (int64_t)n - bsize;
-      f.c = n ? max((int64_t)0, (int64_t)n + (int64_t)mlast - bsize) : 0;
-      const MaxPlus ex = lookback_prefix(P, b, f, lane);
-      if (lane == 0) {
-        s_x = max(ex.c, ex.a);  // (x0 = 0; k_place_fix places again what the real x0 changes)
-        P.bpre[b] = ex;
-        P.carry[b] = s_x;
-      }
-    }
-    __syncthreads();
-    x = s_x;
-  }
   uint32_t bw[kPlaceRegPer], g[kPlaceRegPer];
 #pragma unroll
   for (int k = 0; k < kPlaceRegPer; k++) {
@@ -2075,7 +1966,7 @@ __device__ __forceinline__ void place_reg_bucket(const BuildParams& P, uint64_t 
   __syncthreads();
   // Equal wanted slots in address order: each member counts the members with smaller addresses.
   // Equal-hash PUT pairs are duplicate-key candidates for the pair list (as k_place_reg).
-  const bool want_pairs = ndel == 0 && npairs0 <= P.pair_cap && repair_x < 0;
+  const bool want_pairs = ndel == 0 && npairs0 <= P.pair_cap;
   uint32_t npair = 0;
   uint32_t rank[kPlaceRegPer];
   bool same_prev[kPlaceRegPer];  // the member ranked just before this one has its hash
@@ -2223,7 +2114,6 @@ __device__ __forceinline__ void place_reg_bucket(const BuildParams& P, uint64_t 
 
 // k_place_reg: one block per bucket; the fixed regions' entry loads go out before the head's scalar
 // loads (slots past the count are never used), in one round trip.
-template <bool kLookback>
 __global__ __launch_bounds__(kPlaceRegBlock) void k_place_reg(BuildParams P) {
   Entry pre[kPlaceRegPer];
   if (P.p2_fixed) {
@@ -2231,42 +2121,7 @@ __global__ __launch_bounds__(kPlaceRegBlock) void k_place_reg(BuildParams P) {
 #pragma unroll
     for (int k = 0; k < kPlaceRegPer; k++) pre[k] = P.ent2[e0 + threadIdx.x + k * kPlaceRegBlock];
   }
-  place_reg_bucket<kLookback>(P, blockIdx.x, pre);
-}
-
-// k_place_fix (P.lookback): the carry into bucket 0 is the ring's fixed point x0, the constant of all
-// the buckets' functions composed (when some slot stays empty); k_place_reg assumed 0.  Blocks
-// 0 .. kPlaceFixBuckets - 1 take buckets 0 .. kPlaceFixBuckets - 1: one whose carry x0 changes is placed
-// again (a carry that x0 leaves alone leaves every later one alone too: x0 + pre.a <= pre.c stays true
-// as buckets are composed on); the last block places the last bucket again, whose spill into bucket 0's
-// slots raced with bucket 0's first placement.  A change past the first kPlaceFixBuckets buckets flags
-// lb_fail (the host redoes the build with k_summary's carries).  A table with no empty slot flags
-// `full` (k_carry's rule), and the exact path builds it.
-constexpr int kPlaceFixBuckets = 16;
-__global__ __launch_bounds__(kPlaceRegBlock) void k_place_fix(BuildParams P) {
-  if (build_aborted(P)) return;
-  const uint64_t nb = P.nbuckets;
-  const MaxPlus tot = lb_unpack(P.lb_desc[nb - 1]);
-  if (tot.a >= 0) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(&P.st->full, 1u);
-    return;
-  }
-  const int64_t x0 = tot.c;
-  if (x0 == 0) return;  // (the common case: nothing wraps)
-  const bool tail = blockIdx.x == kPlaceFixBuckets;
-  const uint64_t b = tail ? nb - 1 : blockIdx.x;
-  if (b >= nb || (tail && nb - 1 < kPlaceFixBuckets)) return;  // (small tables: the last bucket is a block's)
-  const MaxPlus ex = P.bpre[b];
-  const int64_t x = max(ex.c, x0 + ex.a);
-  const bool last = b == nb - 1;
-  if (!last && x == P.carry[b]) return;
-  if (!tail && b == kPlaceFixBuckets - 1 && !last && threadIdx.x == 0) atomicOr(&P.st->lb_fail, 1u);
-  Entry pre[kPlaceRegPer];
-  const uint64_t e0 = b * kPlaceLdsMax;
-#pragma unroll
-  for (int k = 0; k < kPlaceRegPer; k++) pre[k] = P.ent2[e0 + threadIdx.x + k * kPlaceRegBlock];
-  __syncthreads();  // (every thread read carry[b] before the placement rewrites it)
-  place_reg_bucket<false>(P, b, pre, x);
+  place_reg_bucket(P, blockIdx.x, pre);
 }
 
 // ================================================================================================
@@ -2298,8 +2153,7 @@ void launch_frame_uniform(const BuildParams& P, hipStream_t s, StageTimer* tm) {
   const uint64_t nblk = (P.uni_n + per - 1) / per;
   // the wave buffers, then the tile regrouped by digit in the same space (entries, digits, run
   // starts), and hist + rbase after either
-  const size_t bufs = (size_t)W * Q.uni_wbytes * (db ? 2 : 1);
-  const size_t body = P.p1_bucket ? bufs : std::max<size_t>(bufs, (size_t)kPartTile * (sizeof(Entry) + 1) + 1024);
+  const size_t body = std::max<size_t>((size_t)W * Q.uni_wbytes * (db ? 2 : 1), (size_t)kPartTile * (sizeof(Entry) + 1) + 1024);
   const size_t lds = body + 2048;
   Q.uni_hist_off = (uint32_t)body;
   hipLaunchKernelGGL((k_frame_uniform<W, db>), dim3((unsigned)nblk), dim3(64 * W), lds, s, Q);
@@ -2368,8 +2222,7 @@ void launch_partition(const BuildParams& P, hipStream_t s, StageTimer* tm) {
 
 void launch_place_buckets(const BuildParams& P, hipStream_t s) {
   if (P.b_hi > P.b_lo)
-    hipLaunchKernelGGL(P.lookback ? k_place_reg<true> : k_place_reg<false>, dim3((unsigned)(P.b_hi - P.b_lo)),
-                       dim3(kPlaceRegBlock), 0, s, P);
+    hipLaunchKernelGGL(k_place_reg, dim3((unsigned)(P.b_hi - P.b_lo)), dim3(kPlaceRegBlock), 0, s, P);
   // buckets above kPlaceLdsMax entries (normally none; never with fixed bucket regions, whose
   // overflow redoes the build with dense runs)
   if (!P.p2_fixed) launch_place_global(P, s, 0, 1);
@@ -2377,10 +2230,8 @@ void launch_place_buckets(const BuildParams& P, hipStream_t s) {
 
 
 void launch_place_fast(const BuildParams& P, hipStream_t s, StageTimer* tm) {
-  if (P.lookback) (void)hipMemsetAsync(P.lb_desc, 0, P.nbuckets * sizeof(unsigned long long), s);
-  else if (!P.fused_carry) launch_summary_carry(P, s, tm);
+  if (!P.fused_carry) launch_summary_carry(P, s, tm);
   launch_place_buckets(P, s);
-  if (P.lookback) hipLaunchKernelGGL(k_place_fix, dim3(kPlaceFixBuckets + 1), dim3(kPlaceRegBlock), 0, s, P);
   tm->mark("place", s);
   if (!P.fused_carry) launch_verify(P, s, tm);  // (fused_carry: k_stats_folded verifies the pairs)
 }

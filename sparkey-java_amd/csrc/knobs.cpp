@@ -19,7 +19,7 @@ const char* const kNames[kN] = {
     "no_uniform",     "no_frame3",        "serial_framing",   "frame_cmin",     "frame_region",
     "frame_look",     "frame3_c",         "frame3_short",     "frame3_cover",   "frame3_stop",
     "frame_ticket",     "frame_spin_ticks", "frame_debug",    "part2_debug",
-    "no_regions",     "no_lookback",      "no_buckets",       "region_cap",       "exact_serial",     "exact_debug",    "exact_reframe",
+    "no_regions",     "no_buckets",       "region_cap",       "exact_serial",     "exact_debug",    "exact_reframe",
     "exact_full_table", "snappy_lds",     "snappy_dir_a",     "snappy_dir_debug", "snappy_chunk",
     "snappy_serial_dir", "zstd_lds",      "shard_sync_frame", "shard_transport", "shard_fail_rank", "file_threads",
     "file_write_threads", "file_debug"};

@@ -28,7 +28,6 @@ enum class Knob : int {
   FrameDebug,       // k_frame / k_frame3 per-wave phase counters to stderr
   Part2Debug,       // k_part2s phase counters to stderr
   NoRegions,        // partition pass 1 into digit regions off (two-pass histogram partition)
-  NoLookback,       // k_place_reg's look-back carries off (k_summary, scan, k_carry)
   NoBuckets,        // uniform framing into the bucket regions off (partition pass 1 into digit regions)
   RegionCap,        // digit region capacity (entries; tests force overflows)
   ExactSerial,      // the exact path on one lane over the whole table

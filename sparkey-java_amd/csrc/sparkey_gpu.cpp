@@ -568,6 +568,9 @@ static bool want_frame3(BuildParams& P, const LogHdr& lh, int64_t entry, int64_t
   while ((1ll << cs) < want) cs++;
   while (cs > 7 && (double)(1ll << cs) / mean > 8.0 && (1ll << (cs - 1)) >= P.max_rec_len) cs--;
   int64_t region = 8192;
+  // small records (WriteHashBenchmark's key_i / value_i: 26 bytes): a region whose records fit the
+  // wave's lists (0.55 x 512) rather than 8 KiB
+  region = std::max<int64_t>(1ll << cs, std::min<int64_t>(region, (int64_t)(0.55 * 512 * mean)));
   if (knob_set(Knob::FrameRegion)) region = std::min<int64_t>(16384, std::max<int64_t>(2048, knob(Knob::FrameRegion)));
   BuildParams Q = P;
   const int64_t C = 1ll << cs;
@@ -687,7 +690,7 @@ static int launch_framing(sparkey_plan* pl, const BuildParams& P, int framing_pa
     launch_sum_deletes(P, s);  // (the spread DELETE counters into the status block)
   } else if (framing_path == 2) {
     launch_frame_uniform(P, s, &pl->timer);
-    if (!P.p1_region && !P.p1_bucket) launch_dense_slabs(P, s);  // (with regions nothing reads the slab counts)
+    if (!P.p1_region) launch_dense_slabs(P, s);  // (with digit regions nothing reads the slab counts)
   } else {
     launch_framing_serial(P, s);
     launch_emit(P, s, &pl->timer);
@@ -1239,7 +1242,6 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
   uint32_t slab_cap = slab_for(geom0);
   bool use_regions = !knob_on(Knob::NoRegions), regions_used = false, buckets_used = false;
   bool use_fixed = true;  // k_part2st / k_part2s in one pass into fixed bucket regions
-  bool use_lookback = !knob_on(Knob::NoLookback);
   bool use_buckets = !knob_on(Knob::NoBuckets);
   for (int attempt = 0; attempt < 8; attempt++) {
     set_geom(P, geom0);
@@ -1266,10 +1268,10 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
     // the other framings' slabs: pass 1 into the same fixed digit regions by k_part1_regions (one read
     // of the entries instead of k_part1_hist + k_part1_scatter's two)
     const bool slab_regions = !tiles;
-    // k_frame_uniform / k_frame3 where the look-back applies: each entry straight into its placement
-    // bucket's fixed region (an atomic on the bucket's count), no partition pass at all
-    const bool to_buckets = (tiles || framing_path == 4) && use_buckets && use_fixed && use_lookback && P.b_lo == 0 &&
-                            P.cap < (1ull << 31) && nrec < (1ull << 30);
+    // k_frame3: each entry straight into its placement bucket's fixed region (an atomic on the bucket's
+    // count), no partition pass at all.  (k_frame_uniform keeps its pass 1 into the digit regions: its
+    // per-tile digit runs beat an atomic per entry, C2 frame 0.28 against 0.62 ms, profiles/r04/)
+    const bool to_buckets = framing_path == 4 && use_buckets && use_fixed && P.b_lo == 0;
     P.p1_bucket = to_buckets ? 1 : 0;
     P.p1_region = 0;
     P.p1_kernel = 0;
@@ -1306,11 +1308,6 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
     // the carry composition inside k_part2st / k_part2s (their fixed-region pass), no summary / scan /
     // carry kernels
     P.fused_carry = P.p2_fixed && P.p2_sorted ? 1 : 0;
-    // past kP2SortedMaxBpp buckets a digit (k_part2f), k_place_reg composes the carries itself by a
-    // look-back over the buckets (k_summary's read of every entry, the scan and k_carry go)
-    P.lookback = !P.fused_carry && P.p2_fixed && use_lookback && P.b_lo == 0 && P.cap < (1ull << 31) &&
-                         std::max<uint64_t>(nrec, P.max_records) < (1ull << 30) ? 1 : 0;
-    P.lb_desc = reinterpret_cast<unsigned long long*>(pl->bfun);  // (bfun: 16 bytes a bucket, unused then)
     P.dfun = pl->dfun;
     P.dcarry = pl->dcarry;
     if (P.fused_carry) {
@@ -1355,10 +1352,7 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
       use_fixed = false;
       continue;
     }
-    if (st.lb_fail && P.lookback) {  // the look-back's wait or its wrap repair gave up: k_summary's carries
-      use_lookback = false;
-      continue;
-    }
+
     if ((st.spec_fail & kSpecRegionFull) && (P.p1_kernel || !(st.spec_fail & ~kSpecRegionFull))) {
       use_regions = false;  // a digit region filled up (skewed hashes): the two-pass partition
       continue;
@@ -1402,7 +1396,7 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
     // The exact path replays the entries in log order, from the framing's slabs (`ent`).  The slab
     // framings left them there (k_part1_regions only read them); the uniform framing wrote straight
     // into the digit regions, so it frames again into `ent`.
-    const bool reframe = (P.p1_region && !P.p1_kernel) || (P.p1_bucket && framing_path == 2);
+    const bool reframe = P.p1_region && !P.p1_kernel;
     P.p1_bucket = 0;  // (k_frame3 left its slabs as well)
     if (reframe) {
       P.p1_region = 0;

@@ -69,12 +69,12 @@ def test_c3_100m_mixed_keys(native, c3_log, c3_want):
     assert stats.framing_path in (0, 4) and stats.placement_path == 0
 
 
-@pytest.mark.parametrize("sw", [{}, {"no_buckets": 1}, {"no_buckets": 1, "no_lookback": 1}])
+@pytest.mark.parametrize("sw", [{}, {"no_buckets": 1}, {"no_buckets": 1, "no_frame3": 1}])
 def test_mixed_20m_fixed_bucket_regions(native, switch, sw):
     """20M mixed records: 25,391 placement buckets, 100 a digit.  By default k_frame3 writes every entry
-    straight into its bucket's fixed region and k_place_reg composes the carries by look-back; with the
-    bucket regions off, pass 1 goes to digit regions and pass 2 is k_part2f (past k_part2st's 64 buckets
-    a digit: one read into the fixed bucket regions), with the look-back or k_summary's carries."""
+    straight into its bucket's fixed region; with the bucket regions off (or k_frame framing), pass 1
+    goes to digit regions and pass 2 is k_part2f (past k_part2st's 64 buckets a digit: one read into the
+    fixed bucket regions).  The carries are k_summary's."""
     from sparkey import synth
     switch(**sw)
     log = synth.mixed_log(20_000_000, 8, 64, 100, seed=11)

@@ -554,18 +554,16 @@ def test_eof_inside_second_vlq(native):
     assert got == want == native.E_CORRUPT_RECORD
 
 
-# --- the look-back placement's wrap (k_place_fix): runs that spill past the table's last slot ---
-@pytest.mark.parametrize("spill,mixed", [(40, False), (900, False), (900, True), (0, False)])
-def test_lookback_wrap_repair(native, switch, spill, mixed):
+# --- the ring's wrap: runs that spill past the table's last slot into bucket 0 ---
+@pytest.mark.parametrize("spill,mixed", [(40, False), (900, False), (900, True), (40, True), (0, True)])
+def test_wrap_into_bucket_0(native, switch, spill, mixed):
     """Keys whose wanted slots crowd the last 4-45 slots of the table (and no other key wants the last
-    bucket): their run spills past the end into bucket 0 (the ring's carry x0 > 0; IndexHash.java:562-665
-    wraps the probe), which k_place_reg's look-back assumed empty.  k_place_fix places the first buckets
-    again (x0 = 900 pushes bucket 0's own run into bucket 1 and on) and the last one, whose spill raced
-    with bucket 0's first placement.  Uniform records go straight into the bucket regions
-    (k_frame_uniform), mixed ones through k_frame3; the bytes are the oracle's, and again with the
-    look-back off (k_summary's carries)."""
+    bucket): their run spills past the end into bucket 0 and on (the ring's carry x0 > 0;
+    IndexHash.java:562-665 wraps the probe).  Uniform records take k_frame_uniform's digit regions and
+    k_part2st's fused carries; mixed ones k_frame3's bucket regions and k_summary's carries, and again
+    through the digit regions (no_buckets).  The bytes are the oracle's."""
     n = 3000
-    cap = 1 | int(n * 1.3)
+    cap = 1 | int(n * 2.0)  # (sparsity 2: every bucket's entries fit its fixed region of 1024)
     seed = 77
     window = max(4, spill // 20)  # (groups of equal wanted slots stay under kGroupMax = 64)
     crowd, rest, i = [], [], 0
@@ -580,12 +578,14 @@ def test_lookback_wrap_repair(native, switch, spill, mixed):
             rest.append(k)
     keys = rest[: (n - spill) // 2] + crowd + rest[(n - spill) // 2:]
     rng = np.random.default_rng(spill)
-    puts = [(k, b"v%05d" % j + (bytes(int(rng.integers(0, 20))) if mixed else b"")) for j, k in enumerate(keys)]
+    # (mixed: values of 90-110 random bytes, C3's record sizes)
+    puts = [(k, b"v%05d" % j + (rng.integers(0, 256, size=int(rng.integers(84, 105)), dtype=np.uint8).tobytes()
+                                if mixed else b"")) for j, k in enumerate(keys)]
     log = make_log(puts)
-    got, stats = check(native, log, seed, hash_size=4)
+    got, stats = check(native, log, seed, hash_size=4, sparsity=2.0)
     assert stats.capacity == cap and stats.placement_path == 0, stats.as_dict()
     assert stats.framing_path == (4 if mixed else 2), stats.as_dict()
-    assert stats.partition_passes == 0, stats.as_dict()  # (the framing wrote the bucket regions)
-    switch(no_lookback=1)
-    got2, _ = gpu_build(native, log, seed, 4)
-    assert got2 == got
+    assert stats.partition_passes == (0 if mixed else 1), stats.as_dict()
+    switch(no_buckets=1)
+    got2, st2 = gpu_build(native, log, seed, 4, sparsity=2.0)
+    assert got2 == got and st2.partition_passes == (2 if mixed else 1), st2.as_dict()

@@ -16,5 +16,7 @@ timeout -k 10 300 python -u bench.py --steps 20 --warmup 3 > $O/c2.jsonl 2> $O/c
 SPARKEY_DEBUG=no_buckets=1 timeout -k 10 300 python -u bench.py --steps 20 --warmup 3 --no-parity > $O/c2_nob.jsonl 2> $O/c2_nob.err &&
 SPARKEY_DEBUG=no_buckets=1 timeout -k 10 400 python -u bench.py --workload c3 --entries 100000000 --steps 5 --warmup 1 \
   > $O/c3_100m_nob.jsonl 2> $O/c3_100m_nob.err &&
+timeout -k 10 300 python -u bench.py --workload c1x --steps 20 --warmup 3 > $O/c1x.jsonl 2> $O/c1x.err &&
+SPARKEY_DEBUG=no_frame3=1 timeout -k 10 300 python -u bench.py --workload c1x --steps 20 --warmup 3 --no-parity > $O/c1x_kframe.jsonl 2> $O/c1x_kframe.err &&
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof_c3_100m -o run -- \
   python -u bench.py --workload c3 --entries 100000000 --steps 5 --warmup 1 --no-parity > $O/prof_c3_100m.log 2>&1
