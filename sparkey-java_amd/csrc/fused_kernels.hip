@@ -1903,12 +1903,7 @@ __device__ __forceinline__ void place_reg_bucket(const BuildParams& P, uint64_t 
     const uint32_t w0 = cnt[2 * tid], w1 = cnt[2 * tid + 1];
     const uint32_t c[4] = {w0 & 0xffffu, w0 >> 16, w1 & 0xffffu, w1 >> 16};
     const uint32_t tot = c[0] + c[1] + c[2] + c[3];
-    uint32_t incl = tot;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t t = __shfl_up(incl, o, 64);
-      if (lane >= o) incl += t;
-    }
+    const uint32_t incl = wave_incl_sum_u32(tot);  // (DPP: no LDS crossbar round trips)
     constexpr int32_t kNone = -(1 << 20);
     uint32_t lb[4];
     int32_t v = kNone;  // max over this thread's occupied slots of s - (wave-local base)
@@ -1921,12 +1916,7 @@ __device__ __forceinline__ void place_reg_bucket(const BuildParams& P, uint64_t 
         run += c[i];
       }
     }
-    int32_t mi = v;  // inclusive wave prefix max
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const int32_t t = __shfl_up(mi, o, 64);
-      if (lane >= o) mi = max(mi, t);
-    }
+    const int32_t mi = wave_incl_max_i32(v);  // inclusive wave prefix max
     if (lane == 63) {
       wsum[wv] = incl;
       wmax[wv] = mi;
@@ -1941,8 +1931,7 @@ __device__ __forceinline__ void place_reg_bucket(const BuildParams& P, uint64_t 
         off += wsum[u];
       }
     }
-    int32_t ex = __shfl_up(mi, 1, 64);  // exclusive wave prefix max (wave-local), then block-level
-    if (lane == 0) ex = kNone;
+    const int32_t ex = wave_prev_i32(mi, kNone);  // exclusive wave prefix max (wave-local), then block-level
     int32_t m = max(pre, ex == kNone ? kNone : ex - (int32_t)off);
 #pragma unroll
     for (int i = 0; i < 4; i++) {

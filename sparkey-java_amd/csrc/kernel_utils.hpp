@@ -97,6 +97,16 @@ __device__ __forceinline__ int32_t wave_prev_i32(int32_t v, int32_t first) {
 __device__ __forceinline__ int32_t wave_next_i32(int32_t v, int32_t last) {
   return __builtin_amdgcn_update_dpp(last, v, 0x130, 0xf, 0xf, false);
 }
+// Inclusive prefix max over the wave's lanes (DPP, as wave_incl_sum_u32).
+__device__ __forceinline__ int32_t wave_incl_max_i32(int32_t v) {
+  v = max(v, __builtin_amdgcn_update_dpp(INT32_MIN, v, 0x111, 0xf, 0xf, false));  // row_shr:1
+  v = max(v, __builtin_amdgcn_update_dpp(INT32_MIN, v, 0x112, 0xf, 0xf, false));  // row_shr:2
+  v = max(v, __builtin_amdgcn_update_dpp(INT32_MIN, v, 0x114, 0xf, 0xf, false));  // row_shr:4
+  v = max(v, __builtin_amdgcn_update_dpp(INT32_MIN, v, 0x118, 0xf, 0xf, false));  // row_shr:8
+  v = max(v, __builtin_amdgcn_update_dpp(INT32_MIN, v, 0x142, 0xa, 0xf, false));  // row_bcast:15
+  v = max(v, __builtin_amdgcn_update_dpp(INT32_MIN, v, 0x143, 0xc, 0xf, false));  // row_bcast:31
+  return v;
+}
 __device__ __forceinline__ int32_t wave_max_i32(int32_t v) {  // (v >= 0 lanes only matter: 0 shifts in)
   v = max(v, __builtin_amdgcn_update_dpp(INT32_MIN, v, 0x111, 0xf, 0xf, false));
   v = max(v, __builtin_amdgcn_update_dpp(INT32_MIN, v, 0x112, 0xf, 0xf, false));

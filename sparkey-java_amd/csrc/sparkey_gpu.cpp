@@ -568,9 +568,6 @@ static bool want_frame3(BuildParams& P, const LogHdr& lh, int64_t entry, int64_t
   while ((1ll << cs) < want) cs++;
   while (cs > 7 && (double)(1ll << cs) / mean > 8.0 && (1ll << (cs - 1)) >= P.max_rec_len) cs--;
   int64_t region = 8192;
-  // small records (WriteHashBenchmark's key_i / value_i: 26 bytes): a region whose records fit the
-  // wave's lists (0.55 x 512) rather than 8 KiB
-  region = std::max<int64_t>(1ll << cs, std::min<int64_t>(region, (int64_t)(0.55 * 512 * mean)));
   if (knob_set(Knob::FrameRegion)) region = std::min<int64_t>(16384, std::max<int64_t>(2048, knob(Knob::FrameRegion)));
   BuildParams Q = P;
   const int64_t C = 1ll << cs;

@@ -22,6 +22,10 @@ for spec in "$@"; do
     > $D/fetch.log 2>&1 || exit 1
   timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $D/write -o run -- python3 bench.py $A \
     > $D/write.log 2>&1 || exit 1
+  if [ -n "$SQ" ]; then
+    timeout -k 10 400 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
+      GRBM_GUI_ACTIVE --output-format csv -d $D/sq -o run -- python3 bench.py $A > $D/sq.log 2>&1 || exit 1
+  fi
   python3 tools/pmc_summary.py $D $O/r04_pmc_summary.json $W > $D/summary.txt 2>&1 || exit 1
   cat $D/summary.txt
 done
