@@ -477,9 +477,6 @@ __device__ __forceinline__ void frame3_region(const BuildParams& P, const uint64
   mark(4);
   if (P.f3_stop == 4) { fail(kF3Caps); return; }  // (SPARKEY_FRAME3_STOP: measurements)
   unsigned long long ndel = 0;
-  // p1_bucket: the entries go to the slab as always, and once the wave's entry is verified, from there
-  // (this lane's own stores) straight to their buckets' regions, an atomic each -- so that a round redone
-  // after a wrong guess of the entry does not count twice
   uint32_t total = 0;
   unsigned long long base = 0;
   for (;;) {
@@ -530,9 +527,18 @@ __device__ __forceinline__ void frame3_region(const BuildParams& P, const uint64
     const int32_t csrc = sel >= 0 ? sel * kF3Lcap + at : 0;
     mark(5);
     if (P.f3_stop == 5) { fail(kF3Caps); return; }  // (SPARKEY_FRAME3_STOP: measurements)
+    if (P.p1_bucket && spec) {  // (bucket regions: the entries leave as they are hashed, so the guessed
+      const int64_t real = wait_prev();  // entry is checked first -- a redone round must not count twice)
+      spec = false;
+      if (real != ext) {
+        ext = real;
+        continue;
+      }
+    }
     // ---- 5 hash ----
     base = wv * (unsigned long long)P.slab_cap;
     ndel = 0;
+    bool bovf = false;
     for (uint32_t r = (uint32_t)lane; r < total; r += 64) {
       int32_t src = 0;
       for (int j = 0; j < nw; j++) {  // (wave-uniform)
@@ -554,8 +560,16 @@ __device__ __forceinline__ void frame3_region(const BuildParams& P, const uint64
       Entry en;
       en.hash = hash;
       en.addr = addr;
-      P.ent[base + r] = en;
+      if (!P.p1_bucket) {
+        P.ent[base + r] = en;
+      } else if (h.put) {  // straight into the bucket's region (DELETEs stay out of the placement)
+        const uint32_t b = bucket_of(P, hash);
+        const uint32_t a = atomicAdd(&P.bcount[b], 1u);
+        if (a < kPlaceLdsMax) P.ent2[(uint64_t)b * kPlaceLdsMax + a] = en;
+        else bovf = true;
+      }
     }
+    if (bovf) atomicOr(&P.st->p2_overflow, 1u);
     if (spec) {  // check the guessed entry against the published exit; redo on a mismatch
       const int64_t real = wait_prev();
       spec = false;
@@ -565,18 +579,6 @@ __device__ __forceinline__ void frame3_region(const BuildParams& P, const uint64
       }
     }
     break;
-  }
-  if (P.p1_bucket) {  // the verified entries into their buckets (PUTs: DELETEs stay out of the placement)
-    bool ovf = false;
-    for (uint32_t r = (uint32_t)lane; r < total; r += 64) {
-      const Entry en = P.ent[base + r];
-      if (en.addr & kDelBit) continue;
-      const uint32_t b = bucket_of(P, en.hash);
-      const uint32_t a = atomicAdd(&P.bcount[b], 1u);
-      if (a < kPlaceLdsMax) P.ent2[(uint64_t)b * kPlaceLdsMax + a] = en;
-      else ovf = true;
-    }
-    if (ovf) atomicOr(&P.st->p2_overflow, 1u);
   }
   ndel = wave_sum_u64(ndel);
   if (ndel && lane == 0) add_deletes(P, wv, ndel);

@@ -1392,13 +1392,28 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
     P.p2_sorted = 0;
     // The exact path replays the entries in log order, from the framing's slabs (`ent`).  The slab
     // framings left them there (k_part1_regions only read them); the uniform framing wrote straight
-    // into the digit regions, so it frames again into `ent`.
-    const bool reframe = P.p1_region && !P.p1_kernel;
-    P.p1_bucket = 0;  // (k_frame3 left its slabs as well)
+    // into the digit regions and k_frame3 into the bucket regions, so they frame again into `ent`.
+    const bool reframe = (P.p1_region && !P.p1_kernel) || P.p1_bucket;  // (k_frame3 wrote the buckets only)
+    P.p1_bucket = 0;
     if (reframe) {
       P.p1_region = 0;
-      rc = launch_framing(pl, P, framing_path, s, err, err_len);
-      if (rc) return rc;
+      // (its DELETE count is the first framing's; a speculative framing that does not hold this time
+      // -- a wait that ran out -- goes down the framing paths like the first one did)
+      const unsigned long long ndel0 = st.n_deletes;
+      for (int fp = framing_path;;) {
+        HIP_TRY(hipMemsetAsync(&pl->d_status->spec_fail, 0, sizeof(unsigned), s));
+        set_geom(P, geom0);
+        rc = launch_framing(pl, P, fp, s, err, err_len);
+        if (rc) return rc;
+        HIP_TRY(hipMemcpyAsync(pl->h_status, pl->d_status, sizeof(Status), hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        if (!st.spec_fail || fp == 1) break;
+        fp = fp == 4 ? 0 : 1;
+        rc = reserve_for_framing(pl, P, fp, std::max<uint64_t>(nrec, st.n_records), slab_cap, err, err_len);
+        if (rc) return rc;
+      }
+      st.n_deletes = ndel0;
+      HIP_TRY(hipMemcpyAsync(&pl->d_status->n_deletes, &ndel0, sizeof(ndel0), hipMemcpyHostToDevice, s));
     }
     P.p1_region = 0;
     P.p1_kernel = 0;
