@@ -1379,9 +1379,12 @@ __global__ __launch_bounds__(kPart2Block) void k_part2d(BuildParams P) {
 // kP2SortedMaxBpp buckets per digit: no histogram pass, the bucket counts are the cursors at the end.
 // A bucket past kPlaceLdsMax entries flags p2_overflow (the host redoes the build with k_part2d's dense
 // runs; kPlaceLdsMax is 8 standard deviations over the mean bucket at the table's load).  The carry
-// functions are k_summary's (no slot counts here: bpp x 1024 of them do not fit the LDS).  Single GPU.
+// functions are k_summary's (no slot counts here: bpp x 1024 of them do not fit the LDS).  kPer entries
+// a thread per round: 6 where the LDS holds them, fewer for the largest tables (C4's 4960 buckets a
+// digit: 2, whose rounds are shorter than the bucket count -- runs of about one entry).  Single GPU.
+template <int kPer>
 __global__ __launch_bounds__(kPart2Block) void k_part2f(BuildParams P) {
-  // cur[nb] | rc0[nb] | rc1[nb] | roff[nb] | gbase[nb] | stage[kPart2Block * kP2dPer]
+  // cur[nb] | rc0[nb] | rc1[nb] | roff[nb] | gbase[nb] | stage[kPart2Block * kPer]
   extern __shared__ __attribute__((aligned(16))) uint32_t dyn[];
   __shared__ uint64_t sh64[kPart2Block / 64 + 1];
   if (build_aborted(P)) return;
@@ -1394,32 +1397,32 @@ __global__ __launch_bounds__(kPart2Block) void k_part2f(BuildParams P) {
   uint32_t* rc[2] = {cur + nbins, cur + 2 * nbins};
   uint32_t* roff = cur + 3 * nbins;
   uint32_t* gbase = cur + 4 * nbins;
-  Entry* stage = reinterpret_cast<Entry*>(dyn + ((6 * nbins + 3) & ~3u));
-  constexpr uint32_t kRound = kPart2Block * kP2dPer;
+  Entry* stage = reinterpret_cast<Entry*>(dyn + ((5 * nbins + 3) & ~3u));
+  constexpr uint32_t kRound = kPart2Block * kPer;
   const int tid = threadIdx.x;
   for (uint32_t b = tid; b < 5 * nbins; b += kPart2Block) dyn[b] = 0;
   __syncthreads();
   const uint32_t per = (nbins + kPart2Block - 1) / kPart2Block;
   bool ovf = false;
-  auto load_round = [&](Entry (&v)[kP2dPer], uint64_t i0) {
+  auto load_round = [&](Entry (&v)[kPer], uint64_t i0) {
 #pragma unroll
-    for (int k = 0; k < kP2dPer; k++) {
+    for (int k = 0; k < kPer; k++) {
       const uint64_t i = i0 + (uint64_t)k * kPart2Block + tid;
       if (i < hi) v[k] = P.ent3[i];
     }
   };
-  Entry nx[kP2dPer];
+  Entry nx[kPer];
   if (lo < hi) load_round(nx, lo);
   int par = 0;
   for (uint64_t i0 = lo; i0 < hi; i0 += kRound, par ^= 1) {
-    Entry v[kP2dPer];
+    Entry v[kPer];
 #pragma unroll
-    for (int k = 0; k < kP2dPer; k++) v[k] = nx[k];
+    for (int k = 0; k < kPer; k++) v[k] = nx[k];
     if (i0 + kRound < hi) load_round(nx, i0 + kRound);  // (in flight through this round)
     uint32_t* rcnt = rc[par];
-    uint32_t bk[kP2dPer], rk[kP2dPer];
+    uint32_t bk[kPer], rk[kPer];
 #pragma unroll
-    for (int k = 0; k < kP2dPer; k++) {
+    for (int k = 0; k < kPer; k++) {
       const uint64_t i = i0 + (uint64_t)k * kPart2Block + tid;
       bk[k] = ~0u;
       if (i >= hi) continue;
@@ -1448,7 +1451,7 @@ __global__ __launch_bounds__(kPart2Block) void k_part2f(BuildParams P) {
     }
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < kP2dPer; k++)
+    for (int k = 0; k < kPer; k++)
       if (bk[k] != ~0u) stage[roff[bk[k]] + rk[k]] = v[k];
     __syncthreads();
     const uint32_t nround = (uint32_t)min((uint64_t)kRound, hi - i0);
@@ -1462,6 +1465,50 @@ __global__ __launch_bounds__(kPart2Block) void k_part2f(BuildParams P) {
     __syncthreads();  // (the stage, roff and gbase are rewritten next round)
   }
   if (ovf) atomicOr(&P.st->p2_overflow, 1u);
+  for (uint32_t b = tid; b < nbins; b += kPart2Block) {
+    const uint64_t bucket = (uint64_t)b0 + b;
+    if (bucket < P.nbuckets) {
+      P.boff[bucket] = (bucket - P.b_lo) * (uint64_t)kPlaceLdsMax;
+      P.bcount[bucket] = cur[b];
+    }
+  }
+}
+
+// k_part2f for tables whose rounds would hold about one entry per bucket (more than 3072 buckets a
+// digit: C4's 4960): no stage, each entry stored at its bucket cursor's place (an LDS atomic), eight
+// loads a thread in flight.  The stores scatter as the staged kernel's would at that size.
+__global__ __launch_bounds__(kPart2Block) void k_part2f_direct(BuildParams P) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t cur[];  // per bucket of the digit
+  if (build_aborted(P)) return;
+  const uint32_t dpart = blockIdx.x;
+  const uint64_t lo = (uint64_t)dpart * P.p1_region;
+  const uint64_t hi = lo + min((uint64_t)P.p1_fill[dpart], P.p1_region);
+  const uint32_t nbins = P.bpp;
+  const uint32_t b0 = dpart * nbins;
+  const int tid = threadIdx.x;
+  for (uint32_t b = tid; b < nbins; b += kPart2Block) cur[b] = 0;
+  __syncthreads();
+  constexpr int kIn = 8;
+  bool ovf = false;
+  for (uint64_t i0 = lo; i0 < hi; i0 += (uint64_t)kPart2Block * kIn) {
+    Entry v[kIn];
+#pragma unroll
+    for (int k = 0; k < kIn; k++) {
+      const uint64_t i = i0 + (uint64_t)k * kPart2Block + tid;
+      if (i < hi) v[k] = P.ent3[i];
+    }
+#pragma unroll
+    for (int k = 0; k < kIn; k++) {
+      const uint64_t i = i0 + (uint64_t)k * kPart2Block + tid;
+      if (i >= hi) continue;
+      const uint32_t b = bucket_of(P, v[k].hash) - b0;
+      const uint32_t r = atomicAdd(&cur[b], 1u);
+      if (r < kPlaceLdsMax) P.ent2[((uint64_t)b0 + b - P.b_lo) * kPlaceLdsMax + r] = v[k];
+      else ovf = true;
+    }
+  }
+  if (ovf) atomicOr(&P.st->p2_overflow, 1u);
+  __syncthreads();
   for (uint32_t b = tid; b < nbins; b += kPart2Block) {
     const uint64_t bucket = (uint64_t)b0 + b;
     if (bucket < P.nbuckets) {
@@ -2178,7 +2225,10 @@ static size_t part2d_lds(uint32_t bpp) {
   return (size_t)((6 * bpp + 3) & ~3u) * 4 + (size_t)kPart2Block * kP2dPer * sizeof(Entry);
 }
 
-bool part2f_fits(uint32_t bpp) { return part2d_lds(bpp) <= 158 * 1024; }
+static size_t part2f_lds(uint32_t bpp, int per) {
+  return (size_t)((5 * bpp + 3) & ~3u) * 4 + (size_t)kPart2Block * per * sizeof(Entry);
+}
+bool part2f_fits(uint32_t bpp) { return bpp > kPart2Block * 3 ? bpp * 4 <= 158 * 1024 : part2f_lds(bpp, 2) <= 158 * 1024; }
 
 // k_part2st's dynamic LDS (the 8-bit counts, the bucket words, the stage of `per` entries a thread)
 static size_t part2st_lds(uint32_t bpp, int per) {
@@ -2200,8 +2250,14 @@ void launch_partition(const BuildParams& P, hipStream_t s, StageTimer* tm) {
     hipLaunchKernelGGL(k_part2st<4>, dim3(256), dim3(kPart2Block), part2st_lds(P.bpp, 4), s, P);
   else if (P.p2_sorted)
     hipLaunchKernelGGL(k_part2s, dim3(256), dim3(kPart2Block), (size_t)(514u * P.bpp) * sizeof(uint32_t), s, P);
-  else if (P.p2_fixed && P.p1_region && !P.p2_seg && part2d_lds(P.bpp) <= kLdsMax)
-    hipLaunchKernelGGL(k_part2f, dim3(256), dim3(kPart2Block), part2d_lds(P.bpp), s, P);
+  else if (P.p2_fixed && P.p1_region && !P.p2_seg && P.bpp > kPart2Block * 3)
+    hipLaunchKernelGGL(k_part2f_direct, dim3(256), dim3(kPart2Block), (size_t)P.bpp * sizeof(uint32_t), s, P);
+  else if (P.p2_fixed && P.p1_region && !P.p2_seg && part2f_lds(P.bpp, 6) <= kLdsMax)
+    hipLaunchKernelGGL(k_part2f<6>, dim3(256), dim3(kPart2Block), part2f_lds(P.bpp, 6), s, P);
+  else if (P.p2_fixed && P.p1_region && !P.p2_seg && part2f_lds(P.bpp, 4) <= kLdsMax)
+    hipLaunchKernelGGL(k_part2f<4>, dim3(256), dim3(kPart2Block), part2f_lds(P.bpp, 4), s, P);
+  else if (P.p2_fixed && P.p1_region && !P.p2_seg && part2f_lds(P.bpp, 2) <= kLdsMax)
+    hipLaunchKernelGGL(k_part2f<2>, dim3(256), dim3(kPart2Block), part2f_lds(P.bpp, 2), s, P);
   else if (!P.p2_seg && part2d_lds(P.bpp) <= kLdsMax)
     hipLaunchKernelGGL(k_part2d, dim3(256), dim3(kPart2Block), part2d_lds(P.bpp), s, P);
   else
