@@ -589,7 +589,9 @@ static bool want_frame3(BuildParams& P, const LogHdr& lh, int64_t entry, int64_t
   // a candidate window (maxRecLen bytes) holds about maxRecLen / mean true starts, all on one chain:
   // when that is well above one, the starts reached by others are marked so that only chain heads
   // walk on (SPARKEY_FRAME3_COVER=0/1 forces it)
-  Q.f3_cover = (double)Q.max_rec_len > 1.5 * mean ? 1 : 0;
+  // (also when a wave has more chunks than half the heads its lanes walk: windows that hold two true
+  // starts -- a log's shorter records -- would otherwise make two heads a chunk)
+  Q.f3_cover = (double)Q.max_rec_len > 1.5 * mean || 2 * Q.fr_w + 8 > 64 ? 1 : 0;
   if (knob_set(Knob::Frame3Cover)) Q.f3_cover = knob(Knob::Frame3Cover) ? 1 : 0;
   if (!frame3_fits(Q, mean, pk)) return false;
   // (C3's shape, pk 0.1: K = 3 measured 0.870 ms against K = 2's 0.903 per 10M records,
