@@ -1882,10 +1882,12 @@ constexpr int kPlaceRegPer = kPlaceLdsMax / kPlaceRegBlock;
 __device__ __forceinline__ void place_reg_bucket(const BuildParams& P, uint64_t bi, const Entry (&pre)[kPlaceRegPer]) {
   constexpr int NW = kPlaceRegBlock / 64;
   static_assert(kBucket == 4 * kPlaceRegBlock, "four wanted slots per thread in the scan");
-  __shared__ uint32_t cnt[kBucket / 2];          // 16-bit entry count per wanted slot
-  __shared__ uint32_t meta[kBucket];             // base[s] | (M[s] + 32768) << 16
-  __shared__ Entry buf[kPlaceLdsMax];            // each group's members together (any order inside)
-  __shared__ int16_t slot_of[2 * kBucket];       // slot x + t -> its entry's buf index, -1: empty
+  // (each array has one more element: the place of the lanes past the bucket's count, so that the
+  //  unrolled loops below run without a branch per entry -- the kernel is SALU-bound)
+  __shared__ uint32_t cnt[kBucket / 2 + 1];      // 16-bit entry count per wanted slot
+  __shared__ uint32_t meta[kBucket + 1];         // base[s] | (M[s] + 32768) << 16
+  __shared__ Entry buf[kPlaceLdsMax + 1];        // each group's members together (any order inside)
+  __shared__ int16_t slot_of[2 * kBucket + 2];   // slot x + t -> its entry's buf index, -1: empty
   __shared__ uint32_t wsum[NW];
   __shared__ int32_t wmax[NW];
   __shared__ uint64_t sh64[NW + 1];
@@ -1937,11 +1939,9 @@ __device__ __forceinline__ void place_reg_bucket(const BuildParams& P, uint64_t 
 #pragma unroll
   for (int k = 0; k < kPlaceRegPer; k++) {
     const uint32_t i = tid + k * kPlaceRegBlock;
-    if (i < n) {
-      want[k] = (uint32_t)(fast_mod(mine[k].hash, P.mod) - start);
-      const uint32_t sh = (want[k] & 1u) * 16u;
-      cur[k] = (atomicAdd(&cnt[want[k] >> 1], 1u << sh) >> sh) & 0xffffu;
-    }
+    want[k] = i < n ? (uint32_t)(fast_mod(mine[k].hash, P.mod) - start) : (uint32_t)kBucket;  // (kBucket: past n)
+    const uint32_t sh = (want[k] & 1u) * 16u;
+    cur[k] = (atomicAdd(&cnt[want[k] >> 1], 1u << sh) >> sh) & 0xffffu;
   }
   __syncthreads();
   // scan of slots 4 tid .. 4 tid + 3: base (exclusive count) and M (prefix max of s - base[s] over
@@ -1992,12 +1992,10 @@ __device__ __forceinline__ void place_reg_bucket(const BuildParams& P, uint64_t 
   uint32_t bw[kPlaceRegPer], g[kPlaceRegPer];
 #pragma unroll
   for (int k = 0; k < kPlaceRegPer; k++) {
-    const uint32_t i = tid + k * kPlaceRegBlock;
-    if (i < n) {
-      bw[k] = meta[want[k]] & 0xffffu;
-      g[k] = (cnt[want[k] >> 1] >> ((want[k] & 1u) * 16u)) & 0xffffu;
-      buf[bw[k] + cur[k]] = mine[k];
-    }
+    const bool valid = want[k] < (uint32_t)kBucket;
+    bw[k] = valid ? meta[want[k]] & 0xffffu : (uint32_t)kPlaceLdsMax;
+    g[k] = valid ? (cnt[want[k] >> 1] >> ((want[k] & 1u) * 16u)) & 0xffffu : 0u;
+    buf[bw[k] + (valid ? cur[k] : 0u)] = mine[k];
   }
   __syncthreads();
   // Equal wanted slots in address order: each member counts the members with smaller addresses.
@@ -2005,34 +2003,27 @@ __device__ __forceinline__ void place_reg_bucket(const BuildParams& P, uint64_t 
   const bool want_pairs = ndel == 0 && npairs0 <= P.pair_cap;
   uint32_t npair = 0;
   uint32_t rank[kPlaceRegPer];
-  bool same_prev[kPlaceRegPer];  // the member ranked just before this one has its hash
+  // One loop per wave over its lanes' largest group (a wave-uniform trip count), selects instead of
+  // branches: per-lane loops' exec-mask bookkeeping made this kernel SALU-bound
+  uint32_t gl = 0;
 #pragma unroll
   for (int k = 0; k < kPlaceRegPer; k++) {
-    const uint32_t i = tid + k * kPlaceRegBlock;
     rank[k] = 0;
-    same_prev[k] = false;
-    if (i >= n || g[k] < 2) continue;
-    const Entry* grp = buf + bw[k];
-    const uint64_t ai = mine[k].addr & ~kDelBit;
-    const bool cp = want_pairs && !(mine[k].addr & kDelBit) && g[k] <= kGroupMax;
+    gl = max(gl, g[k] >= 2 ? g[k] : 0u);
     if (g[k] > kGroupMax && cur[k] == 0) atomicOr(&P.st->dup_overflow, 1u);
-    uint32_t r = 0;
-    uint64_t best = 0;
-    bool have = false;
-    for (uint32_t u = 0; u < g[k]; u++) {
-      const Entry e = grp[u];
+  }
+  const uint32_t gw = (uint32_t)wave_max_i32((int32_t)gl);
+  for (uint32_t u = 0; u < gw; u++) {
+#pragma unroll
+    for (int k = 0; k < kPlaceRegPer; k++) {
+      const bool act = u < g[k] && g[k] >= 2;
+      const Entry e = buf[bw[k] + (act ? u : 0u)];
+      const uint64_t ai = mine[k].addr & ~kDelBit;
       const uint64_t aj = e.addr & ~kDelBit;
-      if (aj < ai) {
-        r++;
-        if (!have || aj > best) {
-          best = aj;
-          have = true;
-          same_prev[k] = e.hash == mine[k].hash;
-        }
-      }
-      npair += cp && aj > ai && e.hash == mine[k].hash && !(e.addr & kDelBit);
+      rank[k] += act && aj < ai ? 1u : 0u;
+      const bool cp = want_pairs && !(mine[k].addr & kDelBit) && g[k] <= kGroupMax;
+      npair += (act && cp && aj > ai && e.hash == mine[k].hash && !(e.addr & kDelBit)) ? 1u : 0u;
     }
-    rank[k] = r;
   }
   const bool any_pair = __syncthreads_or(npair != 0);
   if (any_pair) {  // (block-uniform)
@@ -2068,23 +2059,29 @@ __device__ __forceinline__ void place_reg_bucket(const BuildParams& P, uint64_t 
   int64_t pos[kPlaceRegPer];
 #pragma unroll
   for (int k = 0; k < kPlaceRegPer; k++) {
-    const uint32_t i = tid + k * kPlaceRegBlock;
-    pos[k] = -1;
-    if (i >= n) continue;
+    const bool valid = want[k] < (uint32_t)kBucket;
     const int32_t M = (int32_t)(meta[want[k]] >> 16) - 32768;
     const int64_t p = (int64_t)(bw[k] + rank[k]) + max(x, (int64_t)M);
-    pos[k] = p;
-    slot_of[p - x] = (int16_t)(bw[k] + cur[k]);  // (where the entry sits in buf)
-    sum_d += (unsigned long long)(p - want[k]);  // getDisplacement (IndexHash.java:671-678)
-    max_d = max(max_d, (long long)(p - want[k]));
-    pend = max(pend, (int32_t)(p + 1));
-    // the pair (slot - 1, slot) inside the block's range: equal hashes lie in one group, ranked
-    // next to each other (calculateMaxDisplacement, IndexHash.java:195-245)
-    if (same_prev[k] && wrap_slot(start + (uint64_t)p, P.cap) != 0 && start + (uint64_t)p < lim) col++;
+    pos[k] = valid ? p : -1;
+    slot_of[valid ? p - x : (int64_t)(2 * kBucket + 1)] = (int16_t)(bw[k] + cur[k]);  // (where the entry sits in buf)
+    const int64_t d = valid ? p - (int64_t)want[k] : 0;
+    sum_d += (unsigned long long)d;  // getDisplacement (IndexHash.java:671-678)
+    max_d = max(max_d, (long long)d);
+    pend = max(pend, valid ? (int32_t)(p + 1) : 0);
   }
   pend = wave_max_i32(pend);
   if (lane == 0 && pend > 0) atomicMax(&s_pend, pend);
   __syncthreads();
+  // the pair (slot - 1, slot) inside the block's range: equal hashes share a wanted slot, so they are
+  // members of one group ranked next to each other -- the member in slot p - 1 of a member ranked
+  // after another (calculateMaxDisplacement, IndexHash.java:195-245)
+#pragma unroll
+  for (int k = 0; k < kPlaceRegPer; k++) {
+    const int64_t p = pos[k];
+    const bool act = p >= 0 && rank[k] > 0;
+    const Entry e = buf[act ? slot_of[p - 1 - x] : 0];
+    col += act && e.hash == mine[k].hash && wrap_slot(start + (uint64_t)p, P.cap) != 0 && start + (uint64_t)p < lim;
+  }
   const int64_t hi = max(bsize, (int64_t)s_pend);
   // the block's slots [x, hi) in order, consecutive lanes on consecutive slots: its entries out of
   // buf, zeros where none landed (the run spilled past the bucket has no gap)

@@ -28,7 +28,7 @@ enum class Knob : int {
   FrameDebug,       // k_frame / k_frame3 per-wave phase counters to stderr
   Part2Debug,       // k_part2s phase counters to stderr
   NoRegions,        // partition pass 1 into digit regions off (two-pass histogram partition)
-  NoBuckets,        // uniform framing into the bucket regions off (partition pass 1 into digit regions)
+  NoBuckets,        // k_frame3 into the bucket regions off (digit regions and the two-pass partition)
   RegionCap,        // digit region capacity (entries; tests force overflows)
   ExactSerial,      // the exact path on one lane over the whole table
   ExactDebug,       // exact path phase counters (2: synchronise each class)
