@@ -54,7 +54,7 @@ struct LdsKey {  // key in an 8-byte aligned LDS window
   int base;
   __device__ __forceinline__ uint64_t u64(int o) const { return lds_u64_at(win, base + o); }
 };
-struct GlobalKey {  // key in global memory with at least 16 readable bytes past its end
+struct GlobalKey {  // key in global memory with at least 32 readable bytes past its end
   const uint8_t* p;
   __device__ __forceinline__ uint64_t u64(int o) const {
     const uintptr_t a = reinterpret_cast<uintptr_t>(p + o);
@@ -82,11 +82,11 @@ __device__ inline uint32_t murmur32_ld(const Ld& ld, int32_t len, uint32_t seed)
     block((uint32_t)(x >> 32));
   }
   if (i < nblocks) block((uint32_t)ld.u64(4 * i));
+  // the tail without a branch: a zero tail mixes to zero, and h1 ^= 0 leaves it (the loaders read past
+  // the key's end by contract)
   const int32_t rem = len & 3;
-  if (rem) {
-    uint32_t k1 = (uint32_t)ld.u64(4 * nblocks) & ((1u << (8 * rem)) - 1u);
-    k1 *= c1; k1 = rotl32(k1, 15); k1 *= c2; h1 ^= k1;
-  }
+  uint32_t k1 = (uint32_t)ld.u64(4 * nblocks) & ((1u << (8 * rem)) - 1u);
+  k1 *= c1; k1 = rotl32(k1, 15); k1 *= c2; h1 ^= k1;
   h1 ^= (uint32_t)len;
   h1 ^= h1 >> 16; h1 *= 0x85ebca6bu; h1 ^= h1 >> 13; h1 *= 0xc2b2ae35u; h1 ^= h1 >> 16;
   return h1;
@@ -106,15 +106,14 @@ __device__ inline uint64_t murmur64_ld(const Ld& ld, int32_t len, uint32_t seed)
     k2 *= c2; k2 = rotl64(k2, 33); k2 *= c1; h2 ^= k2;
     h2 = rotl64(h2, 31); h2 += h1; h2 = h2 * 5 + 0x38495ab5ull;
   }
+  // the tail without branches: a zero half mixes to zero, and h ^= 0 leaves it (the loaders read
+  // past the key's end by contract)
   const int32_t rem = len & 15;
   const int t = 16 * nblocks;
-  if (rem > 8) {
-    uint64_t k2 = ld.u64(t + 8) & ((1ull << (8 * (rem - 8))) - 1ull);
+  {
+    uint64_t k2 = ld.u64(t + 8) & (rem > 8 ? (1ull << (8 * (rem - 8))) - 1ull : 0ull);
     k2 *= c2; k2 = rotl64(k2, 33); k2 *= c1; h2 ^= k2;
-  }
-  if (rem > 0) {
-    uint64_t k1 = ld.u64(t);
-    if (rem < 8) k1 &= (1ull << (8 * rem)) - 1ull;
+    uint64_t k1 = ld.u64(t) & (rem >= 8 ? ~0ull : (1ull << (8 * rem)) - 1ull);
     k1 *= c1; k1 = rotl64(k1, 31); k1 *= c2; h1 ^= k1;
   }
   h1 ^= (uint64_t)(int64_t)len;

@@ -552,7 +552,7 @@ __device__ __forceinline__ void frame_region(const BuildParams& P, const uint64_
         const RgnKey ld{rgn, (uint32_t)(kp - R0)};
         hash = P.hash_size == 8 ? murmur64_ld(ld, h.klen, (uint32_t)P.seed)
                                 : (uint64_t)murmur32_ld(ld, h.klen, (uint32_t)P.seed);
-      } else if (kp + h.klen + 16 <= log_len) {  // key runs past the region: unaligned global reads
+      } else if (kp + h.klen + 32 <= log_len) {  // key runs past the region: unaligned global reads
         const GlobalKey ld{P.log + kp};
         hash = P.hash_size == 8 ? murmur64_ld(ld, h.klen, (uint32_t)P.seed)
                                 : (uint64_t)murmur32_ld(ld, h.klen, (uint32_t)P.seed);

@@ -12,4 +12,6 @@ timeout -k 10 700 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_la
 timeout -k 10 300 python -u bench.py --steps 20 --warmup 3 > $O/c2.jsonl 2> $O/c2.err &&
 timeout -k 10 400 python -u bench.py --workload c3 --entries 100000000 --steps 5 --warmup 1 --no-parity > $O/c3_100m.jsonl 2> $O/c3_100m.err &&
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace_c2 -o run -- \
-  python3 bench.py --steps 20 --warmup 3 --no-parity --no-cpu-baseline > $O/trace_c2.log 2>&1
+  python3 bench.py --steps 20 --warmup 3 --no-parity --no-cpu-baseline > $O/trace_c2.log 2>&1 &&
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace_c3 -o run -- \
+  python3 bench.py --workload c3 --entries 100000000 --steps 5 --warmup 1 --no-parity --no-cpu-baseline > $O/trace_c3.log 2>&1
