@@ -297,6 +297,8 @@ void launch_partition(const BuildParams& P, hipStream_t s, StageTimer* tm);
 bool part2f_fits(uint32_t bpp);  // k_part2f's LDS for this many buckets a digit
 void launch_partition1(const BuildParams& P, hipStream_t s);
 void launch_partition2(const BuildParams& P, hipStream_t s, StageTimer* tm);
+void launch_part2_recv(const BuildParams& P, hipStream_t s, StageTimer* tm);  // sharded receive, fixed regions
+bool part2_recv_fits(uint32_t bpp);
 void launch_dense_slabs(const BuildParams& P, hipStream_t s);
 void launch_frame_uniform(const BuildParams& P, hipStream_t s, StageTimer* tm);
 void launch_frame3(const BuildParams& P, hipStream_t s, StageTimer* tm);  // frame3_kernels.hip

@@ -331,32 +331,31 @@ __device__ __forceinline__ void frame3_region(const BuildParams& P, const uint64
 
   // ---- 3 long walk: head `lane` to its chunk end + LOOK, listing its starts in the chunk ----
   bool lovf = false;
-  {
-    // (one wave-uniform loop while any head walks, selects inside: no per-lane break bookkeeping)
-    const bool head = lane < S;
-    int32_t p = head ? s_start[lane] : 0;
+  if (lane < S) {
+    // (a per-lane loop: the wave-uniform form with selects measured slower here, 6.9K against 5.6K
+    //  cycles a wave on C3 -- the heads are few and their walks short)
+    int32_t p = s_start[lane];
     const int32_t e = chunk_end(p >> cs);
     const int32_t stop = min(min(e + look, de), ruse);
     uint16_t* my = lists + lane * kF3Lcap;
     int32_t cnt = 0, ex = -1;
-    bool alive = true, act = head;
-    while (__any(act)) {
-      ex = act && p >= e && ex < 0 ? p : ex;
-      act = act && p < stop;
-      const bool in = act && p < e;
-      if (in && cnt < kF3Lcap) my[cnt] = (uint16_t)p;
-      cnt += in ? 1 : 0;
-      const int32_t q = f3_step(rgn, act ? p : 0, lim, mk, mv, nodel);
-      const bool dead = act && q < 0;
-      alive = alive && !dead;
-      act = act && !dead;
-      p = act ? q : p;
+    bool alive = true;
+    for (;;) {
+      if (p >= e && ex < 0) ex = p;
+      if (p >= stop) break;
+      if (p < e) {
+        if (cnt < kF3Lcap) my[cnt] = (uint16_t)p;
+        cnt++;
+      }
+      p = f3_step(rgn, p, lim, mk, mv, nodel);
+      if (p < 0) {
+        alive = false;
+        break;
+      }
     }
-    if (head) {
-      if (cnt > kF3Lcap) lovf = true;
-      s_exit[lane] = alive && ex >= 0 ? (uint16_t)ex : (uint16_t)0xffff;
-      s_cnt[lane] = (uint8_t)min(cnt, 255);
-    }
+    if (cnt > kF3Lcap) lovf = true;
+    s_exit[lane] = alive && ex >= 0 ? (uint16_t)ex : (uint16_t)0xffff;
+    s_cnt[lane] = (uint8_t)min(cnt, 255);
   }
   if (__any(lovf)) {
     fail(kF3Caps);

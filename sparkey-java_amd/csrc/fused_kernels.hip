@@ -1518,6 +1518,82 @@ __global__ __launch_bounds__(kPart2Block) void k_part2f_direct(BuildParams P) {
   }
 }
 
+// Sharded receive into fixed bucket regions, for tables of more than kP2SortedMaxBpp buckets a digit.
+// Workgroup (x, k) takes slice x of coarse digit k's entries (its runs from every source rank,
+// seg: nsrc (begin, end) runs of ent3, read back to back): it counts the slice per bucket in LDS,
+// reserves each bucket's share of the bucket's fixed region with one returning global atomic on the
+// bucket's count (zeroed by the host), and reads the slice again to store each entry at its place.
+// The entries land in any order -- k_place_reg orders a bucket by (wanted slot, address) itself.
+// Every CU is busy whatever the rank's share of the digits (k_part2 gives a digit one workgroup: 32
+// workgroups a rank at N = 8); one atomic per entry instead of per (slice, bucket) measured 4.2 ms
+// against k_part2's 1.9 at 125M entries.  A bucket past kPlaceLdsMax entries flags p2_overflow (the
+// host redoes the step with dense runs).
+__global__ __launch_bounds__(kPart2Block) void k_part2_recv(BuildParams P) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t cnt[];  // per bucket of the digit
+  if (build_aborted(P)) return;
+  constexpr int kIn = kPart2Items;
+  const int tid = threadIdx.x;
+  const uint32_t k = blockIdx.y, X = gridDim.x, x = blockIdx.x;
+  const uint32_t nbins = P.bpp;
+  const uint64_t b0 = (uint64_t)(P.p2_d0 + k) * nbins;
+  const uint64_t* seg = P.p2_seg + 2ull * k * P.p2_nsrc;
+  uint64_t tot = 0;
+  for (uint32_t q = 0; q < P.p2_nsrc; q++) tot += seg[2 * q + 1] - seg[2 * q];
+  const uint64_t vlo = tot * x / X, vhi = tot * (x + 1) / X;  // the slice, in the runs' concatenation
+  for (uint32_t b = tid; b < nbins; b += kPart2Block) cnt[b] = 0;
+  __syncthreads();
+  // f(i, e) over the slice's entries, kIn loads a thread in flight
+  auto each = [&](auto&& f) {
+    uint64_t v0 = 0;
+    for (uint32_t q = 0; q < P.p2_nsrc; q++) {
+      const uint64_t a = seg[2 * q], n = seg[2 * q + 1] - a;
+      const uint64_t lo = max(vlo, v0), hi = min(vhi, v0 + n);
+      v0 += n;
+      if (lo >= hi) continue;
+      const uint64_t pa = a + (lo - (v0 - n)), pz = pa + (hi - lo);
+      for (uint64_t i0 = pa; i0 < pz; i0 += (uint64_t)kPart2Block * kIn) {
+        Entry v[kIn];
+#pragma unroll
+        for (int u = 0; u < kIn; u++) {
+          const uint64_t i = i0 + (uint64_t)u * kPart2Block + tid;
+          if (i < pz) v[u] = P.ent3[i];
+        }
+#pragma unroll
+        for (int u = 0; u < kIn; u++)
+          if (i0 + (uint64_t)u * kPart2Block + tid < pz) f(v[u]);
+      }
+    }
+  };
+  each([&](const Entry& e) { atomicAdd(&cnt[bucket_of(P, e.hash) - b0], 1u); });
+  __syncthreads();
+  for (uint32_t b = tid; b < nbins; b += kPart2Block) {
+    const uint32_t c = cnt[b];
+    cnt[b] = c ? atomicAdd(&P.bcount[b0 + b], c) : 0u;
+  }
+  __syncthreads();
+  bool ovf = false;
+  each([&](const Entry& e) {
+    const uint32_t b = bucket_of(P, e.hash);
+    const uint32_t r = atomicAdd(&cnt[b - b0], 1u);
+    if (r < kPlaceLdsMax) P.ent2[(uint64_t)(b - P.b_lo) * kPlaceLdsMax + r] = e;
+    else ovf = true;
+  });
+  if (ovf) atomicOr(&P.st->p2_overflow, 1u);
+  const uint64_t nblk = (uint64_t)gridDim.x * gridDim.y;
+  for (uint64_t b = P.b_lo + ((uint64_t)k * gridDim.x + x) * kPart2Block + tid; b < P.b_hi; b += nblk * kPart2Block)
+    P.boff[b] = (b - P.b_lo) * (uint64_t)kPlaceLdsMax;
+}
+
+bool part2_recv_fits(uint32_t bpp) { return (size_t)bpp * sizeof(uint32_t) <= 64 * 1024; }
+
+void launch_part2_recv(const BuildParams& P, hipStream_t s, StageTimer* tm) {
+  if (P.p2_nd == 0) return;
+  // about two workgroups a CU over the rank's digits
+  const unsigned x = (unsigned)std::max<uint32_t>(1u, (512u + P.p2_nd - 1) / P.p2_nd);
+  hipLaunchKernelGGL(k_part2_recv, dim3(x, P.p2_nd), dim3(kPart2Block), (size_t)P.bpp * sizeof(uint32_t), s, P);
+  tm->mark("partition", s);
+}
+
 // Pass 2 for a table of up to kP2SortedMaxBpp buckets per digit (single GPU): the digit's entries
 // are also counted per (bucket, wanted slot) in LDS (16-bit counts), so that the same pass leaves
 // each bucket's max-plus carry function -- k_summary's output: F(x) = max(x + n - bsize,
@@ -1878,7 +1954,8 @@ __device__ __forceinline__ bool is_put_pair(const Entry& x, const Entry& y) {  /
 constexpr int kPlaceRegBlock = 256;
 constexpr int kPlaceRegPer = kPlaceLdsMax / kPlaceRegBlock;
 
-// One bucket of k_place_reg: bucket b_lo + bi; pre[] holds its fixed-region entries when `fixed`.
+// One bucket of k_place_reg: bucket b_lo + bi; pre[] holds its fixed-region entries when kFixed.
+template <bool kFixed>
 __device__ __forceinline__ void place_reg_bucket(const BuildParams& P, uint64_t bi, const Entry (&pre)[kPlaceRegPer]) {
   constexpr int NW = kPlaceRegBlock / 64;
   static_assert(kBucket == 4 * kPlaceRegBlock, "four wanted slots per thread in the scan");
@@ -1897,7 +1974,7 @@ __device__ __forceinline__ void place_reg_bucket(const BuildParams& P, uint64_t 
   __shared__ int32_t s_pend;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   Entry mine[kPlaceRegPer];
-  const bool fixed = P.p2_fixed != 0;
+  constexpr bool fixed = kFixed;
   if (fixed) {
 #pragma unroll
     for (int k = 0; k < kPlaceRegPer; k++) mine[k] = pre[k];
@@ -1999,7 +2076,6 @@ __device__ __forceinline__ void place_reg_bucket(const BuildParams& P, uint64_t 
   }
   __syncthreads();
   // Equal wanted slots in address order: each member counts the members with smaller addresses.
-  // Equal-hash PUT pairs are duplicate-key candidates for the pair list (as k_place_reg).
   const bool want_pairs = ndel == 0 && npairs0 <= P.pair_cap;
   uint32_t npair = 0;
   uint32_t rank[kPlaceRegPer];
@@ -2013,20 +2089,30 @@ __device__ __forceinline__ void place_reg_bucket(const BuildParams& P, uint64_t 
     if (g[k] > kGroupMax && cur[k] == 0) atomicOr(&P.st->dup_overflow, 1u);
   }
   const uint32_t gw = (uint32_t)wave_max_i32((int32_t)gl);
+  uint32_t eqh = 0;  // another member with this entry's hash (duplicate keys: rare)
   for (uint32_t u = 0; u < gw; u++) {
 #pragma unroll
     for (int k = 0; k < kPlaceRegPer; k++) {
-      const bool act = u < g[k] && g[k] >= 2;
+      const bool act = u < g[k];  // (a lone entry meets only itself)
       const Entry e = buf[bw[k] + (act ? u : 0u)];
       const uint64_t ai = mine[k].addr & ~kDelBit;
       const uint64_t aj = e.addr & ~kDelBit;
       rank[k] += act && aj < ai ? 1u : 0u;
-      const bool cp = want_pairs && !(mine[k].addr & kDelBit) && g[k] <= kGroupMax;
-      npair += (act && cp && aj > ai && e.hash == mine[k].hash && !(e.addr & kDelBit)) ? 1u : 0u;
+      eqh |= (uint32_t)act & (uint32_t)(aj != ai) & (uint32_t)(e.hash == mine[k].hash);  // (no branches)
     }
   }
-  const bool any_pair = __syncthreads_or(npair != 0);
-  if (any_pair) {  // (block-uniform)
+  // Equal-hash PUT pairs (duplicate-key candidates, for the pair list): counted and written only by
+  // blocks that met an equal hash at all
+  if (__syncthreads_or(eqh != 0 && want_pairs)) {  // (block-uniform)
+#pragma unroll
+    for (int k = 0; k < kPlaceRegPer; k++) {
+      if (g[k] < 2 || g[k] > kGroupMax || (mine[k].addr & kDelBit)) continue;
+      const uint64_t ai = mine[k].addr & ~kDelBit;
+      for (uint32_t u = 0; u < g[k]; u++) {
+        const Entry e = buf[bw[k] + u];
+        npair += (e.addr & ~kDelBit) > ai && is_put_pair(mine[k], e) ? 1u : 0u;
+      }
+    }
     uint64_t pair_total = 0;
     const uint64_t pair_off = block_excl_sum<kPlaceRegBlock>(npair, sh64, &pair_total);
     if (tid == 0) pair_base = atomicAdd(&P.st->n_pairs, (unsigned long long)pair_total);
@@ -2034,8 +2120,7 @@ __device__ __forceinline__ void place_reg_bucket(const BuildParams& P, uint64_t 
     unsigned long long slotn = pair_base + pair_off;
 #pragma unroll
     for (int k = 0; k < kPlaceRegPer; k++) {
-      const uint32_t i = tid + k * kPlaceRegBlock;
-      if (i >= n || !npair || g[k] < 2 || g[k] > kGroupMax || (mine[k].addr & kDelBit)) continue;
+      if (!npair || g[k] < 2 || g[k] > kGroupMax || (mine[k].addr & kDelBit)) continue;
       const Entry* grp = buf + bw[k];
       const uint64_t ai = mine[k].addr & ~kDelBit;
       for (uint32_t u = 0; u < g[k]; u++) {
@@ -2085,27 +2170,44 @@ __device__ __forceinline__ void place_reg_bucket(const BuildParams& P, uint64_t 
   const int64_t hi = max(bsize, (int64_t)s_pend);
   // the block's slots [x, hi) in order, consecutive lanes on consecutive slots: its entries out of
   // buf, zeros where none landed (the run spilled past the bucket has no gap)
-  for (int64_t t = x + tid; t < hi; t += kPlaceRegBlock) {
-    const int32_t v = slot_of[t - x];
-    const uint64_t slot = t < bsize ? start + (uint64_t)t : wrap_slot(start + (uint64_t)t, P.cap);
-    uint64_t hh = 0, aa = 0;
-    if (v >= 0) {
-      const Entry en = buf[v];
-      hh = en.hash;
-      aa = en.addr & ~kDelBit;
-    }
-    if (nt16) {  // the table is written once: non-temporal stores
-      typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  if (nt16 && hi <= bsize) {  // (block-uniform, the usual case: no run spilled past the bucket) no
+    // wrap, no per-slot branches: 32-bit offsets, selects, one non-temporal 16-byte store a slot
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    u32x4* dst = reinterpret_cast<u32x4*>(P.out + kIndexHeaderSize + start * 16ull);
+    for (int32_t t = (int32_t)x + tid; t < (int32_t)hi; t += kPlaceRegBlock) {
+      const int32_t v = slot_of[t - (int32_t)x];
+      const Entry en = buf[v >= 0 ? v : 0];
+      const uint64_t hh = v >= 0 ? en.hash : 0ull, aa = v >= 0 ? en.addr & ~kDelBit : 0ull;
       u32x4 w;
       w.x = (uint32_t)hh;
       w.y = (uint32_t)(hh >> 32);
       w.z = (uint32_t)aa;
       w.w = (uint32_t)(aa >> 32);
-      __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(P.out + kIndexHeaderSize + slot * 16ull));
-    } else if (v >= 0) {
-      put_slot(P, slot, hh, aa);
-    } else {
-      write_slot(P, slot, 0, 0);
+      __builtin_nontemporal_store(w, dst + t);
+    }
+  } else {
+    for (int64_t t = x + tid; t < hi; t += kPlaceRegBlock) {
+      const int32_t v = slot_of[t - x];
+      const uint64_t slot = t < bsize ? start + (uint64_t)t : wrap_slot(start + (uint64_t)t, P.cap);
+      uint64_t hh = 0, aa = 0;
+      if (v >= 0) {
+        const Entry en = buf[v];
+        hh = en.hash;
+        aa = en.addr & ~kDelBit;
+      }
+      if (nt16) {  // the table is written once: non-temporal stores
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+        u32x4 w;
+        w.x = (uint32_t)hh;
+        w.y = (uint32_t)(hh >> 32);
+        w.z = (uint32_t)aa;
+        w.w = (uint32_t)(aa >> 32);
+        __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(P.out + kIndexHeaderSize + slot * 16ull));
+      } else if (v >= 0) {
+        put_slot(P, slot, hh, aa);
+      } else {
+        write_slot(P, slot, 0, 0);
+      }
     }
   }
   if (!P.fold_stats) return;
@@ -2145,16 +2247,23 @@ __device__ __forceinline__ void place_reg_bucket(const BuildParams& P, uint64_t 
 }
 
 
-// k_place_reg: one block per bucket; the fixed regions' entry loads go out before the head's scalar
-// loads (slots past the count are never used), in one round trip.
+// k_place_reg: one block per bucket.  With fixed regions (kFixed: a template parameter, so that no
+// branch joins the loads and the wave runs on to the head's scalar loads with them in flight) the first
+// three quarters of the region are loaded with the bucket's count (a bucket at load 0.77 holds about
+// 790 entries), the last quarter only up to the count (it read 23% more bytes than the entries).
+template <bool kFixed>
 __global__ __launch_bounds__(kPlaceRegBlock) void k_place_reg(BuildParams P) {
   Entry pre[kPlaceRegPer];
-  if (P.p2_fixed) {
+  if (kFixed) {
     const uint64_t e0 = (uint64_t)blockIdx.x * kPlaceLdsMax;
+    const uint32_t n = P.bcount[P.b_lo + blockIdx.x];
 #pragma unroll
-    for (int k = 0; k < kPlaceRegPer; k++) pre[k] = P.ent2[e0 + threadIdx.x + k * kPlaceRegBlock];
+    for (int k = 0; k < kPlaceRegPer - 1; k++) pre[k] = P.ent2[e0 + threadIdx.x + k * kPlaceRegBlock];
+    constexpr uint32_t kLast = (kPlaceRegPer - 1) * kPlaceRegBlock;
+    // (no branch: lanes past the count reload their first entry's line, which the cache holds)
+    pre[kPlaceRegPer - 1] = P.ent2[e0 + threadIdx.x + (threadIdx.x + kLast < n ? kLast : 0u)];
   }
-  place_reg_bucket(P, blockIdx.x, pre);
+  place_reg_bucket<kFixed>(P, blockIdx.x, pre);
 }
 
 // ================================================================================================
@@ -2264,7 +2373,8 @@ void launch_partition(const BuildParams& P, hipStream_t s, StageTimer* tm) {
 
 void launch_place_buckets(const BuildParams& P, hipStream_t s) {
   if (P.b_hi > P.b_lo)
-    hipLaunchKernelGGL(k_place_reg, dim3((unsigned)(P.b_hi - P.b_lo)), dim3(kPlaceRegBlock), 0, s, P);
+    hipLaunchKernelGGL(P.p2_fixed ? k_place_reg<true> : k_place_reg<false>, dim3((unsigned)(P.b_hi - P.b_lo)),
+                       dim3(kPlaceRegBlock), 0, s, P);
   // buckets above kPlaceLdsMax entries (normally none; never with fixed bucket regions, whose
   // overflow redoes the build with dense runs)
   if (!P.p2_fixed) launch_place_global(P, s, 0, 1);

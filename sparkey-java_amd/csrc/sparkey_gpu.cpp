@@ -2298,14 +2298,23 @@ int sparkey_shard_summarize_dev(sparkey_plan* pl, const uint8_t* d_recv, uint64_
     // regions of the rank's range, the carry functions from the same pass.  A bucket that outgrows its
     // region sets p2_overflow: every later kernel skips, the flags row says "aborted", and the host
     // redoes the step with fixed_regions = 0 (dense runs)
+    // Larger tables over N > 1 ranks: k_part2_recv, several workgroups a digit, into the fixed regions
+    // (k_part2 has one workgroup per digit: 256 / N of them a rank, 32 CUs busy at N = 8).  One rank
+    // keeps k_part2 (125M entries: 1.89 ms against k_part2_recv's 2.41, profiles/r04/shard/).
     P.p2_sorted = P.bpp <= kP2SortedMaxBpp ? 1 : 0;
-    P.p2_fixed = P.p2_sorted && fixed_regions ? 1 : 0;
+    const bool recv = !P.p2_sorted && sh.world > 1 && part2_recv_fits(P.bpp);
+    P.p2_fixed = fixed_regions && (P.p2_sorted || recv) ? 1 : 0;
     if (P.p2_fixed) {
       HIP_TRY(grow(&pl->ent2, pl->c_ent2, std::max<uint64_t>(n_recv, (P.b_hi - P.b_lo) * (uint64_t)kPlaceLdsMax)));
       P.ent2 = pl->ent2;
       P.max_records = pl->c_ent2;
     }
-    launch_partition2(P, s, &pl->timer);
+    if (P.p2_fixed && !P.p2_sorted) {
+      if (P.b_hi > P.b_lo) HIP_TRY(hipMemsetAsync(P.bcount + P.b_lo, 0, (P.b_hi - P.b_lo) * sizeof(uint32_t), s));
+      launch_part2_recv(P, s, &pl->timer);
+    } else {
+      launch_partition2(P, s, &pl->timer);
+    }
     P.ent3 = pl->ent3;  // the later steps' scratch (k_place sorts oversized buckets there)
     P.p2_seg = nullptr;
     P.p2_out = nullptr;

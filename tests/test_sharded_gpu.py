@@ -39,6 +39,16 @@ def test_sharded_gpu_c2_shape(native, world):
     assert metas[0]["path"] == "sharded"
 
 
+@pytest.mark.parametrize("world", [1, 2, 4])
+def test_sharded_gpu_wide_table(native, world):
+    """More than 64 buckets a coarse digit (sparsity 80: about 19.5K buckets for 250K records): the
+    received entries go straight into the fixed bucket regions (k_part2_recv), as at C4's sizes."""
+    from sparkey import synth
+    log = synth.fixed_log(250000, 16, 100, seed=9).tobytes()
+    metas = check(native, log, world, seed=0x51D3, sparsity=80.0)
+    assert metas[0]["path"] == "sharded"
+
+
 @pytest.mark.parametrize("seed", [1, 2, 3])
 def test_sharded_gpu_random_keys(native, seed):
     log = make_log(random_puts(8000, seed=seed, kmin=0, kmax=130, vmax=500))

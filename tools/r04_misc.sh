@@ -10,4 +10,5 @@ O=gpurun_out/$T
 mkdir -p $O
 gcc -O2 -pthread tools/io_probe.c -o /tmp/io_probe && timeout -k 10 300 /tmp/io_probe /tmp > $O/io_probe.txt 2>&1 &&
 export MASTER_ADDR=127.0.0.1 MASTER_PORT=29561 RANK=0 WORLD_SIZE=1 LOCAL_RANK=0 &&
-SQ= bash tools/r04_pmc.sh $T/pmc "sharded_rank_125000000:--sharded --entries 125000000 --no-check"
+SQ= bash tools/r04_pmc.sh $T/pmc "sharded_rank_125000000:--sharded --entries 125000000 --no-check" &&
+SQ=1 bash tools/r04_pmc.sh $T/pmc_c2 "c2:"
