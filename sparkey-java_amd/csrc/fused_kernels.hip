@@ -2170,20 +2170,37 @@ __device__ __forceinline__ void place_reg_bucket(const BuildParams& P, uint64_t 
   const int64_t hi = max(bsize, (int64_t)s_pend);
   // the block's slots [x, hi) in order, consecutive lanes on consecutive slots: its entries out of
   // buf, zeros where none landed (the run spilled past the bucket has no gap)
-  if (nt16 && hi <= bsize) {  // (block-uniform, the usual case: no run spilled past the bucket) no
-    // wrap, no per-slot branches: 32-bit offsets, selects, one non-temporal 16-byte store a slot
+  if (hi <= bsize) {  // (block-uniform, the usual case: no run spilled past the bucket, so every slot
+    // is in a sharded rank's range too) no wrap, no per-slot branches: 32-bit offsets, selects,
+    // non-temporal stores of the slot's words (16-, 12- and 8-byte slots: write_slot's layouts)
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-    u32x4* dst = reinterpret_cast<u32x4*>(P.out + kIndexHeaderSize + start * 16ull);
+    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+    const uint32_t ss = P.slot_size;
+    const bool h8 = P.hash_size == 8;
+    uint8_t* dst = P.out + kIndexHeaderSize + start * (uint64_t)ss;
     for (int32_t t = (int32_t)x + tid; t < (int32_t)hi; t += kPlaceRegBlock) {
       const int32_t v = slot_of[t - (int32_t)x];
       const Entry en = buf[v >= 0 ? v : 0];
       const uint64_t hh = v >= 0 ? en.hash : 0ull, aa = v >= 0 ? en.addr & ~kDelBit : 0ull;
-      u32x4 w;
-      w.x = (uint32_t)hh;
-      w.y = (uint32_t)(hh >> 32);
-      w.z = (uint32_t)aa;
-      w.w = (uint32_t)(aa >> 32);
-      __builtin_nontemporal_store(w, dst + t);
+      uint8_t* q = dst + (uint32_t)t * ss;
+      if (ss == 16) {
+        u32x4 w;
+        w.x = (uint32_t)hh;
+        w.y = (uint32_t)(hh >> 32);
+        w.z = (uint32_t)aa;
+        w.w = (uint32_t)(aa >> 32);
+        __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(q));
+      } else if (ss == 8) {
+        u32x2 w;
+        w.x = (uint32_t)hh;
+        w.y = (uint32_t)aa;
+        __builtin_nontemporal_store(w, reinterpret_cast<u32x2*>(q));
+      } else {  // 12: 8 + 4 or 4 + 8 (4-byte aligned: three dword stores)
+        uint32_t* d = reinterpret_cast<uint32_t*>(q);
+        __builtin_nontemporal_store((uint32_t)hh, d);
+        __builtin_nontemporal_store(h8 ? (uint32_t)(hh >> 32) : (uint32_t)aa, d + 1);
+        __builtin_nontemporal_store(h8 ? (uint32_t)aa : (uint32_t)(aa >> 32), d + 2);
+      }
     }
   } else {
     for (int64_t t = x + tid; t < hi; t += kPlaceRegBlock) {
