@@ -515,6 +515,21 @@ __global__ __launch_bounds__(256) void k_build_init(uint8_t* out, BuildInit h, S
   for (uint32_t i = t; i < n; i += 256) fill[i] = 0;
 }
 
+// The status block into the caller's pinned, device-mapped host copy: one small launch queued behind
+// the build (a runtime device-to-host copy costs a blit launch with about 6 us of setup before it).
+__global__ __launch_bounds__(64) void k_status_out(const Status* st, Status* host) {
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(st);
+  uint32_t* dst = reinterpret_cast<uint32_t*>(host);
+  static_assert(sizeof(Status) % sizeof(uint32_t) == 0, "whole words");
+  constexpr int kWords = (int)(sizeof(Status) / sizeof(uint32_t));
+  for (int i = threadIdx.x; i < kWords; i += 64) dst[i] = __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __threadfence_system();
+}
+
+void launch_status_out(const Status* st, Status* host, hipStream_t s) {
+  hipLaunchKernelGGL(k_status_out, dim3(1), dim3(64), 0, s, st, host);
+}
+
 void launch_build_init(uint8_t* out, const uint8_t* hdr, Status* st, uint32_t* fill, uint32_t n, hipStream_t s) {
   BuildInit h;
   for (int i = 0; i < kIndexHeaderBytes; i++) h.hdr[i] = hdr[i];

@@ -319,6 +319,7 @@ void launch_verify(const BuildParams& P, hipStream_t s, StageTimer* tm);
 void launch_stats(const BuildParams& P, hipStream_t s, int sequential, StageTimer* tm);
 void launch_stats_folded(const BuildParams& P, hipStream_t s, StageTimer* tm);
 void launch_build_init(uint8_t* out, const uint8_t* hdr, Status* st, uint32_t* fill, uint32_t n, hipStream_t s);
+void launch_status_out(const Status* st, Status* host, hipStream_t s);  // host: pinned, device-mapped
 constexpr int kDelParts = 64;
 void launch_sum_deletes(const BuildParams& P, hipStream_t s);
 void launch_stats_folded_shard(const BuildParams& P, hipStream_t s);

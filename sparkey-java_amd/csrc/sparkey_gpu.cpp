@@ -365,6 +365,7 @@ struct sparkey_plan {
   uint64_t* p1_off = nullptr;
   Status* d_status = nullptr;
   Status* h_status = nullptr;
+  Status* h_status_dev = nullptr;  // h_status as the device sees it (k_status_out writes it)
   unsigned long long* dbg = nullptr;  // SPARKEY_FRAME_DEBUG=1: k_frame phase counters
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   SideStreams side{};  // exact path: concurrent segment classes (created on first use)
@@ -1270,7 +1271,9 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
     // k_frame3: each entry straight into its placement bucket's fixed region (an atomic on the bucket's
     // count), no partition pass at all.  (k_frame_uniform keeps its pass 1 into the digit regions: its
     // per-tile digit runs beat an atomic per entry, C2 frame 0.28 against 0.62 ms, profiles/r04/)
-    const bool to_buckets = framing_path == 4 && use_buckets && use_fixed && P.b_lo == 0;
+    // A log whose header counts DELETEs goes to the exact path, which replays from the slabs: it
+    // frames into them from the start (bucket regions first and slabs again cost churn 0.8 ms).
+    const bool to_buckets = framing_path == 4 && use_buckets && use_fixed && P.b_lo == 0 && P.no_deletes;
     P.p1_bucket = to_buckets ? 1 : 0;
     P.p1_region = 0;
     P.p1_kernel = 0;
@@ -1321,7 +1324,8 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
     else launch_stats(P, s, 0, &pl->timer);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(pl->ev1, s));
-    HIP_TRY(hipMemcpyAsync(pl->h_status, pl->d_status, sizeof(Status), hipMemcpyDeviceToHost, s));
+    launch_status_out(pl->d_status, pl->h_status_dev, s);
+    HIP_TRY(hipGetLastError());
     HIP_TRY(hipStreamSynchronize(s));
     HIP_TRY(hipEventElapsedTime(&ms, pl->ev0, pl->ev1));
     print_frame_debug(pl, P);
@@ -1709,7 +1713,8 @@ int sparkey_plan_create(sparkey_plan** plan_out, int32_t device, uint64_t max_lo
   pl->device = device;
   if (hipStreamCreateWithFlags(&pl->own_stream, hipStreamNonBlocking) != hipSuccess ||
       hipMalloc((void**)&pl->d_status, sizeof(Status)) != hipSuccess ||
-      hipHostMalloc((void**)&pl->h_status, sizeof(Status), hipHostMallocDefault) != hipSuccess ||
+      hipHostMalloc((void**)&pl->h_status, sizeof(Status), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+      hipHostGetDevicePointer((void**)&pl->h_status_dev, pl->h_status, 0) != hipSuccess ||
       hipEventCreate(&pl->ev0) != hipSuccess || hipEventCreate(&pl->ev1) != hipSuccess) {
     sparkey_plan_destroy(pl);
     set_err(err, err_len, "HIP allocation failed");
