@@ -106,6 +106,7 @@ struct Status {
   unsigned long long acc_sum, acc_col, acc_max;  // k_stats_folded: totals over its blocks
   unsigned int p2_ticket;        // fused_carry: k_part2s blocks done (the last composes the digits)
   unsigned int pad3;
+  unsigned int seg_next[4];      // exact path: the next listed segment of each size class (work queue)
 };
 
 struct BuildParams {
