@@ -324,8 +324,29 @@ __global__ __launch_bounds__(256) void k_seg_marks(BuildParams P) {
 // reads at once (one slab a workgroup left one chain a thread: 0.51 + 0.59 ms for churn's 10M).
 constexpr uint32_t kSegSlabs = 4;
 
-// Every record finds the first slot of the segment holding its wanted slot.  A slot is occupied when
-// its mark is 0 (k_seg_marks), which is read beside the run start instead of after the slot itself.
+// The first slot of the run holding occupied slot t (a run with no empty slot before it wraps: it
+// starts after the table's last empty slot).
+__device__ __forceinline__ uint64_t run_start(const BuildParams& P, uint64_t t, int64_t last) {
+  const int64_t m = P.seg_start[t];
+  return m > 0 ? (uint64_t)m : (uint64_t)last % P.cap;
+}
+
+// The PUT records of a segment are exactly the entries the canonical placement left in its run (every
+// PUT record, duplicates included, was placed; occ(S) does not depend on the order), so a run's PUT
+// count is its length: the empty slot that ends a run writes it at the run's start, with no atomics.
+__global__ __launch_bounds__(256) void k_seg_runs(BuildParams P) {
+  const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= P.cap || P.seg_mark[e] == 0) return;  // (occupied)
+  const uint64_t p = e == 0 ? P.cap - 1 : e - 1;
+  if (P.seg_mark[p] == 0) {
+    const uint64_t st = run_start(P, p, P.seg_mark[P.cap]);
+    P.seg_cnt[st] = (uint32_t)(e >= st ? e - st : e + P.cap - st);
+  }
+}
+
+// DELETE records (the PUT records come from the table, k_seg_puts): each finds the first slot of the
+// segment holding its wanted slot and counts itself there.  A slot is occupied when its mark is 0.
+// kSegSlabs slabs a 64-thread workgroup (several chains a thread in flight).
 __global__ __launch_bounds__(64) void k_seg_assign(BuildParams P) {
   const int64_t last = P.seg_mark[P.cap];  // (last empty slot) + 1
   uint32_t n[kSegSlabs], nmax = 0;
@@ -337,23 +358,24 @@ __global__ __launch_bounds__(64) void k_seg_assign(BuildParams P) {
   }
   for (uint32_t j = threadIdx.x; j < nmax; j += 64) {
     uint64_t idx[kSegSlabs], sl[kSegSlabs];
-    int64_t mk[kSegSlabs], st[kSegSlabs];
+    bool del[kSegSlabs];
+    int64_t mk[kSegSlabs];
 #pragma unroll
     for (uint32_t k = 0; k < kSegSlabs; k++) {
       idx[k] = ((uint64_t)blockIdx.x * kSegSlabs + k) * P.slab_cap + j;
-      sl[k] = j < n[k] ? fast_mod(P.ent[idx[k]].hash, P.mod) : 0;
+      Entry en{0, 0};
+      if (j < n[k]) en = P.ent[idx[k]];
+      del[k] = j < n[k] && (en.addr & kDelBit);
+      sl[k] = del[k] ? fast_mod(en.hash, P.mod) : 0;
     }
 #pragma unroll
-    for (uint32_t k = 0; k < kSegSlabs; k++) {
-      mk[k] = P.seg_mark[sl[k]];
-      st[k] = P.seg_start[sl[k]];
-    }
+    for (uint32_t k = 0; k < kSegSlabs; k++) mk[k] = del[k] ? P.seg_mark[sl[k]] : 1;
 #pragma unroll
     for (uint32_t k = 0; k < kSegSlabs; k++) {
-      if (j >= n[k]) continue;
+      if (!del[k]) continue;
       uint64_t seg = kNoSeg;
-      if (mk[k] == 0) {
-        seg = st[k] > 0 ? (uint64_t)st[k] : (uint64_t)last % P.cap;
+      if (mk[k] == 0) {  // (a DELETE whose wanted slot is empty is a no-op in every state)
+        seg = run_start(P, sl[k], last);
         atomicAdd(&P.seg_cnt[seg], 1u);
       }
       P.eseg[idx[k]] = seg;
@@ -361,7 +383,24 @@ __global__ __launch_bounds__(64) void k_seg_assign(BuildParams P) {
   }
 }
 
-// Records grouped by segment (any order inside a segment: the replay sorts them).
+// The PUT records grouped by segment straight from the table: occupied slot t is record t - start of
+// its segment's list (slot order; the replay sorts a segment itself).  Reads and writes in slot order.
+__global__ __launch_bounds__(256) void k_seg_puts(BuildParams P) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= P.cap || P.seg_mark[t] != 0) return;
+  const uint64_t st = run_start(P, t, P.seg_mark[P.cap]);
+  const uint64_t dst = P.seg_off[st] + (t >= st ? t - st : t + P.cap - st);
+  if (dst >= P.max_records) {
+    guard_trip(P, 32u);
+    return;
+  }
+  uint64_t h, a;
+  read_slot(P, t, h, a);
+  P.ent3[dst] = Entry{h, a};
+}
+
+// The DELETE records after their segment's PUT records: seg_cnt still holds run length + DELETEs, and
+// each DELETE takes the place its decrement names (the top ones, above the run's PUT records).
 __global__ __launch_bounds__(64) void k_seg_scatter(BuildParams P) {
   uint32_t n[kSegSlabs], nmax = 0;
 #pragma unroll
@@ -376,7 +415,8 @@ __global__ __launch_bounds__(64) void k_seg_scatter(BuildParams P) {
 #pragma unroll
     for (uint32_t k = 0; k < kSegSlabs; k++) {
       idx[k] = ((uint64_t)blockIdx.x * kSegSlabs + k) * P.slab_cap + j;
-      seg[k] = j < n[k] ? P.eseg[idx[k]] : kNoSeg;
+      seg[k] = kNoSeg;
+      if (j < n[k] && (P.ent[idx[k]].addr & kDelBit)) seg[k] = P.eseg[idx[k]];
     }
 #pragma unroll
     for (uint32_t k = 0; k < kSegSlabs; k++) {
@@ -961,12 +1001,15 @@ void launch_segments(const BuildParams& P, hipStream_t s, int sorted_order, Stag
   scan_exclusive<int64_t, int64_t, OpMaxI64>(P.seg_mark, P.seg_start, P.cap, P.seg_mark + P.cap, OpMaxI64(),
                                              reinterpret_cast<int64_t*>(P.scan_scratch_u64), s);
   step("start scan");
+  hipLaunchKernelGGL(k_seg_runs, dim3(slot_grid), dim3(256), 0, s, P);
+  step("runs");
   const unsigned seg_grid = (unsigned)((P.nslabs + kSegSlabs - 1) / kSegSlabs);
   if (P.nslabs) hipLaunchKernelGGL(k_seg_assign, dim3(seg_grid), dim3(64), 0, s, P);
   step("assign");
   scan_exclusive<uint32_t, uint64_t, OpAdd>(P.seg_cnt, P.seg_off, P.cap, P.seg_off + P.cap, OpAdd(),
                                             P.scan_scratch_u64, s);
   step("count scan");
+  hipLaunchKernelGGL(k_seg_puts, dim3(slot_grid), dim3(256), 0, s, P);
   if (P.nslabs) hipLaunchKernelGGL(k_seg_scatter, dim3(seg_grid), dim3(64), 0, s, P);
   step("scatter");
   const unsigned cls_grid = (unsigned)((P.cap + kClsSlots - 1) / kClsSlots);
