@@ -1039,7 +1039,7 @@ void launch_segments(const BuildParams& P, hipStream_t s, int sorted_order, Stag
   step("huge");
   hipLaunchKernelGGL((k_seg_replay_wave<kLargeSegMax, 16, 2>), dim3(kLargeGrid), dim3(64), 0, sl, P, sorted_order);
   step("large");
-  hipLaunchKernelGGL((k_seg_replay_wave<kMidSegMax, 32, 1>), dim3(kMidGrid), dim3(64), 0, sm, P, sorted_order);
+  hipLaunchKernelGGL((k_seg_replay_wave<kMidSegMax, 16, 1>), dim3(kMidGrid), dim3(64), 0, sm, P, sorted_order);
   step("mid");
   hipLaunchKernelGGL(k_seg_small, dim3(slot_grid), dim3(256), 0, s, P, sorted_order);
   step("small");
