@@ -76,13 +76,16 @@ def main(src, dst, workload=None):
             out["per_launch_hbm_bytes"][st] = tot
     # the whole build: every kernel's bytes per dispatch times its dispatches per build (one k_build_init
     # a single-GPU build; a sharded rank counts its frame launches)
-    ref = next((k for k in ("k_build_init", "k_frame_uniform", "k_frame3", "k_frame") if k in out["kernels"]), None)
+    ref = next((k for k in ("k_frame_uniform", "k_frame3", "k_frame", "k_build_init") if k in out["kernels"]), None)
     if ref and all("hbm_bytes" in r for k, r in out["kernels"].items()
                    if k.startswith("k_") and r["total_ns"] > 0.01 * out["kernels"][ref]["total_ns"]):
         nb = out["kernels"][ref]["calls"]
-        # (the library's kernels only: torch's data generation and runtime copies are not the build)
-        out["per_launch_hbm_bytes"]["build"] = sum(r.get("hbm_bytes", 0.0) * r["calls"] / nb
-                                                   for k, r in out["kernels"].items() if k.startswith("k_"))
+        # (the library's kernels only: torch's data generation and runtime copies are not the build; a
+        #  kernel launched fewer times than the framing kernel belongs to another leg of the run, such
+        #  as bench.py's general-framing comparison, and is left out)
+        out["per_launch_hbm_bytes"]["build"] = sum(r.get("hbm_bytes", 0.0) * max(1, round(r["calls"] / nb))
+                                                   for k, r in out["kernels"].items()
+                                                   if k.startswith("k_") and r["calls"] >= nb)
     os.makedirs(os.path.dirname(dst), exist_ok=True)
     if workload:  # merge: one summary file holds every workload's counters
         try:
