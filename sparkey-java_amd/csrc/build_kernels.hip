@@ -147,26 +147,61 @@ __global__ __launch_bounds__(64) void k_emit(BuildParams P) {
 // bucket end as a function of the carry-in x is out(x) = max(c, x + a), c = max(0, n + M_last - B),
 // a = n - B.
 __global__ __launch_bounds__(kPlaceBlock) void k_summary(BuildParams P) {
-  __shared__ uint32_t cnt[kBucket];
-  __shared__ uint32_t base[kBucket];
-  __shared__ int32_t M[kBucket];
-  __shared__ uint64_t sh64[kPlaceBlock / 64 + 1];
-  __shared__ int64_t shm[kPlaceBlock / 64 + 1];
+  // Only M_last = max(0, max over occupied s of s - base[s]) is needed, not base[] and M[] per slot:
+  // 32-bit counts in LDS (4 KiB, was 12 KiB with the two per-slot arrays), each thread's 4 slots
+  // scanned in registers, the wave prefix by DPP and one barrier for the 4 waves' totals.
+  static_assert(kBucket == 4 * kPlaceBlock, "four slots per thread");
+  constexpr int NW = kPlaceBlock / 64;
+  constexpr int32_t kNone = INT32_MIN;
+  __shared__ __attribute__((aligned(16))) uint32_t cnt[kBucket];
+  __shared__ uint32_t wsum[NW];
+  __shared__ int32_t wmx[NW];
   if (build_aborted(P)) return;
   if (P.p2_sorted && !P.st->need_summary) return;  // k_part2s left every carry function
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const uint64_t b = P.b_lo + blockIdx.x;
   const uint64_t start = b << kBucketShift;
   const int64_t bsize = (int64_t)min((uint64_t)kBucket, P.cap - start);
   const uint32_t n = P.bcount[b];
   // (the framing's bucket regions: bucket b at b * kPlaceLdsMax, no offsets written)
   const uint64_t eoff = P.p1_bucket ? (b - P.b_lo) * (uint64_t)kPlaceLdsMax : P.boff[b];
-  bucket_histogram(P, b, n, eoff, start, cnt);
-  uint32_t mlast = 0;
-  bucket_scan(cnt, base, M, sh64, shm, &mlast);
-  if (threadIdx.x == 0) {
+  reinterpret_cast<uint4*>(cnt)[tid] = make_uint4(0u, 0u, 0u, 0u);
+  __syncthreads();
+  for (uint32_t i = tid; i < n; i += kPlaceBlock) {
+    const uint64_t w = fast_mod(P.ent2[eoff + i].hash, P.mod) - start;
+    atomicAdd(&cnt[w], 1u);
+  }
+  __syncthreads();
+  const uint4 c = reinterpret_cast<const uint4*>(cnt)[tid];
+  const uint32_t tot = c.x + c.y + c.z + c.w;
+  const uint32_t incl = wave_incl_sum_u32(tot);
+  // max over this thread's occupied slots of s - (wave-local base of s)
+  int32_t v = kNone;
+  {
+    const uint32_t cc[4] = {c.x, c.y, c.z, c.w};
+    uint32_t run = incl - tot;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      if (cc[i]) v = max(v, (int32_t)(4 * tid + i) - (int32_t)run);
+      run += cc[i];
+    }
+  }
+  const int32_t mv = wave_max_i32(v);
+  if (lane == 63) wsum[wv] = incl;
+  if (lane == 0) wmx[wv] = mv;
+  __syncthreads();
+  if (tid == 0) {
+    int64_t m = -1;  // (M_last counts only when positive)
+    uint32_t off = 0;
+#pragma unroll
+    for (int u = 0; u < NW; u++) {
+      if (wmx[u] != kNone) m = max(m, (int64_t)wmx[u] - (int64_t)off);
+      off += wsum[u];
+    }
+    const int64_t mlast = m < 0 ? 0 : m;
     MaxPlus f;
     f.a = (int64_t)n - bsize;
-    f.c = n ? max((int64_t)0, (int64_t)n + (int64_t)mlast - bsize) : 0;
+    f.c = n ? max((int64_t)0, (int64_t)n + mlast - bsize) : 0;
     P.bfun[b] = f;
   }
 }
