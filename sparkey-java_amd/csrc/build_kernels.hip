@@ -14,6 +14,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "build_kernels.hpp"
 #include "device_common.hpp"
 #include "kernel_utils.hpp"
@@ -272,8 +274,8 @@ __device__ void verify_pair(const BuildParams& P, uint64_t i) {
 __global__ void k_verify_pairs(BuildParams P) {
   if (build_aborted(P)) return;
   const unsigned long long np = min(P.st->n_pairs, (unsigned long long)P.pair_cap);
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < np) verify_pair(P, i);
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < np; i += (uint64_t)gridDim.x * blockDim.x)
+    verify_pair(P, i);
 }
 
 // ================================================================================================
@@ -527,7 +529,9 @@ void launch_place_global(const BuildParams& P, hipStream_t s, int sort_only, int
 }
 
 void launch_verify(const BuildParams& P, hipStream_t s, StageTimer* tm) {
-  hipLaunchKernelGGL(k_verify_pairs, dim3(grid_for(P.pair_cap, 256)), dim3(256), 0, s, P);
+  // (grid-stride over the pairs found: a grid sized to the pair buffer launched 65K idle waves a build)
+  hipLaunchKernelGGL(k_verify_pairs, dim3((unsigned)std::min<uint64_t>(grid_for(P.pair_cap, 256), 1024)), dim3(256), 0,
+                     s, P);
   tm->mark("verify", s);
 }
 
