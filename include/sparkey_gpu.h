@@ -327,7 +327,11 @@ int sparkey_shard_comm_create(sparkey_shard_comm** comm_out, const uint8_t* id, 
  * host memory and calls these on the rank's thread; each returns 0 on success.
  *   all_gather: every rank's `bytes` bytes at `send` -> `recv` (world * bytes, in rank order)
  *   all_to_all: send_bytes[r] bytes to rank r from consecutive runs of `send` in rank order;
- *               recv_bytes[r] bytes from rank r into consecutive runs of `recv` in rank order */
+ *               recv_bytes[r] bytes from rank r into consecutive runs of `recv` in rank order
+ * A rank that fails takes part in every collective up to the next checkpoint (with all-ones rows
+ * where its own cannot leave the device), so its peers fail with it there.  A rank whose process dies
+ * never arrives: the transport must time out on its own and return nonzero (the library has no way
+ * to interrupt a callback). */
 typedef struct sparkey_shard_transport {
   void* ctx;
   int (*all_gather)(void* ctx, const void* send, void* recv, uint64_t bytes);

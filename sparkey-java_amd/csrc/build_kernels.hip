@@ -575,6 +575,20 @@ void launch_build_init(uint8_t* out, const uint8_t* hdr, Status* st, uint32_t* f
   hipLaunchKernelGGL(k_build_init, dim3(1), dim3(256), 0, s, out, h, st, fill, n);
 }
 
+// Before the exact path frames a log again: the framing's status words back to their initial values
+// (err = none, no failed speculation, no overflow, no DELETE counted yet).
+__global__ void k_status_reframe(Status* st) {
+  if (threadIdx.x == 0) {
+    st->err = ~0ull;
+    st->spec_fail = 0;
+    st->overflow = 0;
+    st->max_wave_count = 0;
+    st->n_deletes = 0;
+  }
+}
+
+void launch_status_reframe(Status* st, hipStream_t s) { hipLaunchKernelGGL(k_status_reframe, dim3(1), dim3(64), 0, s, st); }
+
 // The framing's spread DELETE counters into st->n_deletes, cleared for the next framing launch.
 __global__ __launch_bounds__(64) void k_sum_deletes(BuildParams P) {
   const int lane = threadIdx.x;

@@ -211,6 +211,7 @@ struct BuildParams {
   int32_t f3_rgn;    // k_frame3: staged region bytes per wave (W * C + fr_look + 16, 16-byte multiple)
   int32_t f3_cand_cap;  // k_frame3: candidates (and records) per wave its LDS list holds (<= 512)
   int32_t f3_surv_cap;  // k_frame3: chain heads per wave after the short walk (<= 64, one long walk per lane)
+  int32_t f3_lcap;      // k_frame3: record starts a head lists inside its chunk (16 .. 128)
   int32_t fr_ticket;    // k_frame / k_frame3: regions by device-wide ticket, not by workgroup id (builds that
                         // share the device, or the frame_ticket switch)
   // uniform-stride framing (k_frame_uniform): uni_n records of uni_rec bytes from fr_entry
@@ -323,6 +324,7 @@ void launch_build_init(uint8_t* out, const uint8_t* hdr, Status* st, uint32_t* f
 void launch_status_out(const Status* st, Status* host, hipStream_t s);  // host: pinned, device-mapped
 constexpr int kDelParts = 64;
 void launch_sum_deletes(const BuildParams& P, hipStream_t s);
+void launch_status_reframe(Status* st, hipStream_t s);  // the framing's status words reset (exact path reframe)
 void launch_stats_folded_shard(const BuildParams& P, hipStream_t s);
 // exact replay (exact_kernels.hip)
 void launch_sequential(const BuildParams& P, hipStream_t s, int sorted_order);

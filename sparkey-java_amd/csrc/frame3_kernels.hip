@@ -52,35 +52,89 @@ namespace sk {
 
 namespace {
 
-constexpr int kF3Lcap = 16;      // record starts a survivor lists inside its chunk
+constexpr int kF3LcapMax = 128;  // record starts a survivor lists inside its chunk (P.f3_lcap, at most)
 constexpr unsigned kF3Caps = 64u;  // Status.spec_fail: a list cap was exceeded (k_frame redoes it)
 constexpr int kF3WavesPerSimd = 6;  // k_frame3's occupancy bound (its VGPR budget)
 
 // Scratch after the staged region (bytes), sized on the host so that four waves of a workgroup and
 // kF3WavesPerSimd workgroups fit a CU's LDS where the log allows (P.f3_cand_cap candidates, P.f3_surv_cap heads):
-// candidate list, later the wave's record list (u16 each); head starts / exits / counts / per-chunk
-// choice; the heads' record lists, earlier the screen bitmap and then the short walk's reached-start
-// bitmap (one bit per region byte).
+// candidate list; head starts / exits / counts / per-chunk choice (128 B) / a 16-byte sink that lanes
+// with nothing to store write to (so no store needs an exec-mask branch); the heads' record lists,
+// earlier the screen bitmap and then the short walk's reached-start bitmap (one bit per region byte).
 __host__ __device__ __forceinline__ int f3_off_meta(int cand_cap) { return 2 * cand_cap; }
+__host__ __device__ __forceinline__ int f3_off_sink(int cand_cap, int surv_cap) {
+  return f3_off_meta(cand_cap) + surv_cap * 5 + 128;
+}
 __host__ __device__ __forceinline__ int f3_off_lists(int cand_cap, int surv_cap) {
-  return (f3_off_meta(cand_cap) + surv_cap * 5 + 128 + 7) & ~7;
+  return (f3_off_sink(cand_cap, surv_cap) + 16 + 7) & ~7;
 }
 
 // One record step from region offset rp (screen rules, canonical one-byte VLQs): the next start,
-// or -1 when the bytes at rp are no plausible header.
+// or -1 when the bytes at rp are no plausible header.  Branch-free: every rule is a difference whose
+// sign says it failed, all ORed into one sign test (no chain of condition masks on the scalar unit).
+// delmask = -1 when the header counts no DELETE (a 0x00 first byte is then no start).  Bytes >= 0x80
+// (multi-byte VLQs) fail the maxima, which k_frame3's logs keep below 127 (fr_fast).
 __device__ __forceinline__ int32_t f3_step(const uint8_t* rgn, int32_t rp, int32_t lim, int32_t mk, int32_t mv,
-                                           bool nodel) {
+                                           int32_t delmask) {
   const int32_t b0 = rgn[rp], b1 = rgn[rp + 1];
-  const int32_t klen = b0 ? b0 - 1 : b1;
-  const int32_t vlen = b0 ? b1 : 0;
-  const bool ok = ((b0 | b1) & 0x80) == 0 && (b0 || !nodel) && klen <= mk && vlen <= mv && rp + 2 + klen <= lim;
-  return ok ? rp + 2 + klen + vlen : -1;
+  const bool del = b0 == 0;
+  const int32_t klen = del ? b1 : b0 - 1;
+  const int32_t vlen = del ? 0 : b1;
+  const int32_t kend = rp + 2 + klen;
+  const int32_t bad = (mk - klen) | (mv - vlen) | (lim - kend) | ((b0 - 1) & delmask);
+  return bad < 0 ? -1 : kend + vlen;
+}
+
+// LDS hand-offs between the lanes of one wave: a wave's LDS accesses complete in issue order, so a
+// compiler fence is all a later read of another lane's store needs (no s_waitcnt, no barrier).
+__device__ __forceinline__ void lds_fence() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
 }
 
 }  // namespace
 
-// One region (wave index wv) of k_frame3; its exit is published before any return.
-__device__ __forceinline__ void frame3_region(const BuildParams& P, const uint64_t wv, uint8_t* lds) {
+// Stage region wv's bytes [R0, R0 + RLEN) into LDS: every 1 KiB row in flight at once, straight into
+// LDS (the last row's lanes past the region masked off: the region is a 16-byte multiple, not whole
+// rows).  Only issued here; the LDS-DMA completes under vmcnt.
+__device__ __forceinline__ void f3_stage(const BuildParams& P, const uint64_t wv, uint8_t* rgn, const int lane) {
+  const int W = P.fr_w;
+  const int cs = P.fr_cshift;
+  const int64_t log_len = (int64_t)P.log_len;
+  const uint64_t k0 = P.fr_k0 + wv * (uint64_t)W;
+  const int nw = (int)min((uint64_t)W, P.fr_k0 + P.fr_nchunks - k0);
+  const int64_t R0 = (int64_t)(k0 << cs);
+  const int64_t RLEN = (int64_t)P.f3_rgn - ((int64_t)(W - nw) << cs);
+  const int nvec = (int)((RLEN + 15) >> 4);
+  if (R0 + 16ll * nvec <= log_len) {
+    const uint4* src = reinterpret_cast<const uint4*>(P.log + R0);
+    if (P.uni_nt) {  // non-temporal: the log is read once
+      for (int v0 = 0; v0 < nvec; v0 += 64)
+        if (v0 + lane < nvec)
+          __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + v0 + lane),
+                                           (__attribute__((address_space(3))) void*)(rgn + 16u * (uint32_t)v0), 16,
+                                           0, 2);
+    } else {
+      for (int v0 = 0; v0 < nvec; v0 += 64)
+        if (v0 + lane < nvec)
+          __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + v0 + lane),
+                                           (__attribute__((address_space(3))) void*)(rgn + 16u * (uint32_t)v0), 16,
+                                           0, 0);
+    }
+  } else {
+    for (int v = lane; v < nvec; v += 64)
+      *reinterpret_cast<uint4*>(rgn + 16u * v) = load16_guarded(P.log, R0 + 16ll * v, log_len);
+  }
+}
+
+constexpr uint64_t kF3NoNext = ~0ull;
+
+// One region (wave index wv) of k_frame3; its exit is published before any return.  `staged`: its
+// bytes are already in LDS (the wave's previous region prefetched them); `next`: the region this wave
+// frames next (kF3NoNext: none), whose bytes it stages once the last keys of this region are read --
+// under the bucket atomics' round trip.  True when it did.
+__device__ __forceinline__ bool frame3_region(const BuildParams& P, const uint64_t wv, uint8_t* lds, const bool staged,
+                                              const uint64_t next) {
   const int lane = threadIdx.x & 63;
   const int cs = P.fr_cshift;
   const int W = P.fr_w;
@@ -93,15 +147,16 @@ __device__ __forceinline__ void frame3_region(const BuildParams& P, const uint64
   // the staged bytes: the chunks, then at least max(LOOK, maxRecLen) + 16 more, so that every key a
   // listed record holds lies in LDS (records start inside the chunks)
   const int64_t RLEN = (int64_t)P.f3_rgn - ((int64_t)(W - nw) << cs);
-  const int kF3CandCap = P.f3_cand_cap, kF3SurvCap = P.f3_surv_cap;
+  const int kF3CandCap = P.f3_cand_cap, kF3SurvCap = P.f3_surv_cap, kF3Lcap = P.f3_lcap;
   const int kF3OffLists = f3_off_lists(kF3CandCap, kF3SurvCap);
   uint8_t* rgn = lds;
   uint8_t* scr = lds + P.f3_rgn;
-  uint16_t* cand = reinterpret_cast<uint16_t*>(scr);             // candidates, then the record list
+  uint16_t* cand = reinterpret_cast<uint16_t*>(scr);             // candidates (bit 15: alive, with marks)
   uint16_t* s_start = reinterpret_cast<uint16_t*>(scr + f3_off_meta(kF3CandCap));
   uint16_t* s_exit = s_start + kF3SurvCap;                          // 0xffff: died in the long walk
   uint8_t* s_cnt = reinterpret_cast<uint8_t*>(s_exit + kF3SurvCap);
-  int8_t* s_sel = reinterpret_cast<int8_t*>(s_cnt + kF3SurvCap);    // per chunk: chosen head, entry index
+  int8_t* s_sel = reinterpret_cast<int8_t*>(s_cnt + kF3SurvCap);    // per chunk: first / last head
+  uint16_t* sink = reinterpret_cast<uint16_t*>(scr + f3_off_sink(kF3CandCap, kF3SurvCap));
   uint16_t* lists = reinterpret_cast<uint16_t*>(scr + kF3OffLists);
   unsigned long long t_prev = P.dbg ? __builtin_amdgcn_s_memtime() : 0;
   auto mark = [&](int i) {  // diagnostic only: cycles per phase, per wave (no atomics)
@@ -138,34 +193,20 @@ __device__ __forceinline__ void frame3_region(const BuildParams& P, const uint64
       granule_store(&P.exit_desc[wv], (unsigned long long)R0 | kReady);
     }
   };
-
-  // ---- stage [R0, R0 + RLEN): every 1 KiB row in flight at once, straight into LDS (the last row's
-  //      lanes past the region masked off: the region is a 16-byte multiple, not whole rows) ----
-  {
-    const int nvec = (int)((RLEN + 15) >> 4);
-    if (R0 + 16ll * nvec <= log_len) {
-      const uint4* src = reinterpret_cast<const uint4*>(P.log + R0);
-      if (P.uni_nt) {  // non-temporal: the log is read once
-        for (int v0 = 0; v0 < nvec; v0 += 64)
-          if (v0 + lane < nvec)
-            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + v0 + lane),
-                                             (__attribute__((address_space(3))) void*)(rgn + 16u * (uint32_t)v0), 16,
-                                             0, 2);
-      } else {
-        for (int v0 = 0; v0 < nvec; v0 += 64)
-          if (v0 + lane < nvec)
-            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + v0 + lane),
-                                             (__attribute__((address_space(3))) void*)(rgn + 16u * (uint32_t)v0), 16,
-                                             0, 0);
-      }
-    } else {
-      for (int v = lane; v < nvec; v += 64)
-        *reinterpret_cast<uint4*>(rgn + 16u * v) = load16_guarded(P.log, R0 + 16ll * v, log_len);
+  // (frame3_stop: the exit published, the framing failed by wave 0 alone -- one atomic per wave on the
+  //  status word would serialise and swamp what is measured)
+  auto stop = [&]() {
+    if (lane == 0) {
+      if (wv == 0) atomicOr(&P.st->spec_fail, kF3Caps);
+      granule_store(&P.exit_desc[wv], (unsigned long long)R0 | kReady);
     }
-  }
-  wave_sync();
+  };
+
+  // ---- stage (unless the previous region of this wave prefetched it) ----
+  if (!staged) f3_stage(P, wv, rgn, lane);
+  wave_sync();  // (the LDS-DMA counts in vmcnt)
   mark(0);
-  if (P.f3_stop == 0) { fail(kF3Caps); return; }  // (SPARKEY_FRAME3_STOP: measurements)
+  if (P.f3_stop == 0) { stop(); return false; }  // (SPARKEY_FRAME3_STOP: measurements)
 
   // region offsets (32-bit) of the wave's bounds
   const int32_t de = (int32_t)min((int64_t)0x7fffffff, P.data_end - R0);  // records start below this
@@ -175,7 +216,7 @@ __device__ __forceinline__ void frame3_region(const BuildParams& P, const uint64
   const int32_t mk = (int32_t)P.max_key_len, mv = (int32_t)P.max_value_len;
   const int32_t mrl = (int32_t)P.max_rec_len;
   const int32_t look = (int32_t)LOOK;
-  const bool nodel = P.no_deletes != 0;
+  const int32_t delmask = P.no_deletes ? -1 : 0;
   const int32_t ent0 = (int32_t)(P.fr_entry - R0);  // (wave 0) the frame's entry
   const int32_t C = 1 << cs;
   auto chunk_end = [&](int32_t j) -> int32_t { return min((j + 1) * C, de); };
@@ -196,11 +237,12 @@ __device__ __forceinline__ void frame3_region(const BuildParams& P, const uint64
       fb[q] = (uint8_t)screen8(x, (x >> 8) | (r64[rw + 1] << 56), scn);
     }
   }
-  wave_sync();
+  lds_fence();
   mark(1);
-  if (P.f3_stop == 1) { fail(kF3Caps); return; }  // (SPARKEY_FRAME3_STOP: measurements)
+  if (P.f3_stop == 1) { stop(); return false; }  // (SPARKEY_FRAME3_STOP: measurements)
 
-  // ---- candidates, position order: word q = chunk q / nwl, positions 64 (q % nwl) + bit ----
+  // ---- candidates, position order: word q = chunk q / nwl, positions 64 (q % nwl) + bit.  Each lane
+  //      writes one of its set bits per step; the wave's steps are its largest count ----
   int32_t T = 0;
   bool over = false;
   {
@@ -234,136 +276,135 @@ __device__ __forceinline__ void frame3_region(const BuildParams& P, const uint64
         break;
       }
       uint32_t o = (uint32_t)T + incl - c;
-      while (m) {
-        cand[o++] = (uint16_t)(base + __builtin_ctzll(m));
-        m &= m - 1;
+      while (__ballot(m != 0)) {
+        const bool has = m != 0;
+        uint16_t* d = has ? cand + o : sink;
+        *d = (uint16_t)(base + __builtin_ctzll(m));
+        o += has ? 1u : 0u;
+        m &= m - 1ull;
       }
       T += tot;
     }
   }
   if (over) {
     fail(kF3Caps);
-    return;
+    return false;
   }
-  wave_sync();
+  lds_fence();
   mark(7);  // (the candidate list: reported after the other phases)
 
   // ---- 2 short walk: each candidate K records on (or to its stop); a survivor marks the starts it
   //      reached inside its chunk (bit 15 of its list entry: alive).  More heads than the lanes
-  //      (rare: a stretch of bytes that look like headers) walk one step more. ----
+  //      (rare: a stretch of bytes that look like headers) walk one step more.  A dead walk is
+  //      p = -1; every lane runs the K steps (selects, no per-lane exits). ----
   uint32_t* reached = reinterpret_cast<uint32_t*>(scr + kF3OffLists);  // (the screen bitmap is dead)
   const bool cover = P.f3_cover != 0;  // (windows that hold several true starts: mark the reached ones)
+  const unsigned long long lt_mask = (1ull << lane) - 1ull;
   int32_t S = 0;
   for (int K = P.f3_short;; K++) {
     if (cover) {
       for (int32_t i = lane; i < (ruse + 31) / 32 + 1; i += 64) reached[i] = 0u;
-      wave_sync();
+      lds_fence();
     }
     // without marks, a round's survivors are its heads: walk and compact in one pass
     S = 0;
     over = false;
     for (int32_t i0 = 0; i0 < T; i0 += 64) {
       const int32_t i = i0 + lane;
-      bool alive = false;
-      int32_t st = 0;
-      if (i < T) {
-        st = cand[i] & 0x7fff;
-        const int32_t e = chunk_end(st >> cs);
-        const int32_t stop = min(min(e + look, de), ruse);
-        int32_t p = st;
-        alive = true;
-        // (K steps for every lane, selects instead of a loop that breaks per lane: the wave's trip
-        //  count is uniform and its exec-mask bookkeeping goes)
-        for (int t = 0; t < K; t++) {
-          const bool go = alive && p < stop;
-          const int32_t q = f3_step(rgn, go ? p : 0, lim, mk, mv, nodel);
-          alive = alive && (!go || q >= 0);
-          p = go && q >= 0 ? q : p;
-          // (a start reached by a candidate that dies later dies too: marking it is harmless)
-          if (cover && go && q >= 0 && q < e) atomicOr(&reached[q >> 5], 1u << (q & 31));
-        }
-        if (cover) cand[i] = (uint16_t)(st | (alive ? 0x8000 : 0));
+      const bool in = i < T;
+      const int32_t st = in ? (int32_t)(cand[in ? i : 0] & 0x7fff) : 0;
+      const int32_t e = chunk_end(st >> cs);
+      const int32_t stop = min(min(e + look, de), ruse);
+      int32_t p = in ? st : -1;
+      for (int t = 0; t < K; t++) {
+        const bool go = p >= 0 && p < stop;
+        const int32_t q = f3_step(rgn, go ? p : 0, lim, mk, mv, delmask);
+        // (a start reached by a candidate that dies later dies too: marking it is harmless)
+        if (cover && go && q >= 0 && q < e) atomicOr(&reached[q >> 5], 1u << (q & 31));
+        p = go ? q : p;
       }
-      if (cover) continue;
+      const bool alive = in && p >= 0;
+      if (cover) {
+        uint16_t* d = in ? cand + i : sink;
+        *d = (uint16_t)(st | (alive ? 0x8000 : 0));
+        continue;
+      }
       const unsigned long long bal = __ballot(alive);
-      const int32_t before = (int32_t)__builtin_popcountll(bal & ((1ull << lane) - 1ull));
       const int32_t n = (int32_t)__builtin_popcountll(bal);
       if (S + n > kF3SurvCap) {
         over = true;
         break;
       }
-      if (alive) s_start[S + before] = (uint16_t)st;
+      uint16_t* d = alive ? s_start + S + (int32_t)__builtin_popcountll(bal & lt_mask) : sink;
+      *d = (uint16_t)st;
       S += n;
     }
     if (cover) {
-      wave_sync();
+      lds_fence();
       // heads: alive and reached from no other survivor, compacted in position order
       for (int32_t i0 = 0; i0 < T; i0 += 64) {
         const int32_t i = i0 + lane;
-        bool head = false;
-        int32_t st = 0;
-        if (i < T) {
-          const int32_t v = cand[i];
-          st = v & 0x7fff;
-          head = (v & 0x8000) && !((reached[st >> 5] >> (st & 31)) & 1u);
-        }
+        const int32_t v = i < T ? (int32_t)cand[i < T ? i : 0] : 0;
+        const int32_t st = v & 0x7fff;
+        const bool head = (v & 0x8000) && !((reached[st >> 5] >> (st & 31)) & 1u);
         const unsigned long long bal = __ballot(head);
-        const int32_t before = (int32_t)__builtin_popcountll(bal & ((1ull << lane) - 1ull));
         const int32_t n = (int32_t)__builtin_popcountll(bal);
         if (S + n > kF3SurvCap) {
           over = true;
           break;
         }
-        if (head) s_start[S + before] = (uint16_t)st;
+        uint16_t* d = head ? s_start + S + (int32_t)__builtin_popcountll(bal & lt_mask) : sink;
+        *d = (uint16_t)st;
         S += n;
       }
     }
     if (!over) break;
     if (K >= 8) {
       fail(kF3Caps);
-      return;
+      return false;
     }
-    wave_sync();
+    lds_fence();
   }
-  wave_sync();
+  lds_fence();
   mark(2);
-  if (P.f3_stop == 2) { fail(kF3Caps); return; }  // (SPARKEY_FRAME3_STOP: measurements)
+  if (P.f3_stop == 2) { stop(); return false; }  // (SPARKEY_FRAME3_STOP: measurements)
 
-  // ---- 3 long walk: head `lane` to its chunk end + LOOK, listing its starts in the chunk ----
-  bool lovf = false;
-  if (lane < S) {
-    // (a per-lane loop: the wave-uniform form with selects measured slower here, 6.9K against 5.6K
-    //  cycles a wave on C3 -- the heads are few and their walks short)
-    int32_t p = s_start[lane];
-    const int32_t e = chunk_end(p >> cs);
+  // ---- 3 long walk: head `lane` to its chunk end + LOOK, listing its starts in the chunk.  One
+  //      wave-uniform loop while any head walks: a lane whose walk ended (or that has no head) stores
+  //      to the sink, so no store or exit needs an exec-mask branch. ----
+  const bool hlane = lane < S;
+  const int32_t hst = hlane ? (int32_t)s_start[hlane ? lane : 0] : 0;  // this lane's head
+  int32_t hx = -1;                                                       // its exit (-1: died)
+  int32_t hcnt = 0;                                                      // starts it lists
+  {
+    const int32_t e = chunk_end(hst >> cs);
     const int32_t stop = min(min(e + look, de), ruse);
     uint16_t* my = lists + lane * kF3Lcap;
-    int32_t cnt = 0, ex = -1;
-    bool alive = true;
-    for (;;) {
-      if (p >= e && ex < 0) ex = p;
-      if (p >= stop) break;
-      if (p < e) {
-        if (cnt < kF3Lcap) my[cnt] = (uint16_t)p;
-        cnt++;
-      }
-      p = f3_step(rgn, p, lim, mk, mv, nodel);
-      if (p < 0) {
-        alive = false;
-        break;
-      }
+    int32_t p = hlane ? hst : -1;
+    int32_t ex = -1;
+    while (__ballot(p >= 0 && p < stop)) {
+      const bool go = p >= 0 && p < stop;
+      const bool lst = go && p < e;  // (a head starts inside its chunk)
+      uint16_t* d = lst && hcnt < kF3Lcap ? my + hcnt : sink;
+      *d = (uint16_t)p;
+      hcnt += lst ? 1 : 0;
+      const int32_t q = f3_step(rgn, go ? p : 0, lim, mk, mv, delmask);
+      ex = go && ex < 0 && q >= e ? q : ex;  // the first start at or past the chunk end
+      p = go ? q : p;
     }
-    if (cnt > kF3Lcap) lovf = true;
-    s_exit[lane] = alive && ex >= 0 ? (uint16_t)ex : (uint16_t)0xffff;
-    s_cnt[lane] = (uint8_t)min(cnt, 255);
+    hx = p >= 0 ? ex : -1;
+    if (hlane) {
+      s_exit[lane] = hx >= 0 ? (uint16_t)hx : (uint16_t)0xffff;
+      s_cnt[lane] = (uint8_t)min(hcnt, 255);
+    }
   }
-  if (__any(lovf)) {
+  if (__ballot(hcnt > kF3Lcap)) {
     fail(kF3Caps);
-    return;
+    return false;
   }
-  wave_sync();
+  lds_fence();
   mark(3);
-  if (P.f3_stop == 3) { fail(kF3Caps); return; }  // (SPARKEY_FRAME3_STOP: measurements)
+  if (P.f3_stop == 3) { stop(); return false; }  // (SPARKEY_FRAME3_STOP: measurements)
 
   // ---- 4 resolve, lane j = chunk j.  Heads are in position order: chunk j's are a contiguous run
   //      [c_first[j], c_last[j]].  A chunk whose alive heads all reach one exit is converged: its
@@ -374,27 +415,39 @@ __device__ __forceinline__ void frame3_region(const BuildParams& P, const uint64
   uint8_t* c_last = c_first + 64;
   {
     if (lane < nw) c_first[lane] = 0xff;
-    wave_sync();
-    const int32_t hc = lane < S ? ((int32_t)s_start[lane] >> cs) : 127;
+    lds_fence();
+    const int32_t hc = hlane ? (hst >> cs) : 127;
     const int32_t pc = wave_prev_i32(hc, -1), nc = wave_next_i32(hc, -1);
-    if (lane < S && (lane == 0 || pc != hc)) c_first[hc] = (uint8_t)lane;
-    if (lane < S && (lane == S - 1 || nc != hc)) c_last[hc] = (uint8_t)lane;
-    wave_sync();
+    uint8_t* df = hlane && (lane == 0 || pc != hc) ? c_first + hc : reinterpret_cast<uint8_t*>(sink);
+    *df = (uint8_t)lane;
+    uint8_t* dl = hlane && (lane == S - 1 || nc != hc) ? c_last + hc : reinterpret_cast<uint8_t*>(sink) + 1;
+    *dl = (uint8_t)lane;
+    lds_fence();
   }
   constexpr int32_t UNK = -2;
   int32_t hf = 0, hl = -1;  // this chunk's heads
   bool conv = false;
   int32_t cx = UNK;
-  if (lane < nw && c_first[lane] != 0xff) {
-    hf = c_first[lane];
-    hl = c_last[lane];
+  if (lane < nw) {
+    const int32_t f = c_first[lane];
+    if (f != 0xff) {
+      hf = f;
+      hl = c_last[lane];
+    }
+  }
+  {
+    // (the heads' exits by lane shuffles; a chunk's runs of heads are short: the loop runs to the
+    //  longest, every lane on its own run with selects)
+    const int32_t nh = hl - hf + 1;
+    const int32_t nmax = __builtin_amdgcn_readlane(wave_incl_max_i32(nh), 63);
     bool any = false;
     conv = true;
-    for (int32_t h = hf; h <= hl; h++) {
-      const int32_t ex = s_exit[h];
-      if (ex == 0xffff) continue;
-      if (!any) { cx = ex; any = true; }
-      else if (ex != cx) conv = false;
+    for (int32_t d = 0; d < nmax; d++) {
+      const int32_t ex = __shfl(hx, min(hf + d, 63), 64);
+      const bool use = d < nh && ex >= 0;
+      conv = conv && (!use || !any || ex == cx);
+      cx = use && !any ? ex : cx;
+      any = any || use;
     }
     conv = conv && any;
   }
@@ -412,17 +465,14 @@ __device__ __forceinline__ void frame3_region(const BuildParams& P, const uint64
         sel = g;
         return s_exit[g];
       }
+      const uint16_t* lg = lists + g * kF3Lcap;
       const int32_t n = min((int32_t)s_cnt[g], kF3Lcap);
-      for (int32_t k = 1; k < n; k++) {
-        const int32_t v = lists[g * kF3Lcap + k];
-        if (v >= e) {
-          if (v == e) {
-            sel = g;
-            at = k;
-            return s_exit[g];
-          }
-          break;
-        }
+      int32_t k = 1;
+      while (k < n && (int32_t)lg[k] < e) k++;
+      if (k < n && (int32_t)lg[k] == e) {
+        sel = g;
+        at = k;
+        return s_exit[g];
       }
     }
     return -1;
@@ -430,7 +480,7 @@ __device__ __forceinline__ void frame3_region(const BuildParams& P, const uint64
   // entries forward from whatever is known (converged chunks; chunk 0's entry e0 when given).  The
   // chunks resolved without e0 (pre = true) keep their result when e0 arrives or changes.
   int32_t ent = UNK, sel = -1, at = 0, myx = UNK;
-  bool bad = false, pre = false;
+  bool bad = false, pre = false, prefetched = false;
   auto resolve = [&](int32_t e0) {
     if (!pre) {
       ent = lane == 0 ? e0 : UNK;
@@ -448,7 +498,7 @@ __device__ __forceinline__ void frame3_region(const BuildParams& P, const uint64
       const int32_t inx = wave_prev_i32(kx, UNK);
       const bool take = lane >= 1 && lane < nw && ent == UNK && inx != UNK;
       if (take) ent = inx;
-      if (!__any(take || (lane < nw && myx == UNK && ent != UNK && !bad))) break;
+      if (!__ballot(take || (lane < nw && myx == UNK && ent != UNK && !bad))) break;
     }
   };
   // early exit: the wave's exit known without the first entry
@@ -464,20 +514,16 @@ __device__ __forceinline__ void frame3_region(const BuildParams& P, const uint64
   }
   // the first entry: the previous wave's exit; with one alive head in chunk 0, speculatively its start
   int32_t spec_e0 = -1;
-  if (lane == 0 && wv > 0) {
-    int32_t n0 = 0;
-    for (int32_t h = hf; h <= hl; h++)
-      if (s_exit[h] != 0xffff) {
-        n0++;
-        spec_e0 = s_start[h];
-      }
-    if (n0 != 1) spec_e0 = -1;
+  {
+    const int32_t h0f = __builtin_amdgcn_readfirstlane(hf), h0l = __builtin_amdgcn_readfirstlane(hl);
+    const unsigned long long al = __ballot(hx >= 0 && lane >= h0f && lane <= h0l);
+    if (wv > 0 && __builtin_popcountll(al) == 1) spec_e0 = __shfl(hst, (int)__builtin_ctzll(al), 64);
   }
   spec_e0 = __builtin_amdgcn_readfirstlane(spec_e0);
   bool spec = spec_e0 >= 0;
   int64_t ext = wv == 0 ? P.fr_entry : (spec ? R0 + spec_e0 : wait_prev());
   mark(4);
-  if (P.f3_stop == 4) { fail(kF3Caps); return; }  // (SPARKEY_FRAME3_STOP: measurements)
+  if (P.f3_stop == 4) { stop(); return false; }  // (SPARKEY_FRAME3_STOP: measurements)
   unsigned long long ndel = 0;
   uint32_t total = 0;
   unsigned long long base = 0;
@@ -488,7 +534,7 @@ __device__ __forceinline__ void frame3_region(const BuildParams& P, const uint64
     const int32_t nxt = wave_next_i32(ent, UNK);
     const bool broken = lane < nw && (bad || myx < 0 || (lane + 1 < nw && nxt != myx));
     const int32_t wexit = __builtin_amdgcn_readlane(myx, nw - 1);
-    if (__any(broken) || (early >= 0 && early != wexit)) {
+    if (__ballot(broken) || (early >= 0 && early != wexit)) {
       if (spec) {  // the guessed entry may be wrong: decide on the published one
         const int64_t real = wait_prev();
         spec = false;
@@ -499,12 +545,13 @@ __device__ __forceinline__ void frame3_region(const BuildParams& P, const uint64
       }
       if (early < 0) fail(1u);
       else if (lane == 0) atomicOr(&P.st->spec_fail, 1u);
-      return;
+      return false;
     }
     if (early < 0 && lane == 0) granule_store(&P.exit_desc[wv], (unsigned long long)(R0 + wexit) | kReady);
     if (lane == 0 && wv + 1 == (P.fr_nchunks + P.fr_w - 1) / P.fr_w) P.st->exit = R0 + wexit;
     // ---- counts: chunk `lane`'s records, their wave scan ----
-    const uint32_t cnt = sel >= 0 ? (uint32_t)(s_cnt[sel] - at) : 0u;
+    const int32_t scnt = __shfl(hcnt, max(sel, 0), 64);  // (every lane takes part in the shuffle)
+    const uint32_t cnt = sel >= 0 ? (uint32_t)(scnt - at) : 0u;
     const uint32_t incl = wave_incl_sum_u32(cnt);
     total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
     if (total > P.slab_cap) {
@@ -520,7 +567,7 @@ __device__ __forceinline__ void frame3_region(const BuildParams& P, const uint64
         atomicMax(&P.st->max_wave_count, total);
         atomicOr(&P.st->overflow, 1u);
       }
-      return;
+      return false;
     }
     if (lane == 0) P.wcount[wv] = total;
     // record r of the wave is entry r - base[j] of chunk j's chosen list (base: the scan of the
@@ -528,7 +575,7 @@ __device__ __forceinline__ void frame3_region(const BuildParams& P, const uint64
     const int32_t cbase = (int32_t)(incl - cnt);
     const int32_t csrc = sel >= 0 ? sel * kF3Lcap + at : 0;
     mark(5);
-    if (P.f3_stop == 5) { fail(kF3Caps); return; }  // (SPARKEY_FRAME3_STOP: measurements)
+    if (P.f3_stop == 5) { stop(); return false; }  // (SPARKEY_FRAME3_STOP: measurements)
     if (P.p1_bucket && spec) {  // (bucket regions: the entries leave as they are hashed, so the guessed
       const int64_t real = wait_prev();  // entry is checked first -- a redone round must not count twice)
       spec = false;
@@ -537,18 +584,24 @@ __device__ __forceinline__ void frame3_region(const BuildParams& P, const uint64
         continue;
       }
     }
-    // ---- 5 hash ----
+    // ---- 5 hash: rounds of 64 records (a lane past the last record hashes the wave's first one again
+    //      and stores nothing).  In the last round of a bucket-region build the next region's bytes
+    //      are staged between the bucket atomics and their stores: its keys are read by then, and the
+    //      LDS-DMA's latency hides under the atomics' round trip. ----
     base = wv * (unsigned long long)P.slab_cap;
     ndel = 0;
     bool bovf = false;
-    for (uint32_t r = (uint32_t)lane; r < total; r += 64) {
+    for (uint32_t r0 = 0; r0 < total; r0 += 64) {
+      const uint32_t r = r0 + (uint32_t)lane;
+      const bool act = r < total;
       int32_t src = 0;
       for (int j = 0; j < nw; j++) {  // (wave-uniform)
         const int32_t bj = __builtin_amdgcn_readlane(cbase, j);
         const int32_t sj = __builtin_amdgcn_readlane(csrc, j);
         if ((int32_t)r >= bj) src = sj + ((int32_t)r - bj);
       }
-      const int64_t p = R0 + (int64_t)lists[src];
+      const int32_t src0 = __builtin_amdgcn_readfirstlane(src);  // (lane 0's record: r0 < total)
+      const int64_t p = R0 + (int64_t)lists[act ? src : src0];
       const RecHdr h = decode_rgn(rgn, R0, p, log_len);
       const int64_t kp = p + h.hlen;
       const RgnKey ld{rgn, (uint32_t)(kp - R0)};  // (in the region: see RLEN)
@@ -557,18 +610,27 @@ __device__ __forceinline__ void frame3_region(const BuildParams& P, const uint64
       uint64_t addr = (uint64_t)p << P.ebb;
       if (!h.put) {
         addr |= kDelBit;
-        ndel++;
+        ndel += act ? 1 : 0;
       }
       Entry en;
       en.hash = hash;
       en.addr = addr;
       if (!P.p1_bucket) {
-        P.ent[base + r] = en;
-      } else if (h.put) {  // straight into the bucket's region (DELETEs stay out of the placement)
+        if (act) P.ent[base + r] = en;
+      } else {  // straight into the bucket's region (DELETEs stay out of the placement)
+        const bool put = act && h.put;
         const uint32_t b = bucket_of(P, hash);
-        const uint32_t a = atomicAdd(&P.bcount[b], 1u);
-        if (a < kPlaceLdsMax) P.ent2[(uint64_t)b * kPlaceLdsMax + a] = en;
-        else bovf = true;
+        uint32_t a = 0;
+        if (put) a = atomicAdd(&P.bcount[b], 1u);
+        if (next != kF3NoNext && r0 + 64 >= total) {  // (wave-uniform: every lane issues its rows)
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          f3_stage(P, next, rgn, lane);
+          prefetched = true;
+        }
+        if (put) {
+          if (a < kPlaceLdsMax) P.ent2[(uint64_t)b * kPlaceLdsMax + a] = en;
+          else bovf = true;
+        }
       }
     }
     if (bovf) atomicOr(&P.st->p2_overflow, 1u);
@@ -590,8 +652,23 @@ __device__ __forceinline__ void frame3_region(const BuildParams& P, const uint64
     P.dbg[wv * 16 + 9] = (unsigned long long)S;
     P.dbg[wv * 16 + 10] = early >= 0 ? 0ull : 1ull;
   }
+  if (next != kF3NoNext && !prefetched) {  // (slab builds: the last keys are read)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    f3_stage(P, next, rgn, lane);
+    prefetched = true;
+  }
+  return prefetched;
 }
 
+// Persistent: as many one-wave workgroups as the device holds at once (launch_frame3), wave w framing
+// regions w, w + G, w + 2G, ... and staging each next region while its current one finishes.  A region
+// waits only on lower regions' exits; every region below a wave's current one is finished or held by
+// a resident wave, so the waits form no cycle (and stay bounded all the same: the host redoes a framing
+// whose wait ran out).  Round 4 launched one workgroup per region (C3 10M 0.746 ms against 4-wave
+// workgroups' 0.834, one wave's LDS freed as soon as it ends); round 5 keeps the one-wave workgroups
+// and removes their 1.7M launches per 10M records and the exposed staging latency of each.  Builds
+// that share the device take one region per workgroup by a ticket from a device-wide counter instead
+// (fr_ticket): no wave then waits on one that is not resident.
 // One wave per workgroup, one region each: the waves share nothing, and each region's LDS is freed
 // as soon as its wave ends (4-wave workgroups averaged 2.8 resident waves per SIMD of the 4 their
 // LDS allowed, SQ_WAVE_CYCLES / GRBM_GUI_ACTIVE).  Region i is workgroup i: a wave spins on its
@@ -603,14 +680,19 @@ __device__ __forceinline__ void frame3_region(const BuildParams& P, const uint64
 // (frame3_fits).
 __global__ __launch_bounds__(64, kF3WavesPerSimd) void k_frame3(BuildParams P, uint32_t lds_per_wave) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  uint32_t tk = blockIdx.x;
+  const uint64_t nwaves = (P.fr_nchunks + P.fr_w - 1) / P.fr_w;
   if (P.fr_ticket) {
     uint32_t t = 0;
     if (threadIdx.x == 0) t = atomicAdd(P.frame_ticket, 1u);
-    tk = (uint32_t)__builtin_amdgcn_readfirstlane((int)t);
+    const uint32_t tk = (uint32_t)__builtin_amdgcn_readfirstlane((int)t);
+    if (tk < nwaves) frame3_region(P, tk, lds, false, kF3NoNext);
+    return;
   }
-  const uint64_t nwaves = (P.fr_nchunks + P.fr_w - 1) / P.fr_w;
-  if (tk < nwaves) frame3_region(P, tk, lds);
+  bool staged = false;
+  for (uint64_t r = blockIdx.x; r < nwaves; r += gridDim.x) {
+    const uint64_t nx = r + gridDim.x;
+    staged = frame3_region(P, r, lds, staged, nx < nwaves ? nx : kF3NoNext);
+  }
 }
 
 // LDS per wave: the staged region, then the scratch (candidates / record list, survivor data, lists
@@ -618,7 +700,7 @@ __global__ __launch_bounds__(64, kF3WavesPerSimd) void k_frame3(BuildParams P, u
 uint32_t frame3_lds_per_wave(const BuildParams& P) {
   const size_t bitmap = (size_t)P.fr_w * (size_t)((std::min<int64_t>(1ll << P.fr_cshift, P.max_rec_len) + 63) / 64) * 8;
   const size_t reached = P.f3_cover ? (size_t)((((int64_t)P.fr_w << P.fr_cshift) + P.fr_look + 31) / 32 + 1) * 4 : 0;
-  const size_t lists = (size_t)P.f3_surv_cap * kF3Lcap * 2;
+  const size_t lists = (size_t)P.f3_surv_cap * P.f3_lcap * 2;
   const size_t scratch =
       (size_t)f3_off_lists(P.f3_cand_cap, P.f3_surv_cap) + std::max<size_t>(std::max<size_t>(bitmap, reached), lists);
   return (uint32_t)(((size_t)P.f3_rgn + scratch + 15) & ~(size_t)15);
@@ -632,7 +714,10 @@ uint32_t frame3_lds_per_wave(const BuildParams& P) {
 bool frame3_fits(BuildParams& P, double mean_record, double pass) {
   const double C = (double)(1ll << P.fr_cshift);
   if (!P.fr_fast || P.max_rec_len > 4096 || P.fr_cshift < 7) return false;
-  if (mean_record <= 0.0 || C / mean_record > 0.6 * kF3Lcap) return false;
+  if (mean_record <= 0.0 || C / mean_record > 0.6 * kF3LcapMax) return false;
+  // a head's list: 16 starts while a chunk holds up to about 10 mean records, else 1 / 0.6 of its mean
+  // records (long chunks: fewer, longer chains a wave)
+  P.f3_lcap = C / mean_record <= 0.6 * 16 ? 16 : std::min(kF3LcapMax, ((int)std::ceil(C / mean_record / 0.6) + 7) & ~7);
   const int64_t tail = std::max<int64_t>(P.fr_look, P.max_rec_len);  // (the keys of the last chunk's records)
   if (((int64_t)P.fr_w << P.fr_cshift) + tail + 16 >= 32768) return false;  // 15-bit region offsets
   P.f3_rgn = (int32_t)((((int64_t)P.fr_w << P.fr_cshift) + tail + 16 + 15) & ~15ll);
@@ -641,7 +726,7 @@ bool frame3_fits(BuildParams& P, double mean_record, double pass) {
   if (recs > 0.6 * 512 || false_cands > 0.6 * 512) return false;
   const int need = std::min(512, (int)std::ceil(std::max(2.2 * (false_cands + P.fr_w) + 32.0, 1.7 * recs + 32.0)));
   // heads: about one per chunk plus a few false survivors; one long walk per lane
-  P.f3_surv_cap = std::min(64, std::max(32, (2 * P.fr_w + 8 + 7) & ~7));
+  P.f3_surv_cap = std::min(64, std::max(P.f3_lcap == 16 ? 32 : 16, (2 * P.fr_w + 8 + 7) & ~7));
   P.f3_cand_cap = 512;
   // the largest cap >= need (16-multiple) that keeps the most waves (up to kF3WavesPerSimd per SIMD) in
   // 160 KiB of LDS: workgroups of NW waves, + 16 B static each, in 512-byte allocation granules
@@ -659,7 +744,8 @@ void launch_frame3(const BuildParams& P, hipStream_t s, StageTimer* tm) {
   if (P.fr_nchunks == 0) return;
   const uint64_t nwaves = (P.fr_nchunks + P.fr_w - 1) / P.fr_w;
   const uint32_t per = frame3_lds_per_wave(P);
-  hipLaunchKernelGGL(k_frame3, dim3((unsigned)nwaves), dim3(64), (size_t)per, s, P, per);
+  const uint64_t grid = P.fr_ticket ? nwaves : resident_grid(reinterpret_cast<const void*>(k_frame3), 64, per, nwaves);
+  hipLaunchKernelGGL(k_frame3, dim3((unsigned)grid), dim3(64), (size_t)per, s, P, per);
   tm->mark("frame", s);
   scan_exclusive<uint32_t, uint64_t, OpAdd>(P.wcount, P.woff, P.nslabs, (uint64_t*)&P.st->n_records, OpAdd(),
                                             P.scan_scratch_u64, s);

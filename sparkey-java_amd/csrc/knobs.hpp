@@ -46,6 +46,7 @@ enum class Knob : int {
   FileThreads,      // file entry points: reader pool size
   FileWriteThreads, // file entry points: index writer threads
   FileDebug,        // file entry points: phase times to stderr
+  ReframeSpinTicks, // FrameSpinTicks for the exact path's second framing only (tests of its fallbacks)
   kCount
 };
 

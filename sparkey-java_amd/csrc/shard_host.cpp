@@ -291,9 +291,13 @@ class HostColl : public Coll {
   int all_gather(const void* d_send, void* d_recv, size_t bytes, hipStream_t s, std::string* why) override {
     uint8_t* h = stage((uint64_t)bytes * (world + 1));
     if (!h) return err(why, "pinned staging allocation failed");
-    int rc = copy(h, d_send, bytes, hipMemcpyDeviceToHost, s, why);
+    // A rank whose own rows cannot leave the device still takes part, with all-ones rows: the peers
+    // do not block in the transport, and a row whose code words read -1 fails every rank at the next
+    // checkpoint (fail_together).  (A peer that never arrives is the transport's to time out.)
+    const int rc = copy(h, d_send, bytes, hipMemcpyDeviceToHost, s, why);
+    if (rc) memset(h, 0xff, bytes);
+    if (t_.all_gather(t_.ctx, h, h + bytes, bytes) != 0) return rc ? rc : err(why, "host transport all_gather failed");
     if (rc) return rc;
-    if (t_.all_gather(t_.ctx, h, h + bytes, bytes) != 0) return err(why, "host transport all_gather failed");
     return copy(d_recv, h + bytes, (uint64_t)bytes * world, hipMemcpyHostToDevice, s, why);
   }
   int all_to_all(const uint8_t* d_send, const uint64_t* send_bytes, uint8_t* d_recv, const uint64_t* recv_bytes,
@@ -305,9 +309,10 @@ class HostColl : public Coll {
     }
     uint8_t* h = stage(sb + rb);
     if (!h) return err(why, "pinned staging allocation failed");
-    int rc = copy(h, d_send, sb, hipMemcpyDeviceToHost, s, why);
+    const int rc = copy(h, d_send, sb, hipMemcpyDeviceToHost, s, why);  // (as all_gather: take part anyway)
+    if (rc) memset(h, 0xff, sb);
+    if (t_.all_to_all(t_.ctx, h, send_bytes, h + sb, recv_bytes) != 0) return rc ? rc : err(why, "host transport all_to_all failed");
     if (rc) return rc;
-    if (t_.all_to_all(t_.ctx, h, send_bytes, h + sb, recv_bytes) != 0) return err(why, "host transport all_to_all failed");
     return copy(d_recv, h + sb, rb, hipMemcpyHostToDevice, s, why);
   }
 
@@ -1117,23 +1122,28 @@ int Rank::run(const uint8_t* hdr, uint64_t file_len, const uint8_t* d_buf, uint6
   bool fixed = true;
   for (;;) {
     const int64_t* digits = (const int64_t*)cm_->rows.p + (8 + G_);  // &rows[0][8 + G]
+    // (posting a neutral row can itself fail; the rank then still takes part in the collectives up to
+    //  the finish rows, so that no peer waits in one it never enters, and returns that failure there)
+    int post_rc = SPARKEY_OK;
     int lrc = sparkey_shard_summarize_dev(pl_, recv, n_recv, digits, RL, fixed ? 1 : 0, (int64_t*)fun, s_, err_, err_len_);
-    if (lrc) rc = gpu(hipMemsetAsync(fun, 0, 16, s_), "memset");
-    if (!rc) rc = all_gather(fun, cm_->funs, 16);
+    if (lrc) post_rc = gpu(hipMemsetAsync(fun, 0, 16, s_), "memset");
+    rc = all_gather(fun, cm_->funs, 16);
     if (rc) return rc;
     if (!lrc)
       lrc = sparkey_shard_place_dev(pl_, (const int64_t*)cm_->funs.p, d_out + hdr_off, spill, spill_cap, (int64_t*)flags,
                                     kSpillInline, s_, err_, err_len_);
-    if (lrc) rc = gpu(hipMemsetAsync(flags, 0, (uint64_t)FL * 8, s_), "memset");
-    if (!rc) rc = all_gather(flags, cm_->frows, (uint64_t)FL * 8);
+    if (lrc && !post_rc) post_rc = gpu(hipMemsetAsync(flags, 0, (uint64_t)FL * 8, s_), "memset");
+    rc = all_gather(flags, cm_->frows, (uint64_t)FL * 8);
     if (rc) return rc;
     if (!lrc) lrc = sparkey_shard_finish_dev(pl_, (const int64_t*)cm_->frows.p, FL, kSpillInline, (int64_t*)fin, s_, err_, err_len_);
     if (lrc) {
       int64_t f[12] = {0};
       f[3] = lrc;  // (a negative "aborted" flag: this rank failed)
-      rc = gpu(hipMemcpyAsync(fin, f, sizeof(f), hipMemcpyHostToDevice, s_), "H2D");
+      const int hrc = gpu(hipMemcpyAsync(fin, f, sizeof(f), hipMemcpyHostToDevice, s_), "H2D");
+      if (!post_rc) post_rc = hrc;
     }
-    if (!rc) rc = all_gather(fin, cm_->fins, 12 * 8);
+    rc = all_gather(fin, cm_->fins, 12 * 8);
+    if (!rc) rc = post_rc;
     if (!rc) rc = to_host(F.data(), cm_->fins.p, (uint64_t)G_ * 12 * 8);
     if (rc) return rc;
     std::vector<int64_t> codes(G_, 0);

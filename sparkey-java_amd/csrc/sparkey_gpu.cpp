@@ -571,7 +571,7 @@ static bool want_frame3(BuildParams& P, const LogHdr& lh, int64_t entry, int64_t
   if (knob_set(Knob::Frame3C)) want = std::max<int64_t>(P.max_rec_len, knob(Knob::Frame3C));
   int cs = 7;
   while ((1ll << cs) < want) cs++;
-  while (cs > 7 && (double)(1ll << cs) / mean > 8.0 && (1ll << (cs - 1)) >= P.max_rec_len) cs--;
+  while (!knob_set(Knob::Frame3C) && cs > 7 && (double)(1ll << cs) / mean > 8.0 && (1ll << (cs - 1)) >= P.max_rec_len) cs--;
   int64_t region = 8192;
   if (knob_set(Knob::FrameRegion)) region = std::min<int64_t>(16384, std::max<int64_t>(2048, knob(Knob::FrameRegion)));
   BuildParams Q = P;
@@ -1407,23 +1407,44 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
     P.p1_bucket = 0;
     if (reframe) {
       P.p1_region = 0;
-      // (its DELETE count is the first framing's; a speculative framing that does not hold this time
-      // -- a wait that ran out -- goes down the framing paths like the first one did)
+      // Every attempt starts from reset status words (err, spec_fail, overflow, the slab high-water
+      // mark, the DELETE count) and gets the main loop's checks: a slab that overflowed or more records
+      // than the workspace grow and redo it; a speculative framing that fails (spec_fail, or an error
+      // only the serial walk may report) goes down the framing paths like the first framing did.  The
+      // DELETE count is this framing's own, and must equal the first framing's.
       const unsigned long long ndel0 = st.n_deletes;
-      for (int fp = framing_path;;) {
-        HIP_TRY(hipMemsetAsync(&pl->d_status->spec_fail, 0, sizeof(unsigned), s));
+      if (knob_set(Knob::ReframeSpinTicks)) P.fr_spin_ticks = (uint64_t)knob(Knob::ReframeSpinTicks);
+      uint64_t nrec2 = std::max<uint64_t>(nrec, st.n_records);
+      for (int fp = framing_path, tries = 0;; tries++) {
+        if (tries >= 16) {
+          set_err(err, err_len, "internal error: the exact path's framing did not settle");
+          return SPARKEY_E_GPU;
+        }
         set_geom(P, geom0);
+        rc = reserve_for_framing(pl, P, fp, nrec2, slab_cap, err, err_len);
+        if (rc) return rc;
+        if (knob_set(Knob::ReframeSpinTicks)) P.fr_spin_ticks = (uint64_t)knob(Knob::ReframeSpinTicks);
+        launch_status_reframe(pl->d_status, s);
         rc = launch_framing(pl, P, fp, s, err, err_len);
         if (rc) return rc;
         HIP_TRY(hipMemcpyAsync(pl->h_status, pl->d_status, sizeof(Status), hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
-        if (!st.spec_fail || fp == 1) break;
+        if (slab_framing(fp) && st.max_wave_count > slab_cap) {
+          slab_cap = (uint32_t)std::min<uint64_t>(kPartTile, ((uint64_t)st.max_wave_count + 63) & ~63ull);
+          continue;
+        }
+        if (st.overflow || st.n_records > P.max_records) {
+          nrec2 = std::max<uint64_t>(st.n_records, nrec2 * 2 + 1);
+          continue;
+        }
+        if ((!st.spec_fail && st.err == ~0ull) || fp == 1) break;
         fp = fp == 4 ? 0 : 1;
-        rc = reserve_for_framing(pl, P, fp, std::max<uint64_t>(nrec, st.n_records), slab_cap, err, err_len);
-        if (rc) return rc;
       }
-      st.n_deletes = ndel0;
-      HIP_TRY(hipMemcpyAsync(&pl->d_status->n_deletes, &ndel0, sizeof(ndel0), hipMemcpyHostToDevice, s));
+      if (st.err == ~0ull && st.n_deletes != ndel0) {
+        set_err(err, err_len, "internal error: the second framing counted " + std::to_string(st.n_deletes) +
+                                  " DELETEs, the first " + std::to_string(ndel0));
+        return SPARKEY_E_GPU;
+      }
     }
     P.p1_region = 0;
     P.p1_kernel = 0;

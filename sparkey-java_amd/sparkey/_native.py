@@ -257,6 +257,10 @@ def build_index_sharded_device(log_header: bytes, file_len: int, d_bufs, d_outs,
     d_bufs[r] / d_outs[r] are device addresses of rank r's log range and .spi part
     (shard_geometry(..., r, opts.num_gpus))."""
     n = len(d_bufs)
+    if n != len(d_outs) or n != max(1, int(opts.num_gpus)):
+        # (the library reads d_bufs[rank] / d_outs[rank] for every rank < num_gpus)
+        raise ValueError(f"build_index_sharded_device: {len(d_bufs)} log ranges and {len(d_outs)} outputs "
+                         f"for num_gpus = {int(opts.num_gpus)}")
     bufs = (_vp * n)(*[ctypes.c_void_p(int(x)) for x in d_bufs])
     outs = (_vp * n)(*[ctypes.c_void_p(int(x)) for x in d_outs])
     stats = BuildStats()

@@ -103,7 +103,7 @@ def _switch(name: str) -> bool:
     (the CPU simulation of the device steps)."""
     try:
         from . import _native
-    except ImportError:
+    except (ImportError, OSError):  # (OSError: the library is there but cannot load, e.g. no libamdhip64)
         return False
     return _native.debug_get(name) > 0
 

@@ -472,6 +472,7 @@ def test_log_append_then_build(native):
 
 # --- k_frame3: the short/long walk framing of one-byte-VLQ logs ---
 @pytest.mark.parametrize("sw", [{}, {"frame3_c": 256}, {"frame3_c": 512}, {"frame3_c": 2048},
+                                {"frame3_c": 4096}, {"frame3_c": 8192}, {"frame3_c": 8192, "frame_region": 16384},
                                 {"frame_region": 16384}, {"frame_region": 4096}, {"frame_region": 6144},
                                 {"frame_ticket": 1}, {"frame3_short": 2}, {"frame3_cover": 1},
                                 {"frame_look": 16}, {"frame_look": 1024}])
@@ -534,6 +535,18 @@ def test_frame3_wait_timeout(native, switch):
     puts = random_puts(120000, seed=81, kmin=8, kmax=64, vmin=100, vmax=100)
     got, stats = check(native, make_log(puts), 83, hash_size=8)
     assert stats.framing_path == 1, stats.as_dict()
+
+
+@pytest.mark.parametrize("method", [IN_MEMORY, SORTING])
+def test_exact_reframe_wait_timeout(native, switch, method):
+    """The exact path frames a log again when k_frame3 wrote the bucket regions (overwritten keys, no
+    DELETE in the header).  A wait that runs out only in that second framing (reframe_spin_ticks)
+    goes down k_frame and then the serial walk, each attempt from reset status words, and the bytes
+    still match the oracle."""
+    switch(reframe_spin_ticks=0)
+    ops = _churn_ops(60000, 20000, 0.0, 85, klen=(8, 40), vlen=(20, 90))
+    got, stats = check(native, make_log(ops=ops), 85, hash_size=8, method=method)
+    assert stats.framing_path == 4 and stats.placement_path == 2, stats.as_dict()
 
 
 # --- EOF inside the last record's first VLQ ends the iteration quietly (SparkeyLogIterator.java:
