@@ -96,7 +96,7 @@ __device__ __forceinline__ void lds_fence() {
 
 // Stage region wv's bytes [R0, R0 + RLEN) into LDS: every 1 KiB row in flight at once, straight into
 // LDS (the last row's lanes past the region masked off: the region is a 16-byte multiple, not whole
-// rows).  Only issued here; the LDS-DMA completes under vmcnt.
+// rows).  Only issued here; the LDS-DMA completes under vmcnt (the wave_sync after it).
 __device__ __forceinline__ void f3_stage(const BuildParams& P, const uint64_t wv, uint8_t* rgn, const int lane) {
   const int W = P.fr_w;
   const int cs = P.fr_cshift;
@@ -127,14 +127,8 @@ __device__ __forceinline__ void f3_stage(const BuildParams& P, const uint64_t wv
   }
 }
 
-constexpr uint64_t kF3NoNext = ~0ull;
-
-// One region (wave index wv) of k_frame3; its exit is published before any return.  `staged`: its
-// bytes are already in LDS (the wave's previous region prefetched them); `next`: the region this wave
-// frames next (kF3NoNext: none), whose bytes it stages once the last keys of this region are read --
-// under the bucket atomics' round trip.  True when it did.
-__device__ __forceinline__ bool frame3_region(const BuildParams& P, const uint64_t wv, uint8_t* lds, const bool staged,
-                                              const uint64_t next) {
+// One region (wave index wv) of k_frame3; its exit is published before any return.
+__device__ __forceinline__ void frame3_region(const BuildParams& P, const uint64_t wv, uint8_t* lds) {
   const int lane = threadIdx.x & 63;
   const int cs = P.fr_cshift;
   const int W = P.fr_w;
@@ -173,7 +167,8 @@ __device__ __forceinline__ bool frame3_region(const BuildParams& P, const uint64
       const unsigned long long t0 = wall_clock64();
       for (;;) {
         const unsigned long long v = granule_load(&P.exit_desc[wv - 1]);
-        if (v & kReady) { extv = v & ~kReady; break; }
+        // (a bound of 0 gives up at once, even on a published exit: the tests of the host's redo)
+        if ((v & kReady) && P.fr_spin_ticks) { extv = v & ~kReady; break; }
         if (wall_clock64() - t0 >= P.fr_spin_ticks) {  // bounded all the same: serial path
           atomicOr(&P.st->spec_fail, 2u);
           extv = (unsigned long long)R0;
@@ -202,11 +197,11 @@ __device__ __forceinline__ bool frame3_region(const BuildParams& P, const uint64
     }
   };
 
-  // ---- stage (unless the previous region of this wave prefetched it) ----
-  if (!staged) f3_stage(P, wv, rgn, lane);
+  // ---- stage ----
+  f3_stage(P, wv, rgn, lane);
   wave_sync();  // (the LDS-DMA counts in vmcnt)
   mark(0);
-  if (P.f3_stop == 0) { stop(); return false; }  // (SPARKEY_FRAME3_STOP: measurements)
+  if (P.f3_stop == 0) { stop(); return; }  // (SPARKEY_FRAME3_STOP: measurements)
 
   // region offsets (32-bit) of the wave's bounds
   const int32_t de = (int32_t)min((int64_t)0x7fffffff, P.data_end - R0);  // records start below this
@@ -239,7 +234,7 @@ __device__ __forceinline__ bool frame3_region(const BuildParams& P, const uint64
   }
   lds_fence();
   mark(1);
-  if (P.f3_stop == 1) { stop(); return false; }  // (SPARKEY_FRAME3_STOP: measurements)
+  if (P.f3_stop == 1) { stop(); return; }  // (SPARKEY_FRAME3_STOP: measurements)
 
   // ---- candidates, position order: word q = chunk q / nwl, positions 64 (q % nwl) + bit.  Each lane
   //      writes one of its set bits per step; the wave's steps are its largest count ----
@@ -288,7 +283,7 @@ __device__ __forceinline__ bool frame3_region(const BuildParams& P, const uint64
   }
   if (over) {
     fail(kF3Caps);
-    return false;
+    return;
   }
   lds_fence();
   mark(7);  // (the candidate list: reported after the other phases)
@@ -361,13 +356,13 @@ __device__ __forceinline__ bool frame3_region(const BuildParams& P, const uint64
     if (!over) break;
     if (K >= 8) {
       fail(kF3Caps);
-      return false;
+      return;
     }
     lds_fence();
   }
   lds_fence();
   mark(2);
-  if (P.f3_stop == 2) { stop(); return false; }  // (SPARKEY_FRAME3_STOP: measurements)
+  if (P.f3_stop == 2) { stop(); return; }  // (SPARKEY_FRAME3_STOP: measurements)
 
   // ---- 3 long walk: head `lane` to its chunk end + LOOK, listing its starts in the chunk.  One
   //      wave-uniform loop while any head walks: a lane whose walk ended (or that has no head) stores
@@ -400,11 +395,11 @@ __device__ __forceinline__ bool frame3_region(const BuildParams& P, const uint64
   }
   if (__ballot(hcnt > kF3Lcap)) {
     fail(kF3Caps);
-    return false;
+    return;
   }
   lds_fence();
   mark(3);
-  if (P.f3_stop == 3) { stop(); return false; }  // (SPARKEY_FRAME3_STOP: measurements)
+  if (P.f3_stop == 3) { stop(); return; }  // (SPARKEY_FRAME3_STOP: measurements)
 
   // ---- 4 resolve, lane j = chunk j.  Heads are in position order: chunk j's are a contiguous run
   //      [c_first[j], c_last[j]].  A chunk whose alive heads all reach one exit is converged: its
@@ -480,7 +475,7 @@ __device__ __forceinline__ bool frame3_region(const BuildParams& P, const uint64
   // entries forward from whatever is known (converged chunks; chunk 0's entry e0 when given).  The
   // chunks resolved without e0 (pre = true) keep their result when e0 arrives or changes.
   int32_t ent = UNK, sel = -1, at = 0, myx = UNK;
-  bool bad = false, pre = false, prefetched = false;
+  bool bad = false, pre = false;
   auto resolve = [&](int32_t e0) {
     if (!pre) {
       ent = lane == 0 ? e0 : UNK;
@@ -523,7 +518,7 @@ __device__ __forceinline__ bool frame3_region(const BuildParams& P, const uint64
   bool spec = spec_e0 >= 0;
   int64_t ext = wv == 0 ? P.fr_entry : (spec ? R0 + spec_e0 : wait_prev());
   mark(4);
-  if (P.f3_stop == 4) { stop(); return false; }  // (SPARKEY_FRAME3_STOP: measurements)
+  if (P.f3_stop == 4) { stop(); return; }  // (SPARKEY_FRAME3_STOP: measurements)
   unsigned long long ndel = 0;
   uint32_t total = 0;
   unsigned long long base = 0;
@@ -545,7 +540,7 @@ __device__ __forceinline__ bool frame3_region(const BuildParams& P, const uint64
       }
       if (early < 0) fail(1u);
       else if (lane == 0) atomicOr(&P.st->spec_fail, 1u);
-      return false;
+      return;
     }
     if (early < 0 && lane == 0) granule_store(&P.exit_desc[wv], (unsigned long long)(R0 + wexit) | kReady);
     if (lane == 0 && wv + 1 == (P.fr_nchunks + P.fr_w - 1) / P.fr_w) P.st->exit = R0 + wexit;
@@ -567,7 +562,7 @@ __device__ __forceinline__ bool frame3_region(const BuildParams& P, const uint64
         atomicMax(&P.st->max_wave_count, total);
         atomicOr(&P.st->overflow, 1u);
       }
-      return false;
+      return;
     }
     if (lane == 0) P.wcount[wv] = total;
     // record r of the wave is entry r - base[j] of chunk j's chosen list (base: the scan of the
@@ -575,19 +570,24 @@ __device__ __forceinline__ bool frame3_region(const BuildParams& P, const uint64
     const int32_t cbase = (int32_t)(incl - cnt);
     const int32_t csrc = sel >= 0 ? sel * kF3Lcap + at : 0;
     mark(5);
-    if (P.f3_stop == 5) { stop(); return false; }  // (SPARKEY_FRAME3_STOP: measurements)
-    if (P.p1_bucket && spec) {  // (bucket regions: the entries leave as they are hashed, so the guessed
-      const int64_t real = wait_prev();  // entry is checked first -- a redone round must not count twice)
+    if (P.f3_stop == 5) { stop(); return; }  // (SPARKEY_FRAME3_STOP: measurements)
+    // Bucket regions: the entries leave as they are hashed, so a round redone after a wrong guess would
+    // count twice.  With marks (f3_cover) the single head of chunk 0 can be a false start whose chain
+    // joins the true one (the true start is then reached, not a head): the guess is checked first.
+    // Without marks every survivor is a head and the true start always survives, so a single alive head
+    // IS the true start of a log whose header holds: hash at once, and a mismatch (a header that lies)
+    // fails the whole framing below, which the host redoes on k_frame.
+    const bool spec_final = P.p1_bucket && spec && !cover;
+    if (P.p1_bucket && spec && cover) {
+      const int64_t real = wait_prev();
       spec = false;
       if (real != ext) {
         ext = real;
         continue;
       }
     }
-    // ---- 5 hash: rounds of 64 records (a lane past the last record hashes the wave's first one again
-    //      and stores nothing).  In the last round of a bucket-region build the next region's bytes
-    //      are staged between the bucket atomics and their stores: its keys are read by then, and the
-    //      LDS-DMA's latency hides under the atomics' round trip. ----
+    // ---- 5 hash: rounds of 64 records (a lane past the last record hashes the round's first one again
+    //      and stores nothing) ----
     base = wv * (unsigned long long)P.slab_cap;
     ndel = 0;
     bool bovf = false;
@@ -622,11 +622,6 @@ __device__ __forceinline__ bool frame3_region(const BuildParams& P, const uint64
         const uint32_t b = bucket_of(P, hash);
         uint32_t a = 0;
         if (put) a = atomicAdd(&P.bcount[b], 1u);
-        if (next != kF3NoNext && r0 + 64 >= total) {  // (wave-uniform: every lane issues its rows)
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          f3_stage(P, next, rgn, lane);
-          prefetched = true;
-        }
         if (put) {
           if (a < kPlaceLdsMax) P.ent2[(uint64_t)b * kPlaceLdsMax + a] = en;
           else bovf = true;
@@ -638,6 +633,10 @@ __device__ __forceinline__ bool frame3_region(const BuildParams& P, const uint64
       const int64_t real = wait_prev();
       spec = false;
       if (real != ext) {
+        if (spec_final) {  // (the entries are out: the framing fails, see above)
+          if (lane == 0) atomicOr(&P.st->spec_fail, 1u);
+          return;
+        }
         ext = real;
         continue;
       }
@@ -652,23 +651,8 @@ __device__ __forceinline__ bool frame3_region(const BuildParams& P, const uint64
     P.dbg[wv * 16 + 9] = (unsigned long long)S;
     P.dbg[wv * 16 + 10] = early >= 0 ? 0ull : 1ull;
   }
-  if (next != kF3NoNext && !prefetched) {  // (slab builds: the last keys are read)
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    f3_stage(P, next, rgn, lane);
-    prefetched = true;
-  }
-  return prefetched;
 }
 
-// Persistent: as many one-wave workgroups as the device holds at once (launch_frame3), wave w framing
-// regions w, w + G, w + 2G, ... and staging each next region while its current one finishes.  A region
-// waits only on lower regions' exits; every region below a wave's current one is finished or held by
-// a resident wave, so the waits form no cycle (and stay bounded all the same: the host redoes a framing
-// whose wait ran out).  Round 4 launched one workgroup per region (C3 10M 0.746 ms against 4-wave
-// workgroups' 0.834, one wave's LDS freed as soon as it ends); round 5 keeps the one-wave workgroups
-// and removes their 1.7M launches per 10M records and the exposed staging latency of each.  Builds
-// that share the device take one region per workgroup by a ticket from a device-wide counter instead
-// (fr_ticket): no wave then waits on one that is not resident.
 // One wave per workgroup, one region each: the waves share nothing, and each region's LDS is freed
 // as soon as its wave ends (4-wave workgroups averaged 2.8 resident waves per SIMD of the 4 their
 // LDS allowed, SQ_WAVE_CYCLES / GRBM_GUI_ACTIVE).  Region i is workgroup i: a wave spins on its
@@ -676,23 +660,18 @@ __device__ __forceinline__ bool frame3_region(const BuildParams& P, const uint64
 // same: the host redoes a framing whose wait ran out).  Builds that share the device take a ticket
 // from one device-wide counter instead (fr_ticket): no wave then waits on one that is not resident.
 // C3 10M on one box: one wave, no ticket 0.746 ms; 4 waves, ticket 0.856; 4 waves, no ticket 0.834;
-// 8 waves 1.27.  kF3WavesPerSimd waves (80 VGPRs) where a CU's LDS holds as many regions
-// (frame3_fits).
+// 8 waves 1.27.  Persistent waves that stage their next region while the current one
+// finishes measured slower (round 5: 1.02-1.09 ms against 0.83).
 __global__ __launch_bounds__(64, kF3WavesPerSimd) void k_frame3(BuildParams P, uint32_t lds_per_wave) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  const uint64_t nwaves = (P.fr_nchunks + P.fr_w - 1) / P.fr_w;
+  uint32_t tk = blockIdx.x;
   if (P.fr_ticket) {
     uint32_t t = 0;
     if (threadIdx.x == 0) t = atomicAdd(P.frame_ticket, 1u);
-    const uint32_t tk = (uint32_t)__builtin_amdgcn_readfirstlane((int)t);
-    if (tk < nwaves) frame3_region(P, tk, lds, false, kF3NoNext);
-    return;
+    tk = (uint32_t)__builtin_amdgcn_readfirstlane((int)t);
   }
-  bool staged = false;
-  for (uint64_t r = blockIdx.x; r < nwaves; r += gridDim.x) {
-    const uint64_t nx = r + gridDim.x;
-    staged = frame3_region(P, r, lds, staged, nx < nwaves ? nx : kF3NoNext);
-  }
+  const uint64_t nwaves = (P.fr_nchunks + P.fr_w - 1) / P.fr_w;
+  if (tk < nwaves) frame3_region(P, tk, lds);
 }
 
 // LDS per wave: the staged region, then the scratch (candidates / record list, survivor data, lists
@@ -744,8 +723,7 @@ void launch_frame3(const BuildParams& P, hipStream_t s, StageTimer* tm) {
   if (P.fr_nchunks == 0) return;
   const uint64_t nwaves = (P.fr_nchunks + P.fr_w - 1) / P.fr_w;
   const uint32_t per = frame3_lds_per_wave(P);
-  const uint64_t grid = P.fr_ticket ? nwaves : resident_grid(reinterpret_cast<const void*>(k_frame3), 64, per, nwaves);
-  hipLaunchKernelGGL(k_frame3, dim3((unsigned)grid), dim3(64), (size_t)per, s, P, per);
+  hipLaunchKernelGGL(k_frame3, dim3((unsigned)nwaves), dim3(64), (size_t)per, s, P, per);
   tm->mark("frame", s);
   scan_exclusive<uint32_t, uint64_t, OpAdd>(P.wcount, P.woff, P.nslabs, (uint64_t*)&P.st->n_records, OpAdd(),
                                             P.scan_scratch_u64, s);

@@ -557,9 +557,9 @@ static int setup_params(const LogHdr& lh, const IndexParams& ip, const sparkey_b
 // SPARKEY_NO_UNIFORM disables it (tests and the bench's general-framing measurement).
 // k_frame3 (frame3_kernels.hip) frames the log when its VLQs are one byte and the header's mean
 // record lets a chunk's records and a wave's records fit k_frame3's lists (SPARKEY_NO_FRAME3: k_frame).
-// Its chunk: the power of two >= maxRecLen near 4 mean records (a long walk of about four steps, and
-// a chunk's candidate window a small part of it), SPARKEY_FRAME3_C overrides; 8 KiB of chunks per
-// wave (SPARKEY_FRAME_REGION).  The geometry is set on P when k_frame3 is chosen (k_frame can frame
+// Its chunk: the power of two >= maxRecLen of 8-16 mean records (the long walks of about ten steps
+// against a wave's candidate windows and short walks, which grow with the chunk count), the frame3_c
+// switch overrides; 8 KiB of chunks per wave (frame_region).  The geometry is set on P when k_frame3 is chosen (k_frame can frame
 // with it too, which its fallback does).
 static bool want_frame3(BuildParams& P, const LogHdr& lh, int64_t entry, int64_t frame_end) {
   if (knob_on(Knob::NoFrame3) || !P.fr_fast || P.max_rec_len > 4096) return false;
@@ -567,11 +567,14 @@ static bool want_frame3(BuildParams& P, const LogHdr& lh, int64_t entry, int64_t
   const int64_t by = std::max<int64_t>(0, lh.put_size) + std::max<int64_t>(0, lh.delete_size);
   if (nr <= 0 || by <= 0) return false;
   const double mean = (double)by / (double)nr;
-  int64_t want = std::max<int64_t>(std::max<int64_t>(P.max_rec_len, 128), (int64_t)std::ceil(4.0 * mean));
+  // (8-16 mean records a chunk: C3's shape 2048 B, 0.774 ms against 1024 B's 0.815 per 10M records;
+  //  C2's records 1024 B, frame 0.62-0.64 ms against 512 B's 0.72 and 2048 B's 0.68; round 5,
+  //  profiles/r05/frame3/)
+  int64_t want = std::max<int64_t>(std::max<int64_t>(P.max_rec_len, 128), (int64_t)std::ceil(8.0 * mean));
   if (knob_set(Knob::Frame3C)) want = std::max<int64_t>(P.max_rec_len, knob(Knob::Frame3C));
   int cs = 7;
   while ((1ll << cs) < want) cs++;
-  while (!knob_set(Knob::Frame3C) && cs > 7 && (double)(1ll << cs) / mean > 8.0 && (1ll << (cs - 1)) >= P.max_rec_len) cs--;
+  while (!knob_set(Knob::Frame3C) && cs > 7 && (double)(1ll << cs) / mean > 16.0 && (1ll << (cs - 1)) >= P.max_rec_len) cs--;
   int64_t region = 8192;
   if (knob_set(Knob::FrameRegion)) region = std::min<int64_t>(16384, std::max<int64_t>(2048, knob(Knob::FrameRegion)));
   BuildParams Q = P;

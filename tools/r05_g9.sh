@@ -1,0 +1,5 @@
+set -o pipefail
+O=gpurun_out/r05g9; mkdir -p $O
+timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_parity.py > $O/pytest_parity.log 2>&1 || { tail -40 $O/pytest_parity.log; exit 1; }
+tail -2 $O/pytest_parity.log
+ROUNDS=2 bash tools/r05_ab.sh r05g9/ab "--workload c3 --entries 10000000 --steps 5 --warmup 1" r04 new1 new5 new5:frame3_persist=0 new5b new5b:frame3_c=2048 new5:frame3_c=2048
