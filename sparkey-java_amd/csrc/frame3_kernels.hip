@@ -601,14 +601,19 @@ __device__ __forceinline__ void frame3_region(const BuildParams& P, const uint64
         if ((int32_t)r >= bj) src = sj + ((int32_t)r - bj);
       }
       const int32_t src0 = __builtin_amdgcn_readfirstlane(src);  // (lane 0's record: r0 < total)
-      const int64_t p = R0 + (int64_t)lists[act ? src : src0];
-      const RecHdr h = decode_rgn(rgn, R0, p, log_len);
-      const int64_t kp = p + h.hlen;
-      const RgnKey ld{rgn, (uint32_t)(kp - R0)};  // (in the region: see RLEN)
-      const uint64_t hash = P.hash_size == 8 ? murmur64_ld(ld, h.klen, (uint32_t)P.seed)
-                                             : (uint64_t)murmur32_ld(ld, h.klen, (uint32_t)P.seed);
+      const uint32_t off = lists[act ? src : src0];
+      // (listed records passed f3_step's rules on the walk that listed them: one-byte VLQs, PUT =
+      //  klen + 1 then vlen, DELETE = 0 then klen; their keys lie in LDS, see RLEN)
+      const uint64_t hb = rgn_u64(rgn, off);
+      const int32_t b0 = (int32_t)(hb & 0xff), b1 = (int32_t)((hb >> 8) & 0xff);
+      const bool put = b0 != 0;
+      const int32_t klen = put ? b0 - 1 : b1;
+      const RgnKey ld{rgn, off + 2u};
+      const uint64_t hash = P.hash_size == 8 ? murmur64_ld(ld, klen, (uint32_t)P.seed)
+                                             : (uint64_t)murmur32_ld(ld, klen, (uint32_t)P.seed);
+      const int64_t p = R0 + (int64_t)off;
       uint64_t addr = (uint64_t)p << P.ebb;
-      if (!h.put) {
+      if (!put) {
         addr |= kDelBit;
         ndel += act ? 1 : 0;
       }
@@ -618,11 +623,11 @@ __device__ __forceinline__ void frame3_region(const BuildParams& P, const uint64
       if (!P.p1_bucket) {
         if (act) P.ent[base + r] = en;
       } else {  // straight into the bucket's region (DELETEs stay out of the placement)
-        const bool put = act && h.put;
+        const bool bput = act && put;
         const uint32_t b = bucket_of(P, hash);
         uint32_t a = 0;
-        if (put) a = atomicAdd(&P.bcount[b], 1u);
-        if (put) {
+        if (bput) a = atomicAdd(&P.bcount[b], 1u);
+        if (bput) {
           if (a < kPlaceLdsMax) P.ent2[(uint64_t)b * kPlaceLdsMax + a] = en;
           else bovf = true;
         }

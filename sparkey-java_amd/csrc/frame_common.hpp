@@ -18,12 +18,15 @@ namespace sk {
 // LDS byte access
 // ------------------------------------------------------------------------------------------------
 // 8 bytes starting at any offset of an 8-byte-aligned LDS window (two aligned 8-byte reads).
+// Funnel shift of hi:lo right by sh (0..63) without a branch: (hi << 1) << (63 - sh) is hi << (64 - sh)
+// for sh > 0 and 0 for sh = 0.  (`sh ? ... : lo` let the compiler sink the second load into a branch,
+// an exec-mask round trip per 8 bytes read.)
+__device__ __forceinline__ uint64_t funnel64(uint64_t lo, uint64_t hi, uint32_t sh) {
+  return (lo >> sh) | ((hi << 1) << (63u - sh));
+}
 __device__ __forceinline__ uint64_t lds_u64_at(const uint8_t* win, int off) {
   const uint64_t* w = reinterpret_cast<const uint64_t*>(win + (off & ~7));
-  const uint64_t lo = w[0];
-  const uint64_t hi = w[1];
-  const int sh = (off & 7) * 8;
-  return sh ? (lo >> sh) | (hi << (64 - sh)) : lo;
+  return funnel64(w[0], w[1], (uint32_t)(off & 7) * 8u);
 }
 
 // Record header at absolute position p whose bytes lie in the LDS window starting at wb.
@@ -164,10 +167,7 @@ __device__ __forceinline__ uint4 load16_guarded(const uint8_t* log, int64_t a, i
 // 8 bytes at any region offset (two aligned 8-byte reads; the region is allocated in 256 B blocks)
 __device__ __forceinline__ uint64_t rgn_u64(const uint8_t* r, uint32_t o) {
   const uint32_t a = o & ~7u;
-  const uint64_t lo = *reinterpret_cast<const uint64_t*>(r + a);
-  const uint64_t hi = *reinterpret_cast<const uint64_t*>(r + a + 8);
-  const uint32_t sh = (o & 7u) * 8u;
-  return sh ? (lo >> sh) | (hi << (64 - sh)) : lo;
+  return funnel64(*reinterpret_cast<const uint64_t*>(r + a), *reinterpret_cast<const uint64_t*>(r + a + 8), (o & 7u) * 8u);
 }
 struct RgnKey {
   const uint8_t* r;
