@@ -624,7 +624,9 @@ def sharded(args, dev, world, rank):
                                               device=dev)
     torch.cuda.synchronize(dev)
     gen_s = time.time() - t0
-    plan = _native.Plan(dev.index, hi - lo, 2 * args.entries)
+    # (the plan's workspace for twice the rank's records, so that no timed build grows it; the one-GPU
+    #  rehearsal of N ranks reserves for the records alone -- N ranks of C4's 125M fit 288 GB only so)
+    plan = _native.Plan(dev.index, hi - lo, (1 if args.backend == "gloo" else 2) * args.entries)
     stream = torch.cuda.Stream(dev)
     phases = {}
     shared_gpu = args.backend == "gloo"  # (the rehearsal: every rank on one GPU)
@@ -667,9 +669,11 @@ def sharded(args, dev, world, rank):
     torch.cuda.synchronize(dev)
     dist.barrier()
     elapsed = time.perf_counter() - t_start
-    t = torch.tensor([elapsed], dtype=torch.float64)
+    free_b, total_b = torch.cuda.mem_get_info(dev)  # (device-wide: every rank of a one-GPU rehearsal)
+    t = torch.tensor([elapsed, float(total_b - free_b)], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
+    elapsed = float(t[0].item())
+    device_used_gb = round(float(t[1].item()) / 1e9, 1)
     if churn:
         assert info["sharded"] == 2, info
     else:
@@ -740,6 +744,7 @@ def sharded(args, dev, world, rank):
         "phase_ms_rank0": {k: v / args.steps for k, v in phases.items()},
         "bit_identical_to_single_gpu": identical,
         "check_s": check_s,
+        "device_used_gb_after_timed_builds": device_used_gb,
         "cpu_baseline": None,
         "gen_s": gen_s,
         "version": sparkey.version(),

@@ -544,6 +544,7 @@ __device__ __forceinline__ void frame_region(const BuildParams& P, const uint64_
     //      consecutive entries written together); a wave holding more than kCandCap records hashes
     //      per chunk instead. ----
     ndel = 0;
+    bool bovf = false;
     auto emit = [&](int64_t p, uint64_t dst) -> int64_t {
       const RecHdr h = hdr_at(p);
       const int64_t kp = p + h.hlen;
@@ -567,7 +568,14 @@ __device__ __forceinline__ void frame_region(const BuildParams& P, const uint64_
       Entry en;
       en.hash = hash;
       en.addr = addr;
-      P.ent[dst] = en;
+      if (!P.p1_bucket) {
+        P.ent[dst] = en;
+      } else if (h.put) {  // straight into the bucket's fixed region, as k_frame3 (DELETEs stay out)
+        const uint32_t b = bucket_of(P, hash);
+        const uint32_t a = atomicAdd(&P.bcount[b], 1u);
+        if (a < kPlaceLdsMax) P.ent2[(uint64_t)b * kPlaceLdsMax + a] = en;
+        else bovf = true;
+      }
       return record_end(h, p);
     };
     if (total <= (unsigned long long)kCandCap) {  // wave-uniform
@@ -597,10 +605,18 @@ __device__ __forceinline__ void frame_region(const BuildParams& P, const uint64_
         if (go) p = emit(p, dst++);
       }
     }
+    if (bovf) atomicOr(&P.st->p2_overflow, 1u);
     if (spec) {  // check the guessed entry against the published exit; redo on a mismatch
       const int64_t real = wait_prev();
       spec = false;
       if (real != ext) {
+        // (bucket regions: the entries are out, so a redone round would count twice.  The guess is a
+        //  converged first chunk's single survivor, which the true entry of a log whose header holds
+        //  always is: a mismatch is a header that lies, and the framing fails -- the host redoes it)
+        if (P.p1_bucket) {
+          if (lane == 0) atomicOr(&P.st->spec_fail, 1u);
+          return;
+        }
         ext = real;
         continue;
       }
