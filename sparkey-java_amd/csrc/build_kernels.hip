@@ -377,10 +377,24 @@ __global__ __launch_bounds__(1024) void k_stats_final(BuildParams P, uint32_t np
 // first slot with the slot before it.  One thread per bucket; the last block to finish (ticket)
 // writes the header.
 constexpr int kStatFoldBlock = 256;
+// The status block into the host's pinned, mapped copy by one block's threads (k_status_out's work,
+// done by k_stats_folded's last block: one launch and its gap fewer a build).
+__device__ __forceinline__ void copy_status_out(const BuildParams& P) {
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(P.st);
+  uint32_t* dst = reinterpret_cast<uint32_t*>(P.status_host);
+  constexpr int kWords = (int)(sizeof(Status) / sizeof(uint32_t));
+  __threadfence();
+  for (int i = threadIdx.x; i < kWords; i += blockDim.x) dst[i] = __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __threadfence_system();
+}
+
 __global__ __launch_bounds__(kStatFoldBlock) void k_stats_folded(BuildParams P) {
   __shared__ unsigned long long s_sum[kStatFoldBlock / 64], s_col[kStatFoldBlock / 64], s_max[kStatFoldBlock / 64];
   __shared__ bool last;
-  if (build_aborted(P)) return;
+  if (build_aborted(P)) {  // (the host redoes the build: block 0 hands it the status)
+    if (blockIdx.x == 0 && P.status_host) copy_status_out(P);
+    return;
+  }
   Status* st = P.st;
   const int tid = threadIdx.x;
   if (P.fused_carry) {  // k_verify_pairs' work (no launch of its own)
@@ -388,8 +402,10 @@ __global__ __launch_bounds__(kStatFoldBlock) void k_stats_folded(BuildParams P) 
     for (uint64_t i = (uint64_t)blockIdx.x * kStatFoldBlock + tid; i < np; i += (uint64_t)gridDim.x * kStatFoldBlock)
       verify_pair(P, i);
   }
-  if (st->big_buckets || st->full) {  // some slots were placed outside k_place_reg: k_stats runs
-    if (tid == 0) st->stats_pending = 1u;
+  if (st->big_buckets || st->full) {  // some slots were placed outside k_place_reg: k_stats runs (and the
+    if (tid == 0) st->stats_pending = 1u;  // host reads the status again after it)
+    __syncthreads();
+    if (blockIdx.x == 0 && P.status_host) copy_status_out(P);
     return;
   }
   unsigned long long sum = 0, col = 0, mx = 0;
@@ -426,6 +442,10 @@ __global__ __launch_bounds__(kStatFoldBlock) void k_stats_folded(BuildParams P) 
     const unsigned long long tsum = atomicAdd(&st->acc_sum, 0ull), tcol = atomicAdd(&st->acc_col, 0ull);
     const unsigned long long tmax = atomicMax(&st->acc_max, 0ull);
     finish_stats(P, tsum, tcol, (long long)tmax, 0);
+  }
+  if (last && P.status_host) {
+    __syncthreads();
+    copy_status_out(P);
   }
 }
 

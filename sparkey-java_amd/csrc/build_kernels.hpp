@@ -229,6 +229,7 @@ struct BuildParams {
                         // bcount[] is the atomic cursor, zeroed before the framing
   int32_t p2_fixed;     // k_part2s in one pass: bucket b's entries at ent2[b * kPlaceLdsMax, + bcount[b])
   int32_t fold_stats;   // k_place_reg leaves calculateMaxDisplacement's per-bucket parts (no k_stats pass)
+  Status* status_host;  // fold_stats: k_stats_folded also copies the status block here (pinned, mapped; else null)
   int32_t stats_if_pending;  // k_stats / k_stats_final only when the folded stats left stats_pending
   uint64_t* bstat_start;  // fold_stats: per bucket, the first slot of the range it wrote (~0: none)
   uint32_t* p1_fill;

@@ -1333,11 +1333,13 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
     if (rc) return rc;
     launch_partition(P, s, &pl->timer);
     launch_place_fast(P, s, &pl->timer);
+    // (the folded stats' last block also hands the host its status: no k_status_out launch)
+    P.status_host = P.fold_stats ? pl->h_status_dev : nullptr;
     if (P.fold_stats) launch_stats_folded(P, s, &pl->timer);
     else launch_stats(P, s, 0, &pl->timer);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(pl->ev1, s));
-    launch_status_out(pl->d_status, pl->h_status_dev, s);
+    if (!P.fold_stats) launch_status_out(pl->d_status, pl->h_status_dev, s);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipStreamSynchronize(s));
     HIP_TRY(hipEventElapsedTime(&ms, pl->ev0, pl->ev1));
