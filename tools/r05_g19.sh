@@ -1,0 +1,5 @@
+set -o pipefail
+O=gpurun_out/r05g19; mkdir -p $O
+timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_parity.py > $O/pytest.log 2>&1 || { tail -40 $O/pytest.log; exit 1; }
+tail -1 $O/pytest.log
+ROUNDS=3 bash tools/r05_ab.sh r05g19/c2 "--workload c2 --steps 20 --warmup 3" new11 new12 new12:host_spin=0
