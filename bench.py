@@ -606,6 +606,7 @@ def sharded(args, dev, world, rank):
 
     n_total = args.entries * world
     churn = args.workload == "churn"  # overwrites + DELETEs: the sharded exact path
+    compressed = args.workload in ("snappy", "zstd")  # each rank decodes its own blocks
     full_log = None
     t0 = time.time()
     opts = _native.make_opts(hash_size=0, hash_seed=HASH_SEED, method=_native.METHOD_IN_MEMORY, device=dev.index)
@@ -613,11 +614,16 @@ def sharded(args, dev, world, rank):
         full_log = synth.churn_log(n_total, int(n_total * 0.8), 0.1, seed=args.seed + 4)
         file_len = int(full_log.size)
         header = full_log[:84].tobytes()
+    elif compressed:  # (every rank makes the whole compressed log, then keeps its byte range)
+        full_log = synth.snappy_log(synth.fixed_log(n_total, 16, 100, seed=args.seed, file_id=0x5EED0000), 118, 65536,
+                                    codec=args.workload)
+        file_len = int(full_log.size)
+        header = full_log[:84].tobytes()
     else:
         file_len = 84 + n_total * 118
         header, _ = synth.fixed_log_range(n_total, 0, 84, 16, 100, seed=args.seed, file_id=0x5EED0000)
     lo, hi, out_off, out_len = _native.shard_geometry(header, file_len, opts, rank, world)
-    if churn:
+    if churn or compressed:
         buf = torch.from_numpy(full_log[lo:hi]).to(dev)
     else:  # the rank's byte range, generated in HBM
         _, buf = synth_device.fixed_log_range(n_total, lo, hi, 16, 100, seed=args.seed, file_id=0x5EED0000,
@@ -626,7 +632,8 @@ def sharded(args, dev, world, rank):
     gen_s = time.time() - t0
     # (the plan's workspace for twice the rank's records, so that no timed build grows it; the one-GPU
     #  rehearsal of N ranks reserves for the records alone -- N ranks of C4's 125M fit 288 GB only so)
-    plan = _native.Plan(dev.index, hi - lo, (1 if args.backend == "gloo" else 2) * args.entries)
+    plan = _native.Plan(dev.index, (118 * args.entries + 65536 * 4) if compressed else hi - lo,
+                        (1 if args.backend == "gloo" else 2) * args.entries)
     stream = torch.cuda.Stream(dev)
     phases = {}
     shared_gpu = args.backend == "gloo"  # (the rehearsal: every rank on one GPU)
@@ -721,6 +728,8 @@ def sharded(args, dev, world, rank):
     cap = 1 | int(parse_log_header(header)["num_puts"] * 1.3)
     ms_per_step = elapsed * 1000.0 / args.steps
     b_alg_per_gpu = ((file_len - 84) + 112 + slot * cap) / world
+    if compressed:  # + the decoded records written and read back by the framing
+        b_alg_per_gpu += 2 * 118 * n_total / world
     achieved = b_alg_per_gpu / (ms_per_step * 1e-3) / 1e9
     c4 = n_total == 1_000_000_000 and not churn
     return {
@@ -729,7 +738,8 @@ def sharded(args, dev, world, rank):
                                 f"of 0.8 n, 10% DELETEs) in ONE index, sharded exact path" if churn else
                                 ("C4: " if c4 else "") +
                                 f"C2 shape, {args.entries} PUTs per GPU x {world} GPUs = {n_total} in ONE index "
-                                "(16 B key, 100 B value, NONE, IN_MEMORY)"),
+                                f"(16 B key, 100 B value, {args.workload.upper() + ' 64 KiB blocks' if compressed else 'NONE'}"
+                                ", IN_MEMORY)"),
                    "entries": n_total, "entries_per_gpu": args.entries, "log_bytes": file_len, "capacity": cap,
                    "spi_bytes": 112 + slot * cap,
                    "parallelism": f"log byte-range sharded x{world}, " +

@@ -84,8 +84,10 @@ typedef struct sparkey_build_stats {
   int32_t partition_passes;   /* passes over the entries of the bucket partition: 2; 1 when the
                                  uniform framing wrote the per-digit regions itself; 0 when it wrote
                                  every entry straight into its placement bucket */
-  int32_t sharded;            /* multi-GPU builds: 1 sharded canonical placement, 2 sharded exact path, 3 the log
-                                 gathered on every rank and built whole (compressed logs, full tables); else 0 */
+  int32_t sharded;            /* multi-GPU builds: 1 sharded canonical placement (SNAPPY / ZSTD logs too: each
+                                 rank decodes its own blocks), 2 sharded exact path, 3 the log gathered on every
+                                 rank and built whole (full tables, compressed logs with DELETEs or duplicate
+                                 keys); else 0 */
   double device_ms;           /* device time of the build (HIP events), excluding copies; sharded: the rank's
                                  wall time of sparkey_shard_build */
 } sparkey_build_stats;
@@ -340,9 +342,10 @@ typedef struct sparkey_shard_transport {
 int sparkey_shard_comm_create_host(sparkey_shard_comm** comm_out, const sparkey_shard_transport* transport,
                                    int32_t rank, int32_t world, int32_t device, char* err, size_t err_len);
 void sparkey_shard_comm_destroy(sparkey_shard_comm* comm);
-/* What rank `rank` must hold of the log (global bytes [*buf_lo, *buf_hi), buf_lo 4 KiB aligned) and the
- * part of the .spi it produces (bytes [*out_off, *out_off + *out_len) of the file: rank 0 the header and
- * its slots, every other rank its slots). */
+/* What rank `rank` must hold of the log (global bytes [*buf_lo, *buf_hi), buf_lo 4 KiB aligned: its byte
+ * range and a tail, for a SNAPPY / ZSTD log three of the block chain's longest hops) and the part of the
+ * .spi it produces (bytes [*out_off, *out_off + *out_len) of the file: rank 0 the header and its slots,
+ * every other rank its slots). */
 int sparkey_shard_geometry(const uint8_t* log_header, uint64_t file_len, const sparkey_build_opts* opts, int32_t rank,
                            int32_t world, uint64_t* buf_lo, uint64_t* buf_hi, uint64_t* out_off, uint64_t* out_len,
                            char* err, size_t err_len);

@@ -47,6 +47,7 @@ enum class Knob : int {
   FileWriteThreads, // file entry points: index writer threads
   FileDebug,        // file entry points: phase times to stderr
   ReframeSpinTicks, // FrameSpinTicks for the exact path's second framing only (tests of its fallbacks)
+  ShardGatherCompressed,  // num_gpus > 1: compressed logs gathered on every rank (the sharded path off)
   kCount
 };
 

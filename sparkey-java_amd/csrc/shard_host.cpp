@@ -11,8 +11,10 @@
 //                 equal-hash pairs (IndexHash.java:606-636) resolved with small exchanges.
 //   4. stats      calculateMaxDisplacement (IndexHash.java:195-245) per range plus the boundary rows;
 //                 rank 0 writes the 112-byte header.
-// Logs with DELETEs or duplicate keys take the sharded exact path; compressed logs and
-// tables the PUT records fill gather the log on every rank and build it whole (correct, not scaled).
+// Logs with DELETEs or duplicate keys take the sharded exact path.  Compressed logs
+//  are framed as their virtual log: each rank decodes the blocks of its own byte range
+// into its slice of it (Rank::compressed).  Compressed logs with DELETEs or duplicate keys, and tables
+// the PUT records fill, gather the log on every rank and build it whole (correct, not scaled).
 //
 // One rank is one sparkey_shard_build call on its own thread / process and device.  The collectives go
 // through Coll: RCCL (ncclAllGather, grouped ncclSend/ncclRecv; xGMI between the GPUs of a node), or
@@ -368,8 +370,11 @@ struct Layout {
   std::vector<int64_t> lo, hi;
   bool small;
   int64_t uni;  // uniform record size, or 0
+  int64_t cz_h;  // compressed logs: the block chain's hop bound (sk_cz_hop_bound), or 0
   int world;
-  int64_t overlap() const { return 2 * max_rec + window + 64; }
+  // bytes past a rank's range that it loads: records crossing into the next range; compressed logs:
+  // the next range's first anchor (at most 2 hops in) and the hop past it
+  int64_t overlap() const { return cz_h ? 3 * cz_h + 4096 : 2 * max_rec + window + 64; }
 };
 
 Layout make_layout(const uint8_t* h, int world) {
@@ -390,7 +395,8 @@ Layout make_layout(const uint8_t* h, int world) {
   L.world = world;
   for (int g = 0; g < world; g++) L.lo.push_back(kLogHeader + (int64_t)((__int128)g * span / world));
   for (int g = 0; g < world; g++) L.hi.push_back(g + 1 < world ? L.lo[g + 1] : L.data_end);
-  L.small = world > 1 && span / world < 2 * (L.max_rec + L.window) + 64;
+  L.cz_h = L.compression != 0 ? std::max<int64_t>(0, sk_cz_hop_bound(h)) : 0;
+  L.small = world > 1 && span / world < (L.cz_h ? 2 * L.cz_h + 4096 : 2 * (L.max_rec + L.window) + 64);
   // uniform records (sparkey_gpu.cpp uniform_record_size): the shard entries are arithmetic
   const int64_t r = vlq_size(L.max_key_len + 1) + vlq_size(L.max_value_len) + L.max_key_len + L.max_value_len;
   L.uni = (L.num_deletes == 0 && L.num_puts > 0 && L.max_key_len + 1 < 128 && L.max_value_len < 128 && r <= 256 &&
@@ -569,8 +575,8 @@ class Rank {
     return rc;
   }
   int64_t fe(int r) const {  // sharded.py frame_end(r)
-    if (r == G_ - 1) return L_.data_end;
-    return valid_[r + 1] ? entries_[r + 1] : L_.hi[r];
+    if (r == G_ - 1) return F_.data_end;
+    return valid_[r + 1] ? entries_[r + 1] : F_.hi[r];
   }
 
   int range_stats(uint64_t slot_lo, uint64_t slot_hi, std::vector<int64_t>* bnd);
@@ -580,6 +586,8 @@ class Rank {
             uint64_t slot_hi, bool* done, sparkey_build_stats* st);
   int gathered(const uint8_t* hdr, uint64_t file_len, const uint8_t* d_buf, uint64_t buf_lo,
                const sparkey_build_opts& o, uint8_t* out, uint64_t slot_lo, uint64_t out_len, sparkey_build_stats* st);
+  int compressed(const uint8_t* hdr, uint64_t file_len, const uint8_t* d_buf, uint64_t buf_lo, uint64_t buf_hi,
+                 const sparkey_build_opts& o, std::vector<int64_t>* cs, int64_t* vlen, bool* take);
 
   sparkey_plan* pl_;
   sparkey_shard_comm* cm_;
@@ -589,6 +597,9 @@ class Rank {
   size_t err_len_;
   int g_, G_;
   Layout L_;
+  Layout F_;    // the framed log's layout: L_, or the virtual log's (compressed logs)
+  bool virt_ = false;           // compressed log framed as its virtual log (Rank::compressed)
+  std::vector<int64_t> ce_;     // ... each rank's first block in the compressed log
   Geo geo_;
   std::vector<int64_t> entries_;
   std::vector<bool> valid_;
@@ -651,7 +662,7 @@ int Rank::pairs_share_a_key(int64_t n_pairs, bool* dup_any) {
     const int64_t pos = (int64_t)((addrs[i] & ~(1ull << 63)) >> geo_.ebb);
     int o = 0;
     for (int r = 0; r < G_; r++) {
-      const int64_t st = valid_[r] ? entries_[r] : L_.data_end;
+      const int64_t st = virt_ ? ce_[r] : valid_[r] ? entries_[r] : L_.data_end;
       if (st <= pos) o = r;  // searchsorted(starts, pos, right) - 1, clipped
     }
     owner[i] = o;
@@ -685,6 +696,7 @@ int Rank::pairs_share_a_key(int64_t n_pairs, bool* dup_any) {
   if (n2) rc = gpu(hipMemcpyAsync(dreq, req.data(), n2 * 8, hipMemcpyHostToDevice, s_), "H2D");
   std::string why;
   if (!rc) rc = coll_rc(c_->all_to_all(dreq, sb.data(), dgot, rb.data(), s_, &why), why);
+  if (!rc && n_req && virt_) rc = sk_cz_to_virtual(pl_, (uint64_t*)dgot, n_req, s_, err_, err_len_);
   if (!rc && n_req) rc = sparkey_shard_fetch_keys(pl_, (const uint64_t*)dgot, n_req, drec, (uint32_t)rs, s_, err_, err_len_);
   if (!rc) rc = coll_rc(c_->all_to_all(drec, sb2.data(), dback, rb2.data(), s_, &why), why);
   if (rc) return rc;
@@ -900,14 +912,90 @@ int Rank::gathered(const uint8_t* hdr, uint64_t file_len, const uint8_t* d_buf, 
   return rc;
 }
 
+// Compressed logs: each rank finds its part of the block chain from its own byte
+// range (sk_cz_entry), follows it to the next rank's entry (sk_cz_count: induction from 84 as for the
+// record chain) and decodes it into its slice of the virtual log (sk_cz_decode); the slices' starts
+// become the ranks' entries and the NONE steps run over them.  *take = false (every rank alike): the
+// gathered build, for logs these steps do not take (DELETEs, a record spanning two ranks' blocks, a
+// link that misses, an irregular block -- the gathered build reports a corrupt log's error).
+int Rank::compressed(const uint8_t* hdr, uint64_t file_len, const uint8_t* d_buf, uint64_t buf_lo, uint64_t buf_hi,
+                     const sparkey_build_opts& o, std::vector<int64_t>* cs, int64_t* vlen_out, bool* take) {
+  *take = false;
+  if (G_ == 1 || L_.small || !L_.cz_h || L_.num_deletes > 0 || sk::knob_on(sk::Knob::ShardGatherCompressed))
+    return SPARKEY_OK;
+  auto together = [&](const std::vector<int64_t>& rows, int stride, int own) {
+    std::vector<int64_t> codes(G_);
+    for (int r = 0; r < G_; r++) codes[r] = rows[(size_t)r * stride + stride - 1];
+    return fail_together(codes, own);
+  };
+  const int64_t lo = L_.lo[g_], hi = g_ + 1 < G_ ? L_.lo[g_ + 1] : L_.data_end;
+  int64_t e = -1;
+  int own = sk_cz_entry(pl_, hdr, file_len, d_buf, buf_lo, buf_hi, lo, hi, g_, s_, &e, err_, err_len_);
+  std::vector<int64_t> E;
+  int rc = gather_i64({e, own}, &E);
+  if (!rc) rc = together(E, 2, own);
+  if (rc) return rc;
+  mark("cz_directory");
+  std::vector<int64_t> ent(G_);
+  for (int r = 0; r < G_; r++) ent[r] = E[2 * r];
+  bool usable = ent[0] == kLogHeader;
+  for (int r = 1; r < G_; r++) usable = usable && ent[r] >= L_.lo[r] && ent[r] >= ent[r - 1] && ent[r] <= L_.data_end;
+  if (!usable) return SPARKEY_OK;
+  int32_t ok = 0;
+  uint64_t nb = 0, ul = 0;
+  own = sk_cz_count(pl_, ent[g_], g_ + 1 < G_ ? ent[g_ + 1] : L_.data_end, s_, &ok, &nb, &ul, err_, err_len_);
+  std::vector<int64_t> U;
+  rc = gather_i64({ok, (int64_t)ul, own}, &U);
+  if (!rc) rc = together(U, 3, own);
+  if (rc) return rc;
+  mark("cz_links");
+  int64_t vbase = kLogHeader, vlen = kLogHeader;
+  for (int r = 0; r < G_; r++) {
+    if (!U[3 * r]) return SPARKEY_OK;
+    if (r < g_) vbase += U[3 * r + 1];
+    vlen += U[3 * r + 1];
+  }
+  int64_t carry = -1;
+  own = sk_cz_decode(pl_, vbase, s_, &carry, err_, err_len_);
+  rc = gather_i64({carry, own}, &E);
+  if (!rc) rc = together(E, 2, own);
+  if (rc) return rc;
+  for (int r = 0; r < G_; r++)
+    if (E[2 * r] != 0) return SPARKEY_OK;
+  rc = agree(sk_cz_shard_begin(pl_, hdr, file_len, (uint64_t)vlen, &o, g_, G_, err_, err_len_));
+  if (rc) return rc;
+  cs->assign(G_, 0);
+  int64_t v = kLogHeader;
+  for (int r = 0; r < G_; r++) {
+    (*cs)[r] = v;
+    v += U[3 * r + 1];
+  }
+  uint8_t vh[kLogHeader];  // the virtual log's header (plan_build_snappy)
+  memcpy(vh, hdr, kLogHeader);
+  for (int i = 0; i < 8; i++) vh[32 + i] = (uint8_t)((uint64_t)vlen >> (8 * i));
+  memset(vh + 64, 0, 4);
+  vh[80] = 1;
+  memset(vh + 81, 0, 3);
+  F_ = make_layout(vh, G_);
+  ce_ = ent;
+  virt_ = true;
+  *vlen_out = vlen;
+  *take = true;
+  mark("cz_decode");
+  return SPARKEY_OK;
+}
+
 int Rank::run(const uint8_t* hdr, uint64_t file_len, const uint8_t* d_buf, uint64_t buf_lo, uint64_t buf_hi,
               const sparkey_build_opts& o, uint8_t* d_out, uint64_t out_cap, sparkey_build_stats* st, int rc0) {
   cm_->phase.clear();
   clock_ = now_ms();
   hdr_ = hdr;
   L_ = make_layout(hdr, G_);
+  F_ = L_;
+  virt_ = false;
+  ce_.clear();
   geo_ = make_geo(L_, hdr, o);
-  const int64_t data_end = L_.data_end;
+  int64_t data_end = L_.data_end;
   memset(st, 0, sizeof(*st));
   st->capacity = (int64_t)geo_.cap;
   st->hash_size = geo_.hash_size;
@@ -956,13 +1044,22 @@ int Rank::run(const uint8_t* hdr, uint64_t file_len, const uint8_t* d_buf, uint6
     if (rc0) return rc0;
     cs[0] = c_g;
   }
-  if (L_.compression != 0) return gathered(hdr, file_len, d_buf, buf_lo, o, d_out, slot_lo, out_len, st);
+  if (L_.compression != 0) {
+    bool take = false;
+    const int rc = compressed(hdr, file_len, d_buf, buf_lo, buf_hi, o, &cs, &data_end, &take);
+    if (rc) return rc;
+    if (!take) return gathered(hdr, file_len, d_buf, buf_lo, o, d_out, slot_lo, out_len, st);
+  }
   mark("entries");
   entries_.assign(G_, 0);
   valid_.assign(G_, false);
   int64_t last_valid = -1;
   bool have_last = false;
-  for (int r = 0; r < G_; r++) {
+  for (int r = 0; r < G_ && virt_; r++) {  // (the slices of the virtual log: every start is a record start)
+    entries_[r] = cs[r];
+    valid_[r] = true;
+  }
+  for (int r = 0; r < G_ && !virt_; r++) {
     const int64_t v = cs[r];
     bool ok = v >= 0 && (r == 0 || (L_.small && v == data_end) || (L_.lo[r] <= v && v <= data_end));
     if (ok && have_last && v < last_valid) ok = false;
@@ -1062,6 +1159,7 @@ int Rank::run(const uint8_t* hdr, uint64_t file_len, const uint8_t* d_buf, uint6
       if (r == G_ - 1) break;
       const int64_t nxt = std::min<int64_t>(x[2], data_end);
       if (R[(size_t)(r + 1) * RL] == nxt && valid_[r + 1] && entries_[r + 1] == nxt) continue;
+      if (virt_) return gathered(hdr, file_len, d_buf, buf_lo, o, d_out, slot_lo, out_len, st);  // (not a slice end)
       entries_[r + 1] = nxt;  // rank r + 1 re-frames from the verified exit
       valid_[r + 1] = true;
       std::fill(todo.begin(), todo.end(), false);
@@ -1104,7 +1202,13 @@ int Rank::run(const uint8_t* hdr, uint64_t file_len, const uint8_t* d_buf, uint6
   uint8_t* fin = cm_->fin.ensure(12 * 8);
   const bool have = (G_ == 1 || (send && rv)) && spill && flags && fun && fin && cm_->funs.ensure(16ull * G_) &&
                     cm_->frows.ensure((uint64_t)FL * 8 * G_) && cm_->fins.ensure(12ull * 8 * G_);
-  rc = agree(have ? SPARKEY_OK : fail(SPARKEY_E_GPU, "hipMalloc failed"));
+  int cz_rc = SPARKEY_OK;  // compressed log: the entries' virtual offsets -> the compressed log's addresses
+  if (have && virt_) {
+    uint64_t n_send = 0;
+    for (int r = 0; r < G_; r++) n_send += (uint64_t)R[(size_t)g_ * RL + 8 + r];
+    cz_rc = sk_cz_to_real(pl_, send, n_send, s_, err_, err_len_);
+  }
+  rc = agree(have ? cz_rc : fail(SPARKEY_E_GPU, "hipMalloc failed"));
   if (rc) return rc;
   const uint8_t* recv = nullptr;
   if (G_ > 1) {
@@ -1199,6 +1303,7 @@ int Rank::run(const uint8_t* hdr, uint64_t file_len, const uint8_t* d_buf, uint6
   }
   mark("spill");
   if (is_exact) {  // the ring splits at the slots the PUT placement left empty (now complete on every rank)
+    if (virt_) return gathered(hdr, file_len, d_buf, buf_lo, o, d_out, slot_lo, out_len, st);
     bool done = false;
     rc = exact(d_out, hdr_off, R[(size_t)g_ * RL + 3], o, slot_lo, slot_hi, &done, st);
     if (rc) return rc;

@@ -46,3 +46,27 @@ int shard_build_rank(sparkey_plan* plan, sparkey_shard_comm* comm, const uint8_t
                      size_t err_len);
 // the plan's ranks share their device with other builds: framing takes regions by ticket (sparkey_gpu.cpp)
 void sk_plan_set_shared_device(sparkey_plan* plan, bool shared);
+
+// Sharded compressed logs (sparkey_gpu.cpp).  0 or a SPARKEY_E_* code; a log these
+// steps do not take (a missed link, a record spanning two ranks' blocks, an irregular block) is
+// reported through *ok / *carry / *entry and built by the gathered path instead.
+// the hop bound H of the block chain (0: a NONE log, or blocks the parallel directory does not take)
+int64_t sk_cz_hop_bound(const uint8_t* log_header);
+// screen and anchors of [lo, hi) from the rank's compressed bytes [buf_lo, buf_hi); *entry: its first
+// anchor (84 on rank 0, dataEnd when lo >= dataEnd, -1 none)
+int sk_cz_entry(sparkey_plan* pl, const uint8_t* log_header, uint64_t file_len, const uint8_t* d_buf, uint64_t buf_lo,
+                uint64_t buf_hi, int64_t lo, int64_t hi, int32_t rank, hipStream_t s, int64_t* entry, char* err,
+                size_t err_len);
+// the chain from entry through the rank's anchors to next: *ok = 1 when every link lands on its end
+int sk_cz_count(sparkey_plan* pl, int64_t entry, int64_t next, hipStream_t s, int32_t* ok, uint64_t* nblk,
+                uint64_t* ulen, char* err, size_t err_len);
+// the counted blocks decoded into the virtual log's slice from vbase; *carry: bytes of the last record
+// past the rank's last block (-1: an irregular block)
+int sk_cz_decode(sparkey_plan* pl, int64_t vbase, hipStream_t s, int64_t* carry, char* err, size_t err_len);
+// sparkey_shard_begin over the slice (the virtual log is vlen bytes long), the table of the compressed log
+int sk_cz_shard_begin(sparkey_plan* pl, const uint8_t* log_header, uint64_t file_len, uint64_t vlen,
+                      const sparkey_build_opts* opts, int32_t rank, int32_t world, char* err, size_t err_len);
+// n 16-byte (hash, address) entries: virtual offsets -> (blockPosition << entryBlockBits) | entryIndex
+int sk_cz_to_real(sparkey_plan* pl, uint8_t* d_entries, uint64_t n, hipStream_t s, char* err, size_t err_len);
+// n compressed-log addresses of this rank's blocks -> virtual offsets (sparkey_shard_fetch_keys)
+int sk_cz_to_virtual(sparkey_plan* pl, uint64_t* d_addrs, uint64_t n, hipStream_t s, char* err, size_t err_len);

@@ -51,6 +51,7 @@ struct SnappyParams {
   const uint8_t* log;
   int64_t log_len;          // readable bytes of `log` (vector loads stay inside)
   int64_t data_end;
+  int64_t win0;             // parallel directory: the first window's start (84; a rank's range start when sharded)
   int64_t max_block;        // compressionBlockSize: the reader's uncompressed buffer
   SnappyBlock* blocks;
   uint64_t blk_cap;
@@ -95,5 +96,12 @@ hipError_t launch_snappy_decode(const SnappyParams& S, hipStream_t s);
 // blocks [0, nblk): their records
 void launch_snappy_walk(const SnappyParams& S, hipStream_t s);
 void launch_snappy_rewrite(const SnappyParams& S, hipStream_t s);
+// sharded compressed logs: a rank's blocks [0, nblk) with virtual offsets from
+// blocks[0].voff.  to_real: the address field (second word) of n 16-byte (hash, address) entries, a
+// virtual offset, becomes (blockPosition << ebb) | entryIndex; *err |= 1 when it is not a record start.
+// to_virtual: n such compressed-log addresses back to virtual offsets (an address of no block here:
+// all ones, which no rank decodes).
+void launch_cz_to_real(const SnappyParams& S, hipStream_t s, uint64_t* entries, uint64_t n, int32_t* err);
+void launch_cz_to_virtual(const SnappyParams& S, hipStream_t s, uint64_t* addrs, uint64_t n);
 
 }  // namespace sk

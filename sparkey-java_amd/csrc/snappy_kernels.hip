@@ -594,6 +594,57 @@ __global__ void __launch_bounds__(256) k_snappy_rewrite(SnappyParams S) {
   for (int i = 0; i < S.as; i++) os[S.hs + i] = (uint8_t)(fa >> (8 * i));
 }
 
+// Sharded compressed logs: one rank's blocks [0, nblk), their virtual offsets
+// ascending from blocks[0].voff over S.vlog_len decoded bytes, searched as k_snappy_rewrite does.
+__global__ void __launch_bounds__(256) k_cz_to_real(SnappyParams S, uint64_t* e, uint64_t n, int32_t* err) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t a = e[2 * i + 1];
+  const int64_t nb = (int64_t)S.nblk;
+  const uint64_t v0 = nb ? (uint64_t)S.blocks[0].voff : 0;
+  const uint64_t span = S.vlog_len > 0 ? (uint64_t)S.vlog_len : 1;
+  const int64_t g0 = min(nb - 1, (int64_t)((double)(a - min(a, v0)) / (double)span * (double)nb));
+  const int64_t b = nb ? gallop_last(nb, max((int64_t)0, g0), [&](int64_t k) { return (uint64_t)S.blocks[k].voff <= a; }) : -1;
+  if (b < 0) {
+    atomicOr(err, 1);
+    return;
+  }
+  const SnappyBlock B = S.blocks[b];
+  const uint64_t rel = a - (uint64_t)B.voff;
+  const uint32_t* offs = S.rec_off + (uint64_t)b * S.mepb;
+  const uint32_t cnt = min(S.walk[b].count, S.mepb);
+  if (rel >= B.ulen || cnt == 0) {
+    atomicOr(err, 1);
+    return;
+  }
+  const int64_t g = min((int64_t)cnt - 1, (int64_t)((double)rel / (double)max(B.ulen, 1u) * (double)cnt));
+  const uint32_t l = (uint32_t)(gallop_last((int64_t)cnt, g, [&](int64_t j) { return offs[j] < (uint32_t)rel; }) + 1);
+  if (l >= cnt || offs[l] != (uint32_t)rel) {
+    atomicOr(err, 1);
+    return;
+  }
+  e[2 * i + 1] = ((uint64_t)B.file_pos << S.ebb) | l;
+}
+
+__global__ void __launch_bounds__(256) k_cz_to_virtual(SnappyParams S, uint64_t* addrs, uint64_t n) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t a = addrs[i] & ~(1ull << 63);
+  const int64_t p = (int64_t)(a >> S.ebb);
+  const uint32_t idx = (uint32_t)(a & ((1ull << S.ebb) - 1));
+  uint64_t v = ~0ull >> 1;
+  const int64_t nb = (int64_t)S.nblk;
+  if (nb) {
+    const int64_t p0 = S.blocks[0].file_pos, p1 = S.blocks[nb - 1].file_pos;
+    const int64_t g0 = p1 > p0 ? min(nb - 1, (int64_t)((double)(p - min(p, p0)) / (double)(p1 - p0) * (double)(nb - 1)))
+                               : 0;
+    const int64_t b = gallop_last(nb, max((int64_t)0, g0), [&](int64_t k) { return S.blocks[k].file_pos <= p; });
+    if (b >= 0 && S.blocks[b].file_pos == p && idx < min(S.walk[b].count, S.mepb))
+      v = (uint64_t)S.blocks[b].voff + S.rec_off[(uint64_t)b * S.mepb + idx];
+  }
+  addrs[i] = v;
+}
+
 // ------------------------------------------------------------------------------------------------
 // Parallel block directory: anchors on the block chain found by speculation, the
 // chain between them walked from every anchor at once, every link checked.
@@ -777,9 +828,10 @@ constexpr int kDirCand = kSdirCand;  // candidate starts per window
 
 }  // namespace
 
-// Window k = [84 + k A, 84 + k A + H), H = the longest hop (so it holds a true start unless it runs
-// past dataEnd): its plausible starts whose next block is plausible too, into cand[k].  The window's
-// bytes (and 384 past it, for the screen's look-ahead) are staged in LDS first.
+// Window k = [w + k A, w + k A + H) (w = S.win0: 84, or a rank's range start), H = the longest hop
+// (so it holds a true start unless it runs past dataEnd): its plausible starts whose next block is
+// plausible too, into cand[k].  The window's bytes (and 384 past it, for the screen's look-ahead) are
+// staged in LDS first.
 template <int kCodec>
 __global__ __launch_bounds__(1024) void k_sdir_screen(SnappyParams S, int64_t A, int64_t H, int64_t* cand,
                                                      int32_t* ncand) {
@@ -787,7 +839,7 @@ __global__ __launch_bounds__(1024) void k_sdir_screen(SnappyParams S, int64_t A,
   __shared__ int32_t n;
   const uint64_t k = blockIdx.x;
   if (threadIdx.x == 0) n = 0;
-  const int64_t w0 = 84 + (int64_t)k * A;
+  const int64_t w0 = S.win0 + (int64_t)k * A;
   const int64_t w1 = min(w0 + H, S.data_end);
   const int64_t base = w0 & ~15LL;
   const int64_t nst = min<int64_t>(((w1 - base + 384 + 15) & ~15LL), ((S.log_len - base) & ~15LL));
@@ -813,7 +865,7 @@ __global__ __launch_bounds__(64) void k_sdir_anchor(SnappyParams S, int64_t A, i
                                                     const int32_t* ncand, int64_t* anchor) {
   const uint64_t k = blockIdx.x;
   const int lane = threadIdx.x;
-  const int64_t wend = 84 + (int64_t)k * A + H;
+  const int64_t wend = S.win0 + (int64_t)k * A + H;
   const int32_t nc = ncand[k];
   const GlobalWin win{&S};
   int64_t x = -1;
@@ -907,6 +959,13 @@ void launch_sdir_link(const SnappyParams& S, hipStream_t s, int codec, const int
 }
 
 void launch_snappy_dir(const SnappyParams& S, hipStream_t s) { hipLaunchKernelGGL(k_snappy_dir, 1, 64, 0, s, S); }
+
+void launch_cz_to_real(const SnappyParams& S, hipStream_t s, uint64_t* entries, uint64_t n, int32_t* err) {
+  if (n) hipLaunchKernelGGL(k_cz_to_real, dim3((unsigned)((n + 255) / 256)), 256, 0, s, S, entries, n, err);
+}
+void launch_cz_to_virtual(const SnappyParams& S, hipStream_t s, uint64_t* addrs, uint64_t n) {
+  if (n) hipLaunchKernelGGL(k_cz_to_virtual, dim3((unsigned)((n + 255) / 256)), 256, 0, s, S, addrs, n);
+}
 
 hipError_t launch_snappy_decode(const SnappyParams& S, hipStream_t s) {
   if (S.nblk == 0) return hipSuccess;

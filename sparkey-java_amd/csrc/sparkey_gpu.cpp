@@ -25,6 +25,7 @@
 #include "lookup.hpp"
 #include "append.hpp"
 #include "snappy.hpp"
+#include "shard_host.hpp"
 #include "knobs.hpp"
 
 using namespace sk;
@@ -318,6 +319,21 @@ struct sparkey_plan {
   hipStream_t sn_stream = nullptr;  // the decode of one directory chunk overlaps the next chunk
   hipEvent_t sn_ev[2] = {nullptr, nullptr};
   uint64_t c_seg_cls_cnt = 0, c_seg_cls_off = 0;
+  // sharded compressed logs (sk_cz_*): the rank's part of the block directory and its
+  // slice [vbase, vend) of the virtual log, decoded into sn_vlog from global offset vlo
+  struct CzState {
+    LogHdr lh;
+    int codec = 0;
+    int64_t H = 0, A = 0;
+    SnappyParams S;
+    std::vector<int64_t> anchors, ends;
+    std::vector<uint64_t> cnt, usum;
+    int64_t vbase = 0, vlo = 0, vend = 0;
+    uint64_t nblk = 0, ulen = 0;
+    int32_t* flag = nullptr;  // device word: link failures, conversion errors
+    int64_t* d_ends = nullptr;
+    uint64_t *d_cnt = nullptr, *d_usum = nullptr, *d_boff = nullptr, *d_uoff = nullptr;
+  } cz;
   // sharded exact path: the local replay table (the .spi layout with 8-byte addresses), the exact
   // ranges' starts, per-(owner, slab) record counts and their scan
   uint64_t c_xtab = 0, c_ex_starts = 0, c_ex_cnt = 0, c_ex_off = 0;
@@ -756,16 +772,33 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
 // where the candidates agree), then every link of the chain 84 -> anchors -> dataEnd walked from its
 // start at once with k_snappy_dir's checks; a link that does not land on its end, or any check that
 // fails, leaves the directory to the serial chain (*ok = false), which reports errors exactly.
+// The longest hop of the block chain: VLQ + the reader's compressed buffer (Snappy.maxCompressedLength,
+// ZSTD_compressBound); 0 when the parallel directory does not take such blocks (over ~128 KiB: its
+// screen stages a window of H bytes in LDS).
+static int64_t cz_hop_bound(int codec, int64_t mb) {
+  const int64_t H = 5 + (codec == 1 ? mb + (mb >> 8) + (mb < (128 << 10) ? (((128 << 10) - mb) >> 11) : 0)
+                                    : 32 + mb + mb / 6);
+  return mb > 0 && sdir_screen_lds(H) <= 150 * 1024 ? H : 0;
+}
+
+// LDS of the decode kernels (0: global memory)
+static uint32_t cz_decode_lds(bool zstd, int64_t mb) {
+  if (zstd)  // decoded straight into the virtual log (LDS for the entropy tables only: many waves per CU)
+    // measured 3x faster than the block and frame in LDS (one wave per CU); SPARKEY_ZSTD_LDS=1: that
+    return knob_on(Knob::ZstdLds) ? zstd_lds_bytes(mb) : 0u;
+  // SNAPPY: the decoded block, then an 8 KiB window over its stream (k_snappy_lds)
+  const int64_t lds = ((mb + 15) & ~15LL) + 16 + 8192 + 16;
+  return lds <= 160 * 1024 ? (uint32_t)lds : 0u;
+}
+
 static int snappy_par_dir(sparkey_plan* pl, SnappyParams& S, hipStream_t s, int codec, SnappyDirResult* dir, bool* ok,
                           char* err, size_t err_len) {
   *ok = false;
   const int64_t body = S.data_end - kLogHeaderSize;
   if (body <= 0 || S.max_block <= 0) return SPARKEY_OK;
   // the longest hop: VLQ + the reader's compressed buffer (Snappy.maxCompressedLength, ZSTD_compressBound)
-  const int64_t mb = S.max_block;
-  const int64_t H = 5 + (codec == 1 ? mb + (mb >> 8) + (mb < (128 << 10) ? (((128 << 10) - mb) >> 11) : 0)
-                                    : 32 + mb + mb / 6);
-  if (sdir_screen_lds(H) > 150 * 1024) return SPARKEY_OK;   // (blocks over ~128 KiB: the serial chain)
+  const int64_t H = cz_hop_bound(codec, S.max_block);
+  if (!H) return SPARKEY_OK;   // (blocks over ~128 KiB: the serial chain)
   int64_t A = std::max<int64_t>(32 * H, body / (1 << 20) + 1);  // (screen 1/32 of the log; links of ~32 blocks)
   if (knob_set(Knob::SnappyDirA)) A = std::max<int64_t>(H, knob(Knob::SnappyDirA));  // (tests, tuning)
   const uint64_t nwin = body > H ? (uint64_t)((body - H - 1) / A + 1) : 0;
@@ -880,19 +913,13 @@ static int plan_build_snappy(sparkey_plan* pl, const LogHdr& lh, const uint8_t* 
   S.log = d_log;
   S.log_len = (int64_t)log_len;
   S.data_end = lh.data_end;
+  S.win0 = kLogHeaderSize;
   S.max_block = lh.compression_block_size;
   const uint64_t body = (uint64_t)std::max<int64_t>(0, lh.data_end - kLogHeaderSize);
   const bool zstd = lh.compression_type == 2;
   const char* codec = zstd ? "zstd" : "snappy";
   const int64_t mb = lh.compression_block_size;
-  if (zstd) {  // LDS: the decoded block, then the whole frame (k_zstd_decode)
-    // decoded straight into the virtual log (LDS for the entropy tables only: many waves per CU)
-    // measured 3x faster than the block and frame in LDS (one wave per CU); SPARKEY_ZSTD_LDS=1: that
-    S.lds_bytes = knob_on(Knob::ZstdLds) ? zstd_lds_bytes(mb) : 0u;
-  } else {  // LDS: the decoded block, then an 8 KiB window over its stream (k_snappy_lds)
-    const int64_t lds = ((mb + 15) & ~15LL) + 16 + 8192 + 16;
-    S.lds_bytes = lds <= 160 * 1024 ? (uint32_t)lds : 0u;
-  }
+  S.lds_bytes = cz_decode_lds(zstd, mb);
   auto decode_launch = [&](hipStream_t st) { return zstd ? launch_zstd_decode(S, st) : launch_snappy_decode(S, st); };
   // Record offsets per block: maxEntriesPerBlock from the header, bounded by what a block can hold
   // (every record is at least 2 bytes), so a corrupt header cannot size a huge allocation; a block
@@ -1885,6 +1912,10 @@ void shard_slot_split(uint64_t cap, int world, int rank, uint64_t* lo, uint64_t*
   digit_split(cap, nb, bpp, rank, world, &b0, &b1, lo, hi);
 }
 
+static int shard_begin_with(sparkey_plan* pl, const LogHdr& lh, const IndexParams& ip, const LogHdr& hlh,
+                            const IndexParams& hip, const uint8_t* log, uint64_t buf_lo, uint64_t buf_hi,
+                            const sparkey_build_opts* opts, int32_t rank, int32_t world, char* err, size_t err_len);
+
 extern "C" {
 
 int sparkey_shard_begin(sparkey_plan* pl, const uint8_t* log_header, uint64_t file_len, const uint8_t* d_buf,
@@ -1899,27 +1930,43 @@ int sparkey_shard_begin(sparkey_plan* pl, const uint8_t* log_header, uint64_t fi
     set_err(err, err_len, "shard buffer and buf_lo must be 16-byte aligned");
     return SPARKEY_E_ARG;
   }
+  LogHdr lh;
+  IndexParams ip;
+  // (compressed logs: sk_cz_shard_begin takes the sharded path over their virtual log; the Python
+  //  orchestrator gathers them)
+  int rc = parse_log_header(log_header, 84, file_len, &lh, err, err_len, true);
+  if (rc) return rc;
+  rc = make_index_params(lh, *opts, &ip, err, err_len);
+  if (rc) return rc;
+  return shard_begin_with(pl, lh, ip, lh, ip, d_buf - buf_lo, buf_lo, buf_hi, opts, rank, world, err, err_len);
+}
+
+}  // extern "C"
+
+// sparkey_shard_begin's state: framing over `lh` (the log the rank reads at log[p], p in
+// [buf_lo, buf_hi)) with `ip`; the .spi header template from (hlh, hip)
+static int shard_begin_with(sparkey_plan* pl, const LogHdr& lh, const IndexParams& ip, const LogHdr& hlh,
+                            const IndexParams& hip, const uint8_t* log, uint64_t buf_lo, uint64_t buf_hi,
+                            const sparkey_build_opts* opts, int32_t rank, int32_t world, char* err, size_t err_len) {
   ShardState& sh = pl->shard;
   sh.active = false;
-  int rc = parse_log_header(log_header, 84, file_len, &sh.lh, err, err_len, true);  // SNAPPY: gathered (sharded.py)
-  if (rc) return rc;
-  rc = make_index_params(sh.lh, *opts, &sh.ip, err, err_len);
-  if (rc) return rc;
+  sh.lh = lh;
+  sh.ip = ip;
   HIP_TRY(hipSetDevice(pl->device));
   sh.opts = *opts;
   sh.rank = rank;
   sh.world = world;
-  sh.log = d_buf - buf_lo;  // virtual base: global log position p is at log[p] for p in [buf_lo, buf_hi)
+  sh.log = log;  // virtual base: global log position p is at log[p] for p in [buf_lo, buf_hi)
   sh.buf_lo = buf_lo;
   sh.buf_hi = buf_hi;
   sh.n_local = 0;
   sh.n_recv = 0;
-  rc = setup_params(sh.lh, sh.ip, *opts, sh.log, buf_hi, kLogHeaderSize, kLogHeaderSize, &sh.P, err, err_len);
+  int rc = setup_params(sh.lh, sh.ip, *opts, sh.log, buf_hi, kLogHeaderSize, kLogHeaderSize, &sh.P, err, err_len);
   if (rc) return rc;
   sh.P.st = pl->d_status;
   sh.P.sharded = 1;
   shard_range(sh.P, rank, world, &sh.P.b_lo, &sh.P.b_hi, &sh.P.slot_lo, &sh.P.slot_hi);
-  index_header_template(sh.lh, sh.ip, opts->hash_seed, sh.tmpl.b);
+  index_header_template(hlh, hip, opts->hash_seed, sh.tmpl.b);
   sh.local = 0;
   sh.ex_framed = sh.ex_built = false;
   sh.slabs_ok = false;
@@ -1929,6 +1976,8 @@ int sparkey_shard_begin(sparkey_plan* pl, const uint8_t* log_header, uint64_t fi
   sh.active = true;
   return SPARKEY_OK;
 }
+
+extern "C" {
 
 int sparkey_shard_slot_range(const sparkey_plan* pl, int32_t rank, uint64_t* slot_lo, uint64_t* slot_hi) {
   if (!pl || !pl->shard.active || rank < 0 || rank >= pl->shard.world) return SPARKEY_E_ARG;
@@ -2826,7 +2875,8 @@ int sparkey_index_header(const uint8_t* log_header, const sparkey_build_opts* op
                          int64_t total_displacement, uint8_t* out, char* err, size_t err_len) {
   if (!log_header || !opts || !out) return SPARKEY_E_ARG;
   LogHdr lh;
-  int rc = parse_log_header(log_header, 84, (uint64_t)std::max<int64_t>(rd64(log_header + 32), 84), &lh, err, err_len);
+  int rc = parse_log_header(log_header, 84, (uint64_t)std::max<int64_t>(rd64(log_header + 32), 84), &lh, err, err_len,
+                            true);
   if (rc) return rc;
   IndexParams ip;
   rc = make_index_params(lh, *opts, &ip, err, err_len);
@@ -2841,3 +2891,242 @@ int sparkey_index_header(const uint8_t* log_header, const sparkey_build_opts* op
 }
 
 }  // extern "C"
+
+// ================================================================================================
+// Sharded compressed logs (shard_host.cpp Rank::compressed).  Rank g holds the
+// compressed bytes [lo_g, lo_{g+1}) and a tail.  The parallel directory's screen and anchors over its
+// range give its entry e_g (the first anchor; 84 on rank 0); with every rank's entry all-gathered, it
+// follows the chain from e_g through its anchors to e_{g+1}, each link landing exactly on the next
+// anchor (so e_{g+1} is on the chain by induction from 84, as the NONE path's record chain), decodes
+// its blocks into its slice [vbase_g, vbase_{g+1}) of the whole log's virtual log, and the NONE
+// sharded pipeline runs over the slices with the compressed log's index parameters, the entries'
+// virtual offsets rewritten to (blockPosition << entryBlockBits) | entryIndex before the exchange.
+// ================================================================================================
+int64_t sk_cz_hop_bound(const uint8_t* hdr) {
+  const int32_t ct = (int32_t)rd32(hdr + 64);
+  if (ct != 1 && ct != 2) return 0;
+  return cz_hop_bound(ct == 2 ? 1 : 0, (int64_t)(int32_t)rd32(hdr + 68));
+}
+
+int sk_cz_entry(sparkey_plan* pl, const uint8_t* hdr, uint64_t file_len, const uint8_t* d_buf, uint64_t buf_lo,
+                uint64_t buf_hi, int64_t lo, int64_t hi, int32_t rank, hipStream_t s, int64_t* entry, char* err,
+                size_t err_len) {
+  *entry = -1;
+  auto& cz = pl->cz;
+  int rc = parse_log_header(hdr, 84, file_len, &cz.lh, err, err_len, true);
+  if (rc) return rc;
+  cz.anchors.clear();
+  if (cz.lh.compression_type == 0) return SPARKEY_OK;
+  cz.codec = cz.lh.compression_type == 2 ? 1 : 0;
+  cz.H = cz_hop_bound(cz.codec, cz.lh.compression_block_size);
+  if (!cz.H || !d_buf || ((uintptr_t)d_buf & 15) || (buf_lo & 15) || lo < (int64_t)buf_lo) return SPARKEY_OK;
+  HIP_TRY(hipSetDevice(pl->device));
+  const int64_t data_end = std::max<int64_t>(cz.lh.data_end, kLogHeaderSize);
+  cz.A = 32 * cz.H;
+  if (knob_set(Knob::SnappyDirA)) cz.A = std::max<int64_t>(cz.H, knob(Knob::SnappyDirA));  // (tests)
+  memset(&cz.S, 0, sizeof(cz.S));
+  SnappyParams& S = cz.S;
+  S.log = d_buf - buf_lo;  // global offset p at log[p]
+  S.log_len = (int64_t)buf_hi;
+  S.data_end = data_end;
+  S.max_block = cz.lh.compression_block_size;
+  S.win0 = lo;
+  if (rank == 0) *entry = kLogHeaderSize;
+  if (lo >= data_end) {
+    *entry = data_end;
+    return SPARKEY_OK;
+  }
+  const int64_t end = std::min(hi, data_end);
+  const uint64_t nwin = end > lo ? (uint64_t)((end - lo + cz.A - 1) / cz.A) : 0;
+  if (!nwin) return SPARKEY_OK;
+  HIP_TRY(grow(&pl->sn_par, pl->c_sn_par, nwin * (kSdirCand * 8 + 4 + 8) + 64));
+  uint8_t* q = pl->sn_par;
+  int64_t* cand = (int64_t*)q;
+  int32_t* ncand = (int32_t*)(q + ((nwin * kSdirCand * 8 + 15) & ~15ull));
+  int64_t* anchor = (int64_t*)((uint8_t*)ncand + ((nwin * 4 + 15) & ~15ull));
+  launch_sdir_screen(S, s, cz.codec, cz.A, cz.H, nwin, cand, ncand);
+  launch_sdir_anchor(S, s, cz.codec, cz.A, cz.H, nwin, cand, ncand, anchor);
+  HIP_TRY(hipGetLastError());
+  std::vector<int64_t> anc(nwin);
+  HIP_TRY(hipMemcpyAsync(anc.data(), anchor, nwin * 8, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  for (int64_t x : anc)
+    if (x > lo && x <= data_end && (cz.anchors.empty() || x > cz.anchors.back())) cz.anchors.push_back(x);
+  if (rank != 0 && !cz.anchors.empty()) *entry = cz.anchors[0];
+  return SPARKEY_OK;
+}
+
+int sk_cz_count(sparkey_plan* pl, int64_t entry, int64_t next, hipStream_t s, int32_t* ok, uint64_t* nblk,
+                uint64_t* ulen, char* err, size_t err_len) {
+  auto& cz = pl->cz;
+  *ok = 0;
+  *nblk = *ulen = 0;
+  cz.nblk = cz.ulen = 0;
+  cz.ends.clear();
+  if (entry > next || !cz.H) return SPARKEY_OK;
+  if (entry == next) {
+    *ok = 1;
+    return SPARKEY_OK;
+  }
+  cz.ends.push_back(entry);
+  for (int64_t a : cz.anchors)
+    if (a > entry && a < next) cz.ends.push_back(a);
+  cz.ends.push_back(next);
+  const uint64_t nl = cz.ends.size() - 1;
+  HIP_TRY(grow(&pl->sn_par, pl->c_sn_par, (nl + 1) * 8 + 4 * nl * 8 + 256));
+  uint8_t* q = pl->sn_par;
+  auto carve = [&](uint64_t n) { uint8_t* r = q; q += (n + 15) & ~15ull; return r; };
+  cz.d_ends = (int64_t*)carve((nl + 1) * 8);
+  cz.d_cnt = (uint64_t*)carve(nl * 8);
+  cz.d_usum = (uint64_t*)carve(nl * 8);
+  cz.d_boff = (uint64_t*)carve(nl * 8);
+  cz.d_uoff = (uint64_t*)carve(nl * 8);
+  cz.flag = (int32_t*)carve(16);
+  HIP_TRY(hipMemsetAsync(cz.flag, 0, 4, s));
+  HIP_TRY(hipMemcpyAsync(cz.d_ends, cz.ends.data(), (nl + 1) * 8, hipMemcpyHostToDevice, s));
+  launch_sdir_link(cz.S, s, cz.codec, cz.d_ends, nl, 0, cz.d_cnt, cz.d_usum, nullptr, nullptr, cz.flag);
+  HIP_TRY(hipGetLastError());
+  cz.cnt.assign(nl, 0);
+  cz.usum.assign(nl, 0);
+  int32_t f = 0;
+  HIP_TRY(hipMemcpyAsync(cz.cnt.data(), cz.d_cnt, nl * 8, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(cz.usum.data(), cz.d_usum, nl * 8, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(&f, cz.flag, 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  if (f) return SPARKEY_OK;  // a link missed its end (or a block is corrupt): the gathered build says which
+  for (uint64_t i = 0; i < nl; i++) {
+    cz.nblk += cz.cnt[i];
+    cz.ulen += cz.usum[i];
+  }
+  *nblk = cz.nblk;
+  *ulen = cz.ulen;
+  *ok = 1;
+  return SPARKEY_OK;
+}
+
+int sk_cz_decode(sparkey_plan* pl, int64_t vbase, hipStream_t s, int64_t* carry_out, char* err, size_t err_len) {
+  auto& cz = pl->cz;
+  SnappyParams& S = cz.S;
+  *carry_out = -1;
+  const uint64_t nblk = cz.nblk;
+  cz.vbase = vbase;
+  cz.vlo = vbase & ~4095LL;  // (framing chunks start at most 4 KiB before a record)
+  cz.vend = vbase + (int64_t)cz.ulen;
+  const uint64_t front = (uint64_t)(vbase - cz.vlo), body = cz.ulen;
+  HIP_TRY(grow(&pl->sn_vlog, pl->c_sn_vlog, front + body + 4096 + 16));
+  S.vlog = pl->sn_vlog - cz.vlo;
+  S.vlog_len = (int64_t)body;
+  S.nblk = nblk;
+  S.blk_base = 0;
+  S.ebb = calc_entry_block_bits(cz.lh.max_entries_per_block);
+  if (front) HIP_TRY(hipMemsetAsync(pl->sn_vlog, 0, front, s));
+  HIP_TRY(hipMemsetAsync(pl->sn_vlog + front + body, 0, 4096, s));
+  const uint32_t mepb = (uint32_t)std::max<int64_t>(
+      1, std::min<int64_t>(cz.lh.max_entries_per_block, (int64_t)cz.lh.compression_block_size / 2 + 1));
+  S.mepb = mepb;
+  if (nblk) {
+    const uint64_t nl = cz.cnt.size();
+    std::vector<uint64_t> bo(nl), uo(nl);
+    uint64_t nb = 0, tot = 0;
+    for (uint64_t i = 0; i < nl; i++) {
+      bo[i] = nb;
+      uo[i] = (uint64_t)(vbase - kLogHeaderSize) + tot;  // (k_sdir_link: voff = 84 + uoff)
+      nb += cz.cnt[i];
+      tot += cz.usum[i];
+    }
+    HIP_TRY(grow(&pl->sn_blocks, pl->c_sn_blocks, nblk));
+    HIP_TRY(grow(&pl->sn_walk, pl->c_sn_walk, nblk));
+    HIP_TRY(grow(&pl->sn_recoff, pl->c_sn_recoff, nblk * mepb));
+    S.blocks = pl->sn_blocks;
+    S.blk_cap = pl->c_sn_blocks;
+    S.walk = pl->sn_walk;
+    S.rec_off = pl->sn_recoff;
+    HIP_TRY(hipMemcpyAsync(cz.d_boff, bo.data(), nl * 8, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(cz.d_uoff, uo.data(), nl * 8, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemsetAsync(cz.flag, 0, 4, s));
+    launch_sdir_link(S, s, cz.codec, cz.d_ends, nl, 1, cz.d_cnt, cz.d_usum, cz.d_boff, cz.d_uoff, cz.flag);
+    HIP_TRY(hipGetLastError());
+    const bool zstd = cz.codec == 1;
+    S.lds_bytes = cz_decode_lds(zstd, cz.lh.compression_block_size);
+    hipError_t e = zstd ? launch_zstd_decode(S, s) : launch_snappy_decode(S, s);
+    if (e != hipSuccess && S.lds_bytes) {  // the LDS size was refused: decode in global memory
+      (void)hipGetLastError();
+      S.lds_bytes = 0;
+      e = zstd ? launch_zstd_decode(S, s) : launch_snappy_decode(S, s);
+    }
+    HIP_TRY(e);
+    launch_snappy_walk(S, s);
+    HIP_TRY(hipGetLastError());
+  }
+  std::vector<SnappyWalk> walks(nblk);
+  std::vector<SnappyBlock> blocks(nblk);
+  int32_t f = 0;
+  if (nblk) {
+    HIP_TRY(hipMemcpyAsync(walks.data(), pl->sn_walk, nblk * sizeof(SnappyWalk), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(blocks.data(), pl->sn_blocks, nblk * sizeof(SnappyBlock), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(&f, cz.flag, 4, hipMemcpyDeviceToHost, s));
+  }
+  HIP_TRY(hipStreamSynchronize(s));
+  if (f) return SPARKEY_OK;
+  // plan_build_snappy's composition of the block walks; any irregular block: the gathered build
+  int64_t carry = 0;
+  for (uint64_t b = 0; b < nblk; b++) {
+    const SnappyWalk& w = walks[b];
+    if (w.flags & kWalkBadStream) return SPARKEY_OK;
+    if (carry == 0) {
+      if (w.flags) return SPARKEY_OK;
+      carry = w.overflow;
+    } else if (carry >= (int64_t)blocks[b].ulen) {
+      carry -= blocks[b].ulen;
+    } else {
+      return SPARKEY_OK;
+    }
+  }
+  *carry_out = carry;
+  return SPARKEY_OK;
+}
+
+int sk_cz_shard_begin(sparkey_plan* pl, const uint8_t* hdr, uint64_t file_len, uint64_t vlen,
+                      const sparkey_build_opts* opts, int32_t rank, int32_t world, char* err, size_t err_len) {
+  auto& cz = pl->cz;
+  LogHdr lh;
+  int rc = parse_log_header(hdr, 84, file_len, &lh, err, err_len, true);
+  if (rc) return rc;
+  IndexParams ip;
+  rc = make_index_params(lh, *opts, &ip, err, err_len);
+  if (rc) return rc;
+  uint8_t vh[kLogHeaderSize];  // the virtual log's header, as plan_build_snappy writes it
+  memcpy(vh, hdr, kLogHeaderSize);
+  wr64(vh + 32, vlen);
+  wr32(vh + 64, 0u);
+  wr32(vh + 80, 1u);
+  LogHdr vlh;
+  rc = parse_log_header(vh, kLogHeaderSize, vlen, &vlh, err, err_len);
+  if (rc) return rc;
+  IndexParams fip = ip;  // the compressed log's table; entries framed with virtual offsets (ebb 0)
+  fip.ebb = 0;
+  return shard_begin_with(pl, vlh, fip, lh, ip, cz.S.vlog, (uint64_t)cz.vlo, (uint64_t)cz.vend, opts, rank, world, err,
+                          err_len);
+}
+
+int sk_cz_to_real(sparkey_plan* pl, uint8_t* d_entries, uint64_t n, hipStream_t s, char* err, size_t err_len) {
+  auto& cz = pl->cz;
+  if (!n) return SPARKEY_OK;
+  HIP_TRY(hipMemsetAsync(cz.flag, 0, 4, s));
+  launch_cz_to_real(cz.S, s, (uint64_t*)d_entries, n, cz.flag);
+  HIP_TRY(hipGetLastError());
+  int32_t f = 0;
+  HIP_TRY(hipMemcpyAsync(&f, cz.flag, 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  if (f) {
+    set_err(err, err_len, "internal error: a framed entry is not a record start of its block");
+    return SPARKEY_E_CORRUPT_LOG;
+  }
+  return SPARKEY_OK;
+}
+
+int sk_cz_to_virtual(sparkey_plan* pl, uint64_t* d_addrs, uint64_t n, hipStream_t s, char* err, size_t err_len) {
+  launch_cz_to_virtual(pl->cz.S, s, d_addrs, n);
+  HIP_TRY(hipGetLastError());
+  return SPARKEY_OK;
+}
