@@ -632,7 +632,10 @@ def sharded(args, dev, world, rank):
     gen_s = time.time() - t0
     # (the plan's workspace for twice the rank's records, so that no timed build grows it; the one-GPU
     #  rehearsal of N ranks reserves for the records alone -- N ranks of C4's 125M fit 288 GB only so)
-    plan = _native.Plan(dev.index, (118 * args.entries + 65536 * 4) if compressed else hi - lo,
+    # (the one-GPU rehearsal reserves no per-byte framing workspace either: the uniform framing writes
+    #  digit regions, and the warm-up build grows what a rank needs)
+    plan_bytes = (118 * args.entries + 65536 * 4) if compressed else hi - lo
+    plan = _native.Plan(dev.index, 0 if args.backend == "gloo" else plan_bytes,
                         (1 if args.backend == "gloo" else 2) * args.entries)
     stream = torch.cuda.Stream(dev)
     phases = {}
@@ -694,6 +697,10 @@ def sharded(args, dev, world, rank):
         pieces = [None] * world
         dist.all_gather_object(pieces, mine)
         plan.close()
+        if args.orchestrator == "cpp":  # (every rank's buffers go before rank 0's whole-log build)
+            comm.close()
+            del d_out
+        torch.cuda.empty_cache()
         if shared_gpu or rank == 0:
             del buf
             torch.cuda.empty_cache()
