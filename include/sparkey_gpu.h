@@ -85,9 +85,8 @@ typedef struct sparkey_build_stats {
                                  uniform framing wrote the per-digit regions itself; 0 when it wrote
                                  every entry straight into its placement bucket */
   int32_t sharded;            /* multi-GPU builds: 1 sharded canonical placement (SNAPPY / ZSTD logs too: each
-                                 rank decodes its own blocks), 2 sharded exact path, 3 the log gathered on every
-                                 rank and built whole (full tables, compressed logs with DELETEs or duplicate
-                                 keys); else 0 */
+                                 rank decodes its own blocks), 2 sharded exact path (DELETEs, overwrites), 3 the
+                                 log gathered on every rank and built whole (full tables); else 0 */
   double device_ms;           /* device time of the build (HIP events), excluding copies; sharded: the rank's
                                  wall time of sparkey_shard_build */
 } sparkey_build_stats;

@@ -13,8 +13,8 @@
 //                 rank 0 writes the 112-byte header.
 // Logs with DELETEs or duplicate keys take the sharded exact path.  Compressed logs
 //  are framed as their virtual log: each rank decodes the blocks of its own byte range
-// into its slice of it (Rank::compressed).  Compressed logs with DELETEs or duplicate keys, and tables
-// the PUT records fill, gather the log on every rank and build it whole (correct, not scaled).
+// into its slice of it (Rank::compressed).  Tables the PUT records fill gather the log on every rank
+// and build it whole (correct, not scaled).
 //
 // One rank is one sparkey_shard_build call on its own thread / process and device.  The collectives go
 // through Coll: RCCL (ncclAllGather, grouped ncclSend/ncclRecv; xGMI between the GPUs of a node), or
@@ -751,6 +751,9 @@ int Rank::exact(uint8_t* out, uint64_t hdr_off, int64_t n_records, const sparkey
   uint8_t* send = cm_->exsend.ensure(std::max<uint64_t>(1, n_send) * rs);
   if (!send) return fail(SPARKEY_E_GPU, "hipMalloc failed");
   rc = sparkey_shard_exact_pack(pl_, send, cm_->exsend.cap, s_, err_, err_len_);
+  // a compressed log framed as its virtual log: the records' addresses to the compressed log's (the
+  // replay orders by receive-buffer offset; the address field is what the extract writes)
+  if (!rc && virt_) rc = sk_cz_to_real(pl_, send, n_send, (uint32_t)rs, s_, err_, err_len_);
   if (rc) return rc;
   std::vector<int64_t> M;
   rc = gather_i64(std::vector<int64_t>(counts.begin(), counts.end()), &M);
@@ -916,12 +919,13 @@ int Rank::gathered(const uint8_t* hdr, uint64_t file_len, const uint8_t* d_buf, 
 // range (sk_cz_entry), follows it to the next rank's entry (sk_cz_count: induction from 84 as for the
 // record chain) and decodes it into its slice of the virtual log (sk_cz_decode); the slices' starts
 // become the ranks' entries and the NONE steps run over them.  *take = false (every rank alike): the
-// gathered build, for logs these steps do not take (DELETEs, a record spanning two ranks' blocks, a
-// link that misses, an irregular block -- the gathered build reports a corrupt log's error).
+// gathered build, for logs these steps do not take (a record spanning two ranks' blocks, a link that
+// misses, an irregular block -- the gathered build reports a corrupt log's error).  DELETEs and
+// overwrites take the sharded exact path over the slices.
 int Rank::compressed(const uint8_t* hdr, uint64_t file_len, const uint8_t* d_buf, uint64_t buf_lo, uint64_t buf_hi,
                      const sparkey_build_opts& o, std::vector<int64_t>* cs, int64_t* vlen_out, bool* take) {
   *take = false;
-  if (G_ == 1 || L_.small || !L_.cz_h || L_.num_deletes > 0 || sk::knob_on(sk::Knob::ShardGatherCompressed))
+  if (G_ == 1 || L_.small || !L_.cz_h || sk::knob_on(sk::Knob::ShardGatherCompressed))
     return SPARKEY_OK;
   auto together = [&](const std::vector<int64_t>& rows, int stride, int own) {
     std::vector<int64_t> codes(G_);
@@ -1206,7 +1210,7 @@ int Rank::run(const uint8_t* hdr, uint64_t file_len, const uint8_t* d_buf, uint6
   if (have && virt_) {
     uint64_t n_send = 0;
     for (int r = 0; r < G_; r++) n_send += (uint64_t)R[(size_t)g_ * RL + 8 + r];
-    cz_rc = sk_cz_to_real(pl_, send, n_send, s_, err_, err_len_);
+    cz_rc = sk_cz_to_real(pl_, send, n_send, kEntryBytes, s_, err_, err_len_);
   }
   rc = agree(have ? cz_rc : fail(SPARKEY_E_GPU, "hipMalloc failed"));
   if (rc) return rc;
@@ -1303,7 +1307,6 @@ int Rank::run(const uint8_t* hdr, uint64_t file_len, const uint8_t* d_buf, uint6
   }
   mark("spill");
   if (is_exact) {  // the ring splits at the slots the PUT placement left empty (now complete on every rank)
-    if (virt_) return gathered(hdr, file_len, d_buf, buf_lo, o, d_out, slot_lo, out_len, st);
     bool done = false;
     rc = exact(d_out, hdr_off, R[(size_t)g_ * RL + 3], o, slot_lo, slot_hi, &done, st);
     if (rc) return rc;

@@ -49,7 +49,8 @@ void sk_plan_set_shared_device(sparkey_plan* plan, bool shared);
 
 // Sharded compressed logs (sparkey_gpu.cpp).  0 or a SPARKEY_E_* code; a log these
 // steps do not take (a missed link, a record spanning two ranks' blocks, an irregular block) is
-// reported through *ok / *carry / *entry and built by the gathered path instead.
+// reported through *ok / *carry / *entry and built by the gathered path instead (DELETEs and
+// overwrites take the sharded exact path, with the exchange records' addresses rewritten too).
 // the hop bound H of the block chain (0: a NONE log, or blocks the parallel directory does not take)
 int64_t sk_cz_hop_bound(const uint8_t* log_header);
 // screen and anchors of [lo, hi) from the rank's compressed bytes [buf_lo, buf_hi); *entry: its first
@@ -66,7 +67,9 @@ int sk_cz_decode(sparkey_plan* pl, int64_t vbase, hipStream_t s, int64_t* carry,
 // sparkey_shard_begin over the slice (the virtual log is vlen bytes long), the table of the compressed log
 int sk_cz_shard_begin(sparkey_plan* pl, const uint8_t* log_header, uint64_t file_len, uint64_t vlen,
                       const sparkey_build_opts* opts, int32_t rank, int32_t world, char* err, size_t err_len);
-// n 16-byte (hash, address) entries: virtual offsets -> (blockPosition << entryBlockBits) | entryIndex
-int sk_cz_to_real(sparkey_plan* pl, uint8_t* d_entries, uint64_t n, hipStream_t s, char* err, size_t err_len);
+// n records of rec_bytes (16: (hash, address) entries; the exact path's exchange records), address in
+// their second 8-byte word: virtual offsets -> (blockPosition << entryBlockBits) | entryIndex
+int sk_cz_to_real(sparkey_plan* pl, uint8_t* d_records, uint64_t n, uint32_t rec_bytes, hipStream_t s, char* err,
+                  size_t err_len);
 // n compressed-log addresses of this rank's blocks -> virtual offsets (sparkey_shard_fetch_keys)
 int sk_cz_to_virtual(sparkey_plan* pl, uint64_t* d_addrs, uint64_t n, hipStream_t s, char* err, size_t err_len);

@@ -97,11 +97,13 @@ hipError_t launch_snappy_decode(const SnappyParams& S, hipStream_t s);
 void launch_snappy_walk(const SnappyParams& S, hipStream_t s);
 void launch_snappy_rewrite(const SnappyParams& S, hipStream_t s);
 // sharded compressed logs: a rank's blocks [0, nblk) with virtual offsets from
-// blocks[0].voff.  to_real: the address field (second word) of n 16-byte (hash, address) entries, a
-// virtual offset, becomes (blockPosition << ebb) | entryIndex; *err |= 1 when it is not a record start.
+// blocks[0].voff.  to_real: the address field (second word) of n records of stride_words 8-byte
+// words ((hash, address) entries, or the exact path's exchange records), a virtual offset, becomes
+// (blockPosition << ebb) | entryIndex, a DELETE mark kept; *err |= 1 when it is not a record start.
 // to_virtual: n such compressed-log addresses back to virtual offsets (an address of no block here:
 // all ones, which no rank decodes).
-void launch_cz_to_real(const SnappyParams& S, hipStream_t s, uint64_t* entries, uint64_t n, int32_t* err);
+void launch_cz_to_real(const SnappyParams& S, hipStream_t s, uint64_t* records, uint64_t n, uint32_t stride_words,
+                       int32_t* err);
 void launch_cz_to_virtual(const SnappyParams& S, hipStream_t s, uint64_t* addrs, uint64_t n);
 
 }  // namespace sk

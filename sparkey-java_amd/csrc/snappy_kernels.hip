@@ -596,10 +596,13 @@ __global__ void __launch_bounds__(256) k_snappy_rewrite(SnappyParams S) {
 
 // Sharded compressed logs: one rank's blocks [0, nblk), their virtual offsets
 // ascending from blocks[0].voff over S.vlog_len decoded bytes, searched as k_snappy_rewrite does.
-__global__ void __launch_bounds__(256) k_cz_to_real(SnappyParams S, uint64_t* e, uint64_t n, int32_t* err) {
+__global__ void __launch_bounds__(256) k_cz_to_real(SnappyParams S, uint64_t* e, uint64_t n, uint32_t stride,
+                                                    int32_t* err) {
   const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
-  const uint64_t a = e[2 * i + 1];
+  uint64_t* ap = e + (uint64_t)i * stride + 1;  // (the address word of a record: its second)
+  const uint64_t del = *ap & (1ull << 63);       // (a DELETE record's mark stays)
+  const uint64_t a = *ap & ~(1ull << 63);
   const int64_t nb = (int64_t)S.nblk;
   const uint64_t v0 = nb ? (uint64_t)S.blocks[0].voff : 0;
   const uint64_t span = S.vlog_len > 0 ? (uint64_t)S.vlog_len : 1;
@@ -623,7 +626,7 @@ __global__ void __launch_bounds__(256) k_cz_to_real(SnappyParams S, uint64_t* e,
     atomicOr(err, 1);
     return;
   }
-  e[2 * i + 1] = ((uint64_t)B.file_pos << S.ebb) | l;
+  *ap = del | ((uint64_t)B.file_pos << S.ebb) | l;
 }
 
 __global__ void __launch_bounds__(256) k_cz_to_virtual(SnappyParams S, uint64_t* addrs, uint64_t n) {
@@ -960,8 +963,9 @@ void launch_sdir_link(const SnappyParams& S, hipStream_t s, int codec, const int
 
 void launch_snappy_dir(const SnappyParams& S, hipStream_t s) { hipLaunchKernelGGL(k_snappy_dir, 1, 64, 0, s, S); }
 
-void launch_cz_to_real(const SnappyParams& S, hipStream_t s, uint64_t* entries, uint64_t n, int32_t* err) {
-  if (n) hipLaunchKernelGGL(k_cz_to_real, dim3((unsigned)((n + 255) / 256)), 256, 0, s, S, entries, n, err);
+void launch_cz_to_real(const SnappyParams& S, hipStream_t s, uint64_t* records, uint64_t n, uint32_t stride_words,
+                       int32_t* err) {
+  if (n) hipLaunchKernelGGL(k_cz_to_real, dim3((unsigned)((n + 255) / 256)), 256, 0, s, S, records, n, stride_words, err);
 }
 void launch_cz_to_virtual(const SnappyParams& S, hipStream_t s, uint64_t* addrs, uint64_t n) {
   if (n) hipLaunchKernelGGL(k_cz_to_virtual, dim3((unsigned)((n + 255) / 256)), 256, 0, s, S, addrs, n);

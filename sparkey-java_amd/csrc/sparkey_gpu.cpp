@@ -3109,11 +3109,16 @@ int sk_cz_shard_begin(sparkey_plan* pl, const uint8_t* hdr, uint64_t file_len, u
                           err_len);
 }
 
-int sk_cz_to_real(sparkey_plan* pl, uint8_t* d_entries, uint64_t n, hipStream_t s, char* err, size_t err_len) {
+int sk_cz_to_real(sparkey_plan* pl, uint8_t* d_records, uint64_t n, uint32_t rec_bytes, hipStream_t s, char* err,
+                  size_t err_len) {
   auto& cz = pl->cz;
   if (!n) return SPARKEY_OK;
+  if (rec_bytes < 16 || (rec_bytes & 7)) {
+    set_err(err, err_len, "bad record size");
+    return SPARKEY_E_ARG;
+  }
   HIP_TRY(hipMemsetAsync(cz.flag, 0, 4, s));
-  launch_cz_to_real(cz.S, s, (uint64_t*)d_entries, n, cz.flag);
+  launch_cz_to_real(cz.S, s, (uint64_t*)d_records, n, rec_bytes / 8, cz.flag);
   HIP_TRY(hipGetLastError());
   int32_t f = 0;
   HIP_TRY(hipMemcpyAsync(&f, cz.flag, 4, hipMemcpyDeviceToHost, s));

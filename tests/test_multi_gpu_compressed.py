@@ -3,8 +3,9 @@
 byte range of the compressed log, checks its links up to the next rank's entry (induction from 84)
 and decodes its blocks into its slice of the virtual log; the NONE steps run over the slices with
 the compressed log's addresses ((blockPosition << entryBlockBits) | entryIndex, IndexHash.java:270-283).
-Every .spi must equal the oracle's byte for byte; stats.sharded says which path ran (1 sharded, 3 the
-log gathered on every rank: DELETEs, a record spanning two ranks' blocks, the switch)."""
+Every .spi must equal the oracle's byte for byte; stats.sharded says which path ran (1 sharded, 2 the
+sharded exact path for DELETEs and overwrites, 3 the log gathered on every rank: a record spanning two
+ranks' blocks, the switch)."""
 import random
 import struct
 
@@ -81,10 +82,34 @@ def test_write_hash_benchmark_shape(native):
     check(native, cl.finish(), 3, seed=1234, sharded=1)
 
 
-def test_deletes_are_gathered(native):
-    rng = random.Random(5)
-    log = _compressed(_ops(rng, 6000, 1500, 0.2, 120), 1024)
-    check(native, log, 2, seed=4, sharded=3)
+@pytest.mark.parametrize("method", [IN_MEMORY, SORTING])
+@pytest.mark.parametrize("n", [2, 3])
+def test_deletes_and_overwrites_exact(native, method, n):
+    """DELETEs and overwrites: the sharded exact path over the ranks' slices, the
+    exchange records' addresses rewritten to the compressed log's."""
+    rng = random.Random(5 + n)
+    log = _compressed(_ops(rng, 8000, 1500, 0.2, 120), 1024)
+    check(native, log, n, seed=4, method=method, sharded=2)
+
+
+@pytest.mark.parametrize("codec", ["snappy", "zstd"])
+def test_churn_shape_exact(native, codec):
+    """C2-shaped records drawn from a key pool with 10% DELETEs (bench.py's churn), in 4 KiB blocks."""
+    from sparkey import synth
+    from snappy_log import CompressedLog
+    import numpy as np
+    log = synth.churn_log(20000, 15000, 0.1, seed=4).tobytes()
+    cl = CompressedLog(4096, file_identifier=9, codec=codec)
+    p, end = 84, struct.unpack_from("<q", log, 32)[0]
+    while p < end:
+        a, b = log[p], log[p + 1]
+        if a == 0:
+            cl.delete(log[p + 2:p + 2 + b])
+            p += 2 + b
+        else:
+            cl.put(log[p + 2:p + 1 + a], log[p + 1 + a:p + 1 + a + b])
+            p += 1 + a + b
+    check(native, cl.finish(), 4, seed=5, sharded=2)
 
 
 def test_gather_switch(native, switch):
