@@ -127,6 +127,65 @@ __device__ inline uint64_t murmur64_ld(const Ld& ld, int32_t len, uint32_t seed)
   return h1;
 }
 
+// The same two hashes for a key length every lane of the wave shares (k_frame_uniform: every record
+// has the header's maxKeyLen): the block loop and the tail are scalar branches, so a key without a
+// tail (C2's 16 bytes) reads and mixes none.
+template <class Ld>
+__device__ inline uint64_t murmur64_uni(const Ld& ld, int32_t len, uint32_t seed) {
+  const uint64_t c1 = 0x87c37b91114253d5ull, c2 = 0x4cf5ad432745937full;
+  uint64_t h1 = (uint64_t)seed, h2 = h1;
+  const int32_t nblocks = len >> 4;
+  for (int32_t i = 0; i < nblocks; i++) {
+    uint64_t k1 = ld.u64(16 * i);
+    uint64_t k2 = ld.u64(16 * i + 8);
+    k1 *= c1; k1 = rotl64(k1, 31); k1 *= c2; h1 ^= k1;
+    h1 = rotl64(h1, 27); h1 += h2; h1 = h1 * 5 + 0x52dce729ull;
+    k2 *= c2; k2 = rotl64(k2, 33); k2 *= c1; h2 ^= k2;
+    h2 = rotl64(h2, 31); h2 += h1; h2 = h2 * 5 + 0x38495ab5ull;
+  }
+  const int32_t rem = len & 15;
+  if (rem) {
+    const int t = 16 * nblocks;
+    if (rem > 8) {
+      uint64_t k2 = ld.u64(t + 8) & ((1ull << (8 * (rem - 8))) - 1ull);
+      k2 *= c2; k2 = rotl64(k2, 33); k2 *= c1; h2 ^= k2;
+    }
+    uint64_t k1 = ld.u64(t) & (rem >= 8 ? ~0ull : (1ull << (8 * rem)) - 1ull);
+    k1 *= c1; k1 = rotl64(k1, 31); k1 *= c2; h1 ^= k1;
+  }
+  h1 ^= (uint64_t)(int64_t)len;
+  h2 ^= (uint64_t)(int64_t)len;
+  h1 += h2; h2 += h1;
+  h1 = fmix64(h1); h2 = fmix64(h2);
+  h1 += h2;
+  return h1;
+}
+template <class Ld>
+__device__ inline uint32_t murmur32_uni(const Ld& ld, int32_t len, uint32_t seed) {
+  const uint32_t c1 = 0xcc9e2d51u, c2 = 0x1b873593u;
+  uint32_t h1 = seed;
+  const int32_t nblocks = len >> 2;
+  auto block = [&](uint32_t k1) {
+    k1 *= c1; k1 = rotl32(k1, 15); k1 *= c2;
+    h1 ^= k1; h1 = rotl32(h1, 13); h1 = h1 * 5 + 0xe6546b64u;
+  };
+  int32_t i = 0;
+  for (; i + 1 < nblocks; i += 2) {
+    const uint64_t x = ld.u64(4 * i);
+    block((uint32_t)x);
+    block((uint32_t)(x >> 32));
+  }
+  if (i < nblocks) block((uint32_t)ld.u64(4 * i));
+  const int32_t rem = len & 3;
+  if (rem) {
+    uint32_t k1 = (uint32_t)ld.u64(4 * nblocks) & ((1u << (8 * rem)) - 1u);
+    k1 *= c1; k1 = rotl32(k1, 15); k1 *= c2; h1 ^= k1;
+  }
+  h1 ^= (uint32_t)len;
+  h1 ^= h1 >> 16; h1 *= 0x85ebca6bu; h1 ^= h1 >> 13; h1 *= 0xc2b2ae35u; h1 ^= h1 >> 16;
+  return h1;
+}
+
 // ------------------------------------------------------------------------------------------------
 // granules (8-byte {state, value} words) -- relaxed agent-scope atomics, zeroed before the launch
 // ------------------------------------------------------------------------------------------------

@@ -767,9 +767,11 @@ __global__ __launch_bounds__(64 * W) void k_frame_uniform(BuildParams P) {
       if ((x & 0x8080ull) != 0 || klen != (int32_t)P.max_key_len || vlen != (int32_t)P.max_value_len) {
         atomicOr(&P.st->spec_fail, 4u);  // not the uniform log the header describes
       } else {
+        // (klen is the header's maxKeyLen on every lane: the hash's loop and tail are scalar)
+        const int32_t ukl = (int32_t)P.max_key_len;
         const RgnKey ld{buf, off + 2u};
-        const uint64_t hash = P.hash_size == 8 ? murmur64_ld(ld, klen, (uint32_t)P.seed)
-                                               : (uint64_t)murmur32_ld(ld, klen, (uint32_t)P.seed);
+        const uint64_t hash = P.hash_size == 8 ? murmur64_uni(ld, ukl, (uint32_t)P.seed)
+                                               : (uint64_t)murmur32_uni(ld, ukl, (uint32_t)P.seed);
         hsh[r] = hash;
         if (!to_regions) {
           Entry en;
