@@ -30,6 +30,7 @@
 #include "scan.hpp"
 #include "place_common.hpp"
 #include "frame_common.hpp"
+#include "knobs.hpp"
 
 namespace sk {
 
@@ -680,10 +681,19 @@ __device__ __forceinline__ void wait_vmcnt_le(int n) {
 #undef SK_VM
 }
 
+// A workgroup barrier for LDS traffic only: LDS operations complete, global ones may stay in flight
+// (__syncthreads waits for every outstanding load and store first)
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0); vmcnt, expcnt at their maxima
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // W waves per workgroup; DB: each wave double-buffers its staging, the next round's LDS-DMA in flight
 // while it hashes the current one (the only global loads of the rounds, so vmcnt counts just them).
 template <int W, bool DB>
 __global__ __launch_bounds__(64 * W) void k_frame_uniform(BuildParams P) {
+  static_assert(W >= 4, "the write-out's digit steps take one thread per digit (256)");
   // A workgroup frames kSub partition tiles (kSub * kPartTile records), kRounds rounds of 64 records
   // per wave, each wave staging its own records by LDS-DMA.
   constexpr int kSub = 1;  // (2 or 4 -- longer runs per region -- measured slower: registers/scratch)
@@ -805,55 +815,49 @@ __global__ __launch_bounds__(64 * W) void k_frame_uniform(BuildParams P) {
   uint8_t* sdig = lds + kPartTile * sizeof(Entry);                    // digit of each staged entry
   uint32_t* lbase = reinterpret_cast<uint32_t*>(sdig + kPartTile);   // tile-local run starts
   __shared__ uint32_t wsum[4];
-  if (threadIdx.x < 256) {
-    const int d = threadIdx.x;
-    uint32_t c = 0;
+  static_assert(kSub == 1, "one tile a workgroup");
+  // The digit runs' cursors: each returning atomic goes out first, and its round trip overlaps the
+  // tile's scan and regroup (the write-out is the first to need rbase).
+  uint32_t c = 0, incl = 0, b0 = 0;
+  if (threadIdx.x < 256) {  // waves 0-3: the cursor, and the exclusive scan of the tile's 256 digit counts
+    c = hist[threadIdx.x];
+    b0 = c ? atomicAdd(&P.p1_fill[threadIdx.x], c) : 0u;
+    incl = c;
 #pragma unroll
-    for (int t = 0; t < kSub; t++) c += hist[t * 256 + d];
-    const uint32_t b0 = c ? atomicAdd(&P.p1_fill[d], c) : 0u;
-    if ((uint64_t)b0 + c > P.p1_region) atomicOr(&P.st->spec_fail, kSpecRegionFull);
-    rbase[d] = b0;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t v = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += v;
+    }
+    if (lane == 63) wsum[wave] = incl;
   }
+  lds_barrier();
+  if (threadIdx.x < 256) {
+    uint32_t off = 0;
+    for (int w = 0; w < wave; w++) off += wsum[w];
+    lbase[threadIdx.x] = off + incl - c;
+  }
+  lds_barrier();
 #pragma unroll
-  for (int t = 0; t < kSub; t++) {
-    uint32_t c = 0, incl = 0;
-    __syncthreads();  // (rbase; the previous tile's write-out is done with stage and rbase)
-    if (t > 0 && threadIdx.x < 256) rbase[threadIdx.x] += hist[(t - 1) * 256 + threadIdx.x];  // this tile's sub-run
-    if (threadIdx.x < 256) {  // waves 0-3: exclusive scan of the tile's 256 digit counts
-      c = hist[t * 256 + threadIdx.x];
-      incl = c;
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t v = __shfl_up(incl, o, 64);
-        if (lane >= o) incl += v;
-      }
-      if (lane == 63) wsum[wave] = incl;
-    }
-    __syncthreads();
-    if (threadIdx.x < 256) {
-      uint32_t off = 0;
-      for (int w = 0; w < wave; w++) off += wsum[w];
-      lbase[threadIdx.x] = off + incl - c;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int r = t * kTileRounds; r < (t + 1) * kTileRounds; r++) {
-      if (dr[r] == ~0u) continue;
-      const uint32_t d = dr[r] >> 16;
-      const uint32_t i = lbase[d] + (dr[r] & 0xffffu);
-      Entry en;
-      en.hash = hsh[r];
-      en.addr = (uint64_t)(P.fr_entry + (int64_t)(blk0 + (uint64_t)(r * W + wave) * 64 + lane) * R) << P.ebb;
-      stage[i] = en;
-      sdig[i] = (uint8_t)d;
-    }
-    __syncthreads();
-    const uint32_t ntile = wsum[0] + wsum[1] + wsum[2] + wsum[3];
-    for (uint32_t i = threadIdx.x; i < ntile; i += 64 * W) {
-      const uint32_t d = sdig[i];
-      const uint64_t pos = (uint64_t)rbase[d] + (i - lbase[d]);
-      if (pos < P.p1_region) P.ent3[(uint64_t)d * P.p1_region + pos] = stage[i];
-    }
+  for (int r = 0; r < kRounds; r++) {
+    if (dr[r] == ~0u) continue;
+    const uint32_t d = dr[r] >> 16;
+    const uint32_t i = lbase[d] + (dr[r] & 0xffffu);
+    Entry en;
+    en.hash = hsh[r];
+    en.addr = (uint64_t)(P.fr_entry + (int64_t)(blk0 + (uint64_t)(r * W + wave) * 64 + lane) * R) << P.ebb;
+    stage[i] = en;
+    sdig[i] = (uint8_t)d;
+  }
+  if (threadIdx.x < 256) {
+    if ((uint64_t)b0 + c > P.p1_region) atomicOr(&P.st->spec_fail, kSpecRegionFull);
+    rbase[threadIdx.x] = b0;
+  }
+  __syncthreads();
+  const uint32_t ntile = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+  for (uint32_t i = threadIdx.x; i < ntile; i += 64 * W) {
+    const uint32_t d = sdig[i];
+    const uint64_t pos = (uint64_t)rbase[d] + (i - lbase[d]);
+    if (pos < P.p1_region) P.ent3[(uint64_t)d * P.p1_region + pos] = stage[i];
   }
 }
 
@@ -2323,17 +2327,14 @@ void launch_frame_uniform(const BuildParams& P, hipStream_t s, StageTimer* tm) {
   // 4 waves per workgroup, double-buffered: two workgroups per CU, each wave's next DMA in flight while
   // it hashes (single-buffered 16- and 8-wave workgroups, one per CU, measured slower)
   constexpr int W = 4;
-  constexpr bool db = true;
   Q.uni_wbytes = (uint32_t)((64 * P.uni_rec + 32 + 1023) & ~1023ll);
   Q.uni_nt = 1u;  // (the log is read once: non-temporal staging measured 10% faster)
-  const uint64_t per = kPartTile;  // records per workgroup
-  const uint64_t nblk = (P.uni_n + per - 1) / per;
+  const uint64_t nblk = (P.uni_n + kPartTile - 1) / kPartTile;  // a partition tile a workgroup
   // the wave buffers, then the tile regrouped by digit in the same space (entries, digits, run
-  // starts), and hist + rbase after either
-  const size_t body = std::max<size_t>((size_t)W * Q.uni_wbytes * (db ? 2 : 1), (size_t)kPartTile * (sizeof(Entry) + 1) + 1024);
-  const size_t lds = body + 2048;
+  // starts), and hist + rbase after either (tiles of 2048 records measured slower: profiles/r05/c2/)
+  const size_t body = std::max<size_t>((size_t)W * Q.uni_wbytes * 2, (size_t)kPartTile * (sizeof(Entry) + 1) + 1024);
   Q.uni_hist_off = (uint32_t)body;
-  hipLaunchKernelGGL((k_frame_uniform<W, db>), dim3((unsigned)nblk), dim3(64 * W), lds, s, Q);
+  hipLaunchKernelGGL((k_frame_uniform<W, true>), dim3((unsigned)nblk), dim3(64 * W), body + 2048, s, Q);
   tm->mark("frame", s);
 }
 
