@@ -708,6 +708,14 @@ __global__ __launch_bounds__(64 * W) void k_frame_uniform(BuildParams P) {
   // else with p1_hist_ready each tile's digit counts are k_part1_hist's output
   const bool to_regions = P.p1_region != 0;
   const bool with_hist = to_regions || P.p1_hist_ready != 0;
+  long long t_prev = P.dbg ? clock64() : 0;
+  auto mark = [&](int i) {  // (frame_debug: thread 0's cycles per phase of the workgroup)
+    if (P.dbg && threadIdx.x == 0) {
+      const long long now = clock64();
+      P.dbg[(uint64_t)blockIdx.x * 16 + i] = (unsigned long long)(now - t_prev);
+      t_prev = now;
+    }
+  };
 
   if (with_hist) {
     for (int t = threadIdx.x; t < kSub * 256; t += 64 * W) hist[t] = 0;
@@ -800,6 +808,7 @@ __global__ __launch_bounds__(64 * W) void k_frame_uniform(BuildParams P) {
   }
   if (!with_hist) return;
   __syncthreads();
+  mark(0);
   if (!to_regions) {  // k_part1_hist's output for these tiles
     for (int t = threadIdx.x; t < kSub * 256; t += 64 * W) {
       const uint64_t tile = (uint64_t)blockIdx.x * kSub + (t >> 8);
@@ -837,6 +846,7 @@ __global__ __launch_bounds__(64 * W) void k_frame_uniform(BuildParams P) {
     lbase[threadIdx.x] = off + incl - c;
   }
   lds_barrier();
+  mark(1);
 #pragma unroll
   for (int r = 0; r < kRounds; r++) {
     if (dr[r] == ~0u) continue;
@@ -853,11 +863,17 @@ __global__ __launch_bounds__(64 * W) void k_frame_uniform(BuildParams P) {
     rbase[threadIdx.x] = b0;
   }
   __syncthreads();
+  mark(2);
   const uint32_t ntile = wsum[0] + wsum[1] + wsum[2] + wsum[3];
   for (uint32_t i = threadIdx.x; i < ntile; i += 64 * W) {
     const uint32_t d = sdig[i];
     const uint64_t pos = (uint64_t)rbase[d] + (i - lbase[d]);
     if (pos < P.p1_region) P.ent3[(uint64_t)d * P.p1_region + pos] = stage[i];
+  }
+  if (P.dbg) {  // (the write-out to completion)
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    mark(3);
   }
 }
 

@@ -723,6 +723,17 @@ static int launch_framing(sparkey_plan* pl, const BuildParams& P, int framing_pa
 }
 
 static void print_frame_debug(sparkey_plan* pl, const BuildParams& P) {
+  if (P.dbg && P.uni_n && P.p1_region) {  // k_frame_uniform: per workgroup, thread 0's phase cycles
+    const uint64_t nb = (P.uni_n + kPartTile - 1) / kPartTile;
+    std::vector<unsigned long long> h(16 * nb);
+    if (hipMemcpy(h.data(), pl->dbg, h.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return;
+    double sum[4] = {0};
+    for (uint64_t c = 0; c < nb; c++)
+      for (int i = 0; i < 4; i++) sum[i] += (double)h[c * 16 + i];
+    fprintf(stderr, "[k_frame_uniform] workgroups=%llu mean cycles: rounds %.0f runs+scan %.0f regroup %.0f "
+            "write-out %.0f\n", (unsigned long long)nb, sum[0] / nb, sum[1] / nb, sum[2] / nb, sum[3] / nb);
+    return;
+  }
   if (!P.dbg || !P.fr_nchunks) return;
   const uint64_t nwv = (P.fr_nchunks + P.fr_w - 1) / P.fr_w;
   std::vector<unsigned long long> h(16 * nwv);
