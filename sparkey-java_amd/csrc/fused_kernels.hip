@@ -933,7 +933,8 @@ struct SlabTileR {
   uint8_t first[2 * kPartTile / 32];
 };
 
-__device__ __forceinline__ uint32_t load_tile_r(const BuildParams& P, SlabTileR& T, uint64_t g0, uint32_t group) {
+// wave 0's part of load_tile_r: the tile's slab prefix and group map (a barrier must follow)
+__device__ __forceinline__ void tile_r_hdr(const BuildParams& P, SlabTileR& T, uint64_t g0, uint32_t group) {
   const uint32_t ng = (uint32_t)min((uint64_t)group, P.nslabs > g0 ? P.nslabs - g0 : 0);
   const int tid = threadIdx.x;
   if (tid < 64) {
@@ -950,8 +951,6 @@ __device__ __forceinline__ uint32_t load_tile_r(const BuildParams& P, SlabTileR&
     if ((uint32_t)tid < ng)
       for (uint32_t k = (incl - c + 31) / 32; k < (incl + 31) / 32 && k < 2 * kPartTile / 32; k++) T.first[k] = (uint8_t)tid;
   }
-  __syncthreads();
-  return T.pre[64];
 }
 
 __device__ __forceinline__ const Entry& tile_entry_r(const BuildParams& P, const SlabTileR& T, uint64_t g0, uint32_t i) {
@@ -1033,55 +1032,97 @@ __global__ __launch_bounds__(kPartBlock) void k_part1_scatter(BuildParams P) {
 // the tile's entries grouped by digit in LDS and written as one run per digit.  No histogram pass over
 // the entries and no global scan (k_part1_hist + k_part1_scatter read every entry twice).  A region
 // that fills up flags kSpecRegionFull: the host redoes the build with the two-pass partition.
+// Persistent workgroups (two a CU: the stage's LDS), each taking the rounds (kPartTile entries of a
+// tile) of tiles blockIdx.x, + gridDim.x, ...: the next round's entries are loaded while this round's
+// cursors are reserved, its runs grouped and written.  The barriers are LDS-only (lds_barrier): the
+// loads and the cursor atomic stay in flight through them.
+constexpr uint32_t kP1rGrid = 512;
 __global__ __launch_bounds__(kPartBlock) void k_part1_regions(BuildParams P) {
+  static_assert(kPartBlock == 256, "one thread per digit");
   __shared__ Entry stage[kPartTile];
   __shared__ uint8_t sdig[kPartTile];  // digit of each staged entry
   __shared__ uint32_t cnt[256];
   __shared__ uint32_t lbase[256];
   __shared__ int64_t gdst[256];        // global index of the digit's run minus its LDS start
-  __shared__ uint64_t sh64[kPartBlock / 64 + 1];
-  __shared__ SlabTileR T;              // (p1r_group slabs: at most 2 kPartTile entries, host-checked)
+  __shared__ uint32_t wsum[kPartBlock / 64];
+  __shared__ SlabTileR T[2];           // (p1r_group slabs: at most 2 kPartTile entries, host-checked)
   if (build_aborted(P)) return;
-  const uint64_t g0 = (uint64_t)blockIdx.x * P.p1r_group;
-  const int tid = threadIdx.x;
-  const uint32_t ntile = load_tile_r(P, T, g0, P.p1r_group);
-  // kPartTile entries at a time (the second round is for the tiles that came out above the mean)
-  for (uint32_t base = 0; base < ntile; base += kPartTile) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint64_t ntiles = P.p1r_tiles;
+  uint64_t t = blockIdx.x;
+  if (t >= ntiles) return;
+  const uint32_t grp = P.p1r_group;
+  tile_r_hdr(P, T[0], t * grp, grp);
+  lds_barrier();
+  int cb = 0;
+  uint32_t ntile = T[0].pre[64], base = 0;
+  Entry v[kPartItems];
+#pragma unroll
+  for (int k = 0; k < kPartItems; k++) {
+    const uint32_t idx = (uint32_t)k * kPartBlock + tid;
+    if (idx < ntile) v[k] = tile_entry_r(P, T[0], t * grp, idx);
+  }
+  for (;;) {
     const uint32_t n = min((uint32_t)kPartTile, ntile - base);
+    uint64_t tn = t;
+    uint32_t bn = base + kPartTile;
+    int nb = cb;
+    if (bn >= ntile) {
+      tn = t + gridDim.x;
+      bn = 0;
+      nb = cb ^ 1;
+    }
+    const bool more = tn < ntiles;
     cnt[tid] = 0;
-    Entry v[kPartItems];
+    if (more && nb != cb) tile_r_hdr(P, T[nb], tn * grp, grp);  // (T[nb]'s last reader was a load before this round's barriers)
+    lds_barrier();  // (cnt clear, T[nb]; the previous round is done with stage, sdig, gdst, lbase, wsum)
     uint32_t dg[kPartItems];
 #pragma unroll
-    for (int i = 0; i < kPartItems; i++) {
-      const uint32_t idx = (uint32_t)i * kPartBlock + tid;
-      if (idx < n) v[i] = tile_entry_r(P, T, g0, base + idx);
-    }
-    __syncthreads();  // (the clear; the previous round is done with stage and gdst)
-#pragma unroll
-    for (int i = 0; i < kPartItems; i++) {
-      const uint32_t idx = (uint32_t)i * kPartBlock + tid;
-      dg[i] = ~0u;
-      if (idx < n && !(P.skip_del && (v[i].addr & kDelBit))) {  // exact path: DELETEs stay out
-        dg[i] = digit_of(P, bucket_of(P, v[i].hash));
-        dg[i] |= atomicAdd(&cnt[dg[i]], 1u) << 8;  // rank inside the tile's digit run
+    for (int k = 0; k < kPartItems; k++) {
+      const uint32_t idx = (uint32_t)k * kPartBlock + tid;
+      dg[k] = ~0u;
+      if (idx < n && !(P.skip_del && (v[k].addr & kDelBit))) {  // exact path: DELETEs stay out
+        const uint32_t d = digit_of(P, bucket_of(P, v[k].hash));
+        dg[k] = d | (atomicAdd(&cnt[d], 1u) << 8);  // rank inside the round's digit run
       }
     }
-    __syncthreads();
+    lds_barrier();
+    // the digit's cursor first (its round trip overlaps the next round's loads and this one's scan)
     const uint32_t c = cnt[tid];
-    lbase[tid] = (uint32_t)block_excl_sum<kPartBlock>(c, sh64, &sh64[kPartBlock / 64]);
     const uint64_t b0 = c ? atomicAdd(&P.p1_fill[tid], c) : 0u;
-    if (b0 + c > P.p1_region) atomicOr(&P.st->spec_fail, kSpecRegionFull);
-    gdst[tid] = (int64_t)((uint64_t)tid * P.p1_region + b0) - (int64_t)lbase[tid];
-    __syncthreads();
+    Entry nx[kPartItems];
+    if (more) {
+      const uint32_t nn = min((uint32_t)kPartTile, T[nb].pre[64] - bn);
 #pragma unroll
-    for (int i = 0; i < kPartItems; i++) {
-      if (dg[i] == ~0u) continue;
-      const uint32_t d = dg[i] & 255u, pos = lbase[d] + (dg[i] >> 8);
-      stage[pos] = v[i];
+      for (int k = 0; k < kPartItems; k++) {
+        const uint32_t idx = (uint32_t)k * kPartBlock + tid;
+        if (idx < nn) nx[k] = tile_entry_r(P, T[nb], tn * grp, bn + idx);
+      }
+    }
+    uint32_t incl = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t x = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += x;
+    }
+    if (lane == 63) wsum[wave] = incl;
+    lds_barrier();
+    uint32_t off = 0;
+    for (int w = 0; w < wave; w++) off += wsum[w];
+    const uint32_t lb = off + incl - c;
+    lbase[tid] = lb;
+    if (b0 + c > P.p1_region) atomicOr(&P.st->spec_fail, kSpecRegionFull);
+    gdst[tid] = (int64_t)((uint64_t)tid * P.p1_region + b0) - (int64_t)lb;
+    lds_barrier();
+#pragma unroll
+    for (int k = 0; k < kPartItems; k++) {
+      if (dg[k] == ~0u) continue;
+      const uint32_t d = dg[k] & 255u, pos = lbase[d] + (dg[k] >> 8);
+      stage[pos] = v[k];
       sdig[pos] = (uint8_t)d;
     }
-    __syncthreads();
-    const uint32_t nkeep = (uint32_t)sh64[kPartBlock / 64];
+    lds_barrier();
+    const uint32_t nkeep = wsum[0] + wsum[1] + wsum[2] + wsum[3];
 #pragma unroll
     for (int k = 0; k < kPartItems; k++) {
       const uint32_t i = (uint32_t)k * kPartBlock + tid;
@@ -1091,6 +1132,13 @@ __global__ __launch_bounds__(kPartBlock) void k_part1_regions(BuildParams P) {
         if (at < (uint64_t)(d + 1) * P.p1_region) P.ent3[at] = stage[i];
       }
     }
+    if (!more) break;
+    t = tn;
+    base = bn;
+    cb = nb;
+    ntile = T[nb].pre[64];
+#pragma unroll
+    for (int k = 0; k < kPartItems; k++) v[k] = nx[k];
   }
 }
 
@@ -2396,7 +2444,7 @@ static size_t part2st_lds(uint32_t bpp, int per) {
 void launch_partition(const BuildParams& P, hipStream_t s, StageTimer* tm) {
   if (P.p1_bucket) return;  // (the framing wrote the bucket regions)
   if (!P.p1_region) launch_partition1(P, s);
-  else if (P.p1_kernel) hipLaunchKernelGGL(k_part1_regions, dim3((unsigned)P.p1r_tiles), dim3(kPartBlock), 0, s, P);
+  else if (P.p1_kernel) hipLaunchKernelGGL(k_part1_regions, dim3(std::min<unsigned>(P.p1r_tiles, kP1rGrid)), dim3(kPartBlock), 0, s, P);
   // the largest stage (entries a thread per round) that fits: fewer rounds, fewer barriers
   constexpr size_t kLdsMax = 158 * 1024;
   const bool staged = P.p2_sorted && P.p2_fixed && P.fused_carry && P.p1_region && !P.p2_seg;
