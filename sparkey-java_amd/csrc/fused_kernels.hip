@@ -709,10 +709,11 @@ __global__ __launch_bounds__(64 * W) void k_frame_uniform(BuildParams P) {
   const bool to_regions = P.p1_region != 0;
   const bool with_hist = to_regions || P.p1_hist_ready != 0;
   long long t_prev = P.dbg ? clock64() : 0;
-  auto mark = [&](int i) {  // (frame_debug: thread 0's cycles per phase of the workgroup)
+  uint64_t dbg_tile = blockIdx.x;
+  auto mark = [&](int i) {  // (frame_debug: thread 0's cycles per phase of the tile)
     if (P.dbg && threadIdx.x == 0) {
       const long long now = clock64();
-      P.dbg[(uint64_t)blockIdx.x * 16 + i] = (unsigned long long)(now - t_prev);
+      P.dbg[(uint64_t)dbg_tile * 16 + i] = (unsigned long long)(now - t_prev);
       t_prev = now;
     }
   };
@@ -727,9 +728,15 @@ __global__ __launch_bounds__(64 * W) void k_frame_uniform(BuildParams P) {
     P.st->n_records = P.uni_n;
     P.st->exit = P.fr_entry + (int64_t)P.uni_n * R;  // the framed chain's exit
   }
-  const uint64_t blk0 = (uint64_t)blockIdx.x * (kSub * kPartTile);
+  const uint64_t nblk = (P.uni_n + kSub * kPartTile - 1) / (kSub * kPartTile);
   uint64_t hsh[kRounds];  // (the address follows from the round: record blk0 + (r * W + wave) * 64 + lane)
   uint32_t dr[kRounds];   // digit << 16 | rank within its tile's digit run, ~0 = none
+  // Persistent workgroups (two a CU): tiles blockIdx.x, + gridDim.x, ...  A tile's entry stores drain
+  // while the next tile's first rounds stream in (a workgroup that ended after its write-out held its
+  // LDS until the stores completed).
+  for (uint64_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
+  const uint64_t blk0 = blk * (kSub * kPartTile);
+  dbg_tile = blk;
   // stage round r's records into b: LDS-DMA (returns the load instructions in flight), or guarded
   // loads near the end of the buffer (synchronous, returns 0)
   auto stage_round = [&](int r, uint8_t* b) -> int {
@@ -765,7 +772,8 @@ __global__ __launch_bounds__(64 * W) void k_frame_uniform(BuildParams P) {
     uint8_t* buf = DB ? buf0 + (r & 1) * P.uni_wbytes : buf0;
     const uint64_t i0 = blk0 + (uint64_t)(r * W + wave) * 64;
     if (DB) {
-      // the next round's records in flight while this one is hashed; then wait for this one's only
+      // the next round's records in flight while this one is hashed; then wait for this one's (and
+      // for anything issued before it: the previous tile's entry stores)
       const int nxt = r + 1 < kRounds ? stage_round(r + 1, buf0 + ((r + 1) & 1) * P.uni_wbytes) : 0;
       wait_vmcnt_le(nxt);
     } else {
@@ -806,15 +814,18 @@ __global__ __launch_bounds__(64 * W) void k_frame_uniform(BuildParams P) {
     }
     __builtin_amdgcn_wave_barrier();  // every lane is done with the buffer before the next round's DMA
   }
-  if (!with_hist) return;
+  if (!with_hist) continue;
   __syncthreads();
   mark(0);
   if (!to_regions) {  // k_part1_hist's output for these tiles
     for (int t = threadIdx.x; t < kSub * 256; t += 64 * W) {
-      const uint64_t tile = (uint64_t)blockIdx.x * kSub + (t >> 8);
+      const uint64_t tile = blk * kSub + (t >> 8);
       if (tile < P.p1_tiles) P.p1_hist[(uint64_t)(t & 255) * P.p1_tiles + tile] = hist[t];
     }
-    return;
+    __syncthreads();  // (hist is cleared for the next tile)
+    for (int t = threadIdx.x; t < kSub * 256; t += 64 * W) hist[t] = 0;
+    __syncthreads();
+    continue;
   }
   // One run per digit region for the workgroup's kSub tiles together (one atomic per non-empty
   // digit; runs kSub times longer than a tile's, so fewer partial lines at the run ends), then per
@@ -830,6 +841,7 @@ __global__ __launch_bounds__(64 * W) void k_frame_uniform(BuildParams P) {
   uint32_t c = 0, incl = 0, b0 = 0;
   if (threadIdx.x < 256) {  // waves 0-3: the cursor, and the exclusive scan of the tile's 256 digit counts
     c = hist[threadIdx.x];
+    hist[threadIdx.x] = 0;  // (for the next tile: its rounds count after the barriers below)
     b0 = c ? atomicAdd(&P.p1_fill[threadIdx.x], c) : 0u;
     incl = c;
 #pragma unroll
@@ -862,7 +874,7 @@ __global__ __launch_bounds__(64 * W) void k_frame_uniform(BuildParams P) {
     if ((uint64_t)b0 + c > P.p1_region) atomicOr(&P.st->spec_fail, kSpecRegionFull);
     rbase[threadIdx.x] = b0;
   }
-  __syncthreads();
+  lds_barrier();
   mark(2);
   const uint32_t ntile = wsum[0] + wsum[1] + wsum[2] + wsum[3];
   for (uint32_t i = threadIdx.x; i < ntile; i += 64 * W) {
@@ -874,6 +886,8 @@ __global__ __launch_bounds__(64 * W) void k_frame_uniform(BuildParams P) {
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
     mark(3);
+  }
+  lds_barrier();  // the stage's reads are done (its stores may still be in flight): the next tile's DMA
   }
 }
 
@@ -2398,7 +2412,8 @@ void launch_frame_uniform(const BuildParams& P, hipStream_t s, StageTimer* tm) {
   // starts), and hist + rbase after either (tiles of 2048 records measured slower: profiles/r05/c2/)
   const size_t body = std::max<size_t>((size_t)W * Q.uni_wbytes * 2, (size_t)kPartTile * (sizeof(Entry) + 1) + 1024);
   Q.uni_hist_off = (uint32_t)body;
-  hipLaunchKernelGGL((k_frame_uniform<W, true>), dim3((unsigned)nblk), dim3(64 * W), body + 2048, s, Q);
+  // persistent: two workgroups a CU (the LDS), each over every 512th tile
+  hipLaunchKernelGGL((k_frame_uniform<W, true>), dim3((unsigned)std::min<uint64_t>(nblk, 512)), dim3(64 * W), body + 2048, s, Q);
   tm->mark("frame", s);
 }
 
