@@ -348,95 +348,99 @@ __global__ void __launch_bounds__(64) k_snappy_gw(SnappyParams S) {
   const int64_t readable = S.log_len - B.data;
   const uint32_t n = B.clen, ulen = B.ulen;
   uint8_t* out = S.vlog + B.voff;
-  int64_t wa = 0, wend = 0;  // the window holds stream bytes [wa, wend)
+  int32_t wa = 0, wend = 0;  // the window holds stream bytes [wa, wend) (a Snappy block is < 2^31 bytes)
   auto refill = [&](uint32_t p) {
-    wa = (int64_t)p - (int64_t)(((uintptr_t)(g + p)) & 15);
+    wa = (int32_t)p - (int32_t)(((uintptr_t)(g + p)) & 15);
 #pragma unroll 4
     for (uint32_t w = lane; w < kGwWindow / 16; w += 64) {
-      const int64_t q = wa + 16 * (int64_t)w;
+      const int64_t q = (int64_t)wa + 16 * (int64_t)w;
       if (q + 16 <= readable) {
         *(uint4*)(win + 16 * w) = *(const uint4*)(g + q);
       } else {
         for (int i = 0; i < 16 && q + i < readable; i++) win[16 * w + i] = g[q + i];
       }
     }
-    wend = min<int64_t>(wa + kGwWindow, (int64_t)n);
+    wend = min(wa + (int32_t)kGwWindow, (int32_t)n);
     __builtin_amdgcn_wave_barrier();
   };
-  auto byte = [&](uint32_t q) -> uint32_t { return win[(int64_t)q - wa]; };
+  auto byte = [&](uint32_t q) -> uint32_t { return win[(int32_t)q - wa]; };
   refill(0);
   uint32_t p = 0;
   while (byte(p) & 0x80u) p++;  // preamble (<= 5 bytes, validated by the directory)
   p++;
   uint32_t o = 0, flags = 0;
   while (p < n) {
-    if ((int64_t)p + 5 > wend && wend < (int64_t)n) refill(p);
+    if ((int32_t)p + 5 > wend && wend < (int32_t)n) refill(p);
     // the tag and the four bytes after it: one aligned 8-byte LDS read (the window has 16 bytes of
     // slack; bytes at or past the stream end are not used: every use is bounds-checked against n)
-    uint32_t t, e0, e1, e2, e3;
+    uint64_t v;
     {
-      const uint32_t r = (uint32_t)((int64_t)p - wa);
+      const uint32_t r = (uint32_t)((int32_t)p - wa);
       const uint32_t a4 = r & ~3u, sh = (r & 3u) * 8u;
       const uint32_t d0 = __builtin_amdgcn_readfirstlane(*reinterpret_cast<const uint32_t*>(win + a4));
       const uint32_t d1 = __builtin_amdgcn_readfirstlane(*reinterpret_cast<const uint32_t*>(win + a4 + 4));
       const uint32_t d2 = __builtin_amdgcn_readfirstlane(*reinterpret_cast<const uint32_t*>(win + a4 + 8));
       const uint64_t lo = ((uint64_t)d1 << 32 | d0) >> sh;
       const uint32_t hi = sh ? (d2 << (32 - sh)) : 0u;
-      const uint64_t v = lo | ((uint64_t)hi << 32);
-      t = (uint32_t)v & 0xffu;
-      e0 = (uint32_t)(v >> 8) & 0xffu;
-      e1 = (uint32_t)(v >> 16) & 0xffu;
-      e2 = (uint32_t)(v >> 24) & 0xffu;
-      e3 = (uint32_t)(v >> 32) & 0xffu;
+      v = lo | ((uint64_t)hi << 32);
     }
+    // the element from its tag with selects: the bytes after the tag are a literal's length (tag
+    // length field >= 60: 1-4 bytes) or a copy's offset (1, 2 or 4 bytes)
+    const uint32_t t = (uint32_t)v & 0xffu, w = (uint32_t)(v >> 8);
+    const uint32_t kind = t & 3u, hi6 = t >> 2;
+    const uint32_t nb = kind == 0 ? (hi6 >= 60 ? hi6 - 59 : 0u) : (kind == 3 ? 4u : kind);
+    const uint32_t m = nb >= 4 ? 0xffffffffu : (1u << (8 * nb)) - 1u;
     p++;
+    if (p + nb > n) { flags = kWalkBadStream; break; }
+    p += nb;
     uint32_t len, off = 0;
-    if ((t & 3u) == 0) {
-      len = (t >> 2) + 1;
-      if (len > 60) {
-        const uint32_t nb = len - 60;
-        if (p + nb > n) { flags = kWalkBadStream; break; }
-        const uint32_t w = e0 | (e1 << 8) | (e2 << 16) | (e3 << 24);
-        const uint64_t lm1 = nb == 4 ? (uint64_t)w : (uint64_t)(w & ((1u << (8 * nb)) - 1u));
-        if (lm1 + 1 > (uint64_t)(n - p - nb)) { flags = kWalkBadStream; break; }
-        len = (uint32_t)lm1 + 1;
-        p += nb;
-      }
-      if (len > n - p || len > ulen - o) { flags = kWalkBadStream; break; }
-      if ((int64_t)p + len <= wend) {  // from the window
-        const int64_t r = (int64_t)p - wa;
+    if (kind == 0) {
+      const uint64_t len64 = hi6 >= 60 ? (uint64_t)(w & m) + 1 : (uint64_t)hi6 + 1;
+      if (len64 > (uint64_t)(n - p) || len64 > (uint64_t)(ulen - o)) { flags = kWalkBadStream; break; }
+      len = (uint32_t)len64;
+      if ((int32_t)(p + len) <= wend && len <= 128) {  // the usual literal: two lane steps, no loop
+        const uint32_t r = (uint32_t)((int32_t)p - wa), k1 = lane + 64u;
+        const uint8_t v0 = win[r + min(lane, len - 1u)];
+        const uint8_t v1 = win[r + min(k1, len - 1u)];
+        if (lane < len) {
+          if (kExp != 1) out[o + lane] = v0;
+          ring[(o + lane) & RM] = v0;
+        }
+        if (k1 < len) {
+          if (kExp != 1) out[o + k1] = v1;
+          ring[(o + k1) & RM] = v1;
+        }
+      } else if ((int64_t)p + len <= (int64_t)wend) {  // from the window
+        const uint32_t r = (uint32_t)((int32_t)p - wa);
         for (uint32_t k = lane; k < len; k += 64) {
-          const uint8_t v = win[r + k];
-          if (kExp != 1) out[o + k] = v;
-          ring[(o + k) & RM] = v;
+          const uint8_t x = win[r + k];
+          if (kExp != 1) out[o + k] = x;
+          ring[(o + k) & RM] = x;
         }
       } else {  // reaches past the window: from global memory
         for (uint32_t k = lane; k < len; k += 64) {
-          const uint8_t v = g[p + k];
-          out[o + k] = v;
-          ring[(o + k) & RM] = v;
+          const uint8_t x = g[p + k];
+          out[o + k] = x;
+          ring[(o + k) & RM] = x;
         }
       }
       p += len;
     } else {
-      if ((t & 3u) == 1) {
-        if (p + 1 > n) { flags = kWalkBadStream; break; }
-        len = ((t >> 2) & 7u) + 4;
-        off = ((t >> 5) << 8) | e0;
-        p += 1;
-      } else if ((t & 3u) == 2) {
-        if (p + 2 > n) { flags = kWalkBadStream; break; }
-        len = (t >> 2) + 1;
-        off = e0 | (e1 << 8);
-        p += 2;
-      } else {
-        if (p + 4 > n) { flags = kWalkBadStream; break; }
-        len = (t >> 2) + 1;
-        off = e0 | (e1 << 8) | (e2 << 16) | (e3 << 24);
-        p += 4;
-      }
-      if (off == 0 || off > o || len > ulen - o) { flags = kWalkBadStream; break; }
-      if (off + len <= kSnappyRing) {  // out[o + k] = out[o - off + k % off]: sources < o, in the ring
+      len = kind == 1 ? (hi6 & 7u) + 4 : hi6 + 1;
+      off = kind == 1 ? ((t >> 5) << 8) | (w & 0xffu) : (w & m);
+    if (off == 0 || off > o || len > ulen - o) { flags = kWalkBadStream; break; }
+      if (off + len <= kSnappyRing && len <= 64) {  // (every Snappy copy: len <= 64) one lane step
+        const uint32_t kk = min(lane, len - 1u);
+        uint8_t v;
+        if (off >= len) v = ring[(o - off + kk) & RM];  // (scalar branch: no modulo)
+        else v = ring[(o - off + kk % off) & RM];
+        __builtin_amdgcn_wave_barrier();
+        if (lane < len) {
+          if (kExp != 1) out[o + lane] = v;
+          ring[(o + lane) & RM] = v;
+        }
+        __builtin_amdgcn_wave_barrier();
+      } else if (off + len <= kSnappyRing) {  // out[o + k] = out[o - off + k % off]: sources < o, in the ring
         for (uint32_t k0 = 0; k0 < len; k0 += 64) {
           const uint32_t k = k0 + lane;
           uint8_t v = 0;
