@@ -1900,6 +1900,7 @@ __global__ __launch_bounds__(kPart2Block) void k_part2st(BuildParams P) {
   uint32_t* roff = rcnt + nbins;
   uint32_t* gbase = roff + nbins;
   Entry* stage = reinterpret_cast<Entry*>(dyn + ((nbins * 260 + 3) & ~3u));
+  uint8_t* sbk = reinterpret_cast<uint8_t*>(stage + kP2Stage);  // each staged entry's bucket (no second fast_mod)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   long long t_prev2 = P.part_dbg ? clock64() : 0;
   auto mark2 = [&](int i) {  // (SPARKEY_PART2_DEBUG: thread 0's cycles per phase)
@@ -1962,13 +1963,14 @@ __global__ __launch_bounds__(kPart2Block) void k_part2st(BuildParams P) {
     for (int k = 0; k < kP2StagePer; k++) {
       if (bk[k] == ~0u) continue;
       stage[roff[bk[k]] + rk[k]] = v[k];
+      sbk[roff[bk[k]] + rk[k]] = (uint8_t)bk[k];
     }
     __syncthreads();
     // the runs: consecutive lanes on consecutive entries of a bucket's region
     const uint32_t nround = (uint32_t)min((uint64_t)kP2Stage, hi - i0);
     for (uint32_t i = tid; i < nround; i += kPart2Block) {
       const Entry e = stage[i];
-      const uint32_t b = (uint32_t)((fast_mod(e.hash, P.mod) >> kBucketShift) - b0);
+      const uint32_t b = sbk[i];
       const uint32_t r = gbase[b] + (i - roff[b]);
       if (r < kPlaceLdsMax) P.ent2[(b0 + b - P.b_lo) * (uint64_t)kPlaceLdsMax + r] = e;
       else ovf = true;
@@ -2453,7 +2455,7 @@ bool part2f_fits(uint32_t bpp) { return bpp > kPart2Block * 3 ? bpp * 4 <= 158 *
 
 // k_part2st's dynamic LDS (the 8-bit counts, the bucket words, the stage of `per` entries a thread)
 static size_t part2st_lds(uint32_t bpp, int per) {
-  return (size_t)((bpp * 260 + 3) & ~3u) * 4 + (size_t)kPart2Block * per * sizeof(Entry);
+  return (size_t)((bpp * 260 + 3) & ~3u) * 4 + (size_t)kPart2Block * per * (sizeof(Entry) + 1);
 }
 
 void launch_partition(const BuildParams& P, hipStream_t s, StageTimer* tm) {
