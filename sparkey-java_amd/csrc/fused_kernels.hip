@@ -1972,7 +1972,10 @@ __global__ __launch_bounds__(kPart2Block) void k_part2st(BuildParams P) {
       const Entry e = stage[i];
       const uint32_t b = sbk[i];
       const uint32_t r = gbase[b] + (i - roff[b]);
-      if (r < kPlaceLdsMax) P.ent2[(b0 + b - P.b_lo) * (uint64_t)kPlaceLdsMax + r] = e;
+      typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+      if (r < kPlaceLdsMax)
+        __builtin_nontemporal_store(*reinterpret_cast<const u32x4*>(&e),
+                                    reinterpret_cast<u32x4*>(&P.ent2[(b0 + b - P.b_lo) * (uint64_t)kPlaceLdsMax + r]));
       else ovf = true;
     }
     __syncthreads();  // (the stage and the offsets are rewritten next round)
