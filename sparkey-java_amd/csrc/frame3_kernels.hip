@@ -628,7 +628,10 @@ __device__ __forceinline__ void frame3_region(const BuildParams& P, const uint64
         uint32_t a = 0;
         if (bput) a = atomicAdd(&P.bcount[b], 1u);
         if (bput) {
-          if (a < kPlaceLdsMax) P.ent2[(uint64_t)b * kPlaceLdsMax + a] = en;
+          typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+          if (a < kPlaceLdsMax)
+            __builtin_nontemporal_store(*reinterpret_cast<const u32x4*>(&en),
+                                        reinterpret_cast<u32x4*>(&P.ent2[(uint64_t)b * kPlaceLdsMax + a]));
           else bovf = true;
         }
       }
