@@ -330,7 +330,11 @@ int sparkey_shard_comm_create(sparkey_shard_comm** comm_out, const uint8_t* id, 
  *   all_to_all: send_bytes[r] bytes to rank r from consecutive runs of `send` in rank order;
  *               recv_bytes[r] bytes from rank r into consecutive runs of `recv` in rank order
  * A rank that fails takes part in every collective up to the next checkpoint (with all-ones rows
- * where its own cannot leave the device), so its peers fail with it there.  A rank whose process dies
+ * where its own cannot leave the device; a row whose retry or code word reads negative is a failed
+ * rank's), so its peers fail with it there -- also when the failure is a collective's own (its copy
+ * to or from the host): the rank then skips its device steps and still joins the collectives up to
+ * the checkpoint.  A failure before the frame rows' checkpoint that the rank cannot post (its row
+ * cannot be written on the device) still returns at once.  A rank whose process dies
  * never arrives: the transport must time out on its own and return nonzero (the library has no way
  * to interrupt a callback). */
 typedef struct sparkey_shard_transport {

@@ -169,10 +169,13 @@ __global__ __launch_bounds__(kPlaceBlock) void k_summary(BuildParams P) {
   const uint64_t eoff = P.p1_bucket ? (b - P.b_lo) * (uint64_t)kPlaceLdsMax : P.boff[b];
   reinterpret_cast<uint4*>(cnt)[tid] = make_uint4(0u, 0u, 0u, 0u);
   __syncthreads();
+  bool bad = false;  // (kGuardForeign)
   for (uint32_t i = tid; i < n; i += kPlaceBlock) {
     const uint64_t w = fast_mod(P.ent2[eoff + i].hash, P.mod) - start;
-    atomicAdd(&cnt[w], 1u);
+    if (w < (uint64_t)kBucket) atomicAdd(&cnt[w], 1u);
+    else bad = true;
   }
+  report_foreign(P, bad);
   __syncthreads();
   const uint4 c = reinterpret_cast<const uint4*>(cnt)[tid];
   const uint32_t tot = c.x + c.y + c.z + c.w;
@@ -223,6 +226,14 @@ __global__ void k_carry(BuildParams P) {
   int64_t x0 = P.carry_in;
   if (P.carry_funs) {
     const int64_t* f = P.carry_funs;
+    // A rank whose function could not leave its device sent an all-ones row (HostColl): c = -1, which
+    // no carry function has (c >= 0).  This rank skips its placement (build_aborted) and the failed
+    // rank's finish row fails every rank.
+    for (int r = 0; r < P.carry_world; r++)
+      if (f[2 * r] < 0) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(&P.st->p2_overflow, 1u);
+        return;
+      }
     int64_t c = f[0];  // the composed function's constant: the fixed point when N < capacity
     for (int r = 1; r < P.carry_world; r++) c = max(f[2 * r], c + f[2 * r + 1]);
     x0 = c;

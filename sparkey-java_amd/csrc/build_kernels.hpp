@@ -312,6 +312,7 @@ uint32_t frame3_lds_per_wave(const BuildParams& P);
 __host__ __device__ inline bool slab_framing(int path) { return path == 0 || path == 4; }
 void launch_place_fast(const BuildParams& P, hipStream_t s, StageTimer* tm);
 void launch_place_buckets(const BuildParams& P, hipStream_t s);
+void launch_inject_foreign(const BuildParams& P, hipStream_t s, int where);  // (inject_foreign switch, tests)
 // fallbacks and shared stages (build_kernels.hip)
 void launch_framing_serial(const BuildParams& P, hipStream_t s);
 void launch_emit(const BuildParams& P, hipStream_t s, StageTimer* tm);

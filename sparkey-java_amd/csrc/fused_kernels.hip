@@ -684,6 +684,9 @@ __device__ __forceinline__ void wait_vmcnt_le(int n) {
 // A workgroup barrier for LDS traffic only: LDS operations complete, global ones may stay in flight
 // (__syncthreads waits for every outstanding load and store first)
 __device__ __forceinline__ void lds_barrier() {
+  // (a compiler barrier first: s_barrier is IntrNoMem, so without it earlier LDS stores could be
+  //  scheduled past the barrier; it emits no instruction)
+  asm volatile("" ::: "memory");
   __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0); vmcnt, expcnt at their maxima
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -1197,6 +1200,7 @@ __global__ __launch_bounds__(kPart2Block) void k_part2(BuildParams P) {
   const int tid = threadIdx.x;
   for (uint32_t b = tid; b < nbins; b += kPart2Block) hist[b] = 0;
   __syncthreads();
+  bool bad = false;  // (kGuardForeign)
   // (kPart2Items loads per thread in flight: one workgroup per CU needs the memory-level parallelism)
   for (uint32_t q = 0; q < nseg; q++) {
     const uint64_t a = seg ? seg[2 * q] : lo, z = seg ? seg[2 * q + 1] : hi;
@@ -1210,10 +1214,14 @@ __global__ __launch_bounds__(kPart2Block) void k_part2(BuildParams P) {
 #pragma unroll
       for (int k = 0; k < kPart2Items; k++) {
         const uint64_t i = i0 + (uint64_t)k * kPart2Block + tid;
-        if (i < z) atomicAdd(&hist[bucket_of(P, h[k]) - b0], 1u);
+        if (i >= z) continue;
+        const uint32_t b = bucket_of(P, h[k]) - b0;
+        if (b < nbins) atomicAdd(&hist[b], 1u);
+        else bad = true;
       }
     }
   }
+  report_foreign(P, bad);
   __syncthreads();
   // exclusive scan of the bins (per consecutive bins per thread)
   const uint32_t per = (nbins + kPart2Block - 1) / kPart2Block;
@@ -1248,7 +1256,8 @@ __global__ __launch_bounds__(kPart2Block) void k_part2(BuildParams P) {
 #pragma unroll
       for (int k = 0; k < kPart2Items; k++) {
         const uint64_t i = i0 + (uint64_t)k * kPart2Block + tid;
-        if (i < z) P.ent2[lo + atomicAdd(&cur[bucket_of(P, v[k].hash) - b0], 1u)] = v[k];
+        const uint32_t b = bucket_of(P, v[k].hash) - b0;
+        if (i < z && b < nbins) P.ent2[lo + atomicAdd(&cur[b], 1u)] = v[k];  // (foreign: counted above)
       }
     }
   }
@@ -1375,6 +1384,7 @@ __global__ __launch_bounds__(kPart2Block) void k_part2d(BuildParams P) {
   const int tid = threadIdx.x;
   for (uint32_t b = tid; b < 6 * nbins; b += kPart2Block) dyn[b] = 0;
   __syncthreads();
+  bool bad = false;  // (kGuardForeign)
   // pass A: the bucket histogram (hashes only)
   for (uint64_t i0 = lo; i0 < hi; i0 += (uint64_t)kPart2Block * kPart2Items) {
     uint64_t h[kPart2Items];
@@ -1386,9 +1396,13 @@ __global__ __launch_bounds__(kPart2Block) void k_part2d(BuildParams P) {
 #pragma unroll
     for (int k = 0; k < kPart2Items; k++) {
       const uint64_t i = i0 + (uint64_t)k * kPart2Block + tid;
-      if (i < hi) atomicAdd(&hist[bucket_of(P, h[k]) - b0], 1u);
+      if (i >= hi) continue;
+      const uint32_t b = bucket_of(P, h[k]) - b0;
+      if (b < nbins) atomicAdd(&hist[b], 1u);
+      else bad = true;
     }
   }
+  report_foreign(P, bad);
   __syncthreads();
   // bucket offsets: consecutive bins per thread
   const uint32_t per = (nbins + kPart2Block - 1) / kPart2Block;
@@ -1435,9 +1449,10 @@ __global__ __launch_bounds__(kPart2Block) void k_part2d(BuildParams P) {
     for (int k = 0; k < kP2dPer; k++) {
       const uint64_t i = i0 + (uint64_t)k * kPart2Block + tid;
       bk[k] = ~0u;
-      if (i >= hi) continue;
-      bk[k] = bucket_of(P, v[k].hash) - b0;
-      rk[k] = atomicAdd(&rcnt[bk[k]], 1u);
+      const uint32_t b = bucket_of(P, v[k].hash) - b0;
+      if (i >= hi || b >= nbins) continue;  // (foreign: reported by pass A)
+      bk[k] = b;
+      rk[k] = atomicAdd(&rcnt[b], 1u);
     }
     __syncthreads();
     {  // the round's run offsets; each bin's region cursor moves past the round; the other parity's
@@ -1503,7 +1518,7 @@ __global__ __launch_bounds__(kPart2Block) void k_part2f(BuildParams P) {
   for (uint32_t b = tid; b < 5 * nbins; b += kPart2Block) dyn[b] = 0;
   __syncthreads();
   const uint32_t per = (nbins + kPart2Block - 1) / kPart2Block;
-  bool ovf = false;
+  bool ovf = false, bad = false;  // (bad: kGuardForeign)
   auto load_round = [&](Entry (&v)[kPer], uint64_t i0) {
 #pragma unroll
     for (int k = 0; k < kPer; k++) {
@@ -1526,8 +1541,11 @@ __global__ __launch_bounds__(kPart2Block) void k_part2f(BuildParams P) {
       const uint64_t i = i0 + (uint64_t)k * kPart2Block + tid;
       bk[k] = ~0u;
       if (i >= hi) continue;
-      bk[k] = bucket_of(P, v[k].hash) - b0;
-      rk[k] = atomicAdd(&rcnt[bk[k]], 1u);
+      const uint32_t b = bucket_of(P, v[k].hash) - b0;
+      bad |= b >= nbins;
+      if (b >= nbins) continue;
+      bk[k] = b;
+      rk[k] = atomicAdd(&rcnt[b], 1u);
     }
     __syncthreads();
     {  // the round's run offsets; each bucket's cursor moves past the round; the other parity's counts
@@ -1565,6 +1583,7 @@ __global__ __launch_bounds__(kPart2Block) void k_part2f(BuildParams P) {
     __syncthreads();  // (the stage, roff and gbase are rewritten next round)
   }
   if (ovf) atomicOr(&P.st->p2_overflow, 1u);
+  report_foreign(P, bad);
   for (uint32_t b = tid; b < nbins; b += kPart2Block) {
     const uint64_t bucket = (uint64_t)b0 + b;
     if (bucket < P.nbuckets) {
@@ -1589,7 +1608,7 @@ __global__ __launch_bounds__(kPart2Block) void k_part2f_direct(BuildParams P) {
   for (uint32_t b = tid; b < nbins; b += kPart2Block) cur[b] = 0;
   __syncthreads();
   constexpr int kIn = 8;
-  bool ovf = false;
+  bool ovf = false, bad = false;  // (bad: kGuardForeign)
   for (uint64_t i0 = lo; i0 < hi; i0 += (uint64_t)kPart2Block * kIn) {
     Entry v[kIn];
 #pragma unroll
@@ -1602,12 +1621,15 @@ __global__ __launch_bounds__(kPart2Block) void k_part2f_direct(BuildParams P) {
       const uint64_t i = i0 + (uint64_t)k * kPart2Block + tid;
       if (i >= hi) continue;
       const uint32_t b = bucket_of(P, v[k].hash) - b0;
+      bad |= b >= nbins;
+      if (b >= nbins) continue;
       const uint32_t r = atomicAdd(&cur[b], 1u);
       if (r < kPlaceLdsMax) P.ent2[((uint64_t)b0 + b - P.b_lo) * kPlaceLdsMax + r] = v[k];
       else ovf = true;
     }
   }
   if (ovf) atomicOr(&P.st->p2_overflow, 1u);
+  report_foreign(P, bad);
   __syncthreads();
   for (uint32_t b = tid; b < nbins; b += kPart2Block) {
     const uint64_t bucket = (uint64_t)b0 + b;
@@ -1664,7 +1686,13 @@ __global__ __launch_bounds__(kPart2Block) void k_part2_recv(BuildParams P) {
       }
     }
   };
-  each([&](const Entry& e) { atomicAdd(&cnt[bucket_of(P, e.hash) - b0], 1u); });
+  bool bad = false;  // (kGuardForeign)
+  each([&](const Entry& e) {
+    const uint32_t b = (uint32_t)(bucket_of(P, e.hash) - b0);
+    if (b < nbins) atomicAdd(&cnt[b], 1u);
+    else bad = true;
+  });
+  report_foreign(P, bad);
   __syncthreads();
   for (uint32_t b = tid; b < nbins; b += kPart2Block) {
     const uint32_t c = cnt[b];
@@ -1673,9 +1701,10 @@ __global__ __launch_bounds__(kPart2Block) void k_part2_recv(BuildParams P) {
   __syncthreads();
   bool ovf = false;
   each([&](const Entry& e) {
-    const uint32_t b = bucket_of(P, e.hash);
-    const uint32_t r = atomicAdd(&cnt[b - b0], 1u);
-    if (r < kPlaceLdsMax) P.ent2[(uint64_t)(b - P.b_lo) * kPlaceLdsMax + r] = e;
+    const uint32_t b = (uint32_t)(bucket_of(P, e.hash) - b0);
+    if (b >= nbins) return;  // (reported by the count pass)
+    const uint32_t r = atomicAdd(&cnt[b], 1u);
+    if (r < kPlaceLdsMax) P.ent2[(b0 + b - P.b_lo) * kPlaceLdsMax + r] = e;
     else ovf = true;
   });
   if (ovf) atomicOr(&P.st->p2_overflow, 1u);
@@ -1747,7 +1776,7 @@ __global__ __launch_bounds__(kPart2Block) void k_part2s(BuildParams P) {
   if (tid < (int)kP2SortedMaxBpp) s_fun[tid] = MaxPlus{0, 0};
   __syncthreads();
   mark2(0);
-  bool ovf = false;
+  bool ovf = false, bad = false;  // (bad: kGuardForeign)
   // (software-pipelined: the next round's entries are in flight while this round's are counted and
   // stored -- one workgroup per CU, so nothing else hides the load latency; measured 5 rounds of
   // ~31K cycles each at C2 without it, SPARKEY_PART2_DEBUG)
@@ -1776,6 +1805,8 @@ __global__ __launch_bounds__(kPart2Block) void k_part2s(BuildParams P) {
         if (i >= rz) continue;
         const uint64_t slot = fast_mod(v[k].hash, P.mod);
         const uint32_t b = (uint32_t)((slot >> kBucketShift) - b0), sl = (uint32_t)(slot & (kBucket - 1));
+        bad |= b >= nbins;
+        if (b >= nbins) continue;
         atomicAdd(&h[(b << 9) + (sl >> 1)], 1u << ((sl & 1) * 16));
         const uint32_t r = atomicAdd(&btot[b], 1u);
         if (fixed) {  // (regions from the range's first bucket: a sharded rank holds its range only)
@@ -1786,6 +1817,7 @@ __global__ __launch_bounds__(kPart2Block) void k_part2s(BuildParams P) {
     }
   }
   if (ovf) atomicOr(&P.st->p2_overflow, 1u);
+  report_foreign(P, bad);
   mark2(1);
   __syncthreads();
   mark2(2);
@@ -1870,7 +1902,8 @@ __global__ __launch_bounds__(kPart2Block) void k_part2s(BuildParams P) {
 #pragma unroll
       for (int k = 0; k < kPart2Items; k++) {
         const uint64_t i = i0 + (uint64_t)k * kPart2Block + tid;
-        if (i < rz) P.ent2[lo + atomicAdd(&boffl[bucket_of(P, v[k].hash) - b0], 1u)] = v[k];
+        const uint32_t b = (uint32_t)(bucket_of(P, v[k].hash) - b0);
+        if (i < rz && b < nbins) P.ent2[lo + atomicAdd(&boffl[b], 1u)] = v[k];  // (foreign: reported above)
       }
     }
   }
@@ -1914,7 +1947,7 @@ __global__ __launch_bounds__(kPart2Block) void k_part2st(BuildParams P) {
   if (tid < (int)kP2SortedMaxBpp) s_fun[tid] = MaxPlus{0, 0};
   __syncthreads();
   mark2(0);
-  bool ovf = false;
+  bool ovf = false, bad = false;  // (bad: kGuardForeign)
   auto load_round = [&](Entry (&v)[kP2StagePer], uint64_t i0) {
 #pragma unroll
     for (int k = 0; k < kP2StagePer; k++) {
@@ -1937,6 +1970,8 @@ __global__ __launch_bounds__(kPart2Block) void k_part2st(BuildParams P) {
       if (i >= hi) continue;
       const uint64_t slot = fast_mod(v[k].hash, P.mod);
       const uint32_t b = (uint32_t)((slot >> kBucketShift) - b0), sl = (uint32_t)(slot & (kBucket - 1));
+      bad |= b >= nbins;  // (bk stays ~0u: no LDS index, no store)
+      if (b >= nbins) continue;
       const uint32_t sh = (sl & 3u) * 8u;
       if (((atomicAdd(&h[(b << 8) + (sl >> 2)], 1u << sh) >> sh) & 0xffu) == 0xffu) ovf = true;  // (8-bit count full)
       bk[k] = b;
@@ -1981,6 +2016,7 @@ __global__ __launch_bounds__(kPart2Block) void k_part2st(BuildParams P) {
     __syncthreads();  // (the stage and the offsets are rewritten next round)
   }
   if (ovf) atomicOr(&P.st->p2_overflow, 1u);
+  report_foreign(P, bad);
   mark2(1);
   mark2(2);
   // bucket offsets (fixed regions) and counts
@@ -2085,8 +2121,9 @@ __device__ __forceinline__ void place_reg_bucket(const BuildParams& P, uint64_t 
     for (int k = 0; k < kPlaceRegPer; k++) mine[k] = pre[k];
   }
   const Status* st = P.st;
-  const unsigned ovf = st->overflow | st->p2_overflow, full = st->full;
+  const unsigned ovf = st->overflow | st->p2_overflow | (P.abort_on_fail ? st->spec_fail : 0u), full = st->full;
   const unsigned long long nrec = st->n_records, ndel = st->n_deletes, npairs0 = st->n_pairs;
+  const bool failed = P.abort_on_fail && st->err != ~0ull;
   const uint64_t b = P.b_lo + bi;
   const uint32_t n = P.bcount[b];
   const uint64_t eoff = P.boff[b];
@@ -2097,7 +2134,7 @@ __device__ __forceinline__ void place_reg_bucket(const BuildParams& P, uint64_t 
   } else {
     x = P.carry[b];
   }
-  if (ovf != 0 || nrec > P.max_records) return;  // build_aborted
+  if (ovf != 0 || failed || nrec > P.max_records) return;  // build_aborted
   if (P.fused_carry && tid == 0) P.carry[b] = x;  // (for the global-memory placement's readers)
   const uint64_t start = b << kBucketShift;
   const int64_t bsize = (int64_t)min((uint64_t)kBucket, P.cap - start);
@@ -2118,13 +2155,17 @@ __device__ __forceinline__ void place_reg_bucket(const BuildParams& P, uint64_t 
   if (tid == 0) s_pend = 0;
   __syncthreads();
   uint32_t want[kPlaceRegPer], cur[kPlaceRegPer];
+  bool bad = false;  // (kGuardForeign: an entry of another bucket in this bucket's region)
 #pragma unroll
   for (int k = 0; k < kPlaceRegPer; k++) {
     const uint32_t i = tid + k * kPlaceRegBlock;
-    want[k] = i < n ? (uint32_t)(fast_mod(mine[k].hash, P.mod) - start) : (uint32_t)kBucket;  // (kBucket: past n)
+    const uint64_t w = fast_mod(mine[k].hash, P.mod) - start;
+    bad |= i < n && w >= (uint64_t)kBucket;
+    want[k] = i < n && w < (uint64_t)kBucket ? (uint32_t)w : (uint32_t)kBucket;  // (kBucket: past n, or foreign)
     const uint32_t sh = (want[k] & 1u) * 16u;
     cur[k] = (atomicAdd(&cnt[want[k] >> 1], 1u << sh) >> sh) & 0xffffu;
   }
+  report_foreign(P, bad);
   __syncthreads();
   // scan of slots 4 tid .. 4 tid + 3: base (exclusive count) and M (prefix max of s - base[s] over
   // occupied s), one barrier: a wave's max of (s - its local base) needs only the waves' sums after it
@@ -2388,6 +2429,17 @@ __global__ __launch_bounds__(kPlaceRegBlock) void k_place_reg(BuildParams P) {
   place_reg_bucket<kFixed>(P, blockIdx.x, pre);
 }
 
+// (inject_foreign switch: tests of kGuardForeign) The first entry of digit 0's region (ent3, before
+// pass 2: where 1) or of the range's first bucket region (ent2, before the placement: where 2) becomes
+// an entry of the table's last bucket -- a region whose contents disagree with its count, as a bug or
+// a half-written region would leave it.  Its hash is below the capacity, so it wants slot hash.
+__global__ void k_inject_foreign(BuildParams P, int where) {
+  if (threadIdx.x || blockIdx.x || P.nbuckets < 2 || build_aborted(P)) return;
+  const uint64_t h = (P.nbuckets - 1) << kBucketShift;
+  if (where == 1 && P.p1_region && P.p1_fill[0] > 0) P.ent3[0].hash = h;
+  if (where == 2 && P.p2_fixed && P.bcount[P.b_lo] > 0) P.ent2[0].hash = h;
+}
+
 // ================================================================================================
 // launchers
 // ================================================================================================
@@ -2489,6 +2541,10 @@ void launch_partition(const BuildParams& P, hipStream_t s, StageTimer* tm) {
   else
     hipLaunchKernelGGL(k_part2, dim3(256), dim3(kPart2Block), (size_t)(2u * P.bpp) * sizeof(uint32_t), s, P);
   tm->mark("partition", s);
+}
+
+void launch_inject_foreign(const BuildParams& P, hipStream_t s, int where) {
+  hipLaunchKernelGGL(k_inject_foreign, dim3(1), dim3(64), 0, s, P, where);
 }
 
 void launch_place_buckets(const BuildParams& P, hipStream_t s) {

@@ -17,9 +17,21 @@ namespace sk {
 // skipped (its offsets would run past the buffers) and the host redoes the build with more room.
 __device__ __forceinline__ bool build_aborted(const BuildParams& P) {
   // (p2_overflow: the fixed bucket regions did not hold a bucket; the host redoes the build)
-  // (abort_on_fail: a sharded bin right after a speculative framing attempt that did not hold)
+  // (abort_on_fail: the single-GPU build loop, whose host discards an attempt whose framing failed or
+  //  stopped early, and a sharded bin right after a speculative framing attempt that did not hold --
+  //  no stage consumes a region the framing left half-written)
   return P.st->overflow != 0 || P.st->n_records > P.max_records || P.st->p2_overflow != 0 ||
          (P.abort_on_fail && (P.st->spec_fail != 0 || P.st->err != ~0ull));
+}
+
+// An entry whose bucket lies outside the buckets its workgroup owns (a digit or bucket region whose
+// contents disagree with its count).  That is a bug, never a property of the input: the entry is
+// dropped before any LDS or global index is formed from it, st->guard gets kGuardForeign, and the host
+// fails the build with SPARKEY_E_GPU (as IndexHash.put checks its bounds before it touches the table,
+// IndexHash.java:574-576).  Kernels keep a per-thread flag and report it once.
+constexpr unsigned kGuardForeign = 0x100u;
+__device__ __forceinline__ void report_foreign(const BuildParams& P, bool bad) {
+  if (bad) atomicOr(&P.st->guard, kGuardForeign);
 }
 
 __device__ __forceinline__ void set_error(Status* st, int64_t pos, int code) {

@@ -48,6 +48,8 @@ enum class Knob : int {
   FileDebug,        // file entry points: phase times to stderr
   ReframeSpinTicks, // FrameSpinTicks for the exact path's second framing only (tests of its fallbacks)
   ShardGatherCompressed,  // num_gpus > 1: compressed logs gathered on every rank (the sharded path off)
+  InjectForeign,    // tests of the kGuardForeign check: a foreign entry in digit region 0 (1) or bucket region 0 (2)
+  ShardCollFail,    // host transport (HostColl): the k-th collective of a communicator fails its device copy (tests)
   kCount
 };
 

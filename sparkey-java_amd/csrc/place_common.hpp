@@ -16,10 +16,13 @@ __device__ __forceinline__ void bucket_histogram(const BuildParams& P, uint64_t 
                                                  uint64_t start, uint32_t* cnt) {
   for (int t = threadIdx.x; t < kBucket; t += kPlaceBlock) cnt[t] = 0;
   __syncthreads();
+  bool bad = false;  // (kGuardForeign: the entry is left out here and in the sort below)
   for (uint32_t i = threadIdx.x; i < n; i += kPlaceBlock) {
     const uint64_t w = fast_mod(P.ent2[eoff + i].hash, P.mod) - start;
-    atomicAdd(&cnt[w], 1u);
+    if (w < (uint64_t)kBucket) atomicAdd(&cnt[w], 1u);
+    else bad = true;
   }
+  report_foreign(P, bad);
   __syncthreads();
 }
 
@@ -76,6 +79,7 @@ __device__ inline void place_bucket_global(const BuildParams& P, uint64_t b, int
   for (uint32_t i = tid; i < n; i += kPlaceBlock) {
     const Entry en = P.ent2[eoff + i];
     const uint64_t w = fast_mod(en.hash, P.mod) - start;
+    if (w >= (uint64_t)kBucket) continue;  // (foreign: reported by bucket_histogram)
     const uint32_t r = atomicAdd((uint32_t*)&slot_of[w], 1u);
     P.ent3[eoff + base[w] + r] = en;
   }

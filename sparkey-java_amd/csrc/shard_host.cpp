@@ -296,7 +296,7 @@ class HostColl : public Coll {
     // A rank whose own rows cannot leave the device still takes part, with all-ones rows: the peers
     // do not block in the transport, and a row whose code words read -1 fails every rank at the next
     // checkpoint (fail_together).  (A peer that never arrives is the transport's to time out.)
-    const int rc = copy(h, d_send, bytes, hipMemcpyDeviceToHost, s, why);
+    const int rc = injected(why) ? SPARKEY_E_GPU : copy(h, d_send, bytes, hipMemcpyDeviceToHost, s, why);
     if (rc) memset(h, 0xff, bytes);
     if (t_.all_gather(t_.ctx, h, h + bytes, bytes) != 0) return rc ? rc : err(why, "host transport all_gather failed");
     if (rc) return rc;
@@ -311,7 +311,7 @@ class HostColl : public Coll {
     }
     uint8_t* h = stage(sb + rb);
     if (!h) return err(why, "pinned staging allocation failed");
-    const int rc = copy(h, d_send, sb, hipMemcpyDeviceToHost, s, why);  // (as all_gather: take part anyway)
+    const int rc = injected(why) ? SPARKEY_E_GPU : copy(h, d_send, sb, hipMemcpyDeviceToHost, s, why);  // (as all_gather: take part anyway)
     if (rc) memset(h, 0xff, sb);
     if (t_.all_to_all(t_.ctx, h, send_bytes, h + sb, recv_bytes) != 0) return rc ? rc : err(why, "host transport all_to_all failed");
     if (rc) return rc;
@@ -338,9 +338,17 @@ class HostColl : public Coll {
       return err(why, "staging copy failed");
     return SPARKEY_OK;
   }
+  // (shard_coll_fail switch, tests: the k-th collective of this communicator fails its device copy,
+  //  counted from 1 over its lifetime)
+  bool injected(std::string* why) {
+    if (sk::knob(sk::Knob::ShardCollFail) != (int64_t)++calls_) return false;
+    *why = "staging copy failed (shard_coll_fail)";
+    return true;
+  }
   sparkey_shard_transport t_;
   uint8_t* h_ = nullptr;
   uint64_t cap_ = 0;
+  uint64_t calls_ = 0;
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -501,8 +509,12 @@ class Rank {
       if (codes[r]) {
         if (r == g_) return own ? own : (int)codes[r];  // (its own message is in err_)
         if (own) return own;
-        return fail((int)codes[r], std::string("another rank of the sharded build failed (rank ") + std::to_string(r) +
-                                       ": " + code_text((int)codes[r]) + ")");
+        // (-1 from a peer is HostColl's all-ones row: its row could not leave its device.  No step after
+        //  the header checks -- which every rank makes alike before any collective -- returns
+        //  SPARKEY_E_NOT_LOG.)
+        const int code = codes[r] == -1 ? SPARKEY_E_GPU : (int)codes[r];
+        return fail(code, std::string("another rank of the sharded build failed (rank ") + std::to_string(r) + ": " +
+                              (codes[r] == -1 ? "its row could not leave its device" : code_text(code)) + ")");
       }
     return SPARKEY_OK;
   }
@@ -1144,9 +1156,12 @@ int Rank::run(const uint8_t* hdr, uint64_t file_len, const uint8_t* d_buf, uint6
     if (!rc) rc = to_host(R.data(), cm_->rows.p, (uint64_t)G_ * RL * 8);
     if (rc) return rc;
     {
+      // a failed rank: retry -2 with its code (post_failure), or -1 when its row could not leave its
+      // device (HostColl's all-ones row); valid rows carry retry 0 or 1
       std::vector<int64_t> codes(G_, 0);
       for (int r = 0; r < G_; r++)
-        if (R[(size_t)r * RL + 7] == -2) codes[r] = R[(size_t)r * RL + 5] ? R[(size_t)r * RL + 5] : SPARKEY_E_GPU;
+        if (R[(size_t)r * RL + 7] < 0)
+          codes[r] = R[(size_t)r * RL + 7] == -2 && R[(size_t)r * RL + 5] ? R[(size_t)r * RL + 5] : SPARKEY_E_GPU;
       rc = fail_together(codes, own);
       if (rc) return rc;
     }
@@ -1215,10 +1230,14 @@ int Rank::run(const uint8_t* hdr, uint64_t file_len, const uint8_t* d_buf, uint6
   rc = agree(have ? cz_rc : fail(SPARKEY_E_GPU, "hipMalloc failed"));
   if (rc) return rc;
   const uint8_t* recv = nullptr;
+  // A collective that fails on this rank from here to the finish rows does not end its part: it skips
+  // its device steps, posts neutral rows and its code, and joins every collective up to the finish-row
+  // all_gather, where every rank fails together (its peers would otherwise wait in a collective it
+  // never enters).  xrc: this rank's failure so far.
+  int xrc = SPARKEY_OK;
   if (G_ > 1) {
     std::string why;
-    rc = coll_rc(c_->all_to_all(send, sb.data(), rv, rb.data(), s_, &why), why);
-    if (rc) return rc;
+    xrc = coll_rc(c_->all_to_all(send, sb.data(), rv, rb.data(), s_, &why), why);
     recv = rv;
   }
   mark("all_to_all");
@@ -1233,16 +1252,15 @@ int Rank::run(const uint8_t* hdr, uint64_t file_len, const uint8_t* d_buf, uint6
     // (posting a neutral row can itself fail; the rank then still takes part in the collectives up to
     //  the finish rows, so that no peer waits in one it never enters, and returns that failure there)
     int post_rc = SPARKEY_OK;
-    int lrc = sparkey_shard_summarize_dev(pl_, recv, n_recv, digits, RL, fixed ? 1 : 0, (int64_t*)fun, s_, err_, err_len_);
+    int lrc = xrc ? xrc
+                  : sparkey_shard_summarize_dev(pl_, recv, n_recv, digits, RL, fixed ? 1 : 0, (int64_t*)fun, s_, err_, err_len_);
     if (lrc) post_rc = gpu(hipMemsetAsync(fun, 0, 16, s_), "memset");
-    rc = all_gather(fun, cm_->funs, 16);
-    if (rc) return rc;
+    if (const int crc = all_gather(fun, cm_->funs, 16)) lrc = lrc ? lrc : crc;  // (joins the rest regardless)
     if (!lrc)
       lrc = sparkey_shard_place_dev(pl_, (const int64_t*)cm_->funs.p, d_out + hdr_off, spill, spill_cap, (int64_t*)flags,
                                     kSpillInline, s_, err_, err_len_);
     if (lrc && !post_rc) post_rc = gpu(hipMemsetAsync(flags, 0, (uint64_t)FL * 8, s_), "memset");
-    rc = all_gather(flags, cm_->frows, (uint64_t)FL * 8);
-    if (rc) return rc;
+    if (const int crc = all_gather(flags, cm_->frows, (uint64_t)FL * 8)) lrc = lrc ? lrc : crc;
     if (!lrc) lrc = sparkey_shard_finish_dev(pl_, (const int64_t*)cm_->frows.p, FL, kSpillInline, (int64_t*)fin, s_, err_, err_len_);
     if (lrc) {
       int64_t f[12] = {0};

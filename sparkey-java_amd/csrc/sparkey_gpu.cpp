@@ -1367,9 +1367,15 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
       pl->epoch = pl->epoch % ((1u << 22) - 1) + 1;
       P.epoch = pl->epoch;
     }
+    // an attempt whose framing failed, stopped early or overflowed skips every later stage (the host
+    // redoes it or reports the error): no stage reads a region the framing left half-written
+    P.abort_on_fail = 1;
     rc = launch_framing(pl, P, framing_path, s, err, err_len);
     if (rc) return rc;
+    const int64_t inject = knob(Knob::InjectForeign);
+    if (inject == 1) launch_inject_foreign(P, s, 1);
     launch_partition(P, s, &pl->timer);
+    if (inject == 2) launch_inject_foreign(P, s, 2);
     launch_place_fast(P, s, &pl->timer);
     // (the folded stats' last block also hands the host its status: no k_status_out launch)
     P.status_host = P.fold_stats ? pl->h_status_dev : nullptr;
@@ -1383,6 +1389,10 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
     HIP_TRY(hipEventElapsedTime(&ms, pl->ev0, pl->ev1));
     print_frame_debug(pl, P);
     print_part2_debug(P);
+    if (st.guard) {  // (a bounds check tripped: a bug, never a property of the input -- no retry)
+      set_err(err, err_len, "internal error: partition/placement bounds check tripped (bits " + std::to_string(st.guard) + ")");
+      return SPARKEY_E_GPU;
+    }
     if (slab_framing(framing_path) && st.max_wave_count > slab_cap) {  // a wave overflowed its slab
       slab_cap = (uint32_t)std::min<uint64_t>(kPartTile, ((uint64_t)st.max_wave_count + 63) & ~63ull);
       continue;
@@ -1419,18 +1429,18 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
     }
     break;
   }
+  P.abort_on_fail = 0;  // (the exact path's stages report their own errors, at the lowest log position)
   rc = status_error(st, err, err_len);
   if (rc) return rc;
-  if (st.guard) {
-    set_err(err, err_len, "internal error: placement check tripped (bits " + std::to_string(st.guard) + ")");
-    return SPARKEY_E_GPU;
-  }
   if (st.overflow || st.spec_fail) {
     set_err(err, err_len, "Corrupt log file: framing did not converge");
     return SPARKEY_E_CORRUPT_LOG;
   }
   if (st.stats_pending && !(st.n_deletes > 0 || st.dup || st.dup_overflow || st.full || st.n_pairs > P.pair_cap)) {
-    // folded stats did not cover every slot (a bucket was placed by the global kernel): the pass
+    // folded stats did not cover every slot (a bucket was placed by the global kernel): the pass.
+    // The status is read again after it, which this branch needs for correctness: k_stats_folded's
+    // block 0 hands the status over as soon as it sees stats_pending, while other blocks may still be
+    // verifying equal-hash pairs (st->dup).
     float ms2 = 0.f;
     HIP_TRY(hipEventRecord(pl->ev0, s));
     launch_stats(P, s, 0, &pl->timer);

@@ -120,17 +120,39 @@ def test_gather_switch(native, switch):
 @pytest.mark.parametrize("n", [2, 3])
 def test_spanning_records(native, n):
     """Values up to 5000 bytes over 512-byte blocks: records span blocks; a rank boundary inside one
-    gathers the log, elsewhere the ranks shard it."""
+    gathers the log (sharded 3), elsewhere the ranks shard it (sharded 1) -- either way the oracle's
+    bytes.  The two cases are pinned one by one below."""
     rng = random.Random(3)
-    check(native, _compressed(_ops(rng, 1500, 10 ** 9, 0.0, 5000), 512), n, seed=21)
+    st = check(native, _compressed(_ops(rng, 1500, 10 ** 9, 0.0, 5000), 512), n, seed=21)
+    assert st.sharded in (1, 3), st.as_dict()
+
+
+def test_boundary_between_records_shards(native):
+    """Records shorter than the block never span one (CompressedWriter flushes first), so the rank
+    boundary falls between records: the ranks shard the log."""
+    rng = random.Random(4)
+    check(native, _compressed(_ops(rng, 3000, 10 ** 9, 0.0, 100), 512), 2, seed=22, sharded=1)
+
+
+def test_boundary_inside_spanning_record_gathers(native):
+    """One 200 KB record spanning about 400 blocks between a few small ones: the 2-rank boundary falls
+    inside it, a record no rank's slice can end, so the ranks gather the log."""
+    rng = random.Random(6)
+    ops = [("put", b"a%d" % i, b"x%d" % i) for i in range(5)]
+    ops.append(("put", b"big", bytes(rng.randrange(256) for _ in range(200000))))
+    ops += [("put", b"b%d" % i, b"y%d" % i) for i in range(5)]
+    check(native, _compressed(ops, 512), 2, seed=23, sharded=3)
 
 
 def test_small_and_empty(native):
-    check(native, CompressedLog(1024).finish(), 2)
+    """An empty log and a 20-record log (fewer blocks than some ranks' ranges): the oracle's bytes."""
+    st = check(native, CompressedLog(1024).finish(), 2)
+    print("empty:", st.sharded)
     cl = CompressedLog(1024)
     for i in range(20):
         cl.put(b"k%d" % i, b"v")
-    check(native, cl.finish(), 3)
+    st = check(native, cl.finish(), 3)
+    print("20 records:", st.sharded)
 
 
 def test_corrupt_block_is_the_single_gpu_error(native):

@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B of library builds (ablib/NAME.so) and switch settings (gpurun): one bench line per variant,
-# interleaved, ROUNDS rounds.  usage: r05_ab.sh TAG "bench args" NAME[:switches] ...
+# interleaved, ROUNDS rounds.  usage: ab.sh TAG "bench args" NAME[:switches] ...
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp

@@ -1,8 +1,8 @@
 #!/bin/bash
-# Round-5 checkpoint on the GPU (gpurun): the whole -m gpu suite, then smoke().
+# Checkpoint on the GPU (gpurun): the whole -m gpu suite, then smoke().
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-O=gpurun_out/${1:-r05full}; mkdir -p $O
+O=gpurun_out/${1:-full}; mkdir -p $O
 timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 || { tail -40 $O/pytest.log; exit 1; }
 tail -3 $O/pytest.log
 timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }

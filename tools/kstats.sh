@@ -1,6 +1,6 @@
 #!/bin/bash
 # Per-kernel stats of one bench workload for library variants (gpurun):
-#   r05_kstats.sh TAG "bench args" NAME ...   -> gpurun_out/TAG/NAME_kernel_stats.csv
+#   kstats.sh TAG "bench args" NAME ...   -> gpurun_out/TAG/NAME_kernel_stats.csv
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp

@@ -5,7 +5,7 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-O=gpurun_out/${1:-r05rehearse8}; mkdir -p $O
+O=gpurun_out/${1:-rehearse8}; mkdir -p $O
 ( while sleep 50; do echo "alive $(date +%T)" >> $O/heartbeat.txt; done ) &
 HB=$!
 rc=0

@@ -1,6 +1,6 @@
 #!/bin/bash
 # SQ issue/wait counters of one kernel (gpurun): where its waves' cycles go.
-# usage: r05_sq.sh TAG KERNEL "bench args" [lib]   (lib: a build in ablib/, default the in-tree one)
+# usage: sq.sh TAG KERNEL "bench args" [lib]   (lib: a build in ablib/, default the in-tree one)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
