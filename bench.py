@@ -690,6 +690,7 @@ def sharded(args, dev, world, rank):
         assert info["sharded"] == 1 and info["num_entries"] == n_total, info
     identical = None
     check_s = None
+    one_gpu_ms = None
     if not args.no_check:  # every rank's slice against ONE single-GPU build of the whole log (rank 0)
         t_c = time.time()
         mine = (info.get("out_offset", out_off), int(out.numel()), block_sums(out))
@@ -712,7 +713,17 @@ def sharded(args, dev, world, rank):
             size = _native.index_size(header, opts)
             d_spi = torch.empty(size, dtype=torch.uint8, device=dev)
             p1 = _native.Plan(dev.index)
-            p1.build(header, d_full.data_ptr(), d_full.numel(), d_spi.data_ptr(), size, opts)
+            p1.build(header, d_full.data_ptr(), d_full.numel(), d_spi.data_ptr(), size, opts)  # (also the warm-up)
+            # the same whole log built on ONE GPU, timed as the sharded builds are (host clock around
+            # finished builds): the denominator of the N-GPU speed-up (IndexHash.java:131-167: one call,
+            # one index)
+            k1 = max(1, min(args.steps, 5))
+            torch.cuda.synchronize(dev)
+            t1 = time.perf_counter()
+            for _ in range(k1):
+                p1.build(header, d_full.data_ptr(), d_full.numel(), d_spi.data_ptr(), size, opts)
+            torch.cuda.synchronize(dev)
+            one_gpu_ms = (time.perf_counter() - t1) * 1000.0 / k1
             p1.close()
             del d_full
             bad = [r for r, (off, ln, sums) in enumerate(pieces) if block_sums(d_spi[off:off + ln]) != sums]
@@ -760,6 +771,15 @@ def sharded(args, dev, world, rank):
                      "algorithmic_bytes_per_launch": b_alg_per_gpu, "avg_launch_ms": ms_per_step},
         "phase_ms_rank0": {k: v / args.steps for k, v in phases.items()},
         "bit_identical_to_single_gpu": identical,
+        # the same N x entries log built whole on one GPU (rank 0, after the timed region): what N GPUs
+        # buy over one for ONE index (a strong-scaling reference; the driver's own scaling figure is
+        # the weak-scaling curve of `value` over N)
+        "one_gpu_same_log": None if one_gpu_ms is None else {
+            "ms": one_gpu_ms, "keys_per_s": n_total / (one_gpu_ms * 1e-3),
+            "speedup_n_gpus_over_one": one_gpu_ms / ms_per_step,
+            "speedup_per_gpu": one_gpu_ms / ms_per_step / world,
+            "note": ("ranks share one GPU (gloo rehearsal): the sharded time is not an N-GPU time"
+                     if shared_gpu else "one GPU of this node, same log, same plan options")},
         "check_s": check_s,
         "device_used_gb_after_timed_builds": device_used_gb,
         "cpu_baseline": None,
@@ -788,7 +808,8 @@ def main():
     ap.add_argument("--no-check", action="store_true",
                     help="sharded: skip comparing the .spi with a single-GPU build (done after the timed region)")
     ap.add_argument("--orchestrator", default="cpp", choices=["cpp", "python"],
-                    help="sharded: the C-ABI's sparkey_shard_build (C++) or sparkey/sharded.py over torch.distributed")
+                    help="sharded: the C-ABI's sparkey_shard_build (C++, the product) or sparkey/sharded.py over "
+                         "torch.distributed (the test-only reference orchestrator; it gathers compressed logs)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))

@@ -536,20 +536,40 @@ class Rank {
     cm_->phase.emplace_back(name, t - clock_);
     clock_ = t;
   }
-  // every rank's small int64 vector (same length on every rank) -> host rows
+  // every rank's small int64 vector (same length on every rank) -> host rows.  Every such gather is
+  // also a checkpoint: the row carries the rank's sticky failure (sticky_) as one more word, and a
+  // nonzero word in any row -- a failure recorded since the last checkpoint, or -1 from HostColl's
+  // all-ones row of a rank whose copy failed -- fails every rank here, together.
   int gather_i64(const std::vector<int64_t>& v, std::vector<int64_t>* out) {
-    const uint64_t b = v.size() * 8;
+    const size_t w = v.size() + 1;
+    const uint64_t b = w * 8;
+    std::vector<int64_t> row(v);
+    row.push_back(sticky_);
     uint8_t* sd = cm_->small_send.ensure(b);
     uint8_t* rd = cm_->small_recv.ensure(b * G_);
     if (!sd || !rd) return fail(SPARKEY_E_GPU, "hipMalloc failed");
-    int rc = gpu(hipMemcpyAsync(sd, v.data(), b, hipMemcpyHostToDevice, s_), "H2D");
+    int rc = gpu(hipMemcpyAsync(sd, row.data(), b, hipMemcpyHostToDevice, s_), "H2D");
     std::string why;
     if (!rc) rc = coll_rc(c_->all_gather(sd, rd, b, s_, &why), why);
-    out->assign(v.size() * G_, 0);
-    if (!rc) rc = gpu(hipMemcpyAsync(out->data(), rd, b * G_, hipMemcpyDeviceToHost, s_), "D2H");
+    std::vector<int64_t> all(w * G_, 0);
+    if (!rc) rc = gpu(hipMemcpyAsync(all.data(), rd, b * G_, hipMemcpyDeviceToHost, s_), "D2H");
     if (!rc) rc = gpu(hipStreamSynchronize(s_), "sync");
+    out->assign(v.size() * G_, 0);
+    if (rc) return sticky_ ? sticky_ : rc;
+    std::vector<int64_t> codes(G_);
+    for (int r = 0; r < G_; r++) {
+      for (size_t i = 0; i + 1 < w; i++) (*out)[(size_t)r * v.size() + i] = all[(size_t)r * w + i];
+      codes[r] = all[(size_t)r * w + w - 1];
+    }
+    return fail_together(codes, sticky_);
+  }
+  // a failure after which this rank still joins the collectives up to the next gather_i64 (where every
+  // rank fails): it skips its device steps meanwhile (ok() false)
+  int note(int rc) {
+    if (rc && !sticky_) sticky_ = rc;
     return rc;
   }
+  bool ok() const { return sticky_ == SPARKEY_OK; }
   int all_gather(const void* d_send, DBuf& dst, uint64_t bytes) {
     uint8_t* rd = dst.ensure(bytes * G_);
     if (!rd) return fail(SPARKEY_E_GPU, "hipMalloc failed");
@@ -574,17 +594,19 @@ class Rank {
     uint8_t* pad = cm_->pad.ensure(m);
     uint8_t* rv = cm_->var_recv.ensure(m * G_);
     uint8_t* out = dst.ensure(tot + 16);
-    if (!pad || !rv || !out) return fail(SPARKEY_E_GPU, "hipMalloc failed");
-    if (n) rc = gpu(hipMemcpyAsync(pad, d_src, n, hipMemcpyDeviceToDevice, s_), "D2D");
+    // (after the count checkpoint: a failure is noted and the rank still joins the data gather; its
+    //  caller's next checkpoint fails every rank)
+    if (!pad || !rv || !out) note(fail(SPARKEY_E_GPU, "hipMalloc failed"));
+    if (ok() && n) note(gpu(hipMemcpyAsync(pad, d_src, n, hipMemcpyDeviceToDevice, s_), "D2D"));
     std::string why;
-    if (!rc) rc = coll_rc(c_->all_gather(pad, rv, m, s_, &why), why);
+    note(coll_rc(c_->all_gather(pad, rv, m, s_, &why), why));
     uint64_t at = 0;
-    for (int r = 0; r < G_ && !rc; r++) {
-      if (cnt[r]) rc = gpu(hipMemcpyAsync(out + at, rv + (uint64_t)r * m, (uint64_t)cnt[r], hipMemcpyDeviceToDevice, s_), "D2D");
+    for (int r = 0; r < G_ && ok(); r++) {
+      if (cnt[r]) note(gpu(hipMemcpyAsync(out + at, rv + (uint64_t)r * m, (uint64_t)cnt[r], hipMemcpyDeviceToDevice, s_), "D2D"));
       at += (uint64_t)cnt[r];
     }
     *total = tot;
-    return rc;
+    return SPARKEY_OK;  // (the count checkpoint's outcome; a later failure is sticky_)
   }
   int64_t fe(int r) const {  // sharded.py frame_end(r)
     if (r == G_ - 1) return F_.data_end;
@@ -617,18 +639,15 @@ class Rank {
   std::vector<bool> valid_;
   double clock_ = 0;
   const uint8_t* hdr_ = nullptr;
+  int sticky_ = SPARKEY_OK;  // this rank's failure since the last checkpoint (gather_i64)
 };
 
 int Rank::range_stats(uint64_t slot_lo, uint64_t slot_hi, std::vector<int64_t>* bnd) {
   const int nonempty = slot_hi > slot_lo ? 1 : 0;
   uint64_t b[4] = {0, 0, 0, 0};
-  int rc = sparkey_shard_boundary(pl_, s_, b, err_, err_len_);
-  if (rc) return rc;
+  if (ok()) note(sparkey_shard_boundary(pl_, s_, b, err_, err_len_));
   int64_t sx[3] = {0, 0, 0};
-  if (nonempty) {
-    rc = sparkey_shard_stats(pl_, 0, 0, s_, sx, err_, err_len_);
-    if (rc) return rc;
-  }
+  if (nonempty && ok()) note(sparkey_shard_stats(pl_, 0, 0, s_, sx, err_, err_len_));
   return gather_i64({signed64(b[0]), signed64(b[1]), signed64(b[2]), signed64(b[3]), nonempty, sx[0], sx[1], sx[2]}, bnd);
 }
 
@@ -664,10 +683,8 @@ void Rank::combine_stats(const std::vector<int64_t>& bnd, int stride, int off, i
 // (IndexHash.java:606-636: put compares the keys of equal hashes).
 int Rank::pairs_share_a_key(int64_t n_pairs, bool* dup_any) {
   std::vector<uint64_t> addrs((size_t)(2 * n_pairs));
-  if (n_pairs) {
-    const int rc = sparkey_shard_pairs(pl_, addrs.data(), (uint64_t)n_pairs, err_, err_len_);
-    if (rc) return rc;
-  }
+  if (n_pairs && note(sparkey_shard_pairs(pl_, addrs.data(), (uint64_t)n_pairs, err_, err_len_)))
+    n_pairs = 0;  // (noted: the checkpoint below fails every rank)
   const int64_t n2 = 2 * n_pairs;
   std::vector<int> owner((size_t)n2);
   for (int64_t i = 0; i < n2; i++) {
@@ -700,29 +717,27 @@ int Rank::pairs_share_a_key(int64_t n_pairs, bool* dup_any) {
     sb2[r] = (uint64_t)M[(size_t)r * G_ + g_] * rs;
     rb2[r] = (uint64_t)counts[r] * rs;
   }
+  // (from here to the closing checkpoint a failure is noted and the rank still joins both all_to_alls)
   uint8_t* dreq = cm_->req.ensure(std::max<uint64_t>(8, n2 * 8));
   uint8_t* dgot = cm_->got.ensure(std::max<uint64_t>(8, n_req * 8));
   uint8_t* drec = cm_->rec.ensure(std::max<uint64_t>(1, n_req) * rs);
   uint8_t* dback = cm_->back.ensure(std::max<int64_t>(1, n2) * rs);
-  if (!dreq || !dgot || !drec || !dback) return fail(SPARKEY_E_GPU, "hipMalloc failed");
-  if (n2) rc = gpu(hipMemcpyAsync(dreq, req.data(), n2 * 8, hipMemcpyHostToDevice, s_), "H2D");
+  if (!dreq || !dgot || !drec || !dback) note(fail(SPARKEY_E_GPU, "hipMalloc failed"));
+  if (ok() && n2) note(gpu(hipMemcpyAsync(dreq, req.data(), n2 * 8, hipMemcpyHostToDevice, s_), "H2D"));
   std::string why;
-  if (!rc) rc = coll_rc(c_->all_to_all(dreq, sb.data(), dgot, rb.data(), s_, &why), why);
-  if (!rc && n_req && virt_) rc = sk_cz_to_virtual(pl_, (uint64_t*)dgot, n_req, s_, err_, err_len_);
-  if (!rc && n_req) rc = sparkey_shard_fetch_keys(pl_, (const uint64_t*)dgot, n_req, drec, (uint32_t)rs, s_, err_, err_len_);
-  if (!rc) rc = coll_rc(c_->all_to_all(drec, sb2.data(), dback, rb2.data(), s_, &why), why);
-  if (rc) return rc;
+  note(coll_rc(c_->all_to_all(dreq, sb.data(), dgot, rb.data(), s_, &why), why));
+  if (ok() && n_req && virt_) note(sk_cz_to_virtual(pl_, (uint64_t*)dgot, n_req, s_, err_, err_len_));
+  if (ok() && n_req) note(sparkey_shard_fetch_keys(pl_, (const uint64_t*)dgot, n_req, drec, (uint32_t)rs, s_, err_, err_len_));
+  note(coll_rc(c_->all_to_all(drec, sb2.data(), dback, rb2.data(), s_, &why), why));
   int32_t dup = 0;
-  if (n_pairs) {  // the records back in pair order: pair i's address sits at request position inv[i]
+  if (ok() && n_pairs) {  // the records back in pair order: pair i's address sits at request position inv[i]
     std::vector<uint8_t> back((size_t)(n2 * rs)), recs((size_t)(n2 * rs));
-    rc = to_host(back.data(), dback, n2 * rs);
-    if (rc) return rc;
-    for (int64_t i = 0; i < n2; i++) memcpy(&recs[(size_t)(order[i] * rs)], &back[(size_t)(i * rs)], (size_t)rs);
-    uint8_t* drecs = cm_->recs.ensure(n2 * rs);
-    if (!drecs) return fail(SPARKEY_E_GPU, "hipMalloc failed");
-    rc = gpu(hipMemcpyAsync(drecs, recs.data(), n2 * rs, hipMemcpyHostToDevice, s_), "H2D");
-    if (!rc) rc = sparkey_shard_compare_keys(pl_, drecs, (uint64_t)n_pairs, (uint32_t)rs, s_, &dup, err_, err_len_);
-    if (rc) return rc;
+    rc = note(to_host(back.data(), dback, n2 * rs));
+    for (int64_t i = 0; i < n2 && !rc; i++) memcpy(&recs[(size_t)(order[i] * rs)], &back[(size_t)(i * rs)], (size_t)rs);
+    uint8_t* drecs = rc ? nullptr : cm_->recs.ensure(n2 * rs);
+    if (!rc && !drecs) rc = note(fail(SPARKEY_E_GPU, "hipMalloc failed"));
+    if (!rc) rc = note(gpu(hipMemcpyAsync(drecs, recs.data(), n2 * rs, hipMemcpyHostToDevice, s_), "H2D"));
+    if (!rc) note(sparkey_shard_compare_keys(pl_, drecs, (uint64_t)n_pairs, (uint32_t)rs, s_, &dup, err_, err_len_));
   }
   std::vector<int64_t> d;
   rc = gather_i64({dup != 0 ? 1 : 0}, &d);
@@ -738,11 +753,12 @@ int Rank::exact(uint8_t* out, uint64_t hdr_off, int64_t n_records, const sparkey
   *done = false;
   const uint64_t cap = geo_.cap;
   const uint64_t ss = (uint64_t)geo_.slot;
+  // (a failure between two checkpoints is noted and the rank joins the collectives up to the next
+  //  gather_i64, which fails every rank together)
   int64_t fe_slot = -1;
-  int rc = sparkey_shard_first_empty(pl_, s_, &fe_slot, err_, err_len_);
-  if (rc) return rc;
+  if (note(sparkey_shard_first_empty(pl_, s_, &fe_slot, err_, err_len_))) fe_slot = -1;
   std::vector<int64_t> E;
-  rc = gather_i64({fe_slot}, &E);
+  int rc = gather_i64({fe_slot}, &E);
   if (rc) return rc;
   std::vector<int> have;
   for (int r = 0; r < G_; r++)
@@ -755,18 +771,17 @@ int Rank::exact(uint8_t* out, uint64_t hdr_off, int64_t n_records, const sparkey
     ranges[have[i]] = {a, b <= a ? b + cap : b};
   }
   // every record (PUT and DELETE) with its header and key to the owner of its wanted slot's range
-  std::vector<uint64_t> counts(G_);
-  rc = sparkey_shard_exact_frame(pl_, entries_[g_], fe(g_), n_records, E.data(), s_, counts.data(), err_, err_len_);
-  if (rc) return rc;
+  std::vector<uint64_t> counts(G_, 0);
+  if (note(sparkey_shard_exact_frame(pl_, entries_[g_], fe(g_), n_records, E.data(), s_, counts.data(), err_, err_len_)))
+    std::fill(counts.begin(), counts.end(), 0);
   uint64_t n_send = 0;
   for (uint64_t v : counts) n_send += v;
   uint8_t* send = cm_->exsend.ensure(std::max<uint64_t>(1, n_send) * rs);
-  if (!send) return fail(SPARKEY_E_GPU, "hipMalloc failed");
-  rc = sparkey_shard_exact_pack(pl_, send, cm_->exsend.cap, s_, err_, err_len_);
+  if (!send) note(fail(SPARKEY_E_GPU, "hipMalloc failed"));
+  if (ok()) note(sparkey_shard_exact_pack(pl_, send, cm_->exsend.cap, s_, err_, err_len_));
   // a compressed log framed as its virtual log: the records' addresses to the compressed log's (the
   // replay orders by receive-buffer offset; the address field is what the extract writes)
-  if (!rc && virt_) rc = sk_cz_to_real(pl_, send, n_send, (uint32_t)rs, s_, err_, err_len_);
-  if (rc) return rc;
+  if (ok() && virt_) note(sk_cz_to_real(pl_, send, n_send, (uint32_t)rs, s_, err_, err_len_));
   std::vector<int64_t> M;
   rc = gather_i64(std::vector<int64_t>(counts.begin(), counts.end()), &M);
   if (rc) return rc;
@@ -780,16 +795,14 @@ int Rank::exact(uint8_t* out, uint64_t hdr_off, int64_t n_records, const sparkey
   const uint8_t* recv = send;
   if (G_ > 1) {
     uint8_t* rv = cm_->exrecv.ensure(std::max<uint64_t>(1, n_recv) * rs);
-    if (!rv) return fail(SPARKEY_E_GPU, "hipMalloc failed");
+    if (!rv) note(fail(SPARKEY_E_GPU, "hipMalloc failed"));
     std::string why;
-    rc = coll_rc(c_->all_to_all(send, sb.data(), rv, rb.data(), s_, &why), why);
-    if (rc) return rc;
+    note(coll_rc(c_->all_to_all(send, sb.data(), rv, rb.data(), s_, &why), why));
     recv = rv;
   }
   sparkey_shard_exact_result rep;
   memset(&rep, 0, sizeof(rep));
-  rc = sparkey_shard_exact_build(pl_, n_recv ? recv : nullptr, n_recv, s_, &rep, err_, err_len_);
-  if (rc) return rc;
+  if (ok()) note(sparkey_shard_exact_build(pl_, n_recv ? recv : nullptr, n_recv, s_, &rep, err_, err_len_));
   std::vector<int64_t> rows;
   rc = gather_i64({rep.rc, rep.err_pos, rep.num_entries, rep.garbage_size}, &rows);
   if (rc) return rc;
@@ -829,10 +842,7 @@ int Rank::exact(uint8_t* out, uint64_t hdr_off, int64_t n_records, const sparkey
   };
   const std::vector<Piece> mine = pieces(g_);
   for (const Piece& p : mine)
-    if (p.q == g_) {
-      rc = sparkey_shard_exact_extract(pl_, p.u, p.v, out + hdr_off + (p.u - slot_lo) * ss, s_, err_, err_len_);
-      if (rc) return rc;
-    }
+    if (p.q == g_ && ok()) note(sparkey_shard_exact_extract(pl_, p.u, p.v, out + hdr_off + (p.u - slot_lo) * ss, s_, err_, err_len_));
   if (G_ > 1) {
     std::vector<uint64_t> to(G_, 0), frm(G_, 0), at(G_, 0);
     for (const Piece& p : mine)
@@ -843,11 +853,10 @@ int Rank::exact(uint8_t* out, uint64_t hdr_off, int64_t n_records, const sparkey
       tot += to[q];
     }
     uint8_t* send2 = cm_->send2.ensure(std::max<uint64_t>(1, tot));
-    if (!send2) return fail(SPARKEY_E_GPU, "hipMalloc failed");
+    if (!send2) note(fail(SPARKEY_E_GPU, "hipMalloc failed"));
     for (const Piece& p : mine)
       if (p.q != g_) {
-        rc = sparkey_shard_exact_extract(pl_, p.u, p.v, send2 + at[p.q], s_, err_, err_len_);
-        if (rc) return rc;
+        if (ok()) note(sparkey_shard_exact_extract(pl_, p.u, p.v, send2 + at[p.q], s_, err_, err_len_));
         at[p.q] += (p.v - p.u) * ss;
       }
     uint64_t rtot = 0;
@@ -858,22 +867,20 @@ int Rank::exact(uint8_t* out, uint64_t hdr_off, int64_t n_records, const sparkey
       rtot += frm[r];
     }
     uint8_t* recv2 = cm_->recv2.ensure(std::max<uint64_t>(1, rtot));
-    if (!recv2) return fail(SPARKEY_E_GPU, "hipMalloc failed");
+    if (!recv2) note(fail(SPARKEY_E_GPU, "hipMalloc failed"));
     std::string why;
-    rc = coll_rc(c_->all_to_all(send2, to.data(), recv2, frm.data(), s_, &why), why);
-    if (rc) return rc;
+    note(coll_rc(c_->all_to_all(send2, to.data(), recv2, frm.data(), s_, &why), why));
     uint64_t at2 = 0;
-    for (int r = 0; r < G_ && !rc; r++) {
+    for (int r = 0; r < G_ && ok(); r++) {
       if (r == g_) continue;
       for (const Piece& p : pieces(r))
-        if (p.q == g_) {
+        if (p.q == g_ && ok()) {
           const uint64_t nb = (p.v - p.u) * ss;
-          rc = gpu(hipMemcpyAsync(out + hdr_off + (p.u - slot_lo) * ss, recv2 + at2, nb, hipMemcpyDeviceToDevice, s_),
-                   "D2D");
+          note(gpu(hipMemcpyAsync(out + hdr_off + (p.u - slot_lo) * ss, recv2 + at2, nb, hipMemcpyDeviceToDevice, s_),
+                   "D2D"));
           at2 += nb;
         }
     }
-    if (rc) return rc;
   }
   std::vector<int64_t> bnd;
   rc = range_stats(slot_lo, slot_hi, &bnd);
@@ -914,6 +921,7 @@ int Rank::gathered(const uint8_t* hdr, uint64_t file_len, const uint8_t* d_buf, 
   uint64_t total = 0;
   int rc = gather_var(d_buf + (own_lo - buf_lo) * (n ? 1 : 0), n, cm_->glog, &total);
   if (rc) return rc;
+  if (!ok()) return sticky_;  // (no collective follows: this rank fails alone)
   if (total != file_len) return fail(SPARKEY_E_GPU, "gathered log has the wrong length");
   const uint64_t full_len = kIndexHeader + geo_.cap * geo_.slot;
   uint8_t* full = cm_->full.ensure(full_len);
@@ -1006,6 +1014,7 @@ int Rank::run(const uint8_t* hdr, uint64_t file_len, const uint8_t* d_buf, uint6
   cm_->phase.clear();
   clock_ = now_ms();
   hdr_ = hdr;
+  sticky_ = SPARKEY_OK;
   L_ = make_layout(hdr, G_);
   F_ = L_;
   virt_ = false;
@@ -1309,18 +1318,22 @@ int Rank::run(const uint8_t* hdr, uint64_t file_len, const uint8_t* d_buf, uint6
   if (max_spill > kSpillInline) {  // more spilled slots than the rows carry: exchange them all
     host_header = true;
     const uint64_t n_spill = (uint64_t)F[(size_t)g_ * 12];
+    // (a failure is noted and the rank joins the collectives up to the next checkpoint: gather_var's
+    //  count gather, or range_stats' / the exact path's first gather)
+    uint64_t n_send_spill = n_spill;
     if (n_spill > spill_cap) {
       spill_cap = n_spill;
       spill = cm_->spill.ensure(spill_cap * kSpillBytes);
-      if (!spill) return fail(SPARKEY_E_GPU, "hipMalloc failed");
-      rc = sparkey_shard_place_dev(pl_, (const int64_t*)cm_->funs.p, d_out + hdr_off, spill, spill_cap, (int64_t*)flags,
-                                   kSpillInline, s_, err_, err_len_);
-      if (rc) return rc;
+      if (!spill) note(fail(SPARKEY_E_GPU, "hipMalloc failed"));
+      if (ok()) note(sparkey_shard_place_dev(pl_, (const int64_t*)cm_->funs.p, d_out + hdr_off, spill, spill_cap,
+                                             (int64_t*)flags, kSpillInline, s_, err_, err_len_));
     }
+    if (!ok()) n_send_spill = 0;
     uint64_t total = 0;
-    rc = gather_var(spill, n_spill * kSpillBytes, cm_->var_out, &total);
-    if (!rc) rc = sparkey_shard_apply_spill(pl_, cm_->var_out.p, total / kSpillBytes, s_, err_, err_len_);
-    if (!rc && !is_exact) rc = range_stats(slot_lo, slot_hi, &bnd);
+    rc = gather_var(spill, n_send_spill * kSpillBytes, cm_->var_out, &total);
+    if (rc) return rc;
+    note(sparkey_shard_apply_spill(pl_, cm_->var_out.p, total / kSpillBytes, s_, err_, err_len_));
+    if (!is_exact) rc = range_stats(slot_lo, slot_hi, &bnd);
     if (rc) return rc;
   }
   mark("spill");

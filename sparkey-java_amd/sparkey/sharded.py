@@ -1,5 +1,12 @@
 """Sharded .spi build: one process per GPU, the log's byte range split across the ranks.
 
+REFERENCE ORCHESTRATOR, test and rehearsal use only.  The product orchestrator is the C++ one behind
+the C-ABI (csrc/shard_host.cpp: sparkey_shard_build, and sparkey_build_index_file / _mem with
+num_gpus > 1), which also shards SNAPPY / ZSTD logs by their block chain; this module
+gathers those on every rank.  It stays as an independent restatement of the same steps over
+torch.distributed, so that the CPU tests (gloo, tests/shard_sim.py) check the orchestration logic
+against the oracle, and `bench.py --orchestrator python` can compare the two.
+
 The reference build is single-threaded (Sparkey.java:36, IndexHash.createNew IndexHash.java:131-167);
 this module splits the same computation at the points where ranks must exchange data and runs the
 device steps of include/sparkey_gpu.h ("sharded build") in between:

@@ -5,7 +5,8 @@ gloo group (as `bench.py --gpus N --backend gloo` rehearses); the `shard_coll_fa
 part with an all-ones row (or, from the exchange on, joins every collective up to the finish rows), so
 for every k both ranks return an error -- none waits in a collective its peer never enters -- or, for k
 past the build's last collective, both succeed with the single-GPU bytes.  The group stays usable:
-the next k runs in the same processes.
+the next k runs in the same processes.  Every collective of the build is covered: the canonical steps'
+rows and exchanges, and the equal-hash key check's (200K keys: 32-bit hashes with collisions).
 """
 import datetime
 import os
@@ -19,7 +20,18 @@ from sharded_harness import free_port
 pytestmark = pytest.mark.gpu
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KS = list(range(1, 13))
+KS = list(range(1, 14))
+# progress lines (a GPU box kills a run that writes nothing for 3 minutes): gpurun_out/ on the box
+PROGRESS = os.path.join(ROOT, "gpurun_out", "host_coll_failure.log")
+
+
+def _progress(msg):
+    try:
+        os.makedirs(os.path.dirname(PROGRESS), exist_ok=True)
+        with open(PROGRESS, "a") as f:
+            f.write(msg + "\n")
+    except OSError:
+        pass
 
 
 def _worker(rank, world, port, q):
@@ -29,7 +41,9 @@ def _worker(rank, world, port, q):
     import torch
     import torch.distributed as dist
     from sparkey import _native, synth
-    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=60))
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=30))
+    _progress(f"rank {rank}: group up")
+    plan = None
     try:
         dev = torch.device("cuda", 0)
         log = synth.fixed_log(200_000, 16, 100, seed=3, file_id=0x77)
@@ -54,10 +68,16 @@ def _worker(rank, world, port, q):
             finally:
                 _native.debug_set("shard_coll_fail", None)
                 comm.close()
+            _progress(f"rank {rank}: k={k} {res[-1][1]} {res[-1][2]} {res[-1][3] if res[-1][1] == 'err' else ''}")
             dist.barrier()
         q.put((rank, off, res))
+    except Exception as e:  # noqa: BLE001  (reported to the parent at once instead of a silent exit)
+        import traceback
+        _progress(f"rank {rank}: fatal {e!r}")
+        q.put((rank, None, traceback.format_exc()))
     finally:
-        plan.close()
+        if plan is not None:
+            plan.close()
         dist.destroy_process_group()
 
 
@@ -71,9 +91,11 @@ def test_one_rank_collective_failure_fails_every_rank(native):
     for p in procs:
         p.start()
     out = {}
+    _progress("start")
     try:
         for _ in range(2):
-            r, off, res = q.get(timeout=240)
+            r, off, res = q.get(timeout=150)
+            assert off is not None, f"rank {r} failed: {res}"
             out[r] = (off, res)
     finally:
         for p in procs:
@@ -94,5 +116,9 @@ def test_one_rank_collective_failure_fails_every_rank(native):
         else:
             for off, piece in ((out[0][0], a[3]), (out[1][0], b[3])):
                 assert piece == want[off:off + len(piece)], k
-    assert failed >= 5, failed  # the frame rows, the checkpoints, the exchange and the placement rows
+    # the build's collectives: entries checkpoint, frame rows, buffers checkpoint, entry exchange, carry,
+    # flag and finish rows, then (32-bit hashes: equal-hash pairs) the pair counts, address and key
+    # exchanges and the verdict -- a failure in any of them fails both ranks
+    assert failed >= 11, failed
+    assert out[0][1][-2][1] == "ok"  # (k past the last collective: the build)
     assert out[0][1][-1][1] == "ok"  # (no switch: the build)
