@@ -2113,11 +2113,6 @@ __device__ __forceinline__ void place_reg_bucket(const BuildParams& P, uint64_t 
   __shared__ unsigned long long r_sum[NW], r_col[NW];
   __shared__ long long r_max[NW];
   __shared__ int32_t s_pend;
-  __shared__ uint16_t big_list[kPlaceLdsMax];       // buf index of each member of a group of 3 .. kGroupMax
-  __shared__ uint32_t big_n;
-  // by buf index: rank | pe << 15 | eqh << 14 (in cnt's space: the counts are dead once g[] is read)
-  uint16_t* big_rank = reinterpret_cast<uint16_t*>(cnt);
-  static_assert(sizeof(cnt) >= (kPlaceLdsMax + 1) * sizeof(uint16_t), "big_rank fits cnt");
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   Entry mine[kPlaceRegPer];
   constexpr bool fixed = kFixed;
@@ -2157,10 +2152,7 @@ __device__ __forceinline__ void place_reg_bucket(const BuildParams& P, uint64_t 
   // (the loads are in flight while the counts are cleared)
   for (int t = tid; t < kBucket / 2; t += kPlaceRegBlock) cnt[t] = 0;
   for (int t = tid; t < kBucket; t += kPlaceRegBlock) reinterpret_cast<uint32_t*>(slot_of)[t] = 0xffffffffu;
-  if (tid == 0) {
-    s_pend = 0;
-    big_n = 0;
-  }
+  if (tid == 0) s_pend = 0;
   __syncthreads();
   uint32_t want[kPlaceRegPer], cur[kPlaceRegPer];
   bool bad = false;  // (kGuardForeign: an entry of another bucket in this bucket's region)
@@ -2229,65 +2221,31 @@ __device__ __forceinline__ void place_reg_bucket(const BuildParams& P, uint64_t 
     buf[bw[k] + (valid ? cur[k] : 0u)] = mine[k];
   }
   __syncthreads();
-  // Equal wanted slots in address order (IndexHash.java:647-650, SortHelper's (wantedSlot, address)):
-  // each member's rank counts the members with smaller addresses, and pe says whether the member
-  // ranked just before it -- the occupant of the slot before its own -- has its hash (the (p - 1, p)
-  // pair of calculateMaxDisplacement, IndexHash.java:195-245).  A member of a pair (most groups of
-  // several at load 0.77) reads its partner; members of groups of 3 .. kGroupMax (about one entry in
-  // eight) go to a block list, one thread ranking each against its group; past kGroupMax (the exact
-  // path redoes the bucket) the insertion order stands in, a valid permutation, so the occupied slots
-  // stay exact.  (A loop over the wave's largest group for every entry cost about 30% of the
-  // kernel's VALU.)
+  // Equal wanted slots in address order: each member counts the members with smaller addresses.
   const bool want_pairs = ndel == 0 && npairs0 <= P.pair_cap;
   uint32_t npair = 0;
-  uint32_t rank[kPlaceRegPer];  // the rank | pe << 31
-  uint32_t eqh = 0;  // another member with this entry's hash (duplicate keys: rare)
-  const unsigned long long lt_lanes = (1ull << lane) - 1ull;
+  uint32_t rank[kPlaceRegPer];
+  // One loop per wave over its lanes' largest group (a wave-uniform trip count), selects instead of
+  // branches: per-lane loops' exec-mask bookkeeping made this kernel SALU-bound
+  uint32_t gl = 0;
 #pragma unroll
   for (int k = 0; k < kPlaceRegPer; k++) {
+    rank[k] = 0;
+    gl = max(gl, g[k] >= 2 ? g[k] : 0u);
     if (g[k] > kGroupMax && cur[k] == 0) atomicOr(&P.st->dup_overflow, 1u);
-    const bool two = g[k] == 2;
-    const Entry e = buf[bw[k] + (two ? (cur[k] ^ 1u) : cur[k])];  // the partner, or itself
-    const bool lt = two && (e.addr & ~kDelBit) < (mine[k].addr & ~kDelBit);
-    const bool heq = two && e.hash == mine[k].hash;  // (the two members' addresses differ)
-    rank[k] = g[k] > kGroupMax ? cur[k] : (lt ? 1u : 0u) | (lt && heq ? 1u << 31 : 0u);
-    eqh |= heq ? 1u : 0u;
-    const bool big = g[k] >= 3 && g[k] <= kGroupMax;
-    const unsigned long long m = __ballot(big);
-    uint32_t base = 0;
-    if (m && lane == 0) base = atomicAdd(&big_n, (uint32_t)__builtin_popcountll(m));
-    base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
-    if (big) big_list[base + (uint32_t)__builtin_popcountll(m & lt_lanes)] = (uint16_t)(bw[k] + cur[k]);
   }
-  __syncthreads();
-  for (uint32_t t = tid; t < big_n; t += kPlaceRegBlock) {
-    const uint32_t bi_ = big_list[t];
-    const Entry me = buf[bi_];
-    const uint32_t w = (uint32_t)(fast_mod(me.hash, P.mod) - start);  // its group: [base[w], base[w + 1])
-    const uint32_t b_w = meta[w] & 0xffffu;
-    const uint32_t gg = (w + 1 < (uint32_t)kBucket ? meta[w + 1] & 0xffffu : n) - b_w;
-    const uint64_t ai = me.addr & ~kDelBit;
-    uint32_t r = 0, eq = 0;
-    uint64_t best = 0, besth = 0;  // the largest smaller address and its hash
-    for (uint32_t u = 0; u < gg; u++) {
-      const Entry e = buf[b_w + u];
-      const uint64_t aj = e.addr & ~kDelBit;
-      const bool lt = aj < ai;
-      r += lt ? 1u : 0u;
-      const bool nb = lt && (r == 1u || aj > best);
-      best = nb ? aj : best;
-      besth = nb ? e.hash : besth;
-      eq |= (aj != ai && e.hash == me.hash) ? 1u : 0u;
-    }
-    big_rank[bi_] = (uint16_t)(r | (r > 0 && besth == me.hash ? 0x8000u : 0u) | (eq ? 0x4000u : 0u));
-  }
-  __syncthreads();
+  const uint32_t gw = (uint32_t)wave_max_i32((int32_t)gl);
+  uint32_t eqh = 0;  // another member with this entry's hash (duplicate keys: rare)
+  for (uint32_t u = 0; u < gw; u++) {
 #pragma unroll
-  for (int k = 0; k < kPlaceRegPer; k++) {
-    if (g[k] < 3 || g[k] > kGroupMax) continue;
-    const uint32_t v = big_rank[bw[k] + cur[k]];
-    rank[k] = (v & 0x3fffu) | ((v >> 15) << 31);
-    eqh |= (v >> 14) & 1u;
+    for (int k = 0; k < kPlaceRegPer; k++) {
+      const bool act = u < g[k];  // (a lone entry meets only itself)
+      const Entry e = buf[bw[k] + (act ? u : 0u)];
+      const uint64_t ai = mine[k].addr & ~kDelBit;
+      const uint64_t aj = e.addr & ~kDelBit;
+      rank[k] += act && aj < ai ? 1u : 0u;
+      eqh |= (uint32_t)act & (uint32_t)(aj != ai) & (uint32_t)(e.hash == mine[k].hash);  // (no branches)
+    }
   }
   // Equal-hash PUT pairs (duplicate-key candidates, for the pair list): counted and written only by
   // blocks that met an equal hash at all
@@ -2334,7 +2292,7 @@ __device__ __forceinline__ void place_reg_bucket(const BuildParams& P, uint64_t 
   for (int k = 0; k < kPlaceRegPer; k++) {
     const bool valid = want[k] < (uint32_t)kBucket;
     const int32_t M = (int32_t)(meta[want[k]] >> 16) - 32768;
-    const int64_t p = (int64_t)(bw[k] + (rank[k] & 0x7fffffffu)) + max(x, (int64_t)M);
+    const int64_t p = (int64_t)(bw[k] + rank[k]) + max(x, (int64_t)M);
     pos[k] = valid ? p : -1;
     slot_of[valid ? p - x : (int64_t)(2 * kBucket + 1)] = (int16_t)(bw[k] + cur[k]);  // (where the entry sits in buf)
     const int64_t d = valid ? p - (int64_t)want[k] : 0;
@@ -2347,11 +2305,13 @@ __device__ __forceinline__ void place_reg_bucket(const BuildParams& P, uint64_t 
   __syncthreads();
   // the pair (slot - 1, slot) inside the block's range: equal hashes share a wanted slot, so they are
   // members of one group ranked next to each other -- the member in slot p - 1 of a member ranked
-  // after another is the one ranked just before it (pe, from the ranking above)
+  // after another (calculateMaxDisplacement, IndexHash.java:195-245)
 #pragma unroll
   for (int k = 0; k < kPlaceRegPer; k++) {
     const int64_t p = pos[k];
-    col += p >= 0 && (rank[k] >> 31) && wrap_slot(start + (uint64_t)p, P.cap) != 0 && start + (uint64_t)p < lim;
+    const bool act = p >= 0 && rank[k] > 0;
+    const Entry e = buf[act ? slot_of[p - 1 - x] : 0];
+    col += act && e.hash == mine[k].hash && wrap_slot(start + (uint64_t)p, P.cap) != 0 && start + (uint64_t)p < lim;
   }
   const int64_t hi = max(bsize, (int64_t)s_pend);
   // the block's slots [x, hi) in order, consecutive lanes on consecutive slots: its entries out of
@@ -2455,7 +2415,7 @@ __device__ __forceinline__ void place_reg_bucket(const BuildParams& P, uint64_t 
 // three quarters of the region are loaded with the bucket's count (a bucket at load 0.77 holds about
 // 790 entries), the last quarter only up to the count (it read 23% more bytes than the entries).
 template <bool kFixed>
-__global__ __launch_bounds__(kPlaceRegBlock, 5) void k_place_reg(BuildParams P) {
+__global__ __launch_bounds__(kPlaceRegBlock) void k_place_reg(BuildParams P) {
   Entry pre[kPlaceRegPer];
   if (kFixed) {
     const uint64_t e0 = (uint64_t)blockIdx.x * kPlaceLdsMax;

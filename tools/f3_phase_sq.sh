@@ -9,6 +9,9 @@ export TMPDIR=/tmp
 T=$1; A="${2:---workload c3 --entries 10000000} --steps 2 --warmup 1 --quick --no-parity --no-cpu-baseline"; L=$3
 O=gpurun_out/$T; mkdir -p $O
 [ -n "$L" ] && export SPARKEY_GPU_LIB=$PWD/ablib/$L.so
+( while sleep 50; do echo "alive $(date +%T)" >> $O/heartbeat.txt; done ) &
+HB=$!
+trap 'kill $HB 2>/dev/null' EXIT
 for s in none 0 1 2 3 4 5; do
   sw=""; [ "$s" != none ] && sw="frame3_stop=$s"
   SPARKEY_DEBUG=$sw timeout -s KILL 150 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES \

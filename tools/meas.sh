@@ -10,6 +10,9 @@ export TMPDIR=/tmp
 O=gpurun_out/${1:-meas}; mkdir -p $O
 PARTS=${2:-bench,prof,c4prof,shard}
 has() { [[ ",$PARTS," == *",$1,"* ]]; }
+( while sleep 50; do echo "alive $(date +%T)" >> $O/heartbeat.txt; done ) &  # (long passes print nothing)
+HB=$!
+trap 'kill $HB 2>/dev/null' EXIT
 b() { local n=$1; shift; timeout -k 10 600 python -u bench.py "$@" > $O/$n.jsonl 2> $O/$n.err || { tail -5 $O/$n.err; return 1; }; tail -1 $O/$n.jsonl | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('$n', round(d['ms_per_step'],4), d.get('stage_ms'))"; }
 if has bench; then
   b default && b c3_100m --workload c3 --entries 100000000 --steps 10 --warmup 2 --no-cpu-baseline \
