@@ -171,7 +171,8 @@ __global__ __launch_bounds__(kPlaceBlock) void k_summary(BuildParams P) {
   __syncthreads();
   bool bad = false;  // (kGuardForeign)
   for (uint32_t i = tid; i < n; i += kPlaceBlock) {
-    const uint64_t w = fast_mod(P.ent2[eoff + i].hash, P.mod) - start;
+    const uint64_t h = (P.compact & kCompactOut) ? load_craw(reinterpret_cast<const CEntry*>(P.ent2) + eoff + i).hash : P.ent2[eoff + i].hash;
+    const uint64_t w = fast_mod(h, P.mod) - start;
     if (w < (uint64_t)kBucket) atomicAdd(&cnt[w], 1u);
     else bad = true;
   }

@@ -39,6 +39,18 @@ struct alignas(16) Entry {
   uint64_t hash;  // HashType.hash of the key (32-bit hashes zero-extended)
   uint64_t addr;  // position << entryBlockBits (| kDelBit for DELETE records)
 };
+// The entry of a uniform log between the framing and the placement (BuildParams.compact): 12 bytes,
+// the record index in place of the address, which is (fr_entry + idx * uni_rec) << entryBlockBits --
+// every record of such a log has the same size and none is a DELETE (k_frame_uniform's condition).
+// One 3-dword access per entry (a hash array and an index array per region measured slower: the
+// framing's write-out and the partition both lost more than the single stride costs,
+// profiles/r06/c2/compact_soa_ab.txt).
+struct CEntry {
+  uint32_t h0, h1;  // the hash, low and high words
+  uint32_t idx;     // record index in the log
+};
+static_assert(sizeof(CEntry) == 12, "12-byte compact entries");
+constexpr int kCompactIn = 1, kCompactOut = 2;  // BuildParams.compact's bits
 
 // Carry function f(x) = max(c, x + a) of a bucket (see k_summary).
 struct MaxPlus {
@@ -248,6 +260,10 @@ struct BuildParams {
   uint64_t slot_lo, slot_hi;
   int64_t carry_in;
   int32_t abort_on_fail;        // the bin after a speculative framing attempt: skip it when the attempt failed
+  // 12-byte entries (CEntry) of single-GPU uniform logs (C2's, C4's): bit 0 (kCompactIn) the digit
+  // regions (ent3: k_frame_uniform -> pass 2), bit 1 (kCompactOut) the bucket regions (ent2: pass 2 ->
+  // k_summary / k_place_reg); every other path keeps 16-byte Entry
+  int32_t compact;
   // sharded: the carry-in composed on the device from every rank's carry function (world x {c, a});
   // k_carry then also clears the placement's status counters
   const int64_t* carry_funs;
@@ -298,6 +314,8 @@ struct StageTimer {
 void launch_frame_fused(const BuildParams& P, hipStream_t s, StageTimer* tm);
 void launch_partition(const BuildParams& P, hipStream_t s, StageTimer* tm);
 bool part2f_fits(uint32_t bpp);  // k_part2f's LDS for this many buckets a digit
+int part2st_per(const BuildParams& P);  // k_part2st's stage (entries a thread), 0: pass 2 is another kernel
+bool part2_direct(const BuildParams& P);  // pass 2 is k_part2f_direct
 void launch_partition1(const BuildParams& P, hipStream_t s);
 void launch_partition2(const BuildParams& P, hipStream_t s, StageTimer* tm);
 void launch_part2_recv(const BuildParams& P, hipStream_t s, StageTimer* tm);  // sharded receive, fixed regions

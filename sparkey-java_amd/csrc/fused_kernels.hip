@@ -869,7 +869,9 @@ __global__ __launch_bounds__(64 * W) void k_frame_uniform(BuildParams P) {
     const uint32_t i = lbase[d] + (dr[r] & 0xffffu);
     Entry en;
     en.hash = hsh[r];
-    en.addr = (uint64_t)(P.fr_entry + (int64_t)(blk0 + (uint64_t)(r * W + wave) * 64 + lane) * R) << P.ebb;
+    const uint64_t rec = blk0 + (uint64_t)(r * W + wave) * 64 + lane;
+    // (compact: the record index, the write-out stores 12-byte CEntry)
+    en.addr = (P.compact & kCompactIn) ? rec : (uint64_t)(P.fr_entry + (int64_t)rec * R) << P.ebb;
     stage[i] = en;
     sdig[i] = (uint8_t)d;
   }
@@ -880,10 +882,18 @@ __global__ __launch_bounds__(64 * W) void k_frame_uniform(BuildParams P) {
   lds_barrier();
   mark(2);
   const uint32_t ntile = wsum[0] + wsum[1] + wsum[2] + wsum[3];
-  for (uint32_t i = threadIdx.x; i < ntile; i += 64 * W) {
-    const uint32_t d = sdig[i];
-    const uint64_t pos = (uint64_t)rbase[d] + (i - lbase[d]);
-    if (pos < P.p1_region) P.ent3[(uint64_t)d * P.p1_region + pos] = stage[i];
+  if (P.compact & kCompactIn) {
+    for (uint32_t i = threadIdx.x; i < ntile; i += 64 * W) {
+      const uint32_t d = sdig[i];
+      const uint64_t pos = (uint64_t)rbase[d] + (i - lbase[d]);
+      if (pos < P.p1_region) store_craw(reinterpret_cast<CEntry*>(P.ent3) + (uint64_t)d * P.p1_region + pos, stage[i]);
+    }
+  } else {
+    for (uint32_t i = threadIdx.x; i < ntile; i += 64 * W) {
+      const uint32_t d = sdig[i];
+      const uint64_t pos = (uint64_t)rbase[d] + (i - lbase[d]);
+      if (pos < P.p1_region) P.ent3[(uint64_t)d * P.p1_region + pos] = stage[i];
+    }
   }
   if (P.dbg) {  // (the write-out to completion)
     __builtin_amdgcn_s_waitcnt(0);
@@ -1497,7 +1507,8 @@ __global__ __launch_bounds__(kPart2Block) void k_part2d(BuildParams P) {
 // functions are k_summary's (no slot counts here: bpp x 1024 of them do not fit the LDS).  kPer entries
 // a thread per round: 6 where the LDS holds them, fewer for the largest tables (C4's 4960 buckets a
 // digit: 2, whose rounds are shorter than the bucket count -- runs of about one entry).  Single GPU.
-template <int kPer>
+// kC: 12-byte CEntry digit regions in and bucket regions out (BuildParams.compact).
+template <int kPer, bool kC>
 __global__ __launch_bounds__(kPart2Block) void k_part2f(BuildParams P) {
   // cur[nb] | rc0[nb] | rc1[nb] | roff[nb] | gbase[nb] | stage[kPart2Block * kPer]
   extern __shared__ __attribute__((aligned(16))) uint32_t dyn[];
@@ -1523,7 +1534,7 @@ __global__ __launch_bounds__(kPart2Block) void k_part2f(BuildParams P) {
 #pragma unroll
     for (int k = 0; k < kPer; k++) {
       const uint64_t i = i0 + (uint64_t)k * kPart2Block + tid;
-      if (i < hi) v[k] = P.ent3[i];
+      if (i < hi) v[k] = kC ? load_craw(reinterpret_cast<const CEntry*>(P.ent3) + i) : P.ent3[i];
     }
   };
   Entry nx[kPer];
@@ -1577,8 +1588,10 @@ __global__ __launch_bounds__(kPart2Block) void k_part2f(BuildParams P) {
       const Entry e = stage[i];
       const uint32_t b = bucket_of(P, e.hash) - b0;
       const uint32_t r = gbase[b] + (i - roff[b]);
-      if (r < kPlaceLdsMax) P.ent2[((uint64_t)b0 + b - P.b_lo) * kPlaceLdsMax + r] = e;
-      else ovf = true;
+      const uint64_t at = ((uint64_t)b0 + b - P.b_lo) * kPlaceLdsMax + r;
+      if (r >= kPlaceLdsMax) ovf = true;
+      else if (kC) store_craw(reinterpret_cast<CEntry*>(P.ent2) + at, e);
+      else P.ent2[at] = e;
     }
     __syncthreads();  // (the stage, roff and gbase are rewritten next round)
   }
@@ -1596,6 +1609,8 @@ __global__ __launch_bounds__(kPart2Block) void k_part2f(BuildParams P) {
 // k_part2f for tables whose rounds would hold about one entry per bucket (more than 3072 buckets a
 // digit: C4's 4960): no stage, each entry stored at its bucket cursor's place (an LDS atomic), eight
 // loads a thread in flight.  The stores scatter as the staged kernel's would at that size.
+// kCI / kCO: 12-byte CEntry digit regions in / bucket regions out (BuildParams.compact's bits).
+template <bool kCI, bool kCO>
 __global__ __launch_bounds__(kPart2Block) void k_part2f_direct(BuildParams P) {
   extern __shared__ __attribute__((aligned(16))) uint32_t cur[];  // per bucket of the digit
   if (build_aborted(P)) return;
@@ -1614,7 +1629,10 @@ __global__ __launch_bounds__(kPart2Block) void k_part2f_direct(BuildParams P) {
 #pragma unroll
     for (int k = 0; k < kIn; k++) {
       const uint64_t i = i0 + (uint64_t)k * kPart2Block + tid;
-      if (i < hi) v[k] = P.ent3[i];
+      if (i < hi) {
+        const CEntry* c = reinterpret_cast<const CEntry*>(P.ent3) + i;
+        v[k] = !kCI ? P.ent3[i] : kCO ? load_craw(c) : load_centry(P, c);
+      }
     }
 #pragma unroll
     for (int k = 0; k < kIn; k++) {
@@ -1624,8 +1642,10 @@ __global__ __launch_bounds__(kPart2Block) void k_part2f_direct(BuildParams P) {
       bad |= b >= nbins;
       if (b >= nbins) continue;
       const uint32_t r = atomicAdd(&cur[b], 1u);
-      if (r < kPlaceLdsMax) P.ent2[((uint64_t)b0 + b - P.b_lo) * kPlaceLdsMax + r] = v[k];
-      else ovf = true;
+      const uint64_t at = ((uint64_t)b0 + b - P.b_lo) * kPlaceLdsMax + r;
+      if (r >= kPlaceLdsMax) ovf = true;
+      else if (kCO) store_craw(reinterpret_cast<CEntry*>(P.ent2) + at, v[k]);
+      else P.ent2[at] = v[k];
     }
   }
   if (ovf) atomicOr(&P.st->p2_overflow, 1u);
@@ -1915,7 +1935,9 @@ __global__ __launch_bounds__(kPart2Block) void k_part2s(BuildParams P) {
 // LDS and leaves as one run per bucket.  The slot counts are 8-bit (4 per word), which frees the LDS
 // for the stage; a count that would pass 255 flags p2_overflow, and the host redoes the build with
 // dense runs (k_part2s's two-pass path).  Single GPU, fixed regions only.
-template <int kP2StagePer>
+// kCI / kCO: 12-byte CEntry digit regions in / bucket regions out (BuildParams.compact's bits; with
+// both the entries keep the record index in their addr word from the load to the store)
+template <int kP2StagePer, bool kCI, bool kCO>
 __global__ __launch_bounds__(kPart2Block) void k_part2st(BuildParams P) {
   constexpr int kP2Stage = kPart2Block * kP2StagePer;
   // h8[bpp * 256] | btot[bpp] | rcnt[bpp] | roff[bpp] | gbase[bpp] | stage[kP2Stage]
@@ -1952,7 +1974,10 @@ __global__ __launch_bounds__(kPart2Block) void k_part2st(BuildParams P) {
 #pragma unroll
     for (int k = 0; k < kP2StagePer; k++) {
       const uint64_t i = i0 + (uint64_t)k * kPart2Block + tid;
-      if (i < hi) v[k] = P.ent3[i];
+      if (i < hi) {
+        const CEntry* c = reinterpret_cast<const CEntry*>(P.ent3) + i;
+        v[k] = !kCI ? P.ent3[i] : kCO ? load_craw(c) : load_centry(P, c);
+      }
     }
   };
   Entry nx[kP2StagePer];
@@ -2008,10 +2033,10 @@ __global__ __launch_bounds__(kPart2Block) void k_part2st(BuildParams P) {
       const uint32_t b = sbk[i];
       const uint32_t r = gbase[b] + (i - roff[b]);
       typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-      if (r < kPlaceLdsMax)
-        __builtin_nontemporal_store(*reinterpret_cast<const u32x4*>(&e),
-                                    reinterpret_cast<u32x4*>(&P.ent2[(b0 + b - P.b_lo) * (uint64_t)kPlaceLdsMax + r]));
-      else ovf = true;
+      const uint64_t at = (b0 + b - P.b_lo) * (uint64_t)kPlaceLdsMax + r;
+      if (r >= kPlaceLdsMax) ovf = true;
+      else if (kCO) store_craw(reinterpret_cast<CEntry*>(P.ent2) + at, e);  // (a non-temporal 3-dword store measured slower)
+      else __builtin_nontemporal_store(*reinterpret_cast<const u32x4*>(&e), reinterpret_cast<u32x4*>(&P.ent2[at]));
     }
     __syncthreads();  // (the stage and the offsets are rewritten next round)
   }
@@ -2414,17 +2439,26 @@ __device__ __forceinline__ void place_reg_bucket(const BuildParams& P, uint64_t 
 // branch joins the loads and the wave runs on to the head's scalar loads with them in flight) the first
 // three quarters of the region are loaded with the bucket's count (a bucket at load 0.77 holds about
 // 790 entries), the last quarter only up to the count (it read 23% more bytes than the entries).
-template <bool kFixed>
+// kC: the fixed regions hold 12-byte CEntry (BuildParams.compact), expanded to Entry on the load.
+template <bool kFixed, bool kC = false>
 __global__ __launch_bounds__(kPlaceRegBlock) void k_place_reg(BuildParams P) {
   Entry pre[kPlaceRegPer];
   if (kFixed) {
     const uint64_t e0 = (uint64_t)blockIdx.x * kPlaceLdsMax;
     const uint32_t n = P.bcount[P.b_lo + blockIdx.x];
-#pragma unroll
-    for (int k = 0; k < kPlaceRegPer - 1; k++) pre[k] = P.ent2[e0 + threadIdx.x + k * kPlaceRegBlock];
     constexpr uint32_t kLast = (kPlaceRegPer - 1) * kPlaceRegBlock;
     // (no branch: lanes past the count reload their first entry's line, which the cache holds)
-    pre[kPlaceRegPer - 1] = P.ent2[e0 + threadIdx.x + (threadIdx.x + kLast < n ? kLast : 0u)];
+    const uint64_t last = e0 + threadIdx.x + (threadIdx.x + kLast < n ? kLast : 0u);
+    if (kC) {
+      const CEntry* c2 = reinterpret_cast<const CEntry*>(P.ent2);
+#pragma unroll
+      for (int k = 0; k < kPlaceRegPer - 1; k++) pre[k] = load_centry(P, c2 + e0 + threadIdx.x + k * kPlaceRegBlock);
+      pre[kPlaceRegPer - 1] = load_centry(P, c2 + last);
+    } else {
+#pragma unroll
+      for (int k = 0; k < kPlaceRegPer - 1; k++) pre[k] = P.ent2[e0 + threadIdx.x + k * kPlaceRegBlock];
+      pre[kPlaceRegPer - 1] = P.ent2[last];
+    }
   }
   place_reg_bucket<kFixed>(P, blockIdx.x, pre);
 }
@@ -2513,29 +2547,56 @@ static size_t part2st_lds(uint32_t bpp, int per) {
   return (size_t)((bpp * 260 + 3) & ~3u) * 4 + (size_t)kPart2Block * per * (sizeof(Entry) + 1);
 }
 
+// k_part2st's entries a thread per round for this build: the largest stage that fits (fewer rounds,
+// fewer barriers), or 0 when pass 2 is not the staged kernel
+int part2st_per(const BuildParams& P) {
+  constexpr size_t kLdsMax = 158 * 1024;
+  if (!(P.p2_sorted && P.p2_fixed && P.fused_carry && P.p1_region && !P.p2_seg)) return 0;
+  for (int per = 6; per >= 4; per--)
+    if (part2st_lds(P.bpp, per) <= kLdsMax) return per;
+  return 0;
+}
+
+// pass 2 is k_part2f_direct (more buckets a digit than a staged round would group: C4's tables) or
+// k_part2f: fixed bucket regions straight from the digit regions, with k_summary's carries
+bool part2_direct(const BuildParams& P) {
+  return part2st_per(P) == 0 && !P.p2_sorted && P.p2_fixed && P.p1_region && !P.p2_seg &&
+         (P.bpp > kPart2Block * 3 || part2f_lds(P.bpp, 2) <= 158 * 1024);
+}
+
 void launch_partition(const BuildParams& P, hipStream_t s, StageTimer* tm) {
   if (P.p1_bucket) return;  // (the framing wrote the bucket regions)
   if (!P.p1_region) launch_partition1(P, s);
   else if (P.p1_kernel) hipLaunchKernelGGL(k_part1_regions, dim3(std::min<unsigned>(P.p1r_tiles, kP1rGrid)), dim3(kPartBlock), 0, s, P);
-  // the largest stage (entries a thread per round) that fits: fewer rounds, fewer barriers
   constexpr size_t kLdsMax = 158 * 1024;
-  const bool staged = P.p2_sorted && P.p2_fixed && P.fused_carry && P.p1_region && !P.p2_seg;
-  if (staged && part2st_lds(P.bpp, 6) <= kLdsMax)
-    hipLaunchKernelGGL(k_part2st<6>, dim3(256), dim3(kPart2Block), part2st_lds(P.bpp, 6), s, P);
-  else if (staged && part2st_lds(P.bpp, 5) <= kLdsMax)
-    hipLaunchKernelGGL(k_part2st<5>, dim3(256), dim3(kPart2Block), part2st_lds(P.bpp, 5), s, P);
-  else if (staged && part2st_lds(P.bpp, 4) <= kLdsMax)
-    hipLaunchKernelGGL(k_part2st<4>, dim3(256), dim3(kPart2Block), part2st_lds(P.bpp, 4), s, P);
+  const int per = part2st_per(P);  // (the staged kernel: the largest stage that fits; compact only with it)
+  if (per == 6)
+    hipLaunchKernelGGL((P.compact ? k_part2st<6, true, true> : k_part2st<6, false, false>),
+                       dim3(256), dim3(kPart2Block),
+                       part2st_lds(P.bpp, 6), s, P);
+  else if (per == 5)
+    hipLaunchKernelGGL((P.compact ? k_part2st<5, true, true> : k_part2st<5, false, false>),
+                       dim3(256), dim3(kPart2Block),
+                       part2st_lds(P.bpp, 5), s, P);
+  else if (per == 4)
+    hipLaunchKernelGGL((P.compact ? k_part2st<4, true, true> : k_part2st<4, false, false>),
+                       dim3(256), dim3(kPart2Block),
+                       part2st_lds(P.bpp, 4), s, P);
   else if (P.p2_sorted)
     hipLaunchKernelGGL(k_part2s, dim3(256), dim3(kPart2Block), (size_t)(514u * P.bpp) * sizeof(uint32_t), s, P);
-  else if (P.p2_fixed && P.p1_region && !P.p2_seg && P.bpp > kPart2Block * 3)
-    hipLaunchKernelGGL(k_part2f_direct, dim3(256), dim3(kPart2Block), (size_t)P.bpp * sizeof(uint32_t), s, P);
+  else if (part2_direct(P))
+    hipLaunchKernelGGL((P.compact ? k_part2f_direct<true, true> : k_part2f_direct<false, false>),
+                       dim3(256), dim3(kPart2Block),
+                       (size_t)P.bpp * sizeof(uint32_t), s, P);
   else if (P.p2_fixed && P.p1_region && !P.p2_seg && part2f_lds(P.bpp, 6) <= kLdsMax)
-    hipLaunchKernelGGL(k_part2f<6>, dim3(256), dim3(kPart2Block), part2f_lds(P.bpp, 6), s, P);
+    hipLaunchKernelGGL((P.compact ? k_part2f<6, true> : k_part2f<6, false>), dim3(256), dim3(kPart2Block),
+                       part2f_lds(P.bpp, 6), s, P);
   else if (P.p2_fixed && P.p1_region && !P.p2_seg && part2f_lds(P.bpp, 4) <= kLdsMax)
-    hipLaunchKernelGGL(k_part2f<4>, dim3(256), dim3(kPart2Block), part2f_lds(P.bpp, 4), s, P);
+    hipLaunchKernelGGL((P.compact ? k_part2f<4, true> : k_part2f<4, false>), dim3(256), dim3(kPart2Block),
+                       part2f_lds(P.bpp, 4), s, P);
   else if (P.p2_fixed && P.p1_region && !P.p2_seg && part2f_lds(P.bpp, 2) <= kLdsMax)
-    hipLaunchKernelGGL(k_part2f<2>, dim3(256), dim3(kPart2Block), part2f_lds(P.bpp, 2), s, P);
+    hipLaunchKernelGGL((P.compact ? k_part2f<2, true> : k_part2f<2, false>), dim3(256), dim3(kPart2Block),
+                       part2f_lds(P.bpp, 2), s, P);
   else if (!P.p2_seg && part2d_lds(P.bpp) <= kLdsMax)
     hipLaunchKernelGGL(k_part2d, dim3(256), dim3(kPart2Block), part2d_lds(P.bpp), s, P);
   else
@@ -2549,8 +2610,8 @@ void launch_inject_foreign(const BuildParams& P, hipStream_t s, int where) {
 
 void launch_place_buckets(const BuildParams& P, hipStream_t s) {
   if (P.b_hi > P.b_lo)
-    hipLaunchKernelGGL(P.p2_fixed ? k_place_reg<true> : k_place_reg<false>, dim3((unsigned)(P.b_hi - P.b_lo)),
-                       dim3(kPlaceRegBlock), 0, s, P);
+    hipLaunchKernelGGL(((P.compact & kCompactOut) ? k_place_reg<true, true> : P.p2_fixed ? k_place_reg<true> : k_place_reg<false>),
+                       dim3((unsigned)(P.b_hi - P.b_lo)), dim3(kPlaceRegBlock), 0, s, P);
   // buckets above kPlaceLdsMax entries (normally none; never with fixed bucket regions, whose
   // overflow redoes the build with dense runs)
   if (!P.p2_fixed) launch_place_global(P, s, 0, 1);

@@ -34,6 +34,36 @@ __device__ __forceinline__ void report_foreign(const BuildParams& P, bool bad) {
   if (bad) atomicOr(&P.st->guard, kGuardForeign);
 }
 
+// compact entries (CEntry, BuildParams.compact): raw (addr = the record index) or with its address;
+// the stores are one 3-dword store (4-byte aligned), plain or non-temporal
+typedef unsigned int sk_u32x3 __attribute__((ext_vector_type(3), aligned(4)));
+__device__ __forceinline__ Entry load_craw(const CEntry* s) {
+  const CEntry c = *s;
+  Entry e;
+  e.hash = (uint64_t)c.h0 | ((uint64_t)c.h1 << 32);
+  e.addr = c.idx;
+  return e;
+}
+__device__ __forceinline__ Entry load_centry(const BuildParams& P, const CEntry* s) {
+  Entry e = load_craw(s);
+  e.addr = (uint64_t)(P.fr_entry + (int64_t)e.addr * P.uni_rec) << P.ebb;
+  return e;
+}
+__device__ __forceinline__ void store_craw(CEntry* d, const Entry& e) {
+  sk_u32x3 v;
+  v.x = (uint32_t)e.hash;
+  v.y = (uint32_t)(e.hash >> 32);
+  v.z = (uint32_t)e.addr;
+  *reinterpret_cast<sk_u32x3*>(d) = v;
+}
+__device__ __forceinline__ void store_craw_nt(CEntry* d, const Entry& e) {
+  sk_u32x3 v;
+  v.x = (uint32_t)e.hash;
+  v.y = (uint32_t)(e.hash >> 32);
+  v.z = (uint32_t)e.addr;
+  __builtin_nontemporal_store(v, reinterpret_cast<sk_u32x3*>(d));
+}
+
 __device__ __forceinline__ void set_error(Status* st, int64_t pos, int code) {
   atomicMin(&st->err, ((unsigned long long)pos << 8) | (unsigned long long)(-code));
 }

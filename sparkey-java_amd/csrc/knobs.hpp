@@ -50,6 +50,7 @@ enum class Knob : int {
   ShardGatherCompressed,  // num_gpus > 1: compressed logs gathered on every rank (the sharded path off)
   InjectForeign,    // tests of the kGuardForeign check: a foreign entry in digit region 0 (1) or bucket region 0 (2)
   ShardCollFail,    // host transport (HostColl): the k-th collective of a communicator fails its device copy (tests)
+  NoCompact,        // 16-byte entries on the uniform staged path too (BuildParams.compact off)
   kCount
 };
 

@@ -383,6 +383,19 @@ def test_uniform_disabled_gives_same_bytes(native, switch):
     assert sa.framing_path == 2 and sb.framing_path in SPEC and a == b
 
 
+@pytest.mark.parametrize("klen,vlen,hash_size", [(16, 100, 8), (16, 100, 4), (8, 0, 8), (126, 127, 8)])
+def test_uniform_compact_entries(native, switch, klen, vlen, hash_size):
+    """The uniform staged path carries 12-byte entries (hash, record index) from k_frame_uniform through
+    k_part2st to k_place_reg, the address rebuilt from the index (BuildParams.compact); the no_compact
+    switch keeps 16-byte entries.  Both give the oracle's bytes."""
+    log = make_log(_uniform_puts(60000, klen, vlen, seed=klen + vlen))
+    got, stats = check(native, log, 31 + klen, hash_size=hash_size, expect_path=0)
+    assert stats.framing_path == 2, stats.as_dict()
+    switch(no_compact=1)
+    b, _ = gpu_build(native, log, 31 + klen, hash_size)
+    assert b == got
+
+
 @pytest.mark.parametrize("region_cap", [60000, 1])
 def test_uniform_digit_regions(native, switch, region_cap):
     """k_frame_uniform as partition pass 1 (entries straight into digit regions of ent3): a region
