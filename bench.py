@@ -38,16 +38,17 @@ PMC_SUMMARIES = [os.path.join(ROOT, "profiles", f) for f in ("r05_pmc_summary.js
 HASH_SEED = 0x2545F491
 
 
-def stage_bytes(stage, n, data_end, slot, cap, passes=2, comp_end=None):
+def stage_bytes(stage, n, data_end, slot, cap, passes=2, comp_end=None, eb=16):
     """Algorithmic bytes per launch of each stage.  passes: partition passes left to
-    the partition stage (1 when the uniform framing wrote the digit regions itself)."""
+    the partition stage (1 when the uniform framing wrote the digit regions itself); eb: bytes an
+    entry takes between the framing and the placement (stats.entry_bytes: 12 on uniform logs)."""
     log = data_end - 84
     return {
-        "frame": log + 16 * n,                # log read once, 16-byte (hash, address) entries written
-        "emit": log + 16 * n,                 # serial path: same bytes
-        "partition": passes * 32 * n,         # radix passes, entries read + written once each
-        "summary": 16 * n,                    # entries read once
-        "place": 16 * n + slot * cap,         # entries read once, every slot written once
+        "frame": log + eb * n,                # log read once, (hash, address) entries written
+        "emit": log + 16 * n,                 # serial path: 16-byte entries
+        "partition": passes * 2 * eb * n,     # radix passes, entries read + written once each
+        "summary": eb * n,                    # entries read once
+        "place": eb * n + slot * cap,         # entries read once, every slot written once
         "stats": slot * cap,                  # table read once
         "exact": 3 * 16 * n + 2 * slot * cap,  # entries read, grouped, replayed; segment slots cleared + written
         # SNAPPY (data_end = the virtual log's end): blocks read once, decompressed bytes written once
@@ -266,7 +267,8 @@ def single_gpu(args, dev):
     passes = stats.partition_passes
     # SNAPPY: the inner build's stages run over the virtual log (84 + 118 n bytes for C2 records)
     frame_end = 84 + 118 * n if args.workload in ("snappy", "zstd") else log_len
-    dom_bytes = stage_bytes(dom, n, frame_end, slot, cap, passes, comp_end=log_len) if dom else 0
+    eb = stats.entry_bytes or 16
+    dom_bytes = stage_bytes(dom, n, frame_end, slot, cap, passes, comp_end=log_len, eb=eb) if dom else 0
     achieved = dom_bytes / (stage_ms[dom] * 1e-3) / 1e9 if dom and stage_ms[dom] > 0 else 0.0
     b_alg = (log_len - 84) + 112 + slot * cap
     assert stats.placement_path == wl["path"] and stats.framing_path in (0, 2, 4), stats.as_dict()
@@ -401,7 +403,7 @@ def single_gpu(args, dev):
                          (dom, stats.framing_path if dom == "frame" else passes), dom)),
                      "algorithmic_bytes_per_launch": dom_bytes, "avg_launch_ms": stage_ms.get(dom) if dom else None},
         "build_hbm_gbs": b_alg / (ms_per_step * 1e-3) / 1e9,
-        "stage_gbs": {k: stage_bytes(k, n, frame_end, slot, cap, passes, comp_end=log_len) / (v * 1e-3) / 1e9
+        "stage_gbs": {k: stage_bytes(k, n, frame_end, slot, cap, passes, comp_end=log_len, eb=eb) / (v * 1e-3) / 1e9
                       for k, v in stage_ms.items() if v > 0 and stage_bytes(k, n, frame_end, slot, cap, passes)},
         "build_algorithmic_bytes": b_alg,
         "stage_ms": stage_ms,
@@ -462,7 +464,7 @@ def single_gpu_c4(args, dev):
     cap = stats.capacity
     passes = stats.partition_passes
     dom = max(stage_ms, key=lambda k: stage_ms[k])
-    dom_bytes = stage_bytes(dom, n, log_len, slot, cap, passes)
+    dom_bytes = stage_bytes(dom, n, log_len, slot, cap, passes, eb=stats.entry_bytes or 16)
     achieved = dom_bytes / (stage_ms[dom] * 1e-3) / 1e9
     b_alg = (log_len - 84) + 112 + slot * cap
     ms_per_step = elapsed * 1000.0 / args.steps

@@ -89,6 +89,9 @@ typedef struct sparkey_build_stats {
                                  log gathered on every rank and built whole (full tables); else 0 */
   double device_ms;           /* device time of the build (HIP events), excluding copies; sharded: the rank's
                                  wall time of sparkey_shard_build */
+  int32_t entry_bytes;        /* bytes a (hash, address) entry takes between the framing and the placement:
+                                 16, or 12 on uniform logs (hash + record index: DESIGN.md §2.2); 0 if none */
+  int32_t reserved0;
 } sparkey_build_stats;
 
 /* file -> file.  What the JNI shim calls in place of IndexHash.createNew; the Java side keeps

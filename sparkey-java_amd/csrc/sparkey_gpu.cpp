@@ -431,9 +431,11 @@ static int plan_reserve(sparkey_plan* pl, uint64_t nchunks, uint64_t nrec, uint6
 }
 
 static void fill_stats(sparkey_build_stats* s, const Status& st, const IndexParams& ip, int placement, int framing,
-                       double ms, int partition_passes = 2) {
+                       double ms, int partition_passes = 2, int entry_bytes = 16) {
   if (!s) return;
   s->partition_passes = partition_passes;
+  s->entry_bytes = entry_bytes;
+  s->reserved0 = 0;
   s->sharded = 0;
   s->num_records = (int64_t)st.n_records;
   s->num_deletes = (int64_t)st.n_deletes;
@@ -1436,6 +1438,7 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
     break;
   }
   P.abort_on_fail = 0;  // (the exact path's stages report their own errors, at the lowest log position)
+  const int entry_bytes = P.compact ? 12 : 16;
   P.compact = 0;        // (and frame into 16-byte slabs)
   rc = status_error(st, err, err_len);
   if (rc) return rc;
@@ -1554,7 +1557,8 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
       pl->stage_ms.push_back(t);
     }
   }
-  fill_stats(stats_out, st, ip, placement_path, framing_path, ms, buckets_used ? 0 : regions_used ? 1 : 2);
+  fill_stats(stats_out, st, ip, placement_path, framing_path, ms, buckets_used ? 0 : regions_used ? 1 : 2,
+             entry_bytes);
   return SPARKEY_OK;
 }
 

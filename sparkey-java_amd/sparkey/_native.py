@@ -67,7 +67,8 @@ class BuildStats(ctypes.Structure):
                 ("total_displacement", ctypes.c_int64), ("hash_size", ctypes.c_int32),
                 ("address_size", ctypes.c_int32), ("placement_path", ctypes.c_int32),
                 ("framing_path", ctypes.c_int32), ("partition_passes", ctypes.c_int32),
-                ("sharded", ctypes.c_int32), ("device_ms", ctypes.c_double)]
+                ("sharded", ctypes.c_int32), ("device_ms", ctypes.c_double), ("entry_bytes", ctypes.c_int32),
+                ("reserved0", ctypes.c_int32)]
 
     def as_dict(self) -> dict:
         return {f: getattr(self, f) for f, _ in self._fields_}
