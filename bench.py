@@ -33,7 +33,7 @@ import torch  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 METRIC = "keys/s device-resident hash-file build, 10M entries; HBM GB/s vs peak"
-PMC_SUMMARIES = [os.path.join(ROOT, "profiles", f) for f in ("r05_pmc_summary.json", "r04_pmc_summary.json", "r03_pmc_summary.json",
+PMC_SUMMARIES = [os.path.join(ROOT, "profiles", f) for f in ("r06_pmc_summary.json", "r05_pmc_summary.json", "r04_pmc_summary.json", "r03_pmc_summary.json",
                                                                "r02_pmc_summary.json", "r01_pmc_summary.json")]
 HASH_SEED = 0x2545F491
 
