@@ -827,6 +827,8 @@ def main():
         import torch.distributed as dist
         if args.backend == "nccl" and args.orchestrator == "python":
             dist.init_process_group("nccl", device_id=dev)
+        elif world == 1 and "RANK" not in os.environ:  # (--sharded at N = 1 without a launcher: a local store,
+            dist.init_process_group("gloo", store=dist.HashStore(), rank=0, world_size=1)  # so rocprofv3 can run it)
         else:  # (the C++ orchestrator moves the data over its own RCCL communicator)
             dist.init_process_group("gloo")
         r = sharded(args, dev, world, rank)

@@ -74,14 +74,20 @@ __host__ __device__ __forceinline__ int f3_off_lists(int cand_cap, int surv_cap)
 // sign says it failed, all ORed into one sign test (no chain of condition masks on the scalar unit).
 // delmask = -1 when the header counts no DELETE (a 0x00 first byte is then no start).  Bytes >= 0x80
 // (multi-byte VLQs) fail the maxima, which k_frame3's logs keep below 127 (fr_fast).
-__device__ __forceinline__ int32_t f3_step(const uint8_t* rgn, int32_t rp, int32_t lim, int32_t mk, int32_t mv,
-                                           int32_t delmask) {
+// kNoDel (the header counts no DELETE): a PUT's fields need no select (a zero first byte fails b0 - 1).
+template <bool kNoDel>
+__device__ __forceinline__ int32_t f3_step(const uint8_t* rgn, int32_t rp, int32_t lim, int32_t mk, int32_t mv) {
   const int32_t b0 = rgn[rp], b1 = rgn[rp + 1];
+  if (kNoDel) {
+    const int32_t kend = rp + 1 + b0;  // rp + 2 + (b0 - 1)
+    const int32_t bad = (mk + 1 - b0) | (mv - b1) | (lim - kend) | (b0 - 1);
+    return bad < 0 ? -1 : kend + b1;
+  }
   const bool del = b0 == 0;
   const int32_t klen = del ? b1 : b0 - 1;
   const int32_t vlen = del ? 0 : b1;
   const int32_t kend = rp + 2 + klen;
-  const int32_t bad = (mk - klen) | (mv - vlen) | (lim - kend) | ((b0 - 1) & delmask);
+  const int32_t bad = (mk - klen) | (mv - vlen) | (lim - kend);
   return bad < 0 ? -1 : kend + vlen;
 }
 
@@ -128,6 +134,7 @@ __device__ __forceinline__ void f3_stage(const BuildParams& P, const uint64_t wv
 }
 
 // One region (wave index wv) of k_frame3; its exit is published before any return.
+template <bool kNoDel>
 __device__ __forceinline__ void frame3_region(const BuildParams& P, const uint64_t wv, uint8_t* lds) {
   const int lane = threadIdx.x & 63;
   const int cs = P.fr_cshift;
@@ -142,6 +149,7 @@ __device__ __forceinline__ void frame3_region(const BuildParams& P, const uint64
   // listed record holds lies in LDS (records start inside the chunks)
   const int64_t RLEN = (int64_t)P.f3_rgn - ((int64_t)(W - nw) << cs);
   const int kF3CandCap = P.f3_cand_cap, kF3SurvCap = P.f3_surv_cap, kF3Lcap = P.f3_lcap;
+  const int kF3Lstride = kF3Lcap + 1;  // (a head's list: kF3Lcap starts and a spare slot)
   const int kF3OffLists = f3_off_lists(kF3CandCap, kF3SurvCap);
   uint8_t* rgn = lds;
   uint8_t* scr = lds + P.f3_rgn;
@@ -211,7 +219,6 @@ __device__ __forceinline__ void frame3_region(const BuildParams& P, const uint64
   const int32_t mk = (int32_t)P.max_key_len, mv = (int32_t)P.max_value_len;
   const int32_t mrl = (int32_t)P.max_rec_len;
   const int32_t look = (int32_t)LOOK;
-  const int32_t delmask = P.no_deletes ? -1 : 0;
   const int32_t ent0 = (int32_t)(P.fr_entry - R0);  // (wave 0) the frame's entry
   const int32_t C = 1 << cs;
   auto chunk_end = [&](int32_t j) -> int32_t { return min((j + 1) * C, de); };
@@ -313,7 +320,7 @@ __device__ __forceinline__ void frame3_region(const BuildParams& P, const uint64
       int32_t p = in ? st : -1;
       for (int t = 0; t < K; t++) {
         const bool go = p >= 0 && p < stop;
-        const int32_t q = f3_step(rgn, go ? p : 0, lim, mk, mv, delmask);
+        const int32_t q = f3_step<kNoDel>(rgn, go ? p : 0, lim, mk, mv);
         // (a start reached by a candidate that dies later dies too: marking it is harmless)
         if (cover && go && q >= 0 && q < e) atomicOr(&reached[q >> 5], 1u << (q & 31));
         p = go ? q : p;
@@ -364,27 +371,28 @@ __device__ __forceinline__ void frame3_region(const BuildParams& P, const uint64
   mark(2);
   if (P.f3_stop == 2) { stop(); return; }  // (SPARKEY_FRAME3_STOP: measurements)
 
-  // ---- 3 long walk: head `lane` to its chunk end + LOOK, listing its starts in the chunk.  One
-  //      wave-uniform loop while any head walks: a lane whose walk ended (or that has no head) stores
-  //      to the sink, so no store or exit needs an exec-mask branch. ----
+  // ---- 3 long walk: head `lane` to its exit (its first start at or past its chunk end), listing its
+  //      starts in the chunk.  One wave-uniform loop while any head walks.  Every lane stores its p
+  //      each step at its list's min(count, cap): a list has one spare slot past its cap, and a lane
+  //      without a head stores to the sink, so no store needs a select or an exec-mask branch.  (Round
+  //      5 walked on to the chunk end + LOOK, so that a false head dying there did not count; false
+  //      heads are about 1 in 15 waves at C3's shape, and a chunk whose alive heads disagree is
+  //      resolved from its entry all the same.) ----
   const bool hlane = lane < S;
   const int32_t hst = hlane ? (int32_t)s_start[hlane ? lane : 0] : 0;  // this lane's head
   int32_t hx = -1;                                                       // its exit (-1: died)
   int32_t hcnt = 0;                                                      // starts it lists
   {
-    const int32_t e = chunk_end(hst >> cs);
-    const int32_t stop = min(min(e + look, de), ruse);
-    uint16_t* my = lists + lane * kF3Lcap;
+    const int32_t e = chunk_end(hst >> cs);  // (<= de, and < ruse: every header below it is readable)
+    uint16_t* my = hlane ? lists + lane * kF3Lstride : sink;
     int32_t p = hlane ? hst : -1;
     int32_t ex = -1;
-    while (__ballot(p >= 0 && p < stop)) {
-      const bool go = p >= 0 && p < stop;
-      const bool lst = go && p < e;  // (a head starts inside its chunk)
-      uint16_t* d = lst && hcnt < kF3Lcap ? my + hcnt : sink;
-      *d = (uint16_t)p;
-      hcnt += lst ? 1 : 0;
-      const int32_t q = f3_step(rgn, go ? p : 0, lim, mk, mv, delmask);
-      ex = go && ex < 0 && q >= e ? q : ex;  // the first start at or past the chunk end
+    while (__ballot(p >= 0 && p < e)) {
+      const bool go = p >= 0 && p < e;
+      my[min(hcnt, kF3Lcap)] = (uint16_t)p;  // (a stopped lane's store lands past its count)
+      hcnt += go ? 1 : 0;
+      const int32_t q = f3_step<kNoDel>(rgn, max(p, 0), lim, mk, mv);
+      ex = go && q >= e ? q : ex;
       p = go ? q : p;
     }
     hx = p >= 0 ? ex : -1;
@@ -460,7 +468,7 @@ __device__ __forceinline__ void frame3_region(const BuildParams& P, const uint64
         sel = g;
         return s_exit[g];
       }
-      const uint16_t* lg = lists + g * kF3Lcap;
+      const uint16_t* lg = lists + g * kF3Lstride;
       const int32_t n = min((int32_t)s_cnt[g], kF3Lcap);
       int32_t k = 1;
       while (k < n && (int32_t)lg[k] < e) k++;
@@ -568,7 +576,7 @@ __device__ __forceinline__ void frame3_region(const BuildParams& P, const uint64
     // record r of the wave is entry r - base[j] of chunk j's chosen list (base: the scan of the
     // counts; the last chunk whose base is <= r, so empty chunks are passed over)
     const int32_t cbase = (int32_t)(incl - cnt);
-    const int32_t csrc = sel >= 0 ? sel * kF3Lcap + at : 0;
+    const int32_t csrc = sel >= 0 ? sel * kF3Lstride + at : 0;
     mark(5);
     if (P.f3_stop == 5) { stop(); return; }  // (SPARKEY_FRAME3_STOP: measurements)
     // Bucket regions: the entries leave as they are hashed, so a round redone after a wrong guess would
@@ -670,6 +678,7 @@ __device__ __forceinline__ void frame3_region(const BuildParams& P, const uint64
 // C3 10M on one box: one wave, no ticket 0.746 ms; 4 waves, ticket 0.856; 4 waves, no ticket 0.834;
 // 8 waves 1.27.  Persistent waves that stage their next region while the current one
 // finishes measured slower (round 5: 1.02-1.09 ms against 0.83).
+template <bool kNoDel>
 __global__ __launch_bounds__(64, kF3WavesPerSimd) void k_frame3(BuildParams P, uint32_t lds_per_wave) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   uint32_t tk = blockIdx.x;
@@ -679,7 +688,7 @@ __global__ __launch_bounds__(64, kF3WavesPerSimd) void k_frame3(BuildParams P, u
     tk = (uint32_t)__builtin_amdgcn_readfirstlane((int)t);
   }
   const uint64_t nwaves = (P.fr_nchunks + P.fr_w - 1) / P.fr_w;
-  if (tk < nwaves) frame3_region(P, tk, lds);
+  if (tk < nwaves) frame3_region<kNoDel>(P, tk, lds);
 }
 
 // LDS per wave: the staged region, then the scratch (candidates / record list, survivor data, lists
@@ -687,7 +696,7 @@ __global__ __launch_bounds__(64, kF3WavesPerSimd) void k_frame3(BuildParams P, u
 uint32_t frame3_lds_per_wave(const BuildParams& P) {
   const size_t bitmap = (size_t)P.fr_w * (size_t)((std::min<int64_t>(1ll << P.fr_cshift, P.max_rec_len) + 63) / 64) * 8;
   const size_t reached = P.f3_cover ? (size_t)((((int64_t)P.fr_w << P.fr_cshift) + P.fr_look + 31) / 32 + 1) * 4 : 0;
-  const size_t lists = (size_t)P.f3_surv_cap * P.f3_lcap * 2;
+  const size_t lists = (size_t)P.f3_surv_cap * (P.f3_lcap + 1) * 2;
   const size_t scratch =
       (size_t)f3_off_lists(P.f3_cand_cap, P.f3_surv_cap) + std::max<size_t>(std::max<size_t>(bitmap, reached), lists);
   return (uint32_t)(((size_t)P.f3_rgn + scratch + 15) & ~(size_t)15);
@@ -731,7 +740,8 @@ void launch_frame3(const BuildParams& P, hipStream_t s, StageTimer* tm) {
   if (P.fr_nchunks == 0) return;
   const uint64_t nwaves = (P.fr_nchunks + P.fr_w - 1) / P.fr_w;
   const uint32_t per = frame3_lds_per_wave(P);
-  hipLaunchKernelGGL(k_frame3, dim3((unsigned)nwaves), dim3(64), (size_t)per, s, P, per);
+  hipLaunchKernelGGL(P.no_deletes ? k_frame3<true> : k_frame3<false>, dim3((unsigned)nwaves), dim3(64), (size_t)per, s, P,
+                     per);
   tm->mark("frame", s);
   scan_exclusive<uint32_t, uint64_t, OpAdd>(P.wcount, P.woff, P.nslabs, (uint64_t*)&P.st->n_records, OpAdd(),
                                             P.scan_scratch_u64, s);

@@ -3,7 +3,7 @@
 # C2, C3 100M and C4 (1B) with their FETCH_SIZE / WRITE_SIZE passes (tools/pmc_summary.py into
 # $O/pmc_summary.json), the sharded 125M-record rank at N = 1 (the weak-scaling point), and a 2-rank
 # gloo rehearsal whose line carries the one-GPU build of the same log.
-#   usage: tools/meas.sh TAG [parts]   parts: any of bench,prof,c4prof,shard (default: all)
+#   usage: tools/meas.sh TAG [parts]   parts: any of bench,prof,c4prof,shardprof,shard (default: all but shardprof)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -37,8 +37,14 @@ fi
 if has c4prof; then
   prof c4_1000000000 "--workload c4 --steps 2 --warmup 1 --no-cpu-baseline" || exit 1
 fi
+if has shardprof; then  # a sharded rank's kernels and traffic (N = 1: no exchange, the rank's own steps)
+  prof sharded_rank_125000000 "--sharded --entries 125000000 --steps 2 --warmup 1 --no-check" || exit 1
+fi
 if has shard; then
-  b sharded_n1_125m --sharded --entries 125000000 --steps 5 --warmup 1 || exit 1
+  timeout -k 10 600 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
+    --master-port 29592 bench.py --sharded --entries 125000000 --steps 5 --warmup 1 \
+    > $O/sharded_n1_125m.jsonl 2> $O/sharded_n1_125m.err || { tail -20 $O/sharded_n1_125m.err; exit 1; }
+  tail -1 $O/sharded_n1_125m.jsonl | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('sharded n1', d['ms_per_step'], d['bit_identical_to_single_gpu'], d['phase_ms_rank0'], d['one_gpu_same_log'])"
   timeout -k 10 900 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
     --master-port 29593 bench.py --gpus 2 --backend gloo --entries 50000000 --steps 2 --warmup 1 \
     > $O/gloo_n2_50m.jsonl 2> $O/gloo_n2_50m.err || { tail -20 $O/gloo_n2_50m.err; exit 1; }
