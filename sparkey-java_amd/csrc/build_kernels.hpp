@@ -281,6 +281,11 @@ struct BuildParams {
   int64_t* seg_start; // per slot: exclusive max-scan of seg_mark (first slot of its run, 0 = wraps)
   uint32_t* seg_cls_cnt;  // segment lists: per-workgroup counts [3][blocks], and their scan
   uint64_t* seg_cls_off;
+  uint32_t* seg_len;    // per slot: distinct keys wanting it; then, at a segment's start, its length
+  uint64_t* seg_first;  // per segment start: the placement slot of its first placed PUT record
+  MaxPlus* seg_fun;     // per slot: the distinct-key carry functions composed before it (cap + 1)
+  uint32_t* seg_krep;   // per placed record: slots back to the first placed record with its key (0: itself)
+  uint32_t* ecls;       // per grouped record (ent3): its key's class, the rank of that first record in its segment
 };
 
 // Per-stage HIP events on the build stream (only when profiling is enabled).
@@ -323,7 +328,7 @@ bool part2_recv_fits(uint32_t bpp);
 void launch_dense_slabs(const BuildParams& P, hipStream_t s);
 void launch_frame_uniform(const BuildParams& P, hipStream_t s, StageTimer* tm);
 void launch_frame3(const BuildParams& P, hipStream_t s, StageTimer* tm);  // frame3_kernels.hip
-bool frame3_fits(BuildParams& P, double mean_record, double pass);
+bool frame3_fits(BuildParams& P, double mean_record, double pass, double mean_short);
 uint32_t frame3_lds_per_wave(const BuildParams& P);
 // framing paths: 0 k_frame, 1 serial walk, 2 k_frame_uniform, 4 k_frame3 (3 and 5 were the k_frame2 and
 // k_frame_lane experiments, measured slower and removed); the speculative ones with per-wave slabs
@@ -356,8 +361,8 @@ struct SideStreams {
 };
 void launch_segments(const BuildParams& P, hipStream_t s, int sorted_order, StageTimer* tm, bool check_each,
                      const SideStreams* side);
-constexpr unsigned kSegDebugWaves[3] = {4096, 2048, 512};   // k_seg_replay_wave grids (mid, large, huge)
-constexpr unsigned kSegDebugWords = (4096 + 2048 + 512) * 8;  // SPARKEY_EXACT_DEBUG: per-wave phase cycles
+constexpr unsigned kSegDebugWaves[4] = {4096, 2048, 512, 4096};   // k_seg_replay_wave grids (mid, large, huge), k_seg_lanes
+constexpr unsigned kSegDebugWords = (4096 + 2048 + 512 + 4096) * 8;  // SPARKEY_EXACT_DEBUG: per-wave phase cycles
 void launch_partition_quiet(const BuildParams& P, hipStream_t s);
 // sharded builds (shard_kernels.hip)
 void launch_dest_counts(const BuildParams& P, hipStream_t s, int world, uint32_t nd, uint64_t* d_out);

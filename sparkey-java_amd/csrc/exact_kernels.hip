@@ -2,11 +2,14 @@
 // canonical layout does not cover: DELETE records and duplicate keys (overwrites).
 //
 //   k_sequential      one lane over the whole table: tables whose PUT records leave no empty slot
-//   k_seg_marks/scan  the first slot of every run of occupied slots of the canonical PUT placement
-//   k_seg_assign      every record -> the slot segment holding its wanted slot
-//   k_seg_scatter     records grouped by segment
+//   k_seg_dcount      distinct keys per wanted slot, from the canonical placement of every PUT record
+//   scan, k_seg_dmarks the occupied slots of the distinct keys' placement, and their runs (segments)
+//   k_seg_first/runs  each segment's placed PUT records (contiguous in that placement) and its length
+//   k_seg_assign      every DELETE -> the slot segment holding its wanted slot
+//   k_seg_puts/scatter records grouped by segment (the table is then cleared for the replay)
 //   k_seg_classify    segments listed by size class
-//   k_seg_small       one thread per small segment: sort, clear, replay on the .spi slots in HBM
+//   k_seg_lanes       one lane per small segment: records numbered in replay order, key classes, the
+//                     segment's slots in LDS
 //   k_seg_replay_wave one wave per larger segment: records, their header fields, short keys and the
 //                     segment's slots staged in LDS, bitonic sort, put / delete evaluated 64 slots
 //                     per step, slots written back
@@ -14,14 +17,18 @@
 // Why segments are independent.  occ(S), the set of slots a linear-probing table of the multiset S of
 // wanted slots occupies, depends neither on insertion order, nor on the Robin-Hood tie rule, nor on
 // in-place replacement or backward-shift deletion (every entry sits at w + d with slots w .. w + d
-// all occupied), and it grows with S.  Every table state IndexHash passes through holds a subset of
-// the log's PUT keys, so a slot the canonical placement of ALL PUT records (duplicates included,
-// DELETEs left out) leaves empty is empty in every state: no put probe, delete probe or backward
-// shift ever crosses it.  The runs of occupied slots of that placement -- segments -- therefore
-// evolve independently.  Each one replays its own records in the reference's order (log order for
-// IN_MEMORY; SortHelper's (wantedSlot, address) for SORTING, SortHelper.java:153-171) with the
-// reference's put / delete on its own slots; a DELETE whose wanted slot is empty there is a no-op in
-// every state.  The result is the reference's table byte for byte.
+// all occupied), and it grows with S.  Every table state IndexHash passes through holds each of the
+// log's distinct PUT keys at most once: a put of a key the table holds meets it before it can steal
+// a slot (IndexHash.java:606-653: the key's wanted-slot group comes first, and the tie rule never
+// steals inside it, since the new address is the group's largest -- log order, or SortHelper's
+// (wantedSlot, address) order).  So a slot that the canonical placement of the DISTINCT PUT keys
+// leaves empty is empty in every state: no put probe, delete probe or backward shift ever crosses it.
+// The runs of occupied slots of that placement -- segments -- therefore evolve independently.  (Round
+// 5 placed every PUT record, repeats included: a sparser placement with repeats left out has far
+// shorter runs -- churn's 9M PUT records hold 5.4M keys.)  Each segment replays its own records in the
+// reference's order (log order for IN_MEMORY; SortHelper's (wantedSlot, address) for SORTING,
+// SortHelper.java:153-171) with the reference's put / delete on its own slots; a DELETE whose wanted
+// slot is empty there is a no-op in every state.  The result is the reference's table byte for byte.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -44,7 +51,10 @@ constexpr uint32_t kHugeSegMax = 1024;
 constexpr unsigned kMidGrid = 4096;
 constexpr unsigned kLargeGrid = 2048;
 constexpr unsigned kHugeGrid = 512;
-constexpr int kSegClasses = 4;
+constexpr unsigned kLaneGrid = 4096;  // k_seg_lanes: 64 small segments a wave at a time, from a work queue
+constexpr int kSegClasses = 4;   // small (k_seg_lanes), mid, large, huge (k_seg_replay_wave)
+constexpr int kSmallLists = 6;   // the small class's lists, by record count
+constexpr int kSegLists = kSmallLists + kSegClasses - 1;
 constexpr int kClsBlock = 256;            // k_seg_classify: 4 slots per thread
 constexpr int kClsItems = 4;
 constexpr uint64_t kClsSlots = (uint64_t)kClsBlock * kClsItems;
@@ -53,18 +63,57 @@ constexpr uint64_t kClsSlots = (uint64_t)kClsBlock * kClsItems;
 // the input) sets a bit of st->guard, skips the access, and the host fails the build loudly.
 __device__ __forceinline__ void guard_trip(const BuildParams& P, unsigned bit) { atomicOr(&P.st->guard, bit); }
 
+// 16 log bytes from position p >= 0, as four little-endian words: five aligned dword loads, issued
+// together, each 4 bytes out one v_alignbit (a byte loop is one dependent round trip per byte).  A
+// dword is read only when it starts inside the log (the buffer is 16-byte aligned, so the rest of
+// that dword is allocated); bytes at or past log_len are left to the caller's bounds.
+struct Bytes16 {
+  uint32_t w[4];
+  __device__ __forceinline__ uint32_t byte(uint32_t k) const {  // k < 16 (shifts and a select: a dynamic
+    const uint64_t lo = (uint64_t)w[0] | ((uint64_t)w[1] << 32);  // index into w would go to scratch)
+    const uint64_t hi = (uint64_t)w[2] | ((uint64_t)w[3] << 32);
+    return (uint32_t)((k < 8 ? lo >> (8u * k) : hi >> (8u * (k - 8u))) & 0xffu);
+  }
+};
+__device__ __forceinline__ Bytes16 log16(const BuildParams& P, int64_t p) {
+  const int64_t b = p & ~3ll;
+  const uint32_t* d = reinterpret_cast<const uint32_t*>(P.log + b);
+  uint32_t x[5];
+#pragma unroll
+  for (int i = 0; i < 5; i++) x[i] = b + 4 * i < (int64_t)P.log_len ? d[i] : 0u;
+  const uint32_t sh = (uint32_t)(p & 3) * 8u;
+  Bytes16 r;
+#pragma unroll
+  for (int i = 0; i < 4; i++) r.w[i] = __builtin_amdgcn_alignbit(x[i + 1], x[i], sh);
+  return r;
+}
+
 __device__ __forceinline__ bool keys_equal(const BuildParams& P, int64_t k1, int64_t k2, int32_t len) {
   if (len < 0 || k1 < 0 || k2 < 0 || k1 + len > (int64_t)P.log_len || k2 + len > (int64_t)P.log_len) {
     guard_trip(P, 1u);
     return false;
   }
-  for (int32_t j = 0; j < len; j++)
-    if (P.log[k1 + j] != P.log[k2 + j]) return false;
+  for (int32_t j = 0; j < len; j += 16) {  // 16 bytes of each key a step
+    const Bytes16 x = log16(P, k1 + j), y = log16(P, k2 + j);
+    const int32_t r = len - j;
+    uint32_t diff = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const int32_t nb = min(max(r - 4 * i, 0), 4);  // bytes of word i inside the key
+      const uint32_t m = nb >= 4 ? ~0u : (1u << (8 * nb)) - 1u;
+      diff |= (x.w[i] ^ y.w[i]) & m;
+    }
+    if (diff) return false;
+  }
   return true;
 }
+// The record header at address (decode_header's rules, on 16 bytes loaded at once: a header is at
+// most 10 bytes).
 __device__ __forceinline__ RecHdr log_header(const BuildParams& P, uint64_t address) {
-  auto at = [&](int64_t a) -> uint32_t { return P.log[a]; };
-  return decode_header(at, (int64_t)(address >> P.ebb), (int64_t)P.log_len);
+  const int64_t p = (int64_t)(address >> P.ebb);
+  const Bytes16 b = log16(P, p);
+  auto at = [&](int64_t a) -> uint32_t { return b.byte((uint32_t)(a - p)); };
+  return decode_header(at, p, (int64_t)P.log_len);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -307,17 +356,121 @@ __global__ void k_sequential(BuildParams P, int sorted_order) {
 // ================================================================================================
 // Segments
 // ================================================================================================
-__device__ __forceinline__ bool slot_occupied(const BuildParams& P, uint64_t slot) {
-  uint64_t h, a;
-  read_slot(P, slot, h, a);
-  return a != 0;
+__device__ __forceinline__ uint64_t prev_slot(const BuildParams& P, uint64_t t) { return t == 0 ? P.cap - 1 : t - 1; }
+__device__ __forceinline__ uint64_t next_slot(const BuildParams& P, uint64_t t) { return t + 1 == P.cap ? 0 : t + 1; }
+// The wanted slot of the record the canonical placement left in slot t (kNoSeg: t is empty).
+__device__ __forceinline__ uint64_t placed_wanted(const BuildParams& P, uint64_t t, uint64_t& h, uint64_t& a) {
+  read_slot(P, t, h, a);
+  return a ? fast_mod(h, P.mod) : kNoSeg;
 }
 
-// mark[i] = i + 1 for an empty slot, 0 for an occupied one; its exclusive max-scan gives every slot
-// the first slot of its run (<= 0: the run wraps, it starts after the table's last empty slot)
-__global__ __launch_bounds__(256) void k_seg_marks(BuildParams P) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < P.cap) P.seg_mark[i] = slot_occupied(P, i) ? 0 : (int64_t)(i + 1);
+// Do the records at addresses a (header ha) and a2 hold the same key?  (IndexHash.java:606-636)
+__device__ __forceinline__ bool same_key_at(const BuildParams& P, uint64_t a, const RecHdr& ha, uint64_t a2) {
+  const RecHdr hb = log_header(P, a2);
+  return ha.rc == 0 && hb.rc == 0 && ha.klen == hb.klen &&
+         keys_equal(P, (int64_t)(a >> P.ebb) + ha.hlen, (int64_t)(a2 >> P.ebb) + hb.hlen, ha.klen);
+}
+
+// The first member of slot g0's group, from g0 up to (not including) slot `end`, with hash h and the
+// key of the record at address a (header ha): its slot, or kNoSeg.  Equal keys share a hash: the first
+// member with hash h usually holds the key (a second key of that hash is a 64-bit -- or 32-bit --
+// collision), so one comparison settles it.
+__device__ uint64_t first_with_key(const BuildParams& P, uint64_t g0, uint64_t end, uint64_t h, uint64_t a,
+                                   const RecHdr& ha) {
+  for (uint64_t j = g0, g = 0; j != end && g < P.cap; j = next_slot(P, j), g++) {
+    uint64_t h2, a2;
+    read_slot(P, j, h2, a2);
+    if (h2 == h && same_key_at(P, a, ha, a2)) return j;
+  }
+  return kNoSeg;
+}
+
+// c[w] (P.seg_len, zeroed) = the distinct keys among the placed PUT records that want slot w, and each
+// placed record's key class: seg_krep[t] = slots back to the group's first record with its key (0:
+// itself, the key's first).  The canonical placement orders each run by wanted slot, so a wanted
+// slot's records (its group) sit in consecutive slots, and equal keys share a hash and so a group.
+// Each wave sums its lanes' first-of-key flags per group; a group that continues past the wave adds
+// atomically.
+__global__ __launch_bounds__(256) void k_seg_dcount(BuildParams P) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint64_t h = 0, a = 0;
+  const uint64_t w = t < P.cap ? placed_wanted(P, t, h, a) : kNoSeg;
+  bool first_of_key = w != kNoSeg;
+  if (first_of_key) {
+    // the group's first member with this hash (the whole group back: a repeated key's records are
+    // usually its only members with that hash)
+    constexpr int kStep = 4;  // slots read together, backwards
+    uint64_t e = kNoSeg;
+    bool more = true;
+    for (uint64_t g = 0, j = t; more && g < P.cap; g += kStep) {
+      uint64_t hb[kStep], ab[kStep], jb[kStep];
+#pragma unroll
+      for (int q = 0; q < kStep; q++) {
+        const uint64_t back = (uint64_t)(q + 1) % P.cap;
+        jb[q] = j >= back ? j - back : j + P.cap - back;
+        read_slot(P, jb[q], hb[q], ab[q]);
+      }
+#pragma unroll
+      for (int q = 0; q < kStep; q++) {
+        if (!more) continue;
+        if (!ab[q] || fast_mod(hb[q], P.mod) != w || g + (uint64_t)q + 1 >= P.cap) {
+          more = false;
+          continue;
+        }
+        if (hb[q] == h) e = jb[q];
+      }
+      j = jb[kStep - 1];
+    }
+    uint32_t back = 0;
+    if (e != kNoSeg) {
+      const RecHdr ha = log_header(P, a);
+      const uint64_t r = first_with_key(P, e, t, h, a, ha);
+      if (r != kNoSeg) back = (uint32_t)(t >= r ? t - r : t + P.cap - r);
+    }
+    P.seg_krep[t] = back;
+    first_of_key = back == 0;
+  }
+  // this wave's lanes of the group: consecutive, from the head lane (hidx) to the group's last lane
+  const uint32_t wl = (uint32_t)w, wh = (uint32_t)(w >> 32);
+  const uint64_t wp = ((uint64_t)(uint32_t)wave_prev_i32((int32_t)wh, -1) << 32) | (uint32_t)wave_prev_i32((int32_t)wl, -1);
+  const uint64_t wn = ((uint64_t)(uint32_t)wave_next_i32((int32_t)wh, -1) << 32) | (uint32_t)wave_next_i32((int32_t)wl, -1);
+  const bool head = lane == 0 || wp != w;
+  const bool last = lane == 63 || wn != w;
+  const uint32_t incl = wave_incl_sum_u32(first_of_key ? 1u : 0u);
+  const int32_t hidx = wave_incl_max_i32(head ? lane : -1);
+  const uint32_t before = (uint32_t)__shfl((int)incl, max(hidx - 1, 0), 64);
+  if (w == kNoSeg || !last) return;
+  const uint32_t cnt = incl - (hidx > 0 ? before : 0u);
+  // the group may go on before the wave's first slot or after this one (around the ring too)
+  uint64_t h2, a2;
+  bool open = hidx == 0 && placed_wanted(P, prev_slot(P, t - (uint64_t)lane), h2, a2) == w;
+  if (!open && (lane == 63 || t + 1 == P.cap)) open = placed_wanted(P, next_slot(P, t), h2, a2) == w;
+  if (!open) P.seg_len[w] = cnt;
+  else if (cnt) atomicAdd(&P.seg_len[w], cnt);
+}
+
+// The carry out of a slot of the distinct keys' placement: max(0, carry in + c - 1).
+struct DistinctCount {
+  uint32_t c;
+  __device__ __forceinline__ explicit operator MaxPlus() const { return MaxPlus{0, (int64_t)c - 1}; }
+};
+
+// mark[s] = s + 1 for a slot the distinct keys' placement leaves empty, 0 for an occupied one: carry
+// in + c[s] >= 1.  F[s] composes the carry functions of the slots before s from slot 0 (F[cap]: all of
+// them); the carry into slot 0 is F[cap](0), the carry out of the last slot when slot 0 starts from 0
+// -- exact, because the placement of every PUT record has an empty slot (else k_sequential), empty
+// in the sparser placement too, where both carries are 0 and agree from there on.  Its exclusive
+// max-scan gives every slot the first slot of its run (<= 0: the run wraps, it starts after the
+// table's last empty slot).
+__global__ __launch_bounds__(256) void k_seg_dmarks(BuildParams P) {
+  const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= P.cap) return;
+  const MaxPlus tot = P.seg_fun[P.cap];
+  const int64_t c0 = max(tot.c, tot.a);
+  const MaxPlus f = P.seg_fun[s];
+  const int64_t cin = max(f.c, c0 + f.a);
+  P.seg_mark[s] = cin + (int64_t)P.seg_len[s] >= 1 ? 0 : (int64_t)(s + 1);
 }
 
 // kSegSlabs slabs a 64-thread workgroup: each thread follows that many records' dependent random
@@ -331,24 +484,107 @@ __device__ __forceinline__ uint64_t run_start(const BuildParams& P, uint64_t t, 
   return m > 0 ? (uint64_t)m : (uint64_t)last % P.cap;
 }
 
-// The PUT records of a segment are exactly the entries the canonical placement left in its run (every
-// PUT record, duplicates included, was placed; occ(S) does not depend on the order), so a run's PUT
-// count is its length: the empty slot that ends a run writes it at the run's start, with no atomics.
+// The segment of the placed record in slot t (kNoSeg: t is empty); its wanted slot lies in the
+// distinct keys' placement (its key's first record wants it too).
+__device__ __forceinline__ uint64_t placed_segment(const BuildParams& P, uint64_t t, uint64_t& h, uint64_t& a,
+                                                   int64_t last) {
+  const uint64_t w = placed_wanted(P, t, h, a);
+  if (w == kNoSeg) return kNoSeg;
+  if (P.seg_mark[w] != 0) {
+    guard_trip(P, 256u);
+    return kNoSeg;
+  }
+  return run_start(P, w, last);
+}
+
+// A segment's PUT records are the placed records whose wanted slots lie in its run: consecutive in
+// the placement, which orders each of its runs by wanted slot.  The first of them records its slot.
+__global__ __launch_bounds__(256) void k_seg_first(BuildParams P) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= P.cap) return;
+  const int64_t last = P.seg_mark[P.cap];
+  uint64_t h, a;
+  const uint64_t d = placed_segment(P, t, h, a, last);
+  if (d == kNoSeg) return;
+  if (placed_segment(P, prev_slot(P, t), h, a, last) != d) P.seg_first[d] = t;
+}
+
+// Per segment: its PUT record count (written by its last placed record, no atomics) into seg_cnt,
+// and its length (written by the empty slot that ends it) into seg_len.
 __global__ __launch_bounds__(256) void k_seg_runs(BuildParams P) {
-  const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= P.cap || P.seg_mark[e] == 0) return;  // (occupied)
-  const uint64_t p = e == 0 ? P.cap - 1 : e - 1;
-  if (P.seg_mark[p] == 0) {
-    const uint64_t st = run_start(P, p, P.seg_mark[P.cap]);
-    P.seg_cnt[st] = (uint32_t)(e >= st ? e - st : e + P.cap - st);
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= P.cap) return;
+  const int64_t last = P.seg_mark[P.cap];
+  uint64_t h, a;
+  const uint64_t d = placed_segment(P, t, h, a, last);
+  if (d != kNoSeg && placed_segment(P, next_slot(P, t), h, a, last) != d) {
+    const uint64_t f = P.seg_first[d];
+    P.seg_cnt[d] = (uint32_t)((t >= f ? t - f : t + P.cap - f) + 1);
+  }
+  if (P.seg_mark[t] != 0 && P.seg_mark[prev_slot(P, t)] == 0) {
+    const uint64_t st = run_start(P, prev_slot(P, t), last);
+    P.seg_len[st] = (uint32_t)(t >= st ? t - st : t + P.cap - st);
   }
 }
 
-// DELETE records (the PUT records come from the table, k_seg_puts): each finds the first slot of the
-// segment holding its wanted slot and counts itself there.  A slot is occupied when its mark is 0.
-// kSegSlabs slabs a 64-thread workgroup (several chains a thread in flight).
+// A DELETE's key class: the rank in its segment d of the first placed PUT record with its key, or kNoSeg
+// when no PUT record holds its key (the DELETE then removes nothing in any state).  The placement's
+// slots from the wanted slot w on hold records of earlier wanted slots, then w's group.
+__device__ uint64_t delete_class(const BuildParams& P, uint64_t w, uint64_t h, uint64_t a, uint64_t d) {
+  const RecHdr ha = log_header(P, a);  // (its key's length and place: loaded while the slots are probed)
+  constexpr int kStep = 4;             // slots read together (the probe passes about as many at 0.77 load)
+  uint64_t t = w;
+  for (uint64_t g = 0; g < P.cap; g += kStep) {
+    uint64_t hb[kStep], ab[kStep], tb[kStep];
+#pragma unroll
+    for (int j = 0; j < kStep; j++) {
+      tb[j] = wrap_slot(t + (uint64_t)j, P.cap);
+      read_slot(P, tb[j], hb[j], ab[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < kStep; j++) {
+      if (!ab[j]) return kNoSeg;
+      const uint64_t w2 = fast_mod(hb[j], P.mod), u = tb[j];
+      const uint64_t dt = u >= w2 ? u - w2 : u + P.cap - w2;  // (displacements at u)
+      const uint64_t dw = u >= w ? u - w : u + P.cap - w;
+      if (dt < dw) return kNoSeg;  // past where w's group would be: no record wants w
+      if (dt == dw && hb[j] == h && same_key_at(P, a, ha, ab[j])) {  // w's group: the first with the key
+        const uint64_t f = P.seg_first[d];
+        return u >= f ? u - f : u + P.cap - f;
+      }
+    }
+    t = wrap_slot(t + kStep, P.cap);
+  }
+  return kNoSeg;
+}
+
+// The segment and key class of DELETE entry idx (delete_class), counted at the segment's start.
+__device__ __forceinline__ void delete_segment(const BuildParams& P, uint64_t idx, int64_t last) {
+  const Entry en = P.ent[idx];
+  const uint64_t w = fast_mod(en.hash, P.mod);
+  uint64_t seg = run_start(P, w, last);
+  const uint64_t cls = delete_class(P, w, en.hash, en.addr & ~kDelBit, seg);
+  if (cls == kNoSeg) {
+    seg = kNoSeg;  // (no PUT record holds its key: a no-op in every state too)
+  } else if (cls >= (1ull << 24) || seg >= (1ull << 40)) {
+    guard_trip(P, 512u);
+    seg = kNoSeg;
+  } else {
+    atomicAdd(&P.seg_cnt[seg], 1u);
+    seg |= cls << 40;
+  }
+  P.eseg[idx] = seg;
+}
+
+// DELETE records (the PUT records come from the table, k_seg_puts): each whose wanted slot lies in a
+// segment is queued in LDS and the wave works them 64 at a time, one a lane (its probe of the placement
+// is a chain of dependent reads: a lane per record, not one per slab entry, keeps the lanes busy); a
+// DELETE whose wanted slot is empty there is a no-op in every state.  kSegSlabs slabs a 64-thread
+// workgroup.
 __global__ __launch_bounds__(64) void k_seg_assign(BuildParams P) {
-  const int64_t last = P.seg_mark[P.cap];  // (last empty slot) + 1
+  __shared__ uint64_t q[64 * (kSegSlabs + 1)];
+  const int64_t last = P.seg_mark[P.cap];
+  const int lane = threadIdx.x;
   uint32_t n[kSegSlabs], nmax = 0;
 #pragma unroll
   for (uint32_t k = 0; k < kSegSlabs; k++) {
@@ -356,47 +592,49 @@ __global__ __launch_bounds__(64) void k_seg_assign(BuildParams P) {
     n[k] = w < P.nslabs ? P.wcount[w] : 0u;
     nmax = max(nmax, n[k]);
   }
-  for (uint32_t j = threadIdx.x; j < nmax; j += 64) {
-    uint64_t idx[kSegSlabs], sl[kSegSlabs];
-    bool del[kSegSlabs];
-    int64_t mk[kSegSlabs];
+  uint32_t qn = 0;  // (wave-uniform)
+  for (uint32_t j0 = 0; j0 < nmax; j0 += 64) {
+    const uint32_t j = j0 + (uint32_t)lane;
 #pragma unroll
     for (uint32_t k = 0; k < kSegSlabs; k++) {
-      idx[k] = ((uint64_t)blockIdx.x * kSegSlabs + k) * P.slab_cap + j;
-      Entry en{0, 0};
-      if (j < n[k]) en = P.ent[idx[k]];
-      del[k] = j < n[k] && (en.addr & kDelBit);
-      sl[k] = del[k] ? fast_mod(en.hash, P.mod) : 0;
-    }
-#pragma unroll
-    for (uint32_t k = 0; k < kSegSlabs; k++) mk[k] = del[k] ? P.seg_mark[sl[k]] : 1;
-#pragma unroll
-    for (uint32_t k = 0; k < kSegSlabs; k++) {
-      if (!del[k]) continue;
-      uint64_t seg = kNoSeg;
-      if (mk[k] == 0) {  // (a DELETE whose wanted slot is empty is a no-op in every state)
-        seg = run_start(P, sl[k], last);
-        atomicAdd(&P.seg_cnt[seg], 1u);
+      const uint64_t idx = ((uint64_t)blockIdx.x * kSegSlabs + k) * P.slab_cap + j;
+      bool listed = false;
+      if (j < n[k]) {
+        const Entry en = P.ent[idx];
+        if (en.addr & kDelBit) {
+          listed = P.seg_mark[fast_mod(en.hash, P.mod)] == 0;
+          if (!listed) P.eseg[idx] = kNoSeg;
+        }
       }
-      P.eseg[idx[k]] = seg;
+      const unsigned long long bal = __ballot(listed);
+      if (listed) q[qn + (uint32_t)__builtin_popcountll(bal & ((1ull << lane) - 1ull))] = idx;
+      qn += (uint32_t)__builtin_popcountll(bal);
     }
+    __syncthreads();
+    for (; qn >= 64; qn -= 64) delete_segment(P, q[qn - 64 + (uint32_t)lane], last);  // (one a lane)
+    __syncthreads();
   }
+  if ((uint32_t)lane < qn) delete_segment(P, q[lane], last);
 }
 
-// The PUT records grouped by segment straight from the table: occupied slot t is record t - start of
+// The PUT records grouped by segment straight from the table: placed record t is record t - first of
 // its segment's list (slot order; the replay sorts a segment itself).  Reads and writes in slot order.
 __global__ __launch_bounds__(256) void k_seg_puts(BuildParams P) {
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= P.cap || P.seg_mark[t] != 0) return;
-  const uint64_t st = run_start(P, t, P.seg_mark[P.cap]);
-  const uint64_t dst = P.seg_off[st] + (t >= st ? t - st : t + P.cap - st);
-  if (dst >= P.max_records) {
+  if (t >= P.cap) return;
+  uint64_t h, a;
+  const uint64_t d = placed_segment(P, t, h, a, P.seg_mark[P.cap]);
+  if (d == kNoSeg) return;
+  const uint64_t f = P.seg_first[d];
+  const uint64_t r = t >= f ? t - f : t + P.cap - f;
+  const uint64_t dst = P.seg_off[d] + r;
+  const uint32_t back = P.seg_krep[t];
+  if (dst >= P.max_records || dst >= P.seg_off[d + 1] || back > r) {
     guard_trip(P, 32u);
     return;
   }
-  uint64_t h, a;
-  read_slot(P, t, h, a);
   P.ent3[dst] = Entry{h, a};
+  P.ecls[dst] = (uint32_t)(r - back);  // (the rank of its key's first record)
 }
 
 // The DELETE records after their segment's PUT records: seg_cnt still holds run length + DELETEs, and
@@ -418,8 +656,11 @@ __global__ __launch_bounds__(64) void k_seg_scatter(BuildParams P) {
       seg[k] = kNoSeg;
       if (j < n[k] && (P.ent[idx[k]].addr & kDelBit)) seg[k] = P.eseg[idx[k]];
     }
+    uint32_t cls[kSegSlabs];
 #pragma unroll
     for (uint32_t k = 0; k < kSegSlabs; k++) {
+      cls[k] = seg[k] != kNoSeg ? (uint32_t)(seg[k] >> 40) : 0u;  // (delete_class, packed by k_seg_assign)
+      if (seg[k] != kNoSeg) seg[k] &= (1ull << 40) - 1;
       if (seg[k] != kNoSeg && seg[k] >= P.cap) {
         guard_trip(P, 32u);
         seg[k] = kNoSeg;
@@ -435,6 +676,7 @@ __global__ __launch_bounds__(64) void k_seg_scatter(BuildParams P) {
         continue;
       }
       P.ent3[dst] = P.ent[idx[k]];
+      P.ecls[dst] = cls[k];
     }
   }
 }
@@ -442,12 +684,16 @@ __global__ __launch_bounds__(64) void k_seg_scatter(BuildParams P) {
 // Segment lists by size class (the arrays are free once the records are grouped): small segments in
 // seg_mark, mid ones from the front of eseg, big ones from its back.  Stream compaction without
 // global atomics: per-workgroup class counts, one scan, then every workgroup writes its runs.
+// List of segment s: small ones by record count (1, 2, 3-4, 5-8, 9-16, 17-24: lists 0-5, one list in
+// that order, so that a wave's 64 lanes replay segments of about one size), then mid, large, huge (6-8).
 __device__ __forceinline__ int seg_class(const BuildParams& P, uint64_t s) {
   if (s >= P.cap) return -1;
   const uint64_t n = P.seg_off[s + 1] - P.seg_off[s];
   if (n == 0) return -1;
-  return n <= kSmallSegOps ? 0 : n <= kMidSegMax ? 1 : n <= kLargeSegMax ? 2 : 3;
+  if (n <= kSmallSegOps) return n <= 1 ? 0 : n <= 2 ? 1 : n <= 4 ? 2 : n <= 8 ? 3 : n <= 16 ? 4 : 5;
+  return n <= kMidSegMax ? 6 : n <= kLargeSegMax ? 7 : 8;
 }
+__device__ __forceinline__ int list_class(int l) { return l < kSmallLists ? 0 : l - kSmallLists + 1; }
 // list of size class c: small in seg_mark, mid at the front of eseg, large at its back, huge in
 // seg_start (all free once the records are grouped)
 __device__ __forceinline__ uint64_t seg_list_cap(const BuildParams& P, int c) {
@@ -463,35 +709,38 @@ __device__ __forceinline__ uint64_t* seg_list_slot(const BuildParams& P, int c, 
 }
 
 __global__ __launch_bounds__(kClsBlock) void k_seg_classify(BuildParams P, int write) {
-  __shared__ uint32_t wsum[kSegClasses][kClsBlock / 64];
+  __shared__ uint32_t wsum[kSegLists][kClsBlock / 64];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const uint64_t s0 = (uint64_t)blockIdx.x * kClsSlots + (uint64_t)tid * kClsItems;
   int cls[kClsItems];
-  uint32_t c[kSegClasses] = {0, 0, 0, 0};
+  uint32_t c[kSegLists];
+#pragma unroll
+  for (int k = 0; k < kSegLists; k++) c[k] = 0;
 #pragma unroll
   for (int i = 0; i < kClsItems; i++) {
     cls[i] = seg_class(P, s0 + i);
-    if (cls[i] >= 0) c[cls[i]]++;
+#pragma unroll
+    for (int k = 0; k < kSegLists; k++) c[k] += cls[i] == k ? 1u : 0u;
   }
   const uint32_t nblk = gridDim.x;
-  if (!write) {  // per-workgroup counts, class-major
-    for (int k = 0; k < kSegClasses; k++) {
+  if (!write) {  // per-workgroup counts, list-major
+    for (int k = 0; k < kSegLists; k++) {
       uint32_t v = c[k];
 #pragma unroll
       for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
       if (lane == 0) wsum[k][wv] = v;
     }
     __syncthreads();
-    if (tid < kSegClasses) {
+    if (tid < kSegLists) {
       uint32_t t = 0;
       for (int w = 0; w < kClsBlock / 64; w++) t += wsum[tid][w];
       P.seg_cls_cnt[(uint64_t)tid * nblk + blockIdx.x] = t;
     }
     return;
   }
-  // exclusive rank of this thread's segments inside the workgroup, per class
-  uint32_t ex[kSegClasses];
-  for (int k = 0; k < kSegClasses; k++) {
+  // exclusive rank of this thread's segments inside the workgroup, per list
+  uint32_t ex[kSegLists];
+  for (int k = 0; k < kSegLists; k++) {
     uint32_t incl = c[k];
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -502,19 +751,28 @@ __global__ __launch_bounds__(kClsBlock) void k_seg_classify(BuildParams P, int w
     ex[k] = incl - c[k];
   }
   __syncthreads();
-  for (int k = 0; k < kSegClasses; k++)
+  for (int k = 0; k < kSegLists; k++)
     for (int w = 0; w < wv; w++) ex[k] += wsum[k][w];
+  // a list's place in its class list: the small lists one after another, the others alone
   const uint64_t* off = P.seg_cls_off;
-  uint64_t pos[kSegClasses];
-  for (int k = 0; k < kSegClasses; k++) pos[k] = off[(uint64_t)k * nblk + blockIdx.x] - off[(uint64_t)k * nblk] + ex[k];
+  uint64_t pos[kSegLists];
+  for (int k = 0; k < kSegLists; k++)
+    pos[k] = off[(uint64_t)k * nblk + blockIdx.x] - off[(uint64_t)(k < kSmallLists ? 0 : k) * nblk] + ex[k];
 #pragma unroll
   for (int i = 0; i < kClsItems; i++) {
     if (cls[i] < 0) continue;
-    const uint64_t at = pos[cls[i]]++;
-    if (at < seg_list_cap(P, cls[i])) *seg_list_slot(P, cls[i], at) = s0 + i;
+    uint64_t at = 0;
+#pragma unroll
+    for (int k = 0; k < kSegLists; k++)
+      if (cls[i] == k) at = pos[k]++;
+    const int cl = list_class(cls[i]);
+    if (at < seg_list_cap(P, cl)) *seg_list_slot(P, cl, at) = s0 + i;
     else guard_trip(P, 64u);
   }
-  if (blockIdx.x == 0 && tid < kSegClasses) P.st->n_segs[tid] = off[(uint64_t)(tid + 1) * nblk] - off[(uint64_t)tid * nblk];
+  if (blockIdx.x == 0 && tid < kSegClasses) {
+    const int l0 = tid == 0 ? 0 : tid + kSmallLists - 1, l1 = tid == 0 ? kSmallLists : l0 + 1;
+    P.st->n_segs[tid] = off[(uint64_t)l1 * nblk] - off[(uint64_t)l0 * nblk];
+  }
 }
 
 // replay order: IN_MEMORY = address (log order); SORTING = (wantedSlot, address), the table's wanted
@@ -540,11 +798,7 @@ __device__ void replay_segment_hbm(const BuildParams& P, uint64_t s, Entry* L, u
     }
     L[j] = v;
   }
-  uint64_t t = s;
-  for (uint64_t g = 0; g < P.cap && slot_occupied(P, t); g++) {  // clear the canonical placement
-    write_slot(P, t, 0, 0);
-    t = t + 1 == P.cap ? 0 : t + 1;
-  }
+  (void)s;  // (the table was cleared after the grouping: the segment's slots start empty)
   Replay<HbmTable> r{&P, HbmTable{&P}, 0, 0};
   for (uint64_t i = 0; i < n; i++)
     if (!replay_one(r, L[i], 0)) break;
@@ -552,19 +806,214 @@ __device__ void replay_segment_hbm(const BuildParams& P, uint64_t s, Entry* L, u
   acc[1] += r.garbage;
 }
 
-__global__ __launch_bounds__(256) void k_seg_small(BuildParams P, int sorted_order) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  int64_t acc[2] = {0, 0};
-  if (i < P.st->n_segs[0]) {
-    const uint64_t s = *seg_list_slot(P, 0, i);
-    if (s < P.cap && P.seg_off[s + 1] <= P.max_records) {
-      const uint64_t lo = P.seg_off[s];
-      replay_segment_hbm(P, s, P.ent3 + lo, P.seg_off[s + 1] - lo, sorted_order, acc);
-    } else {
-      guard_trip(P, 4u);
+// ------------------------------------------------------------------------------------------------
+// k_seg_lanes: the small segments (<= kSmallSegOps records), one lane each, replayed in LDS.  Every
+// record carries its key's class (ecls: the rank in its segment of the first placed PUT record with
+// that key), so where IndexHash compares hashes and then both keys (IndexHash.java:606-636) a lane
+// compares two bytes, and the log is read only for the garbage sizes of removed records.  Records are
+// renumbered in replay order (IN_MEMORY: address; SORTING: the table's wanted slot, then address), which
+// inside one wanted slot's group is address order: the tie rule (address < address2) compares the
+// numbers.  Slots hold record numbers (0xff: empty); local slot index = slot - segment start, and a
+// record's local wanted slot is its displacement origin (the segment's run never wraps in local terms).
+// LDS arrays are [element][lane]: a lane's accesses to element i of its own arrays hit consecutive
+// words across the wave, free of bank conflicts.
+// ------------------------------------------------------------------------------------------------
+constexpr uint32_t kLaneRecs = kSmallSegOps;
+constexpr uint32_t kLaneDel = 0x80;         // class byte: a DELETE record
+constexpr uint32_t kLaneFree = 0xffffffffu;  // an empty slot
+constexpr uint32_t kLaneBatch = 8;          // global loads a lane issues together
+struct LaneLds {
+  uint64_t key[kLaneRecs][64];       // replay-order keys; then the removed records' numbers (bytes)
+  uint32_t slot[kLaneRecs + 1][64];  // local slot -> its record: number | wanted << 8 | class << 16
+  uint16_t attr[kLaneRecs][64];      // list index, then record number -> local wanted slot | class << 8
+  uint8_t perm[kLaneRecs][64];       // record number -> list index
+};
+
+__global__ __launch_bounds__(64) void k_seg_lanes(BuildParams P, int sorted_order) {
+  __shared__ LaneLds L;
+  const int lane = threadIdx.x;
+  const unsigned long long nseg = P.st->n_segs[0];
+  int64_t entries = 0, garbage = 0;
+  uint8_t* rem = reinterpret_cast<uint8_t*>(&L.key[0][0]);  // (removed numbers: rem[q * 64 + lane])
+  unsigned long long* dbg = P.dbg ? P.dbg + (kMidGrid + kLargeGrid + kHugeGrid + blockIdx.x) * 8 : nullptr;
+  unsigned long long t_prev = 0;
+  auto mark = [&](int i) {  // diagnostic only (SPARKEY_EXACT_DEBUG=1): cycles per phase, per wave
+    if (dbg && lane == 0) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      if (i >= 0) dbg[i] += t - t_prev;
+      t_prev = t;
+    }
+  };
+  for (;;) {
+    uint32_t kq = 0;
+    if (lane == 0) kq = atomicAdd(&P.st->seg_next[0], 64u);
+    const unsigned long long k0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)kq);
+    if (k0 >= nseg) break;
+    mark(-1);
+    const unsigned long long k = k0 + (uint64_t)lane;
+    uint64_t s0 = 0, lo = 0;
+    uint32_t n = 0, len = 0;
+    if (k < nseg) {
+      s0 = *seg_list_slot(P, 0, k);
+      if (s0 < P.cap && P.seg_off[s0 + 1] <= P.max_records && P.seg_off[s0 + 1] - P.seg_off[s0] <= kLaneRecs) {
+        lo = P.seg_off[s0];
+        n = (uint32_t)(P.seg_off[s0 + 1] - lo);
+        len = min(n, P.seg_len[s0]);
+      } else {
+        guard_trip(P, 4u);
+      }
+    }
+    // replay-order keys (IN_MEMORY: address; SORTING: the table's wanted slot -- the segment's local
+    // order, except that slots past the table's end come first -- then address), local wanted slots
+    // and key classes (list indices of first records)
+    const uint64_t t0 = window_to_table(s0, P.mod);
+    for (uint32_t i0 = 0; i0 < n; i0 += kLaneBatch) {  // (a batch's loads in flight together)
+      Entry eb[kLaneBatch];
+      uint32_t cb[kLaneBatch];
+#pragma unroll
+      for (uint32_t j = 0; j < kLaneBatch; j++) {
+        eb[j] = i0 + j < n ? P.ent3[lo + i0 + j] : Entry{0, 0};
+        cb[j] = i0 + j < n ? P.ecls[lo + i0 + j] : 0u;
+      }
+#pragma unroll
+      for (uint32_t j = 0; j < kLaneBatch; j++) {
+        if (i0 + j >= n) continue;
+        const uint64_t wl = fast_mod(eb[j].hash, P.mod);
+        const uint64_t l = wl >= s0 ? wl - s0 : wl + P.cap - s0;
+        const uint64_t addr = eb[j].addr & ~kDelBit;
+        if (l >= len || (addr >> 58)) guard_trip(P, 1024u);
+        uint64_t key = addr;
+        if (sorted_order) key |= (l + (window_to_table(wl, P.mod) < t0 ? 0ull : 32ull)) << 58;
+        L.key[i0 + j][lane] = key;
+        L.attr[i0 + j][lane] = (uint16_t)(min(l, (uint64_t)kLaneRecs) |
+                                          ((min(cb[j], kLaneRecs - 1) | ((eb[j].addr & kDelBit) ? kLaneDel : 0u)) << 8));
+      }
+    }
+    mark(0);
+    // record number = rank of the key (addresses are distinct, so are the keys); perm keeps the list
+    // index and slot[i] (free until the replay) the number of list index i
+    for (uint32_t i = 0; i < n; i++) {
+      const uint64_t ki = L.key[i][lane];
+      uint32_t r = 0;
+#pragma unroll
+      for (uint32_t j = 0; j < kLaneRecs; j++) r += j < n && L.key[j][lane] < ki ? 1u : 0u;
+      L.perm[r][lane] = (uint8_t)i;
+      L.slot[i][lane] = r;
+    }
+    // attributes by number (through the key array, free now), the classes (first records' list
+    // indices) as numbers too
+    uint16_t* tmp = reinterpret_cast<uint16_t*>(&L.key[0][0]);
+    for (uint32_t r = 0; r < n; r++) tmp[r * 64 + lane] = L.attr[L.perm[r][lane]][lane];
+    for (uint32_t r = 0; r < n; r++) {
+      const uint32_t v = tmp[r * 64 + lane];
+      const uint32_t c = v >> 8;
+      const uint32_t cn = L.slot[c & 0x7f][lane];
+      L.attr[r][lane] = (uint16_t)((v & 0xff) | ((cn | (c & kLaneDel)) << 8));
+    }
+    for (uint32_t i = 0; i <= len; i++) L.slot[i][lane] = kLaneFree;
+    mark(1);
+    // the replay: IndexHash.put / delete (IndexHash.java:454-665) on the lane's slots, each probe step
+    // one LDS word (the occupant's number, wanted slot and class)
+    uint32_t nrem = 0;
+    for (uint32_t r = 0; r < n; r++) {
+      const uint32_t at = L.attr[r][lane];
+      uint32_t s = at & 0xff;
+      if (!((at >> 8) & kLaneDel)) {
+        uint32_t C = r | (at << 8);  // the carried entry, packed as a slot word
+        bool might = true;
+        for (uint32_t g = 0; g <= len; g++, s++) {
+          if (s > len) {
+            guard_trip(P, 2048u);
+            break;
+          }
+          const uint32_t o = L.slot[s][lane];
+          if (o == kLaneFree) {
+            L.slot[s][lane] = C;
+            entries++;
+            break;
+          }
+          if (might && ((o >> 16) & 0x7f) == ((C >> 16) & 0x7f)) {  // same key: replaced in place
+            L.slot[s][lane] = C;
+            rem[nrem++ * 64 + lane] = (uint8_t)o;
+            break;
+          }
+          const uint32_t d = s - ((C >> 8) & 0xff), d2 = s - ((o >> 8) & 0xff);
+          if (d > d2 || (d == d2 && (C & 0xff) < (o & 0xff))) {  // steal the slot, carry its occupant on
+            L.slot[s][lane] = C;
+            C = o;
+            might = false;
+          }
+        }
+      } else {
+        const uint32_t myc = (at >> 8) & 0x7f;
+        const uint32_t w0 = s;
+        for (uint32_t g = 0; g <= len; g++, s++) {
+          if (s > len) {
+            guard_trip(P, 2048u);
+            break;
+          }
+          const uint32_t o = L.slot[s][lane];
+          if (o == kLaneFree) break;
+          if (((o >> 16) & 0x7f) == myc) {  // found: backward shift (IndexHash.java:503-524)
+            rem[nrem++ * 64 + lane] = (uint8_t)o;
+            entries--;
+            for (uint32_t g2 = 0; g2 < len && s < len; g2++) {
+              const uint32_t o3 = L.slot[s + 1][lane];
+              if (o3 == kLaneFree || ((o3 >> 8) & 0xff) == s + 1) break;
+              L.slot[s][lane] = o3;
+              s++;
+            }
+            L.slot[s][lane] = kLaneFree;
+            break;
+          }
+          if (s - w0 > s - ((o >> 8) & 0xff)) break;  // displacement > the other's: not there
+        }
+      }
+    }
+    mark(2);
+    // garbage of the removed records (IndexHeader.java:221-228), their headers read together
+    for (uint32_t q0 = 0; q0 < nrem; q0 += kLaneBatch) {
+      uint64_t ab8[kLaneBatch];
+#pragma unroll
+      for (uint32_t j = 0; j < kLaneBatch; j++)
+        ab8[j] = q0 + j < nrem ? P.ent3[lo + L.perm[rem[(q0 + j) * 64 + lane]][lane]].addr & ~kDelBit : 0ull;
+      RecHdr hb[kLaneBatch];
+#pragma unroll
+      for (uint32_t j = 0; j < kLaneBatch; j++)
+        if (q0 + j < nrem) hb[j] = log_header(P, ab8[j]);
+#pragma unroll
+      for (uint32_t j = 0; j < kLaneBatch; j++) {
+        if (q0 + j >= nrem) continue;
+        if (hb[j].rc) set_error(P.st, (int64_t)(ab8[j] >> P.ebb), header_error(hb[j]));
+        else garbage += garbage_of(hb[j].klen, hb[j].vlen);
+      }
+    }
+    // the segment's slots to the table (cleared before the replay)
+    for (uint32_t i0 = 0; i0 < len; i0 += kLaneBatch) {
+      Entry eb[kLaneBatch];
+#pragma unroll
+      for (uint32_t j = 0; j < kLaneBatch; j++) {
+        const uint32_t o = i0 + j < len ? L.slot[i0 + j][lane] : kLaneFree;
+        eb[j] = o != kLaneFree ? P.ent3[lo + L.perm[o & 0xff][lane]] : Entry{0, 0};
+      }
+#pragma unroll
+      for (uint32_t j = 0; j < kLaneBatch; j++) {
+        if (i0 + j >= len || !eb[j].addr) continue;
+        uint64_t t = s0 + i0 + j;
+        if (t >= P.cap) t -= P.cap;
+        write_slot(P, t, eb[j].hash, eb[j].addr & ~kDelBit);
+      }
+    }
+    mark(3);
+    if (dbg) {
+      const unsigned long long nw = wave_sum_u64(n);
+      if (lane == 0) {
+        dbg[4] += 1;
+        dbg[5] += nw;
+      }
     }
   }
-  commit_counts(P, acc[0], acc[1]);
+  commit_counts(P, entries, garbage);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -887,12 +1336,11 @@ __global__ __launch_bounds__(64) void k_seg_replay_wave(BuildParams P, int sorte
     }
     const uint32_t n = (uint32_t)n64;
     if (lane == 0) {
-      L.len = n;
+      L.len = min(n, P.seg_len[s0]);  // (the run of the distinct keys' placement: at most n slots)
       L.nrec = n;
     }
     __syncthreads();
-    // stage the records (header fields, short keys); the segment's length = its first empty slot,
-    // at most n slots in
+    // stage the records (header fields, short keys)
     for (uint32_t i = lane; i < n; i += 64) {
       const Entry en = P.ent3[lo + i];
       L.ops[i] = en;
@@ -905,7 +1353,14 @@ __global__ __launch_bounds__(64) void k_seg_replay_wave(BuildParams P, int sorte
         if (h.rc == 0 && h.klen >= 0 && h.klen <= (int32_t)KEYB) {
           const int64_t kp = (int64_t)((en.addr & ~kDelBit) >> P.ebb) + h.hlen;
           if (kp + h.klen <= (int64_t)P.log_len) {
-            for (int32_t b = 0; b < h.klen; b++) kw[b >> 3] |= (uint64_t)P.log[kp + b] << (8 * (b & 7));
+            static_assert(KEYB <= 16, "keys staged from one 16-byte load");
+            const Bytes16 kb = log16(P, kp);
+#pragma unroll
+            for (uint32_t q = 0; q < KEYB / 8; q++) {
+              const int32_t nb = min(max(h.klen - 8 * (int32_t)q, 0), 8);  // key bytes of word q
+              const uint64_t v = (uint64_t)kb.w[2 * q] | ((uint64_t)kb.w[2 * q + 1] << 32);
+              kw[q] = nb >= 8 ? v : v & ((1ull << (8 * nb)) - 1ull);
+            }
           } else {
             guard_trip(P, 2u);
           }
@@ -913,9 +1368,6 @@ __global__ __launch_bounds__(64) void k_seg_replay_wave(BuildParams P, int sorte
 #pragma unroll
         for (uint32_t q = 0; q < KEYB / 8; q++) L.keys[i * (KEYB / 8) + q] = kw[q];
       }
-      uint64_t slot = s0 + i;
-      if (slot >= P.cap) slot -= P.cap;
-      if (!slot_occupied(P, slot)) atomicMin(&L.len, i);
     }
     uint32_t n2 = 1;
     while (n2 < n) n2 <<= 1;
@@ -996,11 +1448,19 @@ void launch_segments(const BuildParams& P, hipStream_t s, int sorted_order, Stag
     fflush(stderr);
   };
   const unsigned slot_grid = (unsigned)((P.cap + 255) / 256);
-  hipLaunchKernelGGL(k_seg_marks, dim3(slot_grid), dim3(256), 0, s, P);
+  // the distinct keys' placement: its occupied slots, their runs (the segments), each segment's PUT
+  // records in the placement of every PUT record and its length (seg_len zeroed by the caller)
+  hipLaunchKernelGGL(k_seg_dcount, dim3(slot_grid), dim3(256), 0, s, P);
+  step("distinct counts");
+  scan_exclusive<DistinctCount, MaxPlus, OpMaxPlus>(reinterpret_cast<const DistinctCount*>(P.seg_len), P.seg_fun,
+                                                    P.cap, P.seg_fun + P.cap, OpMaxPlus(), P.seg_fun + P.cap + 1, s);
+  step("carry scan");
+  hipLaunchKernelGGL(k_seg_dmarks, dim3(slot_grid), dim3(256), 0, s, P);
   step("marks");
   scan_exclusive<int64_t, int64_t, OpMaxI64>(P.seg_mark, P.seg_start, P.cap, P.seg_mark + P.cap, OpMaxI64(),
                                              reinterpret_cast<int64_t*>(P.scan_scratch_u64), s);
   step("start scan");
+  hipLaunchKernelGGL(k_seg_first, dim3(slot_grid), dim3(256), 0, s, P);
   hipLaunchKernelGGL(k_seg_runs, dim3(slot_grid), dim3(256), 0, s, P);
   step("runs");
   const unsigned seg_grid = (unsigned)((P.nslabs + kSegSlabs - 1) / kSegSlabs);
@@ -1012,11 +1472,14 @@ void launch_segments(const BuildParams& P, hipStream_t s, int sorted_order, Stag
   hipLaunchKernelGGL(k_seg_puts, dim3(slot_grid), dim3(256), 0, s, P);
   if (P.nslabs) hipLaunchKernelGGL(k_seg_scatter, dim3(seg_grid), dim3(64), 0, s, P);
   step("scatter");
+  // the records are grouped: the replays start from an empty table (slots outside every segment stay
+  // empty; the placement of every PUT record filled some of them)
+  (void)hipMemsetAsync(P.out + kIndexHeaderSize, 0, (size_t)P.cap * (size_t)P.slot_size, s);
   const unsigned cls_grid = (unsigned)((P.cap + kClsSlots - 1) / kClsSlots);
   hipLaunchKernelGGL(k_seg_classify, dim3(cls_grid), dim3(kClsBlock), 0, s, P, 0);
   step("classify counts");
-  scan_exclusive<uint32_t, uint64_t, OpAdd>(P.seg_cls_cnt, P.seg_cls_off, (uint64_t)kSegClasses * cls_grid,
-                                            P.seg_cls_off + (uint64_t)kSegClasses * cls_grid, OpAdd(), P.scan_scratch_u64, s);
+  scan_exclusive<uint32_t, uint64_t, OpAdd>(P.seg_cls_cnt, P.seg_cls_off, (uint64_t)kSegLists * cls_grid,
+                                            P.seg_cls_off + (uint64_t)kSegLists * cls_grid, OpAdd(), P.scan_scratch_u64, s);
   step("classify scan");
   hipLaunchKernelGGL(k_seg_classify, dim3(cls_grid), dim3(kClsBlock), 0, s, P, 1);
   step("classify lists");
@@ -1041,7 +1504,7 @@ void launch_segments(const BuildParams& P, hipStream_t s, int sorted_order, Stag
   step("large");
   hipLaunchKernelGGL((k_seg_replay_wave<kMidSegMax, 16, 1>), dim3(kMidGrid), dim3(64), 0, sm, P, sorted_order);
   step("mid");
-  hipLaunchKernelGGL(k_seg_small, dim3(slot_grid), dim3(256), 0, s, P, sorted_order);
+  hipLaunchKernelGGL(k_seg_lanes, dim3(kLaneGrid), dim3(64), 0, s, P, sorted_order);
   step("small");
   if (fork) {
     for (int i = 0; i < 3; i++) {

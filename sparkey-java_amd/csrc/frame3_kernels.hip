@@ -612,11 +612,11 @@ __device__ __forceinline__ void frame3_region(const BuildParams& P, const uint64
       const uint32_t off = lists[act ? src : src0];
       // (listed records passed f3_step's rules on the walk that listed them: one-byte VLQs, PUT =
       //  klen + 1 then vlen, DELETE = 0 then klen; their keys lie in LDS, see RLEN)
-      const uint64_t hb = rgn_u64(rgn, off);
+      const uint32_t hb = rgn_u32(rgn, off);
       const int32_t b0 = (int32_t)(hb & 0xff), b1 = (int32_t)((hb >> 8) & 0xff);
       const bool put = b0 != 0;
       const int32_t klen = put ? b0 - 1 : b1;
-      const RgnKey ld{rgn, off + 2u};
+      const RgnKey4 ld(rgn, off + 2u);
       const uint64_t hash = P.hash_size == 8 ? murmur64_ld(ld, klen, (uint32_t)P.seed)
                                              : (uint64_t)murmur32_ld(ld, klen, (uint32_t)P.seed);
       const int64_t p = R0 + (int64_t)off;
@@ -707,13 +707,16 @@ uint32_t frame3_lds_per_wave(const BuildParams& P) {
 // that a random byte pair passes the screen) plus 32, and at least 1.7x its expected records + 32;
 // when that allows, it is trimmed so that as many workgroups as the VGPRs allow fit a CU.  False when the lists
 // cannot hold what the header's mean record implies (k_frame frames such logs).
-bool frame3_fits(BuildParams& P, double mean_record, double pass) {
+bool frame3_fits(BuildParams& P, double mean_record, double pass, double mean_short) {
   const double C = (double)(1ll << P.fr_cshift);
   if (!P.fr_fast || P.max_rec_len > 4096 || P.fr_cshift < 7) return false;
   if (mean_record <= 0.0 || C / mean_record > 0.6 * kF3LcapMax) return false;
   // a head's list: 16 starts while a chunk holds up to about 10 mean records, else 1 / 0.6 of its mean
   // records (long chunks: fewer, longer chains a wave)
   P.f3_lcap = C / mean_record <= 0.6 * 16 ? 16 : std::min(kF3LcapMax, ((int)std::ceil(C / mean_record / 0.6) + 7) & ~7);
+  // and a chunk of the log's shorter records alone (the mean of its shorter kind, DELETEs or PUTs)
+  if (mean_short > 0.0 && mean_short < mean_record)
+    P.f3_lcap = std::max(P.f3_lcap, std::min(kF3LcapMax, ((int)std::ceil(C / mean_short) + 8 + 7) & ~7));
   const int64_t tail = std::max<int64_t>(P.fr_look, P.max_rec_len);  // (the keys of the last chunk's records)
   if (((int64_t)P.fr_w << P.fr_cshift) + tail + 16 >= 32768) return false;  // 15-bit region offsets
   P.f3_rgn = (int32_t)((((int64_t)P.fr_w << P.fr_cshift) + tail + 16 + 15) & ~15ll);

@@ -233,6 +233,25 @@ struct RgnKey {
   uint32_t base;
   __device__ __forceinline__ uint64_t u64(int o) const { return rgn_u64(r, base + (uint32_t)o); }
 };
+// The same key through aligned dwords: the loaders read at key offsets that are multiples of 8, so
+// the byte shift inside a dword is one per key and each 4 bytes out is one v_alignbit of two dwords
+// (the 64-bit funnel above costs five instructions per 8 bytes).
+__device__ __forceinline__ uint32_t rgn_u32(const uint8_t* r, uint32_t o) {
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(r + (o & ~3u));
+  return __builtin_amdgcn_alignbit(w[1], w[0], (o & 3u) * 8u);
+}
+struct RgnKey4 {
+  const uint32_t* w;  // the dword holding the key's first byte
+  uint32_t sh;        // 8 x the first byte's place in it
+  __device__ __forceinline__ RgnKey4(const uint8_t* r, uint32_t base)
+      : w(reinterpret_cast<const uint32_t*>(r + (base & ~3u))), sh((base & 3u) * 8u) {}
+  __device__ __forceinline__ uint64_t u64(int o) const {
+    const uint32_t* p = w + (o >> 2);
+    const uint32_t a = p[0], b = p[1], c = p[2];
+    return (uint64_t)__builtin_amdgcn_alignbit(b, a, sh) |
+           ((uint64_t)__builtin_amdgcn_alignbit(c, b, sh) << 32);
+  }
+};
 
 // Record header at absolute position p inside the region (p - R0 + 16 <= region bytes).
 __device__ __forceinline__ RecHdr decode_rgn(const uint8_t* r, int64_t R0, int64_t p, int64_t avail) {

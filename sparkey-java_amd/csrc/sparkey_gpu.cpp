@@ -318,7 +318,12 @@ struct sparkey_plan {
   uint8_t* sn_par = nullptr;        // the parallel directory's scratch (candidates, anchors, links)
   hipStream_t sn_stream = nullptr;  // the decode of one directory chunk overlaps the next chunk
   hipEvent_t sn_ev[2] = {nullptr, nullptr};
-  uint64_t c_seg_cls_cnt = 0, c_seg_cls_off = 0;
+  uint64_t c_seg_cls_cnt = 0, c_seg_cls_off = 0, c_seg_len = 0, c_seg_first = 0, c_seg_fun = 0, c_seg_krep = 0, c_ecls = 0;
+  uint32_t* seg_krep = nullptr;   // exact path: per placed record, slots back to its key's first record
+  uint32_t* ecls = nullptr;       // exact path: per grouped record, its key's class
+  uint32_t* seg_len = nullptr;    // exact path: distinct keys per wanted slot, then segment lengths
+  uint64_t* seg_first = nullptr;  // exact path: per segment, the slot of its first placed PUT record
+  MaxPlus* seg_fun = nullptr;     // exact path: the distinct keys' carry functions, scanned
   // sharded compressed logs (sk_cz_*): the rank's part of the block directory and its
   // slice [vbase, vend) of the virtual log, decoded into sn_vlog from global offset vlo
   struct CzState {
@@ -619,7 +624,12 @@ static bool want_frame3(BuildParams& P, const LogHdr& lh, int64_t entry, int64_t
   // starts -- a log's shorter records -- would otherwise make two heads a chunk)
   Q.f3_cover = (double)Q.max_rec_len > 1.5 * mean || 2 * Q.fr_w + 8 > 64 ? 1 : 0;
   if (knob_set(Knob::Frame3Cover)) Q.f3_cover = knob(Knob::Frame3Cover) ? 1 : 0;
-  if (!frame3_fits(Q, mean, pk)) return false;
+  // (a chunk's list holds its records: a stretch of a log's shorter kind -- DELETEs -- packs more of
+  // them than the mean says; churn's 18-byte DELETEs among 118-byte PUTs overflowed 16-start lists)
+  double mean_short = mean;
+  if (lh.num_deletes > 0 && lh.delete_size > 0) mean_short = std::min(mean_short, (double)lh.delete_size / (double)lh.num_deletes);
+  if (lh.num_puts > 0 && lh.put_size > 0) mean_short = std::min(mean_short, (double)lh.put_size / (double)lh.num_puts);
+  if (!frame3_fits(Q, mean, pk, mean_short)) return false;
   // (C3's shape, pk 0.1: K = 3 measured 0.870 ms against K = 2's 0.903 per 10M records,
   // profiles/r03/k_frame3_sweep_c3_10m.txt)
   Q.f3_short = pk < 0.05 ? 2 : pk < 0.3 ? 3 : 4;
@@ -1168,8 +1178,13 @@ static int run_exact_segments(sparkey_plan* pl, BuildParams& P, bool in_memory, 
   HIP_TRY(grow(&pl->seg_off, pl->c_seg_off, P.cap + 1));
   HIP_TRY(grow(&pl->seg_mark, pl->c_seg_mark, P.cap + 1));
   HIP_TRY(grow(&pl->seg_start, pl->c_seg_start, P.cap));
-  HIP_TRY(grow(&pl->seg_cls_cnt, pl->c_seg_cls_cnt, 4 * (P.cap / 1024 + 1)));
-  HIP_TRY(grow(&pl->seg_cls_off, pl->c_seg_cls_off, 4 * (P.cap / 1024 + 1) + 1));
+  HIP_TRY(grow(&pl->seg_cls_cnt, pl->c_seg_cls_cnt, 9 * (P.cap / 1024 + 1)));  // (k_seg_classify's 9 lists)
+  HIP_TRY(grow(&pl->seg_cls_off, pl->c_seg_cls_off, 9 * (P.cap / 1024 + 1) + 1));
+  HIP_TRY(grow(&pl->seg_len, pl->c_seg_len, P.cap));
+  HIP_TRY(grow(&pl->seg_first, pl->c_seg_first, P.cap));
+  HIP_TRY(grow(&pl->seg_fun, pl->c_seg_fun, P.cap + 1 + 2 * (P.cap / kScanTile + 64)));  // (+ the scan's scratch)
+  HIP_TRY(grow(&pl->seg_krep, pl->c_seg_krep, P.cap));
+  HIP_TRY(grow(&pl->ecls, pl->c_ecls, P.max_records));
   const uint64_t scratch = P.cap / kScanTile + 64;
   if (pl->c_su < scratch + 16) {
     HIP_TRY(grow(&pl->scan_u64, pl->c_su, scratch + 16));
@@ -1182,7 +1197,13 @@ static int run_exact_segments(sparkey_plan* pl, BuildParams& P, bool in_memory, 
   P.seg_start = pl->seg_start;
   P.seg_cls_cnt = pl->seg_cls_cnt;
   P.seg_cls_off = pl->seg_cls_off;
+  P.seg_len = pl->seg_len;
+  P.seg_first = pl->seg_first;
+  P.seg_fun = pl->seg_fun;
+  P.seg_krep = pl->seg_krep;
+  P.ecls = pl->ecls;
   HIP_TRY(hipMemsetAsync(P.seg_cnt, 0, P.cap * sizeof(uint32_t), s));
+  HIP_TRY(hipMemsetAsync(P.seg_len, 0, P.cap * sizeof(uint32_t), s));
   HIP_TRY(hipMemsetAsync((uint8_t*)pl->d_status + offsetof(Status, num_entries), 0, 2 * sizeof(long long), s));
   HIP_TRY(hipMemsetAsync((uint8_t*)pl->d_status + offsetof(Status, n_segs), 0, sizeof(((Status*)0)->n_segs), s));
   const int64_t dbg_level = knob(Knob::ExactDebug);
@@ -1207,8 +1228,8 @@ static int run_exact_segments(sparkey_plan* pl, BuildParams& P, bool in_memory, 
     std::vector<unsigned long long> h(kSegDebugWords);
     HIP_TRY(hipMemcpyAsync(h.data(), pl->dbg, h.size() * 8, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
-    static const char* cname[3] = {"mid", "large", "huge"};
-    for (int c = 0, b0 = 0; c < 3; b0 += kSegDebugWaves[c], c++) {
+    static const char* cname[4] = {"mid", "large", "huge", "lanes (stage, rank, replay, write)"};
+    for (int c = 0, b0 = 0; c < 4; b0 += kSegDebugWaves[c], c++) {
       const unsigned b1 = b0 + kSegDebugWaves[c];
       double sum[8] = {0};
       unsigned long long mx[8] = {0};
@@ -1863,7 +1884,7 @@ void sparkey_plan_destroy(sparkey_plan* pl) {
                   pl->bcount, pl->bcursor, pl->boff, pl->bfun, pl->bpre, pl->bfun_total, pl->carry, pl->pairs,
                   pl->dfun, pl->dcarry, pl->parts, pl->p1_fill, pl->scan_u64, pl->scan_mp, pl->desc, pl->p1_hist, pl->p1_off, pl->d_status, pl->dbg, pl->wcount, pl->woff, pl->small,
                   pl->eseg, pl->seg_cnt, pl->seg_off, pl->seg_mark, pl->seg_start, pl->bstat_start,
-                  pl->seg_cls_cnt, pl->seg_cls_off, pl->p2tab,
+                  pl->seg_cls_cnt, pl->seg_cls_off, pl->seg_len, pl->seg_first, pl->seg_fun, pl->seg_krep, pl->ecls, pl->p2tab,
                   pl->app_i64, pl->app_u32, pl->app_u64, pl->app_scan, pl->app_map,
                   pl->sn_blocks, pl->sn_dir, pl->sn_walk, pl->sn_recoff, pl->sn_vlog, pl->sn_itab, pl->sn_err,
                   pl->xtab, pl->ex_starts, pl->ex_cnt, pl->ex_off, pl->sn_par, pl->delp};
