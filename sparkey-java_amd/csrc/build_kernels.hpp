@@ -51,6 +51,7 @@ struct CEntry {
 };
 static_assert(sizeof(CEntry) == 12, "12-byte compact entries");
 constexpr int kCompactIn = 1, kCompactOut = 2;  // BuildParams.compact's bits
+constexpr uint32_t kSub = 64;                   // two-level pass 2: sub-digit regions a coarse digit
 
 // Carry function f(x) = max(c, x + a) of a bucket (see k_summary).
 struct MaxPlus {
@@ -264,6 +265,11 @@ struct BuildParams {
   // regions (ent3: k_frame_uniform -> pass 2), bit 1 (kCompactOut) the bucket regions (ent2: pass 2 ->
   // k_summary / k_place_reg); every other path keeps 16-byte Entry
   int32_t compact;
+  // two-level pass 2 (k_part2_sub -> k_part2f<.., kSubIn>, tables of thousands of buckets a digit): kSub sub-digit
+  // regions of sub_region entries a digit in sub_ent, their fill cursors in sub_fill (0: one level)
+  uint64_t sub_region;
+  uint32_t* sub_fill;
+  Entry* sub_ent;
   // sharded: the carry-in composed on the device from every rank's carry function (world x {c, a});
   // k_carry then also clears the placement's status counters
   const int64_t* carry_funs;

@@ -1499,6 +1499,9 @@ __global__ __launch_bounds__(kPart2Block) void k_part2d(BuildParams P) {
   }
 }
 
+// buckets of a sub-digit of the two-level pass 2 (k_part2_sub)
+__host__ __device__ inline uint32_t sub_buckets(uint32_t bpp) { return (bpp + kSub - 1) / kSub; }
+
 // k_part2f: k_part2d's staged scatter in ONE read of the digit's entries, into fixed bucket regions
 // (bucket b's entries at ent2[b * kPlaceLdsMax ..), as k_part2st writes them) for tables of more than
 // kP2SortedMaxBpp buckets per digit: no histogram pass, the bucket counts are the cursors at the end.
@@ -1508,17 +1511,31 @@ __global__ __launch_bounds__(kPart2Block) void k_part2d(BuildParams P) {
 // a thread per round: 6 where the LDS holds them, fewer for the largest tables (C4's 4960 buckets a
 // digit: 2, whose rounds are shorter than the bucket count -- runs of about one entry).  Single GPU.
 // kC: 12-byte CEntry digit regions in and bucket regions out (BuildParams.compact).
-template <int kPer, bool kC>
+// kSubIn: a workgroup per sub-digit of the two-level pass (k_part2_sub's regions in P.sub_ent: its
+// bucket_sub buckets from the digit's sb-th on) instead of a workgroup per coarse digit.
+template <int kPer, bool kC, bool kSubIn = false>
 __global__ __launch_bounds__(kPart2Block) void k_part2f(BuildParams P) {
   // cur[nb] | rc0[nb] | rc1[nb] | roff[nb] | gbase[nb] | stage[kPart2Block * kPer]
   extern __shared__ __attribute__((aligned(16))) uint32_t dyn[];
   __shared__ uint64_t sh64[kPart2Block / 64 + 1];
   if (build_aborted(P)) return;
   const uint32_t dpart = blockIdx.x;
-  const uint64_t lo = (uint64_t)dpart * P.p1_region;
-  const uint64_t hi = lo + min((uint64_t)P.p1_fill[dpart], P.p1_region);
-  const uint32_t nbins = P.bpp;
-  const uint32_t b0 = dpart * nbins;
+  uint64_t lo, hi;
+  uint32_t nbins, b0;
+  const Entry* src = P.ent3;
+  if (kSubIn) {
+    const uint32_t d = dpart / kSub, first = (dpart % kSub) * sub_buckets(P.bpp);
+    nbins = first < P.bpp ? min(sub_buckets(P.bpp), P.bpp - first) : 0u;
+    b0 = d * P.bpp + first;
+    lo = (uint64_t)dpart * P.sub_region;
+    hi = lo + min((uint64_t)P.sub_fill[dpart], P.sub_region);
+    src = P.sub_ent;
+  } else {
+    lo = (uint64_t)dpart * P.p1_region;
+    hi = lo + min((uint64_t)P.p1_fill[dpart], P.p1_region);
+    nbins = P.bpp;
+    b0 = dpart * nbins;
+  }
   uint32_t* cur = dyn;
   uint32_t* rc[2] = {cur + nbins, cur + 2 * nbins};
   uint32_t* roff = cur + 3 * nbins;
@@ -1534,7 +1551,7 @@ __global__ __launch_bounds__(kPart2Block) void k_part2f(BuildParams P) {
 #pragma unroll
     for (int k = 0; k < kPer; k++) {
       const uint64_t i = i0 + (uint64_t)k * kPart2Block + tid;
-      if (i < hi) v[k] = kC ? load_craw(reinterpret_cast<const CEntry*>(P.ent3) + i) : P.ent3[i];
+      if (i < hi) v[k] = kC ? load_craw(reinterpret_cast<const CEntry*>(src) + i) : src[i];
     }
   };
   Entry nx[kPer];
@@ -1658,6 +1675,92 @@ __global__ __launch_bounds__(kPart2Block) void k_part2f_direct(BuildParams P) {
       P.bcount[bucket] = cur[b];
     }
   }
+}
+
+// Two-level pass 2, for tables of thousands of buckets a digit (C4's 4960).  k_part2f_direct stores
+// every entry at its bucket's cursor across the bucket regions of 256 digits at once: the stores land
+// as partial lines, 3.15x their bytes written (26.5 GB for 8.4 GB of entries at 700M records,
+// profiles/r06/meas/c4_700000000_write.txt).  Here k_part2_sub first splits each digit region into
+// kSub regions of consecutive buckets (sub-digits) -- per tile of kPartTile entries, grouped in LDS and
+// written as one run per sub-digit -- and k_part2f<.., kSubIn> then stages one sub-digit per
+// workgroup into its bucket regions (runs of about a hundred entries a bucket and round).  A sub-digit region that fills up flags
+// kSpecRegionFull (the host redoes the build with the two-pass partition).
+
+// One tile of kPartTile entries a workgroup (persistent workgroups that load the next tile during this
+// one's grouping measured 9.3 against 5.1 ms at C4: 235 VGPRs, two waves a SIMD,
+// profiles/r06/c4/part2_sub_persistent_ab.txt).
+template <bool kC>  // 12-byte CEntry regions in and out (BuildParams.compact)
+__global__ __launch_bounds__(kPartBlock) void k_part2_sub(BuildParams P, uint32_t tiles_per_digit) {
+  __shared__ Entry stage[kPartTile];
+  __shared__ uint8_t ssub[kPartTile];  // sub-digit of each staged entry
+  __shared__ uint32_t cnt[kSub], lbase[kSub + 1];
+  __shared__ int64_t gdst[kSub];       // global index of the sub-digit's run minus its LDS start
+  if (build_aborted(P)) return;
+  const uint32_t d = blockIdx.x / tiles_per_digit, t = blockIdx.x % tiles_per_digit;
+  const uint64_t fill = min((uint64_t)P.p1_fill[d], P.p1_region);
+  const uint64_t lo = (uint64_t)t * kPartTile;
+  if (lo >= fill) return;
+  const uint32_t n = (uint32_t)min((uint64_t)kPartTile, fill - lo);
+  const uint64_t base = (uint64_t)d * P.p1_region + lo;
+  const uint32_t b0 = d * P.bpp, bps = sub_buckets(P.bpp);
+  const int tid = threadIdx.x;
+  if (tid < (int)kSub) cnt[tid] = 0;
+  __syncthreads();
+  Entry v[kPartItems];
+#pragma unroll
+  for (int k = 0; k < kPartItems; k++) {
+    const uint32_t idx = (uint32_t)k * kPartBlock + tid;
+    if (idx < n) v[k] = kC ? load_craw(reinterpret_cast<const CEntry*>(P.ent3) + base + idx) : P.ent3[base + idx];
+  }
+  uint32_t sg[kPartItems];
+  bool bad = false;  // (kGuardForeign)
+#pragma unroll
+  for (int k = 0; k < kPartItems; k++) {
+    const uint32_t idx = (uint32_t)k * kPartBlock + tid;
+    sg[k] = ~0u;
+    if (idx >= n) continue;
+    const uint32_t b = bucket_of(P, v[k].hash) - b0;
+    bad |= b >= P.bpp;
+    if (b >= P.bpp) continue;
+    const uint32_t sb = b / bps;
+    sg[k] = sb | (atomicAdd(&cnt[sb], 1u) << 8);  // rank inside the tile's sub-digit run
+  }
+  __syncthreads();
+  if (tid < (int)kSub) {  // (wave 0: reserve each run, scan the counts)
+    const uint32_t c = cnt[tid];
+    const uint64_t g = c ? atomicAdd(&P.sub_fill[d * kSub + tid], c) : 0u;
+    uint32_t incl = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t x = __shfl_up(incl, o, 64);
+      if (tid >= o) incl += x;
+    }
+    lbase[tid] = incl - c;
+    if (tid == (int)kSub - 1) lbase[kSub] = incl;
+    if (g + c > P.sub_region) atomicOr(&P.st->spec_fail, kSpecRegionFull);
+    gdst[tid] = (int64_t)((uint64_t)(d * kSub + tid) * P.sub_region + g) - (int64_t)(incl - c);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < kPartItems; k++) {
+    if (sg[k] == ~0u) continue;
+    const uint32_t sb = sg[k] & 255u, pos = lbase[sb] + (sg[k] >> 8);
+    stage[pos] = v[k];
+    ssub[pos] = (uint8_t)sb;
+  }
+  __syncthreads();
+  const uint32_t nkeep = lbase[kSub];
+#pragma unroll
+  for (int k = 0; k < kPartItems; k++) {
+    const uint32_t i = (uint32_t)k * kPartBlock + tid;
+    if (i >= nkeep) continue;
+    const uint32_t sb = ssub[i];
+    const uint64_t at = (uint64_t)(gdst[sb] + (int64_t)i);
+    if (at >= (uint64_t)(d * kSub + sb + 1) * P.sub_region) continue;  // (flagged above)
+    if (kC) store_craw(reinterpret_cast<CEntry*>(P.sub_ent) + at, stage[i]);
+    else P.sub_ent[at] = stage[i];
+  }
+  report_foreign(P, bad);
 }
 
 // Sharded receive into fixed bucket regions, for tables of more than kP2SortedMaxBpp buckets a digit.
@@ -2584,7 +2687,13 @@ void launch_partition(const BuildParams& P, hipStream_t s, StageTimer* tm) {
                        part2st_lds(P.bpp, 4), s, P);
   else if (P.p2_sorted)
     hipLaunchKernelGGL(k_part2s, dim3(256), dim3(kPart2Block), (size_t)(514u * P.bpp) * sizeof(uint32_t), s, P);
-  else if (part2_direct(P))
+  else if (part2_direct(P) && P.sub_region) {  // (two levels: sub-digit regions, then the buckets)
+    const uint32_t tpd = (uint32_t)((P.p1_region + kPartTile - 1) / kPartTile);
+    hipLaunchKernelGGL((P.compact ? k_part2_sub<true> : k_part2_sub<false>), dim3(256u * tpd), dim3(kPartBlock), 0, s,
+                       P, tpd);
+    hipLaunchKernelGGL((P.compact ? k_part2f<6, true, true> : k_part2f<6, false, true>), dim3(256u * kSub),
+                       dim3(kPart2Block), part2f_lds(sub_buckets(P.bpp), 6), s, P);
+  } else if (part2_direct(P))
     hipLaunchKernelGGL((P.compact ? k_part2f_direct<true, true> : k_part2f_direct<false, false>),
                        dim3(256), dim3(kPart2Block),
                        (size_t)P.bpp * sizeof(uint32_t), s, P);

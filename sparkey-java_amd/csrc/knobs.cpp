@@ -23,7 +23,8 @@ const char* const kNames[kN] = {
     "exact_full_table", "snappy_lds",     "snappy_dir_a",     "snappy_dir_debug", "snappy_chunk",
     "snappy_serial_dir", "zstd_lds",      "shard_sync_frame", "shard_transport", "shard_fail_rank", "file_threads",
     "file_write_threads", "file_debug", "reframe_spin_ticks",
-    "shard_gather_compressed", "inject_foreign", "shard_coll_fail", "no_compact"};
+    "shard_gather_compressed", "inject_foreign", "shard_coll_fail", "no_compact",
+    "part2_two_level"};
 static_assert(sizeof(kNames) / sizeof(kNames[0]) == kN, "one name per knob");
 
 std::atomic<int64_t> g_val[kN];

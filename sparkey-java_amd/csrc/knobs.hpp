@@ -51,6 +51,7 @@ enum class Knob : int {
   InjectForeign,    // tests of the kGuardForeign check: a foreign entry in digit region 0 (1) or bucket region 0 (2)
   ShardCollFail,    // host transport (HostColl): the k-th collective of a communicator fails its device copy (tests)
   NoCompact,        // 16-byte entries on the uniform staged path too (BuildParams.compact off)
+  Part2TwoLevel,    // pass 2 through sub-digit regions: 1 forces it (any table: tests), 0 keeps k_part2f_direct
   kCount
 };
 

@@ -320,6 +320,9 @@ struct sparkey_plan {
   hipEvent_t sn_ev[2] = {nullptr, nullptr};
   uint64_t c_seg_cls_cnt = 0, c_seg_cls_off = 0, c_seg_len = 0, c_seg_first = 0, c_seg_fun = 0, c_seg_krep = 0, c_ecls = 0;
   uint32_t* seg_krep = nullptr;   // exact path: per placed record, slots back to its key's first record
+  uint64_t c_sub_ent = 0, c_sub_fill = 0;
+  Entry* sub_ent = nullptr;       // two-level pass 2: the sub-digit regions
+  uint32_t* sub_fill = nullptr;   // two-level pass 2: their fill cursors
   uint32_t* ecls = nullptr;       // exact path: per grouped record, its key's class
   uint32_t* seg_len = nullptr;    // exact path: distinct keys per wanted slot, then segment lengths
   uint64_t* seg_first = nullptr;  // exact path: per segment, the slot of its first placed PUT record
@@ -1371,7 +1374,7 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
     regions_used = P.p1_region != 0 && !P.p1_kernel;  // (partition passes: 1 when the framing did pass 1)
     buckets_used = to_buckets;                         // (0 when it wrote the buckets)
     // k_part2s: pass 2 also sorts each bucket by wanted slot and leaves the carry functions
-    P.p2_sorted = P.bpp <= kP2SortedMaxBpp && !to_buckets ? 1 : 0;
+    P.p2_sorted = P.bpp <= kP2SortedMaxBpp && !to_buckets && !knob_on(Knob::Part2TwoLevel) ? 1 : 0;
     // fixed bucket regions: k_part2st (fused carry) up to kP2SortedMaxBpp buckets a digit, k_part2f past
     // that (from the digit regions of pass 1)
     P.p2_fixed = use_fixed && (to_buckets || P.p2_sorted || (P.p1_region && part2f_fits(P.bpp))) ? 1 : 0;
@@ -1396,6 +1399,21 @@ static int plan_build(sparkey_plan* pl, const uint8_t* log_header, const uint8_t
     // digit regions compact (kCompactIn alone) measured slower than neither.
     P.compact = framing_path == 2 && tiles && P.p1_region && !P.p1_kernel && (part2st_per(P) > 0 || part2_direct(P)) &&
                         P.uni_n < (1ull << 32) && !knob_on(Knob::NoCompact) ? (kCompactIn | kCompactOut) : 0;
+    // pass 2 in two levels where it would scatter over thousands of bucket regions a digit (C4): the
+    // digit regions into kSub sub-digit regions each, sized like the digit regions (expected + 8
+    // sigma), then one sub-digit's buckets a workgroup (k_part2_sub, k_part2f<.., kSubIn>)
+    P.sub_region = 0;
+    const int64_t two_level = knob(Knob::Part2TwoLevel);
+    if (part2_direct(P) && two_level != 0 && (two_level > 0 || P.bpp >= 2 * kSub)) {
+      const double expect = (double)nrec * (double)((P.bpp + kSub - 1) / kSub) * (double)kBucket / (double)P.cap;
+      const uint64_t sub_cap = ((uint64_t)(expect + 8.0 * std::sqrt(expect) + 1024.0) + 63) & ~63ull;
+      HIP_TRY(grow(&pl->sub_ent, pl->c_sub_ent, 256ull * kSub * sub_cap));
+      HIP_TRY(grow(&pl->sub_fill, pl->c_sub_fill, 256ull * kSub));
+      HIP_TRY(hipMemsetAsync(pl->sub_fill, 0, 256ull * kSub * sizeof(uint32_t), s));
+      P.sub_region = sub_cap;
+      P.sub_ent = pl->sub_ent;
+      P.sub_fill = pl->sub_fill;
+    }
     // an attempt whose framing failed, stopped early or overflowed skips every later stage (the host
     // redoes it or reports the error): no stage reads a region the framing left half-written
     P.abort_on_fail = 1;
@@ -1884,7 +1902,7 @@ void sparkey_plan_destroy(sparkey_plan* pl) {
                   pl->bcount, pl->bcursor, pl->boff, pl->bfun, pl->bpre, pl->bfun_total, pl->carry, pl->pairs,
                   pl->dfun, pl->dcarry, pl->parts, pl->p1_fill, pl->scan_u64, pl->scan_mp, pl->desc, pl->p1_hist, pl->p1_off, pl->d_status, pl->dbg, pl->wcount, pl->woff, pl->small,
                   pl->eseg, pl->seg_cnt, pl->seg_off, pl->seg_mark, pl->seg_start, pl->bstat_start,
-                  pl->seg_cls_cnt, pl->seg_cls_off, pl->seg_len, pl->seg_first, pl->seg_fun, pl->seg_krep, pl->ecls, pl->p2tab,
+                  pl->seg_cls_cnt, pl->seg_cls_off, pl->seg_len, pl->seg_first, pl->seg_fun, pl->seg_krep, pl->ecls, pl->sub_ent, pl->sub_fill, pl->p2tab,
                   pl->app_i64, pl->app_u32, pl->app_u64, pl->app_scan, pl->app_map,
                   pl->sn_blocks, pl->sn_dir, pl->sn_walk, pl->sn_recoff, pl->sn_vlog, pl->sn_itab, pl->sn_err,
                   pl->xtab, pl->ex_starts, pl->ex_cnt, pl->ex_off, pl->sn_par, pl->delp};

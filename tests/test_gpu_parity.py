@@ -396,6 +396,28 @@ def test_uniform_compact_entries(native, switch, klen, vlen, hash_size):
     assert b == got
 
 
+@pytest.mark.parametrize("shape", ["uniform", "general", "c3"])
+def test_part2_two_level(native, switch, shape):
+    """Pass 2 in two levels (k_part2_sub into sub-digit regions, k_part2_subf into the bucket regions),
+    which C4's 4960 buckets a digit take by default, forced on smaller tables: compact entries from the
+    uniform framing, 16-byte ones from the slab framings.  The oracle's bytes, and those of the one-level
+    pass."""
+    if shape == "uniform":
+        log = make_log(_uniform_puts(120000, 16, 100, seed=5))
+    elif shape == "general":
+        log = make_log(_uniform_puts(120000, 16, 100, seed=6) + [(b"short", b"v")])
+    else:
+        rng = np.random.default_rng(7)
+        log = make_log([(rng.integers(0, 256, int(rng.integers(8, 65)), dtype=np.uint8).tobytes(), bytes(100))
+                        for _ in range(80000)])
+    if shape != "uniform":
+        switch(no_buckets=1)  # (k_frame3 would write the bucket regions itself: slabs and pass 1 instead)
+    one, _ = gpu_build(native, log, 41, 8)
+    switch(part2_two_level=1)
+    got, stats = check(native, log, 41, hash_size=8)
+    assert got == one, diff_report(got, one)
+
+
 @pytest.mark.parametrize("region_cap", [60000, 1])
 def test_uniform_digit_regions(native, switch, region_cap):
     """k_frame_uniform as partition pass 1 (entries straight into digit regions of ent3): a region
