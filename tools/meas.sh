@@ -34,8 +34,11 @@ if has prof; then
   prof c2 "--workload c2 --steps 3 --warmup 1 --no-parity --no-cpu-baseline --quick" || exit 1
   prof c3_100000000 "--workload c3 --entries 100000000 --steps 3 --warmup 1 --no-parity --no-cpu-baseline --quick" || exit 1
 fi
-if has c4prof; then
-  prof c4_1000000000 "--workload c4 --steps 2 --warmup 1 --no-cpu-baseline" || exit 1
+if has c4prof; then  # 1B: the kernel trace; counters at 700M (the WRITE_SIZE pass at 1B hangs in the profiler)
+  D=$O/rocprof_c4_1000000000; mkdir -p $D
+  timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d $D/trace -o run -- python3 bench.py \
+    --workload c4 --steps 2 --warmup 1 --no-cpu-baseline > $D/trace.log 2>&1 || exit 1
+  prof c4_700000000 "--workload c4 --entries 700000000 --steps 2 --warmup 1 --no-cpu-baseline" || exit 1
 fi
 if has shardprof; then  # a sharded rank's kernels and traffic (N = 1: no exchange, the rank's own steps)
   prof sharded_rank_125000000 "--sharded --entries 125000000 --steps 2 --warmup 1 --no-check" || exit 1

@@ -59,8 +59,8 @@ def main(src, dst, workload=None):
     stage_kernels = {"frame": ["k_frame", "k_frame_uniform", "k_frame2", "k_frame3", "k_frame_lane", "k_frame_lane_act",
                                "k_frame_lane_flags"], "frame_uniform": ["k_frame_uniform"],
                      "partition": ["k_part1_hist", "k_part1_scatter", "k_part1_regions", "k_part2", "k_part2s", "k_part2st", "k_part2d",
-                                   "k_part2f", "k_part2f_direct", "k_scan_tiles"],
-                     "partition_regions": ["k_part2", "k_part2s", "k_part2st", "k_part2d", "k_part2f", "k_part2f_direct"],
+                                   "k_part2f", "k_part2f_direct", "k_part2_sub", "k_scan_tiles"],
+                     "partition_regions": ["k_part2", "k_part2s", "k_part2st", "k_part2d", "k_part2f", "k_part2f_direct", "k_part2_sub"],
                      "place": ["k_place_lds", "k_place_reg", "k_place_reg_persist", "k_place", "k_place_fix"],
                      "stats": ["k_stats", "k_stats_final", "k_stats_folded"],
                      "summary": ["k_summary", "k_carry"], "verify": ["k_verify_pairs"]}
