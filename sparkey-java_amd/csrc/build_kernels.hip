@@ -548,7 +548,8 @@ void launch_carry(const BuildParams& P, hipStream_t s) {
 void launch_summary_carry(const BuildParams& P, hipStream_t s, StageTimer* tm) {
   const uint64_t nb = P.b_hi - P.b_lo;
   if (nb == 0) return;
-  hipLaunchKernelGGL(k_summary, dim3((unsigned)nb), dim3(kPlaceBlock), 0, s, P);
+  // (the two-level pass 2 left every bucket's carry function: k_part2f<.., kSubIn>)
+  if (!P.sub_region) hipLaunchKernelGGL(k_summary, dim3((unsigned)nb), dim3(kPlaceBlock), 0, s, P);
   scan_exclusive<MaxPlus, MaxPlus, OpMaxPlus>(P.bfun + P.b_lo, P.bpre + P.b_lo, nb, P.bfun_total, OpMaxPlus(),
                                               P.scan_scratch_mp, s);
   if (!P.sharded) launch_carry(P, s);

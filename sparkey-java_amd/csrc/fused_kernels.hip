@@ -1512,10 +1512,13 @@ __host__ __device__ inline uint32_t sub_buckets(uint32_t bpp) { return (bpp + kS
 // digit: 2, whose rounds are shorter than the bucket count -- runs of about one entry).  Single GPU.
 // kC: 12-byte CEntry digit regions in and bucket regions out (BuildParams.compact).
 // kSubIn: a workgroup per sub-digit of the two-level pass (k_part2_sub's regions in P.sub_ent: its
-// bucket_sub buckets from the digit's sb-th on) instead of a workgroup per coarse digit.
+// bucket_sub buckets from the digit's sb-th on) instead of a workgroup per coarse digit.  A sub-digit's
+// ~78 buckets leave room for their 8-bit slot counts beside a four-entry stage, so the pass also
+// leaves each bucket's carry function, as k_part2st does (k_summary, which would read every entry
+// again, does not run; a count past 255 flags p2_overflow and the host redoes the build dense).
 template <int kPer, bool kC, bool kSubIn = false>
 __global__ __launch_bounds__(kPart2Block) void k_part2f(BuildParams P) {
-  // cur[nb] | rc0[nb] | rc1[nb] | roff[nb] | gbase[nb] | stage[kPart2Block * kPer]
+  // cur[nb] | rc0[nb] | rc1[nb] | roff[nb] | gbase[nb] | (kSubIn: h8[nb * 256]) | stage[kPart2Block * kPer]
   extern __shared__ __attribute__((aligned(16))) uint32_t dyn[];
   __shared__ uint64_t sh64[kPart2Block / 64 + 1];
   if (build_aborted(P)) return;
@@ -1540,10 +1543,12 @@ __global__ __launch_bounds__(kPart2Block) void k_part2f(BuildParams P) {
   uint32_t* rc[2] = {cur + nbins, cur + 2 * nbins};
   uint32_t* roff = cur + 3 * nbins;
   uint32_t* gbase = cur + 4 * nbins;
-  Entry* stage = reinterpret_cast<Entry*>(dyn + ((5 * nbins + 3) & ~3u));
+  uint32_t* h = dyn + ((5 * nbins + 3) & ~3u);  // (kSubIn: 8-bit count per slot, four a word)
+  const uint32_t hwords = kSubIn ? nbins * 256 : 0u;
+  Entry* stage = reinterpret_cast<Entry*>(h + hwords);
   constexpr uint32_t kRound = kPart2Block * kPer;
   const int tid = threadIdx.x;
-  for (uint32_t b = tid; b < 5 * nbins; b += kPart2Block) dyn[b] = 0;
+  for (uint32_t b = tid; b < ((5 * nbins + 3) & ~3u) + hwords; b += kPart2Block) dyn[b] = 0;
   __syncthreads();
   const uint32_t per = (nbins + kPart2Block - 1) / kPart2Block;
   bool ovf = false, bad = false;  // (bad: kGuardForeign)
@@ -1569,11 +1574,16 @@ __global__ __launch_bounds__(kPart2Block) void k_part2f(BuildParams P) {
       const uint64_t i = i0 + (uint64_t)k * kPart2Block + tid;
       bk[k] = ~0u;
       if (i >= hi) continue;
-      const uint32_t b = bucket_of(P, v[k].hash) - b0;
+      const uint64_t slot = fast_mod(v[k].hash, P.mod);
+      const uint32_t b = (uint32_t)(slot >> kBucketShift) - b0;
       bad |= b >= nbins;
       if (b >= nbins) continue;
       bk[k] = b;
       rk[k] = atomicAdd(&rcnt[b], 1u);
+      if (kSubIn) {
+        const uint32_t sl = (uint32_t)(slot & (kBucket - 1)), sh = (sl & 3u) * 8u;
+        if (((atomicAdd(&h[(b << 8) + (sl >> 2)], 1u << sh) >> sh) & 0xffu) == 0xffu) ovf = true;  // (8-bit count full)
+      }
     }
     __syncthreads();
     {  // the round's run offsets; each bucket's cursor moves past the round; the other parity's counts
@@ -1619,6 +1629,43 @@ __global__ __launch_bounds__(kPart2Block) void k_part2f(BuildParams P) {
     if (bucket < P.nbuckets) {
       P.boff[bucket] = (bucket - P.b_lo) * (uint64_t)kPlaceLdsMax;
       P.bcount[bucket] = cur[b];
+    }
+  }
+  if (!kSubIn) return;
+  // per bucket (one wave each): the carry function from the slot counts (k_summary's, k_part2st's)
+  const int lane = tid & 63, wave = tid >> 6;
+  for (uint32_t b = wave; b < nbins; b += kPart2Block / 64) {
+    const uint64_t bucket = (uint64_t)b0 + b;
+    if (bucket >= P.nbuckets) continue;
+    const uint32_t* hw = h + (b << 8) + lane * 4;  // this lane's 16 slots: 16 * lane ...
+    uint32_t cnts[16];
+    uint32_t tot = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const uint32_t w = hw[k];
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        cnts[4 * k + q] = (w >> (8 * q)) & 0xffu;
+        tot += cnts[4 * k + q];
+      }
+    }
+    const uint32_t incl = wave_incl_sum_u32(tot);
+    uint32_t run = incl - tot;
+    long long mx = -(1ll << 40);
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+      if (cnts[k]) mx = max(mx, (long long)(16 * lane + k) - (long long)run);
+      run += cnts[k];
+    }
+    mx = wave_max_i64(mx);
+    if (lane == 0) {
+      const int64_t n = (int64_t)cur[b];
+      const int64_t bsize = (int64_t)min((uint64_t)kBucket, P.cap - (bucket << kBucketShift));
+      const int64_t mlast = mx < 0 ? 0 : mx;
+      MaxPlus f;
+      f.a = n - bsize;
+      f.c = n ? max((int64_t)0, n + mlast - bsize) : 0;
+      P.bfun[bucket] = f;
     }
   }
 }
@@ -2691,8 +2738,8 @@ void launch_partition(const BuildParams& P, hipStream_t s, StageTimer* tm) {
     const uint32_t tpd = (uint32_t)((P.p1_region + kPartTile - 1) / kPartTile);
     hipLaunchKernelGGL((P.compact ? k_part2_sub<true> : k_part2_sub<false>), dim3(256u * tpd), dim3(kPartBlock), 0, s,
                        P, tpd);
-    hipLaunchKernelGGL((P.compact ? k_part2f<6, true, true> : k_part2f<6, false, true>), dim3(256u * kSub),
-                       dim3(kPart2Block), part2f_lds(sub_buckets(P.bpp), 6), s, P);
+    hipLaunchKernelGGL((P.compact ? k_part2f<4, true, true> : k_part2f<4, false, true>), dim3(256u * kSub),
+                       dim3(kPart2Block), part2f_lds(sub_buckets(P.bpp), 4) + (size_t)sub_buckets(P.bpp) * 1024, s, P);
   } else if (part2_direct(P))
     hipLaunchKernelGGL((P.compact ? k_part2f_direct<true, true> : k_part2f_direct<false, false>),
                        dim3(256), dim3(kPart2Block),
