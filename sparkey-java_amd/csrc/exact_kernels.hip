@@ -364,23 +364,48 @@ __device__ __forceinline__ uint64_t placed_wanted(const BuildParams& P, uint64_t
   return a ? fast_mod(h, P.mod) : kNoSeg;
 }
 
-// Do the records at addresses a (header ha) and a2 hold the same key?  (IndexHash.java:606-636)
-__device__ __forceinline__ bool same_key_at(const BuildParams& P, uint64_t a, const RecHdr& ha, uint64_t a2) {
-  const RecHdr hb = log_header(P, a2);
-  return ha.rc == 0 && hb.rc == 0 && ha.klen == hb.klen &&
-         keys_equal(P, (int64_t)(a >> P.ebb) + ha.hlen, (int64_t)(a2 >> P.ebb) + hb.hlen, ha.klen);
+// A record's first 32 bytes (header and, for keys of up to 22-30 bytes, the whole key), loaded at once,
+// and its header decoded from them.
+struct Rec32 {
+  Bytes16 lo, hi;
+  RecHdr h;
+};
+__device__ __forceinline__ Rec32 log32(const BuildParams& P, uint64_t address) {
+  const int64_t p = (int64_t)(address >> P.ebb);
+  const Bytes16 lo = log16(P, p), hi = log16(P, p + 16);
+  auto at = [&](int64_t x) -> uint32_t { return lo.byte((uint32_t)(x - p)); };  // (a header: <= 10 bytes)
+  return Rec32{lo, hi, decode_header(at, p, (int64_t)P.log_len)};
+}
+
+// Do the records at addresses a and a2 hold the same key?  (IndexHash.java:606-636)  From the loaded
+// 32 bytes when both headers have one length and the key ends inside them, else from the log.
+__device__ __forceinline__ bool same_key_at(const BuildParams& P, uint64_t a, const Rec32& ra, uint64_t a2, const Rec32& rb) {
+  const RecHdr &ha = ra.h, &hb = rb.h;
+  if (ha.rc || hb.rc || ha.klen != hb.klen) return false;
+  if (ha.hlen == hb.hlen && ha.hlen + ha.klen <= 32 && ha.klen >= 0 &&
+      (int64_t)(max(a, a2) >> P.ebb) + ha.hlen + ha.klen <= (int64_t)P.log_len) {  // (else keys_equal's guard)
+    const int32_t k0 = ha.hlen, k1 = ha.hlen + ha.klen;  // key bytes [k0, k1) of both windows
+    uint32_t diff = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      const int32_t lo = min(max(k0 - 4 * i, 0), 4), hi = min(max(k1 - 4 * i, 0), 4);
+      const uint32_t m = (uint32_t)(((1ull << (8 * hi)) - 1ull) & ~((1ull << (8 * lo)) - 1ull));
+      const uint32_t x = i < 4 ? ra.lo.w[i & 3] : ra.hi.w[i & 3], y = i < 4 ? rb.lo.w[i & 3] : rb.hi.w[i & 3];
+      diff |= (x ^ y) & m;
+    }
+    return diff == 0;
+  }
+  return keys_equal(P, (int64_t)(a >> P.ebb) + ha.hlen, (int64_t)(a2 >> P.ebb) + hb.hlen, ha.klen);
 }
 
 // The first member of slot g0's group, from g0 up to (not including) slot `end`, with hash h and the
-// key of the record at address a (header ha): its slot, or kNoSeg.  Equal keys share a hash: the first
-// member with hash h usually holds the key (a second key of that hash is a 64-bit -- or 32-bit --
-// collision), so one comparison settles it.
-__device__ uint64_t first_with_key(const BuildParams& P, uint64_t g0, uint64_t end, uint64_t h, uint64_t a,
-                                   const RecHdr& ha) {
+// key of the record at address a (its bytes ra): its slot, or kNoSeg.
+__device__ __forceinline__ uint64_t first_with_key(const BuildParams& P, uint64_t g0, uint64_t end, uint64_t h, uint64_t a,
+                                   const Rec32& ra) {
   for (uint64_t j = g0, g = 0; j != end && g < P.cap; j = next_slot(P, j), g++) {
     uint64_t h2, a2;
     read_slot(P, j, h2, a2);
-    if (h2 == h && same_key_at(P, a, ha, a2)) return j;
+    if (h2 == h && same_key_at(P, a, ra, a2, log32(P, a2))) return j;
   }
   return kNoSeg;
 }
@@ -401,7 +426,7 @@ __global__ __launch_bounds__(256) void k_seg_dcount(BuildParams P) {
     // the group's first member with this hash (the whole group back: a repeated key's records are
     // usually its only members with that hash)
     constexpr int kStep = 4;  // slots read together, backwards
-    uint64_t e = kNoSeg;
+    uint64_t e = kNoSeg, ae = 0;
     bool more = true;
     for (uint64_t g = 0, j = t; more && g < P.cap; g += kStep) {
       uint64_t hb[kStep], ab[kStep], jb[kStep];
@@ -418,14 +443,18 @@ __global__ __launch_bounds__(256) void k_seg_dcount(BuildParams P) {
           more = false;
           continue;
         }
-        if (hb[q] == h) e = jb[q];
+        if (hb[q] == h) {
+          e = jb[q];
+          ae = ab[q];
+        }
       }
       j = jb[kStep - 1];
     }
     uint32_t back = 0;
-    if (e != kNoSeg) {
-      const RecHdr ha = log_header(P, a);
-      const uint64_t r = first_with_key(P, e, t, h, a, ha);
+    if (e != kNoSeg) {  // (both records' bytes in one round trip: the first member with this hash
+                        //  usually holds the key -- a second key of that hash is a collision)
+      const Rec32 ra = log32(P, a), re = log32(P, ae);
+      const uint64_t r = same_key_at(P, a, ra, ae, re) ? e : first_with_key(P, next_slot(P, e), t, h, a, ra);
       if (r != kNoSeg) back = (uint32_t)(t >= r ? t - r : t + P.cap - r);
     }
     P.seg_krep[t] = back;
@@ -531,7 +560,7 @@ __global__ __launch_bounds__(256) void k_seg_runs(BuildParams P) {
 // when no PUT record holds its key (the DELETE then removes nothing in any state).  The placement's
 // slots from the wanted slot w on hold records of earlier wanted slots, then w's group.
 __device__ uint64_t delete_class(const BuildParams& P, uint64_t w, uint64_t h, uint64_t a, uint64_t d) {
-  const RecHdr ha = log_header(P, a);  // (its key's length and place: loaded while the slots are probed)
+  const Rec32 ra = log32(P, a);  // (its header and key: loaded while the slots are probed)
   constexpr int kStep = 4;             // slots read together (the probe passes about as many at 0.77 load)
   uint64_t t = w;
   for (uint64_t g = 0; g < P.cap; g += kStep) {
@@ -548,7 +577,7 @@ __device__ uint64_t delete_class(const BuildParams& P, uint64_t w, uint64_t h, u
       const uint64_t dt = u >= w2 ? u - w2 : u + P.cap - w2;  // (displacements at u)
       const uint64_t dw = u >= w ? u - w : u + P.cap - w;
       if (dt < dw) return kNoSeg;  // past where w's group would be: no record wants w
-      if (dt == dw && hb[j] == h && same_key_at(P, a, ha, ab[j])) {  // w's group: the first with the key
+      if (dt == dw && hb[j] == h && same_key_at(P, a, ra, ab[j], log32(P, ab[j]))) {  // w's group: the first with the key
         const uint64_t f = P.seg_first[d];
         return u >= f ? u - f : u + P.cap - f;
       }
