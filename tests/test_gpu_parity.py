@@ -396,7 +396,7 @@ def test_uniform_compact_entries(native, switch, klen, vlen, hash_size):
     assert b == got
 
 
-@pytest.mark.parametrize("shape", ["uniform", "general", "c3"])
+@pytest.mark.parametrize("shape", ["uniform", "general", "c3", "hot"])
 def test_part2_two_level(native, switch, shape):
     """Pass 2 in two levels (k_part2_sub into sub-digit regions, k_part2_subf into the bucket regions),
     which C4's 4960 buckets a digit take by default, forced on smaller tables: compact entries from the
@@ -404,6 +404,9 @@ def test_part2_two_level(native, switch, shape):
     pass."""
     if shape == "uniform":
         log = make_log(_uniform_puts(120000, 16, 100, seed=5))
+    elif shape == "hot":  # one key 400 times: its slot's 8-bit count wraps (p2_overflow, the dense redo)
+        puts = _uniform_puts(120000, 16, 100, seed=8)
+        log = make_log(puts + [(puts[7][0], bytes(100))] * 400)
     elif shape == "general":
         log = make_log(_uniform_puts(120000, 16, 100, seed=6) + [(b"short", b"v")])
     else:
