@@ -851,15 +851,20 @@ constexpr uint32_t kLaneRecs = kSmallSegOps;
 constexpr uint32_t kLaneDel = 0x80;         // class byte: a DELETE record
 constexpr uint32_t kLaneFree = 0xffffffffu;  // an empty slot
 constexpr uint32_t kLaneBatch = 8;          // global loads a lane issues together
+// KeyT: 32-bit replay keys where every address fits (IN_MEMORY order over a log below 4 GB): 17 KB of
+// LDS a wave instead of 23 KB, so 9 waves a CU instead of 6 hide the lanes' dependent loads.
+template <typename KeyT>
 struct LaneLds {
-  uint64_t key[kLaneRecs][64];       // replay-order keys; then the removed records' numbers (bytes)
+  KeyT key[kLaneRecs][64];           // replay-order keys; then the removed records' numbers (bytes)
   uint32_t slot[kLaneRecs + 1][64];  // local slot -> its record: number | wanted << 8 | class << 16
   uint16_t attr[kLaneRecs][64];      // list index, then record number -> local wanted slot | class << 8
   uint8_t perm[kLaneRecs][64];       // record number -> list index
 };
 
+template <typename KeyT>
 __global__ __launch_bounds__(64) void k_seg_lanes(BuildParams P, int sorted_order) {
-  __shared__ LaneLds L;
+  static_assert(sizeof(KeyT) * kLaneRecs >= 2 * kLaneRecs, "the key array holds the u16 and byte lists after it");
+  __shared__ LaneLds<KeyT> L;
   const int lane = threadIdx.x;
   const unsigned long long nseg = P.st->n_segs[0];
   int64_t entries = 0, garbage = 0;
@@ -913,7 +918,8 @@ __global__ __launch_bounds__(64) void k_seg_lanes(BuildParams P, int sorted_orde
         if (l >= len || (addr >> 58)) guard_trip(P, 1024u);
         uint64_t key = addr;
         if (sorted_order) key |= (l + (window_to_table(wl, P.mod) < t0 ? 0ull : 32ull)) << 58;
-        L.key[i0 + j][lane] = key;
+        if (sizeof(KeyT) < 8 && (key >> 32)) guard_trip(P, 1024u);  // (the host picks 32 bits only below 4 GB)
+        L.key[i0 + j][lane] = (KeyT)key;
         L.attr[i0 + j][lane] = (uint16_t)(min(l, (uint64_t)kLaneRecs) |
                                           ((min(cb[j], kLaneRecs - 1) | ((eb[j].addr & kDelBit) ? kLaneDel : 0u)) << 8));
       }
@@ -922,7 +928,7 @@ __global__ __launch_bounds__(64) void k_seg_lanes(BuildParams P, int sorted_orde
     // record number = rank of the key (addresses are distinct, so are the keys); perm keeps the list
     // index and slot[i] (free until the replay) the number of list index i
     for (uint32_t i = 0; i < n; i++) {
-      const uint64_t ki = L.key[i][lane];
+      const KeyT ki = L.key[i][lane];
       uint32_t r = 0;
 #pragma unroll
       for (uint32_t j = 0; j < kLaneRecs; j++) r += j < n && L.key[j][lane] < ki ? 1u : 0u;
@@ -1533,7 +1539,10 @@ void launch_segments(const BuildParams& P, hipStream_t s, int sorted_order, Stag
   step("large");
   hipLaunchKernelGGL((k_seg_replay_wave<kMidSegMax, 16, 1>), dim3(kMidGrid), dim3(64), 0, sm, P, sorted_order);
   step("mid");
-  hipLaunchKernelGGL(k_seg_lanes, dim3(kLaneGrid), dim3(64), 0, s, P, sorted_order);
+  if (!sorted_order && (((uint64_t)P.log_len + 1) << P.ebb) <= (1ull << 32))
+    hipLaunchKernelGGL(k_seg_lanes<uint32_t>, dim3(kLaneGrid), dim3(64), 0, s, P, sorted_order);
+  else
+    hipLaunchKernelGGL(k_seg_lanes<uint64_t>, dim3(kLaneGrid), dim3(64), 0, s, P, sorted_order);
   step("small");
   if (fork) {
     for (int i = 0; i < 3; i++) {
