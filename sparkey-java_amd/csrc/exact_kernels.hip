@@ -538,8 +538,9 @@ __global__ __launch_bounds__(256) void k_seg_first(BuildParams P) {
   if (placed_segment(P, prev_slot(P, t), h, a, last) != d) P.seg_first[d] = t;
 }
 
-// Per segment: its PUT record count (written by its last placed record, no atomics) into seg_cnt,
-// and its length (written by the empty slot that ends it) into seg_len.
+// Per segment: its PUT record count (added by its last placed record: k_seg_assign adds the DELETEs to
+// the same counter, concurrently) into seg_cnt, and its length (written by the empty slot that ends
+// it) into seg_len.
 __global__ __launch_bounds__(256) void k_seg_runs(BuildParams P) {
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= P.cap) return;
@@ -548,7 +549,7 @@ __global__ __launch_bounds__(256) void k_seg_runs(BuildParams P) {
   const uint64_t d = placed_segment(P, t, h, a, last);
   if (d != kNoSeg && placed_segment(P, next_slot(P, t), h, a, last) != d) {
     const uint64_t f = P.seg_first[d];
-    P.seg_cnt[d] = (uint32_t)((t >= f ? t - f : t + P.cap - f) + 1);
+    atomicAdd(&P.seg_cnt[d], (uint32_t)((t >= f ? t - f : t + P.cap - f) + 1));
   }
   if (P.seg_mark[t] != 0 && P.seg_mark[prev_slot(P, t)] == 0) {
     const uint64_t st = run_start(P, prev_slot(P, t), last);
@@ -1496,11 +1497,22 @@ void launch_segments(const BuildParams& P, hipStream_t s, int sorted_order, Stag
                                              reinterpret_cast<int64_t*>(P.scan_scratch_u64), s);
   step("start scan");
   hipLaunchKernelGGL(k_seg_first, dim3(slot_grid), dim3(256), 0, s, P);
-  hipLaunchKernelGGL(k_seg_runs, dim3(slot_grid), dim3(256), 0, s, P);
+  // k_seg_runs on a side stream beside k_seg_assign: both latency-bound, and they share only seg_cnt,
+  // which both add to
+  const bool fork = side && !check_each;
+  if (fork) {
+    (void)hipEventRecord(side->fork, s);
+    (void)hipStreamWaitEvent(side->s[0], side->fork, 0);
+  }
+  hipLaunchKernelGGL(k_seg_runs, dim3(slot_grid), dim3(256), 0, fork ? side->s[0] : s, P);
   step("runs");
   const unsigned seg_grid = (unsigned)((P.nslabs + kSegSlabs - 1) / kSegSlabs);
   if (P.nslabs) hipLaunchKernelGGL(k_seg_assign, dim3(seg_grid), dim3(64), 0, s, P);
   step("assign");
+  if (fork) {
+    (void)hipEventRecord(side->join[0], side->s[0]);
+    (void)hipStreamWaitEvent(s, side->join[0], 0);
+  }
   scan_exclusive<uint32_t, uint64_t, OpAdd>(P.seg_cnt, P.seg_off, P.cap, P.seg_off + P.cap, OpAdd(),
                                             P.scan_scratch_u64, s);
   step("count scan");
@@ -1526,7 +1538,6 @@ void launch_segments(const BuildParams& P, hipStream_t s, int sorted_order, Stag
   }
   // the size classes replay disjoint slots: huge, large and mid on the side streams, concurrent with
   // small on the build stream (longest tails first), joined back before the stats
-  const bool fork = side && !check_each;
   (void)hipMemsetAsync(P.st->seg_next, 0, sizeof(P.st->seg_next), s);  // (the classes' work queues)
   hipStream_t sh = fork ? side->s[0] : s, sl = fork ? side->s[1] : s, sm = fork ? side->s[2] : s;
   if (fork) {
