@@ -1516,8 +1516,18 @@ void launch_segments(const BuildParams& P, hipStream_t s, int sorted_order, Stag
   scan_exclusive<uint32_t, uint64_t, OpAdd>(P.seg_cnt, P.seg_off, P.cap, P.seg_off + P.cap, OpAdd(),
                                             P.scan_scratch_u64, s);
   step("count scan");
+  // the PUT and DELETE records to their places (disjoint: the DELETEs take the top of each segment's
+  // list), the DELETEs on a side stream; joined before the table is cleared (k_seg_puts reads it)
+  if (fork && P.nslabs) {
+    (void)hipEventRecord(side->fork, s);
+    (void)hipStreamWaitEvent(side->s[0], side->fork, 0);
+  }
   hipLaunchKernelGGL(k_seg_puts, dim3(slot_grid), dim3(256), 0, s, P);
-  if (P.nslabs) hipLaunchKernelGGL(k_seg_scatter, dim3(seg_grid), dim3(64), 0, s, P);
+  if (P.nslabs) hipLaunchKernelGGL(k_seg_scatter, dim3(seg_grid), dim3(64), 0, fork ? side->s[0] : s, P);
+  if (fork && P.nslabs) {
+    (void)hipEventRecord(side->join[0], side->s[0]);
+    (void)hipStreamWaitEvent(s, side->join[0], 0);
+  }
   step("scatter");
   // the records are grouped: the replays start from an empty table (slots outside every segment stay
   // empty; the placement of every PUT record filled some of them)
