@@ -1517,27 +1517,32 @@ void launch_segments(const BuildParams& P, hipStream_t s, int sorted_order, Stag
                                             P.scan_scratch_u64, s);
   step("count scan");
   // the PUT and DELETE records to their places (disjoint: the DELETEs take the top of each segment's
-  // list), the DELETEs on a side stream; joined before the table is cleared (k_seg_puts reads it)
-  if (fork && P.nslabs) {
+  // list), the DELETEs on a side stream, and the size classes' counts (they read seg_off only) on
+  // another; joined before the class lists are written (into arrays k_seg_puts / k_seg_scatter read)
+  const unsigned cls_grid = (unsigned)((P.cap + kClsSlots - 1) / kClsSlots);
+  hipStream_t sd = fork ? side->s[0] : s, sc = fork ? side->s[1] : s;
+  if (fork) {
     (void)hipEventRecord(side->fork, s);
-    (void)hipStreamWaitEvent(side->s[0], side->fork, 0);
+    (void)hipStreamWaitEvent(sd, side->fork, 0);
+    (void)hipStreamWaitEvent(sc, side->fork, 0);
   }
+  hipLaunchKernelGGL(k_seg_classify, dim3(cls_grid), dim3(kClsBlock), 0, sc, P, 0);
+  step("classify counts");
+  scan_exclusive<uint32_t, uint64_t, OpAdd>(P.seg_cls_cnt, P.seg_cls_off, (uint64_t)kSegLists * cls_grid,
+                                            P.seg_cls_off + (uint64_t)kSegLists * cls_grid, OpAdd(), P.scan_scratch_u64, sc);
+  step("classify scan");
+  if (P.nslabs) hipLaunchKernelGGL(k_seg_scatter, dim3(seg_grid), dim3(64), 0, sd, P);
   hipLaunchKernelGGL(k_seg_puts, dim3(slot_grid), dim3(256), 0, s, P);
-  if (P.nslabs) hipLaunchKernelGGL(k_seg_scatter, dim3(seg_grid), dim3(64), 0, fork ? side->s[0] : s, P);
-  if (fork && P.nslabs) {
-    (void)hipEventRecord(side->join[0], side->s[0]);
-    (void)hipStreamWaitEvent(s, side->join[0], 0);
-  }
   step("scatter");
   // the records are grouped: the replays start from an empty table (slots outside every segment stay
   // empty; the placement of every PUT record filled some of them)
   (void)hipMemsetAsync(P.out + kIndexHeaderSize, 0, (size_t)P.cap * (size_t)P.slot_size, s);
-  const unsigned cls_grid = (unsigned)((P.cap + kClsSlots - 1) / kClsSlots);
-  hipLaunchKernelGGL(k_seg_classify, dim3(cls_grid), dim3(kClsBlock), 0, s, P, 0);
-  step("classify counts");
-  scan_exclusive<uint32_t, uint64_t, OpAdd>(P.seg_cls_cnt, P.seg_cls_off, (uint64_t)kSegLists * cls_grid,
-                                            P.seg_cls_off + (uint64_t)kSegLists * cls_grid, OpAdd(), P.scan_scratch_u64, s);
-  step("classify scan");
+  if (fork) {
+    for (int i = 0; i < 2; i++) {
+      (void)hipEventRecord(side->join[i], side->s[i]);
+      (void)hipStreamWaitEvent(s, side->join[i], 0);
+    }
+  }
   hipLaunchKernelGGL(k_seg_classify, dim3(cls_grid), dim3(kClsBlock), 0, s, P, 1);
   step("classify lists");
   if (check_each) {
